@@ -1,0 +1,192 @@
+"""Headline bench: k=8 closest-node queries/sec at a 100M-node table (1/8 per GPU) + % HBM roofline.
+
+Workload (BASELINE.json config 3, per GPU): rank r holds shard r of the 100M-node U(24)
+routing table (2^21 owned buckets, ~12.5M nodes, plus the exact halo from its neighbours) in
+HBM and answers a batch of 1,048,576 RoutingTable::findClosestNodes(target, now, 8) queries
+whose targets it owns. One step = one batched kernel launch over that batch; inputs are
+resident in HBM before the timed region. Weak scaling: per-GPU work is fixed as N grows; at
+N=8 the shards cover the whole 100M-node table and a step answers 8M queries. No data-path
+collective (owner routing, DESIGN.md "Multi-GPU").
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from opendht_amd import DeviceTable  # noqa: E402
+from opendht_amd.metrics import rt_algorithmic_bytes  # noqa: E402
+from opendht_amd.sharded import ShardSpec, build_shard  # noqa: E402
+
+METRIC = "k=8 closest-node queries/sec at 100M-node table (1/8 GPU) + % HBM roofline"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
+
+
+def cpu_baseline(sh, targets, count, budget_s, nthreads):
+    """The oracle's structure-faithful restatement of RoutingTable::findClosestNodes (std::list
+    buckets, linear findBucket, insertion sort: the "port" CPU baseline) on this rank's shard,
+    timed on host cores over a bounded sample of the same queries."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+
+    t0 = time.perf_counter()
+    F = O.FaithfulTable(sh.ids, sh.status, sh.first, sh.off)
+    build_s = time.perf_counter() - t0
+    # calibrate on a small batch, then size the sample to ~budget_s of wall time
+    probe = max(nthreads, 16)
+    t0 = time.perf_counter()
+    F.rt_closest(targets[:probe], count, nthreads=nthreads)
+    per_q = (time.perf_counter() - t0) / probe
+    n = int(min(targets.shape[0], max(probe, budget_s / max(per_q, 1e-9))))
+    t0 = time.perf_counter()
+    F.rt_closest(targets[:n], count, nthreads=nthreads)
+    dt = time.perf_counter() - t0
+    F.close()
+    return {"value": n / dt, "unit": "queries/s", "cores": nthreads, "kind": "port",
+            "sample": f"{n} of the {targets.shape[0]} queries of rank 0's step (same shard table, "
+                      f"{sh.first.shape[0]} buckets, {sh.ids.shape[0]} nodes); structure-faithful "
+                      f"oracle build {build_s:.1f}s excluded"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--count", type=int, default=8)
+    ap.add_argument("--queries", type=int, default=1 << 20, help="queries per GPU per step")
+    ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU baseline sampling")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if world > 8:
+        raise SystemExit("the 100M-node table has 8 shards: at most 8 GPUs")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=dev)
+
+    spec = ShardSpec()  # 100M-node U(24), 8 shards, k_max 32
+    t0 = time.perf_counter()
+    sh = build_shard(spec, rank)
+    targets = spec.targets_for(rank, args.queries, seed=0x0D470002)
+    build_s = time.perf_counter() - t0
+
+    T = DeviceTable(sh.ids, sh.status, sh.first, sh.off, device=local, index_base=sh.index_base, sorted=True)
+    tg = torch.from_numpy(targets).to(dev)
+    out_idx = torch.empty((args.queries, args.count), dtype=torch.int32, device=dev)
+    out_cnt = torch.empty((args.queries,), dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    # algorithmic bytes of one launch (exact, host side; target buckets from the engine's findBucket)
+    tb = T.find_bucket(tg).cpu().numpy().view(np.uint32).astype(np.int64)
+    alg_bytes, mb, mn, mg = rt_algorithmic_bytes(sh.status, sh.off, tb, args.count)
+
+    for _ in range(args.warmup):
+        T.rt_closest(tg, args.count, out_idx, out_cnt, stream=stream.cuda_stream)
+    torch.cuda.synchronize(dev)
+
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t_start = time.perf_counter()
+    ev[0].record(stream)
+    for i in range(args.steps):
+        T.rt_closest(tg, args.count, out_idx, out_cnt, stream=stream.cuda_stream)
+        ev[i + 1].record(stream)
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    wall = time.perf_counter() - t_start
+    kern_ms = [ev[i].elapsed_time(ev[i + 1]) for i in range(args.steps)]
+    t_max = wall
+    if dist:
+        x = torch.tensor([wall], dtype=torch.float64, device=dev)
+        dist.all_reduce(x, op=dist.ReduceOp.MAX)
+        t_max = float(x.item())
+
+    avg_kernel_s = float(np.mean(kern_ms)) / 1e3
+    achieved = alg_bytes / avg_kernel_s / 1e9
+    total_q = world * args.queries * args.steps
+    value = total_q / t_max
+
+    traffic = None
+    if os.path.exists(args.traffic_json):
+        try:
+            traffic = json.load(open(args.traffic_json)).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_baseline(sh, targets, args.count, args.cpu_budget, min(16, os.cpu_count() or 1))
+
+    if rank == 0:
+        line = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "queries/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": t_max / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u64",
+            "data": "synthetic (counter-based uniform 160-bit IDs, 80/10/10 good/expired/dubious)",
+            "config": {
+                "workload": "config3: 100M-node U(24) routing table, 1/8 shard per GPU (2^21 owned buckets "
+                            f"+ halo, {sh.ids.shape[0]} nodes on rank 0), {args.queries} owned queries per GPU "
+                            f"per step, k={args.count}",
+                "table_nodes_per_gpu": int(sh.ids.shape[0]),
+                "buckets_per_gpu": int(sh.first.shape[0]),
+                "queries_per_gpu": args.queries,
+                "k": args.count,
+                "parallelism": f"id-range shards x{world}, owner routing (no data-path collective)",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": traffic,
+                "kernel": "rt_closest_kernel<8>",
+                "avg_kernel_ms": avg_kernel_s * 1e3,
+                "alg_bytes_per_launch": alg_bytes,
+                "alg_bytes_per_query": alg_bytes / args.queries,
+                "window_means": {"buckets": mb, "nodes": mn, "good": mg},
+            },
+            "cpu_baseline": cpu,
+            "setup_s": build_s,
+        }
+        print(json.dumps(line), flush=True)
+    T.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

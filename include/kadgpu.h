@@ -1,0 +1,204 @@
+/*
+ * kadgpu.h — C ABI of the MI355X-native batched Kademlia closest-node engine.
+ *
+ * This is the drop-in boundary for OpenDHT's XOR-distance lookup path. The
+ * reference exposes no C API/FFI for this path: its interface
+ * is the C++ member
+ *     std::vector<std::shared_ptr<Node>>
+ *     RoutingTable::findClosestNodes(const InfoHash id, time_point now,
+ *                                    size_t count) const
+ *         (reference: include/opendht/routing_table.h:48, src/routing_table.cpp:67-111)
+ *     RoutingTable::findBucket(const InfoHash&)
+ *         (reference: include/opendht/routing_table.h:50-51, src/routing_table.cpp:113-135)
+ *     std::vector<std::shared_ptr<Node>>
+ *     NodeCache::getCachedNodes(const InfoHash&, sa_family_t, size_t)
+ *         (reference: include/opendht/node_cache.h:32, src/node_cache.cpp:36-66)
+ * and the InfoHash primitives (include/opendht/infohash.h:84-162).
+ *
+ * Every entry point below replaces one of those; each cites the reference
+ * interface it stands in for. The C++11 shim in kadgpu.hpp wraps these with
+ * the reference's own signatures (RoutingTable::findClosestNodes, the new
+ * Dht-style findClosestNodes(id, af, count) accessor, NodeCache::getCachedNodes).
+ *
+ * Conventions
+ *  - IDs cross the ABI as raw InfoHash bytes: 20 bytes per ID, byte 0 most
+ *    significant (InfoHash::data() layout, reference infohash.h:58).
+ *  - A table is a snapshot of one address family's RoutingTable (and/or its
+ *    NodeCache map) at a chosen `now`: a flat node array grouped by bucket,
+ *    a bucket directory, and one status byte per node (bit0 = Node::isGood(now),
+ *    bit1 = Node::isExpired(); reference src/node.cpp:34-40, node.h:67).
+ *  - Results are uint32 node indices into the snapshot's node array plus
+ *    `index_base` (so shards can return global indices), padded with
+ *    KAD_NO_NODE beyond the per-query result count.
+ *  - Every function returns an int status (KAD_OK = 0, negative on error);
+ *    kad_last_error() gives a thread-local message. No C++ exception crosses
+ *    this ABI. Empty table -> zero results (reference routing_table.cpp:73).
+ *  - `*_batch` entry points take DEVICE pointers and enqueue on `stream`
+ *    (a hipStream_t, NULL = default stream); they do not synchronise.
+ *    `*_batch_host` entry points take HOST pointers and are synchronous
+ *    (H2D, kernel, D2H on an internal stream).
+ *  - A table handle is not safe for concurrent mutation; concurrent const
+ *    queries on distinct streams are safe (as in the reference, where
+ *    findClosestNodes is const: SURVEY.md §8b "Threading").
+ */
+#ifndef KADGPU_H
+#define KADGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KAD_HASH_LEN 20u            /* reference infohash.h:49 HASH_LEN */
+#define KAD_TARGET_NODES 8u         /* reference routing_table.h:26 TARGET_NODES */
+#define KAD_SEARCH_NODES 14u        /* reference dht.h:314 SEARCH_NODES */
+#define KAD_MAX_COUNT 32u           /* largest `count` the batch kernels accept */
+#define KAD_NO_NODE 0xFFFFFFFFu     /* padding index in result rows */
+
+/* status byte bits (snapshot of Node state at `now`) */
+#define KAD_STATUS_GOOD 0x01u       /* Node::isGood(now)   reference node.cpp:34-40 */
+#define KAD_STATUS_EXPIRED 0x02u    /* Node::isExpired()   reference node.h:67       */
+
+/* kad_table_create flags */
+#define KAD_TABLE_SORTED 0x01u      /* node array ascending by ID (enables NodeCache queries) */
+
+/* error codes */
+#define KAD_OK 0
+#define KAD_ERR_INVALID -1          /* bad argument / shape */
+#define KAD_ERR_HIP -2              /* HIP runtime error */
+#define KAD_ERR_NOMEM -3            /* device allocation failed */
+#define KAD_ERR_UNSUPPORTED -4      /* e.g. count > KAD_MAX_COUNT */
+#define KAD_ERR_NOT_SORTED -5       /* NodeCache query on a table without KAD_TABLE_SORTED */
+#define KAD_ERR_NO_DEVICE -6        /* no usable gfx950 device */
+
+typedef struct kad_table kad_table;
+
+typedef struct kad_table_info {
+    uint32_t n_nodes;
+    uint32_t n_buckets;
+    uint32_t index_base;
+    uint32_t flags;
+    int32_t device;
+    uint32_t rt_radix_bits;         /* log2 of the bucket-locate radix table size */
+    uint32_t nc_radix_bits;         /* log2 of the NodeCache lower_bound radix table size (0 if unsorted) */
+    uint32_t n_good;                /* good nodes under the current status snapshot */
+    uint64_t device_bytes;          /* HBM held by the table */
+} kad_table_info;
+
+/* ---- library ---------------------------------------------------------- */
+const char* kad_last_error(void);
+int kad_version(void);                                  /* 10000*major + 100*minor + patch */
+int kad_device_count(int* out_n);                       /* gfx950 devices visible */
+
+/* ---- table lifetime ----------------------------------------------------- */
+/* Snapshot a RoutingTable (reference routing_table.h:28-79) and/or NodeCache map
+ * (node_cache.h:42-50) into device memory.
+ *   ids           host, n_nodes x 20 bytes; bucket b owns [bucket_offset[b], bucket_offset[b+1])
+ *                 (RoutingTable list order inside a bucket; ties between equal IDs resolve by index)
+ *   status        host, n_nodes status bytes (KAD_STATUS_*)
+ *   bucket_first  host, n_buckets x 20 bytes, ascending (Bucket::first, routing_table.h:33)
+ *   bucket_offset host, n_buckets+1 offsets, bucket_offset[0]=0, bucket_offset[n_buckets]=n_nodes
+ *   n_buckets = 0 builds a NodeCache-only table (requires KAD_TABLE_SORTED).
+ *   flags         KAD_TABLE_SORTED if ids are strictly ascending (checked) */
+int kad_table_create(kad_table** out, int device,
+                     uint32_t n_nodes, const uint8_t* ids, const uint8_t* status,
+                     uint32_t n_buckets, const uint8_t* bucket_first, const uint32_t* bucket_offset,
+                     uint32_t index_base, uint32_t flags);
+int kad_table_destroy(kad_table* t);
+int kad_table_get_info(const kad_table* t, kad_table_info* out);
+
+/* Replace the status snapshot (host bytes, n_nodes). Rebuilds the per-bucket good
+ * prefix sums on the device. Synchronous. */
+int kad_table_update_status(kad_table* t, const uint8_t* status);
+
+/* Upload Node liveness (reference node.h:39-40,105: time, reply_time, expired_)
+ * as int64 nanoseconds of steady_clock + expired flag bytes; host arrays, n_nodes each.
+ * INT64_MIN encodes time_point::min(). Synchronous. */
+int kad_table_set_times(kad_table* t, const int64_t* time_ns, const int64_t* reply_time_ns,
+                        const uint8_t* expired);
+/* Recompute the status snapshot on the device at `now_ns` from the uploaded times:
+ * good = !expired && reply_time >= now-120min && time >= now-10min (node.cpp:34-40,
+ * node.h:91-94), then rebuild the good prefix sums. Async on `stream`. */
+int kad_table_refresh_status(kad_table* t, int64_t now_ns, void* stream);
+
+/* ---- queries: RoutingTable::findClosestNodes ---------------------------- */
+/* Batched RoutingTable::findClosestNodes(target, now, count) (routing_table.cpp:67-111)
+ * on the table's status snapshot. Device pointers:
+ *   targets  q x 20 bytes; out_idx q x count uint32; out_cnt q uint8 (may be NULL).
+ * Row i of out_idx holds the result in the reference's order (ascending XOR
+ * distance), out_cnt[i] entries, padded with KAD_NO_NODE. count <= KAD_MAX_COUNT. */
+int kad_rt_closest_batch(const kad_table* t, const uint8_t* targets, uint32_t q, uint32_t count,
+                         uint32_t* out_idx, uint8_t* out_cnt, void* stream);
+int kad_rt_closest_batch_host(const kad_table* t, const uint8_t* targets, uint32_t q, uint32_t count,
+                              uint32_t* out_idx, uint8_t* out_cnt);
+
+/* Batched RoutingTable::findBucket (routing_table.cpp:113-135): bucket index per
+ * target (0 for targets below the first bucket, as the reference's list walk). */
+int kad_rt_find_bucket_batch(const kad_table* t, const uint8_t* targets, uint32_t q,
+                             uint32_t* out_bucket, void* stream);
+
+/* ---- queries: NodeCache::getCachedNodes --------------------------------- */
+/* Batched NodeCache::getCachedNodes(target, af, count) (node_cache.cpp:36-66) over
+ * one family's map, snapshotted as a KAD_TABLE_SORTED table. Emits non-expired
+ * nodes in the reference's two-pointer walk order (NOT sorted by distance). */
+int kad_nc_closest_batch(const kad_table* t, const uint8_t* targets, uint32_t q, uint32_t count,
+                         uint32_t* out_idx, uint8_t* out_cnt, void* stream);
+int kad_nc_closest_batch_host(const kad_table* t, const uint8_t* targets, uint32_t q, uint32_t count,
+                              uint32_t* out_idx, uint8_t* out_cnt);
+
+/* ---- dual-family batch (Dht::onGetValues asks both tables, dht.cpp:3216-3217) ---- */
+/* Per-query family select: af[i] = 0 -> table4, 1 -> table6 (either may be NULL
+ * if no query selects it). Device pointers. */
+int kad_rt_closest_batch_dual(const kad_table* table4, const kad_table* table6,
+                              const uint8_t* targets, const uint8_t* af, uint32_t q, uint32_t count,
+                              uint32_t* out_idx, uint8_t* out_cnt, void* stream);
+
+/* ---- InfoHash primitives (infohash.h), batched, device pointers ---------- */
+/* out[i] = targets[i].xorCmp(a[i], b[i]) in {-1,0,1}   (infohash.h:131-146) */
+int kad_xor_cmp_batch(const uint8_t* targets, const uint8_t* a, const uint8_t* b, uint32_t n,
+                      int8_t* out, void* stream);
+/* out[i] = InfoHash::commonBits(a[i], b[i]) in [0,160] (infohash.h:106-128) */
+int kad_common_bits_batch(const uint8_t* a, const uint8_t* b, uint32_t n, uint32_t* out, void* stream);
+/* out[i] = a[i].lowbit(), 0xFFFFFFFF for the zero ID     (infohash.h:84-95)  */
+int kad_lowbit_batch(const uint8_t* a, uint32_t n, uint32_t* out, void* stream);
+
+/* ---- synthetic tables (host code; bench and tests) ----------------------- */
+/* n distinct random IDs from std::mt19937_64(seed): ID i = big-endian bytes of
+ * draws (3i, 3i+1) and the top 4 bytes of draw 3i+2; duplicates are rejected and
+ * redrawn. */
+int kad_synth_ids(uint64_t seed, uint32_t n, uint8_t* out_ids);
+/* status mix from std::mt19937_64(seed): u = draw % 100; u < good_pct -> GOOD,
+ * u < good_pct+expired_pct -> EXPIRED, else dubious (0). */
+int kad_synth_status(uint64_t seed, uint32_t n, uint32_t good_pct, uint32_t expired_pct,
+                     uint8_t* out_status);
+/* Sort ids ascending (stable permutation out_perm, may be NULL) in place. */
+int kad_sort_ids(uint32_t n, uint8_t* ids, uint32_t* out_perm);
+/* Uniform-depth table U(depth) over ascending ids: bucket firsts = prefix << (160-depth)
+ * for every prefix in [prefix_lo, prefix_hi) (all 2^depth if prefix_hi == 0), bucket
+ * offsets by ID range. out_first: (prefix_hi-prefix_lo) x 20 bytes, out_offset: +1. */
+int kad_uniform_buckets(uint32_t n, const uint8_t* sorted_ids, uint32_t depth,
+                        uint64_t prefix_lo, uint64_t prefix_hi,
+                        uint8_t* out_first, uint32_t* out_offset);
+/* Split-policy table S (Dht::onNewNode, dht.cpp:903-934, without the my-bucket
+ * restriction; RoutingTable::split, routing_table.cpp:137-163): insert ids in
+ * order, split the found bucket while it holds >= bucket_cap nodes.
+ * Outputs the node order grouped by bucket (out_perm: n indices into ids, list
+ * order inside each bucket), bucket firsts and offsets; *out_n_buckets <= n+1. */
+int kad_split_table(uint32_t n, const uint8_t* ids, uint32_t bucket_cap,
+                    uint32_t* out_perm, uint8_t* out_first, uint32_t* out_offset,
+                    uint32_t* out_n_buckets);
+/* Counter-based uniform swarm shard: every bucket of U(depth) in
+ * [prefix_lo, prefix_hi) gets Poisson(mean) nodes drawn from a hash of
+ * (seed, prefix), so any bucket range is reproducible independently (shards and
+ * their halos). First call with out_ids == NULL returns the node count in *out_n. */
+int kad_synth_uniform_shard(uint64_t seed, uint32_t depth, uint64_t prefix_lo, uint64_t prefix_hi,
+                            double mean_per_bucket, uint32_t good_pct, uint32_t expired_pct,
+                            uint32_t* out_n, uint8_t* out_ids, uint8_t* out_status,
+                            uint32_t* out_offset);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KADGPU_H */

@@ -1,0 +1,112 @@
+"""ctypes binding of libkadgpu.so (the C ABI in include/kadgpu.h).
+
+The library is built in-tree by ``__graft_entry__.build()`` (opendht_amd/csrc/Makefile).
+There is no fallback: if the HIP library is missing, importing the query API raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libkadgpu.so")
+
+KAD_HASH_LEN = 20
+KAD_TARGET_NODES = 8
+KAD_SEARCH_NODES = 14
+KAD_MAX_COUNT = 32
+KAD_NO_NODE = 0xFFFFFFFF
+KAD_STATUS_GOOD = 0x01
+KAD_STATUS_EXPIRED = 0x02
+KAD_TABLE_SORTED = 0x01
+
+ERRORS = {
+    -1: "KAD_ERR_INVALID",
+    -2: "KAD_ERR_HIP",
+    -3: "KAD_ERR_NOMEM",
+    -4: "KAD_ERR_UNSUPPORTED",
+    -5: "KAD_ERR_NOT_SORTED",
+    -6: "KAD_ERR_NO_DEVICE",
+}
+
+# Every symbol include/kadgpu.h declares, with its ctypes signature.
+_P = C.c_void_p
+_u8p = C.POINTER(C.c_uint8)
+_u32p = C.POINTER(C.c_uint32)
+_i64p = C.POINTER(C.c_int64)
+SIGNATURES = {
+    "kad_last_error": (C.c_char_p, []),
+    "kad_version": (C.c_int, []),
+    "kad_device_count": (C.c_int, [C.POINTER(C.c_int)]),
+    "kad_table_create": (C.c_int, [C.POINTER(_P), C.c_int, C.c_uint32, _P, _P, C.c_uint32, _P, _P,
+                                   C.c_uint32, C.c_uint32]),
+    "kad_table_destroy": (C.c_int, [_P]),
+    "kad_table_get_info": (C.c_int, [_P, _P]),
+    "kad_table_update_status": (C.c_int, [_P, _P]),
+    "kad_table_set_times": (C.c_int, [_P, _P, _P, _P]),
+    "kad_table_refresh_status": (C.c_int, [_P, C.c_int64, _P]),
+    "kad_rt_closest_batch": (C.c_int, [_P, _P, C.c_uint32, C.c_uint32, _P, _P, _P]),
+    "kad_rt_closest_batch_host": (C.c_int, [_P, _P, C.c_uint32, C.c_uint32, _P, _P]),
+    "kad_rt_find_bucket_batch": (C.c_int, [_P, _P, C.c_uint32, _P, _P]),
+    "kad_nc_closest_batch": (C.c_int, [_P, _P, C.c_uint32, C.c_uint32, _P, _P, _P]),
+    "kad_nc_closest_batch_host": (C.c_int, [_P, _P, C.c_uint32, C.c_uint32, _P, _P]),
+    "kad_rt_closest_batch_dual": (C.c_int, [_P, _P, _P, _P, C.c_uint32, C.c_uint32, _P, _P, _P]),
+    "kad_xor_cmp_batch": (C.c_int, [_P, _P, _P, C.c_uint32, _P, _P]),
+    "kad_common_bits_batch": (C.c_int, [_P, _P, C.c_uint32, _P, _P]),
+    "kad_lowbit_batch": (C.c_int, [_P, C.c_uint32, _P, _P]),
+    "kad_synth_ids": (C.c_int, [C.c_uint64, C.c_uint32, _P]),
+    "kad_synth_status": (C.c_int, [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, _P]),
+    "kad_sort_ids": (C.c_int, [C.c_uint32, _P, _P]),
+    "kad_uniform_buckets": (C.c_int, [C.c_uint32, _P, C.c_uint32, C.c_uint64, C.c_uint64, _P, _P]),
+    "kad_split_table": (C.c_int, [C.c_uint32, _P, C.c_uint32, _P, _P, _P, _P]),
+    "kad_synth_uniform_shard": (C.c_int, [C.c_uint64, C.c_uint32, C.c_uint64, C.c_uint64, C.c_double,
+                                          C.c_uint32, C.c_uint32, _P, _P, _P, _P]),
+}
+
+
+class KadError(RuntimeError):
+    def __init__(self, code: int, where: str, msg: str):
+        super().__init__(f"{where}: {ERRORS.get(code, code)}: {msg}")
+        self.code = code
+
+
+class table_info(C.Structure):
+    _fields_ = [
+        ("n_nodes", C.c_uint32), ("n_buckets", C.c_uint32), ("index_base", C.c_uint32),
+        ("flags", C.c_uint32), ("device", C.c_int32), ("rt_radix_bits", C.c_uint32),
+        ("nc_radix_bits", C.c_uint32), ("n_good", C.c_uint32), ("device_bytes", C.c_uint64),
+    ]
+
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    """Load libkadgpu.so, raising loudly (no fallback) if it is not built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"{LIB_PATH} is missing: build the HIP engine first (python -c "
+                f"'import __graft_entry__ as g; g.build()'). There is no CPU fallback.")
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc: int, where: str) -> None:
+    if rc != 0:
+        raise KadError(rc, where, lib().kad_last_error().decode(errors="replace"))
+
+
+def ptr(a) -> C.c_void_p | None:
+    """Raw pointer of a numpy array or a torch tensor (host or device); None for None."""
+    if a is None:
+        return None
+    if hasattr(a, "data_ptr"):
+        return C.c_void_p(a.data_ptr())
+    return C.c_void_p(a.ctypes.data)

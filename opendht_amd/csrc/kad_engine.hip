@@ -1,0 +1,947 @@
+// kad_engine.hip — MI355X (gfx950) batched Kademlia closest-node engine.
+//
+// Device kernels for OpenDHT's XOR-distance lookup path and the extern "C" ABI declared in
+// include/kadgpu.h. Reference semantics reproduced bit-exactly (paths relative to the
+// OpenDHT 1.2.1 tree):
+//   InfoHash::xorCmp / cmp / commonBits / lowbit   include/opendht/infohash.h:84-146
+//   RoutingTable::findBucket                        src/routing_table.cpp:113-135
+//   RoutingTable::findClosestNodes                  src/routing_table.cpp:67-111
+//   Node::isGood / isExpired (status snapshot)      src/node.cpp:34-40, include/opendht/node.h:67
+//   NodeCache::getCachedNodes                       src/node_cache.cpp:36-66
+//
+// HBM layout of one table (one address family, one shard), all arrays node- or bucket-major:
+//   key[n]      u64  ID bits 0..63 (InfoHash bytes 0..7, big-endian -> native integer)  HOT
+//   tail[n][3]  u32  ID bits 64..159 (bytes 8..19)                                      COLD: read only
+//                    when two candidates' top-64 XOR distances tie
+//   status[n]   u8   bit0 isGood(now), bit1 isExpired()
+//   dir[B+1]    u32x2 {first node of bucket b, good nodes in buckets < b}
+//   fkey[B], ftail[B][3]   bucket `first` IDs (read only when the radix slot is ambiguous)
+//   rrdx[S+1]   u32  #bucket firsts below radix slot s (bit31: bucket starts exactly at slot)
+//   nrdx[S'+1]  u32  #node IDs below radix slot s (NodeCache lower_bound; sorted tables only)
+//
+// A RoutingTable query, one lane per query:
+//   1. target -> radix slot -> bucket b = upper_bound(first, t) - 1 (clamped to 0)
+//   2. good prefix sums -> least round R whose window W(R) = [max(0,b-1-R), min(B-1,b+R)]
+//      holds >= count good nodes or is the whole table (routing_table.cpp:89-104 closed form)
+//   3. stream W(R)'s keys/status, keep the `count` smallest (XOR distance, index) in a
+//      register-resident sorted list (branch-free compare-exchange chain); exact 160-bit
+//      compare only on a top-64 tie.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/kadgpu.h"
+
+#define KAD_VERSION 100  // 0.1.0
+
+namespace {
+
+thread_local std::string g_err;
+
+int set_err(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                      \
+    do {                                                                                   \
+        hipError_t e_ = (expr);                                                            \
+        if (e_ != hipSuccess)                                                              \
+            return set_err(KAD_ERR_HIP, "%s failed: %s", #expr, hipGetErrorString(e_));    \
+    } while (0)
+
+constexpr uint32_t NONE = 0xFFFFFFFFu;
+constexpr uint32_t RDX_EXACT = 0x80000000u;
+constexpr uint32_t RDX_MASK = 0x7FFFFFFFu;
+constexpr int BLOCK = 256;
+
+// ---------------------------------------------------------------------------------------
+// Device view of a table (passed by value as a kernel argument)
+// ---------------------------------------------------------------------------------------
+struct DevTable {
+    const uint64_t* key;
+    const uint32_t* tail;
+    const uint8_t* status;
+    const uint2* dir;
+    const uint64_t* fkey;
+    const uint32_t* ftail;
+    const uint32_t* rrdx;
+    const uint32_t* nrdx;
+    uint64_t rbase, nbase;
+    uint32_t rshift, rslots, nshift, nslots;
+    uint32_t n, B, index_base, pad_;
+};
+
+struct Target {
+    uint64_t hi;       // bits 0..63
+    uint32_t t2, t3, t4;
+};
+
+__device__ __forceinline__ Target load_target(const uint8_t* targets, uint32_t i) {
+    const uint32_t* p = reinterpret_cast<const uint32_t*>(targets + 20ull * i);
+    Target t;
+    uint32_t w0 = __builtin_bswap32(p[0]), w1 = __builtin_bswap32(p[1]);
+    t.hi = ((uint64_t)w0 << 32) | w1;
+    t.t2 = __builtin_bswap32(p[2]);
+    t.t3 = __builtin_bswap32(p[3]);
+    t.t4 = __builtin_bswap32(p[4]);
+    return t;
+}
+
+// 160-bit compare of (hi, a2, a3, a4) vs (hi', b2, b3, b4): returns <0, 0, >0
+__device__ __forceinline__ int cmp160(uint64_t ah, uint32_t a2, uint32_t a3, uint32_t a4,
+                                      uint64_t bh, uint32_t b2, uint32_t b3, uint32_t b4) {
+    if (ah != bh) return ah < bh ? -1 : 1;
+    if (a2 != b2) return a2 < b2 ? -1 : 1;
+    if (a3 != b3) return a3 < b3 ? -1 : 1;
+    if (a4 != b4) return a4 < b4 ? -1 : 1;
+    return 0;
+}
+
+// Is node a strictly before node b in the reference's result order, given equal top-64
+// XOR distance? Full-width XOR compare on the tails, then insertion order (= index order
+// within one bucket, the only place equal IDs can meet: routing_table.cpp:75-87).
+__device__ __forceinline__ bool tail_less(const DevTable& T, const Target& t, uint32_t a, uint32_t b) {
+    const uint32_t* ta = T.tail + 3ull * a;
+    const uint32_t* tb = T.tail + 3ull * b;
+    uint32_t a2 = ta[0] ^ t.t2, a3 = ta[1] ^ t.t3, a4 = ta[2] ^ t.t4;
+    uint32_t b2 = tb[0] ^ t.t2, b3 = tb[1] ^ t.t3, b4 = tb[2] ^ t.t4;
+    if (a2 != b2) return a2 < b2;
+    if (a3 != b3) return a3 < b3;
+    if (a4 != b4) return a4 < b4;
+    return a < b;
+}
+
+// RoutingTable::findBucket (routing_table.cpp:113-127) = upper_bound(first, t) - 1, clamped to 0.
+__device__ __forceinline__ uint32_t locate_bucket(const DevTable& T, const Target& t) {
+    uint32_t ub;
+    if (t.hi < T.rbase) {
+        ub = 0;
+    } else {
+        uint64_t s = (t.hi - T.rbase) >> T.rshift;
+        if (s >= T.rslots) {
+            ub = T.B;
+        } else {
+            uint32_t r0 = T.rrdx[s], r1 = T.rrdx[s + 1];
+            uint32_t lo = r0 & RDX_MASK, hi = r1 & RDX_MASK;
+            if (hi - lo == 1 && (r0 & RDX_EXACT)) {
+                ub = hi;  // a bucket starts exactly at the slot start <= t
+            } else {
+                // count firsts <= t among [lo, hi)
+                while (lo < hi) {
+                    uint32_t mid = (lo + hi) >> 1;
+                    const uint32_t* ft = T.ftail + 3ull * mid;
+                    int c = cmp160(T.fkey[mid], ft[0], ft[1], ft[2], t.hi, t.t2, t.t3, t.t4);
+                    if (c <= 0) lo = mid + 1; else hi = mid;
+                }
+                ub = lo;
+            }
+        }
+    }
+    return ub == 0 ? 0u : ub - 1;
+}
+
+// NodeCache lower_bound (node_cache.cpp:39) on a sorted table: #ids < t.
+__device__ __forceinline__ uint32_t node_lower_bound(const DevTable& T, const Target& t) {
+    if (t.hi < T.nbase) return 0;
+    uint64_t s = (t.hi - T.nbase) >> T.nshift;
+    if (s >= T.nslots) return T.n;
+    uint32_t lo = T.nrdx[s], hi = T.nrdx[s + 1];
+    while (lo < hi) {
+        uint32_t mid = (lo + hi) >> 1;
+        const uint32_t* tt = T.tail + 3ull * mid;
+        int c = cmp160(T.key[mid], tt[0], tt[1], tt[2], t.hi, t.t2, t.t3, t.t4);
+        if (c < 0) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+
+// ---------------------------------------------------------------------------------------
+// RoutingTable::findClosestNodes, one query per lane (routing_table.cpp:67-111)
+// ---------------------------------------------------------------------------------------
+template <int K>
+__device__ __forceinline__ void rt_query(const DevTable& T, const Target& t, uint32_t count,
+                                         uint32_t* __restrict__ out_row, uint8_t* out_cnt_p) {
+    if (T.B == 0 || count == 0) {
+        for (uint32_t s = 0; s < count; s++) out_row[s] = NONE;
+        if (out_cnt_p) *out_cnt_p = 0;
+        return;
+    }
+    const uint32_t B = T.B;
+    const uint32_t b = locate_bucket(T, t);
+
+    // Window rounds from the good prefix sums: W(r) = [max(0,b-1-r), min(B-1,b+r)].
+    // Prefetch the directory entries of rounds 0..2 as independent loads.
+    auto gp = [&](uint32_t j) { return T.dir[j]; };
+    const uint32_t lo0 = b > 0 ? b - 1 : 0;
+    uint2 L0 = gp(lo0), H0 = gp(b + 1);
+    uint2 L1 = gp(b > 1 ? b - 2 : 0), H1 = gp(min(b + 2, B));
+    uint2 L2 = gp(b > 2 ? b - 3 : 0), H2 = gp(min(b + 3, B));
+    uint32_t lo = lo0, hi = b;
+    uint2 dl = L0, dh = H0;
+    uint32_t good = dh.y - dl.y;
+    if (good < count && (lo > 0 || hi < B - 1)) {
+        if (hi < B - 1) { hi++; dh = H1; }
+        if (lo > 0) { lo--; dl = L1; }
+        good = dh.y - dl.y;
+        if (good < count && (lo > 0 || hi < B - 1)) {
+            if (hi < B - 1) { hi++; dh = H2; }
+            if (lo > 0) { lo--; dl = L2; }
+            good = dh.y - dl.y;
+            while (good < count && (lo > 0 || hi < B - 1)) {
+                if (hi < B - 1) { hi++; dh = gp(hi + 1); }
+                if (lo > 0) { lo--; dl = gp(lo); }
+                good = dh.y - dl.y;
+            }
+        }
+    }
+
+    // Select the `count` closest good nodes of [dl.x, dh.x) by (XOR distance, index).
+    uint64_t dk[K];
+    uint32_t di[K];
+#pragma unroll
+    for (int s = 0; s < K; s++) { dk[s] = ~0ull; di[s] = NONE; }
+
+    const uint32_t beg = dl.x, end = dh.x;
+    // software-pipelined: the next node's status/key loads are in flight while this one is ranked
+    uint8_t st_n = 0;
+    uint64_t k_n = 0;
+    if (beg < end) { st_n = T.status[beg]; k_n = T.key[beg]; }
+    for (uint32_t j = beg; j < end; j++) {
+        const uint8_t st = st_n;
+        const uint64_t kj = k_n;
+        if (j + 1 < end) { st_n = T.status[j + 1]; k_n = T.key[j + 1]; }
+        if (!(st & KAD_STATUS_GOOD)) continue;
+        uint64_t cd = kj ^ t.hi;
+        uint32_t ci = j;
+        bool tie = false;
+#pragma unroll
+        for (int s = 0; s < K; s++) tie |= (cd == dk[s]) & (di[s] != NONE);
+        if (__builtin_expect(!tie, 1)) {
+#pragma unroll
+            for (int s = 0; s < K; s++) {
+                // an empty slot (NONE) sorts after every real node
+                const bool lt = (cd < dk[s]) | ((cd == dk[s]) & (di[s] == NONE));
+                const uint64_t nd = lt ? dk[s] : cd;
+                const uint32_t ni = lt ? di[s] : ci;
+                dk[s] = lt ? cd : dk[s];
+                di[s] = lt ? ci : di[s];
+                cd = nd;
+                ci = ni;
+            }
+        } else {
+#pragma unroll
+            for (int s = 0; s < K; s++) {
+                bool lt;
+                if (ci == NONE) lt = false;
+                else if (di[s] == NONE) lt = true;
+                else if (cd != dk[s]) lt = cd < dk[s];
+                else lt = tail_less(T, t, ci, di[s]);
+                const uint64_t nd = lt ? dk[s] : cd;
+                const uint32_t ni = lt ? di[s] : ci;
+                dk[s] = lt ? cd : dk[s];
+                di[s] = lt ? ci : di[s];
+                cd = nd;
+                ci = ni;
+            }
+        }
+    }
+    const uint32_t m = min(good, count);
+#pragma unroll
+    for (int s = 0; s < K; s++)
+        if ((uint32_t)s < count) out_row[s] = (uint32_t)s < m ? di[s] + T.index_base : NONE;
+    if (out_cnt_p) *out_cnt_p = (uint8_t)m;
+}
+
+template <int K>
+__global__ __launch_bounds__(BLOCK) void rt_closest_kernel(DevTable T, const uint8_t* __restrict__ targets,
+                                                           uint32_t q, uint32_t count,
+                                                           uint32_t* __restrict__ out_idx,
+                                                           uint8_t* __restrict__ out_cnt) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= q) return;
+    const Target t = load_target(targets, i);
+    rt_query<K>(T, t, count, out_idx + (size_t)i * count, out_cnt ? out_cnt + i : nullptr);
+}
+
+template <int K>
+__global__ __launch_bounds__(BLOCK) void rt_closest_dual_kernel(DevTable T4, DevTable T6,
+                                                                const uint8_t* __restrict__ targets,
+                                                                const uint8_t* __restrict__ af, uint32_t q,
+                                                                uint32_t count, uint32_t* __restrict__ out_idx,
+                                                                uint8_t* __restrict__ out_cnt) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= q) return;
+    const Target t = load_target(targets, i);
+    const DevTable& T = af[i] ? T6 : T4;
+    rt_query<K>(T, t, count, out_idx + (size_t)i * count, out_cnt ? out_cnt + i : nullptr);
+}
+
+__global__ __launch_bounds__(BLOCK) void find_bucket_kernel(DevTable T, const uint8_t* __restrict__ targets,
+                                                            uint32_t q, uint32_t* __restrict__ out) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= q) return;
+    out[i] = T.B == 0 ? NONE : locate_bucket(T, load_target(targets, i));
+}
+
+// ---------------------------------------------------------------------------------------
+// NodeCache::getCachedNodes, one query per lane (node_cache.cpp:36-66): two-pointer walk
+// outward from lower_bound(t); p-side taken when xorCmp(p, n) < 0; taking node 0 exhausts
+// the p side; expired nodes are walked over but not emitted.
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(BLOCK) void nc_closest_kernel(DevTable T, const uint8_t* __restrict__ targets,
+                                                           uint32_t q, uint32_t count,
+                                                           uint32_t* __restrict__ out_idx,
+                                                           uint8_t* __restrict__ out_cnt) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= q) return;
+    const Target t = load_target(targets, i);
+    uint32_t* row = out_idx + (size_t)i * count;
+    const uint32_t N = T.n;
+    const uint32_t lb = N ? node_lower_bound(T, t) : 0;
+    uint32_t n = lb < N ? lb : NONE;
+    uint32_t p = N == 0 ? NONE : (lb > 0 ? lb - 1 : (lb < N ? lb : NONE));
+    uint64_t kp = p != NONE ? T.key[p] : 0, kn = n != NONE ? T.key[n] : 0;
+    uint32_t m = 0;
+    while (m < count && (n != NONE || p != NONE)) {
+        uint32_t it;
+        bool take_p;
+        if (p == NONE) take_p = false;
+        else if (n == NONE) take_p = true;
+        else if (p == n) take_p = false;  // xorCmp(x, x) == 0
+        else {
+            const uint64_t dp = kp ^ t.hi, dn = kn ^ t.hi;
+            if (dp != dn) take_p = dp < dn;
+            else {
+                const uint32_t* tp = T.tail + 3ull * p;
+                const uint32_t* tn = T.tail + 3ull * n;
+                take_p = cmp160(0, tp[0] ^ t.t2, tp[1] ^ t.t3, tp[2] ^ t.t4,
+                                0, tn[0] ^ t.t2, tn[1] ^ t.t3, tn[2] ^ t.t4) < 0;
+            }
+        }
+        if (take_p) {
+            it = p;
+            p = p > 0 ? p - 1 : NONE;
+            if (p != NONE) kp = T.key[p];
+        } else {
+            it = n;
+            n = n + 1 < N ? n + 1 : NONE;
+            if (n != NONE) kn = T.key[n];
+        }
+        if (it == 0) p = NONE;
+        if (!(T.status[it] & KAD_STATUS_EXPIRED)) row[m++] = it + T.index_base;
+    }
+    for (uint32_t s = m; s < count; s++) row[s] = NONE;
+    if (out_cnt) out_cnt[i] = (uint8_t)m;
+}
+
+// ---------------------------------------------------------------------------------------
+// InfoHash primitives (infohash.h:84-146)
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ void load_words(const uint8_t* p, uint32_t w[5]) {
+    const uint32_t* q = reinterpret_cast<const uint32_t*>(p);
+#pragma unroll
+    for (int k = 0; k < 5; k++) w[k] = __builtin_bswap32(q[k]);
+}
+
+__global__ void xor_cmp_kernel(const uint8_t* t, const uint8_t* a, const uint8_t* b, uint32_t n, int8_t* out) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n) return;
+    uint32_t tw[5], aw[5], bw[5];
+    load_words(t + 20ull * i, tw);
+    load_words(a + 20ull * i, aw);
+    load_words(b + 20ull * i, bw);
+    int r = 0;
+#pragma unroll
+    for (int k = 4; k >= 0; k--) {
+        const uint32_t x = aw[k] ^ tw[k], y = bw[k] ^ tw[k];
+        r = x != y ? (x < y ? -1 : 1) : r;
+    }
+    out[i] = (int8_t)r;
+}
+
+__global__ void common_bits_kernel(const uint8_t* a, const uint8_t* b, uint32_t n, uint32_t* out) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n) return;
+    uint32_t aw[5], bw[5];
+    load_words(a + 20ull * i, aw);
+    load_words(b + 20ull * i, bw);
+    uint32_t r = 160;
+#pragma unroll
+    for (int k = 4; k >= 0; k--) {
+        const uint32_t x = aw[k] ^ bw[k];
+        r = x ? 32u * k + __builtin_clz(x) : r;
+    }
+    out[i] = r;
+}
+
+__global__ void lowbit_kernel(const uint8_t* a, uint32_t n, uint32_t* out) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n) return;
+    uint32_t aw[5];
+    load_words(a + 20ull * i, aw);
+    uint32_t r = NONE;
+#pragma unroll
+    for (int k = 0; k < 5; k++) r = aw[k] ? 32u * k + 31u - __builtin_ctz(aw[k]) : r;
+    out[i] = r;
+}
+
+// ---------------------------------------------------------------------------------------
+// Table maintenance: status from times, per-bucket good counts, exclusive scan -> dir.y
+// ---------------------------------------------------------------------------------------
+__global__ void status_from_times_kernel(const int64_t* time_ns, const int64_t* reply_ns, const uint8_t* expired,
+                                         uint32_t n, int64_t now, uint8_t* status) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n) return;
+    // node.cpp:34-40 with NODE_GOOD_TIME = 120 min, NODE_EXPIRE_TIME = 10 min (node.h:91-94)
+    const int64_t GOOD = 120LL * 60 * 1000000000LL, EXP = 10LL * 60 * 1000000000LL;
+    const bool ex = expired[i] != 0;
+    const bool good = !ex && reply_ns[i] >= now - GOOD && time_ns[i] >= now - EXP;
+    status[i] = (uint8_t)((good ? KAD_STATUS_GOOD : 0u) | (ex ? KAD_STATUS_EXPIRED : 0u));
+}
+
+__global__ void bucket_good_kernel(const uint8_t* status, const uint2* dir, uint32_t B, uint32_t* cnt) {
+    const uint32_t b = blockIdx.x * BLOCK + threadIdx.x;
+    if (b > B) return;
+    if (b == B) { cnt[b] = 0; return; }
+    uint32_t g = 0;
+    for (uint32_t j = dir[b].x; j < dir[b + 1].x; j++) g += status[j] & KAD_STATUS_GOOD;
+    cnt[b] = g;
+}
+
+constexpr int SCAN_ITEMS = 4;
+constexpr int SCAN_TILE = BLOCK * SCAN_ITEMS;
+
+__device__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* lds, uint32_t& total) {
+    // wave-level inclusive scan via shuffles, then across the 4 waves of the block
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) lds[wid] = x;
+    __syncthreads();
+    uint32_t base = 0;
+    for (int w = 0; w < wid; w++) base += lds[w];
+    total = lds[0] + lds[1] + lds[2] + lds[3];
+    __syncthreads();
+    return base + x - v;
+}
+
+// Tile-local exclusive scan of cnt[0..m) written to out; tile sums to sums[tile].
+__global__ __launch_bounds__(BLOCK) void scan_tiles_kernel(const uint32_t* cnt, uint32_t m, uint32_t* out, uint32_t* sums) {
+    __shared__ uint32_t lds[4];
+    const uint32_t base = blockIdx.x * SCAN_TILE + threadIdx.x * SCAN_ITEMS;
+    uint32_t v[SCAN_ITEMS], s = 0;
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; k++) { v[k] = base + k < m ? cnt[base + k] : 0; s += v[k]; }
+    uint32_t total;
+    uint32_t ex = block_exclusive_scan(s, lds, total);
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; k++) {
+        if (base + k < m) out[base + k] = ex;
+        ex += v[k];
+    }
+    if (threadIdx.x == 0) sums[blockIdx.x] = total;
+}
+
+// Single-block exclusive scan of the tile sums (in place), looping over chunks.
+__global__ __launch_bounds__(BLOCK) void scan_sums_kernel(uint32_t* sums, uint32_t m) {
+    __shared__ uint32_t lds[4];
+    uint32_t carry = 0;
+    for (uint32_t c = 0; c < m; c += BLOCK) {
+        const uint32_t i = c + threadIdx.x;
+        const uint32_t v = i < m ? sums[i] : 0;
+        uint32_t total;
+        const uint32_t ex = block_exclusive_scan(v, lds, total);
+        if (i < m) sums[i] = carry + ex;
+        carry += total;
+    }
+}
+
+__global__ void scan_apply_kernel(const uint32_t* part, const uint32_t* sums, uint32_t m, uint2* dir) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= m) return;
+    dir[i].y = part[i] + sums[i / SCAN_TILE];
+}
+
+inline uint32_t grid_for(uint64_t n) { return (uint32_t)((n + BLOCK - 1) / BLOCK); }
+
+// ---------------------------------------------------------------------------------------
+// Host side
+// ---------------------------------------------------------------------------------------
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        int cur;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+struct Radix {
+    uint64_t base = 0;
+    uint32_t shift = 63, slots = 1, bits = 0;
+};
+
+// Choose (base, shift, slots) so that slot(x) = (x - base) >> shift covers [min_hi, max_hi]
+// with at most 2^target_bits slots and the finest shift that fits.
+Radix choose_radix(uint64_t min_hi, uint64_t max_hi, uint32_t target_bits) {
+    Radix r;
+    const unsigned __int128 S = (unsigned __int128)1 << target_bits;
+    int best = -1;
+    for (int sh = 63; sh >= 0; sh--) {
+        const uint64_t base = sh >= 64 ? 0 : (min_hi >> sh) << sh;
+        const unsigned __int128 slots = (((unsigned __int128)(max_hi - base)) >> sh) + 1;
+        if (slots <= S) best = sh; else break;
+    }
+    if (best < 0) best = 63;
+    r.shift = (uint32_t)best;
+    r.base = (min_hi >> best) << best;
+    r.slots = (uint32_t)((((unsigned __int128)(max_hi - r.base)) >> best) + 1);
+    uint32_t bits = 0;
+    while ((1ull << bits) < r.slots) bits++;
+    r.bits = bits;
+    return r;
+}
+
+inline uint64_t id_hi(const uint8_t* p) {
+    uint64_t x = 0;
+    for (int k = 0; k < 8; k++) x = (x << 8) | p[k];
+    return x;
+}
+inline uint32_t id_word(const uint8_t* p, int w) {
+    return ((uint32_t)p[4 * w] << 24) | ((uint32_t)p[4 * w + 1] << 16) | ((uint32_t)p[4 * w + 2] << 8) | p[4 * w + 3];
+}
+inline bool id_low_zero(const uint8_t* p) {
+    for (int k = 8; k < 20; k++)
+        if (p[k]) return false;
+    return true;
+}
+
+// rdx[s] = #items with hi64 < slot_start(s) for s in [0, slots]; items ascending by hi64.
+// exact_flag: mark slots whose first item starts exactly at the slot start (low bits zero).
+std::vector<uint32_t> build_radix(const Radix& r, uint32_t m, const uint8_t* items, bool exact_flag) {
+    std::vector<uint32_t> rdx(r.slots + 1);
+    uint32_t j = 0;
+    for (uint32_t s = 0; s <= r.slots; s++) {
+        const unsigned __int128 start = (unsigned __int128)r.base + ((unsigned __int128)s << r.shift);
+        while (j < m && (unsigned __int128)id_hi(items + 20ull * j) < start) j++;
+        uint32_t v = j;
+        if (exact_flag && j < m && s < r.slots) {
+            const uint8_t* it = items + 20ull * j;
+            if ((unsigned __int128)id_hi(it) == start && id_low_zero(it)) v |= RDX_EXACT;
+        }
+        rdx[s] = v;
+    }
+    return rdx;
+}
+
+template <class T>
+int dev_upload(T** dptr, const void* src, size_t count, std::vector<void*>& owned, uint64_t& bytes) {
+    *dptr = nullptr;
+    size_t nb = std::max<size_t>(count * sizeof(T), 16);
+    void* p = nullptr;
+    hipError_t e = hipMalloc(&p, nb);
+    if (e != hipSuccess) return set_err(KAD_ERR_NOMEM, "hipMalloc(%zu) failed: %s", nb, hipGetErrorString(e));
+    owned.push_back(p);
+    bytes += nb;
+    if (src && count) HIP_TRY(hipMemcpy(p, src, count * sizeof(T), hipMemcpyHostToDevice));
+    *dptr = static_cast<T*>(p);
+    return KAD_OK;
+}
+
+}  // namespace
+
+struct kad_table {
+    int device = 0;
+    uint32_t flags = 0;
+    DevTable d{};
+    std::vector<void*> owned;
+    uint64_t bytes = 0;
+    uint32_t rbits = 0, nbits = 0;
+    uint8_t* status_mut = nullptr;
+    uint2* dir_mut = nullptr;
+    int64_t* time_ns = nullptr;
+    int64_t* reply_ns = nullptr;
+    uint8_t* expired = nullptr;
+    uint32_t* scan_cnt = nullptr;   // B+1
+    uint32_t* scan_part = nullptr;  // B+1
+    uint32_t* scan_sums = nullptr;  // tiles
+    ~kad_table() {
+        for (void* p : owned) (void)hipFree(p);
+    }
+};
+
+namespace {
+
+bool is_gfx950(int dev) {
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return false;
+    return std::strncmp(prop.gcnArchName, "gfx950", 6) == 0;
+}
+
+// Rebuild dir[].y (good prefix sums) from the device status array. Async on stream.
+int rebuild_good_prefix(kad_table* t, hipStream_t s) {
+    const uint32_t B = t->d.B;
+    if (B == 0) return KAD_OK;
+    const uint32_t m = B + 1;
+    const uint32_t tiles = (m + SCAN_TILE - 1) / SCAN_TILE;
+    hipLaunchKernelGGL(bucket_good_kernel, dim3(grid_for(m)), dim3(BLOCK), 0, s, t->d.status, t->d.dir, B, t->scan_cnt);
+    hipLaunchKernelGGL(scan_tiles_kernel, dim3(tiles), dim3(BLOCK), 0, s, t->scan_cnt, m, t->scan_part, t->scan_sums);
+    hipLaunchKernelGGL(scan_sums_kernel, dim3(1), dim3(BLOCK), 0, s, t->scan_sums, tiles);
+    hipLaunchKernelGGL(scan_apply_kernel, dim3(grid_for(m)), dim3(BLOCK), 0, s, t->scan_part, t->scan_sums, m, t->dir_mut);
+    HIP_TRY(hipGetLastError());
+    return KAD_OK;
+}
+
+int check_count(uint32_t count) {
+    if (count > KAD_MAX_COUNT) return set_err(KAD_ERR_UNSUPPORTED, "count %u > KAD_MAX_COUNT (%u)", count, KAD_MAX_COUNT);
+    return KAD_OK;
+}
+
+template <int K>
+void launch_rt(const DevTable& d, const uint8_t* targets, uint32_t q, uint32_t count, uint32_t* out, uint8_t* cnt,
+               hipStream_t s) {
+    hipLaunchKernelGGL(rt_closest_kernel<K>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
+}
+template <int K>
+void launch_rt_dual(const DevTable& d4, const DevTable& d6, const uint8_t* targets, const uint8_t* af, uint32_t q,
+                    uint32_t count, uint32_t* out, uint8_t* cnt, hipStream_t s) {
+    hipLaunchKernelGGL(rt_closest_dual_kernel<K>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d4, d6, targets, af, q, count,
+                       out, cnt);
+}
+
+int rt_dispatch(const DevTable& d, const uint8_t* targets, uint32_t q, uint32_t count, uint32_t* out, uint8_t* cnt,
+                hipStream_t s) {
+    if (count <= 8) launch_rt<8>(d, targets, q, count, out, cnt, s);
+    else if (count <= 16) launch_rt<16>(d, targets, q, count, out, cnt, s);
+    else launch_rt<32>(d, targets, q, count, out, cnt, s);
+    HIP_TRY(hipGetLastError());
+    return KAD_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* kad_last_error(void) { return g_err.c_str(); }
+int kad_version(void) { return KAD_VERSION; }
+
+int kad_device_count(int* out_n) {
+    if (!out_n) return set_err(KAD_ERR_INVALID, "out_n is NULL");
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+    int k = 0;
+    for (int i = 0; i < n; i++) k += is_gfx950(i);
+    *out_n = k;
+    return KAD_OK;
+}
+
+int kad_table_create(kad_table** out, int device, uint32_t n_nodes, const uint8_t* ids, const uint8_t* status,
+                     uint32_t n_buckets, const uint8_t* bucket_first, const uint32_t* bucket_offset,
+                     uint32_t index_base, uint32_t flags) {
+    if (!out) return set_err(KAD_ERR_INVALID, "out is NULL");
+    *out = nullptr;
+    if (n_nodes && (!ids || !status)) return set_err(KAD_ERR_INVALID, "ids/status NULL with n_nodes=%u", n_nodes);
+    if (n_buckets && (!bucket_first || !bucket_offset)) return set_err(KAD_ERR_INVALID, "bucket arrays NULL");
+    if (n_nodes >= 0x7FFFFFFFu || n_buckets >= 0x7FFFFFFFu) return set_err(KAD_ERR_INVALID, "table too large");
+    if ((uint64_t)index_base + n_nodes > 0xFFFFFFFFull) return set_err(KAD_ERR_INVALID, "index_base + n_nodes overflows u32");
+    // validate directory
+    if (n_buckets) {
+        if (bucket_offset[0] != 0 || bucket_offset[n_buckets] != n_nodes)
+            return set_err(KAD_ERR_INVALID, "bucket_offset must start at 0 and end at n_nodes");
+        for (uint32_t b = 0; b < n_buckets; b++) {
+            if (bucket_offset[b + 1] < bucket_offset[b]) return set_err(KAD_ERR_INVALID, "bucket_offset not monotone at %u", b);
+            if (b && std::memcmp(bucket_first + 20ull * (b - 1), bucket_first + 20ull * b, 20) >= 0)
+                return set_err(KAD_ERR_INVALID, "bucket firsts not strictly ascending at %u", b);
+        }
+    } else if (!(flags & KAD_TABLE_SORTED) && n_nodes) {
+        return set_err(KAD_ERR_INVALID, "a table without buckets must be KAD_TABLE_SORTED");
+    }
+    if (flags & KAD_TABLE_SORTED) {
+        for (uint32_t i = 1; i < n_nodes; i++)
+            if (std::memcmp(ids + 20ull * (i - 1), ids + 20ull * i, 20) >= 0)
+                return set_err(KAD_ERR_NOT_SORTED, "ids not strictly ascending at %u", i);
+    }
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev)
+        return set_err(KAD_ERR_NO_DEVICE, "device %d not available (%d devices)", device, ndev);
+    if (!is_gfx950(device)) return set_err(KAD_ERR_NO_DEVICE, "device %d is not gfx950", device);
+    DeviceGuard g(device);
+
+    auto* t = new kad_table();
+    t->device = device;
+    t->flags = flags;
+    DevTable& d = t->d;
+    d.n = n_nodes;
+    d.B = n_buckets;
+    d.index_base = index_base;
+    int rc;
+    // node arrays
+    std::vector<uint64_t> key(n_nodes);
+    std::vector<uint32_t> tail(3ull * n_nodes);
+    for (uint32_t i = 0; i < n_nodes; i++) {
+        const uint8_t* p = ids + 20ull * i;
+        key[i] = id_hi(p);
+        tail[3ull * i] = id_word(p, 2);
+        tail[3ull * i + 1] = id_word(p, 3);
+        tail[3ull * i + 2] = id_word(p, 4);
+    }
+    uint64_t* dkey; uint32_t* dtail; uint8_t* dst;
+    if ((rc = dev_upload(&dkey, key.data(), n_nodes, t->owned, t->bytes)) ||
+        (rc = dev_upload(&dtail, tail.data(), 3ull * n_nodes, t->owned, t->bytes)) ||
+        (rc = dev_upload(&dst, status, n_nodes, t->owned, t->bytes))) { delete t; return rc; }
+    d.key = dkey; d.tail = dtail; d.status = dst; t->status_mut = dst;
+    std::vector<uint64_t>().swap(key);
+    std::vector<uint32_t>().swap(tail);
+
+    // bucket directory
+    if (n_buckets) {
+        std::vector<uint2> dir(n_buckets + 1);
+        uint32_t g = 0;
+        for (uint32_t b = 0; b <= n_buckets; b++) {
+            dir[b].x = bucket_offset[b];
+            dir[b].y = g;
+            if (b < n_buckets)
+                for (uint32_t j = bucket_offset[b]; j < bucket_offset[b + 1]; j++) g += status[j] & KAD_STATUS_GOOD;
+        }
+        std::vector<uint64_t> fkey(n_buckets);
+        std::vector<uint32_t> ftail(3ull * n_buckets);
+        for (uint32_t b = 0; b < n_buckets; b++) {
+            const uint8_t* p = bucket_first + 20ull * b;
+            fkey[b] = id_hi(p);
+            ftail[3ull * b] = id_word(p, 2);
+            ftail[3ull * b + 1] = id_word(p, 3);
+            ftail[3ull * b + 2] = id_word(p, 4);
+        }
+        uint32_t tb = 1;
+        while ((1u << tb) < n_buckets && tb < 24) tb++;
+        const Radix r = choose_radix(fkey[0], fkey[n_buckets - 1], std::min<uint32_t>(tb + 1, 24));
+        std::vector<uint32_t> rdx = build_radix(r, n_buckets, bucket_first, true);
+        uint2* ddir; uint64_t* dfk; uint32_t *dft, *drdx;
+        if ((rc = dev_upload(&ddir, dir.data(), n_buckets + 1, t->owned, t->bytes)) ||
+            (rc = dev_upload(&dfk, fkey.data(), n_buckets, t->owned, t->bytes)) ||
+            (rc = dev_upload(&dft, ftail.data(), 3ull * n_buckets, t->owned, t->bytes)) ||
+            (rc = dev_upload(&drdx, rdx.data(), rdx.size(), t->owned, t->bytes)) ||
+            (rc = dev_upload(&t->scan_cnt, nullptr, n_buckets + 1, t->owned, t->bytes)) ||
+            (rc = dev_upload(&t->scan_part, nullptr, n_buckets + 1, t->owned, t->bytes)) ||
+            (rc = dev_upload(&t->scan_sums, nullptr, (n_buckets + 1 + SCAN_TILE - 1) / SCAN_TILE, t->owned, t->bytes))) {
+            delete t;
+            return rc;
+        }
+        d.dir = ddir; t->dir_mut = ddir; d.fkey = dfk; d.ftail = dft; d.rrdx = drdx;
+        d.rbase = r.base; d.rshift = r.shift; d.rslots = r.slots; t->rbits = r.bits;
+    }
+    // NodeCache radix
+    if ((flags & KAD_TABLE_SORTED) && n_nodes) {
+        uint32_t tb = 1;
+        while ((1u << tb) < n_nodes && tb < 23) tb++;
+        const Radix r = choose_radix(id_hi(ids), id_hi(ids + 20ull * (n_nodes - 1)), tb);
+        std::vector<uint32_t> rdx = build_radix(r, n_nodes, ids, false);
+        uint32_t* dn;
+        if ((rc = dev_upload(&dn, rdx.data(), rdx.size(), t->owned, t->bytes))) { delete t; return rc; }
+        d.nrdx = dn; d.nbase = r.base; d.nshift = r.shift; d.nslots = r.slots; t->nbits = r.bits;
+    }
+    *out = t;
+    return KAD_OK;
+}
+
+int kad_table_destroy(kad_table* t) {
+    if (!t) return KAD_OK;
+    DeviceGuard g(t->device);
+    (void)hipDeviceSynchronize();
+    delete t;
+    return KAD_OK;
+}
+
+int kad_table_get_info(const kad_table* t, kad_table_info* out) {
+    if (!t || !out) return set_err(KAD_ERR_INVALID, "NULL argument");
+    out->n_nodes = t->d.n;
+    out->n_buckets = t->d.B;
+    out->index_base = t->d.index_base;
+    out->flags = t->flags;
+    out->device = t->device;
+    out->rt_radix_bits = t->rbits;
+    out->nc_radix_bits = t->nbits;
+    out->device_bytes = t->bytes;
+    out->n_good = 0;
+    if (t->d.B) {
+        DeviceGuard g(t->device);
+        uint2 last;
+        HIP_TRY(hipMemcpy(&last, t->d.dir + t->d.B, sizeof last, hipMemcpyDeviceToHost));
+        out->n_good = last.y;
+    }
+    return KAD_OK;
+}
+
+int kad_table_update_status(kad_table* t, const uint8_t* status) {
+    if (!t || (!status && t->d.n)) return set_err(KAD_ERR_INVALID, "NULL argument");
+    DeviceGuard g(t->device);
+    if (t->d.n) HIP_TRY(hipMemcpy(t->status_mut, status, t->d.n, hipMemcpyHostToDevice));
+    int rc = rebuild_good_prefix(t, nullptr);
+    if (rc) return rc;
+    HIP_TRY(hipDeviceSynchronize());
+    return KAD_OK;
+}
+
+int kad_table_set_times(kad_table* t, const int64_t* time_ns, const int64_t* reply_ns, const uint8_t* expired) {
+    if (!t || (t->d.n && (!time_ns || !reply_ns || !expired))) return set_err(KAD_ERR_INVALID, "NULL argument");
+    DeviceGuard g(t->device);
+    int rc;
+    if (!t->time_ns) {
+        if ((rc = dev_upload(&t->time_ns, nullptr, t->d.n, t->owned, t->bytes)) ||
+            (rc = dev_upload(&t->reply_ns, nullptr, t->d.n, t->owned, t->bytes)) ||
+            (rc = dev_upload(&t->expired, nullptr, t->d.n, t->owned, t->bytes)))
+            return rc;
+    }
+    if (t->d.n) {
+        HIP_TRY(hipMemcpy(t->time_ns, time_ns, 8ull * t->d.n, hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(t->reply_ns, reply_ns, 8ull * t->d.n, hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(t->expired, expired, t->d.n, hipMemcpyHostToDevice));
+    }
+    return KAD_OK;
+}
+
+int kad_table_refresh_status(kad_table* t, int64_t now_ns, void* stream) {
+    if (!t) return set_err(KAD_ERR_INVALID, "NULL table");
+    if (!t->time_ns) return set_err(KAD_ERR_INVALID, "kad_table_set_times was not called");
+    DeviceGuard g(t->device);
+    hipStream_t s = (hipStream_t)stream;
+    if (t->d.n)
+        hipLaunchKernelGGL(status_from_times_kernel, dim3(grid_for(t->d.n)), dim3(BLOCK), 0, s, t->time_ns, t->reply_ns,
+                           t->expired, t->d.n, now_ns, t->status_mut);
+    HIP_TRY(hipGetLastError());
+    return rebuild_good_prefix(t, s);
+}
+
+int kad_rt_closest_batch(const kad_table* t, const uint8_t* targets, uint32_t q, uint32_t count, uint32_t* out_idx,
+                         uint8_t* out_cnt, void* stream) {
+    if (!t) return set_err(KAD_ERR_INVALID, "NULL table");
+    int rc = check_count(count);
+    if (rc) return rc;
+    if (q == 0) return KAD_OK;
+    if (!targets || (!out_idx && count)) return set_err(KAD_ERR_INVALID, "NULL buffer");
+    if (count == 0 && !out_cnt) return KAD_OK;
+    if (((uintptr_t)targets & 3) || ((uintptr_t)out_idx & 3)) return set_err(KAD_ERR_INVALID, "device buffers must be 4-byte aligned");
+    DeviceGuard g(t->device);
+    return rt_dispatch(t->d, targets, q, count, out_idx, out_cnt, (hipStream_t)stream);
+}
+
+int kad_rt_closest_batch_dual(const kad_table* t4, const kad_table* t6, const uint8_t* targets, const uint8_t* af,
+                              uint32_t q, uint32_t count, uint32_t* out_idx, uint8_t* out_cnt, void* stream) {
+    if (!t4 && !t6) return set_err(KAD_ERR_INVALID, "both tables NULL");
+    if (t4 && t6 && t4->device != t6->device) return set_err(KAD_ERR_INVALID, "tables on different devices");
+    int rc = check_count(count);
+    if (rc) return rc;
+    if (q == 0) return KAD_OK;
+    if (!targets || !af || !out_idx) return set_err(KAD_ERR_INVALID, "NULL buffer");
+    // A missing family behaves as an empty table (zero results), as an empty RoutingTable does.
+    DevTable empty{};
+    const DevTable& d4 = t4 ? t4->d : empty;
+    const DevTable& d6 = t6 ? t6->d : empty;
+    DeviceGuard g(t4 ? t4->device : t6->device);
+    hipStream_t s = (hipStream_t)stream;
+    if (count <= 8) launch_rt_dual<8>(d4, d6, targets, af, q, count, out_idx, out_cnt, s);
+    else if (count <= 16) launch_rt_dual<16>(d4, d6, targets, af, q, count, out_idx, out_cnt, s);
+    else launch_rt_dual<32>(d4, d6, targets, af, q, count, out_idx, out_cnt, s);
+    HIP_TRY(hipGetLastError());
+    return KAD_OK;
+}
+
+int kad_rt_find_bucket_batch(const kad_table* t, const uint8_t* targets, uint32_t q, uint32_t* out_bucket, void* stream) {
+    if (!t) return set_err(KAD_ERR_INVALID, "NULL table");
+    if (q == 0) return KAD_OK;
+    if (!targets || !out_bucket) return set_err(KAD_ERR_INVALID, "NULL buffer");
+    DeviceGuard g(t->device);
+    hipLaunchKernelGGL(find_bucket_kernel, dim3(grid_for(q)), dim3(BLOCK), 0, (hipStream_t)stream, t->d, targets, q,
+                       out_bucket);
+    HIP_TRY(hipGetLastError());
+    return KAD_OK;
+}
+
+int kad_nc_closest_batch(const kad_table* t, const uint8_t* targets, uint32_t q, uint32_t count, uint32_t* out_idx,
+                         uint8_t* out_cnt, void* stream) {
+    if (!t) return set_err(KAD_ERR_INVALID, "NULL table");
+    if (!(t->flags & KAD_TABLE_SORTED)) return set_err(KAD_ERR_NOT_SORTED, "NodeCache query needs a KAD_TABLE_SORTED table");
+    if (count > 255) return set_err(KAD_ERR_UNSUPPORTED, "count %u > 255", count);
+    if (q == 0) return KAD_OK;
+    if (!targets || (!out_idx && count)) return set_err(KAD_ERR_INVALID, "NULL buffer");
+    DeviceGuard g(t->device);
+    hipLaunchKernelGGL(nc_closest_kernel, dim3(grid_for(q)), dim3(BLOCK), 0, (hipStream_t)stream, t->d, targets, q, count,
+                       out_idx, out_cnt);
+    HIP_TRY(hipGetLastError());
+    return KAD_OK;
+}
+
+static int host_query(const kad_table* t, const uint8_t* targets, uint32_t q, uint32_t count, uint32_t* out_idx,
+                      uint8_t* out_cnt, bool nc) {
+    if (!t) return set_err(KAD_ERR_INVALID, "NULL table");
+    if (q == 0) return KAD_OK;
+    if (!targets || !out_idx) return set_err(KAD_ERR_INVALID, "NULL buffer");
+    DeviceGuard g(t->device);
+    uint8_t* dt = nullptr; uint32_t* di = nullptr; uint8_t* dc = nullptr;
+    const size_t nidx = std::max<size_t>((size_t)q * count, 1);
+    HIP_TRY(hipMalloc(&dt, 20ull * q));
+    if (hipMalloc(&di, 4ull * nidx) != hipSuccess || hipMalloc(&dc, q) != hipSuccess) {
+        (void)hipFree(dt); (void)hipFree(di);
+        return set_err(KAD_ERR_NOMEM, "hipMalloc failed");
+    }
+    int rc = KAD_OK;
+    if (hipMemcpy(dt, targets, 20ull * q, hipMemcpyHostToDevice) != hipSuccess) rc = set_err(KAD_ERR_HIP, "H2D failed");
+    if (!rc) rc = nc ? kad_nc_closest_batch(t, dt, q, count, di, dc, nullptr) : kad_rt_closest_batch(t, dt, q, count, di, dc, nullptr);
+    if (!rc && hipDeviceSynchronize() != hipSuccess) rc = set_err(KAD_ERR_HIP, "kernel failed");
+    if (!rc && count && hipMemcpy(out_idx, di, 4ull * q * count, hipMemcpyDeviceToHost) != hipSuccess) rc = set_err(KAD_ERR_HIP, "D2H failed");
+    if (!rc && out_cnt && hipMemcpy(out_cnt, dc, q, hipMemcpyDeviceToHost) != hipSuccess) rc = set_err(KAD_ERR_HIP, "D2H failed");
+    (void)hipFree(dt); (void)hipFree(di); (void)hipFree(dc);
+    return rc;
+}
+
+int kad_rt_closest_batch_host(const kad_table* t, const uint8_t* targets, uint32_t q, uint32_t count, uint32_t* out_idx,
+                              uint8_t* out_cnt) {
+    return host_query(t, targets, q, count, out_idx, out_cnt, false);
+}
+int kad_nc_closest_batch_host(const kad_table* t, const uint8_t* targets, uint32_t q, uint32_t count, uint32_t* out_idx,
+                              uint8_t* out_cnt) {
+    return host_query(t, targets, q, count, out_idx, out_cnt, true);
+}
+
+int kad_xor_cmp_batch(const uint8_t* targets, const uint8_t* a, const uint8_t* b, uint32_t n, int8_t* out, void* stream) {
+    if (n == 0) return KAD_OK;
+    if (!targets || !a || !b || !out) return set_err(KAD_ERR_INVALID, "NULL buffer");
+    hipLaunchKernelGGL(xor_cmp_kernel, dim3(grid_for(n)), dim3(BLOCK), 0, (hipStream_t)stream, targets, a, b, n, out);
+    HIP_TRY(hipGetLastError());
+    return KAD_OK;
+}
+int kad_common_bits_batch(const uint8_t* a, const uint8_t* b, uint32_t n, uint32_t* out, void* stream) {
+    if (n == 0) return KAD_OK;
+    if (!a || !b || !out) return set_err(KAD_ERR_INVALID, "NULL buffer");
+    hipLaunchKernelGGL(common_bits_kernel, dim3(grid_for(n)), dim3(BLOCK), 0, (hipStream_t)stream, a, b, n, out);
+    HIP_TRY(hipGetLastError());
+    return KAD_OK;
+}
+int kad_lowbit_batch(const uint8_t* a, uint32_t n, uint32_t* out, void* stream) {
+    if (n == 0) return KAD_OK;
+    if (!a || !out) return set_err(KAD_ERR_INVALID, "NULL buffer");
+    hipLaunchKernelGGL(lowbit_kernel, dim3(grid_for(n)), dim3(BLOCK), 0, (hipStream_t)stream, a, n, out);
+    HIP_TRY(hipGetLastError());
+    return KAD_OK;
+}
+
+}  // extern "C"

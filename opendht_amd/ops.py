@@ -1,0 +1,42 @@
+"""Batched InfoHash primitives on the GPU (infohash.h:84-146): device tensors in, device out."""
+from __future__ import annotations
+
+import ctypes as C
+
+from ._lib import check, lib, ptr
+
+
+def _stream(t):
+    import torch
+
+    return C.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def xor_cmp(targets, a, b):
+    """out[i] = targets[i].xorCmp(a[i], b[i]) in {-1, 0, 1} (int8)."""
+    import torch
+
+    n = targets.shape[0]
+    out = torch.empty((n,), dtype=torch.int8, device=targets.device)
+    check(lib().kad_xor_cmp_batch(ptr(targets), ptr(a), ptr(b), n, ptr(out), _stream(targets)), "kad_xor_cmp_batch")
+    return out
+
+
+def common_bits(a, b):
+    """out[i] = InfoHash::commonBits(a[i], b[i]) (int32 view of uint32)."""
+    import torch
+
+    n = a.shape[0]
+    out = torch.empty((n,), dtype=torch.int32, device=a.device)
+    check(lib().kad_common_bits_batch(ptr(a), ptr(b), n, ptr(out), _stream(a)), "kad_common_bits_batch")
+    return out
+
+
+def lowbit(a):
+    """out[i] = a[i].lowbit(); 0xFFFFFFFF for the zero ID (int32 view of uint32)."""
+    import torch
+
+    n = a.shape[0]
+    out = torch.empty((n,), dtype=torch.int32, device=a.device)
+    check(lib().kad_lowbit_batch(ptr(a), n, ptr(out), _stream(a)), "kad_lowbit_batch")
+    return out

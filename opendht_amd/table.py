@@ -1,0 +1,183 @@
+"""DeviceTable: a routing-table / NodeCache snapshot resident in HBM, queried in batches.
+
+Thin Python plumbing over the C ABI (include/kadgpu.h) for tests and bench.py. The drop-in
+host interface for OpenDHT's C++ code is include/kadgpu.hpp (RoutingTable::findClosestNodes,
+NodeCache::getCachedNodes, Dht-style findClosestNodes(id, af, count)).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from ._lib import KAD_TABLE_SORTED, check, lib, ptr
+
+
+def _as_ids(a) -> np.ndarray:
+    a = np.ascontiguousarray(a, dtype=np.uint8)
+    if a.ndim == 1:
+        a = a.reshape(-1, 20)
+    if a.ndim != 2 or a.shape[1] != 20:
+        raise ValueError(f"ids must be (n, 20) uint8, got {a.shape}")
+    return a
+
+
+def _stream_of(t, stream):
+    if stream is not None:
+        return C.c_void_p(stream)
+    import torch
+
+    return C.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+class DeviceTable:
+    """One address family's RoutingTable and/or NodeCache map, snapshotted at `now`.
+
+    ids            (n, 20) uint8, InfoHash bytes; grouped by bucket in list order
+    status         (n,) uint8, bit0 Node::isGood(now), bit1 Node::isExpired()
+    bucket_first   (B, 20) uint8 ascending, or None for a NodeCache-only table
+    bucket_offset  (B+1,) uint32
+    sorted         ids strictly ascending (enables NodeCache queries)
+    """
+
+    def __init__(self, ids, status, bucket_first=None, bucket_offset=None, *, device: int = 0,
+                 index_base: int = 0, sorted: bool = False):
+        L = lib()
+        ids = _as_ids(ids)
+        status = np.ascontiguousarray(status, dtype=np.uint8)
+        n = ids.shape[0]
+        if status.shape != (n,):
+            raise ValueError("status must have one byte per node")
+        if bucket_first is not None:
+            bucket_first = _as_ids(bucket_first)
+            bucket_offset = np.ascontiguousarray(bucket_offset, dtype=np.uint32)
+            B = bucket_first.shape[0]
+            if bucket_offset.shape != (B + 1,):
+                raise ValueError("bucket_offset must have B+1 entries")
+        else:
+            B = 0
+        h = C.c_void_p()
+        rc = L.kad_table_create(C.byref(h), device, n, ptr(ids), ptr(status), B,
+                                ptr(bucket_first) if B else None, ptr(bucket_offset) if B else None,
+                                index_base, KAD_TABLE_SORTED if sorted else 0)
+        check(rc, "kad_table_create")
+        self._h = h
+        self.device = device
+        self.n = n
+        self.B = B
+
+    # -- lifetime ------------------------------------------------------------------------
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            lib().kad_table_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    @property
+    def handle(self) -> C.c_void_p:
+        return self._h
+
+    def info(self) -> dict:
+        inf = _lib.table_info()
+        check(lib().kad_table_get_info(self._h, C.byref(inf)), "kad_table_get_info")
+        return {f: getattr(inf, f) for f, _ in inf._fields_}
+
+    # -- status --------------------------------------------------------------------------
+    def update_status(self, status) -> None:
+        status = np.ascontiguousarray(status, dtype=np.uint8)
+        check(lib().kad_table_update_status(self._h, ptr(status)), "kad_table_update_status")
+
+    def set_times(self, time_ns, reply_time_ns, expired) -> None:
+        a = np.ascontiguousarray(time_ns, dtype=np.int64)
+        b = np.ascontiguousarray(reply_time_ns, dtype=np.int64)
+        e = np.ascontiguousarray(expired, dtype=np.uint8)
+        check(lib().kad_table_set_times(self._h, ptr(a), ptr(b), ptr(e)), "kad_table_set_times")
+
+    def refresh_status(self, now_ns: int, stream=None) -> None:
+        check(lib().kad_table_refresh_status(self._h, C.c_int64(now_ns), _stream_of(self, stream)),
+              "kad_table_refresh_status")
+
+    # -- device-pointer batch queries (torch tensors on this table's device) ---------------
+    def rt_closest(self, targets, count: int, out_idx=None, out_cnt=None, stream=None):
+        """RoutingTable::findClosestNodes over a (q, 20) uint8 device tensor of targets.
+        Returns (idx int32 view of uint32 (q, count), cnt uint8 (q,))."""
+        import torch
+
+        q = targets.shape[0]
+        if out_idx is None:
+            out_idx = torch.empty((q, count), dtype=torch.int32, device=targets.device)
+        if out_cnt is None:
+            out_cnt = torch.empty((q,), dtype=torch.uint8, device=targets.device)
+        check(lib().kad_rt_closest_batch(self._h, ptr(targets), q, count, ptr(out_idx), ptr(out_cnt),
+                                         _stream_of(self, stream)), "kad_rt_closest_batch")
+        return out_idx, out_cnt
+
+    def nc_closest(self, targets, count: int, out_idx=None, out_cnt=None, stream=None):
+        """NodeCache::getCachedNodes over a (q, 20) uint8 device tensor of targets."""
+        import torch
+
+        q = targets.shape[0]
+        if out_idx is None:
+            out_idx = torch.empty((q, count), dtype=torch.int32, device=targets.device)
+        if out_cnt is None:
+            out_cnt = torch.empty((q,), dtype=torch.uint8, device=targets.device)
+        check(lib().kad_nc_closest_batch(self._h, ptr(targets), q, count, ptr(out_idx), ptr(out_cnt),
+                                         _stream_of(self, stream)), "kad_nc_closest_batch")
+        return out_idx, out_cnt
+
+    def find_bucket(self, targets, out=None, stream=None):
+        import torch
+
+        q = targets.shape[0]
+        if out is None:
+            out = torch.empty((q,), dtype=torch.int32, device=targets.device)
+        check(lib().kad_rt_find_bucket_batch(self._h, ptr(targets), q, ptr(out), _stream_of(self, stream)),
+              "kad_rt_find_bucket_batch")
+        return out
+
+    # -- host-pointer synchronous queries ---------------------------------------------------
+    def rt_closest_host(self, targets, count: int):
+        t = _as_ids(targets)
+        q = t.shape[0]
+        idx = np.empty((q, count), dtype=np.uint32)
+        cnt = np.empty((q,), dtype=np.uint8)
+        check(lib().kad_rt_closest_batch_host(self._h, ptr(t), q, count, ptr(idx), ptr(cnt)),
+              "kad_rt_closest_batch_host")
+        return idx, cnt
+
+    def nc_closest_host(self, targets, count: int):
+        t = _as_ids(targets)
+        q = t.shape[0]
+        idx = np.empty((q, count), dtype=np.uint32)
+        cnt = np.empty((q,), dtype=np.uint8)
+        check(lib().kad_nc_closest_batch_host(self._h, ptr(t), q, count, ptr(idx), ptr(cnt)),
+              "kad_nc_closest_batch_host")
+        return idx, cnt
+
+
+def rt_closest_dual(table4: DeviceTable | None, table6: DeviceTable | None, targets, af, count: int,
+                    stream=None):
+    """Per-query family select (af 0 -> v4, 1 -> v6), as Dht::onGetValues asks both tables."""
+    import torch
+
+    q = targets.shape[0]
+    out_idx = torch.empty((q, count), dtype=torch.int32, device=targets.device)
+    out_cnt = torch.empty((q,), dtype=torch.uint8, device=targets.device)
+    s = C.c_void_p(stream) if stream is not None else C.c_void_p(
+        torch.cuda.current_stream(targets.device).cuda_stream)
+    check(lib().kad_rt_closest_batch_dual(table4.handle if table4 else None, table6.handle if table6 else None,
+                                          ptr(targets), ptr(af), q, count, ptr(out_idx), ptr(out_cnt), s),
+          "kad_rt_closest_batch_dual")
+    return out_idx, out_cnt

@@ -1,0 +1,191 @@
+"""ctypes binding of the CPU ORACLE (oracle/liboracle.so). TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this module,
+as the checker or as the timed CPU baseline -- never as the product path.
+Parity status: "parity unpinned" (see kad_oracle.cpp header and DESIGN.md "Oracle").
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "liboracle.so")
+NO_NODE = 0xFFFFFFFF
+
+_P = C.c_void_p
+_SIG = {
+    "orc_cmp": (C.c_int, [_P, _P]),
+    "orc_xor_cmp": (C.c_int, [_P, _P, _P]),
+    "orc_common_bits": (C.c_uint, [_P, _P]),
+    "orc_lowbit": (C.c_uint, [_P]),
+    "orc_get_bit": (C.c_int, [_P, C.c_uint]),
+    "orc_set_bit": (None, [_P, C.c_uint, C.c_int]),
+    "orc_synth_ids": (C.c_int, [C.c_uint64, C.c_uint32, _P]),
+    "orc_synth_status": (C.c_int, [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, _P]),
+    "orc_table_build": (_P, [C.c_uint32, _P, _P, C.c_uint32, _P, _P, C.c_int]),
+    "orc_table_free": (None, [_P]),
+    "orc_table_rt_closest": (C.c_int, [_P, C.c_uint32, _P, C.c_uint32, _P, _P, C.c_int]),
+    "orc_table_nc_closest": (C.c_int, [_P, C.c_uint32, _P, C.c_uint32, _P, _P, C.c_int]),
+    "orc_table_find_bucket": (C.c_int, [_P, C.c_uint32, _P, _P]),
+    "orc_flat_rt_closest": (C.c_int, [C.c_uint32, _P, _P, C.c_uint32, _P, _P, C.c_uint32, _P, C.c_uint32,
+                                      _P, _P, C.c_int]),
+    "orc_flat_nc_closest": (C.c_int, [C.c_uint32, _P, _P, C.c_uint32, _P, C.c_uint32, _P, _P, C.c_int]),
+    "orc_flat_rt_bytes": (C.c_uint64, [C.c_uint32, _P, _P, C.c_uint32, _P, _P, C.c_uint32, _P, C.c_uint32,
+                                       C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+    "orc_split_table": (C.c_int, [C.c_uint32, _P, C.c_uint32, _P, _P, _P, _P]),
+}
+_lib = None
+
+
+def build() -> str:
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return LIB_PATH
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = C.CDLL(LIB_PATH)
+        for k, (r, a) in _SIG.items():
+            f = getattr(L, k)
+            f.restype = r
+            f.argtypes = a
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return None if a is None else C.c_void_p(a.ctypes.data)
+
+
+def _ids(a):
+    a = np.ascontiguousarray(a, dtype=np.uint8)
+    return a.reshape(-1, 20)
+
+
+# ---- primitives (bytes in, int out) ----
+def xor_cmp(t: bytes, a: bytes, b: bytes) -> int:
+    return lib().orc_xor_cmp(t, a, b)
+
+
+def common_bits(a: bytes, b: bytes) -> int:
+    return lib().orc_common_bits(a, b)
+
+
+def lowbit(a: bytes) -> int:
+    return lib().orc_lowbit(a)
+
+
+def cmp(a: bytes, b: bytes) -> int:
+    return lib().orc_cmp(a, b)
+
+
+def synth_ids(n: int, seed: int) -> np.ndarray:
+    out = np.empty((n, 20), dtype=np.uint8)
+    lib().orc_synth_ids(seed, n, _p(out))
+    return out
+
+
+def synth_status(n: int, seed: int, good_pct=80, expired_pct=10) -> np.ndarray:
+    out = np.empty((n,), dtype=np.uint8)
+    lib().orc_synth_status(seed, n, good_pct, expired_pct, _p(out))
+    return out
+
+
+def split_table(ids: np.ndarray, cap: int = 8):
+    ids = _ids(ids)
+    n = ids.shape[0]
+    perm = np.empty((n,), dtype=np.uint32)
+    first = np.empty((n + 1, 20), dtype=np.uint8)
+    off = np.empty((n + 2,), dtype=np.uint32)
+    nb = C.c_uint32()
+    lib().orc_split_table(n, _p(ids), cap, _p(perm), _p(first), _p(off), C.byref(nb))
+    B = nb.value
+    return perm[: off[B]].copy(), first[:B].copy(), off[: B + 1].copy()
+
+
+class FaithfulTable:
+    """Structure-faithful restatement: std::list<Bucket> of std::list<shared_ptr<Node>>,
+    linear findBucket, find_if insertion sort, std::map NodeCache (the "port" CPU baseline)."""
+
+    def __init__(self, ids, status, bucket_first=None, bucket_offset=None, with_nc=False):
+        self.ids = _ids(ids)
+        self.status = np.ascontiguousarray(status, dtype=np.uint8)
+        B = 0 if bucket_first is None else bucket_first.shape[0]
+        self._first = None if bucket_first is None else _ids(bucket_first)
+        self._off = None if bucket_offset is None else np.ascontiguousarray(bucket_offset, dtype=np.uint32)
+        self._h = lib().orc_table_build(self.ids.shape[0], _p(self.ids), _p(self.status), B, _p(self._first),
+                                        _p(self._off), 1 if with_nc else 0)
+
+    def close(self):
+        if self._h:
+            lib().orc_table_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def rt_closest(self, targets, count, nthreads=1):
+        t = _ids(targets)
+        q = t.shape[0]
+        idx = np.empty((q, count), dtype=np.uint32)
+        cnt = np.empty((q,), dtype=np.uint8)
+        lib().orc_table_rt_closest(self._h, q, _p(t), count, _p(idx), _p(cnt), nthreads)
+        return idx, cnt
+
+    def nc_closest(self, targets, count, nthreads=1):
+        t = _ids(targets)
+        q = t.shape[0]
+        idx = np.empty((q, count), dtype=np.uint32)
+        cnt = np.empty((q,), dtype=np.uint8)
+        lib().orc_table_nc_closest(self._h, q, _p(t), count, _p(idx), _p(cnt), nthreads)
+        return idx, cnt
+
+    def find_bucket(self, targets):
+        t = _ids(targets)
+        out = np.empty((t.shape[0],), dtype=np.uint32)
+        lib().orc_table_find_bucket(self._h, t.shape[0], _p(t), _p(out))
+        return out
+
+
+def flat_rt_closest(ids, status, bucket_first, bucket_offset, targets, count, nthreads=1):
+    ids, t, f = _ids(ids), _ids(targets), _ids(bucket_first)
+    st = np.ascontiguousarray(status, dtype=np.uint8)
+    off = np.ascontiguousarray(bucket_offset, dtype=np.uint32)
+    q = t.shape[0]
+    idx = np.empty((q, count), dtype=np.uint32)
+    cnt = np.empty((q,), dtype=np.uint8)
+    lib().orc_flat_rt_closest(ids.shape[0], _p(ids), _p(st), f.shape[0], _p(f), _p(off), q, _p(t), count,
+                              _p(idx), _p(cnt), nthreads)
+    return idx, cnt
+
+
+def flat_nc_closest(sorted_ids, status, targets, count, nthreads=1):
+    ids, t = _ids(sorted_ids), _ids(targets)
+    st = np.ascontiguousarray(status, dtype=np.uint8)
+    q = t.shape[0]
+    idx = np.empty((q, count), dtype=np.uint32)
+    cnt = np.empty((q,), dtype=np.uint8)
+    lib().orc_flat_nc_closest(ids.shape[0], _p(ids), _p(st), q, _p(t), count, _p(idx), _p(cnt), nthreads)
+    return idx, cnt
+
+
+def rt_algorithmic_bytes(ids, status, bucket_first, bucket_offset, targets, count):
+    """SURVEY.md §8d algorithmic bytes: 20 + sum_{b in W(R)} (8 + n_b + 20 g_b) + 4 count, summed
+    over the batch. Returns (total_bytes, visited_buckets, visited_nodes, visited_good)."""
+    ids, t, f = _ids(ids), _ids(targets), _ids(bucket_first)
+    st = np.ascontiguousarray(status, dtype=np.uint8)
+    off = np.ascontiguousarray(bucket_offset, dtype=np.uint32)
+    sb, sn, sg = C.c_uint64(), C.c_uint64(), C.c_uint64()
+    tot = lib().orc_flat_rt_bytes(ids.shape[0], _p(ids), _p(st), f.shape[0], _p(f), _p(off), t.shape[0],
+                                  _p(t), count, C.byref(sb), C.byref(sn), C.byref(sg))
+    return int(tot), sb.value, sn.value, sg.value

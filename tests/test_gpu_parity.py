@@ -1,0 +1,223 @@
+"""GPU parity: the HIP engine (through the C ABI) against the CPU oracle and the golden fixtures.
+Bit-exact on indices and counts, including result order. Run with `pytest -m gpu`."""
+import numpy as np
+import pytest
+import torch
+
+import oracle as O
+import tables as TB
+from opendht_amd import DeviceTable, rt_closest_dual
+from opendht_amd import synth as S
+from opendht_amd._lib import KAD_NO_NODE, KadError
+
+pytestmark = pytest.mark.gpu
+
+COUNTS = (0, 1, 7, 8, 9, 14, 16, 17, 32)
+
+
+def dev(a, gpu):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(gpu)
+
+
+def u32(t):
+    return t.cpu().numpy().view(np.uint32)
+
+
+def make(t, gpu, index_base=0):
+    return DeviceTable(t["ids"], t["status"], t["first"], t["off"], device=gpu.index or 0,
+                       index_base=index_base, sorted=t["sorted"])
+
+
+def check_rt(T, t, targets, gpu, counts=COUNTS):
+    tg = dev(targets, gpu)
+    for k in counts:
+        idx, cnt = T.rt_closest(tg, k)
+        torch.cuda.synchronize()
+        want, wcnt = O.flat_rt_closest(t["ids"], t["status"], t["first"], t["off"], targets, k, nthreads=8)
+        np.testing.assert_array_equal(cnt.cpu().numpy(), wcnt, err_msg=f"{t['name']} k={k} counts")
+        np.testing.assert_array_equal(u32(idx), want, err_msg=f"{t['name']} k={k} indices")
+
+
+def check_nc(T, t, targets, gpu, counts=(0, 1, 8, 14, 32, 64)):
+    tg = dev(targets, gpu)
+    for k in counts:
+        idx, cnt = T.nc_closest(tg, k)
+        torch.cuda.synchronize()
+        want, wcnt = O.flat_nc_closest(t["ids"], t["status"], targets, k, nthreads=8)
+        np.testing.assert_array_equal(cnt.cpu().numpy(), wcnt, err_msg=f"{t['name']} nc k={k} counts")
+        np.testing.assert_array_equal(u32(idx), want, err_msg=f"{t['name']} nc k={k} indices")
+
+
+@pytest.mark.parametrize("t", TB.all_small_tables(), ids=lambda t: t["name"])
+def test_rt_closest_parity(gpu, t):
+    with make(t, gpu) as T:
+        check_rt(T, t, TB.adversarial_targets(t, extra=2048), gpu)
+
+
+@pytest.mark.parametrize("t", [x for x in TB.all_small_tables() if x["sorted"]], ids=lambda t: t["name"])
+def test_nc_closest_parity(gpu, t):
+    with make(t, gpu) as T:
+        check_nc(T, t, TB.adversarial_targets(t, extra=2048), gpu)
+
+
+@pytest.mark.parametrize("t", TB.all_small_tables(), ids=lambda t: t["name"])
+def test_find_bucket_parity(gpu, t):
+    if t["first"].shape[0] == 0:
+        pytest.skip("no buckets")
+    targets = TB.adversarial_targets(t, extra=2048)
+    F = O.FaithfulTable(t["ids"], t["status"], t["first"], t["off"])
+    with make(t, gpu) as T:
+        got = u32(T.find_bucket(dev(targets, gpu)))
+    np.testing.assert_array_equal(got, F.find_bucket(targets))
+
+
+def test_golden_config1(gpu):
+    import os
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "config1.npz"), allow_pickle=False)
+    for shape in ("S", "U"):
+        t = TB.table(g[f"{shape}_ids"], g[f"{shape}_status"], g[f"{shape}_first"], g[f"{shape}_off"],
+                     sorted_=shape == "U", name=shape)
+        tg = dev(g[f"{shape}_targets"], gpu)
+        with make(t, gpu) as T:
+            for k in (8, 16, 32):
+                idx, cnt = T.rt_closest(tg, k)
+                np.testing.assert_array_equal(u32(idx), g[f"{shape}_rt_idx_k{k}"])
+                np.testing.assert_array_equal(cnt.cpu().numpy(), g[f"{shape}_rt_cnt_k{k}"])
+            if shape == "U":
+                for k in (8, 14, 32):
+                    idx, cnt = T.nc_closest(tg, k)
+                    np.testing.assert_array_equal(u32(idx), g[f"U_nc_idx_k{k}"])
+                    np.testing.assert_array_equal(cnt.cpu().numpy(), g[f"U_nc_cnt_k{k}"])
+
+
+def test_host_entry_points(gpu):
+    t = TB.split_config(10_000)
+    targets = TB.adversarial_targets(t)
+    with make(t, gpu) as T:
+        idx, cnt = T.rt_closest_host(targets, 8)
+    want, wcnt = O.flat_rt_closest(t["ids"], t["status"], t["first"], t["off"], targets, 8)
+    np.testing.assert_array_equal(idx, want)
+    np.testing.assert_array_equal(cnt, wcnt)
+    u = TB.uniform_config(10_000, 10)
+    with make(u, gpu) as T:
+        idx, cnt = T.nc_closest_host(targets, 14)
+    want, wcnt = O.flat_nc_closest(u["ids"], u["status"], targets, 14)
+    np.testing.assert_array_equal(idx, want)
+
+
+def test_index_base_and_padding(gpu):
+    t = TB.split_config(257, seed=99)
+    targets = TB.adversarial_targets(t)
+    with make(t, gpu, index_base=1_000_000) as T:
+        idx, cnt = T.rt_closest(dev(targets, gpu), 32)
+    idx, cnt = u32(idx), cnt.cpu().numpy()
+    want, wcnt = O.flat_rt_closest(t["ids"], t["status"], t["first"], t["off"], targets, 32)
+    for i in range(targets.shape[0]):
+        np.testing.assert_array_equal(idx[i, : cnt[i]], want[i, : cnt[i]] + 1_000_000)
+        assert (idx[i, cnt[i]:] == KAD_NO_NODE).all()
+
+
+def test_count_limits(gpu):
+    t = TB.split_config(257, seed=98)
+    with make(t, gpu) as T:
+        with pytest.raises(KadError):
+            T.rt_closest(dev(TB.adversarial_targets(t), gpu), 33)
+
+
+def test_status_update_and_refresh_from_times(gpu):
+    """kad_table_update_status and the device-side Node::isGood(now) refresh (node.cpp:34-40)."""
+    t = TB.split_config(10_000)
+    targets = TB.adversarial_targets(t)
+    rng = np.random.default_rng(5)
+    with make(t, gpu) as T:
+        st2 = rng.choice(np.array([0, 1, 1, 1, 2], np.uint8), size=t["ids"].shape[0])
+        T.update_status(st2)
+        t2 = dict(t, status=st2)
+        check_rt(T, t2, targets, gpu, counts=(8, 32))
+        assert T.info()["n_good"] == int((st2 & 1).sum())
+        # times: steady_clock ns; now = 10 h
+        now = 10 * 3600 * 10**9
+        n = t["ids"].shape[0]
+        m = 60 * 10**9
+        time_ns = now - rng.integers(0, 20, n) * m            # 0..19 min ago
+        reply_ns = now - rng.integers(0, 200, n) * m          # 0..199 min ago
+        reply_ns[rng.random(n) < 0.05] = np.iinfo(np.int64).min  # never replied
+        expired = (rng.random(n) < 0.1).astype(np.uint8)
+        T.set_times(time_ns, reply_ns, expired)
+        T.refresh_status(now)
+        torch.cuda.synchronize()
+        good = (expired == 0) & (reply_ns >= now - 120 * m) & (time_ns >= now - 10 * m)
+        st3 = (good.astype(np.uint8) | (expired << 1)).astype(np.uint8)
+        check_rt(T, dict(t, status=st3), targets, gpu, counts=(8, 14))
+
+
+def test_dual_family(gpu):
+    """Config 4: v4 and v6 tables, per-query af, k = 8/16/32."""
+    t4 = TB.uniform_config(20_000, 11, seed=41)
+    t6 = TB.split_config(20_000, seed=61)
+    targets = S.random_targets(4096, seed=9)
+    af = (np.arange(4096) % 2).astype(np.uint8)
+    with make(t4, gpu) as T4, make(t6, gpu) as T6:
+        for k in (8, 16, 32):
+            idx, cnt = rt_closest_dual(T4, T6, dev(targets, gpu), dev(af, gpu), k)
+            idx, cnt = u32(idx), cnt.cpu().numpy()
+            w4, c4 = O.flat_rt_closest(t4["ids"], t4["status"], t4["first"], t4["off"], targets, k)
+            w6, c6 = O.flat_rt_closest(t6["ids"], t6["status"], t6["first"], t6["off"], targets, k)
+            np.testing.assert_array_equal(idx, np.where(af[:, None] == 0, w4, w6))
+            np.testing.assert_array_equal(cnt, np.where(af == 0, c4, c6))
+
+
+def test_primitives_batch(gpu):
+    from opendht_amd import ops
+    rng = np.random.default_rng(11)
+    n = 5000
+    a = rng.integers(0, 256, (n, 20), dtype=np.uint8)
+    b = a.copy()
+    k = rng.integers(0, 21, n)
+    for i in range(n):  # shared prefixes of every length, incl. equal IDs
+        if k[i] < 20:
+            b[i, k[i]:] = rng.integers(0, 256, 20 - k[i], dtype=np.uint8)
+    a[0] = 0
+    t = rng.integers(0, 256, (n, 20), dtype=np.uint8)
+    xc = ops.xor_cmp(dev(t, gpu), dev(a, gpu), dev(b, gpu)).cpu().numpy()
+    cb = ops.common_bits(dev(a, gpu), dev(b, gpu)).cpu().numpy().view(np.uint32)
+    lb = ops.lowbit(dev(a, gpu)).cpu().numpy().view(np.uint32)
+    for i in range(n):
+        tb, ab, bb = t[i].tobytes(), a[i].tobytes(), b[i].tobytes()
+        assert xc[i] == O.xor_cmp(tb, ab, bb)
+        assert cb[i] == O.common_bits(ab, bb)
+        assert lb[i] == O.lowbit(ab)
+
+
+def test_config2_uniform_1M(gpu):
+    """Config 2: 1M-node table U(17) x 64k queries, k = 8, bit-exact on every query."""
+    n, q = 1_000_000, 65_536
+    t = TB.uniform_config(n, 17)
+    targets = S.random_targets(q)
+    with make(t, gpu) as T:
+        check_rt(T, t, targets, gpu, counts=(8,))
+        check_nc(T, t, targets[:16384], gpu, counts=(14,))
+
+
+def test_config3_full_shard_sample(gpu):
+    """Config 3 at full per-GPU size: one 1/8 shard of the 100M-node U(24) table (~12.5M nodes)
+    plus halo, 1M queries; a 16k-query sample is checked bit-exact against the oracle and every
+    query against size-independent properties (sorted by XOR distance, all good, in window)."""
+    from opendht_amd.sharded import ShardSpec, build_shard
+    spec = ShardSpec(n_shards=8, depth=24, mean_per_bucket=100e6 / 2**24)
+    sh = build_shard(spec, 0)
+    q = 1 << 20
+    targets = spec.targets_for(0, q, seed=1234)
+    with DeviceTable(sh.ids, sh.status, sh.first, sh.off, device=gpu.index or 0, sorted=True) as T:
+        idx, cnt = T.rt_closest(dev(targets, gpu), 8)
+        idx, cnt = u32(idx), cnt.cpu().numpy()
+    assert (cnt == 8).all()
+    sample = np.random.default_rng(0).choice(q, 16384, replace=False)
+    want, wcnt = O.flat_rt_closest(sh.ids, sh.status, sh.first, sh.off, targets[sample], 8, nthreads=8)
+    np.testing.assert_array_equal(idx[sample], want)
+    # properties on all queries: results good and ascending in XOR distance
+    assert (sh.status[idx] & 1).all()
+    key = sh.ids[:, :8].copy().view(">u8").reshape(-1)
+    th = targets[:, :8].copy().view(">u8").reshape(-1)
+    d = key[idx] ^ th[:, None]
+    assert (d[:, 1:] >= d[:, :-1]).all()
