@@ -13,19 +13,26 @@
 //   key[n]      u64  ID bits 0..63 (InfoHash bytes 0..7, big-endian -> native integer)  HOT
 //   tail[n][3]  u32  ID bits 64..159 (bytes 8..19)                                      COLD: read only
 //                    when two candidates' top-64 XOR distances tie
-//   status[n]   u8   bit0 isGood(now), bit1 isExpired()
-//   dir[B+1]    u32x2 {first node of bucket b, good nodes in buckets < b}
+//   status[n]   u8   bit0 isGood(now), bit1 isExpired()   (NodeCache walk, wide-bucket fallback)
+//   dir[B+1]    u32x4 {first node of bucket b (bit31: bucket wider than 32 nodes), good nodes in
+//                      buckets < b, good bitmask of b's nodes, "top-64 bits shared" bitmask}
 //   fkey[B], ftail[B][3]   bucket `first` IDs (read only when the radix slot is ambiguous)
 //   rrdx[S+1]   u32  #bucket firsts below radix slot s (bit31: bucket starts exactly at slot)
 //   nrdx[S'+1]  u32  #node IDs below radix slot s (NodeCache lower_bound; sorted tables only)
 //
 // A RoutingTable query, one lane per query:
-//   1. target -> radix slot -> bucket b = upper_bound(first, t) - 1 (clamped to 0)
-//   2. good prefix sums -> least round R whose window W(R) = [max(0,b-1-R), min(B-1,b+R)]
-//      holds >= count good nodes or is the whole table (routing_table.cpp:89-104 closed form)
-//   3. stream W(R)'s keys/status, keep the `count` smallest (XOR distance, index) in a
-//      register-resident sorted list (branch-free compare-exchange chain); exact 160-bit
-//      compare only on a top-64 tie.
+//   1. target -> radix slot -> bucket b = upper_bound(first, t) - 1 (clamped to 0); tables whose
+//      buckets are exactly the radix slots (U(d)) map the slot to the bucket with no load
+//   2. ONE burst of 2P+3 independent 16-byte directory loads around b; the good prefix sums give
+//      the least round R whose window W(R) = [max(0,b-1-R), min(B-1,b+R)] holds >= count good
+//      nodes or is the whole table (routing_table.cpp:89-104 closed form)
+//   3. W(R)'s keys stream in 16-node chunks of eight 16-byte loads issued back to back (each
+//      lane's window lines are fetched once, not once per node); good bits come from the bucket
+//      masks; the `count` smallest (XOR distance, index) live in a register-resident sorted list
+//      (branch-free insertion chain). The exact 160-bit compare runs only for nodes whose top 64
+//      bits are shared with another node of the table (dup mask), so a top-64 tie is impossible
+//      on the fast path. Windows beyond the prefetch or with >32-node buckets take a per-node
+//      slow path with the same results.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -73,15 +80,20 @@ struct DevTable {
     const uint64_t* key;
     const uint32_t* tail;
     const uint8_t* status;
-    const uint2* dir;
+    const uint4* dir;
     const uint64_t* fkey;
     const uint32_t* ftail;
     const uint32_t* rrdx;
     const uint32_t* nrdx;
     uint64_t rbase, nbase;
     uint32_t rshift, rslots, nshift, nslots;
-    uint32_t n, B, index_base, pad_;
+    uint32_t n, B, index_base, flags;
 };
+
+constexpr uint32_t TF_DIRECT = 1u;   // radix slot s holds exactly bucket s (no locate load)
+constexpr uint32_t TF_HAS_DUP = 2u;  // some nodes share their top 64 ID bits
+constexpr uint32_t WIDE = 0x80000000u;  // dir[].x flag: bucket holds > 32 nodes (masks invalid)
+constexpr uint32_t KEY_PAD = 32;        // key[] is padded so 16-node chunk loads never leave it
 
 struct Target {
     uint64_t hi;       // bits 0..63
@@ -125,6 +137,11 @@ __device__ __forceinline__ bool tail_less(const DevTable& T, const Target& t, ui
 
 // RoutingTable::findBucket (routing_table.cpp:113-127) = upper_bound(first, t) - 1, clamped to 0.
 __device__ __forceinline__ uint32_t locate_bucket(const DevTable& T, const Target& t) {
+    if (T.flags & TF_DIRECT) {
+        if (t.hi < T.rbase) return 0;
+        const uint64_t s = (t.hi - T.rbase) >> T.rshift;
+        return s >= T.B ? T.B - 1 : (uint32_t)s;
+    }
     uint32_t ub;
     if (t.hi < T.rbase) {
         ub = 0;
@@ -170,7 +187,105 @@ __device__ __forceinline__ uint32_t node_lower_bound(const DevTable& T, const Ta
 // ---------------------------------------------------------------------------------------
 // RoutingTable::findClosestNodes, one query per lane (routing_table.cpp:67-111)
 // ---------------------------------------------------------------------------------------
+
+// Register-resident sorted list of the K best (XOR distance, index) pairs. Insertion: once the
+// candidate lands at slot s every later entry shifts down one slot (`sh`), so displaced entries
+// keep their relative order; an empty slot (NONE) sorts after every real node.
 template <int K>
+struct TopK {
+    uint64_t dk[K];
+    uint32_t di[K];
+    __device__ __forceinline__ void init() {
+#pragma unroll
+        for (int s = 0; s < K; s++) { dk[s] = ~0ull; di[s] = NONE; }
+    }
+    // No entry can share the candidate's top-64 distance (the candidate's top 64 ID bits are unique).
+    __device__ __forceinline__ void insert_fast(uint64_t cd, uint32_t ci) {
+        bool sh = false;
+#pragma unroll
+        for (int s = 0; s < K; s++) {
+            const bool lt = sh | (cd < dk[s]) | ((cd == dk[s]) & (di[s] == NONE));
+            sh = lt;
+            const uint64_t nd = lt ? dk[s] : cd;
+            const uint32_t ni = lt ? di[s] : ci;
+            dk[s] = lt ? cd : dk[s];
+            di[s] = lt ? ci : di[s];
+            cd = nd;
+            ci = ni;
+        }
+    }
+    // Exact order: equal top-64 distances fall back to the 96-bit tails, then to the index.
+    __device__ __forceinline__ void insert_exact(const DevTable& T, const Target& t, uint64_t cd, uint32_t ci) {
+        bool sh = false;
+#pragma unroll
+        for (int s = 0; s < K; s++) {
+            bool lt;
+            if (sh) lt = true;
+            else if (di[s] == NONE) lt = true;
+            else if (cd != dk[s]) lt = cd < dk[s];
+            else lt = tail_less(T, t, ci, di[s]);
+            sh = lt;
+            const uint64_t nd = lt ? dk[s] : cd;
+            const uint32_t ni = lt ? di[s] : ci;
+            dk[s] = lt ? cd : dk[s];
+            di[s] = lt ? ci : di[s];
+            cd = nd;
+            ci = ni;
+        }
+    }
+    __device__ __forceinline__ void insert(const DevTable& T, const Target& t, uint64_t key, uint32_t j, bool dup) {
+        if (__builtin_expect(dup, 0)) insert_exact(T, t, key ^ t.hi, j);
+        else insert_fast(key ^ t.hi, j);
+    }
+};
+
+template <int K>
+__device__ __forceinline__ void write_row(const TopK<K>& L, const DevTable& T, uint32_t count, uint32_t m,
+                                          uint32_t* __restrict__ out_row, uint8_t* out_cnt_p) {
+    if (count == (uint32_t)K && (K % 4) == 0) {
+#pragma unroll
+        for (int s = 0; s < K; s += 4) {
+            uint4 v;
+            v.x = (uint32_t)s < m ? L.di[s] + T.index_base : NONE;
+            v.y = (uint32_t)s + 1 < m ? L.di[s + 1] + T.index_base : NONE;
+            v.z = (uint32_t)s + 2 < m ? L.di[s + 2] + T.index_base : NONE;
+            v.w = (uint32_t)s + 3 < m ? L.di[s + 3] + T.index_base : NONE;
+            *reinterpret_cast<uint4*>(out_row + s) = v;
+        }
+    } else {
+#pragma unroll
+        for (int s = 0; s < K; s++)
+            if ((uint32_t)s < count) out_row[s] = (uint32_t)s < m ? L.di[s] + T.index_base : NONE;
+    }
+    if (out_cnt_p) *out_cnt_p = (uint8_t)m;
+}
+
+// Slow path: any window (unbounded rounds, wide buckets), per-node status reads.
+template <int K>
+__device__ __forceinline__ void rt_query_slow(const DevTable& T, const Target& t, uint32_t b, uint32_t count,
+                                           uint32_t* __restrict__ out_row, uint8_t* out_cnt_p) {
+    const uint32_t B = T.B;
+    uint32_t lo = b > 0 ? b - 1 : 0, hi = b;
+    uint4 dl = T.dir[lo], dh = T.dir[hi + 1];
+    uint32_t good = dh.y - dl.y;
+    while (good < count && (lo > 0 || hi < B - 1)) {
+        if (hi < B - 1) { hi++; dh = T.dir[hi + 1]; }
+        if (lo > 0) { lo--; dl = T.dir[lo]; }
+        good = dh.y - dl.y;
+    }
+    TopK<K> L;
+    L.init();
+    const uint32_t beg = dl.x & ~WIDE, end = dh.x & ~WIDE;
+    for (uint32_t j = beg; j < end; j++) {
+        const uint8_t st = T.status[j];
+        if (!(st & KAD_STATUS_GOOD)) continue;
+        L.insert_exact(T, t, T.key[j] ^ t.hi, j);
+    }
+    write_row<K>(L, T, count, min(good, count), out_row, out_cnt_p);
+}
+
+// P = directory prefetch radius: windows with R <= P take the fast path.
+template <int K, int P>
 __device__ __forceinline__ void rt_query(const DevTable& T, const Target& t, uint32_t count,
                                          uint32_t* __restrict__ out_row, uint8_t* out_cnt_p) {
     if (T.B == 0 || count == 0) {
@@ -181,87 +296,84 @@ __device__ __forceinline__ void rt_query(const DevTable& T, const Target& t, uin
     const uint32_t B = T.B;
     const uint32_t b = locate_bucket(T, t);
 
-    // Window rounds from the good prefix sums: W(r) = [max(0,b-1-r), min(B-1,b+r)].
-    // Prefetch the directory entries of rounds 0..2 as independent loads.
-    auto gp = [&](uint32_t j) { return T.dir[j]; };
-    const uint32_t lo0 = b > 0 ? b - 1 : 0;
-    uint2 L0 = gp(lo0), H0 = gp(b + 1);
-    uint2 L1 = gp(b > 1 ? b - 2 : 0), H1 = gp(min(b + 2, B));
-    uint2 L2 = gp(b > 2 ? b - 3 : 0), H2 = gp(min(b + 3, B));
-    uint32_t lo = lo0, hi = b;
-    uint2 dl = L0, dh = H0;
-    uint32_t good = dh.y - dl.y;
-    if (good < count && (lo > 0 || hi < B - 1)) {
-        if (hi < B - 1) { hi++; dh = H1; }
-        if (lo > 0) { lo--; dl = L1; }
-        good = dh.y - dl.y;
-        if (good < count && (lo > 0 || hi < B - 1)) {
-            if (hi < B - 1) { hi++; dh = H2; }
-            if (lo > 0) { lo--; dl = L2; }
-            good = dh.y - dl.y;
-            while (good < count && (lo > 0 || hi < B - 1)) {
-                if (hi < B - 1) { hi++; dh = gp(hi + 1); }
-                if (lo > 0) { lo--; dl = gp(lo); }
-                good = dh.y - dl.y;
-            }
+    // rec[i] = dir[clamp(b - P - 1 + i, 0, B)]: then rec[P - r] = dir[lo_r] and
+    // rec[P + r + 2] = dir[hi_r + 1] for round r (the clamp IS the window's edge clamp).
+    constexpr int NR = 2 * P + 3;
+    uint4 rec[NR];
+#pragma unroll
+    for (int i = 0; i < NR; i++) {
+        const int64_t w = (int64_t)b - (P + 1) + i;
+        rec[i] = T.dir[w < 0 ? 0 : (w > (int64_t)B ? B : (uint32_t)w)];
+    }
+    int R = -1;
+    uint32_t good = 0, nb = 0, ne = 0;
+#pragma unroll
+    for (int r = 0; r <= P; r++) {
+        const bool whole = (b <= (uint32_t)r + 1) & (b + r >= B - 1);
+        const uint32_t g = rec[P + r + 2].y - rec[P - r].y;
+        if (R < 0 && (g >= count || whole)) {
+            R = r;
+            good = g;
+            nb = rec[P - r].x & ~WIDE;
+            ne = rec[P + r + 2].x & ~WIDE;
         }
     }
+    // Fast path needs the window inside the prefetch, no >32-node bucket, and at most 64*MW nodes
+    // from the chunk base. Build the window's good / dup bitmaps once (bit x = node base + x).
+    constexpr int MW = K > 16 ? 2 : 1;
+    const uint32_t base = nb & ~1u;
+    uint32_t wide = 0;
+    uint64_t gm[MW], dm[MW];
+#pragma unroll
+    for (int w = 0; w < MW; w++) gm[w] = dm[w] = 0;
+    const bool has_dup = T.flags & TF_HAS_DUP;
+#pragma unroll
+    for (int i = 0; i < NR; i++) {
+        const bool in = (i >= P - R) & (i <= P + R + 1);
+        wide |= in ? (rec[i].x & WIDE) : 0u;
+        const uint32_t rel = (rec[i].x & ~WIDE) - base;  // >= 0 for window buckets
+#pragma unroll
+        for (int w = 0; w < MW; w++) {
+            const uint32_t sh = rel - 64u * w;  // bits of this word: [64w, 64w+64)
+            const bool fits = in & (rel >= 64u * w ? sh < 64u : (64u * w - rel) < 32u);
+            const uint64_t gz = rec[i].z, dz = rec[i].w;
+            const uint64_t cg = rel >= 64u * w ? (gz << (sh & 63)) : (gz >> ((64u * w - rel) & 63));
+            const uint64_t cdp = rel >= 64u * w ? (dz << (sh & 63)) : (dz >> ((64u * w - rel) & 63));
+            gm[w] |= fits ? cg : 0ull;
+            if (has_dup) dm[w] |= fits ? cdp : 0ull;
+        }
+    }
+    if (R < 0 || wide || ne - base > 64u * MW) {
+        rt_query_slow<K>(T, t, b, count, out_row, out_cnt_p);
+        return;
+    }
 
-    // Select the `count` closest good nodes of [dl.x, dh.x) by (XOR distance, index).
-    uint64_t dk[K];
-    uint32_t di[K];
+    TopK<K> L;
+    L.init();
+    for (uint32_t cb = base; cb < ne; cb += 16) {
+        // eight independent 16-byte loads: the chunk's key lines are fetched once
+        const uint4* kp = reinterpret_cast<const uint4*>(T.key + cb);
+        uint4 kv[8];
 #pragma unroll
-    for (int s = 0; s < K; s++) { dk[s] = ~0ull; di[s] = NONE; }
-
-    const uint32_t beg = dl.x, end = dh.x;
-    // software-pipelined: the next node's status/key loads are in flight while this one is ranked
-    uint8_t st_n = 0;
-    uint64_t k_n = 0;
-    if (beg < end) { st_n = T.status[beg]; k_n = T.key[beg]; }
-    for (uint32_t j = beg; j < end; j++) {
-        const uint8_t st = st_n;
-        const uint64_t kj = k_n;
-        if (j + 1 < end) { st_n = T.status[j + 1]; k_n = T.key[j + 1]; }
-        if (!(st & KAD_STATUS_GOOD)) continue;
-        uint64_t cd = kj ^ t.hi;
-        uint32_t ci = j;
-        bool tie = false;
-#pragma unroll
-        for (int s = 0; s < K; s++) tie |= (cd == dk[s]) & (di[s] != NONE);
-        if (__builtin_expect(!tie, 1)) {
-#pragma unroll
-            for (int s = 0; s < K; s++) {
-                // an empty slot (NONE) sorts after every real node
-                const bool lt = (cd < dk[s]) | ((cd == dk[s]) & (di[s] == NONE));
-                const uint64_t nd = lt ? dk[s] : cd;
-                const uint32_t ni = lt ? di[s] : ci;
-                dk[s] = lt ? cd : dk[s];
-                di[s] = lt ? ci : di[s];
-                cd = nd;
-                ci = ni;
-            }
+        for (int x = 0; x < 8; x++) kv[x] = kp[x];
+        const uint32_t c = cb - base;  // multiple of 16, < 64*MW
+        uint32_t g16, d16;
+        if (MW == 1) {
+            g16 = (uint32_t)(gm[0] >> c) & 0xFFFFu;
+            d16 = (uint32_t)(dm[0] >> c) & 0xFFFFu;
         } else {
+            g16 = (uint32_t)((c < 64 ? gm[0] : gm[MW - 1]) >> (c & 63)) & 0xFFFFu;
+            d16 = (uint32_t)((c < 64 ? dm[0] : dm[MW - 1]) >> (c & 63)) & 0xFFFFu;
+        }
 #pragma unroll
-            for (int s = 0; s < K; s++) {
-                bool lt;
-                if (ci == NONE) lt = false;
-                else if (di[s] == NONE) lt = true;
-                else if (cd != dk[s]) lt = cd < dk[s];
-                else lt = tail_less(T, t, ci, di[s]);
-                const uint64_t nd = lt ? dk[s] : cd;
-                const uint32_t ni = lt ? di[s] : ci;
-                dk[s] = lt ? cd : dk[s];
-                di[s] = lt ? ci : di[s];
-                cd = nd;
-                ci = ni;
-            }
+        for (int x = 0; x < 8; x++) {
+            const uint64_t k0 = ((uint64_t)kv[x].y << 32) | kv[x].x;
+            const uint64_t k1 = ((uint64_t)kv[x].w << 32) | kv[x].z;
+            if ((g16 >> (2 * x)) & 1u) L.insert(T, t, k0, cb + 2 * x, (d16 >> (2 * x)) & 1u);
+            if ((g16 >> (2 * x + 1)) & 1u) L.insert(T, t, k1, cb + 2 * x + 1, (d16 >> (2 * x + 1)) & 1u);
         }
     }
-    const uint32_t m = min(good, count);
-#pragma unroll
-    for (int s = 0; s < K; s++)
-        if ((uint32_t)s < count) out_row[s] = (uint32_t)s < m ? di[s] + T.index_base : NONE;
-    if (out_cnt_p) *out_cnt_p = (uint8_t)m;
+    write_row<K>(L, T, count, min(good, count), out_row, out_cnt_p);
 }
 
 template <int K>
@@ -272,7 +384,7 @@ __global__ __launch_bounds__(BLOCK) void rt_closest_kernel(DevTable T, const uin
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (i >= q) return;
     const Target t = load_target(targets, i);
-    rt_query<K>(T, t, count, out_idx + (size_t)i * count, out_cnt ? out_cnt + i : nullptr);
+    rt_query<K, (K > 16 ? 6 : 3)>(T, t, count, out_idx + (size_t)i * count, out_cnt ? out_cnt + i : nullptr);
 }
 
 template <int K>
@@ -285,7 +397,7 @@ __global__ __launch_bounds__(BLOCK) void rt_closest_dual_kernel(DevTable T4, Dev
     if (i >= q) return;
     const Target t = load_target(targets, i);
     const DevTable& T = af[i] ? T6 : T4;
-    rt_query<K>(T, t, count, out_idx + (size_t)i * count, out_cnt ? out_cnt + i : nullptr);
+    rt_query<K, (K > 16 ? 6 : 3)>(T, t, count, out_idx + (size_t)i * count, out_cnt ? out_cnt + i : nullptr);
 }
 
 __global__ __launch_bounds__(BLOCK) void find_bucket_kernel(DevTable T, const uint8_t* __restrict__ targets,
@@ -411,13 +523,20 @@ __global__ void status_from_times_kernel(const int64_t* time_ns, const int64_t* 
     status[i] = (uint8_t)((good ? KAD_STATUS_GOOD : 0u) | (ex ? KAD_STATUS_EXPIRED : 0u));
 }
 
-__global__ void bucket_good_kernel(const uint8_t* status, const uint2* dir, uint32_t B, uint32_t* cnt) {
+// Per bucket: good count (for the prefix sums) and the good bitmask of its nodes (dir[b].z).
+__global__ void bucket_good_kernel(const uint8_t* status, uint4* dir, uint32_t B, uint32_t* cnt) {
     const uint32_t b = blockIdx.x * BLOCK + threadIdx.x;
     if (b > B) return;
     if (b == B) { cnt[b] = 0; return; }
-    uint32_t g = 0;
-    for (uint32_t j = dir[b].x; j < dir[b + 1].x; j++) g += status[j] & KAD_STATUS_GOOD;
+    const uint32_t j0 = dir[b].x & ~WIDE, j1 = dir[b + 1].x & ~WIDE;
+    uint32_t g = 0, mask = 0;
+    for (uint32_t j = j0; j < j1; j++) {
+        const uint32_t gb = status[j] & KAD_STATUS_GOOD;
+        g += gb;
+        if (j - j0 < 32) mask |= gb << (j - j0);
+    }
     cnt[b] = g;
+    dir[b].z = (j1 - j0 <= 32) ? mask : 0u;
 }
 
 constexpr int SCAN_ITEMS = 4;
@@ -472,7 +591,7 @@ __global__ __launch_bounds__(BLOCK) void scan_sums_kernel(uint32_t* sums, uint32
     }
 }
 
-__global__ void scan_apply_kernel(const uint32_t* part, const uint32_t* sums, uint32_t m, uint2* dir) {
+__global__ void scan_apply_kernel(const uint32_t* part, const uint32_t* sums, uint32_t m, uint4* dir) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (i >= m) return;
     dir[i].y = part[i] + sums[i / SCAN_TILE];
@@ -577,7 +696,7 @@ struct kad_table {
     uint64_t bytes = 0;
     uint32_t rbits = 0, nbits = 0;
     uint8_t* status_mut = nullptr;
-    uint2* dir_mut = nullptr;
+    uint4* dir_mut = nullptr;
     int64_t* time_ns = nullptr;
     int64_t* reply_ns = nullptr;
     uint8_t* expired = nullptr;
@@ -603,7 +722,7 @@ int rebuild_good_prefix(kad_table* t, hipStream_t s) {
     if (B == 0) return KAD_OK;
     const uint32_t m = B + 1;
     const uint32_t tiles = (m + SCAN_TILE - 1) / SCAN_TILE;
-    hipLaunchKernelGGL(bucket_good_kernel, dim3(grid_for(m)), dim3(BLOCK), 0, s, t->d.status, t->d.dir, B, t->scan_cnt);
+    hipLaunchKernelGGL(bucket_good_kernel, dim3(grid_for(m)), dim3(BLOCK), 0, s, t->d.status, t->dir_mut, B, t->scan_cnt);
     hipLaunchKernelGGL(scan_tiles_kernel, dim3(tiles), dim3(BLOCK), 0, s, t->scan_cnt, m, t->scan_part, t->scan_sums);
     hipLaunchKernelGGL(scan_sums_kernel, dim3(1), dim3(BLOCK), 0, s, t->scan_sums, tiles);
     hipLaunchKernelGGL(scan_apply_kernel, dim3(grid_for(m)), dim3(BLOCK), 0, s, t->scan_part, t->scan_sums, m, t->dir_mut);
@@ -694,8 +813,8 @@ int kad_table_create(kad_table** out, int device, uint32_t n_nodes, const uint8_
     d.B = n_buckets;
     d.index_base = index_base;
     int rc;
-    // node arrays
-    std::vector<uint64_t> key(n_nodes);
+    // node arrays: key[] padded by KEY_PAD so chunked 16-byte loads stay inside the allocation
+    std::vector<uint64_t> key(n_nodes + KEY_PAD, ~0ull);
     std::vector<uint32_t> tail(3ull * n_nodes);
     for (uint32_t i = 0; i < n_nodes; i++) {
         const uint8_t* p = ids + 20ull * i;
@@ -704,8 +823,30 @@ int kad_table_create(kad_table** out, int device, uint32_t n_nodes, const uint8_
         tail[3ull * i + 1] = id_word(p, 3);
         tail[3ull * i + 2] = id_word(p, 4);
     }
+    // nodes whose top 64 ID bits are shared with another node: only they can tie on the
+    // top-64 XOR distance, so only they take the exact 160-bit compare
+    std::vector<uint8_t> dup(n_nodes, 0);
+    bool any_dup = false;
+    {
+        bool asc = true;
+        for (uint32_t i = 1; i < n_nodes && asc; i++) asc = key[i - 1] <= key[i];
+        if (asc) {
+            for (uint32_t i = 1; i < n_nodes; i++)
+                if (key[i - 1] == key[i]) { dup[i - 1] = dup[i] = 1; any_dup = true; }
+        } else {
+            std::vector<uint64_t> sk(key.begin(), key.begin() + n_nodes);
+            std::sort(sk.begin(), sk.end());
+            for (uint32_t i = 1; i < n_nodes && !any_dup; i++) any_dup = sk[i - 1] == sk[i];
+            if (any_dup)
+                for (uint32_t i = 0; i < n_nodes; i++) {
+                    auto r = std::equal_range(sk.begin(), sk.end(), key[i]);
+                    dup[i] = (r.second - r.first) > 1;
+                }
+        }
+    }
+    if (any_dup) d.flags |= TF_HAS_DUP;
     uint64_t* dkey; uint32_t* dtail; uint8_t* dst;
-    if ((rc = dev_upload(&dkey, key.data(), n_nodes, t->owned, t->bytes)) ||
+    if ((rc = dev_upload(&dkey, key.data(), key.size(), t->owned, t->bytes)) ||
         (rc = dev_upload(&dtail, tail.data(), 3ull * n_nodes, t->owned, t->bytes)) ||
         (rc = dev_upload(&dst, status, n_nodes, t->owned, t->bytes))) { delete t; return rc; }
     d.key = dkey; d.tail = dtail; d.status = dst; t->status_mut = dst;
@@ -714,13 +855,24 @@ int kad_table_create(kad_table** out, int device, uint32_t n_nodes, const uint8_
 
     // bucket directory
     if (n_buckets) {
-        std::vector<uint2> dir(n_buckets + 1);
+        std::vector<uint4> dir(n_buckets + 1);
         uint32_t g = 0;
         for (uint32_t b = 0; b <= n_buckets; b++) {
             dir[b].x = bucket_offset[b];
             dir[b].y = g;
-            if (b < n_buckets)
-                for (uint32_t j = bucket_offset[b]; j < bucket_offset[b + 1]; j++) g += status[j] & KAD_STATUS_GOOD;
+            dir[b].z = dir[b].w = 0;
+            if (b < n_buckets) {
+                const uint32_t j0 = bucket_offset[b], j1 = bucket_offset[b + 1];
+                if (j1 - j0 > 32) dir[b].x |= WIDE;
+                for (uint32_t j = j0; j < j1; j++) {
+                    const uint32_t gb = status[j] & KAD_STATUS_GOOD;
+                    g += gb;
+                    if (j1 - j0 <= 32) {
+                        dir[b].z |= gb << (j - j0);
+                        dir[b].w |= (uint32_t)dup[j] << (j - j0);
+                    }
+                }
+            }
         }
         std::vector<uint64_t> fkey(n_buckets);
         std::vector<uint32_t> ftail(3ull * n_buckets);
@@ -735,7 +887,11 @@ int kad_table_create(kad_table** out, int device, uint32_t n_nodes, const uint8_
         while ((1u << tb) < n_buckets && tb < 24) tb++;
         const Radix r = choose_radix(fkey[0], fkey[n_buckets - 1], std::min<uint32_t>(tb + 1, 24));
         std::vector<uint32_t> rdx = build_radix(r, n_buckets, bucket_first, true);
-        uint2* ddir; uint64_t* dfk; uint32_t *dft, *drdx;
+        // direct-mapped locate: slot s holds exactly bucket s, starting at the slot start
+        bool direct = r.slots == n_buckets;
+        for (uint32_t sl = 0; sl < r.slots && direct; sl++) direct = rdx[sl] == (sl | RDX_EXACT);
+        if (direct) d.flags |= TF_DIRECT;
+        uint4* ddir; uint64_t* dfk; uint32_t *dft, *drdx;
         if ((rc = dev_upload(&ddir, dir.data(), n_buckets + 1, t->owned, t->bytes)) ||
             (rc = dev_upload(&dfk, fkey.data(), n_buckets, t->owned, t->bytes)) ||
             (rc = dev_upload(&dft, ftail.data(), 3ull * n_buckets, t->owned, t->bytes)) ||
@@ -784,7 +940,7 @@ int kad_table_get_info(const kad_table* t, kad_table_info* out) {
     out->n_good = 0;
     if (t->d.B) {
         DeviceGuard g(t->device);
-        uint2 last;
+        uint4 last;
         HIP_TRY(hipMemcpy(&last, t->d.dir + t->d.B, sizeof last, hipMemcpyDeviceToHost));
         out->n_good = last.y;
     }
