@@ -14,8 +14,10 @@
 //   tail[n][3]  u32  ID bits 64..159 (bytes 8..19)                                      COLD: read only
 //                    when two candidates' top-64 XOR distances tie
 //   status[n]   u8   bit0 isGood(now), bit1 isExpired()   (NodeCache walk, wide-bucket fallback)
-//   dir[B+1]    u32x4 {first node of bucket b (bit31: bucket wider than 32 nodes), good nodes in
-//                      buckets < b, good bitmask of b's nodes, "top-64 bits shared" bitmask}
+//   dir[B+1]    u32x2 {first node of bucket b (bit31: bucket wider than 32 nodes), good bitmask of
+//                      b's nodes}: 8 bytes per bucket, good counts are popcounts
+//   gpre[B+1]   u32  good nodes in buckets < b (slow path / deferred queries)
+//   dmask[B]    u32  "top 64 ID bits shared with another node" bitmask (only if any node has one)
 //   fkey[B], ftail[B][3]   bucket `first` IDs (read only when the radix slot is ambiguous)
 //   rrdx[S+1]   u32  #bucket firsts below radix slot s (bit31: bucket starts exactly at slot)
 //   nrdx[S'+1]  u32  #node IDs below radix slot s (NodeCache lower_bound; sorted tables only)
@@ -80,7 +82,9 @@ struct DevTable {
     const uint64_t* key;
     const uint32_t* tail;
     const uint8_t* status;
-    const uint4* dir;
+    const uint2* dir;
+    const uint32_t* gpre;
+    const uint32_t* dmask;
     const uint64_t* fkey;
     const uint32_t* ftail;
     const uint32_t* rrdx;
@@ -199,20 +203,24 @@ struct TopK {
 #pragma unroll
         for (int s = 0; s < K; s++) { dk[s] = ~0ull; di[s] = NONE; }
     }
-    // No entry can share the candidate's top-64 distance (the candidate's top 64 ID bits are unique).
+    // Fast insertion: valid while every list entry has a distinct top-64 distance and the candidate is
+    // not the all-ones distance (which an empty slot also holds). The list is sorted, so the
+    // compares lt[s] = cd < dk[s] are monotone in s and all K of them are independent: slot s
+    // keeps its entry (!lt[s]), takes the candidate (lt[s] && !lt[s-1]) or its predecessor's entry.
+    // Dependency depth 3 instead of a serial compare/select chain through K slots.
     __device__ __forceinline__ void insert_fast(uint64_t cd, uint32_t ci) {
-        bool sh = false;
+        bool lt[K];
 #pragma unroll
-        for (int s = 0; s < K; s++) {
-            const bool lt = sh | (cd < dk[s]) | ((cd == dk[s]) & (di[s] == NONE));
-            sh = lt;
-            const uint64_t nd = lt ? dk[s] : cd;
-            const uint32_t ni = lt ? di[s] : ci;
-            dk[s] = lt ? cd : dk[s];
-            di[s] = lt ? ci : di[s];
-            cd = nd;
-            ci = ni;
+        for (int s = 0; s < K; s++) lt[s] = cd < dk[s];
+#pragma unroll
+        for (int s = K - 1; s > 0; s--) {
+            const uint64_t nk = lt[s - 1] ? dk[s - 1] : cd;
+            const uint32_t ni = lt[s - 1] ? di[s - 1] : ci;
+            dk[s] = lt[s] ? nk : dk[s];
+            di[s] = lt[s] ? ni : di[s];
         }
+        dk[0] = lt[0] ? cd : dk[0];
+        di[0] = lt[0] ? ci : di[0];
     }
     // Exact order: equal top-64 distances fall back to the 96-bit tails, then to the index.
     __device__ __forceinline__ void insert_exact(const DevTable& T, const Target& t, uint64_t cd, uint32_t ci) {
@@ -232,10 +240,6 @@ struct TopK {
             cd = nd;
             ci = ni;
         }
-    }
-    __device__ __forceinline__ void insert(const DevTable& T, const Target& t, uint64_t key, uint32_t j, bool dup) {
-        if (__builtin_expect(dup, 0)) insert_exact(T, t, key ^ t.hi, j);
-        else insert_fast(key ^ t.hi, j);
     }
 };
 
@@ -266,13 +270,13 @@ __device__ __forceinline__ void rt_query_slow(const DevTable& T, const Target& t
                                            uint32_t* __restrict__ out_row, uint8_t* out_cnt_p) {
     const uint32_t B = T.B;
     uint32_t lo = b > 0 ? b - 1 : 0, hi = b;
-    uint4 dl = T.dir[lo], dh = T.dir[hi + 1];
-    uint32_t good = dh.y - dl.y;
+    uint32_t good = T.gpre[hi + 1] - T.gpre[lo];
     while (good < count && (lo > 0 || hi < B - 1)) {
-        if (hi < B - 1) { hi++; dh = T.dir[hi + 1]; }
-        if (lo > 0) { lo--; dl = T.dir[lo]; }
-        good = dh.y - dl.y;
+        if (hi < B - 1) hi++;
+        if (lo > 0) lo--;
+        good = T.gpre[hi + 1] - T.gpre[lo];
     }
+    const uint2 dl = T.dir[lo], dh = T.dir[hi + 1];
     TopK<K> L;
     L.init();
     const uint32_t beg = dl.x & ~WIDE, end = dh.x & ~WIDE;
@@ -284,96 +288,124 @@ __device__ __forceinline__ void rt_query_slow(const DevTable& T, const Target& t
     write_row<K>(L, T, count, min(good, count), out_row, out_cnt_p);
 }
 
-// P = directory prefetch radius: windows with R <= P take the fast path.
+// Fast path. P = directory prefetch radius. Returns false (nothing written) when the query needs
+// the exact per-node path: window beyond the prefetch (R > P), a bucket wider than 32 nodes, more
+// than 64*MW nodes, a good node whose top 64 bits are shared with another node (possible top-64
+// tie) or a good node at the all-ones top-64 distance (which empty list slots also hold).
 template <int K, int P>
-__device__ __forceinline__ void rt_query(const DevTable& T, const Target& t, uint32_t count,
-                                         uint32_t* __restrict__ out_row, uint8_t* out_cnt_p) {
+__device__ __forceinline__ bool rt_query_fast(const DevTable& T, const Target& t, uint32_t count,
+                                              uint32_t* __restrict__ out_row, uint8_t* out_cnt_p) {
     if (T.B == 0 || count == 0) {
         for (uint32_t s = 0; s < count; s++) out_row[s] = NONE;
         if (out_cnt_p) *out_cnt_p = 0;
-        return;
+        return true;
     }
     const uint32_t B = T.B;
     const uint32_t b = locate_bucket(T, t);
 
-    // rec[i] = dir[clamp(b - P - 1 + i, 0, B)]: then rec[P - r] = dir[lo_r] and
-    // rec[P + r + 2] = dir[hi_r + 1] for round r (the clamp IS the window's edge clamp).
+    // rec[i] = dir[clamp(b - P - 1 + i, 0, B)]: rec[P - r] = dir[lo_r] and rec[P + r + 2] =
+    // dir[hi_r + 1] for round r (the clamp IS the window's edge clamp). 2P+3 independent 8-byte loads.
     constexpr int NR = 2 * P + 3;
-    uint4 rec[NR];
+    uint2 rec[NR];
+    uint32_t g[NR];
 #pragma unroll
     for (int i = 0; i < NR; i++) {
         const int64_t w = (int64_t)b - (P + 1) + i;
         rec[i] = T.dir[w < 0 ? 0 : (w > (int64_t)B ? B : (uint32_t)w)];
     }
+#pragma unroll
+    for (int i = 0; i < NR; i++) {  // good count of bucket b-P-1+i (0 outside the table)
+        const int64_t w = (int64_t)b - (P + 1) + i;
+        g[i] = (w >= 0 && w < (int64_t)B) ? (uint32_t)__builtin_popcount(rec[i].y) : 0u;
+    }
+    // rounds: W(r) = buckets b-1-r .. b+r = rec indices P-r .. P+r+1
     int R = -1;
-    uint32_t good = 0, nb = 0, ne = 0;
+    uint32_t good = g[P] + g[P + 1];
 #pragma unroll
     for (int r = 0; r <= P; r++) {
+        if (r > 0) good += (R < 0) ? g[P - r] + g[P + r + 1] : 0u;
         const bool whole = (b <= (uint32_t)r + 1) & (b + r >= B - 1);
-        const uint32_t g = rec[P + r + 2].y - rec[P - r].y;
-        if (R < 0 && (g >= count || whole)) {
-            R = r;
-            good = g;
-            nb = rec[P - r].x & ~WIDE;
-            ne = rec[P + r + 2].x & ~WIDE;
-        }
+        if (R < 0 && (good >= count || whole)) R = r;
     }
-    // Fast path needs the window inside the prefetch, no >32-node bucket, and at most 64*MW nodes
-    // from the chunk base. Build the window's good / dup bitmaps once (bit x = node base + x).
+    if (R < 0) return false;
+    uint32_t nb = 0, ne = 0, wide = 0;
+#pragma unroll
+    for (int r = 0; r <= P; r++)
+        if (r == R) { nb = rec[P - r].x; ne = rec[P + r + 2].x; }
+#pragma unroll
+    for (int i = 0; i < NR - 1; i++) wide |= (i >= P - R && i <= P + R + 1) ? rec[i].x : 0u;
+    nb &= ~WIDE;
+    ne &= ~WIDE;
+    // Window good bitmap relative to the 64-byte aligned chunk base (bit x = node base + x).
     constexpr int MW = K > 16 ? 2 : 1;
-    const uint32_t base = nb & ~1u;
-    uint32_t wide = 0;
-    uint64_t gm[MW], dm[MW];
+    const uint32_t base = nb & ~7u;
+    if ((wide & WIDE) || ne - base > 64u * MW) return false;
+    uint64_t gm[MW];
 #pragma unroll
-    for (int w = 0; w < MW; w++) gm[w] = dm[w] = 0;
-    const bool has_dup = T.flags & TF_HAS_DUP;
+    for (int w = 0; w < MW; w++) gm[w] = 0;
 #pragma unroll
-    for (int i = 0; i < NR; i++) {
+    for (int i = 0; i < NR - 1; i++) {
         const bool in = (i >= P - R) & (i <= P + R + 1);
-        wide |= in ? (rec[i].x & WIDE) : 0u;
-        const uint32_t rel = (rec[i].x & ~WIDE) - base;  // >= 0 for window buckets
+        const uint32_t rel = (rec[i].x & ~WIDE) - base;  // window buckets start at or after base
 #pragma unroll
         for (int w = 0; w < MW; w++) {
-            const uint32_t sh = rel - 64u * w;  // bits of this word: [64w, 64w+64)
-            const bool fits = in & (rel >= 64u * w ? sh < 64u : (64u * w - rel) < 32u);
-            const uint64_t gz = rec[i].z, dz = rec[i].w;
-            const uint64_t cg = rel >= 64u * w ? (gz << (sh & 63)) : (gz >> ((64u * w - rel) & 63));
-            const uint64_t cdp = rel >= 64u * w ? (dz << (sh & 63)) : (dz >> ((64u * w - rel) & 63));
-            gm[w] |= fits ? cg : 0ull;
-            if (has_dup) dm[w] |= fits ? cdp : 0ull;
+            const uint64_t z = rec[i].y;
+            const uint64_t c = rel >= 64u * w ? (rel - 64u * w < 64u ? z << (rel - 64u * w) : 0ull)
+                                              : (64u * w - rel < 32u ? z >> (64u * w - rel) : 0ull);
+            gm[w] |= in ? c : 0ull;
         }
     }
-    if (R < 0 || wide || ne - base > 64u * MW) {
-        rt_query_slow<K>(T, t, b, count, out_row, out_cnt_p);
-        return;
+    if (T.flags & TF_HAS_DUP) {  // a good node sharing its top 64 bits could tie: exact path
+        uint32_t dup = 0;
+#pragma unroll
+        for (int i = 0; i < NR - 1; i++) {
+            const int64_t w = (int64_t)b - (P + 1) + i;
+            const bool in = (i >= P - R) & (i <= P + R + 1) & (w >= 0) & (w < (int64_t)B);
+            dup |= in ? (T.dmask[in ? (uint32_t)w : 0u] & rec[i].y) : 0u;
+        }
+        if (dup) return false;
     }
 
     TopK<K> L;
     L.init();
-    for (uint32_t cb = base; cb < ne; cb += 16) {
-        // eight independent 16-byte loads: the chunk's key lines are fetched once
-        const uint4* kp = reinterpret_cast<const uint4*>(T.key + cb);
-        uint4 kv[8];
+    bool ones = false;
+    // 8-node (64-byte) chunks; the next chunk's four 16-byte loads are in flight while this one is ranked
+    const uint4* kp = reinterpret_cast<const uint4*>(T.key + base);
+    uint4 nx[4];
 #pragma unroll
-        for (int x = 0; x < 8; x++) kv[x] = kp[x];
-        const uint32_t c = cb - base;  // multiple of 16, < 64*MW
-        uint32_t g16, d16;
-        if (MW == 1) {
-            g16 = (uint32_t)(gm[0] >> c) & 0xFFFFu;
-            d16 = (uint32_t)(dm[0] >> c) & 0xFFFFu;
-        } else {
-            g16 = (uint32_t)((c < 64 ? gm[0] : gm[MW - 1]) >> (c & 63)) & 0xFFFFu;
-            d16 = (uint32_t)((c < 64 ? dm[0] : dm[MW - 1]) >> (c & 63)) & 0xFFFFu;
+    for (int x = 0; x < 4; x++) nx[x] = kp[x];
+    for (uint32_t c = 0; base + c < ne; c += 8) {
+        uint4 kv[4];
+#pragma unroll
+        for (int x = 0; x < 4; x++) kv[x] = nx[x];
+        if (base + c + 8 < ne) {
+#pragma unroll
+            for (int x = 0; x < 4; x++) nx[x] = kp[(c >> 1) + 4 + x];
         }
+        const uint32_t g8 = (uint32_t)((MW == 1 || c < 64 ? gm[0] : gm[MW - 1]) >> (c & 63)) & 0xFFu;
 #pragma unroll
-        for (int x = 0; x < 8; x++) {
-            const uint64_t k0 = ((uint64_t)kv[x].y << 32) | kv[x].x;
-            const uint64_t k1 = ((uint64_t)kv[x].w << 32) | kv[x].z;
-            if ((g16 >> (2 * x)) & 1u) L.insert(T, t, k0, cb + 2 * x, (d16 >> (2 * x)) & 1u);
-            if ((g16 >> (2 * x + 1)) & 1u) L.insert(T, t, k1, cb + 2 * x + 1, (d16 >> (2 * x + 1)) & 1u);
+        for (int x = 0; x < 4; x++) {
+            const uint64_t d0 = (((uint64_t)kv[x].y << 32) | kv[x].x) ^ t.hi;
+            const uint64_t d1 = (((uint64_t)kv[x].w << 32) | kv[x].z) ^ t.hi;
+            if ((g8 >> (2 * x)) & 1u) { ones |= d0 == ~0ull; L.insert_fast(d0, base + c + 2 * x); }
+            if ((g8 >> (2 * x + 1)) & 1u) { ones |= d1 == ~0ull; L.insert_fast(d1, base + c + 2 * x + 1); }
         }
     }
+    if (ones) return false;
     write_row<K>(L, T, count, min(good, count), out_row, out_cnt_p);
+    return true;
+}
+
+// Deferral marker: out_cnt[i] = DEFER_CNT when the caller asked for counts, else row[0] = DEFER_IDX.
+constexpr uint8_t DEFER_CNT = 0xFF;
+constexpr uint32_t DEFER_IDX = 0xFFFFFFFEu;
+
+__device__ __forceinline__ void mark_deferred(uint32_t* out_row, uint8_t* out_cnt_p) {
+    if (out_cnt_p) *out_cnt_p = DEFER_CNT;
+    else out_row[0] = DEFER_IDX;
+}
+__device__ __forceinline__ bool is_deferred(const uint32_t* out_row, const uint8_t* out_cnt_p) {
+    return out_cnt_p ? *out_cnt_p == DEFER_CNT : out_row[0] == DEFER_IDX;
 }
 
 template <int K>
@@ -384,7 +416,24 @@ __global__ __launch_bounds__(BLOCK) void rt_closest_kernel(DevTable T, const uin
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (i >= q) return;
     const Target t = load_target(targets, i);
-    rt_query<K, (K > 16 ? 6 : 3)>(T, t, count, out_idx + (size_t)i * count, out_cnt ? out_cnt + i : nullptr);
+    uint32_t* row = out_idx + (size_t)i * count;
+    uint8_t* cp = out_cnt ? out_cnt + i : nullptr;
+    if (!rt_query_fast<K, (K > 16 ? 6 : 3)>(T, t, count, row, cp)) mark_deferred(row, cp);
+}
+
+// Second pass over the batch: the (rare) queries the fast kernel deferred, exact per-node path.
+template <int K>
+__global__ __launch_bounds__(BLOCK) void rt_closest_deferred_kernel(DevTable T, const uint8_t* __restrict__ targets,
+                                                                    uint32_t q, uint32_t count,
+                                                                    uint32_t* __restrict__ out_idx,
+                                                                    uint8_t* __restrict__ out_cnt) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= q) return;
+    uint32_t* row = out_idx + (size_t)i * count;
+    uint8_t* cp = out_cnt ? out_cnt + i : nullptr;
+    if (!is_deferred(row, cp)) return;
+    const Target t = load_target(targets, i);
+    rt_query_slow<K>(T, t, locate_bucket(T, t), count, row, cp);
 }
 
 template <int K>
@@ -397,7 +446,25 @@ __global__ __launch_bounds__(BLOCK) void rt_closest_dual_kernel(DevTable T4, Dev
     if (i >= q) return;
     const Target t = load_target(targets, i);
     const DevTable& T = af[i] ? T6 : T4;
-    rt_query<K, (K > 16 ? 6 : 3)>(T, t, count, out_idx + (size_t)i * count, out_cnt ? out_cnt + i : nullptr);
+    uint32_t* row = out_idx + (size_t)i * count;
+    uint8_t* cp = out_cnt ? out_cnt + i : nullptr;
+    if (!rt_query_fast<K, (K > 16 ? 6 : 3)>(T, t, count, row, cp)) mark_deferred(row, cp);
+}
+
+template <int K>
+__global__ __launch_bounds__(BLOCK) void rt_closest_dual_deferred_kernel(DevTable T4, DevTable T6,
+                                                                         const uint8_t* __restrict__ targets,
+                                                                         const uint8_t* __restrict__ af, uint32_t q,
+                                                                         uint32_t count, uint32_t* __restrict__ out_idx,
+                                                                         uint8_t* __restrict__ out_cnt) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= q) return;
+    uint32_t* row = out_idx + (size_t)i * count;
+    uint8_t* cp = out_cnt ? out_cnt + i : nullptr;
+    if (!is_deferred(row, cp)) return;
+    const Target t = load_target(targets, i);
+    const DevTable& T = af[i] ? T6 : T4;
+    rt_query_slow<K>(T, t, locate_bucket(T, t), count, row, cp);
 }
 
 __global__ __launch_bounds__(BLOCK) void find_bucket_kernel(DevTable T, const uint8_t* __restrict__ targets,
@@ -523,8 +590,8 @@ __global__ void status_from_times_kernel(const int64_t* time_ns, const int64_t* 
     status[i] = (uint8_t)((good ? KAD_STATUS_GOOD : 0u) | (ex ? KAD_STATUS_EXPIRED : 0u));
 }
 
-// Per bucket: good count (for the prefix sums) and the good bitmask of its nodes (dir[b].z).
-__global__ void bucket_good_kernel(const uint8_t* status, uint4* dir, uint32_t B, uint32_t* cnt) {
+// Per bucket: good count (for the prefix sums) and the good bitmask of its nodes (dir[b].y).
+__global__ void bucket_good_kernel(const uint8_t* status, uint2* dir, uint32_t B, uint32_t* cnt) {
     const uint32_t b = blockIdx.x * BLOCK + threadIdx.x;
     if (b > B) return;
     if (b == B) { cnt[b] = 0; return; }
@@ -536,7 +603,7 @@ __global__ void bucket_good_kernel(const uint8_t* status, uint4* dir, uint32_t B
         if (j - j0 < 32) mask |= gb << (j - j0);
     }
     cnt[b] = g;
-    dir[b].z = (j1 - j0 <= 32) ? mask : 0u;
+    dir[b].y = (j1 - j0 <= 32) ? mask : 0u;
 }
 
 constexpr int SCAN_ITEMS = 4;
@@ -591,10 +658,10 @@ __global__ __launch_bounds__(BLOCK) void scan_sums_kernel(uint32_t* sums, uint32
     }
 }
 
-__global__ void scan_apply_kernel(const uint32_t* part, const uint32_t* sums, uint32_t m, uint4* dir) {
+__global__ void scan_apply_kernel(const uint32_t* part, const uint32_t* sums, uint32_t m, uint32_t* gpre) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (i >= m) return;
-    dir[i].y = part[i] + sums[i / SCAN_TILE];
+    gpre[i] = part[i] + sums[i / SCAN_TILE];
 }
 
 inline uint32_t grid_for(uint64_t n) { return (uint32_t)((n + BLOCK - 1) / BLOCK); }
@@ -696,7 +763,8 @@ struct kad_table {
     uint64_t bytes = 0;
     uint32_t rbits = 0, nbits = 0;
     uint8_t* status_mut = nullptr;
-    uint4* dir_mut = nullptr;
+    uint2* dir_mut = nullptr;
+    uint32_t* gpre_mut = nullptr;
     int64_t* time_ns = nullptr;
     int64_t* reply_ns = nullptr;
     uint8_t* expired = nullptr;
@@ -725,7 +793,7 @@ int rebuild_good_prefix(kad_table* t, hipStream_t s) {
     hipLaunchKernelGGL(bucket_good_kernel, dim3(grid_for(m)), dim3(BLOCK), 0, s, t->d.status, t->dir_mut, B, t->scan_cnt);
     hipLaunchKernelGGL(scan_tiles_kernel, dim3(tiles), dim3(BLOCK), 0, s, t->scan_cnt, m, t->scan_part, t->scan_sums);
     hipLaunchKernelGGL(scan_sums_kernel, dim3(1), dim3(BLOCK), 0, s, t->scan_sums, tiles);
-    hipLaunchKernelGGL(scan_apply_kernel, dim3(grid_for(m)), dim3(BLOCK), 0, s, t->scan_part, t->scan_sums, m, t->dir_mut);
+    hipLaunchKernelGGL(scan_apply_kernel, dim3(grid_for(m)), dim3(BLOCK), 0, s, t->scan_part, t->scan_sums, m, t->gpre_mut);
     HIP_TRY(hipGetLastError());
     return KAD_OK;
 }
@@ -739,12 +807,16 @@ template <int K>
 void launch_rt(const DevTable& d, const uint8_t* targets, uint32_t q, uint32_t count, uint32_t* out, uint8_t* cnt,
                hipStream_t s) {
     hipLaunchKernelGGL(rt_closest_kernel<K>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
+    hipLaunchKernelGGL(rt_closest_deferred_kernel<K>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out,
+                       cnt);
 }
 template <int K>
 void launch_rt_dual(const DevTable& d4, const DevTable& d6, const uint8_t* targets, const uint8_t* af, uint32_t q,
                     uint32_t count, uint32_t* out, uint8_t* cnt, hipStream_t s) {
     hipLaunchKernelGGL(rt_closest_dual_kernel<K>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d4, d6, targets, af, q, count,
                        out, cnt);
+    hipLaunchKernelGGL(rt_closest_dual_deferred_kernel<K>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d4, d6, targets, af, q,
+                       count, out, cnt);
 }
 
 int rt_dispatch(const DevTable& d, const uint8_t* targets, uint32_t q, uint32_t count, uint32_t* out, uint8_t* cnt,
@@ -781,7 +853,8 @@ int kad_table_create(kad_table** out, int device, uint32_t n_nodes, const uint8_
     if (n_nodes && (!ids || !status)) return set_err(KAD_ERR_INVALID, "ids/status NULL with n_nodes=%u", n_nodes);
     if (n_buckets && (!bucket_first || !bucket_offset)) return set_err(KAD_ERR_INVALID, "bucket arrays NULL");
     if (n_nodes >= 0x7FFFFFFFu || n_buckets >= 0x7FFFFFFFu) return set_err(KAD_ERR_INVALID, "table too large");
-    if ((uint64_t)index_base + n_nodes > 0xFFFFFFFFull) return set_err(KAD_ERR_INVALID, "index_base + n_nodes overflows u32");
+    if ((uint64_t)index_base + n_nodes >= 0xFFFFFFFEull)
+        return set_err(KAD_ERR_INVALID, "index_base + n_nodes must stay below 0xFFFFFFFE");
     // validate directory
     if (n_buckets) {
         if (bucket_offset[0] != 0 || bucket_offset[n_buckets] != n_nodes)
@@ -855,12 +928,13 @@ int kad_table_create(kad_table** out, int device, uint32_t n_nodes, const uint8_
 
     // bucket directory
     if (n_buckets) {
-        std::vector<uint4> dir(n_buckets + 1);
+        std::vector<uint2> dir(n_buckets + 1);
+        std::vector<uint32_t> gpre(n_buckets + 1), dmask(any_dup ? n_buckets : 0);
         uint32_t g = 0;
         for (uint32_t b = 0; b <= n_buckets; b++) {
             dir[b].x = bucket_offset[b];
-            dir[b].y = g;
-            dir[b].z = dir[b].w = 0;
+            dir[b].y = 0;
+            gpre[b] = g;
             if (b < n_buckets) {
                 const uint32_t j0 = bucket_offset[b], j1 = bucket_offset[b + 1];
                 if (j1 - j0 > 32) dir[b].x |= WIDE;
@@ -868,10 +942,11 @@ int kad_table_create(kad_table** out, int device, uint32_t n_nodes, const uint8_
                     const uint32_t gb = status[j] & KAD_STATUS_GOOD;
                     g += gb;
                     if (j1 - j0 <= 32) {
-                        dir[b].z |= gb << (j - j0);
-                        dir[b].w |= (uint32_t)dup[j] << (j - j0);
+                        dir[b].y |= gb << (j - j0);
+                        if (any_dup) dmask[b] |= (uint32_t)dup[j] << (j - j0);
                     }
                 }
+                // a wide bucket's dup nodes are handled by the slow path (wide -> deferred)
             }
         }
         std::vector<uint64_t> fkey(n_buckets);
@@ -891,8 +966,10 @@ int kad_table_create(kad_table** out, int device, uint32_t n_nodes, const uint8_
         bool direct = r.slots == n_buckets;
         for (uint32_t sl = 0; sl < r.slots && direct; sl++) direct = rdx[sl] == (sl | RDX_EXACT);
         if (direct) d.flags |= TF_DIRECT;
-        uint4* ddir; uint64_t* dfk; uint32_t *dft, *drdx;
+        uint2* ddir; uint64_t* dfk; uint32_t *dft, *drdx, *dgp, *ddm = nullptr;
         if ((rc = dev_upload(&ddir, dir.data(), n_buckets + 1, t->owned, t->bytes)) ||
+            (rc = dev_upload(&dgp, gpre.data(), n_buckets + 1, t->owned, t->bytes)) ||
+            (any_dup && (rc = dev_upload(&ddm, dmask.data(), n_buckets, t->owned, t->bytes))) ||
             (rc = dev_upload(&dfk, fkey.data(), n_buckets, t->owned, t->bytes)) ||
             (rc = dev_upload(&dft, ftail.data(), 3ull * n_buckets, t->owned, t->bytes)) ||
             (rc = dev_upload(&drdx, rdx.data(), rdx.size(), t->owned, t->bytes)) ||
@@ -902,7 +979,7 @@ int kad_table_create(kad_table** out, int device, uint32_t n_nodes, const uint8_
             delete t;
             return rc;
         }
-        d.dir = ddir; t->dir_mut = ddir; d.fkey = dfk; d.ftail = dft; d.rrdx = drdx;
+        d.dir = ddir; t->dir_mut = ddir; d.gpre = dgp; t->gpre_mut = dgp; d.dmask = ddm; d.fkey = dfk; d.ftail = dft; d.rrdx = drdx;
         d.rbase = r.base; d.rshift = r.shift; d.rslots = r.slots; t->rbits = r.bits;
     }
     // NodeCache radix
@@ -940,9 +1017,9 @@ int kad_table_get_info(const kad_table* t, kad_table_info* out) {
     out->n_good = 0;
     if (t->d.B) {
         DeviceGuard g(t->device);
-        uint4 last;
-        HIP_TRY(hipMemcpy(&last, t->d.dir + t->d.B, sizeof last, hipMemcpyDeviceToHost));
-        out->n_good = last.y;
+        uint32_t last;
+        HIP_TRY(hipMemcpy(&last, t->d.gpre + t->d.B, sizeof last, hipMemcpyDeviceToHost));
+        out->n_good = last;
     }
     return KAD_OK;
 }

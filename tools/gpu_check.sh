@@ -24,4 +24,8 @@ if [ -z "$NO_PROF" ]; then
   cd /tmp && export TMPDIR=/tmp
   step prof 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 $R/bench.py --steps 20 --warmup 5 --no-cpu
 fi
+
+if [ -n "$WITH_PMC" ]; then
+  bash $R/tools/pmc.sh
+fi
 echo done >> $O/steps.log
