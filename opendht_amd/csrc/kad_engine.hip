@@ -40,6 +40,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -89,6 +90,7 @@ struct DevTable {
     const uint32_t* ftail;
     const uint32_t* rrdx;
     const uint32_t* nrdx;
+    const uint4* bl;  // bucket lines (TF_BL): 64 bytes per bucket, see rt_bl_kernel
     uint64_t rbase, nbase;
     uint32_t rshift, rslots, nshift, nslots;
     uint32_t n, B, index_base, flags;
@@ -96,6 +98,10 @@ struct DevTable {
 
 constexpr uint32_t TF_DIRECT = 1u;   // radix slot s holds exactly bucket s (no locate load)
 constexpr uint32_t TF_HAS_DUP = 2u;  // some nodes share their top 64 ID bits
+constexpr uint32_t TF_BL = 4u;       // bucket-line layout present (direct-mapped, depth <= 32)
+constexpr uint32_t BL_CAP = 14;      // node keys per 64-byte bucket line
+constexpr uint32_t BL_OVF = 31;      // n field of a bucket that does not fit its line
+constexpr uint32_t BL_OFF_MASK = (1u << 27) - 1;
 constexpr uint32_t WIDE = 0x80000000u;  // dir[].x flag: bucket holds > 32 nodes (masks invalid)
 constexpr uint32_t KEY_PAD = 32;        // key[] is padded so 16-node chunk loads never leave it
 
@@ -288,31 +294,40 @@ __device__ __forceinline__ void rt_query_slow(const DevTable& T, const Target& t
     write_row<K>(L, T, count, min(good, count), out_row, out_cnt_p);
 }
 
-// Fast path. P = directory prefetch radius. Returns false (nothing written) when the query needs
-// the exact per-node path: window beyond the prefetch (R > P), a bucket wider than 32 nodes, more
-// than 64*MW nodes, a good node whose top 64 bits are shared with another node (possible top-64
-// tie) or a good node at the all-ones top-64 distance (which empty list slots also hold).
-template <int K, int P>
-__device__ __forceinline__ bool rt_query_fast(const DevTable& T, const Target& t, uint32_t count,
-                                              uint32_t* __restrict__ out_row, uint8_t* out_cnt_p) {
-    if (T.B == 0 || count == 0) {
-        for (uint32_t s = 0; s < count; s++) out_row[s] = NONE;
-        if (out_cnt_p) *out_cnt_p = 0;
-        return true;
-    }
-    const uint32_t B = T.B;
-    const uint32_t b = locate_bucket(T, t);
+// ---- fast path, phase 1: the window ------------------------------------------------------
+// P = directory prefetch radius (2P+3 records around b). The fast path handles windows with
+// R <= P, no bucket wider than 32 nodes, at most 64*MW nodes from the 64-byte aligned base, no good
+// node whose top 64 bits are shared with another node (a possible top-64 tie) and no good node at
+// the all-ones top-64 distance (which empty list slots also hold). Anything else is deferred to
+// the exact per-node kernel (rt_query_slow).
+template <int K>
+struct Window {
+    static constexpr int MW = K > 16 ? 2 : 1;
+    uint32_t base, ne, good;  // 64-byte aligned first node, one past the last node, good nodes in W(R)
+    uint64_t gm[MW];          // good bitmap of nodes base .. base + 64*MW
+    __device__ __forceinline__ uint32_t chunks() const { return (ne - base + 7) >> 3; }
+};
 
-    // rec[i] = dir[clamp(b - P - 1 + i, 0, B)]: rec[P - r] = dir[lo_r] and rec[P + r + 2] =
-    // dir[hi_r + 1] for round r (the clamp IS the window's edge clamp). 2P+3 independent 8-byte loads.
-    constexpr int NR = 2 * P + 3;
-    uint2 rec[NR];
-    uint32_t g[NR];
+enum { WIN_READY = 1, WIN_DEFER = 2 };
+
+// rec[i] = dir[clamp(b - P - 1 + i, 0, B)]: rec[P - r] = dir[lo_r] and rec[P + r + 2] = dir[hi_r + 1]
+// for round r (the clamp IS the window's edge clamp).
+template <int P>
+__device__ __forceinline__ void load_recs(const DevTable& T, uint32_t b, uint2 (&rec)[2 * P + 3]) {
 #pragma unroll
-    for (int i = 0; i < NR; i++) {
+    for (int i = 0; i < 2 * P + 3; i++) {
         const int64_t w = (int64_t)b - (P + 1) + i;
-        rec[i] = T.dir[w < 0 ? 0 : (w > (int64_t)B ? B : (uint32_t)w)];
+        rec[i] = T.dir[w < 0 ? 0 : (w > (int64_t)T.B ? T.B : (uint32_t)w)];
     }
+}
+
+template <int K, int P>
+__device__ __forceinline__ int rt_window(const DevTable& T, uint32_t b, const uint2 (&rec)[2 * P + 3],
+                                         uint32_t count, Window<K>& W) {
+    constexpr int NR = 2 * P + 3;
+    constexpr int MW = Window<K>::MW;
+    const uint32_t B = T.B;
+    uint32_t g[NR];
 #pragma unroll
     for (int i = 0; i < NR; i++) {  // good count of bucket b-P-1+i (0 outside the table)
         const int64_t w = (int64_t)b - (P + 1) + i;
@@ -327,7 +342,7 @@ __device__ __forceinline__ bool rt_query_fast(const DevTable& T, const Target& t
         const bool whole = (b <= (uint32_t)r + 1) & (b + r >= B - 1);
         if (R < 0 && (good >= count || whole)) R = r;
     }
-    if (R < 0) return false;
+    if (R < 0) return WIN_DEFER;
     uint32_t nb = 0, ne = 0, wide = 0;
 #pragma unroll
     for (int r = 0; r <= P; r++)
@@ -336,13 +351,10 @@ __device__ __forceinline__ bool rt_query_fast(const DevTable& T, const Target& t
     for (int i = 0; i < NR - 1; i++) wide |= (i >= P - R && i <= P + R + 1) ? rec[i].x : 0u;
     nb &= ~WIDE;
     ne &= ~WIDE;
-    // Window good bitmap relative to the 64-byte aligned chunk base (bit x = node base + x).
-    constexpr int MW = K > 16 ? 2 : 1;
     const uint32_t base = nb & ~7u;
-    if ((wide & WIDE) || ne - base > 64u * MW) return false;
-    uint64_t gm[MW];
+    if ((wide & WIDE) || ne - base > 64u * MW) return WIN_DEFER;
 #pragma unroll
-    for (int w = 0; w < MW; w++) gm[w] = 0;
+    for (int w = 0; w < MW; w++) W.gm[w] = 0;
 #pragma unroll
     for (int i = 0; i < NR - 1; i++) {
         const bool in = (i >= P - R) & (i <= P + R + 1);
@@ -352,10 +364,10 @@ __device__ __forceinline__ bool rt_query_fast(const DevTable& T, const Target& t
             const uint64_t z = rec[i].y;
             const uint64_t c = rel >= 64u * w ? (rel - 64u * w < 64u ? z << (rel - 64u * w) : 0ull)
                                               : (64u * w - rel < 32u ? z >> (64u * w - rel) : 0ull);
-            gm[w] |= in ? c : 0ull;
+            W.gm[w] |= in ? c : 0ull;
         }
     }
-    if (T.flags & TF_HAS_DUP) {  // a good node sharing its top 64 bits could tie: exact path
+    if (T.flags & TF_HAS_DUP) {
         uint32_t dup = 0;
 #pragma unroll
         for (int i = 0; i < NR - 1; i++) {
@@ -363,36 +375,78 @@ __device__ __forceinline__ bool rt_query_fast(const DevTable& T, const Target& t
             const bool in = (i >= P - R) & (i <= P + R + 1) & (w >= 0) & (w < (int64_t)B);
             dup |= in ? (T.dmask[in ? (uint32_t)w : 0u] & rec[i].y) : 0u;
         }
-        if (dup) return false;
+        if (dup) return WIN_DEFER;
     }
+    W.base = base;
+    W.ne = ne;
+    W.good = good;
+    return WIN_READY;
+}
 
+// ---- fast path, phase 2: rank one 8-node (64-byte) chunk of keys --------------------------
+template <int K>
+__device__ __forceinline__ void rank_chunk(TopK<K>& L, const uint4 (&kv)[4], uint64_t th, uint32_t g8,
+                                           uint32_t j0, bool& ones) {
+#pragma unroll
+    for (int x = 0; x < 4; x++) {
+        const uint64_t d0 = (((uint64_t)kv[x].y << 32) | kv[x].x) ^ th;
+        const uint64_t d1 = (((uint64_t)kv[x].w << 32) | kv[x].z) ^ th;
+        if ((g8 >> (2 * x)) & 1u) { ones |= d0 == ~0ull; L.insert_fast(d0, j0 + 2 * x); }
+        if ((g8 >> (2 * x + 1)) & 1u) { ones |= d1 == ~0ull; L.insert_fast(d1, j0 + 2 * x + 1); }
+    }
+}
+
+template <int K>
+__device__ __forceinline__ uint32_t chunk_bits(const Window<K>& W, uint32_t c /* node offset, multiple of 8 */) {
+    constexpr int MW = Window<K>::MW;
+    return (uint32_t)((MW == 1 || c < 64 ? W.gm[0] : W.gm[MW - 1]) >> (c & 63)) & 0xFFu;
+}
+
+// Lane-per-query fast path with per-lane loads (the K=32 kernel, and the dual-family kernel).
+// Returns false (nothing written) when the query must be deferred.
+template <int K, int P>
+__device__ __forceinline__ bool rt_query_fast(const DevTable& T, const Target& t, uint32_t count,
+                                              uint32_t* __restrict__ out_row, uint8_t* out_cnt_p) {
+    if (T.B == 0 || count == 0) {
+        for (uint32_t s = 0; s < count; s++) out_row[s] = NONE;
+        if (out_cnt_p) *out_cnt_p = 0;
+        return true;
+    }
+    const uint32_t b = locate_bucket(T, t);
+    uint2 rec[2 * P + 3];
+    load_recs<P>(T, b, rec);
+    Window<K> W;
+    if (rt_window<K, P>(T, b, rec, count, W) != WIN_READY) return false;
     TopK<K> L;
     L.init();
     bool ones = false;
-    // 8-node (64-byte) chunks; the next chunk's four 16-byte loads are in flight while this one is ranked
-    const uint4* kp = reinterpret_cast<const uint4*>(T.key + base);
-    uint4 nx[4];
+    // key chunks double-buffered two deep: chunks c and c+1 are in flight together, chunk c+2 is
+    // issued as soon as chunk c has been ranked
+    const uint4* kp = reinterpret_cast<const uint4*>(T.key + W.base);
+    const uint32_t M = W.chunks();
+    uint4 ba[4], bb[4];
 #pragma unroll
-    for (int x = 0; x < 4; x++) nx[x] = kp[x];
-    for (uint32_t c = 0; base + c < ne; c += 8) {
-        uint4 kv[4];
+    for (int x = 0; x < 4; x++) ba[x] = kp[x];
+    if (M > 1) {
 #pragma unroll
-        for (int x = 0; x < 4; x++) kv[x] = nx[x];
-        if (base + c + 8 < ne) {
+        for (int x = 0; x < 4; x++) bb[x] = kp[4 + x];
+    }
+    for (uint32_t c = 0; c < M; c += 2) {
+        rank_chunk<K>(L, ba, t.hi, chunk_bits<K>(W, 8 * c), W.base + 8 * c, ones);
+        if (c + 2 < M) {
 #pragma unroll
-            for (int x = 0; x < 4; x++) nx[x] = kp[(c >> 1) + 4 + x];
+            for (int x = 0; x < 4; x++) ba[x] = kp[4 * (c + 2) + x];
         }
-        const uint32_t g8 = (uint32_t)((MW == 1 || c < 64 ? gm[0] : gm[MW - 1]) >> (c & 63)) & 0xFFu;
+        if (c + 1 < M) {
+            rank_chunk<K>(L, bb, t.hi, chunk_bits<K>(W, 8 * (c + 1)), W.base + 8 * (c + 1), ones);
+            if (c + 3 < M) {
 #pragma unroll
-        for (int x = 0; x < 4; x++) {
-            const uint64_t d0 = (((uint64_t)kv[x].y << 32) | kv[x].x) ^ t.hi;
-            const uint64_t d1 = (((uint64_t)kv[x].w << 32) | kv[x].z) ^ t.hi;
-            if ((g8 >> (2 * x)) & 1u) { ones |= d0 == ~0ull; L.insert_fast(d0, base + c + 2 * x); }
-            if ((g8 >> (2 * x + 1)) & 1u) { ones |= d1 == ~0ull; L.insert_fast(d1, base + c + 2 * x + 1); }
+                for (int x = 0; x < 4; x++) bb[x] = kp[4 * (c + 3) + x];
+            }
         }
     }
     if (ones) return false;
-    write_row<K>(L, T, count, min(good, count), out_row, out_cnt_p);
+    write_row<K>(L, T, count, min(W.good, count), out_row, out_cnt_p);
     return true;
 }
 
@@ -408,6 +462,204 @@ __device__ __forceinline__ bool is_deferred(const uint32_t* out_row, const uint8
     return out_cnt_p ? *out_cnt_p == DEFER_CNT : out_row[0] == DEFER_IDX;
 }
 
+// ---------------------------------------------------------------------------------------
+// Block-cooperative RoutingTable kernel (K = 8, 16). Ranking stays one query per lane, but every
+// global read is issued cooperatively so that an instruction touches few lines (a lane-per-query
+// load touches 64 distinct lines and keeps the texture-address unit busy), and the block's 256
+// queries are counting-sorted by window length so that a wave ranks windows of equal length:
+//   1. the block's 256 targets (5 KB, contiguous) -> LDS with 16-byte loads
+//   2. bucket per query; directory records of 16 queries per instruction (4 lanes x 16 B each)
+//   3. window per query (rt_window); class = number of 8-node chunks (0: done or deferred)
+//   4. counting sort of the 256 queries by class (wave ballots), query state -> LDS slot
+//   5. per wave: key chunks of 16 queries per instruction (4 lanes x 16 B = one 64-byte line
+//      each) -> swizzled LDS tile -> each lane ranks its own query's 8 nodes
+//   6. result rows -> LDS in query order -> fully coalesced row stores
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ void wave_lds_sync() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ uint32_t lane_rank(uint64_t mask) {  // set bits of mask below this lane
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
+// LDS key tile slot: query j of the wave, 16-byte part x; parts rotated so that the 16 lanes of a
+// ds_read_b128 group and the 8 of a ds_write_b128 group hit 16 / 8 distinct bank quads.
+__device__ __forceinline__ uint32_t ktile(uint32_t j, uint32_t x) { return j * 4u + (x ^ ((j >> 2) & 3u)); }
+
+template <int K>
+__global__ __launch_bounds__(BLOCK) void rt_block_kernel(DevTable T, const uint8_t* __restrict__ targets, uint32_t q,
+                                                         uint32_t count, uint32_t* __restrict__ out_idx,
+                                                         uint8_t* __restrict__ out_cnt) {
+    static_assert(K <= 16, "block kernel: K <= 16");
+    constexpr int P = 2;  // R <= 2 covers all but ~1e-6 of k <= 16 windows on 80%-good uniform tables
+    constexpr int NR = 2 * P + 3;
+    constexpr int RQ = (NR + 2) / 2;  // 16-byte directory pieces per query (even-aligned cover of NR records)
+    constexpr uint32_t NCLS = 9;      // classes 0..8: 8-node chunks per window (MW = 1: <= 64 nodes)
+    __shared__ uint4 lds[1024 + 512 + 64 + 32];
+    uint4* stage = lds;                                   // 16 KB: targets / directory / key tiles / rows
+    uint4* state = lds + 1024;                            // 256 slots x 32 B
+    uint32_t* b_arr = reinterpret_cast<uint32_t*>(lds + 1536);
+    uint32_t* cls = reinterpret_cast<uint32_t*>(lds + 1600);  // [4][NCLS] counts, then [4][NCLS] starts
+
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const uint32_t q0 = blockIdx.x * BLOCK;
+    const uint32_t nq = min((uint32_t)BLOCK, q - q0);
+    const bool active = tid < nq;
+    const bool trivial = (T.B == 0) | (count == 0);
+    const uint32_t B = T.B;
+
+    // 1. targets -> LDS
+    {
+        const uint32_t* src32 = reinterpret_cast<const uint32_t*>(targets + 20ull * q0);
+        if (nq == BLOCK && ((uintptr_t)targets & 15u) == 0) {
+            const uint4* src = reinterpret_cast<const uint4*>(src32);
+            stage[tid] = src[tid];
+            if (tid < 64) stage[256 + tid] = src[256 + tid];
+        } else {
+            uint32_t* tw = reinterpret_cast<uint32_t*>(stage);
+            for (uint32_t k = tid; k < nq * 5; k += BLOCK) tw[k] = src32[k];
+        }
+    }
+    __syncthreads();
+    Target t{};
+    if (active) {
+        const uint32_t* tw = reinterpret_cast<const uint32_t*>(stage) + 5 * tid;
+        const uint32_t w0 = __builtin_bswap32(tw[0]), w1 = __builtin_bswap32(tw[1]);
+        t.hi = ((uint64_t)w0 << 32) | w1;
+        t.t2 = __builtin_bswap32(tw[2]);
+        t.t3 = __builtin_bswap32(tw[3]);
+        t.t4 = __builtin_bswap32(tw[4]);
+    }
+    // 2. bucket, then cooperative directory loads (each query's pieces come from its own wave)
+    const uint32_t b = (active && !trivial) ? locate_bucket(T, t) : 0u;
+    b_arr[tid] = b;
+    __syncthreads();  // targets consumed; buckets visible
+    if (!trivial) {
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const uint32_t qs = wid * 64 + 16 * i + (lane >> 2), part = lane & 3;
+            const uint32_t bq = b_arr[qs];
+            const int64_t r0 = (int64_t)bq - (P + 1);
+            const int64_t a = r0 & ~(int64_t)1;
+            if (part < (uint32_t)RQ && qs < nq && r0 >= 0 && a + 2 * RQ - 1 <= (int64_t)B)
+                stage[qs * RQ + part] = reinterpret_cast<const uint4*>(T.dir + a)[part];
+        }
+    }
+    wave_lds_sync();
+    Window<K> W{};
+    int st = 0;
+    if (active && !trivial) {
+        uint2 rec[NR];
+        const int64_t r0 = (int64_t)b - (P + 1);
+        if (r0 >= 0 && (r0 & ~(int64_t)1) + 2 * RQ - 1 <= (int64_t)B) {
+            // the query's pieces start at an even record; the odd shift is applied in the LDS address
+            const uint2* u = reinterpret_cast<const uint2*>(stage + tid * RQ) + (r0 & 1);
+#pragma unroll
+            for (int i = 0; i < NR; i++) rec[i] = u[i];
+        } else {
+            load_recs<P>(T, b, rec);  // first / last buckets of the table: clamped per-lane loads
+        }
+        st = rt_window<K, P>(T, b, rec, count, W);
+    }
+    uint8_t* cp_own = (out_cnt && active) ? out_cnt + q0 + tid : nullptr;
+    if (active && trivial && cp_own) *cp_own = 0;
+    if (st == WIN_DEFER && cp_own) *cp_own = DEFER_CNT;
+    // 3/4. counting sort by class
+    const uint32_t M = st == WIN_READY ? W.chunks() : 0u;
+    uint32_t myrank = 0;
+#pragma unroll
+    for (uint32_t v = 0; v < NCLS; v++) {
+        const uint64_t m = __ballot(M == v);
+        if (M == v) myrank = lane_rank(m);
+        if (lane == 0) cls[wid * NCLS + v] = (uint32_t)__builtin_popcountll(m);
+    }
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t acc = 0;
+        for (uint32_t v = 0; v < NCLS; v++)
+            for (uint32_t w = 0; w < 4; w++) {
+                const uint32_t c = cls[w * NCLS + v];
+                cls[4 * NCLS + w * NCLS + v] = acc;
+                acc += c;
+            }
+    }
+    __syncthreads();
+    const uint32_t start1 = cls[4 * NCLS + 1];  // first slot of class 1 (= class-0 population)
+    if (M) {
+        const uint32_t pos = cls[4 * NCLS + wid * NCLS + M] + myrank;
+        state[2 * pos] = make_uint4(q0 + tid, (uint32_t)t.hi, (uint32_t)(t.hi >> 32), W.base);
+        state[2 * pos + 1] = make_uint4(W.ne, W.good, (uint32_t)W.gm[0], (uint32_t)(W.gm[0] >> 32));
+    }
+    __syncthreads();
+    // 5. rank: slot tid's query, key tiles loaded cooperatively per wave
+    const bool mine = tid >= start1;
+    uint32_t qid = 0, sgood = 0;
+    Window<K> S{};
+    uint64_t th = 0;
+    if (mine) {
+        const uint4 a0 = state[2 * tid], a1 = state[2 * tid + 1];
+        qid = a0.x;
+        th = ((uint64_t)a0.z << 32) | a0.y;
+        S.base = a0.w;
+        S.ne = a1.x;
+        sgood = a1.y;
+        S.gm[0] = ((uint64_t)a1.w << 32) | a1.z;
+    }
+    const uint32_t Ms = mine ? S.chunks() : 0u;
+    uint32_t lbase[4], lM[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const uint32_t si = wid * 64 + 16 * i + (lane >> 2);
+        const uint4 a0 = state[2 * si], a1 = state[2 * si + 1];
+        lbase[i] = a0.w;
+        lM[i] = si >= start1 ? (a1.x - a0.w + 7) >> 3 : 0u;
+    }
+    uint4* tile = stage + wid * 256;
+    TopK<K> L;
+    L.init();
+    bool ones = false;
+    for (uint32_t c = 0; __ballot(c < Ms) != 0; c++) {
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+            if (c < lM[i])
+                tile[ktile(16 * i + (lane >> 2), lane & 3)] =
+                    reinterpret_cast<const uint4*>(T.key + lbase[i] + 8 * c)[lane & 3];
+        wave_lds_sync();
+        if (c < Ms) {
+            uint4 kv[4];
+#pragma unroll
+            for (int x = 0; x < 4; x++) kv[x] = tile[ktile(lane, x)];
+            rank_chunk<K>(L, kv, th, chunk_bits<K>(S, 8 * c), S.base + 8 * c, ones);
+        }
+        wave_lds_sync();
+    }
+    // 6. rows -> LDS (query order) -> coalesced stores
+    __syncthreads();
+    uint32_t* rows = reinterpret_cast<uint32_t*>(stage);
+    if (mine) {
+        const uint32_t loc = qid - q0;
+        if (ones) {
+            if (out_cnt) out_cnt[qid] = DEFER_CNT;
+            else rows[loc * count] = DEFER_IDX;
+        } else {
+            const uint32_t m = min(sgood, count);
+#pragma unroll
+            for (int s2 = 0; s2 < K; s2++)
+                if ((uint32_t)s2 < count) rows[loc * count + s2] = (uint32_t)s2 < m ? L.di[s2] + T.index_base : NONE;
+            if (out_cnt) out_cnt[qid] = (uint8_t)m;
+        }
+    }
+    if (active && M == 0) {  // trivial (NONE rows) or deferred (marker row when there are no counts)
+        for (uint32_t s2 = 0; s2 < count; s2++) rows[tid * count + s2] = NONE;
+        if (st == WIN_DEFER && !out_cnt && count) rows[tid * count] = DEFER_IDX;
+    }
+    __syncthreads();
+    uint32_t* dst = out_idx + (size_t)q0 * count;
+    for (uint32_t k = tid; k < nq * count; k += BLOCK) dst[k] = rows[k];
+}
+
 template <int K>
 __global__ __launch_bounds__(BLOCK) void rt_closest_kernel(DevTable T, const uint8_t* __restrict__ targets,
                                                            uint32_t q, uint32_t count,
@@ -419,6 +671,201 @@ __global__ __launch_bounds__(BLOCK) void rt_closest_kernel(DevTable T, const uin
     uint32_t* row = out_idx + (size_t)i * count;
     uint8_t* cp = out_cnt ? out_cnt + i : nullptr;
     if (!rt_query_fast<K, (K > 16 ? 6 : 3)>(T, t, count, row, cp)) mark_deferred(row, cp);
+}
+
+// Debug ablation of the lane kernel (KAD_RT_KERNEL=abl1|abl2|abl3): 1 = target + locate + store,
+// 2 = + directory window, 3 = + key loads without ranking. Results are garbage; timing only.
+template <int K, int ABL>
+__global__ __launch_bounds__(BLOCK) void rt_ablate_kernel(DevTable T, const uint8_t* __restrict__ targets, uint32_t q,
+                                                          uint32_t count, uint32_t* __restrict__ out_idx,
+                                                          uint8_t* __restrict__ out_cnt) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= q) return;
+    const Target t = load_target(targets, i);
+    uint32_t* row = out_idx + (size_t)i * count;
+    const uint32_t b = locate_bucket(T, t);
+    uint32_t acc = b ^ (uint32_t)t.hi;
+    if (ABL >= 2) {
+        uint2 rec[7];
+        load_recs<2>(T, b, rec);
+        Window<K> W;
+        const int st = rt_window<K, 2>(T, b, rec, count, W);
+        acc += st + W.base + W.ne + (uint32_t)W.gm[0];
+        if (ABL >= 3 && st == WIN_READY) {
+            const uint4* kp = reinterpret_cast<const uint4*>(T.key + W.base);
+            const uint32_t M = W.chunks();
+            for (uint32_t c = 0; c < M; c++) {
+                uint4 kv[4];
+#pragma unroll
+                for (int x = 0; x < 4; x++) kv[x] = kp[4 * c + x];
+#pragma unroll
+                for (int x = 0; x < 4; x++) acc += kv[x].x ^ kv[x].y ^ kv[x].z ^ kv[x].w;
+            }
+        }
+    }
+    uint4 v = make_uint4(acc, acc, acc, acc);
+    *reinterpret_cast<uint4*>(row) = v;
+    *reinterpret_cast<uint4*>(row + 4) = v;
+    if (out_cnt) out_cnt[i] = 0;
+}
+
+// ---------------------------------------------------------------------------------------
+// Bucket-line RoutingTable kernel (direct-mapped tables of uniform depth d <= 32, the U(d) shape).
+//
+// Random gathers on MI355X cost per 128-byte line touched (~50 G random lines/s whether 32, 64 or
+// 128 bytes of it are used: tools/microbench.py), so the window is laid out to touch as few lines
+// as possible. Each bucket is one 64-byte record:
+//   w0 = first node index (27 bits) | n << 27 (n = BL_OVF if the bucket does not fit)
+//   w1 = good bitmask (bits 0..13) | "needs the exact compare" bitmask (bits 16..29)
+//   w2..w15 = key32 of each node = ID bits [d, d + 32), right after the bucket's d-bit prefix.
+// The round-0 window {b-1, b} is 128 contiguous bytes. Buckets are dyadic, so a node's XOR distance
+// is ordered by (bucket prefix XOR target prefix, key32 XOR target bits [d, d+32)): that 64-bit
+// rank key is exact in the top d+32 distance bits; two nodes can tie only inside one bucket on
+// equal key32, and those nodes carry the exact-compare bit (the query is deferred).
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t bl_key_word(const uint4& a, const uint4& b, const uint4& c, const uint4& e, int s) {
+    switch (s) {  // slot s lives in dword 2 + s of the line (static after unrolling)
+        case 0: return a.z; case 1: return a.w;
+        case 2: return b.x; case 3: return b.y; case 4: return b.z; case 5: return b.w;
+        case 6: return c.x; case 7: return c.y; case 8: return c.z; case 9: return c.w;
+        case 10: return e.x; case 11: return e.y; case 12: return e.z; default: return e.w;
+    }
+}
+
+// One bucket line held in registers, with its rank-relevant values.
+struct BlLine {
+    uint4 v[4];
+    uint32_t gm, off, good;  // good bitmask, first node index, good count
+    uint64_t D;              // bucket prefix XOR target prefix (orders whole buckets)
+    bool present;
+};
+
+__device__ __forceinline__ void bl_load(const DevTable& T, uint32_t w, BlLine& L) {
+    const uint4* p = T.bl + 4ull * w;
+#pragma unroll
+    for (int x = 0; x < 4; x++) L.v[x] = p[x];
+}
+
+__device__ __forceinline__ void bl_header(BlLine& L, uint64_t D, bool present, bool& bad) {
+    L.present = present;
+    L.D = D;
+    const uint32_t nf = L.v[0].x >> 27, xm = L.v[0].y >> 16;
+    L.gm = present ? (L.v[0].y & 0xFFFFu) : 0u;
+    L.off = L.v[0].x & BL_OFF_MASK;
+    L.good = __builtin_popcount(L.gm);
+    bad |= present & ((nf == BL_OVF) | ((L.gm & xm) != 0));
+}
+
+// Rank every good node of line L among the good nodes of its own bucket (32-bit keys suffice: the
+// nodes of one bucket share its prefix) and place it at base + rank among the K output slots.
+template <int K>
+__device__ __forceinline__ void bl_place(const BlLine& L, uint32_t base, uint32_t t32, uint32_t (&out)[K]) {
+    uint32_t k[BL_CAP];
+#pragma unroll
+    for (int s2 = 0; s2 < (int)BL_CAP; s2++) k[s2] = bl_key_word(L.v[0], L.v[1], L.v[2], L.v[3], s2) ^ t32;
+    uint32_t ns = 0;  // one past the highest good slot over the wave: bounds both loops
+#pragma unroll
+    for (int s2 = 0; s2 < (int)BL_CAP; s2++) ns = __any((L.gm >> s2) != 0) ? (uint32_t)s2 + 1 : ns;
+#pragma unroll
+    for (int s2 = 0; s2 < (int)BL_CAP; s2++) {
+        if ((uint32_t)s2 >= ns) break;
+        uint32_t r = base;
+#pragma unroll
+        for (int u = 0; u < (int)BL_CAP; u++) {
+            if ((uint32_t)u >= ns) break;
+            r += ((L.gm >> u) & 1u) & (uint32_t)(k[u] < k[s2]);
+        }
+        const bool g = (L.gm >> s2) & 1u;
+#pragma unroll
+        for (int j = 0; j < K; j++) out[j] = (g & (r == (uint32_t)j)) ? L.off + s2 : out[j];
+    }
+}
+
+template <int K>
+__global__ __launch_bounds__(BLOCK) void rt_bl_kernel(DevTable T, const uint8_t* __restrict__ targets, uint32_t q,
+                                                      uint32_t count, uint32_t* __restrict__ out_idx,
+                                                      uint8_t* __restrict__ out_cnt) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= q) return;
+    uint32_t* row = out_idx + (size_t)i * count;
+    uint8_t* cp = out_cnt ? out_cnt + i : nullptr;
+    if (count == 0) {
+        if (cp) *cp = 0;
+        return;
+    }
+    const Target t = load_target(targets, i);
+    const uint32_t B = T.B, d = 64 - T.rshift;
+    const uint32_t b = locate_bucket(T, t);
+    const uint64_t pre0 = T.rbase >> T.rshift, tp = t.hi >> T.rshift;
+    const uint32_t t32 = (uint32_t)((t.hi << d) >> 32);
+    bool bad = false;
+    // Round 0 window {b-1, b}: both lines in flight together. Round 1 adds {b-2, b+1}; later
+    // rounds (~0.3% of k=8 queries on an 80%-good U(24) shard) are deferred.
+    BlLine Lb, Ll, Lh, Ll2;
+    const bool hasl = b > 0;
+    bl_load(T, b, Lb);
+    bl_load(T, hasl ? b - 1 : b, Ll);
+    bl_header(Lb, (pre0 + b) ^ tp, true, bad);
+    bl_header(Ll, (pre0 + b - 1) ^ tp, hasl, bad);
+    uint32_t good = Lb.good + Ll.good;
+    const bool whole0 = (b <= 1) & (b >= B - 1);
+    const bool r1 = (good < count) & !whole0;
+    const bool hash = r1 & (b + 1 < B), hasl2 = r1 & (b >= 2);
+    if (r1) {
+        bl_load(T, hash ? b + 1 : b, Lh);
+        bl_load(T, hasl2 ? b - 2 : b, Ll2);
+    }
+    bl_header(Lh, (pre0 + b + 1) ^ tp, hash, bad);
+    bl_header(Ll2, (pre0 + b - 2) ^ tp, hasl2, bad);
+    good += Lh.good + Ll2.good;
+    const bool whole1 = (b <= 2) & (b + 1 >= B - 1);
+    bad |= r1 & (good < count) & !whole1;
+    if (bad) {
+        mark_deferred(row, cp);
+        return;
+    }
+    // whole buckets are ordered by D (the XOR images of disjoint dyadic buckets are disjoint intervals)
+    auto base_of = [&](const BlLine& X) {
+        return (Ll.present & (Ll.D < X.D) ? Ll.good : 0u) + (Lb.D < X.D ? Lb.good : 0u) +
+               (Lh.present & (Lh.D < X.D) ? Lh.good : 0u) + (Ll2.present & (Ll2.D < X.D) ? Ll2.good : 0u);
+    };
+    uint32_t out[K];
+#pragma unroll
+    for (int j = 0; j < K; j++) out[j] = NONE;
+    bl_place<K>(Lb, base_of(Lb), t32, out);
+    bl_place<K>(Ll, base_of(Ll), t32, out);
+    if (__any(r1)) {
+        bl_place<K>(Lh, base_of(Lh), t32, out);
+        bl_place<K>(Ll2, base_of(Ll2), t32, out);
+    }
+    const uint32_t m = min(good, count);
+    if (count == (uint32_t)K && (K % 4) == 0) {
+#pragma unroll
+        for (int j = 0; j < K; j += 4)
+            *reinterpret_cast<uint4*>(row + j) =
+                make_uint4((uint32_t)j < m ? out[j] + T.index_base : NONE,
+                           (uint32_t)j + 1 < m ? out[j + 1] + T.index_base : NONE,
+                           (uint32_t)j + 2 < m ? out[j + 2] + T.index_base : NONE,
+                           (uint32_t)j + 3 < m ? out[j + 3] + T.index_base : NONE);
+    } else {
+#pragma unroll
+        for (int j = 0; j < K; j++)
+            if ((uint32_t)j < count) row[j] = (uint32_t)j < m ? out[j] + T.index_base : NONE;
+    }
+    if (cp) *cp = (uint8_t)m;
+}
+
+// Good bitmasks of the bucket lines after a status change (exact-compare bits are kept).
+__global__ void bl_good_kernel(const uint8_t* status, uint4* bl, uint32_t B) {
+    const uint32_t b = blockIdx.x * BLOCK + threadIdx.x;
+    if (b >= B) return;
+    uint4 h = bl[4ull * b];
+    const uint32_t off = h.x & BL_OFF_MASK, nf = h.x >> 27;
+    if (nf == BL_OVF) return;
+    uint32_t gm = 0;
+    for (uint32_t s2 = 0; s2 < nf; s2++) gm |= (uint32_t)(status[off + s2] & KAD_STATUS_GOOD) << s2;
+    h.y = (h.y & 0xFFFF0000u) | gm;
+    bl[4ull * b] = h;
 }
 
 // Second pass over the batch: the (rare) queries the fast kernel deferred, exact per-node path.
@@ -666,6 +1113,13 @@ __global__ void scan_apply_kernel(const uint32_t* part, const uint32_t* sums, ui
 
 inline uint32_t grid_for(uint64_t n) { return (uint32_t)((n + BLOCK - 1) / BLOCK); }
 
+// KAD_RT_KERNEL=lane (default) | block | bl | abl1..3 selects the RoutingTable kernel variant (A/B
+// benching, tools/ab_bench.py); read per call so one process can time several.
+bool force_lane() {
+    const char* e = std::getenv("KAD_RT_KERNEL");
+    return !e || std::strcmp(e, "block") != 0;
+}
+
 // ---------------------------------------------------------------------------------------
 // Host side
 // ---------------------------------------------------------------------------------------
@@ -765,6 +1219,7 @@ struct kad_table {
     uint8_t* status_mut = nullptr;
     uint2* dir_mut = nullptr;
     uint32_t* gpre_mut = nullptr;
+    uint4* bl_mut = nullptr;
     int64_t* time_ns = nullptr;
     int64_t* reply_ns = nullptr;
     uint8_t* expired = nullptr;
@@ -794,6 +1249,7 @@ int rebuild_good_prefix(kad_table* t, hipStream_t s) {
     hipLaunchKernelGGL(scan_tiles_kernel, dim3(tiles), dim3(BLOCK), 0, s, t->scan_cnt, m, t->scan_part, t->scan_sums);
     hipLaunchKernelGGL(scan_sums_kernel, dim3(1), dim3(BLOCK), 0, s, t->scan_sums, tiles);
     hipLaunchKernelGGL(scan_apply_kernel, dim3(grid_for(m)), dim3(BLOCK), 0, s, t->scan_part, t->scan_sums, m, t->gpre_mut);
+    if (t->bl_mut) hipLaunchKernelGGL(bl_good_kernel, dim3(grid_for(B)), dim3(BLOCK), 0, s, t->d.status, t->bl_mut, B);
     HIP_TRY(hipGetLastError());
     return KAD_OK;
 }
@@ -806,7 +1262,21 @@ int check_count(uint32_t count) {
 template <int K>
 void launch_rt(const DevTable& d, const uint8_t* targets, uint32_t q, uint32_t count, uint32_t* out, uint8_t* cnt,
                hipStream_t s) {
-    hipLaunchKernelGGL(rt_closest_kernel<K>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
+    const char* ev = std::getenv("KAD_RT_KERNEL");
+    if (K == 8 && ev && std::strncmp(ev, "abl", 3) == 0) {
+        const int a = ev[3] - '0';
+        if (a == 1) hipLaunchKernelGGL((rt_ablate_kernel<8, 1>), dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
+        if (a == 2) hipLaunchKernelGGL((rt_ablate_kernel<8, 2>), dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
+        if (a == 3) hipLaunchKernelGGL((rt_ablate_kernel<8, 3>), dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
+        return;
+    }
+    if ((d.flags & TF_BL) && ev && std::strcmp(ev, "bl") == 0)
+        hipLaunchKernelGGL(rt_bl_kernel<K>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
+    else if (K <= 16 && !force_lane())
+        hipLaunchKernelGGL(rt_block_kernel<(K <= 16 ? K : 16)>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count,
+                           out, cnt);
+    else
+        hipLaunchKernelGGL(rt_closest_kernel<K>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
     hipLaunchKernelGGL(rt_closest_deferred_kernel<K>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out,
                        cnt);
 }
@@ -960,12 +1430,57 @@ int kad_table_create(kad_table** out, int device, uint32_t n_nodes, const uint8_
         }
         uint32_t tb = 1;
         while ((1u << tb) < n_buckets && tb < 24) tb++;
-        const Radix r = choose_radix(fkey[0], fkey[n_buckets - 1], std::min<uint32_t>(tb + 1, 24));
+        Radix r = choose_radix(fkey[0], fkey[n_buckets - 1], std::min<uint32_t>(tb + 1, 24));
+        // Uniform depth (U(d) tables, shards of them): firsts equally spaced by a power of two
+        // 2^k and aligned to it, low 96 bits zero -> the radix IS the bucket index (shift k).
+        if (n_buckets >= 2) {
+            const uint64_t step = fkey[1] - fkey[0];
+            bool uni = step && (step & (step - 1)) == 0 && (fkey[0] & (step - 1)) == 0;
+            for (uint32_t b = 0; b < n_buckets && uni; b++) {
+                uni = (b == 0 || fkey[b] - fkey[b - 1] == step) && !ftail[3ull * b] && !ftail[3ull * b + 1] &&
+                      !ftail[3ull * b + 2];
+            }
+            if (uni) {
+                r.shift = (uint32_t)__builtin_ctzll(step);
+                r.base = fkey[0];
+                r.slots = n_buckets;
+                r.bits = tb;
+            }
+        }
         std::vector<uint32_t> rdx = build_radix(r, n_buckets, bucket_first, true);
         // direct-mapped locate: slot s holds exactly bucket s, starting at the slot start
         bool direct = r.slots == n_buckets;
         for (uint32_t sl = 0; sl < r.slots && direct; sl++) direct = rdx[sl] == (sl | RDX_EXACT);
         if (direct) d.flags |= TF_DIRECT;
+        // bucket lines for direct-mapped tables of depth <= 32 (see rt_bl_kernel)
+        const uint32_t depth = 64 - r.shift;
+        if (direct && depth >= 1 && depth <= 32 && n_nodes <= BL_OFF_MASK) {
+            std::vector<uint32_t> bl(16ull * n_buckets, 0u);
+            const uint64_t pre0 = r.base >> r.shift;
+            for (uint32_t b = 0; b < n_buckets; b++) {
+                uint32_t* L = &bl[16ull * b];
+                const uint32_t j0 = bucket_offset[b], j1 = bucket_offset[b + 1], nb = j1 - j0;
+                bool fits = nb <= BL_CAP;
+                for (uint32_t j = j0; j < j1 && fits; j++) fits = (id_hi(ids + 20ull * j) >> r.shift) == pre0 + b;
+                L[0] = j0 | ((fits ? nb : BL_OVF) << 27);
+                if (!fits) continue;
+                uint32_t gm = 0, xm = 0;
+                for (uint32_t s2 = 0; s2 < nb; s2++) {
+                    const uint64_t hi = id_hi(ids + 20ull * (j0 + s2));
+                    L[2 + s2] = (uint32_t)((hi << depth) >> 32);
+                    gm |= (uint32_t)(status[j0 + s2] & KAD_STATUS_GOOD) << s2;
+                }
+                for (uint32_t a = 0; a < nb; a++)
+                    for (uint32_t c = a + 1; c < nb; c++)
+                        if (L[2 + a] == L[2 + c]) xm |= (1u << a) | (1u << c);
+                L[1] = gm | (xm << 16);
+            }
+            uint4* dbl;
+            if ((rc = dev_upload(&dbl, bl.data(), 4ull * n_buckets, t->owned, t->bytes))) { delete t; return rc; }
+            d.bl = dbl;
+            t->bl_mut = dbl;
+            d.flags |= TF_BL;
+        }
         uint2* ddir; uint64_t* dfk; uint32_t *dft, *drdx, *dgp, *ddm = nullptr;
         if ((rc = dev_upload(&ddir, dir.data(), n_buckets + 1, t->owned, t->bytes)) ||
             (rc = dev_upload(&dgp, gpre.data(), n_buckets + 1, t->owned, t->bytes)) ||

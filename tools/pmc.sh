@@ -2,7 +2,7 @@
 # PMC passes over a short bench run (one rocprofv3 invocation per counter group, kernel-trace
 # only besides --pmc, as the MI355X guide prescribes). Output: gpurun_out/pmc/<pass>/...
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-O=$R/gpurun_out/pmc
+O=$R/gpurun_out/${PMC_DIR:-pmc}
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
 ARGS=${BENCH_ARGS:---steps 5 --warmup 2 --no-cpu}
