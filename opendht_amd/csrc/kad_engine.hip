@@ -90,7 +90,8 @@ struct DevTable {
     const uint32_t* ftail;
     const uint32_t* rrdx;
     const uint32_t* nrdx;
-    const uint4* bl;  // bucket lines (TF_BL): 64 bytes per bucket, see rt_bl_kernel
+    const uint4* rec;    // bucket records (TF_REC): 4 copies x rec_lines 128-byte lines, see rt_rec_kernel
+    uint32_t rec_lines;  // lines per copy
     uint64_t rbase, nbase;
     uint32_t rshift, rslots, nshift, nslots;
     uint32_t n, B, index_base, flags;
@@ -98,10 +99,7 @@ struct DevTable {
 
 constexpr uint32_t TF_DIRECT = 1u;   // radix slot s holds exactly bucket s (no locate load)
 constexpr uint32_t TF_HAS_DUP = 2u;  // some nodes share their top 64 ID bits
-constexpr uint32_t TF_BL = 4u;       // bucket-line layout present (direct-mapped, depth <= 32)
-constexpr uint32_t BL_CAP = 14;      // node keys per 64-byte bucket line
-constexpr uint32_t BL_OVF = 31;      // n field of a bucket that does not fit its line
-constexpr uint32_t BL_OFF_MASK = (1u << 27) - 1;
+constexpr uint32_t TF_REC = 8u;      // bucket-record layout present (direct-mapped, depth <= 48)
 constexpr uint32_t WIDE = 0x80000000u;  // dir[].x flag: bucket holds > 32 nodes (masks invalid)
 constexpr uint32_t KEY_PAD = 32;        // key[] is padded so 16-node chunk loads never leave it
 
@@ -129,20 +127,6 @@ __device__ __forceinline__ int cmp160(uint64_t ah, uint32_t a2, uint32_t a3, uin
     if (a3 != b3) return a3 < b3 ? -1 : 1;
     if (a4 != b4) return a4 < b4 ? -1 : 1;
     return 0;
-}
-
-// Is node a strictly before node b in the reference's result order, given equal top-64
-// XOR distance? Full-width XOR compare on the tails, then insertion order (= index order
-// within one bucket, the only place equal IDs can meet: routing_table.cpp:75-87).
-__device__ __forceinline__ bool tail_less(const DevTable& T, const Target& t, uint32_t a, uint32_t b) {
-    const uint32_t* ta = T.tail + 3ull * a;
-    const uint32_t* tb = T.tail + 3ull * b;
-    uint32_t a2 = ta[0] ^ t.t2, a3 = ta[1] ^ t.t3, a4 = ta[2] ^ t.t4;
-    uint32_t b2 = tb[0] ^ t.t2, b3 = tb[1] ^ t.t3, b4 = tb[2] ^ t.t4;
-    if (a2 != b2) return a2 < b2;
-    if (a3 != b3) return a3 < b3;
-    if (a4 != b4) return a4 < b4;
-    return a < b;
 }
 
 // RoutingTable::findBucket (routing_table.cpp:113-127) = upper_bound(first, t) - 1, clamped to 0.
@@ -228,25 +212,6 @@ struct TopK {
         dk[0] = lt[0] ? cd : dk[0];
         di[0] = lt[0] ? ci : di[0];
     }
-    // Exact order: equal top-64 distances fall back to the 96-bit tails, then to the index.
-    __device__ __forceinline__ void insert_exact(const DevTable& T, const Target& t, uint64_t cd, uint32_t ci) {
-        bool sh = false;
-#pragma unroll
-        for (int s = 0; s < K; s++) {
-            bool lt;
-            if (sh) lt = true;
-            else if (di[s] == NONE) lt = true;
-            else if (cd != dk[s]) lt = cd < dk[s];
-            else lt = tail_less(T, t, ci, di[s]);
-            sh = lt;
-            const uint64_t nd = lt ? dk[s] : cd;
-            const uint32_t ni = lt ? di[s] : ci;
-            dk[s] = lt ? cd : dk[s];
-            di[s] = lt ? ci : di[s];
-            cd = nd;
-            ci = ni;
-        }
-    }
 };
 
 template <int K>
@@ -268,30 +233,6 @@ __device__ __forceinline__ void write_row(const TopK<K>& L, const DevTable& T, u
             if ((uint32_t)s < count) out_row[s] = (uint32_t)s < m ? L.di[s] + T.index_base : NONE;
     }
     if (out_cnt_p) *out_cnt_p = (uint8_t)m;
-}
-
-// Slow path: any window (unbounded rounds, wide buckets), per-node status reads.
-template <int K>
-__device__ __forceinline__ void rt_query_slow(const DevTable& T, const Target& t, uint32_t b, uint32_t count,
-                                           uint32_t* __restrict__ out_row, uint8_t* out_cnt_p) {
-    const uint32_t B = T.B;
-    uint32_t lo = b > 0 ? b - 1 : 0, hi = b;
-    uint32_t good = T.gpre[hi + 1] - T.gpre[lo];
-    while (good < count && (lo > 0 || hi < B - 1)) {
-        if (hi < B - 1) hi++;
-        if (lo > 0) lo--;
-        good = T.gpre[hi + 1] - T.gpre[lo];
-    }
-    const uint2 dl = T.dir[lo], dh = T.dir[hi + 1];
-    TopK<K> L;
-    L.init();
-    const uint32_t beg = dl.x & ~WIDE, end = dh.x & ~WIDE;
-    for (uint32_t j = beg; j < end; j++) {
-        const uint8_t st = T.status[j];
-        if (!(st & KAD_STATUS_GOOD)) continue;
-        L.insert_exact(T, t, T.key[j] ^ t.hi, j);
-    }
-    write_row<K>(L, T, count, min(good, count), out_row, out_cnt_p);
 }
 
 // ---- fast path, phase 1: the window ------------------------------------------------------
@@ -450,437 +391,491 @@ __device__ __forceinline__ bool rt_query_fast(const DevTable& T, const Target& t
     return true;
 }
 
-// Deferral marker: out_cnt[i] = DEFER_CNT when the caller asked for counts, else row[0] = DEFER_IDX.
-constexpr uint8_t DEFER_CNT = 0xFF;
-constexpr uint32_t DEFER_IDX = 0xFFFFFFFEu;
-
-__device__ __forceinline__ void mark_deferred(uint32_t* out_row, uint8_t* out_cnt_p) {
-    if (out_cnt_p) *out_cnt_p = DEFER_CNT;
-    else out_row[0] = DEFER_IDX;
-}
-__device__ __forceinline__ bool is_deferred(const uint32_t* out_row, const uint8_t* out_cnt_p) {
-    return out_cnt_p ? *out_cnt_p == DEFER_CNT : out_row[0] == DEFER_IDX;
-}
-
 // ---------------------------------------------------------------------------------------
-// Block-cooperative RoutingTable kernel (K = 8, 16). Ranking stays one query per lane, but every
-// global read is issued cooperatively so that an instruction touches few lines (a lane-per-query
-// load touches 64 distinct lines and keeps the texture-address unit busy), and the block's 256
-// queries are counting-sorted by window length so that a wave ranks windows of equal length:
-//   1. the block's 256 targets (5 KB, contiguous) -> LDS with 16-byte loads
-//   2. bucket per query; directory records of 16 queries per instruction (4 lanes x 16 B each)
-//   3. window per query (rt_window); class = number of 8-node chunks (0: done or deferred)
-//   4. counting sort of the 256 queries by class (wave ballots), query state -> LDS slot
-//   5. per wave: key chunks of 16 queries per instruction (4 lanes x 16 B = one 64-byte line
-//      each) -> swizzled LDS tile -> each lane ranks its own query's 8 nodes
-//   6. result rows -> LDS in query order -> fully coalesced row stores
+// Wave-cooperative exact query: the fallback of every RoutingTable kernel for the few queries
+// its fast path cannot rank (windows beyond its prefetch, wide buckets, records with equal short
+// keys, top-64 ties). The whole wave answers ONE query with the reference's exact order:
+//   1. W(R): lane l tests round r0 + l from the good prefix sums; a ballot gives the least R
+//      (routing_table.cpp:89-104 closed form), 64 rounds per probe
+//   2. W(R)'s nodes in tiles of 64 (lane l <- node beg + 64u + l): good bit, full 160-bit XOR
+//      distance to the target, node index
+//   3. in a window of <= 64 nodes (nearly every case) each lane ranks its node against the good
+//      nodes of the window, read back from LDS by wave-uniform (broadcast) reads;
+//      a larger one is ranked tile by tile: each lane ranks its tile node and its list entry
+//      against (list U tile) by broadcasting the candidates (readlane), and entries of rank
+//      < count form the new sorted list in lanes 0..count-1.
+//      Order = (160-bit distance, node index): equal IDs only meet inside one bucket, where index
+//      order is the reference's insertion order (routing_table.cpp:75-87).
+// Must be called from wave-uniform control flow with all 64 lanes active; `t` is wave-uniform.
+// Latency ~ three dependent memory phases + ~1k VALU: the calling wave's other lanes have
+// already written their rows, and other waves hide it.
 // ---------------------------------------------------------------------------------------
-__device__ __forceinline__ void wave_lds_sync() {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_wave_barrier();
+__device__ __forceinline__ uint32_t rdl(uint32_t v, uint32_t l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ __forceinline__ uint64_t rdl64(uint64_t v, uint32_t l) {
+    return ((uint64_t)rdl((uint32_t)(v >> 32), l) << 32) | rdl((uint32_t)v, l);
+}
+__device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, uint32_t h) {
+    return ((uint64_t)(uint32_t)__shfl_xor((int)(v >> 32), (int)h, 64) << 32) | (uint32_t)__shfl_xor((int)(uint32_t)v, (int)h, 64);
+}
+// (a0, a1, a2) < (b0, b1, b2) lexicographically
+__device__ __forceinline__ bool lt3(uint64_t a0, uint64_t a1, uint64_t a2, uint64_t b0, uint64_t b1, uint64_t b2) {
+    return a0 < b0 || (a0 == b0 && (a1 < b1 || (a1 == b1 && a2 < b2)));
 }
 
-__device__ __forceinline__ uint32_t lane_rank(uint64_t mask) {  // set bits of mask below this lane
-    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
-}
+// stamp point (diagnostics): lane 0 records s_memrealtime after waiting for its memory ops
+#define XSTAMP(k)                                                               \
+    do {                                                                        \
+        if (sp && lane == 0) {                                                  \
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");         \
+            sp[k] = __builtin_amdgcn_s_memrealtime();                           \
+        }                                                                       \
+    } while (0)
 
-// LDS key tile slot: query j of the wave, 16-byte part x; parts rotated so that the 16 lanes of a
-// ds_read_b128 group and the 8 of a ds_write_b128 group hit 16 / 8 distinct bank quads.
-__device__ __forceinline__ uint32_t ktile(uint32_t j, uint32_t x) { return j * 4u + (x ^ ((j >> 2) & 3u)); }
-
-template <int K>
-__global__ __launch_bounds__(BLOCK) void rt_block_kernel(DevTable T, const uint8_t* __restrict__ targets, uint32_t q,
-                                                         uint32_t count, uint32_t* __restrict__ out_idx,
-                                                         uint8_t* __restrict__ out_cnt) {
-    static_assert(K <= 16, "block kernel: K <= 16");
-    constexpr int P = 2;  // R <= 2 covers all but ~1e-6 of k <= 16 windows on 80%-good uniform tables
-    constexpr int NR = 2 * P + 3;
-    constexpr int RQ = (NR + 2) / 2;  // 16-byte directory pieces per query (even-aligned cover of NR records)
-    constexpr uint32_t NCLS = 9;      // classes 0..8: 8-node chunks per window (MW = 1: <= 64 nodes)
-    __shared__ uint4 lds[1024 + 512 + 64 + 32];
-    uint4* stage = lds;                                   // 16 KB: targets / directory / key tiles / rows
-    uint4* state = lds + 1024;                            // 256 slots x 32 B
-    uint32_t* b_arr = reinterpret_cast<uint32_t*>(lds + 1536);
-    uint32_t* cls = reinterpret_cast<uint32_t*>(lds + 1600);  // [4][NCLS] counts, then [4][NCLS] starts
-
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const uint32_t q0 = blockIdx.x * BLOCK;
-    const uint32_t nq = min((uint32_t)BLOCK, q - q0);
-    const bool active = tid < nq;
-    const bool trivial = (T.B == 0) | (count == 0);
-    const uint32_t B = T.B;
-
-    // 1. targets -> LDS
-    {
-        const uint32_t* src32 = reinterpret_cast<const uint32_t*>(targets + 20ull * q0);
-        if (nq == BLOCK && ((uintptr_t)targets & 15u) == 0) {
-            const uint4* src = reinterpret_cast<const uint4*>(src32);
-            stage[tid] = src[tid];
-            if (tid < 64) stage[256 + tid] = src[256 + tid];
-        } else {
-            uint32_t* tw = reinterpret_cast<uint32_t*>(stage);
-            for (uint32_t k = tid; k < nq * 5; k += BLOCK) tw[k] = src32[k];
+__device__ void wave_exact(const DevTable& T, const Target& t, uint32_t count, uint32_t* row, uint8_t* cp,
+                           uint64_t* xs /* this wave's 64 x 3 LDS words */, uint64_t* sp = nullptr) {
+    const uint32_t lane = threadIdx.x & 63u, B = T.B;
+    XSTAMP(0);
+    if (B == 0 || count == 0) {
+        if (lane < count) row[lane] = NONE;
+        if (lane == 0 && cp) *cp = 0;
+        return;
+    }
+    const uint32_t b = locate_bucket(T, t);
+    uint32_t beg = 0, end = 0, good = 0;
+    for (uint32_t r0 = 0;; r0 += 64) {  // the window's good count and node range for rounds r0..r0+63
+        const uint32_t r = r0 + lane;
+        const uint32_t l_ = b > r ? b - 1 - r : 0u;
+        const uint32_t h_ = (uint64_t)b + r >= (uint64_t)B - 1 ? B - 1 : b + r;
+        const uint32_t g_ = T.gpre[h_ + 1] - T.gpre[l_];
+        const uint32_t b_ = T.dir[l_].x & ~WIDE, e_ = T.dir[h_ + 1].x & ~WIDE;
+        const uint64_t ok = __ballot(g_ >= count || (l_ == 0 && h_ == B - 1));
+        if (ok) {
+            const uint32_t R = (uint32_t)__builtin_ctzll(ok);
+            beg = rdl(b_, R);
+            end = rdl(e_, R);
+            good = rdl(g_, R);
+            break;
         }
     }
-    __syncthreads();
-    Target t{};
-    if (active) {
-        const uint32_t* tw = reinterpret_cast<const uint32_t*>(stage) + 5 * tid;
-        const uint32_t w0 = __builtin_bswap32(tw[0]), w1 = __builtin_bswap32(tw[1]);
-        t.hi = ((uint64_t)w0 << 32) | w1;
-        t.t2 = __builtin_bswap32(tw[2]);
-        t.t3 = __builtin_bswap32(tw[3]);
-        t.t4 = __builtin_bswap32(tw[4]);
-    }
-    // 2. bucket, then cooperative directory loads (each query's pieces come from its own wave)
-    const uint32_t b = (active && !trivial) ? locate_bucket(T, t) : 0u;
-    b_arr[tid] = b;
-    __syncthreads();  // targets consumed; buckets visible
-    if (!trivial) {
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-            const uint32_t qs = wid * 64 + 16 * i + (lane >> 2), part = lane & 3;
-            const uint32_t bq = b_arr[qs];
-            const int64_t r0 = (int64_t)bq - (P + 1);
-            const int64_t a = r0 & ~(int64_t)1;
-            if (part < (uint32_t)RQ && qs < nq && r0 >= 0 && a + 2 * RQ - 1 <= (int64_t)B)
-                stage[qs * RQ + part] = reinterpret_cast<const uint4*>(T.dir + a)[part];
-        }
-    }
-    wave_lds_sync();
-    Window<K> W{};
-    int st = 0;
-    if (active && !trivial) {
-        uint2 rec[NR];
-        const int64_t r0 = (int64_t)b - (P + 1);
-        if (r0 >= 0 && (r0 & ~(int64_t)1) + 2 * RQ - 1 <= (int64_t)B) {
-            // the query's pieces start at an even record; the odd shift is applied in the LDS address
-            const uint2* u = reinterpret_cast<const uint2*>(stage + tid * RQ) + (r0 & 1);
-#pragma unroll
-            for (int i = 0; i < NR; i++) rec[i] = u[i];
-        } else {
-            load_recs<P>(T, b, rec);  // first / last buckets of the table: clamped per-lane loads
-        }
-        st = rt_window<K, P>(T, b, rec, count, W);
-    }
-    uint8_t* cp_own = (out_cnt && active) ? out_cnt + q0 + tid : nullptr;
-    if (active && trivial && cp_own) *cp_own = 0;
-    if (st == WIN_DEFER && cp_own) *cp_own = DEFER_CNT;
-    // 3/4. counting sort by class
-    const uint32_t M = st == WIN_READY ? W.chunks() : 0u;
-    uint32_t myrank = 0;
-#pragma unroll
-    for (uint32_t v = 0; v < NCLS; v++) {
-        const uint64_t m = __ballot(M == v);
-        if (M == v) myrank = lane_rank(m);
-        if (lane == 0) cls[wid * NCLS + v] = (uint32_t)__builtin_popcountll(m);
-    }
-    __syncthreads();
-    if (tid == 0) {
-        uint32_t acc = 0;
-        for (uint32_t v = 0; v < NCLS; v++)
-            for (uint32_t w = 0; w < 4; w++) {
-                const uint32_t c = cls[w * NCLS + v];
-                cls[4 * NCLS + w * NCLS + v] = acc;
-                acc += c;
+    XSTAMP(1);
+    const uint32_t m = min(count, good);
+    XSTAMP(2);
+    if (end - beg <= 64) {  // one tile (nearly every case): rank by broadcast LDS reads
+        const uint32_t j = beg + lane;
+        uint64_t V0 = ~0ull, V1 = ~0ull, V2 = ~0ull;
+        bool v = false;
+        if (j < end) {  // independent loads, one phase
+            const uint8_t st = T.status[j];
+            const uint64_t k = T.key[j];
+            const uint32_t* tl = T.tail + 3ull * j;
+            const uint32_t a2 = tl[0], a3 = tl[1], a4 = tl[2];
+            v = st & KAD_STATUS_GOOD;
+            if (v) {
+                V0 = k ^ t.hi;
+                V1 = ((uint64_t)(a2 ^ t.t2) << 32) | (a3 ^ t.t3);
+                V2 = ((uint64_t)(a4 ^ t.t4) << 32) | j;
             }
-    }
-    __syncthreads();
-    const uint32_t start1 = cls[4 * NCLS + 1];  // first slot of class 1 (= class-0 population)
-    if (M) {
-        const uint32_t pos = cls[4 * NCLS + wid * NCLS + M] + myrank;
-        state[2 * pos] = make_uint4(q0 + tid, (uint32_t)t.hi, (uint32_t)(t.hi >> 32), W.base);
-        state[2 * pos + 1] = make_uint4(W.ne, W.good, (uint32_t)W.gm[0], (uint32_t)(W.gm[0] >> 32));
-    }
-    __syncthreads();
-    // 5. rank: slot tid's query, key tiles loaded cooperatively per wave
-    const bool mine = tid >= start1;
-    uint32_t qid = 0, sgood = 0;
-    Window<K> S{};
-    uint64_t th = 0;
-    if (mine) {
-        const uint4 a0 = state[2 * tid], a1 = state[2 * tid + 1];
-        qid = a0.x;
-        th = ((uint64_t)a0.z << 32) | a0.y;
-        S.base = a0.w;
-        S.ne = a1.x;
-        sgood = a1.y;
-        S.gm[0] = ((uint64_t)a1.w << 32) | a1.z;
-    }
-    const uint32_t Ms = mine ? S.chunks() : 0u;
-    uint32_t lbase[4], lM[4];
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-        const uint32_t si = wid * 64 + 16 * i + (lane >> 2);
-        const uint4 a0 = state[2 * si], a1 = state[2 * si + 1];
-        lbase[i] = a0.w;
-        lM[i] = si >= start1 ? (a1.x - a0.w + 7) >> 3 : 0u;
-    }
-    uint4* tile = stage + wid * 256;
-    TopK<K> L;
-    L.init();
-    bool ones = false;
-    for (uint32_t c = 0; __ballot(c < Ms) != 0; c++) {
-#pragma unroll
-        for (int i = 0; i < 4; i++)
-            if (c < lM[i])
-                tile[ktile(16 * i + (lane >> 2), lane & 3)] =
-                    reinterpret_cast<const uint4*>(T.key + lbase[i] + 8 * c)[lane & 3];
-        wave_lds_sync();
-        if (c < Ms) {
-            uint4 kv[4];
-#pragma unroll
-            for (int x = 0; x < 4; x++) kv[x] = tile[ktile(lane, x)];
-            rank_chunk<K>(L, kv, th, chunk_bits<K>(S, 8 * c), S.base + 8 * c, ones);
         }
-        wave_lds_sync();
-    }
-    // 6. rows -> LDS (query order) -> coalesced stores
-    __syncthreads();
-    uint32_t* rows = reinterpret_cast<uint32_t*>(stage);
-    if (mine) {
-        const uint32_t loc = qid - q0;
-        if (ones) {
-            if (out_cnt) out_cnt[qid] = DEFER_CNT;
-            else rows[loc * count] = DEFER_IDX;
-        } else {
-            const uint32_t m = min(sgood, count);
-#pragma unroll
-            for (int s2 = 0; s2 < K; s2++)
-                if ((uint32_t)s2 < count) rows[loc * count + s2] = (uint32_t)s2 < m ? L.di[s2] + T.index_base : NONE;
-            if (out_cnt) out_cnt[qid] = (uint8_t)m;
+        xs[3 * lane] = V0;
+        xs[3 * lane + 1] = V1;
+        xs[3 * lane + 2] = V2;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        XSTAMP(3);
+        // rank on the top 64 distance bits (unique unless two nodes share them); ties -> full order
+        uint32_t lt = 0, le = 0;
+#pragma unroll 16
+        for (uint32_t sl = 0; sl < 64; sl++) {
+            const uint64_t S0 = xs[3 * sl];  // wave-uniform address: broadcast read
+            lt += S0 < V0;
+            le += S0 <= V0;
         }
+        uint32_t rank = lt;
+        if (__ballot(v && le - lt > 1)) {
+            rank = 0;
+            for (uint64_t mm = __ballot(v); mm; mm &= mm - 1) {
+                const uint32_t sl = (uint32_t)__builtin_ctzll(mm);
+                rank += lt3(xs[3 * sl], xs[3 * sl + 1], xs[3 * sl + 2], V0, V1, V2);
+            }
+        }
+        XSTAMP(4);
+        __builtin_amdgcn_wave_barrier();  // xs is reused by the wave's next query
+        if (v && rank < count) row[rank] = j + T.index_base;
+        if (lane >= m && lane < count) row[lane] = NONE;
+        if (lane == 0 && cp) *cp = (uint8_t)m;
+        return;
     }
-    if (active && M == 0) {  // trivial (NONE rows) or deferred (marker row when there are no counts)
-        for (uint32_t s2 = 0; s2 < count; s2++) rows[tid * count + s2] = NONE;
-        if (st == WIN_DEFER && !out_cnt && count) rows[tid * count] = DEFER_IDX;
+    uint64_t L0 = ~0ull, L1 = ~0ull, L2 = ~0ull;  // list entry of this lane (lanes < nl)
+    uint32_t nl = 0;
+    for (uint32_t base = beg; base < end; base += 64) {
+        const uint32_t j = base + lane;
+        bool cv = false;
+        uint64_t C0 = 0, C1 = 0, C2 = 0;  // (dist bits 0..63, dist bits 64..127, dist bits 128..159 : index)
+        if (j < end) {
+            cv = T.status[j] & KAD_STATUS_GOOD;
+            const uint32_t* tl = T.tail + 3ull * j;
+            C0 = T.key[j] ^ t.hi;
+            C1 = ((uint64_t)(tl[0] ^ t.t2) << 32) | (tl[1] ^ t.t3);
+            C2 = ((uint64_t)(tl[2] ^ t.t4) << 32) | j;
+        }
+        const bool lv = lane < nl;
+        const uint64_t cm = __ballot(cv);
+        uint32_t rL = 0, rC = 0;
+        for (uint64_t mm = cm; mm; mm &= mm - 1) {
+            const uint32_t sl = (uint32_t)__builtin_ctzll(mm);
+            const uint64_t S0 = rdl64(C0, sl), S1 = rdl64(C1, sl), S2 = rdl64(C2, sl);
+            rL += lt3(S0, S1, S2, L0, L1, L2);
+            rC += lt3(S0, S1, S2, C0, C1, C2);
+        }
+        for (uint32_t e = 0; e < nl; e++) {
+            const uint64_t S0 = rdl64(L0, e), S1 = rdl64(L1, e), S2 = rdl64(L2, e);
+            rL += lt3(S0, S1, S2, L0, L1, L2);
+            rC += lt3(S0, S1, S2, C0, C1, C2);
+        }
+        const uint32_t nn = min(nl + (uint32_t)__builtin_popcountll(cm), count);
+        uint64_t N0 = ~0ull, N1 = ~0ull, N2 = ~0ull;
+        for (uint32_t r = 0; r < nn; r++) {
+            const uint64_t mL = __ballot(lv && rL == r), mC = __ballot(cv && rC == r);
+            uint64_t S0, S1, S2;
+            if (mL) {
+                const uint32_t sl = (uint32_t)__builtin_ctzll(mL);
+                S0 = rdl64(L0, sl); S1 = rdl64(L1, sl); S2 = rdl64(L2, sl);
+            } else {
+                const uint32_t sl = (uint32_t)__builtin_ctzll(mC);
+                S0 = rdl64(C0, sl); S1 = rdl64(C1, sl); S2 = rdl64(C2, sl);
+            }
+            if (lane == r) { N0 = S0; N1 = S1; N2 = S2; }
+        }
+        L0 = N0; L1 = N1; L2 = N2;
+        nl = nn;
     }
-    __syncthreads();
-    uint32_t* dst = out_idx + (size_t)q0 * count;
-    for (uint32_t k = tid; k < nq * count; k += BLOCK) dst[k] = rows[k];
+    if (lane < count) row[lane] = lane < m ? (uint32_t)L2 + T.index_base : NONE;
+    if (lane == 0 && cp) *cp = (uint8_t)m;
 }
 
+// The exact path for every lane of the wave whose fast path gave up (`ex`), one query at a time.
+// `pick` maps a lane's flag to the table it queries (dual-family kernel) - here a single table.
+__device__ __forceinline__ void exact_tail(const DevTable& T, const Target& t, bool ex, uint32_t i, uint32_t count,
+                                           uint32_t* out_idx, uint8_t* out_cnt, uint64_t* xs) {
+    for (uint64_t m = __ballot(ex); m; m &= m - 1) {
+        const uint32_t l = (uint32_t)__builtin_ctzll(m);
+        Target u;
+        u.hi = rdl64(t.hi, l);
+        u.t2 = rdl(t.t2, l);
+        u.t3 = rdl(t.t3, l);
+        u.t4 = rdl(t.t4, l);
+        const uint32_t il = rdl(i, l);
+        wave_exact(T, u, count, out_idx + (size_t)il * count, out_cnt ? out_cnt + il : nullptr, xs);
+    }
+}
+
+// Exact-path queue of the record kernel: the kernel appends the queries its fast path cannot rank
+// (wave-aggregated atomic add), and rt_exact_list_kernel, launched right after on the same stream,
+// answers each with one wave (wave_exact) and resets the counter. Inline wave_exact cost the
+// record kernel ~18 us per 1M queries (0.3% of lanes stall 19% of the waves); the queue turns it
+// into one short launch. Scratch is per (table, stream): see kad_table::exact_scratch.
+struct ExactQ {
+    uint32_t* ctr;   // [0] entries appended, [1] blocks of the list kernel done
+    uint32_t* list;  // 32-byte entries: query index, target (hi64, t2, t3, t4)
+    uint32_t cap;
+};
+
+__device__ __forceinline__ void exact_enqueue(const ExactQ& Q, const DevTable& T, const Target& t, bool ex, uint32_t i,
+                                              uint32_t count, uint32_t* out_idx, uint8_t* out_cnt, uint64_t* xs) {
+    const uint64_t m = __ballot(ex);
+    if (!m) return;
+    if (Q.cap == 0) {  // no queue: answer inline
+        exact_tail(T, t, ex, i, count, out_idx, out_cnt, xs);
+        return;
+    }
+    const uint32_t lane = threadIdx.x & 63u, first = (uint32_t)__builtin_ctzll(m);
+    uint32_t base = 0;
+    if (lane == first) base = atomicAdd(Q.ctr, (uint32_t)__builtin_popcountll(m));
+    base = rdl(base, first);
+    const uint32_t pos = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    const bool over = ex && pos >= Q.cap;
+    if (ex && !over) {  // entry = query index + its target (the list kernel needs no second load)
+        uint4* e = reinterpret_cast<uint4*>(Q.list) + 2ull * pos;
+        e[0] = make_uint4(i, (uint32_t)t.hi, (uint32_t)(t.hi >> 32), t.t2);
+        e[1] = make_uint4(t.t3, t.t4, 0u, 0u);
+    }
+    exact_tail(T, t, over, i, count, out_idx, out_cnt, xs);  // queue full: answer inline
+}
+
+// Diagnostics (KAD_EXACT_STAMPS=1, tools/exact_stamps.py): per wave s_memrealtime at entry, after the
+// counter read, after its first item and at exit (100 MHz ticks), for waves < STAMP_WAVES.
+constexpr uint32_t STAMP_WAVES = 4096;
+__device__ uint64_t g_stamps[STAMP_WAVES * 12];
+
+template <bool ST>
+__global__ __launch_bounds__(BLOCK) void rt_exact_list_kernel(DevTable T, ExactQ Q, const uint8_t* __restrict__ targets,
+                                                              uint32_t count, uint32_t* __restrict__ out_idx,
+                                                              uint8_t* __restrict__ out_cnt) {
+    const uint32_t w = (blockIdx.x * BLOCK + threadIdx.x) >> 6, nw = gridDim.x * (BLOCK / 64);
+    const bool st = ST && w < STAMP_WAVES && (threadIdx.x & 63) == 0;
+    if (st) g_stamps[4 * w] = __builtin_amdgcn_s_memrealtime();
+    const uint32_t n = min(__hip_atomic_load(Q.ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), Q.cap);
+    if (st) g_stamps[4 * w + 1] = __builtin_amdgcn_s_memrealtime() | ((uint64_t)(w < n) << 63);
+    __shared__ uint64_t xs[BLOCK / 64][192];
+    uint4 e0 = make_uint4(0, 0, 0, 0), e1 = e0;
+    if (w < Q.cap) {  // the wave's first entry, loaded together with the counter
+        const uint4* e = reinterpret_cast<const uint4*>(Q.list) + 2ull * w;
+        e0 = e[0];
+        e1 = e[1];
+    }
+    for (uint32_t k = w; k < n; k += nw) {
+        if (k != w) {
+            const uint4* e = reinterpret_cast<const uint4*>(Q.list) + 2ull * k;
+            e0 = e[0];
+            e1 = e[1];
+        }
+        Target t;
+        t.hi = ((uint64_t)e0.z << 32) | e0.y;
+        t.t2 = e0.w;
+        t.t3 = e1.x;
+        t.t4 = e1.y;
+        const uint32_t i = e0.x;
+        wave_exact(T, t, count, out_idx + (size_t)i * count, out_cnt ? out_cnt + i : nullptr, xs[threadIdx.x >> 6],
+                   (ST && k == w && w < STAMP_WAVES) ? g_stamps + STAMP_WAVES * 4 + 8 * w : nullptr);
+        if (st && k == w) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            g_stamps[4 * w + 2] = __builtin_amdgcn_s_memrealtime();
+        }
+    }
+    if (st) g_stamps[4 * w + 3] = __builtin_amdgcn_s_memrealtime();
+    __syncthreads();
+    if (threadIdx.x == 0 && atomicAdd(Q.ctr + 1, 1u) == gridDim.x - 1) {  // every block has read ctr[0]
+        atomicExch(Q.ctr, 0u);
+        atomicExch(Q.ctr + 1, 0u);
+    }
+}
+constexpr uint32_t EXACT_LIST_BLOCKS = 1024;  // 4096 waves: one wave_exact latency for <= 4096 entries
+
+// Lane-per-query RoutingTable kernel (any table shape, count <= 32).
 template <int K>
 __global__ __launch_bounds__(BLOCK) void rt_closest_kernel(DevTable T, const uint8_t* __restrict__ targets,
                                                            uint32_t q, uint32_t count,
                                                            uint32_t* __restrict__ out_idx,
                                                            uint8_t* __restrict__ out_cnt) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
-    if (i >= q) return;
-    const Target t = load_target(targets, i);
-    uint32_t* row = out_idx + (size_t)i * count;
-    uint8_t* cp = out_cnt ? out_cnt + i : nullptr;
-    if (!rt_query_fast<K, (K > 16 ? 6 : 3)>(T, t, count, row, cp)) mark_deferred(row, cp);
-}
-
-// Debug ablation of the lane kernel (KAD_RT_KERNEL=abl1|abl2|abl3): 1 = target + locate + store,
-// 2 = + directory window, 3 = + key loads without ranking. Results are garbage; timing only.
-template <int K, int ABL>
-__global__ __launch_bounds__(BLOCK) void rt_ablate_kernel(DevTable T, const uint8_t* __restrict__ targets, uint32_t q,
-                                                          uint32_t count, uint32_t* __restrict__ out_idx,
-                                                          uint8_t* __restrict__ out_cnt) {
-    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
-    if (i >= q) return;
-    const Target t = load_target(targets, i);
-    uint32_t* row = out_idx + (size_t)i * count;
-    const uint32_t b = locate_bucket(T, t);
-    uint32_t acc = b ^ (uint32_t)t.hi;
-    if (ABL >= 2) {
-        uint2 rec[7];
-        load_recs<2>(T, b, rec);
-        Window<K> W;
-        const int st = rt_window<K, 2>(T, b, rec, count, W);
-        acc += st + W.base + W.ne + (uint32_t)W.gm[0];
-        if (ABL >= 3 && st == WIN_READY) {
-            const uint4* kp = reinterpret_cast<const uint4*>(T.key + W.base);
-            const uint32_t M = W.chunks();
-            for (uint32_t c = 0; c < M; c++) {
-                uint4 kv[4];
-#pragma unroll
-                for (int x = 0; x < 4; x++) kv[x] = kp[4 * c + x];
-#pragma unroll
-                for (int x = 0; x < 4; x++) acc += kv[x].x ^ kv[x].y ^ kv[x].z ^ kv[x].w;
-            }
-        }
+    bool ex = false;
+    Target t{};
+    if (i < q) {
+        t = load_target(targets, i);
+        ex = !rt_query_fast<K, (K > 16 ? 6 : 3)>(T, t, count, out_idx + (size_t)i * count, out_cnt ? out_cnt + i : nullptr);
     }
-    uint4 v = make_uint4(acc, acc, acc, acc);
-    *reinterpret_cast<uint4*>(row) = v;
-    *reinterpret_cast<uint4*>(row + 4) = v;
-    if (out_cnt) out_cnt[i] = 0;
+    __shared__ uint64_t xs[BLOCK / 64][192];
+    exact_tail(T, t, ex, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
 }
 
 // ---------------------------------------------------------------------------------------
-// Bucket-line RoutingTable kernel (direct-mapped tables of uniform depth d <= 32, the U(d) shape).
+// Bucket-record RoutingTable kernel (count <= 8; direct-mapped tables of uniform depth d <= 48,
+// the U(d) shape of the bench shards). The default kernel where the table supports it.
 //
-// Random gathers on MI355X cost per 128-byte line touched (~50 G random lines/s whether 32, 64 or
-// 128 bytes of it are used: tools/microbench.py), so the window is laid out to touch as few lines
-// as possible. Each bucket is one 64-byte record:
-//   w0 = first node index (27 bits) | n << 27 (n = BL_OVF if the bucket does not fit)
-//   w1 = good bitmask (bits 0..13) | "needs the exact compare" bitmask (bits 16..29)
-//   w2..w15 = key32 of each node = ID bits [d, d + 32), right after the bucket's d-bit prefix.
-// The round-0 window {b-1, b} is 128 contiguous bytes. Buckets are dyadic, so a node's XOR distance
-// is ordered by (bucket prefix XOR target prefix, key32 XOR target bits [d, d+32)): that 64-bit
-// rank key is exact in the top d+32 distance bits; two nodes can tie only inside one bucket on
-// equal key32, and those nodes carry the exact-compare bit (the query is deferred).
+// A random gather on MI355X costs one 128-byte line whether 32 or 128 bytes of it are used, and
+// wherever the table sits (tools/mb_line.py: ~34 G lines/s with the target read and row write,
+// the same for 128 MB and 1 GB tables), so a query should touch exactly ONE line. Each bucket is
+// a 32-byte record:
+//   dword 0    first node index (27 bits) | good count G (4 bits) << 27 | defer flag << 31
+//   halfword 2 good bitmask of the bucket's nodes (slot s = node first + s; at most 16 nodes)
+//   halfwords 3..15  key16 of the bucket's good nodes in slot order (at most 13): ID bits [d, d+16)
+// The defer flag marks a record the kernel cannot rank exactly (more than 16 nodes, more than 13
+// good nodes, or two good nodes with equal key16); a query whose window holds one takes the
+// wave-cooperative exact path (wave_exact).
+//
+// Layout: record r = bucket + 2 (two empty records precede bucket 0, empty records pad the end).
+// The records are stored in FOUR copies, copy c cut into aligned 128-byte lines that start at
+// records r = c (mod 4): line k of copy c holds records 4k+c .. 4k+c+3. Bucket b's rounds 0 and 1,
+// buckets b-2 .. b+1 = records b .. b+3, are then line b/4 of copy b%4: one aligned line, always.
+// (4 x 32 B per bucket: 268 MB for a 2^21-bucket shard; table size does not change the gather
+// rate.) Windows needing round 2 (~0.14% at k = 8 on an 80%-good uniform shard) take wave_exact.
+//
+// Ranking. Buckets of equal depth are dyadic: the XOR images of two of them are disjoint
+// intervals ordered by D = prefix(bucket) XOR prefix(b), and inside one bucket the order is that
+// of key16 XOR the target's bits [d, d+16) (exact: two good nodes of a record never share key16).
+// So a node's rank value is the 32-bit word (ord(D) << 23 | record << 20 | key16^t16 << 4 | g),
+// g = its index among the record's good nodes. Each record's up-to-13 values go through a
+// 45-comparator min/max network that leaves its 8 smallest sorted; the per-record lists are merged
+// by bitonic 8+8 merges (min/max only: 2 VALU ops per compare-exchange). The output slot of
+// value (record, g) is the g-th set bit of the record's good mask.
+// Reference semantics: routing_table.cpp:67-111 (window rounds, sorted insertion, truncation).
 // ---------------------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t bl_key_word(const uint4& a, const uint4& b, const uint4& c, const uint4& e, int s) {
-    switch (s) {  // slot s lives in dword 2 + s of the line (static after unrolling)
-        case 0: return a.z; case 1: return a.w;
-        case 2: return b.x; case 3: return b.y; case 4: return b.z; case 5: return b.w;
-        case 6: return c.x; case 7: return c.y; case 8: return c.z; case 9: return c.w;
-        case 10: return e.x; case 11: return e.y; case 12: return e.z; default: return e.w;
-    }
+constexpr uint32_t REC_FIRST_MASK = (1u << 27) - 1;
+constexpr uint32_t REC_MAXG = 13;
+constexpr uint32_t REC_PAD = 2;
+constexpr uint32_t REC_NONE = 0xFFFFFFFFu;
+
+__device__ __forceinline__ uint32_t rec_half(const uint4& lo, const uint4& hi, int h) {
+    const int w = h >> 1;  // static after unrolling
+    const uint32_t d = w == 0 ? lo.x : w == 1 ? lo.y : w == 2 ? lo.z : w == 3 ? lo.w
+                     : w == 4 ? hi.x : w == 5 ? hi.y : w == 6 ? hi.z : hi.w;
+    return (h & 1) ? d >> 16 : d & 0xFFFFu;
 }
 
-// One bucket line held in registers, with its rank-relevant values.
-struct BlLine {
-    uint4 v[4];
-    uint32_t gm, off, good;  // good bitmask, first node index, good count
-    uint64_t D;              // bucket prefix XOR target prefix (orders whole buckets)
-    bool present;
-};
-
-__device__ __forceinline__ void bl_load(const DevTable& T, uint32_t w, BlLine& L) {
-    const uint4* p = T.bl + 4ull * w;
-#pragma unroll
-    for (int x = 0; x < 4; x++) L.v[x] = p[x];
+__device__ __forceinline__ void cx(uint32_t& a, uint32_t& b) {
+    const uint32_t lo = min(a, b);
+    b = max(a, b);
+    a = lo;
 }
 
-__device__ __forceinline__ void bl_header(BlLine& L, uint64_t D, bool present, bool& bad) {
-    L.present = present;
-    L.D = D;
-    const uint32_t nf = L.v[0].x >> 27, xm = L.v[0].y >> 16;
-    L.gm = present ? (L.v[0].y & 0xFFFFu) : 0u;
-    L.off = L.v[0].x & BL_OFF_MASK;
-    L.good = __builtin_popcount(L.gm);
-    bad |= present & ((nf == BL_OVF) | ((L.gm & xm) != 0));
+// Batcher's 16-input odd-even merge sort restricted to 13 inputs and pruned to the 8 smallest
+// outputs (tools/netgen.py; checked exhaustively by the 0-1 principle in tests/test_networks.py).
+constexpr int NET13_TOP8_LEN = 45;
+__device__ constexpr uint8_t NET13_TOP8[NET13_TOP8_LEN][2] = {
+    {0, 1}, {2, 3}, {4, 5}, {6, 7}, {8, 9}, {10, 11}, {0, 2}, {1, 3}, {4, 6}, {5, 7}, {8, 10}, {9, 11},
+    {1, 2}, {5, 6}, {9, 10}, {0, 4}, {1, 5}, {2, 6}, {3, 7}, {8, 12}, {2, 4}, {3, 5}, {10, 12}, {1, 2},
+    {3, 4}, {5, 6}, {9, 10}, {11, 12}, {0, 8}, {1, 9}, {2, 10}, {3, 11}, {4, 12}, {4, 8}, {5, 9}, {6, 10},
+    {7, 11}, {2, 4}, {3, 5}, {6, 8}, {7, 9}, {1, 2}, {3, 4}, {5, 6}, {7, 8}};
+
+// a = the 8 smallest of (a, s), sorted; a and s sorted ascending on entry.
+__device__ __forceinline__ void merge8(uint32_t (&a)[8], const uint32_t (&s)[8]) {
+#pragma unroll
+    for (int i = 0; i < 8; i++) a[i] = min(a[i], s[7 - i]);  // bitonic
+#pragma unroll
+    for (int i = 0; i < 4; i++) cx(a[i], a[i + 4]);
+#pragma unroll
+    for (int i = 0; i < 8; i++)
+        if ((i & 2) == 0) cx(a[i], a[i + 2]);
+#pragma unroll
+    for (int i = 0; i < 8; i += 2) cx(a[i], a[i + 1]);
 }
 
-// Rank every good node of line L among the good nodes of its own bucket (32-bit keys suffice: the
-// nodes of one bucket share its prefix) and place it at base + rank among the K output slots.
-template <int K>
-__device__ __forceinline__ void bl_place(const BlLine& L, uint32_t base, uint32_t t32, uint32_t (&out)[K]) {
-    uint32_t k[BL_CAP];
+// The 8 smallest rank values of one record (NONE-padded), sorted.
+__device__ __forceinline__ void rec_rank(const uint4& lo, const uint4& hi, bool inw, uint32_t tag, uint32_t t16,
+                                         uint32_t (&s)[8]) {
+    const uint32_t G = inw ? (lo.x >> 27) & 15u : 0u;
+    uint32_t v[REC_MAXG];
 #pragma unroll
-    for (int s2 = 0; s2 < (int)BL_CAP; s2++) k[s2] = bl_key_word(L.v[0], L.v[1], L.v[2], L.v[3], s2) ^ t32;
-    uint32_t ns = 0;  // one past the highest good slot over the wave: bounds both loops
+    for (int e = 0; e < (int)REC_MAXG; e++)
+        v[e] = (uint32_t)e < G ? (tag | ((rec_half(lo, hi, 3 + e) ^ t16) << 4) | (uint32_t)e) : REC_NONE;
 #pragma unroll
-    for (int s2 = 0; s2 < (int)BL_CAP; s2++) ns = __any((L.gm >> s2) != 0) ? (uint32_t)s2 + 1 : ns;
+    for (int c = 0; c < NET13_TOP8_LEN; c++) cx(v[NET13_TOP8[c][0]], v[NET13_TOP8[c][1]]);
 #pragma unroll
-    for (int s2 = 0; s2 < (int)BL_CAP; s2++) {
-        if ((uint32_t)s2 >= ns) break;
-        uint32_t r = base;
-#pragma unroll
-        for (int u = 0; u < (int)BL_CAP; u++) {
-            if ((uint32_t)u >= ns) break;
-            r += ((L.gm >> u) & 1u) & (uint32_t)(k[u] < k[s2]);
-        }
-        const bool g = (L.gm >> s2) & 1u;
-#pragma unroll
-        for (int j = 0; j < K; j++) out[j] = (g & (r == (uint32_t)j)) ? L.off + s2 : out[j];
-    }
+    for (int j = 0; j < 8; j++) s[j] = v[j];
 }
 
-template <int K>
-__global__ __launch_bounds__(BLOCK) void rt_bl_kernel(DevTable T, const uint8_t* __restrict__ targets, uint32_t q,
-                                                      uint32_t count, uint32_t* __restrict__ out_idx,
-                                                      uint8_t* __restrict__ out_cnt) {
+// Index of the g-th set bit of a 16-bit mask (g < popcount(mask)).
+__device__ __forceinline__ uint32_t select_bit16(uint32_t m, uint32_t g) {
+    uint32_t s = 0, c;
+    c = __builtin_popcount(m & 0xFFu);
+    if (g >= c) { g -= c; m >>= 8; s = 8; }
+    c = __builtin_popcount(m & 0xFu);
+    if (g >= c) { g -= c; m >>= 4; s += 4; }
+    c = __builtin_popcount(m & 0x3u);
+    if (g >= c) { g -= c; m >>= 2; s += 2; }
+    return s + (g >= (m & 1u) ? 1u : 0u);
+}
+
+// ABL (timing ablations only, KAD_RT_KERNEL=rec_abl1|rec_abl2, results wrong): 1 = no exact
+// path, 2 = also no ranking networks.
+template <int K, int ABL>
+__global__ __launch_bounds__(BLOCK) void rt_rec_kernel(DevTable T, ExactQ Q, const uint8_t* __restrict__ targets,
+                                                       uint32_t q, uint32_t count, uint32_t* __restrict__ out_idx,
+                                                       uint8_t* __restrict__ out_cnt) {
+    static_assert(K == 8, "record kernel: count <= 8");
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
-    if (i >= q) return;
-    uint32_t* row = out_idx + (size_t)i * count;
-    uint8_t* cp = out_cnt ? out_cnt + i : nullptr;
-    if (count == 0) {
-        if (cp) *cp = 0;
-        return;
-    }
-    const Target t = load_target(targets, i);
-    const uint32_t B = T.B, d = 64 - T.rshift;
-    const uint32_t b = locate_bucket(T, t);
-    const uint64_t pre0 = T.rbase >> T.rshift, tp = t.hi >> T.rshift;
-    const uint32_t t32 = (uint32_t)((t.hi << d) >> 32);
-    bool bad = false;
-    // Round 0 window {b-1, b}: both lines in flight together. Round 1 adds {b-2, b+1}; later
-    // rounds (~0.3% of k=8 queries on an 80%-good U(24) shard) are deferred.
-    BlLine Lb, Ll, Lh, Ll2;
-    const bool hasl = b > 0;
-    bl_load(T, b, Lb);
-    bl_load(T, hasl ? b - 1 : b, Ll);
-    bl_header(Lb, (pre0 + b) ^ tp, true, bad);
-    bl_header(Ll, (pre0 + b - 1) ^ tp, hasl, bad);
-    uint32_t good = Lb.good + Ll.good;
-    const bool whole0 = (b <= 1) & (b >= B - 1);
-    const bool r1 = (good < count) & !whole0;
-    const bool hash = r1 & (b + 1 < B), hasl2 = r1 & (b >= 2);
-    if (r1) {
-        bl_load(T, hash ? b + 1 : b, Lh);
-        bl_load(T, hasl2 ? b - 2 : b, Ll2);
-    }
-    bl_header(Lh, (pre0 + b + 1) ^ tp, hash, bad);
-    bl_header(Ll2, (pre0 + b - 2) ^ tp, hasl2, bad);
-    good += Lh.good + Ll2.good;
-    const bool whole1 = (b <= 2) & (b + 1 >= B - 1);
-    bad |= r1 & (good < count) & !whole1;
-    if (bad) {
-        mark_deferred(row, cp);
-        return;
-    }
-    // whole buckets are ordered by D (the XOR images of disjoint dyadic buckets are disjoint intervals)
-    auto base_of = [&](const BlLine& X) {
-        return (Ll.present & (Ll.D < X.D) ? Ll.good : 0u) + (Lb.D < X.D ? Lb.good : 0u) +
-               (Lh.present & (Lh.D < X.D) ? Lh.good : 0u) + (Ll2.present & (Ll2.D < X.D) ? Ll2.good : 0u);
-    };
-    uint32_t out[K];
+    bool ex = false;
+    Target t{};
+    if (i < q && count == 0) {
+        if (out_cnt) out_cnt[i] = 0;
+    } else if (i < q) {
+        uint32_t* row = out_idx + (size_t)i * count;
+        t = load_target(targets, i);
+        const uint32_t B = T.B, d = 64 - T.rshift;
+        const uint32_t b = locate_bucket(T, t);
+        const uint32_t t16 = (uint32_t)((t.hi << d) >> 48);
+        const uint4* L = T.rec + 8ull * ((size_t)(b & 3u) * T.rec_lines + (b >> 2));  // records b-2 .. b+1
+        uint4 v[8];
 #pragma unroll
-    for (int j = 0; j < K; j++) out[j] = NONE;
-    bl_place<K>(Lb, base_of(Lb), t32, out);
-    bl_place<K>(Ll, base_of(Ll), t32, out);
-    if (__any(r1)) {
-        bl_place<K>(Lh, base_of(Lh), t32, out);
-        bl_place<K>(Ll2, base_of(Ll2), t32, out);
-    }
-    const uint32_t m = min(good, count);
-    if (count == (uint32_t)K && (K % 4) == 0) {
+        for (int x = 0; x < 8; x++) v[x] = L[x];
+        const uint32_t G0 = (v[0].x >> 27) & 15u, G1 = (v[2].x >> 27) & 15u, G2 = (v[4].x >> 27) & 15u,
+                       G3 = (v[6].x >> 27) & 15u;
+        const uint32_t good0 = G1 + G2;  // {b-1, b}
+        const bool r0 = good0 >= count || ((b <= 1) & (b + 1 >= B));
+        const uint32_t good1 = good0 + G0 + G3;  // + {b-2, b+1}
+        const bool r1 = !r0 && (good1 >= count || ((b <= 2) & (b + 2 >= B)));
+        ex = !(r0 | r1) | (v[2].x >> 31) | (v[4].x >> 31) | (r1 & ((v[0].x | v[6].x) >> 31));
+        if (!ex) {
+            // bucket order by D = prefix XOR the target's top d bits (b is first unless the target
+            // lies outside the table's range and was clamped to bucket 0 or B-1)
+            const uint64_t pb = (T.rbase >> T.rshift) + b, tp = t.hi >> T.rshift;
+            const uint64_t dm2 = (pb - 2) ^ tp, dm1 = (pb - 1) ^ tp, d00 = pb ^ tp, dp1 = (pb + 1) ^ tp;
+            const uint32_t om2 = (dm1 < dm2) + (d00 < dm2) + (dp1 < dm2), om1 = (dm2 < dm1) + (d00 < dm1) + (dp1 < dm1),
+                           o00 = (dm2 < d00) + (dm1 < d00) + (dp1 < d00), op1 = (dm2 < dp1) + (dm1 < dp1) + (d00 < dp1);
+            uint32_t acc[8], s[8];
+            if (ABL >= 2) {
 #pragma unroll
-        for (int j = 0; j < K; j += 4)
-            *reinterpret_cast<uint4*>(row + j) =
-                make_uint4((uint32_t)j < m ? out[j] + T.index_base : NONE,
-                           (uint32_t)j + 1 < m ? out[j + 1] + T.index_base : NONE,
-                           (uint32_t)j + 2 < m ? out[j + 2] + T.index_base : NONE,
-                           (uint32_t)j + 3 < m ? out[j + 3] + T.index_base : NONE);
-    } else {
+                for (int j = 0; j < 8; j++) acc[j] = (v[j].z ^ om1 ^ t16) & 0x7FFFFFu;
+            } else {
+                rec_rank(v[2], v[3], true, (om1 << 23) | (1u << 20), t16, acc);  // b-1
+                rec_rank(v[4], v[5], true, (o00 << 23) | (2u << 20), t16, s);    // b
+                merge8(acc, s);
+                if (__any(r1)) {
+                    rec_rank(v[0], v[1], r1, (om2 << 23) | (0u << 20), t16, s);  // b-2
+                    merge8(acc, s);
+                    rec_rank(v[6], v[7], r1, (op1 << 23) | (3u << 20), t16, s);  // b+1
+                    merge8(acc, s);
+                }
+            }
+            const uint32_t m = min(r0 ? good0 : good1, count);
+            uint32_t o[8];
 #pragma unroll
-        for (int j = 0; j < K; j++)
-            if ((uint32_t)j < count) row[j] = (uint32_t)j < m ? out[j] + T.index_base : NONE;
+            for (int j = 0; j < 8; j++) {
+                const uint32_t pv = acc[j], p = (pv >> 20) & 3u;
+                const uint32_t h = p == 0 ? v[0].x : p == 1 ? v[2].x : p == 2 ? v[4].x : v[6].x;
+                const uint32_t mk = (p == 0 ? v[0].y : p == 1 ? v[2].y : p == 2 ? v[4].y : v[6].y) & 0xFFFFu;
+                o[j] = (uint32_t)j < m ? (h & REC_FIRST_MASK) + select_bit16(mk, pv & 15u) + T.index_base : NONE;
+            }
+            if (count == 8) {
+                reinterpret_cast<uint4*>(row)[0] = make_uint4(o[0], o[1], o[2], o[3]);
+                reinterpret_cast<uint4*>(row)[1] = make_uint4(o[4], o[5], o[6], o[7]);
+            } else {
+#pragma unroll
+                for (int j = 0; j < 8; j++)
+                    if ((uint32_t)j < count) row[j] = o[j];
+            }
+            if (out_cnt) out_cnt[i] = (uint8_t)m;
+        }
     }
-    if (cp) *cp = (uint8_t)m;
+    __shared__ uint64_t xs[BLOCK / 64][192];
+    if (ABL == 0) exact_enqueue(Q, T, t, ex, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
 }
 
-// Good bitmasks of the bucket lines after a status change (exact-compare bits are kept).
-__global__ void bl_good_kernel(const uint8_t* status, uint4* bl, uint32_t B) {
+// Bucket records after a status change (or at table creation): one thread per bucket.
+__global__ void rec_build_kernel(const uint64_t* key, const uint8_t* status, const uint2* dir, uint32_t B, uint32_t d,
+                                 uint4* rec, uint32_t rec_lines) {
     const uint32_t b = blockIdx.x * BLOCK + threadIdx.x;
     if (b >= B) return;
-    uint4 h = bl[4ull * b];
-    const uint32_t off = h.x & BL_OFF_MASK, nf = h.x >> 27;
-    if (nf == BL_OVF) return;
-    uint32_t gm = 0;
-    for (uint32_t s2 = 0; s2 < nf; s2++) gm |= (uint32_t)(status[off + s2] & KAD_STATUS_GOOD) << s2;
-    h.y = (h.y & 0xFFFF0000u) | gm;
-    bl[4ull * b] = h;
-}
-
-// Second pass over the batch: the (rare) queries the fast kernel deferred, exact per-node path.
-template <int K>
-__global__ __launch_bounds__(BLOCK) void rt_closest_deferred_kernel(DevTable T, const uint8_t* __restrict__ targets,
-                                                                    uint32_t q, uint32_t count,
-                                                                    uint32_t* __restrict__ out_idx,
-                                                                    uint8_t* __restrict__ out_cnt) {
-    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
-    if (i >= q) return;
-    uint32_t* row = out_idx + (size_t)i * count;
-    uint8_t* cp = out_cnt ? out_cnt + i : nullptr;
-    if (!is_deferred(row, cp)) return;
-    const Target t = load_target(targets, i);
-    rt_query_slow<K>(T, t, locate_bucket(T, t), count, row, cp);
+    const uint32_t j0 = dir[b].x & ~WIDE, j1 = dir[b + 1].x & ~WIDE, n = j1 - j0;
+    uint32_t w[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint32_t G = 0, mask = 0;
+    bool flag = n > 16;
+    for (uint32_t j = j0; j < j1; j++) {
+        if (!(status[j] & KAD_STATUS_GOOD)) continue;
+        if (j - j0 < 16) mask |= 1u << (j - j0);
+        const uint32_t k16 = (uint32_t)((key[j] << d) >> 48);
+        if (G < REC_MAXG) {
+            const uint32_t h = 3 + G;
+            w[h >> 1] |= k16 << (16 * (h & 1));
+            for (uint32_t a = 0; a < G; a++) {  // equal key16 among good nodes: not rankable here
+                const uint32_t ha = 3 + a;
+                flag |= ((w[ha >> 1] >> (16 * (ha & 1))) & 0xFFFFu) == k16;
+            }
+        }
+        G++;
+    }
+    flag |= G > REC_MAXG;
+    w[0] = (j0 & REC_FIRST_MASK) | (min(G, 15u) << 27) | ((flag ? 1u : 0u) << 31);
+    w[1] |= flag ? 0u : mask;
+    const uint4 lo = make_uint4(w[0], w[1], w[2], w[3]), hi = make_uint4(w[4], w[5], w[6], w[7]);
+    const uint32_t r = b + REC_PAD;
+#pragma unroll
+    for (uint32_t c = 0; c < 4; c++) {  // copy c: line (r - c) / 4, slot (r - c) % 4
+        if (r < c) continue;
+        uint4* dst = rec + 8ull * ((size_t)c * rec_lines + ((r - c) >> 2)) + 2u * ((r - c) & 3u);
+        dst[0] = lo;
+        dst[1] = hi;
+    }
 }
 
 template <int K>
@@ -890,28 +885,18 @@ __global__ __launch_bounds__(BLOCK) void rt_closest_dual_kernel(DevTable T4, Dev
                                                                 uint32_t count, uint32_t* __restrict__ out_idx,
                                                                 uint8_t* __restrict__ out_cnt) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
-    if (i >= q) return;
-    const Target t = load_target(targets, i);
-    const DevTable& T = af[i] ? T6 : T4;
-    uint32_t* row = out_idx + (size_t)i * count;
-    uint8_t* cp = out_cnt ? out_cnt + i : nullptr;
-    if (!rt_query_fast<K, (K > 16 ? 6 : 3)>(T, t, count, row, cp)) mark_deferred(row, cp);
-}
-
-template <int K>
-__global__ __launch_bounds__(BLOCK) void rt_closest_dual_deferred_kernel(DevTable T4, DevTable T6,
-                                                                         const uint8_t* __restrict__ targets,
-                                                                         const uint8_t* __restrict__ af, uint32_t q,
-                                                                         uint32_t count, uint32_t* __restrict__ out_idx,
-                                                                         uint8_t* __restrict__ out_cnt) {
-    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
-    if (i >= q) return;
-    uint32_t* row = out_idx + (size_t)i * count;
-    uint8_t* cp = out_cnt ? out_cnt + i : nullptr;
-    if (!is_deferred(row, cp)) return;
-    const Target t = load_target(targets, i);
-    const DevTable& T = af[i] ? T6 : T4;
-    rt_query_slow<K>(T, t, locate_bucket(T, t), count, row, cp);
+    bool ex = false, six = false;
+    Target t{};
+    if (i < q) {
+        t = load_target(targets, i);
+        six = af[i] != 0;
+        ex = !rt_query_fast<K, (K > 16 ? 6 : 3)>(six ? T6 : T4, t, count, out_idx + (size_t)i * count,
+                                                  out_cnt ? out_cnt + i : nullptr);
+    }
+    // exact path per family (each call is wave-uniform in its table)
+    __shared__ uint64_t xs[BLOCK / 64][192];
+    exact_tail(T4, t, ex && !six, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
+    exact_tail(T6, t, ex && six, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
 }
 
 __global__ __launch_bounds__(BLOCK) void find_bucket_kernel(DevTable T, const uint8_t* __restrict__ targets,
@@ -1113,13 +1098,6 @@ __global__ void scan_apply_kernel(const uint32_t* part, const uint32_t* sums, ui
 
 inline uint32_t grid_for(uint64_t n) { return (uint32_t)((n + BLOCK - 1) / BLOCK); }
 
-// KAD_RT_KERNEL=lane (default) | block | bl | abl1..3 selects the RoutingTable kernel variant (A/B
-// benching, tools/ab_bench.py); read per call so one process can time several.
-bool force_lane() {
-    const char* e = std::getenv("KAD_RT_KERNEL");
-    return !e || std::strcmp(e, "block") != 0;
-}
-
 // ---------------------------------------------------------------------------------------
 // Host side
 // ---------------------------------------------------------------------------------------
@@ -1219,14 +1197,20 @@ struct kad_table {
     uint8_t* status_mut = nullptr;
     uint2* dir_mut = nullptr;
     uint32_t* gpre_mut = nullptr;
-    uint4* bl_mut = nullptr;
+    uint4* rec_mut = nullptr;
+    uint32_t rec_depth = 0;
     int64_t* time_ns = nullptr;
     int64_t* reply_ns = nullptr;
     uint8_t* expired = nullptr;
     uint32_t* scan_cnt = nullptr;   // B+1
     uint32_t* scan_part = nullptr;  // B+1
     uint32_t* scan_sums = nullptr;  // tiles
+    // exact-path queues of the record kernel, one per stream that queried this table (so that
+    // concurrent const queries on distinct streams stay independent)
+    std::mutex xq_mu;
+    std::vector<std::pair<void*, uint32_t*>> xq;  // (stream, device buffer: 2 counters + list)
     ~kad_table() {
+        for (auto& e : xq) (void)hipFree(e.second);
         for (void* p : owned) (void)hipFree(p);
     }
 };
@@ -1249,7 +1233,9 @@ int rebuild_good_prefix(kad_table* t, hipStream_t s) {
     hipLaunchKernelGGL(scan_tiles_kernel, dim3(tiles), dim3(BLOCK), 0, s, t->scan_cnt, m, t->scan_part, t->scan_sums);
     hipLaunchKernelGGL(scan_sums_kernel, dim3(1), dim3(BLOCK), 0, s, t->scan_sums, tiles);
     hipLaunchKernelGGL(scan_apply_kernel, dim3(grid_for(m)), dim3(BLOCK), 0, s, t->scan_part, t->scan_sums, m, t->gpre_mut);
-    if (t->bl_mut) hipLaunchKernelGGL(bl_good_kernel, dim3(grid_for(B)), dim3(BLOCK), 0, s, t->d.status, t->bl_mut, B);
+    if (t->rec_mut)
+        hipLaunchKernelGGL(rec_build_kernel, dim3(grid_for(B)), dim3(BLOCK), 0, s, t->d.key, t->d.status, t->d.dir, B,
+                           t->rec_depth, t->rec_mut, t->d.rec_lines);
     HIP_TRY(hipGetLastError());
     return KAD_OK;
 }
@@ -1259,41 +1245,73 @@ int check_count(uint32_t count) {
     return KAD_OK;
 }
 
-template <int K>
-void launch_rt(const DevTable& d, const uint8_t* targets, uint32_t q, uint32_t count, uint32_t* out, uint8_t* cnt,
-               hipStream_t s) {
-    const char* ev = std::getenv("KAD_RT_KERNEL");
-    if (K == 8 && ev && std::strncmp(ev, "abl", 3) == 0) {
-        const int a = ev[3] - '0';
-        if (a == 1) hipLaunchKernelGGL((rt_ablate_kernel<8, 1>), dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
-        if (a == 2) hipLaunchKernelGGL((rt_ablate_kernel<8, 2>), dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
-        if (a == 3) hipLaunchKernelGGL((rt_ablate_kernel<8, 3>), dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
-        return;
+// KAD_RT_KERNEL=lane forces the lane-per-query kernel where the record kernel would run (A/B
+// timing, tools/ab_bench.py); read per call so one process can time both.
+constexpr uint32_t EXACT_CAP = 1u << 16;
+
+// The (table, stream) exact-path queue, created zeroed on first use.
+int exact_queue(const kad_table* tc, hipStream_t s, ExactQ& Q) {
+    kad_table* t = const_cast<kad_table*>(tc);
+    std::lock_guard<std::mutex> lk(t->xq_mu);
+    uint32_t* buf = nullptr;
+    for (auto& e : t->xq)
+        if (e.first == (void*)s) buf = e.second;
+    if (!buf) {
+        HIP_TRY(hipMalloc(&buf, 64 + 32ull * EXACT_CAP));
+        HIP_TRY(hipMemset(buf, 0, 8));
+        t->xq.emplace_back((void*)s, buf);
     }
-    if ((d.flags & TF_BL) && ev && std::strcmp(ev, "bl") == 0)
-        hipLaunchKernelGGL(rt_bl_kernel<K>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
-    else if (K <= 16 && !force_lane())
-        hipLaunchKernelGGL(rt_block_kernel<(K <= 16 ? K : 16)>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count,
-                           out, cnt);
-    else
+    Q.ctr = buf;
+    Q.list = buf + 16;  // 64-byte aligned entries
+    Q.cap = EXACT_CAP;
+    return KAD_OK;
+}
+
+template <int K>
+int launch_rt(const kad_table* t, const uint8_t* targets, uint32_t q, uint32_t count, uint32_t* out, uint8_t* cnt,
+              hipStream_t s) {
+    const DevTable& d = t->d;
+    const char* ev = std::getenv("KAD_RT_KERNEL");
+    if (K == 8 && (d.flags & TF_REC) && !(ev && std::strcmp(ev, "lane") == 0)) {
+        ExactQ Q;
+        int rc = exact_queue(t, s, Q);
+        if (rc) return rc;
+        if (ev && std::strcmp(ev, "rec_inline") == 0) Q.cap = 0;  // A/B: exact path inline, no list kernel
+        if (ev && std::strcmp(ev, "rec_abl1") == 0) {
+            hipLaunchKernelGGL((rt_rec_kernel<8, 1>), dim3(grid_for(q)), dim3(BLOCK), 0, s, d, Q, targets, q, count, out, cnt);
+            return KAD_OK;
+        }
+        if (ev && std::strcmp(ev, "rec_abl2") == 0) {
+            hipLaunchKernelGGL((rt_rec_kernel<8, 2>), dim3(grid_for(q)), dim3(BLOCK), 0, s, d, Q, targets, q, count, out, cnt);
+            return KAD_OK;
+        }
+        hipLaunchKernelGGL((rt_rec_kernel<8, 0>), dim3(grid_for(q)), dim3(BLOCK), 0, s, d, Q, targets, q, count, out, cnt);
+        if (Q.cap == 0) return KAD_OK;
+        if (std::getenv("KAD_EXACT_STAMPS"))
+            hipLaunchKernelGGL(rt_exact_list_kernel<true>, dim3(EXACT_LIST_BLOCKS), dim3(BLOCK), 0, s, d, Q, targets, count,
+                               out, cnt);
+        else
+            hipLaunchKernelGGL(rt_exact_list_kernel<false>, dim3(EXACT_LIST_BLOCKS), dim3(BLOCK), 0, s, d, Q, targets, count,
+                               out, cnt);
+    } else {
         hipLaunchKernelGGL(rt_closest_kernel<K>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
-    hipLaunchKernelGGL(rt_closest_deferred_kernel<K>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out,
-                       cnt);
+    }
+    return KAD_OK;
 }
 template <int K>
 void launch_rt_dual(const DevTable& d4, const DevTable& d6, const uint8_t* targets, const uint8_t* af, uint32_t q,
                     uint32_t count, uint32_t* out, uint8_t* cnt, hipStream_t s) {
     hipLaunchKernelGGL(rt_closest_dual_kernel<K>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d4, d6, targets, af, q, count,
                        out, cnt);
-    hipLaunchKernelGGL(rt_closest_dual_deferred_kernel<K>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d4, d6, targets, af, q,
-                       count, out, cnt);
 }
 
-int rt_dispatch(const DevTable& d, const uint8_t* targets, uint32_t q, uint32_t count, uint32_t* out, uint8_t* cnt,
+int rt_dispatch(const kad_table* t, const uint8_t* targets, uint32_t q, uint32_t count, uint32_t* out, uint8_t* cnt,
                 hipStream_t s) {
-    if (count <= 8) launch_rt<8>(d, targets, q, count, out, cnt, s);
-    else if (count <= 16) launch_rt<16>(d, targets, q, count, out, cnt, s);
-    else launch_rt<32>(d, targets, q, count, out, cnt, s);
+    int rc;
+    if (count <= 8) rc = launch_rt<8>(t, targets, q, count, out, cnt, s);
+    else if (count <= 16) rc = launch_rt<16>(t, targets, q, count, out, cnt, s);
+    else rc = launch_rt<32>(t, targets, q, count, out, cnt, s);
+    if (rc) return rc;
     HIP_TRY(hipGetLastError());
     return KAD_OK;
 }
@@ -1452,35 +1470,7 @@ int kad_table_create(kad_table** out, int device, uint32_t n_nodes, const uint8_
         bool direct = r.slots == n_buckets;
         for (uint32_t sl = 0; sl < r.slots && direct; sl++) direct = rdx[sl] == (sl | RDX_EXACT);
         if (direct) d.flags |= TF_DIRECT;
-        // bucket lines for direct-mapped tables of depth <= 32 (see rt_bl_kernel)
         const uint32_t depth = 64 - r.shift;
-        if (direct && depth >= 1 && depth <= 32 && n_nodes <= BL_OFF_MASK) {
-            std::vector<uint32_t> bl(16ull * n_buckets, 0u);
-            const uint64_t pre0 = r.base >> r.shift;
-            for (uint32_t b = 0; b < n_buckets; b++) {
-                uint32_t* L = &bl[16ull * b];
-                const uint32_t j0 = bucket_offset[b], j1 = bucket_offset[b + 1], nb = j1 - j0;
-                bool fits = nb <= BL_CAP;
-                for (uint32_t j = j0; j < j1 && fits; j++) fits = (id_hi(ids + 20ull * j) >> r.shift) == pre0 + b;
-                L[0] = j0 | ((fits ? nb : BL_OVF) << 27);
-                if (!fits) continue;
-                uint32_t gm = 0, xm = 0;
-                for (uint32_t s2 = 0; s2 < nb; s2++) {
-                    const uint64_t hi = id_hi(ids + 20ull * (j0 + s2));
-                    L[2 + s2] = (uint32_t)((hi << depth) >> 32);
-                    gm |= (uint32_t)(status[j0 + s2] & KAD_STATUS_GOOD) << s2;
-                }
-                for (uint32_t a = 0; a < nb; a++)
-                    for (uint32_t c = a + 1; c < nb; c++)
-                        if (L[2 + a] == L[2 + c]) xm |= (1u << a) | (1u << c);
-                L[1] = gm | (xm << 16);
-            }
-            uint4* dbl;
-            if ((rc = dev_upload(&dbl, bl.data(), 4ull * n_buckets, t->owned, t->bytes))) { delete t; return rc; }
-            d.bl = dbl;
-            t->bl_mut = dbl;
-            d.flags |= TF_BL;
-        }
         uint2* ddir; uint64_t* dfk; uint32_t *dft, *drdx, *dgp, *ddm = nullptr;
         if ((rc = dev_upload(&ddir, dir.data(), n_buckets + 1, t->owned, t->bytes)) ||
             (rc = dev_upload(&dgp, gpre.data(), n_buckets + 1, t->owned, t->bytes)) ||
@@ -1496,6 +1486,35 @@ int kad_table_create(kad_table** out, int device, uint32_t n_nodes, const uint8_
         }
         d.dir = ddir; t->dir_mut = ddir; d.gpre = dgp; t->gpre_mut = dgp; d.dmask = ddm; d.fkey = dfk; d.ftail = dft; d.rrdx = drdx;
         d.rbase = r.base; d.rshift = r.shift; d.rslots = r.slots; t->rbits = r.bits;
+        // bucket records (rt_rec_kernel): direct-mapped, uniform depth 1..48, every node inside its
+        // bucket's dyadic range, first node index below 2^27
+        if (direct && depth >= 1 && depth <= 48 && n_nodes <= REC_FIRST_MASK) {
+            bool inside = true;
+            const uint64_t pre0 = r.base >> r.shift;
+            for (uint32_t b = 0; b < n_buckets && inside; b++)
+                for (uint32_t j = bucket_offset[b]; j < bucket_offset[b + 1] && inside; j++)
+                    inside = (id_hi(ids + 20ull * j) >> r.shift) == pre0 + b;
+            if (inside) {
+                const uint32_t lines = (n_buckets + 1) / 4 + 2;  // per copy: covers records 0 .. B+1 (+ pad)
+                uint4* rp;
+                if ((rc = dev_upload(&rp, nullptr, 4ull * 8 * lines, t->owned, t->bytes))) {
+                    delete t;
+                    return rc;
+                }
+                if (hipMemset(rp, 0, 4ull * 128 * lines) != hipSuccess) {
+                    delete t;
+                    return set_err(KAD_ERR_HIP, "hipMemset failed");
+                }
+                hipLaunchKernelGGL(rec_build_kernel, dim3(grid_for(n_buckets)), dim3(BLOCK), 0, 0, d.key, d.status, d.dir,
+                                   n_buckets, depth, rp, lines);
+                if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+                    delete t;
+                    return set_err(KAD_ERR_HIP, "record build failed");
+                }
+                d.rec = rp; d.rec_lines = lines; t->rec_mut = rp; t->rec_depth = depth;
+                d.flags |= TF_REC;
+            }
+        }
     }
     // NodeCache radix
     if ((flags & KAD_TABLE_SORTED) && n_nodes) {
@@ -1589,7 +1608,7 @@ int kad_rt_closest_batch(const kad_table* t, const uint8_t* targets, uint32_t q,
     if (count == 0 && !out_cnt) return KAD_OK;
     if (((uintptr_t)targets & 3) || ((uintptr_t)out_idx & 3)) return set_err(KAD_ERR_INVALID, "device buffers must be 4-byte aligned");
     DeviceGuard g(t->device);
-    return rt_dispatch(t->d, targets, q, count, out_idx, out_cnt, (hipStream_t)stream);
+    return rt_dispatch(t, targets, q, count, out_idx, out_cnt, (hipStream_t)stream);
 }
 
 int kad_rt_closest_batch_dual(const kad_table* t4, const kad_table* t6, const uint8_t* targets, const uint8_t* af,
@@ -1668,6 +1687,13 @@ int kad_rt_closest_batch_host(const kad_table* t, const uint8_t* targets, uint32
 int kad_nc_closest_batch_host(const kad_table* t, const uint8_t* targets, uint32_t q, uint32_t count, uint32_t* out_idx,
                               uint8_t* out_cnt) {
     return host_query(t, targets, q, count, out_idx, out_cnt, true);
+}
+
+/* Diagnostics (not in kadgpu.h): copy the exact-list kernel's per-wave stamps (KAD_EXACT_STAMPS=1). */
+int kad_debug_exact_stamps(uint64_t* host, uint32_t n) {
+    if (!host) return set_err(KAD_ERR_INVALID, "NULL buffer");
+    HIP_TRY(hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), 8ull * std::min<uint32_t>(n, STAMP_WAVES * 12)));
+    return KAD_OK;
 }
 
 int kad_xor_cmp_batch(const uint8_t* targets, const uint8_t* a, const uint8_t* b, uint32_t n, int8_t* out, void* stream) {

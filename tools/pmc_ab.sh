@@ -1,5 +1,5 @@
 #!/bin/bash
-# PMC passes over tools/ab_bench.py for one variant: VARIANT=bl|lane|block  (output gpurun_out/pmc_<variant>)
+# PMC passes over tools/ab_bench.py for one variant: VARIANT=rec|lane  (output gpurun_out/pmc_<variant>)
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 V=${VARIANT:-lane}
 O=$R/gpurun_out/pmc_$V
