@@ -26,6 +26,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from opendht_amd import DeviceTable  # noqa: E402
+from opendht_amd._lib import KAD_INFO_WINDOW_LINES  # noqa: E402
 from opendht_amd.metrics import rt_algorithmic_bytes  # noqa: E402
 from opendht_amd.sharded import ShardSpec, build_shard  # noqa: E402
 
@@ -97,6 +98,8 @@ def main():
     out_idx = torch.empty((args.queries, args.count), dtype=torch.int32, device=dev)
     out_cnt = torch.empty((args.queries,), dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev)
+    wl = args.count <= 8 and bool(T.info()["flags"] & KAD_INFO_WINDOW_LINES)
+    kernel = "rt_wl_kernel<0>" if wl else f"rt_closest_kernel<{8 if args.count <= 8 else 16 if args.count <= 16 else 32}>"
 
     # algorithmic bytes of one launch (exact, host side; target buckets from the engine's findBucket)
     tb = T.find_bucket(tg).cpu().numpy().view(np.uint32).astype(np.int64)
@@ -173,7 +176,7 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
-                "kernel": "rt_closest_kernel<8>",
+                "kernel": kernel,
                 "avg_kernel_ms": avg_kernel_s * 1e3,
                 "alg_bytes_per_launch": alg_bytes,
                 "alg_bytes_per_query": alg_bytes / args.queries,

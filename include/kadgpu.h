@@ -63,6 +63,9 @@ extern "C" {
 
 /* kad_table_create flags */
 #define KAD_TABLE_SORTED 0x01u      /* node array ascending by ID (enables NodeCache queries) */
+/* kad_table_info.flags, reported only */
+#define KAD_INFO_WINDOW_LINES 0x100u /* uniform-depth table: count <= 8 queries use one 128-byte
+                                        window line per query (rt_wl_kernel) */
 
 /* error codes */
 #define KAD_OK 0

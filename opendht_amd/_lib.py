@@ -19,6 +19,7 @@ KAD_NO_NODE = 0xFFFFFFFF
 KAD_STATUS_GOOD = 0x01
 KAD_STATUS_EXPIRED = 0x02
 KAD_TABLE_SORTED = 0x01
+KAD_INFO_WINDOW_LINES = 0x100
 
 ERRORS = {
     -1: "KAD_ERR_INVALID",

@@ -90,8 +90,7 @@ struct DevTable {
     const uint32_t* ftail;
     const uint32_t* rrdx;
     const uint32_t* nrdx;
-    const uint4* rec;    // bucket records (TF_REC): 4 copies x rec_lines 128-byte lines, see rt_rec_kernel
-    uint32_t rec_lines;  // lines per copy
+    const uint4* wl;  // window lines (TF_WL): 128 bytes per bucket, see rt_wl_kernel
     uint64_t rbase, nbase;
     uint32_t rshift, rslots, nshift, nslots;
     uint32_t n, B, index_base, flags;
@@ -99,7 +98,7 @@ struct DevTable {
 
 constexpr uint32_t TF_DIRECT = 1u;   // radix slot s holds exactly bucket s (no locate load)
 constexpr uint32_t TF_HAS_DUP = 2u;  // some nodes share their top 64 ID bits
-constexpr uint32_t TF_REC = 8u;      // bucket-record layout present (direct-mapped, depth <= 48)
+constexpr uint32_t TF_WL = 8u;       // window lines present (direct-mapped, uniform depth 1..43)
 constexpr uint32_t WIDE = 0x80000000u;  // dir[].x flag: bucket holds > 32 nodes (masks invalid)
 constexpr uint32_t KEY_PAD = 32;        // key[] is padded so 16-node chunk loads never leave it
 
@@ -422,19 +421,9 @@ __device__ __forceinline__ bool lt3(uint64_t a0, uint64_t a1, uint64_t a2, uint6
     return a0 < b0 || (a0 == b0 && (a1 < b1 || (a1 == b1 && a2 < b2)));
 }
 
-// stamp point (diagnostics): lane 0 records s_memrealtime after waiting for its memory ops
-#define XSTAMP(k)                                                               \
-    do {                                                                        \
-        if (sp && lane == 0) {                                                  \
-            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");         \
-            sp[k] = __builtin_amdgcn_s_memrealtime();                           \
-        }                                                                       \
-    } while (0)
-
 __device__ void wave_exact(const DevTable& T, const Target& t, uint32_t count, uint32_t* row, uint8_t* cp,
-                           uint64_t* xs /* this wave's 64 x 3 LDS words */, uint64_t* sp = nullptr) {
+                           uint64_t* xs /* this wave's 64 x 3 LDS words */) {
     const uint32_t lane = threadIdx.x & 63u, B = T.B;
-    XSTAMP(0);
     if (B == 0 || count == 0) {
         if (lane < count) row[lane] = NONE;
         if (lane == 0 && cp) *cp = 0;
@@ -457,9 +446,7 @@ __device__ void wave_exact(const DevTable& T, const Target& t, uint32_t count, u
             break;
         }
     }
-    XSTAMP(1);
     const uint32_t m = min(count, good);
-    XSTAMP(2);
     if (end - beg <= 64) {  // one tile (nearly every case): rank by broadcast LDS reads
         const uint32_t j = beg + lane;
         uint64_t V0 = ~0ull, V1 = ~0ull, V2 = ~0ull;
@@ -481,7 +468,6 @@ __device__ void wave_exact(const DevTable& T, const Target& t, uint32_t count, u
         xs[3 * lane + 2] = V2;
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_wave_barrier();
-        XSTAMP(3);
         // rank on the top 64 distance bits (unique unless two nodes share them); ties -> full order
         uint32_t lt = 0, le = 0;
 #pragma unroll 16
@@ -498,7 +484,6 @@ __device__ void wave_exact(const DevTable& T, const Target& t, uint32_t count, u
                 rank += lt3(xs[3 * sl], xs[3 * sl + 1], xs[3 * sl + 2], V0, V1, V2);
             }
         }
-        XSTAMP(4);
         __builtin_amdgcn_wave_barrier();  // xs is reused by the wave's next query
         if (v && rank < count) row[rank] = j + T.index_base;
         if (lane >= m && lane < count) row[lane] = NONE;
@@ -569,88 +554,6 @@ __device__ __forceinline__ void exact_tail(const DevTable& T, const Target& t, b
     }
 }
 
-// Exact-path queue of the record kernel: the kernel appends the queries its fast path cannot rank
-// (wave-aggregated atomic add), and rt_exact_list_kernel, launched right after on the same stream,
-// answers each with one wave (wave_exact) and resets the counter. Inline wave_exact cost the
-// record kernel ~18 us per 1M queries (0.3% of lanes stall 19% of the waves); the queue turns it
-// into one short launch. Scratch is per (table, stream): see kad_table::exact_scratch.
-struct ExactQ {
-    uint32_t* ctr;   // [0] entries appended, [1] blocks of the list kernel done
-    uint32_t* list;  // 32-byte entries: query index, target (hi64, t2, t3, t4)
-    uint32_t cap;
-};
-
-__device__ __forceinline__ void exact_enqueue(const ExactQ& Q, const DevTable& T, const Target& t, bool ex, uint32_t i,
-                                              uint32_t count, uint32_t* out_idx, uint8_t* out_cnt, uint64_t* xs) {
-    const uint64_t m = __ballot(ex);
-    if (!m) return;
-    if (Q.cap == 0) {  // no queue: answer inline
-        exact_tail(T, t, ex, i, count, out_idx, out_cnt, xs);
-        return;
-    }
-    const uint32_t lane = threadIdx.x & 63u, first = (uint32_t)__builtin_ctzll(m);
-    uint32_t base = 0;
-    if (lane == first) base = atomicAdd(Q.ctr, (uint32_t)__builtin_popcountll(m));
-    base = rdl(base, first);
-    const uint32_t pos = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-    const bool over = ex && pos >= Q.cap;
-    if (ex && !over) {  // entry = query index + its target (the list kernel needs no second load)
-        uint4* e = reinterpret_cast<uint4*>(Q.list) + 2ull * pos;
-        e[0] = make_uint4(i, (uint32_t)t.hi, (uint32_t)(t.hi >> 32), t.t2);
-        e[1] = make_uint4(t.t3, t.t4, 0u, 0u);
-    }
-    exact_tail(T, t, over, i, count, out_idx, out_cnt, xs);  // queue full: answer inline
-}
-
-// Diagnostics (KAD_EXACT_STAMPS=1, tools/exact_stamps.py): per wave s_memrealtime at entry, after the
-// counter read, after its first item and at exit (100 MHz ticks), for waves < STAMP_WAVES.
-constexpr uint32_t STAMP_WAVES = 4096;
-__device__ uint64_t g_stamps[STAMP_WAVES * 12];
-
-template <bool ST>
-__global__ __launch_bounds__(BLOCK) void rt_exact_list_kernel(DevTable T, ExactQ Q, const uint8_t* __restrict__ targets,
-                                                              uint32_t count, uint32_t* __restrict__ out_idx,
-                                                              uint8_t* __restrict__ out_cnt) {
-    const uint32_t w = (blockIdx.x * BLOCK + threadIdx.x) >> 6, nw = gridDim.x * (BLOCK / 64);
-    const bool st = ST && w < STAMP_WAVES && (threadIdx.x & 63) == 0;
-    if (st) g_stamps[4 * w] = __builtin_amdgcn_s_memrealtime();
-    const uint32_t n = min(__hip_atomic_load(Q.ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), Q.cap);
-    if (st) g_stamps[4 * w + 1] = __builtin_amdgcn_s_memrealtime() | ((uint64_t)(w < n) << 63);
-    __shared__ uint64_t xs[BLOCK / 64][192];
-    uint4 e0 = make_uint4(0, 0, 0, 0), e1 = e0;
-    if (w < Q.cap) {  // the wave's first entry, loaded together with the counter
-        const uint4* e = reinterpret_cast<const uint4*>(Q.list) + 2ull * w;
-        e0 = e[0];
-        e1 = e[1];
-    }
-    for (uint32_t k = w; k < n; k += nw) {
-        if (k != w) {
-            const uint4* e = reinterpret_cast<const uint4*>(Q.list) + 2ull * k;
-            e0 = e[0];
-            e1 = e[1];
-        }
-        Target t;
-        t.hi = ((uint64_t)e0.z << 32) | e0.y;
-        t.t2 = e0.w;
-        t.t3 = e1.x;
-        t.t4 = e1.y;
-        const uint32_t i = e0.x;
-        wave_exact(T, t, count, out_idx + (size_t)i * count, out_cnt ? out_cnt + i : nullptr, xs[threadIdx.x >> 6],
-                   (ST && k == w && w < STAMP_WAVES) ? g_stamps + STAMP_WAVES * 4 + 8 * w : nullptr);
-        if (st && k == w) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            g_stamps[4 * w + 2] = __builtin_amdgcn_s_memrealtime();
-        }
-    }
-    if (st) g_stamps[4 * w + 3] = __builtin_amdgcn_s_memrealtime();
-    __syncthreads();
-    if (threadIdx.x == 0 && atomicAdd(Q.ctr + 1, 1u) == gridDim.x - 1) {  // every block has read ctr[0]
-        atomicExch(Q.ctr, 0u);
-        atomicExch(Q.ctr + 1, 0u);
-    }
-}
-constexpr uint32_t EXACT_LIST_BLOCKS = 1024;  // 4096 waves: one wave_exact latency for <= 4096 entries
-
 // Lane-per-query RoutingTable kernel (any table shape, count <= 32).
 template <int K>
 __global__ __launch_bounds__(BLOCK) void rt_closest_kernel(DevTable T, const uint8_t* __restrict__ targets,
@@ -669,48 +572,41 @@ __global__ __launch_bounds__(BLOCK) void rt_closest_kernel(DevTable T, const uin
 }
 
 // ---------------------------------------------------------------------------------------
-// Bucket-record RoutingTable kernel (count <= 8; direct-mapped tables of uniform depth d <= 48,
-// the U(d) shape of the bench shards). The default kernel where the table supports it.
+// Window-line RoutingTable kernel (count <= 8; direct-mapped tables of uniform depth d,
+// 1 <= d <= 43: the U(d) shape of the bench shards). The default kernel where the table has lines.
 //
 // A random gather on MI355X costs one 128-byte line whether 32 or 128 bytes of it are used, and
 // wherever the table sits (tools/mb_line.py: ~34 G lines/s with the target read and row write,
-// the same for 128 MB and 1 GB tables), so a query should touch exactly ONE line. Each bucket is
-// a 32-byte record:
-//   dword 0    first node index (27 bits) | good count G (4 bits) << 27 | defer flag << 31
-//   halfword 2 good bitmask of the bucket's nodes (slot s = node first + s; at most 16 nodes)
-//   halfwords 3..15  key16 of the bucket's good nodes in slot order (at most 13): ID bits [d, d+16)
-// The defer flag marks a record the kernel cannot rank exactly (more than 16 nodes, more than 13
-// good nodes, or two good nodes with equal key16); a query whose window holds one takes the
-// wave-cooperative exact path (wave_exact).
+// the same for 128 MB and 1 GB tables), so a query should touch exactly ONE line. Line b holds
+// everything a query whose target lies in bucket b needs, for any count <= 8:
 //
-// Layout: record r = bucket + 2 (two empty records precede bucket 0, empty records pad the end).
-// The records are stored in FOUR copies, copy c cut into aligned 128-byte lines that start at
-// records r = c (mod 4): line k of copy c holds records 4k+c .. 4k+c+3. Bucket b's rounds 0 and 1,
-// buckets b-2 .. b+1 = records b .. b+3, are then line b/4 of copy b%4: one aligned line, always.
-// (4 x 32 B per bucket: 268 MB for a 2^21-bucket shard; table size does not change the gather
-// rate.) Windows needing round 2 (~0.14% at k = 8 on an 80%-good uniform shard) take wave_exact.
+// * For count c <= 8 the window W(R_c) depends on b alone, and W(R_c) is inside W(R_8);
+//   R_8 <= 2 unless the six buckets b-3 .. b+2 hold fewer than 8 good nodes.
+// * Buckets of equal depth are dyadic: the XOR images of two of them are disjoint intervals
+//   ordered by D(x) = prefix(x) XOR prefix(b) (the target has b's prefix), so the reference's
+//   result is W(R_c)'s buckets in D order, each bucket's good nodes by XOR distance to the target.
+// * Inside one bucket that order is the order of ID bits [d, d+21) XOR the target's bits [d, d+21),
+//   unless two good nodes of the bucket share those 21 bits (the line is then marked defer).
 //
-// Ranking. Buckets of equal depth are dyadic: the XOR images of two of them are disjoint
-// intervals ordered by D = prefix(bucket) XOR prefix(b), and inside one bucket the order is that
-// of key16 XOR the target's bits [d, d+16) (exact: two good nodes of a record never share key16).
-// So a node's rank value is the 32-bit word (ord(D) << 23 | record << 20 | key16^t16 << 4 | g),
-// g = its index among the record's good nodes. Each record's up-to-13 values go through a
-// 45-comparator min/max network that leaves its 8 smallest sorted; the per-record lists are merged
-// by bitonic 8+8 merges (min/max only: 2 VALU ops per compare-exchange). The output slot of
-// value (record, g) is the g-th set bit of the record's good mask.
+// Line b, 32 dwords:
+//   dw0      node index of the first node of W(R_8)'s lowest bucket (`base`)
+//   dw1      G(r) for r = 0..2, the good nodes of W(r) (6 bits each, capped at 63) | whole(r) << (18+r)
+//            | R_8 << 21 | S << 23 | defer << 31.  whole(r): W(r) is the whole table
+//   dw2      round of the bucket of D rank j, 2 bits each (j < 6)
+//   dw4..27  slot s (s < S <= 24): jd << 29 | key21 << 8 | off. The good nodes of W(R_8) in
+//            (D rank jd, node index) order, whole buckets only; off = node index - base (< 256)
+//   others   0xFFFFFFFF
+// A query's rank value of slot s is slot XOR (t21 << 8): (D rank, in-bucket distance, offset),
+// distinct within a line. The 8 smallest values (three sorted groups of 8, two bitonic merges,
+// min/max only) are the answer, provided the stored slots hold the first m = min(c, G(R_c)) of
+// W(R_c)'s nodes; otherwise, and for marked lines or targets outside b's range (clamped to the
+// first/last bucket), the query takes the wave-cooperative exact path (wave_exact).
 // Reference semantics: routing_table.cpp:67-111 (window rounds, sorted insertion, truncation).
 // ---------------------------------------------------------------------------------------
-constexpr uint32_t REC_FIRST_MASK = (1u << 27) - 1;
-constexpr uint32_t REC_MAXG = 13;
-constexpr uint32_t REC_PAD = 2;
-constexpr uint32_t REC_NONE = 0xFFFFFFFFu;
-
-__device__ __forceinline__ uint32_t rec_half(const uint4& lo, const uint4& hi, int h) {
-    const int w = h >> 1;  // static after unrolling
-    const uint32_t d = w == 0 ? lo.x : w == 1 ? lo.y : w == 2 ? lo.z : w == 3 ? lo.w
-                     : w == 4 ? hi.x : w == 5 ? hi.y : w == 6 ? hi.z : hi.w;
-    return (h & 1) ? d >> 16 : d & 0xFFFFu;
-}
+constexpr uint32_t WL_SLOTS = 24;
+constexpr uint32_t WL_SLOT0 = 4;   // first slot dword
+constexpr uint32_t WL_KBITS = 21;  // in-bucket key bits
+constexpr uint32_t WL_DEFER = 0x80000000u;
 
 __device__ __forceinline__ void cx(uint32_t& a, uint32_t& b) {
     const uint32_t lo = min(a, b);
@@ -718,17 +614,20 @@ __device__ __forceinline__ void cx(uint32_t& a, uint32_t& b) {
     a = lo;
 }
 
-// Batcher's 16-input odd-even merge sort restricted to 13 inputs and pruned to the 8 smallest
-// outputs (tools/netgen.py; checked exhaustively by the 0-1 principle in tests/test_networks.py).
-constexpr int NET13_TOP8_LEN = 45;
-__device__ constexpr uint8_t NET13_TOP8[NET13_TOP8_LEN][2] = {
-    {0, 1}, {2, 3}, {4, 5}, {6, 7}, {8, 9}, {10, 11}, {0, 2}, {1, 3}, {4, 6}, {5, 7}, {8, 10}, {9, 11},
-    {1, 2}, {5, 6}, {9, 10}, {0, 4}, {1, 5}, {2, 6}, {3, 7}, {8, 12}, {2, 4}, {3, 5}, {10, 12}, {1, 2},
-    {3, 4}, {5, 6}, {9, 10}, {11, 12}, {0, 8}, {1, 9}, {2, 10}, {3, 11}, {4, 12}, {4, 8}, {5, 9}, {6, 10},
-    {7, 11}, {2, 4}, {3, 5}, {6, 8}, {7, 9}, {1, 2}, {3, 4}, {5, 6}, {7, 8}};
+// Batcher's odd-even merge sort for 8 inputs (19 comparators; checked by the 0-1 principle in
+// tests/test_networks.py, which parses this table).
+constexpr int SORT8_LEN = 19;
+__device__ constexpr uint8_t SORT8[SORT8_LEN][2] = {
+    {0, 1}, {2, 3}, {4, 5}, {6, 7}, {0, 2}, {1, 3}, {4, 6}, {5, 7}, {1, 2}, {5, 6},
+    {0, 4}, {1, 5}, {2, 6}, {3, 7}, {2, 4}, {3, 5}, {1, 2}, {3, 4}, {5, 6}};
+
+__device__ __forceinline__ void sort8(uint32_t* v) {
+#pragma unroll
+    for (int c = 0; c < SORT8_LEN; c++) cx(v[SORT8[c][0]], v[SORT8[c][1]]);
+}
 
 // a = the 8 smallest of (a, s), sorted; a and s sorted ascending on entry.
-__device__ __forceinline__ void merge8(uint32_t (&a)[8], const uint32_t (&s)[8]) {
+__device__ __forceinline__ void merge8(uint32_t* a, const uint32_t* s) {
 #pragma unroll
     for (int i = 0; i < 8; i++) a[i] = min(a[i], s[7 - i]);  // bitonic
 #pragma unroll
@@ -740,92 +639,67 @@ __device__ __forceinline__ void merge8(uint32_t (&a)[8], const uint32_t (&s)[8])
     for (int i = 0; i < 8; i += 2) cx(a[i], a[i + 1]);
 }
 
-// The 8 smallest rank values of one record (NONE-padded), sorted.
-__device__ __forceinline__ void rec_rank(const uint4& lo, const uint4& hi, bool inw, uint32_t tag, uint32_t t16,
-                                         uint32_t (&s)[8]) {
-    const uint32_t G = inw ? (lo.x >> 27) & 15u : 0u;
-    uint32_t v[REC_MAXG];
-#pragma unroll
-    for (int e = 0; e < (int)REC_MAXG; e++)
-        v[e] = (uint32_t)e < G ? (tag | ((rec_half(lo, hi, 3 + e) ^ t16) << 4) | (uint32_t)e) : REC_NONE;
-#pragma unroll
-    for (int c = 0; c < NET13_TOP8_LEN; c++) cx(v[NET13_TOP8[c][0]], v[NET13_TOP8[c][1]]);
-#pragma unroll
-    for (int j = 0; j < 8; j++) s[j] = v[j];
+__device__ __forceinline__ uint32_t dw(const uint4 (&L)[8], int k) {  // static k after unrolling
+    const uint4& q = L[k >> 2];
+    return (k & 3) == 0 ? q.x : (k & 3) == 1 ? q.y : (k & 3) == 2 ? q.z : q.w;
 }
 
-// Index of the g-th set bit of a 16-bit mask (g < popcount(mask)).
-__device__ __forceinline__ uint32_t select_bit16(uint32_t m, uint32_t g) {
-    uint32_t s = 0, c;
-    c = __builtin_popcount(m & 0xFFu);
-    if (g >= c) { g -= c; m >>= 8; s = 8; }
-    c = __builtin_popcount(m & 0xFu);
-    if (g >= c) { g -= c; m >>= 4; s += 4; }
-    c = __builtin_popcount(m & 0x3u);
-    if (g >= c) { g -= c; m >>= 2; s += 2; }
-    return s + (g >= (m & 1u) ? 1u : 0u);
-}
-
-// ABL (timing ablations only, KAD_RT_KERNEL=rec_abl1|rec_abl2, results wrong): 1 = no exact
-// path, 2 = also no ranking networks.
-template <int K, int ABL>
-__global__ __launch_bounds__(BLOCK) void rt_rec_kernel(DevTable T, ExactQ Q, const uint8_t* __restrict__ targets,
-                                                       uint32_t q, uint32_t count, uint32_t* __restrict__ out_idx,
-                                                       uint8_t* __restrict__ out_cnt) {
-    static_assert(K == 8, "record kernel: count <= 8");
+// ABL (timing ablations only, KAD_RT_KERNEL=wl_abl1|wl_abl2; results wrong): 1 = no exact path,
+// 2 = also no ranking.
+template <int ABL>
+__global__ __launch_bounds__(BLOCK) void rt_wl_kernel(DevTable T, const uint8_t* __restrict__ targets, uint32_t q,
+                                                      uint32_t count, uint32_t* __restrict__ out_idx,
+                                                      uint8_t* __restrict__ out_cnt) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     bool ex = false;
     Target t{};
     if (i < q && count == 0) {
         if (out_cnt) out_cnt[i] = 0;
     } else if (i < q) {
-        uint32_t* row = out_idx + (size_t)i * count;
         t = load_target(targets, i);
-        const uint32_t B = T.B, d = 64 - T.rshift;
+        const uint32_t d = 64 - T.rshift;
         const uint32_t b = locate_bucket(T, t);
-        const uint32_t t16 = (uint32_t)((t.hi << d) >> 48);
-        const uint4* L = T.rec + 8ull * ((size_t)(b & 3u) * T.rec_lines + (b >> 2));  // records b-2 .. b+1
-        uint4 v[8];
+        const uint4* lp = T.wl + 8ull * b;
+        uint4 L[8];
 #pragma unroll
-        for (int x = 0; x < 8; x++) v[x] = L[x];
-        const uint32_t G0 = (v[0].x >> 27) & 15u, G1 = (v[2].x >> 27) & 15u, G2 = (v[4].x >> 27) & 15u,
-                       G3 = (v[6].x >> 27) & 15u;
-        const uint32_t good0 = G1 + G2;  // {b-1, b}
-        const bool r0 = good0 >= count || ((b <= 1) & (b + 1 >= B));
-        const uint32_t good1 = good0 + G0 + G3;  // + {b-2, b+1}
-        const bool r1 = !r0 && (good1 >= count || ((b <= 2) & (b + 2 >= B)));
-        ex = !(r0 | r1) | (v[2].x >> 31) | (v[4].x >> 31) | (r1 & ((v[0].x | v[6].x) >> 31));
-        if (!ex) {
-            // bucket order by D = prefix XOR the target's top d bits (b is first unless the target
-            // lies outside the table's range and was clamped to bucket 0 or B-1)
-            const uint64_t pb = (T.rbase >> T.rshift) + b, tp = t.hi >> T.rshift;
-            const uint64_t dm2 = (pb - 2) ^ tp, dm1 = (pb - 1) ^ tp, d00 = pb ^ tp, dp1 = (pb + 1) ^ tp;
-            const uint32_t om2 = (dm1 < dm2) + (d00 < dm2) + (dp1 < dm2), om1 = (dm2 < dm1) + (d00 < dm1) + (dp1 < dm1),
-                           o00 = (dm2 < d00) + (dm1 < d00) + (dp1 < d00), op1 = (dm2 < dp1) + (dm1 < dp1) + (d00 < dp1);
-            uint32_t acc[8], s[8];
-            if (ABL >= 2) {
+        for (int x = 0; x < 8; x++) L[x] = lp[x];
+        const uint32_t h = L[0].y, rounds = L[0].z;
+        // R_c = the least r <= R_8 with G(r) >= c or W(r) = the whole table
+        const uint32_t G0 = h & 63u, G1 = (h >> 6) & 63u, G2 = (h >> 12) & 63u, R8 = (h >> 21) & 3u, S = (h >> 23) & 31u;
+        const uint32_t Rc = (G0 >= count || (h >> 18) & 1u) ? 0u : (G1 >= count || (h >> 19) & 1u) ? 1u : 2u;
+        const uint32_t m = min(count, Rc == 0 ? G0 : Rc == 1 ? G1 : G2);
+        const bool own = (t.hi >> T.rshift) == (T.rbase >> T.rshift) + b;  // target inside bucket b's range
+        ex = (h & WL_DEFER) || !own || (Rc == R8 && S < m);
+        const uint32_t tx = (uint32_t)((t.hi << d) >> (64 - WL_KBITS)) << 8;
+        uint32_t v[WL_SLOTS];
 #pragma unroll
-                for (int j = 0; j < 8; j++) acc[j] = (v[j].z ^ om1 ^ t16) & 0x7FFFFFu;
-            } else {
-                rec_rank(v[2], v[3], true, (om1 << 23) | (1u << 20), t16, acc);  // b-1
-                rec_rank(v[4], v[5], true, (o00 << 23) | (2u << 20), t16, s);    // b
-                merge8(acc, s);
-                if (__any(r1)) {
-                    rec_rank(v[0], v[1], r1, (om2 << 23) | (0u << 20), t16, s);  // b-2
-                    merge8(acc, s);
-                    rec_rank(v[6], v[7], r1, (op1 << 23) | (3u << 20), t16, s);  // b+1
-                    merge8(acc, s);
-                }
+        for (int s = 0; s < (int)WL_SLOTS; s++) v[s] = dw(L, WL_SLOT0 + s) ^ tx;
+        if (__any(!ex && Rc < R8)) {  // count < 8 with a smaller window: drop the later rounds' buckets
+            uint32_t inc = 0;
+#pragma unroll
+            for (int j = 0; j < 6; j++) inc |= (((rounds >> (2 * j)) & 3u) <= Rc ? 1u : 0u) << j;
+            uint32_t have = 0;
+#pragma unroll
+            for (int s = 0; s < (int)WL_SLOTS; s++) {
+                const bool in = (uint32_t)s < S && ((inc >> (v[s] >> 29)) & 1u);
+                v[s] = in ? v[s] : NONE;
+                have += in;
             }
-            const uint32_t m = min(r0 ? good0 : good1, count);
+            ex |= have < m;
+        }
+        if (ABL < 2) {
+            sort8(v);
+            sort8(v + 8);
+            sort8(v + 16);
+            merge8(v, v + 8);
+            merge8(v, v + 16);
+        }
+        if (!ex) {
+            uint32_t* row = out_idx + (size_t)i * count;
+            const uint32_t base = L[0].x + T.index_base;
             uint32_t o[8];
 #pragma unroll
-            for (int j = 0; j < 8; j++) {
-                const uint32_t pv = acc[j], p = (pv >> 20) & 3u;
-                const uint32_t h = p == 0 ? v[0].x : p == 1 ? v[2].x : p == 2 ? v[4].x : v[6].x;
-                const uint32_t mk = (p == 0 ? v[0].y : p == 1 ? v[2].y : p == 2 ? v[4].y : v[6].y) & 0xFFFFu;
-                o[j] = (uint32_t)j < m ? (h & REC_FIRST_MASK) + select_bit16(mk, pv & 15u) + T.index_base : NONE;
-            }
+            for (int j = 0; j < 8; j++) o[j] = (uint32_t)j < m ? base + (v[j] & 255u) : NONE;
             if (count == 8) {
                 reinterpret_cast<uint4*>(row)[0] = make_uint4(o[0], o[1], o[2], o[3]);
                 reinterpret_cast<uint4*>(row)[1] = make_uint4(o[4], o[5], o[6], o[7]);
@@ -838,44 +712,54 @@ __global__ __launch_bounds__(BLOCK) void rt_rec_kernel(DevTable T, ExactQ Q, con
         }
     }
     __shared__ uint64_t xs[BLOCK / 64][192];
-    if (ABL == 0) exact_enqueue(Q, T, t, ex, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
+    if (ABL == 0) exact_tail(T, t, ex, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
 }
 
-// Bucket records after a status change (or at table creation): one thread per bucket.
-__global__ void rec_build_kernel(const uint64_t* key, const uint8_t* status, const uint2* dir, uint32_t B, uint32_t d,
-                                 uint4* rec, uint32_t rec_lines) {
+// Window lines after a status change (or at table creation): one thread per bucket (d = depth).
+__global__ void wl_build_kernel(const uint64_t* key, const uint8_t* status, const uint2* dir, const uint32_t* gpre,
+                                uint32_t B, uint32_t d, uint64_t pre0, uint32_t* lines) {
     const uint32_t b = blockIdx.x * BLOCK + threadIdx.x;
     if (b >= B) return;
-    const uint32_t j0 = dir[b].x & ~WIDE, j1 = dir[b + 1].x & ~WIDE, n = j1 - j0;
-    uint32_t w[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    uint32_t G = 0, mask = 0;
-    bool flag = n > 16;
-    for (uint32_t j = j0; j < j1; j++) {
-        if (!(status[j] & KAD_STATUS_GOOD)) continue;
-        if (j - j0 < 16) mask |= 1u << (j - j0);
-        const uint32_t k16 = (uint32_t)((key[j] << d) >> 48);
-        if (G < REC_MAXG) {
-            const uint32_t h = 3 + G;
-            w[h >> 1] |= k16 << (16 * (h & 1));
-            for (uint32_t a = 0; a < G; a++) {  // equal key16 among good nodes: not rankable here
-                const uint32_t ha = 3 + a;
-                flag |= ((w[ha >> 1] >> (16 * (ha & 1))) & 0xFFFFu) == k16;
-            }
+    uint32_t* L = lines + 32ull * b;
+    for (int k = 0; k < 32; k++) L[k] = NONE;
+    // R_8 and the per-round good counts (routing_table.cpp:89-104 closed form)
+    uint32_t h = 0, R8 = 3;
+    for (uint32_t r = 0; r < 3; r++) {
+        const uint32_t lo = b > r ? b - 1 - r : 0u, hi = min(B - 1, b + r);
+        const uint32_t g = gpre[hi + 1] - gpre[lo];
+        const bool whole = lo == 0 && hi == B - 1;
+        h |= (min(g, 63u) << (6 * r)) | ((whole ? 1u : 0u) << (18 + r));
+        if (R8 == 3 && (g >= 8 || whole)) R8 = r;
+    }
+    if (R8 == 3) { L[1] = WL_DEFER; return; }
+    const uint32_t lo = b > R8 ? b - 1 - R8 : 0u, hi = min(B - 1, b + R8), nb = hi - lo + 1;
+    const uint32_t base = dir[lo].x & ~WIDE;
+    uint32_t rounds = 0, S = 0;
+    bool defer = false, full = false;
+    for (uint32_t j = 0; j < nb; j++) {  // buckets in D order: the one whose D rank is j
+        uint32_t x = lo;
+        for (uint32_t y = lo; y <= hi; y++) {
+            uint32_t rk = 0;
+            for (uint32_t z = lo; z <= hi; z++) rk += ((pre0 + z) ^ (pre0 + b)) < ((pre0 + y) ^ (pre0 + b));
+            if (rk == j) x = y;
         }
-        G++;
+        rounds |= (x >= b ? x - b : b - 1 - x) << (2 * j);
+        const uint32_t j0 = dir[x].x & ~WIDE, j1 = dir[x + 1].x & ~WIDE;
+        const uint32_t g = gpre[x + 1] - gpre[x];
+        if (full || S + g > WL_SLOTS) { full = true; continue; }  // whole buckets only
+        const uint32_t s0 = S;
+        for (uint32_t n = j0; n < j1; n++) {
+            if (!(status[n] & KAD_STATUS_GOOD)) continue;
+            const uint32_t k21 = (uint32_t)((key[n] << d) >> (64 - WL_KBITS)), off = n - base;
+            defer |= off > 255u;
+            for (uint32_t s = s0; s < S; s++) defer |= ((L[WL_SLOT0 + s] >> 8) & ((1u << WL_KBITS) - 1)) == k21;
+            L[WL_SLOT0 + S] = (j << 29) | (k21 << 8) | (off & 255u);
+            S++;
+        }
     }
-    flag |= G > REC_MAXG;
-    w[0] = (j0 & REC_FIRST_MASK) | (min(G, 15u) << 27) | ((flag ? 1u : 0u) << 31);
-    w[1] |= flag ? 0u : mask;
-    const uint4 lo = make_uint4(w[0], w[1], w[2], w[3]), hi = make_uint4(w[4], w[5], w[6], w[7]);
-    const uint32_t r = b + REC_PAD;
-#pragma unroll
-    for (uint32_t c = 0; c < 4; c++) {  // copy c: line (r - c) / 4, slot (r - c) % 4
-        if (r < c) continue;
-        uint4* dst = rec + 8ull * ((size_t)c * rec_lines + ((r - c) >> 2)) + 2u * ((r - c) & 3u);
-        dst[0] = lo;
-        dst[1] = hi;
-    }
+    L[0] = base;
+    L[1] = h | (R8 << 21) | (S << 23) | (defer ? WL_DEFER : 0u);
+    L[2] = rounds;
 }
 
 template <int K>
@@ -1197,20 +1081,14 @@ struct kad_table {
     uint8_t* status_mut = nullptr;
     uint2* dir_mut = nullptr;
     uint32_t* gpre_mut = nullptr;
-    uint4* rec_mut = nullptr;
-    uint32_t rec_depth = 0;
+    uint32_t* wl_mut = nullptr;
     int64_t* time_ns = nullptr;
     int64_t* reply_ns = nullptr;
     uint8_t* expired = nullptr;
     uint32_t* scan_cnt = nullptr;   // B+1
     uint32_t* scan_part = nullptr;  // B+1
     uint32_t* scan_sums = nullptr;  // tiles
-    // exact-path queues of the record kernel, one per stream that queried this table (so that
-    // concurrent const queries on distinct streams stay independent)
-    std::mutex xq_mu;
-    std::vector<std::pair<void*, uint32_t*>> xq;  // (stream, device buffer: 2 counters + list)
     ~kad_table() {
-        for (auto& e : xq) (void)hipFree(e.second);
         for (void* p : owned) (void)hipFree(p);
     }
 };
@@ -1233,9 +1111,9 @@ int rebuild_good_prefix(kad_table* t, hipStream_t s) {
     hipLaunchKernelGGL(scan_tiles_kernel, dim3(tiles), dim3(BLOCK), 0, s, t->scan_cnt, m, t->scan_part, t->scan_sums);
     hipLaunchKernelGGL(scan_sums_kernel, dim3(1), dim3(BLOCK), 0, s, t->scan_sums, tiles);
     hipLaunchKernelGGL(scan_apply_kernel, dim3(grid_for(m)), dim3(BLOCK), 0, s, t->scan_part, t->scan_sums, m, t->gpre_mut);
-    if (t->rec_mut)
-        hipLaunchKernelGGL(rec_build_kernel, dim3(grid_for(B)), dim3(BLOCK), 0, s, t->d.key, t->d.status, t->d.dir, B,
-                           t->rec_depth, t->rec_mut, t->d.rec_lines);
+    if (t->wl_mut)
+        hipLaunchKernelGGL(wl_build_kernel, dim3(grid_for(B)), dim3(BLOCK), 0, s, t->d.key, t->d.status, t->d.dir,
+                           t->d.gpre, B, 64 - t->d.rshift, t->d.rbase >> t->d.rshift, t->wl_mut);
     HIP_TRY(hipGetLastError());
     return KAD_OK;
 }
@@ -1245,54 +1123,20 @@ int check_count(uint32_t count) {
     return KAD_OK;
 }
 
-// KAD_RT_KERNEL=lane forces the lane-per-query kernel where the record kernel would run (A/B
-// timing, tools/ab_bench.py); read per call so one process can time both.
-constexpr uint32_t EXACT_CAP = 1u << 16;
-
-// The (table, stream) exact-path queue, created zeroed on first use.
-int exact_queue(const kad_table* tc, hipStream_t s, ExactQ& Q) {
-    kad_table* t = const_cast<kad_table*>(tc);
-    std::lock_guard<std::mutex> lk(t->xq_mu);
-    uint32_t* buf = nullptr;
-    for (auto& e : t->xq)
-        if (e.first == (void*)s) buf = e.second;
-    if (!buf) {
-        HIP_TRY(hipMalloc(&buf, 64 + 32ull * EXACT_CAP));
-        HIP_TRY(hipMemset(buf, 0, 8));
-        t->xq.emplace_back((void*)s, buf);
-    }
-    Q.ctr = buf;
-    Q.list = buf + 16;  // 64-byte aligned entries
-    Q.cap = EXACT_CAP;
-    return KAD_OK;
-}
-
+// KAD_RT_KERNEL=lane forces the lane-per-query kernel where the window-line kernel would run
+// (A/B timing, tools/ab_bench.py); read per call so one process can time both.
 template <int K>
 int launch_rt(const kad_table* t, const uint8_t* targets, uint32_t q, uint32_t count, uint32_t* out, uint8_t* cnt,
               hipStream_t s) {
     const DevTable& d = t->d;
     const char* ev = std::getenv("KAD_RT_KERNEL");
-    if (K == 8 && (d.flags & TF_REC) && !(ev && std::strcmp(ev, "lane") == 0)) {
-        ExactQ Q;
-        int rc = exact_queue(t, s, Q);
-        if (rc) return rc;
-        if (ev && std::strcmp(ev, "rec_inline") == 0) Q.cap = 0;  // A/B: exact path inline, no list kernel
-        if (ev && std::strcmp(ev, "rec_abl1") == 0) {
-            hipLaunchKernelGGL((rt_rec_kernel<8, 1>), dim3(grid_for(q)), dim3(BLOCK), 0, s, d, Q, targets, q, count, out, cnt);
-            return KAD_OK;
-        }
-        if (ev && std::strcmp(ev, "rec_abl2") == 0) {
-            hipLaunchKernelGGL((rt_rec_kernel<8, 2>), dim3(grid_for(q)), dim3(BLOCK), 0, s, d, Q, targets, q, count, out, cnt);
-            return KAD_OK;
-        }
-        hipLaunchKernelGGL((rt_rec_kernel<8, 0>), dim3(grid_for(q)), dim3(BLOCK), 0, s, d, Q, targets, q, count, out, cnt);
-        if (Q.cap == 0) return KAD_OK;
-        if (std::getenv("KAD_EXACT_STAMPS"))
-            hipLaunchKernelGGL(rt_exact_list_kernel<true>, dim3(EXACT_LIST_BLOCKS), dim3(BLOCK), 0, s, d, Q, targets, count,
-                               out, cnt);
+    if (K == 8 && (d.flags & TF_WL) && !(ev && std::strcmp(ev, "lane") == 0)) {
+        if (ev && std::strcmp(ev, "wl_abl1") == 0)
+            hipLaunchKernelGGL(rt_wl_kernel<1>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
+        else if (ev && std::strcmp(ev, "wl_abl2") == 0)
+            hipLaunchKernelGGL(rt_wl_kernel<2>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
         else
-            hipLaunchKernelGGL(rt_exact_list_kernel<false>, dim3(EXACT_LIST_BLOCKS), dim3(BLOCK), 0, s, d, Q, targets, count,
-                               out, cnt);
+            hipLaunchKernelGGL(rt_wl_kernel<0>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
     } else {
         hipLaunchKernelGGL(rt_closest_kernel<K>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
     }
@@ -1486,33 +1330,29 @@ int kad_table_create(kad_table** out, int device, uint32_t n_nodes, const uint8_
         }
         d.dir = ddir; t->dir_mut = ddir; d.gpre = dgp; t->gpre_mut = dgp; d.dmask = ddm; d.fkey = dfk; d.ftail = dft; d.rrdx = drdx;
         d.rbase = r.base; d.rshift = r.shift; d.rslots = r.slots; t->rbits = r.bits;
-        // bucket records (rt_rec_kernel): direct-mapped, uniform depth 1..48, every node inside its
-        // bucket's dyadic range, first node index below 2^27
-        if (direct && depth >= 1 && depth <= 48 && n_nodes <= REC_FIRST_MASK) {
+        // window lines (rt_wl_kernel): direct-mapped, uniform depth 1..43, every node inside its
+        // bucket's dyadic range
+        if (direct && depth >= 1 && depth <= 43) {
             bool inside = true;
             const uint64_t pre0 = r.base >> r.shift;
             for (uint32_t b = 0; b < n_buckets && inside; b++)
                 for (uint32_t j = bucket_offset[b]; j < bucket_offset[b + 1] && inside; j++)
                     inside = (id_hi(ids + 20ull * j) >> r.shift) == pre0 + b;
             if (inside) {
-                const uint32_t lines = (n_buckets + 1) / 4 + 2;  // per copy: covers records 0 .. B+1 (+ pad)
-                uint4* rp;
-                if ((rc = dev_upload(&rp, nullptr, 4ull * 8 * lines, t->owned, t->bytes))) {
+                uint32_t* lp;
+                if ((rc = dev_upload(&lp, nullptr, 32ull * n_buckets, t->owned, t->bytes))) {
                     delete t;
                     return rc;
                 }
-                if (hipMemset(rp, 0, 4ull * 128 * lines) != hipSuccess) {
-                    delete t;
-                    return set_err(KAD_ERR_HIP, "hipMemset failed");
-                }
-                hipLaunchKernelGGL(rec_build_kernel, dim3(grid_for(n_buckets)), dim3(BLOCK), 0, 0, d.key, d.status, d.dir,
-                                   n_buckets, depth, rp, lines);
+                hipLaunchKernelGGL(wl_build_kernel, dim3(grid_for(n_buckets)), dim3(BLOCK), 0, 0, d.key, d.status, d.dir,
+                                   d.gpre, n_buckets, depth, pre0, lp);
                 if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
                     delete t;
-                    return set_err(KAD_ERR_HIP, "record build failed");
+                    return set_err(KAD_ERR_HIP, "window-line build failed");
                 }
-                d.rec = rp; d.rec_lines = lines; t->rec_mut = rp; t->rec_depth = depth;
-                d.flags |= TF_REC;
+                d.wl = reinterpret_cast<const uint4*>(lp);
+                t->wl_mut = lp;
+                d.flags |= TF_WL;
             }
         }
     }
@@ -1543,7 +1383,7 @@ int kad_table_get_info(const kad_table* t, kad_table_info* out) {
     out->n_nodes = t->d.n;
     out->n_buckets = t->d.B;
     out->index_base = t->d.index_base;
-    out->flags = t->flags;
+    out->flags = t->flags | ((t->d.flags & TF_WL) ? KAD_INFO_WINDOW_LINES : 0u);
     out->device = t->device;
     out->rt_radix_bits = t->rbits;
     out->nc_radix_bits = t->nbits;
@@ -1687,13 +1527,6 @@ int kad_rt_closest_batch_host(const kad_table* t, const uint8_t* targets, uint32
 int kad_nc_closest_batch_host(const kad_table* t, const uint8_t* targets, uint32_t q, uint32_t count, uint32_t* out_idx,
                               uint8_t* out_cnt) {
     return host_query(t, targets, q, count, out_idx, out_cnt, true);
-}
-
-/* Diagnostics (not in kadgpu.h): copy the exact-list kernel's per-wave stamps (KAD_EXACT_STAMPS=1). */
-int kad_debug_exact_stamps(uint64_t* host, uint32_t n) {
-    if (!host) return set_err(KAD_ERR_INVALID, "NULL buffer");
-    HIP_TRY(hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), 8ull * std::min<uint32_t>(n, STAMP_WAVES * 12)));
-    return KAD_OK;
 }
 
 int kad_xor_cmp_batch(const uint8_t* targets, const uint8_t* a, const uint8_t* b, uint32_t n, int8_t* out, void* stream) {

@@ -90,6 +90,27 @@ def test_golden_config1(gpu):
                     np.testing.assert_array_equal(cnt.cpu().numpy(), g[f"U_nc_cnt_k{k}"])
 
 
+def _wl_tables():
+    """U(d) tables for the window-line kernel (count <= 8): dense buckets (offsets > 255, buckets
+    with > 24 good nodes), low good fractions (R_c < R_8 for small counts, R_8 > 2), tiny tables
+    whose windows are the whole table."""
+    out = []
+    for n, depth, good, name in ((10_000, 8, 80, "dense_U8"), (20_000, 12, 40, "U12_g40"),
+                                 (20_000, 12, 60, "U12_g60"), (50_000, 14, 80, "U14_g80"),
+                                 (60_000, 13, 15, "U13_g15"), (200, 3, 70, "U3_tiny"), (5, 1, 80, "U1_five")):
+        t = TB.uniform_config(n, depth, seed=0x3100 + depth, good=good, expired=(100 - good) // 2)
+        t["name"] = name
+        out.append(t)
+    return out
+
+
+@pytest.mark.parametrize("t", _wl_tables(), ids=lambda t: t["name"])
+def test_window_lines(gpu, t):
+    """Every count the window-line kernel serves (1..8) on U(d) tables of every density."""
+    with make(t, gpu) as T:
+        check_rt(T, t, TB.adversarial_targets(t, extra=4096), gpu, counts=(1, 2, 3, 4, 5, 6, 7, 8))
+
+
 def test_host_entry_points(gpu):
     t = TB.split_config(10_000)
     targets = TB.adversarial_targets(t)

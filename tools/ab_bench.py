@@ -3,7 +3,7 @@ of the 100M-node table, 1M queries). Variants are selected per call through KAD_
 (rounds interleaved, median reported: cdna_hip_programming.md §5.4 rule 24). Results of every
 variant must be identical.
 
-    python tools/ab_bench.py [--variants rec,lane] [--rounds 5] [--reps 10] [--count 8]
+    python tools/ab_bench.py [--variants wl,lane] [--rounds 5] [--reps 10] [--count 8]
 """
 import argparse
 import json
@@ -22,7 +22,7 @@ from opendht_amd.sharded import ShardSpec, build_shard  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--variants", default="rec,lane")
+    ap.add_argument("--variants", default="wl,lane")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--count", type=int, default=8)

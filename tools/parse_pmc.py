@@ -8,7 +8,7 @@ import sys
 from collections import defaultdict
 
 d = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
-ksub = sys.argv[2] if len(sys.argv) > 2 else "rt_closest_kernel"
+ksub = sys.argv[2] if len(sys.argv) > 2 else "rt_wl_kernel"
 vals = defaultdict(lambda: defaultdict(list))
 for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
     for row in csv.DictReader(open(f)):

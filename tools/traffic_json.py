@@ -1,0 +1,26 @@
+"""HBM traffic per launch of the bench's dominant kernel from rocprofv3 PMC passes (tools/pmc.sh),
+corrected as /opt/skills/guides/MI355X_MICROARCH.md ("HBM [CDNA4]") prescribes: FETCH_SIZE and
+WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports half the bytes of 128-byte reads, so it is
+doubled (every read of the kernel is a whole 128-byte line or a 16-byte-per-lane streaming load).
+Writes: profiles/traffic_<tag>.json, read by bench.py for roofline.traffic.
+
+    python tools/traffic_json.py gpurun_out/pmc rt_wl_kernel r01
+"""
+import json
+import os
+import subprocess
+import sys
+
+d, ksub, tag = sys.argv[1], sys.argv[2], sys.argv[3]
+root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+pm = json.loads(subprocess.check_output([sys.executable, os.path.join(root, "tools", "parse_pmc.py"), d, ksub]))
+fetch = 2 * pm["FETCH_SIZE"] * 1024
+write = pm["WRITE_SIZE"] * 1024
+out = {"kernel": ksub, "hbm_bytes_per_launch": fetch + write, "read_bytes": fetch, "write_bytes": write,
+       "raw_kib": {"FETCH_SIZE": pm["FETCH_SIZE"], "WRITE_SIZE": pm["WRITE_SIZE"]},
+       "l2_hit_rate": pm["TCC_HIT_sum"] / (pm["TCC_HIT_sum"] + pm["TCC_MISS_sum"]) if "TCC_HIT_sum" in pm else None,
+       "correction": "FETCH_SIZE x2 (gfx950 128-B requests tallied at 64 B), KiB -> bytes",
+       "source": f"rocprofv3 --pmc passes over bench.py --steps 5 --warmup 2 --no-cpu ({d})"}
+p = os.path.join(root, "profiles", f"traffic_{tag}.json")
+json.dump(out, open(p, "w"), indent=1)
+print(json.dumps(out, indent=1))
