@@ -63,8 +63,8 @@ def cpu_baseline(sh, targets, count, budget_s, nthreads):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--count", type=int, default=8)
     ap.add_argument("--queries", type=int, default=1 << 20, help="queries per GPU per step")
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU baseline sampling")
