@@ -158,6 +158,47 @@ int kad_rt_closest_batch_dual(const kad_table* table4, const kad_table* table6,
                               const uint8_t* targets, const uint8_t* af, uint32_t q, uint32_t count,
                               uint32_t* out_idx, uint8_t* out_cnt, void* stream);
 
+/* ---- sharded table without halo: the north-star multi-GPU variant ----
+ * A global uniform-depth table U(depth) (bucket b's first ID = global_base + b << (160-depth)) is
+ * cut into contiguous bucket ranges, one table per GPU, with global node indices (index_base).
+ * Every rank holds the global good prefix sums, computes each query's global window W(R)
+ * (routing_table.cpp:89-104) and answers W(R) ∩ its shard for a replicated batch of targets:
+ *   W(R) inside the shard -> a final row appended to one of KAD_SHARD_REGIONS regions of `rows`
+ *                            (region r: row_cap rows at rows + r*row_cap*KAD_ROW_WORDS(count);
+ *                            a row is qid, m, 0, 0, idx[count] padded to 4 words)
+ *   W(R) crosses an edge  -> this shard's part appended to `parts` (KAD_PART_WORDS(count) each:
+ *                            the row, then the entries' 160-bit XOR distances, 5 words each)
+ *   W(R) misses the shard -> nothing (queries with a bucket outside [reach_lo, reach_hi) exit early;
+ *                            reach must cover every bucket whose window can touch the shard).
+ * counters (device, KAD_SHARD_COUNTERS x KAD_SHARD_COUNTER_STRIDE uint32, zeroed by the caller;
+ * counter k at word k*KAD_SHARD_COUNTER_STRIDE): rows appended per region (k < 8), parts appended
+ * (k = 8), overflow flag (k = 9: a region or the parts buffer was full: grow and run again).
+ * Rows of query block k (256 queries) go to region k % 8, so row_cap >= ceil(ceil(q/256)/8)*256
+ * never overflows.
+ * The ranks' rows and parts are all-gathered by the caller (RCCL); kad_rt_scatter_rows and
+ * kad_rt_merge_parts (parts sorted by qid) then give every query's findClosestNodes result.
+ * All pointers are device pointers; count in 1..KAD_MAX_COUNT. */
+#define KAD_ROW_WORDS(count) (4u + (((count) + 3u) & ~3u))
+#define KAD_PART_WORDS(count) (KAD_ROW_WORDS(count) + 5u * (count))
+#define KAD_SHARD_REGIONS 8u
+#define KAD_SHARD_COUNTERS 10u
+#define KAD_SHARD_COUNTER_STRIDE 32u
+int kad_rt_shard_batch(const kad_table* shard, const uint32_t* global_good_prefix, uint32_t global_buckets,
+                       uint64_t global_base_hi, uint32_t depth, uint32_t shard_first_bucket,
+                       uint32_t reach_lo, uint32_t reach_hi, const uint8_t* targets, uint32_t q,
+                       uint32_t count, uint32_t* rows, uint32_t row_cap, uint32_t* parts,
+                       uint32_t part_cap, uint32_t* counters, void* stream);
+/* n_blocks row blocks (block r: n_rows[r * n_rows_stride] rows at rows + r*block_cap*KAD_ROW_WORDS)
+ * -> out_idx[qid] / out_cnt[qid]. n_rows_stride 0 means 1 (gathered counts); pass
+ * KAD_SHARD_COUNTER_STRIDE to scatter a single rank's regions straight from its counters. */
+int kad_rt_scatter_rows(const uint32_t* rows, const uint32_t* n_rows, uint32_t n_rows_stride, uint32_t n_blocks,
+                        uint32_t block_cap, uint32_t count, uint32_t* out_idx, uint8_t* out_cnt, int device,
+                        void* stream);
+/* n_parts partial rows sorted by qid -> the first min(count, sum of m) entries by (XOR distance,
+ * global index) of each query (exact: parts come from disjoint buckets). */
+int kad_rt_merge_parts(const uint32_t* parts, uint32_t n_parts, uint32_t count, uint32_t* out_idx,
+                       uint8_t* out_cnt, int device, void* stream);
+
 /* ---- InfoHash primitives (infohash.h), batched, device pointers ---------- */
 /* out[i] = targets[i].xorCmp(a[i], b[i]) in {-1,0,1}   (infohash.h:131-146) */
 int kad_xor_cmp_batch(const uint8_t* targets, const uint8_t* a, const uint8_t* b, uint32_t n,

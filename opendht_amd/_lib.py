@@ -21,6 +21,16 @@ KAD_STATUS_EXPIRED = 0x02
 KAD_TABLE_SORTED = 0x01
 KAD_INFO_WINDOW_LINES = 0x100
 
+
+def row_words(count: int) -> int:
+    """KAD_ROW_WORDS: uint32 words of one complete row of kad_rt_shard_batch."""
+    return 4 + ((count + 3) & ~3)
+
+
+def part_words(count: int) -> int:
+    """KAD_PART_WORDS: a row plus the entries' 160-bit XOR distances (5 words each)."""
+    return row_words(count) + 5 * count
+
 ERRORS = {
     -1: "KAD_ERR_INVALID",
     -2: "KAD_ERR_HIP",
@@ -52,6 +62,12 @@ SIGNATURES = {
     "kad_nc_closest_batch": (C.c_int, [_P, _P, C.c_uint32, C.c_uint32, _P, _P, _P]),
     "kad_nc_closest_batch_host": (C.c_int, [_P, _P, C.c_uint32, C.c_uint32, _P, _P]),
     "kad_rt_closest_batch_dual": (C.c_int, [_P, _P, _P, _P, C.c_uint32, C.c_uint32, _P, _P, _P]),
+    "kad_rt_shard_batch": (C.c_int, [_P, _P, C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32,
+                                     C.c_uint32, _P, C.c_uint32, C.c_uint32, _P, C.c_uint32, _P, C.c_uint32,
+                                     _P, _P]),
+    "kad_rt_scatter_rows": (C.c_int, [_P, _P, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, _P, _P, C.c_int,
+                                      _P]),
+    "kad_rt_merge_parts": (C.c_int, [_P, C.c_uint32, C.c_uint32, _P, _P, C.c_int, _P]),
     "kad_xor_cmp_batch": (C.c_int, [_P, _P, _P, C.c_uint32, _P, _P]),
     "kad_common_bits_batch": (C.c_int, [_P, _P, C.c_uint32, _P, _P]),
     "kad_lowbit_batch": (C.c_int, [_P, C.c_uint32, _P, _P]),

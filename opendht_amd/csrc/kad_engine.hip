@@ -421,31 +421,13 @@ __device__ __forceinline__ bool lt3(uint64_t a0, uint64_t a1, uint64_t a2, uint6
     return a0 < b0 || (a0 == b0 && (a1 < b1 || (a1 == b1 && a2 < b2)));
 }
 
-__device__ void wave_exact(const DevTable& T, const Target& t, uint32_t count, uint32_t* row, uint8_t* cp,
-                           uint64_t* xs /* this wave's 64 x 3 LDS words */) {
-    const uint32_t lane = threadIdx.x & 63u, B = T.B;
-    if (B == 0 || count == 0) {
-        if (lane < count) row[lane] = NONE;
-        if (lane == 0 && cp) *cp = 0;
-        return;
-    }
-    const uint32_t b = locate_bucket(T, t);
-    uint32_t beg = 0, end = 0, good = 0;
-    for (uint32_t r0 = 0;; r0 += 64) {  // the window's good count and node range for rounds r0..r0+63
-        const uint32_t r = r0 + lane;
-        const uint32_t l_ = b > r ? b - 1 - r : 0u;
-        const uint32_t h_ = (uint64_t)b + r >= (uint64_t)B - 1 ? B - 1 : b + r;
-        const uint32_t g_ = T.gpre[h_ + 1] - T.gpre[l_];
-        const uint32_t b_ = T.dir[l_].x & ~WIDE, e_ = T.dir[h_ + 1].x & ~WIDE;
-        const uint64_t ok = __ballot(g_ >= count || (l_ == 0 && h_ == B - 1));
-        if (ok) {
-            const uint32_t R = (uint32_t)__builtin_ctzll(ok);
-            beg = rdl(b_, R);
-            end = rdl(e_, R);
-            good = rdl(g_, R);
-            break;
-        }
-    }
+// Ranks nodes [beg, end) of T (`good` of them good) for the wave-uniform target t: row[0..count) =
+// the first min(count, good) good nodes by (160-bit XOR distance, index), + index_base, padded with
+// NONE. If `dist` is given, dist[5*r .. 5*r+4] = the XOR distance of row entry r as five native
+// words (most significant first): the merge key of kad_rt_merge_parts.
+__device__ void wave_rank(const DevTable& T, const Target& t, uint32_t beg, uint32_t end, uint32_t good,
+                          uint32_t count, uint32_t* row, uint32_t* dist, uint64_t* xs) {
+    const uint32_t lane = threadIdx.x & 63u;
     const uint32_t m = min(count, good);
     if (end - beg <= 64) {  // one tile (nearly every case): rank by broadcast LDS reads
         const uint32_t j = beg + lane;
@@ -485,9 +467,16 @@ __device__ void wave_exact(const DevTable& T, const Target& t, uint32_t count, u
             }
         }
         __builtin_amdgcn_wave_barrier();  // xs is reused by the wave's next query
-        if (v && rank < count) row[rank] = j + T.index_base;
+        if (v && rank < count) {
+            row[rank] = j + T.index_base;
+            if (dist) {
+                uint32_t* dd = dist + 5 * rank;
+                dd[0] = (uint32_t)(V0 >> 32); dd[1] = (uint32_t)V0;
+                dd[2] = (uint32_t)(V1 >> 32); dd[3] = (uint32_t)V1;
+                dd[4] = (uint32_t)(V2 >> 32);
+            }
+        }
         if (lane >= m && lane < count) row[lane] = NONE;
-        if (lane == 0 && cp) *cp = (uint8_t)m;
         return;
     }
     uint64_t L0 = ~0ull, L1 = ~0ull, L2 = ~0ull;  // list entry of this lane (lanes < nl)
@@ -535,7 +524,48 @@ __device__ void wave_exact(const DevTable& T, const Target& t, uint32_t count, u
         nl = nn;
     }
     if (lane < count) row[lane] = lane < m ? (uint32_t)L2 + T.index_base : NONE;
-    if (lane == 0 && cp) *cp = (uint8_t)m;
+    if (dist && lane < m) {
+        uint32_t* dd = dist + 5 * lane;
+        dd[0] = (uint32_t)(L0 >> 32); dd[1] = (uint32_t)L0;
+        dd[2] = (uint32_t)(L1 >> 32); dd[3] = (uint32_t)L1;
+        dd[4] = (uint32_t)(L2 >> 32);
+    }
+}
+
+// W(R) of a wave-uniform target on one table (routing_table.cpp:89-104 closed form): lane l tests
+// round r0 + l from the good prefix sums, a ballot gives the least R; 64 rounds per probe.
+// Returns the window's buckets [lo, hi] and good count.
+__device__ __forceinline__ void wave_window(const uint32_t* gpre, uint32_t B, uint32_t b, uint32_t count,
+                                            uint32_t& lo, uint32_t& hi, uint32_t& good) {
+    const uint32_t lane = threadIdx.x & 63u;
+    for (uint32_t r0 = 0;; r0 += 64) {
+        const uint32_t r = r0 + lane;
+        const uint32_t l_ = b > r ? b - 1 - r : 0u;
+        const uint32_t h_ = (uint64_t)b + r >= (uint64_t)B - 1 ? B - 1 : b + r;
+        const uint32_t g_ = gpre[h_ + 1] - gpre[l_];
+        const uint64_t ok = __ballot(g_ >= count || (l_ == 0 && h_ == B - 1));
+        if (ok) {
+            const uint32_t R = (uint32_t)__builtin_ctzll(ok);
+            lo = rdl(l_, R);
+            hi = rdl(h_, R);
+            good = rdl(g_, R);
+            return;
+        }
+    }
+}
+
+__device__ void wave_exact(const DevTable& T, const Target& t, uint32_t count, uint32_t* row, uint8_t* cp,
+                           uint64_t* xs /* this wave's 64 x 3 LDS words */) {
+    const uint32_t lane = threadIdx.x & 63u, B = T.B;
+    if (B == 0 || count == 0) {
+        if (lane < count) row[lane] = NONE;
+        if (lane == 0 && cp) *cp = 0;
+        return;
+    }
+    uint32_t lo, hi, good;
+    wave_window(T.gpre, B, locate_bucket(T, t), count, lo, hi, good);
+    wave_rank(T, t, T.dir[lo].x & ~WIDE, T.dir[hi + 1].x & ~WIDE, good, count, row, nullptr, xs);
+    if (lane == 0 && cp) *cp = (uint8_t)min(count, good);
 }
 
 // The exact path for every lane of the wave whose fast path gave up (`ex`), one query at a time.
@@ -644,75 +674,95 @@ __device__ __forceinline__ uint32_t dw(const uint4 (&L)[8], int k) {  // static 
     return (k & 3) == 0 ? q.x : (k & 3) == 1 ? q.y : (k & 3) == 2 ? q.z : q.w;
 }
 
-// ABL (timing ablations only, KAD_RT_KERNEL=wl_abl1|wl_abl2; results wrong): 1 = no exact path,
-// 2 = also no ranking.
+// The window-line answer of lane's query: target t in bucket b of T (lines present, 1 <= count <= 8).
+// Returns true with o[0..8) (node indices + index_base, NONE from m on) and m = min(count, good
+// nodes of W(R_c)), or false when the query needs the exact path (marked line, target outside b's
+// range, too few stored slots). Contains a wave vote: call from uniform control flow, inactive lanes
+// with act = false (they return false).
+// ABL (timing ablations only, KAD_RT_KERNEL=wl_abl1|wl_abl2; results wrong): 2 = no ranking.
+template <int ABL>
+__device__ __forceinline__ bool wl_answer(const DevTable& T, const Target& t, uint32_t b, uint32_t count, bool act,
+                                          uint32_t (&o)[8], uint32_t& m) {
+    uint4 L[8];
+    if (act) {
+        const uint4* lp = T.wl + 8ull * b;
+#pragma unroll
+        for (int x = 0; x < 8; x++) L[x] = lp[x];
+    } else {
+#pragma unroll
+        for (int x = 0; x < 8; x++) L[x] = make_uint4(NONE, NONE, NONE, NONE);
+    }
+    const uint32_t d = 64 - T.rshift;
+    const uint32_t h = L[0].y, rounds = L[0].z;
+    // R_c = the least r <= R_8 with G(r) >= c or W(r) = the whole table
+    const uint32_t G0 = h & 63u, G1 = (h >> 6) & 63u, G2 = (h >> 12) & 63u, R8 = (h >> 21) & 3u, S = (h >> 23) & 31u;
+    const uint32_t Rc = (G0 >= count || (h >> 18) & 1u) ? 0u : (G1 >= count || (h >> 19) & 1u) ? 1u : 2u;
+    m = min(count, Rc == 0 ? G0 : Rc == 1 ? G1 : G2);
+    const bool own = (t.hi >> T.rshift) == (T.rbase >> T.rshift) + b;  // target inside bucket b's range
+    bool ex = !act || (h & WL_DEFER) || !own || (Rc == R8 && S < m);
+    const uint32_t tx = (uint32_t)((t.hi << d) >> (64 - WL_KBITS)) << 8;
+    uint32_t v[WL_SLOTS];
+#pragma unroll
+    for (int s = 0; s < (int)WL_SLOTS; s++) v[s] = dw(L, WL_SLOT0 + s) ^ tx;
+    if (__any(!ex && Rc < R8)) {  // count < 8 with a smaller window: drop the later rounds' buckets
+        uint32_t inc = 0;
+#pragma unroll
+        for (int j = 0; j < 6; j++) inc |= (((rounds >> (2 * j)) & 3u) <= Rc ? 1u : 0u) << j;
+        uint32_t have = 0;
+#pragma unroll
+        for (int s = 0; s < (int)WL_SLOTS; s++) {
+            const bool in = (uint32_t)s < S && ((inc >> (v[s] >> 29)) & 1u);
+            v[s] = in ? v[s] : NONE;
+            have += in;
+        }
+        ex |= have < m;
+    }
+    if (ABL < 2) {
+        sort8(v);
+        sort8(v + 8);
+        sort8(v + 16);
+        merge8(v, v + 8);
+        merge8(v, v + 16);
+    }
+    const uint32_t base = L[0].x + T.index_base;
+#pragma unroll
+    for (int j = 0; j < 8; j++) o[j] = (uint32_t)j < m ? base + (v[j] & 255u) : NONE;
+    return !ex;
+}
+
+__device__ __forceinline__ void store_row8(uint32_t* row, const uint32_t (&o)[8], uint32_t count) {
+    if (count == 8 && ((uintptr_t)row & 15u) == 0) {
+        reinterpret_cast<uint4*>(row)[0] = make_uint4(o[0], o[1], o[2], o[3]);
+        reinterpret_cast<uint4*>(row)[1] = make_uint4(o[4], o[5], o[6], o[7]);
+    } else {
+#pragma unroll
+        for (int j = 0; j < 8; j++)
+            if ((uint32_t)j < count) row[j] = o[j];
+    }
+}
+
+// ABL 1 = no exact path, 2 = also no ranking (timing ablations only).
 template <int ABL>
 __global__ __launch_bounds__(BLOCK) void rt_wl_kernel(DevTable T, const uint8_t* __restrict__ targets, uint32_t q,
                                                       uint32_t count, uint32_t* __restrict__ out_idx,
                                                       uint8_t* __restrict__ out_cnt) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
-    bool ex = false;
+    const bool act = i < q && count > 0;
+    if (i < q && count == 0 && out_cnt) out_cnt[i] = 0;
     Target t{};
-    if (i < q && count == 0) {
-        if (out_cnt) out_cnt[i] = 0;
-    } else if (i < q) {
+    uint32_t b = 0;
+    if (act) {
         t = load_target(targets, i);
-        const uint32_t d = 64 - T.rshift;
-        const uint32_t b = locate_bucket(T, t);
-        const uint4* lp = T.wl + 8ull * b;
-        uint4 L[8];
-#pragma unroll
-        for (int x = 0; x < 8; x++) L[x] = lp[x];
-        const uint32_t h = L[0].y, rounds = L[0].z;
-        // R_c = the least r <= R_8 with G(r) >= c or W(r) = the whole table
-        const uint32_t G0 = h & 63u, G1 = (h >> 6) & 63u, G2 = (h >> 12) & 63u, R8 = (h >> 21) & 3u, S = (h >> 23) & 31u;
-        const uint32_t Rc = (G0 >= count || (h >> 18) & 1u) ? 0u : (G1 >= count || (h >> 19) & 1u) ? 1u : 2u;
-        const uint32_t m = min(count, Rc == 0 ? G0 : Rc == 1 ? G1 : G2);
-        const bool own = (t.hi >> T.rshift) == (T.rbase >> T.rshift) + b;  // target inside bucket b's range
-        ex = (h & WL_DEFER) || !own || (Rc == R8 && S < m);
-        const uint32_t tx = (uint32_t)((t.hi << d) >> (64 - WL_KBITS)) << 8;
-        uint32_t v[WL_SLOTS];
-#pragma unroll
-        for (int s = 0; s < (int)WL_SLOTS; s++) v[s] = dw(L, WL_SLOT0 + s) ^ tx;
-        if (__any(!ex && Rc < R8)) {  // count < 8 with a smaller window: drop the later rounds' buckets
-            uint32_t inc = 0;
-#pragma unroll
-            for (int j = 0; j < 6; j++) inc |= (((rounds >> (2 * j)) & 3u) <= Rc ? 1u : 0u) << j;
-            uint32_t have = 0;
-#pragma unroll
-            for (int s = 0; s < (int)WL_SLOTS; s++) {
-                const bool in = (uint32_t)s < S && ((inc >> (v[s] >> 29)) & 1u);
-                v[s] = in ? v[s] : NONE;
-                have += in;
-            }
-            ex |= have < m;
-        }
-        if (ABL < 2) {
-            sort8(v);
-            sort8(v + 8);
-            sort8(v + 16);
-            merge8(v, v + 8);
-            merge8(v, v + 16);
-        }
-        if (!ex) {
-            uint32_t* row = out_idx + (size_t)i * count;
-            const uint32_t base = L[0].x + T.index_base;
-            uint32_t o[8];
-#pragma unroll
-            for (int j = 0; j < 8; j++) o[j] = (uint32_t)j < m ? base + (v[j] & 255u) : NONE;
-            if (count == 8) {
-                reinterpret_cast<uint4*>(row)[0] = make_uint4(o[0], o[1], o[2], o[3]);
-                reinterpret_cast<uint4*>(row)[1] = make_uint4(o[4], o[5], o[6], o[7]);
-            } else {
-#pragma unroll
-                for (int j = 0; j < 8; j++)
-                    if ((uint32_t)j < count) row[j] = o[j];
-            }
-            if (out_cnt) out_cnt[i] = (uint8_t)m;
-        }
+        b = locate_bucket(T, t);
+    }
+    uint32_t o[8], m;
+    const bool ok = wl_answer<ABL>(T, t, b, count, act, o, m);
+    if (act && ok) {
+        store_row8(out_idx + (size_t)i * count, o, count);
+        if (out_cnt) out_cnt[i] = (uint8_t)m;
     }
     __shared__ uint64_t xs[BLOCK / 64][192];
-    if (ABL == 0) exact_tail(T, t, ex, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
+    if (ABL == 0) exact_tail(T, t, act && !ok, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
 }
 
 // Window lines after a status change (or at table creation): one thread per bucket (d = depth).
@@ -781,6 +831,195 @@ __global__ __launch_bounds__(BLOCK) void rt_closest_dual_kernel(DevTable T4, Dev
     __shared__ uint64_t xs[BLOCK / 64][192];
     exact_tail(T4, t, ex && !six, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
     exact_tail(T6, t, ex && six, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
+}
+
+// ---------------------------------------------------------------------------------------
+// Sharded table without halo: the north-star multi-GPU variant.
+// The global uniform-depth table is cut into contiguous bucket ranges, one per GPU. Every rank
+// holds the GLOBAL good prefix sums (all-gathered once at setup), so it can compute any query's
+// global window W(R), and answers W(R) ∩ its shard for every query of a replicated batch:
+//   * W(R) misses the shard       -> nothing; a lane whose bucket lies outside [reach_lo, reach_hi)
+//                                    exits after one compare, without a load
+//   * W(R) inside the shard       -> its final row, appended to `rows` (compact)
+//   * W(R) crosses a shard edge   -> this shard's top-count of W(R) ∩ shard with the entries' XOR
+//                                    distances, appended to `parts`; kad_rt_merge_parts merges them
+// Queries whose bucket is >= 4 buckets inside the shard use the window line (its local window is the
+// global one); the others take the wave-cooperative path on the global window.
+// Row layout (uint32): qid, m, 0, 0, idx[count] (padded to 4): KAD_ROW_WORDS(count).
+// Part layout: the row, then dist[count][5]: KAD_PART_WORDS(count).
+// Complete rows of block k go to region k % 8 of KAD_SHARD_REGIONS regions of row_cap rows: one
+// atomic per block for the window-line rows, eight counters (a single counter hit by every wave cost
+// ~10 ns per wave, 160 us per 1M queries). A region can hold every query of its blocks, so
+// row_cap >= ceil(ceil(q / 256) / 8) * 256 never overflows.
+// ---------------------------------------------------------------------------------------
+struct ShardCtx {
+    const uint32_t* gpre;  // global good prefix sums, GB + 1
+    uint64_t gbase;        // top 64 bits of global bucket 0's first ID
+    uint32_t gshift, GB;   // global direct locate: b = (t.hi - gbase) >> gshift, clamped to [0, GB)
+    uint32_t s_lo, s_hi;   // global buckets held by this shard (local bucket = global - s_lo)
+    uint32_t reach_lo, reach_hi;
+    uint32_t* rows;
+    uint32_t* parts;
+    uint32_t* ctr;  // counter k at word KAD_SHARD_COUNTER_STRIDE*k (own 128-byte line): [0..7] rows appended
+                    // per region, [8] parts appended, [9] overflow flag
+    uint32_t row_cap, part_cap, rs, ps;
+};
+
+__device__ __forceinline__ uint32_t shard_bucket(const ShardCtx& S, const Target& t) {
+    if (t.hi < S.gbase) return 0;
+    const uint64_t s = (t.hi - S.gbase) >> S.gshift;
+    return s >= S.GB ? S.GB - 1 : (uint32_t)s;
+}
+
+__device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// One query, wave-uniform: global window, intersection with the shard, wave_rank, append.
+__device__ void wave_shard(const DevTable& T, const ShardCtx& S, const Target& t, uint32_t qid, uint32_t count,
+                           uint64_t* xs) {
+    const uint32_t lane = threadIdx.x & 63u;
+    uint32_t lo, hi, good;
+    wave_window(S.gpre, S.GB, shard_bucket(S, t), count, lo, hi, good);
+    const uint32_t a = max(lo, S.s_lo), e = min(hi + 1, S.s_hi);
+    if (a >= e) return;
+    const bool complete = lo >= S.s_lo && hi < S.s_hi;
+    const uint32_t al = a - S.s_lo, el = e - S.s_lo;
+    const uint32_t lgood = T.gpre[el] - T.gpre[al];
+    uint32_t slot = 0;
+    const uint32_t region = blockIdx.x & 7u;
+    if (lane == 0) slot = atomicAdd(S.ctr + KAD_SHARD_COUNTER_STRIDE * (complete ? region : 8u), 1u);
+    slot = rdl(slot, 0);
+    if (slot >= (complete ? S.row_cap : S.part_cap)) {
+        if (lane == 0) atomicOr(S.ctr + KAD_SHARD_COUNTER_STRIDE * 9u, 1u);
+        return;
+    }
+    uint32_t* row = complete ? S.rows + ((size_t)region * S.row_cap + slot) * S.rs : S.parts + (size_t)slot * S.ps;
+    if (lane == 0) {
+        row[0] = qid;
+        row[1] = min(count, lgood);
+        row[2] = 0;
+        row[3] = 0;
+    }
+    wave_rank(T, t, T.dir[al].x & ~WIDE, T.dir[el].x & ~WIDE, lgood, count, row + 4,
+              complete ? nullptr : row + (S.rs), xs);
+}
+
+template <bool WL>
+__global__ __launch_bounds__(BLOCK) void rt_shard_kernel(DevTable T, ShardCtx S, const uint8_t* __restrict__ targets,
+                                                         uint32_t q, uint32_t count) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    Target t{};
+    bool near = false, line = false;
+    uint32_t b = 0;
+    if (i < q) {
+        t = load_target(targets, i);
+        b = shard_bucket(S, t);
+        near = b >= S.reach_lo && b < S.reach_hi;
+        line = WL && near && b >= S.s_lo + 4 && b + 4 <= S.s_hi;
+    }
+    bool edge = near;
+    __shared__ uint64_t xs[BLOCK / 64][192];
+    __shared__ uint32_t wcnt[BLOCK / 64 + 1];
+    if (WL && __syncthreads_or(line)) {  // block-uniform
+        uint32_t o[8], m;
+        const bool ok = wl_answer<0>(T, t, line ? b - S.s_lo : 0u, count, line, o, m);
+        const uint64_t want = __ballot(ok);
+        const uint32_t w = threadIdx.x >> 6;
+        if ((threadIdx.x & 63u) == 0) wcnt[w] = (uint32_t)__builtin_popcountll(want);
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t tot = 0;
+            for (uint32_t k = 0; k < BLOCK / 64; k++) tot += wcnt[k];
+            wcnt[BLOCK / 64] = tot ? atomicAdd(S.ctr + KAD_SHARD_COUNTER_STRIDE * (blockIdx.x & 7u), tot) : 0u;
+        }
+        __syncthreads();
+        uint32_t slot = wcnt[BLOCK / 64] + lanes_below(want);
+        for (uint32_t k = 0; k < w; k++) slot += wcnt[k];
+        if (ok) {
+            if (slot < S.row_cap) {
+                uint32_t* row = S.rows + ((size_t)(blockIdx.x & 7u) * S.row_cap + slot) * S.rs;
+                reinterpret_cast<uint4*>(row)[0] = make_uint4(i, m, 0u, 0u);
+                store_row8(row + 4, o, count);
+                edge = false;
+            } else {
+                atomicOr(S.ctr + KAD_SHARD_COUNTER_STRIDE * 9u, 1u);
+            }
+        }
+    }
+    for (uint64_t mm = __ballot(edge); mm; mm &= mm - 1) {
+        const uint32_t l = (uint32_t)__builtin_ctzll(mm);
+        Target u;
+        u.hi = rdl64(t.hi, l);
+        u.t2 = rdl(t.t2, l);
+        u.t3 = rdl(t.t3, l);
+        u.t4 = rdl(t.t4, l);
+        wave_shard(T, S, u, rdl(i, l), count, xs[threadIdx.x >> 6]);
+    }
+}
+
+// Gathered complete rows -> out rows. Block r of n_blocks holds n_rows[r] rows of `stride` words at
+// rows + r * block_cap * stride.
+__global__ void scatter_rows_kernel(const uint32_t* __restrict__ rows, const uint32_t* __restrict__ n_rows,
+                                    uint32_t n_rows_stride, uint32_t n_blocks, uint32_t block_cap, uint32_t stride,
+                                    uint32_t count,
+                                    uint32_t* __restrict__ out_idx, uint8_t* __restrict__ out_cnt) {
+    const uint64_t g = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    const uint32_t r = (uint32_t)(g / block_cap), k = (uint32_t)(g % block_cap);
+    if (r >= n_blocks || k >= min(n_rows[(size_t)r * n_rows_stride], block_cap)) return;
+    const uint32_t* src = rows + ((size_t)r * block_cap + k) * stride;
+    const uint32_t qid = src[0];
+    if (out_cnt) out_cnt[qid] = (uint8_t)src[1];
+    uint32_t* dst = out_idx + (size_t)qid * count;
+    if (count == 8 && ((uintptr_t)dst & 15u) == 0) {
+        reinterpret_cast<uint4*>(dst)[0] = reinterpret_cast<const uint4*>(src)[1];
+        reinterpret_cast<uint4*>(dst)[1] = reinterpret_cast<const uint4*>(src)[2];
+    } else {
+        for (uint32_t j = 0; j < count; j++) dst[j] = src[4 + j];
+    }
+}
+
+// Partial rows sorted by qid: the thread of a qid segment's first row merges the segment's sorted
+// lists by (XOR distance, global index) and writes the first min(count, sum of m) entries.
+__global__ void merge_parts_kernel(const uint32_t* __restrict__ parts, uint32_t n, uint32_t rs, uint32_t ps,
+                                   uint32_t count, uint32_t* __restrict__ out_idx, uint8_t* __restrict__ out_cnt) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t qid = parts[(size_t)i * ps];
+    if (i > 0 && parts[(size_t)(i - 1) * ps] == qid) return;
+    uint32_t e = i + 1;
+    while (e < n && parts[(size_t)e * ps] == qid) e++;
+    constexpr uint32_t MAXSEG = 16;
+    uint32_t head[MAXSEG], total = 0;
+    const uint32_t nseg = min(e - i, MAXSEG);
+    for (uint32_t s = 0; s < nseg; s++) {
+        head[s] = 0;
+        total += parts[(size_t)(i + s) * ps + 1];
+    }
+    const uint32_t m = min(count, total);
+    uint32_t* dst = out_idx + (size_t)qid * count;
+    for (uint32_t p = 0; p < count; p++) {
+        if (p >= m) {
+            dst[p] = NONE;
+            continue;
+        }
+        uint32_t best = NONE;
+        for (uint32_t s = 0; s < nseg; s++) {
+            const uint32_t* r = parts + (size_t)(i + s) * ps;
+            if (head[s] >= r[1]) continue;
+            if (best == NONE) { best = s; continue; }
+            const uint32_t* rb = parts + (size_t)(i + best) * ps;
+            const uint32_t* da = r + rs + 5 * head[s];
+            const uint32_t* db = rb + rs + 5 * head[best];
+            int c = 0;
+            for (int w = 0; w < 5 && c == 0; w++) c = da[w] < db[w] ? -1 : da[w] > db[w] ? 1 : 0;
+            if (c < 0 || (c == 0 && r[4 + head[s]] < rb[4 + head[best]])) best = s;
+        }
+        const uint32_t* rb = parts + (size_t)(i + best) * ps;
+        dst[p] = rb[4 + head[best]];
+        head[best]++;
+    }
+    if (out_cnt) out_cnt[qid] = (uint8_t)m;
 }
 
 __global__ __launch_bounds__(BLOCK) void find_bucket_kernel(DevTable T, const uint8_t* __restrict__ targets,
@@ -1468,6 +1707,79 @@ int kad_rt_closest_batch_dual(const kad_table* t4, const kad_table* t6, const ui
     if (count <= 8) launch_rt_dual<8>(d4, d6, targets, af, q, count, out_idx, out_cnt, s);
     else if (count <= 16) launch_rt_dual<16>(d4, d6, targets, af, q, count, out_idx, out_cnt, s);
     else launch_rt_dual<32>(d4, d6, targets, af, q, count, out_idx, out_cnt, s);
+    HIP_TRY(hipGetLastError());
+    return KAD_OK;
+}
+
+int kad_rt_shard_batch(const kad_table* t, const uint32_t* global_good_prefix, uint32_t global_buckets,
+                       uint64_t global_base_hi, uint32_t depth, uint32_t shard_first_bucket, uint32_t reach_lo,
+                       uint32_t reach_hi, const uint8_t* targets, uint32_t q, uint32_t count, uint32_t* rows,
+                       uint32_t row_cap, uint32_t* parts, uint32_t part_cap, uint32_t* counters, void* stream) {
+    if (!t) return set_err(KAD_ERR_INVALID, "NULL table");
+    int rc = check_count(count);
+    if (rc) return rc;
+    if (count == 0) return set_err(KAD_ERR_INVALID, "count 0: nothing to answer (the caller writes empty rows)");
+    if (depth < 1 || depth > 63) return set_err(KAD_ERR_INVALID, "depth %u outside 1..63", depth);
+    if ((uint64_t)shard_first_bucket + t->d.B > global_buckets)
+        return set_err(KAD_ERR_INVALID, "shard buckets [%u, %u) exceed the %u global buckets", shard_first_bucket,
+                       shard_first_bucket + t->d.B, global_buckets);
+    if (q == 0) return KAD_OK;
+    if (!global_good_prefix || !targets || !rows || !parts || !counters) return set_err(KAD_ERR_INVALID, "NULL buffer");
+    if (t->d.B == 0) return KAD_OK;
+    ShardCtx S{};
+    S.gpre = global_good_prefix;
+    S.gbase = global_base_hi;
+    S.gshift = 64 - depth;
+    S.GB = global_buckets;
+    S.s_lo = shard_first_bucket;
+    S.s_hi = shard_first_bucket + t->d.B;
+    S.reach_lo = reach_lo;
+    S.reach_hi = reach_hi;
+    S.rows = rows;
+    S.parts = parts;
+    S.ctr = counters;
+    S.row_cap = row_cap;
+    S.part_cap = part_cap;
+    S.rs = KAD_ROW_WORDS(count);
+    S.ps = KAD_PART_WORDS(count);
+    // the window line is valid for a shard of a uniform table of the same depth
+    const bool wl = count <= 8 && (t->d.flags & TF_WL) && (64 - t->d.rshift) == depth;
+    DeviceGuard g(t->device);
+    if (wl)
+        hipLaunchKernelGGL(rt_shard_kernel<true>, dim3(grid_for(q)), dim3(BLOCK), 0, (hipStream_t)stream, t->d, S,
+                           targets, q, count);
+    else
+        hipLaunchKernelGGL(rt_shard_kernel<false>, dim3(grid_for(q)), dim3(BLOCK), 0, (hipStream_t)stream, t->d, S,
+                           targets, q, count);
+    HIP_TRY(hipGetLastError());
+    return KAD_OK;
+}
+
+int kad_rt_scatter_rows(const uint32_t* rows, const uint32_t* n_rows, uint32_t n_rows_stride, uint32_t n_blocks,
+                        uint32_t block_cap, uint32_t count, uint32_t* out_idx, uint8_t* out_cnt, int device,
+                        void* stream) {
+    int rc = check_count(count);
+    if (rc) return rc;
+    if (n_blocks == 0 || block_cap == 0) return KAD_OK;
+    if (!rows || !n_rows || !out_idx) return set_err(KAD_ERR_INVALID, "NULL buffer");
+    DeviceGuard g(device);
+    hipLaunchKernelGGL(scatter_rows_kernel, dim3(grid_for((uint64_t)n_blocks * block_cap)), dim3(BLOCK), 0,
+                       (hipStream_t)stream, rows, n_rows, n_rows_stride ? n_rows_stride : 1u, n_blocks, block_cap,
+                       (uint32_t)KAD_ROW_WORDS(count), count,
+                       out_idx, out_cnt);
+    HIP_TRY(hipGetLastError());
+    return KAD_OK;
+}
+
+int kad_rt_merge_parts(const uint32_t* parts, uint32_t n_parts, uint32_t count, uint32_t* out_idx, uint8_t* out_cnt,
+                       int device, void* stream) {
+    int rc = check_count(count);
+    if (rc) return rc;
+    if (n_parts == 0) return KAD_OK;
+    if (!parts || !out_idx) return set_err(KAD_ERR_INVALID, "NULL buffer");
+    DeviceGuard g(device);
+    hipLaunchKernelGGL(merge_parts_kernel, dim3(grid_for(n_parts)), dim3(BLOCK), 0, (hipStream_t)stream, parts, n_parts,
+                       (uint32_t)KAD_ROW_WORDS(count), (uint32_t)KAD_PART_WORDS(count), count, out_idx, out_cnt);
     HIP_TRY(hipGetLastError());
     return KAD_OK;
 }

@@ -1,0 +1,164 @@
+"""North-star multi-GPU variant (opendht_amd/global_shard.py): shards without halo answer their part
+of every query's global window; complete rows are scattered and partial rows merged on the device.
+The GPU tests simulate the all-gather by concatenating the shards' outputs on one GPU (one process
+cannot open RCCL on one device twice); the gloo test runs the gather plumbing with world_size 2.
+Bit-exact against the oracle on the whole table."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+import oracle as O
+from opendht_amd import synth as S
+from opendht_amd._lib import check, lib, ptr
+from opendht_amd.global_shard import GlobalShard, build_plain_shard, merge_parts, reach
+from opendht_amd.metrics import good_counts, window_radii
+from opendht_amd.sharded import ShardSpec
+
+CASES = [  # (n_shards, depth, mean nodes per bucket, good %)
+    (4, 10, 6.0, 80),
+    (8, 8, 6.0, 30),
+    (8, 6, 2.0, 8),     # windows spanning several whole shards: up to 8 parts per query
+    (1, 9, 6.0, 80),    # one shard = the whole table
+]
+
+
+def _targets(spec, n, seed):
+    """Random targets plus targets in the buckets around every shard edge."""
+    rng = np.random.default_rng(seed)
+    parts = [S.random_targets(n, seed=seed)]
+    B = spec.n_buckets
+    per = B // spec.n_shards
+    edges = np.unique(np.clip(np.concatenate([[0, B - 1]] + [np.arange(e - 5, e + 5) for e in range(per, B, per)]),
+                              0, B - 1))
+    for b in edges:
+        f = S.bucket_firsts(spec.depth, int(b), int(b) + 1).copy()
+        f[0, 8:] = rng.integers(0, 256, 12, dtype=np.uint8)
+        # random low bits below the bucket prefix
+        pre = int.from_bytes(f[0, :8].tobytes(), "big")
+        pre |= int(rng.integers(0, 1 << 62)) >> spec.depth
+        f[0, :8] = np.frombuffer(pre.to_bytes(8, "big"), np.uint8)
+        parts.append(f)
+    return np.ascontiguousarray(np.concatenate(parts), np.uint8)
+
+
+def _build(spec, device):
+    built = [build_plain_shard(spec, s) for s in range(spec.n_shards)]
+    gp = np.concatenate([[0], np.cumsum(np.concatenate([b[6] for b in built]))])
+    shards = [GlobalShard(ids, st, off, lo, hi, spec.depth, base, gp, device=device)
+              for ids, st, off, lo, hi, base, _ in built]
+    return shards
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", CASES, ids=lambda c: f"N{c[0]}_U{c[1]}_g{c[3]}")
+def test_global_shards_simulated_gather(gpu, case):
+    n_shards, depth, mean, good = case
+    spec = ShardSpec(n_shards=n_shards, depth=depth, mean_per_bucket=mean, seed=0x6A7 + depth, good_pct=good,
+                     expired_pct=(100 - good) // 2)
+    gids, gst, goff = spec.bucket_range(0, spec.n_buckets)
+    gfirst = S.bucket_firsts(spec.depth, 0, spec.n_buckets)
+    targets = _targets(spec, 3000, seed=depth)
+    tg = torch.from_numpy(targets).to(gpu)
+    shards = _build(spec, gpu.index or 0)
+    try:
+        for count in (1, 3, 8, 9, 14, 32):
+            outs = [sh.local_compact(tg, count) for sh in shards]
+            nr = [o[0].shape[0] for o in outs]
+            maxr = max(nr)
+            g_rows = torch.stack([torch.cat([o[0], o[0].new_zeros((maxr - o[0].shape[0], o[0].shape[1]))])
+                                  for o in outs]).contiguous()
+            n_rows = torch.tensor(nr, dtype=torch.int32, device=gpu)
+            q = targets.shape[0]
+            out_idx = torch.full((q, count), -1, dtype=torch.int32, device=gpu)
+            out_cnt = torch.full((q,), 255, dtype=torch.uint8, device=gpu)
+            s = torch.cuda.current_stream(gpu).cuda_stream
+            check(lib().kad_rt_scatter_rows(ptr(g_rows), ptr(n_rows), 1, len(shards), maxr, count, ptr(out_idx),
+                                            ptr(out_cnt), gpu.index or 0, s), "scatter")
+            npart = [o[1].shape[0] for o in outs]
+            if max(npart):
+                maxp = max(npart)
+                g_parts = torch.stack([torch.cat([o[1], o[1].new_zeros((maxp - o[1].shape[0], o[1].shape[1]))])
+                                       for o in outs])
+                merge_parts(g_parts, npart, count, out_idx, out_cnt, gpu.index or 0)
+            if n_shards == 1:  # the no-sync single-rank path
+                i2, c2 = shards[0].query(tg, count)
+                torch.cuda.synchronize()
+                np.testing.assert_array_equal(i2.cpu().numpy(), out_idx.cpu().numpy())
+                np.testing.assert_array_equal(c2.cpu().numpy(), out_cnt.cpu().numpy())
+            torch.cuda.synchronize()
+            want, wcnt = O.flat_rt_closest(gids, gst, gfirst, goff, targets, count, nthreads=8)
+            np.testing.assert_array_equal(out_cnt.cpu().numpy(), wcnt, err_msg=f"{case} k={count} counts")
+            np.testing.assert_array_equal(out_idx.cpu().numpy().view(np.uint32), want, err_msg=f"{case} k={count}")
+            if n_shards > 1 and count == 8:
+                assert sum(npart) > 0  # the edge targets produced parts
+    finally:
+        for sh in shards:
+            sh.close()
+
+
+def test_reach_covers_every_touching_bucket():
+    """reach() against the brute-force set of buckets whose window touches [lo, hi)."""
+    rng = np.random.default_rng(4)
+    for trial in range(30):
+        B = 256
+        good = rng.poisson(rng.choice([0.3, 1.0, 5.0]), B)
+        gp = np.concatenate([[0], np.cumsum(good)])
+        lo = int(rng.integers(0, B - 1))
+        hi = int(rng.integers(lo + 1, B + 1))
+        rlo, rhi = reach(gp, lo, hi, 32)
+        for count in (1, 8, 32):
+            R = window_radii(good, count)
+            b = np.arange(B)
+            wlo, whi = np.maximum(0, b - 1 - R), np.minimum(B - 1, b + R)
+            touch = (whi >= lo) & (wlo < hi)
+            assert touch[:rlo].sum() == 0 and touch[rhi:].sum() == 0, (trial, count)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _gather_worker(rank, world, port, q):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path[:0] = [os.path.dirname(here), here]
+    import torch.distributed as dist
+
+    from opendht_amd.global_shard import allgather_padded, global_good_prefix
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        n = 3 + 4 * rank  # ragged row counts
+        rows = torch.arange(100 * 6, dtype=torch.int32).reshape(100, 6) + 1000 * rank
+        g, counts = allgather_padded(rows, n)
+        ok = counts == [3 + 4 * r for r in range(world)] and g.shape == (world, max(counts), 6)
+        for r in range(world):
+            exp = torch.arange(100 * 6, dtype=torch.int32).reshape(100, 6)[:counts[r]] + 1000 * r
+            ok = ok and torch.equal(g[r, :counts[r]], exp)
+        gp = global_good_prefix(np.full(5, rank + 1))
+        ok = ok and np.array_equal(gp, np.concatenate([[0], np.cumsum(np.repeat(np.arange(1, world + 1), 5))]))
+        q.put((rank, bool(ok)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_allgather_padded_gloo_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gather_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res == {0: True, 1: True}
