@@ -162,3 +162,58 @@ def test_allgather_padded_gloo_world2():
         p.join(timeout=60)
         assert p.exitcode == 0
     assert res == {0: True, 1: True}
+
+
+def _query_worker(rank, world, port, q):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path[:0] = [os.path.dirname(here), os.path.join(os.path.dirname(here), "oracle"), here]
+    import torch.distributed as dist
+
+    import oracle as O
+    from opendht_amd import synth as S
+    from opendht_amd.global_shard import GlobalShard, build_plain_shard, global_good_prefix
+    from opendht_amd.sharded import ShardSpec
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    # both ranks share cuda:0 (one GPU box): gloo stages the gathers through the host
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ok = False
+    try:
+        dev = torch.device("cuda:0")
+        spec = ShardSpec(n_shards=world, depth=9, mean_per_bucket=6.0, seed=0x5A, good_pct=40, expired_pct=30)
+        ids, st, off, lo, hi, base, good = build_plain_shard(spec, rank)
+        gp = global_good_prefix(good)
+        G = GlobalShard(ids, st, off, lo, hi, spec.depth, base, gp, device=0)
+        targets = _targets(spec, 2000, seed=3)
+        tg = torch.from_numpy(targets).to(dev)
+        gids, gst, goff = spec.bucket_range(0, spec.n_buckets)
+        gfirst = S.bucket_firsts(spec.depth, 0, spec.n_buckets)
+        ok = True
+        for count in (1, 8, 14, 32):
+            idx, cnt = G.query(tg, count)
+            torch.cuda.synchronize()
+            want, wcnt = O.flat_rt_closest(gids, gst, gfirst, goff, targets, count)
+            ok = ok and np.array_equal(idx.cpu().numpy().view(np.uint32), want) and np.array_equal(cnt.cpu().numpy(), wcnt)
+        G.close()
+    finally:
+        q.put((rank, bool(ok)))
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_global_shard_query_world2_gloo_gpu(gpu):
+    """The whole query() protocol with two ranks (gloo, both on cuda:0): kernels, padded all-gather
+    of rows and parts, scatter, merge."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_query_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res == {0: True, 1: True}
