@@ -199,6 +199,28 @@ int kad_rt_scatter_rows(const uint32_t* rows, const uint32_t* n_rows, uint32_t n
 int kad_rt_merge_parts(const uint32_t* parts, uint32_t n_parts, uint32_t count, uint32_t* out_idx,
                        uint8_t* out_cnt, int device, void* stream);
 
+/* ---- wire step after the query ------------------------ */
+#define KAD_SEND_NODES 8u           /* reference network_engine.cpp:59 SEND_NODES */
+#define KAD_ADDR4_LEN 6u            /* sin_addr (4) + sin_port (2), bytes as stored in sockaddr_in */
+#define KAD_ADDR6_LEN 18u           /* sin6_addr (16) + sin6_port (2) */
+#define KAD_NODE4_INFO_LEN 26u      /* network_engine.h:464 NODE4_INFO_BUF_LEN */
+#define KAD_NODE6_INFO_LEN 38u      /* network_engine.h:466 NODE6_INFO_BUF_LEN */
+/* Attach node addresses to a table (one family): host array, n_nodes x addr_len bytes
+ * (KAD_ADDR4_LEN or KAD_ADDR6_LEN). Synchronous. */
+int kad_table_set_addrs(kad_table* t, uint32_t addr_len, const uint8_t* addrs);
+/* Batched NetworkEngine::bufferNodes(af, id, nodes) (network_engine.cpp:942-974): for query i the
+ * candidates idx[i*k .. i*k + cnt[i]) (node indices incl. index_base, e.g. a findClosestNodes or
+ * getCachedNodes result; cnt may be NULL: entries up to the first KAD_NO_NODE), sorted by XOR
+ * distance to targets[i], the first KAD_SEND_NODES packed as ID + address records into
+ * out[i * KAD_SEND_NODES * (20 + addr_len)]; out_n[i] = records written. Device pointers. */
+int kad_buffer_nodes_batch(const kad_table* t, const uint8_t* targets, uint32_t q, const uint32_t* idx,
+                           const uint8_t* cnt, uint32_t k, uint8_t* out, uint8_t* out_n, void* stream);
+/* NetworkEngine::deserializeNodes' filter (network_engine.cpp:788-828): for n records of rec_len
+ * (KAD_NODE4_INFO_LEN / KAD_NODE6_INFO_LEN) bytes, keep[i] = 0 if the record's ID is myid (host,
+ * 20 bytes) or its address is martian (NetworkEngine::isMartian, :308-339). Device pointers. */
+int kad_parse_nodes_batch(const uint8_t* records, uint32_t n, uint32_t rec_len, const uint8_t* myid,
+                          uint8_t* keep, int device, void* stream);
+
 /* ---- InfoHash primitives (infohash.h), batched, device pointers ---------- */
 /* out[i] = targets[i].xorCmp(a[i], b[i]) in {-1,0,1}   (infohash.h:131-146) */
 int kad_xor_cmp_batch(const uint8_t* targets, const uint8_t* a, const uint8_t* b, uint32_t n,

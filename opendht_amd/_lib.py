@@ -68,6 +68,9 @@ SIGNATURES = {
     "kad_rt_scatter_rows": (C.c_int, [_P, _P, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, _P, _P, C.c_int,
                                       _P]),
     "kad_rt_merge_parts": (C.c_int, [_P, C.c_uint32, C.c_uint32, _P, _P, C.c_int, _P]),
+    "kad_table_set_addrs": (C.c_int, [_P, C.c_uint32, _P]),
+    "kad_buffer_nodes_batch": (C.c_int, [_P, _P, C.c_uint32, _P, _P, C.c_uint32, _P, _P, _P]),
+    "kad_parse_nodes_batch": (C.c_int, [_P, C.c_uint32, C.c_uint32, _P, _P, C.c_int, _P]),
     "kad_xor_cmp_batch": (C.c_int, [_P, _P, _P, C.c_uint32, _P, _P]),
     "kad_common_bits_batch": (C.c_int, [_P, _P, C.c_uint32, _P, _P]),
     "kad_lowbit_batch": (C.c_int, [_P, C.c_uint32, _P, _P]),

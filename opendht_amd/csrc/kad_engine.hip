@@ -1022,6 +1022,102 @@ __global__ void merge_parts_kernel(const uint32_t* __restrict__ parts, uint32_t 
     if (out_cnt) out_cnt[qid] = (uint8_t)m;
 }
 
+// ---------------------------------------------------------------------------------------
+// Wire step after the query
+// NetworkEngine::bufferNodes (network_engine.cpp:942-974): a query's candidate nodes sorted by
+// XOR distance to the target (std::sort on xorCmp, :945-947), the first SEND_NODES = 8 (:948),
+// each packed as its 20-byte ID followed by the stored address + port bytes (26-byte v4 records,
+// 38-byte v6 records). One lane per query: a register top-8 over the exact 160-bit distance
+// (ties, i.e. duplicate IDs, keep input order), then byte stores of the records.
+// ---------------------------------------------------------------------------------------
+constexpr uint32_t SEND_NODES = 8;
+
+__global__ __launch_bounds__(BLOCK) void buffer_nodes_kernel(DevTable T, const uint8_t* __restrict__ addr,
+                                                             uint32_t al, const uint8_t* __restrict__ targets,
+                                                             uint32_t q, const uint32_t* __restrict__ idx,
+                                                             const uint8_t* __restrict__ cnt, uint32_t k,
+                                                             uint8_t* __restrict__ out, uint8_t* __restrict__ out_n) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= q) return;
+    const Target t = load_target(targets, i);
+    const uint32_t* row = idx + (size_t)i * k;
+    uint32_t n = cnt ? min((uint32_t)cnt[i], k) : k;
+    uint64_t L0[SEND_NODES], L1[SEND_NODES];
+    uint32_t L2[SEND_NODES], LN[SEND_NODES];
+    uint32_t nl = 0;
+#pragma unroll
+    for (int s = 0; s < (int)SEND_NODES; s++) { L0[s] = ~0ull; L1[s] = ~0ull; L2[s] = NONE; LN[s] = NONE; }
+    for (uint32_t j = 0; j < n; j++) {
+        const uint32_t g = row[j];
+        if (!cnt && g == NONE) break;
+        const uint32_t v = g - T.index_base;
+        if (v >= T.n) continue;  // not a node of this table
+        const uint32_t* tl = T.tail + 3ull * v;
+        uint64_t c0 = T.key[v] ^ t.hi, c1 = ((uint64_t)(tl[0] ^ t.t2) << 32) | (tl[1] ^ t.t3);
+        uint32_t c2 = tl[2] ^ t.t4, cn = v;
+        bool sh = false;
+#pragma unroll
+        for (int s = 0; s < (int)SEND_NODES; s++) {  // insertion: strictly smaller moves ahead
+            const bool lt = sh || (uint32_t)s >= nl || c0 < L0[s] ||
+                            (c0 == L0[s] && (c1 < L1[s] || (c1 == L1[s] && c2 < L2[s])));
+            sh = lt;
+            const uint64_t n0 = lt ? L0[s] : c0, n1 = lt ? L1[s] : c1;
+            const uint32_t n2 = lt ? L2[s] : c2, nn = lt ? LN[s] : cn;
+            L0[s] = lt ? c0 : L0[s];
+            L1[s] = lt ? c1 : L1[s];
+            L2[s] = lt ? c2 : L2[s];
+            LN[s] = lt ? cn : LN[s];
+            c0 = n0; c1 = n1; c2 = n2; cn = nn;
+        }
+        nl = min(nl + 1, SEND_NODES);
+    }
+    const uint32_t rec = KAD_HASH_LEN + al;
+    uint8_t* dst = out + (size_t)i * SEND_NODES * rec;
+#pragma unroll
+    for (int s = 0; s < (int)SEND_NODES; s++) {
+        if ((uint32_t)s >= nl) break;
+        const uint32_t v = LN[s];
+        uint8_t* d = dst + s * rec;
+        const uint64_t key = T.key[v];
+        const uint32_t* tl = T.tail + 3ull * v;
+#pragma unroll
+        for (int b = 0; b < 8; b++) d[b] = (uint8_t)(key >> (56 - 8 * b));
+#pragma unroll
+        for (int w = 0; w < 3; w++)
+#pragma unroll
+            for (int b = 0; b < 4; b++) d[8 + 4 * w + b] = (uint8_t)(tl[w] >> (24 - 8 * b));
+        const uint8_t* a = addr + (size_t)al * v;
+        for (uint32_t b = 0; b < al; b++) d[KAD_HASH_LEN + b] = a[b];
+    }
+    if (out_n) out_n[i] = (uint8_t)nl;
+}
+
+// NetworkEngine::isMartian (network_engine.cpp:308-339) on address + port bytes; v4prefix = ::ffff:0:0/96.
+__device__ __forceinline__ bool is_martian(const uint8_t* a, uint32_t al) {
+    if (al == 6) return (a[4] == 0 && a[5] == 0) || a[0] == 0 || a[0] == 127 || (a[0] & 0xE0) == 0xE0;
+    bool z15 = true, v4m = a[10] == 0xFF && a[11] == 0xFF;
+    for (int b = 0; b < 15; b++) z15 &= a[b] == 0;
+    for (int b = 0; b < 10; b++) v4m &= a[b] == 0;
+    return (a[16] == 0 && a[17] == 0) || a[0] == 0xFF || (a[0] == 0xFE && (a[1] & 0xC0) == 0x80) ||
+           (z15 && (a[15] == 0 || a[15] == 1)) || v4m;
+}
+
+struct Id20 {
+    uint8_t b[KAD_HASH_LEN];
+};
+
+// NetworkEngine::deserializeNodes' filter (network_engine.cpp:788-828): keep = not our own ID
+// (:798-799) and not a martian address (:806, :822), per 26- or 38-byte record.
+__global__ void parse_nodes_kernel(const uint8_t* __restrict__ in, uint32_t n, uint32_t rec_len, Id20 myid,
+                                   uint8_t* __restrict__ keep) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n) return;
+    const uint8_t* r = in + (size_t)rec_len * i;
+    bool mine = true;
+    for (int b = 0; b < (int)KAD_HASH_LEN; b++) mine &= r[b] == myid.b[b];
+    keep[i] = !(mine || is_martian(r + KAD_HASH_LEN, rec_len - KAD_HASH_LEN));
+}
+
 __global__ __launch_bounds__(BLOCK) void find_bucket_kernel(DevTable T, const uint8_t* __restrict__ targets,
                                                             uint32_t q, uint32_t* __restrict__ out) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
@@ -1321,6 +1417,8 @@ struct kad_table {
     uint2* dir_mut = nullptr;
     uint32_t* gpre_mut = nullptr;
     uint32_t* wl_mut = nullptr;
+    uint8_t* addr = nullptr;  // node address + port records (kad_table_set_addrs)
+    uint32_t addr_len = 0;
     int64_t* time_ns = nullptr;
     int64_t* reply_ns = nullptr;
     uint8_t* expired = nullptr;
@@ -1780,6 +1878,47 @@ int kad_rt_merge_parts(const uint32_t* parts, uint32_t n_parts, uint32_t count, 
     DeviceGuard g(device);
     hipLaunchKernelGGL(merge_parts_kernel, dim3(grid_for(n_parts)), dim3(BLOCK), 0, (hipStream_t)stream, parts, n_parts,
                        (uint32_t)KAD_ROW_WORDS(count), (uint32_t)KAD_PART_WORDS(count), count, out_idx, out_cnt);
+    HIP_TRY(hipGetLastError());
+    return KAD_OK;
+}
+
+int kad_table_set_addrs(kad_table* t, uint32_t addr_len, const uint8_t* addrs) {
+    if (!t || (t->d.n && !addrs)) return set_err(KAD_ERR_INVALID, "NULL argument");
+    if (addr_len != KAD_ADDR4_LEN && addr_len != KAD_ADDR6_LEN)
+        return set_err(KAD_ERR_INVALID, "addr_len %u: 6 (in_addr + port) or 18 (in6_addr + port)", addr_len);
+    DeviceGuard g(t->device);
+    if (t->addr && t->addr_len != addr_len) return set_err(KAD_ERR_INVALID, "address length changed");
+    int rc;
+    if (!t->addr && (rc = dev_upload(&t->addr, nullptr, (size_t)addr_len * t->d.n, t->owned, t->bytes))) return rc;
+    t->addr_len = addr_len;
+    if (t->d.n) HIP_TRY(hipMemcpy(t->addr, addrs, (size_t)addr_len * t->d.n, hipMemcpyHostToDevice));
+    return KAD_OK;
+}
+
+int kad_buffer_nodes_batch(const kad_table* t, const uint8_t* targets, uint32_t q, const uint32_t* idx,
+                           const uint8_t* cnt, uint32_t k, uint8_t* out, uint8_t* out_n, void* stream) {
+    if (!t) return set_err(KAD_ERR_INVALID, "NULL table");
+    if (!t->addr) return set_err(KAD_ERR_INVALID, "kad_table_set_addrs was not called");
+    if (q == 0) return KAD_OK;
+    if (!targets || (!idx && k) || !out) return set_err(KAD_ERR_INVALID, "NULL buffer");
+    DeviceGuard g(t->device);
+    hipLaunchKernelGGL(buffer_nodes_kernel, dim3(grid_for(q)), dim3(BLOCK), 0, (hipStream_t)stream, t->d, t->addr,
+                       t->addr_len, targets, q, idx, cnt, k, out, out_n);
+    HIP_TRY(hipGetLastError());
+    return KAD_OK;
+}
+
+int kad_parse_nodes_batch(const uint8_t* records, uint32_t n, uint32_t rec_len, const uint8_t* myid, uint8_t* keep,
+                          int device, void* stream) {
+    if (rec_len != KAD_NODE4_INFO_LEN && rec_len != KAD_NODE6_INFO_LEN)
+        return set_err(KAD_ERR_INVALID, "rec_len %u: 26 or 38", rec_len);
+    if (n == 0) return KAD_OK;
+    if (!records || !myid || !keep) return set_err(KAD_ERR_INVALID, "NULL buffer");
+    Id20 me;
+    std::memcpy(me.b, myid, KAD_HASH_LEN);
+    DeviceGuard g(device);
+    hipLaunchKernelGGL(parse_nodes_kernel, dim3(grid_for(n)), dim3(BLOCK), 0, (hipStream_t)stream, records, n, rec_len,
+                       me, keep);
     HIP_TRY(hipGetLastError());
     return KAD_OK;
 }

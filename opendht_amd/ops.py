@@ -40,3 +40,17 @@ def lowbit(a):
     out = torch.empty((n,), dtype=torch.int32, device=a.device)
     check(lib().kad_lowbit_batch(ptr(a), n, ptr(out), _stream(a)), "kad_lowbit_batch")
     return out
+
+
+def parse_nodes(records, rec_len: int, myid: bytes):
+    """NetworkEngine::deserializeNodes' filter (network_engine.cpp:788-828) over a device tensor of
+    packed 26- or 38-byte node records: keep flags (uint8), 0 for our own ID or a martian address."""
+    import numpy as np
+    import torch
+
+    n = records.numel() // rec_len
+    keep = torch.empty((n,), dtype=torch.uint8, device=records.device)
+    me = np.frombuffer(bytes(myid), dtype=np.uint8).copy()
+    check(lib().kad_parse_nodes_batch(ptr(records), n, rec_len, ptr(me), ptr(keep), records.device.index or 0,
+                                      _stream(records)), "kad_parse_nodes_batch")
+    return keep

@@ -109,6 +109,28 @@ class DeviceTable:
         check(lib().kad_table_refresh_status(self._h, C.c_int64(now_ns), _stream_of(self, stream)),
               "kad_table_refresh_status")
 
+    def set_addrs(self, addrs) -> None:
+        """Node address records (n, 6) for IPv4 (in_addr + port bytes) or (n, 18) for IPv6."""
+        addrs = np.ascontiguousarray(addrs, dtype=np.uint8)
+        if addrs.ndim != 2 or addrs.shape[0] != self.n or addrs.shape[1] not in (6, 18):
+            raise ValueError(f"addrs must be (n, 6) or (n, 18) uint8, got {addrs.shape}")
+        check(lib().kad_table_set_addrs(self._h, addrs.shape[1], ptr(addrs)), "kad_table_set_addrs")
+        self.addr_len = addrs.shape[1]
+
+    def buffer_nodes(self, targets, idx, cnt=None, stream=None):
+        """NetworkEngine::bufferNodes per query (network_engine.cpp:942-974) over device tensors: the
+        candidates of row i of idx (cnt[i] of them, or up to the first KAD_NO_NODE) sorted by XOR
+        distance, the first 8 packed as 26- / 38-byte records. Returns (out (q, 8 * rec) uint8, n (q,))."""
+        import torch
+
+        q, k = idx.shape
+        rec = 20 + self.addr_len
+        out = torch.zeros((q, 8 * rec), dtype=torch.uint8, device=targets.device)
+        n = torch.empty((q,), dtype=torch.uint8, device=targets.device)
+        check(lib().kad_buffer_nodes_batch(self._h, ptr(targets), q, ptr(idx), ptr(cnt), k, ptr(out), ptr(n),
+                                           _stream_of(self, stream)), "kad_buffer_nodes_batch")
+        return out, n
+
     # -- device-pointer batch queries (torch tensors on this table's device) ---------------
     def rt_closest(self, targets, count: int, out_idx=None, out_cnt=None, stream=None):
         """RoutingTable::findClosestNodes over a (q, 20) uint8 device tensor of targets.

@@ -532,4 +532,59 @@ int orc_split_table(uint32_t n, const uint8_t* ids, uint32_t cap, uint32_t* out_
     return 0;
 }
 
+// ---------------------------------------------------------------------------
+// Wire step after the query
+// ---------------------------------------------------------------------------
+// NetworkEngine::bufferNodes(af, id, nodes) (src/network_engine.cpp:942-974): std::sort of the
+// nodes by id.xorCmp (:945-947), truncation to SEND_NODES = 8 (:59, :948), then per node the
+// 20-byte ID followed by sin_addr (4 bytes) + sin_port (2 bytes) for AF_INET (26-byte records,
+// :950-960) or sin6_addr (16) + sin6_port (2) for AF_INET6 (38-byte records, :961-971).
+// addr: per node addr_len = 6 or 18 bytes (address then port bytes, as stored in the sockaddr).
+// Rows: q queries, candidate list idx[i*k .. i*k + cnt[i]) (node indices); out: q x 8 records.
+uint32_t orc_buffer_nodes(uint32_t q, const uint8_t* targets, const uint8_t* ids, const uint8_t* addr,
+                          uint32_t addr_len, const uint32_t* idx, const uint8_t* cnt, uint32_t k, uint8_t* out,
+                          uint8_t* out_n) {
+    const uint32_t rec = HASH_LEN + addr_len;
+    for (uint32_t i = 0; i < q; i++) {
+        const Id t(targets + (size_t)HASH_LEN * i);
+        std::vector<uint32_t> nodes(idx + (size_t)i * k, idx + (size_t)i * k + cnt[i]);
+        std::sort(nodes.begin(), nodes.end(), [&](uint32_t a, uint32_t b) {
+            return t.xorCmp(Id(ids + (size_t)HASH_LEN * a), Id(ids + (size_t)HASH_LEN * b)) < 0;
+        });
+        const uint32_t nn = std::min<uint32_t>(8, (uint32_t)nodes.size());
+        uint8_t* dst = out + (size_t)i * 8 * rec;
+        for (uint32_t j = 0; j < nn; j++) {
+            std::memcpy(dst + j * rec, ids + (size_t)HASH_LEN * nodes[j], HASH_LEN);
+            std::memcpy(dst + j * rec + HASH_LEN, addr + (size_t)addr_len * nodes[j], addr_len);
+        }
+        out_n[i] = (uint8_t)nn;
+    }
+    return 0;
+}
+
+// NetworkEngine::isMartian (src/network_engine.cpp:308-339) on a 6-byte (v4) / 18-byte (v6)
+// address + port record; v4prefix = ::ffff:0:0/96 (:55-57).
+int orc_is_martian(const uint8_t* a, uint32_t addr_len) {
+    if (addr_len == 6) {
+        const bool port0 = a[4] == 0 && a[5] == 0;
+        return port0 || a[0] == 0 || a[0] == 127 || (a[0] & 0xE0) == 0xE0;
+    }
+    static const uint8_t v4prefix[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0xFF, 0xFF};
+    static const uint8_t z[15] = {0};
+    const bool port0 = a[16] == 0 && a[17] == 0;
+    return port0 || a[0] == 0xFF || (a[0] == 0xFE && (a[1] & 0xC0) == 0x80) ||
+           (std::memcmp(a, z, 15) == 0 && (a[15] == 0 || a[15] == 1)) || std::memcmp(a, v4prefix, 12) == 0;
+}
+
+// NetworkEngine::deserializeNodes (src/network_engine.cpp:788-828) up to the table insertion:
+// records of rec_len = 26 / 38 bytes, keep[i] = 0 for the sender's own ID (:798-799) or a martian
+// address (:806, :822). (The blacklist and cache.getNode / onNewNode are host state.)
+int orc_parse_nodes(uint32_t n, const uint8_t* in, uint32_t rec_len, const uint8_t* myid, uint8_t* keep) {
+    for (uint32_t i = 0; i < n; i++) {
+        const uint8_t* r = in + (size_t)rec_len * i;
+        keep[i] = !(std::memcmp(r, myid, HASH_LEN) == 0 || orc_is_martian(r + HASH_LEN, rec_len - HASH_LEN));
+    }
+    return 0;
+}
+
 }  // extern "C"

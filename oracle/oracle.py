@@ -37,6 +37,9 @@ _SIG = {
     "orc_flat_rt_bytes": (C.c_uint64, [C.c_uint32, _P, _P, C.c_uint32, _P, _P, C.c_uint32, _P, C.c_uint32,
                                        C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     "orc_split_table": (C.c_int, [C.c_uint32, _P, C.c_uint32, _P, _P, _P, _P]),
+    "orc_buffer_nodes": (C.c_uint32, [C.c_uint32, _P, _P, _P, C.c_uint32, _P, _P, C.c_uint32, _P, _P]),
+    "orc_is_martian": (C.c_int, [_P, C.c_uint32]),
+    "orc_parse_nodes": (C.c_int, [C.c_uint32, _P, C.c_uint32, _P, _P]),
 }
 _lib = None
 
@@ -189,3 +192,26 @@ def rt_algorithmic_bytes(ids, status, bucket_first, bucket_offset, targets, coun
     tot = lib().orc_flat_rt_bytes(ids.shape[0], _p(ids), _p(st), f.shape[0], _p(f), _p(off), t.shape[0],
                                   _p(t), count, C.byref(sb), C.byref(sn), C.byref(sg))
     return int(tot), sb.value, sn.value, sg.value
+
+
+def buffer_nodes(targets, ids, addrs, idx, cnt):
+    """NetworkEngine::bufferNodes per query (network_engine.cpp:942-974): (q, 8*rec) bytes, (q,) counts."""
+    t, ids = _ids(targets), _ids(ids)
+    addrs = np.ascontiguousarray(addrs, dtype=np.uint8)
+    idx = np.ascontiguousarray(idx, dtype=np.uint32)
+    cnt = np.ascontiguousarray(cnt, dtype=np.uint8)
+    q, k = idx.shape
+    al = addrs.shape[1]
+    out = np.zeros((q, 8 * (20 + al)), dtype=np.uint8)
+    n = np.zeros((q,), dtype=np.uint8)
+    lib().orc_buffer_nodes(q, _p(t), _p(ids), _p(addrs), al, _p(idx), _p(cnt), k, _p(out), _p(n))
+    return out, n
+
+
+def parse_nodes(records, rec_len, myid):
+    """deserializeNodes' filter (network_engine.cpp:788-828): keep flags per record."""
+    rec = np.ascontiguousarray(records, dtype=np.uint8).reshape(-1, rec_len)
+    my = np.ascontiguousarray(myid, dtype=np.uint8)
+    keep = np.zeros((rec.shape[0],), dtype=np.uint8)
+    lib().orc_parse_nodes(rec.shape[0], _p(rec), rec_len, _p(my), _p(keep))
+    return keep
