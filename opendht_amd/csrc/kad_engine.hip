@@ -833,6 +833,38 @@ __global__ __launch_bounds__(BLOCK) void rt_closest_dual_kernel(DevTable T4, Dev
     exact_tail(T6, t, ex && six, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
 }
 
+// Dual-family batch for count <= 8 where a family has window lines: per lane the family's table,
+// its window line when it has lines, the lane fast path otherwise, then the exact path per family.
+__global__ __launch_bounds__(BLOCK) void rt_dual_wl_kernel(DevTable T4, DevTable T6, const uint8_t* __restrict__ targets,
+                                                           const uint8_t* __restrict__ af, uint32_t q, uint32_t count,
+                                                           uint32_t* __restrict__ out_idx, uint8_t* __restrict__ out_cnt) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    const bool act = i < q && count > 0;
+    if (i < q && count == 0 && out_cnt) out_cnt[i] = 0;
+    Target t{};
+    bool six = false;
+    if (act) {
+        t = load_target(targets, i);
+        six = af[i] != 0;
+    }
+    const DevTable& T = six ? T6 : T4;
+    const bool wl = act && (T.flags & TF_WL);
+    const uint32_t b = wl ? locate_bucket(T, t) : 0u;
+    uint32_t o[8], m;
+    const bool ok = wl_answer<0>(T, t, b, count, wl, o, m);
+    uint32_t* row = out_idx + (size_t)i * count;
+    bool ex = wl && !ok;
+    if (wl && ok) {
+        store_row8(row, o, count);
+        if (out_cnt) out_cnt[i] = (uint8_t)m;
+    } else if (act && !wl) {
+        ex = !rt_query_fast<8, 3>(T, t, count, row, out_cnt ? out_cnt + i : nullptr);
+    }
+    __shared__ uint64_t xs[BLOCK / 64][192];
+    exact_tail(T4, t, ex && !six, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
+    exact_tail(T6, t, ex && six, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
+}
+
 // ---------------------------------------------------------------------------------------
 // Sharded table without halo: the north-star multi-GPU variant.
 // The global uniform-depth table is cut into contiguous bucket ranges, one per GPU. Every rank
@@ -1802,7 +1834,10 @@ int kad_rt_closest_batch_dual(const kad_table* t4, const kad_table* t6, const ui
     const DevTable& d6 = t6 ? t6->d : empty;
     DeviceGuard g(t4 ? t4->device : t6->device);
     hipStream_t s = (hipStream_t)stream;
-    if (count <= 8) launch_rt_dual<8>(d4, d6, targets, af, q, count, out_idx, out_cnt, s);
+    if (count <= 8 && ((d4.flags | d6.flags) & TF_WL))
+        hipLaunchKernelGGL(rt_dual_wl_kernel, dim3(grid_for(q)), dim3(BLOCK), 0, s, d4, d6, targets, af, q, count,
+                           out_idx, out_cnt);
+    else if (count <= 8) launch_rt_dual<8>(d4, d6, targets, af, q, count, out_idx, out_cnt, s);
     else if (count <= 16) launch_rt_dual<16>(d4, d6, targets, af, q, count, out_idx, out_cnt, s);
     else launch_rt_dual<32>(d4, d6, targets, af, q, count, out_idx, out_cnt, s);
     HIP_TRY(hipGetLastError());
