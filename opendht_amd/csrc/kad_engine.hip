@@ -1064,64 +1064,94 @@ __global__ void merge_parts_kernel(const uint32_t* __restrict__ parts, uint32_t 
 // ---------------------------------------------------------------------------------------
 constexpr uint32_t SEND_NODES = 8;
 
-__global__ __launch_bounds__(BLOCK) void buffer_nodes_kernel(DevTable T, const uint8_t* __restrict__ addr,
-                                                             uint32_t al, const uint8_t* __restrict__ targets,
-                                                             uint32_t q, const uint32_t* __restrict__ idx,
+// Per-node wire records, built once by kad_table_set_addrs: the node's 20-byte ID then its address
+// + port bytes, padded to WREC4 = 32 / WREC6 = 48 bytes so a record is two or three aligned 16-byte
+// loads. A query's candidates (one window of adjacent nodes) share a few lines of this array.
+constexpr uint32_t WREC4 = 32, WREC6 = 48;
+
+__global__ void wrec_build_kernel(const uint64_t* key, const uint32_t* tail, const uint8_t* addr, uint32_t al,
+                                  uint32_t n, uint32_t* wrec) {
+    const uint32_t v = blockIdx.x * BLOCK + threadIdx.x;
+    if (v >= n) return;
+    const uint32_t words = (al == KAD_ADDR4_LEN ? WREC4 : WREC6) / 4;
+    uint32_t w[WREC6 / 4] = {0};
+    const uint64_t k = key[v];
+    w[0] = __builtin_bswap32((uint32_t)(k >> 32));
+    w[1] = __builtin_bswap32((uint32_t)k);
+    for (int x = 0; x < 3; x++) w[2 + x] = __builtin_bswap32(tail[3ull * v + x]);
+    for (uint32_t b = 0; b < al; b++) w[(KAD_HASH_LEN + b) >> 2] |= (uint32_t)addr[(size_t)al * v + b] << (8 * (b & 3));
+    for (uint32_t x = 0; x < words; x++) wrec[(size_t)words * v + x] = w[x];
+}
+
+// P lanes per query (P = the candidate count rounded up to a power of two, 8..32): lane j loads
+// candidate j's wire record, ranks it against the other candidates of its query by the exact 160-bit
+// XOR distance (shuffles within the segment; ties keep input order), and the 8 best write their
+// records at byte rank * REC of the query's row in LDS; the block's rows, contiguous in `out`, then
+// leave as coalesced 16-byte stores.
+template <uint32_t AL, uint32_t P>
+__global__ __launch_bounds__(BLOCK) void buffer_nodes_kernel(uint32_t n_nodes, uint32_t index_base,
+                                                             const uint4* __restrict__ wrec,
+                                                             const uint8_t* __restrict__ targets, uint32_t q,
+                                                             const uint32_t* __restrict__ idx,
                                                              const uint8_t* __restrict__ cnt, uint32_t k,
                                                              uint8_t* __restrict__ out, uint8_t* __restrict__ out_n) {
-    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
-    if (i >= q) return;
-    const Target t = load_target(targets, i);
-    const uint32_t* row = idx + (size_t)i * k;
-    uint32_t n = cnt ? min((uint32_t)cnt[i], k) : k;
-    uint64_t L0[SEND_NODES], L1[SEND_NODES];
-    uint32_t L2[SEND_NODES], LN[SEND_NODES];
-    uint32_t nl = 0;
+    constexpr uint32_t RQ = (AL == KAD_ADDR4_LEN ? WREC4 : WREC6) / 16;  // 16-byte pieces per record
+    constexpr uint32_t REC = KAD_HASH_LEN + AL;                          // 26 / 38 bytes
+    constexpr uint32_t ROW = SEND_NODES * REC;                           // 208 / 304 bytes
+    constexpr uint32_t QB = BLOCK / P;                                   // queries per block
+    __shared__ uint4 rows[QB * ROW / 16];
+    const uint32_t tid = threadIdx.x, ql = tid / P, j = tid % P;
+    const uint32_t q0 = blockIdx.x * QB, qi = q0 + ql;
+    const uint32_t nq = min(QB, q - q0);
+    for (uint32_t x = tid; x < nq * ROW / 16; x += BLOCK) rows[x] = make_uint4(0, 0, 0, 0);
+    bool valid = false;
+    uint32_t r[RQ * 4];
+    uint64_t d0 = ~0ull, d1 = ~0ull;
+    uint32_t d2 = NONE;
+    if (qi < q) {
+        const uint32_t n = cnt ? min((uint32_t)cnt[qi], k) : k;
+        const uint32_t g = j < n ? idx[(size_t)qi * k + j] : NONE;
+        const uint32_t v = g - index_base;
+        valid = j < n && g != NONE && v < n_nodes;
+        if (valid) {
+            const Target t = load_target(targets, qi);
 #pragma unroll
-    for (int s = 0; s < (int)SEND_NODES; s++) { L0[s] = ~0ull; L1[s] = ~0ull; L2[s] = NONE; LN[s] = NONE; }
-    for (uint32_t j = 0; j < n; j++) {
-        const uint32_t g = row[j];
-        if (!cnt && g == NONE) break;
-        const uint32_t v = g - T.index_base;
-        if (v >= T.n) continue;  // not a node of this table
-        const uint32_t* tl = T.tail + 3ull * v;
-        uint64_t c0 = T.key[v] ^ t.hi, c1 = ((uint64_t)(tl[0] ^ t.t2) << 32) | (tl[1] ^ t.t3);
-        uint32_t c2 = tl[2] ^ t.t4, cn = v;
-        bool sh = false;
-#pragma unroll
-        for (int s = 0; s < (int)SEND_NODES; s++) {  // insertion: strictly smaller moves ahead
-            const bool lt = sh || (uint32_t)s >= nl || c0 < L0[s] ||
-                            (c0 == L0[s] && (c1 < L1[s] || (c1 == L1[s] && c2 < L2[s])));
-            sh = lt;
-            const uint64_t n0 = lt ? L0[s] : c0, n1 = lt ? L1[s] : c1;
-            const uint32_t n2 = lt ? L2[s] : c2, nn = lt ? LN[s] : cn;
-            L0[s] = lt ? c0 : L0[s];
-            L1[s] = lt ? c1 : L1[s];
-            L2[s] = lt ? c2 : L2[s];
-            LN[s] = lt ? cn : LN[s];
-            c0 = n0; c1 = n1; c2 = n2; cn = nn;
+            for (int x = 0; x < (int)RQ; x++) {
+                const uint4 p = wrec[(size_t)RQ * v + x];
+                r[4 * x] = p.x; r[4 * x + 1] = p.y; r[4 * x + 2] = p.z; r[4 * x + 3] = p.w;
+            }
+            d0 = (((uint64_t)__builtin_bswap32(r[0]) << 32) | __builtin_bswap32(r[1])) ^ t.hi;
+            d1 = ((uint64_t)(__builtin_bswap32(r[2]) ^ t.t2) << 32) | (__builtin_bswap32(r[3]) ^ t.t3);
+            d2 = __builtin_bswap32(r[4]) ^ t.t4;
         }
-        nl = min(nl + 1, SEND_NODES);
     }
-    const uint32_t rec = KAD_HASH_LEN + al;
-    uint8_t* dst = out + (size_t)i * SEND_NODES * rec;
-#pragma unroll
-    for (int s = 0; s < (int)SEND_NODES; s++) {
-        if ((uint32_t)s >= nl) break;
-        const uint32_t v = LN[s];
-        uint8_t* d = dst + s * rec;
-        const uint64_t key = T.key[v];
-        const uint32_t* tl = T.tail + 3ull * v;
-#pragma unroll
-        for (int b = 0; b < 8; b++) d[b] = (uint8_t)(key >> (56 - 8 * b));
-#pragma unroll
-        for (int w = 0; w < 3; w++)
-#pragma unroll
-            for (int b = 0; b < 4; b++) d[8 + 4 * w + b] = (uint8_t)(tl[w] >> (24 - 8 * b));
-        const uint8_t* a = addr + (size_t)al * v;
-        for (uint32_t b = 0; b < al; b++) d[KAD_HASH_LEN + b] = a[b];
+    // rank within the segment of P lanes (invalid lanes sort last and never count)
+    const uint64_t vm = __ballot(valid);
+    const uint32_t seg = (tid & 63u) & ~(P - 1);
+    uint32_t rank = 0;
+#pragma unroll 4
+    for (uint32_t p = 0; p < P; p++) {
+        const int src = (int)(seg + p);
+        const uint64_t e0 = ((uint64_t)(uint32_t)__shfl((int)(d0 >> 32), src, 64) << 32) | (uint32_t)__shfl((int)d0, src, 64);
+        const uint64_t e1 = ((uint64_t)(uint32_t)__shfl((int)(d1 >> 32), src, 64) << 32) | (uint32_t)__shfl((int)d1, src, 64);
+        const uint32_t e2 = (uint32_t)__shfl((int)d2, src, 64);
+        const bool ev = (vm >> src) & 1ull;
+        const bool less = e0 < d0 || (e0 == d0 && (e1 < d1 || (e1 == d1 && (e2 < d2 || (e2 == d2 && p < j)))));
+        rank += ev && less;
     }
-    if (out_n) out_n[i] = (uint8_t)nl;
+    __syncthreads();  // zero fill done
+    if (valid && rank < SEND_NODES) {
+        uint16_t* dst = reinterpret_cast<uint16_t*>(reinterpret_cast<uint8_t*>(rows) + ql * ROW + rank * REC);
+#pragma unroll
+        for (int h = 0; h < (int)REC / 2; h++) dst[h] = (uint16_t)(r[h >> 1] >> (16 * (h & 1)));
+    }
+    if (j == 0 && qi < q && out_n) {
+        const uint32_t segm = (uint32_t)((vm >> seg) & (P == 64 ? ~0ull : ((1ull << P) - 1)));
+        out_n[qi] = (uint8_t)min((uint32_t)__builtin_popcount(segm), SEND_NODES);
+    }
+    __syncthreads();
+    uint4* dst = reinterpret_cast<uint4*>(out + (size_t)q0 * ROW);
+    for (uint32_t x = tid; x < nq * ROW / 16; x += BLOCK) dst[x] = rows[x];
 }
 
 // NetworkEngine::isMartian (network_engine.cpp:308-339) on address + port bytes; v4prefix = ::ffff:0:0/96.
@@ -1449,7 +1479,7 @@ struct kad_table {
     uint2* dir_mut = nullptr;
     uint32_t* gpre_mut = nullptr;
     uint32_t* wl_mut = nullptr;
-    uint8_t* addr = nullptr;  // node address + port records (kad_table_set_addrs)
+    uint32_t* wrec = nullptr;  // per-node wire records: ID + address + port (kad_table_set_addrs)
     uint32_t addr_len = 0;
     int64_t* time_ns = nullptr;
     int64_t* reply_ns = nullptr;
@@ -1922,23 +1952,51 @@ int kad_table_set_addrs(kad_table* t, uint32_t addr_len, const uint8_t* addrs) {
     if (addr_len != KAD_ADDR4_LEN && addr_len != KAD_ADDR6_LEN)
         return set_err(KAD_ERR_INVALID, "addr_len %u: 6 (in_addr + port) or 18 (in6_addr + port)", addr_len);
     DeviceGuard g(t->device);
-    if (t->addr && t->addr_len != addr_len) return set_err(KAD_ERR_INVALID, "address length changed");
+    if (t->wrec && t->addr_len != addr_len) return set_err(KAD_ERR_INVALID, "address length changed");
+    const uint32_t rec = addr_len == KAD_ADDR4_LEN ? WREC4 : WREC6;
     int rc;
-    if (!t->addr && (rc = dev_upload(&t->addr, nullptr, (size_t)addr_len * t->d.n, t->owned, t->bytes))) return rc;
+    if (!t->wrec && (rc = dev_upload(&t->wrec, nullptr, (size_t)rec / 4 * t->d.n + 4, t->owned, t->bytes))) return rc;
     t->addr_len = addr_len;
-    if (t->d.n) HIP_TRY(hipMemcpy(t->addr, addrs, (size_t)addr_len * t->d.n, hipMemcpyHostToDevice));
+    if (t->d.n) {
+        uint8_t* da = nullptr;
+        HIP_TRY(hipMalloc(&da, (size_t)addr_len * t->d.n));
+        hipError_t e = hipMemcpy(da, addrs, (size_t)addr_len * t->d.n, hipMemcpyHostToDevice);
+        if (e == hipSuccess) {
+            hipLaunchKernelGGL(wrec_build_kernel, dim3(grid_for(t->d.n)), dim3(BLOCK), 0, 0, t->d.key, t->d.tail, da,
+                               addr_len, t->d.n, t->wrec);
+            e = hipGetLastError();
+            if (e == hipSuccess) e = hipDeviceSynchronize();
+        }
+        (void)hipFree(da);
+        if (e != hipSuccess) return set_err(KAD_ERR_HIP, "wire record build failed: %s", hipGetErrorString(e));
+    }
     return KAD_OK;
 }
 
 int kad_buffer_nodes_batch(const kad_table* t, const uint8_t* targets, uint32_t q, const uint32_t* idx,
                            const uint8_t* cnt, uint32_t k, uint8_t* out, uint8_t* out_n, void* stream) {
     if (!t) return set_err(KAD_ERR_INVALID, "NULL table");
-    if (!t->addr) return set_err(KAD_ERR_INVALID, "kad_table_set_addrs was not called");
+    if (!t->wrec) return set_err(KAD_ERR_INVALID, "kad_table_set_addrs was not called");
     if (q == 0) return KAD_OK;
     if (!targets || (!idx && k) || !out) return set_err(KAD_ERR_INVALID, "NULL buffer");
+    if (((uintptr_t)out & 15u) != 0) return set_err(KAD_ERR_INVALID, "out must be 16-byte aligned");
     DeviceGuard g(t->device);
-    hipLaunchKernelGGL(buffer_nodes_kernel, dim3(grid_for(q)), dim3(BLOCK), 0, (hipStream_t)stream, t->d, t->addr,
-                       t->addr_len, targets, q, idx, cnt, k, out, out_n);
+    const uint4* w = reinterpret_cast<const uint4*>(t->wrec);
+    if (k > KAD_MAX_COUNT) return set_err(KAD_ERR_UNSUPPORTED, "k %u > KAD_MAX_COUNT", k);
+    hipStream_t st = (hipStream_t)stream;
+#define KAD_BUF_LAUNCH(AL, P)                                                                                      \
+    hipLaunchKernelGGL((buffer_nodes_kernel<AL, P>), dim3((q + BLOCK / P - 1) / (BLOCK / P)), dim3(BLOCK), 0, st, \
+                       t->d.n, t->d.index_base, w, targets, q, idx, cnt, k, out, out_n)
+    if (t->addr_len == KAD_ADDR4_LEN) {
+        if (k <= 8) KAD_BUF_LAUNCH(KAD_ADDR4_LEN, 8);
+        else if (k <= 16) KAD_BUF_LAUNCH(KAD_ADDR4_LEN, 16);
+        else KAD_BUF_LAUNCH(KAD_ADDR4_LEN, 32);
+    } else {
+        if (k <= 8) KAD_BUF_LAUNCH(KAD_ADDR6_LEN, 8);
+        else if (k <= 16) KAD_BUF_LAUNCH(KAD_ADDR6_LEN, 16);
+        else KAD_BUF_LAUNCH(KAD_ADDR6_LEN, 32);
+    }
+#undef KAD_BUF_LAUNCH
     HIP_TRY(hipGetLastError());
     return KAD_OK;
 }
