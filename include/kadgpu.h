@@ -221,6 +221,40 @@ int kad_buffer_nodes_batch(const kad_table* t, const uint8_t* targets, uint32_t 
 int kad_parse_nodes_batch(const uint8_t* records, uint32_t n, uint32_t rec_len, const uint8_t* myid,
                           uint8_t* keep, int device, void* stream);
 
+/* ---- config 5: simulated swarm, iterative lookups ----
+ * BUILD-DEFINED model (kad_swarm.hip header): n peers with shape-K routing tables (Dht::onNewNode
+ * policy, dht.cpp:867-936) built on the device; lookups run synchronous hops of
+ * MAX_REQUESTED_SEARCH_NODES = 4 findClosestNodes(t, 8) answers merged by Search::insertNode
+ * (dht.cpp:961-1047) into a SEARCH_NODES = 14 list, until its first 8 nodes have been queried. */
+#define KAD_SWARM_LEVELS 28u        /* bucket levels per peer table (depth <= 27) */
+#define KAD_SEARCH_NODES_LEN 14u    /* dht.h:314 SEARCH_NODES */
+typedef struct kad_swarm kad_swarm;
+typedef struct kad_search kad_search;
+/* sorted_ids: host, n x 20 bytes, strictly ascending; peer index = position. */
+int kad_swarm_create(kad_swarm** out, int device, uint32_t n, const uint8_t* sorted_ids);
+int kad_swarm_destroy(kad_swarm* s);
+int kad_swarm_info(const kad_swarm* s, uint32_t* n_peers, uint64_t* device_bytes);
+/* Peer `peer`'s table (host outputs): depth D, counts[KAD_SWARM_LEVELS] per level (level D = my
+ * bucket), entries[KAD_SWARM_LEVELS][8] peer indices (KAD_NO_NODE padded). */
+int kad_swarm_get_table(const kad_swarm* s, uint32_t peer, uint32_t* depth, uint8_t* counts,
+                        uint32_t* entries);
+/* RoutingTable::findClosestNodes(targets[i], count) on peer peers[i]'s table (device pointers,
+ * count <= 16): out_idx q x count peer indices, out_cnt q. */
+int kad_swarm_closest_batch(const kad_swarm* s, const uint32_t* peers, const uint8_t* targets, uint32_t q,
+                            uint32_t count, uint32_t* out_idx, uint8_t* out_cnt, void* stream);
+/* S lookups (src peer, target); src/targets host or device. The initial list is the source's
+ * findClosestNodes(t, 14); asynchronous on `stream`. */
+int kad_search_create(kad_search** out, const kad_swarm* s, uint32_t S, const uint32_t* src,
+                      const uint8_t* targets, void* stream);
+/* One synchronous hop for every running lookup; *n_active (if given) = lookups still running
+ * after it (synchronises the stream). */
+int kad_search_hop(kad_search* x, uint32_t* n_active);
+/* Host outputs (any may be NULL): list S x 14 peer indices (KAD_NO_NODE padded), queried flags
+ * S x 14, list length S, hops S, done S (0 running, 1 first 8 queried, 2 stalled). */
+int kad_search_get(const kad_search* x, uint32_t* list, uint8_t* queried, uint8_t* n, uint32_t* hops,
+                   uint8_t* done);
+int kad_search_destroy(kad_search* x);
+
 /* ---- InfoHash primitives (infohash.h), batched, device pointers ---------- */
 /* out[i] = targets[i].xorCmp(a[i], b[i]) in {-1,0,1}   (infohash.h:131-146) */
 int kad_xor_cmp_batch(const uint8_t* targets, const uint8_t* a, const uint8_t* b, uint32_t n,

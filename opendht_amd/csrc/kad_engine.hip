@@ -1564,6 +1564,16 @@ int rt_dispatch(const kad_table* t, const uint8_t* targets, uint32_t q, uint32_t
 extern "C" {
 
 const char* kad_last_error(void) { return g_err.c_str(); }
+}  // extern "C"
+
+// Internal, for the other translation units of libkadgpu.so (kad_swarm.hip): the thread-local
+// error of kad_last_error() and the gfx950 check.
+namespace kadgpu_internal {
+int set_error(int code, const char* msg) { return set_err(code, "%s", msg); }
+bool device_ok(int dev) { return is_gfx950(dev); }
+}  // namespace kadgpu_internal
+
+extern "C" {
 int kad_version(void) { return KAD_VERSION; }
 
 int kad_device_count(int* out_n) {

@@ -1,0 +1,601 @@
+// kad_swarm.hip — config 5: a simulated swarm of n peers, each with its
+// own shape-K routing table in HBM, and synchronous-round iterative lookups over it.
+//
+// BUILD-DEFINED MODEL (the reference has no swarm simulator); parity is pinned per hop against the
+// oracle's restatement (oracle/kad_oracle.cpp "Config 5 swarm model"):
+//   * peer tables of shape K (Dht::onNewNode, dht.cpp:867-936: only my bucket splits, a full bucket
+//     caches newcomers away): peer p of top-64 key k has depth D = the least D with at most 8 other
+//     peers sharing >= D leading bits (capped at KAD_SWARM_LEVELS-1); level d < D holds min(8, |S_d|)
+//     peers of S_d (peers sharing exactly d bits) at positions lo + (off + j|S_d|/8) % |S_d|,
+//     off = mix(k ^ (d+1)*GOLDEN) % |S_d|; my bucket (level D) the first 8 other peers sharing >= D
+//     bits. All peers good.
+//   * a hop queries the first <= 4 unqueried nodes of a search's list (MAX_REQUESTED_SEARCH_NODES,
+//     dht.h:327); each answers RoutingTable::findClosestNodes(t, 8) (routing_table.cpp:67-111) from
+//     its own table; answers equal to the source are dropped (network_engine.cpp:798-799); the rest
+//     go through Search::insertNode (dht.cpp:961-1047: sorted insert, trim to SEARCH_NODES = 14).
+//     Done when the first min(8, |list|) nodes have been queried (Search::isSynced, dht.cpp:1467-1478);
+//     stalled when no unqueried node is left.
+//
+// HBM layout (n peers, L = KAD_SWARM_LEVELS levels, 8 entries per bucket):
+//   key[n] u64 (ID bits 0..63 of the sorted peer IDs), tail[n][3] u32 (bits 64..159, exact ties only)
+//   depth[n] u8, cnt[n][L] u8, ent[n][L][8] u32 (peer indices), ekey[n][L][8] u64 (their keys inline:
+//   one 64-byte line per bucket, so a window of buckets costs a few lines and no per-node gathers)
+// A peer's buckets sorted by `first` (the RoutingTable order) follow from k's bits: the levels whose
+// bit of k is 1 (their bucket lies below k) in ascending d, my bucket, then the levels whose bit is
+// 0 in descending d. The bucket holding a target is level commonBits(k, t) (or my bucket).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/kadgpu.h"
+
+namespace kadgpu_internal {
+int set_error(int code, const char* msg);
+bool device_ok(int dev);
+}  // namespace kadgpu_internal
+
+namespace {
+
+constexpr uint32_t NONE = 0xFFFFFFFFu;
+constexpr uint32_t L = KAD_SWARM_LEVELS;
+constexpr uint32_t BK = 8;   // TARGET_NODES per bucket
+constexpr uint32_t SN = 14;  // SEARCH_NODES (dht.h:314)
+constexpr uint32_t SNP = 16; // list stride
+constexpr uint32_t ALPHA = 4;
+constexpr int BLOCK = 256;
+
+int err(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    return kadgpu_internal::set_error(code, buf);
+}
+
+#define SW_TRY(expr)                                                                          \
+    do {                                                                                      \
+        hipError_t e_ = (expr);                                                               \
+        if (e_ != hipSuccess) return err(KAD_ERR_HIP, "%s: %s", #expr, hipGetErrorString(e_)); \
+    } while (0)
+
+inline uint32_t grid_for(uint64_t n) { return (uint32_t)((n + BLOCK - 1) / BLOCK); }
+
+struct SwarmDev {
+    const uint64_t* key;
+    const uint32_t* tail;
+    uint8_t* depth;
+    uint8_t* cnt;
+    uint32_t* ent;
+    uint64_t* ekey;
+    uint32_t n;
+};
+
+struct Tgt {
+    uint64_t hi;
+    uint32_t t2, t3, t4;
+};
+
+__device__ __forceinline__ Tgt load_tgt(const uint8_t* targets, uint32_t i) {
+    const uint32_t* p = reinterpret_cast<const uint32_t*>(targets + 20ull * i);
+    Tgt t;
+    t.hi = ((uint64_t)__builtin_bswap32(p[0]) << 32) | __builtin_bswap32(p[1]);
+    t.t2 = __builtin_bswap32(p[2]);
+    t.t3 = __builtin_bswap32(p[3]);
+    t.t4 = __builtin_bswap32(p[4]);
+    return t;
+}
+
+__device__ __forceinline__ uint64_t mix(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+__device__ __forceinline__ uint32_t lower_bound(const uint64_t* key, uint32_t n, uint64_t v) {
+    uint32_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (key[mid] < v) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+
+// peers whose key starts with the Lb-bit prefix P (Lb <= 63): [lo, hi)
+__device__ __forceinline__ void prefix_range(const SwarmDev& W, uint64_t P, uint32_t Lb, uint32_t& lo, uint32_t& hi) {
+    if (Lb == 0) { lo = 0; hi = W.n; return; }
+    lo = lower_bound(W.key, W.n, P << (64 - Lb));
+    hi = (P + 1 == (1ull << Lb)) ? W.n : lower_bound(W.key, W.n, (P + 1) << (64 - Lb));
+}
+
+// One thread per peer: depth, level buckets, my bucket (see the header).
+__global__ void swarm_build_kernel(SwarmDev W) {
+    const uint32_t p = blockIdx.x * BLOCK + threadIdx.x;
+    if (p >= W.n) return;
+    const uint64_t k = W.key[p];
+    uint32_t D = 0, lo = 0, hi = W.n;
+    for (;; D++) {
+        prefix_range(W, D ? k >> (64 - D) : 0ull, D, lo, hi);
+        if (hi - lo - 1 <= BK || D == L - 1) break;
+    }
+    W.depth[p] = (uint8_t)D;
+    uint8_t* cp = W.cnt + (size_t)p * L;
+    for (uint32_t d = 0; d < L; d++) cp[d] = 0;
+    for (uint32_t d = 0; d < D; d++) {
+        uint32_t a, e;
+        prefix_range(W, (k >> (63 - d)) ^ 1ull, d + 1, a, e);
+        const uint32_t m = e - a, c = min(m, BK);
+        const uint64_t off = m > BK ? mix(k ^ ((uint64_t)(d + 1) * 0x9E3779B97F4A7C15ull)) % m : 0ull;
+        uint32_t* ep = W.ent + ((size_t)p * L + d) * BK;
+        uint64_t* kp = W.ekey + ((size_t)p * L + d) * BK;
+        for (uint32_t j = 0; j < BK; j++) {
+            const uint32_t x = j < c ? (m > BK ? a + (uint32_t)((off + (uint64_t)j * m / BK) % m) : a + j) : NONE;
+            ep[j] = x;
+            kp[j] = x != NONE ? W.key[x] : ~0ull;
+        }
+        cp[d] = (uint8_t)c;
+    }
+    uint32_t* ep = W.ent + ((size_t)p * L + D) * BK;
+    uint64_t* kp = W.ekey + ((size_t)p * L + D) * BK;
+    uint32_t c = 0;
+    for (uint32_t x = lo; x < hi && c < BK; x++)
+        if (x != p) { ep[c] = x; kp[c] = W.key[x]; c++; }
+    for (uint32_t j = c; j < BK; j++) { ep[j] = NONE; kp[j] = ~0ull; }
+    cp[D] = (uint8_t)c;
+}
+
+// The i-th set bit (ascending) of m (i < popcount(m)).
+__device__ __forceinline__ uint32_t nth_bit(uint32_t m, uint32_t i) {
+    for (uint32_t k = 0; k < i; k++) m &= m - 1;
+    return (uint32_t)__builtin_ctz(m);
+}
+
+// Exact order of two candidates with equal top-64 distance: the 96-bit tail XOR the target's tail.
+__device__ __forceinline__ bool tail_less(const SwarmDev& W, const Tgt& t, uint32_t a, uint32_t b) {
+    const uint32_t* ta = W.tail + 3ull * a;
+    const uint32_t* tb = W.tail + 3ull * b;
+    const uint32_t a2 = ta[0] ^ t.t2, a3 = ta[1] ^ t.t3, a4 = ta[2] ^ t.t4;
+    const uint32_t b2 = tb[0] ^ t.t2, b3 = tb[1] ^ t.t3, b4 = tb[2] ^ t.t4;
+    if (a2 != b2) return a2 < b2;
+    if (a3 != b3) return a3 < b3;
+    return a4 < b4;
+}
+
+// RoutingTable::findClosestNodes(t, count) on peer p's table, count <= K. Writes the result's peer
+// indices and keys (sorted by XOR distance) and returns their number.
+template <uint32_t K>
+__device__ uint32_t peer_closest(const SwarmDev& W, uint32_t p, const Tgt& t, uint32_t count, uint32_t* oi, uint64_t* ok) {
+    const uint64_t k = W.key[p];
+    const uint32_t D = W.depth[p];
+    const uint8_t* cp = W.cnt + (size_t)p * L;
+    const uint32_t lv = (uint32_t)(__builtin_bitreverse64(k) & ((1ull << D) - 1));  // bit d = bit d of k from the top
+    const uint32_t m1 = lv, m0 = ~lv & (uint32_t)((1ull << D) - 1);
+    const uint32_t M = (uint32_t)__builtin_popcount(m1), B = D + 1;
+    // position of the target's bucket
+    const uint64_t x = k ^ t.hi;
+    const uint32_t c = x ? (uint32_t)__builtin_clzll(x) : 64u;
+    uint32_t b;
+    if (c >= D) b = M;
+    else if ((m1 >> c) & 1u) b = (uint32_t)__builtin_popcount(m1 & ((1u << c) - 1u));
+    else b = M + 1 + (uint32_t)__builtin_popcount(m0 & ~((2u << c) - 1u));
+    // level of a position
+    const uint32_t n0 = (uint32_t)__builtin_popcount(m0);
+    auto level = [&](uint32_t P) -> uint32_t {
+        if (P < M) return nth_bit(m1, P);
+        if (P == M) return D;
+        return nth_bit(m0, n0 - 1 - (P - M - 1));
+    };
+    // window rounds (routing_table.cpp:89-104)
+    uint32_t lo = b > 0 ? b - 1 : 0, hi = b, good = cp[level(b)] + (b > 0 ? cp[level(b - 1)] : 0u);
+    while (good < count && !(lo == 0 && hi == B - 1)) {
+        if (hi < B - 1) { hi++; good += cp[level(hi)]; }
+        if (lo > 0) { lo--; good += cp[level(lo)]; }
+    }
+    // top-count of the window's nodes by (XOR distance, insertion order)
+    uint64_t L0[K];
+    uint32_t LI[K];
+#pragma unroll
+    for (uint32_t s = 0; s < K; s++) { L0[s] = ~0ull; LI[s] = NONE; }
+    uint32_t nl = 0;
+    for (uint32_t P = lo; P <= hi; P++) {
+        const uint32_t d = level(P), nb = cp[d];
+        const uint32_t* ep = W.ent + ((size_t)p * L + d) * BK;
+        const uint64_t* kp = W.ekey + ((size_t)p * L + d) * BK;
+        for (uint32_t j = 0; j < nb; j++) {
+            uint64_t cd = kp[j] ^ t.hi;
+            uint32_t ci = ep[j];
+            bool sh = false;
+#pragma unroll
+            for (uint32_t s = 0; s < K; s++) {
+                const bool lt = sh || s >= nl || cd < L0[s] || (cd == L0[s] && tail_less(W, t, ci, LI[s]));
+                sh = lt;
+                const uint64_t n0_ = lt ? L0[s] : cd;
+                const uint32_t n1_ = lt ? LI[s] : ci;
+                if (lt) { L0[s] = cd; LI[s] = ci; }
+                cd = n0_;
+                ci = n1_;
+            }
+            nl = min(nl + 1, K);
+        }
+    }
+    const uint32_t m = min(nl, count);
+    for (uint32_t s = 0; s < m; s++) {
+        oi[s] = LI[s];
+        ok[s] = L0[s] ^ t.hi;
+    }
+    return m;
+}
+
+__global__ void swarm_closest_kernel(SwarmDev W, const uint32_t* peers, const uint8_t* targets, uint32_t q, uint32_t count,
+                                     uint32_t* out_idx, uint8_t* out_cnt) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= q) return;
+    uint32_t oi[SNP];
+    uint64_t ok[SNP];
+    const uint32_t p = peers[i];
+    const uint32_t m = p < W.n ? peer_closest<SNP>(W, p, load_tgt(targets, i), count, oi, ok) : 0u;
+    for (uint32_t s = 0; s < count; s++) out_idx[(size_t)i * count + s] = s < m ? oi[s] : NONE;
+    if (out_cnt) out_cnt[i] = (uint8_t)m;
+}
+
+// ---- search state ------------------------------------------------------------------------
+struct SearchDev {
+    const uint32_t* src;
+    const uint8_t* targets;
+    uint32_t* li;   // [S][SNP] list peer indices
+    uint64_t* lk;   // [S][SNP] their keys
+    uint8_t* lq;    // [S][SNP] queried
+    uint8_t* ln;    // [S] list length
+    uint32_t* hops; // [S]
+    uint8_t* done;  // [S] 0 running, 1 synced, 2 stalled
+    uint32_t* sel;  // [S][ALPHA] nodes queried this hop (NONE padded)
+    uint32_t* ri;   // [S][ALPHA][BK] answers
+    uint64_t* rk;
+    uint8_t* rn;    // [S][ALPHA]
+    uint32_t* active;
+    uint32_t S;
+};
+
+// first <= ALPHA unqueried nodes in list order -> sel, marked queried; none -> stalled
+__device__ __forceinline__ void select_next(const SearchDev& X, uint32_t s, uint32_t n, uint8_t* q, const uint32_t* li) {
+    uint32_t k = 0;
+    for (uint32_t j = 0; j < n && k < ALPHA; j++)
+        if (!q[j]) { X.sel[(size_t)s * ALPHA + k++] = li[j]; q[j] = 1; }
+    for (uint32_t j = k; j < ALPHA; j++) X.sel[(size_t)s * ALPHA + j] = NONE;
+    if (k == 0) X.done[s] = 2;
+}
+
+__global__ void search_init_kernel(SwarmDev W, SearchDev X) {
+    const uint32_t s = blockIdx.x * BLOCK + threadIdx.x;
+    if (s >= X.S) return;
+    uint32_t li[SNP];
+    uint64_t lk[SNP];
+    uint8_t q[SNP] = {0};
+    const uint32_t p = X.src[s];
+    const uint32_t n = p < W.n ? peer_closest<SNP>(W, p, load_tgt(X.targets, s), SN, li, lk) : 0u;
+    X.done[s] = n ? 0 : 2;
+    X.hops[s] = 0;
+    X.ln[s] = (uint8_t)n;
+    if (n) select_next(X, s, n, q, li);
+    for (uint32_t j = 0; j < SNP; j++) {
+        X.li[(size_t)s * SNP + j] = j < n ? li[j] : NONE;
+        X.lk[(size_t)s * SNP + j] = j < n ? lk[j] : ~0ull;
+        X.lq[(size_t)s * SNP + j] = j < n ? q[j] : 0;
+    }
+}
+
+// one lane per (search, queried node): its findClosestNodes(t, 8)
+__global__ void search_query_kernel(SwarmDev W, SearchDev X) {
+    const uint32_t g = blockIdx.x * BLOCK + threadIdx.x;
+    if (g >= X.S * ALPHA) return;
+    const uint32_t s = g / ALPHA;
+    const uint32_t v = X.done[s] ? NONE : X.sel[g];
+    uint32_t oi[BK];
+    uint64_t ok[BK];
+    const uint32_t m = v < W.n ? peer_closest<BK>(W, v, load_tgt(X.targets, s), BK, oi, ok) : 0u;
+    for (uint32_t j = 0; j < m; j++) {
+        X.ri[(size_t)g * BK + j] = oi[j];
+        X.rk[(size_t)g * BK + j] = ok[j];
+    }
+    X.rn[g] = (uint8_t)m;
+}
+
+// one lane per search: Search::insertNode of every answer (order-independent: the list ends as the
+// 14 closest distinct nodes), then the isSynced check and the next hop's selection
+__global__ void search_merge_kernel(SwarmDev W, SearchDev X) {
+    const uint32_t s = blockIdx.x * BLOCK + threadIdx.x;
+    bool running = false;
+    if (s < X.S && !X.done[s]) {
+        const Tgt t = load_tgt(X.targets, s);
+        uint32_t li[SNP];
+        uint64_t ld[SNP];  // top-64 XOR distances
+        uint8_t q[SNP];
+        uint32_t n = X.ln[s];
+        for (uint32_t j = 0; j < SNP; j++) {
+            li[j] = X.li[(size_t)s * SNP + j];
+            ld[j] = X.lk[(size_t)s * SNP + j] ^ t.hi;
+            q[j] = X.lq[(size_t)s * SNP + j];
+        }
+        const uint32_t src = X.src[s];
+        for (uint32_t a = 0; a < ALPHA; a++) {
+            const uint32_t g = s * ALPHA + a;
+            const uint32_t rn = X.rn[g];
+            for (uint32_t j = 0; j < rn; j++) {
+                const uint32_t r = X.ri[(size_t)g * BK + j];
+                if (r == src) continue;  // deserializeNodes drops our own ID (network_engine.cpp:798-799)
+                const uint64_t rd = X.rk[(size_t)g * BK + j] ^ t.hi;
+                bool found = false;
+                uint32_t pos = 0;  // nodes strictly closer than r
+                for (uint32_t k = 0; k < SN; k++) {
+                    if (k >= n) break;
+                    found |= li[k] == r;
+                    pos += ld[k] < rd || (ld[k] == rd && li[k] != r && tail_less(W, t, li[k], r));
+                }
+                if (found || (n >= SN && pos >= SN)) continue;
+                // insert at pos, shift the rest down, trim to SN
+                uint32_t ci = r;
+                uint64_t cd = rd;
+                uint8_t cq = 0;
+                for (uint32_t k = pos; k < SN; k++) {
+                    if (k > n) break;
+                    const uint32_t ti = li[k];
+                    const uint64_t td = ld[k];
+                    const uint8_t tq = q[k];
+                    li[k] = ci; ld[k] = cd; q[k] = cq;
+                    ci = ti; cd = td; cq = tq;
+                }
+                n = min(n + 1, SN);
+            }
+        }
+        X.hops[s] += 1;
+        bool synced = n > 0;
+        for (uint32_t j = 0; j < n && j < BK; j++) synced &= q[j] != 0;
+        if (synced) X.done[s] = 1;
+        else select_next(X, s, n, q, li);
+        X.ln[s] = (uint8_t)n;
+        for (uint32_t j = 0; j < SNP; j++) {
+            X.li[(size_t)s * SNP + j] = j < n ? li[j] : NONE;
+            X.lk[(size_t)s * SNP + j] = j < n ? ld[j] ^ t.hi : ~0ull;
+            X.lq[(size_t)s * SNP + j] = j < n ? q[j] : 0;
+        }
+        running = !X.done[s];
+    }
+    const uint64_t m = __ballot(running);
+    if ((threadIdx.x & 63u) == 0 && m) atomicAdd(X.active, (uint32_t)__builtin_popcountll(m));
+}
+
+}  // namespace
+
+struct kad_swarm {
+    int device = 0;
+    SwarmDev W{};
+    std::vector<void*> owned;
+    uint64_t bytes = 0;
+    ~kad_swarm() {
+        for (void* p : owned) (void)hipFree(p);
+    }
+};
+
+struct kad_search {
+    int device = 0;
+    const kad_swarm* sw = nullptr;
+    SearchDev X{};
+    hipStream_t stream = nullptr;
+    std::vector<void*> owned;
+    ~kad_search() {
+        for (void* p : owned) (void)hipFree(p);
+    }
+};
+
+namespace {
+template <class T>
+int alloc(T** p, size_t count, std::vector<void*>& owned, uint64_t* bytes = nullptr) {
+    void* q = nullptr;
+    const size_t nb = std::max<size_t>(count * sizeof(T), 16);
+    hipError_t e = hipMalloc(&q, nb);
+    if (e != hipSuccess) return err(KAD_ERR_NOMEM, "hipMalloc(%zu) failed: %s", nb, hipGetErrorString(e));
+    owned.push_back(q);
+    if (bytes) *bytes += nb;
+    *p = static_cast<T*>(q);
+    return KAD_OK;
+}
+
+struct Guard {
+    int prev = -1;
+    explicit Guard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~Guard() {
+        int cur;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+}  // namespace
+
+extern "C" {
+
+int kad_swarm_create(kad_swarm** out, int device, uint32_t n, const uint8_t* sorted_ids) {
+    if (!out || (n && !sorted_ids)) return err(KAD_ERR_INVALID, "NULL argument");
+    *out = nullptr;
+    if (n < 2) return err(KAD_ERR_INVALID, "a swarm needs at least 2 peers");
+    if (!kadgpu_internal::device_ok(device)) return err(KAD_ERR_NO_DEVICE, "device %d is not a gfx950 GPU", device);
+    std::vector<uint64_t> key(n);
+    std::vector<uint32_t> tail(3ull * n);
+    for (uint32_t i = 0; i < n; i++) {
+        const uint8_t* p = sorted_ids + 20ull * i;
+        uint64_t k = 0;
+        for (int b = 0; b < 8; b++) k = (k << 8) | p[b];
+        key[i] = k;
+        for (int w = 0; w < 3; w++)
+            tail[3ull * i + w] = ((uint32_t)p[8 + 4 * w] << 24) | ((uint32_t)p[9 + 4 * w] << 16) |
+                                 ((uint32_t)p[10 + 4 * w] << 8) | p[11 + 4 * w];
+        if (i && std::memcmp(sorted_ids + 20ull * (i - 1), p, 20) >= 0)
+            return err(KAD_ERR_INVALID, "peer IDs must be strictly ascending (index %u)", i);
+    }
+    Guard g(device);
+    kad_swarm* s = new kad_swarm;
+    s->device = device;
+    uint64_t* dk;
+    uint32_t* dt;
+    int rc;
+    if ((rc = alloc(&dk, n, s->owned, &s->bytes)) || (rc = alloc(&dt, 3ull * n, s->owned, &s->bytes)) ||
+        (rc = alloc(&s->W.depth, n, s->owned, &s->bytes)) || (rc = alloc(&s->W.cnt, (size_t)n * L, s->owned, &s->bytes)) ||
+        (rc = alloc(&s->W.ent, (size_t)n * L * BK, s->owned, &s->bytes)) ||
+        (rc = alloc(&s->W.ekey, (size_t)n * L * BK, s->owned, &s->bytes))) {
+        delete s;
+        return rc;
+    }
+    if (hipMemcpy(dk, key.data(), 8ull * n, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(dt, tail.data(), 12ull * n, hipMemcpyHostToDevice) != hipSuccess) {
+        delete s;
+        return err(KAD_ERR_HIP, "upload failed");
+    }
+    s->W.key = dk;
+    s->W.tail = dt;
+    s->W.n = n;
+    hipLaunchKernelGGL(swarm_build_kernel, dim3(grid_for(n)), dim3(BLOCK), 0, 0, s->W);
+    if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+        delete s;
+        return err(KAD_ERR_HIP, "swarm table build failed");
+    }
+    *out = s;
+    return KAD_OK;
+}
+
+int kad_swarm_destroy(kad_swarm* s) {
+    if (!s) return KAD_OK;
+    Guard g(s->device);
+    (void)hipDeviceSynchronize();
+    delete s;
+    return KAD_OK;
+}
+
+int kad_swarm_info(const kad_swarm* s, uint32_t* n_peers, uint64_t* device_bytes) {
+    if (!s) return err(KAD_ERR_INVALID, "NULL swarm");
+    if (n_peers) *n_peers = s->W.n;
+    if (device_bytes) *device_bytes = s->bytes;
+    return KAD_OK;
+}
+
+int kad_swarm_get_table(const kad_swarm* s, uint32_t peer, uint32_t* depth, uint8_t* counts, uint32_t* entries) {
+    if (!s || !depth || !counts || !entries) return err(KAD_ERR_INVALID, "NULL argument");
+    if (peer >= s->W.n) return err(KAD_ERR_INVALID, "peer %u >= %u", peer, s->W.n);
+    Guard g(s->device);
+    uint8_t d;
+    SW_TRY(hipMemcpy(&d, s->W.depth + peer, 1, hipMemcpyDeviceToHost));
+    SW_TRY(hipMemcpy(counts, s->W.cnt + (size_t)peer * L, L, hipMemcpyDeviceToHost));
+    SW_TRY(hipMemcpy(entries, s->W.ent + (size_t)peer * L * BK, 4ull * L * BK, hipMemcpyDeviceToHost));
+    *depth = d;
+    return KAD_OK;
+}
+
+int kad_swarm_closest_batch(const kad_swarm* s, const uint32_t* peers, const uint8_t* targets, uint32_t q,
+                            uint32_t count, uint32_t* out_idx, uint8_t* out_cnt, void* stream) {
+    if (!s) return err(KAD_ERR_INVALID, "NULL swarm");
+    if (count > SNP) return err(KAD_ERR_UNSUPPORTED, "count %u > %u", count, SNP);
+    if (q == 0) return KAD_OK;
+    if (!peers || !targets || !out_idx) return err(KAD_ERR_INVALID, "NULL buffer");
+    Guard g(s->device);
+    hipLaunchKernelGGL(swarm_closest_kernel, dim3(grid_for(q)), dim3(BLOCK), 0, (hipStream_t)stream, s->W, peers,
+                       targets, q, count, out_idx, out_cnt);
+    SW_TRY(hipGetLastError());
+    return KAD_OK;
+}
+
+int kad_search_create(kad_search** out, const kad_swarm* s, uint32_t S, const uint32_t* src, const uint8_t* targets,
+                      void* stream) {
+    if (!out || !s || (S && (!src || !targets))) return err(KAD_ERR_INVALID, "NULL argument");
+    *out = nullptr;
+    Guard g(s->device);
+    kad_search* x = new kad_search;
+    x->device = s->device;
+    x->sw = s;
+    x->stream = (hipStream_t)stream;
+    SearchDev& X = x->X;
+    X.S = S;
+    uint32_t* dsrc;
+    uint8_t* dt;
+    int rc;
+    if ((rc = alloc(&dsrc, S, x->owned)) || (rc = alloc(&dt, 20ull * S, x->owned)) ||
+        (rc = alloc(&X.li, (size_t)S * SNP, x->owned)) || (rc = alloc(&X.lk, (size_t)S * SNP, x->owned)) ||
+        (rc = alloc(&X.lq, (size_t)S * SNP, x->owned)) || (rc = alloc(&X.ln, S, x->owned)) ||
+        (rc = alloc(&X.hops, S, x->owned)) || (rc = alloc(&X.done, S, x->owned)) ||
+        (rc = alloc(&X.sel, (size_t)S * ALPHA, x->owned)) || (rc = alloc(&X.ri, (size_t)S * ALPHA * BK, x->owned)) ||
+        (rc = alloc(&X.rk, (size_t)S * ALPHA * BK, x->owned)) || (rc = alloc(&X.rn, (size_t)S * ALPHA, x->owned)) ||
+        (rc = alloc(&X.active, 1, x->owned))) {
+        delete x;
+        return rc;
+    }
+    if (S && (hipMemcpyAsync(dsrc, src, 4ull * S, hipMemcpyDefault, x->stream) != hipSuccess ||
+              hipMemcpyAsync(dt, targets, 20ull * S, hipMemcpyDefault, x->stream) != hipSuccess)) {
+        delete x;
+        return err(KAD_ERR_HIP, "search upload failed");
+    }
+    X.src = dsrc;
+    X.targets = dt;
+    if (S) hipLaunchKernelGGL(search_init_kernel, dim3(grid_for(S)), dim3(BLOCK), 0, x->stream, s->W, X);
+    if (hipGetLastError() != hipSuccess) {
+        delete x;
+        return err(KAD_ERR_HIP, "search init launch failed");
+    }
+    *out = x;
+    return KAD_OK;
+}
+
+int kad_search_hop(kad_search* x, uint32_t* n_active) {
+    if (!x) return err(KAD_ERR_INVALID, "NULL search");
+    Guard g(x->device);
+    const SearchDev& X = x->X;
+    SW_TRY(hipMemsetAsync(X.active, 0, 4, x->stream));
+    if (X.S) {
+        hipLaunchKernelGGL(search_query_kernel, dim3(grid_for((uint64_t)X.S * ALPHA)), dim3(BLOCK), 0, x->stream, x->sw->W, X);
+        hipLaunchKernelGGL(search_merge_kernel, dim3(grid_for(X.S)), dim3(BLOCK), 0, x->stream, x->sw->W, X);
+    }
+    SW_TRY(hipGetLastError());
+    if (n_active) {
+        SW_TRY(hipMemcpyAsync(n_active, X.active, 4, hipMemcpyDeviceToHost, x->stream));
+        SW_TRY(hipStreamSynchronize(x->stream));
+    }
+    return KAD_OK;
+}
+
+int kad_search_get(const kad_search* x, uint32_t* list, uint8_t* queried, uint8_t* n, uint32_t* hops, uint8_t* done) {
+    if (!x) return err(KAD_ERR_INVALID, "NULL search");
+    Guard g(x->device);
+    const SearchDev& X = x->X;
+    SW_TRY(hipStreamSynchronize(x->stream));
+    const size_t S = X.S;
+    if (list || queried) {
+        std::vector<uint32_t> li(S * SNP);
+        std::vector<uint8_t> lq(S * SNP);
+        SW_TRY(hipMemcpy(li.data(), X.li, 4 * S * SNP, hipMemcpyDeviceToHost));
+        SW_TRY(hipMemcpy(lq.data(), X.lq, S * SNP, hipMemcpyDeviceToHost));
+        for (size_t s = 0; s < S; s++)
+            for (uint32_t j = 0; j < SN; j++) {
+                if (list) list[s * SN + j] = li[s * SNP + j];
+                if (queried) queried[s * SN + j] = lq[s * SNP + j];
+            }
+    }
+    if (n) SW_TRY(hipMemcpy(n, X.ln, S, hipMemcpyDeviceToHost));
+    if (hops) SW_TRY(hipMemcpy(hops, X.hops, 4 * S, hipMemcpyDeviceToHost));
+    if (done) SW_TRY(hipMemcpy(done, X.done, S, hipMemcpyDeviceToHost));
+    return KAD_OK;
+}
+
+int kad_search_destroy(kad_search* x) {
+    if (!x) return KAD_OK;
+    Guard g(x->device);
+    (void)hipStreamSynchronize(x->stream);
+    delete x;
+    return KAD_OK;
+}
+
+}  // extern "C"

@@ -588,3 +588,206 @@ int orc_parse_nodes(uint32_t n, const uint8_t* in, uint32_t rec_len, const uint8
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------
+// Config 5 swarm model (SURVEY.md §8d "Config 5", §8f row 2). BUILD-DEFINED: the reference has no
+// swarm simulator; parity is pinned per hop (RoutingTable::findClosestNodes on each peer's table,
+// routing_table.cpp:67-111, and the Search::insertNode ordering, dht.cpp:961-1047).
+//   Peer tables, shape K (Dht::onNewNode, dht.cpp:867-936: only my bucket splits, a full bucket
+//   caches newcomers away): peer p with top-64 key k has depth D = the least D with at most 8 other
+//   peers sharing >= D leading bits with it (capped at SW_LEVELS-1); for d < D the level-d bucket
+//   holds min(8, |S_d|) peers of S_d (peers sharing exactly d bits), picked at positions
+//   lo + (off + j*|S_d|/8) % |S_d|, off = mix(k ^ (d+1)*GOLDEN) % |S_d|; my bucket holds the first 8
+//   other peers sharing >= D bits, in ID order. All peers good.
+//   Lookup: the source's findClosestNodes(t, SEARCH_NODES=14) seeds the list; each synchronous hop
+//   queries the first <= 4 (MAX_REQUESTED_SEARCH_NODES, dht.h:327) unqueried nodes in list order,
+//   each answers findClosestNodes(t, TARGET_NODES=8) from its own table, answers equal to the source
+//   are dropped (deserializeNodes, network_engine.cpp:798-799), the rest go through insertNode (sorted
+//   insert, trim to 14). Done when the first min(8, |list|) nodes have all been queried
+//   (Search::isSynced, dht.cpp:1467-1478), or stalled when no unqueried node is left.
+// ---------------------------------------------------------------------------
+static constexpr uint32_t SW_LEVELS = 28, SW_BUCKET = 8, SW_SEARCH = 14, SW_ALPHA = 4;
+
+static inline uint64_t sw_mix(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+struct Swarm {
+    uint32_t n;
+    const uint8_t* ids;
+    std::vector<uint64_t> key;
+    std::vector<uint8_t> depth, counts;  // counts[p*SW_LEVELS + level]
+    std::vector<uint32_t> ent;           // ent[(p*SW_LEVELS + level)*SW_BUCKET + j]
+    // peers whose top-64 key starts with the L-bit prefix P: [lo, hi)
+    void range(uint64_t P, uint32_t L, uint32_t& lo, uint32_t& hi) const {
+        if (L == 0) { lo = 0; hi = n; return; }
+        const uint64_t a = P << (64 - L);
+        lo = (uint32_t)(std::lower_bound(key.begin(), key.end(), a) - key.begin());
+        if (P + 1 == (L == 64 ? 0 : (1ull << L))) { hi = n; return; }
+        hi = (uint32_t)(std::lower_bound(key.begin(), key.end(), (P + 1) << (64 - L)) - key.begin());
+    }
+    void build(uint32_t p) {
+        const uint64_t k = key[p];
+        uint32_t D = 0, lo, hi;
+        for (;; D++) {
+            range(D ? k >> (64 - D) : 0, D, lo, hi);
+            if (hi - lo - 1 <= SW_BUCKET || D == SW_LEVELS - 1) break;
+        }
+        depth[p] = (uint8_t)D;
+        for (uint32_t d = 0; d < SW_LEVELS; d++) counts[(size_t)p * SW_LEVELS + d] = 0;
+        for (uint32_t d = 0; d < D; d++) {
+            uint32_t a, e;
+            range((k >> (63 - d)) ^ 1ull, d + 1, a, e);
+            const uint32_t m = e - a, c = std::min(m, SW_BUCKET);
+            uint32_t* out = &ent[((size_t)p * SW_LEVELS + d) * SW_BUCKET];
+            const uint64_t off = m > SW_BUCKET ? sw_mix(k ^ ((uint64_t)(d + 1) * 0x9E3779B97F4A7C15ull)) % m : 0;
+            for (uint32_t j = 0; j < c; j++) out[j] = m > SW_BUCKET ? a + (uint32_t)((off + (uint64_t)j * m / SW_BUCKET) % m) : a + j;
+            counts[(size_t)p * SW_LEVELS + d] = (uint8_t)c;
+        }
+        uint32_t* out = &ent[((size_t)p * SW_LEVELS + D) * SW_BUCKET];
+        uint32_t c = 0;
+        for (uint32_t x = lo; x < hi && c < SW_BUCKET; x++)
+            if (x != p) out[c++] = x;
+        counts[(size_t)p * SW_LEVELS + D] = (uint8_t)c;
+    }
+    // p's table as a RoutingTable (buckets sorted by first) -> findClosestNodes(t, count)
+    void closest(uint32_t p, const Id& t, uint32_t count, std::vector<uint32_t>& out) const {
+        out.clear();
+        const Id me(ids + (size_t)HASH_LEN * p);
+        const uint32_t D = depth[p];
+        struct Bk { Id first; uint32_t level; };
+        std::vector<Bk> bk;
+        for (uint32_t d = 0; d <= D; d++) {
+            Id f;  // first: my first d bits, bit d flipped (levels), zeros after; my bucket: my first D bits
+            for (uint32_t b = 0; b < d; b++) f.setBit(b, me.getBit(b));
+            if (d < D) f.setBit(d, !me.getBit(d));
+            bk.push_back({f, d});
+        }
+        std::sort(bk.begin(), bk.end(), [](const Bk& a, const Bk& b) { return a.first < b.first; });
+        const uint32_t B = (uint32_t)bk.size();
+        uint32_t b = 0;  // upper_bound(first, t) - 1, clamped (routing_table.cpp:113-127)
+        while (b + 1 < B && !(t < bk[b + 1].first)) b++;
+        auto cnt = [&](uint32_t i) { return (uint32_t)counts[(size_t)p * SW_LEVELS + bk[i].level]; };
+        uint32_t r = 0, lo, hi;
+        for (;; r++) {
+            lo = b > r ? b - 1 - r : 0;
+            hi = std::min(B - 1, b + r);
+            uint32_t g = 0;
+            for (uint32_t i = lo; i <= hi; i++) g += cnt(i);
+            if (g >= count || (lo == 0 && hi == B - 1)) break;
+        }
+        std::vector<uint32_t> cand;
+        for (uint32_t i = lo; i <= hi; i++)
+            for (uint32_t j = 0; j < cnt(i); j++) cand.push_back(ent[((size_t)p * SW_LEVELS + bk[i].level) * SW_BUCKET + j]);
+        std::stable_sort(cand.begin(), cand.end(), [&](uint32_t x, uint32_t y) {
+            return t.xorCmp(Id(ids + (size_t)HASH_LEN * x), Id(ids + (size_t)HASH_LEN * y)) < 0;
+        });
+        if (cand.size() > count) cand.resize(count);
+        out = cand;
+    }
+};
+
+extern "C" {
+void* orc_swarm_build(uint32_t n, const uint8_t* sorted_ids, int nthreads) {
+    Swarm* s = new Swarm;
+    s->n = n;
+    s->ids = sorted_ids;
+    s->key.resize(n);
+    for (uint32_t i = 0; i < n; i++) {
+        uint64_t k = 0;
+        for (int b = 0; b < 8; b++) k = (k << 8) | sorted_ids[(size_t)HASH_LEN * i + b];
+        s->key[i] = k;
+    }
+    s->depth.resize(n);
+    s->counts.resize((size_t)n * SW_LEVELS);
+    s->ent.assign((size_t)n * SW_LEVELS * SW_BUCKET, 0xFFFFFFFFu);
+    parallel_for(n, nthreads, [&](uint32_t a, uint32_t e) { for (uint32_t p = a; p < e; p++) s->build(p); });
+    return s;
+}
+void orc_swarm_free(void* h) { delete (Swarm*)h; }
+void orc_swarm_table(void* h, uint32_t p, uint32_t* depth, uint8_t* counts, uint32_t* ent) {
+    const Swarm* s = (const Swarm*)h;
+    *depth = s->depth[p];
+    std::memcpy(counts, &s->counts[(size_t)p * SW_LEVELS], SW_LEVELS);
+    std::memcpy(ent, &s->ent[(size_t)p * SW_LEVELS * SW_BUCKET], 4ull * SW_LEVELS * SW_BUCKET);
+}
+int orc_swarm_closest(void* h, uint32_t q, const uint32_t* peers, const uint8_t* targets, uint32_t count,
+                      uint32_t* out_idx, uint8_t* out_cnt, int nthreads) {
+    const Swarm* s = (const Swarm*)h;
+    parallel_for(q, nthreads, [&](uint32_t a, uint32_t e) {
+        std::vector<uint32_t> r;
+        for (uint32_t i = a; i < e; i++) {
+            s->closest(peers[i], Id(targets + (size_t)HASH_LEN * i), count, r);
+            for (uint32_t j = 0; j < count; j++) out_idx[(size_t)i * count + j] = j < r.size() ? r[j] : 0xFFFFFFFFu;
+            out_cnt[i] = (uint8_t)r.size();
+        }
+    });
+    return 0;
+}
+// Lookups for S (source, target) pairs, at most max_hops hops each. Outputs: list S x 14 (NO_NODE
+// padded), queried flags S x 14, list length, hops done, done (1 synced, 2 stalled, 0 running).
+int orc_swarm_search(void* h, uint32_t S, const uint32_t* src, const uint8_t* targets, uint32_t max_hops,
+                     uint32_t* out_list, uint8_t* out_q, uint8_t* out_n, uint32_t* out_hops, uint8_t* out_done,
+                     int nthreads) {
+    const Swarm* s = (const Swarm*)h;
+    parallel_for(S, nthreads, [&](uint32_t a, uint32_t e) {
+      for (uint32_t i = a; i < e; i++) {
+        const Id t(targets + (size_t)HASH_LEN * i);
+        std::vector<uint32_t> L;
+        std::vector<uint8_t> Q;
+        s->closest(src[i], t, SW_SEARCH, L);
+        Q.assign(L.size(), 0);
+        uint32_t hops = 0;
+        uint8_t done = 0;
+        // the nodes of the next hop are chosen (and marked queried) as soon as the list is known:
+        // the first <= 4 unqueried ones in list order (searchSendGetValues, dht.cpp:1171-1235)
+        std::vector<uint32_t> sel;
+        auto select = [&]() {
+            sel.clear();
+            for (size_t j = 0; j < L.size() && sel.size() < SW_ALPHA; j++)
+                if (!Q[j]) { sel.push_back(L[j]); Q[j] = 1; }
+            if (sel.empty()) done = 2;  // stalled
+        };
+        select();
+        while (!done && hops < max_hops) {
+            hops++;
+            std::vector<uint32_t> rep;
+            for (uint32_t v : sel) {
+                s->closest(v, t, SW_BUCKET, rep);
+                for (uint32_t r : rep) {  // Search::insertNode (dht.cpp:961-1047), all nodes good
+                    if (r == src[i]) continue;  // deserializeNodes drops our own ID (network_engine.cpp:798-799)
+                    const Id rid(s->ids + (size_t)HASH_LEN * r);
+                    size_t pos = L.size();
+                    bool found = false;
+                    while (pos > 0) {
+                        if (L[pos - 1] == r) { found = true; break; }
+                        if (t.xorCmp(rid, Id(s->ids + (size_t)HASH_LEN * L[pos - 1])) > 0) break;
+                        pos--;
+                    }
+                    if (found) continue;
+                    if (L.size() >= SW_SEARCH && pos >= SW_SEARCH) continue;
+                    L.insert(L.begin() + pos, r);
+                    Q.insert(Q.begin() + pos, 0);
+                    if (L.size() > SW_SEARCH) { L.pop_back(); Q.pop_back(); }
+                }
+            }
+            bool synced = !L.empty();  // Search::isSynced (dht.cpp:1467-1478)
+            for (size_t j = 0; j < L.size() && j < SW_BUCKET; j++) synced &= Q[j] != 0;
+            if (synced) done = 1;
+            else select();
+        }
+        for (uint32_t j = 0; j < SW_SEARCH; j++) {
+            out_list[(size_t)i * SW_SEARCH + j] = j < L.size() ? L[j] : 0xFFFFFFFFu;
+            out_q[(size_t)i * SW_SEARCH + j] = j < L.size() ? Q[j] : 0;
+        }
+        out_n[i] = (uint8_t)L.size();
+        out_hops[i] = hops;
+        out_done[i] = done;
+      }
+    });
+    return 0;
+}
+}  // extern "C" (swarm)

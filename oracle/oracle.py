@@ -40,6 +40,11 @@ _SIG = {
     "orc_buffer_nodes": (C.c_uint32, [C.c_uint32, _P, _P, _P, C.c_uint32, _P, _P, C.c_uint32, _P, _P]),
     "orc_is_martian": (C.c_int, [_P, C.c_uint32]),
     "orc_parse_nodes": (C.c_int, [C.c_uint32, _P, C.c_uint32, _P, _P]),
+    "orc_swarm_build": (_P, [C.c_uint32, _P, C.c_int]),
+    "orc_swarm_free": (None, [_P]),
+    "orc_swarm_table": (None, [_P, C.c_uint32, _P, _P, _P]),
+    "orc_swarm_closest": (C.c_int, [_P, C.c_uint32, _P, _P, C.c_uint32, _P, _P, C.c_int]),
+    "orc_swarm_search": (C.c_int, [_P, C.c_uint32, _P, _P, C.c_uint32, _P, _P, _P, _P, _P, C.c_int]),
 }
 _lib = None
 
@@ -215,3 +220,56 @@ def parse_nodes(records, rec_len, myid):
     keep = np.zeros((rec.shape[0],), dtype=np.uint8)
     lib().orc_parse_nodes(rec.shape[0], _p(rec), rec_len, _p(my), _p(keep))
     return keep
+
+
+SW_LEVELS, SW_BUCKET, SW_SEARCH = 28, 8, 14
+
+
+class SwarmModel:
+    """Config 5 swarm model (kad_oracle.cpp "Config 5 swarm model"): shape-K peer tables over sorted
+    IDs, per-peer findClosestNodes, synchronous iterative lookups."""
+
+    def __init__(self, sorted_ids, nthreads=8):
+        self.ids = _ids(sorted_ids)
+        self.n = self.ids.shape[0]
+        self._h = lib().orc_swarm_build(self.n, _p(self.ids), nthreads)
+
+    def close(self):
+        if self._h:
+            lib().orc_swarm_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def table(self, p):
+        d = C.c_uint32()
+        cnt = np.zeros(SW_LEVELS, np.uint8)
+        ent = np.zeros((SW_LEVELS, SW_BUCKET), np.uint32)
+        lib().orc_swarm_table(self._h, p, C.byref(d), _p(cnt), _p(ent))
+        return d.value, cnt, ent
+
+    def closest(self, peers, targets, count, nthreads=8):
+        peers = np.ascontiguousarray(peers, np.uint32)
+        t = _ids(targets)
+        q = peers.shape[0]
+        idx = np.empty((q, count), np.uint32)
+        cnt = np.empty((q,), np.uint8)
+        lib().orc_swarm_closest(self._h, q, _p(peers), _p(t), count, _p(idx), _p(cnt), nthreads)
+        return idx, cnt
+
+    def search(self, src, targets, max_hops=64, nthreads=8):
+        src = np.ascontiguousarray(src, np.uint32)
+        t = _ids(targets)
+        S = src.shape[0]
+        lst = np.empty((S, SW_SEARCH), np.uint32)
+        qf = np.empty((S, SW_SEARCH), np.uint8)
+        n = np.empty((S,), np.uint8)
+        hops = np.empty((S,), np.uint32)
+        done = np.empty((S,), np.uint8)
+        lib().orc_swarm_search(self._h, S, _p(src), _p(t), max_hops, _p(lst), _p(qf), _p(n), _p(hops), _p(done),
+                               nthreads)
+        return lst, qf, n, hops, done

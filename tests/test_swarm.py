@@ -1,0 +1,155 @@
+"""Config 5: the simulated swarm's shape-K peer tables, per-peer
+findClosestNodes and synchronous iterative lookups. BUILD-DEFINED model; parity is pinned per hop:
+CPU tests tie the oracle's swarm model to the general RoutingTable restatement (flat_rt_closest on
+each peer's table written out as a RoutingTable) and to the model's table invariants; GPU tests are
+bit-exact against the oracle table by table, query by query and hop by hop."""
+import numpy as np
+import pytest
+import torch
+
+import oracle as O
+from opendht_amd import synth as S
+
+
+def _swarm_ids(n, seed):
+    ids, _ = S.sort_ids(S.random_ids(n, seed))
+    return ids
+
+
+def _key(ids):
+    return ids[:, :8].copy().view(">u8").reshape(-1).astype(np.uint64)
+
+
+def _common_bits64(a, b):
+    x = int(a) ^ int(b)
+    return 64 if x == 0 else 64 - x.bit_length()
+
+
+def _as_routing_table(ids, p, depth, cnt, ent):
+    """Peer p's table as RoutingTable arrays (buckets sorted by first, nodes in list order)."""
+    me = int.from_bytes(ids[p].tobytes(), "big")
+    bks = []
+    for d in range(depth + 1):
+        hi_bits = me >> (160 - d) if d else 0
+        if d < depth:
+            first = (((hi_bits << 1) | (((me >> (159 - d)) & 1) ^ 1)) << (159 - d))
+        else:
+            first = hi_bits << (160 - d) if d else 0
+        bks.append((first, d))
+    bks.sort()
+    firsts = np.stack([np.frombuffer(f.to_bytes(20, "big"), np.uint8) for f, _ in bks])
+    nodes = [ent[d, :cnt[d]] for _, d in bks]
+    off = np.concatenate([[0], np.cumsum([len(x) for x in nodes])]).astype(np.uint32)
+    members = np.concatenate(nodes).astype(np.uint32) if off[-1] else np.zeros(0, np.uint32)
+    return firsts, off, members
+
+
+def test_swarm_tables_shape_k():
+    n = 20_000
+    ids = _swarm_ids(n, 0x5A1)
+    key = _key(ids)
+    M = O.SwarmModel(ids)
+    rng = np.random.default_rng(1)
+    for p in rng.integers(0, n, 300):
+        depth, cnt, ent = M.table(int(p))
+        share = np.array([_common_bits64(key[p], k) for k in key])
+        # depth: the least D with <= 8 other peers sharing >= D bits
+        others = lambda D: int((share >= D).sum()) - 1  # noqa: E731
+        assert others(depth) <= 8 and (depth == 0 or others(depth - 1) > 8)
+        for d in range(depth):
+            members = ent[d, :cnt[d]]
+            assert cnt[d] == min(8, int((share == d).sum()))
+            assert (share[members] == d).all() and len(set(members.tolist())) == cnt[d]
+        mine = ent[depth, :cnt[depth]]
+        assert p not in mine and (share[mine] >= depth).all() and cnt[depth] == others(depth)
+    M.close()
+
+
+def test_swarm_closest_matches_routing_table_restatement():
+    """The swarm model's per-peer findClosestNodes equals the general restatement on the same table."""
+    n = 5000
+    ids = _swarm_ids(n, 0x5A2)
+    M = O.SwarmModel(ids)
+    rng = np.random.default_rng(2)
+    peers = rng.integers(0, n, 200).astype(np.uint32)
+    targets = S.random_targets(200, seed=3)
+    targets[:20] = ids[peers[:20]]  # targets in my bucket
+    for count in (1, 8, 14):
+        got, gc = M.closest(peers, targets, count)
+        for i, p in enumerate(peers):
+            depth, cnt, ent = M.table(int(p))
+            firsts, off, members = _as_routing_table(ids, int(p), depth, cnt, ent)
+            sub = ids[members] if members.size else np.zeros((0, 20), np.uint8)
+            st = np.ones(members.shape[0], np.uint8)
+            w, wc = O.flat_rt_closest(sub, st, firsts, off, targets[i:i + 1], count)
+            want = np.where(w[0] != O.NO_NODE, members[np.minimum(w[0], max(members.size - 1, 0))], O.NO_NODE)
+            assert gc[i] == wc[0]
+            np.testing.assert_array_equal(got[i], want)
+    M.close()
+
+
+def test_swarm_search_converges():
+    n = 50_000
+    ids = _swarm_ids(n, 0x5A3)
+    M = O.SwarmModel(ids)
+    rng = np.random.default_rng(3)
+    src = rng.integers(0, n, 500).astype(np.uint32)
+    tg = S.random_targets(500, seed=4)
+    lst, q, nn, hops, done = M.search(src, tg)
+    assert (done == 1).all() and hops.max() < 12
+    key, tk = _key(ids), _key(tg)
+    hit = 0
+    for i in range(100):
+        best = np.argsort(key ^ tk[i])[:8]
+        hit += len(set(best.tolist()) & set(lst[i, :8].tolist()))
+        d = key[lst[i, :nn[i]]] ^ tk[i]
+        assert (np.diff(d.astype(np.float64)) > 0).all() or (d[1:] > d[:-1]).all()
+        assert q[i, :8].all()
+    assert hit / 800 > 0.9
+    M.close()
+
+
+@pytest.mark.gpu
+def test_swarm_gpu_parity(gpu):
+    from opendht_amd.swarm import Swarm
+    n = 40_000
+    ids = _swarm_ids(n, 0x5A4)
+    M = O.SwarmModel(ids)
+    rng = np.random.default_rng(5)
+    with Swarm(ids, device=gpu.index or 0) as W:
+        for p in list(rng.integers(0, n, 400)) + [0, n - 1]:
+            d, c, e = W.table(int(p))
+            wd, wc, we = M.table(int(p))
+            assert d == wd
+            np.testing.assert_array_equal(c, wc)
+            np.testing.assert_array_equal(e[:d + 1], we[:d + 1])
+        q = 20_000
+        peers = rng.integers(0, n, q).astype(np.uint32)
+        targets = S.random_targets(q, seed=6)
+        targets[:500] = ids[peers[:500]]
+        targets[500:1000] = ids[rng.integers(0, n, 500)]
+        pt = torch.from_numpy(peers.view(np.int32)).to(gpu)
+        tt = torch.from_numpy(targets).to(gpu)
+        for count in (1, 8, 14, 16):
+            idx, cnt = W.closest(pt, tt, count)
+            torch.cuda.synchronize()
+            want, wcnt = M.closest(peers, targets, count)
+            np.testing.assert_array_equal(cnt.cpu().numpy(), wcnt)
+            np.testing.assert_array_equal(idx.cpu().numpy().view(np.uint32), want)
+        # lookups, hop by hop
+        Sn = 3000
+        src = rng.integers(0, n, Sn).astype(np.uint32)
+        tg = S.random_targets(Sn, seed=7)
+        tg[:100] = ids[src[:100]]
+        X = W.search(torch.from_numpy(src.view(np.int32)).to(gpu), torch.from_numpy(tg).to(gpu))
+        for h in range(1, 40):
+            active = X.hop()
+            got = X.get()
+            want = M.search(src, tg, max_hops=h)
+            for a, b, name in zip(got, want, ("list", "queried", "n", "hops", "done")):
+                np.testing.assert_array_equal(a, b, err_msg=f"hop {h}: {name}")
+            if active == 0:
+                break
+        assert active == 0
+        X.close()
+    M.close()

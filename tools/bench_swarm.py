@@ -1,0 +1,70 @@
+"""Config 5 measurement (BASELINE.json configs[4]): a simulated 10M-peer swarm (shape-K tables on the
+GPU) and a batch of iterative lookups run to convergence, hop by hop. Prints one JSON object:
+table build time, lookups/s over the whole convergence, hops histogram, per-hop time, and the
+per-hop findClosestNodes rate. Model: opendht_amd/csrc/kad_swarm.hip (build-defined, parity per hop
+in tests/test_swarm.py)."""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from opendht_amd import synth as S  # noqa: E402
+from opendht_amd.swarm import Swarm  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--peers", type=int, default=10_000_000)
+    ap.add_argument("--lookups", type=int, default=1 << 20)
+    args = ap.parse_args()
+    dev = torch.device("cuda:0")
+    t0 = time.perf_counter()
+    ids, _ = S.sort_ids(S.random_ids(args.peers, 0x0D470500))
+    t_ids = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    W = Swarm(ids, device=0)
+    torch.cuda.synchronize()
+    t_build = time.perf_counter() - t0
+    rng = np.random.default_rng(9)
+    src = torch.from_numpy(rng.integers(0, args.peers, args.lookups).astype(np.int32)).to(dev)
+    tg = torch.from_numpy(S.random_targets(args.lookups, seed=0x0D470501)).to(dev)
+    # warm-up on a small batch
+    X = W.search(src[:4096], tg[:4096])
+    X.run()
+    X.close()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    X = W.search(src, tg)
+    hop_ms, active = [], []
+    for _ in range(64):
+        h0 = time.perf_counter()
+        a = X.hop()
+        hop_ms.append((time.perf_counter() - h0) * 1e3)
+        active.append(a)
+        if a == 0:
+            break
+    torch.cuda.synchronize()
+    t_all = time.perf_counter() - t0
+    lst, q, n, hops, done = X.get()
+    queries = int(hops.sum()) * 4 + args.lookups  # findClosestNodes answers (upper bound: <= 4 per hop)
+    print(json.dumps({
+        "config": f"config5: {args.peers} peers (shape-K tables in HBM), {args.lookups} lookups, alpha 4, list 14",
+        "ids_s": round(t_ids, 2), "table_build_s": round(t_build, 2),
+        "table_gb": round(W.device_bytes() / 1e9, 2),
+        "lookups_per_s": args.lookups / t_all, "convergence_ms": t_all * 1e3, "rounds": len(hop_ms),
+        "hop_ms": [round(x, 3) for x in hop_ms], "active_after_hop": active,
+        "hops_hist": np.bincount(hops).tolist(), "mean_hops": float(hops.mean()),
+        "done_hist": np.bincount(done, minlength=3).tolist(),
+        "peer_queries_per_s_upper": queries / t_all,
+    }), flush=True)
+    X.close()
+    W.close()
+
+
+if __name__ == "__main__":
+    main()
