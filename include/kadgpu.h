@@ -263,6 +263,10 @@ int kad_xor_cmp_batch(const uint8_t* targets, const uint8_t* a, const uint8_t* b
 int kad_common_bits_batch(const uint8_t* a, const uint8_t* b, uint32_t n, uint32_t* out, void* stream);
 /* out[i] = a[i].lowbit(), 0xFFFFFFFF for the zero ID     (infohash.h:84-95)  */
 int kad_lowbit_batch(const uint8_t* a, uint32_t n, uint32_t* out, void* stream);
+/* out_ids[i] = InfoHash::get(key i) = SHA-1 of data[offsets[i] .. offsets[i+1]) (infohash.cpp:46-61,
+ * HASH_LEN 20 -> SHA-1). Device pointers; offsets has n+1 entries. */
+int kad_infohash_get_batch(const uint8_t* data, const uint64_t* offsets, uint32_t n, uint8_t* out_ids,
+                           int device, void* stream);
 
 /* ---- synthetic tables (host code; bench and tests) ----------------------- */
 /* n distinct random IDs from std::mt19937_64(seed): ID i = big-endian bytes of

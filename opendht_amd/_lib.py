@@ -83,6 +83,7 @@ SIGNATURES = {
     "kad_xor_cmp_batch": (C.c_int, [_P, _P, _P, C.c_uint32, _P, _P]),
     "kad_common_bits_batch": (C.c_int, [_P, _P, C.c_uint32, _P, _P]),
     "kad_lowbit_batch": (C.c_int, [_P, C.c_uint32, _P, _P]),
+    "kad_infohash_get_batch": (C.c_int, [_P, _P, C.c_uint32, _P, C.c_int, _P]),
     "kad_synth_ids": (C.c_int, [C.c_uint64, C.c_uint32, _P]),
     "kad_synth_status": (C.c_int, [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, _P]),
     "kad_sort_ids": (C.c_int, [C.c_uint32, _P, _P]),

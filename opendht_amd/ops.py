@@ -54,3 +54,15 @@ def parse_nodes(records, rec_len: int, myid: bytes):
     check(lib().kad_parse_nodes_batch(ptr(records), n, rec_len, ptr(me), ptr(keep), records.device.index or 0,
                                       _stream(records)), "kad_parse_nodes_batch")
     return keep
+
+
+def infohash_get(data, offsets):
+    """InfoHash::get (infohash.cpp:46-61) of every key: SHA-1 of data[offsets[i]:offsets[i+1]].
+    data: device uint8 tensor (keys back to back), offsets: device int64 tensor (n + 1). -> (n, 20) uint8."""
+    import torch
+
+    n = offsets.shape[0] - 1
+    out = torch.empty((max(n, 0), 20), dtype=torch.uint8, device=offsets.device)
+    check(lib().kad_infohash_get_batch(ptr(data), ptr(offsets), n, ptr(out), offsets.device.index or 0,
+                                       _stream(offsets)), "kad_infohash_get_batch")
+    return out

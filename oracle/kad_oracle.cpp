@@ -791,3 +791,44 @@ int orc_swarm_search(void* h, uint32_t S, const uint32_t* src, const uint8_t* ta
     return 0;
 }
 }  // extern "C" (swarm)
+
+// ---------------------------------------------------------------------------
+// InfoHash::get (src/infohash.cpp:46-61): GnuTLS SHA-1 of the data (HASH_LEN 20 -> GNUTLS_DIG_SHA1).
+// GnuTLS is absent here; this is FIPS 180-4 SHA-1, pinned by the standard's test vectors
+// (tests/test_sha1.py). SURVEY.md §8f row 4.
+// ---------------------------------------------------------------------------
+static inline uint32_t rol(uint32_t x, int n) { return (x << n) | (x >> (32 - n)); }
+static void sha1(const uint8_t* m, uint64_t len, uint8_t* out) {
+    uint32_t h[5] = {0x67452301u, 0xEFCDAB89u, 0x98BADCFEu, 0x10325476u, 0xC3D2E1F0u};
+    const uint64_t nblk = (len + 8) / 64 + 1;
+    for (uint64_t b = 0; b < nblk; b++) {
+        uint8_t blk[64];
+        for (int i = 0; i < 64; i++) {
+            const uint64_t j = 64 * b + i;
+            blk[i] = j < len ? m[j] : (j == len ? 0x80 : 0);
+        }
+        if (b == nblk - 1)
+            for (int i = 0; i < 8; i++) blk[56 + i] = (uint8_t)((len * 8) >> (56 - 8 * i));
+        uint32_t w[80];
+        for (int i = 0; i < 16; i++) w[i] = (uint32_t)blk[4 * i] << 24 | (uint32_t)blk[4 * i + 1] << 16 | (uint32_t)blk[4 * i + 2] << 8 | blk[4 * i + 3];
+        for (int i = 16; i < 80; i++) w[i] = rol(w[i - 3] ^ w[i - 8] ^ w[i - 14] ^ w[i - 16], 1);
+        uint32_t a = h[0], bb = h[1], c = h[2], d = h[3], e = h[4];
+        for (int i = 0; i < 80; i++) {
+            uint32_t f, k;
+            if (i < 20) { f = (bb & c) | (~bb & d); k = 0x5A827999u; }
+            else if (i < 40) { f = bb ^ c ^ d; k = 0x6ED9EBA1u; }
+            else if (i < 60) { f = (bb & c) | (bb & d) | (c & d); k = 0x8F1BBCDCu; }
+            else { f = bb ^ c ^ d; k = 0xCA62C1D6u; }
+            const uint32_t t = rol(a, 5) + f + e + k + w[i];
+            e = d; d = c; c = rol(bb, 30); bb = a; a = t;
+        }
+        h[0] += a; h[1] += bb; h[2] += c; h[3] += d; h[4] += e;
+    }
+    for (int i = 0; i < 5; i++)
+        for (int j = 0; j < 4; j++) out[4 * i + j] = (uint8_t)(h[i] >> (24 - 8 * j));
+}
+
+extern "C" int orc_infohash_get(uint32_t n, const uint8_t* data, const uint64_t* off, uint8_t* out) {
+    for (uint32_t i = 0; i < n; i++) sha1(data + off[i], off[i + 1] - off[i], out + (size_t)HASH_LEN * i);
+    return 0;
+}

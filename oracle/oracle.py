@@ -40,6 +40,7 @@ _SIG = {
     "orc_buffer_nodes": (C.c_uint32, [C.c_uint32, _P, _P, _P, C.c_uint32, _P, _P, C.c_uint32, _P, _P]),
     "orc_is_martian": (C.c_int, [_P, C.c_uint32]),
     "orc_parse_nodes": (C.c_int, [C.c_uint32, _P, C.c_uint32, _P, _P]),
+    "orc_infohash_get": (C.c_int, [C.c_uint32, _P, _P, _P]),
     "orc_swarm_build": (_P, [C.c_uint32, _P, C.c_int]),
     "orc_swarm_free": (None, [_P]),
     "orc_swarm_table": (None, [_P, C.c_uint32, _P, _P, _P]),
@@ -273,3 +274,13 @@ class SwarmModel:
         lib().orc_swarm_search(self._h, S, _p(src), _p(t), max_hops, _p(lst), _p(qf), _p(n), _p(hops), _p(done),
                                nthreads)
         return lst, qf, n, hops, done
+
+
+def infohash_get(keys):
+    """InfoHash::get (infohash.cpp:46-61) = SHA-1 of each byte string: (n, 20) uint8."""
+    data = np.frombuffer(b"".join(keys), dtype=np.uint8) if keys else np.zeros(0, np.uint8)
+    data = np.ascontiguousarray(data) if data.size else np.zeros(1, np.uint8)
+    off = np.concatenate([[0], np.cumsum([len(k) for k in keys])]).astype(np.uint64)
+    out = np.zeros((len(keys), 20), np.uint8)
+    lib().orc_infohash_get(len(keys), _p(data), _p(off), _p(out))
+    return out
