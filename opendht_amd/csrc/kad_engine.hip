@@ -1188,18 +1188,11 @@ __global__ __launch_bounds__(BLOCK) void find_bucket_kernel(DevTable T, const ui
 }
 
 // ---------------------------------------------------------------------------------------
-// NodeCache::getCachedNodes, one query per lane (node_cache.cpp:36-66): two-pointer walk
-// outward from lower_bound(t); p-side taken when xorCmp(p, n) < 0; taking node 0 exhausts
-// the p side; expired nodes are walked over but not emitted.
-// ---------------------------------------------------------------------------------------
-__global__ __launch_bounds__(BLOCK) void nc_closest_kernel(DevTable T, const uint8_t* __restrict__ targets,
-                                                           uint32_t q, uint32_t count,
-                                                           uint32_t* __restrict__ out_idx,
-                                                           uint8_t* __restrict__ out_cnt) {
-    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
-    if (i >= q) return;
-    const Target t = load_target(targets, i);
-    uint32_t* row = out_idx + (size_t)i * count;
+// NodeCache::getCachedNodes, one query per lane (node_cache.cpp:36-66): two-pointer walk from
+// lower_bound(t): p = lb-1 (or lb at begin), n = lb; take the closer (xorCmp(p, n) < 0 -> p);
+// taking begin() exhausts p; emit non-expired nodes, stop at count. (Serial form: counts > 16 and
+// the group kernel's rare fallback.)
+__device__ void nc_serial(const DevTable& T, const Target& t, uint32_t count, uint32_t* row, uint8_t* cp) {
     const uint32_t N = T.n;
     const uint32_t lb = N ? node_lower_bound(T, t) : 0;
     uint32_t n = lb < N ? lb : NONE;
@@ -1235,7 +1228,108 @@ __global__ __launch_bounds__(BLOCK) void nc_closest_kernel(DevTable T, const uin
         if (!(T.status[it] & KAD_STATUS_EXPIRED)) row[m++] = it + T.index_base;
     }
     for (uint32_t s = m; s < count; s++) row[s] = NONE;
-    if (out_cnt) out_cnt[i] = (uint8_t)m;
+    if (cp) *cp = (uint8_t)m;
+}
+
+__global__ __launch_bounds__(BLOCK) void nc_closest_kernel(DevTable T, const uint8_t* __restrict__ targets,
+                                                           uint32_t q, uint32_t count,
+                                                           uint32_t* __restrict__ out_idx,
+                                                           uint8_t* __restrict__ out_cnt) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= q) return;
+    nc_serial(T, load_target(targets, i), count, out_idx + (size_t)i * count, out_cnt ? out_cnt + i : nullptr);
+}
+
+// NodeCache::getCachedNodes, one wave per query (count <= 16). The walk is a greedy merge of the
+// left run a_k = lb-1-k and the right run b_k = lb+k by XOR distance (distinct IDs: no ties; the
+// lb == 0 start takes node 0 from the right, which is the same walk with an empty left run). In a
+// greedy merge an element's place is its index plus the number of elements of the other run whose
+// PREFIX MAXIMUM distance is below its own prefix maximum (tests/test_nodecache_merge.py checks the
+// lemma). Lanes 0-31 load a_0..31, lanes 32-63 b_0..31 (top-64 keys and status bytes), take prefix
+// maxima with 5 shuffle steps, find their place by a 6-step binary search over the other run's
+// (monotone) prefix maxima, and the non-expired ones rank themselves through an LDS bit mask.
+// XOR-nearest nodes sit mostly on ONE side of lb (the target's dyadic subtree ends on one side): on
+// the bench shard a k = 14 walk takes up to 20 nodes from one side, so each run gets 32 lanes. Lane 0
+// walks serially (nc_serial) when a run is longer than 32 and the count-th emission does not come
+// before its 32nd element, or when two prefix maxima tie on the top 64 bits (the 160-bit order is
+// then needed).
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
+    return ((uint64_t)(uint32_t)__shfl((int)(v >> 32), src, 64) << 32) | (uint32_t)__shfl((int)(uint32_t)v, src, 64);
+}
+
+__global__ __launch_bounds__(BLOCK) void nc_group_kernel(DevTable T, const uint8_t* __restrict__ targets, uint32_t q,
+                                                         uint32_t count, uint32_t* __restrict__ out_idx,
+                                                         uint8_t* __restrict__ out_cnt) {
+    constexpr uint32_t W = 32, G = 64;  // run window, lanes per query
+    __shared__ unsigned long long emask[BLOCK / G];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, grp = tid / G;
+    const uint32_t qi = blockIdx.x * (BLOCK / G) + grp;
+    const bool right = lane >= W;
+    const uint32_t k = lane & (W - 1);
+    const bool act = qi < q && count > 0;
+    const uint32_t N = T.n;
+    Target t{};
+    uint32_t lb = 0;
+    if (act) {
+        t = load_target(targets, qi);
+        lb = N ? node_lower_bound(T, t) : 0u;
+    }
+    const uint32_t node = right ? lb + k : lb - 1 - k;
+    const bool valid = act && (right ? lb + k < N : lb > k);
+    uint64_t m = ~0ull;  // invalid lanes end their run: the maximum
+    bool expired = true;
+    if (valid) {
+        m = T.key[node] ^ t.hi;
+        expired = T.status[node] & KAD_STATUS_EXPIRED;
+    }
+    bool amb = valid && m == ~0ull;  // indistinguishable from the end-of-run sentinel
+#pragma unroll
+    for (uint32_t s = 1; s < W; s <<= 1) {  // prefix maxima along my run
+        const uint64_t o = shfl64(m, (int)lane - (int)s);
+        if (k >= s && o > m) m = o;  // unsigned (max() may pick a signed overload)
+    }
+    // place: my index + the other run's prefix maxima below mine (lower_bound over a monotone run)
+    const uint32_t obase = right ? 0u : W;
+    uint32_t lo = 0, hi = W;
+#pragma unroll
+    for (int it = 0; it < 6; it++) {  // 33 possible answers: 6 halvings (a settled lane stays put)
+        const uint32_t mid = (lo + hi) >> 1;
+        const uint64_t v = shfl64(m, (int)(obase + (mid < W ? mid : W - 1)));
+        if (lo < hi) {
+            if (v < m) lo = mid + 1; else hi = mid;
+        }
+    }
+    const uint64_t at = shfl64(m, (int)(obase + (lo < W ? lo : W - 1)));
+    amb |= valid && lo < W && at == m;  // equal top-64 prefix maxima: the 160-bit order decides
+    const uint32_t pos = k + lo;
+    const bool emit = valid && !expired;
+    if (lane == 0) emask[grp] = 0;
+    __syncthreads();
+    if (emit) atomicOr(&emask[grp], 1ull << pos);
+    __syncthreads();
+    const uint64_t em = emask[grp];
+    const uint32_t tot = (uint32_t)__builtin_popcountll(em);
+    uint32_t pstar = 64;  // position of the count-th emission (64: not inside the window)
+    if (tot >= count) {
+        uint64_t e = em;
+        for (uint32_t c = 1; c < count; c++) e &= e - 1;
+        pstar = (uint32_t)__builtin_ctzll(e);
+    }
+    const uint32_t posA = (uint32_t)__shfl((int)pos, (int)(W - 1), 64);
+    const uint32_t posB = (uint32_t)__shfl((int)pos, (int)(G - 1), 64);
+    const bool ok = !__any(amb) && (lb <= W || posA > pstar) && (lb + W >= N || posB > pstar);
+    if (act && ok) {
+        uint32_t* row = out_idx + (size_t)qi * count;
+        const uint32_t mm = min(tot, count);
+        if (emit) {
+            const uint32_t rank = (uint32_t)__builtin_popcountll(em & ((1ull << pos) - 1ull));
+            if (rank < count) row[rank] = node + T.index_base;
+        }
+        if (lane >= mm && lane < count) row[lane] = NONE;
+        if (lane == 0 && out_cnt) out_cnt[qi] = (uint8_t)mm;
+    } else if (act && lane == 0) {
+        nc_serial(T, t, count, out_idx + (size_t)qi * count, out_cnt ? out_cnt + qi : nullptr);
+    }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -2045,8 +2139,13 @@ int kad_nc_closest_batch(const kad_table* t, const uint8_t* targets, uint32_t q,
     if (q == 0) return KAD_OK;
     if (!targets || (!out_idx && count)) return set_err(KAD_ERR_INVALID, "NULL buffer");
     DeviceGuard g(t->device);
-    hipLaunchKernelGGL(nc_closest_kernel, dim3(grid_for(q)), dim3(BLOCK), 0, (hipStream_t)stream, t->d, targets, q, count,
-                       out_idx, out_cnt);
+    const char* ev = std::getenv("KAD_NC_KERNEL");
+    if (count >= 1 && count <= 16 && !(ev && std::strcmp(ev, "serial") == 0))
+        hipLaunchKernelGGL(nc_group_kernel, dim3((q + BLOCK / 64 - 1) / (BLOCK / 64)), dim3(BLOCK), 0, (hipStream_t)stream,
+                           t->d, targets, q, count, out_idx, out_cnt);
+    else
+        hipLaunchKernelGGL(nc_closest_kernel, dim3(grid_for(q)), dim3(BLOCK), 0, (hipStream_t)stream, t->d, targets, q,
+                           count, out_idx, out_cnt);
     HIP_TRY(hipGetLastError());
     return KAD_OK;
 }

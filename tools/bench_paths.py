@@ -51,3 +51,14 @@ idx, cnt = T.rt_closest(tg, 8)
 us = timeit(lambda: T.buffer_nodes(tg, idx, cnt))
 res["buffer_nodes_v4_us"] = round(us, 1)
 print(json.dumps(res, indent=1))
+os.environ["KAD_NC_KERNEL"] = "serial"
+us = timeit(lambda: T.nc_closest(tg, 14))
+os.environ.pop("KAD_NC_KERNEL")
+res["nc_k14_serial_us"] = round(us, 1)
+a = T.nc_closest(tg, 14)
+os.environ["KAD_NC_KERNEL"] = "serial"
+b = T.nc_closest(tg, 14)
+os.environ.pop("KAD_NC_KERNEL")
+torch.cuda.synchronize()
+res["nc_group_equals_serial"] = bool(torch.equal(a[0], b[0]) and torch.equal(a[1], b[1]))
+print(json.dumps(res, indent=1))
