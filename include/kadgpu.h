@@ -126,6 +126,32 @@ int kad_table_set_times(kad_table* t, const int64_t* time_ns, const int64_t* rep
  * node.h:91-94), then rebuild the good prefix sums. Async on `stream`. */
 int kad_table_refresh_status(kad_table* t, int64_t now_ns, void* stream);
 
+/* ---- incremental device mirror ----------------------
+ * Replays the table mutations of a live Dht on the device instead of re-snapshotting. Ops are rows
+ * of three uint32 (kind, a, b) applied in order; `a` names a node by its index at the start of
+ * the batch, `b` / `a` of INSERT a slot of the batch's new nodes (new_ids / new_status, host):
+ *   KAD_OP_REMOVE  a     node a leaves its bucket (Dht::expireBuckets, dht.cpp:942-956)
+ *   KAD_OP_REPLACE a b   new node b takes node a's place (onNewNode's expired slot, dht.cpp:917-921)
+ *   KAD_OP_INSERT  a     new node a is emplace_front'ed into findBucket(id) (dht.cpp:934)
+ *   KAD_OP_SPLIT   a     RoutingTable::split of the bucket at current index a (routing_table.cpp:137-163;
+ *                        nodes re-spliced to the front of their new bucket: list order reverses)
+ * The node arrays are re-laid out on the device (one gather over the plan's segments); masks,
+ * prefix sums, dup masks and window lines are re-derived there (a split turns window lines off).
+ * Outputs: remap (device, old n entries, may be NULL) = new index of every old node, KAD_NO_NODE
+ * if removed or replaced; new_index (host, n_new, may be NULL) = index of every new node,
+ * KAD_NO_NODE if unused. Any op clears KAD_TABLE_SORTED (NodeCache queries need a new snapshot);
+ * wire records and node times must be set again. Synchronous. */
+#define KAD_OP_REMOVE 1u
+#define KAD_OP_REPLACE 2u
+#define KAD_OP_INSERT 3u
+#define KAD_OP_SPLIT 4u
+int kad_table_apply(kad_table* t, const uint32_t* ops, uint32_t n_ops, const uint8_t* new_ids,
+                    const uint8_t* new_status, uint32_t n_new, uint32_t* remap, uint32_t* new_index);
+/* The table as host arrays (any may be NULL): ids n x 20 and status in bucket/list order, bucket
+ * firsts B x 20 and offsets B+1 (sizes from kad_table_get_info). */
+int kad_table_export(const kad_table* t, uint8_t* ids, uint8_t* status, uint8_t* bucket_first,
+                     uint32_t* bucket_offset);
+
 /* ---- queries: RoutingTable::findClosestNodes ---------------------------- */
 /* Batched RoutingTable::findClosestNodes(target, now, count) (routing_table.cpp:67-111)
  * on the table's status snapshot. Device pointers:

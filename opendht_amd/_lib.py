@@ -20,6 +20,7 @@ KAD_STATUS_GOOD = 0x01
 KAD_STATUS_EXPIRED = 0x02
 KAD_TABLE_SORTED = 0x01
 KAD_INFO_WINDOW_LINES = 0x100
+KAD_OP_REMOVE, KAD_OP_REPLACE, KAD_OP_INSERT, KAD_OP_SPLIT = 1, 2, 3, 4
 
 
 def row_words(count: int) -> int:
@@ -54,6 +55,8 @@ SIGNATURES = {
     "kad_table_destroy": (C.c_int, [_P]),
     "kad_table_get_info": (C.c_int, [_P, _P]),
     "kad_table_update_status": (C.c_int, [_P, _P]),
+    "kad_table_apply": (C.c_int, [_P, _P, C.c_uint32, _P, _P, C.c_uint32, _P, _P]),
+    "kad_table_export": (C.c_int, [_P, _P, _P, _P, _P]),
     "kad_table_set_times": (C.c_int, [_P, _P, _P, _P]),
     "kad_table_refresh_status": (C.c_int, [_P, C.c_int64, _P]),
     "kad_rt_closest_batch": (C.c_int, [_P, _P, C.c_uint32, C.c_uint32, _P, _P, _P]),

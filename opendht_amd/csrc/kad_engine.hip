@@ -1333,6 +1333,65 @@ __global__ __launch_bounds__(BLOCK) void nc_group_kernel(DevTable T, const uint8
 }
 
 // ---------------------------------------------------------------------------------------
+// Incremental device mirror: kad_table_apply re-lays the node arrays out on
+// the device from a host plan of segments (an untouched bucket is one range of old nodes; an edited
+// bucket an explicit handle list), then re-derives masks, prefix sums, dup masks and lines on the
+// device. Handles: old node index, or MIRROR_NEW | slot for a node of the batch.
+// ---------------------------------------------------------------------------
+constexpr uint32_t MIRROR_NEW = 0x80000000u;
+struct MirrorSeg {
+    uint32_t start, src, len, kind;  // kind 0: old nodes src.., 1: handles list[src..]
+};
+
+__global__ void mirror_gather_kernel(const MirrorSeg* __restrict__ seg, uint32_t nseg, const uint32_t* __restrict__ list,
+                                     uint32_t n_out, const uint64_t* __restrict__ okey, const uint32_t* __restrict__ otail,
+                                     const uint8_t* __restrict__ ost, const uint64_t* __restrict__ nkey,
+                                     const uint32_t* __restrict__ ntail, const uint8_t* __restrict__ nst,
+                                     uint64_t* __restrict__ key, uint32_t* __restrict__ tail, uint8_t* __restrict__ st,
+                                     uint32_t* __restrict__ remap, uint32_t* __restrict__ newidx) {
+    const uint32_t p = blockIdx.x * BLOCK + threadIdx.x;
+    if (p >= n_out) return;
+    uint32_t lo = 0, hi = nseg;  // last segment with start <= p
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (seg[mid].start <= p) lo = mid; else hi = mid;
+    }
+    const MirrorSeg s = seg[lo];
+    const uint32_t h = s.kind == 0 ? s.src + (p - s.start) : list[s.src + (p - s.start)];
+    if (h & MIRROR_NEW) {
+        const uint32_t x = h & ~MIRROR_NEW;
+        key[p] = nkey[x];
+        tail[3ull * p] = ntail[3ull * x];
+        tail[3ull * p + 1] = ntail[3ull * x + 1];
+        tail[3ull * p + 2] = ntail[3ull * x + 2];
+        st[p] = nst[x];
+        newidx[x] = p;
+    } else {
+        key[p] = okey[h];
+        tail[3ull * p] = otail[3ull * h];
+        tail[3ull * p + 1] = otail[3ull * h + 1];
+        tail[3ull * p + 2] = otail[3ull * h + 2];
+        st[p] = ost[h];
+        if (remap) remap[h] = p;
+    }
+}
+
+// Nodes whose top 64 ID bits equal another node's of the same bucket (tables whose bucket firsts
+// have zero low 96 bits cannot hold such a pair across buckets).
+__global__ void mirror_dmask_kernel(const uint64_t* key, const uint2* dir, uint32_t B, uint32_t* dmask, uint32_t* any) {
+    const uint32_t b = blockIdx.x * BLOCK + threadIdx.x;
+    if (b >= B) return;
+    const uint32_t j0 = dir[b].x & ~WIDE, j1 = dir[b + 1].x & ~WIDE;
+    uint32_t m = 0;
+    if (j1 - j0 <= 32)
+        for (uint32_t i = j0; i < j1; i++)
+            for (uint32_t j = j0; j < j1; j++)
+                if (i != j && key[i] == key[j]) m |= 1u << (i - j0);
+    dmask[b] = m;
+    if (m) atomicOr(any, 1u);
+}
+
+// ---------------------------------------------------------------------------------------
 // InfoHash primitives (infohash.h:84-146)
 // ---------------------------------------------------------------------------------------
 __device__ __forceinline__ void load_words(const uint8_t* p, uint32_t w[5]) {
@@ -1573,6 +1632,9 @@ struct kad_table {
     uint2* dir_mut = nullptr;
     uint32_t* gpre_mut = nullptr;
     uint32_t* wl_mut = nullptr;
+    // host copies of the bucket directory, for the incremental mirror (kad_table_apply)
+    std::vector<uint32_t> h_off;
+    std::vector<uint8_t> h_first;
     uint32_t* wrec = nullptr;  // per-node wire records: ID + address + port (kad_table_set_addrs)
     uint32_t addr_len = 0;
     int64_t* time_ns = nullptr;
@@ -1758,6 +1820,10 @@ int kad_table_create(kad_table** out, int device, uint32_t n_nodes, const uint8_
         (rc = dev_upload(&dtail, tail.data(), 3ull * n_nodes, t->owned, t->bytes)) ||
         (rc = dev_upload(&dst, status, n_nodes, t->owned, t->bytes))) { delete t; return rc; }
     d.key = dkey; d.tail = dtail; d.status = dst; t->status_mut = dst;
+    if (n_buckets) {
+        t->h_off.assign(bucket_offset, bucket_offset + n_buckets + 1);
+        t->h_first.assign(bucket_first, bucket_first + 20ull * n_buckets);
+    }
     std::vector<uint64_t>().swap(key);
     std::vector<uint32_t>().swap(tail);
 
@@ -2205,3 +2271,348 @@ int kad_lowbit_batch(const uint8_t* a, uint32_t n, uint32_t* out, void* stream) 
 }
 
 }  // extern "C"
+
+namespace {
+
+void release(kad_table* t, void* p) {
+    if (!p) return;
+    auto it = std::find(t->owned.begin(), t->owned.end(), p);
+    if (it != t->owned.end()) t->owned.erase(it);
+    size_t sz = 0;
+    if (hipMemPtrGetInfo(p, &sz) == hipSuccess && sz <= t->bytes) t->bytes -= sz;
+    (void)hipFree(p);
+}
+
+// Bucket firsts -> fkey/ftail, the locate radix and TF_DIRECT (as kad_table_create builds them).
+int build_bucket_index(kad_table* t) {
+    DevTable& d = t->d;
+    const uint32_t B = d.B;
+    const uint8_t* first = t->h_first.data();
+    std::vector<uint64_t> fkey(B);
+    std::vector<uint32_t> ftail(3ull * B);
+    for (uint32_t b = 0; b < B; b++) {
+        fkey[b] = id_hi(first + 20ull * b);
+        for (int w = 0; w < 3; w++) ftail[3ull * b + w] = id_word(first + 20ull * b, 2 + w);
+    }
+    uint32_t tb = 1;
+    while ((1u << tb) < B && tb < 24) tb++;
+    Radix r = choose_radix(fkey[0], fkey[B - 1], std::min<uint32_t>(tb + 1, 24));
+    if (B >= 2) {
+        const uint64_t step = fkey[1] - fkey[0];
+        bool uni = step && (step & (step - 1)) == 0 && (fkey[0] & (step - 1)) == 0;
+        for (uint32_t b = 0; b < B && uni; b++)
+            uni = (b == 0 || fkey[b] - fkey[b - 1] == step) && !ftail[3ull * b] && !ftail[3ull * b + 1] && !ftail[3ull * b + 2];
+        if (uni) { r.shift = (uint32_t)__builtin_ctzll(step); r.base = fkey[0]; r.slots = B; r.bits = tb; }
+    }
+    std::vector<uint32_t> rdx = build_radix(r, B, first, true);
+    bool direct = r.slots == B;
+    for (uint32_t sl = 0; sl < r.slots && direct; sl++) direct = rdx[sl] == (sl | RDX_EXACT);
+    d.flags = direct ? (d.flags | TF_DIRECT) : (d.flags & ~TF_DIRECT);
+    release(t, const_cast<uint64_t*>(d.fkey));
+    release(t, const_cast<uint32_t*>(d.ftail));
+    release(t, const_cast<uint32_t*>(d.rrdx));
+    uint64_t* dfk; uint32_t *dft, *drdx;
+    int rc;
+    if ((rc = dev_upload(&dfk, fkey.data(), B, t->owned, t->bytes)) ||
+        (rc = dev_upload(&dft, ftail.data(), 3ull * B, t->owned, t->bytes)) ||
+        (rc = dev_upload(&drdx, rdx.data(), rdx.size(), t->owned, t->bytes)))
+        return rc;
+    d.fkey = dfk; d.ftail = dft; d.rrdx = drdx;
+    d.rbase = r.base; d.rshift = r.shift; d.rslots = r.slots; t->rbits = r.bits;
+    return KAD_OK;
+}
+
+inline int lowbit20(const uint8_t* p) {  // InfoHash::lowbit (infohash.h:84-95), -1 for zero
+    for (int i = 19; i >= 0; i--)
+        if (p[i]) {
+            for (int j = 7; j >= 0; j--)
+                if (p[i] & (0x80 >> j)) return 8 * i + j;
+        }
+    return -1;
+}
+
+}  // namespace
+
+extern "C" {
+
+int kad_table_apply(kad_table* t, const uint32_t* ops, uint32_t n_ops, const uint8_t* new_ids, const uint8_t* new_status,
+                    uint32_t n_new, uint32_t* remap, uint32_t* new_index) {
+    if (!t || (n_ops && !ops) || (n_new && (!new_ids || !new_status))) return set_err(KAD_ERR_INVALID, "NULL argument");
+    if (t->d.B == 0 || t->h_off.empty()) return set_err(KAD_ERR_INVALID, "the mirror needs a RoutingTable (buckets)");
+    if ((uint64_t)t->d.n + n_new >= 0x7FFFFFFFull) return set_err(KAD_ERR_INVALID, "table too large");
+    DeviceGuard g(t->device);
+    DevTable& d = t->d;
+    const uint32_t B0 = d.B, n0 = d.n;
+    struct PB {
+        bool raw;
+        uint32_t src, len, origin;
+        std::vector<uint32_t> h;
+    };
+    std::vector<PB> cur(B0);
+    for (uint32_t b = 0; b < B0; b++) cur[b] = PB{true, t->h_off[b], t->h_off[b + 1] - t->h_off[b], b, {}};
+    std::vector<std::array<uint8_t, 20>> firsts(B0);
+    for (uint32_t b = 0; b < B0; b++) std::memcpy(firsts[b].data(), t->h_first.data() + 20ull * b, 20);
+    std::vector<uint32_t> ostart(B0 + 1);  // current index of origin bucket o's first descendant
+    for (uint32_t b = 0; b <= B0; b++) ostart[b] = b;
+    auto mat = [](PB& p) {
+        if (p.raw) {
+            p.h.resize(p.len);
+            for (uint32_t i = 0; i < p.len; i++) p.h[i] = p.src + i;
+            p.raw = false;
+        }
+    };
+    // IDs of old nodes, downloaded per origin bucket on first use (splits only)
+    std::vector<int> have(B0, 0);
+    std::vector<uint8_t> oid;
+    std::vector<uint32_t> oid_at(B0, 0);
+    auto id_of = [&](uint32_t h, uint32_t origin, uint8_t* out) -> int {
+        if (h & MIRROR_NEW) { std::memcpy(out, new_ids + 20ull * (h & ~MIRROR_NEW), 20); return KAD_OK; }
+        if (!have[origin]) {
+            const uint32_t a = t->h_off[origin], e = t->h_off[origin + 1];
+            std::vector<uint64_t> k(e - a);
+            std::vector<uint32_t> tl(3ull * (e - a));
+            if (e > a) {
+                HIP_TRY(hipMemcpy(k.data(), d.key + a, 8ull * (e - a), hipMemcpyDeviceToHost));
+                HIP_TRY(hipMemcpy(tl.data(), d.tail + 3ull * a, 12ull * (e - a), hipMemcpyDeviceToHost));
+            }
+            oid_at[origin] = (uint32_t)(oid.size() / 20);
+            for (uint32_t i = 0; i < e - a; i++) {
+                uint8_t b[20];
+                for (int x = 0; x < 8; x++) b[x] = (uint8_t)(k[i] >> (56 - 8 * x));
+                for (int w = 0; w < 3; w++)
+                    for (int x = 0; x < 4; x++) b[8 + 4 * w + x] = (uint8_t)(tl[3ull * i + w] >> (24 - 8 * x));
+                oid.insert(oid.end(), b, b + 20);
+            }
+            have[origin] = 1;
+        }
+        std::memcpy(out, oid.data() + 20ull * (oid_at[origin] + (h - t->h_off[origin])), 20);
+        return KAD_OK;
+    };
+    auto locate = [&](uint32_t a, uint32_t& c, uint32_t& pos) -> bool {
+        if (a >= n0) return false;
+        const uint32_t o = (uint32_t)(std::upper_bound(t->h_off.begin(), t->h_off.end(), a) - t->h_off.begin()) - 1;
+        for (c = ostart[o]; c < ostart[o + 1]; c++) {
+            PB& p = cur[c];
+            if (p.raw) {
+                if (a >= p.src && a < p.src + p.len) { pos = a - p.src; return true; }
+            } else {
+                auto it = std::find(p.h.begin(), p.h.end(), a);
+                if (it != p.h.end()) { pos = (uint32_t)(it - p.h.begin()); return true; }
+            }
+        }
+        return false;
+    };
+    const bool structural = n_ops > 0;  // node indices move: the NodeCache radix no longer applies
+    for (uint32_t k = 0; k < n_ops; k++) {
+        const uint32_t kind = ops[3ull * k], a = ops[3ull * k + 1], b = ops[3ull * k + 2];
+        uint32_t c = 0, pos = 0;
+        if (kind == KAD_OP_REMOVE || kind == KAD_OP_REPLACE) {
+            if (!locate(a, c, pos)) return set_err(KAD_ERR_INVALID, "op %u: node %u is not in the table", k, a);
+            if (kind == KAD_OP_REPLACE && b >= n_new) return set_err(KAD_ERR_INVALID, "op %u: new slot %u", k, b);
+            mat(cur[c]);
+            if (kind == KAD_OP_REMOVE) cur[c].h.erase(cur[c].h.begin() + pos);
+            else cur[c].h[pos] = MIRROR_NEW | b;
+        } else if (kind == KAD_OP_INSERT) {
+            if (a >= n_new) return set_err(KAD_ERR_INVALID, "op %u: new slot %u", k, a);
+            // RoutingTable::findBucket (routing_table.cpp:113-127): last bucket with first <= id
+            const uint8_t* id = new_ids + 20ull * a;
+            uint32_t lo = 0, hi = (uint32_t)firsts.size();
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (std::memcmp(firsts[mid].data(), id, 20) <= 0) lo = mid + 1; else hi = mid;
+            }
+            c = lo ? lo - 1 : 0;
+            mat(cur[c]);
+            cur[c].h.insert(cur[c].h.begin(), MIRROR_NEW | a);  // emplace_front (dht.cpp:934)
+        } else if (kind == KAD_OP_SPLIT) {
+            if (a >= cur.size()) return set_err(KAD_ERR_INVALID, "op %u: bucket %u of %zu", k, a, cur.size());
+            // RoutingTable::depth / middle / split (routing_table.cpp:47-65, 137-163)
+            const int b1 = lowbit20(firsts[a].data()), b2 = a + 1 < firsts.size() ? lowbit20(firsts[a + 1].data()) : -1;
+            const int depth = std::max(b1, b2) + 1;
+            if (depth >= 160) continue;  // middle() throws: split returns false
+            std::array<uint8_t, 20> mid = firsts[a];
+            mid[depth / 8] |= (uint8_t)(0x80 >> (depth % 8));
+            mat(cur[a]);
+            std::vector<uint32_t> keep, move;
+            for (uint32_t h : cur[a].h) {  // splice each node to the FRONT of its new bucket
+                uint8_t id[20];
+                int rc = id_of(h, cur[a].origin, id);
+                if (rc) return rc;
+                auto& dst = std::memcmp(id, mid.data(), 20) >= 0 ? move : keep;
+                dst.insert(dst.begin(), h);
+            }
+            PB nb{false, 0, 0, cur[a].origin, std::move(move)};
+            cur[a].h = std::move(keep);
+            cur.insert(cur.begin() + a + 1, std::move(nb));
+            firsts.insert(firsts.begin() + a + 1, mid);
+            for (uint32_t o = cur[a].origin + 1; o <= B0; o++) ostart[o]++;
+        } else {
+            return set_err(KAD_ERR_INVALID, "op %u: unknown kind %u", k, kind);
+        }
+    }
+    // window lines need every node inside its bucket's dyadic range: check the new nodes
+    bool lines_ok = (d.flags & TF_WL) && cur.size() == B0;
+    if (lines_ok) {
+        const uint64_t pre0 = d.rbase >> d.rshift;
+        for (uint32_t c = 0; c < B0 && lines_ok; c++)
+            if (!cur[c].raw)
+                for (uint32_t h : cur[c].h)
+                    if (h & MIRROR_NEW) lines_ok &= (id_hi(new_ids + 20ull * (h & ~MIRROR_NEW)) >> d.rshift) == pre0 + c;
+    }
+    // new layout
+    const uint32_t B1 = (uint32_t)cur.size();
+    std::vector<MirrorSeg> segs;
+    std::vector<uint32_t> list, off1(B1 + 1);
+    uint32_t acc = 0;
+    for (uint32_t c = 0; c < B1; c++) {
+        off1[c] = acc;
+        const PB& p = cur[c];
+        const uint32_t len = p.raw ? p.len : (uint32_t)p.h.size();
+        if (len) {
+            if (p.raw) {  // consecutive untouched buckets are one range of old nodes
+                MirrorSeg* last = segs.empty() ? nullptr : &segs.back();
+                if (last && last->kind == 0 && last->src + last->len == p.src) last->len += len;
+                else segs.push_back(MirrorSeg{acc, p.src, len, 0});
+            } else {
+                segs.push_back(MirrorSeg{acc, (uint32_t)list.size(), len, 1});
+                list.insert(list.end(), p.h.begin(), p.h.end());
+            }
+        }
+        acc += len;
+    }
+    off1[B1] = acc;
+    const uint32_t n1 = acc;
+    // new nodes' device rows
+    std::vector<uint64_t> nkey(n_new);
+    std::vector<uint32_t> ntail(3ull * n_new);
+    for (uint32_t s = 0; s < n_new; s++) {
+        nkey[s] = id_hi(new_ids + 20ull * s);
+        for (int w = 0; w < 3; w++) ntail[3ull * s + w] = id_word(new_ids + 20ull * s, 2 + w);
+    }
+    std::vector<void*> tmp;
+    uint64_t tmpb = 0;
+    auto cleanup = [&]() { for (void* p : tmp) (void)hipFree(p); };
+    MirrorSeg* dseg; uint32_t *dlist, *dntail, *dnidx; uint64_t* dnkey; uint8_t* dnst;
+    uint64_t* key1; uint32_t* tail1; uint8_t* st1;
+    int rc;
+    if ((rc = dev_upload(&dseg, segs.data(), segs.size(), tmp, tmpb)) ||
+        (rc = dev_upload(&dlist, list.data(), list.size(), tmp, tmpb)) ||
+        (rc = dev_upload(&dnkey, nkey.data(), n_new, tmp, tmpb)) ||
+        (rc = dev_upload(&dntail, ntail.data(), 3ull * n_new, tmp, tmpb)) ||
+        (rc = dev_upload(&dnst, new_status, n_new, tmp, tmpb)) || (rc = dev_upload(&dnidx, nullptr, n_new, tmp, tmpb))) {
+        cleanup();
+        return rc;
+    }
+    if ((rc = dev_upload(&key1, nullptr, n1 + KEY_PAD, t->owned, t->bytes)) ||
+        (rc = dev_upload(&tail1, nullptr, 3ull * n1, t->owned, t->bytes)) ||
+        (rc = dev_upload(&st1, nullptr, n1, t->owned, t->bytes))) {
+        cleanup();
+        return rc;
+    }
+    if (hipMemset(key1, 0xFF, 8ull * (n1 + KEY_PAD)) != hipSuccess || hipMemset(dnidx, 0xFF, 4ull * n_new) != hipSuccess ||
+        (remap && n0 && hipMemset(remap, 0xFF, 4ull * n0) != hipSuccess)) {
+        cleanup();
+        return set_err(KAD_ERR_HIP, "hipMemset failed");
+    }
+    if (n1)
+        hipLaunchKernelGGL(mirror_gather_kernel, dim3(grid_for(n1)), dim3(BLOCK), 0, 0, dseg, (uint32_t)segs.size(), dlist, n1,
+                           d.key, d.tail, d.status, dnkey, dntail, dnst, key1, tail1, st1, remap, dnidx);
+    if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+        cleanup();
+        return set_err(KAD_ERR_HIP, "mirror gather failed");
+    }
+    if (new_index && n_new && hipMemcpy(new_index, dnidx, 4ull * n_new, hipMemcpyDeviceToHost) != hipSuccess) {
+        cleanup();
+        return set_err(KAD_ERR_HIP, "copy of new indices failed");
+    }
+    cleanup();
+    release(t, const_cast<uint64_t*>(d.key));
+    release(t, const_cast<uint32_t*>(d.tail));
+    release(t, t->status_mut);
+    d.key = key1; d.tail = tail1; d.status = st1; t->status_mut = st1; d.n = n1;
+    // derived state that no longer matches the nodes: NodeCache order, wire records, node times
+    if (structural) {
+        t->flags &= ~KAD_TABLE_SORTED;
+        release(t, const_cast<uint32_t*>(d.nrdx)); d.nrdx = nullptr; t->nbits = 0;
+    }
+    release(t, t->wrec); t->wrec = nullptr; t->addr_len = 0;
+    release(t, t->time_ns); release(t, t->reply_ns); release(t, t->expired);
+    t->time_ns = nullptr; t->reply_ns = nullptr; t->expired = nullptr;
+    // bucket directory
+    t->h_off = off1;
+    t->h_first.resize(20ull * B1);
+    for (uint32_t c = 0; c < B1; c++) std::memcpy(t->h_first.data() + 20ull * c, firsts[c].data(), 20);
+    std::vector<uint2> dir(B1 + 1);
+    for (uint32_t c = 0; c <= B1; c++) {
+        dir[c].x = off1[c] | (c < B1 && off1[c + 1] - off1[c] > 32 ? WIDE : 0u);
+        dir[c].y = 0;
+    }
+    if (B1 != B0) {
+        release(t, t->dir_mut); release(t, t->gpre_mut);
+        release(t, t->scan_cnt); release(t, t->scan_part); release(t, t->scan_sums);
+        uint2* ddir; uint32_t* dgp;
+        if ((rc = dev_upload(&ddir, nullptr, B1 + 1, t->owned, t->bytes)) ||
+            (rc = dev_upload(&dgp, nullptr, B1 + 1, t->owned, t->bytes)) ||
+            (rc = dev_upload(&t->scan_cnt, nullptr, B1 + 1, t->owned, t->bytes)) ||
+            (rc = dev_upload(&t->scan_part, nullptr, B1 + 1, t->owned, t->bytes)) ||
+            (rc = dev_upload(&t->scan_sums, nullptr, (B1 + 1 + SCAN_TILE - 1) / SCAN_TILE, t->owned, t->bytes)))
+            return rc;
+        d.dir = ddir; t->dir_mut = ddir; d.gpre = dgp; t->gpre_mut = dgp; d.B = B1;
+        if ((rc = build_bucket_index(t))) return rc;
+        // a split breaks the uniform depth the window lines need
+        release(t, t->wl_mut); t->wl_mut = nullptr; d.wl = nullptr; d.flags &= ~TF_WL;
+    }
+    if (!lines_ok && t->wl_mut) {
+        release(t, t->wl_mut); t->wl_mut = nullptr; d.wl = nullptr; d.flags &= ~TF_WL;
+    }
+    HIP_TRY(hipMemcpy(t->dir_mut, dir.data(), 8ull * (B1 + 1), hipMemcpyHostToDevice));
+    // duplicate top-64 masks
+    release(t, const_cast<uint32_t*>(d.dmask)); d.dmask = nullptr; d.flags &= ~TF_HAS_DUP;
+    bool low_zero = true;
+    for (uint32_t c = 0; c < B1 && low_zero; c++) low_zero = id_low_zero(t->h_first.data() + 20ull * c);
+    uint32_t* ddm;
+    if ((rc = dev_upload(&ddm, nullptr, B1, t->owned, t->bytes))) return rc;
+    uint32_t* dany;
+    HIP_TRY(hipMalloc(&dany, 4));
+    (void)hipMemset(dany, 0, 4);
+    uint32_t any = 0;
+    if (low_zero) {
+        hipLaunchKernelGGL(mirror_dmask_kernel, dim3(grid_for(B1)), dim3(BLOCK), 0, 0, d.key, t->dir_mut, B1, ddm, dany);
+        (void)hipMemcpy(&any, dany, 4, hipMemcpyDeviceToHost);
+    } else {  // a bucket first below 64-bit granularity: flag every node (exact path, always correct)
+        (void)hipMemset(ddm, 0xFF, 4ull * B1);
+        any = 1;
+    }
+    (void)hipFree(dany);
+    d.dmask = ddm;
+    if (any) d.flags |= TF_HAS_DUP;
+    // masks, good prefix sums, window lines
+    if ((rc = rebuild_good_prefix(t, nullptr))) return rc;
+    HIP_TRY(hipDeviceSynchronize());
+    return KAD_OK;
+}
+
+int kad_table_export(const kad_table* t, uint8_t* ids, uint8_t* status, uint8_t* bucket_first, uint32_t* bucket_offset) {
+    if (!t) return set_err(KAD_ERR_INVALID, "NULL table");
+    DeviceGuard g(t->device);
+    const uint32_t n = t->d.n, B = t->d.B;
+    if (ids && n) {
+        std::vector<uint64_t> k(n);
+        std::vector<uint32_t> tl(3ull * n);
+        HIP_TRY(hipMemcpy(k.data(), t->d.key, 8ull * n, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(tl.data(), t->d.tail, 12ull * n, hipMemcpyDeviceToHost));
+        for (uint32_t i = 0; i < n; i++) {
+            uint8_t* b = ids + 20ull * i;
+            for (int x = 0; x < 8; x++) b[x] = (uint8_t)(k[i] >> (56 - 8 * x));
+            for (int w = 0; w < 3; w++)
+                for (int x = 0; x < 4; x++) b[8 + 4 * w + x] = (uint8_t)(tl[3ull * i + w] >> (24 - 8 * x));
+        }
+    }
+    if (status && n) HIP_TRY(hipMemcpy(status, t->d.status, n, hipMemcpyDeviceToHost));
+    if (bucket_first && B) std::memcpy(bucket_first, t->h_first.data(), 20ull * B);
+    if (bucket_offset && B) std::memcpy(bucket_offset, t->h_off.data(), 4ull * (B + 1));
+    return KAD_OK;
+}
+
+}  // extern "C"
+

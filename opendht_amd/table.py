@@ -109,6 +109,31 @@ class DeviceTable:
         check(lib().kad_table_refresh_status(self._h, C.c_int64(now_ns), _stream_of(self, stream)),
               "kad_table_refresh_status")
 
+    def apply(self, ops, new_ids=None, new_status=None, remap=None):
+        """Incremental mirror (kad_table_apply): ops (m, 3) uint32 rows (kind, a, b). Returns the new
+        nodes' indices (host uint32); `remap` (device int32 tensor, old n) receives every old node's
+        new index."""
+        ops = np.ascontiguousarray(ops, dtype=np.uint32).reshape(-1, 3)
+        nid = _as_ids(new_ids) if new_ids is not None and len(new_ids) else np.zeros((0, 20), np.uint8)
+        nst = np.ascontiguousarray(new_status if new_status is not None else np.zeros(0), dtype=np.uint8)
+        out = np.zeros(max(nid.shape[0], 1), np.uint32)
+        check(lib().kad_table_apply(self._h, ptr(ops), ops.shape[0], ptr(nid), ptr(nst), nid.shape[0], ptr(remap),
+                                    ptr(out)), "kad_table_apply")
+        inf = self.info()
+        self.n, self.B = inf["n_nodes"], inf["n_buckets"]
+        return out[:nid.shape[0]]
+
+    def export(self):
+        """(ids, status, bucket_first, bucket_offset) host arrays of the device table."""
+        inf = self.info()
+        n, B = inf["n_nodes"], inf["n_buckets"]
+        ids = np.zeros((max(n, 1), 20), np.uint8)
+        st = np.zeros(max(n, 1), np.uint8)
+        first = np.zeros((max(B, 1), 20), np.uint8)
+        off = np.zeros(B + 1, np.uint32)
+        check(lib().kad_table_export(self._h, ptr(ids), ptr(st), ptr(first), ptr(off)), "kad_table_export")
+        return ids[:n], st[:n], first[:B], off
+
     def set_addrs(self, addrs) -> None:
         """Node address records (n, 6) for IPv4 (in_addr + port bytes) or (n, 18) for IPv6."""
         addrs = np.ascontiguousarray(addrs, dtype=np.uint8)

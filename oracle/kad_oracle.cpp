@@ -832,3 +832,70 @@ extern "C" int orc_infohash_get(uint32_t n, const uint8_t* data, const uint64_t*
     for (uint32_t i = 0; i < n; i++) sha1(data + off[i], off[i + 1] - off[i], out + (size_t)HASH_LEN * i);
     return 0;
 }
+
+// ---------------------------------------------------------------------------
+// Incremental mirror ops on the structure-faithful table. Ops are applied in
+// order; node operands are indices of the table at the batch start, `slot` operands index the
+// batch's new nodes:
+//   REMOVE  a     the old node a leaves its bucket (Dht::expireBuckets remove_if, dht.cpp:942-956)
+//   REPLACE a s   new node s takes old node a's place (onNewNode's expired replacement, dht.cpp:917-921)
+//   INSERT  s     new node s is emplace_front'ed into findBucket(id) (dht.cpp:934)
+//   SPLIT   b     RoutingTable::split of the bucket at current index b (routing_table.cpp:137-163)
+// Then the table is written out: ids/status in bucket then list order, firsts, offsets, the new
+// index of every old node (NO_NODE if removed or replaced) and of every new node.
+// ---------------------------------------------------------------------------
+extern "C" int orc_table_apply(void* h, uint32_t n_ops, const uint32_t* ops, uint32_t n_new, const uint8_t* new_ids,
+                               const uint8_t* new_status, uint32_t* out_n, uint32_t* out_B, uint8_t* out_ids,
+                               uint8_t* out_status, uint8_t* out_first, uint32_t* out_off, uint32_t* out_remap,
+                               uint32_t* out_new_idx) {
+    auto* T = (FaithfulTable*)h;
+    const uint32_t n_old = (uint32_t)T->all.size();
+    std::vector<std::shared_ptr<Node>> fresh(n_new);
+    for (uint32_t s = 0; s < n_new; s++) {
+        fresh[s] = std::make_shared<Node>();
+        fresh[s]->id = Id(new_ids + (size_t)s * HASH_LEN);
+        fresh[s]->idx = n_old + s;
+        apply_status(*fresh[s], new_status[s], T->now);
+    }
+    auto locate = [&](uint32_t old) {  // (bucket, node) iterators of an old node
+        for (auto b = T->rt.begin(); b != T->rt.end(); ++b)
+            for (auto n = b->nodes.begin(); n != b->nodes.end(); ++n)
+                if ((*n)->idx == old) return std::make_pair(b, n);
+        return std::make_pair(T->rt.end(), std::list<std::shared_ptr<Node>>::iterator());
+    };
+    for (uint32_t o = 0; o < n_ops; o++) {
+        const uint32_t kind = ops[3 * o], a = ops[3 * o + 1], b = ops[3 * o + 2];
+        if (kind == 1) {  // REMOVE
+            auto p = locate(a);
+            if (p.first != T->rt.end()) p.first->nodes.erase(p.second);
+        } else if (kind == 2) {  // REPLACE
+            auto p = locate(a);
+            if (p.first != T->rt.end()) *p.second = fresh[b];
+        } else if (kind == 3) {  // INSERT
+            auto bk = T->rt.findBucket(fresh[a]->id);
+            if (bk != T->rt.end()) bk->nodes.emplace_front(fresh[a]);
+        } else if (kind == 4) {  // SPLIT
+            auto bk = T->rt.begin();
+            std::advance(bk, a);
+            T->rt.split(bk);
+        }
+    }
+    for (uint32_t i = 0; i < n_old; i++) out_remap[i] = 0xFFFFFFFFu;
+    for (uint32_t s = 0; s < n_new; s++) out_new_idx[s] = 0xFFFFFFFFu;
+    uint32_t k = 0, B = 0;
+    for (auto& bk : T->rt) {
+        std::memcpy(out_first + (size_t)B * HASH_LEN, bk.first.data(), HASH_LEN);
+        out_off[B++] = k;
+        for (auto& nd : bk.nodes) {
+            std::memcpy(out_ids + (size_t)k * HASH_LEN, nd->id.data(), HASH_LEN);
+            out_status[k] = (nd->isExpired() ? 2 : 0) | (nd->isGood(T->now) ? 1 : 0);
+            if (nd->idx < n_old) out_remap[nd->idx] = k;
+            else out_new_idx[nd->idx - n_old] = k;
+            k++;
+        }
+    }
+    out_off[B] = k;
+    *out_n = k;
+    *out_B = B;
+    return 0;
+}

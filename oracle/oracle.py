@@ -41,6 +41,7 @@ _SIG = {
     "orc_is_martian": (C.c_int, [_P, C.c_uint32]),
     "orc_parse_nodes": (C.c_int, [C.c_uint32, _P, C.c_uint32, _P, _P]),
     "orc_infohash_get": (C.c_int, [C.c_uint32, _P, _P, _P]),
+    "orc_table_apply": (C.c_int, [_P, C.c_uint32, _P, C.c_uint32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "orc_swarm_build": (_P, [C.c_uint32, _P, C.c_int]),
     "orc_swarm_free": (None, [_P]),
     "orc_swarm_table": (None, [_P, C.c_uint32, _P, _P, _P]),
@@ -158,6 +159,28 @@ class FaithfulTable:
         cnt = np.empty((q,), dtype=np.uint8)
         lib().orc_table_nc_closest(self._h, q, _p(t), count, _p(idx), _p(cnt), nthreads)
         return idx, cnt
+
+    def apply(self, ops, new_ids, new_status):
+        """Mirror ops (kad_oracle.cpp "Incremental mirror ops"): ops (m, 3) uint32 rows (kind, a, b),
+        kinds 1 REMOVE, 2 REPLACE, 3 INSERT, 4 SPLIT. Returns the table written out:
+        (ids, status, firsts, offsets, remap of old nodes, indices of new nodes)."""
+        ops = np.ascontiguousarray(ops, dtype=np.uint32).reshape(-1, 3)
+        new_ids = _ids(new_ids) if len(new_ids) else np.zeros((0, 20), np.uint8)
+        new_status = np.ascontiguousarray(new_status, dtype=np.uint8)
+        n_old = self.ids.shape[0]
+        cap = n_old + new_ids.shape[0]
+        ids = np.zeros((max(cap, 1), 20), np.uint8)
+        st = np.zeros(max(cap, 1), np.uint8)
+        first = np.zeros((cap + ops.shape[0] + 2, 20), np.uint8)
+        off = np.zeros(cap + ops.shape[0] + 3, np.uint32)
+        remap = np.zeros(max(n_old, 1), np.uint32)
+        nidx = np.zeros(max(new_ids.shape[0], 1), np.uint32)
+        n, B = C.c_uint32(), C.c_uint32()
+        lib().orc_table_apply(self._h, ops.shape[0], _p(ops), new_ids.shape[0], _p(new_ids), _p(new_status),
+                              C.byref(n), C.byref(B), _p(ids), _p(st), _p(first), _p(off), _p(remap), _p(nidx))
+        n, B = n.value, B.value
+        return (ids[:n].copy(), st[:n].copy(), first[:B].copy(), off[:B + 1].copy(), remap[:n_old].copy(),
+                nidx[:new_ids.shape[0]].copy())
 
     def find_bucket(self, targets):
         t = _ids(targets)
