@@ -69,6 +69,7 @@ def main():
     ap.add_argument("--queries", type=int, default=1 << 20, help="queries per GPU per step")
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU baseline sampling")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-graph", action="store_true", help="issue the K steps one by one instead of one HIP graph")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
     ap.add_argument("--mode", choices=("owner", "allgather"), default="owner",
                     help="owner: weak scaling, owner-routed shards with halo (the headline); allgather: the "
@@ -115,20 +116,45 @@ def main():
         T.rt_closest(tg, args.count, out_idx, out_cnt, stream=stream.cuda_stream)
     torch.cuda.synchronize(dev)
 
+    # The K steps go out as one HIP graph of K launches (the step is ~30 us; issuing them one by one
+    # from Python leaves ~3 us gaps). --no-graph issues them one by one with an event per step.
+    graph = None
+    if not args.no_graph:
+        try:
+            g = torch.cuda.CUDAGraph()
+            cs = torch.cuda.Stream(dev)
+            cs.wait_stream(stream)
+            with torch.cuda.graph(g, stream=cs):
+                for _ in range(args.steps):
+                    T.rt_closest(tg, args.count, out_idx, out_cnt, stream=cs.cuda_stream)
+            stream.wait_stream(cs)
+            g.replay()  # untimed: the graph's first launch uploads it
+            torch.cuda.synchronize(dev)
+            graph = g
+        except Exception as e:  # capture unsupported: fall back to eager launches
+            print(f"graph capture failed ({e}); eager launches", file=sys.stderr)
+            graph = None
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     if dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t_start = time.perf_counter()
     ev[0].record(stream)
-    for i in range(args.steps):
-        T.rt_closest(tg, args.count, out_idx, out_cnt, stream=stream.cuda_stream)
-        ev[i + 1].record(stream)
+    if graph is not None:
+        graph.replay()
+        ev[-1].record(stream)
+    else:
+        for i in range(args.steps):
+            T.rt_closest(tg, args.count, out_idx, out_cnt, stream=stream.cuda_stream)
+            ev[i + 1].record(stream)
     torch.cuda.synchronize(dev)
     if dist:
         dist.barrier()
     wall = time.perf_counter() - t_start
-    kern_ms = [ev[i].elapsed_time(ev[i + 1]) for i in range(args.steps)]
+    if graph is not None:
+        kern_ms = [ev[0].elapsed_time(ev[-1]) / args.steps]
+    else:
+        kern_ms = [ev[i].elapsed_time(ev[i + 1]) for i in range(args.steps)]
     t_max = wall
     if dist:
         x = torch.tensor([wall], dtype=torch.float64, device=dev)
@@ -183,6 +209,7 @@ def main():
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
                 "kernel": kernel,
+                "launch": "hip graph of K launches" if graph is not None else "K eager launches",
                 "avg_kernel_ms": avg_kernel_s * 1e3,
                 "alg_bytes_per_launch": alg_bytes,
                 "alg_bytes_per_query": alg_bytes / args.queries,
