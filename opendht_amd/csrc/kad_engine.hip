@@ -90,7 +90,8 @@ struct DevTable {
     const uint32_t* ftail;
     const uint32_t* rrdx;
     const uint32_t* nrdx;
-    const uint4* wl;  // window lines (TF_WL): 128 bytes per bucket, see rt_wl_kernel
+    const uint4* wl;    // window lines (TF_WL): 128 bytes per bucket, see rt_wl_kernel
+    const uint4* wl16;  // window lines for counts 9..16 (TF_WL16): 256 bytes per bucket
     uint64_t rbase, nbase;
     uint32_t rshift, rslots, nshift, nslots;
     uint32_t n, B, index_base, flags;
@@ -99,6 +100,7 @@ struct DevTable {
 constexpr uint32_t TF_DIRECT = 1u;   // radix slot s holds exactly bucket s (no locate load)
 constexpr uint32_t TF_HAS_DUP = 2u;  // some nodes share their top 64 ID bits
 constexpr uint32_t TF_WL = 8u;       // window lines present (direct-mapped, uniform depth 1..43)
+constexpr uint32_t TF_WL16 = 16u;    // window lines for counts 9..16 present
 constexpr uint32_t WIDE = 0x80000000u;  // dir[].x flag: bucket holds > 32 nodes (masks invalid)
 constexpr uint32_t KEY_PAD = 32;        // key[] is padded so 16-node chunk loads never leave it
 
@@ -810,6 +812,180 @@ __global__ void wl_build_kernel(const uint64_t* key, const uint8_t* status, cons
     L[0] = base;
     L[1] = h | (R8 << 21) | (S << 23) | (defer ? WL_DEFER : 0u);
     L[2] = rounds;
+}
+
+// ---------------------------------------------------------------------------------------
+// Window lines for 9 <= count <= 16 (TF_WL16): the same construction as the count <= 8 lines with
+// R_16 <= 3 (windows of up to 8 buckets) and 32 slots, so a line is 36 dwords (two 128-byte lines
+// per bucket at a 256-byte stride):
+//   dw0      base (first node of W(R_16)'s lowest bucket)
+//   dw1      G(r) for r = 0..3 (6 bits each) | whole(r) << (24+r) | R_16 << 28 | defer << 31
+//   dw2      round of the bucket of D rank j, 2 bits each (j < 8)
+//   dw3      S (stored slots, whole buckets only, <= 32)
+//   dw4..35  slots: jd << 29 | key21 << 8 | off
+// The 16 smallest of the 32 rank values (two sorted groups of 16 by Batcher's network, one bitonic
+// merge) are the answer when the slots hold the first m of W(R_c)'s nodes: the bucket holding output
+// 15 starts before slot 16 and holds at most 16 good nodes.
+// ---------------------------------------------------------------------------------------
+constexpr uint32_t WL16_SLOTS = 32, WL16_STRIDE = 64;  // dwords
+
+// Batcher's odd-even merge sort for 16 inputs (63 comparators; tests/test_networks.py).
+constexpr int SORT16_LEN = 63;
+__device__ constexpr uint8_t SORT16[SORT16_LEN][2] = {
+    {0, 1}, {2, 3}, {0, 2}, {1, 3}, {1, 2}, {4, 5}, {6, 7}, {4, 6}, {5, 7}, {5, 6}, {0, 4}, {2, 6}, {2, 4},
+    {1, 5}, {3, 7}, {3, 5}, {1, 2}, {3, 4}, {5, 6}, {8, 9}, {10, 11}, {8, 10}, {9, 11}, {9, 10}, {12, 13}, {14, 15},
+    {12, 14}, {13, 15}, {13, 14}, {8, 12}, {10, 14}, {10, 12}, {9, 13}, {11, 15}, {11, 13}, {9, 10}, {11, 12},
+    {13, 14}, {0, 8}, {4, 12}, {4, 8}, {2, 10}, {6, 14}, {6, 10}, {2, 4}, {6, 8}, {10, 12}, {1, 9}, {5, 13},
+    {5, 9}, {3, 11}, {7, 15}, {7, 11}, {3, 5}, {7, 9}, {11, 13}, {1, 2}, {3, 4}, {5, 6}, {7, 8}, {9, 10},
+    {11, 12}, {13, 14}};
+
+__device__ __forceinline__ void sort16(uint32_t* v) {
+#pragma unroll
+    for (int c = 0; c < SORT16_LEN; c++) cx(v[SORT16[c][0]], v[SORT16[c][1]]);
+}
+
+// a = the 16 smallest of (a, s), sorted; a and s sorted ascending on entry.
+__device__ __forceinline__ void merge16(uint32_t* a, const uint32_t* s) {
+#pragma unroll
+    for (int i = 0; i < 16; i++) a[i] = min(a[i], s[15 - i]);
+#pragma unroll
+    for (int w = 8; w >= 1; w >>= 1)
+#pragma unroll
+        for (int i = 0; i < 16; i++)
+            if ((i & w) == 0) cx(a[i], a[i + w]);
+}
+
+__device__ __forceinline__ bool wl16_answer(const DevTable& T, const Target& t, uint32_t b, uint32_t count, bool act,
+                                            uint32_t (&o)[16], uint32_t& m) {
+    uint32_t L[4 + WL16_SLOTS];
+    if (act) {
+        const uint4* lp = T.wl16 + (WL16_STRIDE / 4) * (size_t)b;
+#pragma unroll
+        for (int x = 0; x < (int)(4 + WL16_SLOTS) / 4; x++) {
+            const uint4 q = lp[x];
+            L[4 * x] = q.x; L[4 * x + 1] = q.y; L[4 * x + 2] = q.z; L[4 * x + 3] = q.w;
+        }
+    } else {
+#pragma unroll
+        for (int x = 0; x < (int)(4 + WL16_SLOTS); x++) L[x] = NONE;
+    }
+    const uint32_t d = 64 - T.rshift;
+    const uint32_t h = L[1], rounds = L[2], S = L[3] & 63u, R16 = (h >> 28) & 3u;
+    uint32_t G[4];
+#pragma unroll
+    for (int r = 0; r < 4; r++) G[r] = (h >> (6 * r)) & 63u;
+    uint32_t Rc = 3;
+#pragma unroll
+    for (int r = 3; r >= 0; r--)
+        if (G[r] >= count || ((h >> (24 + r)) & 1u)) Rc = (uint32_t)r;
+    m = min(count, Rc == 0 ? G[0] : Rc == 1 ? G[1] : Rc == 2 ? G[2] : G[3]);
+    const bool own = (t.hi >> T.rshift) == (T.rbase >> T.rshift) + b;
+    bool ex = !act || (h & WL_DEFER) || !own || Rc > R16 || (Rc == R16 && S < m);
+    const uint32_t tx = (uint32_t)((t.hi << d) >> (64 - WL_KBITS)) << 8;
+    uint32_t v[WL16_SLOTS];
+#pragma unroll  // empty slots must stay last: with D rank 7 a real value can exceed NONE ^ tx
+    for (int s = 0; s < (int)WL16_SLOTS; s++) v[s] = (uint32_t)s < S ? L[4 + s] ^ tx : NONE;
+    if (__any(!ex && Rc < R16)) {  // a smaller window: drop the later rounds' buckets
+        uint32_t inc = 0;
+#pragma unroll
+        for (int j = 0; j < 8; j++) inc |= (((rounds >> (2 * j)) & 3u) <= Rc ? 1u : 0u) << j;
+        uint32_t have = 0;
+#pragma unroll
+        for (int s = 0; s < (int)WL16_SLOTS; s++) {
+            const bool in = (uint32_t)s < S && ((inc >> (v[s] >> 29)) & 1u);
+            v[s] = in ? v[s] : NONE;
+            have += in;
+        }
+        ex |= have < m;
+    }
+    sort16(v);
+    sort16(v + 16);
+    merge16(v, v + 16);
+    const uint32_t base = L[0] + T.index_base;
+#pragma unroll
+    for (int j = 0; j < 16; j++) o[j] = (uint32_t)j < m ? base + (v[j] & 255u) : NONE;
+    return !ex;
+}
+
+__global__ __launch_bounds__(BLOCK) void rt_wl16_kernel(DevTable T, const uint8_t* __restrict__ targets, uint32_t q,
+                                                        uint32_t count, uint32_t* __restrict__ out_idx,
+                                                        uint8_t* __restrict__ out_cnt) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    const bool act = i < q;
+    Target t{};
+    uint32_t b = 0;
+    if (act) {
+        t = load_target(targets, i);
+        b = locate_bucket(T, t);
+    }
+    uint32_t o[16], m;
+    const bool ok = wl16_answer(T, t, b, count, act, o, m);
+    if (act && ok) {
+        uint32_t* row = out_idx + (size_t)i * count;
+        if (count == 16 && ((uintptr_t)row & 15u) == 0) {
+#pragma unroll
+            for (int x = 0; x < 4; x++)
+                reinterpret_cast<uint4*>(row)[x] = make_uint4(o[4 * x], o[4 * x + 1], o[4 * x + 2], o[4 * x + 3]);
+        } else if ((count & 1u) == 0 && ((uintptr_t)row & 7u) == 0) {  // e.g. SEARCH_NODES = 14
+#pragma unroll
+            for (int x = 0; x < 8; x++)
+                if ((uint32_t)(2 * x) < count) reinterpret_cast<uint2*>(row)[x] = make_uint2(o[2 * x], o[2 * x + 1]);
+        } else {
+#pragma unroll
+            for (int j = 0; j < 16; j++)
+                if ((uint32_t)j < count) row[j] = o[j];
+        }
+        if (out_cnt) out_cnt[i] = (uint8_t)m;
+    }
+    __shared__ uint64_t xs[BLOCK / 64][192];
+    exact_tail(T, t, act && !ok, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
+}
+
+// Window lines for counts 9..16 after a status change (or at creation): one thread per bucket.
+__global__ void wl16_build_kernel(const uint64_t* key, const uint8_t* status, const uint2* dir, const uint32_t* gpre,
+                                  uint32_t B, uint32_t d, uint64_t pre0, uint32_t* lines) {
+    const uint32_t b = blockIdx.x * BLOCK + threadIdx.x;
+    if (b >= B) return;
+    uint32_t* L = lines + (size_t)WL16_STRIDE * b;
+    for (uint32_t k = 0; k < 4 + WL16_SLOTS; k++) L[k] = NONE;
+    uint32_t h = 0, R = 4;
+    for (uint32_t r = 0; r < 4; r++) {
+        const uint32_t lo = b > r ? b - 1 - r : 0u, hi = min(B - 1, b + r);
+        const uint32_t g = gpre[hi + 1] - gpre[lo];
+        const bool whole = lo == 0 && hi == B - 1;
+        h |= (min(g, 63u) << (6 * r)) | ((whole ? 1u : 0u) << (24 + r));
+        if (R == 4 && (g >= 16 || whole)) R = r;
+    }
+    if (R == 4) { L[1] = WL_DEFER; return; }
+    const uint32_t lo = b > R ? b - 1 - R : 0u, hi = min(B - 1, b + R), nb = hi - lo + 1;
+    const uint32_t base = dir[lo].x & ~WIDE;
+    uint32_t rounds = 0, S = 0;
+    bool defer = false, full = false;
+    for (uint32_t j = 0; j < nb; j++) {  // buckets in D order
+        uint32_t x = lo;
+        for (uint32_t y = lo; y <= hi; y++) {
+            uint32_t rk = 0;
+            for (uint32_t z = lo; z <= hi; z++) rk += ((pre0 + z) ^ (pre0 + b)) < ((pre0 + y) ^ (pre0 + b));
+            if (rk == j) x = y;
+        }
+        rounds |= (x >= b ? x - b : b - 1 - x) << (2 * j);
+        const uint32_t j0 = dir[x].x & ~WIDE, j1 = dir[x + 1].x & ~WIDE;
+        const uint32_t g = gpre[x + 1] - gpre[x];
+        if (full || S + g > WL16_SLOTS) { full = true; continue; }
+        const uint32_t s0 = S;
+        for (uint32_t n = j0; n < j1; n++) {
+            if (!(status[n] & KAD_STATUS_GOOD)) continue;
+            const uint32_t k21 = (uint32_t)((key[n] << d) >> (64 - WL_KBITS)), off = n - base;
+            defer |= off > 255u;
+            for (uint32_t s = s0; s < S; s++) defer |= ((L[4 + s] >> 8) & ((1u << WL_KBITS) - 1)) == k21;
+            L[4 + S] = (j << 29) | (k21 << 8) | (off & 255u);
+            S++;
+        }
+    }
+    L[0] = base;
+    L[1] = h | (R << 28) | (defer ? WL_DEFER : 0u);
+    L[2] = rounds;
+    L[3] = S;
 }
 
 template <int K>
@@ -1632,6 +1808,7 @@ struct kad_table {
     uint2* dir_mut = nullptr;
     uint32_t* gpre_mut = nullptr;
     uint32_t* wl_mut = nullptr;
+    uint32_t* wl16_mut = nullptr;
     // host copies of the bucket directory, for the incremental mirror (kad_table_apply)
     std::vector<uint32_t> h_off;
     std::vector<uint8_t> h_first;
@@ -1669,6 +1846,9 @@ int rebuild_good_prefix(kad_table* t, hipStream_t s) {
     if (t->wl_mut)
         hipLaunchKernelGGL(wl_build_kernel, dim3(grid_for(B)), dim3(BLOCK), 0, s, t->d.key, t->d.status, t->d.dir,
                            t->d.gpre, B, 64 - t->d.rshift, t->d.rbase >> t->d.rshift, t->wl_mut);
+    if (t->wl16_mut)
+        hipLaunchKernelGGL(wl16_build_kernel, dim3(grid_for(B)), dim3(BLOCK), 0, s, t->d.key, t->d.status, t->d.dir,
+                           t->d.gpre, B, 64 - t->d.rshift, t->d.rbase >> t->d.rshift, t->wl16_mut);
     HIP_TRY(hipGetLastError());
     return KAD_OK;
 }
@@ -1692,6 +1872,8 @@ int launch_rt(const kad_table* t, const uint8_t* targets, uint32_t q, uint32_t c
             hipLaunchKernelGGL(rt_wl_kernel<2>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
         else
             hipLaunchKernelGGL(rt_wl_kernel<0>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
+    } else if (K == 16 && (d.flags & TF_WL16) && !(ev && std::strcmp(ev, "lane") == 0)) {
+        hipLaunchKernelGGL(rt_wl16_kernel, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
     } else {
         hipLaunchKernelGGL(rt_closest_kernel<K>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
     }
@@ -1922,6 +2104,20 @@ int kad_table_create(kad_table** out, int device, uint32_t n_nodes, const uint8_
                 d.wl = reinterpret_cast<const uint4*>(lp);
                 t->wl_mut = lp;
                 d.flags |= TF_WL;
+                uint32_t* lp16;
+                if ((rc = dev_upload(&lp16, nullptr, (size_t)WL16_STRIDE * n_buckets, t->owned, t->bytes))) {
+                    delete t;
+                    return rc;
+                }
+                hipLaunchKernelGGL(wl16_build_kernel, dim3(grid_for(n_buckets)), dim3(BLOCK), 0, 0, d.key, d.status, d.dir,
+                                   d.gpre, n_buckets, depth, pre0, lp16);
+                if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+                    delete t;
+                    return set_err(KAD_ERR_HIP, "window-line (16) build failed");
+                }
+                d.wl16 = reinterpret_cast<const uint4*>(lp16);
+                t->wl16_mut = lp16;
+                d.flags |= TF_WL16;
             }
         }
     }
@@ -2561,9 +2757,12 @@ int kad_table_apply(kad_table* t, const uint32_t* ops, uint32_t n_ops, const uin
         if ((rc = build_bucket_index(t))) return rc;
         // a split breaks the uniform depth the window lines need
         release(t, t->wl_mut); t->wl_mut = nullptr; d.wl = nullptr; d.flags &= ~TF_WL;
+        release(t, t->wl16_mut); t->wl16_mut = nullptr; d.wl16 = nullptr; d.flags &= ~TF_WL16;
+        release(t, t->wl16_mut); t->wl16_mut = nullptr; d.wl16 = nullptr; d.flags &= ~TF_WL16;
     }
     if (!lines_ok && t->wl_mut) {
         release(t, t->wl_mut); t->wl_mut = nullptr; d.wl = nullptr; d.flags &= ~TF_WL;
+        release(t, t->wl16_mut); t->wl16_mut = nullptr; d.wl16 = nullptr; d.flags &= ~TF_WL16;
     }
     HIP_TRY(hipMemcpy(t->dir_mut, dir.data(), 8ull * (B1 + 1), hipMemcpyHostToDevice));
     // duplicate top-64 masks

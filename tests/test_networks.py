@@ -11,13 +11,17 @@ import numpy as np
 SRC = os.path.join(os.path.dirname(__file__), "..", "opendht_amd", "csrc", "kad_engine.hip")
 
 
-def _sort8():
+def _net(name):
     s = open(SRC).read()
-    m = re.search(r"SORT8\[SORT8_LEN\]\[2\]\s*=\s*\{(.*?)\};", s, re.S)
+    m = re.search(name + r"\[" + name + r"_LEN\]\[2\]\s*=\s*\{(.*?)\};", s, re.S)
     pairs = [tuple(map(int, p)) for p in re.findall(r"\{(\d+),\s*(\d+)\}", m.group(1))]
-    n = int(re.search(r"SORT8_LEN = (\d+);", s).group(1))
+    n = int(re.search(name + r"_LEN = (\d+);", s).group(1))
     assert len(pairs) == n
     return pairs
+
+
+def _sort8():
+    return _net("SORT8")
 
 
 def _apply(net, v):
@@ -66,3 +70,27 @@ def test_top8_of_24():
         g = [_apply(net, v[i:i + 8]) for i in (0, 8, 16)]
         acc = _merge8(_merge8(g[0], g[1]), g[2])
         assert acc == sorted(v)[:8]
+
+
+def test_sort16_sorts_all_01_inputs():
+    net = _net("SORT16")
+    assert all(a < b for a, b in net)
+    for x in range(1 << 16):
+        bits = [(x >> i) & 1 for i in range(16)]
+        assert _apply(net, bits) == sorted(bits), bits
+
+
+def _merge16(a, s):
+    """merge16 of kad_engine.hip."""
+    a = [min(a[i], s[15 - i]) for i in range(16)]
+    net = [(i, i + w) for w in (8, 4, 2, 1) for i in range(16) if (i & w) == 0]
+    return _apply(net, a)
+
+
+def test_top16_of_32():
+    net = _net("SORT16")
+    rnd = random.Random(12)
+    for _ in range(2000):
+        v = rnd.sample(range(1 << 20), 32)
+        acc = _merge16(_apply(net, v[:16]), _apply(net, v[16:]))
+        assert acc == sorted(v)[:16]
