@@ -131,41 +131,48 @@ def build_shard(spec: ShardSpec, s: int, probe: int = 64) -> Shard:
 
 
 def route_queries(targets, spec: ShardSpec, group=None):
-    """Serving-mode exchange: send each target to its owner shard (top bits), one rank per shard,
-    via torch.distributed all_to_all; returns (local_targets, recv_splits, send_order) so the
-    answers can be sent back with ``return_results``. Works on gloo (CPU) and RCCL."""
+    """Serving-mode exchange: send each target to its owner shard (its top shard_bits bits; one rank
+    per shard) with all_to_all_single. `targets` is a (q, 20) uint8 tensor on the backend's device
+    (cuda for RCCL, cpu for gloo); everything stays on that device except the split sizes.
+    Returns (local_targets, ctx) for ``return_results``."""
     import torch
     import torch.distributed as dist
 
+    if isinstance(targets, np.ndarray):
+        targets = torch.from_numpy(np.ascontiguousarray(targets, dtype=np.uint8))
     world = dist.get_world_size(group)
-    tnp = targets.cpu().numpy() if hasattr(targets, "cpu") else targets
-    owner = (tnp[:, 0].astype(np.int64) >> (8 - spec.shard_bits)) if spec.shard_bits else np.zeros(len(tnp), int)
-    owner = owner % world
-    order = np.argsort(owner, kind="stable")
-    send_counts = np.bincount(owner, minlength=world).astype(np.int64)
-    sc = torch.tensor(send_counts)
-    rc = torch.empty_like(sc)
-    dist.all_to_all_single(rc, sc, group=group)
-    send = torch.from_numpy(np.ascontiguousarray(tnp[order]))
-    recv = torch.empty((int(rc.sum()), 20), dtype=torch.uint8)
-    dist.all_to_all_single(recv, send, output_split_sizes=rc.tolist(), input_split_sizes=sc.tolist(), group=group)
-    return recv, rc.tolist(), sc.tolist(), order
+    if spec.shard_bits:
+        owner = (targets[:, 0].to(torch.int64) >> (8 - spec.shard_bits)) % world
+    else:
+        owner = torch.zeros(targets.shape[0], dtype=torch.int64, device=targets.device)
+    order = torch.argsort(owner, stable=True)
+    send_counts = torch.bincount(owner, minlength=world)
+    recv_counts = torch.empty_like(send_counts)
+    dist.all_to_all_single(recv_counts, send_counts, group=group)
+    sc, rc = send_counts.tolist(), recv_counts.tolist()
+    recv = targets.new_empty((sum(rc), 20))
+    dist.all_to_all_single(recv, targets[order].contiguous(), output_split_sizes=rc, input_split_sizes=sc, group=group)
+    return recv, (rc, sc, order, targets.shape[0])
 
 
-def return_results(local_idx, local_cnt, recv_splits, send_splits, order, group=None):
-    """Inverse of route_queries for (q_local, k) uint32 results and (q_local,) counts."""
+def return_results(local_idx, local_cnt, ctx, group=None):
+    """Inverse of route_queries for (q_local, k) int32 results and (q_local,) counts (tensors on the
+    backend's device, or numpy): each query's answer back at its position on its sender."""
     import torch
     import torch.distributed as dist
 
+    rc, sc, order, q = ctx
+    if isinstance(local_idx, np.ndarray):
+        local_idx = torch.from_numpy(np.ascontiguousarray(local_idx).view(np.int32))
+        local_cnt = torch.from_numpy(np.ascontiguousarray(local_cnt))
     k = local_idx.shape[1]
-    idx = torch.from_numpy(np.ascontiguousarray(local_idx).view(np.int32))
-    cnt = torch.from_numpy(np.ascontiguousarray(local_cnt).astype(np.int32))
-    back_idx = torch.empty((sum(send_splits), k), dtype=torch.int32)
-    back_cnt = torch.empty((sum(send_splits),), dtype=torch.int32)
-    dist.all_to_all_single(back_idx, idx, output_split_sizes=send_splits, input_split_sizes=recv_splits, group=group)
-    dist.all_to_all_single(back_cnt, cnt, output_split_sizes=send_splits, input_split_sizes=recv_splits, group=group)
-    out_idx = np.empty((len(order), k), np.uint32)
-    out_cnt = np.empty((len(order),), np.uint8)
-    out_idx[order] = back_idx.numpy().view(np.uint32)
-    out_cnt[order] = back_cnt.numpy().astype(np.uint8)
+    back_idx = local_idx.new_empty((sum(sc), k))
+    back_cnt = torch.empty((sum(sc),), dtype=torch.int32, device=local_idx.device)
+    dist.all_to_all_single(back_idx, local_idx.contiguous(), output_split_sizes=sc, input_split_sizes=rc, group=group)
+    dist.all_to_all_single(back_cnt, local_cnt.to(torch.int32).contiguous(), output_split_sizes=sc,
+                           input_split_sizes=rc, group=group)
+    out_idx = local_idx.new_empty((q, k))
+    out_cnt = torch.empty((q,), dtype=torch.uint8, device=local_idx.device)
+    out_idx[order] = back_idx
+    out_cnt[order] = back_cnt.to(torch.uint8)
     return out_idx, out_cnt

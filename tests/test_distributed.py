@@ -29,23 +29,25 @@ def _worker(rank, world, port, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    ok = False
     try:
         spec = ShardSpec(n_shards=world, depth=10, mean_per_bucket=6.0, seed=991)
         sh = build_shard(spec, rank)
         # each rank receives a batch of arbitrary targets (any owner)
         tg = S.random_targets(3000, seed=1000 + rank)
-        local, recv_splits, send_splits, order = route_queries(tg, spec)
+        local, ctx = route_queries(tg, spec)
         ltg = local.numpy()
         assert (ltg[:, 0] >> (8 - spec.shard_bits) == rank).all()
         idx, cnt = O.flat_rt_closest(sh.ids, sh.status, sh.first, sh.off, ltg, 8)
         idx = np.where(idx != 0xFFFFFFFF, idx + np.uint32(sh.index_base), idx).astype(np.uint32)
-        out_idx, out_cnt = return_results(idx, cnt, recv_splits, send_splits, order)
+        out_idx, out_cnt = return_results(idx, cnt, ctx)
+        out_idx, out_cnt = out_idx.numpy().view(np.uint32), out_cnt.numpy()
         gids, gst, goff = spec.bucket_range(0, spec.n_buckets)
         gfirst = S.bucket_firsts(spec.depth, 0, spec.n_buckets)
         want, wcnt = O.flat_rt_closest(gids, gst, gfirst, goff, tg, 8)
         ok = np.array_equal(out_idx, want) and np.array_equal(out_cnt, wcnt)
-        q.put((rank, ok))
     finally:
+        q.put((rank, bool(ok)))
         dist.destroy_process_group()
 
 
