@@ -137,7 +137,7 @@ int kad_table_refresh_status(kad_table* t, int64_t now_ns, void* stream);
  *                        nodes re-spliced to the front of their new bucket: list order reverses)
  * The node arrays are re-laid out on the device (one gather over the plan's segments); masks,
  * prefix sums, dup masks and window lines are re-derived there (a split turns window lines off).
- * Outputs: remap (device, old n entries, may be NULL) = new index of every old node, KAD_NO_NODE
+ * Outputs: remap (host or device, old n entries, may be NULL) = new index of every old node, KAD_NO_NODE
  * if removed or replaced; new_index (host, n_new, may be NULL) = index of every new node,
  * KAD_NO_NODE if unused. Any op clears KAD_TABLE_SORTED (NodeCache queries need a new snapshot);
  * wire records and node times must be set again. Synchronous. */

@@ -18,11 +18,14 @@
  * A mirror is a snapshot of the table at `now` (the status byte of every node is Node::isGood(now)
  * / isExpired() evaluated once, on the host thread that owns the table, as the reference does on its
  * dht thread). Results come back as the same shared_ptr<NodeT> objects the table holds, in the
- * reference's order. Re-snapshot after table mutations (Dht::onNewNode / expireBuckets).
+ * reference's order. After table mutations (Dht::onNewNode / expireBuckets / split), either
+ * re-snapshot or record them on the mirror (nodeRemoved / nodeReplaced / nodeAdded / bucketSplit)
+ * and flush(now): kad_table_apply replays them on the device copy.
  */
 #ifndef KADGPU_HPP
 #define KADGPU_HPP
 
+#include <algorithm>
 #include <cstdint>
 #include <cstring>
 #include <iterator>
@@ -168,14 +171,72 @@ public:
         return findClosestNodesBatch(ids.data(), ids.size(), count);
     }
 
+    /* Incremental mirror (kad_table_apply): record the mutations the Dht makes to the host table, in
+     * the order it makes them, then flush(now). Nodes named by nodeRemoved / nodeReplaced must be in
+     * the last snapshot or flush (flush in between otherwise). */
+    void nodeRemoved(const NodePtr& n) {  // Dht::expireBuckets remove_if (dht.cpp:942-956)
+        op(KAD_OP_REMOVE, index_of(n), 0);
+    }
+    void nodeReplaced(const NodePtr& old, const NodePtr& n) {  // onNewNode: `n = node` (dht.cpp:917-921)
+        op(KAD_OP_REPLACE, index_of(old), slot(n));
+    }
+    void nodeAdded(const NodePtr& n) {  // onNewNode: b->nodes.emplace_front(node) (dht.cpp:934)
+        op(KAD_OP_INSERT, slot(n), 0);
+    }
+    void bucketSplit(size_t bucket_index) {  // RoutingTable::split (routing_table.cpp:137-163)
+        op(KAD_OP_SPLIT, (uint32_t)bucket_index, 0);
+        buckets_++;
+    }
+    template <class TimePoint>
+    void flush(TimePoint now) {
+        if (ops_.empty()) return;
+        std::vector<uint8_t> ids, status;
+        for (const auto& n : added_) {
+            ids.insert(ids.end(), id_bytes(n->id), id_bytes(n->id) + KAD_HASH_LEN);
+            status.push_back((uint8_t)((n->isGood(now) ? KAD_STATUS_GOOD : 0u) | (n->isExpired() ? KAD_STATUS_EXPIRED : 0u)));
+        }
+        std::vector<uint32_t> remap(nodes_.size()), idx(added_.size());
+        check(kad_table_apply(table_.get(), ops_.data(), (uint32_t)(ops_.size() / 3), ids.data(), status.data(),
+                              (uint32_t)added_.size(), remap.data(), idx.data()),
+              "kad_table_apply");
+        kad_table_info inf;
+        check(kad_table_get_info(table_.get(), &inf), "kad_table_get_info");
+        std::vector<NodePtr> next(inf.n_nodes);
+        for (size_t i = 0; i < nodes_.size(); i++)
+            if (remap[i] != KAD_NO_NODE) next[remap[i]] = nodes_[i];
+        for (size_t s = 0; s < added_.size(); s++)
+            if (idx[s] != KAD_NO_NODE) next[idx[s]] = added_[s];
+        nodes_.swap(next);
+        buckets_ = inf.n_buckets;
+        ops_.clear();
+        added_.clear();
+    }
+
     size_t bucketCount() const { return buckets_; }
     size_t nodeCount() const { return nodes_.size(); }
     const DeviceTable& table() const { return table_; }
 
 private:
+    void op(uint32_t kind, uint32_t a, uint32_t b) {
+        ops_.push_back(kind);
+        ops_.push_back(a);
+        ops_.push_back(b);
+    }
+    uint32_t index_of(const NodePtr& n) const {
+        auto it = std::find(nodes_.begin(), nodes_.end(), n);
+        if (it == nodes_.end()) throw Error(KAD_ERR_INVALID, "node not in the mirrored snapshot (flush first)");
+        return (uint32_t)(it - nodes_.begin());
+    }
+    uint32_t slot(const NodePtr& n) {
+        added_.push_back(n);
+        return (uint32_t)(added_.size() - 1);
+    }
+
     DeviceTable table_;
     std::vector<NodePtr> nodes_;
     uint32_t buckets_ = 0;
+    std::vector<uint32_t> ops_;
+    std::vector<NodePtr> added_;
 };
 
 /* Device mirror of one NodeCache family map (node_cache.h:42-50). */

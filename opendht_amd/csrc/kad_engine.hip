@@ -2688,14 +2688,15 @@ int kad_table_apply(kad_table* t, const uint32_t* ops, uint32_t n_ops, const uin
     std::vector<void*> tmp;
     uint64_t tmpb = 0;
     auto cleanup = [&]() { for (void* p : tmp) (void)hipFree(p); };
-    MirrorSeg* dseg; uint32_t *dlist, *dntail, *dnidx; uint64_t* dnkey; uint8_t* dnst;
+    MirrorSeg* dseg; uint32_t *dlist, *dntail, *dnidx, *dremap = nullptr; uint64_t* dnkey; uint8_t* dnst;
     uint64_t* key1; uint32_t* tail1; uint8_t* st1;
     int rc;
     if ((rc = dev_upload(&dseg, segs.data(), segs.size(), tmp, tmpb)) ||
         (rc = dev_upload(&dlist, list.data(), list.size(), tmp, tmpb)) ||
         (rc = dev_upload(&dnkey, nkey.data(), n_new, tmp, tmpb)) ||
         (rc = dev_upload(&dntail, ntail.data(), 3ull * n_new, tmp, tmpb)) ||
-        (rc = dev_upload(&dnst, new_status, n_new, tmp, tmpb)) || (rc = dev_upload(&dnidx, nullptr, n_new, tmp, tmpb))) {
+        (rc = dev_upload(&dnst, new_status, n_new, tmp, tmpb)) || (rc = dev_upload(&dnidx, nullptr, n_new, tmp, tmpb)) ||
+        (remap && (rc = dev_upload(&dremap, nullptr, n0, tmp, tmpb)))) {
         cleanup();
         return rc;
     }
@@ -2706,18 +2707,19 @@ int kad_table_apply(kad_table* t, const uint32_t* ops, uint32_t n_ops, const uin
         return rc;
     }
     if (hipMemset(key1, 0xFF, 8ull * (n1 + KEY_PAD)) != hipSuccess || hipMemset(dnidx, 0xFF, 4ull * n_new) != hipSuccess ||
-        (remap && n0 && hipMemset(remap, 0xFF, 4ull * n0) != hipSuccess)) {
+        (remap && n0 && hipMemset(dremap, 0xFF, 4ull * n0) != hipSuccess)) {
         cleanup();
         return set_err(KAD_ERR_HIP, "hipMemset failed");
     }
     if (n1)
         hipLaunchKernelGGL(mirror_gather_kernel, dim3(grid_for(n1)), dim3(BLOCK), 0, 0, dseg, (uint32_t)segs.size(), dlist, n1,
-                           d.key, d.tail, d.status, dnkey, dntail, dnst, key1, tail1, st1, remap, dnidx);
+                           d.key, d.tail, d.status, dnkey, dntail, dnst, key1, tail1, st1, dremap, dnidx);
     if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
         cleanup();
         return set_err(KAD_ERR_HIP, "mirror gather failed");
     }
-    if (new_index && n_new && hipMemcpy(new_index, dnidx, 4ull * n_new, hipMemcpyDeviceToHost) != hipSuccess) {
+    if ((new_index && n_new && hipMemcpy(new_index, dnidx, 4ull * n_new, hipMemcpyDeviceToHost) != hipSuccess) ||
+        (remap && n0 && hipMemcpy(remap, dremap, 4ull * n0, hipMemcpyDefault) != hipSuccess)) {
         cleanup();
         return set_err(KAD_ERR_HIP, "copy of new indices failed");
     }

@@ -2,6 +2,7 @@
 // (InfoHash = std::array<uint8_t,20>, Node with isGood/isExpired, Bucket{first, list<shared_ptr<Node>>},
 // RoutingTable = std::list<Bucket>, NodeCache family map = std::map<InfoHash, weak_ptr<Node>>).
 // Expected results come from the CPU oracle (test infrastructure). Needs a GPU. Exit 0 = pass.
+#include <algorithm>
 #include <array>
 #include <chrono>
 #include <cstdio>
@@ -127,6 +128,115 @@ int main() {
             for (uint32_t j = 0; j < got[i].size() && j < wcnt[i]; j++)
                 EXPECT(got[i][j]->idx == sorted_to_node[want[i * count + j]], "nc node q=%u j=%u", i, j);
         }
+    }
+    // Incremental mirror: Dht::onNewNode (replace an expired node / emplace_front / split my bucket)
+    // and Dht::expireBuckets on the host table, recorded on the mirror and flushed to the device.
+    {
+        auto find_bucket = [&](const InfoHash& id) {  // routing_table.cpp:113-127
+            auto b = rt.begin();
+            while (std::next(b) != rt.end() && !(id < std::next(b)->first)) ++b;
+            return b;
+        };
+        auto lowbit = [](const InfoHash& h) {
+            for (int i = 19; i >= 0; i--)
+                if (h[i])
+                    for (int j = 7; j >= 0; j--)
+                        if (h[i] & (0x80 >> j)) return 8 * i + j;
+            return -1;
+        };
+        auto split = [&](RoutingTable::iterator b) {  // routing_table.cpp:137-163
+            const int depth = std::max(lowbit(b->first), std::next(b) != rt.end() ? lowbit(std::next(b)->first) : -1) + 1;
+            if (depth >= 160) return false;
+            InfoHash mid = b->first;
+            mid[depth / 8] |= (uint8_t)(0x80 >> (depth % 8));
+            auto nb = rt.insert(std::next(b), Bucket{mid, {}});
+            std::list<std::shared_ptr<Node>> tmp;
+            tmp.splice(tmp.begin(), b->nodes);
+            while (!tmp.empty()) {
+                auto it = tmp.begin();
+                auto dst = find_bucket((*it)->id);
+                dst->nodes.splice(dst->nodes.begin(), tmp, it);
+            }
+            (void)nb;
+            return true;
+        };
+        const InfoHash myid = nodes[123]->id;
+        uint32_t replaced = 0, added = 0, splits = 0, removed = 0, next_idx = n;
+        for (int k = 0; k < 3000; k++) {
+            auto nd = std::make_shared<Node>();
+            for (auto& x : nd->id) x = (uint8_t)g();
+            if (k % 5 == 0) {  // some land next to myid, to make my bucket split
+                nd->id = myid;
+                for (int x = 6; x < 20; x++) nd->id[x] = (uint8_t)g();
+            }
+            nd->time = nd->reply_time = now;
+            nd->idx = next_idx++;
+            while (true) {  // Dht::onNewNode (dht.cpp:867-936), confirm = 0, all new nodes good
+                auto b = find_bucket(nd->id);
+                auto exp = std::find_if(b->nodes.begin(), b->nodes.end(), [](const std::shared_ptr<Node>& x) { return x->isExpired(); });
+                if (exp != b->nodes.end()) {
+                    mirror.nodeReplaced(*exp, nd);
+                    *exp = nd;
+                    replaced++;
+                    break;
+                }
+                if (b->nodes.size() >= 8) {
+                    // my bucket splits when full (the reference also requires no dubious node,
+                    // dht.cpp:923; the mirror replays whatever the host does either way)
+                    const bool mine = !(myid < b->first) && (std::next(b) == rt.end() || myid < std::next(b)->first);
+                    if (mine) {
+                        const size_t bi = (size_t)std::distance(rt.begin(), b);
+                        if (split(b)) {
+                            mirror.bucketSplit(bi);
+                            splits++;
+                            continue;
+                        }
+                    }
+                    break;  // cached away
+                }
+                b->nodes.emplace_front(nd);
+                mirror.nodeAdded(nd);
+                added++;
+                break;
+            }
+            if (k == 1500) mirror.flush(now);  // two batches
+        }
+        for (auto& b : rt)  // Dht::expireBuckets (dht.cpp:942-956)
+            b.nodes.remove_if([&](const std::shared_ptr<Node>& x) {
+                if (x->isExpired()) { mirror.nodeRemoved(x); removed++; return true; }
+                return false;
+            });
+        mirror.flush(now);
+        EXPECT(mirror.bucketCount() == rt.size(), "mirror buckets %zu vs %zu", mirror.bucketCount(), rt.size());
+        std::vector<uint8_t> mids, mst, mfirst;
+        std::vector<uint32_t> moff;
+        std::vector<const Node*> mnode;
+        for (auto& b : rt) {
+            moff.push_back((uint32_t)mnode.size());
+            mfirst.insert(mfirst.end(), b.first.begin(), b.first.end());
+            for (auto& nd : b.nodes) {
+                mids.insert(mids.end(), nd->id.begin(), nd->id.end());
+                mst.push_back((uint8_t)((nd->isGood(now) ? 1 : 0) | (nd->isExpired() ? 2 : 0)));
+                mnode.push_back(nd.get());
+            }
+        }
+        moff.push_back((uint32_t)mnode.size());
+        EXPECT(mirror.nodeCount() == mnode.size(), "mirror nodes %zu vs %zu", mirror.nodeCount(), mnode.size());
+        for (uint32_t count : {1u, 8u, 14u}) {
+            auto got = mirror.findClosestNodesBatch(targets, count);
+            std::vector<uint32_t> want(q * count);
+            std::vector<uint8_t> wcnt(q);
+            orc_flat_rt_closest((uint32_t)mnode.size(), mids.data(), mst.data(), (uint32_t)rt.size(), mfirst.data(),
+                                moff.data(), q, reinterpret_cast<const uint8_t*>(targets.data()), count, want.data(),
+                                wcnt.data(), 4);
+            for (uint32_t i = 0; i < q; i++) {
+                EXPECT(got[i].size() == wcnt[i], "mirror count q=%u k=%u", i, count);
+                for (uint32_t j = 0; j < got[i].size() && j < wcnt[i]; j++)
+                    EXPECT(got[i][j].get() == mnode[want[i * count + j]], "mirror node q=%u k=%u j=%u", i, count, j);
+            }
+        }
+        std::printf("mirror: %u replaced, %u added, %u splits, %u removed\n", replaced, added, splits, removed);
+        EXPECT(replaced && added && splits && removed, "every mutation kind exercised");
     }
     // Dht-style accessor over two families
     kadgpu::DhtMirror<RoutingTable> dht;
