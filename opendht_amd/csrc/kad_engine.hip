@@ -907,6 +907,23 @@ __device__ __forceinline__ bool wl16_answer(const DevTable& T, const Target& t, 
     return !ex;
 }
 
+// Row of up to 16 indices: 16-byte stores for count 16, 8-byte stores for even counts (SEARCH_NODES = 14).
+__device__ __forceinline__ void store_row16(uint32_t* row, const uint32_t (&o)[16], uint32_t count) {
+    if (count == 16 && ((uintptr_t)row & 15u) == 0) {
+#pragma unroll
+        for (int x = 0; x < 4; x++)
+            reinterpret_cast<uint4*>(row)[x] = make_uint4(o[4 * x], o[4 * x + 1], o[4 * x + 2], o[4 * x + 3]);
+    } else if ((count & 1u) == 0 && ((uintptr_t)row & 7u) == 0) {
+#pragma unroll
+        for (int x = 0; x < 8; x++)
+            if ((uint32_t)(2 * x) < count) reinterpret_cast<uint2*>(row)[x] = make_uint2(o[2 * x], o[2 * x + 1]);
+    } else {
+#pragma unroll
+        for (int j = 0; j < 16; j++)
+            if ((uint32_t)j < count) row[j] = o[j];
+    }
+}
+
 __global__ __launch_bounds__(BLOCK) void rt_wl16_kernel(DevTable T, const uint8_t* __restrict__ targets, uint32_t q,
                                                         uint32_t count, uint32_t* __restrict__ out_idx,
                                                         uint8_t* __restrict__ out_cnt) {
@@ -921,20 +938,7 @@ __global__ __launch_bounds__(BLOCK) void rt_wl16_kernel(DevTable T, const uint8_
     uint32_t o[16], m;
     const bool ok = wl16_answer(T, t, b, count, act, o, m);
     if (act && ok) {
-        uint32_t* row = out_idx + (size_t)i * count;
-        if (count == 16 && ((uintptr_t)row & 15u) == 0) {
-#pragma unroll
-            for (int x = 0; x < 4; x++)
-                reinterpret_cast<uint4*>(row)[x] = make_uint4(o[4 * x], o[4 * x + 1], o[4 * x + 2], o[4 * x + 3]);
-        } else if ((count & 1u) == 0 && ((uintptr_t)row & 7u) == 0) {  // e.g. SEARCH_NODES = 14
-#pragma unroll
-            for (int x = 0; x < 8; x++)
-                if ((uint32_t)(2 * x) < count) reinterpret_cast<uint2*>(row)[x] = make_uint2(o[2 * x], o[2 * x + 1]);
-        } else {
-#pragma unroll
-            for (int j = 0; j < 16; j++)
-                if ((uint32_t)j < count) row[j] = o[j];
-        }
+        store_row16(out_idx + (size_t)i * count, o, count);
         if (out_cnt) out_cnt[i] = (uint8_t)m;
     }
     __shared__ uint64_t xs[BLOCK / 64][192];
@@ -1035,6 +1039,38 @@ __global__ __launch_bounds__(BLOCK) void rt_dual_wl_kernel(DevTable T4, DevTable
         if (out_cnt) out_cnt[i] = (uint8_t)m;
     } else if (act && !wl) {
         ex = !rt_query_fast<8, 3>(T, t, count, row, out_cnt ? out_cnt + i : nullptr);
+    }
+    __shared__ uint64_t xs[BLOCK / 64][192];
+    exact_tail(T4, t, ex && !six, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
+    exact_tail(T6, t, ex && six, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
+}
+
+// Dual-family batch for counts 9..16 where a family has 16-slot window lines (same structure).
+__global__ __launch_bounds__(BLOCK) void rt_dual_wl16_kernel(DevTable T4, DevTable T6,
+                                                             const uint8_t* __restrict__ targets,
+                                                             const uint8_t* __restrict__ af, uint32_t q, uint32_t count,
+                                                             uint32_t* __restrict__ out_idx,
+                                                             uint8_t* __restrict__ out_cnt) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    const bool act = i < q;
+    Target t{};
+    bool six = false;
+    if (act) {
+        t = load_target(targets, i);
+        six = af[i] != 0;
+    }
+    const DevTable& T = six ? T6 : T4;
+    const bool wl = act && (T.flags & TF_WL16);
+    const uint32_t b = wl ? locate_bucket(T, t) : 0u;
+    uint32_t o[16], m;
+    const bool ok = wl16_answer(T, t, b, count, wl, o, m);
+    uint32_t* row = out_idx + (size_t)i * count;
+    bool ex = wl && !ok;
+    if (wl && ok) {
+        store_row16(row, o, count);
+        if (out_cnt) out_cnt[i] = (uint8_t)m;
+    } else if (act && !wl) {
+        ex = !rt_query_fast<16, 3>(T, t, count, row, out_cnt ? out_cnt + i : nullptr);
     }
     __shared__ uint64_t xs[BLOCK / 64][192];
     exact_tail(T4, t, ex && !six, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
@@ -1433,7 +1469,7 @@ __device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
     return ((uint64_t)(uint32_t)__shfl((int)(v >> 32), src, 64) << 32) | (uint32_t)__shfl((int)(uint32_t)v, src, 64);
 }
 
-__global__ __launch_bounds__(BLOCK) void nc_group_kernel(DevTable T, const uint8_t* __restrict__ targets, uint32_t q,
+__global__ __launch_bounds__(BLOCK) void nc_group_v1_kernel(DevTable T, const uint8_t* __restrict__ targets, uint32_t q,
                                                          uint32_t count, uint32_t* __restrict__ out_idx,
                                                          uint8_t* __restrict__ out_cnt) {
     constexpr uint32_t W = 32, G = 64;  // run window, lanes per query
@@ -1506,6 +1542,192 @@ __global__ __launch_bounds__(BLOCK) void nc_group_kernel(DevTable T, const uint8
     } else if (act && lane == 0) {
         nc_serial(T, t, count, out_idx + (size_t)qi * count, out_cnt ? out_cnt + qi : nullptr);
     }
+}
+
+// The same merge with the lower bound and the runs read from ONE window load (nc_window_kernel):
+// the radix slot of t gives [r0, r1), the nodes whose top 64 bits share t's slot; lanes load the 96
+// nodes r0-32 .. r0+63 (two loads per lane, independent, issued right after the slot lookup), lb =
+// r0 + #(slot nodes < t) is one ballot, and the runs are shuffled out of the window (lb - r0 <= 32
+// keeps both 32-runs inside it). This drops the binary search's dependent loads from the chain
+// (target -> slot -> window -> answer). Emission ranks come from one ballot: a node's rank is the
+// emitting nodes of its own run before it plus those of the other run placed before it (the first
+// `lo` of them), so no LDS mask or block barrier. A slot of more than 32 nodes takes the binary
+// search and per-lane loads.
+// Slot range [r0, r1) of t's top 64 bits (wave-uniform loads).
+__device__ __forceinline__ void nc_slot(const DevTable& T, const Target& t, uint32_t& r0, uint32_t& r1) {
+    r0 = r1 = 0;
+    if (T.n && t.hi >= T.nbase) {
+        const uint64_t sl = (t.hi - T.nbase) >> T.nshift;
+        if (sl >= T.nslots) {
+            r0 = r1 = T.n;
+        } else {
+            r0 = T.nrdx[sl];
+            r1 = T.nrdx[sl + 1];
+        }
+    }
+}
+
+// The window r0-32 .. r0+63: lane l holds nodes r0-32+l (k0, status byte 0 of st) and, for l < 32,
+// r0+32+l (k1, status byte 1).
+struct NcWindow {
+    uint64_t k0, k1;
+    uint32_t st;
+};
+__device__ __forceinline__ NcWindow nc_window(const DevTable& T, uint32_t r0, uint32_t lane) {
+    NcWindow w{0, 0, 0};
+    const int64_t p0 = (int64_t)r0 - 32 + lane, p1 = p0 + 64;
+    if (p0 >= 0 && p0 < (int64_t)T.n) {
+        w.k0 = T.key[p0];
+        w.st = T.status[p0];
+    }
+    if (lane < 32 && p1 < (int64_t)T.n) {
+        w.k1 = T.key[p1];
+        w.st |= (uint32_t)T.status[p1] << 8;
+    }
+    return w;
+}
+
+// One query of the wave from its loaded window: lower bound, runs, merge, emission (see above).
+__device__ __forceinline__ void nc_answer(const DevTable& T, const Target& t, uint32_t r0, uint32_t r1,
+                                          const NcWindow& w, uint32_t lane, uint32_t qi, uint32_t count,
+                                          uint32_t* __restrict__ out_idx, uint8_t* __restrict__ out_cnt) {
+    constexpr uint32_t W = 32, G = 64;
+    const bool right = lane >= W;
+    const uint32_t k = lane & (W - 1);
+    const uint32_t N = T.n;
+    uint32_t lb;
+    if (r1 - r0 <= 32) {
+        bool lt = false;
+        if (lane >= 32 && lane < 32 + (r1 - r0)) {
+            if (w.k0 != t.hi) {
+                lt = w.k0 < t.hi;
+            } else {
+                const uint32_t* tt = T.tail + 3ull * (r0 - 32 + lane);
+                lt = cmp160(0, tt[0], tt[1], tt[2], 0, t.t2, t.t3, t.t4) < 0;
+            }
+        }
+        lb = r0 + (uint32_t)__builtin_popcountll(__ballot(lt));
+    } else {
+        lb = node_lower_bound(T, t);
+    }
+    const uint32_t dl = lb - r0;
+    const uint32_t node = right ? lb + k : lb - 1 - k;
+    const bool valid = right ? lb + k < N : lb > k;
+    uint64_t key;
+    uint32_t sb;
+    if (dl <= 32) {  // wave-uniform
+        const uint32_t idx = right ? 32 + dl + k : 31 + dl - k;  // window slot of `node`, in [0, 96)
+        const uint64_t a = shfl64(w.k0, (int)(idx & 63u)), b = shfl64(w.k1, (int)(idx & 63u));
+        const uint32_t ss = (uint32_t)__shfl((int)w.st, (int)(idx & 63u), 64);
+        key = idx < 64 ? a : b;
+        sb = idx < 64 ? ss & 255u : ss >> 8;
+    } else {
+        key = valid ? T.key[node] : 0;
+        sb = valid ? T.status[node] : 0u;
+    }
+    uint64_t m = valid ? key ^ t.hi : ~0ull;  // invalid lanes end their run: the maximum
+    const bool expired = !valid || (sb & KAD_STATUS_EXPIRED);
+    bool amb = valid && m == ~0ull;  // indistinguishable from the end-of-run sentinel
+#pragma unroll
+    for (uint32_t s = 1; s < W; s <<= 1) {  // prefix maxima along my run
+        const uint64_t o = shfl64(m, (int)lane - (int)s);
+        if (k >= s && o > m) m = o;
+    }
+    const uint32_t obase = right ? 0u : W;
+    uint32_t lo = 0, hi = W;
+#pragma unroll
+    for (int it = 0; it < 6; it++) {  // 33 possible answers: 6 halvings (a settled lane stays put)
+        const uint32_t mid = (lo + hi) >> 1;
+        const uint64_t v = shfl64(m, (int)(obase + (mid < W ? mid : W - 1)));
+        if (lo < hi) {
+            if (v < m) lo = mid + 1; else hi = mid;
+        }
+    }
+    const uint64_t at = shfl64(m, (int)(obase + (lo < W ? lo : W - 1)));
+    amb |= valid && lo < W && at == m;
+    const uint32_t pos = k + lo;
+    const bool emit = valid && !expired;
+    const uint64_t eb = __ballot(emit);
+    const uint32_t mine = right ? (uint32_t)(eb >> 32) : (uint32_t)eb;
+    const uint32_t other = right ? (uint32_t)eb : (uint32_t)(eb >> 32);
+    const uint32_t rank = (uint32_t)__builtin_popcount(mine & ((1u << k) - 1u)) +
+                          (uint32_t)__builtin_popcount(lo >= W ? other : other & ((1u << lo) - 1u));
+    const uint32_t tot = (uint32_t)__builtin_popcountll(eb);
+    uint32_t pstar = 64;  // position of the count-th emission (64: not inside the window)
+    if (tot >= count) {
+        const uint64_t wm = __ballot(emit && rank == count - 1);
+        pstar = (uint32_t)__shfl((int)pos, (int)__builtin_ctzll(wm), 64);
+    }
+    const uint32_t posA = (uint32_t)__shfl((int)pos, (int)(W - 1), 64);
+    const uint32_t posB = (uint32_t)__shfl((int)pos, (int)(G - 1), 64);
+    const bool ok = !__any(amb) && (lb <= W || posA > pstar) && (lb + W >= N || posB > pstar);
+    if (ok) {
+        uint32_t* row = out_idx + (size_t)qi * count;
+        const uint32_t mm = min(tot, count);
+        if (emit && rank < count) row[rank] = node + T.index_base;
+        if (lane >= mm && lane < count) row[lane] = NONE;
+        if (lane == 0 && out_cnt) out_cnt[qi] = (uint8_t)mm;
+    } else if (lane == 0) {
+        nc_serial(T, t, count, out_idx + (size_t)qi * count, out_cnt ? out_cnt + qi : nullptr);
+    }
+}
+
+__global__ __launch_bounds__(BLOCK) void nc_group_kernel(DevTable T, const uint8_t* __restrict__ targets, uint32_t q,
+                                                         uint32_t count, uint32_t* __restrict__ out_idx,
+                                                         uint8_t* __restrict__ out_cnt) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t qi = blockIdx.x * (BLOCK / 64) + threadIdx.x / 64;
+    if (qi >= q) return;  // one query per wave: the whole wave leaves
+    const Target t = load_target(targets, qi);
+    uint32_t r0, r1;
+    nc_slot(T, t, r0, r1);
+    const NcWindow w = nc_window(T, r0, lane);
+    nc_answer(T, t, r0, r1, w, lane, qi, count, out_idx, out_cnt);
+}
+
+// Q queries per wave with their loads interleaved by hand: the Q targets, then the Q slot ranges,
+// then the Q windows are each loaded unconditionally (indices clamped, validity applied after), so
+// the wave waits three memory round trips for Q queries instead of for one. The kernel is latency
+// bound: at one query per wave the waves spent ~60% of their cycles waiting on loads with 8 waves
+// per SIMD resident (PMC). Tables with nodes only (T.n > 0).
+template <int Q>
+__global__ __launch_bounds__(BLOCK) void nc_multi_kernel(DevTable T, const uint8_t* __restrict__ targets, uint32_t q,
+                                                         uint32_t count, uint32_t* __restrict__ out_idx,
+                                                         uint8_t* __restrict__ out_cnt) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t q0 = (blockIdx.x * (BLOCK / 64) + threadIdx.x / 64) * Q;
+    if (q0 >= q) return;
+    const uint32_t N = T.n;
+    Target t[Q];
+#pragma unroll
+    for (int j = 0; j < Q; j++) t[j] = load_target(targets, min(q0 + j, q - 1));
+    uint32_t r0[Q], r1[Q];
+#pragma unroll
+    for (int j = 0; j < Q; j++) {
+        const bool below = t[j].hi < T.nbase;
+        const uint64_t sl = below ? 0 : (t[j].hi - T.nbase) >> T.nshift;
+        const bool above = !below && sl >= T.nslots;
+        const uint32_t c = above ? T.nslots - 1 : (uint32_t)sl;
+        const uint32_t a = T.nrdx[c], b = T.nrdx[c + 1];
+        r0[j] = below ? 0u : (above ? N : a);
+        r1[j] = below ? 0u : (above ? N : b);
+    }
+    NcWindow w[Q];
+#pragma unroll
+    for (int j = 0; j < Q; j++) {
+        const int64_t p0 = (int64_t)r0[j] - 32 + lane, p1 = p0 + 64;
+        const uint32_t c0 = (uint32_t)min(max(p0, (int64_t)0), (int64_t)N - 1);
+        const uint32_t c1 = (uint32_t)min(p1, (int64_t)N - 1);
+        const uint64_t a = T.key[c0], b = T.key[c1];
+        const uint32_t sa = T.status[c0], sb = T.status[c1];
+        const bool v0 = p0 >= 0 && p0 < (int64_t)N, v1 = lane < 32 && p1 < (int64_t)N;
+        w[j].k0 = v0 ? a : 0;
+        w[j].k1 = v1 ? b : 0;
+        w[j].st = (v0 ? sa : 0u) | (v1 ? sb << 8 : 0u);
+    }
+#pragma unroll
+    for (int j = 0; j < Q; j++)
+        if (q0 + j < q) nc_answer(T, t[j], r0[j], r1[j], w[j], lane, q0 + j, count, out_idx, out_cnt);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1707,6 +1929,7 @@ __global__ void scan_apply_kernel(const uint32_t* part, const uint32_t* sums, ui
 }
 
 inline uint32_t grid_for(uint64_t n) { return (uint32_t)((n + BLOCK - 1) / BLOCK); }
+
 
 // ---------------------------------------------------------------------------------------
 // Host side
@@ -2234,6 +2457,9 @@ int kad_rt_closest_batch_dual(const kad_table* t4, const kad_table* t6, const ui
         hipLaunchKernelGGL(rt_dual_wl_kernel, dim3(grid_for(q)), dim3(BLOCK), 0, s, d4, d6, targets, af, q, count,
                            out_idx, out_cnt);
     else if (count <= 8) launch_rt_dual<8>(d4, d6, targets, af, q, count, out_idx, out_cnt, s);
+    else if (count <= 16 && ((d4.flags | d6.flags) & TF_WL16))
+        hipLaunchKernelGGL(rt_dual_wl16_kernel, dim3(grid_for(q)), dim3(BLOCK), 0, s, d4, d6, targets, af, q, count,
+                           out_idx, out_cnt);
     else if (count <= 16) launch_rt_dual<16>(d4, d6, targets, af, q, count, out_idx, out_cnt, s);
     else launch_rt_dual<32>(d4, d6, targets, af, q, count, out_idx, out_cnt, s);
     HIP_TRY(hipGetLastError());
@@ -2402,9 +2628,21 @@ int kad_nc_closest_batch(const kad_table* t, const uint8_t* targets, uint32_t q,
     if (!targets || (!out_idx && count)) return set_err(KAD_ERR_INVALID, "NULL buffer");
     DeviceGuard g(t->device);
     const char* ev = std::getenv("KAD_NC_KERNEL");
-    if (count >= 1 && count <= 16 && !(ev && std::strcmp(ev, "serial") == 0))
-        hipLaunchKernelGGL(nc_group_kernel, dim3((q + BLOCK / 64 - 1) / (BLOCK / 64)), dim3(BLOCK), 0, (hipStream_t)stream,
-                           t->d, targets, q, count, out_idx, out_cnt);
+    if (count >= 1 && count <= 16 && ev && std::strcmp(ev, "group1") == 0)
+        hipLaunchKernelGGL(nc_group_v1_kernel, dim3((q + BLOCK / 64 - 1) / (BLOCK / 64)), dim3(BLOCK), 0,
+                           (hipStream_t)stream, t->d, targets, q, count, out_idx, out_cnt);
+    else if (count >= 1 && count <= 16 && ev && std::strcmp(ev, "group2") == 0)
+        hipLaunchKernelGGL(nc_group_kernel, dim3((q + BLOCK / 64 - 1) / (BLOCK / 64)), dim3(BLOCK), 0,
+                           (hipStream_t)stream, t->d, targets, q, count, out_idx, out_cnt);
+    else if (count >= 1 && count <= 16 && t->d.n > 0 && ev && std::strcmp(ev, "multi4") == 0)
+        hipLaunchKernelGGL(nc_multi_kernel<4>, dim3((q + 4 * (BLOCK / 64) - 1) / (4 * (BLOCK / 64))), dim3(BLOCK), 0,
+                           (hipStream_t)stream, t->d, targets, q, count, out_idx, out_cnt);
+    else if (count >= 1 && count <= 16 && t->d.n > 0 && !(ev && std::strcmp(ev, "serial") == 0))
+        hipLaunchKernelGGL(nc_multi_kernel<2>, dim3((q + 2 * (BLOCK / 64) - 1) / (2 * (BLOCK / 64))), dim3(BLOCK), 0,
+                           (hipStream_t)stream, t->d, targets, q, count, out_idx, out_cnt);
+    else if (count >= 1 && count <= 16 && !(ev && std::strcmp(ev, "serial") == 0))
+        hipLaunchKernelGGL(nc_group_kernel, dim3((q + BLOCK / 64 - 1) / (BLOCK / 64)), dim3(BLOCK), 0,
+                           (hipStream_t)stream, t->d, targets, q, count, out_idx, out_cnt);
     else
         hipLaunchKernelGGL(nc_closest_kernel, dim3(grid_for(q)), dim3(BLOCK), 0, (hipStream_t)stream, t->d, targets, q,
                            count, out_idx, out_cnt);

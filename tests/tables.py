@@ -62,9 +62,10 @@ def sparse_good_table(n=4000):
     return t
 
 
-def tie_table(groups=64, per=6, seed=7):
+def tie_table(groups=64, per=6, seed=7, tag=""):
     """Many nodes share their top 64 bits (exercises the exact 160-bit tie path), plus one
-    bucket holding duplicate IDs (RoutingTable order = index order)."""
+    bucket holding duplicate IDs (RoutingTable order = index order). per > 32 puts more nodes in one
+    NodeCache radix slot than the window kernel loads (its binary-search path)."""
     rng = np.random.default_rng(seed)
     heads = rng.integers(0, 256, size=(groups, 8), dtype=np.uint8)
     ids = np.empty((groups * per, 20), np.uint8)
@@ -77,14 +78,14 @@ def tie_table(groups=64, per=6, seed=7):
     ids, _ = S.sort_ids(ids)
     first, off = S.uniform_buckets(ids, 4)
     st = np.where(rng.random(ids.shape[0]) < 0.85, 1, 0).astype(np.uint8)
-    srt = table(ids, st, first, off, sorted_=True, name="ties")
+    srt = table(ids, st, first, off, sorted_=True, name="ties" + tag)
     # duplicate IDs inside a bucket (unsorted RoutingTable snapshot)
     dup = ids.copy()
     dup[5] = dup[3]
     dup[6] = dup[3]
     st2 = st.copy()
     st2[3:7] = 1
-    return [srt, table(dup, st2, first, off, sorted_=False, name="dups")]
+    return [srt, table(dup, st2, first, off, sorted_=False, name="dups" + tag)]
 
 
 def offset_first_table(n=3000):
@@ -134,5 +135,6 @@ def all_small_tables():
     ts.append(all_bad_table())
     ts.append(sparse_good_table())
     ts.extend(tie_table())
+    ts.extend(tie_table(groups=24, per=48, seed=8, tag="48"))
     ts.append(offset_first_table())
     return ts

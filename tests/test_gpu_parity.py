@@ -172,14 +172,16 @@ def test_status_update_and_refresh_from_times(gpu):
         check_rt(T, dict(t, status=st3), targets, gpu, counts=(8, 14))
 
 
-def test_dual_family(gpu):
-    """Config 4: v4 and v6 tables, per-query af, k = 8/16/32."""
+@pytest.mark.parametrize("pair", ["uniform_split", "uniform_uniform"])
+def test_dual_family(gpu, pair):
+    """Config 4: v4 and v6 tables, per-query af, k = 8/14/16/32. uniform_split: one family with window
+    lines, one without (the lane path); uniform_uniform: both families answered from window lines."""
     t4 = TB.uniform_config(20_000, 11, seed=41)
-    t6 = TB.split_config(20_000, seed=61)
+    t6 = TB.split_config(20_000, seed=61) if pair == "uniform_split" else TB.uniform_config(30_000, 12, seed=62)
     targets = S.random_targets(4096, seed=9)
-    af = (np.arange(4096) % 2).astype(np.uint8)
+    af = (np.random.default_rng(3).random(4096) < 0.5).astype(np.uint8)
     with make(t4, gpu) as T4, make(t6, gpu) as T6:
-        for k in (8, 16, 32):
+        for k in (8, 14, 16, 32):
             idx, cnt = rt_closest_dual(T4, T6, dev(targets, gpu), dev(af, gpu), k)
             idx, cnt = u32(idx), cnt.cpu().numpy()
             w4, c4 = O.flat_rt_closest(t4["ids"], t4["status"], t4["first"], t4["off"], targets, k)

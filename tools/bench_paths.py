@@ -61,4 +61,51 @@ b = T.nc_closest(tg, 14)
 os.environ.pop("KAD_NC_KERNEL")
 torch.cuda.synchronize()
 res["nc_group_equals_serial"] = bool(torch.equal(a[0], b[0]) and torch.equal(a[1], b[1]))
+os.environ["KAD_NC_KERNEL"] = "group1"  # the binary-search + LDS-mask version, for A/B
+us = timeit(lambda: T.nc_closest(tg, 14))
+c = T.nc_closest(tg, 14)
+os.environ.pop("KAD_NC_KERNEL")
+torch.cuda.synchronize()
+res["nc_k14_group1_us"] = round(us, 1)
+res["nc_group1_equals"] = bool(torch.equal(a[0], c[0]) and torch.equal(a[1], c[1]))
+os.environ["KAD_NC_KERNEL"] = "group2"  # window load, one query per wave, not pipelined
+us = timeit(lambda: T.nc_closest(tg, 14))
+c = T.nc_closest(tg, 14)
+os.environ.pop("KAD_NC_KERNEL")
+torch.cuda.synchronize()
+res["nc_k14_group2_us"] = round(us, 1)
+res["nc_group2_equals"] = bool(torch.equal(a[0], c[0]) and torch.equal(a[1], c[1]))
+for k in (1, 8, 16):
+    us = timeit(lambda: T.nc_closest(tg, k))
+    res[f"nc_k{k}_us"] = round(us, 1)
+print(json.dumps(res, indent=1))
+
+# InfoHash primitives and the wire / hash rows: throughput and effective HBM bandwidth (bytes each
+# kernel must read + write, divided by the launch time).
+from opendht_amd import ops  # noqa: E402
+
+n = 1 << 24
+g = torch.Generator(device=dev).manual_seed(7)
+A = torch.randint(0, 256, (n, 20), dtype=torch.uint8, device=dev, generator=g)
+B = torch.randint(0, 256, (n, 20), dtype=torch.uint8, device=dev, generator=g)
+Tg = torch.randint(0, 256, (n, 20), dtype=torch.uint8, device=dev, generator=g)
+for name, fn, nbytes in (("xor_cmp", lambda: ops.xor_cmp(Tg, A, B), 61),
+                         ("common_bits", lambda: ops.common_bits(A, B), 44),
+                         ("lowbit", lambda: ops.lowbit(A), 24)):
+    us = timeit(fn)
+    res[f"{name}_16M_us"] = round(us, 1)
+    res[f"{name}_GB_s"] = round(n * nbytes / us / 1e3, 1)
+del A, B, Tg
+nrec = 1 << 22
+recs = torch.randint(0, 256, (nrec * 26,), dtype=torch.uint8, device=dev, generator=g)
+us = timeit(lambda: ops.parse_nodes(recs, 26, b"\x01" * 20))
+res["parse_nodes4_4M_us"] = round(us, 1)
+res["parse_nodes4_GB_s"] = round(nrec * 27 / us / 1e3, 1)
+for klen in (8, 20, 32, 55, 64, 100, 200):
+    nk = 1 << 22
+    data = torch.randint(0, 256, (nk * klen,), dtype=torch.uint8, device=dev, generator=g)
+    offs = torch.arange(0, nk + 1, dtype=torch.int64, device=dev) * klen
+    us = timeit(lambda: ops.infohash_get(data, offs))
+    res[f"sha1_{klen}B_4M_us"] = round(us, 1)
+    res[f"sha1_{klen}B_Ghash_s"] = round(nk / us / 1e3, 2)
 print(json.dumps(res, indent=1))

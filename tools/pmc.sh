@@ -1,7 +1,8 @@
 #!/bin/bash
 # PMC passes over a short bench run (one rocprofv3 invocation per counter group, kernel-trace
 # only besides --pmc, as the MI355X guide prescribes). Output: gpurun_out/pmc/<pass>/...
-# PMC_PASSES="A B;C D" overrides the pass list (';' between passes).
+# PMC_PASSES="A B;C D" overrides the pass list (';' between passes); PMC_PROG="tools/x.py args"
+# profiles another script instead of bench.py.
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/${PMC_DIR:-pmc}
 mkdir -p $O
@@ -14,7 +15,7 @@ for line in "${PASSES[@]}"; do
   [ -z "$line" ] && continue
   i=$((i+1))
   echo "pass $i: $line" >> $O/passes.txt
-  timeout -s KILL 120 rocprofv3 --pmc $line --kernel-trace --output-format csv -d $O/p$i -o run -- python3 $R/bench.py $ARGS > $O/p$i.log 2>&1
+  timeout -s KILL 120 rocprofv3 --pmc $line --kernel-trace --output-format csv -d $O/p$i -o run -- python3 ${PMC_PROG:+$R/}${PMC_PROG:-$R/bench.py $ARGS} > $O/p$i.log 2>&1
   rc=$?
   echo "pass $i rc=$rc" >> $O/passes.txt
   if [ $rc -ne 0 ]; then exit $rc; fi
