@@ -44,15 +44,16 @@ def cpu_baseline(sh, targets, count, budget_s, nthreads):
     t0 = time.perf_counter()
     F = O.FaithfulTable(sh.ids, sh.status, sh.first, sh.off)
     build_s = time.perf_counter() - t0
-    # calibrate on a small batch, then size the sample to ~budget_s of wall time
-    probe = max(nthreads, 16)
-    t0 = time.perf_counter()
-    F.rt_closest(targets[:probe], count, nthreads=nthreads)
-    per_q = (time.perf_counter() - t0) / probe
-    n = int(min(targets.shape[0], max(probe, budget_s / max(per_q, 1e-9))))
-    t0 = time.perf_counter()
-    F.rt_closest(targets[:n], count, nthreads=nthreads)
-    dt = time.perf_counter() - t0
+    # time successive slices of the same queries (doubling) until the budget is spent: the
+    # first slice also warms the table's pages, so no single-probe extrapolation is needed
+    n, dt, chunk = 0, 0.0, max(nthreads, 16)
+    while n < targets.shape[0] and dt < budget_s:
+        sl = targets[n:n + chunk]
+        t0 = time.perf_counter()
+        F.rt_closest(sl, count, nthreads=nthreads)
+        dt += time.perf_counter() - t0
+        n += sl.shape[0]
+        chunk = min(2 * chunk, max(16, int(n * (budget_s - dt) / max(dt, 1e-9))))
     F.close()
     return {"value": n / dt, "unit": "queries/s", "cores": nthreads, "kind": "port",
             "sample": f"{n} of the {targets.shape[0]} queries of rank 0's step (same shard table, "
