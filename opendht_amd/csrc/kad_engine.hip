@@ -92,6 +92,7 @@ struct DevTable {
     const uint32_t* nrdx;
     const uint4* wl;    // window lines (TF_WL): 128 bytes per bucket, see rt_wl_kernel
     const uint4* wl16;  // window lines for counts 9..16 (TF_WL16): 256 bytes per bucket
+    const uint4* wl32;  // window lines for counts 17..32 (TF_WL32): 384 bytes per bucket
     uint64_t rbase, nbase;
     uint32_t rshift, rslots, nshift, nslots;
     uint32_t n, B, index_base, flags;
@@ -101,6 +102,7 @@ constexpr uint32_t TF_DIRECT = 1u;   // radix slot s holds exactly bucket s (no 
 constexpr uint32_t TF_HAS_DUP = 2u;  // some nodes share their top 64 ID bits
 constexpr uint32_t TF_WL = 8u;       // window lines present (direct-mapped, uniform depth 1..43)
 constexpr uint32_t TF_WL16 = 16u;    // window lines for counts 9..16 present
+constexpr uint32_t TF_WL32 = 32u;    // window lines for counts 17..32 present
 constexpr uint32_t WIDE = 0x80000000u;  // dir[].x flag: bucket holds > 32 nodes (masks invalid)
 constexpr uint32_t KEY_PAD = 32;        // key[] is padded so 16-node chunk loads never leave it
 
@@ -992,6 +994,204 @@ __global__ void wl16_build_kernel(const uint64_t* key, const uint8_t* status, co
     L[3] = S;
 }
 
+// ---------------------------------------------------------------------------------------
+// Window lines for 17 <= count <= 32 (TF_WL32): the count <= 16 construction with R_32 <= 7
+// (windows of up to 16 buckets, a 4-bit D rank) and 64 slots with 20-bit in-bucket keys. A line is
+// 72 dwords (three 128-byte lines per bucket at a 384-byte stride):
+//   dw0      base (first node of W(R_32)'s lowest bucket)
+//   dw1, 2   G(r) for r = 0..3 and 4..7, 8 bits each (clamped to 255)
+//   dw3      whole(r) bits 0..7 | R_32 << 8 | S << 12 (stored slots, whole buckets only, <= 64) | defer << 31
+//   dw4, 5   round of the bucket of D rank j, 3 bits each (j < 10 in dw4, 10..15 in dw5)
+//   dw8..71  slots: jd << 28 | key20 << 8 | off
+// A query ranks the 64 slot values: four sorted groups of 16 (Batcher), two bitonic joins into sorted
+// 32s and one top-32 bitonic merge, min/max only. As for the 16-slot lines the answer is exact when
+// the slots kept (those of W(R_c)'s buckets) number at least m = min(c, G(R_c)): the slots hold whole
+// buckets in D order, so those of W(R_c) are its first buckets in D order.
+// ---------------------------------------------------------------------------------------
+constexpr uint32_t WL32_SLOTS = 64, WL32_HDR = 8, WL32_STRIDE = 96, WL32_KBITS = 20;  // dwords / bits
+
+// a[0..2H) sorted from its two sorted halves: one compare-exchange rank against the reversed upper
+// half splits it into two bitonic halves (lows, highs), then a half-cleaner cascade on each.
+template <int H>
+__device__ __forceinline__ void join_sorted(uint32_t* a) {
+#pragma unroll
+    for (int i = 0; i < H; i++) cx(a[i], a[2 * H - 1 - i]);
+#pragma unroll
+    for (int w = H / 2; w >= 1; w >>= 1)
+#pragma unroll
+        for (int i = 0; i < 2 * H; i++)
+            if ((i & w) == 0) cx(a[i], a[i + w]);
+}
+
+// a = the 32 smallest of (a, s), sorted; a and s sorted ascending on entry.
+__device__ __forceinline__ void merge32(uint32_t* a, const uint32_t* s) {
+#pragma unroll
+    for (int i = 0; i < 32; i++) a[i] = min(a[i], s[31 - i]);
+#pragma unroll
+    for (int w = 16; w >= 1; w >>= 1)
+#pragma unroll
+        for (int i = 0; i < 32; i++)
+            if ((i & w) == 0) cx(a[i], a[i + w]);
+}
+
+__device__ __forceinline__ bool wl32_answer(const DevTable& T, const Target& t, uint32_t b, uint32_t count, bool act,
+                                            uint32_t (&o)[32], uint32_t& m) {
+    uint32_t H[WL32_HDR], v[WL32_SLOTS];
+    if (act) {
+        const uint4* lp = T.wl32 + (WL32_STRIDE / 4) * (size_t)b;
+        uint4 q[(WL32_HDR + WL32_SLOTS) / 4];
+#pragma unroll
+        for (int x = 0; x < (int)(WL32_HDR + WL32_SLOTS) / 4; x++) q[x] = lp[x];
+        H[0] = q[0].x; H[1] = q[0].y; H[2] = q[0].z; H[3] = q[0].w;
+        H[4] = q[1].x; H[5] = q[1].y; H[6] = q[1].z; H[7] = q[1].w;
+#pragma unroll
+        for (int x = 0; x < (int)WL32_SLOTS / 4; x++) {
+            const uint4 u = q[WL32_HDR / 4 + x];
+            v[4 * x] = u.x; v[4 * x + 1] = u.y; v[4 * x + 2] = u.z; v[4 * x + 3] = u.w;
+        }
+    } else {
+#pragma unroll
+        for (int x = 0; x < (int)WL32_HDR; x++) H[x] = NONE;
+#pragma unroll
+        for (int x = 0; x < (int)WL32_SLOTS; x++) v[x] = NONE;
+    }
+    const uint32_t d = 64 - T.rshift;
+    const uint32_t h = H[3], S = (h >> 12) & 127u, R = (h >> 8) & 15u;
+    uint32_t Rc = 8, Gc = 0;
+#pragma unroll
+    for (int r = 7; r >= 0; r--) {
+        const uint32_t g = (H[1 + (r >> 2)] >> (8 * (r & 3))) & 255u;
+        if (g >= count || ((h >> r) & 1u)) { Rc = (uint32_t)r; Gc = g; }
+    }
+    m = min(count, Gc);
+    const bool own = (t.hi >> T.rshift) == (T.rbase >> T.rshift) + b;
+    bool ex = !act || (h & WL_DEFER) || !own || Rc > R;
+    const uint32_t tx = (uint32_t)((t.hi << d) >> (64 - WL32_KBITS)) << 8;
+#pragma unroll  // empty slots stay NONE (a real value of D rank 15 can exceed NONE ^ tx)
+    for (int s = 0; s < (int)WL32_SLOTS; s++) v[s] = (uint32_t)s < S ? v[s] ^ tx : NONE;
+    uint32_t have = S;
+    if (__any(!ex && Rc < R)) {  // a smaller window: drop the later rounds' buckets
+        uint32_t inc = 0;
+#pragma unroll
+        for (int j = 0; j < 16; j++) {
+            const uint32_t rj = j < 10 ? (H[4] >> (3 * j)) & 7u : (H[5] >> (3 * (j - 10))) & 7u;
+            inc |= (rj <= Rc ? 1u : 0u) << j;
+        }
+        have = 0;
+#pragma unroll
+        for (int s = 0; s < (int)WL32_SLOTS; s++) {
+            const bool in = (uint32_t)s < S && ((inc >> (v[s] >> 28)) & 1u);
+            v[s] = in ? v[s] : NONE;
+            have += in;
+        }
+    }
+    ex |= have < m;
+    sort16(v);
+    sort16(v + 16);
+    sort16(v + 32);
+    sort16(v + 48);
+    join_sorted<16>(v);
+    join_sorted<16>(v + 32);
+    merge32(v, v + 32);
+    const uint32_t base = H[0] + T.index_base;
+#pragma unroll
+    for (int j = 0; j < 32; j++) o[j] = (uint32_t)j < m ? base + (v[j] & 255u) : NONE;
+    return !ex;
+}
+
+// Row of up to 32 indices: 16-byte stores for counts divisible by 4, 8-byte stores for even counts.
+__device__ __forceinline__ void store_row32(uint32_t* row, const uint32_t (&o)[32], uint32_t count) {
+    if ((count & 3u) == 0 && ((uintptr_t)row & 15u) == 0) {
+#pragma unroll
+        for (int x = 0; x < 8; x++)
+            if ((uint32_t)(4 * x) < count)
+                reinterpret_cast<uint4*>(row)[x] = make_uint4(o[4 * x], o[4 * x + 1], o[4 * x + 2], o[4 * x + 3]);
+    } else if ((count & 1u) == 0 && ((uintptr_t)row & 7u) == 0) {
+#pragma unroll
+        for (int x = 0; x < 16; x++)
+            if ((uint32_t)(2 * x) < count) reinterpret_cast<uint2*>(row)[x] = make_uint2(o[2 * x], o[2 * x + 1]);
+    } else {
+#pragma unroll
+        for (int j = 0; j < 32; j++)
+            if ((uint32_t)j < count) row[j] = o[j];
+    }
+}
+
+__global__ __launch_bounds__(BLOCK) void rt_wl32_kernel(DevTable T, const uint8_t* __restrict__ targets, uint32_t q,
+                                                        uint32_t count, uint32_t* __restrict__ out_idx,
+                                                        uint8_t* __restrict__ out_cnt) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    const bool act = i < q;
+    Target t{};
+    uint32_t b = 0;
+    if (act) {
+        t = load_target(targets, i);
+        b = locate_bucket(T, t);
+    }
+    uint32_t o[32], m;
+    const bool ok = wl32_answer(T, t, b, count, act, o, m);
+    if (act && ok) {
+        store_row32(out_idx + (size_t)i * count, o, count);
+        if (out_cnt) out_cnt[i] = (uint8_t)m;
+    }
+    __shared__ uint64_t xs[BLOCK / 64][192];
+    exact_tail(T, t, act && !ok, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
+}
+
+// Window lines for counts 17..32 after a status change (or at creation): one thread per bucket.
+// The window's buckets are put in D order by rank (O(buckets^2), at most 16 buckets).
+__global__ void wl32_build_kernel(const uint64_t* key, const uint8_t* status, const uint2* dir, const uint32_t* gpre,
+                                  uint32_t B, uint32_t d, uint64_t pre0, uint32_t* lines) {
+    const uint32_t b = blockIdx.x * BLOCK + threadIdx.x;
+    if (b >= B) return;
+    uint32_t* L = lines + (size_t)WL32_STRIDE * b;
+    for (uint32_t k = 0; k < WL32_HDR + WL32_SLOTS; k++) L[k] = NONE;
+    uint32_t g01 = 0, g23 = 0, whole = 0, R = 8;
+    for (uint32_t r = 0; r < 8; r++) {
+        const uint32_t lo = b > r ? b - 1 - r : 0u, hi = min(B - 1, b + r);
+        const uint32_t g = min(gpre[hi + 1] - gpre[lo], 255u);
+        const bool w = lo == 0 && hi == B - 1;
+        if (r < 4) g01 |= g << (8 * r); else g23 |= g << (8 * (r - 4));
+        whole |= (w ? 1u : 0u) << r;
+        if (R == 8 && (g >= 32 || w)) R = r;
+    }
+    if (R == 8) { L[3] = WL_DEFER; return; }
+    const uint32_t lo = b > R ? b - 1 - R : 0u, hi = min(B - 1, b + R), nb = hi - lo + 1;
+    uint32_t ord[16];
+    for (uint32_t y = lo; y <= hi; y++) {
+        uint32_t rk = 0;
+        for (uint32_t z = lo; z <= hi; z++) rk += ((pre0 + z) ^ (pre0 + b)) < ((pre0 + y) ^ (pre0 + b));
+        ord[rk] = y;
+    }
+    const uint32_t base = dir[lo].x & ~WIDE;
+    uint32_t r04 = 0, r15 = 0, S = 0;
+    bool defer = false, full = false;
+    for (uint32_t j = 0; j < nb; j++) {
+        const uint32_t x = ord[j];
+        const uint32_t rd = x >= b ? x - b : b - 1 - x;
+        if (j < 10) r04 |= rd << (3 * j); else r15 |= rd << (3 * (j - 10));
+        const uint32_t j0 = dir[x].x & ~WIDE, j1 = dir[x + 1].x & ~WIDE;
+        const uint32_t g = gpre[x + 1] - gpre[x];
+        if (full || S + g > WL32_SLOTS) { full = true; continue; }  // whole buckets only
+        const uint32_t s0 = S;
+        for (uint32_t n = j0; n < j1; n++) {
+            if (!(status[n] & KAD_STATUS_GOOD)) continue;
+            const uint32_t k20 = (uint32_t)((key[n] << d) >> (64 - WL32_KBITS)), off = n - base;
+            defer |= off > 255u;
+            for (uint32_t s = s0; s < S; s++)
+                defer |= ((L[WL32_HDR + s] >> 8) & ((1u << WL32_KBITS) - 1)) == k20;
+            L[WL32_HDR + S] = (j << 28) | (k20 << 8) | (off & 255u);
+            S++;
+        }
+    }
+    L[0] = base;
+    L[1] = g01;
+    L[2] = g23;
+    L[3] = whole | (R << 8) | (S << 12) | (defer ? WL_DEFER : 0u);
+    L[4] = r04;
+    L[5] = r15;
+}
+
 template <int K>
 __global__ __launch_bounds__(BLOCK) void rt_closest_dual_kernel(DevTable T4, DevTable T6,
                                                                 const uint8_t* __restrict__ targets,
@@ -1071,6 +1271,38 @@ __global__ __launch_bounds__(BLOCK) void rt_dual_wl16_kernel(DevTable T4, DevTab
         if (out_cnt) out_cnt[i] = (uint8_t)m;
     } else if (act && !wl) {
         ex = !rt_query_fast<16, 3>(T, t, count, row, out_cnt ? out_cnt + i : nullptr);
+    }
+    __shared__ uint64_t xs[BLOCK / 64][192];
+    exact_tail(T4, t, ex && !six, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
+    exact_tail(T6, t, ex && six, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
+}
+
+// Dual-family batch for counts 17..32 where a family has 64-slot window lines (same structure).
+__global__ __launch_bounds__(BLOCK) void rt_dual_wl32_kernel(DevTable T4, DevTable T6,
+                                                             const uint8_t* __restrict__ targets,
+                                                             const uint8_t* __restrict__ af, uint32_t q, uint32_t count,
+                                                             uint32_t* __restrict__ out_idx,
+                                                             uint8_t* __restrict__ out_cnt) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    const bool act = i < q;
+    Target t{};
+    bool six = false;
+    if (act) {
+        t = load_target(targets, i);
+        six = af[i] != 0;
+    }
+    const DevTable& T = six ? T6 : T4;
+    const bool wl = act && (T.flags & TF_WL32);
+    const uint32_t b = wl ? locate_bucket(T, t) : 0u;
+    uint32_t o[32], m;
+    const bool ok = wl32_answer(T, t, b, count, wl, o, m);
+    uint32_t* row = out_idx + (size_t)i * count;
+    bool ex = wl && !ok;
+    if (wl && ok) {
+        store_row32(row, o, count);
+        if (out_cnt) out_cnt[i] = (uint8_t)m;
+    } else if (act && !wl) {
+        ex = !rt_query_fast<32, 6>(T, t, count, row, out_cnt ? out_cnt + i : nullptr);
     }
     __shared__ uint64_t xs[BLOCK / 64][192];
     exact_tail(T4, t, ex && !six, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
@@ -2032,6 +2264,7 @@ struct kad_table {
     uint32_t* gpre_mut = nullptr;
     uint32_t* wl_mut = nullptr;
     uint32_t* wl16_mut = nullptr;
+    uint32_t* wl32_mut = nullptr;
     // host copies of the bucket directory, for the incremental mirror (kad_table_apply)
     std::vector<uint32_t> h_off;
     std::vector<uint8_t> h_first;
@@ -2072,6 +2305,9 @@ int rebuild_good_prefix(kad_table* t, hipStream_t s) {
     if (t->wl16_mut)
         hipLaunchKernelGGL(wl16_build_kernel, dim3(grid_for(B)), dim3(BLOCK), 0, s, t->d.key, t->d.status, t->d.dir,
                            t->d.gpre, B, 64 - t->d.rshift, t->d.rbase >> t->d.rshift, t->wl16_mut);
+    if (t->wl32_mut)
+        hipLaunchKernelGGL(wl32_build_kernel, dim3(grid_for(B)), dim3(BLOCK), 0, s, t->d.key, t->d.status, t->d.dir,
+                           t->d.gpre, B, 64 - t->d.rshift, t->d.rbase >> t->d.rshift, t->wl32_mut);
     HIP_TRY(hipGetLastError());
     return KAD_OK;
 }
@@ -2097,6 +2333,8 @@ int launch_rt(const kad_table* t, const uint8_t* targets, uint32_t q, uint32_t c
             hipLaunchKernelGGL(rt_wl_kernel<0>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
     } else if (K == 16 && (d.flags & TF_WL16) && !(ev && std::strcmp(ev, "lane") == 0)) {
         hipLaunchKernelGGL(rt_wl16_kernel, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
+    } else if (K == 32 && (d.flags & TF_WL32) && !(ev && std::strcmp(ev, "lane") == 0)) {
+        hipLaunchKernelGGL(rt_wl32_kernel, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
     } else {
         hipLaunchKernelGGL(rt_closest_kernel<K>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
     }
@@ -2341,6 +2579,22 @@ int kad_table_create(kad_table** out, int device, uint32_t n_nodes, const uint8_
                 d.wl16 = reinterpret_cast<const uint4*>(lp16);
                 t->wl16_mut = lp16;
                 d.flags |= TF_WL16;
+                if (depth <= 44) {  // 20-bit in-bucket keys
+                    uint32_t* lp32;
+                    if ((rc = dev_upload(&lp32, nullptr, (size_t)WL32_STRIDE * n_buckets, t->owned, t->bytes))) {
+                        delete t;
+                        return rc;
+                    }
+                    hipLaunchKernelGGL(wl32_build_kernel, dim3(grid_for(n_buckets)), dim3(BLOCK), 0, 0, d.key, d.status,
+                                       d.dir, d.gpre, n_buckets, depth, pre0, lp32);
+                    if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+                        delete t;
+                        return set_err(KAD_ERR_HIP, "window-line (32) build failed");
+                    }
+                    d.wl32 = reinterpret_cast<const uint4*>(lp32);
+                    t->wl32_mut = lp32;
+                    d.flags |= TF_WL32;
+                }
             }
         }
     }
@@ -2461,6 +2715,9 @@ int kad_rt_closest_batch_dual(const kad_table* t4, const kad_table* t6, const ui
         hipLaunchKernelGGL(rt_dual_wl16_kernel, dim3(grid_for(q)), dim3(BLOCK), 0, s, d4, d6, targets, af, q, count,
                            out_idx, out_cnt);
     else if (count <= 16) launch_rt_dual<16>(d4, d6, targets, af, q, count, out_idx, out_cnt, s);
+    else if ((d4.flags | d6.flags) & TF_WL32)
+        hipLaunchKernelGGL(rt_dual_wl32_kernel, dim3(grid_for(q)), dim3(BLOCK), 0, s, d4, d6, targets, af, q, count,
+                           out_idx, out_cnt);
     else launch_rt_dual<32>(d4, d6, targets, af, q, count, out_idx, out_cnt, s);
     HIP_TRY(hipGetLastError());
     return KAD_OK;
@@ -2998,11 +3255,12 @@ int kad_table_apply(kad_table* t, const uint32_t* ops, uint32_t n_ops, const uin
         // a split breaks the uniform depth the window lines need
         release(t, t->wl_mut); t->wl_mut = nullptr; d.wl = nullptr; d.flags &= ~TF_WL;
         release(t, t->wl16_mut); t->wl16_mut = nullptr; d.wl16 = nullptr; d.flags &= ~TF_WL16;
-        release(t, t->wl16_mut); t->wl16_mut = nullptr; d.wl16 = nullptr; d.flags &= ~TF_WL16;
+        release(t, t->wl32_mut); t->wl32_mut = nullptr; d.wl32 = nullptr; d.flags &= ~TF_WL32;
     }
     if (!lines_ok && t->wl_mut) {
         release(t, t->wl_mut); t->wl_mut = nullptr; d.wl = nullptr; d.flags &= ~TF_WL;
         release(t, t->wl16_mut); t->wl16_mut = nullptr; d.wl16 = nullptr; d.flags &= ~TF_WL16;
+        release(t, t->wl32_mut); t->wl32_mut = nullptr; d.wl32 = nullptr; d.flags &= ~TF_WL32;
     }
     HIP_TRY(hipMemcpy(t->dir_mut, dir.data(), 8ull * (B1 + 1), hipMemcpyHostToDevice));
     // duplicate top-64 masks

@@ -106,9 +106,9 @@ def _wl_tables():
 
 @pytest.mark.parametrize("t", _wl_tables(), ids=lambda t: t["name"])
 def test_window_lines(gpu, t):
-    """Every count the window-line kernel serves (1..8) on U(d) tables of every density."""
+    """Every count the window-line kernels serve (1..8, 9..16, 17..32) on U(d) tables of every density."""
     with make(t, gpu) as T:
-        check_rt(T, t, TB.adversarial_targets(t, extra=4096), gpu, counts=tuple(range(1, 17)))
+        check_rt(T, t, TB.adversarial_targets(t, extra=4096), gpu, counts=tuple(range(1, 33)))
 
 
 def test_host_entry_points(gpu):
@@ -213,12 +213,13 @@ def test_primitives_batch(gpu):
 
 
 def test_config2_uniform_1M(gpu):
-    """Config 2: 1M-node table U(17) x 64k queries, k = 8, bit-exact on every query."""
+    """Config 2: 1M-node table U(17) x 64k queries, k = 8 (and the config 4 sweep's 16 and 32 on the
+    same table), bit-exact on every query."""
     n, q = 1_000_000, 65_536
     t = TB.uniform_config(n, 17)
     targets = S.random_targets(q)
     with make(t, gpu) as T:
-        check_rt(T, t, targets, gpu, counts=(8,))
+        check_rt(T, t, targets, gpu, counts=(8, 16, 32))
         check_nc(T, t, targets[:16384], gpu, counts=(14,))
 
 
@@ -231,16 +232,17 @@ def test_config3_full_shard_sample(gpu):
     sh = build_shard(spec, 0)
     q = 1 << 20
     targets = spec.targets_for(0, q, seed=1234)
-    with DeviceTable(sh.ids, sh.status, sh.first, sh.off, device=gpu.index or 0, sorted=True) as T:
-        idx, cnt = T.rt_closest(dev(targets, gpu), 8)
-        idx, cnt = u32(idx), cnt.cpu().numpy()
-    assert (cnt == 8).all()
     sample = np.random.default_rng(0).choice(q, 16384, replace=False)
-    want, wcnt = O.flat_rt_closest(sh.ids, sh.status, sh.first, sh.off, targets[sample], 8, nthreads=8)
-    np.testing.assert_array_equal(idx[sample], want)
-    # properties on all queries: results good and ascending in XOR distance
-    assert (sh.status[idx] & 1).all()
     key = sh.ids[:, :8].copy().view(">u8").reshape(-1)
     th = targets[:, :8].copy().view(">u8").reshape(-1)
-    d = key[idx] ^ th[:, None]
-    assert (d[:, 1:] >= d[:, :-1]).all()
+    with DeviceTable(sh.ids, sh.status, sh.first, sh.off, device=gpu.index or 0, sorted=True) as T:
+        for k in (8, 32):
+            idx, cnt = T.rt_closest(dev(targets, gpu), k)
+            idx, cnt = u32(idx), cnt.cpu().numpy()
+            assert (cnt == k).all()
+            want, wcnt = O.flat_rt_closest(sh.ids, sh.status, sh.first, sh.off, targets[sample], k, nthreads=8)
+            np.testing.assert_array_equal(idx[sample], want, err_msg=f"k={k}")
+            # properties on all queries: results good and ascending in XOR distance
+            assert (sh.status[idx] & 1).all()
+            d = key[idx] ^ th[:, None]
+            assert (d[:, 1:] >= d[:, :-1]).all()

@@ -94,3 +94,44 @@ def test_top16_of_32():
         v = rnd.sample(range(1 << 20), 32)
         acc = _merge16(_apply(net, v[:16]), _apply(net, v[16:]))
         assert acc == sorted(v)[:16]
+
+
+def _join_sorted(a):
+    """join_sorted<H> of kad_engine.hip: a sorted 2H from two sorted halves."""
+    h = len(a) // 2
+    net = [(i, 2 * h - 1 - i) for i in range(h)]
+    w = h // 2
+    while w >= 1:
+        net += [(i, i + w) for i in range(2 * h) if (i & w) == 0]
+        w //= 2
+    return _apply(net, a)
+
+
+def _merge32(a, s):
+    """merge32 of kad_engine.hip."""
+    a = [min(a[i], s[31 - i]) for i in range(32)]
+    net = [(i, i + w) for w in (16, 8, 4, 2, 1) for i in range(32) if (i & w) == 0]
+    return _apply(net, a)
+
+
+def test_join_sorted_01():
+    # 0-1 principle: every pair of sorted 0-1 halves of 16
+    for za in range(17):
+        for zb in range(17):
+            a = [0] * za + [1] * (16 - za) + [0] * zb + [1] * (16 - zb)
+            assert _join_sorted(a) == sorted(a)
+
+
+def test_top32_of_64():
+    """sort16 x 4 + join_sorted<16> x 2 + merge32 (the 64-slot lines' ranking) = the 32 smallest of
+    64, sorted; random distinct values and values with duplicates (the NONE padding)."""
+    net = _net("SORT16")
+    rnd = random.Random(13)
+    for trial in range(1500):
+        if trial % 3 == 0:
+            v = [rnd.randrange(40) for _ in range(64)]
+        else:
+            v = rnd.sample(range(1 << 20), 64)
+        g = [_apply(net, v[i:i + 16]) for i in (0, 16, 32, 48)]
+        acc = _merge32(_join_sorted(g[0] + g[1]), _join_sorted(g[2] + g[3]))
+        assert acc == sorted(v)[:32]

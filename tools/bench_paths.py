@@ -39,6 +39,14 @@ for k in (8, 14, 16, 32):
     us = timeit(lambda: T.rt_closest(tg, k))
     res[f"rt_k{k}_us"] = round(us, 1)
     res[f"rt_k{k}_Gq_s"] = round(q / us / 1e3, 2)
+os.environ["KAD_RT_KERNEL"] = "lane"
+for k in (16, 32):
+    us = timeit(lambda: T.rt_closest(tg, k))
+    res[f"rt_k{k}_lane_us"] = round(us, 1)
+a = T.rt_closest(tg, 32)
+os.environ.pop("KAD_RT_KERNEL")
+b = T.rt_closest(tg, 32)
+res["rt_k32_wl_equals_lane"] = bool(torch.equal(a[0], b[0]) and torch.equal(a[1], b[1]))
 us = timeit(lambda: T.nc_closest(tg, 14))
 res["nc_k14_us"], res["nc_k14_Gq_s"] = round(us, 1), round(q / us / 1e3, 2)
 af = (torch.arange(q, device=dev) % 2).to(torch.uint8)
