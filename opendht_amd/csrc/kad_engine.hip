@@ -93,6 +93,7 @@ struct DevTable {
     const uint4* wl;    // window lines (TF_WL): 128 bytes per bucket, see rt_wl_kernel
     const uint4* wl16;  // window lines for counts 9..16 (TF_WL16): 256 bytes per bucket
     const uint4* wl32;  // window lines for counts 17..32 (TF_WL32): 384 bytes per bucket
+    const uint4* ncl;   // NodeCache lines (TF_NCL): 256 bytes per node radix slot
     uint64_t rbase, nbase;
     uint32_t rshift, rslots, nshift, nslots;
     uint32_t n, B, index_base, flags;
@@ -103,6 +104,7 @@ constexpr uint32_t TF_HAS_DUP = 2u;  // some nodes share their top 64 ID bits
 constexpr uint32_t TF_WL = 8u;       // window lines present (direct-mapped, uniform depth 1..43)
 constexpr uint32_t TF_WL16 = 16u;    // window lines for counts 9..16 present
 constexpr uint32_t TF_WL32 = 32u;    // window lines for counts 17..32 present
+constexpr uint32_t TF_NCL = 64u;     // NodeCache lines present (sorted tables)
 constexpr uint32_t WIDE = 0x80000000u;  // dir[].x flag: bucket holds > 32 nodes (masks invalid)
 constexpr uint32_t KEY_PAD = 32;        // key[] is padded so 16-node chunk loads never leave it
 
@@ -1963,6 +1965,185 @@ __global__ __launch_bounds__(BLOCK) void nc_multi_kernel(DevTable T, const uint8
 }
 
 // ---------------------------------------------------------------------------------------
+// NodeCache lines (TF_NCL): one 256-byte line per node radix slot s answers the count <= 16
+// getCachedNodes queries whose target falls in s with one line load per lane (no lower_bound chain,
+// no wave cooperation). Line s holds the 60-node window w0 = r0-28 .. r0+32 of the sorted node array,
+// where [r0, r1) are the slot's nodes:
+//   dw0      w0
+//   dw1      ns = r1 - r0 | sh << 8
+//   dw2      defer | truncated left (w0 > 0) << 1 | truncated right (w0 + 60 < n) << 2
+//   dw4..63  slot j: key24(node w0+j) << 8 | expired
+// key24 = ID bits [40-sh, 64-sh) = (key >> sh) & 0xFFFFFF, starting at or above the window's common
+// prefix: all window nodes share the bits above, so every XOR comparison between them (the walk's
+// xorCmp) is decided inside those 24 bits (a line is deferred when two adjacent nodes share them).
+// The start is also at or above the slot's prefix, so "node < target" for the slot's nodes is a
+// key24 comparison (equal key24: exact path). Windows clamped at the array ends and
+// slots of more than 7 nodes are deferred (exact path): lb = r0 + x with x <= 7.
+//
+// The walk (node_cache.cpp:36-66) is the greedy merge by XOR distance of the left run lb-1, lb-2, ..
+// and the right run lb, lb+1, ..; in a greedy merge an element's place is set by the maximum
+// distance M along its run from lb to itself (tests/test_nodecache_merge.py), so the walk order is
+// the order of (M, side, steps from lb), with no ties between the runs (distinct IDs). A lane shifts
+// its window by x so that lb sits at slot 28 (three conditional shifts), scans 28 left and 32-x right
+// slots for M with static indices, drops expired nodes and keeps the `count` smallest keys (Batcher
+// sorts + bitonic merges). Nodes outside the window come after the window end of their side (larger
+// M or more steps), so the keys up to min(end key of a truncated side) are exact; fewer than `count`
+// of them means the walk leaves the window: the wave answers those lanes' queries one by one with
+// nc_answer (32-node runs each side of lb, wave-cooperative).
+// ---------------------------------------------------------------------------------------
+constexpr uint32_t NCL_SLOTS = 60, NCL_LEFT = 28, NCL_XMAX = 7, NCL_STRIDE = 64;  // dwords
+
+__device__ __forceinline__ bool ncl_answer(const DevTable& T, const Target& t, uint32_t s, uint32_t count,
+                                           uint32_t (&o)[16], uint32_t& m) {
+    const uint4* lp = T.ncl + (NCL_STRIDE / 4) * (size_t)s;
+    uint32_t v[64];
+    const uint4 hd = lp[0];
+#pragma unroll
+    for (int x = 1; x < (int)NCL_STRIDE / 4; x++) {
+        const uint4 u = lp[x];
+        v[4 * x - 4] = u.x; v[4 * x - 3] = u.y; v[4 * x - 2] = u.z; v[4 * x - 1] = u.w;
+    }
+    v[60] = v[61] = v[62] = v[63] = NONE;
+    const uint32_t w0 = hd.x, ns = hd.y & 255u, sh = (hd.y >> 8) & 63u, fl = hd.z;
+    const uint32_t t24 = (uint32_t)(t.hi >> sh) & 0xFFFFFFu;
+    bool ex = fl & 1u;
+    uint64_t expm = 0;
+    uint32_t x = 0;  // lb = r0 + x: the slot's nodes below the target
+#pragma unroll
+    for (int j = 0; j < (int)NCL_SLOTS; j++) {
+        const uint32_t k24 = v[j] >> 8;
+        expm |= (uint64_t)(v[j] & 1u) << j;
+        if (j >= (int)NCL_LEFT && j < (int)(NCL_LEFT + NCL_XMAX) && (uint32_t)j - NCL_LEFT < ns) {
+            ex |= k24 == t24;
+            x += k24 < t24 ? 1u : 0u;
+        }
+        v[j] = k24 ^ t24;  // XOR distance inside the window's 24 bits
+    }
+    // shift the window by x: lb at slot 28, the left run 27..0, the right run 28..59-x
+    {
+        uint32_t u[64];
+#pragma unroll
+        for (int j = 0; j < 64; j++) u[j] = (x & 1u) ? (j < 63 ? v[j + 1] : NONE) : v[j];
+#pragma unroll
+        for (int j = 0; j < 64; j++) v[j] = (x & 2u) ? (j < 62 ? u[j + 2] : NONE) : u[j];
+#pragma unroll
+        for (int j = 0; j < 64; j++) u[j] = (x & 4u) ? (j < 60 ? v[j + 4] : NONE) : v[j];
+#pragma unroll
+        for (int j = 0; j < 64; j++) v[j] = u[j];
+    }
+    expm >>= x;
+    const uint32_t nv = NCL_SLOTS - x;  // valid slots after the shift
+    // keys: (M along the run) << 8 | side << 7 | window slot (63 - j on the left, j on the right: the
+    // order of the steps from lb inside each run)
+    uint32_t run = 0;
+#pragma unroll
+    for (int j = (int)NCL_LEFT - 1; j >= 0; j--) {
+        run = max(run, v[j]);
+        v[j] = (run << 8) | (63u - (uint32_t)j);
+    }
+    const uint32_t endL = ((fl & 2u) || x > 0) ? v[0] : NONE;  // more nodes left of the window?
+    run = 0;
+    uint32_t endR = NONE;
+#pragma unroll
+    for (int j = (int)NCL_LEFT; j < (int)NCL_SLOTS; j++) {
+        run = max(run, (uint32_t)j < nv ? v[j] : 0u);
+        v[j] = (run << 8) | 128u | (uint32_t)j;
+        if (j >= (int)(NCL_SLOTS - NCL_XMAX - 1) && (uint32_t)j == nv - 1) endR = v[j];
+    }
+    if (!(fl & 4u)) endR = NONE;  // the window reaches the array end
+    const uint32_t lim = min(endL, endR);  // keys <= lim are the walk's first steps
+    uint32_t have = 0;
+#pragma unroll
+    for (int j = 0; j < (int)NCL_SLOTS; j++) {
+        const bool in = !((expm >> j) & 1u) && (uint32_t)j < nv && v[j] <= lim;
+        v[j] = in ? v[j] : NONE;
+        have += in;
+    }
+    m = min(count, have);
+    ex |= have < count && lim != NONE;
+    sort16(v);
+    sort16(v + 16);
+    sort16(v + 32);
+    sort16(v + 48);
+    merge16(v, v + 16);
+    merge16(v + 32, v + 48);
+    merge16(v, v + 32);
+    const uint32_t base = w0 + x + T.index_base;
+#pragma unroll
+    for (int r = 0; r < 16; r++) {
+        const uint32_t k = v[r], st = k & 127u;
+        const uint32_t j = (k & 128u) ? st : 63u - st;
+        o[r] = (uint32_t)r < m ? base + j : NONE;
+    }
+    return !ex;
+}
+
+__global__ __launch_bounds__(BLOCK) void nc_line_kernel(DevTable T, const uint8_t* __restrict__ targets, uint32_t q,
+                                                        uint32_t count, uint32_t* __restrict__ out_idx,
+                                                        uint8_t* __restrict__ out_cnt) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x, lane = threadIdx.x & 63u;
+    const bool act = i < q;
+    Target t{};
+    bool ok = false;
+    if (act) {
+        t = load_target(targets, i);
+        // below the first slot / past the last: lb = 0 / n, windows clamped at the ends (exact path)
+        const bool inside = t.hi >= T.nbase && ((t.hi - T.nbase) >> T.nshift) < T.nslots;
+        uint32_t o[16], m;
+        if (inside && ncl_answer(T, t, (uint32_t)((t.hi - T.nbase) >> T.nshift), count, o, m)) {
+            ok = true;
+            uint32_t* row = out_idx + (size_t)i * count;
+            store_row16(row, o, count);
+            if (out_cnt) out_cnt[i] = (uint8_t)m;
+        }
+    }
+    // the lanes the lines could not answer: one query at a time by the whole wave (nc_answer: 32-node
+    // runs each side of lb, itself falling back to lane 0's serial walk)
+    uint64_t pend = __ballot(act && !ok);
+    while (pend) {
+        const uint32_t l = (uint32_t)__builtin_ctzll(pend);
+        pend &= pend - 1;
+        Target u;
+        u.hi = shfl64(t.hi, (int)l);
+        u.t2 = (uint32_t)__shfl((int)t.t2, (int)l, 64);
+        u.t3 = (uint32_t)__shfl((int)t.t3, (int)l, 64);
+        u.t4 = (uint32_t)__shfl((int)t.t4, (int)l, 64);
+        uint32_t r0, r1;
+        nc_slot(T, u, r0, r1);
+        const NcWindow w = nc_window(T, r0, lane);
+        nc_answer(T, u, r0, r1, w, lane, i - lane + l, count, out_idx, out_cnt);
+    }
+}
+
+// NodeCache lines after a status change (or at creation): one thread per radix slot.
+__global__ void ncl_build_kernel(const uint64_t* key, const uint8_t* status, const uint32_t* nrdx, uint32_t nslots,
+                                 uint32_t n, uint32_t slot_prefix, uint32_t* lines) {
+    const uint32_t s = blockIdx.x * BLOCK + threadIdx.x;
+    if (s >= nslots) return;
+    uint32_t* L = lines + (size_t)NCL_STRIDE * s;
+    const uint32_t r0 = nrdx[s], r1 = nrdx[s + 1], ns = r1 - r0;
+    if (r0 < NCL_LEFT || (uint64_t)r0 - NCL_LEFT + NCL_SLOTS > n || ns > NCL_XMAX) {  // clamped window / wide slot
+        L[0] = 0; L[1] = 0; L[2] = 1u; L[3] = 0;
+        return;
+    }
+    const uint32_t w0 = r0 - NCL_LEFT;
+    const uint32_t P = (uint32_t)__builtin_clzll((key[w0] ^ key[w0 + NCL_SLOTS - 1]) | 1ull);
+    const uint32_t Pp = min(min(P, slot_prefix), 40u), sh = 40 - Pp;
+    bool defer = false;
+    uint32_t prev = 0;
+    for (uint32_t j = 0; j < NCL_SLOTS; j++) {
+        const uint32_t k24 = (uint32_t)(key[w0 + j] >> sh) & 0xFFFFFFu;
+        defer |= j > 0 && k24 == prev;
+        prev = k24;
+        L[4 + j] = (k24 << 8) | ((status[w0 + j] & KAD_STATUS_EXPIRED) ? 1u : 0u);
+    }
+    L[0] = w0;
+    L[1] = ns | (sh << 8);
+    L[2] = (defer ? 1u : 0u) | (w0 > 0 ? 2u : 0u) | (w0 + NCL_SLOTS < n ? 4u : 0u);
+    L[3] = 0;
+}
+
+// ---------------------------------------------------------------------------------------
 // Incremental device mirror: kad_table_apply re-lays the node arrays out on
 // the device from a host plan of segments (an untouched bucket is one range of old nodes; an edited
 // bucket an explicit handle list), then re-derives masks, prefix sums, dup masks and lines on the
@@ -2265,6 +2446,7 @@ struct kad_table {
     uint32_t* wl_mut = nullptr;
     uint32_t* wl16_mut = nullptr;
     uint32_t* wl32_mut = nullptr;
+    uint32_t* ncl_mut = nullptr;
     // host copies of the bucket directory, for the incremental mirror (kad_table_apply)
     std::vector<uint32_t> h_off;
     std::vector<uint8_t> h_first;
@@ -2292,6 +2474,9 @@ bool is_gfx950(int dev) {
 // Rebuild dir[].y (good prefix sums) from the device status array. Async on stream.
 int rebuild_good_prefix(kad_table* t, hipStream_t s) {
     const uint32_t B = t->d.B;
+    if (t->ncl_mut)  // NodeCache lines carry the expired bits
+        hipLaunchKernelGGL(ncl_build_kernel, dim3(grid_for(t->d.nslots)), dim3(BLOCK), 0, s, t->d.key, t->d.status,
+                           t->d.nrdx, t->d.nslots, t->d.n, 64 - t->d.nshift, t->ncl_mut);
     if (B == 0) return KAD_OK;
     const uint32_t m = B + 1;
     const uint32_t tiles = (m + SCAN_TILE - 1) / SCAN_TILE;
@@ -2607,6 +2792,17 @@ int kad_table_create(kad_table** out, int device, uint32_t n_nodes, const uint8_
         uint32_t* dn;
         if ((rc = dev_upload(&dn, rdx.data(), rdx.size(), t->owned, t->bytes))) { delete t; return rc; }
         d.nrdx = dn; d.nbase = r.base; d.nshift = r.shift; d.nslots = r.slots; t->nbits = r.bits;
+        uint32_t* lp;
+        if ((rc = dev_upload(&lp, nullptr, (size_t)NCL_STRIDE * r.slots, t->owned, t->bytes))) { delete t; return rc; }
+        hipLaunchKernelGGL(ncl_build_kernel, dim3(grid_for(r.slots)), dim3(BLOCK), 0, 0, d.key, d.status, dn, r.slots,
+                           n_nodes, 64 - r.shift, lp);
+        if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+            delete t;
+            return set_err(KAD_ERR_HIP, "NodeCache line build failed");
+        }
+        d.ncl = reinterpret_cast<const uint4*>(lp);
+        t->ncl_mut = lp;
+        d.flags |= TF_NCL;
     }
     *out = t;
     return KAD_OK;
@@ -2885,7 +3081,11 @@ int kad_nc_closest_batch(const kad_table* t, const uint8_t* targets, uint32_t q,
     if (!targets || (!out_idx && count)) return set_err(KAD_ERR_INVALID, "NULL buffer");
     DeviceGuard g(t->device);
     const char* ev = std::getenv("KAD_NC_KERNEL");
-    if (count >= 1 && count <= 16 && ev && std::strcmp(ev, "group1") == 0)
+    const bool lines = (t->d.flags & TF_NCL) && !ev;  // KAD_NC_KERNEL=<kernel> picks another one (A/B timing)
+    if (lines && count >= 1 && count <= 16)
+        hipLaunchKernelGGL(nc_line_kernel, dim3(grid_for(q)), dim3(BLOCK), 0, (hipStream_t)stream, t->d, targets, q,
+                           count, out_idx, out_cnt);
+    else if (count >= 1 && count <= 16 && ev && std::strcmp(ev, "group1") == 0)
         hipLaunchKernelGGL(nc_group_v1_kernel, dim3((q + BLOCK / 64 - 1) / (BLOCK / 64)), dim3(BLOCK), 0,
                            (hipStream_t)stream, t->d, targets, q, count, out_idx, out_cnt);
     else if (count >= 1 && count <= 16 && ev && std::strcmp(ev, "group2") == 0)
@@ -3227,6 +3427,7 @@ int kad_table_apply(kad_table* t, const uint32_t* ops, uint32_t n_ops, const uin
     if (structural) {
         t->flags &= ~KAD_TABLE_SORTED;
         release(t, const_cast<uint32_t*>(d.nrdx)); d.nrdx = nullptr; t->nbits = 0;
+        release(t, t->ncl_mut); t->ncl_mut = nullptr; d.ncl = nullptr; d.flags &= ~TF_NCL;
     }
     release(t, t->wrec); t->wrec = nullptr; t->addr_len = 0;
     release(t, t->time_ns); release(t, t->reply_ns); release(t, t->expired);

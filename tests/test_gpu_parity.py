@@ -246,3 +246,65 @@ def test_config3_full_shard_sample(gpu):
             assert (sh.status[idx] & 1).all()
             d = key[idx] ^ th[:, None]
             assert (d[:, 1:] >= d[:, :-1]).all()
+
+
+def _nc_tables():
+    """Sorted tables for the NodeCache lines: U(d) tables of every density and good/expired mix,
+    and a clustered table (300 IDs sharing their top 56 bits, 80 sharing the top 72: windows whose
+    common prefix is deeper than the 24-bit line keys reach, and top-64 ties)."""
+    out = _wl_tables()
+    rng = np.random.default_rng(0xC1)
+    base = S.random_ids(3000, 0xC1C1)
+    c1 = np.repeat(base[:1], 300, 0)
+    c1[:, 7:] = rng.integers(0, 256, (300, 13), dtype=np.uint8)
+    c2 = np.repeat(base[1:2], 80, 0)
+    c2[:, 9:] = rng.integers(0, 256, (80, 11), dtype=np.uint8)
+    ids = np.unique(np.concatenate([base, c1, c2]), axis=0)
+    first, off = S.uniform_buckets(ids, 8)
+    t = TB.table(ids, S.random_status(ids.shape[0], 0xC2, 70, 20), first, off, sorted_=True, name="clustered")
+    t["near"] = np.concatenate([c1[:64], c2[:32]])
+    out.append(t)
+    return out
+
+
+def _nc_targets(t):
+    parts = [TB.adversarial_targets(t, extra=4096)]
+    if "near" in t:  # cluster members with their last byte changed: targets inside the clusters
+        near = t["near"].copy()
+        near[:, 19] ^= 0x5A
+        parts.append(near)
+    return np.ascontiguousarray(np.concatenate(parts))
+
+
+@pytest.mark.parametrize("kernel", ["lines", "multi2"])
+@pytest.mark.parametrize("t", _nc_tables(), ids=lambda t: t["name"])
+def test_nc_lines(gpu, t, kernel, monkeypatch):
+    """NodeCache::getCachedNodes for every count 1..16 (the line kernel, default; KAD_NC_KERNEL=multi2:
+    the wave-per-query kernel) and 17..32, 40 (the serial walk)."""
+    if kernel != "lines":
+        monkeypatch.setenv("KAD_NC_KERNEL", kernel)
+    with make(t, gpu) as T:
+        check_nc(T, t, _nc_targets(t), gpu, counts=tuple(range(1, 33)) + (40,))
+
+
+def test_nc_lines_after_status_change(gpu):
+    """The lines carry the expired bits: kad_table_update_status and the device isGood/isExpired
+    refresh rebuild them."""
+    t = TB.uniform_config(20_000, 11, seed=0x57A7)
+    targets = TB.adversarial_targets(t, extra=4096)
+    rng = np.random.default_rng(6)
+    n = t["ids"].shape[0]
+    with make(t, gpu) as T:
+        st2 = rng.choice(np.array([0, 1, 2, 2, 3], np.uint8), size=n)
+        T.update_status(st2)
+        check_nc(T, dict(t, status=st2), targets, gpu, counts=(8, 14, 32))
+        now, m = 10 * 3600 * 10**9, 60 * 10**9
+        time_ns = now - rng.integers(0, 20, n) * m
+        reply_ns = now - rng.integers(0, 200, n) * m
+        expired = (rng.random(n) < 0.3).astype(np.uint8)
+        T.set_times(time_ns, reply_ns, expired)
+        T.refresh_status(now)
+        torch.cuda.synchronize()
+        good = (expired == 0) & (reply_ns >= now - 120 * m) & (time_ns >= now - 10 * m)
+        st3 = (good.astype(np.uint8) | (expired << 1)).astype(np.uint8)
+        check_nc(T, dict(t, status=st3), targets, gpu, counts=(8, 14, 32))

@@ -83,7 +83,14 @@ os.environ.pop("KAD_NC_KERNEL")
 torch.cuda.synchronize()
 res["nc_k14_group2_us"] = round(us, 1)
 res["nc_group2_equals"] = bool(torch.equal(a[0], c[0]) and torch.equal(a[1], c[1]))
-for k in (1, 8, 16):
+os.environ["KAD_NC_KERNEL"] = "multi2"  # wave per query, two queries' loads interleaved
+us = timeit(lambda: T.nc_closest(tg, 14))
+c = T.nc_closest(tg, 14)
+os.environ.pop("KAD_NC_KERNEL")
+torch.cuda.synchronize()
+res["nc_k14_multi2_us"] = round(us, 1)
+res["nc_multi2_equals"] = bool(torch.equal(a[0], c[0]) and torch.equal(a[1], c[1]))
+for k in (1, 8, 16, 32):
     us = timeit(lambda: T.nc_closest(tg, k))
     res[f"nc_k{k}_us"] = round(us, 1)
 print(json.dumps(res, indent=1))
