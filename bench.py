@@ -106,8 +106,9 @@ def main():
     out_idx = torch.empty((args.queries, args.count), dtype=torch.int32, device=dev)
     out_cnt = torch.empty((args.queries,), dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev)
-    wl = args.count <= 8 and bool(T.info()["flags"] & KAD_INFO_WINDOW_LINES)
-    kernel = "rt_wl_kernel<0>" if wl else f"rt_closest_kernel<{8 if args.count <= 8 else 16 if args.count <= 16 else 32}>"
+    wl = bool(T.info()["flags"] & KAD_INFO_WINDOW_LINES)  # the shard's U(24) table carries all three line sets
+    kernel = (("rt_wl_kernel<0>" if args.count <= 8 else "rt_wl16_kernel" if args.count <= 16 else "rt_wl32_kernel")
+              if wl else f"rt_closest_kernel<{8 if args.count <= 8 else 16 if args.count <= 16 else 32}>")
 
     # algorithmic bytes of one launch (exact, host side; target buckets from the engine's findBucket)
     tb = T.find_bucket(tg).cpu().numpy().view(np.uint32).astype(np.int64)
