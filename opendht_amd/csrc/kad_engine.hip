@@ -1978,20 +1978,20 @@ __global__ __launch_bounds__(BLOCK) void nc_multi_kernel(DevTable T, const uint8
 // xorCmp) is decided inside those 24 bits (a line is deferred when two adjacent nodes share them).
 // The start is also at or above the slot's prefix, so "node < target" for the slot's nodes is a
 // key24 comparison (equal key24: exact path). Windows clamped at the array ends and
-// slots of more than 7 nodes are deferred (exact path): lb = r0 + x with x <= 7.
+// slots of more than 15 nodes are deferred (exact path): lb = r0 + x with x <= 15.
 //
 // The walk (node_cache.cpp:36-66) is the greedy merge by XOR distance of the left run lb-1, lb-2, ..
 // and the right run lb, lb+1, ..; in a greedy merge an element's place is set by the maximum
 // distance M along its run from lb to itself (tests/test_nodecache_merge.py), so the walk order is
 // the order of (M, side, steps from lb), with no ties between the runs (distinct IDs). A lane shifts
-// its window by x so that lb sits at slot 28 (three conditional shifts), scans 28 left and 32-x right
-// slots for M with static indices, drops expired nodes and keeps the `count` smallest keys (Batcher
-// sorts + bitonic merges). Nodes outside the window come after the window end of their side (larger
+// its window by x so that lb sits at slot 28 (four conditional shifts) and scans 28 left and 32-x
+// right slots for M with static indices. Each run's keys ascend outward from lb, so the walk's first
+// 32 steps are one top-32 bitonic merge of the two runs; the non-expired ones are then compacted. Nodes outside the window come after the window end of their side (larger
 // M or more steps), so the keys up to min(end key of a truncated side) are exact; fewer than `count`
 // of them means the walk leaves the window: the wave answers those lanes' queries one by one with
 // nc_answer (32-node runs each side of lb, wave-cooperative).
 // ---------------------------------------------------------------------------------------
-constexpr uint32_t NCL_SLOTS = 60, NCL_LEFT = 28, NCL_XMAX = 7, NCL_STRIDE = 64;  // dwords
+constexpr uint32_t NCL_SLOTS = 60, NCL_LEFT = 28, NCL_XMAX = 15, NCL_STRIDE = 64;  // dwords
 
 __device__ __forceinline__ bool ncl_answer(const DevTable& T, const Target& t, uint32_t s, uint32_t count,
                                            uint32_t (&o)[16], uint32_t& m) {
@@ -2007,17 +2007,15 @@ __device__ __forceinline__ bool ncl_answer(const DevTable& T, const Target& t, u
     const uint32_t w0 = hd.x, ns = hd.y & 255u, sh = (hd.y >> 8) & 63u, fl = hd.z;
     const uint32_t t24 = (uint32_t)(t.hi >> sh) & 0xFFFFFFu;
     bool ex = fl & 1u;
-    uint64_t expm = 0;
     uint32_t x = 0;  // lb = r0 + x: the slot's nodes below the target
 #pragma unroll
     for (int j = 0; j < (int)NCL_SLOTS; j++) {
         const uint32_t k24 = v[j] >> 8;
-        expm |= (uint64_t)(v[j] & 1u) << j;
         if (j >= (int)NCL_LEFT && j < (int)(NCL_LEFT + NCL_XMAX) && (uint32_t)j - NCL_LEFT < ns) {
             ex |= k24 == t24;
             x += k24 < t24 ? 1u : 0u;
         }
-        v[j] = k24 ^ t24;  // XOR distance inside the window's 24 bits
+        v[j] = ((k24 ^ t24) << 8) | (v[j] & 1u);  // XOR distance inside the window's 24 bits | expired
     }
     // shift the window by x: lb at slot 28, the left run 27..0, the right run 28..59-x
     {
@@ -2029,55 +2027,71 @@ __device__ __forceinline__ bool ncl_answer(const DevTable& T, const Target& t, u
 #pragma unroll
         for (int j = 0; j < 64; j++) u[j] = (x & 4u) ? (j < 60 ? v[j + 4] : NONE) : v[j];
 #pragma unroll
-        for (int j = 0; j < 64; j++) v[j] = u[j];
+        for (int j = 0; j < 64; j++) v[j] = (x & 8u) ? (j < 56 ? u[j + 8] : NONE) : u[j];
     }
-    expm >>= x;
     const uint32_t nv = NCL_SLOTS - x;  // valid slots after the shift
-    // keys: (M along the run) << 8 | side << 7 | window slot (63 - j on the left, j on the right: the
-    // order of the steps from lb inside each run)
+    // keys: (M along the run) << 8 | side << 7 | steps from lb << 1 | expired. Each run's keys ascend
+    // outward from lb (M never decreases, the steps grow), and the expired bit is below the steps.
     uint32_t run = 0;
 #pragma unroll
     for (int j = (int)NCL_LEFT - 1; j >= 0; j--) {
-        run = max(run, v[j]);
-        v[j] = (run << 8) | (63u - (uint32_t)j);
+        run = max(run, v[j] & ~255u);
+        v[j] = run | ((uint32_t)(NCL_LEFT - 1 - j) << 1) | (v[j] & 1u);
     }
     const uint32_t endL = ((fl & 2u) || x > 0) ? v[0] : NONE;  // more nodes left of the window?
     run = 0;
     uint32_t endR = NONE;
 #pragma unroll
     for (int j = (int)NCL_LEFT; j < (int)NCL_SLOTS; j++) {
-        run = max(run, (uint32_t)j < nv ? v[j] : 0u);
-        v[j] = (run << 8) | 128u | (uint32_t)j;
+        const bool in = (uint32_t)j < nv;
+        run = max(run, in ? v[j] & ~255u : 0u);
+        v[j] = in ? run | 128u | ((uint32_t)(j - NCL_LEFT) << 1) | (v[j] & 1u) : NONE;
         if (j >= (int)(NCL_SLOTS - NCL_XMAX - 1) && (uint32_t)j == nv - 1) endR = v[j];
     }
     if (!(fl & 4u)) endR = NONE;  // the window reaches the array end
     const uint32_t lim = min(endL, endR);  // keys <= lim are the walk's first steps
-    uint32_t have = 0;
+    // the walk's first 32 steps: top-32 merge of the two ascending runs (left 28 reversed + 4 NONE,
+    // right 32), then a bitonic half-cleaner cascade
+    uint32_t w[32];
 #pragma unroll
-    for (int j = 0; j < (int)NCL_SLOTS; j++) {
-        const bool in = !((expm >> j) & 1u) && (uint32_t)j < nv && v[j] <= lim;
-        v[j] = in ? v[j] : NONE;
-        have += in;
+    for (int r = 0; r < 32; r++) {
+        const uint32_t a = r < (int)NCL_LEFT ? v[NCL_LEFT - 1 - r] : NONE;  // left, ascending
+        w[r] = min(a, v[NCL_LEFT + 31 - r]);                              // right, descending
+    }
+#pragma unroll
+    for (int h = 16; h >= 1; h >>= 1)
+#pragma unroll
+        for (int r = 0; r < 32; r++)
+            if ((r & h) == 0) cx(w[r], w[r + h]);
+    // emit the non-expired steps up to lim: the c-th emission lies at step c..c+7
+    uint32_t have = 0, rank[32];
+    bool keep[32];
+#pragma unroll
+    for (int r = 0; r < 32; r++) {
+        keep[r] = w[r] <= lim && !(w[r] & 1u);
+        rank[r] = have;
+        have += keep[r];
     }
     m = min(count, have);
-    ex |= have < count && lim != NONE;
-    sort16(v);
-    sort16(v + 16);
-    sort16(v + 32);
-    sort16(v + 48);
-    merge16(v, v + 16);
-    merge16(v + 32, v + 48);
-    merge16(v, v + 32);
+    ex |= have < count && (lim != NONE || w[31] != NONE);  // the walk goes on past the window / step 32
     const uint32_t base = w0 + x + T.index_base;
 #pragma unroll
-    for (int r = 0; r < 16; r++) {
-        const uint32_t k = v[r], st = k & 127u;
-        const uint32_t j = (k & 128u) ? st : 63u - st;
-        o[r] = (uint32_t)r < m ? base + j : NONE;
+    for (int c = 0; c < 16; c++) {
+        uint32_t oc = NONE;
+#pragma unroll
+        for (int r = c; r < c + 8 && r < 32; r++) {
+            const uint32_t st = (w[r] >> 1) & 63u;
+            const uint32_t j = (w[r] & 128u) ? NCL_LEFT + st : NCL_LEFT - 1 - st;
+            oc = keep[r] && rank[r] == (uint32_t)c ? base + j : oc;
+        }
+        ex |= (uint32_t)c < m && oc == NONE;  // more than 7 skipped steps before emission c
+        o[c] = (uint32_t)c < m ? oc : NONE;
     }
     return !ex;
 }
 
+// ABL 1 (timing ablation only, KAD_NC_KERNEL=lines_abl1; results wrong): no exact path.
+template <int ABL>
 __global__ __launch_bounds__(BLOCK) void nc_line_kernel(DevTable T, const uint8_t* __restrict__ targets, uint32_t q,
                                                         uint32_t count, uint32_t* __restrict__ out_idx,
                                                         uint8_t* __restrict__ out_cnt) {
@@ -2099,7 +2113,7 @@ __global__ __launch_bounds__(BLOCK) void nc_line_kernel(DevTable T, const uint8_
     }
     // the lanes the lines could not answer: one query at a time by the whole wave (nc_answer: 32-node
     // runs each side of lb, itself falling back to lane 0's serial walk)
-    uint64_t pend = __ballot(act && !ok);
+    uint64_t pend = ABL ? 0ull : __ballot(act && !ok);
     while (pend) {
         const uint32_t l = (uint32_t)__builtin_ctzll(pend);
         pend &= pend - 1;
@@ -3082,8 +3096,11 @@ int kad_nc_closest_batch(const kad_table* t, const uint8_t* targets, uint32_t q,
     DeviceGuard g(t->device);
     const char* ev = std::getenv("KAD_NC_KERNEL");
     const bool lines = (t->d.flags & TF_NCL) && !ev;  // KAD_NC_KERNEL=<kernel> picks another one (A/B timing)
-    if (lines && count >= 1 && count <= 16)
-        hipLaunchKernelGGL(nc_line_kernel, dim3(grid_for(q)), dim3(BLOCK), 0, (hipStream_t)stream, t->d, targets, q,
+    if ((t->d.flags & TF_NCL) && ev && std::strcmp(ev, "lines_abl1") == 0 && count >= 1 && count <= 16)
+        hipLaunchKernelGGL(nc_line_kernel<1>, dim3(grid_for(q)), dim3(BLOCK), 0, (hipStream_t)stream, t->d, targets, q,
+                           count, out_idx, out_cnt);
+    else if (lines && count >= 1 && count <= 16)
+        hipLaunchKernelGGL(nc_line_kernel<0>, dim3(grid_for(q)), dim3(BLOCK), 0, (hipStream_t)stream, t->d, targets, q,
                            count, out_idx, out_cnt);
     else if (count >= 1 && count <= 16 && ev && std::strcmp(ev, "group1") == 0)
         hipLaunchKernelGGL(nc_group_v1_kernel, dim3((q + BLOCK / 64 - 1) / (BLOCK / 64)), dim3(BLOCK), 0,

@@ -93,6 +93,20 @@ res["nc_multi2_equals"] = bool(torch.equal(a[0], c[0]) and torch.equal(a[1], c[1
 for k in (1, 8, 16, 32):
     us = timeit(lambda: T.nc_closest(tg, k))
     res[f"nc_k{k}_us"] = round(us, 1)
+os.environ["KAD_NC_KERNEL"] = "lines_abl1"  # ablation: the line kernel without its exact path
+for k in (1, 14):
+    us = timeit(lambda: T.nc_closest(tg, k))
+    res[f"nc_k{k}_lines_no_exact_us"] = round(us, 1)
+c = T.nc_closest(tg, 14)
+os.environ.pop("KAD_NC_KERNEL")
+torch.cuda.synchronize()
+res["nc_k14_lines_exact_rows"] = int((c[0] != a[0]).any(dim=1).sum().item())  # rows the exact path fixes
+a1 = T.nc_closest(tg, 1)
+os.environ["KAD_NC_KERNEL"] = "lines_abl1"
+c1 = T.nc_closest(tg, 1)
+os.environ.pop("KAD_NC_KERNEL")
+torch.cuda.synchronize()
+res["nc_k1_lines_exact_rows"] = int((c1[0] != a1[0]).any(dim=1).sum().item())
 print(json.dumps(res, indent=1))
 
 # InfoHash primitives and the wire / hash rows: throughput and effective HBM bandwidth (bytes each
