@@ -92,7 +92,7 @@ struct DevTable {
     const uint32_t* nrdx;
     const uint4* wl;    // window lines (TF_WL): 128 bytes per bucket, see rt_wl_kernel
     const uint4* wl16;  // window lines for counts 9..16 (TF_WL16): 256 bytes per bucket
-    const uint4* wl32;  // window lines for counts 17..32 (TF_WL32): 384 bytes per bucket
+    const uint4* wl32;  // window lines for counts 17..32 (TF_WL32): 256 bytes per bucket
     const uint4* ncl;   // NodeCache lines (TF_NCL): 256 bytes per node radix slot
     uint64_t rbase, nbase;
     uint32_t rshift, rslots, nshift, nslots;
@@ -998,19 +998,20 @@ __global__ void wl16_build_kernel(const uint64_t* key, const uint8_t* status, co
 
 // ---------------------------------------------------------------------------------------
 // Window lines for 17 <= count <= 32 (TF_WL32): the count <= 16 construction with R_32 <= 7
-// (windows of up to 16 buckets, a 4-bit D rank) and 64 slots with 20-bit in-bucket keys. A line is
-// 72 dwords (three 128-byte lines per bucket at a 384-byte stride):
+// (windows of up to 16 buckets, a 4-bit D rank) and 58 slots with 20-bit in-bucket keys. A line is
+// 64 dwords (two 128-byte lines per bucket):
 //   dw0      base (first node of W(R_32)'s lowest bucket)
 //   dw1, 2   G(r) for r = 0..3 and 4..7, 8 bits each (clamped to 255)
-//   dw3      whole(r) bits 0..7 | R_32 << 8 | S << 12 (stored slots, whole buckets only, <= 64) | defer << 31
+//   dw3      whole(r) bits 0..7 | R_32 << 8 | S << 12 (stored slots, whole buckets only, <= 58) | defer << 31
 //   dw4, 5   round of the bucket of D rank j, 3 bits each (j < 10 in dw4, 10..15 in dw5)
-//   dw8..71  slots: jd << 28 | key20 << 8 | off
-// A query ranks the 64 slot values: four sorted groups of 16 (Batcher), two bitonic joins into sorted
-// 32s and one top-32 bitonic merge, min/max only. As for the 16-slot lines the answer is exact when
-// the slots kept (those of W(R_c)'s buckets) number at least m = min(c, G(R_c)): the slots hold whole
-// buckets in D order, so those of W(R_c) are its first buckets in D order.
+//   dw6..63  slots: jd << 28 | key20 << 8 | off
+// A query ranks the 58 slot values (padded to 64): four sorted groups of 16 (Batcher), two bitonic joins into sorted
+// 32s and one top-32 bitonic merge, min/max only. (Ranking only slots 0..47 when no lane masks rounds, valid with at
+// most 16 good nodes per bucket, measured slower: 120 against 111 us per 1M queries.) As for the 16-slot lines the answer is exact when the slots kept (those of W(R_c)'s buckets)
+// number at least m = min(c, G(R_c)): the slots hold whole buckets in D order, so those of W(R_c) are its
+// first buckets in D order.
 // ---------------------------------------------------------------------------------------
-constexpr uint32_t WL32_SLOTS = 64, WL32_HDR = 8, WL32_STRIDE = 96, WL32_KBITS = 20;  // dwords / bits
+constexpr uint32_t WL32_SLOTS = 58, WL32_HDR = 6, WL32_STRIDE = 64, WL32_KBITS = 20;  // dwords / bits
 
 // a[0..2H) sorted from its two sorted halves: one compare-exchange rank against the reversed upper
 // half splits it into two bitonic halves (lows, highs), then a half-cleaner cascade on each.
@@ -1038,25 +1039,19 @@ __device__ __forceinline__ void merge32(uint32_t* a, const uint32_t* s) {
 
 __device__ __forceinline__ bool wl32_answer(const DevTable& T, const Target& t, uint32_t b, uint32_t count, bool act,
                                             uint32_t (&o)[32], uint32_t& m) {
-    uint32_t H[WL32_HDR], v[WL32_SLOTS];
+    uint32_t L[WL32_STRIDE], v[64];
     if (act) {
         const uint4* lp = T.wl32 + (WL32_STRIDE / 4) * (size_t)b;
-        uint4 q[(WL32_HDR + WL32_SLOTS) / 4];
 #pragma unroll
-        for (int x = 0; x < (int)(WL32_HDR + WL32_SLOTS) / 4; x++) q[x] = lp[x];
-        H[0] = q[0].x; H[1] = q[0].y; H[2] = q[0].z; H[3] = q[0].w;
-        H[4] = q[1].x; H[5] = q[1].y; H[6] = q[1].z; H[7] = q[1].w;
-#pragma unroll
-        for (int x = 0; x < (int)WL32_SLOTS / 4; x++) {
-            const uint4 u = q[WL32_HDR / 4 + x];
-            v[4 * x] = u.x; v[4 * x + 1] = u.y; v[4 * x + 2] = u.z; v[4 * x + 3] = u.w;
+        for (int x = 0; x < (int)WL32_STRIDE / 4; x++) {
+            const uint4 u = lp[x];
+            L[4 * x] = u.x; L[4 * x + 1] = u.y; L[4 * x + 2] = u.z; L[4 * x + 3] = u.w;
         }
     } else {
 #pragma unroll
-        for (int x = 0; x < (int)WL32_HDR; x++) H[x] = NONE;
-#pragma unroll
-        for (int x = 0; x < (int)WL32_SLOTS; x++) v[x] = NONE;
+        for (int x = 0; x < (int)WL32_STRIDE; x++) L[x] = NONE;
     }
+    const uint32_t* H = L;
     const uint32_t d = 64 - T.rshift;
     const uint32_t h = H[3], S = (h >> 12) & 127u, R = (h >> 8) & 15u;
     uint32_t Rc = 8, Gc = 0;
@@ -1070,7 +1065,10 @@ __device__ __forceinline__ bool wl32_answer(const DevTable& T, const Target& t, 
     bool ex = !act || (h & WL_DEFER) || !own || Rc > R;
     const uint32_t tx = (uint32_t)((t.hi << d) >> (64 - WL32_KBITS)) << 8;
 #pragma unroll  // empty slots stay NONE (a real value of D rank 15 can exceed NONE ^ tx)
-    for (int s = 0; s < (int)WL32_SLOTS; s++) v[s] = (uint32_t)s < S ? v[s] ^ tx : NONE;
+    for (int s = 0; s < 64; s++) {
+        const int li = s < (int)WL32_SLOTS ? (int)WL32_HDR + s : 0;
+        v[s] = s < (int)WL32_SLOTS && (uint32_t)s < S ? L[li] ^ tx : NONE;
+    }
     uint32_t have = S;
     if (__any(!ex && Rc < R)) {  // a smaller window: drop the later rounds' buckets
         uint32_t inc = 0;
@@ -1087,7 +1085,6 @@ __device__ __forceinline__ bool wl32_answer(const DevTable& T, const Target& t, 
             have += in;
         }
     }
-    ex |= have < m;
     sort16(v);
     sort16(v + 16);
     sort16(v + 32);
@@ -1095,6 +1092,7 @@ __device__ __forceinline__ bool wl32_answer(const DevTable& T, const Target& t, 
     join_sorted<16>(v);
     join_sorted<16>(v + 32);
     merge32(v, v + 32);
+    ex |= have < m;
     const uint32_t base = H[0] + T.index_base;
 #pragma unroll
     for (int j = 0; j < 32; j++) o[j] = (uint32_t)j < m ? base + (v[j] & 255u) : NONE;

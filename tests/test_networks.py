@@ -135,3 +135,4 @@ def test_top32_of_64():
         g = [_apply(net, v[i:i + 16]) for i in (0, 16, 32, 48)]
         acc = _merge32(_join_sorted(g[0] + g[1]), _join_sorted(g[2] + g[3]))
         assert acc == sorted(v)[:32]
+
