@@ -91,7 +91,7 @@ struct DevTable {
     const uint32_t* rrdx;
     const uint32_t* nrdx;
     const uint4* wl;    // window lines (TF_WL): 128 bytes per bucket, see rt_wl_kernel
-    const uint4* wl16;  // window lines for counts 9..16 (TF_WL16): 256 bytes per bucket
+    const uint4* wl16;  // window lines for counts 9..16 (TF_WL16): 128 bytes per bucket
     const uint4* wl32;  // window lines for counts 17..32 (TF_WL32): 256 bytes per bucket
     const uint4* ncl;   // NodeCache lines (TF_NCL): 256 bytes per node radix slot
     uint64_t rbase, nbase;
@@ -820,18 +820,23 @@ __global__ void wl_build_kernel(const uint64_t* key, const uint8_t* status, cons
 
 // ---------------------------------------------------------------------------------------
 // Window lines for 9 <= count <= 16 (TF_WL16): the same construction as the count <= 8 lines with
-// R_16 <= 3 (windows of up to 8 buckets) and 32 slots, so a line is 36 dwords (two 128-byte lines
-// per bucket at a 256-byte stride):
+// R_16 <= 3 (windows of up to 8 buckets) and 28 slots, so a line is 32 dwords: one aligned 128-byte
+// line per bucket, one random line gather per query (the 32-slot, 144-byte form took two):
 //   dw0      base (first node of W(R_16)'s lowest bucket)
 //   dw1      G(r) for r = 0..3 (6 bits each) | whole(r) << (24+r) | R_16 << 28 | defer << 31
 //   dw2      round of the bucket of D rank j, 2 bits each (j < 8)
-//   dw3      S (stored slots, whole buckets only, <= 32)
-//   dw4..35  slots: jd << 29 | key21 << 8 | off
-// The 16 smallest of the 32 rank values (two sorted groups of 16 by Batcher's network, one bitonic
-// merge) are the answer when the slots hold the first m of W(R_c)'s nodes: the bucket holding output
-// 15 starts before slot 16 and holds at most 16 good nodes.
+//   dw3      S (stored slots, whole buckets only, <= 28) | stored D-rank mask << 8 | buckets in W(R_16) << 16
+//   dw4..31  slots: jd << 29 | key21 << 8 | off
+// Buckets are stored whole: first the D-rank prefix of W(R_16) holding its 16 closest good nodes, then the
+// rest of W(R_16 - 1) (< 16 good nodes), then whatever fits.
+// The 16 smallest of the 28 rank values (padded to 32 with NONE: two sorted groups of 16 by Batcher's
+// network, one bitonic merge), restricted to the longest fully stored D-rank prefix of W(R_c), are the
+// answer when that prefix holds at least m good nodes (checked; otherwise the query takes the exact path).
 // ---------------------------------------------------------------------------------------
-constexpr uint32_t WL16_SLOTS = 32, WL16_STRIDE = 64;  // dwords
+constexpr uint32_t WL16_SLOTS = 28, WL16_STRIDE = 32;  // dwords
+#ifndef WL16_P1
+#define WL16_P1 16u
+#endif
 
 // Batcher's odd-even merge sort for 16 inputs (63 comparators; tests/test_networks.py).
 constexpr int SORT16_LEN = 63;
@@ -875,6 +880,7 @@ __device__ __forceinline__ bool wl16_answer(const DevTable& T, const Target& t, 
     }
     const uint32_t d = 64 - T.rshift;
     const uint32_t h = L[1], rounds = L[2], S = L[3] & 63u, R16 = (h >> 28) & 3u;
+    const uint32_t st = (L[3] >> 8) & 255u, nb = (L[3] >> 16) & 15u;
     uint32_t G[4];
 #pragma unroll
     for (int r = 0; r < 4; r++) G[r] = (h >> (6 * r)) & 63u;
@@ -886,17 +892,22 @@ __device__ __forceinline__ bool wl16_answer(const DevTable& T, const Target& t, 
     const bool own = (t.hi >> T.rshift) == (T.rbase >> T.rshift) + b;
     bool ex = !act || (h & WL_DEFER) || !own || Rc > R16 || (Rc == R16 && S < m);
     const uint32_t tx = (uint32_t)((t.hi << d) >> (64 - WL_KBITS)) << 8;
-    uint32_t v[WL16_SLOTS];
+    uint32_t v[32];
 #pragma unroll  // empty slots must stay last: with D rank 7 a real value can exceed NONE ^ tx
-    for (int s = 0; s < (int)WL16_SLOTS; s++) v[s] = (uint32_t)s < S ? L[4 + s] ^ tx : NONE;
-    if (__any(!ex && Rc < R16)) {  // a smaller window: drop the later rounds' buckets
-        uint32_t inc = 0;
+    for (int s = 0; s < 32; s++) v[s] = s < (int)WL16_SLOTS && (uint32_t)s < S ? L[4 + s] ^ tx : NONE;
+    // W(R_c)'s buckets (D ranks with round <= R_c); the answer is the first m good nodes of the longest D-rank
+    // prefix of them that the line stores whole (a bucket of round R_16 may not have fit).
+    uint32_t inc = 0;
 #pragma unroll
-        for (int j = 0; j < 8; j++) inc |= (((rounds >> (2 * j)) & 3u) <= Rc ? 1u : 0u) << j;
+    for (int j = 0; j < 8; j++) inc |= ((uint32_t)j < nb && ((rounds >> (2 * j)) & 3u) <= Rc ? 1u : 0u) << j;
+    const uint32_t miss = inc & ~st;
+    if (__any(!ex && (Rc < R16 || miss))) {  // drop the buckets outside that prefix
+        const uint32_t lim = miss ? (uint32_t)__builtin_ctz(miss) : 8u;
         uint32_t have = 0;
 #pragma unroll
         for (int s = 0; s < (int)WL16_SLOTS; s++) {
-            const bool in = (uint32_t)s < S && ((inc >> (v[s] >> 29)) & 1u);
+            const uint32_t j = v[s] >> 29;
+            const bool in = (uint32_t)s < S && ((inc >> j) & 1u) && j < lim;
             v[s] = in ? v[s] : NONE;
             have += in;
         }
@@ -928,6 +939,41 @@ __device__ __forceinline__ void store_row16(uint32_t* row, const uint32_t (&o)[1
     }
 }
 
+// The block's rows (count 9..16 or 17..32) leave through LDS as one contiguous run of 16-byte stores: per-lane
+// rows of 36..128 bytes (a 56-byte stride for count 14) left every store instruction part-filling its lines. Rows
+// whose lane takes the exact path (ok false) are skipped dword by dword; exact_tail writes them afterwards.
+template <int MAXK>  // count in 4..MAXK: a 16-byte chunk spans at most two rows
+__device__ __forceinline__ void store_rows_block(uint32_t* __restrict__ out_idx, uint32_t q, uint32_t count,
+                                                 const uint32_t (&o)[MAXK], bool ok) {
+    __shared__ uint32_t rows[BLOCK * MAXK];
+    __shared__ uint32_t okm[BLOCK / 32];
+    const uint32_t tid = threadIdx.x, q0 = blockIdx.x * BLOCK;
+    if (tid < BLOCK / 32) okm[tid] = 0;
+    __syncthreads();
+    if (ok) atomicOr(&okm[tid >> 5], 1u << (tid & 31));
+#pragma unroll
+    for (int j = 0; j < MAXK; j++)
+        if ((uint32_t)j < count) rows[tid * count + j] = o[j];
+    __syncthreads();
+    const uint32_t nq = min((uint32_t)BLOCK, q - q0), nw = nq * count;
+    uint32_t* dst = out_idx + (size_t)q0 * count;  // 16-byte aligned: BLOCK * count * 4 is a multiple of 16
+    for (uint32_t c = tid; 4 * c < nw; c += BLOCK) {
+        const uint32_t w0 = 4 * c;
+        const uint32_t r0 = w0 / count, r1 = min(w0 + 3, nw - 1) / count;
+        const bool ok0 = (okm[r0 >> 5] >> (r0 & 31)) & 1u, ok1 = (okm[r1 >> 5] >> (r1 & 31)) & 1u;
+        if (ok0 && ok1 && w0 + 4 <= nw && (((uintptr_t)out_idx & 15u) == 0)) {
+            reinterpret_cast<uint4*>(dst)[c] = make_uint4(rows[w0], rows[w0 + 1], rows[w0 + 2], rows[w0 + 3]);
+        } else {
+            for (uint32_t w = w0; w < min(w0 + 4, nw); w++) {
+                const uint32_t r = w / count;
+                if ((okm[r >> 5] >> (r & 31)) & 1u) dst[w] = rows[w];
+            }
+        }
+    }
+}
+
+// ABL 1 = no exact path (timing ablation only, KAD_RT_KERNEL=wl16_abl1; deferred rows are left unwritten).
+template <int ABL>
 __global__ __launch_bounds__(BLOCK) void rt_wl16_kernel(DevTable T, const uint8_t* __restrict__ targets, uint32_t q,
                                                         uint32_t count, uint32_t* __restrict__ out_idx,
                                                         uint8_t* __restrict__ out_cnt) {
@@ -941,12 +987,10 @@ __global__ __launch_bounds__(BLOCK) void rt_wl16_kernel(DevTable T, const uint8_
     }
     uint32_t o[16], m;
     const bool ok = wl16_answer(T, t, b, count, act, o, m);
-    if (act && ok) {
-        store_row16(out_idx + (size_t)i * count, o, count);
-        if (out_cnt) out_cnt[i] = (uint8_t)m;
-    }
+    if (act && ok && out_cnt) out_cnt[i] = (uint8_t)m;
+    store_rows_block<16>(out_idx, q, count, o, act && ok);
     __shared__ uint64_t xs[BLOCK / 64][192];
-    exact_tail(T, t, act && !ok, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
+    if (ABL == 0) exact_tail(T, t, act && !ok, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
 }
 
 // Window lines for counts 9..16 after a status change (or at creation): one thread per bucket.
@@ -967,19 +1011,26 @@ __global__ void wl16_build_kernel(const uint64_t* key, const uint8_t* status, co
     if (R == 4) { L[1] = WL_DEFER; return; }
     const uint32_t lo = b > R ? b - 1 - R : 0u, hi = min(B - 1, b + R), nb = hi - lo + 1;
     const uint32_t base = dir[lo].x & ~WIDE;
-    uint32_t rounds = 0, S = 0;
-    bool defer = false, full = false;
-    for (uint32_t j = 0; j < nb; j++) {  // buckets in D order
+    uint32_t rounds = 0, S = 0, st = 0, xj[8];
+    bool defer = false;
+    for (uint32_t j = 0; j < nb; j++) {  // the bucket of D rank j and its round
         uint32_t x = lo;
         for (uint32_t y = lo; y <= hi; y++) {
             uint32_t rk = 0;
             for (uint32_t z = lo; z <= hi; z++) rk += ((pre0 + z) ^ (pre0 + b)) < ((pre0 + y) ^ (pre0 + b));
             if (rk == j) x = y;
         }
+        xj[j] = x;
         rounds |= (x >= b ? x - b : b - 1 - x) << (2 * j);
-        const uint32_t j0 = dir[x].x & ~WIDE, j1 = dir[x + 1].x & ~WIDE;
+    }
+    // Whole buckets, in three passes: (1) the D-rank prefix of W(R_16) up to its 16th good node (every count
+    // with R_c = R_16); (2) the rest of W(R_16 - 1), which holds < 16 good nodes (every count with R_c < R_16);
+    // (3) whatever else fits, in D order.
+    auto put = [&](uint32_t j) {
+        const uint32_t x = xj[j], j0 = dir[x].x & ~WIDE, j1 = dir[x + 1].x & ~WIDE;
         const uint32_t g = gpre[x + 1] - gpre[x];
-        if (full || S + g > WL16_SLOTS) { full = true; continue; }
+        if (((st >> j) & 1u) || S + g > WL16_SLOTS) return;
+        st |= 1u << j;
         const uint32_t s0 = S;
         for (uint32_t n = j0; n < j1; n++) {
             if (!(status[n] & KAD_STATUS_GOOD)) continue;
@@ -989,11 +1040,18 @@ __global__ void wl16_build_kernel(const uint64_t* key, const uint8_t* status, co
             L[4 + S] = (j << 29) | (k21 << 8) | (off & 255u);
             S++;
         }
+    };
+    for (uint32_t j = 0, cum = 0; j < nb && cum < WL16_P1; j++) {
+        put(j);
+        cum += gpre[xj[j] + 1] - gpre[xj[j]];
     }
+    for (uint32_t j = 0; j < nb; j++)
+        if (((rounds >> (2 * j)) & 3u) < R) put(j);
+    for (uint32_t j = 0; j < nb; j++) put(j);
     L[0] = base;
     L[1] = h | (R << 28) | (defer ? WL_DEFER : 0u);
     L[2] = rounds;
-    L[3] = S;
+    L[3] = S | (st << 8) | (nb << 16);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1130,10 +1188,8 @@ __global__ __launch_bounds__(BLOCK) void rt_wl32_kernel(DevTable T, const uint8_
     }
     uint32_t o[32], m;
     const bool ok = wl32_answer(T, t, b, count, act, o, m);
-    if (act && ok) {
-        store_row32(out_idx + (size_t)i * count, o, count);
-        if (out_cnt) out_cnt[i] = (uint8_t)m;
-    }
+    if (act && ok && out_cnt) out_cnt[i] = (uint8_t)m;
+    store_rows_block<32>(out_idx, q, count, o, act && ok);
     __shared__ uint64_t xs[BLOCK / 64][192];
     exact_tail(T, t, act && !ok, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
 }
@@ -2529,7 +2585,10 @@ int launch_rt(const kad_table* t, const uint8_t* targets, uint32_t q, uint32_t c
         else
             hipLaunchKernelGGL(rt_wl_kernel<0>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
     } else if (K == 16 && (d.flags & TF_WL16) && !(ev && std::strcmp(ev, "lane") == 0)) {
-        hipLaunchKernelGGL(rt_wl16_kernel, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
+        if (ev && std::strcmp(ev, "wl16_abl1") == 0)
+            hipLaunchKernelGGL(rt_wl16_kernel<1>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
+        else
+            hipLaunchKernelGGL(rt_wl16_kernel<0>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
     } else if (K == 32 && (d.flags & TF_WL32) && !(ev && std::strcmp(ev, "lane") == 0)) {
         hipLaunchKernelGGL(rt_wl32_kernel, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
     } else {

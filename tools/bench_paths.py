@@ -39,6 +39,14 @@ for k in (8, 14, 16, 32):
     us = timeit(lambda: T.rt_closest(tg, k))
     res[f"rt_k{k}_us"] = round(us, 1)
     res[f"rt_k{k}_Gq_s"] = round(q / us / 1e3, 2)
+for k in (14, 16):  # ablation: the count 9..16 line kernel without its exact path
+    a = T.rt_closest(tg, k)
+    os.environ["KAD_RT_KERNEL"] = "wl16_abl1"
+    res[f"rt_k{k}_no_exact_us"] = round(timeit(lambda: T.rt_closest(tg, k)), 1)
+    c = T.rt_closest(tg, k, out_idx=torch.full((q, k), -1, dtype=torch.int32, device=dev))
+    os.environ.pop("KAD_RT_KERNEL")
+    torch.cuda.synchronize()
+    res[f"rt_k{k}_exact_rows"] = int((c[0] != a[0]).any(dim=1).sum().item())
 os.environ["KAD_RT_KERNEL"] = "lane"
 for k in (16, 32):
     us = timeit(lambda: T.rt_closest(tg, k))
@@ -97,13 +105,13 @@ os.environ["KAD_NC_KERNEL"] = "lines_abl1"  # ablation: the line kernel without 
 for k in (1, 14):
     us = timeit(lambda: T.nc_closest(tg, k))
     res[f"nc_k{k}_lines_no_exact_us"] = round(us, 1)
-c = T.nc_closest(tg, 14)
+c = T.nc_closest(tg, 14, out_idx=torch.full((q, 14), -1, dtype=torch.int32, device=dev))
 os.environ.pop("KAD_NC_KERNEL")
 torch.cuda.synchronize()
 res["nc_k14_lines_exact_rows"] = int((c[0] != a[0]).any(dim=1).sum().item())  # rows the exact path fixes
 a1 = T.nc_closest(tg, 1)
 os.environ["KAD_NC_KERNEL"] = "lines_abl1"
-c1 = T.nc_closest(tg, 1)
+c1 = T.nc_closest(tg, 1, out_idx=torch.full((q, 1), -1, dtype=torch.int32, device=dev))
 os.environ.pop("KAD_NC_KERNEL")
 torch.cuda.synchronize()
 res["nc_k1_lines_exact_rows"] = int((c1[0] != a1[0]).any(dim=1).sum().item())
