@@ -19,7 +19,7 @@ blocks = re.findall(r"\{[^{}]*\}", txt, re.S)
 times = json.loads(blocks[-1]) if blocks else {}
 KERNELS = [  # (kernel-name substring, path, paths.log timing key)
     ("rt_wl_kernel<0>", "RoutingTable k=8 (window line)", "rt_k8_us"),
-    ("rt_wl16_kernel", "RoutingTable k=16 (two lines)", "rt_k16_us"),
+    ("rt_wl16_kernel", "RoutingTable k=16 (one line)", "rt_k16_us"),
     ("rt_wl32_kernel", "RoutingTable k=32 (two lines)", "rt_k32_us"),
     ("rt_closest_kernel<32>", "RoutingTable k=32 (lane kernel, KAD_RT_KERNEL=lane)", "rt_k32_lane_us"),
     ("nc_line_kernel", "NodeCache k=14 (line)", "nc_k14_us"),
