@@ -1740,7 +1740,7 @@ __global__ __launch_bounds__(BLOCK) void nc_closest_kernel(DevTable T, const uin
     nc_serial(T, load_target(targets, i), count, out_idx + (size_t)i * count, out_cnt ? out_cnt + i : nullptr);
 }
 
-// NodeCache::getCachedNodes, one wave per query (count <= 16). The walk is a greedy merge of the
+// NodeCache::getCachedNodes, one wave per query (count <= 32). The walk is a greedy merge of the
 // left run a_k = lb-1-k and the right run b_k = lb+k by XOR distance (distinct IDs: no ties; the
 // lb == 0 start takes node 0 from the right, which is the same walk with an empty left run). In a
 // greedy merge an element's place is its index plus the number of elements of the other run whose
@@ -3168,10 +3168,10 @@ int kad_nc_closest_batch(const kad_table* t, const uint8_t* targets, uint32_t q,
     else if (count >= 1 && count <= 16 && t->d.n > 0 && ev && std::strcmp(ev, "multi4") == 0)
         hipLaunchKernelGGL(nc_multi_kernel<4>, dim3((q + 4 * (BLOCK / 64) - 1) / (4 * (BLOCK / 64))), dim3(BLOCK), 0,
                            (hipStream_t)stream, t->d, targets, q, count, out_idx, out_cnt);
-    else if (count >= 1 && count <= 16 && t->d.n > 0 && !(ev && std::strcmp(ev, "serial") == 0))
+    else if (count >= 1 && count <= 32 && t->d.n > 0 && !(ev && std::strcmp(ev, "serial") == 0))
         hipLaunchKernelGGL(nc_multi_kernel<2>, dim3((q + 2 * (BLOCK / 64) - 1) / (2 * (BLOCK / 64))), dim3(BLOCK), 0,
                            (hipStream_t)stream, t->d, targets, q, count, out_idx, out_cnt);
-    else if (count >= 1 && count <= 16 && !(ev && std::strcmp(ev, "serial") == 0))
+    else if (count >= 1 && count <= 32 && !(ev && std::strcmp(ev, "serial") == 0))
         hipLaunchKernelGGL(nc_group_kernel, dim3((q + BLOCK / 64 - 1) / (BLOCK / 64)), dim3(BLOCK), 0,
                            (hipStream_t)stream, t->d, targets, q, count, out_idx, out_cnt);
     else

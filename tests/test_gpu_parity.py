@@ -280,7 +280,7 @@ def _nc_targets(t):
 @pytest.mark.parametrize("t", _nc_tables(), ids=lambda t: t["name"])
 def test_nc_lines(gpu, t, kernel, monkeypatch):
     """NodeCache::getCachedNodes for every count 1..16 (the line kernel, default; KAD_NC_KERNEL=multi2:
-    the wave-per-query kernel) and 17..32, 40 (the serial walk)."""
+    the wave-per-query kernel), 17..32 (the wave-per-query kernel in both modes) and 40 (the serial walk)."""
     if kernel != "lines":
         monkeypatch.setenv("KAD_NC_KERNEL", kernel)
     with make(t, gpu) as T:
