@@ -2018,6 +2018,142 @@ __global__ __launch_bounds__(BLOCK) void nc_multi_kernel(DevTable T, const uint8
         if (q0 + j < q) nc_answer(T, t[j], r0[j], r1[j], w[j], lane, q0 + j, count, out_idx, out_cnt);
 }
 
+// NodeCache counts 17..64, one query per wave at a time, 64-node runs each side of lb (two per lane):
+// lanes 0-31 hold left elements k and k+32 (a_k = lb-1-k), lanes 32-63 right elements k and k+32
+// (b_k = lb+k). The same greedy-merge placement as nc_answer (place = index + the other run's
+// elements whose prefix maximum is below mine) over runs twice as long, so a walk that takes a whole
+// subtree from one side (common for 32 emissions) stays inside the runs; the serial walk remains the
+// fallback. Merge and emission for one query whose elements are loaded:
+__device__ __forceinline__ void nc64_answer(const DevTable& T, const Target& t, uint32_t lb, uint32_t lane, uint32_t qi,
+                                            uint32_t count, uint32_t* __restrict__ out_idx,
+                                            uint8_t* __restrict__ out_cnt, uint64_t (&m)[2], const uint32_t (&node)[2],
+                                            const bool (&valid)[2], const bool (&emit)[2], bool amb, bool serial) {
+    constexpr uint32_t W = 64;  // run length
+    const uint32_t N = T.n;
+    const bool right = lane >= 32;
+    const uint32_t k = lane & 31u, base = right ? 32u : 0u, obase = right ? 0u : 32u;
+#pragma unroll
+    for (int e = 0; e < 2; e++)
+#pragma unroll
+        for (uint32_t s = 1; s < 32; s <<= 1) {  // prefix maxima along each half-run
+            const uint64_t o = shfl64(m[e], (int)lane - (int)s);
+            if (k >= s && o > m[e]) m[e] = o;
+        }
+    {
+        const uint64_t top = shfl64(m[0], (int)(base + 31));  // the first half-run's maximum
+        if (top > m[1]) m[1] = top;
+    }
+    uint32_t pos[2];
+#pragma unroll
+    for (int e = 0; e < 2; e++) {
+        uint32_t lo = 0, hi = W;
+#pragma unroll
+        for (int it = 0; it < 7; it++) {  // 65 possible answers: 7 halvings
+            const uint32_t mid = (lo + hi) >> 1, mc = mid < W ? mid : W - 1;
+            const uint64_t v0 = shfl64(m[0], (int)(obase + (mc & 31u))), v1 = shfl64(m[1], (int)(obase + (mc & 31u)));
+            const uint64_t v = mc < 32 ? v0 : v1;
+            if (lo < hi) {
+                if (v < m[e]) lo = mid + 1; else hi = mid;
+            }
+        }
+        const uint32_t lc = lo < W ? lo : W - 1;
+        const uint64_t a0 = shfl64(m[0], (int)(obase + (lc & 31u))), a1 = shfl64(m[1], (int)(obase + (lc & 31u)));
+        amb |= valid[e] && lo < W && (lc < 32 ? a0 : a1) == m[e];
+        pos[e] = k + 32u * e + lo;
+    }
+    const uint64_t eb0 = __ballot(emit[0]), eb1 = __ballot(emit[1]);
+    const uint32_t mine0 = (uint32_t)(eb0 >> base), mine1 = (uint32_t)(eb1 >> base);
+    const uint32_t oth0 = (uint32_t)(eb0 >> obase), oth1 = (uint32_t)(eb1 >> obase);
+    const uint32_t below = (1u << k) - 1u;
+    uint32_t rank[2];
+#pragma unroll
+    for (int e = 0; e < 2; e++) {
+        const uint32_t lo = pos[e] - k - 32u * e;
+        const uint32_t oth = lo >= 64 ? __builtin_popcount(oth0) + __builtin_popcount(oth1)
+                             : lo >= 32 ? __builtin_popcount(oth0) + __builtin_popcount(oth1 & ((1u << (lo - 32)) - 1u))
+                                        : __builtin_popcount(oth0 & ((1u << lo) - 1u));
+        rank[e] = (e == 0 ? __builtin_popcount(mine0 & below)
+                          : __builtin_popcount(mine0) + __builtin_popcount(mine1 & below)) + oth;
+    }
+    const uint32_t tot = (uint32_t)(__builtin_popcountll(eb0) + __builtin_popcountll(eb1));
+    uint32_t pstar = 128;  // merge position of the count-th emission (128: not inside the runs)
+    if (tot >= count) {
+        const uint64_t w0 = __ballot(emit[0] && rank[0] == count - 1), w1 = __ballot(emit[1] && rank[1] == count - 1);
+        pstar = w0 ? (uint32_t)__shfl((int)pos[0], (int)__builtin_ctzll(w0), 64)
+                   : (uint32_t)__shfl((int)pos[1], (int)__builtin_ctzll(w1 | (1ull << 63)), 64);
+    }
+    const uint32_t posA = (uint32_t)__shfl((int)pos[1], 31, 64);  // left element 63
+    const uint32_t posB = (uint32_t)__shfl((int)pos[1], 63, 64);  // right element 63
+    const bool ok = !__any(amb) && (lb <= W || posA > pstar) && (lb + W >= N || posB > pstar);
+    if (ok) {
+        uint32_t* row = out_idx + (size_t)qi * count;
+        const uint32_t mm = min(tot, count);
+#pragma unroll
+        for (int e = 0; e < 2; e++)
+            if (emit[e] && rank[e] < count) row[rank[e]] = node[e] + T.index_base;
+        if (lane >= mm && lane < count) row[lane] = NONE;
+        if (lane == 0 && out_cnt) out_cnt[qi] = (uint8_t)mm;
+    } else if (lane == 0 && serial) {
+        nc_serial(T, t, count, out_idx + (size_t)qi * count, out_cnt ? out_cnt + qi : nullptr);
+    }
+}
+
+// One query per wave: target -> slot -> lb (one ballot over the slot's nodes when it holds <= 64, else
+// the binary search) -> the 128 run elements (direct loads; a 192-node window load around r0 read
+// 1.5x the bytes and took 1036 against 890 us per 1M k = 32 queries, with no gain from interleaving two
+// queries per wave: the kernel is bound by those bytes, not by latency).
+// ABL 1 (timing ablation only, KAD_NC_KERNEL=w64_abl1; results wrong): no serial fallback.
+template <int ABL>
+__global__ __launch_bounds__(BLOCK) void nc_wave64_kernel(DevTable T, const uint8_t* __restrict__ targets, uint32_t q,
+                                                          uint32_t count, uint32_t* __restrict__ out_idx,
+                                                          uint8_t* __restrict__ out_cnt) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t qi = blockIdx.x * (BLOCK / 64) + threadIdx.x / 64;
+    if (qi >= q) return;  // one query per wave: the whole wave leaves
+    const Target t = load_target(targets, qi);
+    const uint32_t N = T.n;
+    uint32_t r0, r1;
+    nc_slot(T, t, r0, r1);
+    uint32_t lb;
+    if (r1 - r0 <= 64) {
+        bool lt = false;
+        if (lane < r1 - r0) {
+            const uint32_t n = r0 + lane;
+            const uint64_t kk = T.key[n];
+            if (kk != t.hi) {
+                lt = kk < t.hi;
+            } else {
+                const uint32_t* tt = T.tail + 3ull * n;
+                lt = cmp160(0, tt[0], tt[1], tt[2], 0, t.t2, t.t3, t.t4) < 0;
+            }
+        }
+        lb = r0 + (uint32_t)__builtin_popcountll(__ballot(lt));
+    } else {
+        lb = node_lower_bound(T, t);
+    }
+    const bool right = lane >= 32;
+    const uint32_t k = lane & 31u;
+    uint64_t m[2];
+    uint32_t node[2];
+    bool valid[2], emit[2], amb = false;
+#pragma unroll
+    for (int e = 0; e < 2; e++) {
+        const uint32_t kk = k + 32u * e;
+        node[e] = right ? lb + kk : lb - 1 - kk;
+        valid[e] = right ? lb + kk < N : lb > kk;
+        uint64_t key = 0;
+        uint32_t sb = 0;
+        if (valid[e]) {
+            key = T.key[node[e]];
+            sb = T.status[node[e]];
+        }
+        m[e] = valid[e] ? key ^ t.hi : ~0ull;
+        emit[e] = valid[e] && !(sb & KAD_STATUS_EXPIRED);
+        amb |= valid[e] && m[e] == ~0ull;
+    }
+    nc64_answer(T, t, lb, lane, qi, count, out_idx, out_cnt, m, node, valid, emit, amb, ABL == 0);
+}
+
 // ---------------------------------------------------------------------------------------
 // NodeCache lines (TF_NCL): one 256-byte line per node radix slot s answers the count <= 16
 // getCachedNodes queries whose target falls in s with one line load per lane (no lower_bound chain,
@@ -3167,6 +3303,13 @@ int kad_nc_closest_batch(const kad_table* t, const uint8_t* targets, uint32_t q,
                            (hipStream_t)stream, t->d, targets, q, count, out_idx, out_cnt);
     else if (count >= 1 && count <= 16 && t->d.n > 0 && ev && std::strcmp(ev, "multi4") == 0)
         hipLaunchKernelGGL(nc_multi_kernel<4>, dim3((q + 4 * (BLOCK / 64) - 1) / (4 * (BLOCK / 64))), dim3(BLOCK), 0,
+                           (hipStream_t)stream, t->d, targets, q, count, out_idx, out_cnt);
+    else if (count > 16 && count <= 64 && t->d.n > 0 && ev && std::strcmp(ev, "w64_abl1") == 0)
+        hipLaunchKernelGGL(nc_wave64_kernel<1>, dim3((q + BLOCK / 64 - 1) / (BLOCK / 64)), dim3(BLOCK), 0,
+                           (hipStream_t)stream, t->d, targets, q, count, out_idx, out_cnt);
+    else if (count > 16 && count <= 64 && t->d.n > 0 && !(ev && std::strcmp(ev, "serial") == 0) &&
+             !(ev && std::strcmp(ev, "multi2") == 0))
+        hipLaunchKernelGGL(nc_wave64_kernel<0>, dim3((q + BLOCK / 64 - 1) / (BLOCK / 64)), dim3(BLOCK), 0,
                            (hipStream_t)stream, t->d, targets, q, count, out_idx, out_cnt);
     else if (count >= 1 && count <= 32 && t->d.n > 0 && !(ev && std::strcmp(ev, "serial") == 0))
         hipLaunchKernelGGL(nc_multi_kernel<2>, dim3((q + 2 * (BLOCK / 64) - 1) / (2 * (BLOCK / 64))), dim3(BLOCK), 0,

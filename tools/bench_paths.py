@@ -101,6 +101,14 @@ res["nc_multi2_equals"] = bool(torch.equal(a[0], c[0]) and torch.equal(a[1], c[1
 for k in (1, 8, 16, 32):
     us = timeit(lambda: T.nc_closest(tg, k))
     res[f"nc_k{k}_us"] = round(us, 1)
+a32 = T.nc_closest(tg, 32)
+for kern in ("multi2", "w64_abl1"):  # counts > 16: 32-node runs; 64-node runs without the serial fallback
+    os.environ["KAD_NC_KERNEL"] = kern
+    res[f"nc_k32_{kern}_us"] = round(timeit(lambda: T.nc_closest(tg, 32)), 1)
+    c = T.nc_closest(tg, 32, out_idx=torch.full((q, 32), -1, dtype=torch.int32, device=dev))
+    os.environ.pop("KAD_NC_KERNEL")
+    torch.cuda.synchronize()
+    res[f"nc_k32_{kern}_rows_differ"] = int((c[0] != a32[0]).any(dim=1).sum().item())
 os.environ["KAD_NC_KERNEL"] = "lines_abl1"  # ablation: the line kernel without its exact path
 for k in (1, 14):
     us = timeit(lambda: T.nc_closest(tg, k))
