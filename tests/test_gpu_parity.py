@@ -280,8 +280,8 @@ def _nc_targets(t):
 @pytest.mark.parametrize("t", _nc_tables(), ids=lambda t: t["name"])
 def test_nc_lines(gpu, t, kernel, monkeypatch):
     """NodeCache::getCachedNodes for every count 1..16 (the line kernel, default; KAD_NC_KERNEL=multi2:
-    the wave-per-query kernel), 17..32 and 40 (the 64-node-run wave kernel; KAD_NC_KERNEL=multi2: the 32-node-run kernel up to 32,
-    the serial walk for 40)."""
+    the wave-per-query kernel), 17..32 and 40 (the 64-node-run wave kernel; KAD_NC_KERNEL=multi2: the
+    32-node-run kernel up to 32, the serial walk for 40)."""
     if kernel != "lines":
         monkeypatch.setenv("KAD_NC_KERNEL", kernel)
     with make(t, gpu) as T:
