@@ -820,20 +820,20 @@ __global__ void wl_build_kernel(const uint64_t* key, const uint8_t* status, cons
 
 // ---------------------------------------------------------------------------------------
 // Window lines for 9 <= count <= 16 (TF_WL16): the same construction as the count <= 8 lines with
-// R_16 <= 3 (windows of up to 8 buckets) and 28 slots, so a line is 32 dwords: one aligned 128-byte
+// R_16 <= 3 (windows of up to 8 buckets) and 29 slots, so a line is 32 dwords: one aligned 128-byte
 // line per bucket, one random line gather per query (the 32-slot, 144-byte form took two):
 //   dw0      base (first node of W(R_16)'s lowest bucket)
-//   dw1      G(r) for r = 0..3 (6 bits each) | whole(r) << (24+r) | R_16 << 28 | defer << 31
-//   dw2      round of the bucket of D rank j, 2 bits each (j < 8)
-//   dw3      S (stored slots, whole buckets only, <= 28) | stored D-rank mask << 8 | buckets in W(R_16) << 16
-//   dw4..31  slots: jd << 29 | key21 << 8 | off
+//   dw1      G(r) for r = 0..3 (5 bits each, capped at 31) | whole(r) << (20+r) | R_16 << 24 | S << 26 | defer << 31
+//            (S = stored slots, whole buckets only, <= 29)
+//   dw2      round of the bucket of D rank j, 2 bits each (j < 8) | stored D-rank mask << 16 | buckets in W(R_16) << 24
+//   dw3..31  slots: jd << 29 | key21 << 8 | off
 // Buckets are stored whole: first the D-rank prefix of W(R_16) holding its 16 closest good nodes, then the
 // rest of W(R_16 - 1) (< 16 good nodes), then whatever fits.
-// The 16 smallest of the 28 rank values (padded to 32 with NONE: two sorted groups of 16 by Batcher's
+// The 16 smallest of the 29 rank values (padded to 32 with NONE: two sorted groups of 16 by Batcher's
 // network, one bitonic merge), restricted to the longest fully stored D-rank prefix of W(R_c), are the
 // answer when that prefix holds at least m good nodes (checked; otherwise the query takes the exact path).
 // ---------------------------------------------------------------------------------------
-constexpr uint32_t WL16_SLOTS = 28, WL16_STRIDE = 32;  // dwords
+constexpr uint32_t WL16_SLOTS = 29, WL16_HDR = 3, WL16_STRIDE = 32;  // dwords
 #ifndef WL16_P1
 #define WL16_P1 16u
 #endif
@@ -866,35 +866,35 @@ __device__ __forceinline__ void merge16(uint32_t* a, const uint32_t* s) {
 
 __device__ __forceinline__ bool wl16_answer(const DevTable& T, const Target& t, uint32_t b, uint32_t count, bool act,
                                             uint32_t (&o)[16], uint32_t& m) {
-    uint32_t L[4 + WL16_SLOTS];
+    uint32_t L[WL16_HDR + WL16_SLOTS];
     if (act) {
         const uint4* lp = T.wl16 + (WL16_STRIDE / 4) * (size_t)b;
 #pragma unroll
-        for (int x = 0; x < (int)(4 + WL16_SLOTS) / 4; x++) {
+        for (int x = 0; x < (int)(WL16_HDR + WL16_SLOTS) / 4; x++) {
             const uint4 q = lp[x];
             L[4 * x] = q.x; L[4 * x + 1] = q.y; L[4 * x + 2] = q.z; L[4 * x + 3] = q.w;
         }
     } else {
 #pragma unroll
-        for (int x = 0; x < (int)(4 + WL16_SLOTS); x++) L[x] = NONE;
+        for (int x = 0; x < (int)(WL16_HDR + WL16_SLOTS); x++) L[x] = NONE;
     }
     const uint32_t d = 64 - T.rshift;
-    const uint32_t h = L[1], rounds = L[2], S = L[3] & 63u, R16 = (h >> 28) & 3u;
-    const uint32_t st = (L[3] >> 8) & 255u, nb = (L[3] >> 16) & 15u;
+    const uint32_t h = L[1], rounds = L[2] & 0xFFFFu, S = (h >> 26) & 31u, R16 = (h >> 24) & 3u;
+    const uint32_t st = (L[2] >> 16) & 255u, nb = (L[2] >> 24) & 15u;
     uint32_t G[4];
 #pragma unroll
-    for (int r = 0; r < 4; r++) G[r] = (h >> (6 * r)) & 63u;
+    for (int r = 0; r < 4; r++) G[r] = (h >> (5 * r)) & 31u;
     uint32_t Rc = 3;
 #pragma unroll
     for (int r = 3; r >= 0; r--)
-        if (G[r] >= count || ((h >> (24 + r)) & 1u)) Rc = (uint32_t)r;
+        if (G[r] >= count || ((h >> (20 + r)) & 1u)) Rc = (uint32_t)r;
     m = min(count, Rc == 0 ? G[0] : Rc == 1 ? G[1] : Rc == 2 ? G[2] : G[3]);
     const bool own = (t.hi >> T.rshift) == (T.rbase >> T.rshift) + b;
     bool ex = !act || (h & WL_DEFER) || !own || Rc > R16 || (Rc == R16 && S < m);
     const uint32_t tx = (uint32_t)((t.hi << d) >> (64 - WL_KBITS)) << 8;
     uint32_t v[32];
 #pragma unroll  // empty slots must stay last: with D rank 7 a real value can exceed NONE ^ tx
-    for (int s = 0; s < 32; s++) v[s] = s < (int)WL16_SLOTS && (uint32_t)s < S ? L[4 + s] ^ tx : NONE;
+    for (int s = 0; s < 32; s++) v[s] = s < (int)WL16_SLOTS && (uint32_t)s < S ? L[WL16_HDR + s] ^ tx : NONE;
     // W(R_c)'s buckets (D ranks with round <= R_c); the answer is the first m good nodes of the longest D-rank
     // prefix of them that the line stores whole (a bucket of round R_16 may not have fit).
     uint32_t inc = 0;
@@ -999,13 +999,13 @@ __global__ void wl16_build_kernel(const uint64_t* key, const uint8_t* status, co
     const uint32_t b = blockIdx.x * BLOCK + threadIdx.x;
     if (b >= B) return;
     uint32_t* L = lines + (size_t)WL16_STRIDE * b;
-    for (uint32_t k = 0; k < 4 + WL16_SLOTS; k++) L[k] = NONE;
+    for (uint32_t k = 0; k < WL16_HDR + WL16_SLOTS; k++) L[k] = NONE;
     uint32_t h = 0, R = 4;
     for (uint32_t r = 0; r < 4; r++) {
         const uint32_t lo = b > r ? b - 1 - r : 0u, hi = min(B - 1, b + r);
         const uint32_t g = gpre[hi + 1] - gpre[lo];
         const bool whole = lo == 0 && hi == B - 1;
-        h |= (min(g, 63u) << (6 * r)) | ((whole ? 1u : 0u) << (24 + r));
+        h |= (min(g, 31u) << (5 * r)) | ((whole ? 1u : 0u) << (20 + r));
         if (R == 4 && (g >= 16 || whole)) R = r;
     }
     if (R == 4) { L[1] = WL_DEFER; return; }
@@ -1036,8 +1036,8 @@ __global__ void wl16_build_kernel(const uint64_t* key, const uint8_t* status, co
             if (!(status[n] & KAD_STATUS_GOOD)) continue;
             const uint32_t k21 = (uint32_t)((key[n] << d) >> (64 - WL_KBITS)), off = n - base;
             defer |= off > 255u;
-            for (uint32_t s = s0; s < S; s++) defer |= ((L[4 + s] >> 8) & ((1u << WL_KBITS) - 1)) == k21;
-            L[4 + S] = (j << 29) | (k21 << 8) | (off & 255u);
+            for (uint32_t s = s0; s < S; s++) defer |= ((L[WL16_HDR + s] >> 8) & ((1u << WL_KBITS) - 1)) == k21;
+            L[WL16_HDR + S] = (j << 29) | (k21 << 8) | (off & 255u);
             S++;
         }
     };
@@ -1049,9 +1049,8 @@ __global__ void wl16_build_kernel(const uint64_t* key, const uint8_t* status, co
         if (((rounds >> (2 * j)) & 3u) < R) put(j);
     for (uint32_t j = 0; j < nb; j++) put(j);
     L[0] = base;
-    L[1] = h | (R << 28) | (defer ? WL_DEFER : 0u);
-    L[2] = rounds;
-    L[3] = S | (st << 8) | (nb << 16);
+    L[1] = h | (R << 24) | (S << 26) | (defer ? WL_DEFER : 0u);
+    L[2] = rounds | (st << 16) | (nb << 24);
 }
 
 // ---------------------------------------------------------------------------------------
