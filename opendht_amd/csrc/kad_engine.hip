@@ -1875,9 +1875,10 @@ __device__ __forceinline__ NcWindow nc_window(const DevTable& T, uint32_t r0, ui
 }
 
 // One query of the wave from its loaded window: lower bound, runs, merge, emission (see above).
-__device__ __forceinline__ void nc_answer(const DevTable& T, const Target& t, uint32_t r0, uint32_t r1,
+__device__ __forceinline__ bool nc_answer(const DevTable& T, const Target& t, uint32_t r0, uint32_t r1,
                                           const NcWindow& w, uint32_t lane, uint32_t qi, uint32_t count,
-                                          uint32_t* __restrict__ out_idx, uint8_t* __restrict__ out_cnt) {
+                                          uint32_t* __restrict__ out_idx, uint8_t* __restrict__ out_cnt,
+                                          bool fallback = true) {
     constexpr uint32_t W = 32, G = 64;
     const bool right = lane >= W;
     const uint32_t k = lane & (W - 1);
@@ -1954,9 +1955,10 @@ __device__ __forceinline__ void nc_answer(const DevTable& T, const Target& t, ui
         if (emit && rank < count) row[rank] = node + T.index_base;
         if (lane >= mm && lane < count) row[lane] = NONE;
         if (lane == 0 && out_cnt) out_cnt[qi] = (uint8_t)mm;
-    } else if (lane == 0) {
+    } else if (lane == 0 && fallback) {
         nc_serial(T, t, count, out_idx + (size_t)qi * count, out_cnt ? out_cnt + qi : nullptr);
     }
+    return ok;
 }
 
 __global__ __launch_bounds__(BLOCK) void nc_group_kernel(DevTable T, const uint8_t* __restrict__ targets, uint32_t q,
@@ -2102,14 +2104,8 @@ __device__ __forceinline__ void nc64_answer(const DevTable& T, const Target& t, 
 // 1.5x the bytes and took 1036 against 890 us per 1M k = 32 queries, with no gain from interleaving two
 // queries per wave: the kernel is bound by those bytes, not by latency).
 // ABL 1 (timing ablation only, KAD_NC_KERNEL=w64_abl1; results wrong): no serial fallback.
-template <int ABL>
-__global__ __launch_bounds__(BLOCK) void nc_wave64_kernel(DevTable T, const uint8_t* __restrict__ targets, uint32_t q,
-                                                          uint32_t count, uint32_t* __restrict__ out_idx,
-                                                          uint8_t* __restrict__ out_cnt) {
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t qi = blockIdx.x * (BLOCK / 64) + threadIdx.x / 64;
-    if (qi >= q) return;  // one query per wave: the whole wave leaves
-    const Target t = load_target(targets, qi);
+__device__ __forceinline__ void nc64_query(const DevTable& T, const Target& t, uint32_t lane, uint32_t qi, uint32_t count,
+                                           uint32_t* __restrict__ out_idx, uint8_t* __restrict__ out_cnt, bool serial) {
     const uint32_t N = T.n;
     uint32_t r0, r1;
     nc_slot(T, t, r0, r1);
@@ -2150,7 +2146,33 @@ __global__ __launch_bounds__(BLOCK) void nc_wave64_kernel(DevTable T, const uint
         emit[e] = valid[e] && !(sb & KAD_STATUS_EXPIRED);
         amb |= valid[e] && m[e] == ~0ull;
     }
-    nc64_answer(T, t, lb, lane, qi, count, out_idx, out_cnt, m, node, valid, emit, amb, ABL == 0);
+    nc64_answer(T, t, lb, lane, qi, count, out_idx, out_cnt, m, node, valid, emit, amb, serial);
+}
+
+template <int ABL>
+__global__ __launch_bounds__(BLOCK) void nc_wave64_kernel(DevTable T, const uint8_t* __restrict__ targets, uint32_t q,
+                                                          uint32_t count, uint32_t* __restrict__ out_idx,
+                                                          uint8_t* __restrict__ out_cnt) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t qi = blockIdx.x * (BLOCK / 64) + threadIdx.x / 64;
+    if (qi >= q) return;  // one query per wave: the whole wave leaves
+    nc64_query(T, load_target(targets, qi), lane, qi, count, out_idx, out_cnt, ABL == 0);
+}
+
+// Counts 17..64, cheaper first pass: the 96-node window and 32-node runs (nc_answer, ~0.9 KB less per
+// query); only the queries whose walk leaves those runs load the 64-node runs (nc64_query).
+__global__ __launch_bounds__(BLOCK) void nc_two_pass_kernel(DevTable T, const uint8_t* __restrict__ targets, uint32_t q,
+                                                            uint32_t count, uint32_t* __restrict__ out_idx,
+                                                            uint8_t* __restrict__ out_cnt) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t qi = blockIdx.x * (BLOCK / 64) + threadIdx.x / 64;
+    if (qi >= q) return;  // one query per wave: the whole wave leaves
+    const Target t = load_target(targets, qi);
+    uint32_t r0, r1;
+    nc_slot(T, t, r0, r1);
+    const NcWindow w = nc_window(T, r0, lane);
+    if (!nc_answer(T, t, r0, r1, w, lane, qi, count, out_idx, out_cnt, false))
+        nc64_query(T, t, lane, qi, count, out_idx, out_cnt, true);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -3303,12 +3325,15 @@ int kad_nc_closest_batch(const kad_table* t, const uint8_t* targets, uint32_t q,
     else if (count >= 1 && count <= 16 && t->d.n > 0 && ev && std::strcmp(ev, "multi4") == 0)
         hipLaunchKernelGGL(nc_multi_kernel<4>, dim3((q + 4 * (BLOCK / 64) - 1) / (4 * (BLOCK / 64))), dim3(BLOCK), 0,
                            (hipStream_t)stream, t->d, targets, q, count, out_idx, out_cnt);
+    else if (count > 16 && count <= 64 && t->d.n > 0 && ev && std::strcmp(ev, "wave64") == 0)
+        hipLaunchKernelGGL(nc_wave64_kernel<0>, dim3((q + BLOCK / 64 - 1) / (BLOCK / 64)), dim3(BLOCK), 0,
+                           (hipStream_t)stream, t->d, targets, q, count, out_idx, out_cnt);
     else if (count > 16 && count <= 64 && t->d.n > 0 && ev && std::strcmp(ev, "w64_abl1") == 0)
         hipLaunchKernelGGL(nc_wave64_kernel<1>, dim3((q + BLOCK / 64 - 1) / (BLOCK / 64)), dim3(BLOCK), 0,
                            (hipStream_t)stream, t->d, targets, q, count, out_idx, out_cnt);
     else if (count > 16 && count <= 64 && t->d.n > 0 && !(ev && std::strcmp(ev, "serial") == 0) &&
              !(ev && std::strcmp(ev, "multi2") == 0))
-        hipLaunchKernelGGL(nc_wave64_kernel<0>, dim3((q + BLOCK / 64 - 1) / (BLOCK / 64)), dim3(BLOCK), 0,
+        hipLaunchKernelGGL(nc_two_pass_kernel, dim3((q + BLOCK / 64 - 1) / (BLOCK / 64)), dim3(BLOCK), 0,
                            (hipStream_t)stream, t->d, targets, q, count, out_idx, out_cnt);
     else if (count >= 1 && count <= 32 && t->d.n > 0 && !(ev && std::strcmp(ev, "serial") == 0))
         hipLaunchKernelGGL(nc_multi_kernel<2>, dim3((q + 2 * (BLOCK / 64) - 1) / (2 * (BLOCK / 64))), dim3(BLOCK), 0,

@@ -102,7 +102,7 @@ for k in (1, 8, 16, 32):
     us = timeit(lambda: T.nc_closest(tg, k))
     res[f"nc_k{k}_us"] = round(us, 1)
 a32 = T.nc_closest(tg, 32)
-for kern in ("multi2", "w64_abl1"):  # counts > 16: 32-node runs; 64-node runs without the serial fallback
+for kern in ("multi2", "wave64", "w64_abl1"):  # counts > 16: 32-node runs only; 64-node runs only; without the serial fallback
     os.environ["KAD_NC_KERNEL"] = kern
     res[f"nc_k32_{kern}_us"] = round(timeit(lambda: T.nc_closest(tg, 32)), 1)
     c = T.nc_closest(tg, 32, out_idx=torch.full((q, 32), -1, dtype=torch.int32, device=dev))
