@@ -114,6 +114,16 @@ class table_info(C.Structure):
 _lib = None
 
 
+def use_ablation_build() -> None:
+    """Tools only (tools/bench_paths.py, tools/ab_bench.py): load libkadgpu_abl.so, the build with the
+    timing-ablation kernels (make -C opendht_amd/csrc ablations), instead of the product library.
+    Must run before the first lib() call."""
+    global LIB_PATH
+    if _lib is not None:
+        raise RuntimeError("libkadgpu.so is already loaded")
+    LIB_PATH = os.path.join(_HERE, "libkadgpu_abl.so")
+
+
 def lib() -> C.CDLL:
     """Load libkadgpu.so, raising loudly (no fallback) if it is not built."""
     global _lib

@@ -685,7 +685,8 @@ __device__ __forceinline__ uint32_t dw(const uint4 (&L)[8], int k) {  // static 
 // nodes of W(R_c)), or false when the query needs the exact path (marked line, target outside b's
 // range, too few stored slots). Contains a wave vote: call from uniform control flow, inactive lanes
 // with act = false (they return false).
-// ABL (timing ablations only, KAD_RT_KERNEL=wl_abl1|wl_abl2; results wrong): 2 = no ranking.
+// ABL (timing ablations only, KAD_RT_KERNEL=wl_abl1|wl_abl2 in the KAD_ABLATIONS tools build; results
+// wrong): 2 = no ranking.
 template <int ABL>
 __device__ __forceinline__ bool wl_answer(const DevTable& T, const Target& t, uint32_t b, uint32_t count, bool act,
                                           uint32_t (&o)[8], uint32_t& m) {
@@ -2735,16 +2736,20 @@ int launch_rt(const kad_table* t, const uint8_t* targets, uint32_t q, uint32_t c
     const DevTable& d = t->d;
     const char* ev = std::getenv("KAD_RT_KERNEL");
     if (K == 8 && (d.flags & TF_WL) && !(ev && std::strcmp(ev, "lane") == 0)) {
+#ifdef KAD_ABLATIONS  // timing ablations with WRONG results: only in the tools build (Makefile target `ablations`)
         if (ev && std::strcmp(ev, "wl_abl1") == 0)
             hipLaunchKernelGGL(rt_wl_kernel<1>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
         else if (ev && std::strcmp(ev, "wl_abl2") == 0)
             hipLaunchKernelGGL(rt_wl_kernel<2>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
         else
+#endif
             hipLaunchKernelGGL(rt_wl_kernel<0>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
     } else if (K == 16 && (d.flags & TF_WL16) && !(ev && std::strcmp(ev, "lane") == 0)) {
+#ifdef KAD_ABLATIONS
         if (ev && std::strcmp(ev, "wl16_abl1") == 0)
             hipLaunchKernelGGL(rt_wl16_kernel<1>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
         else
+#endif
             hipLaunchKernelGGL(rt_wl16_kernel<0>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
     } else if (K == 32 && (d.flags & TF_WL32) && !(ev && std::strcmp(ev, "lane") == 0)) {
         hipLaunchKernelGGL(rt_wl32_kernel, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
@@ -3310,10 +3315,16 @@ int kad_nc_closest_batch(const kad_table* t, const uint8_t* targets, uint32_t q,
     DeviceGuard g(t->device);
     const char* ev = std::getenv("KAD_NC_KERNEL");
     const bool lines = (t->d.flags & TF_NCL) && !ev;  // KAD_NC_KERNEL=<kernel> picks another one (A/B timing)
+#ifdef KAD_ABLATIONS  // timing ablations with WRONG results: only in the tools build
     if ((t->d.flags & TF_NCL) && ev && std::strcmp(ev, "lines_abl1") == 0 && count >= 1 && count <= 16)
         hipLaunchKernelGGL(nc_line_kernel<1>, dim3(grid_for(q)), dim3(BLOCK), 0, (hipStream_t)stream, t->d, targets, q,
                            count, out_idx, out_cnt);
-    else if (lines && count >= 1 && count <= 16)
+    else if (count > 16 && count <= 64 && t->d.n > 0 && ev && std::strcmp(ev, "w64_abl1") == 0)
+        hipLaunchKernelGGL(nc_wave64_kernel<1>, dim3((q + BLOCK / 64 - 1) / (BLOCK / 64)), dim3(BLOCK), 0,
+                           (hipStream_t)stream, t->d, targets, q, count, out_idx, out_cnt);
+    else
+#endif
+    if (lines && count >= 1 && count <= 16)
         hipLaunchKernelGGL(nc_line_kernel<0>, dim3(grid_for(q)), dim3(BLOCK), 0, (hipStream_t)stream, t->d, targets, q,
                            count, out_idx, out_cnt);
     else if (count >= 1 && count <= 16 && ev && std::strcmp(ev, "group1") == 0)
@@ -3327,9 +3338,6 @@ int kad_nc_closest_batch(const kad_table* t, const uint8_t* targets, uint32_t q,
                            (hipStream_t)stream, t->d, targets, q, count, out_idx, out_cnt);
     else if (count > 16 && count <= 64 && t->d.n > 0 && ev && std::strcmp(ev, "wave64") == 0)
         hipLaunchKernelGGL(nc_wave64_kernel<0>, dim3((q + BLOCK / 64 - 1) / (BLOCK / 64)), dim3(BLOCK), 0,
-                           (hipStream_t)stream, t->d, targets, q, count, out_idx, out_cnt);
-    else if (count > 16 && count <= 64 && t->d.n > 0 && ev && std::strcmp(ev, "w64_abl1") == 0)
-        hipLaunchKernelGGL(nc_wave64_kernel<1>, dim3((q + BLOCK / 64 - 1) / (BLOCK / 64)), dim3(BLOCK), 0,
                            (hipStream_t)stream, t->d, targets, q, count, out_idx, out_cnt);
     else if (count > 16 && count <= 64 && t->d.n > 0 && !(ev && std::strcmp(ev, "serial") == 0) &&
              !(ev && std::strcmp(ev, "multi2") == 0))

@@ -16,6 +16,9 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
+import opendht_amd._lib as _kl  # noqa: E402
+
+_kl.use_ablation_build()  # the wl_abl* / *_abl1 timing ablations live only in the tools build
 from opendht_amd import DeviceTable  # noqa: E402
 from opendht_amd.sharded import ShardSpec, build_shard  # noqa: E402
 

@@ -9,6 +9,9 @@ import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import opendht_amd._lib as _kl  # noqa: E402
+
+_kl.use_ablation_build()  # the wl_abl* / *_abl1 timing ablations live only in the tools build
 from opendht_amd import DeviceTable, rt_closest_dual  # noqa: E402
 from opendht_amd.sharded import ShardSpec, build_shard  # noqa: E402
 

@@ -79,9 +79,11 @@ extern "C" int mb_line(const void* table, uint64_t bytes, const uint8_t* targets
     hipStream_t st = (hipStream_t)s;
     const uint64_t np = bytes / (16ull * nx);
     if (coop) hipLaunchKernelGGL(k_coop, g, b, 0, st, t, bytes / 128, targets, n, p2, out);
+    else if (nx == 1) hipLaunchKernelGGL(k_lane<1>, g, b, 0, st, t, np, targets, n, p2, out);
     else if (nx == 2) hipLaunchKernelGGL(k_lane<2>, g, b, 0, st, t, np, targets, n, p2, out);
     else if (nx == 4) hipLaunchKernelGGL(k_lane<4>, g, b, 0, st, t, np, targets, n, p2, out);
     else if (nx == 8) hipLaunchKernelGGL(k_lane<8>, g, b, 0, st, t, np, targets, n, p2, out);
+    else if (nx == 16) hipLaunchKernelGGL(k_lane<16>, g, b, 0, st, t, np, targets, n, p2, out);
     return hipGetLastError();
 }
 

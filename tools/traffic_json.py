@@ -12,15 +12,17 @@ import subprocess
 import sys
 
 d, ksub, tag = sys.argv[1], sys.argv[2], sys.argv[3]
+count = int(sys.argv[4]) if len(sys.argv) > 4 else 8
+args = sys.argv[5] if len(sys.argv) > 5 else "--steps 5 --warmup 2 --no-cpu"
 root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 pm = json.loads(subprocess.check_output([sys.executable, os.path.join(root, "tools", "parse_pmc.py"), d, ksub]))
 fetch = 2 * pm["FETCH_SIZE"] * 1024
 write = pm["WRITE_SIZE"] * 1024
-out = {"kernel": ksub, "hbm_bytes_per_launch": fetch + write, "read_bytes": fetch, "write_bytes": write,
+out = {"kernel": ksub, "count": count, "hbm_bytes_per_launch": fetch + write, "read_bytes": fetch, "write_bytes": write,
        "raw_kib": {"FETCH_SIZE": pm["FETCH_SIZE"], "WRITE_SIZE": pm["WRITE_SIZE"]},
        "l2_hit_rate": pm["TCC_HIT_sum"] / (pm["TCC_HIT_sum"] + pm["TCC_MISS_sum"]) if "TCC_HIT_sum" in pm else None,
        "correction": "FETCH_SIZE x2 (gfx950 128-B requests tallied at 64 B), KiB -> bytes",
-       "source": f"rocprofv3 --pmc passes over bench.py --steps 5 --warmup 2 --no-cpu ({d})"}
+       "source": f"rocprofv3 --pmc passes over bench.py {args} ({d})"}
 p = os.path.join(root, "profiles", f"traffic_{tag}.json")
 json.dump(out, open(p, "w"), indent=1)
 print(json.dumps(out, indent=1))
