@@ -410,26 +410,61 @@ def cold_pass(T, tgs, outs, ocnt, cnt_k, Q, moved_q, dev, stream, reps=8):
 
 
 def refresh_pass(T, sh, tgs, outs, ocnt, cnt_k, Q, avg_kernel_s, dev, stream, reps=5):
-    """Cost of re-deriving every node's isGood(now) on the device (kad_table_refresh_status: the
-    status bytes, good masks, prefix sums and all line sets) after node times were uploaded."""
+    """Cost of keeping every node's isGood(now) / isExpired() current on the device (node.cpp:34-40):
+    kad_table_refresh_status(now) re-derives the status from the node times in one pass and rebuilds
+    only the masks and lines that the flips touch; kad_table_patch_status applies a changed-node list."""
     import torch
 
     now = 10**15
+    n = sh.ids.shape[0]
     t, rt, ex = node_times(sh.status, now)
     T.set_times(t, rt, ex)
-    ts = []
-    for j in range(reps):
+
+    def ev_time(fn):
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record(stream)
-        T.refresh_status(now + j, stream=stream.cuda_stream)
+        fn()
         b.record(stream)
         torch.cuda.synchronize(dev)
-        ts.append(a.elapsed_time(b) / 1e3)
-    tr = float(np.median(ts))
-    return {"full_refresh_ms": tr * 1e3, "nodes": int(sh.ids.shape[0]),
-            "refresh_plus_query_queries_per_s": Q / (tr + avg_kernel_s),
-            "how": "kad_table_refresh_status(now) on the shard (status from node times, masks, prefix sums, "
-                   f"window and NodeCache lines), median of {reps}; + one {Q}-query step"}
+        return a.elapsed_time(b) / 1e3
+
+    T.refresh_status(now, stream=stream.cuda_stream)
+    torch.cuda.synchronize(dev)
+    no_flip = float(np.median([ev_time(lambda j=j: T.refresh_status(now + 1 + j, stream=stream.cuda_stream))
+                               for j in range(reps)]))
+    rng = np.random.default_rng(0xF11)
+    good = np.flatnonzero(sh.status & 1).astype(np.uint32)
+    ageing = {}
+    for frac in (0.001, 0.01):  # that share of the good nodes was last heard 10 min + 1 ns before `now`
+        sel = rng.choice(good, size=int(good.shape[0] * frac), replace=False).astype(np.uint32)
+        now += 10**9
+        T.patch_times(sel, np.full(sel.shape[0], now - 10 * 60 * 10**9 - 1, np.int64), np.full(sel.shape[0], now, np.int64),
+                      np.zeros(sel.shape[0], np.uint8))
+        ageing[f"{frac:g}"] = ev_time(lambda: T.refresh_status(now, stream=stream.cuda_stream)) * 1e3
+        T.patch_times(sel, np.full(sel.shape[0], now, np.int64), np.full(sel.shape[0], now, np.int64),
+                      np.zeros(sel.shape[0], np.uint8))
+        T.refresh_status(now, stream=stream.cuda_stream)
+        torch.cuda.synchronize(dev)
+    patch = {}
+    st = sh.status.copy()
+    for frac in (0.001, 0.01, 0.1):
+        m = int(n * frac)
+        nodes = rng.choice(n, size=m, replace=False).astype(np.uint32)
+        vals = st[nodes] ^ np.uint8(1)  # good <-> dubious
+        t0 = time.perf_counter()
+        T.patch_status(nodes, vals)
+        patch[f"{frac:g}"] = (time.perf_counter() - t0) * 1e3
+        T.patch_status(nodes, st[nodes])  # back
+    return {"refresh_no_flip_ms": no_flip * 1e3,
+            "refresh_ageing_ms": ageing,
+            "patch_status_ms": patch,
+            "nodes": int(n),
+            "refresh_plus_query_queries_per_s": Q / (no_flip + avg_kernel_s),
+            "how": "refresh_no_flip: kad_table_refresh_status(now) with `now` moved and no status flipping (one "
+                   f"pass over {n} nodes' times + good-prefix scan), median of {reps}, HIP events; refresh_ageing: "
+                   "the same with that share of the good nodes ageing past 10 min; patch_status: "
+                   "kad_table_patch_status of a random changed-node list of that share of the nodes (host list, "
+                   "synchronous, wall clock incl. the H2D copy); refresh_plus_query: one refresh + one step"}
 
 
 # ---------------------------------------------------------------------------------------------

@@ -112,18 +112,29 @@ int kad_table_create(kad_table** out, int device,
 int kad_table_destroy(kad_table* t);
 int kad_table_get_info(const kad_table* t, kad_table_info* out);
 
-/* Replace the status snapshot (host bytes, n_nodes). Rebuilds the per-bucket good
- * prefix sums on the device. Synchronous. */
+/* Replace the status snapshot (host bytes, n_nodes). Synchronous. Incremental: only the buckets whose
+ * good set changed get new masks, and only the window / NodeCache lines whose window reaches a changed
+ * node are rebuilt (the good prefix sums are re-scanned). */
 int kad_table_update_status(kad_table* t, const uint8_t* status);
+/* Incremental status update for a changed-node list (reference: the isGood/isExpired flips that
+ * Node::received / setExpired cause, node.cpp:82-108; network_engine.cpp:245): node nodes[j] gets
+ * status[j] (host arrays, m entries; nodes == NULL means all n_nodes in order). Rebuilds only what
+ * the flips touch, as kad_table_update_status. Synchronous. */
+int kad_table_patch_status(kad_table* t, uint32_t m, const uint32_t* nodes, const uint8_t* status);
 
 /* Upload Node liveness (reference node.h:39-40,105: time, reply_time, expired_)
  * as int64 nanoseconds of steady_clock + expired flag bytes; host arrays, n_nodes each.
  * INT64_MIN encodes time_point::min(). Synchronous. */
 int kad_table_set_times(kad_table* t, const int64_t* time_ns, const int64_t* reply_time_ns,
                         const uint8_t* expired);
+/* Update the uploaded liveness of m listed nodes (Node::received / setExpired on the host: node.cpp:82-108):
+ * host arrays of m entries. Takes effect at the next kad_table_refresh_status. Synchronous. */
+int kad_table_patch_times(kad_table* t, uint32_t m, const uint32_t* nodes, const int64_t* time_ns,
+                          const int64_t* reply_time_ns, const uint8_t* expired);
 /* Recompute the status snapshot on the device at `now_ns` from the uploaded times:
  * good = !expired && reply_time >= now-120min && time >= now-10min (node.cpp:34-40,
- * node.h:91-94), then rebuild the good prefix sums. Async on `stream`. */
+ * node.h:91-94): one pass over the node times; only the nodes whose status flips at this `now`
+ * cause mask and line rebuilds (then the good prefix sums are re-scanned). Async on `stream`. */
 int kad_table_refresh_status(kad_table* t, int64_t now_ns, void* stream);
 
 /* ---- incremental device mirror ----------------------

@@ -15,18 +15,28 @@
  *   NodeT         : `id` (20 bytes via .data()), `bool isGood(time_point) const`, `bool isExpired() const`
  *   NodeMapT      : std::map<InfoHash, std::weak_ptr<NodeT>> (one NodeCache family, node_cache.h:42-50)
  *
- * A mirror is a snapshot of the table at `now` (the status byte of every node is Node::isGood(now)
- * / isExpired() evaluated once, on the host thread that owns the table, as the reference does on its
- * dht thread). Results come back as the same shared_ptr<NodeT> objects the table holds, in the
- * reference's order. After table mutations (Dht::onNewNode / expireBuckets / split), either
- * re-snapshot or record them on the mirror (nodeRemoved / nodeReplaced / nodeAdded / bucketSplit)
- * and flush(now): kad_table_apply replays them on the device copy.
+ * A mirror holds the table's node IDs, bucket directory and every node's liveness (Node::time,
+ * reply_time, isExpired(); node.h:39-40, 67) on the device. findClosestNodes(id, now, count) evaluates
+ * Node::isGood(now) for the `now` it is given, as the reference does per call (routing_table.cpp:77):
+ * when `now` moves, kad_table_refresh_status re-derives the status on the device and rebuilds only what
+ * flipped. Results come back as the same shared_ptr<NodeT> objects the table holds, in the reference's
+ * order. What the mirror cannot observe must be reported:
+ *   - liveness changes of a node (Node::received, setExpired, reset, a search writing node->time):
+ *     nodeUpdated(node) before the next query (or syncTimes() to re-read every node);
+ *   - table mutations (Dht::onNewNode / expireBuckets / split): nodeRemoved / nodeReplaced / nodeAdded /
+ *     bucketSplit, then flush(now): kad_table_apply replays them on the device copy; or re-snapshot.
  */
 #ifndef KADGPU_HPP
 #define KADGPU_HPP
 
+#include <sys/socket.h>  // AF_INET (sa_family_t), as OpenDHT's sockaddr.h
+
 #include <algorithm>
+#include <chrono>
+#include <climits>
 #include <cstdint>
+#include <functional>
+#include <unordered_map>
 #include <cstring>
 #include <iterator>
 #include <memory>
@@ -97,9 +107,45 @@ public:
                      "kad_nc_closest_batch_host");
     }
 
+    /* Node liveness (kad_table_set_times / kad_table_patch_times) and the device-side isGood(now)
+     * refresh (kad_table_refresh_status, incremental). */
+    void setTimes(const std::vector<int64_t>& time_ns, const std::vector<int64_t>& reply_ns,
+                  const std::vector<uint8_t>& expired) {
+        check(kad_table_set_times(t_, time_ns.data(), reply_ns.data(), expired.data()), "kad_table_set_times");
+    }
+    void patchTimes(const std::vector<uint32_t>& nodes, const std::vector<int64_t>& time_ns,
+                    const std::vector<int64_t>& reply_ns, const std::vector<uint8_t>& expired) {
+        if (!nodes.empty())
+            check(kad_table_patch_times(t_, (uint32_t)nodes.size(), nodes.data(), time_ns.data(), reply_ns.data(),
+                                        expired.data()), "kad_table_patch_times");
+    }
+    void patchStatus(const std::vector<uint32_t>& nodes, const std::vector<uint8_t>& status) {
+        if (!nodes.empty())
+            check(kad_table_patch_status(t_, (uint32_t)nodes.size(), nodes.data(), status.data()),
+                  "kad_table_patch_status");
+    }
+    void refreshStatus(int64_t now_ns) {
+        check(kad_table_refresh_status(t_, now_ns, nullptr), "kad_table_refresh_status");
+    }
+
 private:
     kad_table* t_ = nullptr;
 };
+
+/* time_point -> int64 nanoseconds of its clock, time_point::min()/max() -> INT64_MIN/MAX (Node::time and
+ * reply_time start at time_point::min(), node.h:39-40). */
+template <class TimePoint>
+inline int64_t to_ns(TimePoint tp) {
+    if (tp == TimePoint::min()) return INT64_MIN;
+    if (tp == TimePoint::max()) return INT64_MAX;
+    return (int64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(tp.time_since_epoch()).count();
+}
+
+/* Status byte of a node at `now`: Node::isGood(now) | Node::isExpired() << 1 (node.cpp:34-40, node.h:67). */
+template <class NodePtr, class TimePoint>
+inline uint8_t status_of(const NodePtr& n, TimePoint now) {
+    return (uint8_t)((n->isGood(now) ? KAD_STATUS_GOOD : 0u) | (n->isExpired() ? KAD_STATUS_EXPIRED : 0u));
+}
 
 template <class T>
 inline const uint8_t* id_bytes(const T& id) {
@@ -121,7 +167,7 @@ public:
         snapshot(rt, now, device);
     }
 
-    /* Snapshot `rt` at `now`: nodes grouped by bucket in list order, status = isGood(now) | isExpired()<<1. */
+    /* Snapshot `rt`: nodes grouped by bucket in list order, their liveness, status at `now`. */
     template <class TimePoint>
     void snapshot(const RoutingTableT& rt, TimePoint now, int device = 0) {
         std::vector<uint8_t> ids, status, first;
@@ -133,26 +179,30 @@ public:
             for (const auto& n : b.nodes) {
                 nodes_.push_back(n);
                 ids.insert(ids.end(), id_bytes(n->id), id_bytes(n->id) + KAD_HASH_LEN);
-                status.push_back((uint8_t)((n->isGood(now) ? KAD_STATUS_GOOD : 0u) |
-                                           (n->isExpired() ? KAD_STATUS_EXPIRED : 0u)));
+                status.push_back(status_of(n, now));
             }
         }
         off.push_back((uint32_t)nodes_.size());
         buckets_ = (uint32_t)(off.size() - 1);
         table_ = DeviceTable(device, ids, status, first, off);
+        reindex();
+        syncTimes();
+        now_ns_ = to_ns(now);
+        refresh_ = false;
     }
 
-    /* RoutingTable::findClosestNodes(id, now, count) at the snapshot's `now` (routing_table.cpp:67-111). */
-    template <class InfoHashT>
-    std::vector<NodePtr> findClosestNodes(const InfoHashT& id, size_t count = KAD_TARGET_NODES) const {
-        std::vector<std::vector<NodePtr>> r = findClosestNodesBatch(&id, 1, count);
+    /* RoutingTable::findClosestNodes(id, now, count) (routing_table.h:48, routing_table.cpp:67-111). */
+    template <class InfoHashT, class TimePoint>
+    std::vector<NodePtr> findClosestNodes(const InfoHashT& id, TimePoint now, size_t count = KAD_TARGET_NODES) const {
+        std::vector<std::vector<NodePtr>> r = findClosestNodesBatch(&id, 1, now, count);
         return std::move(r[0]);
     }
 
-    /* Batched form: one result vector per target. */
-    template <class InfoHashT>
-    std::vector<std::vector<NodePtr>> findClosestNodesBatch(const InfoHashT* ids, size_t q,
+    /* Batched form: one result vector per target, all at the same `now`. */
+    template <class InfoHashT, class TimePoint>
+    std::vector<std::vector<NodePtr>> findClosestNodesBatch(const InfoHashT* ids, size_t q, TimePoint now,
                                                             size_t count = KAD_TARGET_NODES) const {
+        advance(to_ns(now));
         std::vector<uint8_t> targets(q * KAD_HASH_LEN);
         for (size_t i = 0; i < q; i++) std::memcpy(&targets[i * KAD_HASH_LEN], id_bytes(ids[i]), KAD_HASH_LEN);
         std::vector<uint32_t> idx;
@@ -165,10 +215,27 @@ public:
         }
         return out;
     }
-    template <class InfoHashT>
-    std::vector<std::vector<NodePtr>> findClosestNodesBatch(const std::vector<InfoHashT>& ids,
+    template <class InfoHashT, class TimePoint>
+    std::vector<std::vector<NodePtr>> findClosestNodesBatch(const std::vector<InfoHashT>& ids, TimePoint now,
                                                             size_t count = KAD_TARGET_NODES) const {
-        return findClosestNodesBatch(ids.data(), ids.size(), count);
+        return findClosestNodesBatch(ids.data(), ids.size(), now, count);
+    }
+
+    /* A mirrored node's time / reply_time / expired_ changed (Node::received, setExpired, reset,
+     * Search::insertNode writing node->time): re-read at the next query. */
+    void nodeUpdated(const NodePtr& n) { updated_.push_back(index_of(n)); }
+    /* Re-read every mirrored node's liveness (kad_table_set_times); status re-derived at the next query. */
+    void syncTimes() {
+        std::vector<int64_t> t(nodes_.size()), r(nodes_.size());
+        std::vector<uint8_t> e(nodes_.size());
+        for (size_t i = 0; i < nodes_.size(); i++) {
+            t[i] = to_ns(nodes_[i]->time);
+            r[i] = to_ns(nodes_[i]->reply_time);
+            e[i] = nodes_[i]->isExpired() ? 1 : 0;
+        }
+        if (!nodes_.empty()) table_.setTimes(t, r, e);
+        updated_.clear();
+        refresh_ = true;
     }
 
     /* Incremental mirror (kad_table_apply): record the mutations the Dht makes to the host table, in
@@ -193,7 +260,7 @@ public:
         std::vector<uint8_t> ids, status;
         for (const auto& n : added_) {
             ids.insert(ids.end(), id_bytes(n->id), id_bytes(n->id) + KAD_HASH_LEN);
-            status.push_back((uint8_t)((n->isGood(now) ? KAD_STATUS_GOOD : 0u) | (n->isExpired() ? KAD_STATUS_EXPIRED : 0u)));
+            status.push_back(status_of(n, now));
         }
         std::vector<uint32_t> remap(nodes_.size()), idx(added_.size());
         check(kad_table_apply(table_.get(), ops_.data(), (uint32_t)(ops_.size() / 3), ids.data(), status.data(),
@@ -210,6 +277,10 @@ public:
         buckets_ = inf.n_buckets;
         ops_.clear();
         added_.clear();
+        reindex();
+        syncTimes();  // kad_table_apply drops the node times (the layout moved)
+        now_ns_ = to_ns(now);
+        refresh_ = true;
     }
 
     size_t bucketCount() const { return buckets_; }
@@ -217,47 +288,82 @@ public:
     const DeviceTable& table() const { return table_; }
 
 private:
+    // status at the query's `now`: reported liveness changes first, then the device refresh
+    void advance(int64_t now_ns) const {
+        if (nodes_.empty()) {  // nothing to evaluate (and no times on the device)
+            now_ns_ = now_ns;
+            return;
+        }
+        if (!updated_.empty()) {
+            std::vector<int64_t> t, r;
+            std::vector<uint8_t> e;
+            for (uint32_t i : updated_) {
+                t.push_back(to_ns(nodes_[i]->time));
+                r.push_back(to_ns(nodes_[i]->reply_time));
+                e.push_back(nodes_[i]->isExpired() ? 1 : 0);
+            }
+            table_.patchTimes(updated_, t, r, e);
+            updated_.clear();
+            refresh_ = true;
+        }
+        if (refresh_ || now_ns != now_ns_) {
+            table_.refreshStatus(now_ns);
+            now_ns_ = now_ns;
+            refresh_ = false;
+        }
+    }
+    void reindex() {
+        index_.clear();
+        for (size_t i = 0; i < nodes_.size(); i++) index_[nodes_[i].get()] = (uint32_t)i;
+    }
     void op(uint32_t kind, uint32_t a, uint32_t b) {
         ops_.push_back(kind);
         ops_.push_back(a);
         ops_.push_back(b);
     }
     uint32_t index_of(const NodePtr& n) const {
-        auto it = std::find(nodes_.begin(), nodes_.end(), n);
-        if (it == nodes_.end()) throw Error(KAD_ERR_INVALID, "node not in the mirrored snapshot (flush first)");
-        return (uint32_t)(it - nodes_.begin());
+        auto it = index_.find(n.get());
+        if (it == index_.end()) throw Error(KAD_ERR_INVALID, "node not in the mirrored snapshot (flush first)");
+        return it->second;
     }
     uint32_t slot(const NodePtr& n) {
         added_.push_back(n);
         return (uint32_t)(added_.size() - 1);
     }
 
-    DeviceTable table_;
+    mutable DeviceTable table_;
     std::vector<NodePtr> nodes_;
+    std::unordered_map<const void*, uint32_t> index_;
     uint32_t buckets_ = 0;
     std::vector<uint32_t> ops_;
     std::vector<NodePtr> added_;
+    mutable std::vector<uint32_t> updated_;
+    mutable int64_t now_ns_ = INT64_MIN;
+    mutable bool refresh_ = false;
 };
 
-/* Device mirror of one NodeCache family map (node_cache.h:42-50). */
+/* Device mirror of one NodeCache family map (node_cache.h:42-50: std::map<InfoHash, weak_ptr<Node>>). */
 template <class NodeMapT>
-class NodeCacheMirror {
+class NodeCacheFamilyMirror {
 public:
-    using NodePtr = decltype(std::declval<const NodeMapT&>().begin()->second.lock());
+    using WeakPtr = typename std::decay<decltype(std::declval<const NodeMapT&>().begin()->second)>::type;
+    using NodePtr = decltype(std::declval<const WeakPtr&>().lock());
 
-    NodeCacheMirror() {}
-    explicit NodeCacheMirror(const NodeMapT& m, int device = 0) { snapshot(m, device); }
+    NodeCacheFamilyMirror() {}
+    explicit NodeCacheFamilyMirror(const NodeMapT& m, int device = 0) { snapshot(m, device); }
 
     /* Snapshot: map order (ascending ID); dead weak_ptrs and expired nodes are walked over but never
      * emitted (node_cache.cpp:60-62), so both get the "expired" status bit. */
     void snapshot(const NodeMapT& m, int device = 0) {
         std::vector<uint8_t> ids, status;
         nodes_.clear();
+        index_.clear();
         for (const auto& kv : m) {
             NodePtr n = kv.second.lock();
             ids.insert(ids.end(), id_bytes(kv.first), id_bytes(kv.first) + KAD_HASH_LEN);
             status.push_back((uint8_t)((!n || n->isExpired()) ? KAD_STATUS_EXPIRED : 0u));
-            nodes_.push_back(n);
+            if (n) index_[n.get()] = (uint32_t)nodes_.size();
+            nodes_.push_back(kv.second);
         }
         table_ = DeviceTable(device, ids, status, std::vector<uint8_t>(), std::vector<uint32_t>(), 0, true);
     }
@@ -265,54 +371,121 @@ public:
     /* NodeCache::getCachedNodes(id, af, count) for this family (node_cache.cpp:36-66). */
     template <class InfoHashT>
     std::vector<NodePtr> getCachedNodes(const InfoHashT& id, size_t count) const {
-        std::vector<uint32_t> idx;
-        std::vector<uint8_t> cnt;
-        table_.getCachedNodesBatch(id_bytes(id), 1, count, idx, cnt);
-        std::vector<NodePtr> out;
-        for (size_t j = 0; j < cnt[0]; j++) out.push_back(nodes_[idx[j]]);
+        std::vector<std::vector<NodePtr>> r = getCachedNodesBatch(&id, 1, count);
+        return std::move(r[0]);
+    }
+    /* Batched form. A returned node found dead or expired on the host (the reference skips it without
+     * counting it) is marked expired on the device and its queries re-run, so results stay exact without
+     * a notification for deaths and expiries; an expired node that comes back (Node::received with a
+     * reply, reset(), clearBadNodes) must be reported with nodeUpdated. */
+    template <class InfoHashT>
+    std::vector<std::vector<NodePtr>> getCachedNodesBatch(const InfoHashT* ids, size_t q, size_t count) const {
+        std::vector<std::vector<NodePtr>> out(q);
+        std::vector<size_t> todo(q);
+        for (size_t i = 0; i < q; i++) todo[i] = i;
+        while (!todo.empty()) {
+            std::vector<uint8_t> targets(todo.size() * KAD_HASH_LEN);
+            for (size_t k = 0; k < todo.size(); k++)
+                std::memcpy(&targets[k * KAD_HASH_LEN], id_bytes(ids[todo[k]]), KAD_HASH_LEN);
+            std::vector<uint32_t> idx, stale;
+            std::vector<uint8_t> cnt;
+            table_.getCachedNodesBatch(targets.data(), todo.size(), count, idx, cnt);
+            std::vector<size_t> again;
+            for (size_t k = 0; k < todo.size(); k++) {
+                std::vector<NodePtr>& o = out[todo[k]];
+                o.clear();
+                bool ok = true;
+                for (size_t j = 0; j < cnt[k]; j++) {
+                    const uint32_t x = idx[k * count + j];
+                    NodePtr n = nodes_[x].lock();
+                    if (!n || n->isExpired()) { stale.push_back(x); ok = false; continue; }
+                    o.push_back(std::move(n));
+                }
+                if (!ok) again.push_back(todo[k]);
+            }
+            if (!stale.empty()) {
+                std::sort(stale.begin(), stale.end());
+                stale.erase(std::unique(stale.begin(), stale.end()), stale.end());
+                table_.patchStatus(stale, std::vector<uint8_t>(stale.size(), (uint8_t)KAD_STATUS_EXPIRED));
+            }
+            todo.swap(again);
+        }
         return out;
     }
     template <class InfoHashT>
     std::vector<std::vector<NodePtr>> getCachedNodesBatch(const std::vector<InfoHashT>& ids, size_t count) const {
-        const size_t q = ids.size();
-        std::vector<uint8_t> targets(q * KAD_HASH_LEN);
-        for (size_t i = 0; i < q; i++) std::memcpy(&targets[i * KAD_HASH_LEN], id_bytes(ids[i]), KAD_HASH_LEN);
-        std::vector<uint32_t> idx;
-        std::vector<uint8_t> cnt;
-        table_.getCachedNodesBatch(targets.data(), q, count, idx, cnt);
-        std::vector<std::vector<NodePtr>> out(q);
-        for (size_t i = 0; i < q; i++)
-            for (size_t j = 0; j < cnt[i]; j++) out[i].push_back(nodes_[idx[i * count + j]]);
-        return out;
+        return getCachedNodesBatch(ids.data(), ids.size(), count);
     }
+    /* A cached node's isExpired() changed (setExpired, Node::received with a reply, reset()). */
+    void nodeUpdated(const NodePtr& n) {
+        auto it = index_.find(n.get());
+        if (it == index_.end()) return;  // not in this family's map
+        table_.patchStatus(std::vector<uint32_t>{it->second},
+                           std::vector<uint8_t>{(uint8_t)(n->isExpired() ? KAD_STATUS_EXPIRED : 0u)});
+    }
+    size_t size() const { return nodes_.size(); }
 
 private:
-    DeviceTable table_;
-    std::vector<NodePtr> nodes_;
+    mutable DeviceTable table_;
+    std::vector<WeakPtr> nodes_;
+    std::unordered_map<const void*, uint32_t> index_;
+};
+
+/* Device mirror of a whole NodeCache (cache_4 and cache_6, node_cache.h:49-50). */
+template <class NodeMapT>
+class NodeCacheMirror {
+public:
+    using NodePtr = typename NodeCacheFamilyMirror<NodeMapT>::NodePtr;
+
+    void snapshot(const NodeMapT& cache4, const NodeMapT& cache6, int device = 0) {
+        v4_.snapshot(cache4, device);
+        v6_.snapshot(cache6, device);
+    }
+    /* NodeCache::getCachedNodes(const InfoHash&, sa_family_t, size_t) (node_cache.h:32, node_cache.cpp:36-66). */
+    template <class InfoHashT>
+    std::vector<NodePtr> getCachedNodes(const InfoHashT& id, sa_family_t sa_f, size_t count) const {
+        return family(sa_f).getCachedNodes(id, count);
+    }
+    void nodeUpdated(const NodePtr& n) {
+        v4_.nodeUpdated(n);
+        v6_.nodeUpdated(n);
+    }
+    const NodeCacheFamilyMirror<NodeMapT>& family(sa_family_t sa_f) const { return sa_f == AF_INET ? v4_ : v6_; }
+    NodeCacheFamilyMirror<NodeMapT>& family(sa_family_t sa_f) { return sa_f == AF_INET ? v4_ : v6_; }
+
+private:
+    NodeCacheFamilyMirror<NodeMapT> v4_, v6_;
 };
 
 /* Dht-level accessor over both families: findClosestNodes(id, af, count)
- * = buckets(af).findClosestNodes(id, now, count) (dht.h:437-438; call sites dht.cpp:3196-3217). */
-template <class RoutingTableT>
+ * = buckets(af).findClosestNodes(id, scheduler.time(), count) (dht.h:437-438; call sites dht.cpp:3196-3217).
+ * `now` comes from the mirror's clock: steady_clock::now() by default, or the Dht scheduler's time
+ * (setClock([&]{ return scheduler.time(); })). */
+template <class RoutingTableT, class Clock = std::chrono::steady_clock>
 class DhtMirror {
 public:
     using NodePtr = typename RoutingTableMirror<RoutingTableT>::NodePtr;
+    using time_point = typename Clock::time_point;
 
-    template <class TimePoint>
-    void snapshot(const RoutingTableT& buckets4, const RoutingTableT& buckets6, TimePoint now, int device = 0) {
+    DhtMirror() : clock_([] { return Clock::now(); }) {}
+
+    void snapshot(const RoutingTableT& buckets4, const RoutingTableT& buckets6, time_point now, int device = 0) {
         v4_.snapshot(buckets4, now, device);
         v6_.snapshot(buckets6, now, device);
     }
-    /* af: the caller's AF_INET / AF_INET6 values (passed in so this header needs no socket headers). */
+    void setClock(std::function<time_point()> clock) { clock_ = std::move(clock); }
+
     template <class InfoHashT>
-    std::vector<NodePtr> findClosestNodes(const InfoHashT& id, int af, size_t count, int af_inet) const {
-        return (af == af_inet ? v4_ : v6_).findClosestNodes(id, count);
+    std::vector<NodePtr> findClosestNodes(const InfoHashT& id, sa_family_t af, size_t count = KAD_TARGET_NODES) const {
+        return buckets(af).findClosestNodes(id, clock_(), count);
     }
-    const RoutingTableMirror<RoutingTableT>& family4() const { return v4_; }
-    const RoutingTableMirror<RoutingTableT>& family6() const { return v6_; }
+    /* Dht::buckets(af) (dht.h:437-438) */
+    const RoutingTableMirror<RoutingTableT>& buckets(sa_family_t af) const { return af == AF_INET ? v4_ : v6_; }
+    RoutingTableMirror<RoutingTableT>& buckets(sa_family_t af) { return af == AF_INET ? v4_ : v6_; }
 
 private:
     RoutingTableMirror<RoutingTableT> v4_, v6_;
+    std::function<time_point()> clock_;
 };
 
 }  // namespace kadgpu

@@ -59,6 +59,8 @@ SIGNATURES = {
     "kad_table_export": (C.c_int, [_P, _P, _P, _P, _P]),
     "kad_table_set_times": (C.c_int, [_P, _P, _P, _P]),
     "kad_table_refresh_status": (C.c_int, [_P, C.c_int64, _P]),
+    "kad_table_patch_status": (C.c_int, [_P, C.c_uint32, _P, _P]),
+    "kad_table_patch_times": (C.c_int, [_P, C.c_uint32, _P, _P, _P, _P]),
     "kad_rt_closest_batch": (C.c_int, [_P, _P, C.c_uint32, C.c_uint32, _P, _P, _P]),
     "kad_rt_closest_batch_host": (C.c_int, [_P, _P, C.c_uint32, C.c_uint32, _P, _P]),
     "kad_rt_find_bucket_batch": (C.c_int, [_P, _P, C.c_uint32, _P, _P]),

@@ -113,6 +113,19 @@ struct Target {
     uint32_t t2, t3, t4;
 };
 
+// Which lines a line builder (re)builds: every one (idx == NULL) or the *n listed ones (the compacted
+// dirty flags of an incremental status refresh). Thread j picks line b.
+struct LineSel {
+    const uint32_t* idx;
+    const uint32_t* n;
+    __device__ __forceinline__ bool pick(uint32_t j, uint32_t total, uint32_t& b) const {
+        if (!idx) { b = j; return j < total; }
+        if (j >= *n) return false;
+        b = idx[j];
+        return true;
+    }
+};
+
 __device__ __forceinline__ Target load_target(const uint8_t* targets, uint32_t i) {
     const uint32_t* p = reinterpret_cast<const uint32_t*>(targets + 20ull * i);
     Target t;
@@ -772,12 +785,58 @@ __global__ __launch_bounds__(BLOCK) void rt_wl_kernel(DevTable T, const uint8_t*
     if (ABL == 0) exact_tail(T, t, act && !ok, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
 }
 
+// The good nodes of bucket x in index order: fn(node index, key). Buckets of <= 32 nodes take their good
+// mask from dir[x].y (current whenever a line builder runs) and load the keys 8 at a time, independently,
+// so a builder thread waits for one round trip per 8 good nodes instead of two per node.
+template <class F>
+__device__ __forceinline__ void for_good(const uint64_t* key, const uint8_t* status, const uint2* dir, uint32_t x, F fn) {
+    const uint2 a = dir[x];
+    const uint32_t j0 = a.x & ~WIDE;
+    if (!(a.x & WIDE)) {
+        uint32_t m = a.y;
+        while (m) {
+            uint32_t pos[8];
+            uint64_t kk[8];
+            int c = 0;
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                pos[u] = m ? (uint32_t)__builtin_ctz(m) : 0u;
+                if (m) { m &= m - 1; c = u + 1; }
+            }
+#pragma unroll
+            for (int u = 0; u < 8; u++) kk[u] = u < c ? key[j0 + pos[u]] : 0ull;
+            for (int u = 0; u < c; u++) fn(j0 + pos[u], kk[u]);
+        }
+    } else {
+        const uint32_t j1 = dir[x + 1].x & ~WIDE;
+        for (uint32_t n = j0; n < j1; n++)
+            if (status[n] & KAD_STATUS_GOOD) fn(n, key[n]);
+    }
+}
+
+// The good-node count of bucket x (popcount of its mask; gpre for wide buckets).
+__device__ __forceinline__ uint32_t good_of(const uint2* dir, const uint32_t* gpre, uint32_t x) {
+    const uint2 a = dir[x];
+    return (a.x & WIDE) ? gpre[x + 1] - gpre[x] : (uint32_t)__popc(a.y);
+}
+
+// A line assembled in the thread's LDS row (odd stride: conflict-free), then stored as 16-byte pieces.
+template <int W>
+__device__ __forceinline__ void store_line(const uint32_t* L, uint32_t* dst) {
+#pragma unroll
+    for (int k = 0; k < W; k += 4)
+        *reinterpret_cast<uint4*>(dst + k) = make_uint4(L[k], L[k + 1], L[k + 2], L[k + 3]);
+}
+
 // Window lines after a status change (or at table creation): one thread per bucket (d = depth).
-__global__ void wl_build_kernel(const uint64_t* key, const uint8_t* status, const uint2* dir, const uint32_t* gpre,
-                                uint32_t B, uint32_t d, uint64_t pre0, uint32_t* lines) {
-    const uint32_t b = blockIdx.x * BLOCK + threadIdx.x;
-    if (b >= B) return;
-    uint32_t* L = lines + 32ull * b;
+// sel: every bucket's line, or only the listed ones (incremental status refresh).
+__global__ __launch_bounds__(BLOCK) void wl_build_kernel(const uint64_t* key, const uint8_t* status, const uint2* dir,
+                                                          const uint32_t* gpre, uint32_t B, uint32_t d, uint64_t pre0,
+                                                          uint32_t* lines, LineSel sel) {
+    __shared__ uint32_t lds[BLOCK][33];
+    uint32_t b;
+    if (!sel.pick(blockIdx.x * BLOCK + threadIdx.x, B, b)) return;
+    uint32_t* L = lds[threadIdx.x];
     for (int k = 0; k < 32; k++) L[k] = NONE;
     // R_8 and the per-round good counts (routing_table.cpp:89-104 closed form)
     uint32_t h = 0, R8 = 3;
@@ -788,7 +847,11 @@ __global__ void wl_build_kernel(const uint64_t* key, const uint8_t* status, cons
         h |= (min(g, 63u) << (6 * r)) | ((whole ? 1u : 0u) << (18 + r));
         if (R8 == 3 && (g >= 8 || whole)) R8 = r;
     }
-    if (R8 == 3) { L[1] = WL_DEFER; return; }
+    if (R8 == 3) {
+        L[1] = WL_DEFER;
+        store_line<32>(L, lines + 32ull * b);
+        return;
+    }
     const uint32_t lo = b > R8 ? b - 1 - R8 : 0u, hi = min(B - 1, b + R8), nb = hi - lo + 1;
     const uint32_t base = dir[lo].x & ~WIDE;
     uint32_t rounds = 0, S = 0;
@@ -801,22 +864,21 @@ __global__ void wl_build_kernel(const uint64_t* key, const uint8_t* status, cons
             if (rk == j) x = y;
         }
         rounds |= (x >= b ? x - b : b - 1 - x) << (2 * j);
-        const uint32_t j0 = dir[x].x & ~WIDE, j1 = dir[x + 1].x & ~WIDE;
-        const uint32_t g = gpre[x + 1] - gpre[x];
+        const uint32_t g = good_of(dir, gpre, x);
         if (full || S + g > WL_SLOTS) { full = true; continue; }  // whole buckets only
         const uint32_t s0 = S;
-        for (uint32_t n = j0; n < j1; n++) {
-            if (!(status[n] & KAD_STATUS_GOOD)) continue;
-            const uint32_t k21 = (uint32_t)((key[n] << d) >> (64 - WL_KBITS)), off = n - base;
+        for_good(key, status, dir, x, [&](uint32_t n, uint64_t kn) {
+            const uint32_t k21 = (uint32_t)((kn << d) >> (64 - WL_KBITS)), off = n - base;
             defer |= off > 255u;
             for (uint32_t s = s0; s < S; s++) defer |= ((L[WL_SLOT0 + s] >> 8) & ((1u << WL_KBITS) - 1)) == k21;
             L[WL_SLOT0 + S] = (j << 29) | (k21 << 8) | (off & 255u);
             S++;
-        }
+        });
     }
     L[0] = base;
     L[1] = h | (R8 << 21) | (S << 23) | (defer ? WL_DEFER : 0u);
     L[2] = rounds;
+    store_line<32>(L, lines + 32ull * b);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -995,12 +1057,14 @@ __global__ __launch_bounds__(BLOCK) void rt_wl16_kernel(DevTable T, const uint8_
 }
 
 // Window lines for counts 9..16 after a status change (or at creation): one thread per bucket.
-__global__ void wl16_build_kernel(const uint64_t* key, const uint8_t* status, const uint2* dir, const uint32_t* gpre,
-                                  uint32_t B, uint32_t d, uint64_t pre0, uint32_t* lines) {
-    const uint32_t b = blockIdx.x * BLOCK + threadIdx.x;
-    if (b >= B) return;
-    uint32_t* L = lines + (size_t)WL16_STRIDE * b;
-    for (uint32_t k = 0; k < WL16_HDR + WL16_SLOTS; k++) L[k] = NONE;
+__global__ __launch_bounds__(BLOCK) void wl16_build_kernel(const uint64_t* key, const uint8_t* status, const uint2* dir,
+                                                            const uint32_t* gpre, uint32_t B, uint32_t d, uint64_t pre0,
+                                                            uint32_t* lines, LineSel sel) {
+    __shared__ uint32_t lds[BLOCK][33];
+    uint32_t b;
+    if (!sel.pick(blockIdx.x * BLOCK + threadIdx.x, B, b)) return;
+    uint32_t* L = lds[threadIdx.x];
+    for (uint32_t k = 0; k < WL16_STRIDE; k++) L[k] = NONE;
     uint32_t h = 0, R = 4;
     for (uint32_t r = 0; r < 4; r++) {
         const uint32_t lo = b > r ? b - 1 - r : 0u, hi = min(B - 1, b + r);
@@ -1009,10 +1073,14 @@ __global__ void wl16_build_kernel(const uint64_t* key, const uint8_t* status, co
         h |= (min(g, 31u) << (5 * r)) | ((whole ? 1u : 0u) << (20 + r));
         if (R == 4 && (g >= 16 || whole)) R = r;
     }
-    if (R == 4) { L[1] = WL_DEFER; return; }
+    if (R == 4) {
+        L[1] = WL_DEFER;
+        store_line<32>(L, lines + (size_t)WL16_STRIDE * b);
+        return;
+    }
     const uint32_t lo = b > R ? b - 1 - R : 0u, hi = min(B - 1, b + R), nb = hi - lo + 1;
     const uint32_t base = dir[lo].x & ~WIDE;
-    uint32_t rounds = 0, S = 0, st = 0, xj[8];
+    uint32_t rounds = 0, S = 0, st = 0, xj[8], gj[8];
     bool defer = false;
     for (uint32_t j = 0; j < nb; j++) {  // the bucket of D rank j and its round
         uint32_t x = lo;
@@ -1022,29 +1090,27 @@ __global__ void wl16_build_kernel(const uint64_t* key, const uint8_t* status, co
             if (rk == j) x = y;
         }
         xj[j] = x;
+        gj[j] = good_of(dir, gpre, x);
         rounds |= (x >= b ? x - b : b - 1 - x) << (2 * j);
     }
     // Whole buckets, in three passes: (1) the D-rank prefix of W(R_16) up to its 16th good node (every count
     // with R_c = R_16); (2) the rest of W(R_16 - 1), which holds < 16 good nodes (every count with R_c < R_16);
     // (3) whatever else fits, in D order.
     auto put = [&](uint32_t j) {
-        const uint32_t x = xj[j], j0 = dir[x].x & ~WIDE, j1 = dir[x + 1].x & ~WIDE;
-        const uint32_t g = gpre[x + 1] - gpre[x];
-        if (((st >> j) & 1u) || S + g > WL16_SLOTS) return;
+        if (((st >> j) & 1u) || S + gj[j] > WL16_SLOTS) return;
         st |= 1u << j;
         const uint32_t s0 = S;
-        for (uint32_t n = j0; n < j1; n++) {
-            if (!(status[n] & KAD_STATUS_GOOD)) continue;
-            const uint32_t k21 = (uint32_t)((key[n] << d) >> (64 - WL_KBITS)), off = n - base;
+        for_good(key, status, dir, xj[j], [&](uint32_t n, uint64_t kn) {
+            const uint32_t k21 = (uint32_t)((kn << d) >> (64 - WL_KBITS)), off = n - base;
             defer |= off > 255u;
             for (uint32_t s = s0; s < S; s++) defer |= ((L[WL16_HDR + s] >> 8) & ((1u << WL_KBITS) - 1)) == k21;
             L[WL16_HDR + S] = (j << 29) | (k21 << 8) | (off & 255u);
             S++;
-        }
+        });
     };
     for (uint32_t j = 0, cum = 0; j < nb && cum < WL16_P1; j++) {
         put(j);
-        cum += gpre[xj[j] + 1] - gpre[xj[j]];
+        cum += gj[j];
     }
     for (uint32_t j = 0; j < nb; j++)
         if (((rounds >> (2 * j)) & 3u) < R) put(j);
@@ -1052,6 +1118,7 @@ __global__ void wl16_build_kernel(const uint64_t* key, const uint8_t* status, co
     L[0] = base;
     L[1] = h | (R << 24) | (S << 26) | (defer ? WL_DEFER : 0u);
     L[2] = rounds | (st << 16) | (nb << 24);
+    store_line<32>(L, lines + (size_t)WL16_STRIDE * b);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1196,12 +1263,14 @@ __global__ __launch_bounds__(BLOCK) void rt_wl32_kernel(DevTable T, const uint8_
 
 // Window lines for counts 17..32 after a status change (or at creation): one thread per bucket.
 // The window's buckets are put in D order by rank (O(buckets^2), at most 16 buckets).
-__global__ void wl32_build_kernel(const uint64_t* key, const uint8_t* status, const uint2* dir, const uint32_t* gpre,
-                                  uint32_t B, uint32_t d, uint64_t pre0, uint32_t* lines) {
-    const uint32_t b = blockIdx.x * BLOCK + threadIdx.x;
-    if (b >= B) return;
-    uint32_t* L = lines + (size_t)WL32_STRIDE * b;
-    for (uint32_t k = 0; k < WL32_HDR + WL32_SLOTS; k++) L[k] = NONE;
+__global__ __launch_bounds__(BLOCK) void wl32_build_kernel(const uint64_t* key, const uint8_t* status, const uint2* dir,
+                                                            const uint32_t* gpre, uint32_t B, uint32_t d, uint64_t pre0,
+                                                            uint32_t* lines, LineSel sel) {
+    __shared__ uint32_t lds[BLOCK][WL32_STRIDE + 1];
+    uint32_t b;
+    if (!sel.pick(blockIdx.x * BLOCK + threadIdx.x, B, b)) return;
+    uint32_t* L = lds[threadIdx.x];
+    for (uint32_t k = 0; k < WL32_STRIDE; k++) L[k] = NONE;
     uint32_t g01 = 0, g23 = 0, whole = 0, R = 8;
     for (uint32_t r = 0; r < 8; r++) {
         const uint32_t lo = b > r ? b - 1 - r : 0u, hi = min(B - 1, b + r);
@@ -1211,7 +1280,11 @@ __global__ void wl32_build_kernel(const uint64_t* key, const uint8_t* status, co
         whole |= (w ? 1u : 0u) << r;
         if (R == 8 && (g >= 32 || w)) R = r;
     }
-    if (R == 8) { L[3] = WL_DEFER; return; }
+    if (R == 8) {
+        L[3] = WL_DEFER;
+        store_line<WL32_STRIDE>(L, lines + (size_t)WL32_STRIDE * b);
+        return;
+    }
     const uint32_t lo = b > R ? b - 1 - R : 0u, hi = min(B - 1, b + R), nb = hi - lo + 1;
     uint32_t ord[16];
     for (uint32_t y = lo; y <= hi; y++) {
@@ -1226,19 +1299,17 @@ __global__ void wl32_build_kernel(const uint64_t* key, const uint8_t* status, co
         const uint32_t x = ord[j];
         const uint32_t rd = x >= b ? x - b : b - 1 - x;
         if (j < 10) r04 |= rd << (3 * j); else r15 |= rd << (3 * (j - 10));
-        const uint32_t j0 = dir[x].x & ~WIDE, j1 = dir[x + 1].x & ~WIDE;
-        const uint32_t g = gpre[x + 1] - gpre[x];
+        const uint32_t g = good_of(dir, gpre, x);
         if (full || S + g > WL32_SLOTS) { full = true; continue; }  // whole buckets only
         const uint32_t s0 = S;
-        for (uint32_t n = j0; n < j1; n++) {
-            if (!(status[n] & KAD_STATUS_GOOD)) continue;
-            const uint32_t k20 = (uint32_t)((key[n] << d) >> (64 - WL32_KBITS)), off = n - base;
+        for_good(key, status, dir, x, [&](uint32_t n, uint64_t kn) {
+            const uint32_t k20 = (uint32_t)((kn << d) >> (64 - WL32_KBITS)), off = n - base;
             defer |= off > 255u;
             for (uint32_t s = s0; s < S; s++)
                 defer |= ((L[WL32_HDR + s] >> 8) & ((1u << WL32_KBITS) - 1)) == k20;
             L[WL32_HDR + S] = (j << 28) | (k20 << 8) | (off & 255u);
             S++;
-        }
+        });
     }
     L[0] = base;
     L[1] = g01;
@@ -1246,6 +1317,7 @@ __global__ void wl32_build_kernel(const uint64_t* key, const uint8_t* status, co
     L[3] = whole | (R << 8) | (S << 12) | (defer ? WL_DEFER : 0u);
     L[4] = r04;
     L[5] = r15;
+    store_line<WL32_STRIDE>(L, lines + (size_t)WL32_STRIDE * b);
 }
 
 template <int K>
@@ -2343,9 +2415,9 @@ __global__ __launch_bounds__(BLOCK) void nc_line_kernel(DevTable T, const uint8_
 
 // NodeCache lines after a status change (or at creation): one thread per radix slot.
 __global__ void ncl_build_kernel(const uint64_t* key, const uint8_t* status, const uint32_t* nrdx, uint32_t nslots,
-                                 uint32_t n, uint32_t slot_prefix, uint32_t* lines) {
-    const uint32_t s = blockIdx.x * BLOCK + threadIdx.x;
-    if (s >= nslots) return;
+                                 uint32_t n, uint32_t slot_prefix, uint32_t* lines, LineSel sel) {
+    uint32_t s;
+    if (!sel.pick(blockIdx.x * BLOCK + threadIdx.x, nslots, s)) return;
     uint32_t* L = lines + (size_t)NCL_STRIDE * s;
     const uint32_t r0 = nrdx[s], r1 = nrdx[s + 1], ns = r1 - r0;
     if (r0 < NCL_LEFT || (uint64_t)r0 - NCL_LEFT + NCL_SLOTS > n || ns > NCL_XMAX) {  // clamped window / wide slot
@@ -2482,15 +2554,105 @@ __global__ void lowbit_kernel(const uint8_t* a, uint32_t n, uint32_t* out) {
 // ---------------------------------------------------------------------------------------
 // Table maintenance: status from times, per-bucket good counts, exclusive scan -> dir.y
 // ---------------------------------------------------------------------------------------
+// Where a status change must be re-derived (incremental refresh): bdirty[b] = bucket b's good set changed
+// (its mask, count and every line whose window reaches it), ndirty[s] = a NodeCache line whose 60-node
+// window holds a node whose expired bit changed. Any of the pointers may be NULL (no such structure).
+struct StatusMarks {
+    uint8_t* bdirty;     // B
+    uint8_t* ndirty;     // NodeCache radix slots
+    const uint2* dir;    // bucket starts (node -> bucket)
+    uint32_t B;
+    const uint64_t* key; // node -> NodeCache slot
+    uint64_t nbase;
+    uint32_t nshift, nslots, n;
+};
+
+__device__ __forceinline__ void mark_status_change(const StatusMarks& M, uint32_t i, uint32_t old_st, uint32_t st) {
+    if (M.bdirty && ((old_st ^ st) & KAD_STATUS_GOOD)) {
+        uint32_t lo = 0, hi = M.B;  // the last bucket whose first node is <= i (upper_bound - 1)
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if ((M.dir[mid].x & ~WIDE) <= i) lo = mid + 1; else hi = mid;
+        }
+        if (lo) M.bdirty[lo - 1] = 1;
+    }
+    if (M.ndirty && ((old_st ^ st) & KAD_STATUS_EXPIRED)) {
+        // NodeCache line s holds nodes r0(s)-28 .. r0(s)+31: every slot from that of node i-32 to that of
+        // node i+28 (a superset of the slots whose window holds i)
+        const uint32_t a = i >= 32 ? i - 32 : 0u, e = min(M.n - 1, i + 28);
+        const uint64_t ka = M.key[a], ke = M.key[e];
+        const uint64_t sa = ka < M.nbase ? 0 : min<uint64_t>((ka - M.nbase) >> M.nshift, M.nslots - 1);
+        const uint64_t se = ke < M.nbase ? 0 : min<uint64_t>((ke - M.nbase) >> M.nshift, M.nslots - 1);
+        for (uint64_t x = sa; x <= se; x++) M.ndirty[x] = 1;
+    }
+}
+
 __global__ void status_from_times_kernel(const int64_t* time_ns, const int64_t* reply_ns, const uint8_t* expired,
-                                         uint32_t n, int64_t now, uint8_t* status) {
+                                         uint32_t n, int64_t now, uint8_t* status, StatusMarks M) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (i >= n) return;
     // node.cpp:34-40 with NODE_GOOD_TIME = 120 min, NODE_EXPIRE_TIME = 10 min (node.h:91-94)
     const int64_t GOOD = 120LL * 60 * 1000000000LL, EXP = 10LL * 60 * 1000000000LL;
     const bool ex = expired[i] != 0;
     const bool good = !ex && reply_ns[i] >= now - GOOD && time_ns[i] >= now - EXP;
-    status[i] = (uint8_t)((good ? KAD_STATUS_GOOD : 0u) | (ex ? KAD_STATUS_EXPIRED : 0u));
+    const uint32_t st = (good ? KAD_STATUS_GOOD : 0u) | (ex ? KAD_STATUS_EXPIRED : 0u);
+    const uint32_t old = status[i];
+    if (old != st) {
+        status[i] = (uint8_t)st;
+        mark_status_change(M, i, old, st);
+    }
+}
+
+// New status bytes: all n nodes (nodes == NULL) or the m listed ones; only changes are written and marked.
+__global__ void status_patch_kernel(const uint32_t* nodes, const uint8_t* vals, uint32_t m, uint8_t* status,
+                                    StatusMarks M) {
+    const uint32_t j = blockIdx.x * BLOCK + threadIdx.x;
+    if (j >= m) return;
+    const uint32_t i = nodes ? nodes[j] : j;
+    if (i >= M.n) return;
+    const uint32_t st = vals[j] & (KAD_STATUS_GOOD | KAD_STATUS_EXPIRED), old = status[i];
+    if (old != st) {
+        status[i] = (uint8_t)st;
+        mark_status_change(M, i, old, st);
+    }
+}
+
+// Node times of the m listed nodes (Node::received / setExpired on the host side).
+__global__ void times_patch_kernel(const uint32_t* nodes, const int64_t* t, const int64_t* rt, const uint8_t* ex,
+                                   uint32_t m, uint32_t n, int64_t* time_ns, int64_t* reply_ns, uint8_t* expired) {
+    const uint32_t j = blockIdx.x * BLOCK + threadIdx.x;
+    if (j >= m || nodes[j] >= n) return;
+    time_ns[nodes[j]] = t[j];
+    reply_ns[nodes[j]] = rt[j];
+    expired[nodes[j]] = ex[j];
+}
+
+// Incremental form of bucket_good_kernel: only flagged buckets get a new mask and count (cnt keeps every
+// other bucket's count from the last rebuild); each flags the lines whose window can reach it and is
+// cleared. A line of bucket c reads buckets [c-3, c+2] (count <= 8: W(r <= 2)), [c-4, c+3] (9..16:
+// W(r <= 3)) or [c-8, c+7] (17..32: W(r <= 7)), so bucket b dirties lines [b-2, b+3], [b-3, b+4], [b-7, b+8].
+__global__ void bucket_good_dirty_kernel(const uint8_t* status, uint2* dir, uint32_t B, uint32_t* cnt,
+                                         uint8_t* bdirty, uint8_t* ld8, uint8_t* ld16, uint8_t* ld32) {
+    const uint32_t b = blockIdx.x * BLOCK + threadIdx.x;
+    if (b >= B || !bdirty[b]) return;
+    bdirty[b] = 0;
+    const uint32_t j0 = dir[b].x & ~WIDE, j1 = dir[b + 1].x & ~WIDE;
+    uint32_t g = 0, mask = 0;
+    for (uint32_t j = j0; j < j1; j++) {
+        const uint32_t gb = status[j] & KAD_STATUS_GOOD;
+        g += gb;
+        if (j - j0 < 32) mask |= gb << (j - j0);
+    }
+    cnt[b] = g;
+    dir[b].y = (j1 - j0 <= 32) ? mask : 0u;
+    auto flag = [&](uint8_t* f, uint32_t below, uint32_t above) {
+        if (!f) return;
+        const uint32_t c0 = b >= below ? b - below : 0u, c1 = min(B - 1, b + above);
+        for (uint32_t c = c0; c <= c1; c++) f[c] = 1;
+    };
+    flag(ld8, 2, 3);
+    flag(ld16, 3, 4);
+    flag(ld32, 7, 8);
 }
 
 // Per bucket: good count (for the prefix sums) and the good bitmask of its nodes (dir[b].y).
@@ -2528,6 +2690,32 @@ __device__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* lds, uint32_t& to
     total = lds[0] + lds[1] + lds[2] + lds[3];
     __syncthreads();
     return base + x - v;
+}
+
+// Flags -> a compact list of their indices, flags cleared. Each thread takes 16 flags (one 16-byte load;
+// flag arrays are padded to 16 bytes), the block scans the counts in LDS and claims its range with ONE
+// atomic (a single counter hit by every wave saturates at ~90 adds per microsecond).
+__global__ __launch_bounds__(BLOCK) void compact_flags_kernel(uint8_t* flags, uint32_t m, uint32_t* list, uint32_t* ctr) {
+    __shared__ uint32_t lds[4];
+    __shared__ uint32_t base_s;
+    const uint32_t g = blockIdx.x * BLOCK + threadIdx.x, i0 = 16 * g;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (i0 < m) v = reinterpret_cast<const uint4*>(flags)[g];
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    uint32_t c = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) c += __popc(w[k] & 0x01010101u);  // flags are 0 or 1
+    uint32_t total;
+    const uint32_t ex = block_exclusive_scan(c, lds, total);
+    if (total == 0) return;  // block-uniform
+    if (threadIdx.x == 0) base_s = atomicAdd(ctr, total);
+    __syncthreads();
+    if (!c) return;
+    uint32_t o = base_s + ex;
+#pragma unroll
+    for (int k = 0; k < 16; k++)
+        if ((w[k >> 2] >> (8 * (k & 3))) & 1u) list[o++] = i0 + k;
+    reinterpret_cast<uint4*>(flags)[g] = make_uint4(0, 0, 0, 0);
 }
 
 // Tile-local exclusive scan of cnt[0..m) written to out; tile sums to sums[tile].
@@ -2681,11 +2869,23 @@ struct kad_table {
     int64_t* time_ns = nullptr;
     int64_t* reply_ns = nullptr;
     uint8_t* expired = nullptr;
-    uint32_t* scan_cnt = nullptr;   // B+1
+    uint32_t* scan_cnt = nullptr;   // B+1 (after every rebuild: the per-bucket good counts)
     uint32_t* scan_part = nullptr;  // B+1
     uint32_t* scan_sums = nullptr;  // tiles
+    // incremental status refresh (allocated on first use, see StatusMarks)
+    uint8_t* bdirty = nullptr;      // B
+    uint8_t* ld8 = nullptr;         // B each, per line set present: lines to rebuild
+    uint8_t* ld16 = nullptr;
+    uint8_t* ld32 = nullptr;
+    uint8_t* ndirty = nullptr;      // NodeCache radix slots (only with NodeCache lines)
+    uint32_t* dlist = nullptr;      // compacted dirty lists: 3 x B line indices + NodeCache slots
+    uint32_t* dctr = nullptr;       // 4 list lengths
+    void* stage = nullptr;          // host -> device staging of patch lists
+    size_t stage_bytes = 0;
     ~kad_table() {
         for (void* p : owned) (void)hipFree(p);
+        for (void* p : {(void*)bdirty, (void*)ld8, (void*)ld16, (void*)ld32, (void*)ndirty, (void*)dlist, (void*)dctr, stage})
+            if (p) (void)hipFree(p);
     }
 };
 
@@ -2697,29 +2897,114 @@ bool is_gfx950(int dev) {
     return std::strncmp(prop.gcnArchName, "gfx950", 6) == 0;
 }
 
-// Rebuild dir[].y (good prefix sums) from the device status array. Async on stream.
-int rebuild_good_prefix(kad_table* t, hipStream_t s) {
+// Re-derive what depends on the status bytes: good masks, per-bucket good counts, the good prefix sums,
+// the window lines and the NodeCache lines. full: every bucket and line; otherwise only what the
+// StatusMarks of the last status change flagged (kad_table_refresh_status / update / patch; ensure_marks
+// must have run). Async on stream.
+int rebuild_good_prefix(kad_table* t, hipStream_t s, bool full = true) {
     const uint32_t B = t->d.B;
-    if (t->ncl_mut)  // NodeCache lines carry the expired bits
+    uint32_t* ctr = t->dctr;
+    if (!full) HIP_TRY(hipMemsetAsync(ctr, 0, 4 * sizeof(uint32_t), s));
+    if (t->ncl_mut) {  // NodeCache lines carry the expired bits
+        LineSel sel{};
+        if (!full) {
+            uint32_t* lst = t->dlist + 3ull * B;
+            hipLaunchKernelGGL(compact_flags_kernel, dim3(grid_for((t->d.nslots + 15) / 16)), dim3(BLOCK), 0, s,
+                               t->ndirty, t->d.nslots, lst, ctr + 3);
+            sel = LineSel{lst, ctr + 3};
+        }
         hipLaunchKernelGGL(ncl_build_kernel, dim3(grid_for(t->d.nslots)), dim3(BLOCK), 0, s, t->d.key, t->d.status,
-                           t->d.nrdx, t->d.nslots, t->d.n, 64 - t->d.nshift, t->ncl_mut);
+                           t->d.nrdx, t->d.nslots, t->d.n, 64 - t->d.nshift, t->ncl_mut, sel);
+    }
     if (B == 0) return KAD_OK;
     const uint32_t m = B + 1;
     const uint32_t tiles = (m + SCAN_TILE - 1) / SCAN_TILE;
-    hipLaunchKernelGGL(bucket_good_kernel, dim3(grid_for(m)), dim3(BLOCK), 0, s, t->d.status, t->dir_mut, B, t->scan_cnt);
+    if (full)
+        hipLaunchKernelGGL(bucket_good_kernel, dim3(grid_for(m)), dim3(BLOCK), 0, s, t->d.status, t->dir_mut, B,
+                           t->scan_cnt);
+    else
+        hipLaunchKernelGGL(bucket_good_dirty_kernel, dim3(grid_for(B)), dim3(BLOCK), 0, s, t->d.status, t->dir_mut, B,
+                           t->scan_cnt, t->bdirty, t->wl_mut ? t->ld8 : nullptr, t->wl16_mut ? t->ld16 : nullptr,
+                           t->wl32_mut ? t->ld32 : nullptr);
     hipLaunchKernelGGL(scan_tiles_kernel, dim3(tiles), dim3(BLOCK), 0, s, t->scan_cnt, m, t->scan_part, t->scan_sums);
     hipLaunchKernelGGL(scan_sums_kernel, dim3(1), dim3(BLOCK), 0, s, t->scan_sums, tiles);
     hipLaunchKernelGGL(scan_apply_kernel, dim3(grid_for(m)), dim3(BLOCK), 0, s, t->scan_part, t->scan_sums, m, t->gpre_mut);
+    // the lines of every bucket (full) or only the compacted dirty ones
+    auto sel_for = [&](uint8_t* flags, uint32_t k) -> LineSel {
+        if (full) return LineSel{};
+        hipLaunchKernelGGL(compact_flags_kernel, dim3(grid_for((B + 15) / 16)), dim3(BLOCK), 0, s, flags, B,
+                           t->dlist + (size_t)k * B, ctr + k);
+        return LineSel{t->dlist + (size_t)k * B, ctr + k};
+    };
     if (t->wl_mut)
         hipLaunchKernelGGL(wl_build_kernel, dim3(grid_for(B)), dim3(BLOCK), 0, s, t->d.key, t->d.status, t->d.dir,
-                           t->d.gpre, B, 64 - t->d.rshift, t->d.rbase >> t->d.rshift, t->wl_mut);
+                           t->d.gpre, B, 64 - t->d.rshift, t->d.rbase >> t->d.rshift, t->wl_mut, sel_for(t->ld8, 0));
     if (t->wl16_mut)
         hipLaunchKernelGGL(wl16_build_kernel, dim3(grid_for(B)), dim3(BLOCK), 0, s, t->d.key, t->d.status, t->d.dir,
-                           t->d.gpre, B, 64 - t->d.rshift, t->d.rbase >> t->d.rshift, t->wl16_mut);
+                           t->d.gpre, B, 64 - t->d.rshift, t->d.rbase >> t->d.rshift, t->wl16_mut, sel_for(t->ld16, 1));
     if (t->wl32_mut)
         hipLaunchKernelGGL(wl32_build_kernel, dim3(grid_for(B)), dim3(BLOCK), 0, s, t->d.key, t->d.status, t->d.dir,
-                           t->d.gpre, B, 64 - t->d.rshift, t->d.rbase >> t->d.rshift, t->wl32_mut);
+                           t->d.gpre, B, 64 - t->d.rshift, t->d.rbase >> t->d.rshift, t->wl32_mut, sel_for(t->ld32, 2));
     HIP_TRY(hipGetLastError());
+    return KAD_OK;
+}
+
+// Allocate (zeroed) the incremental-refresh flags for the table's current shape.
+int ensure_marks(kad_table* t) {
+    auto alloc = [](uint8_t** p, size_t n) -> int {
+        if (*p || n == 0) return KAD_OK;
+        n = (n + 15) & ~(size_t)15;  // compact_flags_kernel reads 16 flags at a time
+        void* q = nullptr;
+        hipError_t e = hipMalloc(&q, n);
+        if (e != hipSuccess) return set_err(KAD_ERR_NOMEM, "hipMalloc(%zu) failed: %s", n, hipGetErrorString(e));
+        e = hipMemset(q, 0, n);
+        if (e != hipSuccess) { (void)hipFree(q); return set_err(KAD_ERR_HIP, "hipMemset failed: %s", hipGetErrorString(e)); }
+        *p = static_cast<uint8_t*>(q);
+        return KAD_OK;
+    };
+    int rc;
+    if ((rc = alloc(&t->bdirty, t->d.B))) return rc;
+    if (t->wl_mut && (rc = alloc(&t->ld8, t->d.B))) return rc;
+    if (t->wl16_mut && (rc = alloc(&t->ld16, t->d.B))) return rc;
+    if (t->wl32_mut && (rc = alloc(&t->ld32, t->d.B))) return rc;
+    if (t->ncl_mut && (rc = alloc(&t->ndirty, t->d.nslots))) return rc;
+    uint8_t *l = reinterpret_cast<uint8_t*>(t->dlist), *c = reinterpret_cast<uint8_t*>(t->dctr);
+    if ((rc = alloc(&l, 4 * (3ull * t->d.B + (t->ncl_mut ? t->d.nslots : 0u) + 1)))) return rc;
+    if ((rc = alloc(&c, 4 * sizeof(uint32_t)))) return rc;
+    t->dlist = reinterpret_cast<uint32_t*>(l);
+    t->dctr = reinterpret_cast<uint32_t*>(c);
+    return KAD_OK;
+}
+
+// Drop the incremental-refresh flags (the table's shape changed: kad_table_apply).
+void drop_marks(kad_table* t) {
+    for (uint8_t** p : {&t->bdirty, &t->ld8, &t->ld16, &t->ld32, &t->ndirty})
+        if (*p) { (void)hipFree(*p); *p = nullptr; }
+    if (t->dlist) { (void)hipFree(t->dlist); t->dlist = nullptr; }
+    if (t->dctr) { (void)hipFree(t->dctr); t->dctr = nullptr; }
+}
+
+StatusMarks marks_of(const kad_table* t) {
+    StatusMarks M{};
+    M.bdirty = t->d.B ? t->bdirty : nullptr;
+    M.ndirty = t->ncl_mut ? t->ndirty : nullptr;
+    M.dir = t->d.dir;
+    M.B = t->d.B;
+    M.key = t->d.key;
+    M.nbase = t->d.nbase;
+    M.nshift = t->d.nshift;
+    M.nslots = t->d.nslots;
+    M.n = t->d.n;
+    return M;
+}
+
+// Device staging buffer of at least `bytes` (host patch lists).
+int stage_reserve(kad_table* t, size_t bytes) {
+    if (t->stage_bytes >= bytes) return KAD_OK;
+    if (t->stage) { (void)hipFree(t->stage); t->stage = nullptr; t->stage_bytes = 0; }
+    hipError_t e = hipMalloc(&t->stage, std::max<size_t>(bytes, 4096));
+    if (e != hipSuccess) { t->stage = nullptr; return set_err(KAD_ERR_NOMEM, "hipMalloc(%zu) failed", bytes); }
+    t->stage_bytes = std::max<size_t>(bytes, 4096);
     return KAD_OK;
 }
 
@@ -2911,6 +3196,9 @@ int kad_table_create(kad_table** out, int device, uint32_t n_nodes, const uint8_
                 // a wide bucket's dup nodes are handled by the slow path (wide -> deferred)
             }
         }
+        // per-bucket good counts: the scan input, kept current by every rebuild (incremental refresh)
+        std::vector<uint32_t> cnt(n_buckets + 1, 0);
+        for (uint32_t b = 0; b < n_buckets; b++) cnt[b] = gpre[b + 1] - gpre[b];
         std::vector<uint64_t> fkey(n_buckets);
         std::vector<uint32_t> ftail(3ull * n_buckets);
         for (uint32_t b = 0; b < n_buckets; b++) {
@@ -2952,7 +3240,7 @@ int kad_table_create(kad_table** out, int device, uint32_t n_nodes, const uint8_
             (rc = dev_upload(&dfk, fkey.data(), n_buckets, t->owned, t->bytes)) ||
             (rc = dev_upload(&dft, ftail.data(), 3ull * n_buckets, t->owned, t->bytes)) ||
             (rc = dev_upload(&drdx, rdx.data(), rdx.size(), t->owned, t->bytes)) ||
-            (rc = dev_upload(&t->scan_cnt, nullptr, n_buckets + 1, t->owned, t->bytes)) ||
+            (rc = dev_upload(&t->scan_cnt, cnt.data(), n_buckets + 1, t->owned, t->bytes)) ||
             (rc = dev_upload(&t->scan_part, nullptr, n_buckets + 1, t->owned, t->bytes)) ||
             (rc = dev_upload(&t->scan_sums, nullptr, (n_buckets + 1 + SCAN_TILE - 1) / SCAN_TILE, t->owned, t->bytes))) {
             delete t;
@@ -2975,7 +3263,7 @@ int kad_table_create(kad_table** out, int device, uint32_t n_nodes, const uint8_
                     return rc;
                 }
                 hipLaunchKernelGGL(wl_build_kernel, dim3(grid_for(n_buckets)), dim3(BLOCK), 0, 0, d.key, d.status, d.dir,
-                                   d.gpre, n_buckets, depth, pre0, lp);
+                                   d.gpre, n_buckets, depth, pre0, lp, LineSel{});
                 if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
                     delete t;
                     return set_err(KAD_ERR_HIP, "window-line build failed");
@@ -2989,7 +3277,7 @@ int kad_table_create(kad_table** out, int device, uint32_t n_nodes, const uint8_
                     return rc;
                 }
                 hipLaunchKernelGGL(wl16_build_kernel, dim3(grid_for(n_buckets)), dim3(BLOCK), 0, 0, d.key, d.status, d.dir,
-                                   d.gpre, n_buckets, depth, pre0, lp16);
+                                   d.gpre, n_buckets, depth, pre0, lp16, LineSel{});
                 if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
                     delete t;
                     return set_err(KAD_ERR_HIP, "window-line (16) build failed");
@@ -3004,7 +3292,7 @@ int kad_table_create(kad_table** out, int device, uint32_t n_nodes, const uint8_
                         return rc;
                     }
                     hipLaunchKernelGGL(wl32_build_kernel, dim3(grid_for(n_buckets)), dim3(BLOCK), 0, 0, d.key, d.status,
-                                       d.dir, d.gpre, n_buckets, depth, pre0, lp32);
+                                       d.dir, d.gpre, n_buckets, depth, pre0, lp32, LineSel{});
                     if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
                         delete t;
                         return set_err(KAD_ERR_HIP, "window-line (32) build failed");
@@ -3028,7 +3316,7 @@ int kad_table_create(kad_table** out, int device, uint32_t n_nodes, const uint8_
         uint32_t* lp;
         if ((rc = dev_upload(&lp, nullptr, (size_t)NCL_STRIDE * r.slots, t->owned, t->bytes))) { delete t; return rc; }
         hipLaunchKernelGGL(ncl_build_kernel, dim3(grid_for(r.slots)), dim3(BLOCK), 0, 0, d.key, d.status, dn, r.slots,
-                           n_nodes, 64 - r.shift, lp);
+                           n_nodes, 64 - r.shift, lp, LineSel{});
         if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
             delete t;
             return set_err(KAD_ERR_HIP, "NodeCache line build failed");
@@ -3071,10 +3359,54 @@ int kad_table_get_info(const kad_table* t, kad_table_info* out) {
 
 int kad_table_update_status(kad_table* t, const uint8_t* status) {
     if (!t || (!status && t->d.n)) return set_err(KAD_ERR_INVALID, "NULL argument");
+    return kad_table_patch_status(t, t->d.n, nullptr, status);
+}
+
+int kad_table_patch_status(kad_table* t, uint32_t m, const uint32_t* nodes, const uint8_t* status) {
+    if (!t || (m && !status)) return set_err(KAD_ERR_INVALID, "NULL argument");
+    if (!nodes && m != t->d.n) return set_err(KAD_ERR_INVALID, "nodes NULL needs m = n_nodes");
+    if (nodes)
+        for (uint32_t j = 0; j < m; j++)
+            if (nodes[j] >= t->d.n) return set_err(KAD_ERR_INVALID, "node %u out of range (n=%u)", nodes[j], t->d.n);
     DeviceGuard g(t->device);
-    if (t->d.n) HIP_TRY(hipMemcpy(t->status_mut, status, t->d.n, hipMemcpyHostToDevice));
-    int rc = rebuild_good_prefix(t, nullptr);
-    if (rc) return rc;
+    int rc;
+    if ((rc = ensure_marks(t))) return rc;
+    if (m) {
+        const size_t ib = nodes ? ((4ull * m + 15) & ~15ull) : 0;
+        if ((rc = stage_reserve(t, ib + m))) return rc;
+        uint8_t* st = static_cast<uint8_t*>(t->stage);
+        if (nodes) HIP_TRY(hipMemcpy(st, nodes, 4ull * m, hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(st + ib, status, m, hipMemcpyHostToDevice));
+        hipLaunchKernelGGL(status_patch_kernel, dim3(grid_for(m)), dim3(BLOCK), 0, 0,
+                           nodes ? reinterpret_cast<const uint32_t*>(st) : nullptr, st + ib, m, t->status_mut,
+                           marks_of(t));
+        HIP_TRY(hipGetLastError());
+    }
+    if ((rc = rebuild_good_prefix(t, nullptr, false))) return rc;
+    HIP_TRY(hipDeviceSynchronize());
+    return KAD_OK;
+}
+
+int kad_table_patch_times(kad_table* t, uint32_t m, const uint32_t* nodes, const int64_t* time_ns,
+                          const int64_t* reply_ns, const uint8_t* expired) {
+    if (!t || (m && (!nodes || !time_ns || !reply_ns || !expired))) return set_err(KAD_ERR_INVALID, "NULL argument");
+    if (!t->time_ns) return set_err(KAD_ERR_INVALID, "kad_table_set_times was not called");
+    for (uint32_t j = 0; j < m; j++)
+        if (nodes[j] >= t->d.n) return set_err(KAD_ERR_INVALID, "node %u out of range (n=%u)", nodes[j], t->d.n);
+    if (!m) return KAD_OK;
+    DeviceGuard g(t->device);
+    int rc;
+    const size_t a = (4ull * m + 15) & ~15ull, b = 8ull * m;
+    if ((rc = stage_reserve(t, a + 2 * b + m))) return rc;
+    uint8_t* st = static_cast<uint8_t*>(t->stage);
+    HIP_TRY(hipMemcpy(st, nodes, 4ull * m, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(st + a, time_ns, b, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(st + a + b, reply_ns, b, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(st + a + 2 * b, expired, m, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(times_patch_kernel, dim3(grid_for(m)), dim3(BLOCK), 0, 0, reinterpret_cast<const uint32_t*>(st),
+                       reinterpret_cast<const int64_t*>(st + a), reinterpret_cast<const int64_t*>(st + a + b),
+                       st + a + 2 * b, m, t->d.n, t->time_ns, t->reply_ns, t->expired);
+    HIP_TRY(hipGetLastError());
     HIP_TRY(hipDeviceSynchronize());
     return KAD_OK;
 }
@@ -3102,11 +3434,13 @@ int kad_table_refresh_status(kad_table* t, int64_t now_ns, void* stream) {
     if (!t->time_ns) return set_err(KAD_ERR_INVALID, "kad_table_set_times was not called");
     DeviceGuard g(t->device);
     hipStream_t s = (hipStream_t)stream;
+    int rc;
+    if ((rc = ensure_marks(t))) return rc;
     if (t->d.n)
         hipLaunchKernelGGL(status_from_times_kernel, dim3(grid_for(t->d.n)), dim3(BLOCK), 0, s, t->time_ns, t->reply_ns,
-                           t->expired, t->d.n, now_ns, t->status_mut);
+                           t->expired, t->d.n, now_ns, t->status_mut, marks_of(t));
     HIP_TRY(hipGetLastError());
-    return rebuild_good_prefix(t, s);
+    return rebuild_good_prefix(t, s, false);
 }
 
 int kad_rt_closest_batch(const kad_table* t, const uint8_t* targets, uint32_t q, uint32_t count, uint32_t* out_idx,
@@ -3423,11 +3757,20 @@ void release(kad_table* t, void* p) {
     (void)hipFree(p);
 }
 
-// Bucket firsts -> fkey/ftail, the locate radix and TF_DIRECT (as kad_table_create builds them).
-int build_bucket_index(kad_table* t) {
-    DevTable& d = t->d;
-    const uint32_t B = d.B;
-    const uint8_t* first = t->h_first.data();
+// Bucket firsts -> fkey/ftail, the locate radix and TF_DIRECT (as kad_table_create builds them), uploaded into
+// new buffers listed in `fresh` (the table is not touched: kad_table_apply commits them only once every
+// allocation has succeeded).
+struct BucketIndex {
+    uint64_t* fkey = nullptr;
+    uint32_t* ftail = nullptr;
+    uint32_t* rrdx = nullptr;
+    Radix r;
+    bool direct = false;
+};
+
+int make_bucket_index(const std::vector<uint8_t>& h_first, uint32_t B, BucketIndex& out, std::vector<void*>& fresh,
+                      uint64_t& fresh_bytes) {
+    const uint8_t* first = h_first.data();
     std::vector<uint64_t> fkey(B);
     std::vector<uint32_t> ftail(3ull * B);
     for (uint32_t b = 0; b < B; b++) {
@@ -3447,18 +3790,13 @@ int build_bucket_index(kad_table* t) {
     std::vector<uint32_t> rdx = build_radix(r, B, first, true);
     bool direct = r.slots == B;
     for (uint32_t sl = 0; sl < r.slots && direct; sl++) direct = rdx[sl] == (sl | RDX_EXACT);
-    d.flags = direct ? (d.flags | TF_DIRECT) : (d.flags & ~TF_DIRECT);
-    release(t, const_cast<uint64_t*>(d.fkey));
-    release(t, const_cast<uint32_t*>(d.ftail));
-    release(t, const_cast<uint32_t*>(d.rrdx));
-    uint64_t* dfk; uint32_t *dft, *drdx;
     int rc;
-    if ((rc = dev_upload(&dfk, fkey.data(), B, t->owned, t->bytes)) ||
-        (rc = dev_upload(&dft, ftail.data(), 3ull * B, t->owned, t->bytes)) ||
-        (rc = dev_upload(&drdx, rdx.data(), rdx.size(), t->owned, t->bytes)))
+    if ((rc = dev_upload(&out.fkey, fkey.data(), B, fresh, fresh_bytes)) ||
+        (rc = dev_upload(&out.ftail, ftail.data(), 3ull * B, fresh, fresh_bytes)) ||
+        (rc = dev_upload(&out.rrdx, rdx.data(), rdx.size(), fresh, fresh_bytes)))
         return rc;
-    d.fkey = dfk; d.ftail = dft; d.rrdx = drdx;
-    d.rbase = r.base; d.rshift = r.shift; d.rslots = r.slots; t->rbits = r.bits;
+    out.r = r;
+    out.direct = direct;
     return KAD_OK;
 }
 
@@ -3629,9 +3967,16 @@ int kad_table_apply(kad_table* t, const uint32_t* ops, uint32_t n_ops, const uin
         nkey[s] = id_hi(new_ids + 20ull * s);
         for (int w = 0; w < 3; w++) ntail[3ull * s + w] = id_word(new_ids + 20ull * s, 2 + w);
     }
-    std::vector<void*> tmp;
-    uint64_t tmpb = 0;
-    auto cleanup = [&]() { for (void* p : tmp) (void)hipFree(p); };
+    // Everything the new layout needs is allocated and filled first (`fresh`: owned by the table only once
+    // all of it exists; `tmp`: scratch). Until the commit below the table is untouched, so any failure
+    // leaves it exactly as it was.
+    std::vector<void*> tmp, fresh;
+    uint64_t tmpb = 0, freshb = 0;
+    auto fail = [&](int code) {
+        for (void* p : tmp) (void)hipFree(p);
+        for (void* p : fresh) (void)hipFree(p);
+        return code;
+    };
     MirrorSeg* dseg; uint32_t *dlist, *dntail, *dnidx, *dremap = nullptr; uint64_t* dnkey; uint8_t* dnst;
     uint64_t* key1; uint32_t* tail1; uint8_t* st1;
     int rc;
@@ -3640,34 +3985,60 @@ int kad_table_apply(kad_table* t, const uint32_t* ops, uint32_t n_ops, const uin
         (rc = dev_upload(&dnkey, nkey.data(), n_new, tmp, tmpb)) ||
         (rc = dev_upload(&dntail, ntail.data(), 3ull * n_new, tmp, tmpb)) ||
         (rc = dev_upload(&dnst, new_status, n_new, tmp, tmpb)) || (rc = dev_upload(&dnidx, nullptr, n_new, tmp, tmpb)) ||
-        (remap && (rc = dev_upload(&dremap, nullptr, n0, tmp, tmpb)))) {
-        cleanup();
-        return rc;
-    }
-    if ((rc = dev_upload(&key1, nullptr, n1 + KEY_PAD, t->owned, t->bytes)) ||
-        (rc = dev_upload(&tail1, nullptr, 3ull * n1, t->owned, t->bytes)) ||
-        (rc = dev_upload(&st1, nullptr, n1, t->owned, t->bytes))) {
-        cleanup();
-        return rc;
-    }
+        (remap && (rc = dev_upload(&dremap, nullptr, n0, tmp, tmpb))))
+        return fail(rc);
+    if ((rc = dev_upload(&key1, nullptr, n1 + KEY_PAD, fresh, freshb)) ||
+        (rc = dev_upload(&tail1, nullptr, 3ull * n1, fresh, freshb)) ||
+        (rc = dev_upload(&st1, nullptr, n1, fresh, freshb)))
+        return fail(rc);
     if (hipMemset(key1, 0xFF, 8ull * (n1 + KEY_PAD)) != hipSuccess || hipMemset(dnidx, 0xFF, 4ull * n_new) != hipSuccess ||
-        (remap && n0 && hipMemset(dremap, 0xFF, 4ull * n0) != hipSuccess)) {
-        cleanup();
-        return set_err(KAD_ERR_HIP, "hipMemset failed");
-    }
+        (remap && n0 && hipMemset(dremap, 0xFF, 4ull * n0) != hipSuccess))
+        return fail(set_err(KAD_ERR_HIP, "hipMemset failed"));
     if (n1)
         hipLaunchKernelGGL(mirror_gather_kernel, dim3(grid_for(n1)), dim3(BLOCK), 0, 0, dseg, (uint32_t)segs.size(), dlist, n1,
                            d.key, d.tail, d.status, dnkey, dntail, dnst, key1, tail1, st1, dremap, dnidx);
-    if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
-        cleanup();
-        return set_err(KAD_ERR_HIP, "mirror gather failed");
+    if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess)
+        return fail(set_err(KAD_ERR_HIP, "mirror gather failed"));
+    // bucket directory (always a new array, so the old one stays valid until the commit)
+    std::vector<uint2> dir(B1 + 1);
+    for (uint32_t c = 0; c <= B1; c++) {
+        dir[c].x = off1[c] | (c < B1 && off1[c + 1] - off1[c] > 32 ? WIDE : 0u);
+        dir[c].y = 0;
+    }
+    uint2* ddir; uint32_t *dgp = nullptr, *scnt = nullptr, *spart = nullptr, *ssums = nullptr, *ddm, *dany;
+    if ((rc = dev_upload(&ddir, dir.data(), B1 + 1, fresh, freshb))) return fail(rc);
+    const bool reshape = B1 != B0;
+    BucketIndex bix;
+    if (reshape &&
+        ((rc = dev_upload(&dgp, nullptr, B1 + 1, fresh, freshb)) ||
+         (rc = dev_upload(&scnt, nullptr, B1 + 1, fresh, freshb)) ||
+         (rc = dev_upload(&spart, nullptr, B1 + 1, fresh, freshb)) ||
+         (rc = dev_upload(&ssums, nullptr, (B1 + 1 + SCAN_TILE - 1) / SCAN_TILE, fresh, freshb))))
+        return fail(rc);
+    std::vector<uint8_t> first1(20ull * B1);
+    for (uint32_t c = 0; c < B1; c++) std::memcpy(first1.data() + 20ull * c, firsts[c].data(), 20);
+    if (reshape && (rc = make_bucket_index(first1, B1, bix, fresh, freshb))) return fail(rc);
+    // duplicate top-64 masks of the new layout
+    if ((rc = dev_upload(&ddm, nullptr, B1, fresh, freshb)) || (rc = dev_upload(&dany, nullptr, 1, tmp, tmpb)))
+        return fail(rc);
+    bool low_zero = true;
+    for (uint32_t c = 0; c < B1 && low_zero; c++) low_zero = id_low_zero(first1.data() + 20ull * c);
+    uint32_t any = 0;
+    if (low_zero) {
+        if (hipMemset(dany, 0, 4) != hipSuccess) return fail(set_err(KAD_ERR_HIP, "hipMemset failed"));
+        hipLaunchKernelGGL(mirror_dmask_kernel, dim3(grid_for(B1)), dim3(BLOCK), 0, 0, key1, ddir, B1, ddm, dany);
+        if (hipGetLastError() != hipSuccess || hipMemcpy(&any, dany, 4, hipMemcpyDeviceToHost) != hipSuccess)
+            return fail(set_err(KAD_ERR_HIP, "dup mask failed"));
+    } else {  // a bucket first below 64-bit granularity: flag every node (exact path, always correct)
+        if (hipMemset(ddm, 0xFF, 4ull * B1) != hipSuccess) return fail(set_err(KAD_ERR_HIP, "hipMemset failed"));
+        any = 1;
     }
     if ((new_index && n_new && hipMemcpy(new_index, dnidx, 4ull * n_new, hipMemcpyDeviceToHost) != hipSuccess) ||
-        (remap && n0 && hipMemcpy(remap, dremap, 4ull * n0, hipMemcpyDefault) != hipSuccess)) {
-        cleanup();
-        return set_err(KAD_ERR_HIP, "copy of new indices failed");
-    }
-    cleanup();
+        (remap && n0 && hipMemcpy(remap, dremap, 4ull * n0, hipMemcpyDefault) != hipSuccess))
+        return fail(set_err(KAD_ERR_HIP, "copy of new indices failed"));
+    for (void* p : tmp) (void)hipFree(p);
+
+    // ---- commit: nothing below can fail before the derived state is rebuilt ----
     release(t, const_cast<uint64_t*>(d.key));
     release(t, const_cast<uint32_t*>(d.tail));
     release(t, t->status_mut);
@@ -3681,58 +4052,32 @@ int kad_table_apply(kad_table* t, const uint32_t* ops, uint32_t n_ops, const uin
     release(t, t->wrec); t->wrec = nullptr; t->addr_len = 0;
     release(t, t->time_ns); release(t, t->reply_ns); release(t, t->expired);
     t->time_ns = nullptr; t->reply_ns = nullptr; t->expired = nullptr;
-    // bucket directory
     t->h_off = off1;
-    t->h_first.resize(20ull * B1);
-    for (uint32_t c = 0; c < B1; c++) std::memcpy(t->h_first.data() + 20ull * c, firsts[c].data(), 20);
-    std::vector<uint2> dir(B1 + 1);
-    for (uint32_t c = 0; c <= B1; c++) {
-        dir[c].x = off1[c] | (c < B1 && off1[c + 1] - off1[c] > 32 ? WIDE : 0u);
-        dir[c].y = 0;
-    }
-    if (B1 != B0) {
-        release(t, t->dir_mut); release(t, t->gpre_mut);
+    t->h_first.swap(first1);
+    release(t, t->dir_mut);
+    d.dir = ddir; t->dir_mut = ddir;
+    if (reshape) {
+        release(t, t->gpre_mut);
         release(t, t->scan_cnt); release(t, t->scan_part); release(t, t->scan_sums);
-        uint2* ddir; uint32_t* dgp;
-        if ((rc = dev_upload(&ddir, nullptr, B1 + 1, t->owned, t->bytes)) ||
-            (rc = dev_upload(&dgp, nullptr, B1 + 1, t->owned, t->bytes)) ||
-            (rc = dev_upload(&t->scan_cnt, nullptr, B1 + 1, t->owned, t->bytes)) ||
-            (rc = dev_upload(&t->scan_part, nullptr, B1 + 1, t->owned, t->bytes)) ||
-            (rc = dev_upload(&t->scan_sums, nullptr, (B1 + 1 + SCAN_TILE - 1) / SCAN_TILE, t->owned, t->bytes)))
-            return rc;
-        d.dir = ddir; t->dir_mut = ddir; d.gpre = dgp; t->gpre_mut = dgp; d.B = B1;
-        if ((rc = build_bucket_index(t))) return rc;
-        // a split breaks the uniform depth the window lines need
+        d.gpre = dgp; t->gpre_mut = dgp; t->scan_cnt = scnt; t->scan_part = spart; t->scan_sums = ssums; d.B = B1;
+        release(t, const_cast<uint64_t*>(d.fkey));
+        release(t, const_cast<uint32_t*>(d.ftail));
+        release(t, const_cast<uint32_t*>(d.rrdx));
+        d.fkey = bix.fkey; d.ftail = bix.ftail; d.rrdx = bix.rrdx;
+        d.rbase = bix.r.base; d.rshift = bix.r.shift; d.rslots = bix.r.slots; t->rbits = bix.r.bits;
+        d.flags = bix.direct ? (d.flags | TF_DIRECT) : (d.flags & ~TF_DIRECT);
+    }
+    if (reshape || !lines_ok) {  // a split (or a new node outside its dyadic range) breaks the uniform depth
         release(t, t->wl_mut); t->wl_mut = nullptr; d.wl = nullptr; d.flags &= ~TF_WL;
         release(t, t->wl16_mut); t->wl16_mut = nullptr; d.wl16 = nullptr; d.flags &= ~TF_WL16;
         release(t, t->wl32_mut); t->wl32_mut = nullptr; d.wl32 = nullptr; d.flags &= ~TF_WL32;
     }
-    if (!lines_ok && t->wl_mut) {
-        release(t, t->wl_mut); t->wl_mut = nullptr; d.wl = nullptr; d.flags &= ~TF_WL;
-        release(t, t->wl16_mut); t->wl16_mut = nullptr; d.wl16 = nullptr; d.flags &= ~TF_WL16;
-        release(t, t->wl32_mut); t->wl32_mut = nullptr; d.wl32 = nullptr; d.flags &= ~TF_WL32;
-    }
-    HIP_TRY(hipMemcpy(t->dir_mut, dir.data(), 8ull * (B1 + 1), hipMemcpyHostToDevice));
-    // duplicate top-64 masks
-    release(t, const_cast<uint32_t*>(d.dmask)); d.dmask = nullptr; d.flags &= ~TF_HAS_DUP;
-    bool low_zero = true;
-    for (uint32_t c = 0; c < B1 && low_zero; c++) low_zero = id_low_zero(t->h_first.data() + 20ull * c);
-    uint32_t* ddm;
-    if ((rc = dev_upload(&ddm, nullptr, B1, t->owned, t->bytes))) return rc;
-    uint32_t* dany;
-    HIP_TRY(hipMalloc(&dany, 4));
-    (void)hipMemset(dany, 0, 4);
-    uint32_t any = 0;
-    if (low_zero) {
-        hipLaunchKernelGGL(mirror_dmask_kernel, dim3(grid_for(B1)), dim3(BLOCK), 0, 0, d.key, t->dir_mut, B1, ddm, dany);
-        (void)hipMemcpy(&any, dany, 4, hipMemcpyDeviceToHost);
-    } else {  // a bucket first below 64-bit granularity: flag every node (exact path, always correct)
-        (void)hipMemset(ddm, 0xFF, 4ull * B1);
-        any = 1;
-    }
-    (void)hipFree(dany);
+    release(t, const_cast<uint32_t*>(d.dmask));
     d.dmask = ddm;
-    if (any) d.flags |= TF_HAS_DUP;
+    d.flags = any ? (d.flags | TF_HAS_DUP) : (d.flags & ~TF_HAS_DUP);
+    t->owned.insert(t->owned.end(), fresh.begin(), fresh.end());
+    t->bytes += freshb;
+    drop_marks(t);  // the incremental-refresh flags are sized for the old shape
     // masks, good prefix sums, window lines
     if ((rc = rebuild_good_prefix(t, nullptr))) return rc;
     HIP_TRY(hipDeviceSynchronize());

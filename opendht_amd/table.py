@@ -105,6 +105,25 @@ class DeviceTable:
         e = np.ascontiguousarray(expired, dtype=np.uint8)
         check(lib().kad_table_set_times(self._h, ptr(a), ptr(b), ptr(e)), "kad_table_set_times")
 
+    def patch_status(self, nodes, status) -> None:
+        """Incremental status update of the listed nodes (kad_table_patch_status)."""
+        nodes = np.ascontiguousarray(nodes, dtype=np.uint32)
+        status = np.ascontiguousarray(status, dtype=np.uint8)
+        if nodes.shape != status.shape:
+            raise ValueError("nodes and status must have the same length")
+        check(lib().kad_table_patch_status(self._h, nodes.shape[0], ptr(nodes), ptr(status)), "kad_table_patch_status")
+
+    def patch_times(self, nodes, time_ns, reply_time_ns, expired) -> None:
+        """New liveness of the listed nodes (kad_table_patch_times); applied at the next refresh_status."""
+        nodes = np.ascontiguousarray(nodes, dtype=np.uint32)
+        a = np.ascontiguousarray(time_ns, dtype=np.int64)
+        b = np.ascontiguousarray(reply_time_ns, dtype=np.int64)
+        e = np.ascontiguousarray(expired, dtype=np.uint8)
+        if not (nodes.shape == a.shape == b.shape == e.shape):
+            raise ValueError("patch arrays must have the same length")
+        check(lib().kad_table_patch_times(self._h, nodes.shape[0], ptr(nodes), ptr(a), ptr(b), ptr(e)),
+              "kad_table_patch_times")
+
     def refresh_status(self, now_ns: int, stream=None) -> None:
         check(lib().kad_table_refresh_status(self._h, C.c_int64(now_ns), _stream_of(self, stream)),
               "kad_table_refresh_status")

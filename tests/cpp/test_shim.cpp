@@ -1,7 +1,8 @@
 // C++ test of include/kadgpu.hpp against test doubles shaped like OpenDHT's types
-// (InfoHash = std::array<uint8_t,20>, Node with isGood/isExpired, Bucket{first, list<shared_ptr<Node>>},
-// RoutingTable = std::list<Bucket>, NodeCache family map = std::map<InfoHash, weak_ptr<Node>>).
-// Expected results come from the CPU oracle (test infrastructure). Needs a GPU. Exit 0 = pass.
+// (InfoHash = std::array<uint8_t,20>, Node with time / reply_time / isGood(now) / isExpired(),
+// Bucket{first, list<shared_ptr<Node>>}, RoutingTable = std::list<Bucket>, NodeCache family map =
+// std::map<InfoHash, weak_ptr<Node>>). Expected results come from the CPU oracle (test infrastructure)
+// on the host objects' state at each query's `now`. Needs a GPU. Exit 0 = pass.
 #include <algorithm>
 #include <array>
 #include <chrono>
@@ -25,6 +26,7 @@ using time_point = clock::time_point;
 struct InfoHash : std::array<uint8_t, 20> {
     bool operator<(const InfoHash& o) const { return std::memcmp(data(), o.data(), 20) < 0; }
 };
+// node.h:35-105 / node.cpp:34-40, 82-108 in miniature
 struct Node {
     InfoHash id;
     time_point time{time_point::min()}, reply_time{time_point::min()};
@@ -34,6 +36,11 @@ struct Node {
     bool isGood(time_point now) const {
         return !expired_ && reply_time >= now - std::chrono::minutes(120) && time >= now - std::chrono::minutes(10);
     }
+    void received(time_point now, bool reply) {
+        time = now;
+        if (reply) { reply_time = now; expired_ = false; }
+    }
+    void setExpired() { expired_ = true; }
 };
 struct Bucket {
     InfoHash first;
@@ -44,10 +51,61 @@ using NodeMap = std::map<InfoHash, std::weak_ptr<Node>>;
 }  // namespace mock
 
 static int fails = 0;
-#define EXPECT(c, ...) do { if (!(c)) { fails++; std::fprintf(stderr, __VA_ARGS__); std::fprintf(stderr, "\n"); } } while (0)
+#define EXPECT(c, ...) do { if (!(c)) { fails++; if (fails < 30) { std::fprintf(stderr, __VA_ARGS__); std::fprintf(stderr, "\n"); } } } while (0)
+
+using namespace mock;
+
+// The oracle's answer on the host table as it is now, compared with the mirror's result vectors.
+static void check_rt(const RoutingTable& rt, const std::vector<std::vector<std::shared_ptr<Node>>>& got,
+                     const std::vector<InfoHash>& targets, uint32_t count, time_point now, const char* what) {
+    std::vector<uint8_t> ids, st, first;
+    std::vector<uint32_t> off;
+    std::vector<const Node*> flat;
+    for (auto& b : rt) {
+        off.push_back((uint32_t)flat.size());
+        first.insert(first.end(), b.first.begin(), b.first.end());
+        for (auto& nd : b.nodes) {
+            ids.insert(ids.end(), nd->id.begin(), nd->id.end());
+            st.push_back((uint8_t)((nd->isGood(now) ? 1 : 0) | (nd->isExpired() ? 2 : 0)));
+            flat.push_back(nd.get());
+        }
+    }
+    off.push_back((uint32_t)flat.size());
+    const uint32_t q = (uint32_t)targets.size();
+    std::vector<uint32_t> want(q * count);
+    std::vector<uint8_t> wcnt(q);
+    orc_flat_rt_closest((uint32_t)flat.size(), ids.data(), st.data(), (uint32_t)rt.size(), first.data(), off.data(), q,
+                        reinterpret_cast<const uint8_t*>(targets.data()), count, want.data(), wcnt.data(), 4);
+    for (uint32_t i = 0; i < q; i++) {
+        EXPECT(got[i].size() == wcnt[i], "%s: rt count q=%u k=%u (%zu vs %u)", what, i, count, got[i].size(), wcnt[i]);
+        for (uint32_t j = 0; j < got[i].size() && j < wcnt[i]; j++)
+            EXPECT(got[i][j].get() == flat[want[i * count + j]], "%s: rt node q=%u k=%u j=%u", what, i, count, j);
+    }
+}
+
+static void check_nc(const NodeMap& nm, const std::vector<std::vector<std::shared_ptr<Node>>>& got,
+                     const std::vector<InfoHash>& targets, uint32_t count, const char* what) {
+    std::vector<uint8_t> ids, st;
+    std::vector<const Node*> flat;
+    for (auto& kv : nm) {
+        auto n = kv.second.lock();
+        ids.insert(ids.end(), kv.first.begin(), kv.first.end());
+        st.push_back((!n || n->isExpired()) ? 2 : 0);
+        flat.push_back(n.get());
+    }
+    const uint32_t q = (uint32_t)targets.size();
+    std::vector<uint32_t> want(q * count);
+    std::vector<uint8_t> wcnt(q);
+    orc_flat_nc_closest((uint32_t)flat.size(), ids.data(), st.data(), q, reinterpret_cast<const uint8_t*>(targets.data()),
+                        count, want.data(), wcnt.data(), 4);
+    for (uint32_t i = 0; i < q; i++) {
+        EXPECT(got[i].size() == wcnt[i], "%s: nc count q=%u k=%u", what, i, count);
+        for (uint32_t j = 0; j < got[i].size() && j < wcnt[i]; j++)
+            EXPECT(got[i][j].get() == flat[want[i * count + j]], "%s: nc node q=%u j=%u", what, i, j);
+    }
+}
 
 int main() {
-    using namespace mock;
     const uint32_t n = 20000, q = 3000;
     std::vector<uint8_t> ids(20ull * n);
     kadgpu::check(kad_synth_ids(0xC0FFEE, n, ids.data()), "synth");
@@ -55,34 +113,31 @@ int main() {
     std::vector<uint8_t> first(20ull * (n + 1));
     uint32_t B = 0;
     kadgpu::check(kad_split_table(n, ids.data(), 8, perm.data(), first.data(), off.data(), &B), "split");
-    const time_point now = clock::now();
+    const time_point t0 = clock::now();
     std::mt19937_64 g(7);
     std::vector<std::shared_ptr<Node>> nodes(n);
+    const auto MIN = std::chrono::minutes(1);
     for (uint32_t i = 0; i < n; i++) {
         auto nd = std::make_shared<Node>();
         std::memcpy(nd->id.data(), &ids[20ull * i], 20);
         nd->idx = i;
         const unsigned u = g() % 100;
-        nd->time = nd->reply_time = now;
-        if (u >= 80 && u < 90) nd->expired_ = true;
-        else if (u >= 90) nd->time = now - std::chrono::minutes(11);
+        // heard 0..9.9 min and replied 0..119 min before t0; edges: exactly 10 and 120 min
+        nd->time = t0 - std::chrono::milliseconds(g() % 594000);
+        nd->reply_time = t0 - std::chrono::seconds(g() % 7140);
+        if (u < 3) nd->time = t0 - 10 * MIN;                // good at t0, dubious 1 ns later
+        else if (u < 6) nd->reply_time = t0 - 120 * MIN;    // likewise through reply_time
+        else if (u < 8) nd->reply_time = time_point::min(); // never replied
+        else if (u >= 85 && u < 95) nd->expired_ = true;
         nodes[i] = nd;
     }
     RoutingTable rt;
-    std::vector<uint8_t> fids, fst;  // flattened in list order for the oracle
     for (uint32_t b = 0; b < B; b++) {
         Bucket bk;
         std::memcpy(bk.first.data(), &first[20ull * b], 20);
         for (uint32_t j = off[b]; j < off[b + 1]; j++) bk.nodes.push_back(nodes[perm[j]]);
         rt.push_back(bk);
     }
-    std::vector<uint32_t> flat_to_node;
-    for (auto& b : rt)
-        for (auto& nd : b.nodes) {
-            fids.insert(fids.end(), nd->id.begin(), nd->id.end());
-            fst.push_back((uint8_t)((nd->isGood(now) ? 1 : 0) | (nd->isExpired() ? 2 : 0)));
-            flat_to_node.push_back(nd->idx);
-        }
     std::vector<InfoHash> targets(q);
     for (auto& t : targets)
         for (auto& x : t) x = (uint8_t)g();
@@ -90,48 +145,91 @@ int main() {
     targets[1].fill(0);
     targets[2].fill(0xFF);
 
-    kadgpu::RoutingTableMirror<RoutingTable> mirror(rt, now, 0);
+    // RoutingTable::findClosestNodes(id, now, count) at a moving `now` (routing_table.h:48)
+    kadgpu::RoutingTableMirror<RoutingTable> mirror(rt, t0, 0);
     EXPECT(mirror.bucketCount() == B, "bucket count");
-    for (uint32_t count : {1u, 8u, 14u, 32u}) {
-        auto got = mirror.findClosestNodesBatch(targets, count);
-        std::vector<uint32_t> want(q * count);
-        std::vector<uint8_t> wcnt(q);
-        orc_flat_rt_closest(n, fids.data(), fst.data(), B, first.data(), off.data(), q,
-                            reinterpret_cast<const uint8_t*>(targets.data()), count, want.data(), wcnt.data(), 4);
-        for (uint32_t i = 0; i < q; i++) {
-            EXPECT(got[i].size() == wcnt[i], "rt count q=%u k=%u", i, count);
-            for (uint32_t j = 0; j < got[i].size() && j < wcnt[i]; j++)
-                EXPECT(got[i][j]->idx == flat_to_node[want[i * count + j]], "rt node q=%u k=%u j=%u", i, count, j);
+    const std::chrono::nanoseconds steps[] = {std::chrono::nanoseconds(0), std::chrono::nanoseconds(1),
+                                              std::chrono::seconds(30), std::chrono::minutes(3), std::chrono::minutes(9),
+                                              std::chrono::minutes(11), std::chrono::minutes(125)};
+    for (auto dt : steps) {
+        const time_point now = t0 + dt;
+        for (uint32_t count : {1u, 8u, 14u, 32u}) {
+            auto got = mirror.findClosestNodesBatch(targets, now, count);
+            check_rt(rt, got, targets, count, now, "moving now");
         }
-        auto one = mirror.findClosestNodes(targets[3], count);
-        EXPECT(one.size() == got[3].size(), "single query");
+        auto one = mirror.findClosestNodes(targets[3], now, 8);
+        auto ref = mirror.findClosestNodesBatch(&targets[3], 1, now, 8);
+        EXPECT(one == ref[0], "single query");
     }
-    // NodeCache family map
-    NodeMap nm;
-    for (auto& nd : nodes) nm.emplace(nd->id, nd);
-    std::vector<uint8_t> sids, sst;
-    std::vector<uint32_t> sorted_to_node;
-    for (auto& kv : nm) {
-        sids.insert(sids.end(), kv.first.begin(), kv.first.end());
-        sst.push_back(kv.second.lock()->isExpired() ? 2 : 0);
-        sorted_to_node.push_back(kv.second.lock()->idx);
+    // going back in time is allowed too (the status is a function of now)
+    {
+        auto got = mirror.findClosestNodesBatch(targets, t0, 8);
+        check_rt(rt, got, targets, 8, t0, "now moved back");
     }
-    kadgpu::NodeCacheMirror<NodeMap> nc(nm, 0);
-    for (uint32_t count : {8u, 14u}) {
-        auto got = nc.getCachedNodesBatch(targets, count);
-        std::vector<uint32_t> want(q * count);
-        std::vector<uint8_t> wcnt(q);
-        orc_flat_nc_closest(n, sids.data(), sst.data(), q, reinterpret_cast<const uint8_t*>(targets.data()), count,
-                            want.data(), wcnt.data(), 4);
-        for (uint32_t i = 0; i < q; i++) {
-            EXPECT(got[i].size() == wcnt[i], "nc count q=%u", i);
-            for (uint32_t j = 0; j < got[i].size() && j < wcnt[i]; j++)
-                EXPECT(got[i][j]->idx == sorted_to_node[want[i * count + j]], "nc node q=%u j=%u", i, j);
+    // liveness changes on the host, reported with nodeUpdated: Node::received / setExpired
+    {
+        const time_point now = t0 + 11 * MIN;
+        for (uint32_t i = 0; i < n; i += 7) {
+            nodes[i]->received(now, i % 2 == 0);
+            mirror.nodeUpdated(nodes[i]);
+        }
+        for (uint32_t i = 3; i < n; i += 29) {
+            nodes[i]->setExpired();
+            mirror.nodeUpdated(nodes[i]);
+        }
+        for (uint32_t count : {1u, 8u, 14u, 32u}) {
+            auto got = mirror.findClosestNodesBatch(targets, now, count);
+            check_rt(rt, got, targets, count, now, "nodeUpdated");
+        }
+        // the same changes through syncTimes()
+        for (uint32_t i = 1; i < n; i += 13) nodes[i]->received(now, true);
+        mirror.syncTimes();
+        auto got = mirror.findClosestNodesBatch(targets, now, 8);
+        check_rt(rt, got, targets, 8, now, "syncTimes");
+    }
+
+    // NodeCache::getCachedNodes(id, sa_family_t, count) over both families (node_cache.h:32)
+    {
+        NodeMap c4, c6;
+        std::vector<std::shared_ptr<Node>> extra;  // cache-only nodes, some of which die
+        for (auto& nd : nodes) (nd->idx % 3 == 0 ? c6 : c4).emplace(nd->id, nd);
+        for (int k = 0; k < 3000; k++) {
+            auto nd = std::make_shared<Node>();
+            for (auto& x : nd->id) x = (uint8_t)g();
+            nd->idx = 100000 + k;
+            nd->time = nd->reply_time = t0;
+            extra.push_back(nd);
+            c4.emplace(nd->id, nd);
+        }
+        kadgpu::NodeCacheMirror<NodeMap> nc;
+        nc.snapshot(c4, c6, 0);
+        for (uint32_t count : {8u, 14u, 32u}) {
+            std::vector<std::vector<std::shared_ptr<Node>>> g4, g6;
+            for (auto& t : targets) {
+                g4.push_back(nc.getCachedNodes(t, AF_INET, count));
+                g6.push_back(nc.getCachedNodes(t, AF_INET6, count));
+            }
+            check_nc(c4, g4, targets, count, "nc v4");
+            check_nc(c6, g6, targets, count, "nc v6");
+        }
+        // deaths and expiries need no notification (detected on the results, re-run)
+        for (size_t k = 0; k < extra.size(); k += 3) extra[k].reset();
+        for (uint32_t i = 0; i < n; i += 17) nodes[i]->setExpired();
+        // an expired node that answers again must be reported
+        for (uint32_t i = 0; i < n; i += 31)
+            if (nodes[i]->isExpired()) { nodes[i]->received(t0, true); nc.nodeUpdated(nodes[i]); }
+        for (uint32_t count : {8u, 14u}) {
+            auto b4 = nc.family(AF_INET).getCachedNodesBatch(targets, count);
+            auto b6 = nc.family(AF_INET6).getCachedNodesBatch(targets, count);
+            check_nc(c4, b4, targets, count, "nc v4 after deaths");
+            check_nc(c6, b6, targets, count, "nc v6 after expiries");
         }
     }
+
     // Incremental mirror: Dht::onNewNode (replace an expired node / emplace_front / split my bucket)
     // and Dht::expireBuckets on the host table, recorded on the mirror and flushed to the device.
     {
+        const time_point now = t0 + 12 * MIN;
         auto find_bucket = [&](const InfoHash& id) {  // routing_table.cpp:113-127
             auto b = rt.begin();
             while (std::next(b) != rt.end() && !(id < std::next(b)->first)) ++b;
@@ -149,7 +247,7 @@ int main() {
             if (depth >= 160) return false;
             InfoHash mid = b->first;
             mid[depth / 8] |= (uint8_t)(0x80 >> (depth % 8));
-            auto nb = rt.insert(std::next(b), Bucket{mid, {}});
+            rt.insert(std::next(b), Bucket{mid, {}});
             std::list<std::shared_ptr<Node>> tmp;
             tmp.splice(tmp.begin(), b->nodes);
             while (!tmp.empty()) {
@@ -157,7 +255,6 @@ int main() {
                 auto dst = find_bucket((*it)->id);
                 dst->nodes.splice(dst->nodes.begin(), tmp, it);
             }
-            (void)nb;
             return true;
         };
         const InfoHash myid = nodes[123]->id;
@@ -208,42 +305,36 @@ int main() {
             });
         mirror.flush(now);
         EXPECT(mirror.bucketCount() == rt.size(), "mirror buckets %zu vs %zu", mirror.bucketCount(), rt.size());
-        std::vector<uint8_t> mids, mst, mfirst;
-        std::vector<uint32_t> moff;
-        std::vector<const Node*> mnode;
-        for (auto& b : rt) {
-            moff.push_back((uint32_t)mnode.size());
-            mfirst.insert(mfirst.end(), b.first.begin(), b.first.end());
-            for (auto& nd : b.nodes) {
-                mids.insert(mids.end(), nd->id.begin(), nd->id.end());
-                mst.push_back((uint8_t)((nd->isGood(now) ? 1 : 0) | (nd->isExpired() ? 2 : 0)));
-                mnode.push_back(nd.get());
-            }
-        }
-        moff.push_back((uint32_t)mnode.size());
-        EXPECT(mirror.nodeCount() == mnode.size(), "mirror nodes %zu vs %zu", mirror.nodeCount(), mnode.size());
+        size_t total = 0;
+        for (auto& b : rt) total += b.nodes.size();
+        EXPECT(mirror.nodeCount() == total, "mirror nodes %zu vs %zu", mirror.nodeCount(), total);
         for (uint32_t count : {1u, 8u, 14u}) {
-            auto got = mirror.findClosestNodesBatch(targets, count);
-            std::vector<uint32_t> want(q * count);
-            std::vector<uint8_t> wcnt(q);
-            orc_flat_rt_closest((uint32_t)mnode.size(), mids.data(), mst.data(), (uint32_t)rt.size(), mfirst.data(),
-                                moff.data(), q, reinterpret_cast<const uint8_t*>(targets.data()), count, want.data(),
-                                wcnt.data(), 4);
-            for (uint32_t i = 0; i < q; i++) {
-                EXPECT(got[i].size() == wcnt[i], "mirror count q=%u k=%u", i, count);
-                for (uint32_t j = 0; j < got[i].size() && j < wcnt[i]; j++)
-                    EXPECT(got[i][j].get() == mnode[want[i * count + j]], "mirror node q=%u k=%u j=%u", i, count, j);
-            }
+            auto got = mirror.findClosestNodesBatch(targets, now, count);
+            check_rt(rt, got, targets, count, now, "mirror");
         }
+        // and the mirrored table keeps tracking `now` after the flush
+        const time_point later = now + 10 * MIN;
+        auto got = mirror.findClosestNodesBatch(targets, later, 8);
+        check_rt(rt, got, targets, 8, later, "mirror later");
         std::printf("mirror: %u replaced, %u added, %u splits, %u removed\n", replaced, added, splits, removed);
         EXPECT(replaced && added && splits && removed, "every mutation kind exercised");
     }
-    // Dht-style accessor over two families
-    kadgpu::DhtMirror<RoutingTable> dht;
-    RoutingTable empty6;
-    dht.snapshot(rt, empty6, now, 0);
-    EXPECT(dht.findClosestNodes(targets[4], 2 /*AF_INET*/, 8, 2).size() == 8, "dht v4");
-    EXPECT(dht.findClosestNodes(targets[4], 10 /*AF_INET6*/, 8, 2).empty(), "dht v6 empty table");
+
+    // Dht::findClosestNodes(id, af, count) with exactly three arguments; `now` from the mirror's clock
+    {
+        kadgpu::DhtMirror<RoutingTable> dht;
+        RoutingTable empty6;
+        time_point sched = t0 + 12 * MIN;
+        dht.snapshot(rt, empty6, sched, 0);
+        dht.setClock([&] { return sched; });  // Dht's scheduler.time()
+        for (time_point at : {t0 + 12 * MIN, t0 + 20 * MIN, t0 + 200 * MIN}) {
+            sched = at;
+            std::vector<std::vector<std::shared_ptr<Node>>> got;
+            for (auto& t : targets) got.push_back(dht.findClosestNodes(t, AF_INET, 8));
+            check_rt(rt, got, targets, 8, at, "dht v4");
+            EXPECT(dht.findClosestNodes(targets[4], AF_INET6, 8).empty(), "dht v6 empty table");
+        }
+    }
     std::printf("%s (%d failures)\n", fails ? "FAIL" : "PASS", fails);
     return fails ? 1 : 0;
 }

@@ -280,13 +280,13 @@ def _nc_targets(t):
 @pytest.mark.parametrize("t", _nc_tables(), ids=lambda t: t["name"])
 def test_nc_lines(gpu, t, kernel, monkeypatch):
     """NodeCache::getCachedNodes for every count 1..16 (the line kernel, default; KAD_NC_KERNEL=multi2:
-    the wave-per-query kernel), 17..32 and 40 (default: 32-node runs first, 64-node runs for the queries that
+    the wave-per-query kernel), 17..32, 40, 48, 63 and 64 (default: 32-node runs first, 64-node runs for the queries that
     leave them; KAD_NC_KERNEL=wave64: 64-node runs only; KAD_NC_KERNEL=multi2: 32-node runs up to 32, the
     serial walk for 40)."""
     if kernel != "lines":
         monkeypatch.setenv("KAD_NC_KERNEL", kernel)
     with make(t, gpu) as T:
-        check_nc(T, t, _nc_targets(t), gpu, counts=tuple(range(1, 33)) + (40,))
+        check_nc(T, t, _nc_targets(t), gpu, counts=tuple(range(1, 33)) + (40, 48, 63, 64))
 
 
 def test_nc_lines_after_status_change(gpu):

@@ -1,0 +1,146 @@
+"""Incremental status refresh (kad_table_patch_status / update_status / patch_times + refresh_status):
+after isGood / isExpired flips (Node::received, setExpired, ageing past NODE_EXPIRE_TIME; node.cpp:34-40,
+82-108) only the flipped buckets' masks and the lines whose window reaches them are rebuilt. Every result
+must equal the oracle on the new status: RoutingTable counts 1..32 (window lines of all three kinds and the
+lane kernel) and NodeCache counts 1..32 (NodeCache lines), after 0.1 % and 1 % flips, repeated patches,
+and a moving `now`."""
+import numpy as np
+import pytest
+import torch
+
+import oracle as O
+import tables as TB
+from opendht_amd import DeviceTable
+
+pytestmark = pytest.mark.gpu
+
+RT_COUNTS = (1, 2, 3, 5, 7, 8, 9, 12, 14, 16, 17, 20, 24, 31, 32)
+NC_COUNTS = (1, 2, 8, 13, 14, 16, 17, 24, 32)
+
+
+def _dev(a, gpu):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(gpu)
+
+
+def _check(T, t, status, targets, gpu, rt=RT_COUNTS, nc=NC_COUNTS):
+    tg = _dev(targets, gpu)
+    for k in rt:
+        idx, cnt = T.rt_closest(tg, k)
+        torch.cuda.synchronize()
+        want, wcnt = O.flat_rt_closest(t["ids"], status, t["first"], t["off"], targets, k, nthreads=8)
+        np.testing.assert_array_equal(cnt.cpu().numpy(), wcnt, err_msg=f"{t['name']} rt k={k} counts")
+        np.testing.assert_array_equal(idx.cpu().numpy().view(np.uint32), want, err_msg=f"{t['name']} rt k={k}")
+    if t["sorted"]:
+        for k in nc:
+            idx, cnt = T.nc_closest(tg, k)
+            torch.cuda.synchronize()
+            want, wcnt = O.flat_nc_closest(t["ids"], status, targets, k, nthreads=8)
+            np.testing.assert_array_equal(cnt.cpu().numpy(), wcnt, err_msg=f"{t['name']} nc k={k} counts")
+            np.testing.assert_array_equal(idx.cpu().numpy().view(np.uint32), want, err_msg=f"{t['name']} nc k={k}")
+
+
+def _tables():
+    return [TB.uniform_config(60_000, 13, seed=0x5E1), TB.uniform_config(20_000, 10, seed=0x5E2),
+            TB.split_config(20_000, seed=0x5E3)]
+
+
+def _flip(rng, status, frac):
+    n = status.shape[0]
+    m = max(1, int(n * frac))
+    nodes = rng.choice(n, size=m, replace=False).astype(np.uint32)
+    new = rng.choice(np.array([0, 1, 1, 2, 3], np.uint8), size=m)
+    st = status.copy()
+    st[nodes] = new
+    return nodes, new, st
+
+
+@pytest.mark.parametrize("frac", [0.001, 0.01])
+@pytest.mark.parametrize("t", _tables(), ids=lambda t: t["name"])
+def test_patch_status(gpu, t, frac):
+    rng = np.random.default_rng(int(frac * 1e4) + t["ids"].shape[0])
+    targets = TB.adversarial_targets(t, extra=3000)
+    st = t["status"].copy()
+    with DeviceTable(t["ids"], st, t["first"], t["off"], device=0, sorted=t["sorted"]) as T:
+        for rep in range(3):  # repeated patches: the flags must be cleared and the state consistent
+            nodes, new, st = _flip(rng, st, frac)
+            T.patch_status(nodes, new)
+            assert T.info()["n_good"] == int((st & 1).sum())
+            _check(T, t, st, targets, gpu, rt=RT_COUNTS if rep == 2 else (1, 8, 16, 32),
+                   nc=NC_COUNTS if rep == 2 else (1, 14, 32))
+
+
+def test_patch_status_neighbourhood(gpu):
+    """Flips concentrated in one region (every node of 40 consecutive buckets): windows that grow or
+    shrink by several rounds, lines deferred and un-deferred, targets right there."""
+    t = TB.uniform_config(40_000, 12, seed=0x5E4)
+    off = t["off"]
+    b0 = 1000
+    nodes = np.arange(off[b0], off[b0 + 40], dtype=np.uint32)
+    near = t["ids"][off[b0 - 10]:off[b0 + 50]]
+    targets = np.ascontiguousarray(np.concatenate([TB.adversarial_targets(t, extra=1000), near]))
+    with DeviceTable(t["ids"], t["status"], t["first"], t["off"], device=0, sorted=True) as T:
+        st = t["status"].copy()
+        st[nodes] = 0  # the region goes dubious
+        T.patch_status(nodes, st[nodes])
+        _check(T, t, st, targets, gpu)
+        st[nodes] = 1  # and comes back good
+        T.patch_status(nodes, st[nodes])
+        _check(T, t, st, targets, gpu)
+
+
+def test_update_status_full_array_incremental(gpu):
+    t = TB.uniform_config(30_000, 12, seed=0x5E5)
+    rng = np.random.default_rng(9)
+    targets = TB.adversarial_targets(t, extra=2000)
+    with DeviceTable(t["ids"], t["status"], t["first"], t["off"], device=0, sorted=True) as T:
+        _, _, st = _flip(rng, t["status"], 0.01)
+        T.update_status(st)
+        _check(T, t, st, targets, gpu)
+
+
+def test_moving_now(gpu):
+    """Node times on the device, `now` advancing: nodes age past 10 min (time) and 120 min (reply_time),
+    then some are heard again (patch_times) and some expire."""
+    t = TB.uniform_config(50_000, 13, seed=0x5E6)
+    n = t["ids"].shape[0]
+    rng = np.random.default_rng(11)
+    targets = TB.adversarial_targets(t, extra=2000)
+    MIN = 60 * 10**9
+    now = 100 * 3600 * 10**9
+    time_ns = now - rng.integers(0, 10 * MIN, n)         # all heard within the last 10 min
+    reply_ns = now - rng.integers(0, 120 * MIN, n)       # all replied within 120 min
+    expired = (rng.random(n) < 0.05).astype(np.uint8)
+
+    def status_at(tnow):
+        good = (expired == 0) & (reply_ns >= tnow - 120 * MIN) & (time_ns >= tnow - 10 * MIN)
+        return (good.astype(np.uint8) | (expired << 1)).astype(np.uint8)
+
+    with DeviceTable(t["ids"], status_at(now), t["first"], t["off"], device=0, sorted=True) as T:
+        T.set_times(time_ns, reply_ns, expired)
+        for dt in (1, 5 * 10**8, 10 * 10**9, 60 * 10**9, 3 * MIN):  # small steps: ~0.01 % .. 30 % flips
+            now += dt
+            T.refresh_status(now)
+            torch.cuda.synchronize()
+            _check(T, t, status_at(now), targets, gpu, rt=(1, 8, 14, 32), nc=(1, 14, 32))
+        # 1 % of the nodes answer now; 0.5 % get expired (setExpired); refresh at the same now
+        heard = rng.choice(n, size=n // 100, replace=False).astype(np.uint32)
+        time_ns[heard] = now
+        reply_ns[heard] = now
+        gone = rng.choice(n, size=n // 200, replace=False).astype(np.uint32)
+        expired[gone] = 1
+        sel = np.unique(np.concatenate([heard, gone])).astype(np.uint32)
+        T.patch_times(sel, time_ns[sel], reply_ns[sel], expired[sel])
+        T.refresh_status(now)
+        torch.cuda.synchronize()
+        _check(T, t, status_at(now), targets, gpu)
+
+
+def test_patch_rejects_bad_index(gpu):
+    t = TB.uniform_config(2000, 8, seed=0x5E7)
+    from opendht_amd._lib import KadError
+
+    with DeviceTable(t["ids"], t["status"], t["first"], t["off"], device=0) as T:
+        with pytest.raises(KadError):
+            T.patch_status(np.array([t["ids"].shape[0]], np.uint32), np.array([1], np.uint8))
+        with pytest.raises(KadError):  # no times uploaded yet
+            T.patch_times(np.array([0], np.uint32), np.array([0]), np.array([0]), np.array([0], np.uint8))

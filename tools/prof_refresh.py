@@ -1,0 +1,61 @@
+"""Incremental status refresh on the bench shard (1/8 of the 100M-node U(24) table), for a rocprofv3
+kernel trace: refresh_status(now) with no flips, then with 0.001 % / 0.1 % / 1 % of the good nodes ageing
+past 10 min, then patch_status lists of the same sizes.
+
+    rocprofv3 --kernel-trace --stats -d gpurun_out/x -o run -- python3 tools/prof_refresh.py
+"""
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from bench import node_times  # noqa: E402
+from opendht_amd import DeviceTable  # noqa: E402
+from opendht_amd.sharded import ShardSpec, build_shard  # noqa: E402
+
+sh = build_shard(ShardSpec(), 0)
+T = DeviceTable(sh.ids, sh.status, sh.first, sh.off, device=0, index_base=sh.index_base, sorted=True)
+now = 10**15
+t, rt, ex = node_times(sh.status, now)
+T.set_times(t, rt, ex)
+T.refresh_status(now)
+torch.cuda.synchronize()
+rng = np.random.default_rng(1)
+good = np.flatnonzero(sh.status & 1).astype(np.uint32)
+res = {}
+for j in range(3):
+    a = time.perf_counter()
+    T.refresh_status(now + 1 + j)
+    torch.cuda.synchronize()
+    res.setdefault("no_flip_ms", []).append((time.perf_counter() - a) * 1e3)
+now += 10
+for frac in (0.00001, 0.001, 0.01):
+    for rep in range(2):
+        sel = rng.choice(good, size=max(1, int(good.shape[0] * frac)), replace=False).astype(np.uint32)
+        now += 10**9
+        T.patch_times(sel, np.full(sel.shape[0], now - 10 * 60 * 10**9 - 1, np.int64),
+                      np.full(sel.shape[0], now, np.int64), np.zeros(sel.shape[0], np.uint8))
+        torch.cuda.synchronize()
+        a = time.perf_counter()
+        T.refresh_status(now)
+        torch.cuda.synchronize()
+        res.setdefault(f"ageing_{frac:g}_ms", []).append((time.perf_counter() - a) * 1e3)
+        T.patch_times(sel, np.full(sel.shape[0], now, np.int64), np.full(sel.shape[0], now, np.int64),
+                      np.zeros(sel.shape[0], np.uint8))
+        T.refresh_status(now)
+        torch.cuda.synchronize()
+n = sh.ids.shape[0]
+st = sh.status.copy()
+for frac in (0.00001, 0.001, 0.01, 0.1):
+    nodes = rng.choice(n, size=max(1, int(n * frac)), replace=False).astype(np.uint32)
+    a = time.perf_counter()
+    T.patch_status(nodes, st[nodes] ^ np.uint8(1))
+    res[f"patch_{frac:g}_ms"] = (time.perf_counter() - a) * 1e3
+    T.patch_status(nodes, st[nodes])
+print({k: (np.round(v, 3).tolist() if isinstance(v, list) else round(v, 3)) for k, v in res.items()})
+T.close()
