@@ -66,6 +66,9 @@ extern "C" {
 /* kad_table_info.flags, reported only */
 #define KAD_INFO_WINDOW_LINES 0x100u /* uniform-depth table: count <= 8 queries use one 128-byte
                                         window line per query (rt_wl_kernel) */
+#define KAD_INFO_GENERAL_LINES 0x200u /* any other bucket shape: count <= 8 queries use one 128-byte
+                                         general window line per query (rt_gl_kernel) */
+#define KAD_INFO_GENERAL_LINES32 0x400u /* ... and counts 9..32 one 256-byte line (rt_gl32_kernel) */
 
 /* error codes */
 #define KAD_OK 0

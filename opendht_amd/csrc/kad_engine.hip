@@ -94,6 +94,8 @@ struct DevTable {
     const uint4* wl16;  // window lines for counts 9..16 (TF_WL16): 128 bytes per bucket
     const uint4* wl32;  // window lines for counts 17..32 (TF_WL32): 256 bytes per bucket
     const uint4* ncl;   // NodeCache lines (TF_NCL): 256 bytes per node radix slot
+    const uint4* gl;    // general window lines, count <= 8 (TF_GL, any table shape): 128 bytes per bucket
+    const uint4* gl32;  // general window lines, counts 9..32 (TF_GL32): 256 bytes per bucket
     uint64_t rbase, nbase;
     uint32_t rshift, rslots, nshift, nslots;
     uint32_t n, B, index_base, flags;
@@ -105,6 +107,8 @@ constexpr uint32_t TF_WL = 8u;       // window lines present (direct-mapped, uni
 constexpr uint32_t TF_WL16 = 16u;    // window lines for counts 9..16 present
 constexpr uint32_t TF_WL32 = 32u;    // window lines for counts 17..32 present
 constexpr uint32_t TF_NCL = 64u;     // NodeCache lines present (sorted tables)
+constexpr uint32_t TF_GL = 128u;     // general window lines (tables without TF_WL: split-policy, per-peer shapes)
+constexpr uint32_t TF_GL32 = 256u;   // general window lines for counts 9..32
 constexpr uint32_t WIDE = 0x80000000u;  // dir[].x flag: bucket holds > 32 nodes (masks invalid)
 constexpr uint32_t KEY_PAD = 32;        // key[] is padded so 16-node chunk loads never leave it
 
@@ -1318,6 +1322,317 @@ __global__ __launch_bounds__(BLOCK) void wl32_build_kernel(const uint64_t* key, 
     L[4] = r04;
     L[5] = r15;
     store_line<WL32_STRIDE>(L, lines + (size_t)WL32_STRIDE * b);
+}
+
+// ---------------------------------------------------------------------------------------
+// General window lines (TF_GL / TF_GL32): one line per bucket for tables of ANY bucket shape -- the
+// reference split policy (dht.cpp:903-934), per-peer K tables, shards -- where the uniform-depth lines
+// above do not apply. The bucket of the target comes from the locate radix (locate_bucket).
+//
+// Every ID of the window W(R) = [lo, hi] lies in [first_lo, end) (end = first_{hi+1}, or 2^160 after the
+// last bucket), and so does every target of bucket b (except a target below the first bucket, which
+// findBucket clamps to bucket 0: exact path). All of them share that range's common prefix of cp bits,
+// so the XOR distance of two window nodes to the target compares like their ID bits [cp, cp+24) XOR the
+// target's, unless two stored nodes agree on those 24 bits (the line is then marked defer). A slot is
+// key24 << 8 | off (off = node index - base < 256); a query XORs every slot with t24 << 8 and keeps the
+// smallest: (distance, offset) order, no bucket ranks needed.
+//
+// Which nodes a line stores: all good nodes of W(R) when they fit; otherwise whole buckets in D order
+// (the order of their XOR images, first_c ^ first_b), as the uniform lines do. That order holds for every
+// target of b unless two window buckets first differ at a bit >= b's depth (or b is not dyadic): such a
+// line is marked defer when it had to truncate. Slots are placed ring by ring (W(0), then the buckets
+// added by round 1, ...), so the stored nodes of W(r) are exactly the first S_r slots: a count with a
+// smaller window R_c masks the slots from S_{R_c} on, and the answer is exact when S_{R_c} >= m.
+//
+// GL (count <= 8, 32 dwords):                      GL32 (counts 9..32, 64 dwords):
+//   dw0  base                                        dw0  base
+//   dw1  G(0..2) 6 bits | whole(r) << 18 |           dw1, 2  G(0..7), 8 bits each
+//        R_8 << 21 | S << 23 | defer << 31           dw3  whole(r) | R_32 << 8 | S << 12 | defer << 31
+//   dw2  S_0 | S_1 << 5 | cp << 10                   dw4  S_0..S_4, 6 bits each; dw5 S_5 | S_6 << 6 | cp << 12
+//   dw4..27  24 slots                                dw6..63  58 slots
+// Reference semantics: routing_table.cpp:67-111 (window rounds, sorted insertion, truncation).
+// ---------------------------------------------------------------------------------------
+constexpr uint32_t GL_SLOTS = 24, GL_HDR = 4, GL_STRIDE = 32;
+constexpr uint32_t GL32_SLOTS = 58, GL32_HDR = 6, GL32_STRIDE = 64;
+constexpr uint32_t GL_MAXCP = 40;  // key24 = ID bits [cp, cp + 24) from the top 64 bits
+
+// A target below the first bucket (findBucket clamps it to bucket 0; it shares no window prefix).
+__device__ __forceinline__ bool below_first(const DevTable& T, const Target& t) {
+    const uint32_t* ft = T.ftail;
+    return cmp160(t.hi, t.t2, t.t3, t.t4, T.fkey[0], ft[0], ft[1], ft[2]) < 0;
+}
+
+__device__ __forceinline__ bool gl_answer(const DevTable& T, const Target& t, uint32_t b, uint32_t count, bool act,
+                                          uint32_t (&o)[8], uint32_t& m) {
+    uint4 L[8];
+    if (act) {
+        const uint4* lp = T.gl + (GL_STRIDE / 4) * (size_t)b;
+#pragma unroll
+        for (int x = 0; x < 8; x++) L[x] = lp[x];
+    } else {
+#pragma unroll
+        for (int x = 0; x < 8; x++) L[x] = make_uint4(NONE, NONE, NONE, NONE);
+    }
+    const uint32_t h = L[0].y, h2 = L[0].z;
+    const uint32_t G0 = h & 63u, G1 = (h >> 6) & 63u, G2 = (h >> 12) & 63u, R = (h >> 21) & 3u, S = (h >> 23) & 31u;
+    const uint32_t Rc = (G0 >= count || (h >> 18) & 1u) ? 0u : (G1 >= count || (h >> 19) & 1u) ? 1u : 2u;
+    m = min(count, Rc == 0 ? G0 : Rc == 1 ? G1 : G2);
+    const uint32_t lim = Rc >= R ? S : Rc == 0 ? (h2 & 31u) : ((h2 >> 5) & 31u);
+    bool ex = !act || (h & WL_DEFER) || lim < m || Rc > R;
+    if (act && b == 0) ex |= below_first(T, t);
+    const uint32_t cp = (h2 >> 10) & 63u;
+    const uint32_t tx = (uint32_t)((t.hi << (cp & 63u)) >> 40) << 8;
+    uint32_t v[GL_SLOTS];
+#pragma unroll
+    for (int s = 0; s < (int)GL_SLOTS; s++) v[s] = (uint32_t)s < lim ? dw(L, GL_HDR + s) ^ tx : NONE;
+    sort8(v);
+    sort8(v + 8);
+    sort8(v + 16);
+    merge8(v, v + 8);
+    merge8(v, v + 16);
+    const uint32_t base = L[0].x + T.index_base;
+#pragma unroll
+    for (int j = 0; j < 8; j++) o[j] = (uint32_t)j < m ? base + (v[j] & 255u) : NONE;
+    return !ex;
+}
+
+__global__ __launch_bounds__(BLOCK) void rt_gl_kernel(DevTable T, const uint8_t* __restrict__ targets, uint32_t q,
+                                                      uint32_t count, uint32_t* __restrict__ out_idx,
+                                                      uint8_t* __restrict__ out_cnt) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    const bool act = i < q && count > 0;
+    if (i < q && count == 0 && out_cnt) out_cnt[i] = 0;
+    Target t{};
+    uint32_t b = 0;
+    if (act) {
+        t = load_target(targets, i);
+        b = locate_bucket(T, t);
+    }
+    uint32_t o[8], m;
+    const bool ok = gl_answer(T, t, b, count, act, o, m);
+    if (act && ok) {
+        store_row8(out_idx + (size_t)i * count, o, count);
+        if (out_cnt) out_cnt[i] = (uint8_t)m;
+    }
+    __shared__ uint64_t xs[BLOCK / 64][192];
+    exact_tail(T, t, act && !ok, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
+}
+
+__device__ __forceinline__ bool gl32_answer(const DevTable& T, const Target& t, uint32_t b, uint32_t count, bool act,
+                                            uint32_t (&o)[32], uint32_t& m) {
+    uint32_t L[GL32_STRIDE], v[64];
+    if (act) {
+        const uint4* lp = T.gl32 + (GL32_STRIDE / 4) * (size_t)b;
+#pragma unroll
+        for (int x = 0; x < (int)GL32_STRIDE / 4; x++) {
+            const uint4 u = lp[x];
+            L[4 * x] = u.x; L[4 * x + 1] = u.y; L[4 * x + 2] = u.z; L[4 * x + 3] = u.w;
+        }
+    } else {
+#pragma unroll
+        for (int x = 0; x < (int)GL32_STRIDE; x++) L[x] = NONE;
+    }
+    const uint32_t h = L[3], S = (h >> 12) & 127u, R = (h >> 8) & 15u;
+    uint32_t Rc = 8, Gc = 0;
+#pragma unroll
+    for (int r = 7; r >= 0; r--) {
+        const uint32_t g = (L[1 + (r >> 2)] >> (8 * (r & 3))) & 255u;
+        if (g >= count || ((h >> r) & 1u)) { Rc = (uint32_t)r; Gc = g; }
+    }
+    m = min(count, Gc);
+    uint32_t lim = S;
+#pragma unroll
+    for (int r = 0; r < 7; r++) {
+        const uint32_t sr = r < 5 ? (L[4] >> (6 * r)) & 63u : (L[5] >> (6 * (r - 5))) & 63u;
+        if ((uint32_t)r == Rc && Rc < R) lim = sr;
+    }
+    bool ex = !act || (h & WL_DEFER) || Rc > R || lim < m;
+    if (act && b == 0) ex |= below_first(T, t);
+    const uint32_t cp = (L[5] >> 12) & 63u;
+    const uint32_t tx = (uint32_t)((t.hi << (cp & 63u)) >> 40) << 8;
+#pragma unroll
+    for (int s = 0; s < 64; s++) {
+        const int li = s < (int)GL32_SLOTS ? (int)GL32_HDR + s : 0;
+        v[s] = s < (int)GL32_SLOTS && (uint32_t)s < lim ? L[li] ^ tx : NONE;
+    }
+    sort16(v);
+    sort16(v + 16);
+    sort16(v + 32);
+    sort16(v + 48);
+    join_sorted<16>(v);
+    join_sorted<16>(v + 32);
+    merge32(v, v + 32);
+    const uint32_t base = L[0] + T.index_base;
+#pragma unroll
+    for (int j = 0; j < 32; j++) o[j] = (uint32_t)j < m ? base + (v[j] & 255u) : NONE;
+    return !ex;
+}
+
+__global__ __launch_bounds__(BLOCK) void rt_gl32_kernel(DevTable T, const uint8_t* __restrict__ targets, uint32_t q,
+                                                        uint32_t count, uint32_t* __restrict__ out_idx,
+                                                        uint8_t* __restrict__ out_cnt) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    const bool act = i < q;
+    Target t{};
+    uint32_t b = 0;
+    if (act) {
+        t = load_target(targets, i);
+        b = locate_bucket(T, t);
+    }
+    uint32_t o[32], m;
+    const bool ok = gl32_answer(T, t, b, count, act, o, m);
+    if (act && ok && out_cnt) out_cnt[i] = (uint8_t)m;
+    store_rows_block<32>(out_idx, q, count, o, act && ok);
+    __shared__ uint64_t xs[BLOCK / 64][192];
+    exact_tail(T, t, act && !ok, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
+}
+
+// One general window line of bucket b into L (LDS, W dwords, slots from HDR): see the layout above.
+// NEED = 8 or 32 (the count the window radius is sized for), RMAX = 2 or 7.
+struct GlInfo {
+    uint32_t R, S, cp, base, whole, G[8], Sr[8];
+    bool defer;
+};
+
+template <int RMAX, uint32_t NEED, uint32_t SLOTS, uint32_t HDR>
+__device__ void gl_build_line(const uint64_t* key, const uint8_t* status, const uint2* dir, const uint32_t* gpre,
+                              const uint64_t* fkey, const uint32_t* ftail, uint32_t B, uint32_t b, uint32_t* L,
+                              GlInfo& I) {
+    I.R = RMAX + 1; I.S = 0; I.cp = 0; I.base = 0; I.whole = 0; I.defer = false;
+    for (int r = 0; r < 8; r++) { I.G[r] = 0; I.Sr[r] = 0; }
+    for (uint32_t r = 0; r <= (uint32_t)RMAX; r++) {
+        const uint32_t lo = b > r ? b - 1 - r : 0u, hi = min(B - 1, b + r);
+        I.G[r] = gpre[hi + 1] - gpre[lo];
+        const bool w = lo == 0 && hi == B - 1;
+        I.whole |= (w ? 1u : 0u) << r;
+        if (I.R > (uint32_t)RMAX && (I.G[r] >= NEED || w)) I.R = r;
+    }
+    if (I.R > (uint32_t)RMAX) { I.defer = true; return; }
+    const uint32_t R = I.R, lo = b > R ? b - 1 - R : 0u, hi = min(B - 1, b + R), nb = hi - lo + 1;
+    I.base = dir[lo].x & ~WIDE;
+    // common prefix of the window's ID range [first_lo, end)
+    const uint64_t klo = fkey[lo];
+    uint64_t kend = ~0ull;
+    if (hi + 1 < B) {
+        const uint32_t* te = ftail + 3ull * (hi + 1);
+        kend = fkey[hi + 1] - ((te[0] | te[1] | te[2]) == 0 ? 1ull : 0ull);
+    }
+    const uint32_t cp = klo == kend ? 64u : (uint32_t)__builtin_clzll(klo ^ kend);
+    if (cp > GL_MAXCP) { I.defer = true; return; }
+    I.cp = cp;
+    // D order of the window's buckets (XOR images first_c ^ first_b) and whether it can depend on the target
+    const uint64_t kb = fkey[b];
+    uint32_t ord[16];
+    bool amb = false;
+    for (uint32_t y = lo; y <= hi; y++) {
+        uint32_t rk = 0;
+        for (uint32_t z = lo; z <= hi; z++) {
+            const uint64_t iz = fkey[z] ^ kb, iy = fkey[y] ^ kb;
+            rk += iz < iy || (iz == iy && z < y);
+            amb |= z != y && iz == iy;  // buckets that differ only below bit 64
+        }
+        ord[rk] = y;
+    }
+    {   // b's depth: its size must be a power of two, aligned, with the low 96 bits of both ends zero
+        const uint32_t* tb = ftail + 3ull * b;
+        uint64_t size = (b + 1 < B ? fkey[b + 1] : 0ull) - kb;  // 2^64 wrap for the last bucket
+        bool dy = (tb[0] | tb[1] | tb[2]) == 0 && size && (size & (size - 1)) == 0 && (kb & (size - 1)) == 0;
+        if (b + 1 < B) {
+            const uint32_t* tn = ftail + 3ull * (b + 1);
+            dy &= (tn[0] | tn[1] | tn[2]) == 0;
+        } else if (kb == 0) {
+            dy = true;  // one bucket covers everything: depth 0
+            size = 0;
+        }
+        const uint32_t db = size ? 64u - (uint32_t)__builtin_ctzll(size) : 0u;
+        amb |= !dy;
+        for (uint32_t y = lo; y <= hi && !amb; y++)
+            for (uint32_t z = y + 1; z <= hi; z++)
+                if ((uint32_t)__builtin_clzll((fkey[y] ^ fkey[z]) | 1ull) >= db) { amb = true; break; }
+    }
+    // whole buckets in D order while they fit
+    uint32_t stored = 0, used = 0;  // bit (c - lo)
+    bool full = false;
+    for (uint32_t j = 0; j < nb; j++) {
+        const uint32_t x = ord[j], g = good_of(dir, gpre, x);
+        if (full || used + g > SLOTS) { full = true; continue; }
+        used += g;
+        stored |= 1u << (x - lo);
+    }
+    if (full && amb) { I.defer = true; return; }
+    // slots ring by ring: W(0) = {b-1, b}, round r >= 1 adds b+r and b-1-r
+    uint32_t S = 0;
+    for (uint32_t r = 0; r <= R; r++) {
+        const uint32_t cand[2] = {r == 0 ? b : b + r, b >= r + 1 ? b - 1 - r : NONE};
+        for (int k = 0; k < 2; k++) {
+            const uint32_t x = cand[k];
+            if (x == NONE || x < lo || x > hi || !((stored >> (x - lo)) & 1u)) continue;
+            for_good(key, status, dir, x, [&](uint32_t n, uint64_t kn) {
+                const uint32_t off = n - I.base;
+                I.defer |= off > 255u || (cp && ((kn ^ klo) >> (64 - cp)) != 0);  // outside the window's range
+                const uint32_t k24 = (uint32_t)((kn << cp) >> 40);
+                for (uint32_t u = 0; u < S; u++) I.defer |= (L[HDR + u] >> 8) == k24;
+                L[HDR + S] = (k24 << 8) | (off & 255u);
+                S++;
+            });
+        }
+        I.Sr[r] = S;
+    }
+    I.S = S;
+}
+
+__global__ __launch_bounds__(BLOCK) void gl_build_kernel(const uint64_t* key, const uint8_t* status, const uint2* dir,
+                                                         const uint32_t* gpre, const uint64_t* fkey, const uint32_t* ftail,
+                                                         uint32_t B, uint32_t* lines, LineSel sel) {
+    __shared__ uint32_t lds[BLOCK][GL_STRIDE + 1];
+    uint32_t b;
+    if (!sel.pick(blockIdx.x * BLOCK + threadIdx.x, B, b)) return;
+    uint32_t* L = lds[threadIdx.x];
+    for (uint32_t k = 0; k < GL_STRIDE; k++) L[k] = NONE;
+    GlInfo I;
+    gl_build_line<2, 8, GL_SLOTS, GL_HDR>(key, status, dir, gpre, fkey, ftail, B, b, L, I);
+    uint32_t h = 0;
+    for (int r = 0; r < 3; r++) h |= min(I.G[r], 63u) << (6 * r);
+    h |= (I.whole & 7u) << 18;
+    L[0] = I.base;
+    L[1] = h | (min(I.R, 3u) << 21) | (I.S << 23) | (I.defer ? WL_DEFER : 0u);
+    L[2] = I.Sr[0] | (I.Sr[1] << 5) | (I.cp << 10);
+    L[3] = 0;
+    store_line<GL_STRIDE>(L, lines + (size_t)GL_STRIDE * b);
+}
+
+__global__ __launch_bounds__(BLOCK) void gl32_build_kernel(const uint64_t* key, const uint8_t* status, const uint2* dir,
+                                                           const uint32_t* gpre, const uint64_t* fkey,
+                                                           const uint32_t* ftail, uint32_t B, uint32_t* lines,
+                                                           LineSel sel) {
+    __shared__ uint32_t lds[BLOCK][GL32_STRIDE + 1];
+    uint32_t b;
+    if (!sel.pick(blockIdx.x * BLOCK + threadIdx.x, B, b)) return;
+    uint32_t* L = lds[threadIdx.x];
+    for (uint32_t k = 0; k < GL32_STRIDE; k++) L[k] = NONE;
+    GlInfo I;
+    gl_build_line<7, 32, GL32_SLOTS, GL32_HDR>(key, status, dir, gpre, fkey, ftail, B, b, L, I);
+    uint32_t g01 = 0, g23 = 0;
+    for (int r = 0; r < 8; r++) {
+        const uint32_t g = min(I.G[r], 255u);
+        if (r < 4) g01 |= g << (8 * r); else g23 |= g << (8 * (r - 4));
+    }
+    L[0] = I.base;
+    L[1] = g01;
+    L[2] = g23;
+    L[3] = (I.whole & 255u) | (min(I.R, 15u) << 8) | (I.S << 12) | (I.defer ? WL_DEFER : 0u);
+    L[4] = I.Sr[0] | (I.Sr[1] << 6) | (I.Sr[2] << 12) | (I.Sr[3] << 18) | (I.Sr[4] << 24);
+    L[5] = I.Sr[5] | (I.Sr[6] << 6) | (I.cp << 12);
+    store_line<GL32_STRIDE>(L, lines + (size_t)GL32_STRIDE * b);
+}
+
+// Deferred lines of a line set (decides at table creation whether the general lines pay off).
+__global__ void count_deferred_kernel(const uint32_t* lines, uint32_t stride, uint32_t hdr_word, uint32_t B,
+                                      uint32_t* n) {
+    const uint32_t b = blockIdx.x * BLOCK + threadIdx.x;
+    const bool d = b < B && (lines[(size_t)stride * b + hdr_word] & WL_DEFER);
+    const uint64_t bal = __ballot(d);
+    if ((threadIdx.x & 63) == 0 && bal) atomicAdd(n, (uint32_t)__popcll(bal));
 }
 
 template <int K>
@@ -2861,6 +3176,8 @@ struct kad_table {
     uint32_t* wl16_mut = nullptr;
     uint32_t* wl32_mut = nullptr;
     uint32_t* ncl_mut = nullptr;
+    uint32_t* gl_mut = nullptr;
+    uint32_t* gl32_mut = nullptr;
     // host copies of the bucket directory, for the incremental mirror (kad_table_apply)
     std::vector<uint32_t> h_off;
     std::vector<uint8_t> h_first;
@@ -2924,8 +3241,8 @@ int rebuild_good_prefix(kad_table* t, hipStream_t s, bool full = true) {
                            t->scan_cnt);
     else
         hipLaunchKernelGGL(bucket_good_dirty_kernel, dim3(grid_for(B)), dim3(BLOCK), 0, s, t->d.status, t->dir_mut, B,
-                           t->scan_cnt, t->bdirty, t->wl_mut ? t->ld8 : nullptr, t->wl16_mut ? t->ld16 : nullptr,
-                           t->wl32_mut ? t->ld32 : nullptr);
+                           t->scan_cnt, t->bdirty, (t->wl_mut || t->gl_mut) ? t->ld8 : nullptr,
+                           t->wl16_mut ? t->ld16 : nullptr, (t->wl32_mut || t->gl32_mut) ? t->ld32 : nullptr);
     hipLaunchKernelGGL(scan_tiles_kernel, dim3(tiles), dim3(BLOCK), 0, s, t->scan_cnt, m, t->scan_part, t->scan_sums);
     hipLaunchKernelGGL(scan_sums_kernel, dim3(1), dim3(BLOCK), 0, s, t->scan_sums, tiles);
     hipLaunchKernelGGL(scan_apply_kernel, dim3(grid_for(m)), dim3(BLOCK), 0, s, t->scan_part, t->scan_sums, m, t->gpre_mut);
@@ -2945,7 +3262,63 @@ int rebuild_good_prefix(kad_table* t, hipStream_t s, bool full = true) {
     if (t->wl32_mut)
         hipLaunchKernelGGL(wl32_build_kernel, dim3(grid_for(B)), dim3(BLOCK), 0, s, t->d.key, t->d.status, t->d.dir,
                            t->d.gpre, B, 64 - t->d.rshift, t->d.rbase >> t->d.rshift, t->wl32_mut, sel_for(t->ld32, 2));
+    if (t->gl_mut)
+        hipLaunchKernelGGL(gl_build_kernel, dim3(grid_for(B)), dim3(BLOCK), 0, s, t->d.key, t->d.status, t->d.dir,
+                           t->d.gpre, t->d.fkey, t->d.ftail, B, t->gl_mut, sel_for(t->ld8, 0));
+    if (t->gl32_mut)
+        hipLaunchKernelGGL(gl32_build_kernel, dim3(grid_for(B)), dim3(BLOCK), 0, s, t->d.key, t->d.status, t->d.dir,
+                           t->d.gpre, t->d.fkey, t->d.ftail, B, t->gl32_mut, sel_for(t->ld32, 2));
     HIP_TRY(hipGetLastError());
+    return KAD_OK;
+}
+
+// General window lines (TF_GL / TF_GL32) for a table without uniform-depth lines: allocated, built from the
+// current status, and kept only when at most 1/16 of them are deferred (otherwise the lane kernel is the
+// faster path). Synchronous. A failure leaves the table without general lines (still correct).
+int setup_general_lines(kad_table* t) {
+    DevTable& d = t->d;
+    if (d.B == 0 || (d.flags & TF_WL) || !d.fkey) return KAD_OK;
+    const uint32_t B = d.B;
+    uint32_t *lp = nullptr, *lp32 = nullptr, *cnt = nullptr;
+    int rc;
+    std::vector<void*> fresh;
+    uint64_t fb = 0;
+    auto drop = [&]() { for (void* p : fresh) (void)hipFree(p); };
+    if ((rc = dev_upload(&lp, nullptr, (size_t)GL_STRIDE * B, fresh, fb)) ||
+        (rc = dev_upload(&lp32, nullptr, (size_t)GL32_STRIDE * B, fresh, fb)) ||
+        (rc = dev_upload(&cnt, nullptr, 2, fresh, fb))) {
+        drop();
+        return KAD_OK;
+    }
+    if (hipMemset(cnt, 0, 8) != hipSuccess) { drop(); return KAD_OK; }
+    hipLaunchKernelGGL(gl_build_kernel, dim3(grid_for(B)), dim3(BLOCK), 0, 0, d.key, d.status, d.dir, d.gpre, d.fkey,
+                       d.ftail, B, lp, LineSel{});
+    hipLaunchKernelGGL(gl32_build_kernel, dim3(grid_for(B)), dim3(BLOCK), 0, 0, d.key, d.status, d.dir, d.gpre, d.fkey,
+                       d.ftail, B, lp32, LineSel{});
+    hipLaunchKernelGGL(count_deferred_kernel, dim3(grid_for(B)), dim3(BLOCK), 0, 0, lp, GL_STRIDE, 1u, B, cnt);
+    hipLaunchKernelGGL(count_deferred_kernel, dim3(grid_for(B)), dim3(BLOCK), 0, 0, lp32, GL32_STRIDE, 3u, B, cnt + 1);
+    uint32_t nd[2] = {B, B};
+    if (hipGetLastError() != hipSuccess || hipMemcpy(nd, cnt, 8, hipMemcpyDeviceToHost) != hipSuccess) {
+        drop();
+        return set_err(KAD_ERR_HIP, "general window-line build failed");
+    }
+    (void)hipFree(cnt);
+    fresh.pop_back();
+    fb -= 16;
+    const bool keep8 = (uint64_t)nd[0] * 16 <= B, keep32 = (uint64_t)nd[1] * 16 <= B;
+    if (std::getenv("KAD_DEBUG")) std::fprintf(stderr, "general lines: B=%u deferred %u / %u\n", B, nd[0], nd[1]);
+    if (keep8) {
+        t->owned.push_back(lp); t->bytes += (uint64_t)GL_STRIDE * 4 * B;
+        t->gl_mut = lp; d.gl = reinterpret_cast<const uint4*>(lp); d.flags |= TF_GL;
+    } else {
+        (void)hipFree(lp);
+    }
+    if (keep32) {
+        t->owned.push_back(lp32); t->bytes += (uint64_t)GL32_STRIDE * 4 * B;
+        t->gl32_mut = lp32; d.gl32 = reinterpret_cast<const uint4*>(lp32); d.flags |= TF_GL32;
+    } else {
+        (void)hipFree(lp32);
+    }
     return KAD_OK;
 }
 
@@ -2964,9 +3337,9 @@ int ensure_marks(kad_table* t) {
     };
     int rc;
     if ((rc = alloc(&t->bdirty, t->d.B))) return rc;
-    if (t->wl_mut && (rc = alloc(&t->ld8, t->d.B))) return rc;
+    if ((t->wl_mut || t->gl_mut) && (rc = alloc(&t->ld8, t->d.B))) return rc;
     if (t->wl16_mut && (rc = alloc(&t->ld16, t->d.B))) return rc;
-    if (t->wl32_mut && (rc = alloc(&t->ld32, t->d.B))) return rc;
+    if ((t->wl32_mut || t->gl32_mut) && (rc = alloc(&t->ld32, t->d.B))) return rc;
     if (t->ncl_mut && (rc = alloc(&t->ndirty, t->d.nslots))) return rc;
     uint8_t *l = reinterpret_cast<uint8_t*>(t->dlist), *c = reinterpret_cast<uint8_t*>(t->dctr);
     if ((rc = alloc(&l, 4 * (3ull * t->d.B + (t->ncl_mut ? t->d.nslots : 0u) + 1)))) return rc;
@@ -3038,6 +3411,10 @@ int launch_rt(const kad_table* t, const uint8_t* targets, uint32_t q, uint32_t c
             hipLaunchKernelGGL(rt_wl16_kernel<0>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
     } else if (K == 32 && (d.flags & TF_WL32) && !(ev && std::strcmp(ev, "lane") == 0)) {
         hipLaunchKernelGGL(rt_wl32_kernel, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
+    } else if (K == 8 && (d.flags & TF_GL) && !(ev && std::strcmp(ev, "lane") == 0)) {
+        hipLaunchKernelGGL(rt_gl_kernel, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
+    } else if (K > 8 && (d.flags & TF_GL32) && !(ev && std::strcmp(ev, "lane") == 0)) {
+        hipLaunchKernelGGL(rt_gl32_kernel, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
     } else {
         hipLaunchKernelGGL(rt_closest_kernel<K>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
     }
@@ -3304,6 +3681,11 @@ int kad_table_create(kad_table** out, int device, uint32_t n_nodes, const uint8_
             }
         }
     }
+    // general window lines for every other bucket shape (split policy, per-peer tables, shards)
+    if (n_buckets && !(d.flags & TF_WL) && (rc = setup_general_lines(t))) {
+        delete t;
+        return rc;
+    }
     // NodeCache radix
     if ((flags & KAD_TABLE_SORTED) && n_nodes) {
         uint32_t tb = 1;
@@ -3342,7 +3724,8 @@ int kad_table_get_info(const kad_table* t, kad_table_info* out) {
     out->n_nodes = t->d.n;
     out->n_buckets = t->d.B;
     out->index_base = t->d.index_base;
-    out->flags = t->flags | ((t->d.flags & TF_WL) ? KAD_INFO_WINDOW_LINES : 0u);
+    out->flags = t->flags | ((t->d.flags & TF_WL) ? KAD_INFO_WINDOW_LINES : 0u) |
+                 ((t->d.flags & TF_GL) ? KAD_INFO_GENERAL_LINES : 0u) | ((t->d.flags & TF_GL32) ? KAD_INFO_GENERAL_LINES32 : 0u);
     out->device = t->device;
     out->rt_radix_bits = t->rbits;
     out->nc_radix_bits = t->nbits;
@@ -4072,6 +4455,10 @@ int kad_table_apply(kad_table* t, const uint32_t* ops, uint32_t n_ops, const uin
         release(t, t->wl16_mut); t->wl16_mut = nullptr; d.wl16 = nullptr; d.flags &= ~TF_WL16;
         release(t, t->wl32_mut); t->wl32_mut = nullptr; d.wl32 = nullptr; d.flags &= ~TF_WL32;
     }
+    if (reshape) {  // general lines are per bucket: re-created below for the new bucket count
+        release(t, t->gl_mut); t->gl_mut = nullptr; d.gl = nullptr; d.flags &= ~TF_GL;
+        release(t, t->gl32_mut); t->gl32_mut = nullptr; d.gl32 = nullptr; d.flags &= ~TF_GL32;
+    }
     release(t, const_cast<uint32_t*>(d.dmask));
     d.dmask = ddm;
     d.flags = any ? (d.flags | TF_HAS_DUP) : (d.flags & ~TF_HAS_DUP);
@@ -4081,6 +4468,8 @@ int kad_table_apply(kad_table* t, const uint32_t* ops, uint32_t n_ops, const uin
     // masks, good prefix sums, window lines
     if ((rc = rebuild_good_prefix(t, nullptr))) return rc;
     HIP_TRY(hipDeviceSynchronize());
+    // a table that lost (or never had) uniform-depth lines gets general ones (built from the new state)
+    if (!(d.flags & TF_WL) && !t->gl_mut && !t->gl32_mut && (rc = setup_general_lines(t))) return rc;
     return KAD_OK;
 }
 

@@ -12,9 +12,11 @@
 #include <cmath>
 #include <cstdint>
 #include <cstring>
+#include <map>
 #include <random>
 #include <set>
 #include <thread>
+
 #include <vector>
 
 #include "../../include/kadgpu.h"
@@ -165,56 +167,59 @@ int kad_split_table(uint32_t n, const uint8_t* ids, uint32_t cap, uint32_t* out_
                     uint32_t* out_offset, uint32_t* out_n_buckets) {
     if (n && !ids) return KAD_ERR_INVALID;
     if (!out_perm || !out_first || !out_offset || !out_n_buckets || cap == 0) return KAD_ERR_INVALID;
-    // Flat mirror of the list-of-buckets: firsts ascending, per-bucket node lists in
-    // RoutingTable list order (front = most recently emplaced, dht.cpp:934).
-    std::vector<Id> first(1);
-    first[0].fill(0);  // the initial bucket covers the whole space from zeroes
-    std::vector<std::vector<uint32_t>> nodes(1);
-    auto find_bucket = [&](const uint8_t* id) -> size_t {
-        // routing_table.cpp:113-127: last bucket with first <= id, clamped to 0
-        size_t lo = 0, hi = first.size();
-        while (lo < hi) {
-            size_t mid = (lo + hi) / 2;
-            if (cmp_id(first[mid].data(), id) <= 0) lo = mid + 1; else hi = mid;
-        }
-        return lo == 0 ? 0 : lo - 1;
+    // The list of buckets as an ordered map first -> node list (RoutingTable list order inside a bucket:
+    // front = most recently emplaced, dht.cpp:934); O(log B) per findBucket and per split.
+    struct IdLess {
+        bool operator()(const Id& a, const Id& b) const { return cmp_id(a.data(), b.data()) < 0; }
     };
-    auto split = [&](size_t b) -> bool {
+    using Map = std::map<Id, std::vector<uint32_t>, IdLess>;
+    Map buckets;
+    Id zero;
+    zero.fill(0);  // the initial bucket covers the whole space from zeroes
+    buckets.emplace(zero, std::vector<uint32_t>());
+    auto find_bucket = [&](const uint8_t* id) -> Map::iterator {
+        // routing_table.cpp:113-127: last bucket with first <= id, clamped to the first bucket
+        Id key;
+        std::memcpy(key.data(), id, 20);
+        auto it = buckets.upper_bound(key);
+        return it == buckets.begin() ? it : std::prev(it);
+    };
+    auto split = [&](Map::iterator b) -> bool {
         // depth (routing_table.cpp:59-65), middle (:47-57), split (:137-163)
-        const int bit1 = lowbit(first[b].data());
-        const int bit2 = b + 1 < first.size() ? lowbit(first[b + 1].data()) : -1;
+        const auto next = std::next(b);
+        const int bit1 = lowbit(b->first.data());
+        const int bit2 = next != buckets.end() ? lowbit(next->first.data()) : -1;
         const int bit = std::max(bit1, bit2) + 1;
         if (bit >= 160) return false;
-        Id mid = first[b];
+        Id mid = b->first;
         mid[bit / 8] |= (uint8_t)(0x80 >> (bit % 8));
-        first.insert(first.begin() + b + 1, mid);
-        nodes.insert(nodes.begin() + b + 1, std::vector<uint32_t>());
+        auto nb = buckets.emplace_hint(next, mid, std::vector<uint32_t>());
         std::vector<uint32_t> moving;
-        moving.swap(nodes[b]);
+        moving.swap(b->second);
         for (uint32_t idx : moving) {  // each spliced to the FRONT of its bucket, in list order
-            const size_t nb = cmp_id(ids + 20ull * idx, mid.data()) < 0 ? b : b + 1;
-            nodes[nb].insert(nodes[nb].begin(), idx);
+            auto& dst = cmp_id(ids + 20ull * idx, mid.data()) < 0 ? b->second : nb->second;
+            dst.insert(dst.begin(), idx);
         }
         return true;
     };
     for (uint32_t i = 0; i < n; i++) {
         const uint8_t* id = ids + 20ull * i;
         bool placed = true;
-        size_t b = find_bucket(id);
-        while (nodes[b].size() >= cap) {
+        auto b = find_bucket(id);
+        while (b->second.size() >= cap) {
             if (!split(b)) { placed = false; break; }  // unsplittable: the node is cached away, not added
             b = find_bucket(id);
         }
-        if (placed) nodes[b].insert(nodes[b].begin(), i);
+        if (placed) b->second.insert(b->second.begin(), i);
     }
-    uint32_t k = 0;
-    for (size_t b = 0; b < first.size(); b++) {
-        std::memcpy(out_first + 20ull * b, first[b].data(), 20);
-        out_offset[b] = k;
-        for (uint32_t idx : nodes[b]) out_perm[k++] = idx;
+    uint32_t k = 0, j = 0;
+    for (const auto& kv : buckets) {
+        std::memcpy(out_first + 20ull * j, kv.first.data(), 20);
+        out_offset[j++] = k;
+        for (uint32_t idx : kv.second) out_perm[k++] = idx;
     }
-    out_offset[first.size()] = k;
-    *out_n_buckets = (uint32_t)first.size();
+    out_offset[j] = k;
+    *out_n_buckets = j;
     return KAD_OK;
 }
 

@@ -1,0 +1,87 @@
+"""General window lines (rt_gl_kernel / rt_gl32_kernel): RoutingTable::findClosestNodes on tables of any
+bucket shape -- the reference split policy (dht.cpp:903-934, routing_table.cpp:137-163) at 10k..300k
+nodes, a mostly-bad one and a clustered one (neighbouring buckets of very different depths) -- bit-exact
+against the oracle for every count 1..32, with the tables confirmed to carry the general lines (so the
+new path is the one under test), before and after status changes and mirror mutations."""
+import numpy as np
+import pytest
+import torch
+
+import oracle as O
+import tables as TB
+from opendht_amd import DeviceTable
+from opendht_amd import synth as S
+from opendht_amd._lib import KAD_INFO_GENERAL_LINES, KAD_INFO_GENERAL_LINES32, KAD_INFO_WINDOW_LINES, KAD_OP_SPLIT
+
+pytestmark = pytest.mark.gpu
+
+ALL = tuple(range(1, 33))
+
+
+def _check(T, t, targets, gpu, counts=ALL, status=None):
+    st = t["status"] if status is None else status
+    tg = torch.from_numpy(np.ascontiguousarray(targets)).to(gpu)
+    for k in counts:
+        idx, cnt = T.rt_closest(tg, k)
+        torch.cuda.synchronize()
+        want, wcnt = O.flat_rt_closest(t["ids"], st, t["first"], t["off"], targets, k, nthreads=8)
+        np.testing.assert_array_equal(cnt.cpu().numpy(), wcnt, err_msg=f"{t['name']} k={k} counts")
+        np.testing.assert_array_equal(idx.cpu().numpy().view(np.uint32), want, err_msg=f"{t['name']} k={k}")
+
+
+def _s_tables():
+    out = [TB.split_config(10_000, seed=0x61), TB.split_config(100_000, seed=0x62),
+           TB.split_config(300_000, seed=0x63, good=60, expired=25)]
+    # mostly bad: windows grow past the lines' rounds, the table keeps the lane kernel (no general lines)
+    bad = TB.split_config(20_000, seed=0x69, good=15, expired=40)
+    bad["name"] = "S20000_mostly_bad"
+    bad["lane"] = True
+    out.append(bad)
+    # a split table of clustered IDs: neighbouring buckets of very different depths
+    rng = np.random.default_rng(0x64)
+    base = S.random_ids(20_000, 0x64)
+    cl = np.repeat(base[:8], 500, 0)
+    cl[:, 3:] = rng.integers(0, 256, (4000, 17), dtype=np.uint8)
+    ids = np.unique(np.concatenate([base, cl]), axis=0)
+    rng.shuffle(ids)
+    perm, first, off = S.split_table(ids)
+    out.append(TB.table(ids[perm], S.random_status(perm.shape[0], 0x65), first, off, name="S_clustered"))
+    return out
+
+
+@pytest.mark.parametrize("t", _s_tables(), ids=lambda t: t["name"])
+def test_general_lines_parity(gpu, t):
+    with DeviceTable(t["ids"], t["status"], t["first"], t["off"], device=0) as T:
+        f = T.info()["flags"]
+        assert not (f & KAD_INFO_WINDOW_LINES)
+        if not t.get("lane"):
+            assert f & KAD_INFO_GENERAL_LINES and f & KAD_INFO_GENERAL_LINES32, hex(f)
+        _check(T, t, TB.adversarial_targets(t, extra=4000), gpu)
+
+
+def test_general_lines_after_status_patch(gpu):
+    t = TB.split_config(50_000, seed=0x66)
+    rng = np.random.default_rng(0x67)
+    targets = TB.adversarial_targets(t, extra=3000)
+    with DeviceTable(t["ids"], t["status"], t["first"], t["off"], device=0) as T:
+        st = t["status"].copy()
+        for frac in (0.001, 0.01, 0.2):
+            m = int(st.shape[0] * frac)
+            nodes = rng.choice(st.shape[0], size=m, replace=False).astype(np.uint32)
+            st[nodes] = rng.choice(np.array([0, 1, 1, 2], np.uint8), size=m)
+            T.patch_status(nodes, st[nodes])
+            _check(T, t, targets, gpu, counts=(1, 5, 8, 9, 14, 16, 20, 32), status=st)
+
+
+def test_uniform_table_switches_to_general_lines_after_split(gpu):
+    """A U(d) table answers from uniform lines; a split breaks the uniform depth and the mirror moves it to
+    general lines (kad_table_apply), still bit-exact."""
+    t = TB.uniform_config(30_000, 11, seed=0x68)
+    with DeviceTable(t["ids"], t["status"], t["first"], t["off"], device=0) as T:
+        assert T.info()["flags"] & KAD_INFO_WINDOW_LINES
+        T.apply(np.array([[KAD_OP_SPLIT, 100, 0], [KAD_OP_SPLIT, 7, 0]], np.uint32))
+        ids, st, first, off = T.export()
+        f = T.info()["flags"]
+        assert not (f & KAD_INFO_WINDOW_LINES) and f & KAD_INFO_GENERAL_LINES, hex(f)
+        t2 = TB.table(ids, st, first, off, name="U11_split")
+        _check(T, t2, TB.adversarial_targets(t2, extra=3000), gpu, counts=(1, 7, 8, 9, 16, 17, 32))
