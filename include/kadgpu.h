@@ -198,6 +198,13 @@ int kad_rt_closest_batch_dual(const kad_table* table4, const kad_table* table6,
                               const uint8_t* targets, const uint8_t* af, uint32_t q, uint32_t count,
                               uint32_t* out_idx, uint8_t* out_cnt, void* stream);
 
+/* Per-query family select for NodeCache::getCachedNodes(id, sa_family, count) (node_cache.cpp:36-66:
+ * cache_4 or cache_6 by family; Dht::refill asks the search's family, dht.cpp:1650): af[i] = 0 -> table4,
+ * 1 -> table6 (KAD_TABLE_SORTED tables; either may be NULL = an empty map). count <= 64. Device pointers. */
+int kad_nc_closest_batch_dual(const kad_table* table4, const kad_table* table6,
+                              const uint8_t* targets, const uint8_t* af, uint32_t q, uint32_t count,
+                              uint32_t* out_idx, uint8_t* out_cnt, void* stream);
+
 /* ---- sharded table without halo: the north-star multi-GPU variant ----
  * A global uniform-depth table U(depth) (bucket b's first ID = global_base + b << (160-depth)) is
  * cut into contiguous bucket ranges, one table per GPU, with global node indices (index_base).

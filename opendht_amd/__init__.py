@@ -8,9 +8,9 @@ the drop-in host interface for OpenDHT's C++ code is include/kadgpu.hpp.
 from ._lib import (KAD_MAX_COUNT, KAD_NO_NODE, KAD_SEARCH_NODES, KAD_STATUS_EXPIRED, KAD_STATUS_GOOD,
                    KAD_TARGET_NODES, KadError, lib)
 from .infohash import InfoHash, zeroes
-from .table import DeviceTable, rt_closest_dual
+from .table import DeviceTable, nc_closest_dual, rt_closest_dual
 
 __all__ = [
     "DeviceTable", "InfoHash", "KadError", "KAD_MAX_COUNT", "KAD_NO_NODE", "KAD_SEARCH_NODES",
-    "KAD_STATUS_EXPIRED", "KAD_STATUS_GOOD", "KAD_TARGET_NODES", "lib", "rt_closest_dual", "zeroes",
+    "KAD_STATUS_EXPIRED", "KAD_STATUS_GOOD", "KAD_TARGET_NODES", "lib", "nc_closest_dual", "rt_closest_dual", "zeroes",
 ]

@@ -69,6 +69,7 @@ SIGNATURES = {
     "kad_nc_closest_batch": (C.c_int, [_P, _P, C.c_uint32, C.c_uint32, _P, _P, _P]),
     "kad_nc_closest_batch_host": (C.c_int, [_P, _P, C.c_uint32, C.c_uint32, _P, _P]),
     "kad_rt_closest_batch_dual": (C.c_int, [_P, _P, _P, _P, C.c_uint32, C.c_uint32, _P, _P, _P]),
+    "kad_nc_closest_batch_dual": (C.c_int, [_P, _P, _P, _P, C.c_uint32, C.c_uint32, _P, _P, _P]),
     "kad_rt_shard_batch": (C.c_int, [_P, _P, C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32,
                                      C.c_uint32, _P, C.c_uint32, C.c_uint32, _P, C.c_uint32, _P, C.c_uint32,
                                      _P, _P]),

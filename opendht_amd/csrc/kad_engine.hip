@@ -2592,9 +2592,9 @@ __global__ __launch_bounds__(BLOCK) void nc_two_pass_kernel(DevTable T, const ui
 // ---------------------------------------------------------------------------------------
 constexpr uint32_t NCL_SLOTS = 60, NCL_LEFT = 28, NCL_XMAX = 15, NCL_STRIDE = 64;  // dwords
 
-__device__ __forceinline__ bool ncl_answer(const DevTable& T, const Target& t, uint32_t s, uint32_t count,
-                                           uint32_t (&o)[16], uint32_t& m) {
-    const uint4* lp = T.ncl + (NCL_STRIDE / 4) * (size_t)s;
+__device__ __forceinline__ bool ncl_answer(const uint4* ncl, uint32_t index_base, const Target& t, uint32_t s,
+                                           uint32_t count, uint32_t (&o)[16], uint32_t& m) {
+    const uint4* lp = ncl + (NCL_STRIDE / 4) * (size_t)s;
     uint32_t v[64];
     const uint4 hd = lp[0];
 #pragma unroll
@@ -2673,7 +2673,7 @@ __device__ __forceinline__ bool ncl_answer(const DevTable& T, const Target& t, u
     }
     m = min(count, have);
     ex |= have < count && (lim != NONE || w[31] != NONE);  // the walk goes on past the window / step 32
-    const uint32_t base = w0 + x + T.index_base;
+    const uint32_t base = w0 + x + index_base;
 #pragma unroll
     for (int c = 0; c < 16; c++) {
         uint32_t oc = NONE;
@@ -2690,29 +2690,45 @@ __device__ __forceinline__ bool ncl_answer(const DevTable& T, const Target& t, u
 }
 
 // ABL 1 (timing ablation only, KAD_NC_KERNEL=lines_abl1; results wrong): no exact path.
-template <int ABL>
-__global__ __launch_bounds__(BLOCK) void nc_line_kernel(DevTable T, const uint8_t* __restrict__ targets, uint32_t q,
+// DUAL: per-query family (af[i] = 0 -> T4, 1 -> T6; NodeCache::getCachedNodes picks cache_4 / cache_6 by
+// sa_family, node_cache.cpp:37); an empty family map (n = 0) gives zero results.
+template <int ABL, bool DUAL>
+__global__ __launch_bounds__(BLOCK) void nc_line_kernel(DevTable T4, DevTable T6, const uint8_t* __restrict__ af,
+                                                        const uint8_t* __restrict__ targets, uint32_t q,
                                                         uint32_t count, uint32_t* __restrict__ out_idx,
                                                         uint8_t* __restrict__ out_cnt) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x, lane = threadIdx.x & 63u;
     const bool act = i < q;
+    const bool fam = DUAL && act && af[i] != 0;
     Target t{};
     bool ok = false;
     if (act) {
         t = load_target(targets, i);
-        // below the first slot / past the last: lb = 0 / n, windows clamped at the ends (exact path)
-        const bool inside = t.hi >= T.nbase && ((t.hi - T.nbase) >> T.nshift) < T.nslots;
-        uint32_t o[16], m;
-        if (inside && ncl_answer(T, t, (uint32_t)((t.hi - T.nbase) >> T.nshift), count, o, m)) {
+        // this lane's family: only the fields the line path reads
+        const uint64_t nbase = fam ? T6.nbase : T4.nbase;
+        const uint32_t nshift = fam ? T6.nshift : T4.nshift, nslots = fam ? T6.nslots : T4.nslots;
+        const uint32_t n = fam ? T6.n : T4.n, flags = fam ? T6.flags : T4.flags;
+        uint32_t* row = out_idx + (size_t)i * count;
+        if (n == 0) {  // empty map: no nodes
+            for (uint32_t j = 0; j < count; j++) row[j] = NONE;
+            if (out_cnt) out_cnt[i] = 0;
             ok = true;
-            uint32_t* row = out_idx + (size_t)i * count;
-            store_row16(row, o, count);
-            if (out_cnt) out_cnt[i] = (uint8_t)m;
+        } else if (flags & TF_NCL) {
+            // below the first slot / past the last: lb = 0 / n, windows clamped at the ends (exact path)
+            const bool inside = t.hi >= nbase && ((t.hi - nbase) >> nshift) < nslots;
+            uint32_t o[16], m;
+            if (inside && ncl_answer(fam ? T6.ncl : T4.ncl, fam ? T6.index_base : T4.index_base, t,
+                                     (uint32_t)((t.hi - nbase) >> nshift), count, o, m)) {
+                ok = true;
+                store_row16(row, o, count);
+                if (out_cnt) out_cnt[i] = (uint8_t)m;
+            }
         }
     }
     // the lanes the lines could not answer: one query at a time by the whole wave (nc_answer: 32-node
     // runs each side of lb, itself falling back to lane 0's serial walk)
     uint64_t pend = ABL ? 0ull : __ballot(act && !ok);
+    const uint64_t fm = DUAL ? __ballot(fam) : 0ull;
     while (pend) {
         const uint32_t l = (uint32_t)__builtin_ctzll(pend);
         pend &= pend - 1;
@@ -2721,11 +2737,35 @@ __global__ __launch_bounds__(BLOCK) void nc_line_kernel(DevTable T, const uint8_
         u.t2 = (uint32_t)__shfl((int)t.t2, (int)l, 64);
         u.t3 = (uint32_t)__shfl((int)t.t3, (int)l, 64);
         u.t4 = (uint32_t)__shfl((int)t.t4, (int)l, 64);
+        const DevTable& T = (DUAL && ((fm >> l) & 1ull)) ? T6 : T4;  // wave-uniform
         uint32_t r0, r1;
         nc_slot(T, u, r0, r1);
         const NcWindow w = nc_window(T, r0, lane);
         nc_answer(T, u, r0, r1, w, lane, i - lane + l, count, out_idx, out_cnt);
     }
+}
+
+// NodeCache counts 17..64 for two families (af per query): nc_two_pass_kernel with the table chosen per
+// wave (one query per wave); an empty family map gives zero results.
+__global__ __launch_bounds__(BLOCK) void nc_two_pass_dual_kernel(DevTable T4, DevTable T6, const uint8_t* __restrict__ af,
+                                                                 const uint8_t* __restrict__ targets, uint32_t q,
+                                                                 uint32_t count, uint32_t* __restrict__ out_idx,
+                                                                 uint8_t* __restrict__ out_cnt) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t qi = blockIdx.x * (BLOCK / 64) + threadIdx.x / 64;
+    if (qi >= q) return;  // one query per wave: the whole wave leaves
+    const DevTable& T = af[qi] ? T6 : T4;
+    if (T.n == 0) {
+        if (lane < count) out_idx[(size_t)qi * count + lane] = NONE;
+        if (lane == 0 && out_cnt) out_cnt[qi] = 0;
+        return;
+    }
+    const Target t = load_target(targets, qi);
+    uint32_t r0, r1;
+    nc_slot(T, t, r0, r1);
+    const NcWindow w = nc_window(T, r0, lane);
+    if (!nc_answer(T, t, r0, r1, w, lane, qi, count, out_idx, out_cnt, false))
+        nc64_query(T, t, lane, qi, count, out_idx, out_cnt, true);
 }
 
 // NodeCache lines after a status change (or at creation): one thread per radix slot.
@@ -4034,16 +4074,16 @@ int kad_nc_closest_batch(const kad_table* t, const uint8_t* targets, uint32_t q,
     const bool lines = (t->d.flags & TF_NCL) && !ev;  // KAD_NC_KERNEL=<kernel> picks another one (A/B timing)
 #ifdef KAD_ABLATIONS  // timing ablations with WRONG results: only in the tools build
     if ((t->d.flags & TF_NCL) && ev && std::strcmp(ev, "lines_abl1") == 0 && count >= 1 && count <= 16)
-        hipLaunchKernelGGL(nc_line_kernel<1>, dim3(grid_for(q)), dim3(BLOCK), 0, (hipStream_t)stream, t->d, targets, q,
-                           count, out_idx, out_cnt);
+        hipLaunchKernelGGL((nc_line_kernel<1, false>), dim3(grid_for(q)), dim3(BLOCK), 0, (hipStream_t)stream, t->d,
+                           t->d, nullptr, targets, q, count, out_idx, out_cnt);
     else if (count > 16 && count <= 64 && t->d.n > 0 && ev && std::strcmp(ev, "w64_abl1") == 0)
         hipLaunchKernelGGL(nc_wave64_kernel<1>, dim3((q + BLOCK / 64 - 1) / (BLOCK / 64)), dim3(BLOCK), 0,
                            (hipStream_t)stream, t->d, targets, q, count, out_idx, out_cnt);
     else
 #endif
     if (lines && count >= 1 && count <= 16)
-        hipLaunchKernelGGL(nc_line_kernel<0>, dim3(grid_for(q)), dim3(BLOCK), 0, (hipStream_t)stream, t->d, targets, q,
-                           count, out_idx, out_cnt);
+        hipLaunchKernelGGL((nc_line_kernel<0, false>), dim3(grid_for(q)), dim3(BLOCK), 0, (hipStream_t)stream, t->d,
+                           t->d, nullptr, targets, q, count, out_idx, out_cnt);
     else if (count >= 1 && count <= 16 && ev && std::strcmp(ev, "group1") == 0)
         hipLaunchKernelGGL(nc_group_v1_kernel, dim3((q + BLOCK / 64 - 1) / (BLOCK / 64)), dim3(BLOCK), 0,
                            (hipStream_t)stream, t->d, targets, q, count, out_idx, out_cnt);
@@ -4069,6 +4109,35 @@ int kad_nc_closest_batch(const kad_table* t, const uint8_t* targets, uint32_t q,
     else
         hipLaunchKernelGGL(nc_closest_kernel, dim3(grid_for(q)), dim3(BLOCK), 0, (hipStream_t)stream, t->d, targets, q,
                            count, out_idx, out_cnt);
+    HIP_TRY(hipGetLastError());
+    return KAD_OK;
+}
+
+int kad_nc_closest_batch_dual(const kad_table* t4, const kad_table* t6, const uint8_t* targets, const uint8_t* af,
+                              uint32_t q, uint32_t count, uint32_t* out_idx, uint8_t* out_cnt, void* stream) {
+    if (!t4 && !t6) return set_err(KAD_ERR_INVALID, "both tables NULL");
+    if (t4 && t6 && t4->device != t6->device) return set_err(KAD_ERR_INVALID, "tables on different devices");
+    for (const kad_table* t : {t4, t6})
+        if (t && t->d.n && !(t->flags & KAD_TABLE_SORTED))
+            return set_err(KAD_ERR_NOT_SORTED, "NodeCache query needs KAD_TABLE_SORTED tables");
+    if (count > 64) return set_err(KAD_ERR_UNSUPPORTED, "count %u > 64 (dual-family NodeCache batch)", count);
+    if (q == 0) return KAD_OK;
+    if (!targets || !af || (!out_idx && count)) return set_err(KAD_ERR_INVALID, "NULL buffer");
+    DevTable empty{};  // a missing family behaves as an empty map (no results)
+    const DevTable& d4 = t4 ? t4->d : empty;
+    const DevTable& d6 = t6 ? t6->d : empty;
+    DeviceGuard g(t4 ? t4->device : t6->device);
+    hipStream_t s = (hipStream_t)stream;
+    if (count == 0) {
+        if (out_cnt) HIP_TRY(hipMemsetAsync(out_cnt, 0, q, s));
+        return KAD_OK;
+    }
+    if (count <= 16)
+        hipLaunchKernelGGL((nc_line_kernel<0, true>), dim3(grid_for(q)), dim3(BLOCK), 0, s, d4, d6, af, targets, q, count,
+                           out_idx, out_cnt);
+    else
+        hipLaunchKernelGGL(nc_two_pass_dual_kernel, dim3((q + BLOCK / 64 - 1) / (BLOCK / 64)), dim3(BLOCK), 0, s, d4, d6,
+                           af, targets, q, count, out_idx, out_cnt);
     HIP_TRY(hipGetLastError());
     return KAD_OK;
 }

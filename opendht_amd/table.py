@@ -247,3 +247,18 @@ def rt_closest_dual(table4: DeviceTable | None, table6: DeviceTable | None, targ
                                           ptr(targets), ptr(af), q, count, ptr(out_idx), ptr(out_cnt), s),
           "kad_rt_closest_batch_dual")
     return out_idx, out_cnt
+
+
+def nc_closest_dual(table4: DeviceTable | None, table6: DeviceTable | None, targets, af, count: int, stream=None):
+    """NodeCache::getCachedNodes with a per-query family (af 0 -> cache_4, 1 -> cache_6; node_cache.cpp:36-66)."""
+    import torch
+
+    q = targets.shape[0]
+    out_idx = torch.empty((q, count), dtype=torch.int32, device=targets.device)
+    out_cnt = torch.empty((q,), dtype=torch.uint8, device=targets.device)
+    s = C.c_void_p(stream) if stream is not None else C.c_void_p(
+        torch.cuda.current_stream(targets.device).cuda_stream)
+    check(lib().kad_nc_closest_batch_dual(table4.handle if table4 else None, table6.handle if table6 else None,
+                                          ptr(targets), ptr(af), q, count, ptr(out_idx), ptr(out_cnt), s),
+          "kad_nc_closest_batch_dual")
+    return out_idx, out_cnt
