@@ -161,6 +161,16 @@ int kad_table_refresh_status(kad_table* t, int64_t now_ns, void* stream);
 #define KAD_OP_SPLIT 4u
 int kad_table_apply(kad_table* t, const uint32_t* ops, uint32_t n_ops, const uint8_t* new_ids,
                     const uint8_t* new_status, uint32_t n_new, uint32_t* remap, uint32_t* new_index);
+/* NodeCache map mutations (node_cache.cpp:91-115) on a NodeCache-only table (n_buckets = 0,
+ * KAD_TABLE_SORTED), without a re-snapshot: erase the n_erase listed nodes (indices at the call, each at
+ * most once: NodeMap::getNode(id) erasing a dead weak_ptr, clearBadNodes' erase of dead entries), then
+ * insert n_ins new IDs (host, any order, none already a kept key: NodeMap::getNode(id, addr, now, confirm)'s
+ * emplace) with their status bytes. The node array is merged on the device and stays sorted; the NodeCache
+ * radix and lines are re-derived there. remap (host, old n entries, may be NULL): new index of every old
+ * node, KAD_NO_NODE if erased; new_index (host, n_ins, may be NULL): index of every new node. Node times and
+ * wire records must be set again. Failure leaves the table unchanged. Synchronous. */
+int kad_nc_apply(kad_table* t, const uint32_t* erase, uint32_t n_erase, const uint8_t* ins_ids,
+                 const uint8_t* ins_status, uint32_t n_ins, uint32_t* remap, uint32_t* new_index);
 /* The table as host arrays (any may be NULL): ids n x 20 and status in bucket/list order, bucket
  * firsts B x 20 and offsets B+1 (sizes from kad_table_get_info). */
 int kad_table_export(const kad_table* t, uint8_t* ids, uint8_t* status, uint8_t* bucket_first,

@@ -355,17 +355,73 @@ public:
     /* Snapshot: map order (ascending ID); dead weak_ptrs and expired nodes are walked over but never
      * emitted (node_cache.cpp:60-62), so both get the "expired" status bit. */
     void snapshot(const NodeMapT& m, int device = 0) {
-        std::vector<uint8_t> ids, status;
+        std::vector<uint8_t> status;
+        ids_.clear();
         nodes_.clear();
-        index_.clear();
         for (const auto& kv : m) {
             NodePtr n = kv.second.lock();
-            ids.insert(ids.end(), id_bytes(kv.first), id_bytes(kv.first) + KAD_HASH_LEN);
-            status.push_back((uint8_t)((!n || n->isExpired()) ? KAD_STATUS_EXPIRED : 0u));
-            if (n) index_[n.get()] = (uint32_t)nodes_.size();
+            ids_.insert(ids_.end(), id_bytes(kv.first), id_bytes(kv.first) + KAD_HASH_LEN);
+            status.push_back(status_of(n));
             nodes_.push_back(kv.second);
         }
-        table_ = DeviceTable(device, ids, status, std::vector<uint8_t>(), std::vector<uint32_t>(), 0, true);
+        table_ = DeviceTable(device, ids_, status, std::vector<uint8_t>(), std::vector<uint32_t>(), 0, true);
+        reindex();
+    }
+
+    /* Bring the device copy in line with the host map after NodeMap::getNode emplaced new IDs or erased
+     * dead entries, or clearBadNodes erased them (node_cache.cpp:79-115): a sorted diff of the map against
+     * the mirrored IDs, then one kad_nc_apply (a device merge, no re-snapshot). An entry whose weak_ptr now
+     * names another Node (getNode recreated it) or whose expiry changed gets its status patched. */
+    void sync(const NodeMapT& m) {
+        std::vector<uint32_t> erase, changed;
+        std::vector<uint8_t> ins, ist, chst;
+        std::vector<WeakPtr> added;
+        size_t i = 0;
+        auto it = m.begin();
+        const size_t n = nodes_.size();
+        while (i < n || it != m.end()) {
+            const int c = i == n ? 1 : it == m.end() ? -1 : std::memcmp(&ids_[i * KAD_HASH_LEN], id_bytes(it->first), KAD_HASH_LEN);
+            if (c < 0) {
+                erase.push_back((uint32_t)i++);
+            } else if (c > 0) {
+                ins.insert(ins.end(), id_bytes(it->first), id_bytes(it->first) + KAD_HASH_LEN);
+                ist.push_back(status_of(it->second.lock()));
+                added.push_back(it->second);
+                ++it;
+            } else {
+                const bool same = !nodes_[i].owner_before(it->second) && !it->second.owner_before(nodes_[i]);
+                if (!same) {
+                    nodes_[i] = it->second;
+                    changed.push_back((uint32_t)i);
+                    chst.push_back(status_of(it->second.lock()));
+                }
+                ++i;
+                ++it;
+            }
+        }
+        if (!changed.empty()) table_.patchStatus(changed, chst);
+        if (erase.empty() && added.empty()) {
+            if (!changed.empty()) reindex();
+            return;
+        }
+        std::vector<uint32_t> remap(n ? n : 1), idx(added.empty() ? 1 : added.size());
+        check(kad_nc_apply(table_.get(), erase.data(), (uint32_t)erase.size(), ins.data(), ist.data(),
+                           (uint32_t)added.size(), remap.data(), idx.data()), "kad_nc_apply");
+        const size_t n1 = n - erase.size() + added.size();
+        std::vector<WeakPtr> next(n1);
+        std::vector<uint8_t> ids1(n1 * KAD_HASH_LEN);
+        for (size_t k = 0; k < n; k++)
+            if (remap[k] != KAD_NO_NODE) {
+                next[remap[k]] = nodes_[k];
+                std::memcpy(&ids1[remap[k] * KAD_HASH_LEN], &ids_[k * KAD_HASH_LEN], KAD_HASH_LEN);
+            }
+        for (size_t k = 0; k < added.size(); k++) {
+            next[idx[k]] = added[k];
+            std::memcpy(&ids1[idx[k] * KAD_HASH_LEN], &ins[k * KAD_HASH_LEN], KAD_HASH_LEN);
+        }
+        nodes_.swap(next);
+        ids_.swap(ids1);
+        reindex();
     }
 
     /* NodeCache::getCachedNodes(id, af, count) for this family (node_cache.cpp:36-66). */
@@ -426,7 +482,17 @@ public:
     size_t size() const { return nodes_.size(); }
 
 private:
+    static uint8_t status_of(const NodePtr& n) {
+        return (uint8_t)((!n || n->isExpired()) ? KAD_STATUS_EXPIRED : 0u);
+    }
+    void reindex() {
+        index_.clear();
+        for (size_t i = 0; i < nodes_.size(); i++)
+            if (NodePtr n = nodes_[i].lock()) index_[n.get()] = (uint32_t)i;
+    }
+
     mutable DeviceTable table_;
+    std::vector<uint8_t> ids_;  // the mirrored map's keys, in map order
     std::vector<WeakPtr> nodes_;
     std::unordered_map<const void*, uint32_t> index_;
 };
@@ -449,6 +515,11 @@ public:
     void nodeUpdated(const NodePtr& n) {
         v4_.nodeUpdated(n);
         v6_.nodeUpdated(n);
+    }
+    /* After NodeCache::getNode / clearBadNodes changed the maps (inserted or erased entries). */
+    void sync(const NodeMapT& cache4, const NodeMapT& cache6) {
+        v4_.sync(cache4);
+        v6_.sync(cache6);
     }
     const NodeCacheFamilyMirror<NodeMapT>& family(sa_family_t sa_f) const { return sa_f == AF_INET ? v4_ : v6_; }
     NodeCacheFamilyMirror<NodeMapT>& family(sa_family_t sa_f) { return sa_f == AF_INET ? v4_ : v6_; }

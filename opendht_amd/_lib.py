@@ -59,6 +59,7 @@ SIGNATURES = {
     "kad_table_update_status": (C.c_int, [_P, _P]),
     "kad_table_apply": (C.c_int, [_P, _P, C.c_uint32, _P, _P, C.c_uint32, _P, _P]),
     "kad_table_export": (C.c_int, [_P, _P, _P, _P, _P]),
+    "kad_nc_apply": (C.c_int, [_P, _P, C.c_uint32, _P, _P, C.c_uint32, _P, _P]),
     "kad_table_set_times": (C.c_int, [_P, _P, _P, _P]),
     "kad_table_refresh_status": (C.c_int, [_P, C.c_int64, _P]),
     "kad_table_patch_status": (C.c_int, [_P, C.c_uint32, _P, _P]),

@@ -2907,6 +2907,90 @@ __global__ void lowbit_kernel(const uint8_t* a, uint32_t n, uint32_t* out) {
 }
 
 // ---------------------------------------------------------------------------------------
+// NodeCache map mutations (kad_nc_apply; node_cache.cpp:91-115): the sorted node array of a NodeCache-only
+// table merged with a sorted batch of new IDs (NodeMap::getNode's emplace) minus erased entries (a dead
+// weak_ptr found by getNode, clearBadNodes). Every kept old node and every new node computes its new
+// position by binary search in the other sorted list; the NodeCache radix is re-derived by a binary search
+// per radix slot. No host copy of the IDs is needed.
+// ---------------------------------------------------------------------------------------
+// #elements of the sorted (key, tail) list [0, n) that are < (k, t2, t3, t4) (strict lower bound); *eq = an
+// element equals it.
+__device__ __forceinline__ uint32_t lower_bound160(const uint64_t* key, const uint32_t* tail, uint32_t n, uint64_t k,
+                                                   uint32_t t2, uint32_t t3, uint32_t t4, bool* eq) {
+    uint32_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        const uint32_t* tm = tail + 3ull * mid;
+        if (cmp160(key[mid], tm[0], tm[1], tm[2], k, t2, t3, t4) < 0) lo = mid + 1; else hi = mid;
+    }
+    if (eq) {
+        const uint32_t* tl = tail + 3ull * lo;
+        *eq = lo < n && cmp160(key[lo], tl[0], tl[1], tl[2], k, t2, t3, t4) == 0;
+    }
+    return lo;
+}
+
+__global__ void nc_merge_old_kernel(const uint64_t* key, const uint32_t* tail, const uint8_t* st, const uint8_t* eflag,
+                                    const uint32_t* erased_before, uint32_t n, const uint64_t* ikey,
+                                    const uint32_t* itail, uint32_t m, uint64_t* key1, uint32_t* tail1, uint8_t* st1,
+                                    uint32_t* remap) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n) return;
+    if (eflag[i]) { remap[i] = NONE; return; }
+    const uint32_t* tl = tail + 3ull * i;
+    const uint32_t c = lower_bound160(ikey, itail, m, key[i], tl[0], tl[1], tl[2], nullptr);
+    const uint32_t pos = i - erased_before[i] + c;
+    key1[pos] = key[i];
+    tail1[3ull * pos] = tl[0]; tail1[3ull * pos + 1] = tl[1]; tail1[3ull * pos + 2] = tl[2];
+    st1[pos] = st[i];
+    remap[i] = pos;
+}
+
+// err: set when a new ID is already a (kept) key of the map (the caller's emplace would not insert it)
+__global__ void nc_merge_new_kernel(const uint64_t* key, const uint32_t* tail, const uint8_t* eflag,
+                                    const uint32_t* erased_before, uint32_t n, const uint64_t* ikey,
+                                    const uint32_t* itail, const uint8_t* ist, uint32_t m, uint64_t* key1,
+                                    uint32_t* tail1, uint8_t* st1, uint32_t* new_index, uint32_t* err) {
+    const uint32_t j = blockIdx.x * BLOCK + threadIdx.x;
+    if (j >= m) return;
+    const uint32_t* tl = itail + 3ull * j;
+    bool eq = false;
+    const uint32_t c = lower_bound160(key, tail, n, ikey[j], tl[0], tl[1], tl[2], &eq);
+    if (eq && !eflag[c]) atomicOr(err, 1u);
+    const uint32_t pos = j + c - erased_before[c];
+    key1[pos] = ikey[j];
+    tail1[3ull * pos] = tl[0]; tail1[3ull * pos + 1] = tl[1]; tail1[3ull * pos + 2] = tl[2];
+    st1[pos] = ist[j];
+    new_index[j] = pos;
+}
+
+// NodeCache radix over a sorted key array: rdx[s] = #keys whose top 64 bits are below slot s's start.
+__global__ void nc_radix_kernel(const uint64_t* key, uint32_t n, uint64_t base, uint32_t shift, uint32_t slots,
+                                uint32_t* rdx) {
+    const uint32_t s = blockIdx.x * BLOCK + threadIdx.x;
+    if (s > slots) return;
+    const unsigned __int128 start = (unsigned __int128)base + ((unsigned __int128)s << shift);
+    uint32_t lo = 0, hi = n;
+    if (start >> 64) {
+        lo = n;
+    } else {
+        const uint64_t st64 = (uint64_t)start;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (key[mid] < st64) lo = mid + 1; else hi = mid;
+        }
+    }
+    rdx[s] = lo;
+}
+
+__global__ void flags_from_list_kernel(const uint32_t* list, uint32_t m, uint32_t n, uint8_t* flags, uint32_t* cnt) {
+    const uint32_t j = blockIdx.x * BLOCK + threadIdx.x;
+    if (j >= m) return;
+    flags[list[j]] = 1;
+    cnt[list[j]] = 1;
+}
+
+// ---------------------------------------------------------------------------------------
 // Table maintenance: status from times, per-bucket good counts, exclusive scan -> dir.y
 // ---------------------------------------------------------------------------------------
 // Where a status change must be re-derived (incremental refresh): bdirty[b] = bucket b's good set changed
@@ -4539,6 +4623,129 @@ int kad_table_apply(kad_table* t, const uint32_t* ops, uint32_t n_ops, const uin
     HIP_TRY(hipDeviceSynchronize());
     // a table that lost (or never had) uniform-depth lines gets general ones (built from the new state)
     if (!(d.flags & TF_WL) && !t->gl_mut && !t->gl32_mut && (rc = setup_general_lines(t))) return rc;
+    return KAD_OK;
+}
+
+int kad_nc_apply(kad_table* t, const uint32_t* erase, uint32_t n_erase, const uint8_t* ins_ids,
+                 const uint8_t* ins_status, uint32_t n_ins, uint32_t* remap, uint32_t* new_index) {
+    if (!t || (n_erase && !erase) || (n_ins && (!ins_ids || !ins_status))) return set_err(KAD_ERR_INVALID, "NULL argument");
+    if (t->d.B != 0 || !(t->flags & KAD_TABLE_SORTED))
+        return set_err(KAD_ERR_INVALID, "kad_nc_apply needs a NodeCache-only table (no buckets, KAD_TABLE_SORTED)");
+    DevTable& d = t->d;
+    const uint32_t n0 = d.n;
+    std::vector<uint8_t> seen(n0, 0);
+    for (uint32_t j = 0; j < n_erase; j++) {
+        if (erase[j] >= n0) return set_err(KAD_ERR_INVALID, "erase: node %u out of range (n=%u)", erase[j], n0);
+        if (seen[erase[j]]++) return set_err(KAD_ERR_INVALID, "erase: node %u listed twice", erase[j]);
+    }
+    if ((uint64_t)n0 - n_erase + n_ins >= 0x7FFFFFFFull) return set_err(KAD_ERR_INVALID, "table too large");
+    // the insert batch, sorted (remember each slot's place for new_index), strictly ascending
+    std::vector<uint32_t> order(n_ins);
+    for (uint32_t j = 0; j < n_ins; j++) order[j] = j;
+    std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
+        return std::memcmp(ins_ids + 20ull * a, ins_ids + 20ull * b, 20) < 0;
+    });
+    std::vector<uint64_t> ik(n_ins);
+    std::vector<uint32_t> it(3ull * n_ins);
+    std::vector<uint8_t> ist(n_ins);
+    for (uint32_t j = 0; j < n_ins; j++) {
+        const uint8_t* p = ins_ids + 20ull * order[j];
+        if (j && std::memcmp(ins_ids + 20ull * order[j - 1], p, 20) == 0)
+            return set_err(KAD_ERR_INVALID, "insert: an ID is listed twice");
+        ik[j] = id_hi(p);
+        for (int w = 0; w < 3; w++) it[3ull * j + w] = id_word(p, 2 + w);
+        ist[j] = ins_status[order[j]];
+    }
+    const uint32_t n1 = n0 - n_erase + n_ins;
+    DeviceGuard g(t->device);
+    std::vector<void*> tmp, fresh;
+    uint64_t tmpb = 0, freshb = 0;
+    auto fail = [&](int code) {
+        for (void* p : tmp) (void)hipFree(p);
+        for (void* p : fresh) (void)hipFree(p);
+        return code;
+    };
+    uint64_t *dik, *key1; uint32_t *dit, *del, *dcnt, *dpre, *dsums, *dremap, *dnew, *derr, *tail1, *rdx1, *ncl1;
+    uint8_t *dist, *deflag, *st1;
+    const uint32_t tiles = (n0 + 1 + SCAN_TILE - 1) / SCAN_TILE;
+    int rc;
+    if ((rc = dev_upload(&dik, ik.data(), n_ins, tmp, tmpb)) || (rc = dev_upload(&dit, it.data(), 3ull * n_ins, tmp, tmpb)) ||
+        (rc = dev_upload(&dist, ist.data(), n_ins, tmp, tmpb)) || (rc = dev_upload(&del, erase, n_erase, tmp, tmpb)) ||
+        (rc = dev_upload(&deflag, nullptr, n0 + 1, tmp, tmpb)) || (rc = dev_upload(&dcnt, nullptr, n0 + 1, tmp, tmpb)) ||
+        (rc = dev_upload(&dpre, nullptr, n0 + 1, tmp, tmpb)) || (rc = dev_upload(&dsums, nullptr, tiles, tmp, tmpb)) ||
+        (rc = dev_upload(&dremap, nullptr, n0, tmp, tmpb)) || (rc = dev_upload(&dnew, nullptr, n_ins, tmp, tmpb)) ||
+        (rc = dev_upload(&derr, nullptr, 1, tmp, tmpb)))
+        return fail(rc);
+    if ((rc = dev_upload(&key1, nullptr, n1 + KEY_PAD, fresh, freshb)) ||
+        (rc = dev_upload(&tail1, nullptr, 3ull * n1, fresh, freshb)) ||
+        (rc = dev_upload(&st1, nullptr, n1, fresh, freshb)))
+        return fail(rc);
+    if (hipMemset(deflag, 0, n0 + 1) != hipSuccess || hipMemset(dcnt, 0, 4ull * (n0 + 1)) != hipSuccess ||
+        hipMemset(derr, 0, 4) != hipSuccess || hipMemset(key1, 0xFF, 8ull * (n1 + KEY_PAD)) != hipSuccess)
+        return fail(set_err(KAD_ERR_HIP, "hipMemset failed"));
+    if (n_erase)
+        hipLaunchKernelGGL(flags_from_list_kernel, dim3(grid_for(n_erase)), dim3(BLOCK), 0, 0, del, n_erase, n0, deflag, dcnt);
+    // erased_before[i] = erased nodes below i (exclusive scan of the flags, n0 + 1 entries)
+    hipLaunchKernelGGL(scan_tiles_kernel, dim3(tiles), dim3(BLOCK), 0, 0, dcnt, n0 + 1, dpre, dsums);
+    hipLaunchKernelGGL(scan_sums_kernel, dim3(1), dim3(BLOCK), 0, 0, dsums, tiles);
+    hipLaunchKernelGGL(scan_apply_kernel, dim3(grid_for(n0 + 1)), dim3(BLOCK), 0, 0, dpre, dsums, n0 + 1, dpre);
+    if (n0)
+        hipLaunchKernelGGL(nc_merge_old_kernel, dim3(grid_for(n0)), dim3(BLOCK), 0, 0, d.key, d.tail, d.status, deflag, dpre,
+                           n0, dik, dit, n_ins, key1, tail1, st1, dremap);
+    if (n_ins)
+        hipLaunchKernelGGL(nc_merge_new_kernel, dim3(grid_for(n_ins)), dim3(BLOCK), 0, 0, d.key, d.tail, deflag, dpre, n0,
+                           dik, dit, dist, n_ins, key1, tail1, st1, dnew, derr);
+    uint32_t err = 0;
+    uint64_t kmin = 0, kmax = 0;
+    if (hipGetLastError() != hipSuccess || hipMemcpy(&err, derr, 4, hipMemcpyDeviceToHost) != hipSuccess ||
+        (n1 && (hipMemcpy(&kmin, key1, 8, hipMemcpyDeviceToHost) != hipSuccess ||
+                hipMemcpy(&kmax, key1 + (n1 - 1), 8, hipMemcpyDeviceToHost) != hipSuccess)))
+        return fail(set_err(KAD_ERR_HIP, "NodeCache merge failed"));
+    if (err) return fail(set_err(KAD_ERR_INVALID, "insert: an ID is already in the map"));
+    // NodeCache radix and lines of the new array
+    Radix r;
+    uint32_t tb = 1;
+    while ((1u << tb) < n1 && tb < 23) tb++;
+    if (n1) r = choose_radix(kmin, kmax, tb);
+    if (n1 && ((rc = dev_upload(&rdx1, nullptr, (size_t)r.slots + 1, fresh, freshb)) ||
+               (rc = dev_upload(&ncl1, nullptr, (size_t)NCL_STRIDE * r.slots, fresh, freshb))))
+        return fail(rc);
+    if (n1) {
+        hipLaunchKernelGGL(nc_radix_kernel, dim3(grid_for((uint64_t)r.slots + 1)), dim3(BLOCK), 0, 0, key1, n1, r.base,
+                           r.shift, r.slots, rdx1);
+        hipLaunchKernelGGL(ncl_build_kernel, dim3(grid_for(r.slots)), dim3(BLOCK), 0, 0, key1, st1, rdx1, r.slots, n1,
+                           64 - r.shift, ncl1, LineSel{});
+    }
+    if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess)
+        return fail(set_err(KAD_ERR_HIP, "NodeCache radix / line build failed"));
+    if ((remap && n0 && hipMemcpy(remap, dremap, 4ull * n0, hipMemcpyDeviceToHost) != hipSuccess))
+        return fail(set_err(KAD_ERR_HIP, "copy of the remap failed"));
+    if (new_index && n_ins) {
+        std::vector<uint32_t> sorted_idx(n_ins);
+        if (hipMemcpy(sorted_idx.data(), dnew, 4ull * n_ins, hipMemcpyDeviceToHost) != hipSuccess)
+            return fail(set_err(KAD_ERR_HIP, "copy of the new indices failed"));
+        for (uint32_t j = 0; j < n_ins; j++) new_index[order[j]] = sorted_idx[j];
+    }
+    for (void* p : tmp) (void)hipFree(p);
+    // ---- commit ----
+    release(t, const_cast<uint64_t*>(d.key));
+    release(t, const_cast<uint32_t*>(d.tail));
+    release(t, t->status_mut);
+    release(t, const_cast<uint32_t*>(d.nrdx));
+    release(t, t->ncl_mut);
+    d.key = key1; d.tail = tail1; d.status = st1; t->status_mut = st1; d.n = n1;
+    if (n1) {
+        d.nrdx = rdx1; d.nbase = r.base; d.nshift = r.shift; d.nslots = r.slots; t->nbits = r.bits;
+        d.ncl = reinterpret_cast<const uint4*>(ncl1); t->ncl_mut = ncl1; d.flags |= TF_NCL;
+    } else {
+        d.nrdx = nullptr; d.nslots = 0; t->nbits = 0; d.ncl = nullptr; t->ncl_mut = nullptr; d.flags &= ~TF_NCL;
+    }
+    release(t, t->wrec); t->wrec = nullptr; t->addr_len = 0;
+    release(t, t->time_ns); release(t, t->reply_ns); release(t, t->expired);
+    t->time_ns = nullptr; t->reply_ns = nullptr; t->expired = nullptr;
+    t->owned.insert(t->owned.end(), fresh.begin(), fresh.end());
+    t->bytes += freshb;
+    drop_marks(t);
     return KAD_OK;
 }
 

@@ -142,6 +142,22 @@ class DeviceTable:
         self.n, self.B = inf["n_nodes"], inf["n_buckets"]
         return out[:nid.shape[0]]
 
+    def nc_apply(self, erase=None, ins_ids=None, ins_status=None):
+        """NodeCache map mutations (kad_nc_apply) on a NodeCache-only table: erase the listed node indices,
+        insert new IDs. Returns (remap (old n,) uint32, new_index (n_ins,) uint32), both host arrays."""
+        er = np.ascontiguousarray(erase if erase is not None else np.zeros(0), dtype=np.uint32)
+        nid = _as_ids(ins_ids) if ins_ids is not None and len(ins_ids) else np.zeros((0, 20), np.uint8)
+        nst = np.ascontiguousarray(ins_status if ins_status is not None else np.zeros(0), dtype=np.uint8)
+        if nst.shape[0] != nid.shape[0]:
+            raise ValueError("one status byte per inserted ID")
+        remap = np.zeros(max(self.n, 1), np.uint32)
+        new_index = np.zeros(max(nid.shape[0], 1), np.uint32)
+        check(lib().kad_nc_apply(self._h, ptr(er), er.shape[0], ptr(nid), ptr(nst), nid.shape[0], ptr(remap),
+                                 ptr(new_index)), "kad_nc_apply")
+        old_n = self.n
+        self.n = self.info()["n_nodes"]
+        return remap[:old_n], new_index[:nid.shape[0]]
+
     def export(self):
         """(ids, status, bucket_first, bucket_offset) host arrays of the device table."""
         inf = self.info()

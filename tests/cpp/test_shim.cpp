@@ -224,6 +224,27 @@ int main() {
             check_nc(c4, b4, targets, count, "nc v4 after deaths");
             check_nc(c6, b6, targets, count, "nc v6 after expiries");
         }
+        // the maps change: NodeMap::getNode(id, addr, now, confirm) emplaces new IDs (node_cache.cpp:91-103),
+        // getNode(id) erases entries whose node died (:79-89); the mirror follows with sync() (kad_nc_apply)
+        for (int k = 0; k < 2000; k++) {
+            auto nd = std::make_shared<Node>();
+            for (auto& x : nd->id) x = (uint8_t)g();
+            nd->idx = 200000 + k;
+            nd->time = nd->reply_time = t0;
+            if (k % 4 == 0) nd->expired_ = true;
+            extra.push_back(nd);
+            (k % 2 ? c6 : c4).emplace(nd->id, nd);
+        }
+        for (auto it = c4.begin(); it != c4.end();)  // erase dead entries, as getNode(id) does on lookup
+            if (it->second.expired() && (g() % 2)) it = c4.erase(it); else ++it;
+        nc.sync(c4, c6);
+        for (uint32_t count : {8u, 14u, 32u}) {
+            auto b4 = nc.family(AF_INET).getCachedNodesBatch(targets, count);
+            auto b6 = nc.family(AF_INET6).getCachedNodesBatch(targets, count);
+            check_nc(c4, b4, targets, count, "nc v4 after sync");
+            check_nc(c6, b6, targets, count, "nc v6 after sync");
+        }
+        EXPECT(nc.family(AF_INET).size() == c4.size() && nc.family(AF_INET6).size() == c6.size(), "nc sizes after sync");
     }
 
     // Incremental mirror: Dht::onNewNode (replace an expired node / emplace_front / split my bucket)
