@@ -131,6 +131,7 @@ int kad_sort_ids(uint32_t n, uint8_t* ids, uint32_t* out_perm) {
     std::stable_sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) { return cmp_id(ids + 20ull * a, ids + 20ull * b) < 0; });
     std::vector<uint8_t> tmp((size_t)n * 20);
     for (uint32_t i = 0; i < n; i++) std::memcpy(tmp.data() + 20ull * i, ids + 20ull * ord[i], 20);
+    if (n == 0) return KAD_OK;  // (memcpy from an empty vector's NULL data() is undefined)
     std::memcpy(ids, tmp.data(), tmp.size());
     if (out_perm) std::memcpy(out_perm, ord.data(), 4ull * n);
     return KAD_OK;

@@ -130,6 +130,67 @@ def build_shard(spec: ShardSpec, s: int, probe: int = 64) -> Shard:
     return Shard(spec, s, lo, hi, b0, b1, spec.nodes_below(b0), ids, st, first, off)
 
 
+class HaloError(RuntimeError):
+    """A status change made some owned window reach past the shard's halo: the shard can no longer answer
+    every owned query as the whole table would. Rebuild the shard (build_shard) with the new status."""
+
+
+def halo_ok(sh: Shard, status) -> bool:
+    """Whether the shard's held buckets [b0, b1) still contain every owned window W(R) for counts <= k_max
+    under `status` (the shard's node statuses). The held good counts get a sentinel bucket of k_max good
+    nodes on each side that is not a global edge: a window stays inside [b0, b1) exactly when its local
+    rounds (routing_table.cpp:89-104) never reach a sentinel."""
+    g = _good_counts(np.asarray(status), sh.off).astype(np.int64)
+    left, right = sh.b0 > 0, sh.b1 < sh.spec.n_buckets
+    k = sh.spec.k_max
+    ext = np.concatenate([[k] if left else [], g, [k] if right else []]).astype(np.int64)
+    R = window_radii(ext, k)
+    b = np.arange(sh.lo - sh.b0, sh.hi - sh.b0) + (1 if left else 0)
+    wl, wh = b - 1 - R[b], b + R[b]
+    return not ((left and (wl <= 0).any()) or (right and (wh >= ext.shape[0] - 1).any()))
+
+
+class ShardTable:
+    """A shard's DeviceTable whose status changes are checked against the halo it was built with: the
+    halo width comes from the good counts at build time, so a refresh that turns enough nodes bad next to
+    a shard edge would let a window run past the held buckets and the shard would answer with its local
+    edge as the table edge. Every status change here re-checks the halo and raises HaloError instead."""
+
+    def __init__(self, sh: Shard, device: int = 0):
+        from .table import DeviceTable
+
+        self.shard = sh
+        self.table = DeviceTable(sh.ids, sh.status, sh.first, sh.off, device=device, index_base=sh.index_base,
+                                 sorted=True)
+
+    def _check(self):
+        st = self.table.export_status()
+        if not halo_ok(self.shard, st):
+            raise HaloError(f"shard {self.shard.s}: an owned window now reaches past the halo "
+                            f"[{self.shard.b0}, {self.shard.b1}); rebuild the shard")
+
+    def update_status(self, status):
+        self.table.update_status(status)
+        self._check()
+
+    def patch_status(self, nodes, status):
+        self.table.patch_status(nodes, status)
+        self._check()
+
+    def refresh_status(self, now_ns: int, stream=None):
+        import torch
+
+        self.table.refresh_status(now_ns, stream=stream)
+        torch.cuda.synchronize(self.table.device)
+        self._check()
+
+    def __getattr__(self, name):  # queries and the rest: the DeviceTable's
+        return getattr(self.table, name)
+
+    def close(self):
+        self.table.close()
+
+
 def route_queries(targets, spec: ShardSpec, group=None):
     """Serving-mode exchange: send each target to its owner shard (its top shard_bits bits; one rank
     per shard) with all_to_all_single. `targets` is a (q, 20) uint8 tensor on the backend's device

@@ -169,6 +169,12 @@ class DeviceTable:
         check(lib().kad_table_export(self._h, ptr(ids), ptr(st), ptr(first), ptr(off)), "kad_table_export")
         return ids[:n], st[:n], first[:B], off
 
+    def export_status(self):
+        """The device's status bytes (n,), e.g. after refresh_status."""
+        st = np.zeros(max(self.n, 1), np.uint8)
+        check(lib().kad_table_export(self._h, None, ptr(st), None, None), "kad_table_export")
+        return st[:self.n]
+
     def set_addrs(self, addrs) -> None:
         """Node address records (n, 6) for IPv4 (in_addr + port bytes) or (n, 18) for IPv6."""
         addrs = np.ascontiguousarray(addrs, dtype=np.uint8)

@@ -48,3 +48,33 @@ def test_window_radii_matches_oracle_rounds():
                     lo -= 1
                     g += good[lo]
             assert R[b] == r
+
+
+def test_halo_ok_detects_a_shrunk_halo():
+    """The halo is sized from the build-time good counts; turning the owned edge buckets' nodes bad makes
+    windows run past it, which halo_ok must report (ShardTable raises HaloError on it)."""
+    from opendht_amd.sharded import halo_ok
+
+    spec = ShardSpec(n_shards=4, depth=10, mean_per_bucket=6.0, seed=91)
+    sh = build_shard(spec, 1)
+    assert halo_ok(sh, sh.status)
+    st = sh.status.copy()
+    lo_node = int(sh.off[sh.lo - sh.b0])
+    st[lo_node:lo_node + 400] = 0  # the first owned buckets go dubious: their windows grow leftwards
+    assert not halo_ok(sh, st)
+
+
+@pytest.mark.gpu
+def test_shard_table_raises_on_halo_overrun(gpu):
+    from opendht_amd.sharded import HaloError, ShardTable
+
+    spec = ShardSpec(n_shards=4, depth=10, mean_per_bucket=6.0, seed=92)
+    sh = build_shard(spec, 2)
+    T = ShardTable(sh, device=0)
+    st = sh.status.copy()
+    T.patch_status(np.arange(5, dtype=np.uint32), st[:5])  # no change: fine
+    lo_node = int(sh.off[sh.lo - sh.b0])
+    nodes = np.arange(lo_node, lo_node + 400, dtype=np.uint32)
+    with pytest.raises(HaloError):
+        T.patch_status(nodes, np.zeros(400, np.uint8))
+    T.close()
