@@ -282,9 +282,12 @@ int kad_parse_nodes_batch(const uint8_t* records, uint32_t n, uint32_t rec_len, 
  * BUILD-DEFINED model (kad_swarm.hip header): n peers with shape-K routing tables (Dht::onNewNode
  * policy, dht.cpp:867-936) built on the device; lookups run synchronous hops of
  * MAX_REQUESTED_SEARCH_NODES = 4 findClosestNodes(t, 8) answers merged by Search::insertNode
- * (dht.cpp:961-1047) into a SEARCH_NODES = 14 list, until its first 8 nodes have been queried. */
+ * (dht.cpp:961-1047, with its bad-node accounting) into a list of SEARCH_NODES = 14 non-bad nodes, until
+ * the first 8 non-bad nodes have answered. A share of the peers can be offline: queried, they do not answer
+ * and become bad (expired) search nodes. */
 #define KAD_SWARM_LEVELS 28u        /* bucket levels per peer table (depth <= 27) */
 #define KAD_SEARCH_NODES_LEN 14u    /* dht.h:314 SEARCH_NODES */
+#define KAD_SEARCH_LIST 32u         /* list capacity: SEARCH_NODES non-bad nodes + the bad ones kept among them */
 typedef struct kad_swarm kad_swarm;
 typedef struct kad_search kad_search;
 /* sorted_ids: host, n x 20 bytes, strictly ascending; peer index = position. */
@@ -300,16 +303,19 @@ int kad_swarm_get_table(const kad_swarm* s, uint32_t peer, uint32_t* depth, uint
 int kad_swarm_closest_batch(const kad_swarm* s, const uint32_t* peers, const uint8_t* targets, uint32_t q,
                             uint32_t count, uint32_t* out_idx, uint8_t* out_cnt, void* stream);
 /* S lookups (src peer, target); src/targets host or device. The initial list is the source's
- * findClosestNodes(t, 14); asynchronous on `stream`. */
+ * findClosestNodes(t, 14). offline_per_10k: share of the peers (by a hash of the index) that never answer,
+ * per 10,000 (0: all online). Asynchronous on `stream`. */
 int kad_search_create(kad_search** out, const kad_swarm* s, uint32_t S, const uint32_t* src,
-                      const uint8_t* targets, void* stream);
+                      const uint8_t* targets, uint32_t offline_per_10k, void* stream);
 /* One synchronous hop for every running lookup; *n_active (if given) = lookups still running
  * after it (synchronises the stream). */
 int kad_search_hop(kad_search* x, uint32_t* n_active);
-/* Host outputs (any may be NULL): list S x 14 peer indices (KAD_NO_NODE padded), queried flags
- * S x 14, list length S, hops S, done S (0 running, 1 first 8 queried, 2 stalled). */
-int kad_search_get(const kad_search* x, uint32_t* list, uint8_t* queried, uint8_t* n, uint32_t* hops,
-                   uint8_t* done);
+/* Host outputs (any may be NULL): list S x KAD_SEARCH_LIST peer indices (KAD_NO_NODE padded), queried and
+ * bad flags S x KAD_SEARCH_LIST, list length S, hops S, done S (0 running, 1 synced: the first 8 non-bad
+ * nodes answered, 2 stalled, 3 expired: the first min(size, 25) nodes are bad), overflow (1 value: lists that
+ * reached KAD_SEARCH_LIST entries). */
+int kad_search_get(const kad_search* x, uint32_t* list, uint8_t* queried, uint8_t* bad, uint8_t* n, uint32_t* hops,
+                   uint8_t* done, uint32_t* overflow);
 int kad_search_destroy(kad_search* x);
 
 /* ---- InfoHash primitives (infohash.h), batched, device pointers ---------- */

@@ -85,9 +85,9 @@ SIGNATURES = {
     "kad_swarm_info": (C.c_int, [_P, _P, _P]),
     "kad_swarm_get_table": (C.c_int, [_P, C.c_uint32, _P, _P, _P]),
     "kad_swarm_closest_batch": (C.c_int, [_P, _P, _P, C.c_uint32, C.c_uint32, _P, _P, _P]),
-    "kad_search_create": (C.c_int, [C.POINTER(_P), _P, C.c_uint32, _P, _P, _P]),
+    "kad_search_create": (C.c_int, [C.POINTER(_P), _P, C.c_uint32, _P, _P, C.c_uint32, _P]),
     "kad_search_hop": (C.c_int, [_P, _P]),
-    "kad_search_get": (C.c_int, [_P, _P, _P, _P, _P, _P]),
+    "kad_search_get": (C.c_int, [_P, _P, _P, _P, _P, _P, _P, _P]),
     "kad_search_destroy": (C.c_int, [_P]),
     "kad_xor_cmp_batch": (C.c_int, [_P, _P, _P, C.c_uint32, _P, _P]),
     "kad_common_bits_batch": (C.c_int, [_P, _P, C.c_uint32, _P, _P]),

@@ -46,7 +46,9 @@ constexpr uint32_t NONE = 0xFFFFFFFFu;
 constexpr uint32_t L = KAD_SWARM_LEVELS;
 constexpr uint32_t BK = 8;   // TARGET_NODES per bucket
 constexpr uint32_t SN = 14;  // SEARCH_NODES (dht.h:314)
-constexpr uint32_t SNP = 16; // list stride
+constexpr uint32_t SNP = 16; // per-peer answer width (count <= 16)
+constexpr uint32_t LST = KAD_SEARCH_LIST;  // search list capacity: SEARCH_NODES non-bad nodes + the bad ones
+constexpr uint32_t MAX_BAD = 25;           // SEARCH_MAX_BAD_NODES (dht.h:316-324)
 constexpr uint32_t ALPHA = 4;
 constexpr int BLOCK = 256;
 
@@ -249,25 +251,42 @@ __global__ void swarm_closest_kernel(SwarmDev W, const uint32_t* peers, const ui
 struct SearchDev {
     const uint32_t* src;
     const uint8_t* targets;
-    uint32_t* li;   // [S][SNP] list peer indices
-    uint64_t* lk;   // [S][SNP] their keys
-    uint8_t* lq;    // [S][SNP] queried
+    uint32_t* li;   // [S][LST] list peer indices
+    uint64_t* lk;   // [S][LST] their keys
+    uint8_t* lq;    // [S][LST] queried
+    uint8_t* lb;    // [S][LST] bad (SearchNode::isBad: expired)
     uint8_t* ln;    // [S] list length
     uint32_t* hops; // [S]
-    uint8_t* done;  // [S] 0 running, 1 synced, 2 stalled
+    uint8_t* done;  // [S] 0 running, 1 synced, 2 stalled, 3 expired
     uint32_t* sel;  // [S][ALPHA] nodes queried this hop (NONE padded)
     uint32_t* ri;   // [S][ALPHA][BK] answers
     uint64_t* rk;
     uint8_t* rn;    // [S][ALPHA]
     uint32_t* active;
+    uint32_t* overflow;  // lists that hit LST entries (a bad node was dropped from the end)
     uint32_t S;
+    uint32_t offline;    // peers offline per 10,000 (swarm_offline)
 };
 
-// first <= ALPHA unqueried nodes in list order -> sel, marked queried; none -> stalled
-__device__ __forceinline__ void select_next(const SearchDev& X, uint32_t s, uint32_t n, uint8_t* q, const uint32_t* li) {
+__device__ __forceinline__ uint64_t sw_mix(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+// Whether peer p is offline (never answers) in a lookup run: a fixed share of the peers by a hash of the index.
+__device__ __forceinline__ bool swarm_offline(uint32_t p, uint32_t per10k) {
+    return per10k && (uint32_t)(sw_mix((uint64_t)p * 0x9E37ull + 0xBADull) % 10000ull) < per10k;
+}
+
+// first <= ALPHA nodes in list order that are neither queried nor bad (searchSendGetValues / canGet,
+// dht.cpp:302-304, 1171-1235) -> sel, marked queried; none -> stalled
+__device__ __forceinline__ void select_next(const SearchDev& X, uint32_t s, uint32_t n, uint8_t* q, const uint8_t* bd,
+                                            const uint32_t* li) {
     uint32_t k = 0;
     for (uint32_t j = 0; j < n && k < ALPHA; j++)
-        if (!q[j]) { X.sel[(size_t)s * ALPHA + k++] = li[j]; q[j] = 1; }
+        if (!q[j] && !bd[j]) { X.sel[(size_t)s * ALPHA + k++] = li[j]; q[j] = 1; }
     for (uint32_t j = k; j < ALPHA; j++) X.sel[(size_t)s * ALPHA + j] = NONE;
     if (k == 0) X.done[s] = 2;
 }
@@ -277,21 +296,22 @@ __global__ void search_init_kernel(SwarmDev W, SearchDev X) {
     if (s >= X.S) return;
     uint32_t li[SNP];
     uint64_t lk[SNP];
-    uint8_t q[SNP] = {0};
+    uint8_t q[SNP] = {0}, bd[SNP] = {0};
     const uint32_t p = X.src[s];
     const uint32_t n = p < W.n ? peer_closest<SNP>(W, p, load_tgt(X.targets, s), SN, li, lk) : 0u;
     X.done[s] = n ? 0 : 2;
     X.hops[s] = 0;
     X.ln[s] = (uint8_t)n;
-    if (n) select_next(X, s, n, q, li);
-    for (uint32_t j = 0; j < SNP; j++) {
-        X.li[(size_t)s * SNP + j] = j < n ? li[j] : NONE;
-        X.lk[(size_t)s * SNP + j] = j < n ? lk[j] : ~0ull;
-        X.lq[(size_t)s * SNP + j] = j < n ? q[j] : 0;
+    if (n) select_next(X, s, n, q, bd, li);
+    for (uint32_t j = 0; j < LST; j++) {
+        X.li[(size_t)s * LST + j] = j < n ? li[j] : NONE;
+        X.lk[(size_t)s * LST + j] = j < n ? lk[j] : ~0ull;
+        X.lq[(size_t)s * LST + j] = j < n ? q[j] : 0;
+        X.lb[(size_t)s * LST + j] = 0;
     }
 }
 
-// one lane per (search, queried node): its findClosestNodes(t, 8)
+// one lane per (search, queried node): its findClosestNodes(t, 8), or nothing if it is offline
 __global__ void search_query_kernel(SwarmDev W, SearchDev X) {
     const uint32_t g = blockIdx.x * BLOCK + threadIdx.x;
     if (g >= X.S * ALPHA) return;
@@ -299,7 +319,8 @@ __global__ void search_query_kernel(SwarmDev W, SearchDev X) {
     const uint32_t v = X.done[s] ? NONE : X.sel[g];
     uint32_t oi[BK];
     uint64_t ok[BK];
-    const uint32_t m = v < W.n ? peer_closest<BK>(W, v, load_tgt(X.targets, s), BK, oi, ok) : 0u;
+    const bool up = v < W.n && !swarm_offline(v, X.offline);
+    const uint32_t m = up ? peer_closest<BK>(W, v, load_tgt(X.targets, s), BK, oi, ok) : 0u;
     for (uint32_t j = 0; j < m; j++) {
         X.ri[(size_t)g * BK + j] = oi[j];
         X.rk[(size_t)g * BK + j] = ok[j];
@@ -307,64 +328,126 @@ __global__ void search_query_kernel(SwarmDev W, SearchDev X) {
     X.rn[g] = (uint8_t)m;
 }
 
-// one lane per search: Search::insertNode of every answer (order-independent: the list ends as the
-// 14 closest distinct nodes), then the isSynced check and the next hop's selection
+// Search::insertNode of node r (not expired) at top-64 distance rd (dht.cpp:961-1047, expired search = false):
+// its place is after every closer entry; if the list already holds SEARCH_NODES non-bad nodes it is first cut
+// after the last prefix with SEARCH_NODES non-bad nodes (an insert beyond that point is refused), then
+// trimmed from the end while it holds more than SEARCH_NODES non-bad nodes. Static indices only.
+__device__ __forceinline__ void search_insert(const SwarmDev& W, const Tgt& t, uint32_t (&li)[LST], uint64_t (&ld)[LST],
+                                              uint8_t (&q)[LST], uint8_t (&bd)[LST], uint32_t& n, uint32_t r,
+                                              uint64_t rd, bool& ovf) {
+    bool found = false;
+    uint32_t pos = 0, bad = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < LST; k++) {
+        if (k < n) {
+            found |= li[k] == r;
+            pos += ld[k] < rd || (ld[k] == rd && li[k] != r && tail_less(W, t, li[k], r));
+            bad += bd[k];
+        }
+    }
+    if (found) return;
+    const bool full = n - bad >= SN;
+    // tt = the largest t <= n whose prefix [0, t) holds at most SEARCH_NODES non-bad nodes
+    uint32_t tt = 0, nb = 0, badt = 0, bb = 0;
+#pragma unroll
+    for (uint32_t k = 0; k <= LST; k++) {
+        if (k <= n && nb <= SN) { tt = k; badt = bb; }
+        if (k < n && k < LST) { nb += bd[k] ? 0u : 1u; bb += bd[k]; }
+    }
+    if (full) {
+        n = tt;
+        bad = badt;
+        if (pos >= tt) return;
+    }
+    if (n == LST) {  // capacity: drop the farthest entry (counted; never reached in the tests)
+        bad -= bd[LST - 1];
+        n--;
+        ovf = true;
+        if (pos >= n) return;
+    }
+    // insert at pos
+#pragma unroll
+    for (uint32_t k = LST - 1; k > 0; k--) {
+        if (k > pos && k <= n) { li[k] = li[k - 1]; ld[k] = ld[k - 1]; q[k] = q[k - 1]; bd[k] = bd[k - 1]; }
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < LST; k++) {
+        if (k == pos) { li[k] = r; ld[k] = rd; q[k] = 0; bd[k] = 0; }
+    }
+    n++;
+    // while more than SEARCH_NODES non-bad nodes: drop the last one
+#pragma unroll
+    for (int k = (int)LST - 1; k >= 0; k--) {
+        if ((uint32_t)k == n - 1 && n - bad > SN) {
+            bad -= bd[k];
+            n--;
+        }
+    }
+}
+
+// one lane per search: Search::insertNode of every answer in the order of the queried nodes, then the
+// offline queried nodes turn bad (expired), then the isSynced / expired checks and the next hop's selection
 __global__ void search_merge_kernel(SwarmDev W, SearchDev X) {
     const uint32_t s = blockIdx.x * BLOCK + threadIdx.x;
     bool running = false;
     if (s < X.S && !X.done[s]) {
         const Tgt t = load_tgt(X.targets, s);
-        uint32_t li[SNP];
-        uint64_t ld[SNP];  // top-64 XOR distances
-        uint8_t q[SNP];
+        uint32_t li[LST];
+        uint64_t ld[LST];  // top-64 XOR distances
+        uint8_t q[LST], bd[LST];
         uint32_t n = X.ln[s];
-        for (uint32_t j = 0; j < SNP; j++) {
-            li[j] = X.li[(size_t)s * SNP + j];
-            ld[j] = X.lk[(size_t)s * SNP + j] ^ t.hi;
-            q[j] = X.lq[(size_t)s * SNP + j];
+#pragma unroll
+        for (uint32_t j = 0; j < LST; j++) {
+            li[j] = X.li[(size_t)s * LST + j];
+            ld[j] = X.lk[(size_t)s * LST + j] ^ t.hi;
+            q[j] = X.lq[(size_t)s * LST + j];
+            bd[j] = X.lb[(size_t)s * LST + j];
         }
         const uint32_t src = X.src[s];
+        bool ovf = false;
         for (uint32_t a = 0; a < ALPHA; a++) {
             const uint32_t g = s * ALPHA + a;
             const uint32_t rn = X.rn[g];
             for (uint32_t j = 0; j < rn; j++) {
                 const uint32_t r = X.ri[(size_t)g * BK + j];
                 if (r == src) continue;  // deserializeNodes drops our own ID (network_engine.cpp:798-799)
-                const uint64_t rd = X.rk[(size_t)g * BK + j] ^ t.hi;
-                bool found = false;
-                uint32_t pos = 0;  // nodes strictly closer than r
-                for (uint32_t k = 0; k < SN; k++) {
-                    if (k >= n) break;
-                    found |= li[k] == r;
-                    pos += ld[k] < rd || (ld[k] == rd && li[k] != r && tail_less(W, t, li[k], r));
-                }
-                if (found || (n >= SN && pos >= SN)) continue;
-                // insert at pos, shift the rest down, trim to SN
-                uint32_t ci = r;
-                uint64_t cd = rd;
-                uint8_t cq = 0;
-                for (uint32_t k = pos; k < SN; k++) {
-                    if (k > n) break;
-                    const uint32_t ti = li[k];
-                    const uint64_t td = ld[k];
-                    const uint8_t tq = q[k];
-                    li[k] = ci; ld[k] = cd; q[k] = cq;
-                    ci = ti; cd = td; cq = tq;
-                }
-                n = min(n + 1, SN);
+                search_insert(W, t, li, ld, q, bd, n, r, X.rk[(size_t)g * BK + j] ^ t.hi, ovf);
             }
         }
-        X.hops[s] += 1;
-        bool synced = n > 0;
-        for (uint32_t j = 0; j < n && j < BK; j++) synced &= q[j] != 0;
-        if (synced) X.done[s] = 1;
-        else select_next(X, s, n, q, li);
-        X.ln[s] = (uint8_t)n;
-        for (uint32_t j = 0; j < SNP; j++) {
-            X.li[(size_t)s * SNP + j] = j < n ? li[j] : NONE;
-            X.lk[(size_t)s * SNP + j] = j < n ? ld[j] ^ t.hi : ~0ull;
-            X.lq[(size_t)s * SNP + j] = j < n ? q[j] : 0;
+        for (uint32_t a = 0; a < ALPHA; a++) {  // the silent ones: expired after their tries -> bad
+            const uint32_t v = X.sel[(size_t)s * ALPHA + a];
+            if (v == NONE || !swarm_offline(v, X.offline)) continue;
+#pragma unroll
+            for (uint32_t k = 0; k < LST; k++)
+                if (k < n && li[k] == v) bd[k] = 1;
         }
+        X.hops[s] += 1;
+        // Search::isSynced: the first TARGET_NODES non-bad nodes answered; consecutive bad nodes from the front
+        uint32_t good = 0, cb = 0;
+        bool synced = true, stop = false, lead = true;
+#pragma unroll
+        for (uint32_t k = 0; k < LST; k++) {
+            if (k < n) {
+                lead &= bd[k] != 0;
+                cb += lead ? 1u : 0u;
+                if (!stop && !bd[k]) {
+                    if (!q[k]) { synced = false; stop = true; }
+                    else if (++good == BK) stop = true;
+                }
+            }
+        }
+        if (synced && good > 0) X.done[s] = 1;
+        else if (n > 0 && cb >= min(n, MAX_BAD)) X.done[s] = 3;
+        else select_next(X, s, n, q, bd, li);
+        X.ln[s] = (uint8_t)n;
+#pragma unroll
+        for (uint32_t j = 0; j < LST; j++) {
+            X.li[(size_t)s * LST + j] = j < n ? li[j] : NONE;
+            X.lk[(size_t)s * LST + j] = j < n ? ld[j] ^ t.hi : ~0ull;
+            X.lq[(size_t)s * LST + j] = j < n ? q[j] : 0;
+            X.lb[(size_t)s * LST + j] = j < n ? bd[j] : 0;
+        }
+        if (ovf) atomicAdd(X.overflow, 1u);
         running = !X.done[s];
     }
     const uint64_t m = __ballot(running);
@@ -511,7 +594,7 @@ int kad_swarm_closest_batch(const kad_swarm* s, const uint32_t* peers, const uin
 }
 
 int kad_search_create(kad_search** out, const kad_swarm* s, uint32_t S, const uint32_t* src, const uint8_t* targets,
-                      void* stream) {
+                      uint32_t offline_per_10k, void* stream) {
     if (!out || !s || (S && (!src || !targets))) return err(KAD_ERR_INVALID, "NULL argument");
     *out = nullptr;
     Guard g(s->device);
@@ -521,12 +604,18 @@ int kad_search_create(kad_search** out, const kad_swarm* s, uint32_t S, const ui
     x->stream = (hipStream_t)stream;
     SearchDev& X = x->X;
     X.S = S;
+    if (offline_per_10k > 10000) {
+        delete x;
+        return err(KAD_ERR_INVALID, "offline_per_10k %u > 10000", offline_per_10k);
+    }
+    X.offline = offline_per_10k;
     uint32_t* dsrc;
     uint8_t* dt;
     int rc;
     if ((rc = alloc(&dsrc, S, x->owned)) || (rc = alloc(&dt, 20ull * S, x->owned)) ||
-        (rc = alloc(&X.li, (size_t)S * SNP, x->owned)) || (rc = alloc(&X.lk, (size_t)S * SNP, x->owned)) ||
-        (rc = alloc(&X.lq, (size_t)S * SNP, x->owned)) || (rc = alloc(&X.ln, S, x->owned)) ||
+        (rc = alloc(&X.li, (size_t)S * LST, x->owned)) || (rc = alloc(&X.lk, (size_t)S * LST, x->owned)) ||
+        (rc = alloc(&X.lq, (size_t)S * LST, x->owned)) || (rc = alloc(&X.lb, (size_t)S * LST, x->owned)) ||
+        (rc = alloc(&X.ln, S, x->owned)) || (rc = alloc(&X.overflow, 1, x->owned)) ||
         (rc = alloc(&X.hops, S, x->owned)) || (rc = alloc(&X.done, S, x->owned)) ||
         (rc = alloc(&X.sel, (size_t)S * ALPHA, x->owned)) || (rc = alloc(&X.ri, (size_t)S * ALPHA * BK, x->owned)) ||
         (rc = alloc(&X.rk, (size_t)S * ALPHA * BK, x->owned)) || (rc = alloc(&X.rn, (size_t)S * ALPHA, x->owned)) ||
@@ -541,6 +630,10 @@ int kad_search_create(kad_search** out, const kad_swarm* s, uint32_t S, const ui
     }
     X.src = dsrc;
     X.targets = dt;
+    if (hipMemsetAsync(X.overflow, 0, 4, x->stream) != hipSuccess) {
+        delete x;
+        return err(KAD_ERR_HIP, "search init failed");
+    }
     if (S) hipLaunchKernelGGL(search_init_kernel, dim3(grid_for(S)), dim3(BLOCK), 0, x->stream, s->W, X);
     if (hipGetLastError() != hipSuccess) {
         delete x;
@@ -567,26 +660,20 @@ int kad_search_hop(kad_search* x, uint32_t* n_active) {
     return KAD_OK;
 }
 
-int kad_search_get(const kad_search* x, uint32_t* list, uint8_t* queried, uint8_t* n, uint32_t* hops, uint8_t* done) {
+int kad_search_get(const kad_search* x, uint32_t* list, uint8_t* queried, uint8_t* bad, uint8_t* n, uint32_t* hops,
+                   uint8_t* done, uint32_t* overflow) {
     if (!x) return err(KAD_ERR_INVALID, "NULL search");
     Guard g(x->device);
     const SearchDev& X = x->X;
     SW_TRY(hipStreamSynchronize(x->stream));
     const size_t S = X.S;
-    if (list || queried) {
-        std::vector<uint32_t> li(S * SNP);
-        std::vector<uint8_t> lq(S * SNP);
-        SW_TRY(hipMemcpy(li.data(), X.li, 4 * S * SNP, hipMemcpyDeviceToHost));
-        SW_TRY(hipMemcpy(lq.data(), X.lq, S * SNP, hipMemcpyDeviceToHost));
-        for (size_t s = 0; s < S; s++)
-            for (uint32_t j = 0; j < SN; j++) {
-                if (list) list[s * SN + j] = li[s * SNP + j];
-                if (queried) queried[s * SN + j] = lq[s * SNP + j];
-            }
-    }
+    if (list) SW_TRY(hipMemcpy(list, X.li, 4 * S * LST, hipMemcpyDeviceToHost));
+    if (queried) SW_TRY(hipMemcpy(queried, X.lq, S * LST, hipMemcpyDeviceToHost));
+    if (bad) SW_TRY(hipMemcpy(bad, X.lb, S * LST, hipMemcpyDeviceToHost));
     if (n) SW_TRY(hipMemcpy(n, X.ln, S, hipMemcpyDeviceToHost));
     if (hops) SW_TRY(hipMemcpy(hops, X.hops, 4 * S, hipMemcpyDeviceToHost));
     if (done) SW_TRY(hipMemcpy(done, X.done, S, hipMemcpyDeviceToHost));
+    if (overflow) SW_TRY(hipMemcpy(overflow, X.overflow, 4, hipMemcpyDeviceToHost));
     return KAD_OK;
 }
 

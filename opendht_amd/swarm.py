@@ -11,6 +11,7 @@ from ._lib import check, lib, ptr
 
 LEVELS = 28
 SEARCH_NODES = 14
+SEARCH_LIST = 32  # KAD_SEARCH_LIST
 
 
 class Swarm:
@@ -63,19 +64,20 @@ class Swarm:
               "kad_swarm_closest_batch")
         return idx, cnt
 
-    def search(self, src, targets) -> "Search":
-        return Search(self, src, targets)
+    def search(self, src, targets, offline_per_10k: int = 0) -> "Search":
+        return Search(self, src, targets, offline_per_10k)
 
 
 class Search:
-    def __init__(self, swarm: Swarm, src, targets):
+    def __init__(self, swarm: Swarm, src, targets, offline_per_10k: int = 0):
         import torch
 
         self.S = src.shape[0]
         self.swarm = swarm
         h = C.c_void_p()
         s = C.c_void_p(torch.cuda.current_stream(swarm.device).cuda_stream)
-        check(lib().kad_search_create(C.byref(h), swarm._h, self.S, ptr(src), ptr(targets), s), "kad_search_create")
+        check(lib().kad_search_create(C.byref(h), swarm._h, self.S, ptr(src), ptr(targets), offline_per_10k, s),
+              "kad_search_create")
         self._h = h
 
     def hop(self) -> int:
@@ -90,15 +92,22 @@ class Search:
                 return h + 1
         return max_hops
 
-    def get(self):
+    def get(self, full: bool = False):
+        """(list, queried, n, hops, done) with lists cut to SEARCH_NODES entries; full=True: (list, queried,
+        bad, n, hops, done, overflow) with the KAD_SEARCH_LIST-wide lists."""
         S = self.S
-        lst = np.empty((S, SEARCH_NODES), np.uint32)
-        q = np.empty((S, SEARCH_NODES), np.uint8)
+        lst = np.empty((S, SEARCH_LIST), np.uint32)
+        q = np.empty((S, SEARCH_LIST), np.uint8)
+        bad = np.empty((S, SEARCH_LIST), np.uint8)
         n = np.empty((S,), np.uint8)
         hops = np.empty((S,), np.uint32)
         done = np.empty((S,), np.uint8)
-        check(lib().kad_search_get(self._h, ptr(lst), ptr(q), ptr(n), ptr(hops), ptr(done)), "kad_search_get")
-        return lst, q, n, hops, done
+        ovf = C.c_uint32()
+        check(lib().kad_search_get(self._h, ptr(lst), ptr(q), ptr(bad), ptr(n), ptr(hops), ptr(done), C.byref(ovf)),
+              "kad_search_get")
+        if full:
+            return lst, q, bad, n, hops, done, ovf.value
+        return lst[:, :SEARCH_NODES].copy(), q[:, :SEARCH_NODES].copy(), n, hops, done
 
     def close(self):
         if getattr(self, "_h", None):

@@ -727,28 +727,75 @@ int orc_swarm_closest(void* h, uint32_t q, const uint32_t* peers, const uint8_t*
     });
     return 0;
 }
-// Lookups for S (source, target) pairs, at most max_hops hops each. Outputs: list S x 14 (NO_NODE
-// padded), queried flags S x 14, list length, hops done, done (1 synced, 2 stalled, 0 running).
-int orc_swarm_search(void* h, uint32_t S, const uint32_t* src, const uint8_t* targets, uint32_t max_hops,
-                     uint32_t* out_list, uint8_t* out_q, uint8_t* out_n, uint32_t* out_hops, uint8_t* out_done,
-                     int nthreads) {
+// Lookups for S (source, target) pairs, at most max_hops hops each, with a share of the peers offline
+// (offline_per_10k / 10000 of them, by a hash of the peer index: swarm_offline). Outputs: list S x
+// SW_LIST (NO_NODE padded), queried flags and bad flags S x SW_LIST, list length, hops done, done
+// (0 running, 1 synced, 2 stalled, 3 expired). Search::insertNode (dht.cpp:961-1047) with its bad-node
+// accounting: the list keeps SEARCH_NODES non-bad nodes and the bad ones among them, an insert beyond the
+// trim point is refused. A queried peer that is offline does not answer; after the hop its node is
+// expired (the request's MAX_ATTEMPT_COUNT = 3 tries ran out, network_engine.cpp:243-247) and it is a bad
+// search node (SearchNode::isBad, dht.cpp:458-460). Within a hop the answers are merged in the order of the
+// queried nodes, then the silent ones turn bad. The next hop queries the first <= 4 nodes in list order
+// that are neither queried nor bad (searchSendGetValues / canGet, dht.cpp:302-304, 1171-1235). Synced:
+// the first TARGET_NODES non-bad nodes have all answered (Search::isSynced, dht.cpp:1467-1478). Expired:
+// the first min(size, SEARCH_MAX_BAD_NODES = 25) nodes are all bad (searchStep, dht.cpp:1451-1457).
+// Not modelled (documented in DESIGN.md §7.2): removeExpiredNode needs a node expired for 10 minutes,
+// longer than a lookup; `candidate` only matters after a search is synced.
+static constexpr uint32_t SW_LIST = 32, SW_MAX_BAD = 25;
+
+static inline bool swarm_offline(uint32_t p, uint32_t per10k) {
+    return per10k && (uint32_t)(sw_mix((uint64_t)p * 0x9E37ull + 0xBADull) % 10000ull) < per10k;
+}
+
+int orc_swarm_search_ex(void* h, uint32_t S, const uint32_t* src, const uint8_t* targets, uint32_t max_hops,
+                        uint32_t offline_per_10k, uint32_t* out_list, uint8_t* out_q, uint8_t* out_bad, uint8_t* out_n,
+                        uint32_t* out_hops, uint8_t* out_done, int nthreads) {
     const Swarm* s = (const Swarm*)h;
+    struct SN { uint32_t idx; uint8_t queried, bad; };
     parallel_for(S, nthreads, [&](uint32_t a, uint32_t e) {
       for (uint32_t i = a; i < e; i++) {
         const Id t(targets + (size_t)HASH_LEN * i);
-        std::vector<uint32_t> L;
-        std::vector<uint8_t> Q;
-        s->closest(src[i], t, SW_SEARCH, L);
-        Q.assign(L.size(), 0);
+        std::vector<SN> L;
+        std::vector<uint32_t> init;
+        s->closest(src[i], t, SW_SEARCH, init);
+        for (uint32_t v : init) L.push_back(SN{v, 0, 0});
         uint32_t hops = 0;
         uint8_t done = 0;
-        // the nodes of the next hop are chosen (and marked queried) as soon as the list is known:
-        // the first <= 4 unqueried ones in list order (searchSendGetValues, dht.cpp:1171-1235)
+        auto id_of = [&](uint32_t v) { return Id(s->ids + (size_t)HASH_LEN * v); };
+        // Search::insertNode(node) for a node that is not expired (dht.cpp:961-1047, expired search = false)
+        auto insert = [&](uint32_t r) {
+            const Id rid = id_of(r);
+            size_t n = L.size();
+            bool found = false;
+            while (n > 0) {
+                --n;
+                if (L[n].idx == r) { found = true; break; }
+                if (t.xorCmp(rid, id_of(L[n].idx)) > 0) { ++n; break; }
+            }
+            if (found) return;
+            size_t bad = 0;
+            for (const SN& x : L) bad += x.bad;
+            const bool full = L.size() - bad >= SW_SEARCH;
+            size_t tt = L.size();
+            while (tt - bad > SW_SEARCH) {
+                --tt;
+                if (L[tt].bad) bad--;
+            }
+            if (full) {
+                if (tt != L.size()) L.resize(tt);
+                if (n >= tt) return;
+            }
+            L.insert(L.begin() + n, SN{r, 0, 0});
+            while (L.size() - bad > SW_SEARCH) {
+                if (L.back().bad) bad--;
+                L.pop_back();
+            }
+        };
         std::vector<uint32_t> sel;
         auto select = [&]() {
             sel.clear();
             for (size_t j = 0; j < L.size() && sel.size() < SW_ALPHA; j++)
-                if (!Q[j]) { sel.push_back(L[j]); Q[j] = 1; }
+                if (!L[j].queried && !L[j].bad) { sel.push_back(L[j].idx); L[j].queried = 1; }
             if (sel.empty()) done = 2;  // stalled
         };
         select();
@@ -756,38 +803,54 @@ int orc_swarm_search(void* h, uint32_t S, const uint32_t* src, const uint8_t* ta
             hops++;
             std::vector<uint32_t> rep;
             for (uint32_t v : sel) {
+                if (swarm_offline(v, offline_per_10k)) continue;  // no answer this hop
                 s->closest(v, t, SW_BUCKET, rep);
-                for (uint32_t r : rep) {  // Search::insertNode (dht.cpp:961-1047), all nodes good
-                    if (r == src[i]) continue;  // deserializeNodes drops our own ID (network_engine.cpp:798-799)
-                    const Id rid(s->ids + (size_t)HASH_LEN * r);
-                    size_t pos = L.size();
-                    bool found = false;
-                    while (pos > 0) {
-                        if (L[pos - 1] == r) { found = true; break; }
-                        if (t.xorCmp(rid, Id(s->ids + (size_t)HASH_LEN * L[pos - 1])) > 0) break;
-                        pos--;
-                    }
-                    if (found) continue;
-                    if (L.size() >= SW_SEARCH && pos >= SW_SEARCH) continue;
-                    L.insert(L.begin() + pos, r);
-                    Q.insert(Q.begin() + pos, 0);
-                    if (L.size() > SW_SEARCH) { L.pop_back(); Q.pop_back(); }
-                }
+                for (uint32_t r : rep)
+                    if (r != src[i]) insert(r);  // deserializeNodes drops our own ID (network_engine.cpp:798-799)
             }
-            bool synced = !L.empty();  // Search::isSynced (dht.cpp:1467-1478)
-            for (size_t j = 0; j < L.size() && j < SW_BUCKET; j++) synced &= Q[j] != 0;
-            if (synced) done = 1;
+            for (uint32_t v : sel)  // the silent ones: expired after their tries, bad search nodes
+                if (swarm_offline(v, offline_per_10k))
+                    for (SN& x : L)
+                        if (x.idx == v) x.bad = 1;
+            uint32_t good = 0;  // Search::isSynced
+            bool synced = true;
+            for (const SN& x : L) {
+                if (x.bad) continue;
+                if (!x.queried) { synced = false; break; }
+                if (++good == SW_BUCKET) break;
+            }
+            uint32_t cb = 0;  // getNumberOfConsecutiveBadNodes
+            while (cb < L.size() && L[cb].bad) cb++;
+            if (synced && good > 0) done = 1;
+            else if (!L.empty() && cb >= std::min<size_t>(L.size(), SW_MAX_BAD)) done = 3;
             else select();
         }
-        for (uint32_t j = 0; j < SW_SEARCH; j++) {
-            out_list[(size_t)i * SW_SEARCH + j] = j < L.size() ? L[j] : 0xFFFFFFFFu;
-            out_q[(size_t)i * SW_SEARCH + j] = j < L.size() ? Q[j] : 0;
+        for (uint32_t j = 0; j < SW_LIST; j++) {
+            out_list[(size_t)i * SW_LIST + j] = j < L.size() ? L[j].idx : 0xFFFFFFFFu;
+            out_q[(size_t)i * SW_LIST + j] = j < L.size() ? L[j].queried : 0;
+            out_bad[(size_t)i * SW_LIST + j] = j < L.size() ? L[j].bad : 0;
         }
-        out_n[i] = (uint8_t)L.size();
+        out_n[i] = (uint8_t)std::min<size_t>(L.size(), 255);
         out_hops[i] = hops;
         out_done[i] = done;
       }
     });
+    return 0;
+}
+
+// All peers online (the round-1 interface): lists of SEARCH_NODES.
+int orc_swarm_search(void* h, uint32_t S, const uint32_t* src, const uint8_t* targets, uint32_t max_hops,
+                     uint32_t* out_list, uint8_t* out_q, uint8_t* out_n, uint32_t* out_hops, uint8_t* out_done,
+                     int nthreads) {
+    std::vector<uint32_t> l((size_t)S * SW_LIST);
+    std::vector<uint8_t> q((size_t)S * SW_LIST), bad((size_t)S * SW_LIST);
+    orc_swarm_search_ex(h, S, src, targets, max_hops, 0, l.data(), q.data(), bad.data(), out_n, out_hops, out_done,
+                        nthreads);
+    for (size_t i = 0; i < S; i++)
+        for (uint32_t j = 0; j < SW_SEARCH; j++) {
+            out_list[i * SW_SEARCH + j] = l[i * SW_LIST + j];
+            out_q[i * SW_SEARCH + j] = q[i * SW_LIST + j];
+        }
     return 0;
 }
 }  // extern "C" (swarm)

@@ -47,6 +47,7 @@ _SIG = {
     "orc_swarm_table": (None, [_P, C.c_uint32, _P, _P, _P]),
     "orc_swarm_closest": (C.c_int, [_P, C.c_uint32, _P, _P, C.c_uint32, _P, _P, C.c_int]),
     "orc_swarm_search": (C.c_int, [_P, C.c_uint32, _P, _P, C.c_uint32, _P, _P, _P, _P, _P, C.c_int]),
+    "orc_swarm_search_ex": (C.c_int, [_P, C.c_uint32, _P, _P, C.c_uint32, C.c_uint32, _P, _P, _P, _P, _P, _P, C.c_int]),
 }
 _lib = None
 
@@ -246,7 +247,7 @@ def parse_nodes(records, rec_len, myid):
     return keep
 
 
-SW_LEVELS, SW_BUCKET, SW_SEARCH = 28, 8, 14
+SW_LEVELS, SW_BUCKET, SW_SEARCH, SW_LIST = 28, 8, 14, 32
 
 
 class SwarmModel:
@@ -297,6 +298,22 @@ class SwarmModel:
         lib().orc_swarm_search(self._h, S, _p(src), _p(t), max_hops, _p(lst), _p(qf), _p(n), _p(hops), _p(done),
                                nthreads)
         return lst, qf, n, hops, done
+
+    def search_ex(self, src, targets, offline_per_10k, max_hops=64, nthreads=8):
+        """Lookups with offline peers and Search::insertNode's bad-node accounting: (list, queried, bad, n,
+        hops, done), lists SW_LIST (32) wide."""
+        src = np.ascontiguousarray(src, np.uint32)
+        t = _ids(targets)
+        S = src.shape[0]
+        lst = np.empty((S, SW_LIST), np.uint32)
+        qf = np.empty((S, SW_LIST), np.uint8)
+        bad = np.empty((S, SW_LIST), np.uint8)
+        n = np.empty((S,), np.uint8)
+        hops = np.empty((S,), np.uint32)
+        done = np.empty((S,), np.uint8)
+        lib().orc_swarm_search_ex(self._h, S, _p(src), _p(t), max_hops, offline_per_10k, _p(lst), _p(qf), _p(bad),
+                                  _p(n), _p(hops), _p(done), nthreads)
+        return lst, qf, bad, n, hops, done
 
 
 def infohash_get(keys):

@@ -153,3 +153,119 @@ def test_swarm_gpu_parity(gpu):
         assert active == 0
         X.close()
     M.close()
+
+
+def _check_lookup_properties(ids, lst, q, bad, n, done, offline_per_10k, tg):
+    """Invariants of Search::insertNode with bad-node accounting on every lookup: the list ascends in XOR
+    distance, holds at most SEARCH_NODES non-bad nodes, its bad nodes are exactly queried offline peers, and a
+    synced lookup has its first 8 non-bad nodes queried."""
+    from opendht_amd.swarm import SEARCH_NODES
+
+    key, tk = _key(ids), _key(tg)
+    peer_off = _offline(np.arange(ids.shape[0]), offline_per_10k)
+    for i in range(lst.shape[0]):
+        m = int(n[i])
+        li = lst[i, :m].astype(np.int64)
+        assert (lst[i, m:] == O.NO_NODE).all()
+        d = key[li] ^ tk[i]
+        assert (d[1:] >= d[:-1]).all()
+        b = bad[i, :m].astype(bool)
+        assert (~b).sum() <= SEARCH_NODES
+        assert (peer_off[li[b]]).all() and q[i, :m][b].all()  # bad = an offline peer that was queried
+        assert not (peer_off[li] & q[i, :m].astype(bool) & ~b).any()  # every queried offline peer turned bad
+        if done[i] == 1:
+            nb = np.flatnonzero(~b)[:8]
+            assert nb.size > 0 and q[i, nb].all()
+
+
+def _offline(p, per10k):
+    """swarm_offline (kad_swarm.hip / kad_oracle.cpp): splitmix64 of p * 0x9E37 + 0xBAD, mod 10000 < per10k."""
+    x = (np.asarray(p, np.uint64) * np.uint64(0x9E37) + np.uint64(0xBAD)) + np.uint64(0x9E3779B97F4A7C15)
+    x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    x = x ^ (x >> np.uint64(31))
+    return (x % np.uint64(10000)) < np.uint64(per10k)
+
+
+@pytest.mark.parametrize("off", [0, 1000, 3000])
+def test_swarm_search_offline_peers_oracle(off):
+    """Config 5 with offline peers (Search::insertNode's bad-node branches, dht.cpp:961-1047): the model's
+    invariants on every lookup, and the all-online case equal to the round-1 interface."""
+    n = 30_000
+    ids = _swarm_ids(n, 0x5A6)
+    M = O.SwarmModel(ids)
+    rng = np.random.default_rng(8 + off)
+    src = rng.integers(0, n, 400).astype(np.uint32)
+    src = src[~_offline(src, off)]  # the searching peer is online
+    tg = S.random_targets(src.shape[0], seed=9)
+    lst, q, bad, nn, hops, done = M.search_ex(src, tg, off)
+    _check_lookup_properties(ids, lst, q, bad, nn, done, off, tg)
+    assert set(np.unique(done)) <= {1, 2, 3}
+    if off == 0:
+        a = M.search(src, tg)
+        np.testing.assert_array_equal(lst[:, :14], a[0])
+        np.testing.assert_array_equal(nn, a[2])
+        np.testing.assert_array_equal(done, a[4])
+        assert not bad.any()
+    else:
+        assert bad.any() and (done == 1).mean() > 0.9
+    M.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("off", [1500, 4000])
+def test_swarm_gpu_offline_hop_by_hop(gpu, off):
+    from opendht_amd.swarm import Swarm
+    n = 40_000
+    ids = _swarm_ids(n, 0x5A7)
+    M = O.SwarmModel(ids)
+    rng = np.random.default_rng(off)
+    src = rng.integers(0, n, 4000).astype(np.uint32)
+    src = src[~_offline(src, off)]
+    tg = S.random_targets(src.shape[0], seed=10)
+    with Swarm(ids, device=gpu.index or 0) as W:
+        X = W.search(torch.from_numpy(src.view(np.int32)).to(gpu), torch.from_numpy(tg).to(gpu), off)
+        for h in range(1, 48):
+            active = X.hop()
+            got = X.get(full=True)
+            want = M.search_ex(src, tg, off, max_hops=h)
+            for a, b, name in zip(got[:6], want, ("list", "queried", "bad", "n", "hops", "done")):
+                np.testing.assert_array_equal(a, b, err_msg=f"hop {h}: {name}")
+            assert got[6] == 0  # no list reached its capacity
+            if active == 0:
+                break
+        assert active == 0
+        X.close()
+    M.close()
+
+
+@pytest.mark.gpu
+def test_swarm_gpu_1m_peers(gpu):
+    """Config 5 at >= 1M peers: 200k lookups with 10 % of the peers offline, run to the end on the GPU; the
+    model's invariants on every lookup, convergence, and a sample of 1,500 lookups hop by hop against the oracle."""
+    from opendht_amd.swarm import Swarm
+    n, off = 1_000_000, 1000
+    ids = _swarm_ids(n, 0x5A8)
+    rng = np.random.default_rng(12)
+    Sn = 200_000
+    src = rng.integers(0, n, Sn).astype(np.uint32)
+    src = src[~_offline(src, off)]
+    tg = S.random_targets(src.shape[0], seed=13)
+    samp = rng.choice(src.shape[0], 1500, replace=False)
+    M = O.SwarmModel(ids, nthreads=16)
+    with Swarm(ids, device=gpu.index or 0) as W:
+        X = W.search(torch.from_numpy(src.view(np.int32)).to(gpu), torch.from_numpy(tg).to(gpu), off)
+        for h in range(1, 64):
+            active = X.hop()
+            if h in (1, 2, 4, 7) or active == 0:
+                lst, q, bad, nn, hops, done, ovf = X.get(full=True)
+                want = M.search_ex(src[samp], tg[samp], off, max_hops=h, nthreads=16)
+                for a, b, name in zip((lst, q, bad, nn, hops, done), want, ("list", "queried", "bad", "n", "hops", "done")):
+                    np.testing.assert_array_equal(a[samp], b, err_msg=f"hop {h}: {name}")
+            if active == 0:
+                break
+        assert active == 0 and ovf == 0
+        _check_lookup_properties(ids, lst, q, bad, nn, done, off, tg)
+        assert (done == 1).mean() > 0.97 and hops.max() < 30
+        X.close()
+    M.close()

@@ -21,6 +21,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--peers", type=int, default=10_000_000)
     ap.add_argument("--lookups", type=int, default=1 << 20)
+    ap.add_argument("--offline", type=int, nargs="*", default=[0, 1000],
+                    help="peers offline per 10,000 (one run per value)")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     t0 = time.perf_counter()
@@ -38,31 +40,34 @@ def main():
     X.run()
     X.close()
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    X = W.search(src, tg)
-    hop_ms, active = [], []
-    for _ in range(64):
-        h0 = time.perf_counter()
-        a = X.hop()
-        hop_ms.append((time.perf_counter() - h0) * 1e3)
-        active.append(a)
-        if a == 0:
-            break
-    torch.cuda.synchronize()
-    t_all = time.perf_counter() - t0
-    lst, q, n, hops, done = X.get()
-    queries = int(hops.sum()) * 4 + args.lookups  # findClosestNodes answers (upper bound: <= 4 per hop)
-    print(json.dumps({
-        "config": f"config5: {args.peers} peers (shape-K tables in HBM), {args.lookups} lookups, alpha 4, list 14",
-        "ids_s": round(t_ids, 2), "table_build_s": round(t_build, 2),
-        "table_gb": round(W.device_bytes() / 1e9, 2),
-        "lookups_per_s": args.lookups / t_all, "convergence_ms": t_all * 1e3, "rounds": len(hop_ms),
-        "hop_ms": [round(x, 3) for x in hop_ms], "active_after_hop": active,
-        "hops_hist": np.bincount(hops).tolist(), "mean_hops": float(hops.mean()),
-        "done_hist": np.bincount(done, minlength=3).tolist(),
-        "peer_queries_per_s_upper": queries / t_all,
-    }), flush=True)
-    X.close()
+    for off in args.offline:
+        t0 = time.perf_counter()
+        X = W.search(src, tg, off)
+        hop_ms, active = [], []
+        for _ in range(64):
+            h0 = time.perf_counter()
+            a = X.hop()
+            hop_ms.append((time.perf_counter() - h0) * 1e3)
+            active.append(a)
+            if a == 0:
+                break
+        torch.cuda.synchronize()
+        t_all = time.perf_counter() - t0
+        lst, q, bad, n, hops, done, ovf = X.get(full=True)
+        queries = int(hops.sum()) * 4 + args.lookups  # findClosestNodes answers (upper bound: <= 4 per hop)
+        print(json.dumps({
+            "config": f"config5: {args.peers} peers (shape-K tables in HBM), {args.lookups} lookups, alpha 4, "
+                      f"list 14, {off / 100:g} % of the peers offline",
+            "ids_s": round(t_ids, 2), "table_build_s": round(t_build, 2),
+            "table_gb": round(W.device_bytes() / 1e9, 2),
+            "lookups_per_s": args.lookups / t_all, "convergence_ms": t_all * 1e3, "rounds": len(hop_ms),
+            "hop_ms": [round(x, 3) for x in hop_ms], "active_after_hop": active,
+            "hops_hist": np.bincount(hops).tolist(), "mean_hops": float(hops.mean()),
+            "done_hist (running, synced, stalled, expired)": np.bincount(done, minlength=4).tolist(),
+            "bad_nodes_in_lists_mean": float(bad.sum(axis=1).mean()), "list_overflows": ovf,
+            "peer_queries_per_s_upper": queries / t_all,
+        }), flush=True)
+        X.close()
     W.close()
 
 
