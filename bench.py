@@ -87,9 +87,15 @@ def spawn(args) -> int:
     return bad[0] if bad else 0
 
 
+# Rehearsal of the N-rank flow on a one-GPU box (tests/test_bench_multirank.py): every rank on cuda:0 and gloo
+# instead of RCCL (RCCL needs one GPU per rank). Never set by the driver.
+REHEARSE_ONE_GPU = os.environ.get("KADGPU_BENCH_ONE_GPU") == "1"
+
+
 def dist_env():
-    return (int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")),
-            int(os.environ.get("LOCAL_RANK", "0")))
+    world, rank = int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0"))
+    local = 0 if REHEARSE_ONE_GPU else int(os.environ.get("LOCAL_RANK", "0"))
+    return world, rank, local
 
 
 def init_dist(world, dev):
@@ -97,9 +103,10 @@ def init_dist(world, dev):
         return None
     import torch.distributed as dist
 
-    backend = "nccl" if dev.type == "cuda" else "gloo"
-    kw = {"device_id": dev} if dev.type == "cuda" else {}
-    dist.init_process_group(backend, **kw)
+    if dev.type == "cuda" and not REHEARSE_ONE_GPU:
+        dist.init_process_group("nccl", device_id=dev)  # RCCL over xGMI
+    else:
+        dist.init_process_group("gloo")
     return dist
 
 
