@@ -218,7 +218,7 @@ def main_owner(args):
     import torch
 
     from opendht_amd import DeviceTable
-    from opendht_amd._lib import KAD_INFO_WINDOW_LINES
+    from opendht_amd._lib import KAD_INFO_SHORT_LINES, KAD_INFO_WINDOW_LINES
     from opendht_amd.metrics import rt_algorithmic_bytes
     from opendht_amd.sharded import ShardSpec, build_shard
 
@@ -242,10 +242,13 @@ def main_owner(args):
     ocnt = [torch.empty((Q,), dtype=torch.uint8, device=dev) for _ in range(NB)]
     setup_s = time.perf_counter() - t0
     stream = torch.cuda.current_stream(dev)
-    wl = bool(T.info()["flags"] & KAD_INFO_WINDOW_LINES)  # the shard's U(24) table carries all three line sets
+    flags = T.info()["flags"]
+    wl = bool(flags & KAD_INFO_WINDOW_LINES)  # the shard's U(24) table carries every line set
     kk = 8 if cnt_k <= 8 else 16 if cnt_k <= 16 else 32
-    kernel = ({8: "rt_wl_kernel<0>", 16: "rt_wl16_kernel<0>", 32: "rt_wl32_kernel"}[kk] if wl
-              else f"rt_closest_kernel<{kk}>")
+    ws = kk == 8 and bool(flags & KAD_INFO_SHORT_LINES) and os.environ.get("KAD_RT_KERNEL") not in ("wl", "lane")
+    kernel = ("rt_ws_kernel<0>" if ws else {8: "rt_wl_kernel<0>", 16: "rt_wl16_kernel<0>", 32: "rt_wl32_kernel"}[kk]
+              if wl else f"rt_closest_kernel<{kk}>")
+    line_b = 64 if ws else LINE_BYTES[kk]
 
     def step(j, s):
         T.rt_closest(tgs[j % NB], cnt_k, outs[j % NB], ocnt[j % NB], stream=s)
@@ -302,7 +305,7 @@ def main_owner(args):
     avg_kernel_s = float(np.mean(kern_ms)) / 1e3
 
     # bytes the timed kernel must move per query: the target, its ONE window line, the row and count
-    moved_q = 20 + LINE_BYTES[kk] + 4 * cnt_k + 1
+    moved_q = 20 + line_b + 4 * cnt_k + 1
     achieved = moved_q * Q / avg_kernel_s / 1e9
     # SURVEY §8(d)'s reference-structure bytes (IDs of every good node of W(R), status bytes, extents)
     # over the first batches, exact on the host; reported without a fraction (the layout reads less)
@@ -314,6 +317,16 @@ def main_owner(args):
     if tj and tj.get("kernel", "") in kernel and tj.get("count") == cnt_k:
         traffic = tj.get("hbm_bytes_per_launch")
     gath = load_json(args.gather_json)
+    # the ceiling row for this line size and table footprint (64-byte lines: 134 MB; 128-byte: 268 MB)
+    ceil = None
+    if gath and line_b in (64, 128):
+        row = "128MB_64B" if line_b == 64 else "256MB_128B"
+        a = gath.get("all", {})
+        if row in a and row + "_cold" in a:
+            ceil = {"what": f"random {line_b}-byte line gather + 20 B target read + 32 B row write per query, 1M "
+                            "queries per launch, rotated batches (tools/mb_gather.py)",
+                    "table_MB": int(row.split("MB")[0]), "line_bytes": line_b,
+                    "us_per_1M_rotated": a[row]["us_per_1M"], "us_per_1M_cold": a[row + "_cold"]["us_per_1M"]}
 
     extras = {}
     if not args.no_extras:
@@ -364,14 +377,13 @@ def main_owner(args):
                 "traffic": traffic,
                 "kernel": kernel,
                 "bytes_per_query": moved_q,
-                "bytes_basis": f"bytes the kernel must move per query: 20 target + {LINE_BYTES[kk]} window line "
-                               f"+ {4 * cnt_k} row + 1 count (exact-path extras of the rare deferred queries "
-                               "not counted)",
+                "bytes_basis": f"bytes the kernel must move per query: 20 target + {line_b} window line "
+                               f"+ {4 * cnt_k} row + 1 count (the 128-byte fallback lines and exact-path reads of "
+                               "the rare queries that need them not counted)",
                 "launch": "hip graph of K launches" if graph is not None else "K eager launches",
                 "avg_kernel_ms": avg_kernel_s * 1e3,
-                "random_line_ceiling": (gath or {}).get("ceiling"),
-                "frac_of_ceiling": ((gath or {}).get("ceiling", {}).get("us_per_1M_rotated", 0) * Q / 2**20 / 1e3
-                                    / (avg_kernel_s * 1e3)) if gath and LINE_BYTES[kk] == 128 else None,
+                "random_line_ceiling": ceil,
+                "frac_of_ceiling": (ceil["us_per_1M_rotated"] * Q / 2**20 / 1e3 / (avg_kernel_s * 1e3)) if ceil else None,
                 "alg_bytes_ref_structure": {
                     "bytes_per_query": ref_bytes / Q,
                     "basis": "SURVEY.md §8(d): 20 + sum over W(R) of (8 + n_b + 20 g_b) + 4k, the bytes the "

@@ -96,6 +96,7 @@ struct DevTable {
     const uint4* ncl;   // NodeCache lines (TF_NCL): 256 bytes per node radix slot
     const uint4* gl;    // general window lines, count <= 8 (TF_GL, any table shape): 128 bytes per bucket
     const uint4* gl32;  // general window lines, counts 9..32 (TF_GL32): 256 bytes per bucket
+    const uint4* ws;    // short window lines, count <= 8 (TF_WS, with TF_WL): 64 bytes per bucket
     uint64_t rbase, nbase;
     uint32_t rshift, rslots, nshift, nslots;
     uint32_t n, B, index_base, flags;
@@ -109,6 +110,7 @@ constexpr uint32_t TF_WL32 = 32u;    // window lines for counts 17..32 present
 constexpr uint32_t TF_NCL = 64u;     // NodeCache lines present (sorted tables)
 constexpr uint32_t TF_GL = 128u;     // general window lines (tables without TF_WL: split-policy, per-peer shapes)
 constexpr uint32_t TF_GL32 = 256u;   // general window lines for counts 9..32
+constexpr uint32_t TF_WS = 512u;     // short (64-byte) window lines for count <= 8 (uniform tables, with TF_WL)
 constexpr uint32_t WIDE = 0x80000000u;  // dir[].x flag: bucket holds > 32 nodes (masks invalid)
 constexpr uint32_t KEY_PAD = 32;        // key[] is padded so 16-node chunk loads never leave it
 
@@ -883,6 +885,185 @@ __global__ __launch_bounds__(BLOCK) void wl_build_kernel(const uint64_t* key, co
     L[1] = h | (R8 << 21) | (S << 23) | (defer ? WL_DEFER : 0u);
     L[2] = rounds;
     store_line<32>(L, lines + 32ull * b);
+}
+
+// ---------------------------------------------------------------------------------------
+// Short window lines (TF_WS): the count <= 8 line in 64 bytes, so a uniform table's lines take half the
+// bytes (a 2^21-bucket shard: 134 MB, inside the 256 MiB Infinity Cache, instead of 268 MB) and a query's
+// random gather is one 64-byte line. A short line is transcoded from the 128-byte line of the same bucket,
+// as a 512-bit little-endian bit string:
+//   [0, 32)    base (as the 128-byte line)
+//   [32, 55)   G0 | G1 << 4 | G2 << 8 (G(r) capped at 15: only compared with counts <= 8) | whole(r) << 12
+//              | R_8 << 15 | S << 17 (short slots stored: whole buckets, <= 19) | fallback << 22
+//   [55, 67)   round of the k-th stored bucket, 2 bits each (k < 6)
+//   [67, 504)  19 slots of 23 bits: start << 22 | key16 << 6 | off. start marks a slot that opens the next
+//              stored bucket (D-rank order), key16 = the top 16 of the 21 key bits; unused slots are all
+//              ones. fallback: the 128-byte line is deferred, a stored node has off >= 64, or two stored
+//              nodes of one bucket share their 16 key bits.
+// A query's rank value of slot s is (k << 22) | (slot's low 22 bits XOR t16 << 6), k = the number of start
+// bits up to s: (stored-bucket rank, in-bucket distance, offset), distinct within a line unless marked. A
+// query the short line cannot answer (fallback, or fewer stored slots than its m) reads the 128-byte line
+// (wl_answer), and from there the exact path: results are those of the 128-byte line. The stored slots
+// are a D-rank prefix of whole buckets of the 128-byte line's (buckets without good nodes store nothing
+// and are skipped by k), so the 128-byte line's argument carries over: the m smallest stored values are
+// W(R_c)'s first m nodes.
+// ---------------------------------------------------------------------------------------
+constexpr uint32_t WS_SLOTS = 19;
+constexpr uint32_t WS_KBITS = 16;
+constexpr uint32_t WS_SBITS = 23;  // slot bits
+constexpr uint32_t WS_HDR = 32, WS_ROUNDS = 55, WS_SLOT0 = 67;
+
+__device__ __forceinline__ uint32_t dw(const uint4 (&L)[4], int k) {  // static k after unrolling
+    const uint4& q = L[k >> 2];
+    return (k & 3) == 0 ? q.x : (k & 3) == 1 ? q.y : (k & 3) == 2 ? q.z : q.w;
+}
+
+// w (<= 32) bits at bit p of a short line held as 4 x uint4 (static p, w after unrolling)
+__device__ __forceinline__ uint32_t ws_bits(const uint4 (&L)[4], int p, int w) {
+    const int k = p >> 5, sh = p & 31;
+    const uint32_t mask = w == 32 ? NONE : (1u << w) - 1u;
+    if (sh + w <= 32) return (dw(L, k) >> sh) & mask;
+    return (uint32_t)((((uint64_t)dw(L, k + 1) << 32) | dw(L, k)) >> sh) & mask;
+}
+
+__device__ __forceinline__ void put_bits(uint32_t* L, uint32_t p, uint32_t w, uint32_t v) {
+    const uint32_t k = p >> 5, sh = p & 31;
+    const uint64_t mask = ((1ull << w) - 1ull) << sh;
+    uint64_t x = (uint64_t)L[k] | ((uint64_t)L[k + 1] << 32);
+    x = (x & ~mask) | (((uint64_t)v << sh) & mask);
+    L[k] = (uint32_t)x;
+    L[k + 1] = (uint32_t)(x >> 32);
+}
+
+// One thread per bucket: short line b from 128-byte line b (sel as the 128-byte builder's), assembled in
+// the thread's LDS row (odd stride), then stored as 16-byte pieces.
+__global__ __launch_bounds__(BLOCK) void ws_build_kernel(const uint32_t* __restrict__ wl, uint32_t B,
+                                                          uint32_t* __restrict__ ws, LineSel sel) {
+    __shared__ uint32_t lds[BLOCK][17];
+    uint32_t b;
+    if (!sel.pick(blockIdx.x * BLOCK + threadIdx.x, B, b)) return;
+    const uint32_t* W = wl + 32ull * b;
+    uint32_t* L = lds[threadIdx.x];
+    const uint32_t h = W[1], rounds = W[2], S = (h >> 23) & 31u;
+    bool fb = (h & WL_DEFER) != 0;
+    // the longest whole-bucket prefix of the 128-byte line's slots that fits
+    uint32_t keep = 0;
+    for (uint32_t s = 0; s < S && s < WS_SLOTS; s++)
+        if (s + 1 == S || (W[WL_SLOT0 + s + 1] >> 29) != (W[WL_SLOT0 + s] >> 29)) keep = s + 1;
+    for (int k = 0; k < 17; k++) L[k] = NONE;
+    constexpr uint32_t KSH = 8 + WL_KBITS - WS_KBITS;
+    uint32_t nb = 0, rk = 0;
+    for (uint32_t s = 0; s < keep; s++) {
+        const uint32_t v = W[WL_SLOT0 + s], j = v >> 29, k16 = (v >> KSH) & 0xFFFFu, off = v & 255u;
+        fb |= off >= 64u;
+        for (uint32_t r = 0; r < s; r++) {
+            const uint32_t u = W[WL_SLOT0 + r];
+            fb |= (u >> 29) == j && ((u >> KSH) & 0xFFFFu) == k16;
+        }
+        const bool start = s == 0 || (W[WL_SLOT0 + s - 1] >> 29) != j;
+        if (start) rk |= ((rounds >> (2 * j)) & 3u) << (2 * nb++);
+        put_bits(L, WS_SLOT0 + WS_SBITS * s, WS_SBITS, (start ? 1u << 22 : 0u) | (k16 << 6) | off);
+    }
+    const uint32_t G0 = min(h & 63u, 15u), G1 = min((h >> 6) & 63u, 15u), G2 = min((h >> 12) & 63u, 15u);
+    const uint32_t hw = G0 | (G1 << 4) | (G2 << 8) | (((h >> 18) & 7u) << 12) | (((h >> 21) & 3u) << 15) |
+                        (keep << 17) | ((fb ? 1u : 0u) << 22);
+    L[0] = W[0];
+    put_bits(L, WS_HDR, 23, hw);
+    put_bits(L, WS_ROUNDS, 12, rk);
+    store_line<16>(L, ws + 16ull * b);
+}
+
+// The short-line answer (same contract as wl_answer; the caller falls back to wl_answer when it fails).
+// ABL 2 (timing ablation, tools build only; results wrong): no ranking.
+template <int ABL>
+__device__ __forceinline__ bool ws_answer(const DevTable& T, const Target& t, uint32_t b, uint32_t count, bool act,
+                                          uint32_t (&o)[8], uint32_t& m) {
+    uint4 L[4];
+    if (act) {
+        const uint4* lp = T.ws + 4ull * b;
+#pragma unroll
+        for (int x = 0; x < 4; x++) L[x] = lp[x];
+    } else {
+#pragma unroll
+        for (int x = 0; x < 4; x++) L[x] = make_uint4(NONE, NONE, NONE, NONE);
+    }
+    const uint32_t d = 64 - T.rshift;
+    const uint32_t h = ws_bits(L, WS_HDR, 23), rounds = ws_bits(L, WS_ROUNDS, 12);
+    const uint32_t G0 = h & 15u, G1 = (h >> 4) & 15u, G2 = (h >> 8) & 15u, R8 = (h >> 15) & 3u, S = (h >> 17) & 31u;
+    const uint32_t Rc = (G0 >= count || (h >> 12) & 1u) ? 0u : (G1 >= count || (h >> 13) & 1u) ? 1u : 2u;
+    m = min(count, Rc == 0 ? G0 : Rc == 1 ? G1 : G2);
+    const bool own = (t.hi >> T.rshift) == (T.rbase >> T.rshift) + b;  // target inside bucket b's range
+    bool ex = !act || ((h >> 22) & 1u) || !own || (Rc == R8 && S < m);
+    const uint32_t tx = (uint32_t)((t.hi << d) >> (64 - WS_KBITS)) << 6;
+    uint32_t v[WS_SLOTS], k = 0;
+#pragma unroll
+    for (int s = 0; s < (int)WS_SLOTS; s++) {
+        const uint32_t x = ws_bits(L, WS_SLOT0 + WS_SBITS * s, WS_SBITS);
+        k += x >> 22;
+        v[s] = (k << 22) | ((x & 0x3FFFFFu) ^ tx);
+    }
+    if (__any(!ex && Rc < R8)) {  // count < 8 with a smaller window: drop the later rounds' buckets
+        uint32_t inc = 0;
+#pragma unroll
+        for (int j = 0; j < 6; j++) inc |= (((rounds >> (2 * j)) & 3u) <= Rc ? 1u : 0u) << (j + 1);
+        uint32_t have = 0;
+#pragma unroll
+        for (int s = 0; s < (int)WS_SLOTS; s++) {
+            const bool in = (uint32_t)s < S && ((inc >> (v[s] >> 22)) & 1u);
+            v[s] = in ? v[s] : NONE;
+            have += in;
+        }
+        ex |= have < m;
+    }
+    if (ABL < 2) {
+        sort8(v);
+        sort8(v + 8);
+        merge8(v, v + 8);
+#pragma unroll
+        for (int s = 16; s < (int)WS_SLOTS; s++) {  // insert the rest: one bubble pass each
+            v[7] = min(v[7], v[s]);
+#pragma unroll
+            for (int j = 7; j > 0; j--) cx(v[j - 1], v[j]);
+        }
+    }
+    const uint32_t base = L[0].x + T.index_base;
+#pragma unroll
+    for (int j = 0; j < 8; j++) o[j] = (uint32_t)j < m ? base + (v[j] & 63u) : NONE;
+    return !ex;
+}
+
+// 8 waves per SIMD (<= 64 VGPRs): the gather is latency-bound, occupancy is what hides it.
+// ABL 1 = no fallback and no exact path, 2 = also no ranking (timing ablations only).
+template <int ABL>
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) void rt_ws_kernel(DevTable T, const uint8_t* __restrict__ targets, uint32_t q,
+                                                      uint32_t count, uint32_t* __restrict__ out_idx,
+                                                      uint8_t* __restrict__ out_cnt) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    const bool act = i < q && count > 0;
+    if (i < q && count == 0 && out_cnt) out_cnt[i] = 0;
+    Target t{};
+    uint32_t b = 0;
+    if (act) {
+        t = load_target(targets, i);
+        b = locate_bucket(T, t);
+    }
+    uint32_t o[8], m;
+    const bool ok = ws_answer<ABL>(T, t, b, count, act, o, m);
+    if (act && ok) {
+        store_row8(out_idx + (size_t)i * count, o, count);
+        if (out_cnt) out_cnt[i] = (uint8_t)m;
+    }
+    bool need = ABL == 0 && act && !ok;
+    if (__any(need)) {  // the 128-byte line of the (few) queries the short line cannot answer
+        const bool ok2 = wl_answer<0>(T, t, b, count, need, o, m);
+        if (need && ok2) {
+            store_row8(out_idx + (size_t)i * count, o, count);
+            if (out_cnt) out_cnt[i] = (uint8_t)m;
+        }
+        need = need && !ok2;
+    }
+    __shared__ uint64_t xs[BLOCK / 64][192];
+    exact_tail(T, t, need, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -3297,6 +3478,7 @@ struct kad_table {
     uint2* dir_mut = nullptr;
     uint32_t* gpre_mut = nullptr;
     uint32_t* wl_mut = nullptr;
+    uint32_t* ws_mut = nullptr;
     uint32_t* wl16_mut = nullptr;
     uint32_t* wl32_mut = nullptr;
     uint32_t* ncl_mut = nullptr;
@@ -3377,9 +3559,13 @@ int rebuild_good_prefix(kad_table* t, hipStream_t s, bool full = true) {
                            t->dlist + (size_t)k * B, ctr + k);
         return LineSel{t->dlist + (size_t)k * B, ctr + k};
     };
+    LineSel s8{};
+    if (t->wl_mut || t->gl_mut) s8 = sel_for(t->ld8, 0);
     if (t->wl_mut)
         hipLaunchKernelGGL(wl_build_kernel, dim3(grid_for(B)), dim3(BLOCK), 0, s, t->d.key, t->d.status, t->d.dir,
-                           t->d.gpre, B, 64 - t->d.rshift, t->d.rbase >> t->d.rshift, t->wl_mut, sel_for(t->ld8, 0));
+                           t->d.gpre, B, 64 - t->d.rshift, t->d.rbase >> t->d.rshift, t->wl_mut, s8);
+    if (t->ws_mut)  // transcoded from the 128-byte lines just rebuilt, the same selection
+        hipLaunchKernelGGL(ws_build_kernel, dim3(grid_for(B)), dim3(BLOCK), 0, s, t->wl_mut, B, t->ws_mut, s8);
     if (t->wl16_mut)
         hipLaunchKernelGGL(wl16_build_kernel, dim3(grid_for(B)), dim3(BLOCK), 0, s, t->d.key, t->d.status, t->d.dir,
                            t->d.gpre, B, 64 - t->d.rshift, t->d.rbase >> t->d.rshift, t->wl16_mut, sel_for(t->ld16, 1));
@@ -3388,7 +3574,7 @@ int rebuild_good_prefix(kad_table* t, hipStream_t s, bool full = true) {
                            t->d.gpre, B, 64 - t->d.rshift, t->d.rbase >> t->d.rshift, t->wl32_mut, sel_for(t->ld32, 2));
     if (t->gl_mut)
         hipLaunchKernelGGL(gl_build_kernel, dim3(grid_for(B)), dim3(BLOCK), 0, s, t->d.key, t->d.status, t->d.dir,
-                           t->d.gpre, t->d.fkey, t->d.ftail, B, t->gl_mut, sel_for(t->ld8, 0));
+                           t->d.gpre, t->d.fkey, t->d.ftail, B, t->gl_mut, s8);
     if (t->gl32_mut)
         hipLaunchKernelGGL(gl32_build_kernel, dim3(grid_for(B)), dim3(BLOCK), 0, s, t->d.key, t->d.status, t->d.dir,
                            t->d.gpre, t->d.fkey, t->d.ftail, B, t->gl32_mut, sel_for(t->ld32, 2));
@@ -3510,14 +3696,25 @@ int check_count(uint32_t count) {
     return KAD_OK;
 }
 
-// KAD_RT_KERNEL=lane forces the lane-per-query kernel where the window-line kernel would run
-// (A/B timing, tools/ab_bench.py); read per call so one process can time both.
+// KAD_RT_KERNEL=lane forces the lane-per-query kernel where the window-line kernel would run, =wl the
+// 128-byte window lines where the short ones would (A/B timing, tools/ab_bench.py); read per call so one
+// process can time both.
 template <int K>
 int launch_rt(const kad_table* t, const uint8_t* targets, uint32_t q, uint32_t count, uint32_t* out, uint8_t* cnt,
               hipStream_t s) {
     const DevTable& d = t->d;
     const char* ev = std::getenv("KAD_RT_KERNEL");
-    if (K == 8 && (d.flags & TF_WL) && !(ev && std::strcmp(ev, "lane") == 0)) {
+    if (K == 8 && (d.flags & TF_WS) && !(ev && (std::strcmp(ev, "lane") == 0 || std::strcmp(ev, "wl") == 0 ||
+                                                 std::strncmp(ev, "wl_abl", 6) == 0))) {
+#ifdef KAD_ABLATIONS
+        if (ev && std::strcmp(ev, "ws_abl1") == 0)
+            hipLaunchKernelGGL(rt_ws_kernel<1>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
+        else if (ev && std::strcmp(ev, "ws_abl2") == 0)
+            hipLaunchKernelGGL(rt_ws_kernel<2>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
+        else
+#endif
+            hipLaunchKernelGGL(rt_ws_kernel<0>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
+    } else if (K == 8 && (d.flags & TF_WL) && !(ev && std::strcmp(ev, "lane") == 0)) {
 #ifdef KAD_ABLATIONS  // timing ablations with WRONG results: only in the tools build (Makefile target `ablations`)
         if (ev && std::strcmp(ev, "wl_abl1") == 0)
             hipLaunchKernelGGL(rt_wl_kernel<1>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
@@ -3772,6 +3969,20 @@ int kad_table_create(kad_table** out, int device, uint32_t n_nodes, const uint8_
                 d.wl = reinterpret_cast<const uint4*>(lp);
                 t->wl_mut = lp;
                 d.flags |= TF_WL;
+                uint32_t* lps;
+                if ((rc = dev_upload(&lps, nullptr, 16ull * n_buckets, t->owned, t->bytes))) {
+                    delete t;
+                    return rc;
+                }
+                hipLaunchKernelGGL(ws_build_kernel, dim3(grid_for(n_buckets)), dim3(BLOCK), 0, 0, lp, n_buckets, lps,
+                                   LineSel{});
+                if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+                    delete t;
+                    return set_err(KAD_ERR_HIP, "short window-line build failed");
+                }
+                d.ws = reinterpret_cast<const uint4*>(lps);
+                t->ws_mut = lps;
+                d.flags |= TF_WS;
                 uint32_t* lp16;
                 if ((rc = dev_upload(&lp16, nullptr, (size_t)WL16_STRIDE * n_buckets, t->owned, t->bytes))) {
                     delete t;
@@ -3849,7 +4060,8 @@ int kad_table_get_info(const kad_table* t, kad_table_info* out) {
     out->n_buckets = t->d.B;
     out->index_base = t->d.index_base;
     out->flags = t->flags | ((t->d.flags & TF_WL) ? KAD_INFO_WINDOW_LINES : 0u) |
-                 ((t->d.flags & TF_GL) ? KAD_INFO_GENERAL_LINES : 0u) | ((t->d.flags & TF_GL32) ? KAD_INFO_GENERAL_LINES32 : 0u);
+                 ((t->d.flags & TF_GL) ? KAD_INFO_GENERAL_LINES : 0u) | ((t->d.flags & TF_GL32) ? KAD_INFO_GENERAL_LINES32 : 0u) |
+                 ((t->d.flags & TF_WS) ? KAD_INFO_SHORT_LINES : 0u);
     out->device = t->device;
     out->rt_radix_bits = t->rbits;
     out->nc_radix_bits = t->nbits;
@@ -4605,6 +4817,7 @@ int kad_table_apply(kad_table* t, const uint32_t* ops, uint32_t n_ops, const uin
     }
     if (reshape || !lines_ok) {  // a split (or a new node outside its dyadic range) breaks the uniform depth
         release(t, t->wl_mut); t->wl_mut = nullptr; d.wl = nullptr; d.flags &= ~TF_WL;
+        release(t, t->ws_mut); t->ws_mut = nullptr; d.ws = nullptr; d.flags &= ~TF_WS;
         release(t, t->wl16_mut); t->wl16_mut = nullptr; d.wl16 = nullptr; d.flags &= ~TF_WL16;
         release(t, t->wl32_mut); t->wl32_mut = nullptr; d.wl32 = nullptr; d.flags &= ~TF_WL32;
     }

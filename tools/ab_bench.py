@@ -30,11 +30,13 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--count", type=int, default=8)
     ap.add_argument("--queries", type=int, default=1 << 20)
+    ap.add_argument("--batches", type=int, default=8, help="distinct target batches, one per launch in turn")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     spec = ShardSpec()
     sh = build_shard(spec, 0)
-    targets = torch.from_numpy(spec.targets_for(0, args.queries, seed=0x0D470002)).to(dev)
+    tgs = [torch.from_numpy(spec.targets_for(0, args.queries, seed=0x0D470002 + j)).to(dev) for j in range(args.batches)]
+    targets = tgs[0]
     T = DeviceTable(sh.ids, sh.status, sh.first, sh.off, device=0, index_base=sh.index_base, sorted=True)
     variants = args.variants.split(",")
     outs = {}
@@ -54,8 +56,8 @@ def main():
             os.environ["KAD_RT_KERNEL"] = v
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
-            for _ in range(args.reps):
-                T.rt_closest(targets, args.count, idx, cnt, stream=stream.cuda_stream)
+            for r in range(args.reps):
+                T.rt_closest(tgs[r % args.batches], args.count, idx, cnt, stream=stream.cuda_stream)
             e1.record(stream)
             torch.cuda.synchronize()
             times[v].append(e0.elapsed_time(e1) / args.reps)
