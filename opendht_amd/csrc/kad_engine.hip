@@ -935,14 +935,26 @@ __device__ __forceinline__ void put_bits(uint32_t* L, uint32_t p, uint32_t w, ui
     L[k + 1] = (uint32_t)(x >> 32);
 }
 
-// One thread per bucket: short line b from 128-byte line b (sel as the 128-byte builder's), assembled in
-// the thread's LDS row (odd stride), then stored as 16-byte pieces.
+// One thread per bucket: short line b from 128-byte line b (sel as the 128-byte builder's). The source line is
+// staged in the thread's LDS row with eight 16-byte loads, the short line assembled in another (odd strides),
+// then stored as 16-byte pieces.
 __global__ __launch_bounds__(BLOCK) void ws_build_kernel(const uint32_t* __restrict__ wl, uint32_t B,
                                                           uint32_t* __restrict__ ws, LineSel sel) {
     __shared__ uint32_t lds[BLOCK][17];
+    __shared__ uint32_t src[BLOCK][33];
     uint32_t b;
     if (!sel.pick(blockIdx.x * BLOCK + threadIdx.x, B, b)) return;
-    const uint32_t* W = wl + 32ull * b;
+    uint32_t* W = src[threadIdx.x];
+    {
+        const uint4* g = reinterpret_cast<const uint4*>(wl + 32ull * b);
+        uint4 v[8];
+#pragma unroll
+        for (int x = 0; x < 8; x++) v[x] = g[x];
+#pragma unroll
+        for (int x = 0; x < 8; x++) {
+            W[4 * x] = v[x].x; W[4 * x + 1] = v[x].y; W[4 * x + 2] = v[x].z; W[4 * x + 3] = v[x].w;
+        }
+    }
     uint32_t* L = lds[threadIdx.x];
     const uint32_t h = W[1], rounds = W[2], S = (h >> 23) & 31u;
     bool fb = (h & WL_DEFER) != 0;
@@ -1033,7 +1045,8 @@ __device__ __forceinline__ bool ws_answer(const DevTable& T, const Target& t, ui
 }
 
 // 8 waves per SIMD (<= 64 VGPRs): the gather is latency-bound, occupancy is what hides it.
-// ABL 1 = no fallback and no exact path, 2 = also no ranking (timing ablations only).
+// ABL 1 = no fallback and no exact path, 2 = also no ranking, 3 = fallback but no exact path (timing ablations
+// only); 4 = path statistics: out_cnt = 100 + m for queries answered by the 128-byte line, 250 for the exact path.
 template <int ABL>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) void rt_ws_kernel(DevTable T, const uint8_t* __restrict__ targets, uint32_t q,
                                                       uint32_t count, uint32_t* __restrict__ out_idx,
@@ -1053,17 +1066,42 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) v
         store_row8(out_idx + (size_t)i * count, o, count);
         if (out_cnt) out_cnt[i] = (uint8_t)m;
     }
-    bool need = ABL == 0 && act && !ok;
+    bool need = (ABL == 0 || ABL >= 3) && act && !ok;
     if (__any(need)) {  // the 128-byte line of the (few) queries the short line cannot answer
         const bool ok2 = wl_answer<0>(T, t, b, count, need, o, m);
         if (need && ok2) {
             store_row8(out_idx + (size_t)i * count, o, count);
-            if (out_cnt) out_cnt[i] = (uint8_t)m;
+            if (out_cnt) out_cnt[i] = (uint8_t)(ABL == 4 ? 100 + m : m);
         }
         need = need && !ok2;
     }
-    __shared__ uint64_t xs[BLOCK / 64][192];
-    exact_tail(T, t, need, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
+    if (ABL == 0 || ABL == 4) {
+        __shared__ uint64_t xs[BLOCK / 64][192];
+        exact_tail(T, t, need, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
+        if (ABL == 4 && need && out_cnt) out_cnt[i] = 250;
+    }
+}
+
+// The count <= 8 line answer for kernels that serve other paths too (dual-family, shard): lanes with `ws`
+// (their table has short lines) try the 64-byte line, lanes with `act` it did not answer read the 128-byte
+// line. Same contract as wl_answer; call from uniform control flow.
+__device__ __forceinline__ bool line8_answer(const DevTable& T, const Target& t, uint32_t b, uint32_t count, bool act,
+                                             bool ws, uint32_t (&o)[8], uint32_t& m) {
+    bool ok = false;
+    m = 0;
+    if (__any(ws)) ok = ws_answer<0>(T, t, b, count, ws, o, m) && ws;
+    const bool need = act && !ok;
+    if (__any(need)) {
+        uint32_t o2[8], m2;
+        const bool ok2 = wl_answer<0>(T, t, b, count, need, o2, m2);
+        if (need) {
+#pragma unroll
+            for (int j = 0; j < 8; j++) o[j] = o2[j];
+            m = m2;
+            ok = ok2;
+        }
+    }
+    return ok;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1855,7 +1893,7 @@ __global__ __launch_bounds__(BLOCK) void rt_dual_wl_kernel(DevTable T4, DevTable
     const bool wl = act && (T.flags & TF_WL);
     const uint32_t b = wl ? locate_bucket(T, t) : 0u;
     uint32_t o[8], m;
-    const bool ok = wl_answer<0>(T, t, b, count, wl, o, m);
+    const bool ok = line8_answer(T, t, b, count, wl, wl && (T.flags & TF_WS), o, m);
     uint32_t* row = out_idx + (size_t)i * count;
     bool ex = wl && !ok;
     if (wl && ok) {
@@ -2023,7 +2061,7 @@ __global__ __launch_bounds__(BLOCK) void rt_shard_kernel(DevTable T, ShardCtx S,
     __shared__ uint32_t wcnt[BLOCK / 64 + 1];
     if (WL && __syncthreads_or(line)) {  // block-uniform
         uint32_t o[8], m;
-        const bool ok = wl_answer<0>(T, t, line ? b - S.s_lo : 0u, count, line, o, m);
+        const bool ok = line8_answer(T, t, line ? b - S.s_lo : 0u, count, line, line && (T.flags & TF_WS), o, m);
         const uint64_t want = __ballot(ok);
         const uint32_t w = threadIdx.x >> 6;
         if ((threadIdx.x & 63u) == 0) wcnt[w] = (uint32_t)__builtin_popcountll(want);
@@ -3711,6 +3749,10 @@ int launch_rt(const kad_table* t, const uint8_t* targets, uint32_t q, uint32_t c
             hipLaunchKernelGGL(rt_ws_kernel<1>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
         else if (ev && std::strcmp(ev, "ws_abl2") == 0)
             hipLaunchKernelGGL(rt_ws_kernel<2>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
+        else if (ev && std::strcmp(ev, "ws_abl3") == 0)
+            hipLaunchKernelGGL(rt_ws_kernel<3>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
+        else if (ev && std::strcmp(ev, "ws_stats") == 0)
+            hipLaunchKernelGGL(rt_ws_kernel<4>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
         else
 #endif
             hipLaunchKernelGGL(rt_ws_kernel<0>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
