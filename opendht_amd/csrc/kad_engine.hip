@@ -143,6 +143,12 @@ __device__ __forceinline__ Target load_target(const uint8_t* targets, uint32_t i
     return t;
 }
 
+// The top 64 bits of target i (direct-mapped tables locate with these alone).
+__device__ __forceinline__ uint64_t load_target_hi(const uint8_t* targets, uint32_t i) {
+    const uint32_t* p = reinterpret_cast<const uint32_t*>(targets + 20ull * i);
+    return ((uint64_t)__builtin_bswap32(p[0]) << 32) | __builtin_bswap32(p[1]);
+}
+
 // 160-bit compare of (hi, a2, a3, a4) vs (hi', b2, b3, b4): returns <0, 0, >0
 __device__ __forceinline__ int cmp160(uint64_t ah, uint32_t a2, uint32_t a3, uint32_t a4,
                                       uint64_t bh, uint32_t b2, uint32_t b3, uint32_t b4) {
@@ -648,6 +654,10 @@ __global__ __launch_bounds__(BLOCK) void rt_closest_kernel(DevTable T, const uin
 //   dw1      G(r) for r = 0..2, the good nodes of W(r) (6 bits each, capped at 63) | whole(r) << (18+r)
 //            | R_8 << 21 | S << 23 | defer << 31.  whole(r): W(r) is the whole table
 //   dw2      round of the bucket of D rank j, 2 bits each (j < 6)
+//   dw3      tie: 0, or one pair of stored nodes of one bucket sharing key21, valid << 31 | bn << 30 | p << 16 |
+//            off_a << 8 | off_b (off_a < off_b; p = the first of the top 64 ID bits where they differ, bn = node
+//            b's bit p). Their rank values differ only in off, so off_a ranks first; a target whose bit p is bn
+//            is closer to node b, and the answer exchanges the two offsets.
 //   dw4..27  slot s (s < S <= 24): jd << 29 | key21 << 8 | off. The good nodes of W(R_8) in
 //            (D rank jd, node index) order, whole buckets only; off = node index - base (< 256)
 //   others   0xFFFFFFFF
@@ -703,7 +713,7 @@ __device__ __forceinline__ uint32_t dw(const uint4 (&L)[8], int k) {  // static 
 // Returns true with o[0..8) (node indices + index_base, NONE from m on) and m = min(count, good
 // nodes of W(R_c)), or false when the query needs the exact path (marked line, target outside b's
 // range, too few stored slots). Contains a wave vote: call from uniform control flow, inactive lanes
-// with act = false (they return false).
+// with act = false (they return false). The line's key21 tie (dw3), if any, is applied to the answer.
 // ABL (timing ablations only, KAD_RT_KERNEL=wl_abl1|wl_abl2 in the KAD_ABLATIONS tools build; results
 // wrong): 2 = no ranking.
 template <int ABL>
@@ -750,9 +760,17 @@ __device__ __forceinline__ bool wl_answer(const DevTable& T, const Target& t, ui
         merge8(v, v + 8);
         merge8(v, v + 16);
     }
-    const uint32_t base = L[0].x + T.index_base;
+    const uint32_t base = L[0].x + T.index_base, tie = L[0].w;
+    uint32_t oa = NONE, ob = NONE;
+    if ((tie >> 31) && ((t.hi >> (63 - ((tie >> 16) & 63u))) & 1u) == ((tie >> 30) & 1u)) {
+        oa = (tie >> 8) & 255u;
+        ob = tie & 255u;
+    }
 #pragma unroll
-    for (int j = 0; j < 8; j++) o[j] = (uint32_t)j < m ? base + (v[j] & 255u) : NONE;
+    for (int j = 0; j < 8; j++) {
+        const uint32_t x = v[j] & 255u, y = x == oa ? ob : x == ob ? oa : x;
+        o[j] = (uint32_t)j < m ? base + y : NONE;
+    }
     return !ex;
 }
 
@@ -855,12 +873,13 @@ __global__ __launch_bounds__(BLOCK) void wl_build_kernel(const uint64_t* key, co
     }
     if (R8 == 3) {
         L[1] = WL_DEFER;
+        L[3] = 0;
         store_line<32>(L, lines + 32ull * b);
         return;
     }
     const uint32_t lo = b > R8 ? b - 1 - R8 : 0u, hi = min(B - 1, b + R8), nb = hi - lo + 1;
     const uint32_t base = dir[lo].x & ~WIDE;
-    uint32_t rounds = 0, S = 0;
+    uint32_t rounds = 0, S = 0, tie = 0;
     bool defer = false, full = false;
     for (uint32_t j = 0; j < nb; j++) {  // buckets in D order: the one whose D rank is j
         uint32_t x = lo;
@@ -876,7 +895,19 @@ __global__ __launch_bounds__(BLOCK) void wl_build_kernel(const uint64_t* key, co
         for_good(key, status, dir, x, [&](uint32_t n, uint64_t kn) {
             const uint32_t k21 = (uint32_t)((kn << d) >> (64 - WL_KBITS)), off = n - base;
             defer |= off > 255u;
-            for (uint32_t s = s0; s < S; s++) defer |= ((L[WL_SLOT0 + s] >> 8) & ((1u << WL_KBITS) - 1)) == k21;
+            for (uint32_t s = s0; s < S; s++) {
+                if (((L[WL_SLOT0 + s] >> 8) & ((1u << WL_KBITS) - 1)) != k21) continue;
+                // one pair sharing key21 is resolved by the first bit p where the two keys differ (dw3);
+                // a second pair, or keys equal in all 64 bits, defers the line
+                const uint32_t oa = L[WL_SLOT0 + s] & 255u;
+                const uint64_t x = kn ^ key[base + oa];
+                if (tie || x == 0 || off > 255u) {
+                    defer = true;
+                } else {
+                    const uint32_t p = (uint32_t)__builtin_clzll(x), bn = (uint32_t)(kn >> (63 - p)) & 1u;
+                    tie = WL_DEFER | (bn << 30) | (p << 16) | (oa << 8) | (off & 255u);
+                }
+            }
             L[WL_SLOT0 + S] = (j << 29) | (k21 << 8) | (off & 255u);
             S++;
         });
@@ -884,6 +915,7 @@ __global__ __launch_bounds__(BLOCK) void wl_build_kernel(const uint64_t* key, co
     L[0] = base;
     L[1] = h | (R8 << 21) | (S << 23) | (defer ? WL_DEFER : 0u);
     L[2] = rounds;
+    L[3] = tie;
     store_line<32>(L, lines + 32ull * b);
 }
 
@@ -1046,7 +1078,8 @@ __device__ __forceinline__ bool ws_answer(const DevTable& T, const Target& t, ui
 
 // 8 waves per SIMD (<= 64 VGPRs): the gather is latency-bound, occupancy is what hides it.
 // ABL 1 = no fallback and no exact path, 2 = also no ranking, 3 = fallback but no exact path (timing ablations
-// only); 4 = path statistics: out_cnt = 100 + m for queries answered by the 128-byte line, 250 for the exact path.
+// only); 4 = path statistics: out_cnt = 100 + m for queries answered by the 128-byte line, 250 for the exact path;
+// 5 = the exact path compiled in but never taken.
 template <int ABL>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) void rt_ws_kernel(DevTable T, const uint8_t* __restrict__ targets, uint32_t q,
                                                       uint32_t count, uint32_t* __restrict__ out_idx,
@@ -1054,10 +1087,12 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     const bool act = i < q && count > 0;
     if (i < q && count == 0 && out_cnt) out_cnt[i] = 0;
+    // short lines exist only on direct-mapped tables, whose locate and line paths use the target's top 64
+    // bits alone: the other 96 are loaded by the (rare) exact path
     Target t{};
     uint32_t b = 0;
     if (act) {
-        t = load_target(targets, i);
+        t.hi = load_target_hi(targets, i);
         b = locate_bucket(T, t);
     }
     uint32_t o[8], m;
@@ -1075,9 +1110,13 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) v
         }
         need = need && !ok2;
     }
-    if (ABL == 0 || ABL == 4) {
+    if (ABL == 0 || ABL == 4 || ABL == 5) {
         __shared__ uint64_t xs[BLOCK / 64][192];
-        exact_tail(T, t, need, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
+        if (ABL == 5) need = need && T.n == 0xFFFFFFFFu;  // opaque to the compiler, false in practice
+        if (__any(need)) {
+            if (need) t = load_target(targets, i);
+            exact_tail(T, t, need, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
+        }
         if (ABL == 4 && need && out_cnt) out_cnt[i] = 250;
     }
 }
@@ -3751,6 +3790,8 @@ int launch_rt(const kad_table* t, const uint8_t* targets, uint32_t q, uint32_t c
             hipLaunchKernelGGL(rt_ws_kernel<2>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
         else if (ev && std::strcmp(ev, "ws_abl3") == 0)
             hipLaunchKernelGGL(rt_ws_kernel<3>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
+        else if (ev && std::strcmp(ev, "ws_abl5") == 0)
+            hipLaunchKernelGGL(rt_ws_kernel<5>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
         else if (ev && std::strcmp(ev, "ws_stats") == 0)
             hipLaunchKernelGGL(rt_ws_kernel<4>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
         else
