@@ -23,6 +23,7 @@ KAD_INFO_WINDOW_LINES = 0x100
 KAD_INFO_GENERAL_LINES = 0x200
 KAD_INFO_GENERAL_LINES32 = 0x400
 KAD_INFO_SHORT_LINES = 0x800
+KAD_INFO_NODECACHE_LINES32 = 0x1000
 KAD_OP_REMOVE, KAD_OP_REPLACE, KAD_OP_INSERT, KAD_OP_SPLIT = 1, 2, 3, 4
 
 

@@ -97,6 +97,7 @@ struct DevTable {
     const uint4* gl;    // general window lines, count <= 8 (TF_GL, any table shape): 128 bytes per bucket
     const uint4* gl32;  // general window lines, counts 9..32 (TF_GL32): 256 bytes per bucket
     const uint4* ws;    // short window lines, count <= 8 (TF_WS, with TF_WL): 64 bytes per bucket
+    const uint4* ncl32; // NodeCache lines for counts 17..32 (TF_NCL32): 512 bytes per node radix slot
     uint64_t rbase, nbase;
     uint32_t rshift, rslots, nshift, nslots;
     uint32_t n, B, index_base, flags;
@@ -110,6 +111,7 @@ constexpr uint32_t TF_WL32 = 32u;    // window lines for counts 17..32 present
 constexpr uint32_t TF_NCL = 64u;     // NodeCache lines present (sorted tables)
 constexpr uint32_t TF_GL = 128u;     // general window lines (tables without TF_WL: split-policy, per-peer shapes)
 constexpr uint32_t TF_GL32 = 256u;   // general window lines for counts 9..32
+constexpr uint32_t TF_NCL32 = 1024u; // 512-byte NodeCache lines (counts 17..32) present
 constexpr uint32_t TF_WS = 512u;     // short (64-byte) window lines for count <= 8 (uniform tables, with TF_WL)
 constexpr uint32_t WIDE = 0x80000000u;  // dir[].x flag: bucket holds > 32 nodes (masks invalid)
 constexpr uint32_t KEY_PAD = 32;        // key[] is padded so 16-node chunk loads never leave it
@@ -3055,6 +3057,251 @@ __global__ void ncl_build_kernel(const uint64_t* key, const uint8_t* status, con
 }
 
 // ---------------------------------------------------------------------------------------
+// NodeCache lines for counts 17..32 (TF_NCL32): one 512-byte line per node radix slot s, the 124-node window
+// w0 = r0-56 .. r0+67 of the sorted node array ([r0, r1) = the slot's nodes, at most 15):
+//   dw0      w0
+//   dw1      ns = r1 - r0 | sh << 8
+//   dw2      defer | truncated left (w0 > 0) << 1 | truncated right (w0 + 124 < n) << 2
+//   dw4..127 element e (node w0 + e): key24 << 8 | expired, key24 as in the 256-byte lines
+// A query is answered by 8 lanes (an octet; 8 queries per wave). The octet stages its line in LDS with
+// 16-byte loads, counts the slot's nodes below the target (lb = w0 + p, p = 56 + x), and reads the
+// first 64 steps of each run: lane g holds left steps 8g..8g+7 (element p-1-step) and right steps
+// 63-8g-u (element p+step). A run's prefix maxima of the XOR distance (in-lane, then across the octet)
+// give each element the key (M << 8 | side << 7 | step << 1 | expired); each run's keys ascend with the
+// step, the walk's order is the keys' order (node_cache.cpp:36-66, the greedy merge of the 256-byte
+// lines), so the walk's first 64 steps are min(left[r], right[63-r]) followed by a bitonic half-cleaner
+// cascade (three stages across lanes, three inside). The first `count` non-expired steps are the answer;
+// a run cut by the window's truncated end limits the trusted keys to that end's key. A query with fewer
+// than `count` trusted emissions, a deferred line, or a target equal in key24 to a slot node takes the
+// two-pass wave path (nc_answer, then nc64_query / the serial walk).
+// ---------------------------------------------------------------------------------------
+constexpr uint32_t NC32_SLOTS = 124, NC32_LEFT = 56, NC32_XMAX = 15, NC32_STRIDE = 128;  // dwords
+
+// One octet per radix slot: lane g builds dwords [16g, 16g + 16) of line s.
+__global__ __launch_bounds__(BLOCK) void ncl32_build_kernel(const uint64_t* key, const uint8_t* status,
+                                                             const uint32_t* nrdx, uint32_t nslots, uint32_t n,
+                                                             uint32_t slot_prefix, uint32_t* lines, LineSel sel) {
+    const uint32_t g = threadIdx.x & 7u;
+    uint32_t s;
+    if (!sel.pick((blockIdx.x * BLOCK + threadIdx.x) >> 3, nslots, s)) return;  // whole octets leave
+    uint4* dst = reinterpret_cast<uint4*>(lines + (size_t)NC32_STRIDE * s) + 4 * g;
+    const uint32_t r0 = nrdx[s], r1 = nrdx[s + 1], ns = r1 - r0;
+    if (r0 < NC32_LEFT || (uint64_t)r0 - NC32_LEFT + NC32_SLOTS > n || ns > NC32_XMAX) {  // clamped / wide slot
+        if (g == 0) dst[0] = make_uint4(0u, 0u, 1u, 0u);
+        return;
+    }
+    const uint32_t w0 = r0 - NC32_LEFT;
+    const uint32_t P = (uint32_t)__builtin_clzll((key[w0] ^ key[w0 + NC32_SLOTS - 1]) | 1ull);
+    const uint32_t Pp = min(min(P, slot_prefix), 40u), sh = 40 - Pp;
+    uint32_t v[16];
+    bool defer = false;
+    uint32_t prev = 0;
+    if (g > 0) prev = (uint32_t)(key[w0 + 16 * g - 5] >> sh) & 0xFFFFFFu;  // element 16g - 5
+#pragma unroll
+    for (int u = 0; u < 16; u++) {
+        const int j = 16 * (int)g + u, e = j - 4;
+        if (e < 0) { v[u] = 0; continue; }
+        const uint32_t k24 = (uint32_t)(key[w0 + e] >> sh) & 0xFFFFFFu;
+        defer |= e > 0 && k24 == prev;
+        prev = k24;
+        v[u] = (k24 << 8) | ((status[w0 + e] & KAD_STATUS_EXPIRED) ? 1u : 0u);
+    }
+    uint32_t df = defer ? 1u : 0u;
+    df |= (uint32_t)__shfl_xor((int)df, 1, 8);
+    df |= (uint32_t)__shfl_xor((int)df, 2, 8);
+    df |= (uint32_t)__shfl_xor((int)df, 4, 8);
+    if (g == 0) {
+        v[0] = w0;
+        v[1] = ns | (sh << 8);
+        v[2] = df | (w0 > 0 ? 2u : 0u) | (w0 + NC32_SLOTS < n ? 4u : 0u);
+        v[3] = 0;
+    }
+#pragma unroll
+    for (int x = 0; x < 4; x++) dst[x] = make_uint4(v[4 * x], v[4 * x + 1], v[4 * x + 2], v[4 * x + 3]);
+}
+
+// DUAL: the family per query (af[i] = 0 -> T4, 1 -> T6), an empty family map gives zero results.
+// ABL 1 (timing ablations only, results wrong): no wave fallback; 2: also no merge (the line loads and one store);
+// 3: path statistics (out_cnt = 250 for the queries the wave path answers).
+template <int ABL, bool DUAL>
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) void nc32_line_kernel(DevTable T4, DevTable T6, const uint8_t* __restrict__ af,
+                                                          const uint8_t* __restrict__ targets, uint32_t q,
+                                                          uint32_t count, uint32_t* __restrict__ out_idx,
+                                                          uint8_t* __restrict__ out_cnt) {
+    __shared__ uint32_t lds[BLOCK / 8][NC32_STRIDE + 4];
+    const uint32_t lane = threadIdx.x & 63u, g = threadIdx.x & 7u;
+    const uint32_t qi = (blockIdx.x * BLOCK + threadIdx.x) >> 3;
+    const bool act = qi < q;
+    const bool fam = DUAL && act && af[qi] != 0;
+    const DevTable& T = fam ? T6 : T4;  // octet-uniform
+    uint32_t* W = lds[threadIdx.x >> 3];
+    bool ok = false, line = false;
+    uint64_t thi = 0;
+    uint32_t s = 0;
+    if (act) {
+        if (T.n == 0) {  // empty map
+            for (uint32_t j = g; j < count; j += 8) out_idx[(size_t)qi * count + j] = NONE;
+            if (g == 0 && out_cnt) out_cnt[qi] = 0;
+            ok = true;
+        } else if (T.flags & TF_NCL32) {
+            thi = load_target_hi(targets, qi);
+            line = thi >= T.nbase && ((thi - T.nbase) >> T.nshift) < T.nslots;
+            s = line ? (uint32_t)((thi - T.nbase) >> T.nshift) : 0u;
+        }
+    }
+    if (line) {  // load x: the octet reads 128 contiguous bytes, lane g the 16 at 128x + 16g
+        const uint4* src = T.ncl32 + (size_t)(NC32_STRIDE / 4) * s + g;
+        uint4 x4[4];
+#pragma unroll
+        for (int x = 0; x < 4; x++) x4[x] = src[8 * x];
+#pragma unroll
+        for (int x = 0; x < 4; x++) {
+            W[32 * x + 4 * g] = x4[x].x; W[32 * x + 4 * g + 1] = x4[x].y;
+            W[32 * x + 4 * g + 2] = x4[x].z; W[32 * x + 4 * g + 3] = x4[x].w;
+        }
+    }
+    __syncthreads();
+    if (ABL == 2) {
+        if (line) out_idx[(size_t)qi * count + g] = W[g] ^ W[64 + g] ^ W[127 - g];
+        return;
+    }
+    if (line) {
+        const uint32_t w0 = W[0], ns = W[1] & 255u, sh = (W[1] >> 8) & 63u, fl = W[2];
+        const uint32_t t24 = (uint32_t)(thi >> sh) & 0xFFFFFFu;
+        // lb: the slot's nodes below the target (elements 56 .. 56+ns-1, two per lane)
+        uint32_t below = 0, eq = 0;
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+            const uint32_t e = NC32_LEFT + 2 * g + u;
+            if (e < NC32_LEFT + ns) {
+                const uint32_t k24 = W[4 + e] >> 8;
+                below += k24 < t24 ? 1u : 0u;
+                eq |= k24 == t24 ? 1u : 0u;
+            }
+        }
+#pragma unroll
+        for (int o = 1; o < 8; o <<= 1) {
+            below += (uint32_t)__shfl_xor((int)below, o, 8);
+            eq |= (uint32_t)__shfl_xor((int)eq, o, 8);
+        }
+        const uint32_t p = NC32_LEFT + below;
+        bool ex = (fl & 1u) || eq;
+        // the runs' first 64 steps: left step 8g+u = element p-1-step, right step 63-8g-u = element p+step
+        uint32_t ka[8], kb[8], runA = 0, runB = 0;
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const uint32_t ra = 8 * g + u, rb = 63 - 8 * g - u;
+            const bool va = ra < p, vb = p + rb < NC32_SLOTS;
+            const uint32_t xa = va ? W[4 + p - 1 - ra] : 0u, xb = vb ? W[4 + p + rb] : 0u;
+            ka[u] = va ? ((((xa >> 8) ^ t24) << 8) | (ra << 1) | (xa & 1u)) : NONE;
+            kb[u] = vb ? ((((xb >> 8) ^ t24) << 8) | 128u | (rb << 1) | (xb & 1u)) : NONE;
+        }
+        // prefix maxima of the distances along each run: in the lane (left: u ascending, right: u descending),
+        // then the runs' earlier lanes (left: lower g, right: higher g)
+        uint32_t pa[8], pb[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            runA = max(runA, ka[u] == NONE ? 0u : ka[u] & ~255u);
+            pa[u] = runA;
+        }
+#pragma unroll
+        for (int u = 7; u >= 0; u--) {
+            runB = max(runB, kb[u] == NONE ? 0u : kb[u] & ~255u);
+            pb[u] = runB;
+        }
+        uint32_t ca = runA, cb = runB;
+#pragma unroll
+        for (int o = 1; o < 8; o <<= 1) {
+            const uint32_t ya = (uint32_t)__shfl_up((int)ca, o, 8), yb = (uint32_t)__shfl_down((int)cb, o, 8);
+            if (g >= (uint32_t)o) ca = max(ca, ya);
+            if (g + o < 8) cb = max(cb, yb);
+        }
+        // exclusive carries (the shuffles run in every lane: a lane reading a lane that skipped the read gets 0)
+        const uint32_t ua = (uint32_t)__shfl_up((int)ca, 1, 8), ub = (uint32_t)__shfl_down((int)cb, 1, 8);
+        const uint32_t inA = g > 0 ? ua : 0u, inB = g < 7 ? ub : 0u;
+        uint32_t endA = 0, endB = 0;
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            if (ka[u] != NONE) { ka[u] = max(pa[u], inA) | (ka[u] & 255u); endA = max(endA, ka[u]); }
+            if (kb[u] != NONE) { kb[u] = max(pb[u], inB) | (kb[u] & 255u); endB = max(endB, kb[u]); }
+        }
+#pragma unroll
+        for (int o = 1; o < 8; o <<= 1) {
+            endA = max(endA, (uint32_t)__shfl_xor((int)endA, o, 8));
+            endB = max(endB, (uint32_t)__shfl_xor((int)endB, o, 8));
+        }
+        // keys beyond a truncated run end (fewer than 64 steps inside the window) are not trusted
+        uint32_t lim = NONE;
+        if ((fl & 2u) && p <= 64) lim = min(lim, endA);
+        if ((fl & 4u) && NC32_SLOTS - p <= 64) lim = min(lim, endB);
+        // the walk's first 64 steps: min(left[r], right[63-r]) is bitonic; half-cleaners sort it
+        uint32_t w[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) w[u] = min(ka[u], kb[u]);
+#pragma unroll
+        for (int o = 4; o >= 1; o >>= 1) {
+            const bool lo = (g & (uint32_t)o) == 0;
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                const uint32_t y = (uint32_t)__shfl_xor((int)w[u], o, 8);
+                w[u] = lo ? min(w[u], y) : max(w[u], y);
+            }
+        }
+#pragma unroll
+        for (int h = 4; h >= 1; h >>= 1)
+#pragma unroll
+            for (int u = 0; u < 8; u++)
+                if ((u & h) == 0) cx(w[u], w[u + h]);
+        // emissions: non-expired steps up to lim, ranked across the octet
+        uint32_t kept = 0;
+        bool keep[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            keep[u] = w[u] != NONE && w[u] <= lim && !(w[u] & 1u);
+            kept += keep[u];
+        }
+        uint32_t cr = kept;
+#pragma unroll
+        for (int o = 1; o < 8; o <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)cr, o, 8);
+            if (g >= (uint32_t)o) cr += y;
+        }
+        const uint32_t tot = (uint32_t)__shfl((int)cr, (int)((lane & ~7u) | 7u), 64);
+        ok = !ex && tot >= count;
+        if (ok) {
+            uint32_t rank = cr - kept;
+            uint32_t* row = out_idx + (size_t)qi * count;
+            const uint32_t base = w0 + T.index_base;
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                if (keep[u]) {
+                    if (rank < count) {
+                        const uint32_t st = (w[u] >> 1) & 63u;
+                        row[rank] = base + ((w[u] & 128u) ? p + st : p - 1 - st);
+                    }
+                    rank++;
+                }
+            }
+            if (g == 0 && out_cnt) out_cnt[qi] = (uint8_t)count;
+        }
+    }
+    if (ABL == 1 || ABL == 2) return;
+    // the queries the lines could not answer: one at a time by the whole wave (the two-pass path)
+    for (uint64_t pend = __ballot(act && g == 0 && !ok); pend; pend &= pend - 1) {
+        const uint32_t l = (uint32_t)__builtin_ctzll(pend);
+        const uint32_t qj = rdl(qi, l);
+        const DevTable& Tj = (DUAL && rdl(fam ? 1u : 0u, l)) ? T6 : T4;  // wave-uniform
+        const Target u = load_target(targets, qj);
+        uint32_t r0, r1;
+        nc_slot(Tj, u, r0, r1);
+        const NcWindow wn = nc_window(Tj, r0, lane);
+        if (!nc_answer(Tj, u, r0, r1, wn, lane, qj, count, out_idx, out_cnt, false))
+            nc64_query(Tj, u, lane, qj, count, out_idx, out_cnt, true);
+        if (ABL == 3 && lane == 0 && out_cnt) out_cnt[qj] = 250;
+    }
+}
+
+// ---------------------------------------------------------------------------------------
 // Incremental device mirror: kad_table_apply re-lays the node arrays out on
 // the device from a host plan of segments (an untouched bucket is one range of old nodes; an edited
 // bucket an explicit handle list), then re-derives masks, prefix sums, dup masks and lines on the
@@ -3262,6 +3509,7 @@ struct StatusMarks {
     const uint64_t* key; // node -> NodeCache slot
     uint64_t nbase;
     uint32_t nshift, nslots, n;
+    uint32_t nback, nfwd; // NodeCache lines hold nodes r0(s)-nfwd .. r0(s)+nback-1 (the widest line set present)
 };
 
 __device__ __forceinline__ void mark_status_change(const StatusMarks& M, uint32_t i, uint32_t old_st, uint32_t st) {
@@ -3274,9 +3522,10 @@ __device__ __forceinline__ void mark_status_change(const StatusMarks& M, uint32_
         if (lo) M.bdirty[lo - 1] = 1;
     }
     if (M.ndirty && ((old_st ^ st) & KAD_STATUS_EXPIRED)) {
-        // NodeCache line s holds nodes r0(s)-28 .. r0(s)+31: every slot from that of node i-32 to that of
-        // node i+28 (a superset of the slots whose window holds i)
-        const uint32_t a = i >= 32 ? i - 32 : 0u, e = min(M.n - 1, i + 28);
+        // NodeCache line s holds nodes r0(s)-nfwd .. r0(s)+nback-1 (28 / 32 for the 256-byte lines, 56 / 68 with
+        // the 512-byte ones): every slot from that of node i-nback to that of node i+nfwd (a superset of the
+        // slots whose window holds i)
+        const uint32_t a = i >= M.nback ? i - M.nback : 0u, e = min(M.n - 1, i + M.nfwd);
         const uint64_t ka = M.key[a], ke = M.key[e];
         const uint64_t sa = ka < M.nbase ? 0 : min<uint64_t>((ka - M.nbase) >> M.nshift, M.nslots - 1);
         const uint64_t se = ke < M.nbase ? 0 : min<uint64_t>((ke - M.nbase) >> M.nshift, M.nslots - 1);
@@ -3559,6 +3808,7 @@ struct kad_table {
     uint32_t* wl16_mut = nullptr;
     uint32_t* wl32_mut = nullptr;
     uint32_t* ncl_mut = nullptr;
+    uint32_t* ncl32_mut = nullptr;
     uint32_t* gl_mut = nullptr;
     uint32_t* gl32_mut = nullptr;
     // host copies of the bucket directory, for the incremental mirror (kad_table_apply)
@@ -3615,6 +3865,9 @@ int rebuild_good_prefix(kad_table* t, hipStream_t s, bool full = true) {
         }
         hipLaunchKernelGGL(ncl_build_kernel, dim3(grid_for(t->d.nslots)), dim3(BLOCK), 0, s, t->d.key, t->d.status,
                            t->d.nrdx, t->d.nslots, t->d.n, 64 - t->d.nshift, t->ncl_mut, sel);
+        if (t->ncl32_mut)  // the same slots: the marks cover the wider windows when these lines exist
+            hipLaunchKernelGGL(ncl32_build_kernel, dim3(grid_for(8ull * t->d.nslots)), dim3(BLOCK), 0, s, t->d.key,
+                               t->d.status, t->d.nrdx, t->d.nslots, t->d.n, 64 - t->d.nshift, t->ncl32_mut, sel);
     }
     if (B == 0) return KAD_OK;
     const uint32_t m = B + 1;
@@ -3755,6 +4008,8 @@ StatusMarks marks_of(const kad_table* t) {
     M.nshift = t->d.nshift;
     M.nslots = t->d.nslots;
     M.n = t->d.n;
+    M.nback = t->ncl32_mut ? NC32_SLOTS - NC32_LEFT : NCL_SLOTS - NCL_LEFT;
+    M.nfwd = t->ncl32_mut ? NC32_LEFT : NCL_LEFT;
     return M;
 }
 
@@ -4124,6 +4379,17 @@ int kad_table_create(kad_table** out, int device, uint32_t n_nodes, const uint8_
         d.ncl = reinterpret_cast<const uint4*>(lp);
         t->ncl_mut = lp;
         d.flags |= TF_NCL;
+        uint32_t* lp32;
+        if ((rc = dev_upload(&lp32, nullptr, (size_t)NC32_STRIDE * r.slots, t->owned, t->bytes))) { delete t; return rc; }
+        hipLaunchKernelGGL(ncl32_build_kernel, dim3(grid_for(8ull * r.slots)), dim3(BLOCK), 0, 0, d.key, d.status, dn,
+                           r.slots, n_nodes, 64 - r.shift, lp32, LineSel{});
+        if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+            delete t;
+            return set_err(KAD_ERR_HIP, "NodeCache line (32) build failed");
+        }
+        d.ncl32 = reinterpret_cast<const uint4*>(lp32);
+        t->ncl32_mut = lp32;
+        d.flags |= TF_NCL32;
     }
     *out = t;
     return KAD_OK;
@@ -4144,7 +4410,8 @@ int kad_table_get_info(const kad_table* t, kad_table_info* out) {
     out->index_base = t->d.index_base;
     out->flags = t->flags | ((t->d.flags & TF_WL) ? KAD_INFO_WINDOW_LINES : 0u) |
                  ((t->d.flags & TF_GL) ? KAD_INFO_GENERAL_LINES : 0u) | ((t->d.flags & TF_GL32) ? KAD_INFO_GENERAL_LINES32 : 0u) |
-                 ((t->d.flags & TF_WS) ? KAD_INFO_SHORT_LINES : 0u);
+                 ((t->d.flags & TF_WS) ? KAD_INFO_SHORT_LINES : 0u) |
+                 ((t->d.flags & TF_NCL32) ? KAD_INFO_NODECACHE_LINES32 : 0u);
     out->device = t->device;
     out->rt_radix_bits = t->rbits;
     out->nc_radix_bits = t->nbits;
@@ -4455,6 +4722,15 @@ int kad_nc_closest_batch(const kad_table* t, const uint8_t* targets, uint32_t q,
     if ((t->d.flags & TF_NCL) && ev && std::strcmp(ev, "lines_abl1") == 0 && count >= 1 && count <= 16)
         hipLaunchKernelGGL((nc_line_kernel<1, false>), dim3(grid_for(q)), dim3(BLOCK), 0, (hipStream_t)stream, t->d,
                            t->d, nullptr, targets, q, count, out_idx, out_cnt);
+    else if ((t->d.flags & TF_NCL32) && ev && std::strcmp(ev, "l32_abl1") == 0 && count > 16 && count <= 32)
+        hipLaunchKernelGGL((nc32_line_kernel<1, false>), dim3(grid_for(8ull * q)), dim3(BLOCK), 0, (hipStream_t)stream,
+                           t->d, t->d, nullptr, targets, q, count, out_idx, out_cnt);
+    else if ((t->d.flags & TF_NCL32) && ev && std::strcmp(ev, "l32_stats") == 0 && count > 16 && count <= 32)
+        hipLaunchKernelGGL((nc32_line_kernel<3, false>), dim3(grid_for(8ull * q)), dim3(BLOCK), 0, (hipStream_t)stream,
+                           t->d, t->d, nullptr, targets, q, count, out_idx, out_cnt);
+    else if ((t->d.flags & TF_NCL32) && ev && std::strcmp(ev, "l32_abl2") == 0 && count > 16 && count <= 32)
+        hipLaunchKernelGGL((nc32_line_kernel<2, false>), dim3(grid_for(8ull * q)), dim3(BLOCK), 0, (hipStream_t)stream,
+                           t->d, t->d, nullptr, targets, q, count, out_idx, out_cnt);
     else if (count > 16 && count <= 64 && t->d.n > 0 && ev && std::strcmp(ev, "w64_abl1") == 0)
         hipLaunchKernelGGL(nc_wave64_kernel<1>, dim3((q + BLOCK / 64 - 1) / (BLOCK / 64)), dim3(BLOCK), 0,
                            (hipStream_t)stream, t->d, targets, q, count, out_idx, out_cnt);
@@ -4463,6 +4739,9 @@ int kad_nc_closest_batch(const kad_table* t, const uint8_t* targets, uint32_t q,
     if (lines && count >= 1 && count <= 16)
         hipLaunchKernelGGL((nc_line_kernel<0, false>), dim3(grid_for(q)), dim3(BLOCK), 0, (hipStream_t)stream, t->d,
                            t->d, nullptr, targets, q, count, out_idx, out_cnt);
+    else if ((t->d.flags & TF_NCL32) && !ev && count > 16 && count <= 32)
+        hipLaunchKernelGGL((nc32_line_kernel<0, false>), dim3(grid_for(8ull * q)), dim3(BLOCK), 0, (hipStream_t)stream,
+                           t->d, t->d, nullptr, targets, q, count, out_idx, out_cnt);
     else if (count >= 1 && count <= 16 && ev && std::strcmp(ev, "group1") == 0)
         hipLaunchKernelGGL(nc_group_v1_kernel, dim3((q + BLOCK / 64 - 1) / (BLOCK / 64)), dim3(BLOCK), 0,
                            (hipStream_t)stream, t->d, targets, q, count, out_idx, out_cnt);
@@ -4514,6 +4793,9 @@ int kad_nc_closest_batch_dual(const kad_table* t4, const kad_table* t6, const ui
     if (count <= 16)
         hipLaunchKernelGGL((nc_line_kernel<0, true>), dim3(grid_for(q)), dim3(BLOCK), 0, s, d4, d6, af, targets, q, count,
                            out_idx, out_cnt);
+    else if (count <= 32 && ((d4.flags | d6.flags) & TF_NCL32))  // a family without the lines takes the wave path
+        hipLaunchKernelGGL((nc32_line_kernel<0, true>), dim3(grid_for(8ull * q)), dim3(BLOCK), 0, s, d4, d6, af, targets,
+                           q, count, out_idx, out_cnt);
     else
         hipLaunchKernelGGL(nc_two_pass_dual_kernel, dim3((q + BLOCK / 64 - 1) / (BLOCK / 64)), dim3(BLOCK), 0, s, d4, d6,
                            af, targets, q, count, out_idx, out_cnt);
@@ -4879,6 +5161,7 @@ int kad_table_apply(kad_table* t, const uint32_t* ops, uint32_t n_ops, const uin
         t->flags &= ~KAD_TABLE_SORTED;
         release(t, const_cast<uint32_t*>(d.nrdx)); d.nrdx = nullptr; t->nbits = 0;
         release(t, t->ncl_mut); t->ncl_mut = nullptr; d.ncl = nullptr; d.flags &= ~TF_NCL;
+        release(t, t->ncl32_mut); t->ncl32_mut = nullptr; d.ncl32 = nullptr; d.flags &= ~TF_NCL32;
     }
     release(t, t->wrec); t->wrec = nullptr; t->addr_len = 0;
     release(t, t->time_ns); release(t, t->reply_ns); release(t, t->expired);
@@ -5003,14 +5286,18 @@ int kad_nc_apply(kad_table* t, const uint32_t* erase, uint32_t n_erase, const ui
     uint32_t tb = 1;
     while ((1u << tb) < n1 && tb < 23) tb++;
     if (n1) r = choose_radix(kmin, kmax, tb);
+    uint32_t* ncl32 = nullptr;
     if (n1 && ((rc = dev_upload(&rdx1, nullptr, (size_t)r.slots + 1, fresh, freshb)) ||
-               (rc = dev_upload(&ncl1, nullptr, (size_t)NCL_STRIDE * r.slots, fresh, freshb))))
+               (rc = dev_upload(&ncl1, nullptr, (size_t)NCL_STRIDE * r.slots, fresh, freshb)) ||
+               (rc = dev_upload(&ncl32, nullptr, (size_t)NC32_STRIDE * r.slots, fresh, freshb))))
         return fail(rc);
     if (n1) {
         hipLaunchKernelGGL(nc_radix_kernel, dim3(grid_for((uint64_t)r.slots + 1)), dim3(BLOCK), 0, 0, key1, n1, r.base,
                            r.shift, r.slots, rdx1);
         hipLaunchKernelGGL(ncl_build_kernel, dim3(grid_for(r.slots)), dim3(BLOCK), 0, 0, key1, st1, rdx1, r.slots, n1,
                            64 - r.shift, ncl1, LineSel{});
+        hipLaunchKernelGGL(ncl32_build_kernel, dim3(grid_for(8ull * r.slots)), dim3(BLOCK), 0, 0, key1, st1, rdx1,
+                           r.slots, n1, 64 - r.shift, ncl32, LineSel{});
     }
     if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess)
         return fail(set_err(KAD_ERR_HIP, "NodeCache radix / line build failed"));
@@ -5029,12 +5316,15 @@ int kad_nc_apply(kad_table* t, const uint32_t* erase, uint32_t n_erase, const ui
     release(t, t->status_mut);
     release(t, const_cast<uint32_t*>(d.nrdx));
     release(t, t->ncl_mut);
+    release(t, t->ncl32_mut);
     d.key = key1; d.tail = tail1; d.status = st1; t->status_mut = st1; d.n = n1;
     if (n1) {
         d.nrdx = rdx1; d.nbase = r.base; d.nshift = r.shift; d.nslots = r.slots; t->nbits = r.bits;
         d.ncl = reinterpret_cast<const uint4*>(ncl1); t->ncl_mut = ncl1; d.flags |= TF_NCL;
+        d.ncl32 = reinterpret_cast<const uint4*>(ncl32); t->ncl32_mut = ncl32; d.flags |= TF_NCL32;
     } else {
         d.nrdx = nullptr; d.nslots = 0; t->nbits = 0; d.ncl = nullptr; t->ncl_mut = nullptr; d.flags &= ~TF_NCL;
+        d.ncl32 = nullptr; t->ncl32_mut = nullptr; d.flags &= ~TF_NCL32;
     }
     release(t, t->wrec); t->wrec = nullptr; t->addr_len = 0;
     release(t, t->time_ns); release(t, t->reply_ns); release(t, t->expired);
