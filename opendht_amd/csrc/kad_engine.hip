@@ -860,8 +860,11 @@ __global__ __launch_bounds__(BLOCK) void wl_build_kernel(const uint64_t* key, co
                                                           const uint32_t* gpre, uint32_t B, uint32_t d, uint64_t pre0,
                                                           uint32_t* lines, LineSel sel) {
     __shared__ uint32_t lds[BLOCK][33];
-    uint32_t b;
-    if (!sel.pick(blockIdx.x * BLOCK + threadIdx.x, B, b)) return;
+    // one item per thread, grid-stride (an incremental rebuild launches a capped grid)
+    for (uint32_t j_ = blockIdx.x * BLOCK + threadIdx.x;; j_ += gridDim.x * BLOCK) {
+        uint32_t b;
+        if (!sel.pick(j_, B, b)) return;
+        [&] {
     uint32_t* L = lds[threadIdx.x];
     for (int k = 0; k < 32; k++) L[k] = NONE;
     // R_8 and the per-round good counts (routing_table.cpp:89-104 closed form)
@@ -919,6 +922,8 @@ __global__ __launch_bounds__(BLOCK) void wl_build_kernel(const uint64_t* key, co
     L[2] = rounds;
     L[3] = tie;
     store_line<32>(L, lines + 32ull * b);
+        }();
+    }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -976,8 +981,11 @@ __global__ __launch_bounds__(BLOCK) void ws_build_kernel(const uint32_t* __restr
                                                           uint32_t* __restrict__ ws, LineSel sel) {
     __shared__ uint32_t lds[BLOCK][17];
     __shared__ uint32_t src[BLOCK][33];
-    uint32_t b;
-    if (!sel.pick(blockIdx.x * BLOCK + threadIdx.x, B, b)) return;
+    // one item per thread, grid-stride (an incremental rebuild launches a capped grid)
+    for (uint32_t j_ = blockIdx.x * BLOCK + threadIdx.x;; j_ += gridDim.x * BLOCK) {
+        uint32_t b;
+        if (!sel.pick(j_, B, b)) return;
+        [&] {
     uint32_t* W = src[threadIdx.x];
     {
         const uint4* g = reinterpret_cast<const uint4*>(wl + 32ull * b);
@@ -1017,6 +1025,8 @@ __global__ __launch_bounds__(BLOCK) void ws_build_kernel(const uint32_t* __restr
     put_bits(L, WS_HDR, 23, hw);
     put_bits(L, WS_ROUNDS, 12, rk);
     store_line<16>(L, ws + 16ull * b);
+        }();
+    }
 }
 
 // The short-line answer (same contract as wl_answer; the caller falls back to wl_answer when it fails).
@@ -1325,8 +1335,11 @@ __global__ __launch_bounds__(BLOCK) void wl16_build_kernel(const uint64_t* key, 
                                                             const uint32_t* gpre, uint32_t B, uint32_t d, uint64_t pre0,
                                                             uint32_t* lines, LineSel sel) {
     __shared__ uint32_t lds[BLOCK][33];
-    uint32_t b;
-    if (!sel.pick(blockIdx.x * BLOCK + threadIdx.x, B, b)) return;
+    // one item per thread, grid-stride (an incremental rebuild launches a capped grid)
+    for (uint32_t j_ = blockIdx.x * BLOCK + threadIdx.x;; j_ += gridDim.x * BLOCK) {
+        uint32_t b;
+        if (!sel.pick(j_, B, b)) return;
+        [&] {
     uint32_t* L = lds[threadIdx.x];
     for (uint32_t k = 0; k < WL16_STRIDE; k++) L[k] = NONE;
     uint32_t h = 0, R = 4;
@@ -1383,6 +1396,8 @@ __global__ __launch_bounds__(BLOCK) void wl16_build_kernel(const uint64_t* key, 
     L[1] = h | (R << 24) | (S << 26) | (defer ? WL_DEFER : 0u);
     L[2] = rounds | (st << 16) | (nb << 24);
     store_line<32>(L, lines + (size_t)WL16_STRIDE * b);
+        }();
+    }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1531,8 +1546,11 @@ __global__ __launch_bounds__(BLOCK) void wl32_build_kernel(const uint64_t* key, 
                                                             const uint32_t* gpre, uint32_t B, uint32_t d, uint64_t pre0,
                                                             uint32_t* lines, LineSel sel) {
     __shared__ uint32_t lds[BLOCK][WL32_STRIDE + 1];
-    uint32_t b;
-    if (!sel.pick(blockIdx.x * BLOCK + threadIdx.x, B, b)) return;
+    // one item per thread, grid-stride (an incremental rebuild launches a capped grid)
+    for (uint32_t j_ = blockIdx.x * BLOCK + threadIdx.x;; j_ += gridDim.x * BLOCK) {
+        uint32_t b;
+        if (!sel.pick(j_, B, b)) return;
+        [&] {
     uint32_t* L = lds[threadIdx.x];
     for (uint32_t k = 0; k < WL32_STRIDE; k++) L[k] = NONE;
     uint32_t g01 = 0, g23 = 0, whole = 0, R = 8;
@@ -1582,6 +1600,8 @@ __global__ __launch_bounds__(BLOCK) void wl32_build_kernel(const uint64_t* key, 
     L[4] = r04;
     L[5] = r15;
     store_line<WL32_STRIDE>(L, lines + (size_t)WL32_STRIDE * b);
+        }();
+    }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1845,8 +1865,11 @@ __global__ __launch_bounds__(BLOCK) void gl_build_kernel(const uint64_t* key, co
                                                          const uint32_t* gpre, const uint64_t* fkey, const uint32_t* ftail,
                                                          uint32_t B, uint32_t* lines, LineSel sel) {
     __shared__ uint32_t lds[BLOCK][GL_STRIDE + 1];
-    uint32_t b;
-    if (!sel.pick(blockIdx.x * BLOCK + threadIdx.x, B, b)) return;
+    // one item per thread, grid-stride (an incremental rebuild launches a capped grid)
+    for (uint32_t j_ = blockIdx.x * BLOCK + threadIdx.x;; j_ += gridDim.x * BLOCK) {
+        uint32_t b;
+        if (!sel.pick(j_, B, b)) return;
+        [&] {
     uint32_t* L = lds[threadIdx.x];
     for (uint32_t k = 0; k < GL_STRIDE; k++) L[k] = NONE;
     GlInfo I;
@@ -1859,6 +1882,8 @@ __global__ __launch_bounds__(BLOCK) void gl_build_kernel(const uint64_t* key, co
     L[2] = I.Sr[0] | (I.Sr[1] << 5) | (I.cp << 10);
     L[3] = 0;
     store_line<GL_STRIDE>(L, lines + (size_t)GL_STRIDE * b);
+        }();
+    }
 }
 
 __global__ __launch_bounds__(BLOCK) void gl32_build_kernel(const uint64_t* key, const uint8_t* status, const uint2* dir,
@@ -1866,8 +1891,11 @@ __global__ __launch_bounds__(BLOCK) void gl32_build_kernel(const uint64_t* key, 
                                                            const uint32_t* ftail, uint32_t B, uint32_t* lines,
                                                            LineSel sel) {
     __shared__ uint32_t lds[BLOCK][GL32_STRIDE + 1];
-    uint32_t b;
-    if (!sel.pick(blockIdx.x * BLOCK + threadIdx.x, B, b)) return;
+    // one item per thread, grid-stride (an incremental rebuild launches a capped grid)
+    for (uint32_t j_ = blockIdx.x * BLOCK + threadIdx.x;; j_ += gridDim.x * BLOCK) {
+        uint32_t b;
+        if (!sel.pick(j_, B, b)) return;
+        [&] {
     uint32_t* L = lds[threadIdx.x];
     for (uint32_t k = 0; k < GL32_STRIDE; k++) L[k] = NONE;
     GlInfo I;
@@ -1884,6 +1912,8 @@ __global__ __launch_bounds__(BLOCK) void gl32_build_kernel(const uint64_t* key, 
     L[4] = I.Sr[0] | (I.Sr[1] << 6) | (I.Sr[2] << 12) | (I.Sr[3] << 18) | (I.Sr[4] << 24);
     L[5] = I.Sr[5] | (I.Sr[6] << 6) | (I.cp << 12);
     store_line<GL32_STRIDE>(L, lines + (size_t)GL32_STRIDE * b);
+        }();
+    }
 }
 
 // Deferred lines of a line set (decides at table creation whether the general lines pay off).
@@ -3031,8 +3061,11 @@ __global__ __launch_bounds__(BLOCK) void nc_two_pass_dual_kernel(DevTable T4, De
 // NodeCache lines after a status change (or at creation): one thread per radix slot.
 __global__ void ncl_build_kernel(const uint64_t* key, const uint8_t* status, const uint32_t* nrdx, uint32_t nslots,
                                  uint32_t n, uint32_t slot_prefix, uint32_t* lines, LineSel sel) {
-    uint32_t s;
-    if (!sel.pick(blockIdx.x * BLOCK + threadIdx.x, nslots, s)) return;
+    // one item per thread, grid-stride (an incremental rebuild launches a capped grid)
+    for (uint32_t j_ = blockIdx.x * BLOCK + threadIdx.x;; j_ += gridDim.x * BLOCK) {
+        uint32_t s;
+        if (!sel.pick(j_, nslots, s)) return;
+        [&] {
     uint32_t* L = lines + (size_t)NCL_STRIDE * s;
     const uint32_t r0 = nrdx[s], r1 = nrdx[s + 1], ns = r1 - r0;
     if (r0 < NCL_LEFT || (uint64_t)r0 - NCL_LEFT + NCL_SLOTS > n || ns > NCL_XMAX) {  // clamped window / wide slot
@@ -3054,6 +3087,8 @@ __global__ void ncl_build_kernel(const uint64_t* key, const uint8_t* status, con
     L[1] = ns | (sh << 8);
     L[2] = (defer ? 1u : 0u) | (w0 > 0 ? 2u : 0u) | (w0 + NCL_SLOTS < n ? 4u : 0u);
     L[3] = 0;
+        }();
+    }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -3082,8 +3117,11 @@ __global__ __launch_bounds__(BLOCK) void ncl32_build_kernel(const uint64_t* key,
                                                              const uint32_t* nrdx, uint32_t nslots, uint32_t n,
                                                              uint32_t slot_prefix, uint32_t* lines, LineSel sel) {
     const uint32_t g = threadIdx.x & 7u;
-    uint32_t s;
-    if (!sel.pick((blockIdx.x * BLOCK + threadIdx.x) >> 3, nslots, s)) return;  // whole octets leave
+    // one item per thread, grid-stride (an incremental rebuild launches a capped grid)
+    for (uint32_t j_ = (blockIdx.x * BLOCK + threadIdx.x) >> 3;; j_ += (gridDim.x * BLOCK) >> 3) {
+        uint32_t s;
+        if (!sel.pick(j_, nslots, s)) return;
+        [&] {
     uint4* dst = reinterpret_cast<uint4*>(lines + (size_t)NC32_STRIDE * s) + 4 * g;
     const uint32_t r0 = nrdx[s], r1 = nrdx[s + 1], ns = r1 - r0;
     if (r0 < NC32_LEFT || (uint64_t)r0 - NC32_LEFT + NC32_SLOTS > n || ns > NC32_XMAX) {  // clamped / wide slot
@@ -3118,6 +3156,8 @@ __global__ __launch_bounds__(BLOCK) void ncl32_build_kernel(const uint64_t* key,
     }
 #pragma unroll
     for (int x = 0; x < 4; x++) dst[x] = make_uint4(v[4 * x], v[4 * x + 1], v[4 * x + 2], v[4 * x + 3]);
+        }();
+    }
 }
 
 // DUAL: the family per query (af[i] = 0 -> T4, 1 -> T6), an empty family map gives zero results.
@@ -3855,6 +3895,9 @@ int rebuild_good_prefix(kad_table* t, hipStream_t s, bool full = true) {
     const uint32_t B = t->d.B;
     uint32_t* ctr = t->dctr;
     if (!full) HIP_TRY(hipMemsetAsync(ctr, 0, 4 * sizeof(uint32_t), s));
+    // line builders loop over their items: an incremental rebuild (a dirty list whose length only the device
+    // knows) launches at most one chip-filling grid instead of one thread per line
+    auto lgrid = [&](uint64_t threads) { return dim3(full ? grid_for(threads) : std::min(grid_for(threads), 2048u)); };
     if (t->ncl_mut) {  // NodeCache lines carry the expired bits
         LineSel sel{};
         if (!full) {
@@ -3863,10 +3906,10 @@ int rebuild_good_prefix(kad_table* t, hipStream_t s, bool full = true) {
                                t->ndirty, t->d.nslots, lst, ctr + 3);
             sel = LineSel{lst, ctr + 3};
         }
-        hipLaunchKernelGGL(ncl_build_kernel, dim3(grid_for(t->d.nslots)), dim3(BLOCK), 0, s, t->d.key, t->d.status,
+        hipLaunchKernelGGL(ncl_build_kernel, lgrid(t->d.nslots), dim3(BLOCK), 0, s, t->d.key, t->d.status,
                            t->d.nrdx, t->d.nslots, t->d.n, 64 - t->d.nshift, t->ncl_mut, sel);
         if (t->ncl32_mut)  // the same slots: the marks cover the wider windows when these lines exist
-            hipLaunchKernelGGL(ncl32_build_kernel, dim3(grid_for(8ull * t->d.nslots)), dim3(BLOCK), 0, s, t->d.key,
+            hipLaunchKernelGGL(ncl32_build_kernel, lgrid(8ull * t->d.nslots), dim3(BLOCK), 0, s, t->d.key,
                                t->d.status, t->d.nrdx, t->d.nslots, t->d.n, 64 - t->d.nshift, t->ncl32_mut, sel);
     }
     if (B == 0) return KAD_OK;
@@ -3892,21 +3935,21 @@ int rebuild_good_prefix(kad_table* t, hipStream_t s, bool full = true) {
     LineSel s8{};
     if (t->wl_mut || t->gl_mut) s8 = sel_for(t->ld8, 0);
     if (t->wl_mut)
-        hipLaunchKernelGGL(wl_build_kernel, dim3(grid_for(B)), dim3(BLOCK), 0, s, t->d.key, t->d.status, t->d.dir,
+        hipLaunchKernelGGL(wl_build_kernel, lgrid(B), dim3(BLOCK), 0, s, t->d.key, t->d.status, t->d.dir,
                            t->d.gpre, B, 64 - t->d.rshift, t->d.rbase >> t->d.rshift, t->wl_mut, s8);
     if (t->ws_mut)  // transcoded from the 128-byte lines just rebuilt, the same selection
-        hipLaunchKernelGGL(ws_build_kernel, dim3(grid_for(B)), dim3(BLOCK), 0, s, t->wl_mut, B, t->ws_mut, s8);
+        hipLaunchKernelGGL(ws_build_kernel, lgrid(B), dim3(BLOCK), 0, s, t->wl_mut, B, t->ws_mut, s8);
     if (t->wl16_mut)
-        hipLaunchKernelGGL(wl16_build_kernel, dim3(grid_for(B)), dim3(BLOCK), 0, s, t->d.key, t->d.status, t->d.dir,
+        hipLaunchKernelGGL(wl16_build_kernel, lgrid(B), dim3(BLOCK), 0, s, t->d.key, t->d.status, t->d.dir,
                            t->d.gpre, B, 64 - t->d.rshift, t->d.rbase >> t->d.rshift, t->wl16_mut, sel_for(t->ld16, 1));
     if (t->wl32_mut)
-        hipLaunchKernelGGL(wl32_build_kernel, dim3(grid_for(B)), dim3(BLOCK), 0, s, t->d.key, t->d.status, t->d.dir,
+        hipLaunchKernelGGL(wl32_build_kernel, lgrid(B), dim3(BLOCK), 0, s, t->d.key, t->d.status, t->d.dir,
                            t->d.gpre, B, 64 - t->d.rshift, t->d.rbase >> t->d.rshift, t->wl32_mut, sel_for(t->ld32, 2));
     if (t->gl_mut)
-        hipLaunchKernelGGL(gl_build_kernel, dim3(grid_for(B)), dim3(BLOCK), 0, s, t->d.key, t->d.status, t->d.dir,
+        hipLaunchKernelGGL(gl_build_kernel, lgrid(B), dim3(BLOCK), 0, s, t->d.key, t->d.status, t->d.dir,
                            t->d.gpre, t->d.fkey, t->d.ftail, B, t->gl_mut, s8);
     if (t->gl32_mut)
-        hipLaunchKernelGGL(gl32_build_kernel, dim3(grid_for(B)), dim3(BLOCK), 0, s, t->d.key, t->d.status, t->d.dir,
+        hipLaunchKernelGGL(gl32_build_kernel, lgrid(B), dim3(BLOCK), 0, s, t->d.key, t->d.status, t->d.dir,
                            t->d.gpre, t->d.fkey, t->d.ftail, B, t->gl32_mut, sel_for(t->ld32, 2));
     HIP_TRY(hipGetLastError());
     return KAD_OK;
