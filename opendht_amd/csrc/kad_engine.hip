@@ -181,11 +181,17 @@ __device__ __forceinline__ uint32_t locate_bucket(const DevTable& T, const Targe
             if (hi - lo == 1 && (r0 & RDX_EXACT)) {
                 ub = hi;  // a bucket starts exactly at the slot start <= t
             } else {
-                // count firsts <= t among [lo, hi)
+                // count firsts <= t among [lo, hi); the first's low 96 bits are read only on a top-64 tie
                 while (lo < hi) {
                     uint32_t mid = (lo + hi) >> 1;
-                    const uint32_t* ft = T.ftail + 3ull * mid;
-                    int c = cmp160(T.fkey[mid], ft[0], ft[1], ft[2], t.hi, t.t2, t.t3, t.t4);
+                    const uint64_t fk = T.fkey[mid];
+                    int c;
+                    if (fk != t.hi) {
+                        c = fk < t.hi ? -1 : 1;
+                    } else {
+                        const uint32_t* ft = T.ftail + 3ull * mid;
+                        c = cmp160(fk, ft[0], ft[1], ft[2], t.hi, t.t2, t.t3, t.t4);
+                    }
                     if (c <= 0) lo = mid + 1; else hi = mid;
                 }
                 ub = lo;

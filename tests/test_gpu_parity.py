@@ -223,29 +223,36 @@ def test_config2_uniform_1M(gpu):
         check_nc(T, t, targets[:16384], gpu, counts=(14,))
 
 
-def test_config3_full_shard_sample(gpu):
-    """Config 3 at full per-GPU size: one 1/8 shard of the 100M-node U(24) table (~12.5M nodes)
-    plus halo, 1M queries; a 16k-query sample is checked bit-exact against the oracle and every
-    query against size-independent properties (sorted by XOR distance, all good, in window)."""
+@pytest.mark.parametrize("shard", [0, 3, 7])
+def test_config3_full_shard_every_query(gpu, shard):
+    """Config 3 at full per-GPU size: a 1/8 shard of the 100M-node U(24) table (~12.5M nodes plus halo;
+    the first, a middle and the last shard), 1M owned queries, EVERY query bit-exact against the oracle's
+    closed form (16 threads) for k = 8, 16, 32 and NodeCache k = 14, 32 (shard 0), plus the row properties
+    (good, ascending XOR distance)."""
     from opendht_amd.sharded import ShardSpec, build_shard
     spec = ShardSpec(n_shards=8, depth=24, mean_per_bucket=100e6 / 2**24)
-    sh = build_shard(spec, 0)
+    sh = build_shard(spec, shard)
     q = 1 << 20
-    targets = spec.targets_for(0, q, seed=1234)
-    sample = np.random.default_rng(0).choice(q, 16384, replace=False)
+    targets = spec.targets_for(shard, q, seed=1234 + shard)
     key = sh.ids[:, :8].copy().view(">u8").reshape(-1)
     th = targets[:, :8].copy().view(">u8").reshape(-1)
     with DeviceTable(sh.ids, sh.status, sh.first, sh.off, device=gpu.index or 0, sorted=True) as T:
-        for k in (8, 32):
+        for k in (8, 16, 32):
             idx, cnt = T.rt_closest(dev(targets, gpu), k)
             idx, cnt = u32(idx), cnt.cpu().numpy()
             assert (cnt == k).all()
-            want, wcnt = O.flat_rt_closest(sh.ids, sh.status, sh.first, sh.off, targets[sample], k, nthreads=8)
-            np.testing.assert_array_equal(idx[sample], want, err_msg=f"k={k}")
-            # properties on all queries: results good and ascending in XOR distance
+            want, wcnt = O.flat_rt_closest(sh.ids, sh.status, sh.first, sh.off, targets, k, nthreads=16)
+            np.testing.assert_array_equal(cnt, wcnt, err_msg=f"shard {shard} k={k} counts")
+            np.testing.assert_array_equal(idx, want, err_msg=f"shard {shard} k={k}")
             assert (sh.status[idx] & 1).all()
             d = key[idx] ^ th[:, None]
             assert (d[:, 1:] >= d[:, :-1]).all()
+        if shard == 0:
+            for k in (14, 32):
+                idx, cnt = T.nc_closest(dev(targets, gpu), k)
+                want, wcnt = O.flat_nc_closest(sh.ids, sh.status, targets, k, nthreads=16)
+                np.testing.assert_array_equal(cnt.cpu().numpy(), wcnt, err_msg=f"nc k={k} counts")
+                np.testing.assert_array_equal(u32(idx), want, err_msg=f"nc k={k}")
 
 
 def _nc_tables():

@@ -65,7 +65,7 @@ for n in [int(x) for x in sys.argv[1:]] or [1_000_000, 12_500_000]:
     d = max(1, int(round(np.log2(n / 8))))
     fu, ou = S.uniform_buckets(sid, d)
     U = DeviceTable(sid, st, fu, ou, device=0)
-    for k in (8, 32):
+    for k in (8, 16, 32):
         res[f"U{d}_{n}_k{k}_wl_us"] = round(timeit(U, k), 1)
     U.close()
     print(json.dumps(res), flush=True)
