@@ -69,6 +69,9 @@ extern "C" {
 #define KAD_INFO_GENERAL_LINES 0x200u /* any other bucket shape: count <= 8 queries use one 128-byte
                                          general window line per query (rt_gl_kernel) */
 #define KAD_INFO_GENERAL_LINES32 0x400u /* ... and counts 9..32 one 256-byte line (rt_gl32_kernel) */
+#define KAD_INFO_SLOT_LINES 0x2000u /* other bucket shapes: count <= 8 queries read one 64-byte line indexed by
+                                       the target's top bits (rt_sl_kernel), the locate + 128-byte line only
+                                       as fallback */
 #define KAD_INFO_NODECACHE_LINES32 0x1000u /* sorted table: NodeCache counts 17..32 read one 512-byte line
                                              per query, 8 lanes per query (nc32_line_kernel) */
 #define KAD_INFO_SHORT_LINES 0x800u /* uniform-depth table: count <= 8 queries read one 64-byte short

@@ -24,6 +24,7 @@ KAD_INFO_GENERAL_LINES = 0x200
 KAD_INFO_GENERAL_LINES32 = 0x400
 KAD_INFO_SHORT_LINES = 0x800
 KAD_INFO_NODECACHE_LINES32 = 0x1000
+KAD_INFO_SLOT_LINES = 0x2000
 KAD_OP_REMOVE, KAD_OP_REPLACE, KAD_OP_INSERT, KAD_OP_SPLIT = 1, 2, 3, 4
 
 

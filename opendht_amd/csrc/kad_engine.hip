@@ -98,6 +98,8 @@ struct DevTable {
     const uint4* gl32;  // general window lines, counts 9..32 (TF_GL32): 256 bytes per bucket
     const uint4* ws;    // short window lines, count <= 8 (TF_WS, with TF_WL): 64 bytes per bucket
     const uint4* ncl32; // NodeCache lines for counts 17..32 (TF_NCL32): 512 bytes per node radix slot
+    const uint4* sl;    // slot lines, count <= 8 (TF_SL, with TF_GL): 64 bytes per coarse radix slot
+    uint32_t slshift, slslots;
     uint64_t rbase, nbase;
     uint32_t rshift, rslots, nshift, nslots;
     uint32_t n, B, index_base, flags;
@@ -112,6 +114,7 @@ constexpr uint32_t TF_NCL = 64u;     // NodeCache lines present (sorted tables)
 constexpr uint32_t TF_GL = 128u;     // general window lines (tables without TF_WL: split-policy, per-peer shapes)
 constexpr uint32_t TF_GL32 = 256u;   // general window lines for counts 9..32
 constexpr uint32_t TF_NCL32 = 1024u; // 512-byte NodeCache lines (counts 17..32) present
+constexpr uint32_t TF_SL = 2048u;    // slot lines (count <= 8, general tables: no locate load)
 constexpr uint32_t TF_WS = 512u;     // short (64-byte) window lines for count <= 8 (uniform tables, with TF_WL)
 constexpr uint32_t WIDE = 0x80000000u;  // dir[].x flag: bucket holds > 32 nodes (masks invalid)
 constexpr uint32_t KEY_PAD = 32;        // key[] is padded so 16-node chunk loads never leave it
@@ -1702,6 +1705,158 @@ __global__ __launch_bounds__(BLOCK) void rt_gl_kernel(DevTable T, const uint8_t*
     }
     __shared__ uint64_t xs[BLOCK / 64][192];
     exact_tail(T, t, act && !ok, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
+}
+
+// ---------------------------------------------------------------------------------------
+// Slot lines (TF_SL): general tables locate the target's bucket through the radix (one dependent load, plus a
+// search over bucket firsts when the slot holds several bucket starts) before reading the bucket's line. A
+// slot line is indexed by the target's top bits alone: coarse radix slot j = (t - rbase) >> slshift covers
+// 2^(slshift - rshift) locate slots; when no bucket starts strictly inside it, every target in it lies in
+// one bucket b, and slot line j is b's count <= 8 general line in 64 bytes (a 512-bit string):
+//   [0, 32) base   [32, 44) G(0..2) capped at 15   [44, 47) whole(r)   [47, 49) R   [49, 54) S (the 128-byte
+//   line's stored slots)   [54, 59) S_0   [59, 64) S_1   [64, 70) cp   [70] fallback
+//   [71, 503) 18 slots of 24 bits: key18 << 6 | off (key18 = the top 18 of the 128-byte line's key24)
+// fallback: a bucket starts inside the slot (or the slot lies below the first bucket), the 128-byte line is
+// deferred, a stored node has off >= 64, or two stored nodes share key18. A query reads the first lim slots
+// (lim as in gl_answer); lim > 18 or a fallback line sends it to the locate + 128-byte line path, then the
+// exact path, so the results are the 128-byte line's.
+// ---------------------------------------------------------------------------------------
+constexpr uint32_t SL_SLOTS = 18, SL_SBITS = 24, SL_SLOT0 = 71;
+
+// The bucket of every coarse slot (NONE: a bucket starts inside it, or it lies below the first bucket).
+__global__ void sl_index_kernel(const uint32_t* __restrict__ rrdx, uint32_t rslots, uint32_t k, uint32_t slslots,
+                                uint32_t* __restrict__ slb) {
+    const uint32_t j = blockIdx.x * BLOCK + threadIdx.x;
+    if (j >= slslots) return;
+    const uint32_t a = j << k, e = min((j + 1) << k, rslots);
+    const uint32_t r0 = rrdx[a], r1 = rrdx[e];
+    const uint32_t lo = r0 & RDX_MASK, hi = r1 & RDX_MASK;
+    const bool exact = (r0 & RDX_EXACT) != 0;
+    const uint32_t inner = hi - lo - (exact ? 1u : 0u);
+    slb[j] = inner || (lo == 0 && !exact) ? NONE : (exact ? lo : lo - 1);
+}
+
+// Slot line j from 128-byte general line slb[j]: every slot (gdirty == NULL) or those whose bucket is flagged.
+__global__ __launch_bounds__(BLOCK) void sl_build_kernel(const uint32_t* __restrict__ gl, const uint32_t* __restrict__ slb,
+                                                          uint32_t slslots, const uint8_t* __restrict__ gdirty,
+                                                          uint32_t* __restrict__ sl) {
+    __shared__ uint32_t lds[BLOCK][17];
+    for (uint32_t j = blockIdx.x * BLOCK + threadIdx.x; j < slslots; j += gridDim.x * BLOCK) {
+        const uint32_t b = slb[j];
+        if (gdirty && (b == NONE || !gdirty[b])) continue;
+        uint32_t* L = lds[threadIdx.x];
+        for (int x = 0; x < 17; x++) L[x] = NONE;
+        bool fb = b == NONE;
+        uint32_t hw = 0, sw = 0, base = 0;
+        if (!fb) {
+            const uint32_t* W = gl + (size_t)GL_STRIDE * b;
+            const uint32_t h = W[1], h2 = W[2], S = (h >> 23) & 31u;
+            fb = (h & WL_DEFER) != 0;
+            base = W[0];
+            const uint32_t keep = min(S, SL_SLOTS);
+            for (uint32_t u = 0; u < keep; u++) {
+                const uint32_t v = W[GL_HDR + u], k18 = v >> 14, off = v & 255u;
+                fb |= off >= 64u;
+                for (uint32_t r = 0; r < u; r++) fb |= (W[GL_HDR + r] >> 14) == k18;
+                put_bits(L, SL_SLOT0 + SL_SBITS * u, SL_SBITS, (k18 << 6) | off);
+            }
+            hw = min(h & 63u, 15u) | (min((h >> 6) & 63u, 15u) << 4) | (min((h >> 12) & 63u, 15u) << 8) |
+                 (((h >> 18) & 7u) << 12) | (min((h >> 21) & 3u, 2u) << 15) | (S << 17) | ((h2 & 31u) << 22) |
+                 (((h2 >> 5) & 31u) << 27);
+            sw = (h2 >> 10) & 63u;
+            fb |= ((h >> 21) & 3u) > 2u;
+        }
+        L[0] = base;
+        L[1] = hw;
+        put_bits(L, 64, 7, sw | (fb ? 64u : 0u));
+        store_line<16>(L, sl + 16ull * j);
+    }
+}
+
+// The slot-line answer of a query in coarse slot j (same contract as gl_answer).
+__device__ __forceinline__ bool sl_answer(const DevTable& T, uint64_t thi, uint32_t j, uint32_t count, bool act,
+                                          uint32_t (&o)[8], uint32_t& m) {
+    uint4 L[4];
+    if (act) {
+        const uint4* lp = T.sl + 4ull * j;
+#pragma unroll
+        for (int x = 0; x < 4; x++) L[x] = lp[x];
+    } else {
+#pragma unroll
+        for (int x = 0; x < 4; x++) L[x] = make_uint4(NONE, NONE, NONE, NONE);
+    }
+    const uint32_t h = L[0].y, x6 = ws_bits(L, 64, 7);
+    const uint32_t G0 = h & 15u, G1 = (h >> 4) & 15u, G2 = (h >> 8) & 15u, R = (h >> 15) & 3u, S = (h >> 17) & 31u;
+    const uint32_t Rc = (G0 >= count || (h >> 12) & 1u) ? 0u : (G1 >= count || (h >> 13) & 1u) ? 1u : 2u;
+    m = min(count, Rc == 0 ? G0 : Rc == 1 ? G1 : G2);
+    const uint32_t lim = Rc >= R ? S : Rc == 0 ? ((h >> 22) & 31u) : ((h >> 27) & 31u);
+    const bool ex = !act || (x6 & 64u) || lim < m || Rc > R || lim > SL_SLOTS;
+    const uint32_t cp = x6 & 63u;
+    const uint32_t tx = (uint32_t)((thi << cp) >> 46) << 6;
+    uint32_t v[24];
+#pragma unroll
+    for (int u = 0; u < 24; u++)
+        v[u] = u < (int)SL_SLOTS && (uint32_t)u < lim ? ws_bits(L, SL_SLOT0 + SL_SBITS * (u < (int)SL_SLOTS ? u : 0), SL_SBITS) ^ tx
+                                                      : NONE;
+    sort8(v);
+    sort8(v + 8);
+    merge8(v, v + 8);
+#pragma unroll
+    for (int u = 16; u < (int)SL_SLOTS; u++) {  // insert the rest: one bubble pass each
+        v[7] = min(v[7], v[u]);
+#pragma unroll
+        for (int r = 7; r > 0; r--) cx(v[r - 1], v[r]);
+    }
+    const uint32_t base = L[0].x + T.index_base;
+#pragma unroll
+    for (int r = 0; r < 8; r++) o[r] = (uint32_t)r < m ? base + (v[r] & 63u) : NONE;
+    return !ex;
+}
+
+// count <= 8 on a general table with slot lines: the slot line, else locate + the 128-byte line, else exact.
+// ABL 1 (timing ablation only, results wrong): slot lines only.
+template <int ABL>
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) void rt_sl_kernel(
+    DevTable T, const uint8_t* __restrict__ targets, uint32_t q, uint32_t count, uint32_t* __restrict__ out_idx,
+    uint8_t* __restrict__ out_cnt) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    const bool act = i < q && count > 0;
+    if (i < q && count == 0 && out_cnt) out_cnt[i] = 0;
+    const uint64_t thi = act ? load_target_hi(targets, i) : 0ull;
+    const bool in = act && thi >= T.rbase && ((thi - T.rbase) >> T.slshift) < T.slslots;
+    uint32_t o[8], m;
+    const bool ok = sl_answer(T, thi, in ? (uint32_t)((thi - T.rbase) >> T.slshift) : 0u, count, in, o, m);
+    if (act && ok) {
+        store_row8(out_idx + (size_t)i * count, o, count);
+        if (out_cnt) out_cnt[i] = (uint8_t)m;
+    }
+    if (ABL) return;
+    bool need = act && !ok;
+    if (__any(need)) {  // locate and the 128-byte line (the full target: the locate may compare the low bits)
+        Target t{};
+        uint32_t b = 0;
+        if (need) {
+            t = load_target(targets, i);
+            b = locate_bucket(T, t);
+        }
+        const bool ok2 = gl_answer(T, t, b, count, need, o, m);
+        if (need && ok2) {
+            store_row8(out_idx + (size_t)i * count, o, count);
+            if (out_cnt) out_cnt[i] = (uint8_t)m;
+        }
+        need = need && !ok2;
+        __shared__ uint64_t xs[BLOCK / 64][192];
+        exact_tail(T, t, need, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
+    }
+}
+
+// flags[b] = v for the buckets of a line selection (a compacted dirty list)
+__global__ void mark_sel_kernel(LineSel sel, uint32_t B, uint8_t* flags, uint8_t v) {
+    for (uint32_t j = blockIdx.x * BLOCK + threadIdx.x;; j += gridDim.x * BLOCK) {
+        uint32_t b;
+        if (!sel.pick(j, B, b)) return;
+        flags[b] = v;
+    }
 }
 
 __device__ __forceinline__ bool gl32_answer(const DevTable& T, const Target& t, uint32_t b, uint32_t count, bool act,
@@ -3857,6 +4012,9 @@ struct kad_table {
     uint32_t* ncl32_mut = nullptr;
     uint32_t* gl_mut = nullptr;
     uint32_t* gl32_mut = nullptr;
+    uint32_t* sl_mut = nullptr;     // slot lines (TF_SL) and the bucket of every coarse slot
+    uint32_t* slb = nullptr;
+    uint8_t* gdirty = nullptr;      // B: general lines rebuilt by an incremental refresh (slot-line transcode)
     // host copies of the bucket directory, for the incremental mirror (kad_table_apply)
     std::vector<uint32_t> h_off;
     std::vector<uint8_t> h_first;
@@ -3954,10 +4112,73 @@ int rebuild_good_prefix(kad_table* t, hipStream_t s, bool full = true) {
     if (t->gl_mut)
         hipLaunchKernelGGL(gl_build_kernel, lgrid(B), dim3(BLOCK), 0, s, t->d.key, t->d.status, t->d.dir,
                            t->d.gpre, t->d.fkey, t->d.ftail, B, t->gl_mut, s8);
+    if (t->sl_mut) {  // slot lines: transcoded from the general lines just rebuilt (all, or the flagged buckets')
+        if (!full) hipLaunchKernelGGL(mark_sel_kernel, lgrid(B), dim3(BLOCK), 0, s, s8, B, t->gdirty, (uint8_t)1);
+        hipLaunchKernelGGL(sl_build_kernel, lgrid(t->d.slslots), dim3(BLOCK), 0, s, t->gl_mut, t->slb, t->d.slslots,
+                           full ? nullptr : t->gdirty, t->sl_mut);
+        if (!full) hipLaunchKernelGGL(mark_sel_kernel, lgrid(B), dim3(BLOCK), 0, s, s8, B, t->gdirty, (uint8_t)0);
+    }
     if (t->gl32_mut)
         hipLaunchKernelGGL(gl32_build_kernel, lgrid(B), dim3(BLOCK), 0, s, t->d.key, t->d.status, t->d.dir,
                            t->d.gpre, t->d.fkey, t->d.ftail, B, t->gl32_mut, sel_for(t->ld32, 2));
     HIP_TRY(hipGetLastError());
+    return KAD_OK;
+}
+
+// Slot lines (TF_SL) for a table with general lines: the coarsening k (coarse slot = 2^k locate slots) is the
+// finest whose lines fit 192 MiB (inside the Infinity Cache with the query streams) while at most 1/32 of the
+// coarse slots hold a bucket start (those fall back to the locate path); failing that, the finest under
+// 512 MiB with the same bound; otherwise no slot lines. Synchronous; a failure leaves the table without them.
+int setup_slot_lines(kad_table* t) {
+    DevTable& d = t->d;
+    if (!(d.flags & TF_GL) || !t->gl_mut || d.B == 0 || d.rslots == 0 || t->h_first.size() < 20ull * d.B) return KAD_OK;
+    const uint32_t B = d.B;
+    const uint8_t* f = t->h_first.data();
+    int pick = -1, pick2 = -1;
+    for (uint32_t k = 0; k <= 4 && d.rshift + k <= 63; k++) {
+        const uint32_t sh = d.rshift + k;
+        const uint64_t slots = ((uint64_t)d.rslots + (1ull << k) - 1) >> k;
+        uint64_t inner = 0, last = ~0ull;
+        for (uint32_t b = 0; b < B; b++) {
+            const uint64_t rel = id_hi(f + 20ull * b) - d.rbase;
+            if ((rel & ((1ull << sh) - 1)) == 0 && id_low_zero(f + 20ull * b)) continue;  // starts at a slot start
+            const uint64_t j = rel >> sh;
+            if (j != last) { inner++; last = j; }
+        }
+        const bool few = inner * 32 <= slots;
+        if (std::getenv("KAD_DEBUG"))
+            std::fprintf(stderr, "slot lines: k=%u slots=%llu inner=%llu\n", k, (unsigned long long)slots,
+                         (unsigned long long)inner);
+        if (few && slots * 64 <= (192ull << 20) && pick < 0) pick = (int)k;
+        if (few && slots * 64 <= (512ull << 20) && pick2 < 0) pick2 = (int)k;
+    }
+    if (pick < 0) pick = pick2;
+    if (pick < 0) return KAD_OK;
+    const uint32_t k = (uint32_t)pick;
+    const uint32_t slslots = (uint32_t)(((uint64_t)d.rslots + (1ull << k) - 1) >> k);
+    uint32_t *lines = nullptr, *slb = nullptr;
+    uint8_t* gd = nullptr;
+    std::vector<void*> fresh;
+    uint64_t fb = 0;
+    auto drop = [&]() { for (void* p : fresh) (void)hipFree(p); };
+    if (dev_upload(&lines, nullptr, 16ull * slslots, fresh, fb) || dev_upload(&slb, nullptr, slslots, fresh, fb) ||
+        dev_upload(&gd, nullptr, B, fresh, fb) || hipMemset(gd, 0, B) != hipSuccess) {
+        drop();
+        return KAD_OK;
+    }
+    hipLaunchKernelGGL(sl_index_kernel, dim3(grid_for(slslots)), dim3(BLOCK), 0, 0, d.rrdx, d.rslots, k, slslots, slb);
+    hipLaunchKernelGGL(sl_build_kernel, dim3(grid_for(slslots)), dim3(BLOCK), 0, 0, t->gl_mut, slb, slslots, nullptr, lines);
+    if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+        drop();
+        return set_err(KAD_ERR_HIP, "slot-line build failed");
+    }
+    t->owned.insert(t->owned.end(), fresh.begin(), fresh.end());
+    t->bytes += fb;
+    t->sl_mut = lines; t->slb = slb; t->gdirty = gd;
+    d.sl = reinterpret_cast<const uint4*>(lines);
+    d.slshift = d.rshift + k;
+    d.slslots = slslots;
+    d.flags |= TF_SL;
     return KAD_OK;
 }
 
@@ -4008,7 +4229,7 @@ int setup_general_lines(kad_table* t) {
     } else {
         (void)hipFree(lp32);
     }
-    return KAD_OK;
+    return setup_slot_lines(t);
 }
 
 // Allocate (zeroed) the incremental-refresh flags for the table's current shape.
@@ -4119,6 +4340,13 @@ int launch_rt(const kad_table* t, const uint8_t* targets, uint32_t q, uint32_t c
             hipLaunchKernelGGL(rt_wl16_kernel<0>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
     } else if (K == 32 && (d.flags & TF_WL32) && !(ev && std::strcmp(ev, "lane") == 0)) {
         hipLaunchKernelGGL(rt_wl32_kernel, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
+    } else if (K == 8 && (d.flags & TF_SL) && !(ev && (std::strcmp(ev, "lane") == 0 || std::strcmp(ev, "gl") == 0 ||
+                                                        std::strcmp(ev, "sl_abl1") == 0))) {
+        hipLaunchKernelGGL(rt_sl_kernel<0>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
+#ifdef KAD_ABLATIONS
+    } else if (K == 8 && (d.flags & TF_SL) && ev && std::strcmp(ev, "sl_abl1") == 0) {
+        hipLaunchKernelGGL(rt_sl_kernel<1>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
+#endif
     } else if (K == 8 && (d.flags & TF_GL) && !(ev && std::strcmp(ev, "lane") == 0)) {
         hipLaunchKernelGGL(rt_gl_kernel, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
     } else if (K > 8 && (d.flags & TF_GL32) && !(ev && std::strcmp(ev, "lane") == 0)) {
@@ -4460,7 +4688,8 @@ int kad_table_get_info(const kad_table* t, kad_table_info* out) {
     out->flags = t->flags | ((t->d.flags & TF_WL) ? KAD_INFO_WINDOW_LINES : 0u) |
                  ((t->d.flags & TF_GL) ? KAD_INFO_GENERAL_LINES : 0u) | ((t->d.flags & TF_GL32) ? KAD_INFO_GENERAL_LINES32 : 0u) |
                  ((t->d.flags & TF_WS) ? KAD_INFO_SHORT_LINES : 0u) |
-                 ((t->d.flags & TF_NCL32) ? KAD_INFO_NODECACHE_LINES32 : 0u);
+                 ((t->d.flags & TF_NCL32) ? KAD_INFO_NODECACHE_LINES32 : 0u) |
+                 ((t->d.flags & TF_SL) ? KAD_INFO_SLOT_LINES : 0u);
     out->device = t->device;
     out->rt_radix_bits = t->rbits;
     out->nc_radix_bits = t->nbits;
@@ -5239,6 +5468,8 @@ int kad_table_apply(kad_table* t, const uint32_t* ops, uint32_t n_ops, const uin
     if (reshape) {  // general lines are per bucket: re-created below for the new bucket count
         release(t, t->gl_mut); t->gl_mut = nullptr; d.gl = nullptr; d.flags &= ~TF_GL;
         release(t, t->gl32_mut); t->gl32_mut = nullptr; d.gl32 = nullptr; d.flags &= ~TF_GL32;
+        release(t, t->sl_mut); release(t, t->slb); release(t, t->gdirty);
+        t->sl_mut = nullptr; t->slb = nullptr; t->gdirty = nullptr; d.sl = nullptr; d.slslots = 0; d.flags &= ~TF_SL;
     }
     release(t, const_cast<uint32_t*>(d.dmask));
     d.dmask = ddm;

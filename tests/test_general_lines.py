@@ -1,4 +1,5 @@
-"""General window lines (rt_gl_kernel / rt_gl32_kernel): RoutingTable::findClosestNodes on tables of any
+"""General window lines (rt_gl_kernel / rt_gl32_kernel) and their slot lines (rt_sl_kernel, count <= 8):
+RoutingTable::findClosestNodes on tables of any
 bucket shape -- the reference split policy (dht.cpp:903-934, routing_table.cpp:137-163) at 10k..300k
 nodes, a mostly-bad one and a clustered one (neighbouring buckets of very different depths) -- bit-exact
 against the oracle for every count 1..32, with the tables confirmed to carry the general lines (so the
@@ -11,14 +12,17 @@ import oracle as O
 import tables as TB
 from opendht_amd import DeviceTable
 from opendht_amd import synth as S
-from opendht_amd._lib import KAD_INFO_GENERAL_LINES, KAD_INFO_GENERAL_LINES32, KAD_INFO_WINDOW_LINES, KAD_OP_SPLIT
+from opendht_amd._lib import (KAD_INFO_GENERAL_LINES, KAD_INFO_GENERAL_LINES32, KAD_INFO_SLOT_LINES,
+                              KAD_INFO_WINDOW_LINES, KAD_OP_SPLIT)
 
 pytestmark = pytest.mark.gpu
 
 ALL = tuple(range(1, 33))
 
 
-def _check(T, t, targets, gpu, counts=ALL, status=None):
+def _check(T, t, targets, gpu, counts=ALL, status=None, mp=None):
+    """Every count against the oracle; with `mp` (monkeypatch) the count <= 8 queries also through the
+    128-byte general lines alone (KAD_RT_KERNEL=gl), so the slot lines and their fallback are compared."""
     st = t["status"] if status is None else status
     tg = torch.from_numpy(np.ascontiguousarray(targets)).to(gpu)
     for k in counts:
@@ -27,6 +31,11 @@ def _check(T, t, targets, gpu, counts=ALL, status=None):
         want, wcnt = O.flat_rt_closest(t["ids"], st, t["first"], t["off"], targets, k, nthreads=8)
         np.testing.assert_array_equal(cnt.cpu().numpy(), wcnt, err_msg=f"{t['name']} k={k} counts")
         np.testing.assert_array_equal(idx.cpu().numpy().view(np.uint32), want, err_msg=f"{t['name']} k={k}")
+        if mp is not None and k <= 8:
+            mp.setenv("KAD_RT_KERNEL", "gl")
+            idx2, cnt2 = T.rt_closest(tg, k)
+            mp.delenv("KAD_RT_KERNEL")
+            np.testing.assert_array_equal(idx2.cpu().numpy().view(np.uint32), want, err_msg=f"{t['name']} k={k} gl")
 
 
 def _s_tables():
@@ -50,16 +59,16 @@ def _s_tables():
 
 
 @pytest.mark.parametrize("t", _s_tables(), ids=lambda t: t["name"])
-def test_general_lines_parity(gpu, t):
+def test_general_lines_parity(gpu, t, monkeypatch):
     with DeviceTable(t["ids"], t["status"], t["first"], t["off"], device=0) as T:
         f = T.info()["flags"]
         assert not (f & KAD_INFO_WINDOW_LINES)
         if not t.get("lane"):
-            assert f & KAD_INFO_GENERAL_LINES and f & KAD_INFO_GENERAL_LINES32, hex(f)
-        _check(T, t, TB.adversarial_targets(t, extra=4000), gpu)
+            assert f & KAD_INFO_GENERAL_LINES and f & KAD_INFO_GENERAL_LINES32 and f & KAD_INFO_SLOT_LINES, hex(f)
+        _check(T, t, TB.adversarial_targets(t, extra=4000), gpu, mp=monkeypatch)
 
 
-def test_general_lines_after_status_patch(gpu):
+def test_general_lines_after_status_patch(gpu, monkeypatch):
     t = TB.split_config(50_000, seed=0x66)
     rng = np.random.default_rng(0x67)
     targets = TB.adversarial_targets(t, extra=3000)
@@ -70,7 +79,7 @@ def test_general_lines_after_status_patch(gpu):
             nodes = rng.choice(st.shape[0], size=m, replace=False).astype(np.uint32)
             st[nodes] = rng.choice(np.array([0, 1, 1, 2], np.uint8), size=m)
             T.patch_status(nodes, st[nodes])
-            _check(T, t, targets, gpu, counts=(1, 5, 8, 9, 14, 16, 20, 32), status=st)
+            _check(T, t, targets, gpu, counts=(1, 5, 8, 9, 14, 16, 20, 32), status=st, mp=monkeypatch)
 
 
 def test_uniform_table_switches_to_general_lines_after_split(gpu):
@@ -82,6 +91,6 @@ def test_uniform_table_switches_to_general_lines_after_split(gpu):
         T.apply(np.array([[KAD_OP_SPLIT, 100, 0], [KAD_OP_SPLIT, 7, 0]], np.uint32))
         ids, st, first, off = T.export()
         f = T.info()["flags"]
-        assert not (f & KAD_INFO_WINDOW_LINES) and f & KAD_INFO_GENERAL_LINES, hex(f)
+        assert not (f & KAD_INFO_WINDOW_LINES) and f & KAD_INFO_GENERAL_LINES and f & KAD_INFO_SLOT_LINES, hex(f)
         t2 = TB.table(ids, st, first, off, name="U11_split")
         _check(T, t2, TB.adversarial_targets(t2, extra=3000), gpu, counts=(1, 7, 8, 9, 16, 17, 32))

@@ -16,6 +16,10 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
+import opendht_amd._lib as _kl  # noqa: E402
+
+if os.environ.get("SHAPES_ABL"):
+    _kl.use_ablation_build()
 from opendht_amd import DeviceTable  # noqa: E402
 from opendht_amd import synth as S  # noqa: E402
 
@@ -51,6 +55,11 @@ for n in [int(x) for x in sys.argv[1:]] or [1_000_000, 12_500_000]:
     inf = T.info()
     res[f"S{n}_buckets"] = inf["n_buckets"]
     res[f"S{n}_flags"] = hex(inf["flags"])
+    if os.environ.get("SHAPES_ABL"):  # k = 8: slot lines alone (results wrong), the 128-byte general lines alone
+        for v in ("sl_abl1", "gl"):
+            os.environ["KAD_RT_KERNEL"] = v
+            res[f"S{n}_k8_{v}_us"] = round(timeit(T, 8), 1)
+            os.environ.pop("KAD_RT_KERNEL")
     for k in (8, 14, 16, 32):
         res[f"S{n}_k{k}_gl_us"] = round(timeit(T, k), 1)
         a = T.rt_closest(tgs[0], k)[0].clone()
