@@ -1715,13 +1715,16 @@ __global__ __launch_bounds__(BLOCK) void rt_gl_kernel(DevTable T, const uint8_t*
 // one bucket b, and slot line j is b's count <= 8 general line in 64 bytes (a 512-bit string):
 //   [0, 32) base   [32, 44) G(0..2) capped at 15   [44, 47) whole(r)   [47, 49) R   [49, 54) S (the 128-byte
 //   line's stored slots)   [54, 59) S_0   [59, 64) S_1   [64, 70) cp   [70] fallback
-//   [71, 503) 18 slots of 24 bits: key18 << 6 | off (key18 = the top 18 of the 128-byte line's key24)
-// fallback: a bucket starts inside the slot (or the slot lies below the first bucket), the 128-byte line is
-// deferred, a stored node has off >= 64, or two stored nodes share key18. A query reads the first lim slots
-// (lim as in gl_answer); lim > 18 or a fallback line sends it to the locate + 128-byte line path, then the
-// exact path, so the results are the 128-byte line's.
+//   [71, 511) 20 slots of 22 bits: key16 << 6 | off (key16 = the top 16 of the 128-byte line's key24)
+// A slot whose line cannot answer count 8 (the 128-byte line is deferred or stores more than 20 slots, a
+// stored node has off >= 64, two stored nodes share key16) or in which a bucket starts holds a FALLBACK line
+// instead: dw0 = the bucket at the slot start (NONE below the first bucket, or with several inner starts /
+// an inner first with nonzero low bits), dw1 = NONE (the marker: a line's dw1 never is), dw2:dw3 = the top
+// 64 bits of the one bucket first inside the slot, dw4 bit 0 = there is one. Its query reads the 128-byte
+// line of the bucket that gives (no locate load); dw0 = NONE takes the locate path. The results are always
+// the 128-byte line's (and from there the exact path's).
 // ---------------------------------------------------------------------------------------
-constexpr uint32_t SL_SLOTS = 18, SL_SBITS = 24, SL_SLOT0 = 71;
+constexpr uint32_t SL_SLOTS = 20, SL_SBITS = 22, SL_SLOT0 = 71;
 
 // The bucket of every coarse slot (NONE: a bucket starts inside it, or it lies below the first bucket).
 __global__ void sl_index_kernel(const uint32_t* __restrict__ rrdx, uint32_t rslots, uint32_t k, uint32_t slslots,
@@ -1736,10 +1739,13 @@ __global__ void sl_index_kernel(const uint32_t* __restrict__ rrdx, uint32_t rslo
     slb[j] = inner || (lo == 0 && !exact) ? NONE : (exact ? lo : lo - 1);
 }
 
-// Slot line j from 128-byte general line slb[j]: every slot (gdirty == NULL) or those whose bucket is flagged.
+// Slot line j from 128-byte general line slb[j] (or its fallback line): every slot (gdirty == NULL) or those whose
+// bucket is flagged (a fallback line of a slot with a bucket start depends on the bucket firsts only).
 __global__ __launch_bounds__(BLOCK) void sl_build_kernel(const uint32_t* __restrict__ gl, const uint32_t* __restrict__ slb,
                                                           uint32_t slslots, const uint8_t* __restrict__ gdirty,
-                                                          uint32_t* __restrict__ sl) {
+                                                          const uint32_t* __restrict__ rrdx, uint32_t rslots, uint32_t k,
+                                                          const uint64_t* __restrict__ fkey,
+                                                          const uint32_t* __restrict__ ftail, uint32_t* __restrict__ sl) {
     __shared__ uint32_t lds[BLOCK][17];
     for (uint32_t j = blockIdx.x * BLOCK + threadIdx.x; j < slslots; j += gridDim.x * BLOCK) {
         const uint32_t b = slb[j];
@@ -1747,35 +1753,60 @@ __global__ __launch_bounds__(BLOCK) void sl_build_kernel(const uint32_t* __restr
         uint32_t* L = lds[threadIdx.x];
         for (int x = 0; x < 17; x++) L[x] = NONE;
         bool fb = b == NONE;
-        uint32_t hw = 0, sw = 0, base = 0;
-        if (!fb) {
+        uint32_t fb_b = b, split_hi = 0, split_lo = 0, has_split = 0;
+        if (b == NONE) {  // a bucket starts inside the slot: the bucket at its start and the one inner first
+            const uint32_t r0 = rrdx[j << k], r1 = rrdx[min((j + 1) << k, rslots)];
+            const uint32_t lo = r0 & RDX_MASK, hi = r1 & RDX_MASK;
+            const bool exact = (r0 & RDX_EXACT) != 0;
+            const uint32_t inner = hi - lo - (exact ? 1u : 0u);
+            fb_b = (lo == 0 && !exact) ? NONE : (exact ? lo : lo - 1);
+            if (fb_b != NONE && inner == 1) {
+                const uint32_t ii = exact ? lo + 1 : lo;
+                const uint32_t* ft = ftail + 3ull * ii;
+                if ((ft[0] | ft[1] | ft[2]) == 0) {
+                    split_hi = (uint32_t)(fkey[ii] >> 32);
+                    split_lo = (uint32_t)fkey[ii];
+                    has_split = 1;
+                } else {
+                    fb_b = NONE;
+                }
+            } else {
+                fb_b = NONE;
+            }
+        } else {
             const uint32_t* W = gl + (size_t)GL_STRIDE * b;
             const uint32_t h = W[1], h2 = W[2], S = (h >> 23) & 31u;
-            fb = (h & WL_DEFER) != 0;
-            base = W[0];
-            const uint32_t keep = min(S, SL_SLOTS);
-            for (uint32_t u = 0; u < keep; u++) {
-                const uint32_t v = W[GL_HDR + u], k18 = v >> 14, off = v & 255u;
+            fb = (h & WL_DEFER) != 0 || S > SL_SLOTS || ((h >> 21) & 3u) > 2u;
+            for (uint32_t u = 0; u < S && !fb; u++) {
+                const uint32_t v = W[GL_HDR + u], k16 = v >> 16, off = v & 255u;
                 fb |= off >= 64u;
-                for (uint32_t r = 0; r < u; r++) fb |= (W[GL_HDR + r] >> 14) == k18;
-                put_bits(L, SL_SLOT0 + SL_SBITS * u, SL_SBITS, (k18 << 6) | off);
+                for (uint32_t r = 0; r < u; r++) fb |= (W[GL_HDR + r] >> 16) == k16;
+                put_bits(L, SL_SLOT0 + SL_SBITS * u, SL_SBITS, (k16 << 6) | off);
             }
-            hw = min(h & 63u, 15u) | (min((h >> 6) & 63u, 15u) << 4) | (min((h >> 12) & 63u, 15u) << 8) |
-                 (((h >> 18) & 7u) << 12) | (min((h >> 21) & 3u, 2u) << 15) | (S << 17) | ((h2 & 31u) << 22) |
-                 (((h2 >> 5) & 31u) << 27);
-            sw = (h2 >> 10) & 63u;
-            fb |= ((h >> 21) & 3u) > 2u;
+            if (!fb) {
+                L[0] = W[0];
+                L[1] = min(h & 63u, 15u) | (min((h >> 6) & 63u, 15u) << 4) | (min((h >> 12) & 63u, 15u) << 8) |
+                       (((h >> 18) & 7u) << 12) | (((h >> 21) & 3u) << 15) | (S << 17) | ((h2 & 31u) << 22) |
+                       (((h2 >> 5) & 31u) << 27);
+                put_bits(L, 64, 7, (h2 >> 10) & 63u);
+            }
         }
-        L[0] = base;
-        L[1] = hw;
-        put_bits(L, 64, 7, sw | (fb ? 64u : 0u));
+        if (fb) {
+            for (int x = 0; x < 17; x++) L[x] = 0;
+            L[0] = fb_b;
+            L[1] = NONE;
+            L[2] = split_hi;
+            L[3] = split_lo;
+            L[4] = has_split;
+        }
         store_line<16>(L, sl + 16ull * j);
     }
 }
 
-// The slot-line answer of a query in coarse slot j (same contract as gl_answer).
+// The slot-line answer of a query in coarse slot j (same contract as gl_answer). bh: the bucket whose 128-byte line
+// a failed query reads next (a fallback line names it), NONE: locate it.
 __device__ __forceinline__ bool sl_answer(const DevTable& T, uint64_t thi, uint32_t j, uint32_t count, bool act,
-                                          uint32_t (&o)[8], uint32_t& m) {
+                                          uint32_t (&o)[8], uint32_t& m, uint32_t& bh) {
     uint4 L[4];
     if (act) {
         const uint4* lp = T.sl + 4ull * j;
@@ -1786,13 +1817,17 @@ __device__ __forceinline__ bool sl_answer(const DevTable& T, uint64_t thi, uint3
         for (int x = 0; x < 4; x++) L[x] = make_uint4(NONE, NONE, NONE, NONE);
     }
     const uint32_t h = L[0].y, x6 = ws_bits(L, 64, 7);
+    const bool fbl = h == NONE;
+    bh = NONE;
+    if (act && fbl && L[0].x != NONE)
+        bh = L[0].x + ((L[1].x & 1u) && thi >= (((uint64_t)L[0].z << 32) | L[0].w) ? 1u : 0u);
     const uint32_t G0 = h & 15u, G1 = (h >> 4) & 15u, G2 = (h >> 8) & 15u, R = (h >> 15) & 3u, S = (h >> 17) & 31u;
     const uint32_t Rc = (G0 >= count || (h >> 12) & 1u) ? 0u : (G1 >= count || (h >> 13) & 1u) ? 1u : 2u;
     m = min(count, Rc == 0 ? G0 : Rc == 1 ? G1 : G2);
     const uint32_t lim = Rc >= R ? S : Rc == 0 ? ((h >> 22) & 31u) : ((h >> 27) & 31u);
-    const bool ex = !act || (x6 & 64u) || lim < m || Rc > R || lim > SL_SLOTS;
+    const bool ex = !act || fbl || lim < m || Rc > R || lim > SL_SLOTS;
     const uint32_t cp = x6 & 63u;
-    const uint32_t tx = (uint32_t)((thi << cp) >> 46) << 6;
+    const uint32_t tx = (uint32_t)((thi << cp) >> 48) << 6;
     uint32_t v[24];
 #pragma unroll
     for (int u = 0; u < 24; u++)
@@ -1824,8 +1859,8 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     if (i < q && count == 0 && out_cnt) out_cnt[i] = 0;
     const uint64_t thi = act ? load_target_hi(targets, i) : 0ull;
     const bool in = act && thi >= T.rbase && ((thi - T.rbase) >> T.slshift) < T.slslots;
-    uint32_t o[8], m;
-    const bool ok = sl_answer(T, thi, in ? (uint32_t)((thi - T.rbase) >> T.slshift) : 0u, count, in, o, m);
+    uint32_t o[8], m, bh;
+    const bool ok = sl_answer(T, thi, in ? (uint32_t)((thi - T.rbase) >> T.slshift) : 0u, count, in, o, m, bh);
     if (act && ok) {
         store_row8(out_idx + (size_t)i * count, o, count);
         if (out_cnt) out_cnt[i] = (uint8_t)m;
@@ -1837,7 +1872,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) v
         uint32_t b = 0;
         if (need) {
             t = load_target(targets, i);
-            b = locate_bucket(T, t);
+            b = bh != NONE ? bh : locate_bucket(T, t);
         }
         const bool ok2 = gl_answer(T, t, b, count, need, o, m);
         if (need && ok2) {
@@ -1848,6 +1883,14 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) v
         __shared__ uint64_t xs[BLOCK / 64][192];
         exact_tail(T, t, need, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
     }
+}
+
+// Fallback slot lines (dw1 == NONE) and those without a bucket (dw0 == NONE): cnt[0], cnt[1] (KAD_DEBUG).
+__global__ void sl_count_kernel(const uint32_t* sl, uint32_t slslots, uint32_t* cnt) {
+    const uint32_t j = blockIdx.x * BLOCK + threadIdx.x;
+    if (j >= slslots || sl[16ull * j + 1] != NONE) return;
+    atomicAdd(cnt, 1u);
+    if (sl[16ull * j] == NONE) atomicAdd(cnt + 1, 1u);
 }
 
 // flags[b] = v for the buckets of a line selection (a compacted dirty list)
@@ -4115,7 +4158,8 @@ int rebuild_good_prefix(kad_table* t, hipStream_t s, bool full = true) {
     if (t->sl_mut) {  // slot lines: transcoded from the general lines just rebuilt (all, or the flagged buckets')
         if (!full) hipLaunchKernelGGL(mark_sel_kernel, lgrid(B), dim3(BLOCK), 0, s, s8, B, t->gdirty, (uint8_t)1);
         hipLaunchKernelGGL(sl_build_kernel, lgrid(t->d.slslots), dim3(BLOCK), 0, s, t->gl_mut, t->slb, t->d.slslots,
-                           full ? nullptr : t->gdirty, t->sl_mut);
+                           full ? nullptr : t->gdirty, t->d.rrdx, t->d.rslots, t->d.slshift - t->d.rshift, t->d.fkey,
+                           t->d.ftail, t->sl_mut);
         if (!full) hipLaunchKernelGGL(mark_sel_kernel, lgrid(B), dim3(BLOCK), 0, s, s8, B, t->gdirty, (uint8_t)0);
     }
     if (t->gl32_mut)
@@ -4126,15 +4170,15 @@ int rebuild_good_prefix(kad_table* t, hipStream_t s, bool full = true) {
 }
 
 // Slot lines (TF_SL) for a table with general lines: the coarsening k (coarse slot = 2^k locate slots) is the
-// finest whose lines fit 192 MiB (inside the Infinity Cache with the query streams) while at most 1/32 of the
-// coarse slots hold a bucket start (those fall back to the locate path); failing that, the finest under
-// 512 MiB with the same bound; otherwise no slot lines. Synchronous; a failure leaves the table without them.
+// coarsest (smallest table) at which at most 1/32 of the coarse slots hold a bucket start (their queries take a
+// fallback line), provided the lines fit 512 MiB; otherwise no slot lines. Synchronous; a failure leaves the
+// table without them.
 int setup_slot_lines(kad_table* t) {
     DevTable& d = t->d;
     if (!(d.flags & TF_GL) || !t->gl_mut || d.B == 0 || d.rslots == 0 || t->h_first.size() < 20ull * d.B) return KAD_OK;
     const uint32_t B = d.B;
     const uint8_t* f = t->h_first.data();
-    int pick = -1, pick2 = -1;
+    int pick = -1;
     for (uint32_t k = 0; k <= 4 && d.rshift + k <= 63; k++) {
         const uint32_t sh = d.rshift + k;
         const uint64_t slots = ((uint64_t)d.rslots + (1ull << k) - 1) >> k;
@@ -4149,10 +4193,8 @@ int setup_slot_lines(kad_table* t) {
         if (std::getenv("KAD_DEBUG"))
             std::fprintf(stderr, "slot lines: k=%u slots=%llu inner=%llu\n", k, (unsigned long long)slots,
                          (unsigned long long)inner);
-        if (few && slots * 64 <= (192ull << 20) && pick < 0) pick = (int)k;
-        if (few && slots * 64 <= (512ull << 20) && pick2 < 0) pick2 = (int)k;
+        if (few && slots * 64 <= (512ull << 20)) pick = (int)k;  // the coarsest (smallest) that qualifies
     }
-    if (pick < 0) pick = pick2;
     if (pick < 0) return KAD_OK;
     const uint32_t k = (uint32_t)pick;
     const uint32_t slslots = (uint32_t)(((uint64_t)d.rslots + (1ull << k) - 1) >> k);
@@ -4167,10 +4209,21 @@ int setup_slot_lines(kad_table* t) {
         return KAD_OK;
     }
     hipLaunchKernelGGL(sl_index_kernel, dim3(grid_for(slslots)), dim3(BLOCK), 0, 0, d.rrdx, d.rslots, k, slslots, slb);
-    hipLaunchKernelGGL(sl_build_kernel, dim3(grid_for(slslots)), dim3(BLOCK), 0, 0, t->gl_mut, slb, slslots, nullptr, lines);
+    hipLaunchKernelGGL(sl_build_kernel, dim3(grid_for(slslots)), dim3(BLOCK), 0, 0, t->gl_mut, slb, slslots, nullptr,
+                       d.rrdx, d.rslots, k, d.fkey, d.ftail, lines);
     if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
         drop();
         return set_err(KAD_ERR_HIP, "slot-line build failed");
+    }
+    if (std::getenv("KAD_DEBUG")) {
+        uint32_t* dc = nullptr;
+        uint32_t hc[2] = {0, 0};
+        if (hipMalloc(&dc, 8) == hipSuccess && hipMemset(dc, 0, 8) == hipSuccess) {
+            hipLaunchKernelGGL(sl_count_kernel, dim3(grid_for(slslots)), dim3(BLOCK), 0, 0, lines, slslots, dc);
+            (void)hipMemcpy(hc, dc, 8, hipMemcpyDeviceToHost);
+        }
+        if (dc) (void)hipFree(dc);
+        std::fprintf(stderr, "slot lines: k=%u, %u slots, %u fallback lines (%u without a bucket)\n", k, slslots, hc[0], hc[1]);
     }
     t->owned.insert(t->owned.end(), fresh.begin(), fresh.end());
     t->bytes += fb;

@@ -58,7 +58,7 @@ for n in [int(x) for x in sys.argv[1:]] or [1_000_000, 12_500_000]:
     if os.environ.get("SHAPES_ABL"):  # k = 8: slot lines alone (results wrong), the 128-byte general lines alone
         for v in ("sl_abl1", "gl"):
             os.environ["KAD_RT_KERNEL"] = v
-            res[f"S{n}_k8_{v}_us"] = round(timeit(T, 8), 1)
+            res[f"S{n}_k8_only_{v}_us"] = round(timeit(T, 8), 1)
             os.environ.pop("KAD_RT_KERNEL")
     for k in (8, 14, 16, 32):
         res[f"S{n}_k{k}_gl_us"] = round(timeit(T, k), 1)
