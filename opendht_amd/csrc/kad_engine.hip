@@ -99,6 +99,7 @@ struct DevTable {
     const uint4* ws;    // short window lines, count <= 8 (TF_WS, with TF_WL): 64 bytes per bucket
     const uint4* ncl32; // NodeCache lines for counts 17..32 (TF_NCL32): 512 bytes per node radix slot
     const uint4* sl;    // slot lines, count <= 8 (TF_SL, with TF_GL): 64 bytes per coarse radix slot
+    const uint4* gl16;  // general window lines, counts 9..16 (TF_GL16): 128 bytes per bucket
     uint32_t slshift, slslots;
     uint64_t rbase, nbase;
     uint32_t rshift, rslots, nshift, nslots;
@@ -115,6 +116,7 @@ constexpr uint32_t TF_GL = 128u;     // general window lines (tables without TF_
 constexpr uint32_t TF_GL32 = 256u;   // general window lines for counts 9..32
 constexpr uint32_t TF_NCL32 = 1024u; // 512-byte NodeCache lines (counts 17..32) present
 constexpr uint32_t TF_SL = 2048u;    // slot lines (count <= 8, general tables: no locate load)
+constexpr uint32_t TF_GL16 = 4096u;  // general window lines for counts 9..16 (one 128-byte line)
 constexpr uint32_t TF_WS = 512u;     // short (64-byte) window lines for count <= 8 (uniform tables, with TF_WL)
 constexpr uint32_t WIDE = 0x80000000u;  // dir[].x flag: bucket holds > 32 nodes (masks invalid)
 constexpr uint32_t KEY_PAD = 32;        // key[] is padded so 16-node chunk loads never leave it
@@ -1971,8 +1973,79 @@ __global__ __launch_bounds__(BLOCK) void rt_gl32_kernel(DevTable T, const uint8_
     exact_tail(T, t, act && !ok, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
 }
 
+// ---------------------------------------------------------------------------------------
+// General window lines for counts 9..16 (TF_GL16): the count <= 8 construction sized for 16 (R_16 <= 3, windows of up
+// to 8 buckets) in ONE 128-byte line, so SEARCH_NODES = 14 (dht.cpp:1650, the refill of a search) reads 128 bytes
+// instead of the 256-byte line of counts 17..32. Line b (32 dwords):
+//   dw0  base    dw1  G(0..3), 6 bits each | whole(r) << 24 | R_16 << 28 | defer << 31
+//   dw2  S | S_0 << 5 | S_1 << 10 | S_2 << 15 | cp << 20     dw3  0     dw4..31  28 slots: key24 << 8 | off
+// The ranking is wl16's: 28 slot values padded to 32, two Batcher-16 sorts and one top-16 bitonic merge.
+// ---------------------------------------------------------------------------------------
+constexpr uint32_t GL16_SLOTS = 28, GL16_HDR = 4, GL16_STRIDE = 32;
+
+__device__ __forceinline__ bool gl16_answer(const DevTable& T, const Target& t, uint32_t b, uint32_t count, bool act,
+                                            uint32_t (&o)[16], uint32_t& m) {
+    uint32_t L[GL16_STRIDE];
+    if (act) {
+        const uint4* lp = T.gl16 + (GL16_STRIDE / 4) * (size_t)b;
+#pragma unroll
+        for (int x = 0; x < (int)GL16_STRIDE / 4; x++) {
+            const uint4 u = lp[x];
+            L[4 * x] = u.x; L[4 * x + 1] = u.y; L[4 * x + 2] = u.z; L[4 * x + 3] = u.w;
+        }
+    } else {
+#pragma unroll
+        for (int x = 0; x < (int)GL16_STRIDE; x++) L[x] = NONE;
+    }
+    const uint32_t h = L[1], h2 = L[2], R = (h >> 28) & 3u, S = h2 & 31u;
+    uint32_t Rc = 4, Gc = 0;
+#pragma unroll
+    for (int r = 3; r >= 0; r--) {
+        const uint32_t g = (h >> (6 * r)) & 63u;
+        if (g >= count || ((h >> (24 + r)) & 1u)) { Rc = (uint32_t)r; Gc = g; }
+    }
+    m = min(count, Gc);
+    const uint32_t lim = Rc >= R ? S : (h2 >> (5 + 5 * min(Rc, 2u))) & 31u;
+    bool ex = !act || (h & WL_DEFER) || Rc > R || lim < m;
+    if (act && b == 0) ex |= below_first(T, t);
+    const uint32_t cp = (h2 >> 20) & 63u;
+    const uint32_t tx = (uint32_t)((t.hi << (cp & 63u)) >> 40) << 8;
+    uint32_t v[32];
+#pragma unroll
+    for (int s = 0; s < 32; s++) {
+        const int li = s < (int)GL16_SLOTS ? (int)GL16_HDR + s : 0;
+        v[s] = s < (int)GL16_SLOTS && (uint32_t)s < lim ? L[li] ^ tx : NONE;
+    }
+    sort16(v);
+    sort16(v + 16);
+    merge16(v, v + 16);
+    const uint32_t base = L[0] + T.index_base;
+#pragma unroll
+    for (int j = 0; j < 16; j++) o[j] = (uint32_t)j < m ? base + (v[j] & 255u) : NONE;
+    return !ex;
+}
+
+__global__ __launch_bounds__(BLOCK) void rt_gl16_kernel(DevTable T, const uint8_t* __restrict__ targets, uint32_t q,
+                                                        uint32_t count, uint32_t* __restrict__ out_idx,
+                                                        uint8_t* __restrict__ out_cnt) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    const bool act = i < q;
+    Target t{};
+    uint32_t b = 0;
+    if (act) {
+        t = load_target(targets, i);
+        b = locate_bucket(T, t);
+    }
+    uint32_t o[16], m;
+    const bool ok = gl16_answer(T, t, b, count, act, o, m);
+    if (act && ok && out_cnt) out_cnt[i] = (uint8_t)m;
+    store_rows_block<16>(out_idx, q, count, o, act && ok);
+    __shared__ uint64_t xs[BLOCK / 64][192];
+    exact_tail(T, t, act && !ok, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
+}
+
 // One general window line of bucket b into L (LDS, W dwords, slots from HDR): see the layout above.
-// NEED = 8 or 32 (the count the window radius is sized for), RMAX = 2 or 7.
+// NEED = 8, 16 or 32 (the count the window radius is sized for), RMAX = 2, 3 or 7.
 struct GlInfo {
     uint32_t R, S, cp, base, whole, G[8], Sr[8];
     bool defer;
@@ -2087,6 +2160,28 @@ __global__ __launch_bounds__(BLOCK) void gl_build_kernel(const uint64_t* key, co
     L[3] = 0;
     store_line<GL_STRIDE>(L, lines + (size_t)GL_STRIDE * b);
         }();
+    }
+}
+
+__global__ __launch_bounds__(BLOCK) void gl16_build_kernel(const uint64_t* key, const uint8_t* status, const uint2* dir,
+                                                           const uint32_t* gpre, const uint64_t* fkey,
+                                                           const uint32_t* ftail, uint32_t B, uint32_t* lines,
+                                                           LineSel sel) {
+    __shared__ uint32_t lds[BLOCK][GL16_STRIDE + 1];
+    for (uint32_t j_ = blockIdx.x * BLOCK + threadIdx.x;; j_ += gridDim.x * BLOCK) {
+        uint32_t b;
+        if (!sel.pick(j_, B, b)) return;
+        uint32_t* L = lds[threadIdx.x];
+        for (uint32_t k = 0; k < GL16_STRIDE; k++) L[k] = NONE;
+        GlInfo I;
+        gl_build_line<3, 16, GL16_SLOTS, GL16_HDR>(key, status, dir, gpre, fkey, ftail, B, b, L, I);
+        uint32_t h = 0;
+        for (int r = 0; r < 4; r++) h |= min(I.G[r], 63u) << (6 * r);
+        L[0] = I.base;
+        L[1] = h | ((I.whole & 15u) << 24) | (min(I.R, 3u) << 28) | (I.defer ? WL_DEFER : 0u);
+        L[2] = I.S | (I.Sr[0] << 5) | (I.Sr[1] << 10) | (I.Sr[2] << 15) | (I.cp << 20);
+        L[3] = 0;
+        store_line<GL16_STRIDE>(L, lines + (size_t)GL16_STRIDE * b);
     }
 }
 
@@ -4055,6 +4150,7 @@ struct kad_table {
     uint32_t* ncl32_mut = nullptr;
     uint32_t* gl_mut = nullptr;
     uint32_t* gl32_mut = nullptr;
+    uint32_t* gl16_mut = nullptr;
     uint32_t* sl_mut = nullptr;     // slot lines (TF_SL) and the bucket of every coarse slot
     uint32_t* slb = nullptr;
     uint8_t* gdirty = nullptr;      // B: general lines rebuilt by an incremental refresh (slot-line transcode)
@@ -4128,7 +4224,7 @@ int rebuild_good_prefix(kad_table* t, hipStream_t s, bool full = true) {
     else
         hipLaunchKernelGGL(bucket_good_dirty_kernel, dim3(grid_for(B)), dim3(BLOCK), 0, s, t->d.status, t->dir_mut, B,
                            t->scan_cnt, t->bdirty, (t->wl_mut || t->gl_mut) ? t->ld8 : nullptr,
-                           t->wl16_mut ? t->ld16 : nullptr, (t->wl32_mut || t->gl32_mut) ? t->ld32 : nullptr);
+                           (t->wl16_mut || t->gl16_mut) ? t->ld16 : nullptr, (t->wl32_mut || t->gl32_mut) ? t->ld32 : nullptr);
     hipLaunchKernelGGL(scan_tiles_kernel, dim3(tiles), dim3(BLOCK), 0, s, t->scan_cnt, m, t->scan_part, t->scan_sums);
     hipLaunchKernelGGL(scan_sums_kernel, dim3(1), dim3(BLOCK), 0, s, t->scan_sums, tiles);
     hipLaunchKernelGGL(scan_apply_kernel, dim3(grid_for(m)), dim3(BLOCK), 0, s, t->scan_part, t->scan_sums, m, t->gpre_mut);
@@ -4162,6 +4258,9 @@ int rebuild_good_prefix(kad_table* t, hipStream_t s, bool full = true) {
                            t->d.ftail, t->sl_mut);
         if (!full) hipLaunchKernelGGL(mark_sel_kernel, lgrid(B), dim3(BLOCK), 0, s, s8, B, t->gdirty, (uint8_t)0);
     }
+    if (t->gl16_mut)
+        hipLaunchKernelGGL(gl16_build_kernel, lgrid(B), dim3(BLOCK), 0, s, t->d.key, t->d.status, t->d.dir,
+                           t->d.gpre, t->d.fkey, t->d.ftail, B, t->gl16_mut, sel_for(t->ld16, 1));
     if (t->gl32_mut)
         hipLaunchKernelGGL(gl32_build_kernel, lgrid(B), dim3(BLOCK), 0, s, t->d.key, t->d.status, t->d.dir,
                            t->d.gpre, t->d.fkey, t->d.ftail, B, t->gl32_mut, sel_for(t->ld32, 2));
@@ -4242,26 +4341,30 @@ int setup_general_lines(kad_table* t) {
     DevTable& d = t->d;
     if (d.B == 0 || (d.flags & TF_WL) || !d.fkey) return KAD_OK;
     const uint32_t B = d.B;
-    uint32_t *lp = nullptr, *lp32 = nullptr, *cnt = nullptr;
+    uint32_t *lp = nullptr, *lp16 = nullptr, *lp32 = nullptr, *cnt = nullptr;
     int rc;
     std::vector<void*> fresh;
     uint64_t fb = 0;
     auto drop = [&]() { for (void* p : fresh) (void)hipFree(p); };
     if ((rc = dev_upload(&lp, nullptr, (size_t)GL_STRIDE * B, fresh, fb)) ||
+        (rc = dev_upload(&lp16, nullptr, (size_t)GL16_STRIDE * B, fresh, fb)) ||
         (rc = dev_upload(&lp32, nullptr, (size_t)GL32_STRIDE * B, fresh, fb)) ||
-        (rc = dev_upload(&cnt, nullptr, 2, fresh, fb))) {
+        (rc = dev_upload(&cnt, nullptr, 3, fresh, fb))) {
         drop();
         return KAD_OK;
     }
-    if (hipMemset(cnt, 0, 8) != hipSuccess) { drop(); return KAD_OK; }
+    if (hipMemset(cnt, 0, 12) != hipSuccess) { drop(); return KAD_OK; }
     hipLaunchKernelGGL(gl_build_kernel, dim3(grid_for(B)), dim3(BLOCK), 0, 0, d.key, d.status, d.dir, d.gpre, d.fkey,
                        d.ftail, B, lp, LineSel{});
+    hipLaunchKernelGGL(gl16_build_kernel, dim3(grid_for(B)), dim3(BLOCK), 0, 0, d.key, d.status, d.dir, d.gpre, d.fkey,
+                       d.ftail, B, lp16, LineSel{});
     hipLaunchKernelGGL(gl32_build_kernel, dim3(grid_for(B)), dim3(BLOCK), 0, 0, d.key, d.status, d.dir, d.gpre, d.fkey,
                        d.ftail, B, lp32, LineSel{});
     hipLaunchKernelGGL(count_deferred_kernel, dim3(grid_for(B)), dim3(BLOCK), 0, 0, lp, GL_STRIDE, 1u, B, cnt);
     hipLaunchKernelGGL(count_deferred_kernel, dim3(grid_for(B)), dim3(BLOCK), 0, 0, lp32, GL32_STRIDE, 3u, B, cnt + 1);
-    uint32_t nd[2] = {B, B};
-    if (hipGetLastError() != hipSuccess || hipMemcpy(nd, cnt, 8, hipMemcpyDeviceToHost) != hipSuccess) {
+    hipLaunchKernelGGL(count_deferred_kernel, dim3(grid_for(B)), dim3(BLOCK), 0, 0, lp16, GL16_STRIDE, 1u, B, cnt + 2);
+    uint32_t nd[3] = {B, B, B};
+    if (hipGetLastError() != hipSuccess || hipMemcpy(nd, cnt, 12, hipMemcpyDeviceToHost) != hipSuccess) {
         drop();
         return set_err(KAD_ERR_HIP, "general window-line build failed");
     }
@@ -4269,12 +4372,20 @@ int setup_general_lines(kad_table* t) {
     fresh.pop_back();
     fb -= 16;
     const bool keep8 = (uint64_t)nd[0] * 16 <= B, keep32 = (uint64_t)nd[1] * 16 <= B;
-    if (std::getenv("KAD_DEBUG")) std::fprintf(stderr, "general lines: B=%u deferred %u / %u\n", B, nd[0], nd[1]);
+    const bool keep16 = keep32 && (uint64_t)nd[2] * 16 <= B;  // counts 9..16 fall back to the 256-byte lines
+    if (std::getenv("KAD_DEBUG"))
+        std::fprintf(stderr, "general lines: B=%u deferred %u / %u / %u (8 / 32 / 16)\n", B, nd[0], nd[1], nd[2]);
     if (keep8) {
         t->owned.push_back(lp); t->bytes += (uint64_t)GL_STRIDE * 4 * B;
         t->gl_mut = lp; d.gl = reinterpret_cast<const uint4*>(lp); d.flags |= TF_GL;
     } else {
         (void)hipFree(lp);
+    }
+    if (keep16) {
+        t->owned.push_back(lp16); t->bytes += (uint64_t)GL16_STRIDE * 4 * B;
+        t->gl16_mut = lp16; d.gl16 = reinterpret_cast<const uint4*>(lp16); d.flags |= TF_GL16;
+    } else {
+        (void)hipFree(lp16);
     }
     if (keep32) {
         t->owned.push_back(lp32); t->bytes += (uint64_t)GL32_STRIDE * 4 * B;
@@ -4301,7 +4412,7 @@ int ensure_marks(kad_table* t) {
     int rc;
     if ((rc = alloc(&t->bdirty, t->d.B))) return rc;
     if ((t->wl_mut || t->gl_mut) && (rc = alloc(&t->ld8, t->d.B))) return rc;
-    if (t->wl16_mut && (rc = alloc(&t->ld16, t->d.B))) return rc;
+    if ((t->wl16_mut || t->gl16_mut) && (rc = alloc(&t->ld16, t->d.B))) return rc;
     if ((t->wl32_mut || t->gl32_mut) && (rc = alloc(&t->ld32, t->d.B))) return rc;
     if (t->ncl_mut && (rc = alloc(&t->ndirty, t->d.nslots))) return rc;
     uint8_t *l = reinterpret_cast<uint8_t*>(t->dlist), *c = reinterpret_cast<uint8_t*>(t->dctr);
@@ -4402,6 +4513,8 @@ int launch_rt(const kad_table* t, const uint8_t* targets, uint32_t q, uint32_t c
 #endif
     } else if (K == 8 && (d.flags & TF_GL) && !(ev && std::strcmp(ev, "lane") == 0)) {
         hipLaunchKernelGGL(rt_gl_kernel, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
+    } else if (K == 16 && (d.flags & TF_GL16) && !(ev && (std::strcmp(ev, "lane") == 0 || std::strcmp(ev, "gl32") == 0))) {
+        hipLaunchKernelGGL(rt_gl16_kernel, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
     } else if (K > 8 && (d.flags & TF_GL32) && !(ev && std::strcmp(ev, "lane") == 0)) {
         hipLaunchKernelGGL(rt_gl32_kernel, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
     } else {
@@ -4740,6 +4853,7 @@ int kad_table_get_info(const kad_table* t, kad_table_info* out) {
     out->index_base = t->d.index_base;
     out->flags = t->flags | ((t->d.flags & TF_WL) ? KAD_INFO_WINDOW_LINES : 0u) |
                  ((t->d.flags & TF_GL) ? KAD_INFO_GENERAL_LINES : 0u) | ((t->d.flags & TF_GL32) ? KAD_INFO_GENERAL_LINES32 : 0u) |
+                 ((t->d.flags & TF_GL16) ? KAD_INFO_GENERAL_LINES16 : 0u) |
                  ((t->d.flags & TF_WS) ? KAD_INFO_SHORT_LINES : 0u) |
                  ((t->d.flags & TF_NCL32) ? KAD_INFO_NODECACHE_LINES32 : 0u) |
                  ((t->d.flags & TF_SL) ? KAD_INFO_SLOT_LINES : 0u);
@@ -5521,6 +5635,7 @@ int kad_table_apply(kad_table* t, const uint32_t* ops, uint32_t n_ops, const uin
     if (reshape) {  // general lines are per bucket: re-created below for the new bucket count
         release(t, t->gl_mut); t->gl_mut = nullptr; d.gl = nullptr; d.flags &= ~TF_GL;
         release(t, t->gl32_mut); t->gl32_mut = nullptr; d.gl32 = nullptr; d.flags &= ~TF_GL32;
+        release(t, t->gl16_mut); t->gl16_mut = nullptr; d.gl16 = nullptr; d.flags &= ~TF_GL16;
         release(t, t->sl_mut); release(t, t->slb); release(t, t->gdirty);
         t->sl_mut = nullptr; t->slb = nullptr; t->gdirty = nullptr; d.sl = nullptr; d.slslots = 0; d.flags &= ~TF_SL;
     }
