@@ -4804,8 +4804,9 @@ int kad_table_create(kad_table** out, int device, uint32_t n_nodes, const uint8_
     }
     // NodeCache radix
     if ((flags & KAD_TABLE_SORTED) && n_nodes) {
-        uint32_t tb = 1;
-        while ((1u << tb) < n_nodes && tb < 23) tb++;
+        uint32_t tb = 1, tb_max = 23;
+        if (const char* e = std::getenv("KAD_NC_RADIX_BITS")) tb_max = (uint32_t)std::max(1, std::min(23, std::atoi(e)));
+        while ((1u << tb) < n_nodes && tb < tb_max) tb++;
         const Radix r = choose_radix(id_hi(ids), id_hi(ids + 20ull * (n_nodes - 1)), tb);
         std::vector<uint32_t> rdx = build_radix(r, n_nodes, ids, false);
         uint32_t* dn;
