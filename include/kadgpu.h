@@ -70,6 +70,7 @@ extern "C" {
                                          general window line per query (rt_gl_kernel) */
 #define KAD_INFO_GENERAL_LINES32 0x400u /* ... and counts 9..32 one 256-byte line (rt_gl32_kernel) */
 #define KAD_INFO_GENERAL_LINES16 0x4000u /* ... and counts 9..16 one 128-byte line (rt_gl16_kernel) */
+#define KAD_INFO_SLOT_LINES16 0x8000u /* ... read through a 128-byte copy indexed by the target's top bits (rt_sl16_kernel) */
 #define KAD_INFO_SLOT_LINES 0x2000u /* other bucket shapes: count <= 8 queries read one 64-byte line indexed by
                                        the target's top bits (rt_sl_kernel), the locate + 128-byte line only
                                        as fallback */

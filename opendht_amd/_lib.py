@@ -23,6 +23,7 @@ KAD_INFO_WINDOW_LINES = 0x100
 KAD_INFO_GENERAL_LINES = 0x200
 KAD_INFO_GENERAL_LINES32 = 0x400
 KAD_INFO_GENERAL_LINES16 = 0x4000
+KAD_INFO_SLOT_LINES16 = 0x8000
 KAD_INFO_SHORT_LINES = 0x800
 KAD_INFO_NODECACHE_LINES32 = 0x1000
 KAD_INFO_SLOT_LINES = 0x2000

@@ -100,6 +100,7 @@ struct DevTable {
     const uint4* ncl32; // NodeCache lines for counts 17..32 (TF_NCL32): 512 bytes per node radix slot
     const uint4* sl;    // slot lines, count <= 8 (TF_SL, with TF_GL): 64 bytes per coarse radix slot
     const uint4* gl16;  // general window lines, counts 9..16 (TF_GL16): 128 bytes per bucket
+    const uint4* sl16;  // slot lines, counts 9..16 (TF_SL16, with TF_SL): 128 bytes per coarse radix slot
     uint32_t slshift, slslots;
     uint64_t rbase, nbase;
     uint32_t rshift, rslots, nshift, nslots;
@@ -117,6 +118,7 @@ constexpr uint32_t TF_GL32 = 256u;   // general window lines for counts 9..32
 constexpr uint32_t TF_NCL32 = 1024u; // 512-byte NodeCache lines (counts 17..32) present
 constexpr uint32_t TF_SL = 2048u;    // slot lines (count <= 8, general tables: no locate load)
 constexpr uint32_t TF_GL16 = 4096u;  // general window lines for counts 9..16 (one 128-byte line)
+constexpr uint32_t TF_SL16 = 8192u;  // slot lines for counts 9..16 (copies of the gl16 lines by coarse radix slot)
 constexpr uint32_t TF_WS = 512u;     // short (64-byte) window lines for count <= 8 (uniform tables, with TF_WL)
 constexpr uint32_t WIDE = 0x80000000u;  // dir[].x flag: bucket holds > 32 nodes (masks invalid)
 constexpr uint32_t KEY_PAD = 32;        // key[] is padded so 16-node chunk loads never leave it
@@ -1983,20 +1985,10 @@ __global__ __launch_bounds__(BLOCK) void rt_gl32_kernel(DevTable T, const uint8_
 // ---------------------------------------------------------------------------------------
 constexpr uint32_t GL16_SLOTS = 28, GL16_HDR = 4, GL16_STRIDE = 32;
 
-__device__ __forceinline__ bool gl16_answer(const DevTable& T, const Target& t, uint32_t b, uint32_t count, bool act,
-                                            uint32_t (&o)[16], uint32_t& m) {
-    uint32_t L[GL16_STRIDE];
-    if (act) {
-        const uint4* lp = T.gl16 + (GL16_STRIDE / 4) * (size_t)b;
-#pragma unroll
-        for (int x = 0; x < (int)GL16_STRIDE / 4; x++) {
-            const uint4 u = lp[x];
-            L[4 * x] = u.x; L[4 * x + 1] = u.y; L[4 * x + 2] = u.z; L[4 * x + 3] = u.w;
-        }
-    } else {
-#pragma unroll
-        for (int x = 0; x < (int)GL16_STRIDE; x++) L[x] = NONE;
-    }
+// The count 9..16 answer from a loaded gl16 line (also the slot-indexed copies, TF_SL16): false when the query
+// must take the exact path (deferred line, the window's slots do not hold m nodes).
+__device__ __forceinline__ bool gl16_rank(const uint32_t (&L)[GL16_STRIDE], uint64_t thi, uint32_t count,
+                                          uint32_t index_base, uint32_t (&o)[16], uint32_t& m) {
     const uint32_t h = L[1], h2 = L[2], R = (h >> 28) & 3u, S = h2 & 31u;
     uint32_t Rc = 4, Gc = 0;
 #pragma unroll
@@ -2006,10 +1998,9 @@ __device__ __forceinline__ bool gl16_answer(const DevTable& T, const Target& t, 
     }
     m = min(count, Gc);
     const uint32_t lim = Rc >= R ? S : (h2 >> (5 + 5 * min(Rc, 2u))) & 31u;
-    bool ex = !act || (h & WL_DEFER) || Rc > R || lim < m;
-    if (act && b == 0) ex |= below_first(T, t);
+    const bool ex = (h & WL_DEFER) || Rc > R || lim < m;
     const uint32_t cp = (h2 >> 20) & 63u;
-    const uint32_t tx = (uint32_t)((t.hi << (cp & 63u)) >> 40) << 8;
+    const uint32_t tx = (uint32_t)((thi << (cp & 63u)) >> 40) << 8;
     uint32_t v[32];
 #pragma unroll
     for (int s = 0; s < 32; s++) {
@@ -2019,10 +2010,32 @@ __device__ __forceinline__ bool gl16_answer(const DevTable& T, const Target& t, 
     sort16(v);
     sort16(v + 16);
     merge16(v, v + 16);
-    const uint32_t base = L[0] + T.index_base;
+    const uint32_t base = L[0] + index_base;
 #pragma unroll
     for (int j = 0; j < 16; j++) o[j] = (uint32_t)j < m ? base + (v[j] & 255u) : NONE;
     return !ex;
+}
+
+__device__ __forceinline__ void load_line32(const uint4* lp, bool act, uint32_t (&L)[32]) {
+    if (act) {
+#pragma unroll
+        for (int x = 0; x < 8; x++) {
+            const uint4 u = lp[x];
+            L[4 * x] = u.x; L[4 * x + 1] = u.y; L[4 * x + 2] = u.z; L[4 * x + 3] = u.w;
+        }
+    } else {
+#pragma unroll
+        for (int x = 0; x < 32; x++) L[x] = NONE;
+    }
+}
+
+__device__ __forceinline__ bool gl16_answer(const DevTable& T, const Target& t, uint32_t b, uint32_t count, bool act,
+                                            uint32_t (&o)[16], uint32_t& m) {
+    uint32_t L[GL16_STRIDE];
+    load_line32(T.gl16 + (GL16_STRIDE / 4) * (size_t)b, act, L);
+    bool ok = gl16_rank(L, t.hi, count, T.index_base, o, m) && act;
+    if (act && b == 0) ok &= !below_first(T, t);
+    return ok;
 }
 
 __global__ __launch_bounds__(BLOCK) void rt_gl16_kernel(DevTable T, const uint8_t* __restrict__ targets, uint32_t q,
@@ -2038,6 +2051,93 @@ __global__ __launch_bounds__(BLOCK) void rt_gl16_kernel(DevTable T, const uint8_
     }
     uint32_t o[16], m;
     const bool ok = gl16_answer(T, t, b, count, act, o, m);
+    if (act && ok && out_cnt) out_cnt[i] = (uint8_t)m;
+    store_rows_block<16>(out_idx, q, count, o, act && ok);
+    __shared__ uint64_t xs[BLOCK / 64][192];
+    exact_tail(T, t, act && !ok, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
+}
+
+// ---------------------------------------------------------------------------------------
+// Slot lines for counts 9..16 (TF_SL16): the count <= 8 slot lines' indexing (coarse radix slot j of the target's
+// top bits, no locate load) for the gl16 lines. Line j (128 bytes) is a copy of gl16[b] when slot j lies inside one
+// bucket b (slb[j]), else a fallback line in the count <= 8 slot lines' form: dw0 = the bucket at the slot start
+// (NONE: locate), dw1 = NONE, dw2:dw3 = the top 64 bits of the one bucket first inside the slot, dw4 bit 0 = there
+// is one. A query whose copied line cannot answer takes the exact path (the copy IS the bucket's line); a
+// fallback query reads the named (or located) bucket's gl16 line. Results are the gl16 lines' in every case.
+// ---------------------------------------------------------------------------------------
+// Eight lanes per slot line: lane g copies 16-byte piece g (every slot, or those whose bucket is flagged).
+__global__ __launch_bounds__(BLOCK) void sl16_build_kernel(const uint32_t* __restrict__ gl16,
+                                                            const uint32_t* __restrict__ slb, uint32_t slslots,
+                                                            const uint8_t* __restrict__ gdirty,
+                                                            const uint32_t* __restrict__ rrdx, uint32_t rslots,
+                                                            uint32_t k, const uint64_t* __restrict__ fkey,
+                                                            const uint32_t* __restrict__ ftail, uint32_t* __restrict__ sl16) {
+    const uint32_t g = threadIdx.x & 7u;
+    for (uint32_t j = (blockIdx.x * BLOCK + threadIdx.x) >> 3; j < slslots; j += (gridDim.x * BLOCK) >> 3) {
+        const uint32_t b = slb[j];
+        if (gdirty && (b == NONE || !gdirty[b])) continue;
+        uint4* dst = reinterpret_cast<uint4*>(sl16 + (size_t)GL16_STRIDE * j);
+        if (b != NONE) {
+            dst[g] = reinterpret_cast<const uint4*>(gl16 + (size_t)GL16_STRIDE * b)[g];
+            continue;
+        }
+        if (g > 1) continue;
+        const uint32_t r0 = rrdx[j << k], r1 = rrdx[min((j + 1) << k, rslots)];
+        const uint32_t lo = r0 & RDX_MASK, hi = r1 & RDX_MASK;
+        const bool exact = (r0 & RDX_EXACT) != 0;
+        const uint32_t inner = hi - lo - (exact ? 1u : 0u);
+        uint32_t fb_b = (lo == 0 && !exact) ? NONE : (exact ? lo : lo - 1), split_hi = 0, split_lo = 0, has_split = 0;
+        if (fb_b != NONE && inner == 1) {
+            const uint32_t ii = exact ? lo + 1 : lo;
+            const uint32_t* ft = ftail + 3ull * ii;
+            if ((ft[0] | ft[1] | ft[2]) == 0) {
+                split_hi = (uint32_t)(fkey[ii] >> 32);
+                split_lo = (uint32_t)fkey[ii];
+                has_split = 1;
+            } else {
+                fb_b = NONE;
+            }
+        } else {
+            fb_b = NONE;
+        }
+        dst[g] = g == 0 ? make_uint4(fb_b, NONE, split_hi, split_lo) : make_uint4(has_split, 0u, 0u, 0u);
+    }
+}
+
+__global__ __launch_bounds__(BLOCK) void rt_sl16_kernel(DevTable T, const uint8_t* __restrict__ targets, uint32_t q,
+                                                        uint32_t count, uint32_t* __restrict__ out_idx,
+                                                        uint8_t* __restrict__ out_cnt) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    const bool act = i < q;
+    const uint64_t thi = act ? load_target_hi(targets, i) : 0ull;
+    const bool in = act && thi >= T.rbase && ((thi - T.rbase) >> T.slshift) < T.slslots;
+    uint32_t L[GL16_STRIDE];
+    load_line32(T.sl16 + (GL16_STRIDE / 4) * (size_t)(in ? (thi - T.rbase) >> T.slshift : 0ull), in, L);
+    const bool fbl = L[1] == NONE;
+    uint32_t o[16], m;
+    bool ok = gl16_rank(L, thi, count, T.index_base, o, m) && in && !fbl;
+    // fallback lines and targets outside the slot range: the named (or located) bucket's gl16 line; the rest of
+    // the misses (a copied line that cannot answer) go straight to the exact path
+    const bool miss = act && !ok;
+    Target t{};
+    if (miss) t = load_target(targets, i);
+    const bool need = miss && (!in || fbl);
+    if (__any(need)) {
+        uint32_t b = 0;
+        if (need) {
+            const uint32_t bh = L[0] == NONE ? NONE
+                                             : L[0] + ((L[4] & 1u) && thi >= (((uint64_t)L[2] << 32) | L[3]) ? 1u : 0u);
+            b = in && bh != NONE ? bh : locate_bucket(T, t);
+        }
+        uint32_t o2[16], m2;
+        const bool ok2 = gl16_answer(T, t, b, count, need, o2, m2) && need;
+        if (ok2) {
+#pragma unroll
+            for (int j = 0; j < 16; j++) o[j] = o2[j];
+            m = m2;
+            ok = true;
+        }
+    }
     if (act && ok && out_cnt) out_cnt[i] = (uint8_t)m;
     store_rows_block<16>(out_idx, q, count, o, act && ok);
     __shared__ uint64_t xs[BLOCK / 64][192];
@@ -4153,6 +4253,7 @@ struct kad_table {
     uint32_t* gl16_mut = nullptr;
     uint32_t* sl_mut = nullptr;     // slot lines (TF_SL) and the bucket of every coarse slot
     uint32_t* slb = nullptr;
+    uint32_t* sl16_mut = nullptr;   // slot lines for counts 9..16 (TF_SL16)
     uint8_t* gdirty = nullptr;      // B: general lines rebuilt by an incremental refresh (slot-line transcode)
     // host copies of the bucket directory, for the incremental mirror (kad_table_apply)
     std::vector<uint32_t> h_off;
@@ -4258,9 +4359,18 @@ int rebuild_good_prefix(kad_table* t, hipStream_t s, bool full = true) {
                            t->d.ftail, t->sl_mut);
         if (!full) hipLaunchKernelGGL(mark_sel_kernel, lgrid(B), dim3(BLOCK), 0, s, s8, B, t->gdirty, (uint8_t)0);
     }
-    if (t->gl16_mut)
+    if (t->gl16_mut) {
+        const LineSel s16 = sel_for(t->ld16, 1);
         hipLaunchKernelGGL(gl16_build_kernel, lgrid(B), dim3(BLOCK), 0, s, t->d.key, t->d.status, t->d.dir,
-                           t->d.gpre, t->d.fkey, t->d.ftail, B, t->gl16_mut, sel_for(t->ld16, 1));
+                           t->d.gpre, t->d.fkey, t->d.ftail, B, t->gl16_mut, s16);
+        if (t->sl16_mut) {  // their slot-indexed copies: all, or the flagged buckets'
+            if (!full) hipLaunchKernelGGL(mark_sel_kernel, lgrid(B), dim3(BLOCK), 0, s, s16, B, t->gdirty, (uint8_t)1);
+            hipLaunchKernelGGL(sl16_build_kernel, lgrid(8ull * t->d.slslots), dim3(BLOCK), 0, s, t->gl16_mut, t->slb,
+                               t->d.slslots, full ? nullptr : t->gdirty, t->d.rrdx, t->d.rslots,
+                               t->d.slshift - t->d.rshift, t->d.fkey, t->d.ftail, t->sl16_mut);
+            if (!full) hipLaunchKernelGGL(mark_sel_kernel, lgrid(B), dim3(BLOCK), 0, s, s16, B, t->gdirty, (uint8_t)0);
+        }
+    }
     if (t->gl32_mut)
         hipLaunchKernelGGL(gl32_build_kernel, lgrid(B), dim3(BLOCK), 0, s, t->d.key, t->d.status, t->d.dir,
                            t->d.gpre, t->d.fkey, t->d.ftail, B, t->gl32_mut, sel_for(t->ld32, 2));
@@ -4331,6 +4441,25 @@ int setup_slot_lines(kad_table* t) {
     d.slshift = d.rshift + k;
     d.slslots = slslots;
     d.flags |= TF_SL;
+    // counts 9..16: copies of the gl16 lines at the same slots (optional: without them, locate + gl16)
+    if (t->gl16_mut) {
+        std::vector<void*> f16;
+        uint64_t b16 = 0;
+        uint32_t* l16 = nullptr;
+        if (dev_upload(&l16, nullptr, (size_t)GL16_STRIDE * slslots, f16, b16) == KAD_OK) {
+            hipLaunchKernelGGL(sl16_build_kernel, dim3(grid_for(8ull * slslots)), dim3(BLOCK), 0, 0, t->gl16_mut, slb,
+                               slslots, nullptr, d.rrdx, d.rslots, k, d.fkey, d.ftail, l16);
+            if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+                for (void* p : f16) (void)hipFree(p);
+                return set_err(KAD_ERR_HIP, "slot-line (16) build failed");
+            }
+            t->owned.insert(t->owned.end(), f16.begin(), f16.end());
+            t->bytes += b16;
+            t->sl16_mut = l16;
+            d.sl16 = reinterpret_cast<const uint4*>(l16);
+            d.flags |= TF_SL16;
+        }
+    }
     return KAD_OK;
 }
 
@@ -4513,6 +4642,9 @@ int launch_rt(const kad_table* t, const uint8_t* targets, uint32_t q, uint32_t c
 #endif
     } else if (K == 8 && (d.flags & TF_GL) && !(ev && std::strcmp(ev, "lane") == 0)) {
         hipLaunchKernelGGL(rt_gl_kernel, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
+    } else if (K == 16 && (d.flags & TF_SL16) && !(ev && (std::strcmp(ev, "lane") == 0 || std::strcmp(ev, "gl32") == 0 ||
+                                                          std::strcmp(ev, "gl") == 0))) {
+        hipLaunchKernelGGL(rt_sl16_kernel, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
     } else if (K == 16 && (d.flags & TF_GL16) && !(ev && (std::strcmp(ev, "lane") == 0 || std::strcmp(ev, "gl32") == 0))) {
         hipLaunchKernelGGL(rt_gl16_kernel, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
     } else if (K > 8 && (d.flags & TF_GL32) && !(ev && std::strcmp(ev, "lane") == 0)) {
@@ -4855,6 +4987,7 @@ int kad_table_get_info(const kad_table* t, kad_table_info* out) {
     out->flags = t->flags | ((t->d.flags & TF_WL) ? KAD_INFO_WINDOW_LINES : 0u) |
                  ((t->d.flags & TF_GL) ? KAD_INFO_GENERAL_LINES : 0u) | ((t->d.flags & TF_GL32) ? KAD_INFO_GENERAL_LINES32 : 0u) |
                  ((t->d.flags & TF_GL16) ? KAD_INFO_GENERAL_LINES16 : 0u) |
+                 ((t->d.flags & TF_SL16) ? KAD_INFO_SLOT_LINES16 : 0u) |
                  ((t->d.flags & TF_WS) ? KAD_INFO_SHORT_LINES : 0u) |
                  ((t->d.flags & TF_NCL32) ? KAD_INFO_NODECACHE_LINES32 : 0u) |
                  ((t->d.flags & TF_SL) ? KAD_INFO_SLOT_LINES : 0u);
@@ -5639,6 +5772,7 @@ int kad_table_apply(kad_table* t, const uint32_t* ops, uint32_t n_ops, const uin
         release(t, t->gl16_mut); t->gl16_mut = nullptr; d.gl16 = nullptr; d.flags &= ~TF_GL16;
         release(t, t->sl_mut); release(t, t->slb); release(t, t->gdirty);
         t->sl_mut = nullptr; t->slb = nullptr; t->gdirty = nullptr; d.sl = nullptr; d.slslots = 0; d.flags &= ~TF_SL;
+        release(t, t->sl16_mut); t->sl16_mut = nullptr; d.sl16 = nullptr; d.flags &= ~TF_SL16;
     }
     release(t, const_cast<uint32_t*>(d.dmask));
     d.dmask = ddm;

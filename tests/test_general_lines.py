@@ -14,7 +14,7 @@ import tables as TB
 from opendht_amd import DeviceTable
 from opendht_amd import synth as S
 from opendht_amd._lib import (KAD_INFO_GENERAL_LINES, KAD_INFO_GENERAL_LINES16, KAD_INFO_GENERAL_LINES32,
-                              KAD_INFO_SLOT_LINES, KAD_INFO_WINDOW_LINES, KAD_OP_SPLIT)
+                              KAD_INFO_SLOT_LINES, KAD_INFO_SLOT_LINES16, KAD_INFO_WINDOW_LINES, KAD_OP_SPLIT)
 
 pytestmark = pytest.mark.gpu
 
@@ -24,7 +24,8 @@ ALL = tuple(range(1, 33))
 def _check(T, t, targets, gpu, counts=ALL, status=None, mp=None):
     """Every count against the oracle; with `mp` (monkeypatch) the count <= 8 queries also through the
     128-byte general lines alone (KAD_RT_KERNEL=gl), so the slot lines and their fallback are compared, and
-    counts 9..16 through the 256-byte lines (KAD_RT_KERNEL=gl32) as well as the 128-byte count-16 lines."""
+    counts 9..16 through the 128-byte gl16 lines without their slot-indexed copies (KAD_RT_KERNEL=gl) and through
+    the 256-byte lines (KAD_RT_KERNEL=gl32) as well as the default slot lines."""
     st = t["status"] if status is None else status
     tg = torch.from_numpy(np.ascontiguousarray(targets)).to(gpu)
     for k in counts:
@@ -39,11 +40,12 @@ def _check(T, t, targets, gpu, counts=ALL, status=None, mp=None):
             mp.delenv("KAD_RT_KERNEL")
             np.testing.assert_array_equal(idx2.cpu().numpy().view(np.uint32), want, err_msg=f"{t['name']} k={k} gl")
         if mp is not None and 8 < k <= 16:
-            mp.setenv("KAD_RT_KERNEL", "gl32")
-            idx2, cnt2 = T.rt_closest(tg, k)
-            mp.delenv("KAD_RT_KERNEL")
-            np.testing.assert_array_equal(idx2.cpu().numpy().view(np.uint32), want, err_msg=f"{t['name']} k={k} gl32")
-            np.testing.assert_array_equal(cnt2.cpu().numpy(), wcnt, err_msg=f"{t['name']} k={k} gl32 counts")
+            for env in ("gl", "gl32"):  # the gl16 lines without their slot-indexed copies; the 256-byte lines
+                mp.setenv("KAD_RT_KERNEL", env)
+                idx2, cnt2 = T.rt_closest(tg, k)
+                mp.delenv("KAD_RT_KERNEL")
+                np.testing.assert_array_equal(idx2.cpu().numpy().view(np.uint32), want, err_msg=f"{t['name']} k={k} {env}")
+                np.testing.assert_array_equal(cnt2.cpu().numpy(), wcnt, err_msg=f"{t['name']} k={k} {env} counts")
 
 
 def _s_tables():
@@ -73,7 +75,7 @@ def test_general_lines_parity(gpu, t, monkeypatch):
         assert not (f & KAD_INFO_WINDOW_LINES)
         if not t.get("lane"):
             assert f & KAD_INFO_GENERAL_LINES and f & KAD_INFO_GENERAL_LINES32 and f & KAD_INFO_SLOT_LINES, hex(f)
-            assert f & KAD_INFO_GENERAL_LINES16, hex(f)
+            assert f & KAD_INFO_GENERAL_LINES16 and f & KAD_INFO_SLOT_LINES16, hex(f)
         _check(T, t, TB.adversarial_targets(t, extra=4000), gpu, mp=monkeypatch)
 
 
@@ -101,6 +103,6 @@ def test_uniform_table_switches_to_general_lines_after_split(gpu):
         ids, st, first, off = T.export()
         f = T.info()["flags"]
         assert not (f & KAD_INFO_WINDOW_LINES) and f & KAD_INFO_GENERAL_LINES and f & KAD_INFO_SLOT_LINES, hex(f)
-        assert f & KAD_INFO_GENERAL_LINES16, hex(f)
+        assert f & KAD_INFO_GENERAL_LINES16 and f & KAD_INFO_SLOT_LINES16, hex(f)
         t2 = TB.table(ids, st, first, off, name="U11_split")
         _check(T, t2, TB.adversarial_targets(t2, extra=3000), gpu, counts=(1, 7, 8, 9, 16, 17, 32))

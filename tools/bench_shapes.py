@@ -69,13 +69,14 @@ for n in [int(x) for x in sys.argv[1:]] or [1_000_000, 12_500_000]:
         os.environ.pop("KAD_RT_KERNEL")
         torch.cuda.synchronize()
         res[f"S{n}_k{k}_equal"] = bool(torch.equal(a, c))
-        if k in (14, 16):  # the 256-byte count 9..32 lines these counts read before the 128-byte gl16 lines
-            os.environ["KAD_RT_KERNEL"] = "gl32"
-            res[f"S{n}_k{k}_gl32_us"] = round(timeit(T, k), 1)
-            c = T.rt_closest(tgs[0], k)[0].clone()
-            os.environ.pop("KAD_RT_KERNEL")
-            torch.cuda.synchronize()
-            res[f"S{n}_k{k}_gl32_equal"] = bool(torch.equal(a, c))
+        if k in (14, 16):  # the gl16 lines without their slot copies (gl), the 256-byte count 9..32 lines (gl32)
+            for env in ("gl", "gl32"):
+                os.environ["KAD_RT_KERNEL"] = env
+                res[f"S{n}_k{k}_{env}_only_us"] = round(timeit(T, k), 1)
+                c = T.rt_closest(tgs[0], k)[0].clone()
+                os.environ.pop("KAD_RT_KERNEL")
+                torch.cuda.synchronize()
+                res[f"S{n}_k{k}_{env}_only_equal"] = bool(torch.equal(a, c))
     T.close()
     sid, _ = S.sort_ids(ids)
     d = max(1, int(round(np.log2(n / 8))))
