@@ -3281,8 +3281,9 @@ __global__ __launch_bounds__(BLOCK) void nc_two_pass_kernel(DevTable T, const ui
 // ---------------------------------------------------------------------------------------
 constexpr uint32_t NCL_SLOTS = 60, NCL_LEFT = 28, NCL_XMAX = 15, NCL_STRIDE = 64;  // dwords
 
+// The answer's node indices go to lrow[0..m) (the lane's LDS row) by emission rank.
 __device__ __forceinline__ bool ncl_answer(const uint4* ncl, uint32_t index_base, const Target& t, uint32_t s,
-                                           uint32_t count, uint32_t (&o)[16], uint32_t& m) {
+                                           uint32_t count, uint32_t* lrow, uint32_t& m) {
     const uint4* lp = ncl + (NCL_STRIDE / 4) * (size_t)s;
     uint32_t v[64];
     const uint4 hd = lp[0];
@@ -3293,17 +3294,18 @@ __device__ __forceinline__ bool ncl_answer(const uint4* ncl, uint32_t index_base
     }
     v[60] = v[61] = v[62] = v[63] = NONE;
     const uint32_t w0 = hd.x, ns = hd.y & 255u, sh = (hd.y >> 8) & 63u, fl = hd.z;
-    const uint32_t t24 = (uint32_t)(t.hi >> sh) & 0xFFFFFFu;
+    const uint32_t tx = ((uint32_t)(t.hi >> sh) & 0xFFFFFFu) << 8;
     bool ex = fl & 1u;
     uint32_t x = 0;  // lb = r0 + x: the slot's nodes below the target
 #pragma unroll
     for (int j = 0; j < (int)NCL_SLOTS; j++) {
-        const uint32_t k24 = v[j] >> 8;
+        // a slot word is key24 << 8 | expired (bits 1..7 zero): key24 < t24 iff word < t24 << 8, and the XOR
+        // with t24 << 8 is the distance inside the window's 24 bits | expired
         if (j >= (int)NCL_LEFT && j < (int)(NCL_LEFT + NCL_XMAX) && (uint32_t)j - NCL_LEFT < ns) {
-            ex |= k24 == t24;
-            x += k24 < t24 ? 1u : 0u;
+            ex |= (v[j] ^ tx) < 256u;
+            x += v[j] < tx ? 1u : 0u;
         }
-        v[j] = ((k24 ^ t24) << 8) | (v[j] & 1u);  // XOR distance inside the window's 24 bits | expired
+        v[j] ^= tx;
     }
     // shift the window by x: lb at slot 28, the left run 27..0, the right run 28..59-x
     {
@@ -3351,31 +3353,50 @@ __device__ __forceinline__ bool ncl_answer(const uint4* ncl, uint32_t index_base
 #pragma unroll
         for (int r = 0; r < 32; r++)
             if ((r & h) == 0) cx(w[r], w[r + h]);
-    // emit the non-expired steps up to lim: the c-th emission lies at step c..c+7
-    uint32_t have = 0, rank[32];
-    bool keep[32];
+    // emit the non-expired steps up to lim in walk order into the lane's LDS row (one pass, no rank arrays)
+    const uint32_t base = w0 + x + index_base;
+    uint32_t have = 0;
 #pragma unroll
     for (int r = 0; r < 32; r++) {
-        keep[r] = w[r] <= lim && !(w[r] & 1u);
-        rank[r] = have;
-        have += keep[r];
+        const bool keep = w[r] <= lim && !(w[r] & 1u);
+        if (keep && have < count) {
+            const uint32_t st = (w[r] >> 1) & 63u;
+            lrow[have] = base + ((w[r] & 128u) ? NCL_LEFT + st : NCL_LEFT - 1 - st);
+        }
+        have += keep ? 1u : 0u;
     }
     m = min(count, have);
     ex |= have < count && (lim != NONE || w[31] != NONE);  // the walk goes on past the window / step 32
-    const uint32_t base = w0 + x + index_base;
-#pragma unroll
-    for (int c = 0; c < 16; c++) {
-        uint32_t oc = NONE;
-#pragma unroll
-        for (int r = c; r < c + 8 && r < 32; r++) {
-            const uint32_t st = (w[r] >> 1) & 63u;
-            const uint32_t j = (w[r] & 128u) ? NCL_LEFT + st : NCL_LEFT - 1 - st;
-            oc = keep[r] && rank[r] == (uint32_t)c ? base + j : oc;
-        }
-        ex |= (uint32_t)c < m && oc == NONE;  // more than 7 skipped steps before emission c
-        o[c] = (uint32_t)c < m ? oc : NONE;
-    }
     return !ex;
+}
+
+// The block's rows of count <= 16 from LDS (rows[tid * 16 + c], the first m[tid] valid, the rest NONE) as one run of
+// 16-byte stores; rows whose lane did not answer (ok false) are skipped dword by dword.
+__device__ __forceinline__ void store_rows_lds16(uint32_t* __restrict__ out_idx, uint32_t q, uint32_t count,
+                                                 const uint32_t* rows, const uint8_t* mrow, const uint32_t* okm) {
+    const uint32_t tid = threadIdx.x, q0 = blockIdx.x * BLOCK;
+    const uint32_t nq = min((uint32_t)BLOCK, q - q0), nw = nq * count;
+    uint32_t* dst = out_idx + (size_t)q0 * count;
+    const bool al = ((uintptr_t)out_idx & 15u) == 0;  // BLOCK * count * 4 is a multiple of 16
+    for (uint32_t c4 = tid; 4 * c4 < nw; c4 += BLOCK) {
+        const uint32_t w0 = 4 * c4;
+        uint32_t r = w0 / count, c = w0 - r * count, v[4];
+        bool okv[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const bool in = w0 + u < nw;
+            okv[u] = in && ((okm[r >> 5] >> (r & 31)) & 1u);
+            v[u] = in && c < mrow[r] ? rows[r * 16 + c] : NONE;
+            if (++c == count) { c = 0; r++; }
+        }
+        if (al && okv[0] && okv[1] && okv[2] && okv[3]) {
+            reinterpret_cast<uint4*>(dst)[c4] = make_uint4(v[0], v[1], v[2], v[3]);
+        } else {
+#pragma unroll
+            for (int u = 0; u < 4; u++)
+                if (okv[u]) dst[w0 + u] = v[u];
+        }
+    }
 }
 
 // ABL 1 (timing ablation only, KAD_NC_KERNEL=lines_abl1; results wrong): no exact path.
@@ -3386,34 +3407,37 @@ __global__ __launch_bounds__(BLOCK) void nc_line_kernel(DevTable T4, DevTable T6
                                                         const uint8_t* __restrict__ targets, uint32_t q,
                                                         uint32_t count, uint32_t* __restrict__ out_idx,
                                                         uint8_t* __restrict__ out_cnt) {
-    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x, lane = threadIdx.x & 63u;
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x, lane = threadIdx.x & 63u, tid = threadIdx.x;
     const bool act = i < q;
     const bool fam = DUAL && act && af[i] != 0;
+    __shared__ uint32_t rows[BLOCK * 16];
+    __shared__ uint8_t mrow[BLOCK];
+    __shared__ uint32_t okm[BLOCK / 32];
+    if (tid < BLOCK / 32) okm[tid] = 0;
     Target t{};
     bool ok = false;
+    uint32_t m = 0;
     if (act) {
         t = load_target(targets, i);
         // this lane's family: only the fields the line path reads
         const uint64_t nbase = fam ? T6.nbase : T4.nbase;
         const uint32_t nshift = fam ? T6.nshift : T4.nshift, nslots = fam ? T6.nslots : T4.nslots;
         const uint32_t n = fam ? T6.n : T4.n, flags = fam ? T6.flags : T4.flags;
-        uint32_t* row = out_idx + (size_t)i * count;
         if (n == 0) {  // empty map: no nodes
-            for (uint32_t j = 0; j < count; j++) row[j] = NONE;
-            if (out_cnt) out_cnt[i] = 0;
             ok = true;
         } else if (flags & TF_NCL) {
             // below the first slot / past the last: lb = 0 / n, windows clamped at the ends (exact path)
             const bool inside = t.hi >= nbase && ((t.hi - nbase) >> nshift) < nslots;
-            uint32_t o[16], m;
-            if (inside && ncl_answer(fam ? T6.ncl : T4.ncl, fam ? T6.index_base : T4.index_base, t,
-                                     (uint32_t)((t.hi - nbase) >> nshift), count, o, m)) {
-                ok = true;
-                store_row16(row, o, count);
-                if (out_cnt) out_cnt[i] = (uint8_t)m;
-            }
+            ok = inside && ncl_answer(fam ? T6.ncl : T4.ncl, fam ? T6.index_base : T4.index_base, t,
+                                      (uint32_t)((t.hi - nbase) >> nshift), count, rows + 16 * tid, m);
         }
+        if (ok && out_cnt) out_cnt[i] = (uint8_t)m;
     }
+    mrow[tid] = (uint8_t)m;
+    __syncthreads();
+    if (ok) atomicOr(&okm[tid >> 5], 1u << (tid & 31));
+    __syncthreads();
+    store_rows_lds16(out_idx, q, count, rows, mrow, okm);
     // the lanes the lines could not answer: one query at a time by the whole wave (nc_answer: 32-node
     // runs each side of lb, itself falling back to lane 0's serial walk)
     uint64_t pend = ABL ? 0ull : __ballot(act && !ok);
