@@ -338,6 +338,7 @@ def main_owner(args):
         extras["cold"] = cold_pass(T, tgs, outs, ocnt, cnt_k, Q, moved_q, dev, stream)
         extras["refresh"] = refresh_pass(T, sh, tgs, outs, ocnt, cnt_k, Q, avg_kernel_s, dev, stream)
         extras["host_buffers"] = host_pass(T, tgs, cnt_k, Q, dev)
+        extras["other_counts"] = counts_pass(T, tgs, Q, dev, stream)
     cpu = fast = None
     if rank == 0 and world == 1 and not args.no_cpu:
         host_t = tgs[0][:1 << 17].cpu().numpy()
@@ -432,6 +433,32 @@ def cold_pass(T, tgs, outs, ocnt, cnt_k, Q, moved_q, dev, stream, reps=8):
     return {"kernel_ms": t * 1e3, "queries_per_s": Q / t, "achieved_GBs": moved_q * Q / t / 1e9,
             "frac": moved_q * Q / t / 1e9 / HBM_PEAK_GBS,
             "how": f"median of {reps} launches, each after a 1 GiB read that empties the 256 MiB Infinity Cache"}
+
+
+def counts_pass(T, tgs, Q, dev, stream, reps=16):
+    """The shard table's other call sites at the same batch size (kernel time per launch over rotated batches,
+    K launches between two events): findClosestNodes(id, now, SEARCH_NODES = 14) (dht.cpp:3354), count 16 and 32
+    (BASELINE config 4's sweep), and NodeCache::getCachedNodes(id, af, 14) (dht.cpp:1650) and 32."""
+    import torch
+
+    res = {}
+    for name, fn, k in (("rt_k14", T.rt_closest, 14), ("rt_k16", T.rt_closest, 16), ("rt_k32", T.rt_closest, 32),
+                        ("nc_k14", T.nc_closest, 14), ("nc_k32", T.nc_closest, 32)):
+        out = [torch.empty((Q, k), dtype=torch.int32, device=dev) for _ in range(2)]
+        cnt = [torch.empty((Q,), dtype=torch.uint8, device=dev) for _ in range(2)]
+        for j in range(2):
+            fn(tgs[j], k, out[j], cnt[j], stream=stream.cuda_stream)
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        for j in range(reps):
+            fn(tgs[j % len(tgs)], k, out[j % 2], cnt[j % 2], stream=stream.cuda_stream)
+        b.record(stream)
+        torch.cuda.synchronize(dev)
+        us = a.elapsed_time(b) / reps * 1e3
+        res[name] = {"us_per_launch": us, "queries_per_s": Q / (us * 1e-6)}
+    res["how"] = (f"{reps} launches of {Q} queries over rotated target batches between two HIP events (eager launches), "
+                  "the bench shard's own line sets; rt = RoutingTable::findClosestNodes, nc = NodeCache::getCachedNodes")
+    return res
 
 
 def host_pass(T, tgs, cnt_k, Q, dev, nb=8):

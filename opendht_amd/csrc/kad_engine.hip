@@ -3281,15 +3281,15 @@ __global__ __launch_bounds__(BLOCK) void nc_two_pass_kernel(DevTable T, const ui
 // ---------------------------------------------------------------------------------------
 constexpr uint32_t NCL_SLOTS = 60, NCL_LEFT = 28, NCL_XMAX = 15, NCL_STRIDE = 64;  // dwords
 
-// The answer's node indices go to lrow[0..m) (the lane's LDS row) by emission rank.
-__device__ __forceinline__ bool ncl_answer(const uint4* ncl, uint32_t index_base, const Target& t, uint32_t s,
+// The answer from the lane's line (Lq: its 16 pieces, loaded by the wave): the node indices go to lrow[0..m) (the
+// lane's LDS row) by emission rank.
+__device__ __forceinline__ bool ncl_answer(const uint4 (&Lq)[16], uint32_t index_base, const Target& t,
                                            uint32_t count, uint32_t* lrow, uint32_t& m) {
-    const uint4* lp = ncl + (NCL_STRIDE / 4) * (size_t)s;
     uint32_t v[64];
-    const uint4 hd = lp[0];
+    const uint4 hd = Lq[0];
 #pragma unroll
     for (int x = 1; x < (int)NCL_STRIDE / 4; x++) {
-        const uint4 u = lp[x];
+        const uint4 u = Lq[x];
         v[4 * x - 4] = u.x; v[4 * x - 3] = u.y; v[4 * x - 2] = u.z; v[4 * x - 1] = u.w;
     }
     v[60] = v[61] = v[62] = v[63] = NONE;
@@ -3370,10 +3370,22 @@ __device__ __forceinline__ bool ncl_answer(const uint4* ncl, uint32_t index_base
     return !ex;
 }
 
-// The block's rows of count <= 16 from LDS (rows[tid * 16 + c], the first m[tid] valid, the rest NONE) as one run of
-// 16-byte stores; rows whose lane did not answer (ok false) are skipped dword by dword.
+// Wave-level LDS ordering (the rocPRIM wave barrier): the wave's LDS writes before it are seen by its reads after.
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Row r of the NodeCache line kernel's block inside its wave's staging region (64 x 9 uint4 = 2304 words per wave).
+__device__ __forceinline__ uint32_t ncl_wrow(uint32_t r) { return (r >> 6) * 2304u + (r & 63u) * 16u; }
+
+// The block's rows of count <= 16 from LDS (row r at rows[r * 16 + c], or rows[ncl_wrow(r) + c] with wrow; the first
+// m[r] valid, the rest NONE) as one run of 16-byte stores; rows whose lane did not answer (ok false) are skipped
+// dword by dword.
 __device__ __forceinline__ void store_rows_lds16(uint32_t* __restrict__ out_idx, uint32_t q, uint32_t count,
-                                                 const uint32_t* rows, const uint8_t* mrow, const uint32_t* okm) {
+                                                 const uint32_t* rows, const uint8_t* mrow, const uint32_t* okm,
+                                                 bool wrow = false) {
     const uint32_t tid = threadIdx.x, q0 = blockIdx.x * BLOCK;
     const uint32_t nq = min((uint32_t)BLOCK, q - q0), nw = nq * count;
     uint32_t* dst = out_idx + (size_t)q0 * count;
@@ -3386,7 +3398,7 @@ __device__ __forceinline__ void store_rows_lds16(uint32_t* __restrict__ out_idx,
         for (int u = 0; u < 4; u++) {
             const bool in = w0 + u < nw;
             okv[u] = in && ((okm[r >> 5] >> (r & 31)) & 1u);
-            v[u] = in && c < mrow[r] ? rows[r * 16 + c] : NONE;
+            v[u] = in && c < mrow[r] ? rows[(wrow ? ncl_wrow(r) : r * 16) + c] : NONE;
             if (++c == count) { c = 0; r++; }
         }
         if (al && okv[0] && okv[1] && okv[2] && okv[3]) {
@@ -3399,9 +3411,14 @@ __device__ __forceinline__ void store_rows_lds16(uint32_t* __restrict__ out_idx,
     }
 }
 
-// ABL 1 (timing ablation only, KAD_NC_KERNEL=lines_abl1; results wrong): no exact path.
+// ABL 1 (timing ablation only, KAD_NC_KERNEL=lines_abl1; results wrong): no exact path. ABL 2 (lines_abl2): the
+// line load and the row store only (every word of the line folded into one value), the memory floor.
 // DUAL: per-query family (af[i] = 0 -> T4, 1 -> T6; NodeCache::getCachedNodes picks cache_4 / cache_6 by
 // sa_family, node_cache.cpp:37); an empty family map (n = 0) gives zero results.
+// The lines are loaded by the wave, not by their lanes: a lane-private 256-byte line is 16 random 16-byte loads,
+// each instruction touching 64 lines (64 address translations), and a 2 GB line table is bound by those
+// translations (tools/nc_abl.py). The wave loads its 64 lines in two halves of 128 bytes, eight lanes per line
+// (one translation per line per instruction), and hands each lane its line through LDS.
 template <int ABL, bool DUAL>
 __global__ __launch_bounds__(BLOCK) void nc_line_kernel(DevTable T4, DevTable T6, const uint8_t* __restrict__ af,
                                                         const uint8_t* __restrict__ targets, uint32_t q,
@@ -3410,13 +3427,13 @@ __global__ __launch_bounds__(BLOCK) void nc_line_kernel(DevTable T4, DevTable T6
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x, lane = threadIdx.x & 63u, tid = threadIdx.x;
     const bool act = i < q;
     const bool fam = DUAL && act && af[i] != 0;
-    __shared__ uint32_t rows[BLOCK * 16];
+    __shared__ uint4 stg[BLOCK / 64][64][9];  // a wave's 64 line halves (8 pieces + 1 pad); afterwards the rows
     __shared__ uint8_t mrow[BLOCK];
     __shared__ uint32_t okm[BLOCK / 32];
     if (tid < BLOCK / 32) okm[tid] = 0;
     Target t{};
     bool ok = false;
-    uint32_t m = 0;
+    uint32_t m = 0, sl = NONE;  // this lane's line: radix slot | family << 31 (NONE: no line)
     if (act) {
         t = load_target(targets, i);
         // this lane's family: only the fields the line path reads
@@ -3427,17 +3444,54 @@ __global__ __launch_bounds__(BLOCK) void nc_line_kernel(DevTable T4, DevTable T6
             ok = true;
         } else if (flags & TF_NCL) {
             // below the first slot / past the last: lb = 0 / n, windows clamped at the ends (exact path)
-            const bool inside = t.hi >= nbase && ((t.hi - nbase) >> nshift) < nslots;
-            ok = inside && ncl_answer(fam ? T6.ncl : T4.ncl, fam ? T6.index_base : T4.index_base, t,
-                                      (uint32_t)((t.hi - nbase) >> nshift), count, rows + 16 * tid, m);
+            if (t.hi >= nbase && ((t.hi - nbase) >> nshift) < nslots)
+                sl = (uint32_t)((t.hi - nbase) >> nshift) | (fam ? 0x80000000u : 0u);
         }
-        if (ok && out_cnt) out_cnt[i] = (uint8_t)m;
     }
+    // round r: lane L loads pieces (L & 7) and 8 + (L & 7) of the line of query 8r + (L >> 3)
+    uint4 ld[16], L[16];
+#pragma unroll
+    for (int r = 0; r < 8; r++) {
+        const uint32_t so = (uint32_t)__shfl((int)sl, 8 * r + (int)(lane >> 3), 64);
+        uint4 a = make_uint4(0u, 0u, 0u, 0u), b = a;
+        if (so != NONE) {
+            const uint4* lp = ((DUAL && (so >> 31)) ? T6.ncl : T4.ncl) + (NCL_STRIDE / 4) * (size_t)(so & 0x7FFFFFFFu);
+            a = lp[lane & 7];
+            b = lp[8 + (lane & 7)];
+        }
+        ld[r] = a;
+        ld[8 + r] = b;
+    }
+    uint4 (*S)[9] = stg[tid >> 6];  // this wave's region: only wave-level ordering is needed
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+#pragma unroll
+        for (int r = 0; r < 8; r++) S[8 * r + (lane >> 3)][lane & 7] = ld[8 * h + r];
+        wave_sync();
+#pragma unroll
+        for (int x = 0; x < 8; x++) L[8 * h + x] = S[lane][x];
+        wave_sync();
+    }
+    // the wave's rows (64 x 16 words) reuse its region: row r of the block at rows + NCL_WROWS(r)
+    uint32_t* rows = reinterpret_cast<uint32_t*>(&stg[0][0][0]);
+    if (sl != NONE) {
+        if (ABL == 2) {
+            uint32_t f = 0;
+#pragma unroll
+            for (int x = 0; x < 16; x++) f ^= L[x].x + L[x].y + L[x].z + L[x].w;
+            for (uint32_t c = 0; c < count; c++) rows[ncl_wrow(tid) + c] = f + c;
+            m = count;
+            ok = true;
+        } else {
+            ok = ncl_answer(L, fam ? T6.index_base : T4.index_base, t, count, rows + ncl_wrow(tid), m);
+        }
+    }
+    if (act && ok && out_cnt) out_cnt[i] = (uint8_t)m;
     mrow[tid] = (uint8_t)m;
     __syncthreads();
     if (ok) atomicOr(&okm[tid >> 5], 1u << (tid & 31));
     __syncthreads();
-    store_rows_lds16(out_idx, q, count, rows, mrow, okm);
+    store_rows_lds16(out_idx, q, count, rows, mrow, okm, true);
     // the lanes the lines could not answer: one query at a time by the whole wave (nc_answer: 32-node
     // runs each side of lb, itself falling back to lane 0's serial walk)
     uint64_t pend = ABL ? 0ull : __ballot(act && !ok);
@@ -5324,6 +5378,9 @@ int kad_nc_closest_batch(const kad_table* t, const uint8_t* targets, uint32_t q,
 #ifdef KAD_ABLATIONS  // timing ablations with WRONG results: only in the tools build
     if ((t->d.flags & TF_NCL) && ev && std::strcmp(ev, "lines_abl1") == 0 && count >= 1 && count <= 16)
         hipLaunchKernelGGL((nc_line_kernel<1, false>), dim3(grid_for(q)), dim3(BLOCK), 0, (hipStream_t)stream, t->d,
+                           t->d, nullptr, targets, q, count, out_idx, out_cnt);
+    else if ((t->d.flags & TF_NCL) && ev && std::strcmp(ev, "lines_abl2") == 0 && count >= 1 && count <= 16)
+        hipLaunchKernelGGL((nc_line_kernel<2, false>), dim3(grid_for(q)), dim3(BLOCK), 0, (hipStream_t)stream, t->d,
                            t->d, nullptr, targets, q, count, out_idx, out_cnt);
     else if ((t->d.flags & TF_NCL32) && ev && std::strcmp(ev, "l32_abl1") == 0 && count > 16 && count <= 32)
         hipLaunchKernelGGL((nc32_line_kernel<1, false>), dim3(grid_for(8ull * q)), dim3(BLOCK), 0, (hipStream_t)stream,
