@@ -1322,6 +1322,9 @@ __device__ __forceinline__ void store_rows_block(uint32_t* __restrict__ out_idx,
     }
 }
 
+__device__ bool wave_wl32(const DevTable& T, const Target& t, uint32_t b, uint32_t count, uint32_t lane, uint32_t* row,
+                          uint8_t* cp);  // below, with the 32-count lines
+
 // ABL 1 = no exact path (timing ablation only, KAD_RT_KERNEL=wl16_abl1; deferred rows are left unwritten).
 template <int ABL>
 __global__ __launch_bounds__(BLOCK) void rt_wl16_kernel(DevTable T, const uint8_t* __restrict__ targets, uint32_t q,
@@ -1336,11 +1339,31 @@ __global__ __launch_bounds__(BLOCK) void rt_wl16_kernel(DevTable T, const uint8_
         b = locate_bucket(T, t);
     }
     uint32_t o[16], m;
-    const bool ok = wl16_answer(T, t, b, count, act, o, m);
+    bool ok = wl16_answer(T, t, b, count, act, o, m);
     if (act && ok && out_cnt) out_cnt[i] = (uint8_t)m;
     store_rows_block<16>(out_idx, q, count, o, act && ok);
+    if (ABL) return;
+    // the queries the 16-count line cannot answer (its 29 slots could not hold both the count 14 and the count 16
+    // D-rank prefixes, a deferred line): the 32-count line of the same bucket (58 slots) by the wave, one query at a
+    // time, then the exact path
+    bool need = act && !ok;
+    if (T.flags & TF_WL32) {
+        const uint32_t lane = threadIdx.x & 63u;
+        for (uint64_t pm = __ballot(need); pm; pm &= pm - 1) {
+            const uint32_t l = (uint32_t)__builtin_ctzll(pm);
+            Target u;
+            u.hi = rdl64(t.hi, l);
+            u.t2 = rdl(t.t2, l);
+            u.t3 = rdl(t.t3, l);
+            u.t4 = rdl(t.t4, l);
+            const uint32_t il = rdl(i, l);
+            if (wave_wl32(T, u, rdl(b, l), count, lane, out_idx + (size_t)il * count, out_cnt ? out_cnt + il : nullptr) &&
+                lane == l)
+                need = false;
+        }
+    }
     __shared__ uint64_t xs[BLOCK / 64][192];
-    if (ABL == 0) exact_tail(T, t, act && !ok, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
+    exact_tail(T, t, need, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
 }
 
 // Window lines for counts 9..16 after a status change (or at creation): one thread per bucket.
@@ -1383,9 +1406,10 @@ __global__ __launch_bounds__(BLOCK) void wl16_build_kernel(const uint64_t* key, 
         gj[j] = good_of(dir, gpre, x);
         rounds |= (x >= b ? x - b : b - 1 - x) << (2 * j);
     }
-    // Whole buckets, in three passes: (1) the D-rank prefix of W(R_16) up to its 16th good node (every count
-    // with R_c = R_16); (2) the rest of W(R_16 - 1), which holds < 16 good nodes (every count with R_c < R_16);
-    // (3) whatever else fits, in D order.
+    // Whole buckets, in four passes: (0) the D-rank prefix of W(R_14) up to its 14th good node (count 14 =
+    // SEARCH_NODES, dht.cpp:3354, the count the reference asks for); (1) the D-rank prefix of W(R_16) up to its
+    // 16th good node (every count with R_c = R_16); (2) the rest of W(R_16 - 1), which holds < 16 good nodes (every
+    // count with R_c < R_16); (3) whatever else fits, in D order.
     auto put = [&](uint32_t j) {
         if (((st >> j) & 1u) || S + gj[j] > WL16_SLOTS) return;
         st |= 1u << j;
@@ -1398,6 +1422,16 @@ __global__ __launch_bounds__(BLOCK) void wl16_build_kernel(const uint64_t* key, 
             S++;
         });
     };
+    uint32_t R14 = R;
+    for (int r = (int)R; r >= 0; r--) {
+        const uint32_t lo_r = b > (uint32_t)r ? b - 1 - r : 0u, hi_r = min(B - 1, b + r);
+        if (gpre[hi_r + 1] - gpre[lo_r] >= 14u || (lo_r == 0 && hi_r == B - 1)) R14 = (uint32_t)r;
+    }
+    for (uint32_t j = 0, cum = 0; j < nb && cum < 14u; j++)
+        if (((rounds >> (2 * j)) & 3u) <= R14) {
+            put(j);
+            cum += gj[j];
+        }
     for (uint32_t j = 0, cum = 0; j < nb && cum < WL16_P1; j++) {
         put(j);
         cum += gj[j];
@@ -1517,6 +1551,43 @@ __device__ __forceinline__ bool wl32_answer(const DevTable& T, const Target& t, 
 }
 
 // Row of up to 32 indices: 16-byte stores for counts divisible by 4, 8-byte stores for even counts.
+// One query of count <= 32 by the whole wave from its bucket's 32-count line (wave-uniform b and t): lane s holds slot
+// s (the rounds beyond R_c masked), one 64-lane bitonic sort, lanes < count write the row. False when the line cannot
+// answer (deferred, clamped target, R_c > R_32, fewer stored nodes than m): the caller takes the exact path.
+__device__ bool wave_wl32(const DevTable& T, const Target& t, uint32_t b, uint32_t count, uint32_t lane, uint32_t* row,
+                          uint8_t* cp) {
+    const uint32_t* L = reinterpret_cast<const uint32_t*>(T.wl32) + (size_t)WL32_STRIDE * b;
+    const uint32_t h = L[3], S = (h >> 12) & 127u, R = (h >> 8) & 15u;
+    uint32_t Rc = 8, Gc = 0;
+    for (int r = 7; r >= 0; r--) {
+        const uint32_t g = (L[1 + (r >> 2)] >> (8 * (r & 3))) & 255u;
+        if (g >= count || ((h >> r) & 1u)) { Rc = (uint32_t)r; Gc = g; }
+    }
+    const uint32_t m = min(count, Gc);
+    const bool own = (t.hi >> T.rshift) == (T.rbase >> T.rshift) + b;
+    if ((h & WL_DEFER) || !own || Rc > R) return false;
+    const uint32_t tx = (uint32_t)((t.hi << (64 - T.rshift)) >> (64 - WL32_KBITS)) << 8;
+    uint32_t v = NONE;
+    bool in = false;
+    if (lane < WL32_SLOTS && lane < S) {
+        const uint32_t w = L[WL32_HDR + lane], j = w >> 28;
+        const uint32_t rj = j < 10 ? (L[4] >> (3 * j)) & 7u : (L[5] >> (3 * (j - 10))) & 7u;
+        in = rj <= Rc;
+        v = in ? w ^ tx : NONE;
+    }
+    if ((uint32_t)__popcll(__ballot(in)) < m) return false;
+#pragma unroll
+    for (uint32_t k = 2; k <= 64; k <<= 1)
+#pragma unroll
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            const uint32_t o = (uint32_t)__shfl_xor((int)v, (int)j, 64);
+            v = (((lane & j) == 0) == ((lane & k) == 0)) ? min(v, o) : max(v, o);
+        }
+    if (lane < count) row[lane] = lane < m ? L[0] + T.index_base + (v & 255u) : NONE;
+    if (lane == 0 && cp) *cp = (uint8_t)m;
+    return true;
+}
+
 __device__ __forceinline__ void store_row32(uint32_t* row, const uint32_t (&o)[32], uint32_t count) {
     if ((count & 3u) == 0 && ((uintptr_t)row & 15u) == 0) {
 #pragma unroll
