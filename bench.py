@@ -225,7 +225,7 @@ def main_owner(args):
     from opendht_amd import DeviceTable
     from opendht_amd._lib import KAD_INFO_SHORT_LINES, KAD_INFO_WINDOW_LINES
     from opendht_amd.metrics import rt_algorithmic_bytes
-    from opendht_amd.sharded import ShardSpec, build_shard
+    from opendht_amd.sharded import build_shard, config3_spec
 
     world, rank, local = dist_env()
     if world != args.gpus:
@@ -236,7 +236,7 @@ def main_owner(args):
     dev = torch.device("cuda", local)
     dist = init_dist(world, dev)
 
-    spec = ShardSpec()  # 100M-node U(24), 8 shards, k_max 32
+    spec = config3_spec()  # SURVEY §8d's 100M-node U(24) table, 8 shards, k_max 32
     t0 = time.perf_counter()
     sh = build_shard(spec, rank)
     T = DeviceTable(sh.ids, sh.status, sh.first, sh.off, device=local, index_base=sh.index_base, sorted=True)
@@ -363,7 +363,8 @@ def main_owner(args):
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u64",
-            "data": "synthetic (counter-based uniform 160-bit IDs, 80/10/10 good/expired/dubious; uniform targets, "
+            "data": "synthetic (SURVEY.md §8d recipe: 100M mt19937_64 IDs, seed 0x0D470001, status 80/10/10 "
+                    "good/expired/dubious from seed 0x0D470003, U(24) buckets; uniform targets, "
                     f"{NB} distinct batches of {Q} per GPU, one per step)",
             "config": {
                 "workload": "config3: 100M-node U(24) routing table, 1/8 shard per GPU (2^21 owned buckets "
@@ -572,11 +573,11 @@ def allgather_pass(args, world, rank, local, dev, dist):
     import torch
 
     from opendht_amd.global_shard import GlobalShard, build_plain_shard, global_good_prefix
-    from opendht_amd.sharded import ShardSpec
+    from opendht_amd.sharded import config3_spec
 
     if world & (world - 1) or world > 8:
         return {"skipped": "world size must be a power of two <= 8"}
-    spec = ShardSpec(n_shards=world)  # the 100M-node U(24) table in `world` shards
+    spec = config3_spec(world)  # the 100M-node U(24) table in `world` shards
     t0 = time.perf_counter()
     ids, st, off, lo, hi, base, good = build_plain_shard(spec, rank)
     gp = global_good_prefix(good, device=dev if world > 1 else None)

@@ -373,6 +373,18 @@ int kad_synth_uniform_shard(uint64_t seed, uint32_t depth, uint64_t prefix_lo, u
                             double mean_per_bucket, uint32_t good_pct, uint32_t expired_pct,
                             uint32_t* out_n, uint8_t* out_ids, uint8_t* out_status,
                             uint32_t* out_offset);
+/* The SURVEY.md §8d recipe of a whole n-node table (kad_synth_ids(seed_ids, n) and
+ * kad_synth_status(seed_status, n, ...)) restricted to the U(depth) buckets
+ * [prefix_lo, prefix_hi): ids ascending, status, bucket offsets (+1), and in
+ * *out_below the number of the table's IDs below the range (global index of the
+ * range's first node). One sequential pass over the n draws; fails on a duplicate
+ * ID instead of redrawing it (probability < 1e-30 at n = 1e8). With out_ids ==
+ * NULL: counts only; out arrays hold cap nodes (more in the range: KAD_ERR_NOMEM,
+ * the count in *out_n). */
+int kad_synth_recipe_range(uint64_t seed_ids, uint64_t seed_status, uint64_t n, uint32_t depth,
+                           uint64_t prefix_lo, uint64_t prefix_hi, uint32_t good_pct,
+                           uint32_t expired_pct, uint64_t cap, uint32_t* out_n, uint64_t* out_below,
+                           uint8_t* out_ids, uint8_t* out_status, uint32_t* out_offset);
 
 #ifdef __cplusplus
 }

@@ -39,6 +39,8 @@ def part_words(count: int) -> int:
     """KAD_PART_WORDS: a row plus the entries' 160-bit XOR distances (5 words each)."""
     return row_words(count) + 5 * count
 
+KAD_ERR_NOMEM = -3
+
 ERRORS = {
     -1: "KAD_ERR_INVALID",
     -2: "KAD_ERR_HIP",
@@ -105,6 +107,8 @@ SIGNATURES = {
     "kad_split_table": (C.c_int, [C.c_uint32, _P, C.c_uint32, _P, _P, _P, _P]),
     "kad_synth_uniform_shard": (C.c_int, [C.c_uint64, C.c_uint32, C.c_uint64, C.c_uint64, C.c_double,
                                           C.c_uint32, C.c_uint32, _P, _P, _P, _P]),
+    "kad_synth_recipe_range": (C.c_int, [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint64, C.c_uint64,
+                                         C.c_uint32, C.c_uint32, C.c_uint64, _P, _P, _P, _P, _P]),
 }
 
 

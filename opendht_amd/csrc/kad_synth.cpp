@@ -8,6 +8,7 @@
 //   swarm counter-based U(d) shard: any bucket range reproducible alone   kad_synth_uniform_shard
 // IDs: std::mt19937_64 recipe of SURVEY.md §8d                            kad_synth_ids
 #include <algorithm>
+#include <atomic>
 #include <array>
 #include <cmath>
 #include <cstdint>
@@ -278,6 +279,74 @@ int kad_synth_uniform_shard(uint64_t seed, uint32_t depth, uint64_t prefix_lo, u
         }
     });
     return KAD_OK;
+}
+
+// SURVEY.md §8d recipe (kad_synth_ids + kad_synth_status over n nodes: ID i from draws 3i..3i+2 of mt19937_64(seed_ids),
+// status of node i from draw i of mt19937_64(seed_status)) restricted to the U(depth) buckets [prefix_lo, prefix_hi):
+// one sequential pass over the n draws, sorted by ID, with the bucket offsets and the number of IDs below the range
+// (the global index of the range's first node). kad_synth_ids rejects and redraws a duplicate ID; among 1e8 random
+// 160-bit IDs one has probability < 1e-30, so this pass fails (KAD_ERR_INVALID) on a duplicate instead. With
+// out_ids == NULL: counts only (*out_n, *out_below); more than cap nodes in the range: KAD_ERR_NOMEM with the
+// count in *out_n.
+int kad_synth_recipe_range(uint64_t seed_ids, uint64_t seed_status, uint64_t n, uint32_t depth, uint64_t prefix_lo,
+                           uint64_t prefix_hi, uint32_t good_pct, uint32_t expired_pct, uint64_t cap, uint32_t* out_n,
+                           uint64_t* out_below, uint8_t* out_ids, uint8_t* out_status, uint32_t* out_offset) {
+    if (depth == 0 || depth > 63 || !out_n || !out_below) return KAD_ERR_INVALID;
+    if (prefix_hi == 0) prefix_hi = 1ull << depth;
+    if (prefix_hi <= prefix_lo || prefix_hi > (1ull << depth) || prefix_hi - prefix_lo >= 0x7FFFFFFFull)
+        return KAD_ERR_INVALID;
+    const uint64_t B = prefix_hi - prefix_lo;
+    const uint32_t sh = 64 - depth;
+    struct Rec {
+        uint64_t hi, mid;
+        uint32_t lo;
+        uint8_t st;
+    };
+    std::vector<Rec> keep;
+    if (out_ids) keep.reserve(cap);
+    std::mt19937_64 g(seed_ids), h(seed_status);
+    uint64_t below = 0, kept = 0;
+    for (uint64_t i = 0; i < n; i++) {
+        const uint64_t d0 = g(), d1 = g(), d2 = g();
+        const uint32_t u = (uint32_t)(h() % 100);
+        const uint64_t p = d0 >> sh;
+        if (p < prefix_lo) { below++; continue; }
+        if (p >= prefix_hi) continue;
+        kept++;
+        if (out_ids && kept <= cap)
+            keep.push_back(Rec{d0, d1, (uint32_t)(d2 >> 32),
+                               (uint8_t)(u < good_pct ? KAD_STATUS_GOOD : (u < good_pct + expired_pct ? KAD_STATUS_EXPIRED : 0))});
+    }
+    if (kept >= 0x7FFFFFFFull) return KAD_ERR_INVALID;
+    *out_n = (uint32_t)kept;
+    *out_below = below;
+    if (!out_ids) return KAD_OK;
+    if (!out_status || !out_offset) return KAD_ERR_INVALID;
+    if (kept > cap) return KAD_ERR_NOMEM;  // *out_n holds the count: call again with cap >= it
+    // counting sort by bucket, then by ID inside each bucket
+    std::vector<uint32_t> pos(B + 1, 0);
+    for (const Rec& r : keep) pos[(r.hi >> sh) - prefix_lo + 1]++;
+    for (uint64_t j = 0; j < B; j++) pos[j + 1] += pos[j];
+    for (uint64_t j = 0; j <= B; j++) out_offset[j] = pos[j];
+    std::vector<uint32_t> order(keep.size());
+    for (uint32_t k = 0; k < (uint32_t)keep.size(); k++) order[pos[(keep[k].hi >> sh) - prefix_lo]++] = k;
+    std::atomic<bool> dup{false};
+    par_for(B, [&](uint64_t a, uint64_t e) {
+        for (uint64_t j = a; j < e; j++) {
+            auto lt = [&](uint32_t x, uint32_t y) {
+                const Rec &p = keep[x], &q = keep[y];
+                return p.hi != q.hi ? p.hi < q.hi : p.mid != q.mid ? p.mid < q.mid : p.lo < q.lo;
+            };
+            std::sort(order.begin() + out_offset[j], order.begin() + out_offset[j + 1], lt);
+            for (uint32_t k = out_offset[j]; k < out_offset[j + 1]; k++) {
+                const Rec& r = keep[order[k]];
+                write_draws(out_ids + 20ull * k, r.hi, r.mid, (uint64_t)r.lo << 32);
+                out_status[k] = r.st;
+                if (k > out_offset[j] && !lt(order[k - 1], order[k])) dup = true;
+            }
+        }
+    });
+    return dup ? KAD_ERR_INVALID : KAD_OK;
 }
 
 }  // extern "C"

@@ -205,5 +205,5 @@ def build_plain_shard(spec, s: int):
     """Shard s of spec's global U(depth) table without halo: (ids, status, off, lo, hi, index_base,
     good counts per bucket)."""
     lo, hi = spec.owned(s)
-    ids, st, off = spec.bucket_range(lo, hi)
-    return ids, st, off.astype(np.uint32), lo, hi, spec.nodes_below(lo), good_counts(st, off)
+    ids, st, off, below = spec.bucket_range_below(lo, hi)
+    return ids, st, off.astype(np.uint32), lo, hi, below, good_counts(st, off)

@@ -32,6 +32,10 @@ SEED_SWARM = 0x0D470100
 
 @dataclass
 class ShardSpec:
+    """A global U(depth) table cut into n_shards ID ranges. recipe_n > 0: the table is SURVEY.md §8d's recipe of
+    recipe_n nodes (std::mt19937_64 IDs and status, synth.recipe_range: any shard regenerated from the seeds alone,
+    in one pass over all recipe_n draws); recipe_n = 0: counter-based Poisson(mean_per_bucket) buckets (any bucket
+    range generated on its own; the small multi-shard tests)."""
     n_shards: int = 8
     depth: int = 24
     mean_per_bucket: float = 100e6 / 2**24
@@ -39,6 +43,7 @@ class ShardSpec:
     good_pct: int = 80
     expired_pct: int = 10
     k_max: int = 32
+    recipe_n: int = 0
 
     @property
     def shard_bits(self) -> int:
@@ -61,13 +66,30 @@ class ShardSpec:
 
     def bucket_range(self, lo: int, hi: int):
         """(ids sorted, status, offsets) of global buckets [lo, hi)."""
-        return S.uniform_shard(self.seed, self.depth, lo, hi, self.mean_per_bucket, self.good_pct,
-                               self.expired_pct)
+        return self.bucket_range_below(lo, hi)[:3]
+
+    def bucket_range_below(self, lo: int, hi: int):
+        """(ids sorted, status, offsets, global index of the range's first node) of global buckets [lo, hi)."""
+        if self.recipe_n:
+            return S.recipe_range(self.recipe_n, self.depth, lo, hi, self.good_pct, self.expired_pct)
+        ids, st, off = S.uniform_shard(self.seed, self.depth, lo, hi, self.mean_per_bucket, self.good_pct,
+                                       self.expired_pct)
+        return ids, st, off, self.nodes_below(lo)
 
     def nodes_below(self, b: int) -> int:
         """Global index of the first node of bucket b."""
         if b <= 0:
             return 0
+        if self.recipe_n:
+            import ctypes as C
+
+            from ._lib import check, lib
+
+            n, below = C.c_uint32(), C.c_uint64()
+            check(lib().kad_synth_recipe_range(S.SEED_IDS, S.SEED_STATUS, self.recipe_n, self.depth, b,
+                                               self.n_buckets, self.good_pct, self.expired_pct, 0, C.byref(n),
+                                               C.byref(below), None, None, None), "kad_synth_recipe_range")
+            return int(below.value)
         import ctypes as C
 
         from ._lib import check, lib
@@ -77,6 +99,11 @@ class ShardSpec:
                                             self.expired_pct, C.byref(n), None, None, None),
               "kad_synth_uniform_shard")
         return n.value
+
+
+def config3_spec(n_shards: int = 8) -> ShardSpec:
+    """BASELINE config 3: SURVEY.md §8d's 100M-node U(24) table (mt19937_64 recipe) in n_shards ID-range shards."""
+    return ShardSpec(n_shards=n_shards, depth=24, recipe_n=100_000_000)
 
 
 def halo_widths_from(good: np.ndarray, a: int, lo: int, hi: int, n_buckets: int, count: int):
@@ -115,7 +142,7 @@ def build_shard(spec: ShardSpec, s: int, probe: int = 64) -> Shard:
     B = spec.n_buckets
     while True:
         a, e = max(0, lo - probe), min(B, hi + probe)
-        ids, st, off = spec.bucket_range(a, e)
+        ids, st, off, below_a = spec.bucket_range_below(a, e)
         hw = halo_widths_from(_good_counts(st, off), a, lo, hi, B, spec.k_max)
         if hw is not None:
             break
@@ -127,7 +154,7 @@ def build_shard(spec: ShardSpec, s: int, probe: int = 64) -> Shard:
     st = np.ascontiguousarray(st[n0:n1])
     off = np.ascontiguousarray(off[b0 - a:b1 - a + 1] - n0).astype(np.uint32)
     first = S.bucket_firsts(spec.depth, b0, b1)
-    return Shard(spec, s, lo, hi, b0, b1, spec.nodes_below(b0), ids, st, first, off)
+    return Shard(spec, s, lo, hi, b0, b1, below_a + int(n0), ids, st, first, off)
 
 
 class HaloError(RuntimeError):

@@ -229,8 +229,8 @@ def test_config3_full_shard_every_query(gpu, shard):
     the first, a middle and the last shard), 1M owned queries, EVERY query bit-exact against the oracle's
     closed form (16 threads) for k = 8, 16, 32 and NodeCache k = 14, 32 (shard 0), plus the row properties
     (good, ascending XOR distance)."""
-    from opendht_amd.sharded import ShardSpec, build_shard
-    spec = ShardSpec(n_shards=8, depth=24, mean_per_bucket=100e6 / 2**24)
+    from opendht_amd.sharded import build_shard, config3_spec
+    spec = config3_spec()
     sh = build_shard(spec, shard)
     q = 1 << 20
     targets = spec.targets_for(shard, q, seed=1234 + shard)

@@ -20,7 +20,7 @@ import opendht_amd._lib as _kl  # noqa: E402
 
 _kl.use_ablation_build()  # the wl_abl* / *_abl1 timing ablations live only in the tools build
 from opendht_amd import DeviceTable  # noqa: E402
-from opendht_amd.sharded import ShardSpec, build_shard  # noqa: E402
+from opendht_amd.sharded import build_shard, config3_spec  # noqa: E402
 
 
 def main():
@@ -33,7 +33,7 @@ def main():
     ap.add_argument("--batches", type=int, default=8, help="distinct target batches, one per launch in turn")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
-    spec = ShardSpec()
+    spec = config3_spec()
     sh = build_shard(spec, 0)
     tgs = [torch.from_numpy(spec.targets_for(0, args.queries, seed=0x0D470002 + j)).to(dev) for j in range(args.batches)]
     targets = tgs[0]

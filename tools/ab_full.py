@@ -11,7 +11,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from opendht_amd import synth as S  # noqa: E402
 from opendht_amd.global_shard import GlobalShard, build_plain_shard  # noqa: E402
-from opendht_amd.sharded import ShardSpec  # noqa: E402
+from opendht_amd.sharded import config3_spec  # noqa: E402
 
 
 def timeit(fn, reps=10):
@@ -28,7 +28,7 @@ def timeit(fn, reps=10):
 
 dev = torch.device("cuda:0")
 n_shards = int(os.environ.get("NSH", "1"))
-spec = ShardSpec(n_shards=n_shards)
+spec = config3_spec(n_shards)
 ids, st, off, lo, hi, base, good = build_plain_shard(spec, 0)
 gp = np.concatenate([[0], np.cumsum(good)])
 if n_shards > 1:  # pretend the other shards' good counts equal this one's (timing only)

@@ -12,9 +12,9 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from opendht_amd import DeviceTable  # noqa: E402
 from opendht_amd._lib import KAD_OP_INSERT, KAD_OP_REMOVE, KAD_OP_REPLACE, KAD_OP_SPLIT  # noqa: E402
-from opendht_amd.sharded import ShardSpec, build_shard  # noqa: E402
+from opendht_amd.sharded import build_shard, config3_spec  # noqa: E402
 
-sh = build_shard(ShardSpec(), 0)
+sh = build_shard(config3_spec(), 0)
 t0 = time.perf_counter()
 T = DeviceTable(sh.ids, sh.status, sh.first, sh.off, device=0, index_base=sh.index_base, sorted=True)
 torch.cuda.synchronize()
@@ -49,7 +49,7 @@ for label, n_ops, splits in (("ops_10k", 10_000, 0), ("ops_100k", 100_000, 0), (
     torch.cuda.synchronize()
     res[label + "_s"] = round(time.perf_counter() - t0, 4)
 q = 1 << 20
-tg = torch.from_numpy(ShardSpec().targets_for(0, q, seed=5)).to(torch.device("cuda:0"))
+tg = torch.from_numpy(config3_spec().targets_for(0, q, seed=5)).to(torch.device("cuda:0"))
 T.rt_closest(tg, 8)
 torch.cuda.synchronize()
 a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

@@ -13,7 +13,7 @@ import opendht_amd._lib as _kl  # noqa: E402
 
 _kl.use_ablation_build()  # the wl_abl* / *_abl1 timing ablations live only in the tools build
 from opendht_amd import DeviceTable, rt_closest_dual  # noqa: E402
-from opendht_amd.sharded import ShardSpec, build_shard  # noqa: E402
+from opendht_amd.sharded import build_shard, config3_spec  # noqa: E402
 
 
 def timeit(fn, reps=10, rounds=3):
@@ -32,7 +32,7 @@ def timeit(fn, reps=10, rounds=3):
 
 
 dev = torch.device("cuda:0")
-spec = ShardSpec()
+spec = config3_spec()
 sh = build_shard(spec, 0)
 q = 1 << 20
 tg = torch.from_numpy(spec.targets_for(0, q, seed=0x0D470002)).to(dev)

@@ -16,11 +16,11 @@ import opendht_amd._lib as _kl  # noqa: E402
 if os.environ.get("NC_ABL"):
     _kl.use_ablation_build()
 from opendht_amd import DeviceTable  # noqa: E402
-from opendht_amd.sharded import ShardSpec, build_shard  # noqa: E402
+from opendht_amd.sharded import build_shard, config3_spec  # noqa: E402
 
 REPS, NB, Q = 8, 8, 1 << 20
 dev = torch.device("cuda:0")
-spec = ShardSpec()
+spec = config3_spec()
 sh = build_shard(spec, 0)
 T = DeviceTable(sh.ids, sh.status, sh.first, sh.off, device=0, index_base=sh.index_base, sorted=True)
 tgs = [torch.from_numpy(spec.targets_for(0, Q, seed=0x0D470100 + j)).to(dev) for j in range(NB)]

@@ -13,11 +13,11 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from opendht_amd import DeviceTable, rt_closest_dual  # noqa: E402
-from opendht_amd.sharded import ShardSpec, build_shard  # noqa: E402
+from opendht_amd.sharded import build_shard, config3_spec  # noqa: E402
 
 REPS = 5
 dev = torch.device("cuda:0")
-spec = ShardSpec()
+spec = config3_spec()
 sh = build_shard(spec, 0)
 q = 1 << 20
 tg = torch.from_numpy(spec.targets_for(0, q, seed=0x0D470002)).to(dev)

@@ -14,7 +14,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from opendht_amd import DeviceTable  # noqa: E402
 from opendht_amd import synth as S  # noqa: E402
-from opendht_amd.sharded import ShardSpec, build_shard  # noqa: E402
+from opendht_amd.sharded import build_shard, config3_spec  # noqa: E402
 
 REPS, NB, Q = 6, 8, 1 << 20
 dev = torch.device("cuda:0")
@@ -38,7 +38,7 @@ def run(name, fn):
     res[name] = round(float(np.median(ts)), 2)
 
 
-sh = build_shard(ShardSpec(), 0)
+sh = build_shard(config3_spec(), 0)
 T = DeviceTable(sh.ids, sh.status, sh.first, sh.off, device=0, index_base=sh.index_base, sorted=True)
 run("U24shard_rt_k8_us", lambda t: T.rt_closest(t, 8))
 run("U24shard_rt_k16_us", lambda t: T.rt_closest(t, 16))

@@ -16,9 +16,9 @@ sys.path.insert(0, ROOT)
 
 from bench import node_times  # noqa: E402
 from opendht_amd import DeviceTable  # noqa: E402
-from opendht_amd.sharded import ShardSpec, build_shard  # noqa: E402
+from opendht_amd.sharded import build_shard, config3_spec  # noqa: E402
 
-sh = build_shard(ShardSpec(), 0)
+sh = build_shard(config3_spec(), 0)
 T = DeviceTable(sh.ids, sh.status, sh.first, sh.off, device=0, index_base=sh.index_base, sorted=True)
 now = 10**15
 t, rt, ex = node_times(sh.status, now)

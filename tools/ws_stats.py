@@ -14,9 +14,9 @@ import opendht_amd._lib as _kl  # noqa: E402
 
 _kl.use_ablation_build()
 from opendht_amd import DeviceTable  # noqa: E402
-from opendht_amd.sharded import ShardSpec, build_shard  # noqa: E402
+from opendht_amd.sharded import build_shard, config3_spec  # noqa: E402
 
-spec = ShardSpec()
+spec = config3_spec()
 sh = build_shard(spec, 0)
 T = DeviceTable(sh.ids, sh.status, sh.first, sh.off, device=0, index_base=sh.index_base, sorted=True)
 res = {}
