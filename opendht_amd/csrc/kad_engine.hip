@@ -2448,6 +2448,44 @@ __global__ __launch_bounds__(BLOCK) void rt_dual_wl_kernel(DevTable T4, DevTable
     exact_tail(T6, t, ex && six, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
 }
 
+// Dual-family batch (af per query) for families with general window lines (split-policy tables, the shape the
+// reference builds): count range K = 8 / 16 / 32 -> the gl / gl16 / gl32 line of the lane's family (locate first);
+// a family without that line set takes the lane path, an unanswered query the exact path of its family.
+template <int K>
+__global__ __launch_bounds__(BLOCK) void rt_dual_gl_kernel(DevTable T4, DevTable T6, const uint8_t* __restrict__ targets,
+                                                           const uint8_t* __restrict__ af, uint32_t q, uint32_t count,
+                                                           uint32_t* __restrict__ out_idx, uint8_t* __restrict__ out_cnt) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    const bool act = i < q && count > 0;
+    if (i < q && count == 0 && out_cnt) out_cnt[i] = 0;
+    Target t{};
+    bool six = false;
+    if (act) {
+        t = load_target(targets, i);
+        six = af[i] != 0;
+    }
+    const DevTable& T = six ? T6 : T4;
+    const bool gl = act && (T.flags & (K == 8 ? TF_GL : K == 16 ? TF_GL16 : TF_GL32));
+    const uint32_t b = gl ? locate_bucket(T, t) : 0u;
+    uint32_t o[K], m = 0;
+    bool ok;
+    if constexpr (K == 8) ok = gl_answer(T, t, b, count, gl, o, m);
+    else if constexpr (K == 16) ok = gl16_answer(T, t, b, count, gl, o, m);
+    else ok = gl32_answer(T, t, b, count, gl, o, m);
+    ok = ok && gl;
+    if (ok && out_cnt) out_cnt[i] = (uint8_t)m;
+    if constexpr (K == 8) {
+        if (ok) store_row8(out_idx + (size_t)i * count, o, count);
+    } else {
+        store_rows_block<K>(out_idx, q, count, o, ok);
+    }
+    bool ex = gl && !ok;
+    if (act && !gl) ex = !rt_query_fast<K, 3>(T, t, count, out_idx + (size_t)i * count, out_cnt ? out_cnt + i : nullptr);
+    __shared__ uint64_t xs[BLOCK / 64][192];
+    exact_tail(T4, t, ex && !six, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
+    exact_tail(T6, t, ex && six, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
+}
+
 // Dual-family batch for counts 9..16 where a family has 16-slot window lines (same structure).
 __global__ __launch_bounds__(BLOCK) void rt_dual_wl16_kernel(DevTable T4, DevTable T6,
                                                              const uint8_t* __restrict__ targets,
@@ -5270,13 +5308,22 @@ int kad_rt_closest_batch_dual(const kad_table* t4, const kad_table* t6, const ui
     if (count <= 8 && ((d4.flags | d6.flags) & TF_WL))
         hipLaunchKernelGGL(rt_dual_wl_kernel, dim3(grid_for(q)), dim3(BLOCK), 0, s, d4, d6, targets, af, q, count,
                            out_idx, out_cnt);
+    else if (count <= 8 && ((d4.flags | d6.flags) & TF_GL))
+        hipLaunchKernelGGL(rt_dual_gl_kernel<8>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d4, d6, targets, af, q, count,
+                           out_idx, out_cnt);
     else if (count <= 8) launch_rt_dual<8>(d4, d6, targets, af, q, count, out_idx, out_cnt, s);
     else if (count <= 16 && ((d4.flags | d6.flags) & TF_WL16))
         hipLaunchKernelGGL(rt_dual_wl16_kernel, dim3(grid_for(q)), dim3(BLOCK), 0, s, d4, d6, targets, af, q, count,
                            out_idx, out_cnt);
+    else if (count <= 16 && ((d4.flags | d6.flags) & TF_GL16))
+        hipLaunchKernelGGL(rt_dual_gl_kernel<16>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d4, d6, targets, af, q, count,
+                           out_idx, out_cnt);
     else if (count <= 16) launch_rt_dual<16>(d4, d6, targets, af, q, count, out_idx, out_cnt, s);
     else if ((d4.flags | d6.flags) & TF_WL32)
         hipLaunchKernelGGL(rt_dual_wl32_kernel, dim3(grid_for(q)), dim3(BLOCK), 0, s, d4, d6, targets, af, q, count,
+                           out_idx, out_cnt);
+    else if ((d4.flags | d6.flags) & TF_GL32)
+        hipLaunchKernelGGL(rt_dual_gl_kernel<32>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d4, d6, targets, af, q, count,
                            out_idx, out_cnt);
     else launch_rt_dual<32>(d4, d6, targets, af, q, count, out_idx, out_cnt, s);
     HIP_TRY(hipGetLastError());

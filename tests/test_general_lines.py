@@ -106,3 +106,30 @@ def test_uniform_table_switches_to_general_lines_after_split(gpu):
         assert f & KAD_INFO_GENERAL_LINES16 and f & KAD_INFO_SLOT_LINES16, hex(f)
         t2 = TB.table(ids, st, first, off, name="U11_split")
         _check(T, t2, TB.adversarial_targets(t2, extra=3000), gpu, counts=(1, 7, 8, 9, 16, 17, 32))
+
+
+def test_dual_family_general_lines(gpu):
+    """kad_rt_closest_batch_dual on two split-policy families (af per query) through rt_dual_gl_kernel: every
+    count range reads its family's general lines, bit-exact against the oracle per family."""
+    from opendht_amd import rt_closest_dual
+    t4 = TB.split_config(100_000, seed=0x6B4)
+    t6 = TB.split_config(60_000, seed=0x6B6, good=60, expired=25)
+    rng = np.random.default_rng(0x6B)
+    targets = np.ascontiguousarray(np.concatenate([TB.adversarial_targets(t4, extra=3000),
+                                                   TB.adversarial_targets(t6, extra=3000)]))
+    af = rng.integers(0, 2, targets.shape[0]).astype(np.uint8)
+    with DeviceTable(t4["ids"], t4["status"], t4["first"], t4["off"], device=0) as T4, \
+            DeviceTable(t6["ids"], t6["status"], t6["first"], t6["off"], device=0) as T6:
+        for T in (T4, T6):
+            f = T.info()["flags"]
+            assert f & KAD_INFO_GENERAL_LINES and f & KAD_INFO_GENERAL_LINES16 and f & KAD_INFO_GENERAL_LINES32, hex(f)
+        tg, afd = torch.from_numpy(targets).to(gpu), torch.from_numpy(af).to(gpu)
+        for k in (1, 5, 8, 9, 14, 16, 17, 24, 32):
+            idx, cnt = rt_closest_dual(T4, T6, tg, afd, k)
+            torch.cuda.synchronize()
+            idx, cnt = idx.cpu().numpy().view(np.uint32), cnt.cpu().numpy()
+            for fam, t in ((0, t4), (1, t6)):
+                sel = np.flatnonzero(af == fam)
+                want, wcnt = O.flat_rt_closest(t["ids"], t["status"], t["first"], t["off"], targets[sel], k, nthreads=8)
+                np.testing.assert_array_equal(cnt[sel], wcnt, err_msg=f"af={fam} k={k} counts")
+                np.testing.assert_array_equal(idx[sel], want, err_msg=f"af={fam} k={k}")

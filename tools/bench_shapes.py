@@ -77,6 +77,20 @@ for n in [int(x) for x in sys.argv[1:]] or [1_000_000, 12_500_000]:
                 os.environ.pop("KAD_RT_KERNEL")
                 torch.cuda.synchronize()
                 res[f"S{n}_k{k}_{env}_only_equal"] = bool(torch.equal(a, c))
+    # dual-family batch (af alternating, the table as both families): rt_dual_gl_kernel vs the lane kernel
+    from opendht_amd import rt_closest_dual
+    afd = (torch.arange(Q, device=dev) % 2).to(torch.uint8)
+    for k in (8, 14, 32):
+        for j in range(NB):
+            rt_closest_dual(T, T, tgs[j], afd, k)
+        torch.cuda.synchronize()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for j in range(24):
+            rt_closest_dual(T, T, tgs[j % NB], afd, k)
+        b.record()
+        torch.cuda.synchronize()
+        res[f"S{n}_dual_k{k}_us"] = round(a.elapsed_time(b) / 24 * 1e3, 1)
     T.close()
     sid, _ = S.sort_ids(ids)
     d = max(1, int(round(np.log2(n / 8))))
