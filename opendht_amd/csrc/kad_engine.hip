@@ -2513,6 +2513,23 @@ __global__ __launch_bounds__(BLOCK) void rt_dual_wl16_kernel(DevTable T4, DevTab
     } else if (act && !wl) {
         ex = !rt_query_fast<16, 3>(T, t, count, row, out_cnt ? out_cnt + i : nullptr);
     }
+    // the line's misses: the family's 32-count line by the wave (as rt_wl16_kernel), then the exact path
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t sixm = __ballot(six);
+    for (uint64_t pm = __ballot(wl && !ok); pm; pm &= pm - 1) {
+        const uint32_t l = (uint32_t)__builtin_ctzll(pm);
+        const DevTable& Tl = ((sixm >> l) & 1ull) ? T6 : T4;  // wave-uniform
+        if (!(Tl.flags & TF_WL32)) continue;
+        Target u;
+        u.hi = rdl64(t.hi, l);
+        u.t2 = rdl(t.t2, l);
+        u.t3 = rdl(t.t3, l);
+        u.t4 = rdl(t.t4, l);
+        const uint32_t il = rdl(i, l);
+        if (wave_wl32(Tl, u, rdl(b, l), count, lane, out_idx + (size_t)il * count, out_cnt ? out_cnt + il : nullptr) &&
+            lane == l)
+            ex = false;
+    }
     __shared__ uint64_t xs[BLOCK / 64][192];
     exact_tail(T4, t, ex && !six, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
     exact_tail(T6, t, ex && six, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
