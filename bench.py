@@ -184,8 +184,16 @@ def cpu_baselines(sh, targets, count, budget_s, nthreads, min_port=1000, fast_mi
         n += sl.shape[0]
         rate = n / max(dt, 1e-9)
         chunk = int(min(4 * chunk, max(2 * nthreads, rate * max(budget_s - dt, 0.5), min_port - n)))
+    # the same on one thread (1 thread and all cores), a few seconds of it
+    n1, dt1 = 0, 0.0
+    while dt1 < budget_s / 3 and n1 < targets.shape[0]:
+        t0 = time.perf_counter()
+        F.rt_closest(targets[n1:n1 + 4], count, nthreads=1)
+        dt1 += time.perf_counter() - t0
+        n1 += 4
     F.close()
     port = {"value": n / dt, "unit": "queries/s", "cores": nthreads, "kind": "port",
+            "value_1thread": n1 / dt1, "sample_1thread": f"{n1} queries in {dt1:.1f} s on one thread",
             "sample": f"{n} of the {targets.shape[0]} queries of rank 0's first batch (same shard table, "
                       f"{sh.first.shape[0]} buckets, {sh.ids.shape[0]} nodes) in {dt:.1f} s; structure-faithful "
                       f"restatement of routing_table.cpp:67-135 (std::list walk); table build {build_s:.1f}s excluded",
@@ -200,7 +208,11 @@ def cpu_baselines(sh, targets, count, budget_s, nthreads, min_port=1000, fast_mi
         fdt += time.perf_counter() - t0
         fq += targets.shape[0]
         passes += 1
+    t0 = time.perf_counter()
+    O.flat_rt_closest(sh.ids, sh.status, sh.first, sh.off, targets[:1 << 14], count, nthreads=1)
+    fdt1 = time.perf_counter() - t0
     fast = {"value": fq / fdt, "unit": "queries/s", "cores": nthreads, "kind": "port",
+            "value_1thread": (1 << 14) / fdt1, "sample_1thread": f"{1 << 14} queries in {fdt1:.2f} s on one thread",
             "sample": f"{passes} passes over {targets.shape[0]} queries of rank 0's first batch ({fq} queries) in "
                       f"{fdt:.2f} s; closed-form flat restatement "
                       f"(upper_bound findBucket + window rounds + sort by XOR distance), {nthreads} threads",
