@@ -38,6 +38,10 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
+#include <chrono>
+#include <map>
+#include <unordered_map>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -4462,6 +4466,7 @@ struct kad_table {
     // host copies of the bucket directory, for the incremental mirror (kad_table_apply)
     std::vector<uint32_t> h_off;
     std::vector<uint8_t> h_first;
+    int8_t firsts_low_zero = -1, firsts_low_zero_next = -1;  // all h_first low 96 bits zero (-1: not known yet)
     uint32_t* wrec = nullptr;  // per-node wire records: ID + address + port (kad_table_set_addrs)
     uint32_t addr_len = 0;
     int64_t* time_ns = nullptr;
@@ -5729,17 +5734,39 @@ int kad_table_apply(kad_table* t, const uint32_t* ops, uint32_t n_ops, const uin
     DeviceGuard g(t->device);
     DevTable& d = t->d;
     const uint32_t B0 = d.B, n0 = d.n;
+    // KAD_DEBUG: the phases' wall times (host plan, layout, gather, directory, line rebuild)
+    const bool dbg = std::getenv("KAD_DEBUG") != nullptr;
+    auto tp = std::chrono::steady_clock::now();
+    auto phase = [&](const char* what) {
+        if (!dbg) return;
+        const auto now = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "kad_table_apply %s: %.3f ms\n", what, std::chrono::duration<double, std::milli>(now - tp).count());
+        tp = now;
+    };
+    // Sparse plan: an origin bucket (a bucket of the table as it is now) that an op touches gets the list of its
+    // current buckets (splits add some), each an untouched range of old nodes (raw) or an explicit handle list;
+    // every other origin stays one untouched range. Host work is proportional to the batch, except the new
+    // offsets and the bucket directory (simple O(buckets) passes).
     struct PB {
         bool raw;
-        uint32_t src, len, origin;
+        uint32_t src, len;
         std::vector<uint32_t> h;
+        std::array<uint8_t, 20> first;
     };
-    std::vector<PB> cur(B0);
-    for (uint32_t b = 0; b < B0; b++) cur[b] = PB{true, t->h_off[b], t->h_off[b + 1] - t->h_off[b], b, {}};
-    std::vector<std::array<uint8_t, 20>> firsts(B0);
-    for (uint32_t b = 0; b < B0; b++) std::memcpy(firsts[b].data(), t->h_first.data() + 20ull * b, 20);
-    std::vector<uint32_t> ostart(B0 + 1);  // current index of origin bucket o's first descendant
-    for (uint32_t b = 0; b <= B0; b++) ostart[b] = b;
+    const std::vector<uint32_t>& off0 = t->h_off;
+    const uint8_t* first0 = t->h_first.data();
+    std::unordered_map<uint32_t, std::vector<PB>> tb;  // touched origin -> its current buckets
+    std::map<uint32_t, uint32_t> extra;                // split origin -> buckets its splits added
+    uint32_t Bcur = B0;
+    auto touch = [&](uint32_t o) -> std::vector<PB>& {
+        auto it = tb.find(o);
+        if (it == tb.end()) {
+            PB p{true, off0[o], off0[o + 1] - off0[o], {}, {}};
+            std::memcpy(p.first.data(), first0 + 20ull * o, 20);
+            it = tb.emplace(o, std::vector<PB>(1, std::move(p))).first;
+        }
+        return it->second;
+    };
     auto mat = [](PB& p) {
         if (p.raw) {
             p.h.resize(p.len);
@@ -5747,21 +5774,32 @@ int kad_table_apply(kad_table* t, const uint32_t* ops, uint32_t n_ops, const uin
             p.raw = false;
         }
     };
+    // current bucket index c -> (origin, index among the origin's current buckets)
+    auto origin_of = [&](uint32_t c, uint32_t& o, uint32_t& sub) {
+        uint32_t shift = 0;  // buckets added by the splits of the origins below
+        for (const auto& e : extra) {
+            if (c < e.first + shift) break;
+            if (c <= e.first + shift + e.second) { o = e.first; sub = c - e.first - shift; return; }
+            shift += e.second;
+        }
+        o = c - shift;
+        sub = 0;
+    };
     // IDs of old nodes, downloaded per origin bucket on first use (splits only)
-    std::vector<int> have(B0, 0);
+    std::unordered_map<uint32_t, uint32_t> oid_at;
     std::vector<uint8_t> oid;
-    std::vector<uint32_t> oid_at(B0, 0);
     auto id_of = [&](uint32_t h, uint32_t origin, uint8_t* out) -> int {
         if (h & MIRROR_NEW) { std::memcpy(out, new_ids + 20ull * (h & ~MIRROR_NEW), 20); return KAD_OK; }
-        if (!have[origin]) {
-            const uint32_t a = t->h_off[origin], e = t->h_off[origin + 1];
+        auto it = oid_at.find(origin);
+        if (it == oid_at.end()) {
+            const uint32_t a = off0[origin], e = off0[origin + 1];
             std::vector<uint64_t> k(e - a);
             std::vector<uint32_t> tl(3ull * (e - a));
             if (e > a) {
                 HIP_TRY(hipMemcpy(k.data(), d.key + a, 8ull * (e - a), hipMemcpyDeviceToHost));
                 HIP_TRY(hipMemcpy(tl.data(), d.tail + 3ull * a, 12ull * (e - a), hipMemcpyDeviceToHost));
             }
-            oid_at[origin] = (uint32_t)(oid.size() / 20);
+            it = oid_at.emplace(origin, (uint32_t)(oid.size() / 20)).first;
             for (uint32_t i = 0; i < e - a; i++) {
                 uint8_t b[20];
                 for (int x = 0; x < 8; x++) b[x] = (uint8_t)(k[i] >> (56 - 8 * x));
@@ -5769,21 +5807,23 @@ int kad_table_apply(kad_table* t, const uint32_t* ops, uint32_t n_ops, const uin
                     for (int x = 0; x < 4; x++) b[8 + 4 * w + x] = (uint8_t)(tl[3ull * i + w] >> (24 - 8 * x));
                 oid.insert(oid.end(), b, b + 20);
             }
-            have[origin] = 1;
         }
-        std::memcpy(out, oid.data() + 20ull * (oid_at[origin] + (h - t->h_off[origin])), 20);
+        std::memcpy(out, oid.data() + 20ull * (it->second + (h - off0[origin])), 20);
         return KAD_OK;
     };
-    auto locate = [&](uint32_t a, uint32_t& c, uint32_t& pos) -> bool {
+    // node a (index at the batch start) -> its origin, current bucket and position
+    auto locate = [&](uint32_t a, uint32_t& o, uint32_t& sub, uint32_t& pos) -> bool {
         if (a >= n0) return false;
-        const uint32_t o = (uint32_t)(std::upper_bound(t->h_off.begin(), t->h_off.end(), a) - t->h_off.begin()) - 1;
-        for (c = ostart[o]; c < ostart[o + 1]; c++) {
-            PB& p = cur[c];
+        o = (uint32_t)(std::upper_bound(off0.begin(), off0.end(), a) - off0.begin()) - 1;
+        auto it = tb.find(o);
+        if (it == tb.end()) { sub = 0; pos = a - off0[o]; return true; }
+        for (sub = 0; sub < it->second.size(); sub++) {
+            const PB& p = it->second[sub];
             if (p.raw) {
                 if (a >= p.src && a < p.src + p.len) { pos = a - p.src; return true; }
             } else {
-                auto it = std::find(p.h.begin(), p.h.end(), a);
-                if (it != p.h.end()) { pos = (uint32_t)(it - p.h.begin()); return true; }
+                auto f = std::find(p.h.begin(), p.h.end(), a);
+                if (f != p.h.end()) { pos = (uint32_t)(f - p.h.begin()); return true; }
             }
         }
         return false;
@@ -5791,83 +5831,108 @@ int kad_table_apply(kad_table* t, const uint32_t* ops, uint32_t n_ops, const uin
     const bool structural = n_ops > 0;  // node indices move: the NodeCache radix no longer applies
     for (uint32_t k = 0; k < n_ops; k++) {
         const uint32_t kind = ops[3ull * k], a = ops[3ull * k + 1], b = ops[3ull * k + 2];
-        uint32_t c = 0, pos = 0;
+        uint32_t o = 0, sub = 0, pos = 0;
         if (kind == KAD_OP_REMOVE || kind == KAD_OP_REPLACE) {
-            if (!locate(a, c, pos)) return set_err(KAD_ERR_INVALID, "op %u: node %u is not in the table", k, a);
+            if (!locate(a, o, sub, pos)) return set_err(KAD_ERR_INVALID, "op %u: node %u is not in the table", k, a);
             if (kind == KAD_OP_REPLACE && b >= n_new) return set_err(KAD_ERR_INVALID, "op %u: new slot %u", k, b);
-            mat(cur[c]);
-            if (kind == KAD_OP_REMOVE) cur[c].h.erase(cur[c].h.begin() + pos);
-            else cur[c].h[pos] = MIRROR_NEW | b;
+            PB& p = touch(o)[sub];
+            mat(p);
+            if (kind == KAD_OP_REMOVE) p.h.erase(p.h.begin() + pos);
+            else p.h[pos] = MIRROR_NEW | b;
         } else if (kind == KAD_OP_INSERT) {
             if (a >= n_new) return set_err(KAD_ERR_INVALID, "op %u: new slot %u", k, a);
             // RoutingTable::findBucket (routing_table.cpp:113-127): last bucket with first <= id
             const uint8_t* id = new_ids + 20ull * a;
-            uint32_t lo = 0, hi = (uint32_t)firsts.size();
+            uint32_t lo = 0, hi = B0;
             while (lo < hi) {
                 const uint32_t mid = (lo + hi) >> 1;
-                if (std::memcmp(firsts[mid].data(), id, 20) <= 0) lo = mid + 1; else hi = mid;
+                if (std::memcmp(first0 + 20ull * mid, id, 20) <= 0) lo = mid + 1; else hi = mid;
             }
-            c = lo ? lo - 1 : 0;
-            mat(cur[c]);
-            cur[c].h.insert(cur[c].h.begin(), MIRROR_NEW | a);  // emplace_front (dht.cpp:934)
+            o = lo ? lo - 1 : 0;
+            std::vector<PB>& v = touch(o);
+            sub = 0;
+            while (sub + 1 < v.size() && std::memcmp(v[sub + 1].first.data(), id, 20) <= 0) sub++;
+            mat(v[sub]);
+            v[sub].h.insert(v[sub].h.begin(), MIRROR_NEW | a);  // emplace_front (dht.cpp:934)
         } else if (kind == KAD_OP_SPLIT) {
-            if (a >= cur.size()) return set_err(KAD_ERR_INVALID, "op %u: bucket %u of %zu", k, a, cur.size());
+            if (a >= Bcur) return set_err(KAD_ERR_INVALID, "op %u: bucket %u of %u", k, a, Bcur);
+            origin_of(a, o, sub);
+            std::vector<PB>& v = touch(o);
             // RoutingTable::depth / middle / split (routing_table.cpp:47-65, 137-163)
-            const int b1 = lowbit20(firsts[a].data()), b2 = a + 1 < firsts.size() ? lowbit20(firsts[a + 1].data()) : -1;
+            const uint8_t* nf = sub + 1 < v.size() ? v[sub + 1].first.data() : o + 1 < B0 ? first0 + 20ull * (o + 1) : nullptr;
+            const int b1 = lowbit20(v[sub].first.data()), b2 = nf ? lowbit20(nf) : -1;
             const int depth = std::max(b1, b2) + 1;
             if (depth >= 160) continue;  // middle() throws: split returns false
-            std::array<uint8_t, 20> mid = firsts[a];
+            std::array<uint8_t, 20> mid = v[sub].first;
             mid[depth / 8] |= (uint8_t)(0x80 >> (depth % 8));
-            mat(cur[a]);
+            mat(v[sub]);
             std::vector<uint32_t> keep, move;
-            for (uint32_t h : cur[a].h) {  // splice each node to the FRONT of its new bucket
+            for (uint32_t h : v[sub].h) {  // splice each node to the FRONT of its new bucket
                 uint8_t id[20];
-                int rc = id_of(h, cur[a].origin, id);
+                int rc = id_of(h, o, id);
                 if (rc) return rc;
                 auto& dst = std::memcmp(id, mid.data(), 20) >= 0 ? move : keep;
                 dst.insert(dst.begin(), h);
             }
-            PB nb{false, 0, 0, cur[a].origin, std::move(move)};
-            cur[a].h = std::move(keep);
-            cur.insert(cur.begin() + a + 1, std::move(nb));
-            firsts.insert(firsts.begin() + a + 1, mid);
-            for (uint32_t o = cur[a].origin + 1; o <= B0; o++) ostart[o]++;
+            v[sub].h = std::move(keep);
+            v.insert(v.begin() + sub + 1, PB{false, 0, 0, std::move(move), mid});
+            extra[o]++;
+            Bcur++;
         } else {
             return set_err(KAD_ERR_INVALID, "op %u: unknown kind %u", k, kind);
         }
     }
+    phase("plan (ops)");
+    std::vector<uint32_t> tk;  // touched origins, ascending
+    tk.reserve(tb.size());
+    for (const auto& e : tb) tk.push_back(e.first);
+    std::sort(tk.begin(), tk.end());
     // window lines need every node inside its bucket's dyadic range: check the new nodes
-    bool lines_ok = (d.flags & TF_WL) && cur.size() == B0;
+    bool lines_ok = (d.flags & TF_WL) && Bcur == B0;
     if (lines_ok) {
         const uint64_t pre0 = d.rbase >> d.rshift;
-        for (uint32_t c = 0; c < B0 && lines_ok; c++)
-            if (!cur[c].raw)
-                for (uint32_t h : cur[c].h)
-                    if (h & MIRROR_NEW) lines_ok &= (id_hi(new_ids + 20ull * (h & ~MIRROR_NEW)) >> d.rshift) == pre0 + c;
+        for (uint32_t o : tk)
+            for (const PB& p : tb[o])
+                if (!p.raw)
+                    for (uint32_t h : p.h)
+                        if (h & MIRROR_NEW) lines_ok &= (id_hi(new_ids + 20ull * (h & ~MIRROR_NEW)) >> d.rshift) == pre0 + o;
     }
-    // new layout
-    const uint32_t B1 = (uint32_t)cur.size();
+    // new layout: untouched origins between touched ones are one range of old nodes
+    const uint32_t B1 = Bcur;
     std::vector<MirrorSeg> segs;
     std::vector<uint32_t> list, off1(B1 + 1);
-    uint32_t acc = 0;
-    for (uint32_t c = 0; c < B1; c++) {
-        off1[c] = acc;
-        const PB& p = cur[c];
-        const uint32_t len = p.raw ? p.len : (uint32_t)p.h.size();
-        if (len) {
-            if (p.raw) {  // consecutive untouched buckets are one range of old nodes
-                MirrorSeg* last = segs.empty() ? nullptr : &segs.back();
-                if (last && last->kind == 0 && last->src + last->len == p.src) last->len += len;
-                else segs.push_back(MirrorSeg{acc, p.src, len, 0});
-            } else {
+    uint32_t acc = 0, c = 0, prev = 0;
+    auto raw_seg = [&](uint32_t src, uint32_t len) {
+        if (!len) return;
+        MirrorSeg* last = segs.empty() ? nullptr : &segs.back();
+        if (last && last->kind == 0 && last->src + last->len == src && last->start + last->len == acc) last->len += len;
+        else segs.push_back(MirrorSeg{acc, src, len, 0});
+    };
+    auto untouched = [&](uint32_t e) {  // origins [prev, e)
+        const uint32_t base = off0[prev];
+        for (uint32_t u = prev; u < e; u++) off1[c++] = acc + (off0[u] - base);
+        raw_seg(base, off0[e] - base);
+        acc += off0[e] - base;
+    };
+    for (uint32_t o : tk) {
+        untouched(o);
+        for (const PB& p : tb[o]) {
+            off1[c++] = acc;
+            const uint32_t len = p.raw ? p.len : (uint32_t)p.h.size();
+            if (p.raw) {
+                raw_seg(p.src, len);
+            } else if (len) {
                 segs.push_back(MirrorSeg{acc, (uint32_t)list.size(), len, 1});
                 list.insert(list.end(), p.h.begin(), p.h.end());
             }
+            acc += len;
         }
-        acc += len;
+        prev = o + 1;
     }
+    untouched(B0);
     off1[B1] = acc;
     const uint32_t n1 = acc;
+    phase("layout (segments)");
     // new nodes' device rows
     std::vector<uint64_t> nkey(n_new);
     std::vector<uint32_t> ntail(3ull * n_new);
@@ -5907,6 +5972,7 @@ int kad_table_apply(kad_table* t, const uint32_t* ops, uint32_t n_ops, const uin
                            d.key, d.tail, d.status, dnkey, dntail, dnst, key1, tail1, st1, dremap, dnidx);
     if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess)
         return fail(set_err(KAD_ERR_HIP, "mirror gather failed"));
+    phase("upload + gather");
     // bucket directory (always a new array, so the old one stays valid until the commit)
     std::vector<uint2> dir(B1 + 1);
     for (uint32_t c = 0; c <= B1; c++) {
@@ -5923,14 +5989,31 @@ int kad_table_apply(kad_table* t, const uint32_t* ops, uint32_t n_ops, const uin
          (rc = dev_upload(&spart, nullptr, B1 + 1, fresh, freshb)) ||
          (rc = dev_upload(&ssums, nullptr, (B1 + 1 + SCAN_TILE - 1) / SCAN_TILE, fresh, freshb))))
         return fail(rc);
-    std::vector<uint8_t> first1(20ull * B1);
-    for (uint32_t c = 0; c < B1; c++) std::memcpy(first1.data() + 20ull * c, firsts[c].data(), 20);
-    if (reshape && (rc = make_bucket_index(first1, B1, bix, fresh, freshb))) return fail(rc);
+    std::vector<uint8_t> first1;  // the new bucket firsts (only splits change them)
+    if (reshape) {
+        first1.resize(20ull * B1);
+        uint32_t j = 0, pv = 0;
+        for (uint32_t o : tk) {
+            if (o > pv) std::memcpy(first1.data() + 20ull * j, first0 + 20ull * pv, 20ull * (o - pv));
+            j += o - pv;
+            for (const PB& p : tb[o]) std::memcpy(first1.data() + 20ull * j++, p.first.data(), 20);
+            pv = o + 1;
+        }
+        if (B0 > pv) std::memcpy(first1.data() + 20ull * j, first0 + 20ull * pv, 20ull * (B0 - pv));
+        if ((rc = make_bucket_index(first1, B1, bix, fresh, freshb))) return fail(rc);
+    }
+    const uint8_t* fnew = reshape ? first1.data() : first0;
     // duplicate top-64 masks of the new layout
     if ((rc = dev_upload(&ddm, nullptr, B1, fresh, freshb)) || (rc = dev_upload(&dany, nullptr, 1, tmp, tmpb)))
         return fail(rc);
-    bool low_zero = true;
-    for (uint32_t c = 0; c < B1 && low_zero; c++) low_zero = id_low_zero(first1.data() + 20ull * c);
+    if (reshape || t->firsts_low_zero < 0) {  // every bucket first is 64-bit granular (cached until a split)
+        bool lz = true;
+        for (uint32_t c = 0; c < B1 && lz; c++) lz = id_low_zero(fnew + 20ull * c);
+        t->firsts_low_zero_next = lz ? 1 : 0;
+    } else {
+        t->firsts_low_zero_next = t->firsts_low_zero;
+    }
+    const bool low_zero = t->firsts_low_zero_next == 1;
     uint32_t any = 0;
     if (low_zero) {
         if (hipMemset(dany, 0, 4) != hipSuccess) return fail(set_err(KAD_ERR_HIP, "hipMemset failed"));
@@ -5946,6 +6029,7 @@ int kad_table_apply(kad_table* t, const uint32_t* ops, uint32_t n_ops, const uin
         return fail(set_err(KAD_ERR_HIP, "copy of new indices failed"));
     for (void* p : tmp) (void)hipFree(p);
 
+    phase("directory, bucket index, dup masks");
     // ---- commit: nothing below can fail before the derived state is rebuilt ----
     release(t, const_cast<uint64_t*>(d.key));
     release(t, const_cast<uint32_t*>(d.tail));
@@ -5961,8 +6045,9 @@ int kad_table_apply(kad_table* t, const uint32_t* ops, uint32_t n_ops, const uin
     release(t, t->wrec); t->wrec = nullptr; t->addr_len = 0;
     release(t, t->time_ns); release(t, t->reply_ns); release(t, t->expired);
     t->time_ns = nullptr; t->reply_ns = nullptr; t->expired = nullptr;
-    t->h_off = off1;
-    t->h_first.swap(first1);
+    t->h_off.swap(off1);
+    if (reshape) t->h_first.swap(first1);
+    t->firsts_low_zero = t->firsts_low_zero_next;
     release(t, t->dir_mut);
     d.dir = ddir; t->dir_mut = ddir;
     if (reshape) {
@@ -5999,8 +6084,10 @@ int kad_table_apply(kad_table* t, const uint32_t* ops, uint32_t n_ops, const uin
     // masks, good prefix sums, window lines
     if ((rc = rebuild_good_prefix(t, nullptr))) return rc;
     HIP_TRY(hipDeviceSynchronize());
+    phase("masks, prefix sums, lines");
     // a table that lost (or never had) uniform-depth lines gets general ones (built from the new state)
     if (!(d.flags & TF_WL) && !t->gl_mut && !t->gl32_mut && (rc = setup_general_lines(t))) return rc;
+    phase("general lines");
     return KAD_OK;
 }
 

@@ -31,6 +31,7 @@ for label, n_ops, splits in (("ops_10k", 10_000, 0), ("ops_100k", 100_000, 0), (
             ops.append((KAD_OP_REMOVE, int(a), 0))
         else:
             x = rng.integers(0, 256, 20, dtype=np.uint8)
+            x[0] &= 0x1F  # inside shard 0's ID range (top 3 bits 000): the node joins an owned bucket
             if r == 1:
                 exp = T.export() if False else None  # noqa: F841
                 ops.append((KAD_OP_INSERT, len(nid), 0))
