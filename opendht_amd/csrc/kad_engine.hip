@@ -4408,19 +4408,28 @@ inline bool id_low_zero(const uint8_t* p) {
 
 // rdx[s] = #items with hi64 < slot_start(s) for s in [0, slots]; items ascending by hi64.
 // exact_flag: mark slots whose first item starts exactly at the slot start (low bits zero).
+// One pass over the items (their slot by a shift) and one over the slots: O(items + slots), 64-bit arithmetic.
 std::vector<uint32_t> build_radix(const Radix& r, uint32_t m, const uint8_t* items, bool exact_flag) {
-    std::vector<uint32_t> rdx(r.slots + 1);
-    uint32_t j = 0;
-    for (uint32_t s = 0; s <= r.slots; s++) {
-        const unsigned __int128 start = (unsigned __int128)r.base + ((unsigned __int128)s << r.shift);
-        while (j < m && (unsigned __int128)id_hi(items + 20ull * j) < start) j++;
-        uint32_t v = j;
-        if (exact_flag && j < m && s < r.slots) {
-            const uint8_t* it = items + 20ull * j;
-            if ((unsigned __int128)id_hi(it) == start && id_low_zero(it)) v |= RDX_EXACT;
-        }
-        rdx[s] = v;
+    std::vector<uint32_t> rdx(r.slots + 1, 0);
+    // rdx[s + 1] counts the items of slot s, rdx[0] the items below the base; items past the last slot count
+    // in no slot (rdx[slots] = #items below the end of the last slot)
+    uint32_t below = 0;
+    for (uint32_t j = 0; j < m; j++) {
+        const uint64_t hi = id_hi(items + 20ull * j);
+        if (hi < r.base) { below++; continue; }
+        const uint64_t sl = (hi - r.base) >> r.shift;
+        if (sl < r.slots) rdx[sl + 1]++;
     }
+    rdx[0] = below;
+    for (uint32_t sl = 0; sl < r.slots; sl++) rdx[sl + 1] += rdx[sl];
+    if (exact_flag)
+        for (uint32_t sl = 0; sl < r.slots; sl++) {
+            const uint32_t j = rdx[sl];
+            if (j >= m) continue;
+            const uint8_t* it = items + 20ull * j;
+            const uint64_t start = r.base + ((uint64_t)sl << r.shift);  // sl < slots: inside 64 bits
+            if (id_hi(it) == start && id_low_zero(it)) rdx[sl] |= RDX_EXACT;
+        }
     return rdx;
 }
 
