@@ -3507,8 +3507,8 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// Row r of the NodeCache line kernel's block inside its wave's staging region (64 x 9 uint4 = 2304 words per wave).
-__device__ __forceinline__ uint32_t ncl_wrow(uint32_t r) { return (r >> 6) * 2304u + (r & 63u) * 16u; }
+// Row r of the NodeCache line kernel's block inside its wave's staging region (64 x 8 uint4 = 2048 words per wave).
+__device__ __forceinline__ uint32_t ncl_wrow(uint32_t r) { return (r >> 6) * 2048u + (r & 63u) * 16u; }
 
 // The block's rows of count <= 16 from LDS (row r at rows[r * 16 + c], or rows[ncl_wrow(r) + c] with wrow; the first
 // m[r] valid, the rest NONE) as one run of 16-byte stores; rows whose lane did not answer (ok false) are skipped
@@ -3541,6 +3541,37 @@ __device__ __forceinline__ void store_rows_lds16(uint32_t* __restrict__ out_idx,
     }
 }
 
+// The block's rows from the waves' staging regions (2048 words each: row r's words at ncl_wrow(r), its meta word
+// m | answered << 8 at word 1024 + (r & 63) of its wave's region) as one run of 16-byte stores; rows not answered
+// are skipped dword by dword.
+__device__ __forceinline__ void store_rows_wave16(uint32_t* __restrict__ out_idx, uint32_t q, uint32_t count,
+                                                  const uint32_t* stgw) {
+    const uint32_t tid = threadIdx.x, q0 = blockIdx.x * BLOCK;
+    const uint32_t nq = min((uint32_t)BLOCK, q - q0), nw = nq * count;
+    uint32_t* dst = out_idx + (size_t)q0 * count;
+    const bool al = ((uintptr_t)out_idx & 15u) == 0;  // BLOCK * count * 4 is a multiple of 16
+    for (uint32_t c4 = tid; 4 * c4 < nw; c4 += BLOCK) {
+        const uint32_t w0 = 4 * c4;
+        uint32_t r = w0 / count, c = w0 - r * count, v[4];
+        bool okv[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const bool in = w0 + u < nw;
+            const uint32_t meta = in ? stgw[(r >> 6) * 2048u + 1024u + (r & 63u)] : 0u;
+            okv[u] = in && ((meta >> 8) & 1u);
+            v[u] = in && c < (meta & 255u) ? stgw[ncl_wrow(r) + c] : NONE;
+            if (++c == count) { c = 0; r++; }
+        }
+        if (al && okv[0] && okv[1] && okv[2] && okv[3]) {
+            reinterpret_cast<uint4*>(dst)[c4] = make_uint4(v[0], v[1], v[2], v[3]);
+        } else {
+#pragma unroll
+            for (int u = 0; u < 4; u++)
+                if (okv[u]) dst[w0 + u] = v[u];
+        }
+    }
+}
+
 // ABL 1 (timing ablation only, KAD_NC_KERNEL=lines_abl1; results wrong): no exact path. ABL 2 (lines_abl2): the
 // line load and the row store only (every word of the line folded into one value), the memory floor.
 // DUAL: per-query family (af[i] = 0 -> T4, 1 -> T6; NodeCache::getCachedNodes picks cache_4 / cache_6 by
@@ -3557,10 +3588,9 @@ __global__ __launch_bounds__(BLOCK) void nc_line_kernel(DevTable T4, DevTable T6
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x, lane = threadIdx.x & 63u, tid = threadIdx.x;
     const bool act = i < q;
     const bool fam = DUAL && act && af[i] != 0;
-    __shared__ uint4 stg[BLOCK / 64][64][9];  // a wave's 64 line halves (8 pieces + 1 pad); afterwards the rows
-    __shared__ uint8_t mrow[BLOCK];
-    __shared__ uint32_t okm[BLOCK / 32];
-    if (tid < BLOCK / 32) okm[tid] = 0;
+    // a wave's 64 line halves, piece p of line q at [q][p ^ (q & 7)] (the XOR spreads a lane's 16-byte reads over
+    // the banks without a pad: 8 KB per wave, 5 waves per SIMD); afterwards the wave's rows
+    __shared__ uint4 stg[BLOCK / 64][64][8];  // 32 KB: five blocks per CU
     Target t{};
     bool ok = false;
     uint32_t m = 0, sl = NONE;  // this lane's line: radix slot | family << 31 (NONE: no line)
@@ -3592,14 +3622,14 @@ __global__ __launch_bounds__(BLOCK) void nc_line_kernel(DevTable T4, DevTable T6
         ld[r] = a;
         ld[8 + r] = b;
     }
-    uint4 (*S)[9] = stg[tid >> 6];  // this wave's region: only wave-level ordering is needed
+    uint4 (*S)[8] = stg[tid >> 6];  // this wave's region: only wave-level ordering is needed
 #pragma unroll
     for (int h = 0; h < 2; h++) {
 #pragma unroll
-        for (int r = 0; r < 8; r++) S[8 * r + (lane >> 3)][lane & 7] = ld[8 * h + r];
+        for (int r = 0; r < 8; r++) S[8 * r + (lane >> 3)][(lane & 7) ^ ((lane >> 3) & 7)] = ld[8 * h + r];
         wave_sync();
 #pragma unroll
-        for (int x = 0; x < 8; x++) L[8 * h + x] = S[lane][x];
+        for (int x = 0; x < 8; x++) L[8 * h + x] = S[lane][x ^ (lane & 7)];
         wave_sync();
     }
     // the wave's rows (64 x 16 words) reuse its region: row r of the block at rows + NCL_WROWS(r)
@@ -3617,11 +3647,9 @@ __global__ __launch_bounds__(BLOCK) void nc_line_kernel(DevTable T4, DevTable T6
         }
     }
     if (act && ok && out_cnt) out_cnt[i] = (uint8_t)m;
-    mrow[tid] = (uint8_t)m;
+    rows[(tid >> 6) * 2048u + 1024u + lane] = m | (ok ? 256u : 0u);  // the row's meta word (its wave's region)
     __syncthreads();
-    if (ok) atomicOr(&okm[tid >> 5], 1u << (tid & 31));
-    __syncthreads();
-    store_rows_lds16(out_idx, q, count, rows, mrow, okm, true);
+    store_rows_wave16(out_idx, q, count, rows);
     // the lanes the lines could not answer: one query at a time by the whole wave (nc_answer: 32-node
     // runs each side of lb, itself falling back to lane 0's serial walk)
     uint64_t pend = ABL ? 0ull : __ballot(act && !ok);
