@@ -615,6 +615,17 @@ def allgather_pass(args, world, rank, local, dev, dist):
     if dist:
         dist.barrier()
     t_max = max_over_ranks(dist, time.perf_counter() - t_start, dev)
+    shard_path = None
+    if world == 1:  # the shard kernel + scatter on the whole table: each rank's local work at N > 1
+        for j in range(2):
+            G.query(tgs[K + j], cnt_k, out_idx=out_idx, out_cnt=out_cnt, single_rank_shard_kernel=True)
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        for j in range(K):
+            G.query(tgs[j], cnt_k, out_idx=out_idx, out_cnt=out_cnt, single_rank_shard_kernel=True)
+        torch.cuda.synchronize(dev)
+        shard_path = {"ms_per_step": (time.perf_counter() - t1) / K * 1e3,
+                      "how": "N = 1 through kad_rt_shard_batch + kad_rt_scatter_rows instead of the plain batch"}
     # bytes gathered per step (the all-gather payload of every rank, summed)
     rows, parts = G.local_compact(tgs[0], cnt_k) if world > 1 else (None, None)
     gathered = None
@@ -630,8 +641,9 @@ def allgather_pass(args, world, rank, local, dev, dist):
             "ms_per_step": t_max / K * 1e3, "scaling": "strong",
             "workload": f"100M-node U(24) table, 1/{world} per GPU without halo ({n_local} nodes on rank 0), "
                         f"{Q} global queries per step (a distinct batch per step, replicated on every rank), "
-                        f"k={cnt_k}; kad_rt_shard_batch + RCCL all-gather of rows/parts + scatter/merge",
-            "gathered_bytes_per_step": gathered, "setup_s": setup}
+                        f"k={cnt_k}; " + ("kad_rt_shard_batch + RCCL all-gather of rows/parts + scatter/merge"
+                                          if world > 1 else "one rank holds the whole table: the plain batch"),
+            "gathered_bytes_per_step": gathered, "setup_s": setup, "shard_kernel_path": shard_path}
 
 
 def main_allgather_line(args):

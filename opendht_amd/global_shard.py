@@ -135,9 +135,11 @@ class GlobalShard:
         valid = torch.cat([rows[r * cap:r * cap + int(c[r])] for r in range(REGIONS)])
         return valid, parts[:int(c[8])]
 
-    def query(self, targets, count: int, group=None, out_idx=None, out_cnt=None):
+    def query(self, targets, count: int, group=None, out_idx=None, out_cnt=None, single_rank_shard_kernel=False):
         """Every query's RoutingTable::findClosestNodes result on every rank: local rows and parts,
-        all-gather (RCCL / gloo), device scatter and merge."""
+        all-gather (RCCL / gloo), device scatter and merge. A single rank holds the whole table: the
+        exchange is empty and the batch is the plain kad_rt_closest_batch (single_rank_shard_kernel:
+        the shard kernel and the scatter instead, what each rank runs at N > 1 minus the exchange)."""
         import torch
         import torch.distributed as dist
 
@@ -154,6 +156,8 @@ class GlobalShard:
         if world == 1:
             if (self.lo, self.hi) != (0, self.GB):
                 raise ValueError("a single rank must hold the whole table")
+            if not single_rank_shard_kernel:
+                return self.table.rt_closest(targets, count, out_idx=out_idx, out_cnt=out_cnt)
             # one shard = the whole table: every window is complete, no parts, no host sync
             rows, _, ctr = self.local(targets, count)
             check(lib().kad_rt_scatter_rows(ptr(rows), ptr(ctr), CSTRIDE, REGIONS, self._cap[2], count, ptr(out_idx),

@@ -84,11 +84,12 @@ def test_global_shards_simulated_gather(gpu, case):
                 g_parts = torch.stack([torch.cat([o[1], o[1].new_zeros((maxp - o[1].shape[0], o[1].shape[1]))])
                                        for o in outs])
                 merge_parts(g_parts, npart, count, out_idx, out_cnt, gpu.index or 0)
-            if n_shards == 1:  # the no-sync single-rank path
-                i2, c2 = shards[0].query(tg, count)
-                torch.cuda.synchronize()
-                np.testing.assert_array_equal(i2.cpu().numpy(), out_idx.cpu().numpy())
-                np.testing.assert_array_equal(c2.cpu().numpy(), out_cnt.cpu().numpy())
+            if n_shards == 1:  # the single-rank paths: the plain batch, the shard kernel without host sync
+                for sk in (False, True):
+                    i2, c2 = shards[0].query(tg, count, single_rank_shard_kernel=sk)
+                    torch.cuda.synchronize()
+                    np.testing.assert_array_equal(i2.cpu().numpy(), out_idx.cpu().numpy())
+                    np.testing.assert_array_equal(c2.cpu().numpy(), out_cnt.cpu().numpy())
             torch.cuda.synchronize()
             want, wcnt = O.flat_rt_closest(gids, gst, gfirst, goff, targets, count, nthreads=8)
             np.testing.assert_array_equal(out_cnt.cpu().numpy(), wcnt, err_msg=f"{case} k={count} counts")
