@@ -154,7 +154,8 @@ int kad_table_refresh_status(kad_table* t, int64_t now_ns, void* stream);
  * of three uint32 (kind, a, b) applied in order; `a` names a node by its index at the start of
  * the batch, `b` / `a` of INSERT a slot of the batch's new nodes (new_ids / new_status, host):
  *   KAD_OP_REMOVE  a     node a leaves its bucket (Dht::expireBuckets, dht.cpp:942-956)
- *   KAD_OP_REPLACE a b   new node b takes node a's place (onNewNode's expired slot, dht.cpp:917-921)
+ *   KAD_OP_REPLACE a b   new node b takes node a's place (onNewNode's expired slot, dht.cpp:917-921);
+ *                        b must belong to a's bucket (findBucket(id_b)), else KAD_ERR_INVALID
  *   KAD_OP_INSERT  a     new node a is emplace_front'ed into findBucket(id) (dht.cpp:934)
  *   KAD_OP_SPLIT   a     RoutingTable::split of the bucket at current index a (routing_table.cpp:137-163;
  *                        nodes re-spliced to the front of their new bucket: list order reverses)

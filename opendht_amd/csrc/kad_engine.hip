@@ -51,6 +51,7 @@
 #include <vector>
 
 #include "../../include/kadgpu.h"
+#include "kad_mirror_plan.h"
 
 #define KAD_VERSION 100  // 0.1.0
 
@@ -3982,10 +3983,8 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) v
 // bucket an explicit handle list), then re-derives masks, prefix sums, dup masks and lines on the
 // device. Handles: old node index, or MIRROR_NEW | slot for a node of the batch.
 // ---------------------------------------------------------------------------
-constexpr uint32_t MIRROR_NEW = 0x80000000u;
-struct MirrorSeg {
-    uint32_t start, src, len, kind;  // kind 0: old nodes src.., 1: handles list[src..]
-};
+using kadplan::MIRROR_NEW;
+using kadplan::MirrorSeg;
 
 __global__ void mirror_gather_kernel(const MirrorSeg* __restrict__ seg, uint32_t nseg, const uint32_t* __restrict__ list,
                                      uint32_t n_out, const uint64_t* __restrict__ okey, const uint32_t* __restrict__ otail,
@@ -5750,15 +5749,6 @@ int make_bucket_index(const std::vector<uint8_t>& h_first, uint32_t B, BucketInd
     return KAD_OK;
 }
 
-inline int lowbit20(const uint8_t* p) {  // InfoHash::lowbit (infohash.h:84-95), -1 for zero
-    for (int i = 19; i >= 0; i--)
-        if (p[i]) {
-            for (int j = 7; j >= 0; j--)
-                if (p[i] & (0x80 >> j)) return 8 * i + j;
-        }
-    return -1;
-}
-
 }  // namespace
 
 extern "C" {
@@ -5780,196 +5770,36 @@ int kad_table_apply(kad_table* t, const uint32_t* ops, uint32_t n_ops, const uin
         std::fprintf(stderr, "kad_table_apply %s: %.3f ms\n", what, std::chrono::duration<double, std::milli>(now - tp).count());
         tp = now;
     };
-    // Sparse plan: an origin bucket (a bucket of the table as it is now) that an op touches gets the list of its
-    // current buckets (splits add some), each an untouched range of old nodes (raw) or an explicit handle list;
-    // every other origin stays one untouched range. Host work is proportional to the batch, except the new
-    // offsets and the bucket directory (simple O(buckets) passes).
-    struct PB {
-        bool raw;
-        uint32_t src, len;
-        std::vector<uint32_t> h;
-        std::array<uint8_t, 20> first;
-    };
+    // the host plan (kad_mirror_plan.cpp): the new layout as segments of old-node ranges and handle lists
     const std::vector<uint32_t>& off0 = t->h_off;
     const uint8_t* first0 = t->h_first.data();
-    std::unordered_map<uint32_t, std::vector<PB>> tb;  // touched origin -> its current buckets
-    std::map<uint32_t, uint32_t> extra;                // split origin -> buckets its splits added
-    uint32_t Bcur = B0;
-    auto touch = [&](uint32_t o) -> std::vector<PB>& {
-        auto it = tb.find(o);
-        if (it == tb.end()) {
-            PB p{true, off0[o], off0[o + 1] - off0[o], {}, {}};
-            std::memcpy(p.first.data(), first0 + 20ull * o, 20);
-            it = tb.emplace(o, std::vector<PB>(1, std::move(p))).first;
+    kadplan::MirrorPlan plan;
+    std::string perr;
+    const kadplan::OldIds old_ids = [&](uint32_t a, uint32_t e, uint8_t* out) -> int {  // IDs of old nodes [a, e)
+        std::vector<uint64_t> k(e - a);
+        std::vector<uint32_t> tl(3ull * (e - a));
+        HIP_TRY(hipMemcpy(k.data(), d.key + a, 8ull * (e - a), hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(tl.data(), d.tail + 3ull * a, 12ull * (e - a), hipMemcpyDeviceToHost));
+        for (uint32_t i = 0; i < e - a; i++) {
+            uint8_t* b = out + 20ull * i;
+            for (int x = 0; x < 8; x++) b[x] = (uint8_t)(k[i] >> (56 - 8 * x));
+            for (int w = 0; w < 3; w++)
+                for (int x = 0; x < 4; x++) b[8 + 4 * w + x] = (uint8_t)(tl[3ull * i + w] >> (24 - 8 * x));
         }
-        return it->second;
-    };
-    auto mat = [](PB& p) {
-        if (p.raw) {
-            p.h.resize(p.len);
-            for (uint32_t i = 0; i < p.len; i++) p.h[i] = p.src + i;
-            p.raw = false;
-        }
-    };
-    // current bucket index c -> (origin, index among the origin's current buckets)
-    auto origin_of = [&](uint32_t c, uint32_t& o, uint32_t& sub) {
-        uint32_t shift = 0;  // buckets added by the splits of the origins below
-        for (const auto& e : extra) {
-            if (c < e.first + shift) break;
-            if (c <= e.first + shift + e.second) { o = e.first; sub = c - e.first - shift; return; }
-            shift += e.second;
-        }
-        o = c - shift;
-        sub = 0;
-    };
-    // IDs of old nodes, downloaded per origin bucket on first use (splits only)
-    std::unordered_map<uint32_t, uint32_t> oid_at;
-    std::vector<uint8_t> oid;
-    auto id_of = [&](uint32_t h, uint32_t origin, uint8_t* out) -> int {
-        if (h & MIRROR_NEW) { std::memcpy(out, new_ids + 20ull * (h & ~MIRROR_NEW), 20); return KAD_OK; }
-        auto it = oid_at.find(origin);
-        if (it == oid_at.end()) {
-            const uint32_t a = off0[origin], e = off0[origin + 1];
-            std::vector<uint64_t> k(e - a);
-            std::vector<uint32_t> tl(3ull * (e - a));
-            if (e > a) {
-                HIP_TRY(hipMemcpy(k.data(), d.key + a, 8ull * (e - a), hipMemcpyDeviceToHost));
-                HIP_TRY(hipMemcpy(tl.data(), d.tail + 3ull * a, 12ull * (e - a), hipMemcpyDeviceToHost));
-            }
-            it = oid_at.emplace(origin, (uint32_t)(oid.size() / 20)).first;
-            for (uint32_t i = 0; i < e - a; i++) {
-                uint8_t b[20];
-                for (int x = 0; x < 8; x++) b[x] = (uint8_t)(k[i] >> (56 - 8 * x));
-                for (int w = 0; w < 3; w++)
-                    for (int x = 0; x < 4; x++) b[8 + 4 * w + x] = (uint8_t)(tl[3ull * i + w] >> (24 - 8 * x));
-                oid.insert(oid.end(), b, b + 20);
-            }
-        }
-        std::memcpy(out, oid.data() + 20ull * (it->second + (h - off0[origin])), 20);
         return KAD_OK;
     };
-    // node a (index at the batch start) -> its origin, current bucket and position
-    auto locate = [&](uint32_t a, uint32_t& o, uint32_t& sub, uint32_t& pos) -> bool {
-        if (a >= n0) return false;
-        o = (uint32_t)(std::upper_bound(off0.begin(), off0.end(), a) - off0.begin()) - 1;
-        auto it = tb.find(o);
-        if (it == tb.end()) { sub = 0; pos = a - off0[o]; return true; }
-        for (sub = 0; sub < it->second.size(); sub++) {
-            const PB& p = it->second[sub];
-            if (p.raw) {
-                if (a >= p.src && a < p.src + p.len) { pos = a - p.src; return true; }
-            } else {
-                auto f = std::find(p.h.begin(), p.h.end(), a);
-                if (f != p.h.end()) { pos = (uint32_t)(f - p.h.begin()); return true; }
-            }
-        }
-        return false;
-    };
+    const bool wl_table = (d.flags & TF_WL) != 0;
+    int rc = kadplan::mirror_plan(off0, first0, n0, ops, n_ops, new_ids, n_new, wl_table ? (int)d.rshift : -1,
+                                  wl_table ? d.rbase >> d.rshift : 0, old_ids, plan, perr);
+    if (rc) return perr.empty() ? rc : set_err(rc, "%s", perr.c_str());
     const bool structural = n_ops > 0;  // node indices move: the NodeCache radix no longer applies
-    for (uint32_t k = 0; k < n_ops; k++) {
-        const uint32_t kind = ops[3ull * k], a = ops[3ull * k + 1], b = ops[3ull * k + 2];
-        uint32_t o = 0, sub = 0, pos = 0;
-        if (kind == KAD_OP_REMOVE || kind == KAD_OP_REPLACE) {
-            if (!locate(a, o, sub, pos)) return set_err(KAD_ERR_INVALID, "op %u: node %u is not in the table", k, a);
-            if (kind == KAD_OP_REPLACE && b >= n_new) return set_err(KAD_ERR_INVALID, "op %u: new slot %u", k, b);
-            PB& p = touch(o)[sub];
-            mat(p);
-            if (kind == KAD_OP_REMOVE) p.h.erase(p.h.begin() + pos);
-            else p.h[pos] = MIRROR_NEW | b;
-        } else if (kind == KAD_OP_INSERT) {
-            if (a >= n_new) return set_err(KAD_ERR_INVALID, "op %u: new slot %u", k, a);
-            // RoutingTable::findBucket (routing_table.cpp:113-127): last bucket with first <= id
-            const uint8_t* id = new_ids + 20ull * a;
-            uint32_t lo = 0, hi = B0;
-            while (lo < hi) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if (std::memcmp(first0 + 20ull * mid, id, 20) <= 0) lo = mid + 1; else hi = mid;
-            }
-            o = lo ? lo - 1 : 0;
-            std::vector<PB>& v = touch(o);
-            sub = 0;
-            while (sub + 1 < v.size() && std::memcmp(v[sub + 1].first.data(), id, 20) <= 0) sub++;
-            mat(v[sub]);
-            v[sub].h.insert(v[sub].h.begin(), MIRROR_NEW | a);  // emplace_front (dht.cpp:934)
-        } else if (kind == KAD_OP_SPLIT) {
-            if (a >= Bcur) return set_err(KAD_ERR_INVALID, "op %u: bucket %u of %u", k, a, Bcur);
-            origin_of(a, o, sub);
-            std::vector<PB>& v = touch(o);
-            // RoutingTable::depth / middle / split (routing_table.cpp:47-65, 137-163)
-            const uint8_t* nf = sub + 1 < v.size() ? v[sub + 1].first.data() : o + 1 < B0 ? first0 + 20ull * (o + 1) : nullptr;
-            const int b1 = lowbit20(v[sub].first.data()), b2 = nf ? lowbit20(nf) : -1;
-            const int depth = std::max(b1, b2) + 1;
-            if (depth >= 160) continue;  // middle() throws: split returns false
-            std::array<uint8_t, 20> mid = v[sub].first;
-            mid[depth / 8] |= (uint8_t)(0x80 >> (depth % 8));
-            mat(v[sub]);
-            std::vector<uint32_t> keep, move;
-            for (uint32_t h : v[sub].h) {  // splice each node to the FRONT of its new bucket
-                uint8_t id[20];
-                int rc = id_of(h, o, id);
-                if (rc) return rc;
-                auto& dst = std::memcmp(id, mid.data(), 20) >= 0 ? move : keep;
-                dst.insert(dst.begin(), h);
-            }
-            v[sub].h = std::move(keep);
-            v.insert(v.begin() + sub + 1, PB{false, 0, 0, std::move(move), mid});
-            extra[o]++;
-            Bcur++;
-        } else {
-            return set_err(KAD_ERR_INVALID, "op %u: unknown kind %u", k, kind);
-        }
-    }
-    phase("plan (ops)");
-    std::vector<uint32_t> tk;  // touched origins, ascending
-    tk.reserve(tb.size());
-    for (const auto& e : tb) tk.push_back(e.first);
-    std::sort(tk.begin(), tk.end());
-    // window lines need every node inside its bucket's dyadic range: check the new nodes
-    bool lines_ok = (d.flags & TF_WL) && Bcur == B0;
-    if (lines_ok) {
-        const uint64_t pre0 = d.rbase >> d.rshift;
-        for (uint32_t o : tk)
-            for (const PB& p : tb[o])
-                if (!p.raw)
-                    for (uint32_t h : p.h)
-                        if (h & MIRROR_NEW) lines_ok &= (id_hi(new_ids + 20ull * (h & ~MIRROR_NEW)) >> d.rshift) == pre0 + o;
-    }
-    // new layout: untouched origins between touched ones are one range of old nodes
-    const uint32_t B1 = Bcur;
-    std::vector<MirrorSeg> segs;
-    std::vector<uint32_t> list, off1(B1 + 1);
-    uint32_t acc = 0, c = 0, prev = 0;
-    auto raw_seg = [&](uint32_t src, uint32_t len) {
-        if (!len) return;
-        MirrorSeg* last = segs.empty() ? nullptr : &segs.back();
-        if (last && last->kind == 0 && last->src + last->len == src && last->start + last->len == acc) last->len += len;
-        else segs.push_back(MirrorSeg{acc, src, len, 0});
-    };
-    auto untouched = [&](uint32_t e) {  // origins [prev, e)
-        const uint32_t base = off0[prev];
-        for (uint32_t u = prev; u < e; u++) off1[c++] = acc + (off0[u] - base);
-        raw_seg(base, off0[e] - base);
-        acc += off0[e] - base;
-    };
-    for (uint32_t o : tk) {
-        untouched(o);
-        for (const PB& p : tb[o]) {
-            off1[c++] = acc;
-            const uint32_t len = p.raw ? p.len : (uint32_t)p.h.size();
-            if (p.raw) {
-                raw_seg(p.src, len);
-            } else if (len) {
-                segs.push_back(MirrorSeg{acc, (uint32_t)list.size(), len, 1});
-                list.insert(list.end(), p.h.begin(), p.h.end());
-            }
-            acc += len;
-        }
-        prev = o + 1;
-    }
-    untouched(B0);
-    off1[B1] = acc;
-    const uint32_t n1 = acc;
-    phase("layout (segments)");
+    // window lines need every node inside its bucket's dyadic range
+    const bool lines_ok = wl_table && plan.B1 == B0 && plan.new_in_range;
+    const uint32_t B1 = plan.B1, n1 = plan.n1;
+    std::vector<MirrorSeg>& segs = plan.segs;
+    std::vector<uint32_t>& list = plan.list;
+    std::vector<uint32_t>& off1 = plan.off1;
+    phase("plan (ops, layout)");
     // new nodes' device rows
     std::vector<uint64_t> nkey(n_new);
     std::vector<uint32_t> ntail(3ull * n_new);
@@ -5989,7 +5819,6 @@ int kad_table_apply(kad_table* t, const uint32_t* ops, uint32_t n_ops, const uin
     };
     MirrorSeg* dseg; uint32_t *dlist, *dntail, *dnidx, *dremap = nullptr; uint64_t* dnkey; uint8_t* dnst;
     uint64_t* key1; uint32_t* tail1; uint8_t* st1;
-    int rc;
     if ((rc = dev_upload(&dseg, segs.data(), segs.size(), tmp, tmpb)) ||
         (rc = dev_upload(&dlist, list.data(), list.size(), tmp, tmpb)) ||
         (rc = dev_upload(&dnkey, nkey.data(), n_new, tmp, tmpb)) ||
@@ -6026,19 +5855,8 @@ int kad_table_apply(kad_table* t, const uint32_t* ops, uint32_t n_ops, const uin
          (rc = dev_upload(&spart, nullptr, B1 + 1, fresh, freshb)) ||
          (rc = dev_upload(&ssums, nullptr, (B1 + 1 + SCAN_TILE - 1) / SCAN_TILE, fresh, freshb))))
         return fail(rc);
-    std::vector<uint8_t> first1;  // the new bucket firsts (only splits change them)
-    if (reshape) {
-        first1.resize(20ull * B1);
-        uint32_t j = 0, pv = 0;
-        for (uint32_t o : tk) {
-            if (o > pv) std::memcpy(first1.data() + 20ull * j, first0 + 20ull * pv, 20ull * (o - pv));
-            j += o - pv;
-            for (const PB& p : tb[o]) std::memcpy(first1.data() + 20ull * j++, p.first.data(), 20);
-            pv = o + 1;
-        }
-        if (B0 > pv) std::memcpy(first1.data() + 20ull * j, first0 + 20ull * pv, 20ull * (B0 - pv));
-        if ((rc = make_bucket_index(first1, B1, bix, fresh, freshb))) return fail(rc);
-    }
+    std::vector<uint8_t>& first1 = plan.first1;  // the new bucket firsts (only splits change them)
+    if (reshape && (rc = make_bucket_index(first1, B1, bix, fresh, freshb))) return fail(rc);
     const uint8_t* fnew = reshape ? first1.data() : first0;
     // duplicate top-64 masks of the new layout
     if ((rc = dev_upload(&ddm, nullptr, B1, fresh, freshb)) || (rc = dev_upload(&dany, nullptr, 1, tmp, tmpb)))

@@ -1,15 +1,19 @@
 // Host code under AddressSanitizer + UndefinedBehaviorSanitizer (CPU only, no GPU): the native table
 // builders of libkadgpu.so (opendht_amd/csrc/kad_synth.cpp: synthetic IDs and status, sort, U(d) and
-// split-policy tables, counter-based shards) and the CPU oracle (oracle/kad_oracle.cpp: both
+// split-policy tables, counter-based shards), the mirror's host plan (kad_mirror_plan.cpp, checked
+// against the oracle's std::list table after random op batches) and the CPU oracle (oracle/kad_oracle.cpp: both
 // restatements, NodeCache walk, mirror ops, swarm model, wire filter, SHA-1), compiled from source with
 // -fsanitize=address,undefined and exercised on tables from 0 to 60k nodes. Built and run by
 // tests/test_sanitizers.py (make -C tests/cpp sanitize_host). Exit 0 and "PASS" = no report.
+#include <algorithm>
 #include <cstdio>
 #include <cstring>
 #include <random>
+#include <string>
 #include <vector>
 
 #include "kadgpu.h"
+#include "../../opendht_amd/csrc/kad_mirror_plan.h"
 
 extern "C" {
 int orc_flat_rt_closest(uint32_t, const uint8_t*, const uint8_t*, uint32_t, const uint8_t*, const uint32_t*, uint32_t,
@@ -33,6 +37,88 @@ int orc_infohash_get(uint32_t, const uint8_t*, const uint64_t*, uint8_t*);
 
 static int fails = 0;
 #define EXPECT(c, ...) do { if (!(c)) { fails++; std::fprintf(stderr, __VA_ARGS__); std::fprintf(stderr, "\n"); } } while (0)
+
+// Random batches of removals, replacements, insertions and splits: kad_table_apply's host plan, with its
+// segments resolved to IDs on the host, against orc_table_apply on the structure-faithful table.
+static void check_mirror_plan(std::mt19937_64& g, uint32_t n, const std::vector<uint8_t>& sid,
+                              const std::vector<uint8_t>& sst, uint32_t B, const std::vector<uint8_t>& first,
+                              const std::vector<uint32_t>& off) {
+    const std::vector<uint32_t> off0(off.begin(), off.begin() + B + 1);
+    for (int trial = 0; trial < 6; trial++) {
+        const uint32_t n_new = 1 + (uint32_t)(g() % 40), n_rm = (uint32_t)(g() % 30), n_split = (uint32_t)(g() % 6);
+        std::vector<uint8_t> nid(20ull * n_new), nst(n_new, 1);
+        for (auto& x : nid) x = (uint8_t)g();
+        std::vector<uint32_t> pick(n);  // distinct old nodes for removals / replacements
+        for (uint32_t i = 0; i < n; i++) pick[i] = i;
+        std::shuffle(pick.begin(), pick.end(), g);
+        std::vector<uint32_t> ops;
+        uint32_t used = 0, slot = 0;
+        for (uint32_t r = 0; r < n_rm && used < n; r++) ops.insert(ops.end(), {KAD_OP_REMOVE, pick[used++], 0});
+        for (; slot < n_new / 2 && used < n; slot++) {  // the new ID: the old one's top 96 bits (same bucket)
+            std::memcpy(&nid[20ull * slot], &sid[20ull * pick[used]], 12);
+            ops.insert(ops.end(), {KAD_OP_REPLACE, pick[used++], slot});
+        }
+        for (; slot < n_new; slot++) ops.insert(ops.end(), {KAD_OP_INSERT, slot, 0});
+        for (uint32_t s = 0; s < n_split; s++) ops.insert(ops.end(), {KAD_OP_SPLIT, (uint32_t)(g() % B), 0});
+        // shuffle the op rows (node operands stay batch-start indices)
+        const uint32_t n_ops = (uint32_t)(ops.size() / 3);
+        std::vector<uint32_t> ord(n_ops);
+        for (uint32_t i = 0; i < n_ops; i++) ord[i] = i;
+        std::shuffle(ord.begin(), ord.end(), g);
+        std::vector<uint32_t> rows(3ull * n_ops);
+        for (uint32_t i = 0; i < n_ops; i++) std::memcpy(&rows[3ull * i], &ops[3ull * ord[i]], 12);
+        kadplan::MirrorPlan plan;
+        std::string err;
+        const kadplan::OldIds old_ids = [&](uint32_t a, uint32_t e, uint8_t* out) {
+            std::memcpy(out, sid.data() + 20ull * a, 20ull * (e - a));
+            return KAD_OK;
+        };
+        const int rc = kadplan::mirror_plan(off0, first.data(), n, rows.data(), n_ops, nid.data(), n_new, -1, 0, old_ids,
+                                            plan, err);
+        EXPECT(rc == KAD_OK, "mirror plan n=%u: %s", n, err.c_str());
+        if (rc) continue;
+        if (trial == 0 && B > 1 && off[1] > 0 && off[B] > off[B - 1]) {  // a replacement from another bucket is refused
+            std::vector<uint8_t> far(sid.begin() + 20ull * off[B - 1], sid.begin() + 20ull * off[B - 1] + 20);
+            far[19] ^= 1;
+            const uint32_t bad[] = {KAD_OP_REPLACE, 0, 0};
+            kadplan::MirrorPlan p2;
+            std::string e2;
+            EXPECT(kadplan::mirror_plan(off0, first.data(), n, bad, 1, far.data(), 1, -1, 0, old_ids, p2, e2) ==
+                       KAD_ERR_INVALID,
+                   "out-of-bucket replacement accepted n=%u", n);
+        }
+        // the plan's layout as IDs
+        std::vector<uint8_t> got(20ull * plan.n1 + 1);
+        uint32_t at = 0;
+        for (const auto& sg : plan.segs) {
+            EXPECT(sg.start == at, "segment start %u, expected %u", sg.start, at);
+            for (uint32_t i = 0; i < sg.len; i++) {
+                const uint32_t h = sg.kind ? plan.list[sg.src + i] : sg.src + i;
+                const uint8_t* src = h & kadplan::MIRROR_NEW ? nid.data() + 20ull * (h & ~kadplan::MIRROR_NEW)
+                                                             : sid.data() + 20ull * h;
+                std::memcpy(&got[20ull * at++], src, 20);
+            }
+        }
+        EXPECT(at == plan.n1, "segments cover %u of %u nodes", at, plan.n1);
+        // the same ops on the oracle
+        void* T = orc_table_build(n, sid.data(), sst.data(), B, first.data(), off.data(), 1);
+        const uint32_t cap = n + n_new + 1, capB = B + n_split + 1;
+        std::vector<uint8_t> oid(20ull * cap), ost(cap), of(20ull * capB);
+        std::vector<uint32_t> oo(capB + 1), rm(n + 1), ni(n_new);
+        uint32_t on = 0, oB = 0;
+        orc_table_apply(T, n_ops, rows.data(), n_new, nid.data(), nst.data(), &on, &oB, oid.data(), ost.data(), of.data(),
+                        oo.data(), rm.data(), ni.data());
+        orc_table_free(T);
+        const uint8_t* f1 = plan.B1 != B ? plan.first1.data() : first.data();
+        EXPECT(on == plan.n1 && oB == plan.B1, "mirror plan n=%u trial %d: %u nodes / %u buckets, oracle %u / %u", n, trial,
+               plan.n1, plan.B1, on, oB);
+        if (on == plan.n1 && oB == plan.B1) {
+            EXPECT(std::memcmp(got.data(), oid.data(), 20ull * on) == 0, "mirror plan n=%u trial %d: node order", n, trial);
+            EXPECT(std::equal(oo.begin(), oo.begin() + oB + 1, plan.off1.begin()), "mirror plan n=%u: offsets", n);
+            EXPECT(std::memcmp(f1, of.data(), 20ull * oB) == 0, "mirror plan n=%u: firsts", n);
+        }
+    }
+}
 
 int main() {
     std::mt19937_64 g(11);
@@ -80,6 +166,7 @@ int main() {
             }
             orc_table_free(T);
         }
+        if (n >= 50) check_mirror_plan(g, n, sid, sst, B, first, off);
         // uniform buckets + NodeCache walk over the sorted array
         std::vector<uint8_t> srt(ids.begin(), ids.begin() + 20ull * n);
         srt.push_back(0);
