@@ -8,10 +8,11 @@ Per rank s (one process per GPU):
   * the GLOBAL good prefix sums (4 bytes per global bucket) are all-gathered once at setup, so the
     rank can compute any query's global window W(R) (routing_table.cpp:89-104);
   * a step: kad_rt_shard_batch over the replicated batch appends complete rows (W(R) inside the
-    shard) and partial rows (W(R) crossing an edge, with XOR distances); the ranks' rows are
-    all-gathered, kad_rt_scatter_rows writes them, kad_rt_merge_parts merges the parts. Every
-    rank ends with every query's result, bit-exact with RoutingTable::findClosestNodes on the
-    whole table.
+    shard) and partial rows (W(R) crossing an edge, with XOR distances); the ranks' counters are
+    all-gathered (one small collective, one host read), then one payload per rank (its rows, then
+    its parts) in one all_gather_into_tensor; kad_rt_scatter_rows writes the rows straight from
+    the received buffer, kad_rt_merge_parts merges the parts. Every rank ends with every query's
+    result, bit-exact with RoutingTable::findClosestNodes on the whole table.
 
 The owner-routed halo variant (sharded.py) moves only results a client asked for; this variant
 is the one the north star describes and config 3 names ("RCCL all-gather + top-k merge").
@@ -163,14 +164,63 @@ class GlobalShard:
             check(lib().kad_rt_scatter_rows(ptr(rows), ptr(ctr), CSTRIDE, REGIONS, self._cap[2], count, ptr(out_idx),
                                             ptr(out_cnt), self.device, s), "kad_rt_scatter_rows")
             return out_idx, out_cnt
-        rows, parts = self.local_compact(targets, count)
-        g_rows, counts = allgather_padded(rows, rows.shape[0], group)
-        n_rows = torch.tensor(counts, dtype=torch.int32, device=self.dev)
-        check(lib().kad_rt_scatter_rows(ptr(g_rows), ptr(n_rows), 1, world, g_rows.shape[1], count, ptr(out_idx),
+        rw, pw = row_words(count), part_words(count)
+        while True:  # every rank's counters in one small gather, read once on the host
+            rows, parts, ctr = self.local(targets, count)
+            c_all = torch.empty((world, COUNTERS), dtype=torch.int32, device=self.dev)
+            gather_into(c_all.view(-1), ctr[::CSTRIDE][:COUNTERS].contiguous(), group)
+            c = c_all.cpu().numpy()
+            if not c[:, 9].any():
+                break
+            if (c[:, :REGIONS] > self._cap[2]).any():
+                raise RuntimeError("kad_rt_shard_batch: row region overflow")
+            # a part buffer overflowed somewhere: every rank grows its buffer and runs again
+            self._buffers(q, count, part_cap=2 * int(c[:, 8].max()))
+        n_r = c[:, :REGIONS].sum(axis=1)
+        maxr, maxp = int(n_r.max()), int(c[:, 8].max())
+        # one payload per rank: its rows, then its parts, padded to block_cap rows of rw words
+        block_cap = maxr + -(-maxp * pw // rw)
+        send = torch.empty((block_cap * rw,), dtype=torch.int32, device=self.dev)
+        cap, at = self._cap[2], 0
+        for r in range(REGIONS):
+            n = int(c[rank_of(group), r])
+            send[at:at + n * rw] = rows[r * cap:r * cap + n].reshape(-1)
+            at += n * rw
+        n_p = int(c[rank_of(group), 8])
+        send[maxr * rw:maxr * rw + n_p * pw] = parts[:n_p].reshape(-1)
+        recv = torch.empty((world * block_cap * rw,), dtype=torch.int32, device=self.dev)
+        gather_into(recv, send, group)
+        n_rows = torch.from_numpy(n_r.astype(np.int32)).to(self.dev)
+        check(lib().kad_rt_scatter_rows(ptr(recv), ptr(n_rows), 1, world, block_cap, count, ptr(out_idx),
                                         ptr(out_cnt), self.device, s), "kad_rt_scatter_rows")
-        g_parts, pcounts = allgather_padded(parts, parts.shape[0], group)
-        merge_parts(g_parts, pcounts, count, out_idx, out_cnt, self.device)
+        if maxp:
+            g = recv.view(world, block_cap * rw)
+            valid = torch.cat([g[r, maxr * rw:maxr * rw + int(c[r, 8]) * pw].view(-1, pw) for r in range(world)
+                               if c[r, 8]])
+            merge_valid_parts(valid, count, out_idx, out_cnt, self.device)
         return out_idx, out_cnt
+
+
+def gather_into(recv, send, group=None):
+    """recv (world * send.numel(),) <- every rank's send, in rank order: one all_gather_into_tensor on RCCL;
+    a list all-gather elsewhere (gloo, which stages device tensors through the host)."""
+    import torch
+    import torch.distributed as dist
+
+    if dist.get_backend(group) == "nccl":
+        dist.all_gather_into_tensor(recv, send, group=group)
+    else:
+        out = list(recv.view(dist.get_world_size(group), -1).unbind(0))
+        tmp = [torch.empty_like(send) for _ in out]
+        dist.all_gather(tmp, send, group=group)
+        for o, t in zip(out, tmp):
+            o.copy_(t)
+
+
+def rank_of(group=None) -> int:
+    import torch.distributed as dist
+
+    return dist.get_rank(group)
 
 
 def merge_parts(g_parts, pcounts, count: int, out_idx, out_cnt, device: int):
@@ -179,7 +229,14 @@ def merge_parts(g_parts, pcounts, count: int, out_idx, out_cnt, device: int):
 
     if sum(pcounts) == 0:
         return
-    valid = torch.cat([g_parts[r, :n] for r, n in enumerate(pcounts) if n])
+    merge_valid_parts(torch.cat([g_parts[r, :n] for r, n in enumerate(pcounts) if n]), count, out_idx, out_cnt,
+                      device)
+
+
+def merge_valid_parts(valid, count: int, out_idx, out_cnt, device: int):
+    """Parts (n, part_words) of every rank, in any order: sorted by qid, merged by kad_rt_merge_parts."""
+    import torch
+
     order = torch.argsort(valid[:, 0], stable=True)
     valid = valid[order].contiguous()
     s = C.c_void_p(torch.cuda.current_stream(valid.device).cuda_stream)

@@ -131,7 +131,7 @@ def _gather_worker(rank, world, port, q):
     sys.path[:0] = [os.path.dirname(here), here]
     import torch.distributed as dist
 
-    from opendht_amd.global_shard import allgather_padded, global_good_prefix
+    from opendht_amd.global_shard import allgather_padded, gather_into, global_good_prefix
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -144,6 +144,9 @@ def _gather_worker(rank, world, port, q):
         for r in range(world):
             exp = torch.arange(100 * 6, dtype=torch.int32).reshape(100, 6)[:counts[r]] + 1000 * r
             ok = ok and torch.equal(g[r, :counts[r]], exp)
+        recv = torch.full((world * 7,), -1, dtype=torch.int32)
+        gather_into(recv, torch.arange(7, dtype=torch.int32) + 100 * rank)
+        ok = ok and torch.equal(recv, torch.cat([torch.arange(7, dtype=torch.int32) + 100 * r for r in range(world)]))
         gp = global_good_prefix(np.full(5, rank + 1))
         ok = ok and np.array_equal(gp, np.concatenate([[0], np.cumsum(np.repeat(np.arange(1, world + 1), 5))]))
         q.put((rank, bool(ok)))
