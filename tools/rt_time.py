@@ -1,0 +1,31 @@
+"""RoutingTable::findClosestNodes timings on the bench shard (1/8 of the 100M-node U(24) table), 1M queries per
+launch over 8 rotated target batches, HIP events around 16 launches: counts 8, 14, 16, 17, 24, 32 (the 64-byte,
+128-byte and 256-byte window lines)."""
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from opendht_amd import DeviceTable  # noqa: E402
+from opendht_amd.sharded import build_shard, config3_spec  # noqa: E402
+
+NB, Q, REPS = 8, 1 << 20, 16
+dev = torch.device("cuda:0")
+spec = config3_spec()
+sh = build_shard(spec, 0)
+T = DeviceTable(sh.ids, sh.status, sh.first, sh.off, device=0, index_base=sh.index_base, sorted=True)
+tgs = [torch.from_numpy(spec.targets_for(0, Q, seed=0x0D470200 + j)).to(dev) for j in range(NB)]
+res = {}
+for k in (8, 14, 16, 17, 24, 32):
+    outs = [T.rt_closest(tgs[j], k) for j in range(NB)]
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for j in range(REPS):
+        T.rt_closest(tgs[j % NB], k, outs[j % NB][0], outs[j % NB][1])
+    b.record()
+    torch.cuda.synchronize()
+    res[f"rt_k{k}_us"] = round(a.elapsed_time(b) / REPS * 1e3, 1)
+print(json.dumps(res), flush=True)
