@@ -1298,8 +1298,9 @@ __device__ __forceinline__ void store_row16(uint32_t* row, const uint32_t (&o)[1
 // rows of 36..128 bytes (a 56-byte stride for count 14) left every store instruction part-filling its lines. Rows
 // whose lane takes the exact path (ok false) are skipped dword by dword; exact_tail writes them afterwards.
 template <int MAXK>  // count in 4..MAXK: a 16-byte chunk spans at most two rows
-__device__ __forceinline__ void store_rows_block_in(uint32_t* __restrict__ out_idx, uint32_t q, uint32_t count,
-                                                    const uint32_t (&o)[MAXK], bool ok, uint32_t* rows) {
+__device__ __forceinline__ void store_rows_block(uint32_t* __restrict__ out_idx, uint32_t q, uint32_t count,
+                                                 const uint32_t (&o)[MAXK], bool ok) {
+    __shared__ uint32_t rows[BLOCK * MAXK];
     __shared__ uint32_t okm[BLOCK / 32];
     const uint32_t tid = threadIdx.x, q0 = blockIdx.x * BLOCK;
     if (tid < BLOCK / 32) okm[tid] = 0;
@@ -1324,14 +1325,6 @@ __device__ __forceinline__ void store_rows_block_in(uint32_t* __restrict__ out_i
             }
         }
     }
-}
-
-// the same, with its own LDS rows (BLOCK * MAXK words)
-template <int MAXK>
-__device__ __forceinline__ void store_rows_block(uint32_t* __restrict__ out_idx, uint32_t q, uint32_t count,
-                                                 const uint32_t (&o)[MAXK], bool ok) {
-    __shared__ uint32_t rows[BLOCK * MAXK];
-    store_rows_block_in<MAXK>(out_idx, q, count, o, ok, rows);
 }
 
 __device__ bool wave_wl32(const DevTable& T, const Target& t, uint32_t b, uint32_t count, uint32_t lane, uint32_t* row,
@@ -1500,17 +1493,20 @@ __device__ __forceinline__ void merge32(uint32_t* a, const uint32_t* s) {
             if ((i & w) == 0) cx(a[i], a[i + w]);
 }
 
-// Wave-level LDS ordering (the rocPRIM wave barrier): the wave's LDS writes before it are seen by its reads after.
-__device__ __forceinline__ void wave_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-// the answer from bucket b's line L (in registers; ignored when !act)
-__device__ __forceinline__ bool wl32_answer_line(const DevTable& T, const Target& t, uint32_t b, uint32_t count, bool act,
-                                                 const uint32_t (&L)[WL32_STRIDE], uint32_t (&o)[32], uint32_t& m) {
-    uint32_t v[64];
+__device__ __forceinline__ bool wl32_answer(const DevTable& T, const Target& t, uint32_t b, uint32_t count, bool act,
+                                            uint32_t (&o)[32], uint32_t& m) {
+    uint32_t L[WL32_STRIDE], v[64];
+    if (act) {
+        const uint4* lp = T.wl32 + (WL32_STRIDE / 4) * (size_t)b;
+#pragma unroll
+        for (int x = 0; x < (int)WL32_STRIDE / 4; x++) {
+            const uint4 u = lp[x];
+            L[4 * x] = u.x; L[4 * x + 1] = u.y; L[4 * x + 2] = u.z; L[4 * x + 3] = u.w;
+        }
+    } else {
+#pragma unroll
+        for (int x = 0; x < (int)WL32_STRIDE; x++) L[x] = NONE;
+    }
     const uint32_t* H = L;
     const uint32_t d = 64 - T.rshift;
     const uint32_t h = H[3], S = (h >> 12) & 127u, R = (h >> 8) & 15u;
@@ -1557,23 +1553,6 @@ __device__ __forceinline__ bool wl32_answer_line(const DevTable& T, const Target
 #pragma unroll
     for (int j = 0; j < 32; j++) o[j] = (uint32_t)j < m ? base + (v[j] & 255u) : NONE;
     return !ex;
-}
-
-__device__ __forceinline__ bool wl32_answer(const DevTable& T, const Target& t, uint32_t b, uint32_t count, bool act,
-                                            uint32_t (&o)[32], uint32_t& m) {
-    uint32_t L[WL32_STRIDE];
-    if (act) {
-        const uint4* lp = T.wl32 + (WL32_STRIDE / 4) * (size_t)b;
-#pragma unroll
-        for (int x = 0; x < (int)WL32_STRIDE / 4; x++) {
-            const uint4 u = lp[x];
-            L[4 * x] = u.x; L[4 * x + 1] = u.y; L[4 * x + 2] = u.z; L[4 * x + 3] = u.w;
-        }
-    } else {
-#pragma unroll
-        for (int x = 0; x < (int)WL32_STRIDE; x++) L[x] = NONE;
-    }
-    return wl32_answer_line(T, t, b, count, act, L, o, m);
 }
 
 // Row of up to 32 indices: 16-byte stores for counts divisible by 4, 8-byte stores for even counts.
@@ -1634,7 +1613,7 @@ __device__ __forceinline__ void store_row32(uint32_t* row, const uint32_t (&o)[3
 __global__ __launch_bounds__(BLOCK) void rt_wl32_kernel(DevTable T, const uint8_t* __restrict__ targets, uint32_t q,
                                                         uint32_t count, uint32_t* __restrict__ out_idx,
                                                         uint8_t* __restrict__ out_cnt) {
-    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x, lane = threadIdx.x & 63u;
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     const bool act = i < q;
     Target t{};
     uint32_t b = 0;
@@ -1642,43 +1621,10 @@ __global__ __launch_bounds__(BLOCK) void rt_wl32_kernel(DevTable T, const uint8_
         t = load_target(targets, i);
         b = locate_bucket(T, t);
     }
-    // The wave loads its 64 lines together, 8 lanes per 128-byte half (one address translation per line per load,
-    // not 16), and hands each lane its line through LDS: piece p of line q at [q][p ^ (q & 7)] (no pad, 8 KB per
-    // wave per half). Afterwards the same 32 KB stage the block's rows.
-    __shared__ uint4 stg[BLOCK / 64][64][8];
-    const uint32_t sl = act ? b : NONE;
-    uint4 ld[16];
-#pragma unroll
-    for (int r = 0; r < 8; r++) {  // round r: lane L loads pieces (L & 7) and 8 + (L & 7) of query 8r + (L >> 3)'s line
-        const uint32_t so = (uint32_t)__shfl((int)sl, 8 * r + (int)(lane >> 3), 64);
-        uint4 x = make_uint4(0u, 0u, 0u, 0u), y = x;
-        if (so != NONE) {
-            const uint4* lp = T.wl32 + (WL32_STRIDE / 4) * (size_t)so;
-            x = lp[lane & 7];
-            y = lp[8 + (lane & 7)];
-        }
-        ld[r] = x;
-        ld[8 + r] = y;
-    }
-    uint4 (*S)[8] = stg[threadIdx.x >> 6];  // this wave's region: only wave-level ordering is needed
-    uint32_t L[WL32_STRIDE];
-#pragma unroll
-    for (int h = 0; h < 2; h++) {
-#pragma unroll
-        for (int r = 0; r < 8; r++) S[8 * r + (lane >> 3)][(lane & 7) ^ ((lane >> 3) & 7)] = ld[8 * h + r];
-        wave_sync();
-#pragma unroll
-        for (int x = 0; x < 8; x++) {
-            const uint4 u = S[lane][x ^ (lane & 7)];
-            L[32 * h + 4 * x] = u.x; L[32 * h + 4 * x + 1] = u.y; L[32 * h + 4 * x + 2] = u.z; L[32 * h + 4 * x + 3] = u.w;
-        }
-        wave_sync();
-    }
     uint32_t o[32], m;
-    const bool ok = wl32_answer_line(T, t, b, count, act, L, o, m);
+    const bool ok = wl32_answer(T, t, b, count, act, o, m);
     if (act && ok && out_cnt) out_cnt[i] = (uint8_t)m;
-    // store_rows_block_in syncs the block before its first row write: every wave has read its lines by then
-    store_rows_block_in<32>(out_idx, q, count, o, act && ok, reinterpret_cast<uint32_t*>(&stg[0][0][0]));
+    store_rows_block<32>(out_idx, q, count, o, act && ok);
     __shared__ uint64_t xs[BLOCK / 64][192];
     exact_tail(T, t, act && !ok, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
 }
@@ -3553,6 +3499,13 @@ __device__ __forceinline__ bool ncl_answer(const uint4 (&Lq)[16], uint32_t index
     m = min(count, have);
     ex |= have < count && (lim != NONE || w[31] != NONE);  // the walk goes on past the window / step 32
     return !ex;
+}
+
+// Wave-level LDS ordering (the rocPRIM wave barrier): the wave's LDS writes before it are seen by its reads after.
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 // Row r of the NodeCache line kernel's block inside its wave's staging region (64 x 8 uint4 = 2048 words per wave).

@@ -8,6 +8,10 @@ import sys
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import opendht_amd._lib as _kl  # noqa: E402
+
+if os.environ.get("RT_ABL"):  # A/B against another build placed as libkadgpu_abl.so
+    _kl.use_ablation_build()
 from opendht_amd import DeviceTable  # noqa: E402
 from opendht_amd.sharded import build_shard, config3_spec  # noqa: E402
 
