@@ -133,3 +133,29 @@ def test_dual_family_general_lines(gpu):
                 want, wcnt = O.flat_rt_closest(t["ids"], t["status"], t["first"], t["off"], targets[sel], k, nthreads=8)
                 np.testing.assert_array_equal(cnt[sel], wcnt, err_msg=f"af={fam} k={k} counts")
                 np.testing.assert_array_equal(idx[sel], want, err_msg=f"af={fam} k={k}")
+
+
+def test_general_lines_full_size_split_table(gpu):
+    """The reference split policy at the per-GPU size of config 3 (12.5M nodes, ~2M buckets of mixed depth):
+    1M random targets, EVERY query bit-exact against the oracle's closed form for k = 8 (slot lines), 14 and 16
+    (gl16 slot copies) and 32 (256-byte lines), plus the row properties (good, ascending XOR distance)."""
+    t = TB.split_config(12_500_000, seed=0x6C)
+    q = 1 << 20
+    g = torch.Generator(device=gpu).manual_seed(0x6C)
+    tg = torch.randint(0, 256, (q, 20), dtype=torch.uint8, device=gpu, generator=g)
+    targets = tg.cpu().numpy()
+    key = t["ids"][:, :8].copy().view(">u8").reshape(-1)
+    th = targets[:, :8].copy().view(">u8").reshape(-1)
+    with DeviceTable(t["ids"], t["status"], t["first"], t["off"], device=0) as T:
+        f = T.info()["flags"]
+        assert f & KAD_INFO_SLOT_LINES and f & KAD_INFO_SLOT_LINES16 and f & KAD_INFO_GENERAL_LINES32, hex(f)
+        for k in (8, 14, 16, 32):
+            idx, cnt = T.rt_closest(tg, k)
+            idx, cnt = idx.cpu().numpy().view(np.uint32), cnt.cpu().numpy()
+            want, wcnt = O.flat_rt_closest(t["ids"], t["status"], t["first"], t["off"], targets, k, nthreads=16)
+            np.testing.assert_array_equal(cnt, wcnt, err_msg=f"k={k} counts")
+            np.testing.assert_array_equal(idx, want, err_msg=f"k={k}")
+            assert (cnt == k).all()
+            assert (t["status"][idx] & 1).all()
+            d = key[idx] ^ th[:, None]
+            assert (d[:, 1:] >= d[:, :-1]).all()
