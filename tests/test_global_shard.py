@@ -12,6 +12,7 @@ import torch
 import torch.multiprocessing as mp
 
 import oracle as O
+from opendht_amd import DeviceTable
 from opendht_amd import synth as S
 from opendht_amd._lib import check, lib, ptr
 from opendht_amd.global_shard import GlobalShard, build_plain_shard, merge_parts, reach
@@ -99,6 +100,29 @@ def test_global_shards_simulated_gather(gpu, case):
     finally:
         for sh in shards:
             sh.close()
+
+
+@pytest.mark.gpu
+def test_whole_100M_table_one_gpu(gpu):
+    """The north-star table whole on one GPU (config 3's 100M-node U(24) table from the SURVEY §8d recipe, what
+    GlobalShard.query answers at N = 1): 1M random targets, EVERY query bit-exact against the oracle's closed
+    form for k = 8 and 14."""
+    from opendht_amd.sharded import config3_spec
+
+    spec = config3_spec(1)
+    ids, st, off, lo, hi, base, _ = build_plain_shard(spec, 0)
+    assert (lo, hi, base) == (0, spec.n_buckets, 0) and ids.shape[0] == 100_000_000
+    first = S.bucket_firsts(spec.depth, 0, spec.n_buckets)
+    q = 1 << 20
+    g = torch.Generator(device=gpu).manual_seed(0x100)
+    tg = torch.randint(0, 256, (q, 20), dtype=torch.uint8, device=gpu, generator=g)
+    targets = tg.cpu().numpy()
+    with DeviceTable(ids, st, first, off, device=gpu.index or 0, sorted=True) as T:
+        for k in (8, 14):
+            idx, cnt = T.rt_closest(tg, k)
+            want, wcnt = O.flat_rt_closest(ids, st, first, off, targets, k, nthreads=16)
+            np.testing.assert_array_equal(cnt.cpu().numpy(), wcnt, err_msg=f"k={k} counts")
+            np.testing.assert_array_equal(idx.cpu().numpy().view(np.uint32), want, err_msg=f"k={k}")
 
 
 def test_reach_covers_every_touching_bucket():
