@@ -476,13 +476,13 @@ def counts_pass(T, tgs, Q, dev, stream, reps=16):
 
 def host_pass(T, tgs, cnt_k, Q, dev, nb=8):
     """The PCIe-inclusive rate (targets in host memory, rows back to host memory; never the headline `value`):
-    `sync_abi`: kad_rt_closest_batch_host, the synchronous host-pointer call (device buffers allocated per call,
-    pageable copies); `pipelined`: pinned host buffers, H2D + kernel + D2H of consecutive batches on two
+    `sync_abi`: kad_rt_closest_batch_host, the synchronous host-pointer call on pageable buffers (the table's pinned
+    staging, chunks pipelined over four host threads); `pipelined`: pinned host buffers, H2D + kernel + D2H of consecutive batches on two
     streams so one batch's copies overlap the other's."""
     import torch
 
     ht = [tgs[j % len(tgs)].cpu().pin_memory() for j in range(4)]
-    hn = ht[0].numpy()
+    hn = ht[0].numpy().copy()  # pageable, as a caller's buffers are
     T.rt_closest_host(hn, cnt_k)  # warm
     ts = []
     for _ in range(3):
@@ -514,8 +514,9 @@ def host_pass(T, tgs, cnt_k, Q, dev, nb=8):
     bytes_q = 20 + 4 * cnt_k + 1
     return {"sync_abi_queries_per_s": Q / sync_s, "pipelined_queries_per_s": nb * Q / pipe_s,
             "pcie_bytes_per_query": bytes_q, "pipelined_GBs": nb * Q * bytes_q / pipe_s / 1e9,
-            "how": f"sync_abi: kad_rt_closest_batch_host over {Q} queries (pageable host buffers, device buffers "
-                   f"allocated per call), median of 3; pipelined: {nb} batches of {Q}, pinned host buffers, H2D + "
+            "how": f"sync_abi: kad_rt_closest_batch_host over {Q} queries (pageable host buffers in and out; "
+                   f"inside, 64k-query chunks through pinned staging on two streams per host thread, four threads), "
+                   f"median of 3; pipelined: {nb} batches of {Q}, pinned host buffers, H2D + "
                    "kernel + D2H per batch on two alternating streams, wall clock. Not the headline: the "
                    "boundary's device-pointer batch API is the path measured by `value`"}
 

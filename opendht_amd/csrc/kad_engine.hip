@@ -47,6 +47,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <thread>
 #include <string>
 #include <vector>
 
@@ -4476,6 +4477,35 @@ int dev_upload(T** dptr, const void* src, size_t count, std::vector<void*>& owne
 
 }  // namespace
 
+// Host-pointer batches (kad_*_closest_batch_host): pinned staging and device buffers kept with the table, and a
+// chunked pipeline per worker thread: host copy into pinned memory, H2D, kernel, D2H, host copy out. Each worker has
+// two slots on their own streams, so one slot's copies and kernel overlap the other slot's host copies, and the
+// workers split the batch so that the pageable host copies run on several cores.
+struct HostPipe {
+    static constexpr uint32_t CHUNK = 1u << 16;  // queries per slot
+    static constexpr int WORKERS = 4, SLOTS = 2;
+    struct Slot {
+        uint8_t *ht = nullptr, *hc = nullptr, *dt = nullptr, *dc = nullptr;  // pinned / device: targets, counts
+        uint32_t *hi = nullptr, *di = nullptr;                               // pinned / device: indices
+        hipStream_t s = nullptr;
+        hipEvent_t done = nullptr;
+        uint32_t c0 = 0, n = 0;
+        bool pending = false;
+    };
+    Slot slot[WORKERS][SLOTS];
+    std::mutex mu;      // one host batch per table at a time
+    ~HostPipe() {
+        for (auto& w : slot)
+            for (Slot& S : w) {
+                if (S.s) (void)hipStreamSynchronize(S.s);
+                for (void* p : {(void*)S.ht, (void*)S.hc, (void*)S.hi}) if (p) (void)hipHostFree(p);
+                for (void* p : {(void*)S.dt, (void*)S.dc, (void*)S.di}) if (p) (void)hipFree(p);
+                if (S.done) (void)hipEventDestroy(S.done);
+                if (S.s) (void)hipStreamDestroy(S.s);
+            }
+    }
+};
+
 struct kad_table {
     int device = 0;
     uint32_t flags = 0;
@@ -4521,7 +4551,10 @@ struct kad_table {
     uint32_t* dctr = nullptr;       // 4 list lengths
     void* stage = nullptr;          // host -> device staging of patch lists
     size_t stage_bytes = 0;
+    mutable std::mutex pipe_mu;     // creates `pipe` on the first host-pointer batch
+    mutable HostPipe* pipe = nullptr;
     ~kad_table() {
+        delete pipe;
         for (void* p : owned) (void)hipFree(p);
         for (void* p : {(void*)bdirty, (void*)ld8, (void*)ld16, (void*)ld32, (void*)ndirty, (void*)dlist, (void*)dctr, stage})
             if (p) (void)hipFree(p);
@@ -5639,27 +5672,97 @@ int kad_nc_closest_batch_dual(const kad_table* t4, const kad_table* t6, const ui
     return KAD_OK;
 }
 
+// Pinned and device buffers of every slot (index buffers of 32 * CHUNK words: a chunk holds CHUNK queries of count
+// <= 32, fewer of a larger count).
+static int pipe_ready(HostPipe& P) {
+    for (auto& w : P.slot)
+        for (HostPipe::Slot& S : w) {
+            if (S.s) continue;
+            HIP_TRY(hipStreamCreateWithFlags(&S.s, hipStreamNonBlocking));
+            HIP_TRY(hipEventCreateWithFlags(&S.done, hipEventDisableTiming));
+            HIP_TRY(hipHostMalloc((void**)&S.ht, 20ull * HostPipe::CHUNK, hipHostMallocDefault));
+            HIP_TRY(hipHostMalloc((void**)&S.hc, HostPipe::CHUNK, hipHostMallocDefault));
+            HIP_TRY(hipHostMalloc((void**)&S.hi, 4ull * 32 * HostPipe::CHUNK, hipHostMallocDefault));
+            HIP_TRY(hipMalloc(&S.dt, 20ull * HostPipe::CHUNK));
+            HIP_TRY(hipMalloc(&S.dc, HostPipe::CHUNK));
+            HIP_TRY(hipMalloc(&S.di, 4ull * 32 * HostPipe::CHUNK));
+        }
+    return KAD_OK;
+}
+
 static int host_query(const kad_table* t, const uint8_t* targets, uint32_t q, uint32_t count, uint32_t* out_idx,
                       uint8_t* out_cnt, bool nc) {
     if (!t) return set_err(KAD_ERR_INVALID, "NULL table");
     if (q == 0) return KAD_OK;
-    if (!targets || !out_idx) return set_err(KAD_ERR_INVALID, "NULL buffer");
-    DeviceGuard g(t->device);
-    uint8_t* dt = nullptr; uint32_t* di = nullptr; uint8_t* dc = nullptr;
-    const size_t nidx = std::max<size_t>((size_t)q * count, 1);
-    HIP_TRY(hipMalloc(&dt, 20ull * q));
-    if (hipMalloc(&di, 4ull * nidx) != hipSuccess || hipMalloc(&dc, q) != hipSuccess) {
-        (void)hipFree(dt); (void)hipFree(di);
-        return set_err(KAD_ERR_NOMEM, "hipMalloc failed");
+    if (!targets || (!out_idx && count)) return set_err(KAD_ERR_INVALID, "NULL buffer");
+    if (!nc && check_count(count)) return KAD_ERR_UNSUPPORTED;
+    if (nc && count > 255) return set_err(KAD_ERR_UNSUPPORTED, "count %u > 255", count);
+    {
+        std::lock_guard<std::mutex> lk(t->pipe_mu);
+        if (!t->pipe) t->pipe = new HostPipe();
     }
-    int rc = KAD_OK;
-    if (hipMemcpy(dt, targets, 20ull * q, hipMemcpyHostToDevice) != hipSuccess) rc = set_err(KAD_ERR_HIP, "H2D failed");
-    if (!rc) rc = nc ? kad_nc_closest_batch(t, dt, q, count, di, dc, nullptr) : kad_rt_closest_batch(t, dt, q, count, di, dc, nullptr);
-    if (!rc && hipDeviceSynchronize() != hipSuccess) rc = set_err(KAD_ERR_HIP, "kernel failed");
-    if (!rc && count && hipMemcpy(out_idx, di, 4ull * q * count, hipMemcpyDeviceToHost) != hipSuccess) rc = set_err(KAD_ERR_HIP, "D2H failed");
-    if (!rc && out_cnt && hipMemcpy(out_cnt, dc, q, hipMemcpyDeviceToHost) != hipSuccess) rc = set_err(KAD_ERR_HIP, "D2H failed");
-    (void)hipFree(dt); (void)hipFree(di); (void)hipFree(dc);
-    return rc;
+    HostPipe& P = *t->pipe;
+    std::lock_guard<std::mutex> lk(P.mu);
+    DeviceGuard g(t->device);
+    int rc = pipe_ready(P);
+    if (rc) return rc;
+    const uint32_t chunk = count <= 32 ? HostPipe::CHUNK : 32u * HostPipe::CHUNK / count;
+    // worker w takes chunks [w * nch / W, (w + 1) * nch / W) of the batch
+    const uint32_t nch = (q + chunk - 1) / chunk;
+    const int W = (int)std::min<uint32_t>(HostPipe::WORKERS, nch);
+    std::vector<int> wrc(W, KAD_OK);
+    std::vector<std::string> werr(W);
+    auto work = [&](int w) {
+        DeviceGuard gw(t->device);
+        const uint32_t lo = (uint32_t)((uint64_t)w * nch / W * chunk);
+        const uint32_t hi = (uint32_t)std::min<uint64_t>((uint64_t)(w + 1) * nch / W * chunk, q);
+        auto finish = [&](HostPipe::Slot& S) -> int {  // the slot's chunk out to the caller's buffers
+            if (!S.pending) return KAD_OK;
+            S.pending = false;
+            if (hipEventSynchronize(S.done) != hipSuccess) return set_err(KAD_ERR_HIP, "host batch: chunk failed");
+            if (count) std::memcpy(out_idx + (size_t)S.c0 * count, S.hi, 4ull * S.n * count);
+            if (out_cnt) std::memcpy(out_cnt + S.c0, S.hc, S.n);
+            return KAD_OK;
+        };
+        int r = KAD_OK;
+        uint32_t j = 0;
+        for (uint32_t c0 = lo; c0 < hi && !r; c0 += chunk, j++) {
+            HostPipe::Slot& S = P.slot[w][j & 1u];
+            if ((r = finish(S))) break;
+            const uint32_t n = std::min(chunk, hi - c0);
+            std::memcpy(S.ht, targets + 20ull * c0, 20ull * n);
+            if (hipMemcpyAsync(S.dt, S.ht, 20ull * n, hipMemcpyHostToDevice, S.s) != hipSuccess) {
+                r = set_err(KAD_ERR_HIP, "host batch: H2D failed");
+                break;
+            }
+            r = nc ? kad_nc_closest_batch(t, S.dt, n, count, S.di, S.dc, S.s)
+                   : kad_rt_closest_batch(t, S.dt, n, count, S.di, S.dc, S.s);
+            if (r) break;
+            if ((count && hipMemcpyAsync(S.hi, S.di, 4ull * n * count, hipMemcpyDeviceToHost, S.s) != hipSuccess) ||
+                hipMemcpyAsync(S.hc, S.dc, n, hipMemcpyDeviceToHost, S.s) != hipSuccess ||
+                hipEventRecord(S.done, S.s) != hipSuccess) {
+                r = set_err(KAD_ERR_HIP, "host batch: D2H failed");
+                (void)hipStreamSynchronize(S.s);
+                break;
+            }
+            S.c0 = c0;
+            S.n = n;
+            S.pending = true;
+        }
+        for (HostPipe::Slot& S : P.slot[w]) {  // drain: no copy may still target the pinned buffers
+            const int r2 = finish(S);
+            if (!r) r = r2;
+        }
+        wrc[w] = r;
+        if (r) werr[w] = kad_last_error();
+    };
+    std::vector<std::thread> th;
+    for (int w = 1; w < W; w++) th.emplace_back(work, w);
+    work(0);
+    for (auto& x : th) x.join();
+    for (int w = 0; w < W; w++)
+        if (wrc[w]) return set_err(wrc[w], "%s", werr[w].c_str());
+    return KAD_OK;
 }
 
 int kad_rt_closest_batch_host(const kad_table* t, const uint8_t* targets, uint32_t q, uint32_t count, uint32_t* out_idx,

@@ -126,6 +126,29 @@ def test_host_entry_points(gpu):
     np.testing.assert_array_equal(idx, want)
 
 
+def test_host_entry_points_pipelined(gpu):
+    """Host-pointer batches large enough for the chunked pipeline (several chunks per worker, uneven splits, the
+    last chunk partial), repeated calls reusing the table's buffers, counts above 32 (smaller chunks): equal to the
+    device-pointer batch and the oracle."""
+    u = TB.uniform_config(200_000, 14)
+    rng = np.random.default_rng(0x405)
+    targets = rng.integers(0, 256, (300_001, 20), dtype=np.uint8)
+    with make(u, gpu) as T:
+        for k in (8, 32, 8):
+            idx, cnt = T.rt_closest_host(targets, k)
+            want, wcnt = O.flat_rt_closest(u["ids"], u["status"], u["first"], u["off"], targets, k, nthreads=8)
+            np.testing.assert_array_equal(idx, want, err_msg=f"k={k}")
+            np.testing.assert_array_equal(cnt, wcnt, err_msg=f"k={k} counts")
+        for k in (14, 100):
+            idx, cnt = T.nc_closest_host(targets[:150_000], k)
+            di, dc = T.nc_closest(dev(targets[:150_000], gpu), k)
+            np.testing.assert_array_equal(idx, u32(di), err_msg=f"nc k={k}")
+            np.testing.assert_array_equal(cnt, dc.cpu().numpy(), err_msg=f"nc k={k} counts")
+        want, wcnt = O.flat_nc_closest(u["ids"], u["status"], targets[:150_000], 14, nthreads=8)
+        idx, cnt = T.nc_closest_host(targets[:150_000], 14)
+        np.testing.assert_array_equal(idx, want)
+
+
 def test_index_base_and_padding(gpu):
     t = TB.split_config(257, seed=99)
     targets = TB.adversarial_targets(t)
