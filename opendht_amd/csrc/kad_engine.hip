@@ -4493,6 +4493,7 @@ struct HostPipe {
         bool pending = false;
     };
     Slot slot[WORKERS][SLOTS];
+    hipEvent_t start = nullptr;  // recorded on the null stream: the slots' streams wait for prior device work
     std::mutex mu;      // one host batch per table at a time
     ~HostPipe() {
         for (auto& w : slot)
@@ -4503,6 +4504,7 @@ struct HostPipe {
                 if (S.done) (void)hipEventDestroy(S.done);
                 if (S.s) (void)hipStreamDestroy(S.s);
             }
+        if (start) (void)hipEventDestroy(start);
     }
 };
 
@@ -5675,6 +5677,7 @@ int kad_nc_closest_batch_dual(const kad_table* t4, const kad_table* t6, const ui
 // Pinned and device buffers of every slot (index buffers of 32 * CHUNK words: a chunk holds CHUNK queries of count
 // <= 32, fewer of a larger count).
 static int pipe_ready(HostPipe& P) {
+    if (!P.start) HIP_TRY(hipEventCreateWithFlags(&P.start, hipEventDisableTiming));
     for (auto& w : P.slot)
         for (HostPipe::Slot& S : w) {
             if (S.s) continue;
@@ -5706,6 +5709,10 @@ static int host_query(const kad_table* t, const uint8_t* targets, uint32_t q, ui
     DeviceGuard g(t->device);
     int rc = pipe_ready(P);
     if (rc) return rc;
+    // ordered after the work already issued, as a null-stream call is (a status refresh, a mirror update, ...)
+    HIP_TRY(hipEventRecord(P.start, nullptr));
+    for (auto& w : P.slot)
+        for (HostPipe::Slot& S : w) HIP_TRY(hipStreamWaitEvent(S.s, P.start, 0));
     const uint32_t chunk = count <= 32 ? HostPipe::CHUNK : 32u * HostPipe::CHUNK / count;
     // worker w takes chunks [w * nch / W, (w + 1) * nch / W) of the batch
     const uint32_t nch = (q + chunk - 1) / chunk;
