@@ -482,14 +482,16 @@ def host_pass(T, tgs, cnt_k, Q, dev, nb=8):
     import torch
 
     ht = [tgs[j % len(tgs)].cpu().pin_memory() for j in range(4)]
-    hn = ht[0].numpy().copy()  # pageable, as a caller's buffers are
-    T.rt_closest_host(hn, cnt_k)  # warm
+    from opendht_amd._lib import check, lib, ptr
+
+    hn = ht[0].numpy().copy()  # pageable, as a caller's buffers are; result arrays reused across calls
+    oi, oc = np.zeros((Q, cnt_k), np.uint32), np.zeros((Q,), np.uint8)
     ts = []
-    for _ in range(3):
+    for _ in range(6):  # the first call sets up the table's staging
         t0 = time.perf_counter()
-        T.rt_closest_host(hn, cnt_k)
+        check(lib().kad_rt_closest_batch_host(T.handle, ptr(hn), Q, cnt_k, ptr(oi), ptr(oc)), "host batch")
         ts.append(time.perf_counter() - t0)
-    sync_s = float(np.median(ts))
+    sync_s = float(np.median(ts[1:]))
     ho = [torch.empty((Q, cnt_k), dtype=torch.int32).pin_memory() for _ in range(4)]
     hc = [torch.empty((Q,), dtype=torch.uint8).pin_memory() for _ in range(4)]
     dt = [torch.empty((Q, 20), dtype=torch.uint8, device=dev) for _ in range(2)]
@@ -514,9 +516,10 @@ def host_pass(T, tgs, cnt_k, Q, dev, nb=8):
     bytes_q = 20 + 4 * cnt_k + 1
     return {"sync_abi_queries_per_s": Q / sync_s, "pipelined_queries_per_s": nb * Q / pipe_s,
             "pcie_bytes_per_query": bytes_q, "pipelined_GBs": nb * Q * bytes_q / pipe_s / 1e9,
-            "how": f"sync_abi: kad_rt_closest_batch_host over {Q} queries (pageable host buffers in and out; "
+            "how": f"sync_abi: kad_rt_closest_batch_host over {Q} queries (pageable host buffers in and out, the "
+                   f"result arrays reused across calls; "
                    f"inside, 64k-query chunks through pinned staging on two streams per host thread, four threads), "
-                   f"median of 3; pipelined: {nb} batches of {Q}, pinned host buffers, H2D + "
+                   f"median of 5; pipelined: {nb} batches of {Q}, pinned host buffers, H2D + "
                    "kernel + D2H per batch on two alternating streams, wall clock. Not the headline: the "
                    "boundary's device-pointer batch API is the path measured by `value`"}
 
