@@ -194,6 +194,9 @@ int kad_table_export(const kad_table* t, uint8_t* ids, uint8_t* status, uint8_t*
  * distance), out_cnt[i] entries, padded with KAD_NO_NODE. count <= KAD_MAX_COUNT. */
 int kad_rt_closest_batch(const kad_table* t, const uint8_t* targets, uint32_t q, uint32_t count,
                          uint32_t* out_idx, uint8_t* out_cnt, void* stream);
+/* The same on host buffers (any memory), synchronous and ordered after the device work issued before the
+ * call. The first call gives the table ~80 MB of pinned staging and device buffers (freed with it); batches
+ * run as 64k-query chunks pipelined over four host threads. One host batch per table at a time. */
 int kad_rt_closest_batch_host(const kad_table* t, const uint8_t* targets, uint32_t q, uint32_t count,
                               uint32_t* out_idx, uint8_t* out_cnt);
 
