@@ -8,4 +8,4 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 600 --timeout
 timeout -k 10 400 python -u bench.py > $O/bench_default.log 2>&1 || exit $?
 timeout -k 10 600 python -u tools/bench_swarm.py > $O/swarm.log 2>&1 || exit $?
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 $R/bench.py --no-cpu > $O/prof.log 2>&1 || exit $?
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 $R/bench.py --no-cpu --no-extras > $O/prof.log 2>&1 || exit $?
