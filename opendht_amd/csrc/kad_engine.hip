@@ -5680,15 +5680,15 @@ static int pipe_ready(HostPipe& P) {
     if (!P.start) HIP_TRY(hipEventCreateWithFlags(&P.start, hipEventDisableTiming));
     for (auto& w : P.slot)
         for (HostPipe::Slot& S : w) {
-            if (S.s) continue;
-            HIP_TRY(hipStreamCreateWithFlags(&S.s, hipStreamNonBlocking));
-            HIP_TRY(hipEventCreateWithFlags(&S.done, hipEventDisableTiming));
-            HIP_TRY(hipHostMalloc((void**)&S.ht, 20ull * HostPipe::CHUNK, hipHostMallocDefault));
-            HIP_TRY(hipHostMalloc((void**)&S.hc, HostPipe::CHUNK, hipHostMallocDefault));
-            HIP_TRY(hipHostMalloc((void**)&S.hi, 4ull * 32 * HostPipe::CHUNK, hipHostMallocDefault));
-            HIP_TRY(hipMalloc(&S.dt, 20ull * HostPipe::CHUNK));
-            HIP_TRY(hipMalloc(&S.dc, HostPipe::CHUNK));
-            HIP_TRY(hipMalloc(&S.di, 4ull * 32 * HostPipe::CHUNK));
+            // each piece on its own, so that a call after a failed one completes the slot
+            if (!S.s) HIP_TRY(hipStreamCreateWithFlags(&S.s, hipStreamNonBlocking));
+            if (!S.done) HIP_TRY(hipEventCreateWithFlags(&S.done, hipEventDisableTiming));
+            if (!S.ht) HIP_TRY(hipHostMalloc((void**)&S.ht, 20ull * HostPipe::CHUNK, hipHostMallocDefault));
+            if (!S.hc) HIP_TRY(hipHostMalloc((void**)&S.hc, HostPipe::CHUNK, hipHostMallocDefault));
+            if (!S.hi) HIP_TRY(hipHostMalloc((void**)&S.hi, 4ull * 32 * HostPipe::CHUNK, hipHostMallocDefault));
+            if (!S.dt) HIP_TRY(hipMalloc(&S.dt, 20ull * HostPipe::CHUNK));
+            if (!S.dc) HIP_TRY(hipMalloc(&S.dc, HostPipe::CHUNK));
+            if (!S.di) HIP_TRY(hipMalloc(&S.di, 4ull * 32 * HostPipe::CHUNK));
         }
     return KAD_OK;
 }
@@ -5764,8 +5764,16 @@ static int host_query(const kad_table* t, const uint8_t* targets, uint32_t q, ui
         if (r) werr[w] = kad_last_error();
     };
     std::vector<std::thread> th;
-    for (int w = 1; w < W; w++) th.emplace_back(work, w);
+    std::vector<int> inline_w;  // workers whose thread could not be started run here
+    for (int w = 1; w < W; w++) {
+        try {
+            th.emplace_back(work, w);
+        } catch (...) {
+            inline_w.push_back(w);
+        }
+    }
     work(0);
+    for (int w : inline_w) work(w);
     for (auto& x : th) x.join();
     for (int w = 0; w < W; w++)
         if (wrc[w]) return set_err(wrc[w], "%s", werr[w].c_str());
