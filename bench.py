@@ -61,9 +61,14 @@ def parse_args(argv=None):
     ap.add_argument("--gather-json", default=os.path.join(ROOT, "profiles", "r02_mb_gather.json"))
     ap.add_argument("--plumbing", action="store_true",
                     help="launcher/rendezvous check without a GPU: gloo ranks, barrier, max-over-ranks, one line")
-    ap.add_argument("--mode", choices=("owner", "allgather"), default="owner",
+    ap.add_argument("--mode", choices=("owner", "allgather", "allgather-child"), default="owner",
                     help="owner: the headline (allgather measured as a sub-object); allgather: only the "
-                         "north-star variant, as its own line")
+                         "north-star variant, as its own line; allgather-child: internal (allgather_child)")
+    ap.add_argument("--verify-rows", type=int, default=1 << 16,
+                    help="rows of the last timed step checked against the CPU restatement on every rank")
+    ap.add_argument("--ag-timeout", type=float, default=240.0,
+                    help="seconds before the north-star child processes (N > 1) are killed")
+    ap.add_argument("--ag-out", default="", help="internal: where an allgather child writes its result")
     return ap.parse_args(argv)
 
 
@@ -98,26 +103,66 @@ def dist_env():
     return world, rank, local
 
 
-def init_dist(world, dev):
+def init_dist(world, dev, rccl=False):
+    """The process group. The headline (owner routing) has no data-path collective: its barriers and
+    max-over-ranks run on gloo, so no RCCL call can stall or fail the headline line. rccl=True (the
+    north-star child processes, allgather_child) opens RCCL over xGMI. A finite timeout ends a hung
+    collective with an error instead of stalling the run."""
     if world == 1:
         return None
+    from datetime import timedelta
+
     import torch.distributed as dist
 
-    if dev.type == "cuda" and not REHEARSE_ONE_GPU:
-        dist.init_process_group("nccl", device_id=dev)  # RCCL over xGMI
+    if rccl and dev.type == "cuda" and not REHEARSE_ONE_GPU:
+        dist.init_process_group("nccl", device_id=dev, timeout=timedelta(seconds=120))  # RCCL over xGMI
     else:
-        dist.init_process_group("gloo")
+        dist.init_process_group("gloo", timeout=timedelta(seconds=600))
     return dist
 
 
-def max_over_ranks(dist, x: float, dev) -> float:
+def max_over_ranks(dist, x: float, dev=None) -> float:
     if dist is None:
         return x
     import torch
 
-    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    t = torch.tensor([x], dtype=torch.float64,
+                     device=dev if (dev is not None and dist.get_backend() == "nccl") else "cpu")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def sum_over_ranks(dist, x: int, dev=None) -> int:
+    if dist is None:
+        return x
+    import torch
+
+    t = torch.tensor([x], dtype=torch.int64,
+                     device=dev if (dev is not None and dist.get_backend() == "nccl") else "cpu")
+    dist.all_reduce(t)
+    return int(t.item())
+
+
+def host_cores() -> dict:
+    """The CPU this process may use: affinity set, cgroup quota, nproc."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    return {"affinity": aff, "cgroup_quota_cpus": quota, "nproc": os.cpu_count()}
+
+
+def all_cores() -> int:
+    """Threads for the all-cores CPU baseline: the affinity set, capped by the cgroup CPU quota."""
+    h = host_cores()
+    n = h["affinity"]
+    if h["cgroup_quota_cpus"]:
+        n = min(n, max(1, int(h["cgroup_quota_cpus"])))
+    return max(1, n)
 
 
 # ---------------------------------------------------------------------------------------------
@@ -197,7 +242,7 @@ def cpu_baselines(sh, targets, count, budget_s, nthreads, min_port=1000, fast_mi
             "sample": f"{n} of the {targets.shape[0]} queries of rank 0's first batch (same shard table, "
                       f"{sh.first.shape[0]} buckets, {sh.ids.shape[0]} nodes) in {dt:.1f} s; structure-faithful "
                       f"restatement of routing_table.cpp:67-135 (std::list walk); table build {build_s:.1f}s excluded",
-            "cpu_model": cpu_model(), "nproc": os.cpu_count()}
+            "cpu_model": cpu_model(), "host": host_cores()}
     # fast_cpu: the closed-form window (binary-search findBucket, good counts, sort), all cores; passes over
     # the whole host sample until at least fast_min_s of CPU work is timed
     O.flat_rt_closest(sh.ids, sh.status, sh.first, sh.off, targets[:4096], count, nthreads=nthreads)  # warm pages
@@ -216,8 +261,22 @@ def cpu_baselines(sh, targets, count, budget_s, nthreads, min_port=1000, fast_mi
             "sample": f"{passes} passes over {targets.shape[0]} queries of rank 0's first batch ({fq} queries) in "
                       f"{fdt:.2f} s; closed-form flat restatement "
                       f"(upper_bound findBucket + window rounds + sort by XOR distance), {nthreads} threads",
-            "cpu_model": cpu_model(), "nproc": os.cpu_count()}
+            "cpu_model": cpu_model(), "host": host_cores()}
     return port, fast
+
+
+def verify_rows(ids, status, first, off, index_base, targets, idx, cnt, count, nthreads=None) -> int:
+    """Rows of a timed step against the closed-form CPU restatement (oracle/, the checker) on the same
+    table: the number of rows whose indices or count differ."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+
+    if targets.shape[0] == 0:
+        return 0
+    want, wcnt = O.flat_rt_closest(ids, status, first, off, targets, count, nthreads=nthreads or all_cores())
+    want = np.where(want != 0xFFFFFFFF, want + np.uint32(index_base), want)
+    got = np.ascontiguousarray(idx).view(np.uint32).reshape(want.shape)
+    return int(((got != want).any(axis=1) | (np.asarray(cnt) != wcnt)).sum())
 
 
 def load_json(path, key=None):
@@ -351,16 +410,31 @@ def main_owner(args):
         extras["refresh"] = refresh_pass(T, sh, tgs, outs, ocnt, cnt_k, Q, avg_kernel_s, dev, stream)
         extras["host_buffers"] = host_pass(T, tgs, cnt_k, Q, dev)
         extras["other_counts"] = counts_pass(T, tgs, Q, dev, stream)
+    # the rows of the last timed step (batch K-1), checked against the CPU restatement on this rank's
+    # shard table (exact halo: every owned window lies inside it)
+    vrows = min(Q, args.verify_rows)
+    vt = tgs[(K - 1) % NB][:vrows].cpu().numpy()
+    bad = verify_rows(sh.ids, sh.status, sh.first, sh.off, sh.index_base, vt,
+                      outs[(K - 1) % NB][:vrows].cpu().numpy(), ocnt[(K - 1) % NB][:vrows].cpu().numpy(), cnt_k)
+    verified = {"rows": sum_over_ranks(dist, vrows), "mismatches": sum_over_ranks(dist, bad),
+                "what": f"the first {vrows} rows (indices, counts) of every rank's last timed step, against the "
+                        "closed-form CPU restatement (oracle/) on the rank's shard table"}
     cpu = fast = None
     if rank == 0 and world == 1 and not args.no_cpu:
         host_t = tgs[0][:1 << 17].cpu().numpy()
-        cpu, fast = cpu_baselines(sh, host_t, cnt_k, args.cpu_budget, min(16, os.cpu_count() or 1))
+        cpu, fast = cpu_baselines(sh, host_t, cnt_k, args.cpu_budget, all_cores())
     ag = None
     if not args.no_extras and not args.no_allgather:
         T.close()
         del tgs, outs, ocnt
         torch.cuda.empty_cache()
-        ag = allgather_pass(args, world, rank, local, dev, dist)
+        if world == 1:
+            try:
+                ag = allgather_pass(args, world, rank, local, dev, None)
+            except Exception as e:  # the headline line is printed whatever happens here
+                ag = {"error": f"{type(e).__name__}: {e}"}
+        else:
+            ag = allgather_child(args, world, rank, local, dist)
 
     if rank == 0:
         line = {
@@ -413,6 +487,7 @@ def main_owner(args):
                                      "good": float(np.mean([r[3] for r in ref]))},
                 },
             },
+            "verified": verified,
             "cpu_baseline": cpu,
             "fast_cpu": fast,
             "setup_s": setup_s,
@@ -585,11 +660,61 @@ def refresh_pass(T, sh, tgs, outs, ocnt, cnt_k, Q, avg_kernel_s, dev, stream, re
 # ---------------------------------------------------------------------------------------------
 # north-star variant: halo-free shards, replicated batch, all-gather + device merge
 # ---------------------------------------------------------------------------------------------
+def graph_steps(step, K, W, dev, dist, use_graph=True):
+    """W untimed warm-up steps, then exactly K steps (one HIP graph of K steps unless use_graph is False)
+    between a barrier + synchronize on both sides. step(j) issues step j on the current stream.
+    Returns (max wall over ranks, the kernels' average ms per step from HIP events, launch kind)."""
+    import torch
+
+    stream = torch.cuda.current_stream(dev)
+    for j in range(W):
+        step(K + j)
+    torch.cuda.synchronize(dev)
+    graph = None
+    if use_graph:
+        try:
+            g = torch.cuda.CUDAGraph()
+            cs = torch.cuda.Stream(dev)
+            cs.wait_stream(stream)
+            with torch.cuda.graph(g, stream=cs):
+                for j in range(K):
+                    step(j)
+            stream.wait_stream(cs)
+            torch.cuda.synchronize(dev)
+            g.replay()  # the first replay uploads the graph
+            torch.cuda.synchronize(dev)
+            graph = g
+        except Exception as e:
+            print(f"graph capture failed ({e}); eager launches", file=sys.stderr)
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    a.record(stream)
+    if graph is not None:
+        graph.replay()
+    else:
+        for j in range(K):
+            step(j)
+    b.record(stream)
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    return max_over_ranks(dist, wall, dev), a.elapsed_time(b) / K, ("hip graph of K steps" if graph is not None
+                                                                     else "K eager steps")
+
+
 def allgather_pass(args, world, rank, local, dev, dist):
+    """The north-star variant: the 100M-node table in `world` halo-free shards, the same
+    1M-query batch on every rank, each rank's part of every window, one all-gather of fixed-size blocks,
+    the device scatter + merge; no host read inside the K steps (the overflow word is read after them)."""
     import torch
 
     from opendht_amd.global_shard import GlobalShard, build_plain_shard, global_good_prefix
-    from opendht_amd.sharded import config3_spec
+    from opendht_amd.sharded import build_shard, config3_spec
+    from opendht_amd.synth import bucket_firsts
 
     if world & (world - 1) or world > 8:
         return {"skipped": "world size must be a power of two <= 8"}
@@ -599,55 +724,128 @@ def allgather_pass(args, world, rank, local, dev, dist):
     gp = global_good_prefix(good, device=dev if world > 1 else None)
     G = GlobalShard(ids, st, off, lo, hi, spec.depth, base, gp, device=local)
     n_local = ids.shape[0]
-    del ids, st
     Q, K, cnt_k = args.queries, max(4, min(args.steps, 20)), args.count
     NB = K + 2
     tgs = device_targets(NB, Q, 0, 0, 0x0D470002, dev)  # the same global batches on every rank
     out_idx = torch.empty((Q, cnt_k), dtype=torch.int32, device=dev)
     out_cnt = torch.empty((Q,), dtype=torch.uint8, device=dev)
     setup = time.perf_counter() - t0
-    for j in range(2):
-        G.query(tgs[K + j], cnt_k, out_idx=out_idx, out_cnt=out_cnt)
-    torch.cuda.synchronize(dev)
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t_start = time.perf_counter()
-    for j in range(K):
-        G.query(tgs[j], cnt_k, out_idx=out_idx, out_cnt=out_cnt)
-    torch.cuda.synchronize(dev)
-    if dist:
-        dist.barrier()
-    t_max = max_over_ranks(dist, time.perf_counter() - t_start, dev)
-    shard_path = None
-    if world == 1:  # the shard kernel + scatter on the whole table: each rank's local work at N > 1
-        for j in range(2):
-            G.query(tgs[K + j], cnt_k, out_idx=out_idx, out_cnt=out_cnt, single_rank_shard_kernel=True)
-        torch.cuda.synchronize(dev)
-        t1 = time.perf_counter()
-        for j in range(K):
-            G.query(tgs[j], cnt_k, out_idx=out_idx, out_cnt=out_cnt, single_rank_shard_kernel=True)
-        torch.cuda.synchronize(dev)
-        shard_path = {"ms_per_step": (time.perf_counter() - t1) / K * 1e3,
-                      "how": "N = 1 through kad_rt_shard_batch + kad_rt_scatter_rows instead of the plain batch"}
-    # bytes gathered per step (the all-gather payload of every rank, summed)
-    rows, parts = G.local_compact(tgs[0], cnt_k) if world > 1 else (None, None)
-    gathered = None
-    if world > 1:
-        from opendht_amd._lib import part_words, row_words
-
-        nb = torch.tensor([rows.shape[0] * row_words(cnt_k) * 4 + parts.shape[0] * part_words(cnt_k) * 4],
-                          dtype=torch.float64, device=dev)
-        dist.all_reduce(nb)
-        gathered = float(nb.item())
+    vrows = min(Q, args.verify_rows)
+    res = {"unit": "queries/s", "n_gpus": world, "steps": K, "scaling": "strong", "setup_s": setup}
+    if world == 1:
+        # one rank holds the whole table: the query is the plain batch (nothing to exchange)
+        t_max, kern_ms, how = graph_steps(lambda j: G.table.rt_closest(tgs[j % NB], cnt_k, out_idx, out_cnt), K, 2,
+                                          dev, None)
+        first = bucket_firsts(spec.depth, lo, hi)
+        vt = tgs[(K - 1) % NB][:vrows].cpu().numpy()
+        bad = verify_rows(ids, st, first, off, 0, vt, out_idx[:vrows].cpu().numpy(), out_cnt[:vrows].cpu().numpy(),
+                          cnt_k)
+        res.update({"value": Q * K / t_max, "ms_per_step": t_max / K * 1e3, "avg_kernel_ms": kern_ms, "launch": how,
+                    "workload": f"100M-node U(24) table whole on one GPU ({n_local} nodes), {Q} queries per step "
+                                f"(a distinct batch per step), k={cnt_k}: the plain batch",
+                    "verified": {"rows": vrows, "mismatches": bad}})
+        # what each rank runs at N > 1 minus the collective: shard kernel + kad_rt_gather_finish, as a graph
+        ex = G.exchange(Q, cnt_k, 1)
+        t_sh, kern_sh, how_sh = graph_steps(lambda j: G.step(tgs[j % NB], ex, out_idx, out_cnt), K, 2, dev, None)
+        ovf = ex.overflowed()
+        bad_sh = verify_rows(ids, st, first, off, 0, vt, out_idx[:vrows].cpu().numpy(),
+                             out_cnt[:vrows].cpu().numpy(), cnt_k)
+        res["shard_kernel_path"] = {"ms_per_step": t_sh / K * 1e3, "avg_kernel_ms": kern_sh, "launch": how_sh,
+                                    "overflow": ovf, "verified": {"rows": vrows, "mismatches": bad_sh},
+                                    "how": "N = 1 through kad_rt_shard_batch + kad_rt_gather_finish (device-only "
+                                           "step) instead of the plain batch"}
+    else:
+        ex = G.exchange(Q, cnt_k, world)
+        for _ in range(4):  # capacities: grow until a step fits (every rank reads the same gathered counters)
+            G.step(tgs[K], ex, out_idx, out_cnt)
+            if not ex.overflowed():
+                break
+            ex = G._ex[(Q, cnt_k, world)] = ex.grown()
+        for _ in range(3):
+            t_max, kern_ms, how = graph_steps(lambda j: G.step(tgs[j % NB], ex, out_idx, out_cnt), K, 1, dev, dist,
+                                              use_graph=False)
+            if not ex.overflowed():
+                break
+            ex = G._ex[(Q, cnt_k, world)] = ex.grown()
+        else:
+            raise RuntimeError("exchange buffers kept overflowing")
+        # verification: the rows of the last step whose targets this rank owns, against the restatement on
+        # this rank's shard WITH its exact halo (owner-routing shard: every owned window lies inside it)
+        G.close()
+        del ids, st
+        vt = tgs[(K - 1) % NB][:vrows].cpu().numpy()
+        own = (vt[:, 0].astype(np.int64) >> (8 - spec.shard_bits)) == rank
+        sh = build_shard(spec, rank)
+        bad = verify_rows(sh.ids, sh.status, sh.first, sh.off, sh.index_base, vt[own],
+                          out_idx[:vrows].cpu().numpy()[own], out_cnt[:vrows].cpu().numpy()[own], cnt_k)
+        res.update({"value": Q * K / t_max, "ms_per_step": t_max / K * 1e3, "avg_step_ms_events": kern_ms,
+                    "launch": how,
+                    "workload": f"100M-node U(24) table, 1/{world} per GPU without halo ({n_local} nodes on rank 0), "
+                                f"{Q} global queries per step (a distinct batch per step, replicated on every rank), "
+                                f"k={cnt_k}; kad_rt_shard_batch into a fixed-size block, RCCL all_gather_into_tensor of "
+                                "the blocks, kad_rt_gather_finish (scatter + merge on the device)",
+                    "gathered_bytes_per_step": ex.gathered_bytes,
+                    "row_cap": ex.row_cap, "part_cap": ex.part_cap,
+                    "verified": {"rows": sum_over_ranks(dist, int(own.sum()), dev),
+                                 "mismatches": sum_over_ranks(dist, bad, dev)}})
+        return res
     G.close()
-    return {"value": Q * K / t_max, "unit": "queries/s", "n_gpus": world, "steps": K,
-            "ms_per_step": t_max / K * 1e3, "scaling": "strong",
-            "workload": f"100M-node U(24) table, 1/{world} per GPU without halo ({n_local} nodes on rank 0), "
-                        f"{Q} global queries per step (a distinct batch per step, replicated on every rank), "
-                        f"k={cnt_k}; " + ("kad_rt_shard_batch + RCCL all-gather of rows/parts + scatter/merge"
-                                          if world > 1 else "one rank holds the whole table: the plain batch"),
-            "gathered_bytes_per_step": gathered, "setup_s": setup, "shard_kernel_path": shard_path}
+    return res
+
+
+def allgather_child(args, world, rank, local, dist) -> dict:
+    """The north-star variant at N > 1 in child processes (one per rank, the same GPU), so that a failing or
+    hanging RCCL collective can cost only the `allgather` object, never the headline line: each rank starts
+    its child with a shared fresh port and waits at most --ag-timeout seconds."""
+    import tempfile
+
+    port = [0]
+    if rank == 0:
+        with socket.socket() as so:
+            so.bind(("127.0.0.1", 0))
+            port[0] = so.getsockname()[1]
+    dist.broadcast_object_list(port, src=0)
+    out = os.path.join(tempfile.gettempdir(), f"kadgpu_ag_{port[0]}_{rank}.json")
+    env = dict(os.environ, RANK=str(rank), LOCAL_RANK=str(local), WORLD_SIZE=str(world),
+               LOCAL_WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port[0]))
+    argv = [sys.executable, "-u", os.path.abspath(__file__), "--gpus", str(world), "--mode", "allgather-child",
+            "--ag-out", out, "--queries", str(args.queries), "--steps", str(args.steps), "--count", str(args.count),
+            "--verify-rows", str(args.verify_rows)]
+    p = subprocess.Popen(argv, env=env, stdout=sys.stderr)  # the child's output never reaches the JSON line
+    try:
+        rc = p.wait(timeout=args.ag_timeout)
+    except subprocess.TimeoutExpired:
+        p.kill()
+        p.wait()
+        return {"error": f"rank {rank}: the north-star child was killed after {args.ag_timeout:.0f} s"}
+    try:
+        with open(out) as f:
+            res = json.load(f)
+        os.unlink(out)
+    except (OSError, ValueError):
+        res = {"error": f"rank {rank}: the north-star child exited with {rc} and no result"}
+    return res
+
+
+def main_allgather_child(args):
+    import torch
+
+    world, rank, local = dist_env()
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist = init_dist(world, dev, rccl=True)
+    try:
+        ag = allgather_pass(args, world, rank, local, dev, dist)
+    except Exception as e:
+        ag = {"error": f"rank {rank}: {type(e).__name__}: {e}"}
+    with open(args.ag_out, "w") as f:
+        json.dump(ag, f)
+    if dist:
+        try:
+            dist.destroy_process_group()
+        except Exception:
+            pass
+    return 0 if "error" not in ag else 1
 
 
 def main_allgather_line(args):
@@ -658,7 +856,7 @@ def main_allgather_line(args):
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    dist = init_dist(world, dev)
+    dist = init_dist(world, dev, rccl=True)
     ag = allgather_pass(args, world, rank, local, dev, dist)
     if rank == 0:
         print(json.dumps({"metric": "k=8 closest-node queries/sec, 1M queries vs the 100M-node table split over N "
@@ -705,6 +903,8 @@ def main(argv=None):
         return main_plumbing(args)
     if args.mode == "allgather":
         return main_allgather_line(args)
+    if args.mode == "allgather-child":
+        return main_allgather_child(args)
     return main_owner(args)
 
 

@@ -268,6 +268,29 @@ int kad_rt_scatter_rows(const uint32_t* rows, const uint32_t* n_rows, uint32_t n
  * global index) of each query (exact: parts come from disjoint buckets). */
 int kad_rt_merge_parts(const uint32_t* parts, uint32_t n_parts, uint32_t count, uint32_t* out_idx,
                        uint8_t* out_cnt, int device, void* stream);
+/* The device-only exchange step (no host read between the shard kernel, the collective and the merge,
+ * so a step can be captured in a HIP graph). Every rank lays out ONE send block of
+ * KAD_SHARD_BLOCK_WORDS(count, row_cap, part_cap) words and passes its pieces to kad_rt_shard_batch:
+ *   rows     = block                                        (KAD_SHARD_REGIONS regions of row_cap rows)
+ *   parts    = block + KAD_SHARD_REGIONS*row_cap*KAD_ROW_WORDS(count)      (part_cap partial rows)
+ *   counters = parts + part_cap*KAD_PART_WORDS(count)       (zeroed before kad_rt_shard_batch)
+ * The blocks of all `world` ranks are all-gathered in rank order (one fixed-size all_gather, RCCL)
+ * into `recv`; kad_rt_gather_finish then writes every query's findClosestNodes row: complete rows
+ * scattered by qid, the parts of edge-crossing windows merged by (XOR distance, global index).
+ *   q        queries of the replicated batch (qids < q)
+ *   scratch  device, q + world*part_cap words; its first q words must be KAD_NO_NODE (0xFFFFFFFF)
+ *            before the first call, and every call leaves them so
+ *   overflow device word: set to 1 (never cleared here) when any rank's region or part buffer was
+ *            full, i.e. some rows are missing: grow row_cap / part_cap and run the batch again. A
+ *            caller checks it once per batch or once per K steps.
+ * world <= KAD_SHARD_MAX_WORLD. All pointers are device pointers; count in 1..KAD_MAX_COUNT. */
+#define KAD_SHARD_MAX_WORLD 16u
+#define KAD_SHARD_BLOCK_WORDS(count, row_cap, part_cap)                                                \
+    ((uint64_t)KAD_SHARD_REGIONS * (row_cap) * KAD_ROW_WORDS(count) +                                  \
+     (uint64_t)(part_cap) * KAD_PART_WORDS(count) + (uint64_t)KAD_SHARD_COUNTERS * KAD_SHARD_COUNTER_STRIDE)
+int kad_rt_gather_finish(const uint32_t* recv, uint32_t world, uint32_t row_cap, uint32_t part_cap, uint32_t q,
+                         uint32_t count, uint32_t* scratch, uint32_t* out_idx, uint8_t* out_cnt,
+                         uint32_t* overflow, int device, void* stream);
 
 /* ---- wire step after the query ------------------------ */
 #define KAD_SEND_NODES 8u           /* reference network_engine.cpp:59 SEND_NODES */

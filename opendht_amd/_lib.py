@@ -39,6 +39,19 @@ def part_words(count: int) -> int:
     """KAD_PART_WORDS: a row plus the entries' 160-bit XOR distances (5 words each)."""
     return row_words(count) + 5 * count
 
+
+KAD_SHARD_REGIONS = 8
+KAD_SHARD_COUNTERS = 10
+KAD_SHARD_COUNTER_STRIDE = 32
+KAD_SHARD_MAX_WORLD = 16
+
+
+def shard_block_words(count: int, row_cap: int, part_cap: int) -> int:
+    """KAD_SHARD_BLOCK_WORDS: one rank's send block (regions of rows, parts, counters)."""
+    return (KAD_SHARD_REGIONS * row_cap * row_words(count) + part_cap * part_words(count)
+            + KAD_SHARD_COUNTERS * KAD_SHARD_COUNTER_STRIDE)
+
+
 KAD_ERR_NOMEM = -3
 
 ERRORS = {
@@ -84,6 +97,8 @@ SIGNATURES = {
     "kad_rt_scatter_rows": (C.c_int, [_P, _P, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, _P, _P, C.c_int,
                                       _P]),
     "kad_rt_merge_parts": (C.c_int, [_P, C.c_uint32, C.c_uint32, _P, _P, C.c_int, _P]),
+    "kad_rt_gather_finish": (C.c_int, [_P, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, _P, _P, _P,
+                                       _P, C.c_int, _P]),
     "kad_table_set_addrs": (C.c_int, [_P, C.c_uint32, _P]),
     "kad_buffer_nodes_batch": (C.c_int, [_P, _P, C.c_uint32, _P, _P, C.c_uint32, _P, _P, _P]),
     "kad_parse_nodes_batch": (C.c_int, [_P, C.c_uint32, C.c_uint32, _P, _P, C.c_int, _P]),

@@ -2763,6 +2763,105 @@ __global__ void merge_parts_kernel(const uint32_t* __restrict__ parts, uint32_t 
 }
 
 // ---------------------------------------------------------------------------------------
+// The all-gathered step of the north-star variant (kad_rt_gather_finish). A rank's send block is its
+// kad_rt_shard_batch output in place: KAD_SHARD_REGIONS regions of row_cap complete rows, then part_cap
+// partial rows, then the counters (KAD_SHARD_BLOCK_WORDS). After one all-gather of fixed-size blocks,
+// block r of the received buffer is rank r's, and every count the kernels need is read on the device:
+// no host read between the shard kernel, the collective and the merge, so a step can be captured in a
+// graph. Parts of one query are chained through a per-query head word (atomicExch), merged by the
+// thread of the chain's head, and the head is reset to NONE for the next step.
+// ---------------------------------------------------------------------------------------
+struct GatherCtx {
+    const uint32_t* recv;
+    uint64_t block;               // words per rank block
+    uint64_t parts_off, ctr_off;  // word offsets of the parts and the counters inside a block
+    uint32_t world, row_cap, part_cap, rs, ps, count, q;
+};
+
+__device__ __forceinline__ const uint32_t* gather_ctr(const GatherCtx& G, uint32_t r) {
+    return G.recv + (size_t)r * G.block + G.ctr_off;
+}
+
+__global__ void gather_scatter_kernel(GatherCtx G, uint32_t* __restrict__ out_idx, uint8_t* __restrict__ out_cnt,
+                                      uint32_t* __restrict__ overflow) {
+    const uint64_t g = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    const uint64_t per = (uint64_t)KAD_SHARD_REGIONS * G.row_cap;
+    const uint32_t r = (uint32_t)(g / per);
+    if (r >= G.world) return;
+    const uint32_t rem = (uint32_t)(g % per), region = rem / G.row_cap, k = rem % G.row_cap;
+    const uint32_t* ctr = gather_ctr(G, r);
+    if (rem == 0 && ctr[KAD_SHARD_COUNTER_STRIDE * 9u] && overflow) atomicOr(overflow, 1u);
+    if (k >= min(ctr[KAD_SHARD_COUNTER_STRIDE * region], G.row_cap)) return;
+    const uint32_t* src = G.recv + (size_t)r * G.block + ((size_t)region * G.row_cap + k) * G.rs;
+    const uint32_t qid = src[0];
+    if (qid >= G.q) return;
+    if (out_cnt) out_cnt[qid] = (uint8_t)src[1];
+    uint32_t* dst = out_idx + (size_t)qid * G.count;
+    if (G.count == 8 && ((uintptr_t)dst & 15u) == 0) {
+        reinterpret_cast<uint4*>(dst)[0] = reinterpret_cast<const uint4*>(src)[1];
+        reinterpret_cast<uint4*>(dst)[1] = reinterpret_cast<const uint4*>(src)[2];
+    } else {
+        for (uint32_t j = 0; j < G.count; j++) dst[j] = src[4 + j];
+    }
+}
+
+// Part x = (rank r, slot p) of the gathered buffer, or NULL if the slot is empty.
+__device__ __forceinline__ const uint32_t* gather_part(const GatherCtx& G, uint64_t x) {
+    const uint32_t r = (uint32_t)(x / G.part_cap), p = (uint32_t)(x % G.part_cap);
+    if (r >= G.world || p >= min(gather_ctr(G, r)[KAD_SHARD_COUNTER_STRIDE * 8u], G.part_cap)) return nullptr;
+    return G.recv + (size_t)r * G.block + G.parts_off + (size_t)p * G.ps;
+}
+
+__global__ void gather_link_kernel(GatherCtx G, uint32_t* __restrict__ head, uint32_t* __restrict__ next) {
+    const uint64_t x = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    const uint32_t* part = gather_part(G, x);
+    if (!part || part[0] >= G.q) return;
+    next[x] = atomicExch(head + part[0], (uint32_t)x);
+}
+
+// The thread of a query's chain head merges its parts (at most one per rank, KAD_SHARD_MAX_WORLD) by
+// (XOR distance, global index), as merge_parts_kernel, and resets the head.
+__global__ void gather_merge_kernel(GatherCtx G, uint32_t* __restrict__ head, const uint32_t* __restrict__ next,
+                                    uint32_t* __restrict__ out_idx, uint8_t* __restrict__ out_cnt) {
+    const uint64_t x = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    const uint32_t* part = gather_part(G, x);
+    if (!part) return;
+    const uint32_t qid = part[0];
+    if (qid >= G.q || head[qid] != (uint32_t)x) return;
+    constexpr uint32_t MAXSEG = KAD_SHARD_MAX_WORLD;
+    const uint32_t* seg[MAXSEG];
+    uint32_t at[MAXSEG], nseg = 0, total = 0;
+    for (uint32_t y = (uint32_t)x; y != NONE && nseg < MAXSEG; y = next[y]) {
+        seg[nseg] = gather_part(G, y);
+        at[nseg] = 0;
+        total += seg[nseg][1];
+        nseg++;
+    }
+    const uint32_t count = G.count, m = min(count, total);
+    uint32_t* dst = out_idx + (size_t)qid * count;
+    for (uint32_t p = 0; p < count; p++) {
+        if (p >= m) {
+            dst[p] = NONE;
+            continue;
+        }
+        uint32_t best = NONE;
+        for (uint32_t s = 0; s < nseg; s++) {
+            if (at[s] >= seg[s][1]) continue;
+            if (best == NONE) { best = s; continue; }
+            const uint32_t* da = seg[s] + G.rs + 5 * at[s];
+            const uint32_t* db = seg[best] + G.rs + 5 * at[best];
+            int c = 0;
+            for (int w = 0; w < 5 && c == 0; w++) c = da[w] < db[w] ? -1 : da[w] > db[w] ? 1 : 0;
+            if (c < 0 || (c == 0 && seg[s][4 + at[s]] < seg[best][4 + at[best]])) best = s;
+        }
+        dst[p] = seg[best][4 + at[best]];
+        at[best]++;
+    }
+    if (out_cnt) out_cnt[qid] = (uint8_t)m;
+    head[qid] = NONE;
+}
+
+// ---------------------------------------------------------------------------------------
 // Wire step after the query
 // NetworkEngine::bufferNodes (network_engine.cpp:942-974): a query's candidate nodes sorted by
 // XOR distance to the target (std::sort on xorCmp, :945-947), the first SEND_NODES = 8 (:948),
@@ -5492,6 +5591,42 @@ int kad_rt_merge_parts(const uint32_t* parts, uint32_t n_parts, uint32_t count, 
     DeviceGuard g(device);
     hipLaunchKernelGGL(merge_parts_kernel, dim3(grid_for(n_parts)), dim3(BLOCK), 0, (hipStream_t)stream, parts, n_parts,
                        (uint32_t)KAD_ROW_WORDS(count), (uint32_t)KAD_PART_WORDS(count), count, out_idx, out_cnt);
+    HIP_TRY(hipGetLastError());
+    return KAD_OK;
+}
+
+int kad_rt_gather_finish(const uint32_t* recv, uint32_t world, uint32_t row_cap, uint32_t part_cap, uint32_t q,
+                         uint32_t count, uint32_t* scratch, uint32_t* out_idx, uint8_t* out_cnt, uint32_t* overflow,
+                         int device, void* stream) {
+    int rc = check_count(count);
+    if (rc) return rc;
+    if (count == 0) return set_err(KAD_ERR_INVALID, "count 0: nothing to answer (the caller writes empty rows)");
+    if (world == 0 || world > KAD_SHARD_MAX_WORLD)
+        return set_err(KAD_ERR_INVALID, "world %u outside 1..%u", world, KAD_SHARD_MAX_WORLD);
+    if (row_cap == 0 || part_cap == 0) return set_err(KAD_ERR_INVALID, "row_cap and part_cap must be > 0");
+    if (q == 0) return KAD_OK;
+    if (!recv || !scratch || !out_idx) return set_err(KAD_ERR_INVALID, "NULL buffer");
+    GatherCtx G{};
+    G.recv = recv;
+    G.rs = KAD_ROW_WORDS(count);
+    G.ps = KAD_PART_WORDS(count);
+    G.parts_off = (uint64_t)KAD_SHARD_REGIONS * row_cap * G.rs;
+    G.ctr_off = G.parts_off + (uint64_t)part_cap * G.ps;
+    G.block = KAD_SHARD_BLOCK_WORDS(count, row_cap, part_cap);
+    G.world = world;
+    G.row_cap = row_cap;
+    G.part_cap = part_cap;
+    G.count = count;
+    G.q = q;
+    uint32_t* head = scratch;
+    uint32_t* next = scratch + q;
+    DeviceGuard g(device);
+    hipStream_t s = (hipStream_t)stream;
+    const uint64_t nrows = (uint64_t)world * KAD_SHARD_REGIONS * row_cap, nparts = (uint64_t)world * part_cap;
+    if (nrows > 0xFFFFFFFFull * BLOCK || nparts >= 0xFFFFFFFFull) return set_err(KAD_ERR_INVALID, "buffers too large");
+    hipLaunchKernelGGL(gather_scatter_kernel, dim3(grid_for(nrows)), dim3(BLOCK), 0, s, G, out_idx, out_cnt, overflow);
+    hipLaunchKernelGGL(gather_link_kernel, dim3(grid_for(nparts)), dim3(BLOCK), 0, s, G, head, next);
+    hipLaunchKernelGGL(gather_merge_kernel, dim3(grid_for(nparts)), dim3(BLOCK), 0, s, G, head, next, out_idx, out_cnt);
     HIP_TRY(hipGetLastError());
     return KAD_OK;
 }

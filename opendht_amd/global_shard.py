@@ -7,12 +7,13 @@ Per rank s (one process per GPU):
     indices (index_base = nodes below lo); window lines make its interior queries one line each;
   * the GLOBAL good prefix sums (4 bytes per global bucket) are all-gathered once at setup, so the
     rank can compute any query's global window W(R) (routing_table.cpp:89-104);
-  * a step: kad_rt_shard_batch over the replicated batch appends complete rows (W(R) inside the
-    shard) and partial rows (W(R) crossing an edge, with XOR distances); the ranks' counters are
-    all-gathered (one small collective, one host read), then one payload per rank (its rows, then
-    its parts) in one all_gather_into_tensor; kad_rt_scatter_rows writes the rows straight from
-    the received buffer, kad_rt_merge_parts merges the parts. Every rank ends with every query's
-    result, bit-exact with RoutingTable::findClosestNodes on the whole table.
+  * a step is device-only: kad_rt_shard_batch over the replicated batch appends complete rows (W(R)
+    inside the shard) and partial rows (W(R) crossing an edge, with XOR distances) straight into the
+    rank's fixed-size send block; one all_gather_into_tensor of the blocks (RCCL over xGMI);
+    kad_rt_gather_finish scatters the complete rows by qid and merges each query's parts, reading every
+    count on the device. Every rank ends with every query's result, bit-exact with
+    RoutingTable::findClosestNodes on the whole table. No host read per step (a full buffer sets a
+    sticky overflow word checked once per batch), so steps can be captured in a HIP graph.
 
 The owner-routed halo variant (sharded.py) moves only results a client asked for; this variant
 is the one the north star describes and config 3 names ("RCCL all-gather + top-k merge").
@@ -24,7 +25,7 @@ import ctypes as C
 import numpy as np
 
 from . import synth as S
-from ._lib import check, lib, part_words, ptr, row_words
+from ._lib import check, lib, part_words, ptr, row_words, shard_block_words
 from .metrics import good_counts
 from .table import DeviceTable
 
@@ -70,6 +71,68 @@ def allgather_padded(x, n: int, group=None):
     return torch.stack(out), counts
 
 
+class Exchange:
+    """Fixed-size send / receive blocks of one step shape (q queries, count, world ranks): the layout of
+    kad_rt_gather_finish (include/kadgpu.h). A rank's send block is its kad_rt_shard_batch output in place
+    (REGIONS regions of row_cap complete rows, part_cap partial rows, the counters); one all-gather of the
+    blocks, then the device scatter + merge. The capacities are the same on every rank (they depend on
+    q, count and world only), so the collective is always matched. No host read per step: a region or
+    part buffer that fills sets the sticky overflow word, which the caller checks once per batch (query)
+    or once per K steps (bench.py) and then runs again with grown(); every rank reads the same gathered
+    counters, so every rank grows the same way."""
+
+    def __init__(self, q: int, count: int, world: int, device, row_cap: int | None = None,
+                 part_cap: int | None = None):
+        import torch
+
+        self.q, self.count, self.world, self.dev = q, count, world, device
+        # rows of query block k go to region k % 8, so this capacity can never overflow
+        self.row_cap_max = -(-(-(-q // 256)) // 8) * 256
+        est = -(-q // (REGIONS * world)) * 5 // 4 + 256  # uniform targets: ~q / world rows per rank
+        self.row_cap = max(1, min(self.row_cap_max, row_cap or est))
+        self.part_cap = max(1, part_cap or 1024)
+        rw, pw = row_words(count), part_words(count)
+        self.parts_off = REGIONS * self.row_cap * rw
+        self.ctr_off = self.parts_off + self.part_cap * pw
+        self.block = shard_block_words(count, self.row_cap, self.part_cap)
+        self.send = torch.empty((self.block,), dtype=torch.int32, device=device)
+        self.recv = self.send if world == 1 else torch.empty((world * self.block,), dtype=torch.int32, device=device)
+        self.scratch = torch.full((q + world * self.part_cap,), -1, dtype=torch.int32, device=device)
+        self.overflow = torch.zeros((1,), dtype=torch.int32, device=device)
+
+    @property
+    def gathered_bytes(self) -> int:
+        """Bytes every rank receives per step (world fixed-size blocks)."""
+        return 4 * self.world * self.block
+
+    def counters(self):
+        """This rank's counter words (a view of the send block)."""
+        return self.send[self.ctr_off:self.ctr_off + COUNTERS * CSTRIDE]
+
+    def overflowed(self) -> bool:
+        """Host read of the sticky overflow word (synchronises), cleared."""
+        v = bool(int(self.overflow.item()))
+        if v:
+            self.overflow.zero_()
+        return v
+
+    def grown(self) -> "Exchange":
+        """A new layout sized from the gathered counters of the last step (the same on every rank)."""
+        c = self.recv.view(self.world, self.block)[:, self.ctr_off:self.ctr_off + COUNTERS * CSTRIDE]
+        c = c.cpu().numpy().reshape(self.world, COUNTERS, CSTRIDE)[:, :, 0].astype(np.int64)
+        need_r, need_p = int(c[:, :REGIONS].max()), int(c[:, 8].max())
+        row_cap = self.row_cap if need_r <= self.row_cap else max(2 * self.row_cap, need_r * 5 // 4)
+        part_cap = self.part_cap if need_p <= self.part_cap else max(2 * self.part_cap, need_p * 5 // 4)
+        return Exchange(self.q, self.count, self.world, self.dev, row_cap=min(row_cap, self.row_cap_max),
+                        part_cap=part_cap)
+
+    def finish(self, out_idx, out_cnt, stream):
+        """kad_rt_gather_finish over the received blocks (device only)."""
+        check(lib().kad_rt_gather_finish(ptr(self.recv), self.world, self.row_cap, self.part_cap, self.q, self.count,
+                                         ptr(self.scratch), ptr(out_idx), ptr(out_cnt), ptr(self.overflow),
+                                         self.dev.index or 0, stream), "kad_rt_gather_finish")
+
+
 class GlobalShard:
     """Rank s's shard of a global U(depth) table, queried with the replicated-batch protocol."""
 
@@ -86,61 +149,59 @@ class GlobalShard:
         self.gpre = torch.from_numpy(gp.astype(np.uint32).view(np.int32)).to(self.dev)
         self.reach = reach(gp, lo, hi, count_max)
         self.base_hi = base_hi
-        self.ctr = torch.zeros(COUNTERS * CSTRIDE, dtype=torch.int32, device=self.dev)
-        self._cap = (0, 0, 0, 0)
+        self._ex = {}
 
     def close(self):
         self.table.close()
 
-    def _buffers(self, q: int, count: int, part_cap: int = 0):
+    def exchange(self, q: int, count: int, world: int) -> Exchange:
+        """The cached step layout for (q, count, world)."""
+        key = (q, count, world)
+        if key not in self._ex:
+            self._ex[key] = Exchange(q, count, world, self.dev)
+        return self._ex[key]
+
+    def local_block(self, targets, ex: Exchange, stream=None):
+        """kad_rt_shard_batch over a replicated (q, 20) device batch into ex's send block (counters zeroed
+        first); async on `stream` (a raw hipStream_t; default: the current torch stream)."""
         import torch
 
-        if self._cap[:2] != (q, count) or part_cap > self._cap[3]:
-            # rows of query block k go to region k % 8: this capacity can never overflow
-            row_cap = -(-(-(-q // 256)) // 8) * 256
-            part_cap = max(part_cap, 4096, q // 16)
-            self.rows = torch.empty((REGIONS * row_cap, row_words(count)), dtype=torch.int32, device=self.dev)
-            self.parts = torch.empty((part_cap, part_words(count)), dtype=torch.int32, device=self.dev)
-            self._cap = (q, count, row_cap, part_cap)
-        return self._cap[2], self._cap[3]
-
-    def local(self, targets, count: int, stream=None):
-        """This rank's rows (REGIONS regions of row_cap) and parts for a replicated (q, 20) device batch;
-        async on `stream`. Counters: rows per region, parts, overflow flag."""
-        import torch
-
-        q = targets.shape[0]
-        row_cap, part_cap = self._buffers(q, count)
-        s = C.c_void_p(stream if stream is not None else torch.cuda.current_stream(self.dev).cuda_stream)
-        self.ctr.zero_()
+        ctr = ex.counters()
+        if stream is None:
+            s = torch.cuda.current_stream(self.dev).cuda_stream
+            ctr.zero_()
+        else:
+            s = stream
+            with torch.cuda.stream(torch.cuda.ExternalStream(s, device=self.dev)):
+                ctr.zero_()
+        base = ex.send.data_ptr()
         check(lib().kad_rt_shard_batch(self.table.handle, ptr(self.gpre), self.GB, C.c_uint64(self.base_hi),
-                                       self.depth, self.lo, self.reach[0], self.reach[1], ptr(targets), q, count,
-                                       ptr(self.rows), row_cap, ptr(self.parts), part_cap, ptr(self.ctr), s),
-              "kad_rt_shard_batch")
-        return self.rows, self.parts, self.ctr
+                                       self.depth, self.lo, self.reach[0], self.reach[1], ptr(targets), ex.q,
+                                       ex.count, C.c_void_p(base), ex.row_cap, C.c_void_p(base + 4 * ex.parts_off),
+                                       ex.part_cap, ptr(ctr), C.c_void_p(s)), "kad_rt_shard_batch")
 
-    def local_compact(self, targets, count: int):
-        """local(), a host sync, and the valid rows / parts as contiguous (n, words) tensors. A part
-        buffer overflow (windows crossing many shard edges) grows the buffer and runs again."""
+    def step(self, targets, ex: Exchange, out_idx, out_cnt, group=None, stream=None):
+        """One device-only step: local block, all-gather of the fixed-size blocks (RCCL; gloo lists in the
+        CPU-rank tests; nothing at world 1), scatter + merge. No host read: check ex.overflowed() after.
+        `stream`: a raw hipStream_t, default the current torch stream (what graph capture uses)."""
         import torch
 
-        while True:
-            rows, parts, ctr = self.local(targets, count)
-            c = ctr.cpu().numpy()[::CSTRIDE]
-            if not c[9]:
-                break
-            if (c[:REGIONS] > self._cap[2]).any():
-                raise RuntimeError("kad_rt_shard_batch: row region overflow")
-            self._buffers(targets.shape[0], count, part_cap=2 * int(c[8]))
-        cap = self._cap[2]
-        valid = torch.cat([rows[r * cap:r * cap + int(c[r])] for r in range(REGIONS)])
-        return valid, parts[:int(c[8])]
+        self.local_block(targets, ex, stream)
+        s = stream if stream is not None else torch.cuda.current_stream(self.dev).cuda_stream
+        if ex.world > 1:
+            if stream is None:
+                gather_into(ex.recv, ex.send, group)
+            else:
+                with torch.cuda.stream(torch.cuda.ExternalStream(s, device=self.dev)):
+                    gather_into(ex.recv, ex.send, group)
+        ex.finish(out_idx, out_cnt, C.c_void_p(s))
 
     def query(self, targets, count: int, group=None, out_idx=None, out_cnt=None, single_rank_shard_kernel=False):
         """Every query's RoutingTable::findClosestNodes result on every rank: local rows and parts,
-        all-gather (RCCL / gloo), device scatter and merge. A single rank holds the whole table: the
-        exchange is empty and the batch is the plain kad_rt_closest_batch (single_rank_shard_kernel:
-        the shard kernel and the scatter instead, what each rank runs at N > 1 minus the exchange)."""
+        all-gather (RCCL / gloo), device scatter and merge; one host read of the overflow word per call
+        (a full buffer grows the layout and runs the batch again on every rank). A single rank holds the
+        whole table: the plain kad_rt_closest_batch (single_rank_shard_kernel: the shard kernel and the
+        finish instead, what each rank runs at N > 1 minus the collective)."""
         import torch
         import torch.distributed as dist
 
@@ -149,56 +210,48 @@ class GlobalShard:
             out_idx = torch.empty((q, count), dtype=torch.int32, device=self.dev)
         if out_cnt is None:
             out_cnt = torch.empty((q,), dtype=torch.uint8, device=self.dev)
-        if count == 0:
+        if count == 0 or q == 0:
             out_cnt.zero_()
             return out_idx, out_cnt
-        s = C.c_void_p(torch.cuda.current_stream(self.dev).cuda_stream)
         world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
         if world == 1:
             if (self.lo, self.hi) != (0, self.GB):
                 raise ValueError("a single rank must hold the whole table")
             if not single_rank_shard_kernel:
                 return self.table.rt_closest(targets, count, out_idx=out_idx, out_cnt=out_cnt)
-            # one shard = the whole table: every window is complete, no parts, no host sync
-            rows, _, ctr = self.local(targets, count)
-            check(lib().kad_rt_scatter_rows(ptr(rows), ptr(ctr), CSTRIDE, REGIONS, self._cap[2], count, ptr(out_idx),
-                                            ptr(out_cnt), self.device, s), "kad_rt_scatter_rows")
-            return out_idx, out_cnt
-        rw, pw = row_words(count), part_words(count)
-        while True:  # every rank's counters in one small gather, read once on the host
-            rows, parts, ctr = self.local(targets, count)
-            c_all = torch.empty((world, COUNTERS), dtype=torch.int32, device=self.dev)
-            gather_into(c_all.view(-1), ctr[::CSTRIDE][:COUNTERS].contiguous(), group)
-            c = c_all.cpu().numpy()
-            if not c[:, 9].any():
-                break
-            if (c[:, :REGIONS] > self._cap[2]).any():
-                raise RuntimeError("kad_rt_shard_batch: row region overflow")
-            # a part buffer overflowed somewhere: every rank grows its buffer and runs again
-            self._buffers(q, count, part_cap=2 * int(c[:, 8].max()))
-        n_r = c[:, :REGIONS].sum(axis=1)
-        maxr, maxp = int(n_r.max()), int(c[:, 8].max())
-        # one payload per rank: its rows, then its parts, padded to block_cap rows of rw words
-        block_cap = maxr + -(-maxp * pw // rw)
-        send = torch.empty((block_cap * rw,), dtype=torch.int32, device=self.dev)
-        cap, at = self._cap[2], 0
-        for r in range(REGIONS):
-            n = int(c[rank_of(group), r])
-            send[at:at + n * rw] = rows[r * cap:r * cap + n].reshape(-1)
-            at += n * rw
-        n_p = int(c[rank_of(group), 8])
-        send[maxr * rw:maxr * rw + n_p * pw] = parts[:n_p].reshape(-1)
-        recv = torch.empty((world * block_cap * rw,), dtype=torch.int32, device=self.dev)
-        gather_into(recv, send, group)
-        n_rows = torch.from_numpy(n_r.astype(np.int32)).to(self.dev)
-        check(lib().kad_rt_scatter_rows(ptr(recv), ptr(n_rows), 1, world, block_cap, count, ptr(out_idx),
-                                        ptr(out_cnt), self.device, s), "kad_rt_scatter_rows")
-        if maxp:
-            g = recv.view(world, block_cap * rw)
-            valid = torch.cat([g[r, maxr * rw:maxr * rw + int(c[r, 8]) * pw].view(-1, pw) for r in range(world)
-                               if c[r, 8]])
-            merge_valid_parts(valid, count, out_idx, out_cnt, self.device)
-        return out_idx, out_cnt
+        while True:
+            ex = self.exchange(q, count, world)
+            self.step(targets, ex, out_idx, out_cnt, group)
+            if not ex.overflowed():
+                return out_idx, out_cnt
+            self._ex[(q, count, world)] = ex.grown()
+
+
+def query_simulated(shards, targets, count: int, out_idx=None, out_cnt=None, row_cap=None, part_cap=None):
+    """Every shard of a global table in ONE process (one GPU, no collective): each shard's send block, the
+    blocks concatenated in rank order (exactly what all_gather_into_tensor delivers to every rank), the same
+    kad_rt_gather_finish. How the tests drive the exchange of N ranks on one GPU. Returns (out_idx, out_cnt,
+    the last Exchange)."""
+    import torch
+
+    q, world = targets.shape[0], len(shards)
+    dev = shards[0].dev
+    if out_idx is None:
+        out_idx = torch.empty((q, count), dtype=torch.int32, device=dev)
+    if out_cnt is None:
+        out_cnt = torch.empty((q,), dtype=torch.uint8, device=dev)
+    while True:
+        exs = [Exchange(q, count, world, dev, row_cap=row_cap, part_cap=part_cap) for _ in shards]
+        for sh, ex in zip(shards, exs):
+            sh.local_block(targets, ex)
+        ex0 = exs[0]
+        if world > 1:
+            torch.cat([e.send for e in exs], out=ex0.recv)
+        ex0.finish(out_idx, out_cnt, C.c_void_p(torch.cuda.current_stream(dev).cuda_stream))
+        if not ex0.overflowed():
+            return out_idx, out_cnt, ex0
+        g = ex0.grown()
+        row_cap, part_cap = g.row_cap, g.part_cap
 
 
 def gather_into(recv, send, group=None):

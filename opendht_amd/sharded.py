@@ -44,6 +44,7 @@ class ShardSpec:
     expired_pct: int = 10
     k_max: int = 32
     recipe_n: int = 0
+    _below: dict = field(default_factory=dict, repr=False, compare=False)  # nodes_below cache (recipe passes)
 
     @property
     def shard_bits(self) -> int:
@@ -81,15 +82,19 @@ class ShardSpec:
         if b <= 0:
             return 0
         if self.recipe_n:
-            import ctypes as C
+            if b >= self.n_buckets:
+                return self.recipe_n
+            if b not in self._below:  # one pass over all recipe_n draws: cached per spec
+                import ctypes as C
 
-            from ._lib import check, lib
+                from ._lib import check, lib
 
-            n, below = C.c_uint32(), C.c_uint64()
-            check(lib().kad_synth_recipe_range(S.SEED_IDS, S.SEED_STATUS, self.recipe_n, self.depth, b,
-                                               self.n_buckets, self.good_pct, self.expired_pct, 0, C.byref(n),
-                                               C.byref(below), None, None, None), "kad_synth_recipe_range")
-            return int(below.value)
+                n, below = C.c_uint32(), C.c_uint64()
+                check(lib().kad_synth_recipe_range(S.SEED_IDS, S.SEED_STATUS, self.recipe_n, self.depth, b,
+                                                   self.n_buckets, self.good_pct, self.expired_pct, 0, C.byref(n),
+                                                   C.byref(below), None, None, None), "kad_synth_recipe_range")
+                self._below[b] = int(below.value)
+            return self._below[b]
         import ctypes as C
 
         from ._lib import check, lib

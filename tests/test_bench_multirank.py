@@ -25,5 +25,8 @@ def test_bench_two_ranks_on_one_gpu():
     d = json.loads(lines[0])
     print(lines[0])
     assert d["n_gpus"] == 2 and d["value"] > 0
+    assert d["verified"]["rows"] == 2 * (1 << 16) and d["verified"]["mismatches"] == 0
     ag = d["allgather"]
+    assert "error" not in ag, ag
     assert ag["n_gpus"] == 2 and ag["value"] > 0 and ag["gathered_bytes_per_step"] > 0
+    assert ag["verified"]["rows"] > 0 and ag["verified"]["mismatches"] == 0

@@ -14,8 +14,8 @@ import torch.multiprocessing as mp
 import oracle as O
 from opendht_amd import DeviceTable
 from opendht_amd import synth as S
-from opendht_amd._lib import check, lib, ptr
-from opendht_amd.global_shard import GlobalShard, build_plain_shard, merge_parts, reach
+from opendht_amd._lib import check, lib, part_words, ptr, row_words
+from opendht_amd.global_shard import Exchange, GlobalShard, build_plain_shard, merge_parts, query_simulated, reach
 from opendht_amd.metrics import good_counts, window_radii
 from opendht_amd.sharded import ShardSpec
 
@@ -54,9 +54,44 @@ def _build(spec, device):
     return shards
 
 
+def _compact_path(shards, tg, count, gpu):
+    """The per-rank-compacted exchange through kad_rt_scatter_rows + kad_rt_merge_parts (the ABI's other
+    finish): every shard's rows and parts read out of its send block on the host side."""
+    q = tg.shape[0]
+    rw, pw = row_words(count), part_words(count)
+    rows, parts = [], []
+    for sh in shards:
+        ex = Exchange(q, count, len(shards), gpu, row_cap=-(-(-(-q // 256)) // 8) * 256, part_cap=max(4096, 8 * q))
+        sh.local_block(tg, ex)
+        c = ex.counters().cpu().numpy().reshape(-1, 32)[:, 0]
+        assert c[9] == 0
+        reg = ex.send[:ex.parts_off].view(8, ex.row_cap, rw)
+        rows.append(torch.cat([reg[r, :c[r]] for r in range(8)]))
+        parts.append(ex.send[ex.parts_off:ex.ctr_off].view(ex.part_cap, pw)[:c[8]])
+    out_idx = torch.full((q, count), -1, dtype=torch.int32, device=gpu)
+    out_cnt = torch.full((q,), 255, dtype=torch.uint8, device=gpu)
+    nr = [r.shape[0] for r in rows]
+    maxr = max(nr)
+    g_rows = torch.stack([torch.cat([r, r.new_zeros((maxr - r.shape[0], rw))]) for r in rows]).contiguous()
+    n_rows = torch.tensor(nr, dtype=torch.int32, device=gpu)
+    s = torch.cuda.current_stream(gpu).cuda_stream
+    check(lib().kad_rt_scatter_rows(ptr(g_rows), ptr(n_rows), 1, len(shards), maxr, count, ptr(out_idx),
+                                    ptr(out_cnt), gpu.index or 0, s), "scatter")
+    npart = [p.shape[0] for p in parts]
+    if max(npart):
+        maxp = max(npart)
+        g_parts = torch.stack([torch.cat([p, p.new_zeros((maxp - p.shape[0], pw))]) for p in parts])
+        merge_parts(g_parts, npart, count, out_idx, out_cnt, gpu.index or 0)
+    return out_idx, out_cnt, sum(npart)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("case", CASES, ids=lambda c: f"N{c[0]}_U{c[1]}_g{c[3]}")
 def test_global_shards_simulated_gather(gpu, case):
+    """N shards on one GPU: the fixed-block exchange (kad_rt_gather_finish, what every rank runs after
+    all_gather_into_tensor), started with capacities too small so that the overflow word makes it grow
+    and run again, and the compacted exchange (kad_rt_scatter_rows + kad_rt_merge_parts); both bit-exact
+    against the oracle on the whole table."""
     n_shards, depth, mean, good = case
     spec = ShardSpec(n_shards=n_shards, depth=depth, mean_per_bucket=mean, seed=0x6A7 + depth, good_pct=good,
                      expired_pct=(100 - good) // 2)
@@ -65,64 +100,120 @@ def test_global_shards_simulated_gather(gpu, case):
     targets = _targets(spec, 3000, seed=depth)
     tg = torch.from_numpy(targets).to(gpu)
     shards = _build(spec, gpu.index or 0)
+    grew = False
     try:
         for count in (1, 3, 8, 9, 14, 32):
-            outs = [sh.local_compact(tg, count) for sh in shards]
-            nr = [o[0].shape[0] for o in outs]
-            maxr = max(nr)
-            g_rows = torch.stack([torch.cat([o[0], o[0].new_zeros((maxr - o[0].shape[0], o[0].shape[1]))])
-                                  for o in outs]).contiguous()
-            n_rows = torch.tensor(nr, dtype=torch.int32, device=gpu)
-            q = targets.shape[0]
-            out_idx = torch.full((q, count), -1, dtype=torch.int32, device=gpu)
-            out_cnt = torch.full((q,), 255, dtype=torch.uint8, device=gpu)
-            s = torch.cuda.current_stream(gpu).cuda_stream
-            check(lib().kad_rt_scatter_rows(ptr(g_rows), ptr(n_rows), 1, len(shards), maxr, count, ptr(out_idx),
-                                            ptr(out_cnt), gpu.index or 0, s), "scatter")
-            npart = [o[1].shape[0] for o in outs]
-            if max(npart):
-                maxp = max(npart)
-                g_parts = torch.stack([torch.cat([o[1], o[1].new_zeros((maxp - o[1].shape[0], o[1].shape[1]))])
-                                       for o in outs])
-                merge_parts(g_parts, npart, count, out_idx, out_cnt, gpu.index or 0)
-            if n_shards == 1:  # the single-rank paths: the plain batch, the shard kernel without host sync
+            want, wcnt = O.flat_rt_closest(gids, gst, gfirst, goff, targets, count, nthreads=8)
+            for caps in ((None, None), (1, 1)):
+                idx, cnt, ex = query_simulated(shards, tg, count, row_cap=caps[0], part_cap=caps[1])
+                torch.cuda.synchronize()
+                np.testing.assert_array_equal(cnt.cpu().numpy(), wcnt, err_msg=f"{case} k={count} {caps} counts")
+                np.testing.assert_array_equal(idx.cpu().numpy().view(np.uint32), want, err_msg=f"{case} k={count} {caps}")
+                if caps[0] == 1:
+                    grew = grew or ex.row_cap > 1 or ex.part_cap > 1
+            idx, cnt, nparts = _compact_path(shards, tg, count, gpu)
+            torch.cuda.synchronize()
+            np.testing.assert_array_equal(cnt.cpu().numpy(), wcnt, err_msg=f"{case} k={count} compacted counts")
+            np.testing.assert_array_equal(idx.cpu().numpy().view(np.uint32), want, err_msg=f"{case} k={count} compacted")
+            if n_shards == 1:  # the single-rank paths: the plain batch, the shard kernel + finish (no host sync)
                 for sk in (False, True):
                     i2, c2 = shards[0].query(tg, count, single_rank_shard_kernel=sk)
                     torch.cuda.synchronize()
-                    np.testing.assert_array_equal(i2.cpu().numpy(), out_idx.cpu().numpy())
-                    np.testing.assert_array_equal(c2.cpu().numpy(), out_cnt.cpu().numpy())
-            torch.cuda.synchronize()
-            want, wcnt = O.flat_rt_closest(gids, gst, gfirst, goff, targets, count, nthreads=8)
-            np.testing.assert_array_equal(out_cnt.cpu().numpy(), wcnt, err_msg=f"{case} k={count} counts")
-            np.testing.assert_array_equal(out_idx.cpu().numpy().view(np.uint32), want, err_msg=f"{case} k={count}")
+                    np.testing.assert_array_equal(i2.cpu().numpy().view(np.uint32), want)
+                    np.testing.assert_array_equal(c2.cpu().numpy(), wcnt)
             if n_shards > 1 and count == 8:
-                assert sum(npart) > 0  # the edge targets produced parts
+                assert nparts > 0  # the edge targets produced parts
+        assert grew  # capacities of 1 overflowed and grew
     finally:
         for sh in shards:
             sh.close()
 
 
-@pytest.mark.gpu
-def test_whole_100M_table_one_gpu(gpu):
-    """The north-star table whole on one GPU (config 3's 100M-node U(24) table from the SURVEY §8d recipe, what
-    GlobalShard.query answers at N = 1): 1M random targets, EVERY query bit-exact against the oracle's closed
-    form for k = 8 and 14."""
+@pytest.fixture(scope="module")
+def table_100M():
+    """Config 3's 100M-node U(24) table from the SURVEY §8d recipe (what every rank's shard is cut from)."""
     from opendht_amd.sharded import config3_spec
 
     spec = config3_spec(1)
-    ids, st, off, lo, hi, base, _ = build_plain_shard(spec, 0)
+    ids, st, off, lo, hi, base, good = build_plain_shard(spec, 0)
     assert (lo, hi, base) == (0, spec.n_buckets, 0) and ids.shape[0] == 100_000_000
-    first = S.bucket_firsts(spec.depth, 0, spec.n_buckets)
-    q = 1 << 20
-    g = torch.Generator(device=gpu).manual_seed(0x100)
+    return spec, ids, st, off, good
+
+
+def _random_and_edge_targets(n_shards, depth, q, seed, gpu):
+    """q uniform random targets plus, for every shard edge, targets in the 5 buckets either side of it."""
+    g = torch.Generator(device=gpu).manual_seed(seed)
     tg = torch.randint(0, 256, (q, 20), dtype=torch.uint8, device=gpu, generator=g)
+    edge = ShardSpec(n_shards=n_shards, depth=depth, mean_per_bucket=1.0, seed=1)
+    et = _targets(edge, 0, seed=seed)
+    return torch.cat([tg, torch.from_numpy(et).to(gpu)]).contiguous()
+
+
+@pytest.mark.gpu
+def test_whole_100M_table_one_gpu(gpu, table_100M):
+    """The north-star table whole on one GPU (what GlobalShard.query answers at N = 1): 1M random targets plus
+    the targets next to the 8-shard edges, EVERY query bit-exact against the oracle's closed form for k = 8,
+    14 and 32, through the plain batch and through the shard kernel + kad_rt_gather_finish
+    (single_rank_shard_kernel, what each rank runs at N > 1 minus the collective)."""
+    spec, ids, st, off, good = table_100M
+    first = S.bucket_firsts(spec.depth, 0, spec.n_buckets)
+    gp = np.concatenate([[0], np.cumsum(good)])
+    tg = _random_and_edge_targets(8, spec.depth, 1 << 20, 0x100, gpu)
     targets = tg.cpu().numpy()
-    with DeviceTable(ids, st, first, off, device=gpu.index or 0, sorted=True) as T:
-        for k in (8, 14):
-            idx, cnt = T.rt_closest(tg, k)
+    G = GlobalShard(ids, st, off, 0, spec.n_buckets, spec.depth, 0, gp, device=gpu.index or 0)
+    try:
+        for k in (8, 14, 32):
             want, wcnt = O.flat_rt_closest(ids, st, first, off, targets, k, nthreads=16)
+            for sk in (False, True):
+                idx, cnt = G.query(tg, k, single_rank_shard_kernel=sk)
+                torch.cuda.synchronize()
+                np.testing.assert_array_equal(cnt.cpu().numpy(), wcnt, err_msg=f"k={k} shard_kernel={sk} counts")
+                np.testing.assert_array_equal(idx.cpu().numpy().view(np.uint32), want, err_msg=f"k={k} sk={sk}")
+    finally:
+        G.close()
+
+
+@pytest.mark.gpu
+def test_north_star_8_shards_100M(gpu, table_100M):
+    """BASELINE config 3 as the north star states it: the 100M-node table in 8 halo-free shards (the shards
+    bench.py's allgather variant builds at N = 8; all 8 on one GPU here), each answering its part of every
+    query's global window, the blocks concatenated as the RCCL all-gather delivers them, the device scatter
+    + merge. EVERY one of 1M random targets plus the shard-edge targets bit-exact against the oracle on the
+    whole table, k = 8, 14 and 32 (routing_table.cpp:89-104: windows that cross shard edges)."""
+    from opendht_amd.sharded import config3_spec
+
+    spec, ids, st, off, good = table_100M
+    first = S.bucket_firsts(spec.depth, 0, spec.n_buckets)
+    gp = np.concatenate([[0], np.cumsum(good)])
+    s8 = config3_spec(8)
+    per = spec.n_buckets // 8
+    # shard 5 as rank 5 of an 8-GPU run builds it (its own pass over the recipe) = the slice of the whole table
+    i5, st5, off5, lo5, hi5, base5, _ = build_plain_shard(s8, 5)
+    assert (lo5, hi5, base5) == (5 * per, 6 * per, int(off[5 * per]))
+    np.testing.assert_array_equal(i5, ids[off[lo5]:off[hi5]])
+    np.testing.assert_array_equal(st5, st[off[lo5]:off[hi5]])
+    np.testing.assert_array_equal(off5, (off[lo5:hi5 + 1] - off[lo5]).astype(np.uint32))
+    del i5, st5, off5
+    tg = _random_and_edge_targets(8, spec.depth, 1 << 20, 0x800, gpu)
+    targets = tg.cpu().numpy()
+    shards = []
+    try:
+        for s in range(8):
+            a, e = s * per, (s + 1) * per
+            n0, n1 = int(off[a]), int(off[e])
+            shards.append(GlobalShard(ids[n0:n1], st[n0:n1], (off[a:e + 1] - n0).astype(np.uint32), a, e, spec.depth,
+                                      n0, gp, device=gpu.index or 0))
+        for k in (8, 14, 32):
+            idx, cnt, ex = query_simulated(shards, tg, k)
+            want, wcnt = O.flat_rt_closest(ids, st, first, off, targets, k, nthreads=16)
+            torch.cuda.synchronize()
             np.testing.assert_array_equal(cnt.cpu().numpy(), wcnt, err_msg=f"k={k} counts")
             np.testing.assert_array_equal(idx.cpu().numpy().view(np.uint32), want, err_msg=f"k={k}")
+            c = ex.recv.view(8, ex.block)[:, ex.ctr_off:ex.ctr_off + 320].cpu().numpy().reshape(8, 10, 32)[:, :, 0]
+            assert c[:, 8].sum() > 0, "edge targets must produce parts"
+    finally:
+        for sh in shards:
+            sh.close()
 
 
 def test_reach_covers_every_touching_bucket():
