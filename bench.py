@@ -185,15 +185,18 @@ def device_targets(n_batches, q, shard_bits, shard, seed, dev):
     return out
 
 
-def node_times(status, now_ns):
+def node_times(status, now_ns, seed=0x71E):
     """Node::time / reply_time / expired_ arrays (node.h:39-40,105) that give `status` at now_ns under
-    Node::isGood (node.cpp:34-40): good -> heard now; expired -> expired_ set; dubious -> last query
-    answered 11 minutes ago (time < now - 10 min)."""
+    Node::isGood (node.cpp:34-40), shaped like a live table: good nodes were last heard uniformly over the
+    last 10 minutes and last replied over the last 120, so their isGood deadlines spread over the next 10
+    minutes; expired -> expired_ set; dubious -> last heard 11 minutes ago."""
     n = status.shape[0]
-    t = np.full(n, now_ns, np.int64)
-    rt = np.full(n, now_ns, np.int64)
+    rng = np.random.default_rng(seed)
+    MIN = 60 * 10**9
+    t = now_ns - rng.integers(0, 10 * MIN, n, dtype=np.int64)
+    rt = now_ns - rng.integers(0, 120 * MIN, n, dtype=np.int64)
     dub = (status & 3) == 0
-    t[dub] = now_ns - 11 * 60 * 10**9
+    t[dub] = now_ns - 11 * MIN
     expired = ((status & 2) != 0).astype(np.uint8)
     return t, rt, expired
 
@@ -410,6 +413,8 @@ def main_owner(args):
         extras["refresh"] = refresh_pass(T, sh, tgs, outs, ocnt, cnt_k, Q, avg_kernel_s, dev, stream)
         extras["host_buffers"] = host_pass(T, tgs, cnt_k, Q, dev)
         extras["other_counts"] = counts_pass(T, tgs, Q, dev, stream)
+        if rank == 0:
+            extras["latency"] = latency_pass(dev)
     # the rows of the last timed step (batch K-1), checked against the CPU restatement on this rank's
     # shard table (exact halo: every owned window lies inside it)
     vrows = min(Q, args.verify_rows)
@@ -549,6 +554,49 @@ def counts_pass(T, tgs, Q, dev, stream, reps=16):
     return res
 
 
+def latency_pass(dev, nodes=170, reps=2000):
+    """One Dht request's findClosestNodes through the boundary: kad_rt_closest_batch_host (what
+    RoutingTableMirror::findClosestNodes calls) with 1 and 64 queries on a live-sized table (~170 nodes in the
+    reference split policy, SURVEY.md §6: the reference answers one such call in ~8 us at 10k nodes).
+    Beside it, the structure-faithful CPU restatement (oracle/, the port) on the same table and targets."""
+    from opendht_amd import DeviceTable
+    from opendht_amd import synth as S
+    from opendht_amd._lib import check, lib, ptr
+
+    ids = S.random_ids(nodes, 0x1A7)
+    st = S.random_status(nodes, 0x1A8, 80, 10)
+    perm, first, off = S.split_table(ids, 8)
+    ids, st = np.ascontiguousarray(ids[perm]), np.ascontiguousarray(st[perm])
+    tg = S.random_targets(4096, seed=0x1A9)
+    res = {"nodes": nodes, "buckets": int(first.shape[0])}
+    with DeviceTable(ids, st, first, off, device=dev.index or 0) as T:
+        for q in (1, 64):
+            oi, oc = np.zeros((q, 8), np.uint32), np.zeros((q,), np.uint8)
+            ts = []
+            for r in range(reps):
+                x = np.ascontiguousarray(tg[(r * q) % (4096 - q):(r * q) % (4096 - q) + q])
+                t0 = time.perf_counter()
+                check(lib().kad_rt_closest_batch_host(T.handle, ptr(x), q, 8, ptr(oi), ptr(oc)), "host batch")
+                ts.append(time.perf_counter() - t0)
+            res[f"gpu_call_q{q}_us"] = float(np.median(ts)) * 1e6
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+
+    F = O.FaithfulTable(ids, st, first, off)
+    ts = []
+    for r in range(reps):
+        x = np.ascontiguousarray(tg[r % 4096:r % 4096 + 1])
+        t0 = time.perf_counter()
+        F.rt_closest(x, 8, nthreads=1)
+        ts.append(time.perf_counter() - t0)
+    F.close()
+    res["cpu_port_call_us"] = float(np.median(ts)) * 1e6
+    res["how"] = (f"median of {reps} synchronous calls, k=8, host buffers in and out (ctypes overhead included); "
+                  "gpu: one kernel launch reading the targets from and writing the rows to mapped pinned memory; "
+                  "cpu_port: the std::list restatement of routing_table.cpp:67-135 on one thread, same table")
+    return res
+
+
 def host_pass(T, tgs, cnt_k, Q, dev, nb=8):
     """The PCIe-inclusive rate (targets in host memory, rows back to host memory; never the headline `value`):
     `sync_abi`: kad_rt_closest_batch_host, the synchronous host-pointer call on pageable buffers (the table's pinned
@@ -600,43 +648,59 @@ def host_pass(T, tgs, cnt_k, Q, dev, nb=8):
 
 
 def refresh_pass(T, sh, tgs, outs, ocnt, cnt_k, Q, avg_kernel_s, dev, stream, reps=5):
-    """Cost of keeping every node's isGood(now) / isExpired() current on the device (node.cpp:34-40):
-    kad_table_refresh_status(now) re-derives the status from the node times in one pass and rebuilds
-    only the masks and lines that the flips touch; kad_table_patch_status applies a changed-node list."""
+    """Cost of keeping every node's isGood(now) / isExpired() current on the device (node.cpp:34-40).
+    kad_table_refresh_status(now) keeps the nodes' deadlines min(time + 10 min, reply_time + 120 min) sorted:
+    a refresh re-derives only the nodes whose deadline `now` passed and the patched ones, and returns without
+    touching the GPU while `now` is below the next deadline. The node times are those of a live table (good
+    nodes heard over the last 10 minutes), so moving `now` by dt ages ~dt / 10 min of the good nodes."""
     import torch
 
     now = 10**15
     n = sh.ids.shape[0]
     t, rt, ex = node_times(sh.status, now)
     T.set_times(t, rt, ex)
+    MIN = 60 * 10**9
+    D = np.sort(np.minimum(t + 10 * MIN, rt + 120 * MIN)[ex == 0])
 
-    def ev_time(fn):
+    def timed(fn):
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize(dev)
+        h0 = time.perf_counter()
         a.record(stream)
         fn()
         b.record(stream)
+        h1 = time.perf_counter()
         torch.cuda.synchronize(dev)
-        return a.elapsed_time(b) / 1e3
+        return a.elapsed_time(b), (h1 - h0) * 1e3  # GPU ms (events), host ms of the call
 
-    T.refresh_status(now, stream=stream.cuda_stream)
+    first = timed(lambda: T.refresh_status(now, stream=stream.cuda_stream))  # every node, the deadline runs built
     torch.cuda.synchronize(dev)
-    no_flip = float(np.median([ev_time(lambda j=j: T.refresh_status(now + 1 + j, stream=stream.cuda_stream))
-                               for j in range(reps)]))
+    # `now` moving by 1 ns .. 1 us: below the next deadline, so no GPU work at all
+    nf = [timed(lambda j=j: T.refresh_status(now + 1 + j, stream=stream.cuda_stream)) for j in range(reps)]
+    now += 1 + reps
+    ticks = {}
+    for dt_ms in (1, 10, 100, 1000, 10000):  # one refresh after `now` moved by dt: the deadlines it passes
+        t0 = now
+        now += dt_ms * 10**6
+        flips = int(np.searchsorted(D, now, "left") - np.searchsorted(D, t0, "left"))
+        g_ms, h_ms = timed(lambda: T.refresh_status(now, stream=stream.cuda_stream))
+        ticks[f"{dt_ms}ms"] = {"gpu_ms": g_ms, "host_call_ms": h_ms, "aged_nodes": flips}
     rng = np.random.default_rng(0xF11)
-    good = np.flatnonzero(sh.status & 1).astype(np.uint32)
+    st_now = T.export_status()
+    good = np.flatnonzero(st_now & 1).astype(np.uint32)
     ageing = {}
-    for frac in (0.001, 0.01):  # that share of the good nodes was last heard 10 min + 1 ns before `now`
+    for frac in (0.001, 0.01):  # that share of the good nodes reported last heard 10 min + 1 ns before `now`
         sel = rng.choice(good, size=int(good.shape[0] * frac), replace=False).astype(np.uint32)
-        now += 10**9
-        T.patch_times(sel, np.full(sel.shape[0], now - 10 * 60 * 10**9 - 1, np.int64), np.full(sel.shape[0], now, np.int64),
+        now += 10**6
+        T.patch_times(sel, np.full(sel.shape[0], now - 10 * MIN - 1, np.int64), np.full(sel.shape[0], now, np.int64),
                       np.zeros(sel.shape[0], np.uint8))
-        ageing[f"{frac:g}"] = ev_time(lambda: T.refresh_status(now, stream=stream.cuda_stream)) * 1e3
+        ageing[f"{frac:g}"] = timed(lambda: T.refresh_status(now, stream=stream.cuda_stream))[0]
         T.patch_times(sel, np.full(sel.shape[0], now, np.int64), np.full(sel.shape[0], now, np.int64),
                       np.zeros(sel.shape[0], np.uint8))
         T.refresh_status(now, stream=stream.cuda_stream)
         torch.cuda.synchronize(dev)
     patch = {}
-    st = sh.status.copy()
+    st = T.export_status()
     for frac in (0.001, 0.01, 0.1):
         m = int(n * frac)
         nodes = rng.choice(n, size=m, replace=False).astype(np.uint32)
@@ -645,16 +709,25 @@ def refresh_pass(T, sh, tgs, outs, ocnt, cnt_k, Q, avg_kernel_s, dev, stream, re
         T.patch_status(nodes, vals)
         patch[f"{frac:g}"] = (time.perf_counter() - t0) * 1e3
         T.patch_status(nodes, st[nodes])  # back
-    return {"refresh_no_flip_ms": no_flip * 1e3,
+    no_flip_gpu = float(np.median([x[0] for x in nf]))
+    no_flip_host = float(np.median([x[1] for x in nf]))
+    return {"refresh_no_flip_ms": no_flip_gpu,
+            "refresh_no_flip_host_call_ms": no_flip_host,
+            "refresh_first_ms": first[0],
+            "refresh_tick_ms": ticks,
             "refresh_ageing_ms": ageing,
             "patch_status_ms": patch,
             "nodes": int(n),
-            "refresh_plus_query_queries_per_s": Q / (no_flip + avg_kernel_s),
-            "how": "refresh_no_flip: kad_table_refresh_status(now) with `now` moved and no status flipping (one "
-                   f"pass over {n} nodes' times + good-prefix scan), median of {reps}, HIP events; refresh_ageing: "
-                   "the same with that share of the good nodes ageing past 10 min; patch_status: "
-                   "kad_table_patch_status of a random changed-node list of that share of the nodes (host list, "
-                   "synchronous, wall clock incl. the H2D copy); refresh_plus_query: one refresh + one step"}
+            "refresh_plus_query_queries_per_s": Q / (no_flip_gpu * 1e-3 + avg_kernel_s),
+            "how": "refresh_no_flip: kad_table_refresh_status(now) with `now` moved by 1 ns .. 5 ns (below the next "
+                   "isGood deadline: the call returns without GPU work), median of 5: GPU time between HIP events and "
+                   "the host time of the call; refresh_first: the first refresh after set_times (every node, the "
+                   "deadline runs sorted); refresh_tick: one refresh after `now` moved by dt, aged_nodes = the good "
+                   "nodes whose deadline it passes (live-table times: good nodes heard over the last 10 min); "
+                   "refresh_ageing: patch_times of that share of the good nodes as last heard 10 min + 1 ns ago, "
+                   "then the refresh (GPU ms); patch_status: kad_table_patch_status of a random changed-node list of "
+                   "that share of the nodes (host list, synchronous, wall clock incl. the H2D copy); "
+                   "refresh_plus_query: one no-flip refresh + one step"}
 
 
 # ---------------------------------------------------------------------------------------------

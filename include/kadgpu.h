@@ -54,7 +54,9 @@ extern "C" {
 #define KAD_HASH_LEN 20u            /* reference infohash.h:49 HASH_LEN */
 #define KAD_TARGET_NODES 8u         /* reference routing_table.h:26 TARGET_NODES */
 #define KAD_SEARCH_NODES 14u        /* reference dht.h:314 SEARCH_NODES */
-#define KAD_MAX_COUNT 32u           /* largest `count` the batch kernels accept */
+#define KAD_MAX_COUNT 32u           /* largest `count` of the line kernels; RoutingTable queries take any
+                                       count (larger ones run one wave per query); the shard / wire
+                                       entry points stay at <= KAD_MAX_COUNT */
 #define KAD_NO_NODE 0xFFFFFFFFu     /* padding index in result rows */
 
 /* status byte bits (snapshot of Node state at `now`) */
@@ -191,12 +193,16 @@ int kad_table_export(const kad_table* t, uint8_t* ids, uint8_t* status, uint8_t*
  * on the table's status snapshot. Device pointers:
  *   targets  q x 20 bytes; out_idx q x count uint32; out_cnt q uint8 (may be NULL).
  * Row i of out_idx holds the result in the reference's order (ascending XOR
- * distance), out_cnt[i] entries, padded with KAD_NO_NODE. count <= KAD_MAX_COUNT. */
+ * distance), out_cnt[i] entries, padded with KAD_NO_NODE. Any count, as the reference's
+ * size_t count (routing_table.h:48): counts up to KAD_MAX_COUNT run the line kernels, larger
+ * ones one wave per query; out_cnt saturates at 255 (for count > 255 the result length is the
+ * row's entries before the first KAD_NO_NODE). */
 int kad_rt_closest_batch(const kad_table* t, const uint8_t* targets, uint32_t q, uint32_t count,
                          uint32_t* out_idx, uint8_t* out_cnt, void* stream);
 /* The same on host buffers (any memory), synchronous and ordered after the device work issued before the
- * call. The first call gives the table ~80 MB of pinned staging and device buffers (freed with it); batches
- * run as 64k-query chunks pipelined over four host threads. One host batch per table at a time. */
+ * call on the null stream. The first call gives the table ~80 MB of pinned staging and device buffers (freed
+ * with it); batches run as 64k-query chunks pipelined over four host threads. One host batch per table at a
+ * time. count <= 2,097,152 (one chunk row; larger counts: the device-pointer batch). */
 int kad_rt_closest_batch_host(const kad_table* t, const uint8_t* targets, uint32_t q, uint32_t count,
                               uint32_t* out_idx, uint8_t* out_cnt);
 

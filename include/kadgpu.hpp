@@ -203,15 +203,21 @@ public:
     std::vector<std::vector<NodePtr>> findClosestNodesBatch(const InfoHashT* ids, size_t q, TimePoint now,
                                                             size_t count = KAD_TARGET_NODES) const {
         advance(to_ns(now));
+        std::vector<std::vector<NodePtr>> out(q);
+        // any size_t count, as routing_table.h:48: a result never holds more than the table's nodes
+        count = std::min(count, nodes_.size());
+        if (count == 0 || q == 0) return out;
         std::vector<uint8_t> targets(q * KAD_HASH_LEN);
         for (size_t i = 0; i < q; i++) std::memcpy(&targets[i * KAD_HASH_LEN], id_bytes(ids[i]), KAD_HASH_LEN);
         std::vector<uint32_t> idx;
         std::vector<uint8_t> cnt;
         table_.findClosestNodesBatch(targets.data(), q, count, idx, cnt);
-        std::vector<std::vector<NodePtr>> out(q);
         for (size_t i = 0; i < q; i++) {
-            out[i].reserve(cnt[i]);
-            for (size_t j = 0; j < cnt[i]; j++) out[i].push_back(nodes_[idx[i * count + j]]);
+            size_t m = cnt[i];
+            if (count > 255)  // the count byte saturates: the row's padding gives the length
+                for (m = 0; m < count && idx[i * count + m] != KAD_NO_NODE; m++) {}
+            out[i].reserve(m);
+            for (size_t j = 0; j < m; j++) out[i].push_back(nodes_[idx[i * count + j]]);
         }
         return out;
     }

@@ -36,6 +36,7 @@
 //      on the fast path. Windows beyond the prefetch or with >32-node buckets take a per-node
 //      slow path with the same results.
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <array>
@@ -651,6 +652,76 @@ __global__ __launch_bounds__(BLOCK) void rt_closest_kernel(DevTable T, const uin
     }
     __shared__ uint64_t xs[BLOCK / 64][192];
     exact_tail(T, t, ex, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
+}
+
+// ---------------------------------------------------------------------------------------
+// Any count (the reference takes any size_t, routing_table.h:48): counts above the line kernels' 32 take one
+// wave per query. The window W(R) comes from the good prefix sums (wave_window), and every good node of it
+// is ranked by counting, tile against tile: a lane holds one node of its 64-node tile and counts the good
+// nodes of every tile that precede it in (160-bit XOR distance, index) order, so windows of any size need
+// only the wave's 1.5 KB of LDS. Rows beyond the result are padded with NONE; the count byte saturates at
+// 255 (a caller asking for more reads the count off the padding).
+// ---------------------------------------------------------------------------------------
+__device__ void wave_rank_any(const DevTable& T, const Target& t, uint32_t beg, uint32_t end, uint32_t good,
+                              uint32_t count, uint32_t* row, uint8_t* cp, uint64_t* xs) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t m = min(count, good);
+    for (uint32_t a = beg; a < end; a += 64) {
+        const uint32_t j = a + lane;
+        uint64_t V0 = ~0ull, V1 = ~0ull, V2 = ~0ull;
+        const bool v = j < end && (T.status[j] & KAD_STATUS_GOOD);
+        if (v) {
+            const uint32_t* tl = T.tail + 3ull * j;
+            V0 = T.key[j] ^ t.hi;
+            V1 = ((uint64_t)(tl[0] ^ t.t2) << 32) | (tl[1] ^ t.t3);
+            V2 = ((uint64_t)(tl[2] ^ t.t4) << 32) | j;
+        }
+        uint32_t rank = 0;
+        for (uint32_t c = beg; c < end; c += 64) {
+            const uint32_t jc = c + lane;
+            uint64_t C0 = ~0ull, C1 = ~0ull, C2 = ~0ull;  // not good: after every node
+            if (jc < end && (T.status[jc] & KAD_STATUS_GOOD)) {
+                const uint32_t* tl = T.tail + 3ull * jc;
+                C0 = T.key[jc] ^ t.hi;
+                C1 = ((uint64_t)(tl[0] ^ t.t2) << 32) | (tl[1] ^ t.t3);
+                C2 = ((uint64_t)(tl[2] ^ t.t4) << 32) | jc;
+            }
+            __builtin_amdgcn_wave_barrier();
+            xs[3 * lane] = C0;
+            xs[3 * lane + 1] = C1;
+            xs[3 * lane + 2] = C2;
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_wave_barrier();
+#pragma unroll 8
+            for (uint32_t sl = 0; sl < 64; sl++) rank += lt3(xs[3 * sl], xs[3 * sl + 1], xs[3 * sl + 2], V0, V1, V2);
+            __builtin_amdgcn_wave_barrier();
+        }
+        if (v && rank < count) row[rank] = j + T.index_base;
+    }
+    for (uint32_t p = m + lane; p < count; p += 64) row[p] = NONE;
+    if (lane == 0 && cp) *cp = (uint8_t)min(m, 255u);
+}
+
+// One wave per query; af (may be NULL): the query's family, 0 -> T4, 1 -> T6 (kad_rt_closest_batch_dual).
+__global__ __launch_bounds__(BLOCK) void rt_wave_kernel(DevTable T4, DevTable T6, const uint8_t* __restrict__ af,
+                                                        const uint8_t* __restrict__ targets, uint32_t q, uint32_t count,
+                                                        uint32_t* __restrict__ out_idx, uint8_t* __restrict__ out_cnt) {
+    __shared__ uint64_t xs[BLOCK / 64][192];
+    const uint32_t w = threadIdx.x >> 6, i = blockIdx.x * (BLOCK / 64) + w;
+    if (i >= q) return;  // wave-uniform
+    const DevTable& T = (af && af[i]) ? T6 : T4;
+    const Target t = load_target(targets, i);
+    uint32_t* row = out_idx + (size_t)i * count;
+    uint8_t* cp = out_cnt ? out_cnt + i : nullptr;
+    const uint32_t lane = threadIdx.x & 63u;
+    if (T.B == 0) {  // an empty table: an empty result (routing_table.cpp:73)
+        for (uint32_t p = lane; p < count; p += 64) row[p] = NONE;
+        if (lane == 0 && cp) *cp = 0;
+        return;
+    }
+    uint32_t lo, hi, good;
+    wave_window(T.gpre, T.B, locate_bucket(T, t), count, lo, hi, good);
+    wave_rank_any(T, t, T.dir[lo].x & ~WIDE, T.dir[hi + 1].x & ~WIDE, good, count, row, cp, xs[w]);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -4284,9 +4355,11 @@ struct StatusMarks {
     uint64_t nbase;
     uint32_t nshift, nslots, n;
     uint32_t nback, nfwd; // NodeCache lines hold nodes r0(s)-nfwd .. r0(s)+nback-1 (the widest line set present)
+    uint32_t* any;        // set to 1 by any change: the incremental rebuild's kernels exit at once without one
 };
 
 __device__ __forceinline__ void mark_status_change(const StatusMarks& M, uint32_t i, uint32_t old_st, uint32_t st) {
+    if (M.any && *M.any == 0) *M.any = 1;  // a plain store of the same value: at most one per wave instruction
     if (M.bdirty && ((old_st ^ st) & KAD_STATUS_GOOD)) {
         uint32_t lo = 0, hi = M.B;  // the last bucket whose first node is <= i (upper_bound - 1)
         while (lo < hi) {
@@ -4307,19 +4380,101 @@ __device__ __forceinline__ void mark_status_change(const StatusMarks& M, uint32_
     }
 }
 
-__global__ void status_from_times_kernel(const int64_t* time_ns, const int64_t* reply_ns, const uint8_t* expired,
-                                         uint32_t n, int64_t now, uint8_t* status, StatusMarks M) {
-    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
-    if (i >= n) return;
-    // node.cpp:34-40 with NODE_GOOD_TIME = 120 min, NODE_EXPIRE_TIME = 10 min (node.h:91-94)
-    const int64_t GOOD = 120LL * 60 * 1000000000LL, EXP = 10LL * 60 * 1000000000LL;
-    const bool ex = expired[i] != 0;
-    const bool good = !ex && reply_ns[i] >= now - GOOD && time_ns[i] >= now - EXP;
-    const uint32_t st = (good ? KAD_STATUS_GOOD : 0u) | (ex ? KAD_STATUS_EXPIRED : 0u);
-    const uint32_t old = status[i];
+// node.cpp:34-40 with NODE_GOOD_TIME = 120 min, NODE_EXPIRE_TIME = 10 min (node.h:91-94)
+constexpr int64_t NODE_GOOD_NS = 120LL * 60 * 1000000000LL, NODE_EXPIRE_NS = 10LL * 60 * 1000000000LL;
+
+struct NodeTimes {
+    const int64_t* time_ns;
+    const int64_t* reply_ns;
+    const uint8_t* expired;
+};
+
+// The status byte of node i at `now`: Node::isGood(now) (node.cpp:34-40) and Node::isExpired() (node.h:67).
+__device__ __forceinline__ uint32_t status_at(const NodeTimes& N, uint32_t i, int64_t now) {
+    const bool ex = N.expired[i] != 0;
+    const bool good = !ex && N.reply_ns[i] >= now - NODE_GOOD_NS && N.time_ns[i] >= now - NODE_EXPIRE_NS;
+    return (good ? KAD_STATUS_GOOD : 0u) | (ex ? KAD_STATUS_EXPIRED : 0u);
+}
+
+__device__ __forceinline__ void refresh_node(const NodeTimes& N, uint32_t i, int64_t now, uint8_t* status,
+                                             const StatusMarks& M) {
+    const uint32_t st = status_at(N, i, now), old = status[i];
     if (old != st) {
         status[i] = (uint8_t)st;
         mark_status_change(M, i, old, st);
+    }
+}
+
+__global__ void status_from_times_kernel(NodeTimes N, uint32_t n, int64_t now, uint8_t* status, StatusMarks M) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i < n) refresh_node(N, i, now, status, M);
+}
+
+// ---------------------------------------------------------------------------------------
+// isGood(now) deadlines. A node that is good at `now` stays good exactly while now <= D with
+// D = min(time + 10 min, reply_time + 120 min) (node.cpp:34-40); a later `now` can only turn it bad, and
+// only new times (patch_times) can turn a node good. So a refresh at a later `now` has to look at the
+// nodes whose D it passes and at the patched ones, nothing else. The deadlines are kept as two sorted
+// runs of (key = D as an order-preserving unsigned, node): the main run (every node, built on the device
+// by a radix sort at the first refresh after set_times) and a side run (the deadlines of patched nodes,
+// merged on the host at patch time). A cursor per run separates the deadlines already passed. A refresh
+// finds how far `now` moves each cursor with one 64-ary wave search, re-derives the status of the nodes
+// in between and of the patched ones, and publishes the next deadline (the smallest unpassed key) to the
+// host, which skips the next refresh entirely while `now` stays at or below it.
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ int64_t sat_add(int64_t a, int64_t b /* > 0 */) {
+    return a > INT64_MAX - b ? INT64_MAX : a + b;
+}
+__host__ __device__ __forceinline__ uint64_t dl_key(int64_t d) { return (uint64_t)d ^ 0x8000000000000000ull; }
+constexpr uint64_t DL_NEVER = ~0ull;  // expired nodes: never good, whatever `now`
+
+__global__ void deadline_kernel(NodeTimes N, uint32_t n, uint64_t* __restrict__ key, uint32_t* __restrict__ node) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n) return;
+    key[i] = N.expired[i] ? DL_NEVER
+                          : dl_key(min(sat_add(N.time_ns[i], NODE_EXPIRE_NS), sat_add(N.reply_ns[i], NODE_GOOD_NS)));
+    node[i] = i;
+}
+
+// lower_bound of x in the ascending k[lo, n), by the whole wave: each round 64 lanes probe evenly spaced
+// points and a ballot keeps the one interval that holds the answer (4 dependent loads for 12.5M keys).
+__device__ uint32_t wave_lower_bound(const uint64_t* k, uint32_t lo, uint32_t n, uint64_t x) {
+    const uint32_t lane = threadIdx.x & 63u;
+    uint32_t hi = n;  // the answer lies in [lo, hi]
+    while (hi - lo > 64) {
+        const uint32_t p = lo + (uint32_t)(((uint64_t)(hi - lo) * (lane + 1)) / 65);
+        const uint32_t c = (uint32_t)__builtin_popcountll(__ballot(k[p] < x));  // monotone in the lane
+        const uint32_t nlo = c ? rdl(p, c - 1) + 1 : lo;
+        const uint32_t nhi = c < 64 ? rdl(p, c) : hi;
+        lo = nlo;
+        hi = nhi;
+    }
+    const uint32_t j = lo + lane;
+    return lo + (uint32_t)__builtin_popcountll(__ballot(j < hi && k[j] < x));
+}
+
+// One wave. cur: [0] main cursor, [1] side cursor, [2..3] the main range passed now, [4..5] the side range.
+__global__ void dl_search_kernel(const uint64_t* __restrict__ km, uint32_t nm, const uint64_t* __restrict__ ks,
+                                 uint32_t ns, uint64_t nowk, uint32_t* __restrict__ cur, uint64_t* __restrict__ next) {
+    const uint32_t cm = cur[0], cs = cur[1];
+    const uint32_t hm = wave_lower_bound(km, cm, nm, nowk), hs = wave_lower_bound(ks, cs, ns, nowk);
+    if (threadIdx.x == 0) {
+        cur[2] = cm; cur[3] = hm; cur[4] = cs; cur[5] = hs;
+        cur[0] = hm; cur[1] = hs;
+        *next = min(hm < nm ? km[hm] : DL_NEVER, hs < ns ? ks[hs] : DL_NEVER);
+    }
+}
+
+// The nodes whose deadline `now` passed (both runs' ranges from dl_search_kernel) and the patched nodes:
+// status re-derived from their times. A node listed twice gets the same status twice.
+__global__ void dl_process_kernel(NodeTimes N, const uint32_t* __restrict__ mnode, const uint32_t* __restrict__ snode,
+                                  const uint32_t* __restrict__ cur, const uint32_t* __restrict__ pend, uint32_t np,
+                                  uint32_t n, int64_t now, uint8_t* status, StatusMarks M) {
+    const uint32_t a = cur[3] - cur[2], b = cur[5] - cur[4];
+    const uint64_t total = (uint64_t)a + b + np;
+    for (uint64_t j = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; j < total; j += (uint64_t)gridDim.x * BLOCK) {
+        const uint32_t i = j < a ? mnode[cur[2] + j] : j < (uint64_t)a + b ? snode[cur[4] + (j - a)] : pend[j - a - b];
+        if (i < n) refresh_node(N, i, now, status, M);
     }
 }
 
@@ -4352,9 +4507,10 @@ __global__ void times_patch_kernel(const uint32_t* nodes, const int64_t* t, cons
 // cleared. A line of bucket c reads buckets [c-3, c+2] (count <= 8: W(r <= 2)), [c-4, c+3] (9..16:
 // W(r <= 3)) or [c-8, c+7] (17..32: W(r <= 7)), so bucket b dirties lines [b-2, b+3], [b-3, b+4], [b-7, b+8].
 __global__ void bucket_good_dirty_kernel(const uint8_t* status, uint2* dir, uint32_t B, uint32_t* cnt,
-                                         uint8_t* bdirty, uint8_t* ld8, uint8_t* ld16, uint8_t* ld32) {
+                                         uint8_t* bdirty, uint8_t* ld8, uint8_t* ld16, uint8_t* ld32,
+                                         const uint32_t* any) {
     const uint32_t b = blockIdx.x * BLOCK + threadIdx.x;
-    if (b >= B || !bdirty[b]) return;
+    if (!*any || b >= B || !bdirty[b]) return;
     bdirty[b] = 0;
     const uint32_t j0 = dir[b].x & ~WIDE, j1 = dir[b + 1].x & ~WIDE;
     uint32_t g = 0, mask = 0;
@@ -4415,9 +4571,12 @@ __device__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* lds, uint32_t& to
 // Flags -> a compact list of their indices, flags cleared. Each thread takes 16 flags (one 16-byte load;
 // flag arrays are padded to 16 bytes), the block scans the counts in LDS and claims its range with ONE
 // atomic (a single counter hit by every wave saturates at ~90 adds per microsecond).
-__global__ __launch_bounds__(BLOCK) void compact_flags_kernel(uint8_t* flags, uint32_t m, uint32_t* list, uint32_t* ctr) {
+// any: NULL, or a word that is 0 when no flag can be set (the kernel exits at once).
+__global__ __launch_bounds__(BLOCK) void compact_flags_kernel(uint8_t* flags, uint32_t m, uint32_t* list, uint32_t* ctr,
+                                                              const uint32_t* any) {
     __shared__ uint32_t lds[4];
     __shared__ uint32_t base_s;
+    if (any && !*any) return;  // grid-uniform
     const uint32_t g = blockIdx.x * BLOCK + threadIdx.x, i0 = 16 * g;
     uint4 v = make_uint4(0, 0, 0, 0);
     if (i0 < m) v = reinterpret_cast<const uint4*>(flags)[g];
@@ -4439,8 +4598,11 @@ __global__ __launch_bounds__(BLOCK) void compact_flags_kernel(uint8_t* flags, ui
 }
 
 // Tile-local exclusive scan of cnt[0..m) written to out; tile sums to sums[tile].
-__global__ __launch_bounds__(BLOCK) void scan_tiles_kernel(const uint32_t* cnt, uint32_t m, uint32_t* out, uint32_t* sums) {
+// any (scan kernels): NULL, or a word that is 0 when the counts did not change (the kernel exits at once).
+__global__ __launch_bounds__(BLOCK) void scan_tiles_kernel(const uint32_t* cnt, uint32_t m, uint32_t* out, uint32_t* sums,
+                                                           const uint32_t* any) {
     __shared__ uint32_t lds[4];
+    if (any && !*any) return;
     const uint32_t base = blockIdx.x * SCAN_TILE + threadIdx.x * SCAN_ITEMS;
     uint32_t v[SCAN_ITEMS], s = 0;
 #pragma unroll
@@ -4456,8 +4618,9 @@ __global__ __launch_bounds__(BLOCK) void scan_tiles_kernel(const uint32_t* cnt, 
 }
 
 // Single-block exclusive scan of the tile sums (in place), looping over chunks.
-__global__ __launch_bounds__(BLOCK) void scan_sums_kernel(uint32_t* sums, uint32_t m) {
+__global__ __launch_bounds__(BLOCK) void scan_sums_kernel(uint32_t* sums, uint32_t m, const uint32_t* any) {
     __shared__ uint32_t lds[4];
+    if (any && !*any) return;
     uint32_t carry = 0;
     for (uint32_t c = 0; c < m; c += BLOCK) {
         const uint32_t i = c + threadIdx.x;
@@ -4469,9 +4632,10 @@ __global__ __launch_bounds__(BLOCK) void scan_sums_kernel(uint32_t* sums, uint32
     }
 }
 
-__global__ void scan_apply_kernel(const uint32_t* part, const uint32_t* sums, uint32_t m, uint32_t* gpre) {
+__global__ void scan_apply_kernel(const uint32_t* part, const uint32_t* sums, uint32_t m, uint32_t* gpre,
+                                  const uint32_t* any) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
-    if (i >= m) return;
+    if ((any && !*any) || i >= m) return;
     gpre[i] = part[i] + sums[i / SCAN_TILE];
 }
 
@@ -4594,7 +4758,17 @@ struct HostPipe {
     Slot slot[WORKERS][SLOTS];
     hipEvent_t start = nullptr;  // recorded on the null stream: the slots' streams wait for prior device work
     std::mutex mu;      // one host batch per table at a time
+    // Small batches (single Dht requests): one launch on pinned host memory the kernel reads and writes
+    // directly (mapped into the device's address space), no copies, one stream synchronise.
+    static constexpr uint32_t SMALL = 1024, SMALL_COUNT = 64;
+    uint8_t *st = nullptr, *sc = nullptr;  // pinned: targets, counts
+    uint32_t* si = nullptr;                // pinned: rows
+    uint8_t *dst = nullptr, *dsc = nullptr;  // their device addresses
+    uint32_t* dsi = nullptr;
+    hipStream_t ss = nullptr;
     ~HostPipe() {
+        if (ss) { (void)hipStreamSynchronize(ss); (void)hipStreamDestroy(ss); }
+        for (void* p : {(void*)st, (void*)sc, (void*)si}) if (p) (void)hipHostFree(p);
         for (auto& w : slot)
             for (Slot& S : w) {
                 if (S.s) (void)hipStreamSynchronize(S.s);
@@ -4604,6 +4778,47 @@ struct HostPipe {
                 if (S.s) (void)hipStreamDestroy(S.s);
             }
         if (start) (void)hipEventDestroy(start);
+    }
+};
+
+// isGood(now) deadlines of a table with node times (kad_table_refresh_status; the device side is at
+// deadline_kernel). valid: the runs, cursors and status bytes agree with the device times at last_now.
+struct Deadlines {
+    bool valid = false;
+    int64_t last_now = INT64_MIN;
+    uint64_t* km = nullptr;        // main run: keys and nodes, n entries (device)
+    uint32_t* kn = nullptr;
+    uint32_t nm = 0, mcap = 0;
+    uint64_t* ks = nullptr;        // side run: deadlines of patched nodes (device), kept sorted on the host
+    uint32_t* sn = nullptr;
+    uint32_t ns = 0, scap = 0;
+    std::vector<uint64_t> hks;
+    std::vector<uint32_t> hsn;
+    uint32_t* pend = nullptr;      // nodes patched since the last refresh (device), re-derived at the next one
+    uint32_t np = 0, pcap = 0;
+    std::vector<uint32_t> hpend;
+    uint32_t* cur = nullptr;       // 8 words: cursors and the ranges passed (dl_search_kernel)
+    uint64_t* next_dev = nullptr;  // the smallest unpassed key after the last refresh
+    uint64_t* next_host = nullptr; // its pinned copy, valid once `ev` completed
+    hipEvent_t ev = nullptr;
+    bool ev_pending = false, next_known = false;
+    uint64_t next = 0;
+    void* tmp = nullptr;           // radix-sort scratch: keys, nodes, hipcub temp storage
+    size_t tmp_bytes = 0;
+    ~Deadlines() {
+        for (void* p : {(void*)km, (void*)kn, (void*)ks, (void*)sn, (void*)pend, (void*)cur, (void*)next_dev, tmp})
+            if (p) (void)hipFree(p);
+        if (next_host) (void)hipHostFree(next_host);
+        if (ev) (void)hipEventDestroy(ev);
+    }
+    void invalidate() {
+        valid = false;
+        np = 0;
+        ns = 0;
+        hpend.clear();
+        hks.clear();
+        hsn.clear();
+        next_known = false;
     }
 };
 
@@ -4654,7 +4869,14 @@ struct kad_table {
     size_t stage_bytes = 0;
     mutable std::mutex pipe_mu;     // creates `pipe` on the first host-pointer batch
     mutable HostPipe* pipe = nullptr;
+    Deadlines dl;                   // isGood(now) deadlines (kad_table_refresh_status)
+    hipStream_t ss[2] = {nullptr, nullptr};  // side streams of an incremental rebuild (side_streams)
+    hipEvent_t ev_fork = nullptr, ev_join[2] = {nullptr, nullptr};
     ~kad_table() {
+        for (hipStream_t x : ss)
+            if (x) { (void)hipStreamSynchronize(x); (void)hipStreamDestroy(x); }
+        for (hipEvent_t e : {ev_fork, ev_join[0], ev_join[1]})
+            if (e) (void)hipEventDestroy(e);
         delete pipe;
         for (void* p : owned) (void)hipFree(p);
         for (void* p : {(void*)bdirty, (void*)ld8, (void*)ld16, (void*)ld32, (void*)ndirty, (void*)dlist, (void*)dctr, stage})
@@ -4674,9 +4896,28 @@ bool is_gfx950(int dev) {
 // the window lines and the NodeCache lines. full: every bucket and line; otherwise only what the
 // StatusMarks of the last status change flagged (kad_table_refresh_status / update / patch; ensure_marks
 // must have run). Async on stream.
+// The table's two side streams and the fork / join events of an incremental rebuild (created on first use).
+int side_streams(kad_table* t) {
+    for (hipStream_t& x : t->ss)
+        if (!x) HIP_TRY(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
+    if (!t->ev_fork) HIP_TRY(hipEventCreateWithFlags(&t->ev_fork, hipEventDisableTiming));
+    for (hipEvent_t& e : t->ev_join)
+        if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    return KAD_OK;
+}
+
+int rebuild_good_prefix_(kad_table* t, hipStream_t s, bool full);
 int rebuild_good_prefix(kad_table* t, hipStream_t s, bool full = true) {
+    const int rc = rebuild_good_prefix_(t, s, full);
+    // the change flag of the marks just consumed (StatusMarks::any)
+    if (rc == KAD_OK && t->dctr) HIP_TRY(hipMemsetAsync(t->dctr + 4, 0, sizeof(uint32_t), s));
+    return rc;
+}
+int rebuild_good_prefix_(kad_table* t, hipStream_t s, bool full) {
     const uint32_t B = t->d.B;
     uint32_t* ctr = t->dctr;
+    // incremental: every kernel exits at once when no status changed (dctr[4], set by mark_status_change)
+    const uint32_t* any = full ? nullptr : t->dctr + 4;
     if (!full) HIP_TRY(hipMemsetAsync(ctr, 0, 4 * sizeof(uint32_t), s));
     // line builders loop over their items: an incremental rebuild (a dirty list whose length only the device
     // knows) launches at most one chip-filling grid instead of one thread per line
@@ -4686,7 +4927,7 @@ int rebuild_good_prefix(kad_table* t, hipStream_t s, bool full = true) {
         if (!full) {
             uint32_t* lst = t->dlist + 3ull * B;
             hipLaunchKernelGGL(compact_flags_kernel, dim3(grid_for((t->d.nslots + 15) / 16)), dim3(BLOCK), 0, s,
-                               t->ndirty, t->d.nslots, lst, ctr + 3);
+                               t->ndirty, t->d.nslots, lst, ctr + 3, any);
             sel = LineSel{lst, ctr + 3};
         }
         hipLaunchKernelGGL(ncl_build_kernel, lgrid(t->d.nslots), dim3(BLOCK), 0, s, t->d.key, t->d.status,
@@ -4704,30 +4945,48 @@ int rebuild_good_prefix(kad_table* t, hipStream_t s, bool full = true) {
     else
         hipLaunchKernelGGL(bucket_good_dirty_kernel, dim3(grid_for(B)), dim3(BLOCK), 0, s, t->d.status, t->dir_mut, B,
                            t->scan_cnt, t->bdirty, (t->wl_mut || t->gl_mut) ? t->ld8 : nullptr,
-                           (t->wl16_mut || t->gl16_mut) ? t->ld16 : nullptr, (t->wl32_mut || t->gl32_mut) ? t->ld32 : nullptr);
-    hipLaunchKernelGGL(scan_tiles_kernel, dim3(tiles), dim3(BLOCK), 0, s, t->scan_cnt, m, t->scan_part, t->scan_sums);
-    hipLaunchKernelGGL(scan_sums_kernel, dim3(1), dim3(BLOCK), 0, s, t->scan_sums, tiles);
-    hipLaunchKernelGGL(scan_apply_kernel, dim3(grid_for(m)), dim3(BLOCK), 0, s, t->scan_part, t->scan_sums, m, t->gpre_mut);
+                           (t->wl16_mut || t->gl16_mut) ? t->ld16 : nullptr, (t->wl32_mut || t->gl32_mut) ? t->ld32 : nullptr,
+                           any);
+    hipLaunchKernelGGL(scan_tiles_kernel, dim3(tiles), dim3(BLOCK), 0, s, t->scan_cnt, m, t->scan_part, t->scan_sums, any);
+    hipLaunchKernelGGL(scan_sums_kernel, dim3(1), dim3(BLOCK), 0, s, t->scan_sums, tiles, any);
+    hipLaunchKernelGGL(scan_apply_kernel, dim3(grid_for(m)), dim3(BLOCK), 0, s, t->scan_part, t->scan_sums, m, t->gpre_mut,
+                       any);
     // the lines of every bucket (full) or only the compacted dirty ones
-    auto sel_for = [&](uint8_t* flags, uint32_t k) -> LineSel {
+    auto sel_for = [&](uint8_t* flags, uint32_t k, hipStream_t st) -> LineSel {
         if (full) return LineSel{};
-        hipLaunchKernelGGL(compact_flags_kernel, dim3(grid_for((B + 15) / 16)), dim3(BLOCK), 0, s, flags, B,
-                           t->dlist + (size_t)k * B, ctr + k);
+        hipLaunchKernelGGL(compact_flags_kernel, dim3(grid_for((B + 15) / 16)), dim3(BLOCK), 0, st, flags, B,
+                           t->dlist + (size_t)k * B, ctr + k, any);
         return LineSel{t->dlist + (size_t)k * B, ctr + k};
     };
+    // Three independent chains (an incremental rebuild is a few latency-bound items per builder, so they
+    // overlap): A = count <= 8 lines and everything that shares the general tables' gdirty flags, on s;
+    // B = the uniform count 9..16 lines and C = the count 17..32 lines on the table's side streams, forked
+    // from s after the prefix sums and joined back into s.
+    hipStream_t sB = s, sC = s;
+    const bool fork = !full && t->wl16_mut && (t->wl32_mut || t->gl32_mut) && side_streams(t) == KAD_OK;
+    if (fork) {
+        HIP_TRY(hipEventRecord(t->ev_fork, s));
+        sB = t->ss[0];
+        sC = t->ss[1];
+        HIP_TRY(hipStreamWaitEvent(sB, t->ev_fork, 0));
+        HIP_TRY(hipStreamWaitEvent(sC, t->ev_fork, 0));
+    }
+    if (t->wl16_mut)
+        hipLaunchKernelGGL(wl16_build_kernel, lgrid(B), dim3(BLOCK), 0, sB, t->d.key, t->d.status, t->d.dir,
+                           t->d.gpre, B, 64 - t->d.rshift, t->d.rbase >> t->d.rshift, t->wl16_mut, sel_for(t->ld16, 1, sB));
+    if (t->wl32_mut)
+        hipLaunchKernelGGL(wl32_build_kernel, lgrid(B), dim3(BLOCK), 0, sC, t->d.key, t->d.status, t->d.dir,
+                           t->d.gpre, B, 64 - t->d.rshift, t->d.rbase >> t->d.rshift, t->wl32_mut, sel_for(t->ld32, 2, sC));
+    if (t->gl32_mut)
+        hipLaunchKernelGGL(gl32_build_kernel, lgrid(B), dim3(BLOCK), 0, sC, t->d.key, t->d.status, t->d.dir,
+                           t->d.gpre, t->d.fkey, t->d.ftail, B, t->gl32_mut, sel_for(t->ld32, 2, sC));
     LineSel s8{};
-    if (t->wl_mut || t->gl_mut) s8 = sel_for(t->ld8, 0);
+    if (t->wl_mut || t->gl_mut) s8 = sel_for(t->ld8, 0, s);
     if (t->wl_mut)
         hipLaunchKernelGGL(wl_build_kernel, lgrid(B), dim3(BLOCK), 0, s, t->d.key, t->d.status, t->d.dir,
                            t->d.gpre, B, 64 - t->d.rshift, t->d.rbase >> t->d.rshift, t->wl_mut, s8);
     if (t->ws_mut)  // transcoded from the 128-byte lines just rebuilt, the same selection
         hipLaunchKernelGGL(ws_build_kernel, lgrid(B), dim3(BLOCK), 0, s, t->wl_mut, B, t->ws_mut, s8);
-    if (t->wl16_mut)
-        hipLaunchKernelGGL(wl16_build_kernel, lgrid(B), dim3(BLOCK), 0, s, t->d.key, t->d.status, t->d.dir,
-                           t->d.gpre, B, 64 - t->d.rshift, t->d.rbase >> t->d.rshift, t->wl16_mut, sel_for(t->ld16, 1));
-    if (t->wl32_mut)
-        hipLaunchKernelGGL(wl32_build_kernel, lgrid(B), dim3(BLOCK), 0, s, t->d.key, t->d.status, t->d.dir,
-                           t->d.gpre, B, 64 - t->d.rshift, t->d.rbase >> t->d.rshift, t->wl32_mut, sel_for(t->ld32, 2));
     if (t->gl_mut)
         hipLaunchKernelGGL(gl_build_kernel, lgrid(B), dim3(BLOCK), 0, s, t->d.key, t->d.status, t->d.dir,
                            t->d.gpre, t->d.fkey, t->d.ftail, B, t->gl_mut, s8);
@@ -4739,7 +4998,7 @@ int rebuild_good_prefix(kad_table* t, hipStream_t s, bool full = true) {
         if (!full) hipLaunchKernelGGL(mark_sel_kernel, lgrid(B), dim3(BLOCK), 0, s, s8, B, t->gdirty, (uint8_t)0);
     }
     if (t->gl16_mut) {
-        const LineSel s16 = sel_for(t->ld16, 1);
+        const LineSel s16 = sel_for(t->ld16, 1, s);
         hipLaunchKernelGGL(gl16_build_kernel, lgrid(B), dim3(BLOCK), 0, s, t->d.key, t->d.status, t->d.dir,
                            t->d.gpre, t->d.fkey, t->d.ftail, B, t->gl16_mut, s16);
         if (t->sl16_mut) {  // their slot-indexed copies: all, or the flagged buckets'
@@ -4750,9 +5009,12 @@ int rebuild_good_prefix(kad_table* t, hipStream_t s, bool full = true) {
             if (!full) hipLaunchKernelGGL(mark_sel_kernel, lgrid(B), dim3(BLOCK), 0, s, s16, B, t->gdirty, (uint8_t)0);
         }
     }
-    if (t->gl32_mut)
-        hipLaunchKernelGGL(gl32_build_kernel, lgrid(B), dim3(BLOCK), 0, s, t->d.key, t->d.status, t->d.dir,
-                           t->d.gpre, t->d.fkey, t->d.ftail, B, t->gl32_mut, sel_for(t->ld32, 2));
+    if (fork) {
+        HIP_TRY(hipEventRecord(t->ev_join[0], sB));
+        HIP_TRY(hipEventRecord(t->ev_join[1], sC));
+        HIP_TRY(hipStreamWaitEvent(s, t->ev_join[0], 0));
+        HIP_TRY(hipStreamWaitEvent(s, t->ev_join[1], 0));
+    }
     HIP_TRY(hipGetLastError());
     return KAD_OK;
 }
@@ -4925,7 +5187,7 @@ int ensure_marks(kad_table* t) {
     if (t->ncl_mut && (rc = alloc(&t->ndirty, t->d.nslots))) return rc;
     uint8_t *l = reinterpret_cast<uint8_t*>(t->dlist), *c = reinterpret_cast<uint8_t*>(t->dctr);
     if ((rc = alloc(&l, 4 * (3ull * t->d.B + (t->ncl_mut ? t->d.nslots : 0u) + 1)))) return rc;
-    if ((rc = alloc(&c, 4 * sizeof(uint32_t)))) return rc;
+    if ((rc = alloc(&c, 8 * sizeof(uint32_t)))) return rc;  // 4 list lengths, [4] the change flag
     t->dlist = reinterpret_cast<uint32_t*>(l);
     t->dctr = reinterpret_cast<uint32_t*>(c);
     return KAD_OK;
@@ -4952,6 +5214,7 @@ StatusMarks marks_of(const kad_table* t) {
     M.n = t->d.n;
     M.nback = t->ncl32_mut ? NC32_SLOTS - NC32_LEFT : NCL_SLOTS - NCL_LEFT;
     M.nfwd = t->ncl32_mut ? NC32_LEFT : NCL_LEFT;
+    M.any = t->dctr ? t->dctr + 4 : nullptr;
     return M;
 }
 
@@ -4962,6 +5225,142 @@ int stage_reserve(kad_table* t, size_t bytes) {
     hipError_t e = hipMalloc(&t->stage, std::max<size_t>(bytes, 4096));
     if (e != hipSuccess) { t->stage = nullptr; return set_err(KAD_ERR_NOMEM, "hipMalloc(%zu) failed", bytes); }
     t->stage_bytes = std::max<size_t>(bytes, 4096);
+    return KAD_OK;
+}
+
+// ---- isGood(now) deadlines, host side (see deadline_kernel) ----
+NodeTimes times_of(const kad_table* t) { return NodeTimes{t->time_ns, t->reply_ns, t->expired}; }
+
+int dl_alloc(void** p, size_t bytes) {
+    hipError_t e = hipMalloc(p, std::max<size_t>(bytes, 16));
+    if (e != hipSuccess) { *p = nullptr; return set_err(KAD_ERR_NOMEM, "hipMalloc(%zu) failed: %s", bytes, hipGetErrorString(e)); }
+    return KAD_OK;
+}
+
+// The next deadline to the host: an async copy into pinned memory and an event (read by the next refresh).
+int dl_publish(kad_table* t, hipStream_t s) {
+    Deadlines& D = t->dl;
+    HIP_TRY(hipMemcpyAsync(D.next_host, D.next_dev, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipEventRecord(D.ev, s));
+    D.ev_pending = true;
+    D.next_known = false;
+    return KAD_OK;
+}
+
+// Main run of every node's deadline from the device times (radix sort by key), the side run emptied, the
+// cursors at the first deadline >= nowk (everything before it counts as passed). Async on s.
+int dl_build_main(kad_table* t, hipStream_t s, uint64_t nowk) {
+    Deadlines& D = t->dl;
+    const uint32_t n = t->d.n;
+    int rc;
+    if (!D.cur) {
+        if ((rc = dl_alloc((void**)&D.cur, 8 * sizeof(uint32_t))) || (rc = dl_alloc((void**)&D.next_dev, 8))) return rc;
+        HIP_TRY(hipHostMalloc((void**)&D.next_host, sizeof(uint64_t), hipHostMallocDefault));
+        HIP_TRY(hipEventCreateWithFlags(&D.ev, hipEventDisableTiming));
+    }
+    if (D.mcap < n) {
+        if (D.km) { (void)hipFree(D.km); D.km = nullptr; }
+        if (D.kn) { (void)hipFree(D.kn); D.kn = nullptr; }
+        if (D.tmp) { (void)hipFree(D.tmp); D.tmp = nullptr; D.tmp_bytes = 0; }
+        D.mcap = 0;
+        if ((rc = dl_alloc((void**)&D.km, 8ull * n)) || (rc = dl_alloc((void**)&D.kn, 4ull * n))) return rc;
+        size_t cub = 0;
+        HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, cub, (const uint64_t*)nullptr, (uint64_t*)nullptr,
+                                                   (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)n, 0, 64, s));
+        const size_t kb = (8ull * n + 255) & ~255ull, nb = (4ull * n + 255) & ~255ull;
+        if ((rc = dl_alloc(&D.tmp, kb + nb + cub))) return rc;
+        D.tmp_bytes = kb + nb + cub;
+        D.mcap = n;
+    }
+    const size_t kb = (8ull * n + 255) & ~255ull, nb = (4ull * n + 255) & ~255ull;
+    uint64_t* tk = static_cast<uint64_t*>(D.tmp);
+    uint32_t* tn = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(D.tmp) + kb);
+    void* ct = static_cast<uint8_t*>(D.tmp) + kb + nb;
+    size_t cb = D.tmp_bytes - kb - nb;
+    hipLaunchKernelGGL(deadline_kernel, dim3(grid_for(n)), dim3(BLOCK), 0, s, times_of(t), n, tk, tn);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipcub::DeviceRadixSort::SortPairs(ct, cb, tk, D.km, tn, D.kn, (int)n, 0, 64, s));
+    D.nm = n;
+    D.ns = 0;
+    D.hks.clear();
+    D.hsn.clear();
+    HIP_TRY(hipMemsetAsync(D.cur, 0, 8 * sizeof(uint32_t), s));
+    hipLaunchKernelGGL(dl_search_kernel, dim3(1), dim3(64), 0, s, D.km, D.nm, D.ks, 0u, nowk, D.cur, D.next_dev);
+    HIP_TRY(hipGetLastError());
+    return dl_publish(t, s);
+}
+
+// patch_times on the deadline runs (synchronous; the device times are already updated): the patched nodes
+// join the pending list (re-derived at the next refresh, whatever `now`), their new deadlines the side run.
+// Side entries below last_now are dropped (passed; the pending list covers them). A side run grown past an
+// eighth of the main run is folded into a rebuilt main run.
+int dl_patch(kad_table* t, uint32_t m, const uint32_t* nodes, const int64_t* time_ns, const int64_t* reply_ns,
+             const uint8_t* expired) {
+    Deadlines& D = t->dl;
+    if (!D.valid) return KAD_OK;
+    if ((uint64_t)D.hpend.size() + m > t->d.n) {  // more patched than nodes: a full refresh is cheaper
+        D.invalidate();
+        return KAD_OK;
+    }
+    const uint64_t lk = dl_key(D.last_now);
+    auto sat = [](int64_t a, int64_t b) { return a > INT64_MAX - b ? INT64_MAX : a + b; };
+    std::vector<std::pair<uint64_t, uint32_t>> add;
+    add.reserve(m);
+    for (uint32_t j = 0; j < m; j++) {
+        D.hpend.push_back(nodes[j]);
+        const uint64_t k = expired[j] ? DL_NEVER
+                                      : dl_key(std::min(sat(time_ns[j], NODE_EXPIRE_NS), sat(reply_ns[j], NODE_GOOD_NS)));
+        if (k >= lk) add.emplace_back(k, nodes[j]);
+    }
+    std::sort(add.begin(), add.end());
+    std::vector<uint64_t> nk;
+    std::vector<uint32_t> nn;
+    nk.reserve(D.hks.size() + add.size());
+    nn.reserve(D.hks.size() + add.size());
+    size_t x = 0, y = 0;
+    while (x < D.hks.size() || y < add.size()) {
+        const bool take_old = y == add.size() || (x < D.hks.size() && D.hks[x] <= add[y].first);
+        const uint64_t k = take_old ? D.hks[x] : add[y].first;
+        const uint32_t v = take_old ? D.hsn[x] : add[y].second;
+        if (take_old) x++; else y++;
+        if (k >= lk) { nk.push_back(k); nn.push_back(v); }
+    }
+    D.hks.swap(nk);
+    D.hsn.swap(nn);
+    int rc;
+    // (re)allocate a pair of device arrays to hold `need` entries; on failure both are freed and cap is 0
+    auto grow = [&](void** a, size_t ea, void** b, size_t eb, uint32_t& cap, size_t need) -> int {
+        if (cap >= need) return KAD_OK;
+        const size_t c = std::max<size_t>(need + need / 2, 4096);
+        for (void** p : {a, b})
+            if (p && *p) { (void)hipFree(*p); *p = nullptr; }
+        cap = 0;
+        int r = dl_alloc(a, c * ea);
+        if (r == KAD_OK && b) r = dl_alloc(b, c * eb);
+        if (r != KAD_OK) {
+            for (void** p : {a, b})
+                if (p && *p) { (void)hipFree(*p); *p = nullptr; }
+            return r;
+        }
+        cap = (uint32_t)c;
+        return KAD_OK;
+    };
+    if ((rc = grow((void**)&D.pend, 4, nullptr, 0, D.pcap, D.hpend.size()))) return rc;
+    HIP_TRY(hipMemcpy(D.pend, D.hpend.data(), 4ull * D.hpend.size(), hipMemcpyHostToDevice));
+    D.np = (uint32_t)D.hpend.size();
+    if (D.hks.size() > D.nm / 8 + 65536) {  // fold the side run into a rebuilt main run
+        if ((rc = dl_build_main(t, nullptr, lk))) return rc;
+        HIP_TRY(hipDeviceSynchronize());
+        return KAD_OK;
+    }
+    if ((rc = grow((void**)&D.ks, 8, (void**)&D.sn, 4, D.scap, D.hks.size()))) return rc;
+    if (!D.hks.empty()) {
+        HIP_TRY(hipMemcpy(D.ks, D.hks.data(), 8ull * D.hks.size(), hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(D.sn, D.hsn.data(), 4ull * D.hsn.size(), hipMemcpyHostToDevice));
+    }
+    D.ns = (uint32_t)D.hks.size();
+    const uint32_t zero = 0;
+    HIP_TRY(hipMemcpy(D.cur + 1, &zero, sizeof zero, hipMemcpyHostToDevice));  // every side entry is unpassed
     return KAD_OK;
 }
 
@@ -5042,8 +5441,12 @@ void launch_rt_dual(const DevTable& d4, const DevTable& d6, const uint8_t* targe
 
 int rt_dispatch(const kad_table* t, const uint8_t* targets, uint32_t q, uint32_t count, uint32_t* out, uint8_t* cnt,
                 hipStream_t s) {
-    int rc;
-    if (count <= 8) rc = launch_rt<8>(t, targets, q, count, out, cnt, s);
+    int rc = KAD_OK;
+    if (count > KAD_MAX_COUNT) {
+        if ((uint64_t)q > 0xFFFFFFFFull / 4 * BLOCK / 64) return set_err(KAD_ERR_INVALID, "batch too large");
+        hipLaunchKernelGGL(rt_wave_kernel, dim3((q + BLOCK / 64 - 1) / (BLOCK / 64)), dim3(BLOCK), 0, s, t->d, t->d,
+                           nullptr, targets, q, count, out, cnt);
+    } else if (count <= 8) rc = launch_rt<8>(t, targets, q, count, out, cnt, s);
     else if (count <= 16) rc = launch_rt<16>(t, targets, q, count, out, cnt, s);
     else rc = launch_rt<32>(t, targets, q, count, out, cnt, s);
     if (rc) return rc;
@@ -5398,6 +5801,7 @@ int kad_table_patch_status(kad_table* t, uint32_t m, const uint32_t* nodes, cons
     DeviceGuard g(t->device);
     int rc;
     if ((rc = ensure_marks(t))) return rc;
+    t->dl.invalidate();  // status bytes set directly: the next refresh_status re-derives every node from its times
     if (m) {
         const size_t ib = nodes ? ((4ull * m + 15) & ~15ull) : 0;
         if ((rc = stage_reserve(t, ib + m))) return rc;
@@ -5423,6 +5827,7 @@ int kad_table_patch_times(kad_table* t, uint32_t m, const uint32_t* nodes, const
     if (!m) return KAD_OK;
     DeviceGuard g(t->device);
     int rc;
+    HIP_TRY(hipDeviceSynchronize());  // a refresh still running reads the staging and the deadline runs
     const size_t a = (4ull * m + 15) & ~15ull, b = 8ull * m;
     if ((rc = stage_reserve(t, a + 2 * b + m))) return rc;
     uint8_t* st = static_cast<uint8_t*>(t->stage);
@@ -5435,6 +5840,10 @@ int kad_table_patch_times(kad_table* t, uint32_t m, const uint32_t* nodes, const
                        st + a + 2 * b, m, t->d.n, t->time_ns, t->reply_ns, t->expired);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipDeviceSynchronize());
+    if ((rc = dl_patch(t, m, nodes, time_ns, reply_ns, expired))) {
+        t->dl.invalidate();  // the next refresh re-derives every node: still exact
+        return rc;
+    }
     return KAD_OK;
 }
 
@@ -5448,6 +5857,7 @@ int kad_table_set_times(kad_table* t, const int64_t* time_ns, const int64_t* rep
             (rc = dev_upload(&t->expired, nullptr, t->d.n, t->owned, t->bytes)))
             return rc;
     }
+    t->dl.invalidate();  // the next refresh re-derives every node and rebuilds the deadline runs
     if (t->d.n) {
         HIP_TRY(hipMemcpy(t->time_ns, time_ns, 8ull * t->d.n, hipMemcpyHostToDevice));
         HIP_TRY(hipMemcpy(t->reply_ns, reply_ns, 8ull * t->d.n, hipMemcpyHostToDevice));
@@ -5463,18 +5873,47 @@ int kad_table_refresh_status(kad_table* t, int64_t now_ns, void* stream) {
     hipStream_t s = (hipStream_t)stream;
     int rc;
     if ((rc = ensure_marks(t))) return rc;
-    if (t->d.n)
-        hipLaunchKernelGGL(status_from_times_kernel, dim3(grid_for(t->d.n)), dim3(BLOCK), 0, s, t->time_ns, t->reply_ns,
-                           t->expired, t->d.n, now_ns, t->status_mut, marks_of(t));
+    Deadlines& D = t->dl;
+    const uint32_t n = t->d.n;
+    const uint64_t nowk = dl_key(now_ns);
+    if (D.valid && now_ns >= D.last_now) {
+        if (D.ev_pending && hipEventQuery(D.ev) == hipSuccess) {
+            D.next = *D.next_host;
+            D.next_known = true;
+            D.ev_pending = false;
+        }
+        if (D.np == 0 && D.next_known && nowk <= D.next) {  // no deadline passed, nothing patched: no status can change
+            D.last_now = now_ns;
+            return KAD_OK;
+        }
+        // the nodes whose deadline `now` passes, and the patched ones
+        hipLaunchKernelGGL(dl_search_kernel, dim3(1), dim3(64), 0, s, D.km, D.nm, D.ks, D.ns, nowk, D.cur, D.next_dev);
+        hipLaunchKernelGGL(dl_process_kernel, dim3(512), dim3(BLOCK), 0, s, times_of(t), D.kn, D.sn, D.cur, D.pend, D.np,
+                           n, now_ns, t->status_mut, marks_of(t));
+        HIP_TRY(hipGetLastError());
+        D.np = 0;
+        D.hpend.clear();
+        D.last_now = now_ns;
+        if ((rc = dl_publish(t, s))) { D.invalidate(); return rc; }
+        return rebuild_good_prefix(t, s, false);
+    }
+    // first refresh after set_times / a status patch, or `now` moved back: every node, then the runs
+    D.invalidate();
+    if (n)
+        hipLaunchKernelGGL(status_from_times_kernel, dim3(grid_for(n)), dim3(BLOCK), 0, s, times_of(t), n, now_ns,
+                           t->status_mut, marks_of(t));
     HIP_TRY(hipGetLastError());
-    return rebuild_good_prefix(t, s, false);
+    if ((rc = rebuild_good_prefix(t, s, false))) return rc;
+    if (n && dl_build_main(t, s, nowk) == KAD_OK) {  // without the runs (no memory) every refresh takes this path
+        D.valid = true;
+        D.last_now = now_ns;
+    }
+    return KAD_OK;
 }
 
 int kad_rt_closest_batch(const kad_table* t, const uint8_t* targets, uint32_t q, uint32_t count, uint32_t* out_idx,
                          uint8_t* out_cnt, void* stream) {
     if (!t) return set_err(KAD_ERR_INVALID, "NULL table");
-    int rc = check_count(count);
-    if (rc) return rc;
     if (q == 0) return KAD_OK;
     if (!targets || (!out_idx && count)) return set_err(KAD_ERR_INVALID, "NULL buffer");
     if (count == 0 && !out_cnt) return KAD_OK;
@@ -5487,17 +5926,22 @@ int kad_rt_closest_batch_dual(const kad_table* t4, const kad_table* t6, const ui
                               uint32_t q, uint32_t count, uint32_t* out_idx, uint8_t* out_cnt, void* stream) {
     if (!t4 && !t6) return set_err(KAD_ERR_INVALID, "both tables NULL");
     if (t4 && t6 && t4->device != t6->device) return set_err(KAD_ERR_INVALID, "tables on different devices");
-    int rc = check_count(count);
-    if (rc) return rc;
     if (q == 0) return KAD_OK;
-    if (!targets || !af || !out_idx) return set_err(KAD_ERR_INVALID, "NULL buffer");
+    if (!targets || !af || (!out_idx && count)) return set_err(KAD_ERR_INVALID, "NULL buffer");
     // A missing family behaves as an empty table (zero results), as an empty RoutingTable does.
     DevTable empty{};
     const DevTable& d4 = t4 ? t4->d : empty;
     const DevTable& d6 = t6 ? t6->d : empty;
     DeviceGuard g(t4 ? t4->device : t6->device);
     hipStream_t s = (hipStream_t)stream;
-    if (count <= 8 && ((d4.flags | d6.flags) & TF_WL))
+    if (count == 0) {
+        if (out_cnt) HIP_TRY(hipMemsetAsync(out_cnt, 0, q, s));
+        return KAD_OK;
+    }
+    if (count > KAD_MAX_COUNT)
+        hipLaunchKernelGGL(rt_wave_kernel, dim3((q + BLOCK / 64 - 1) / (BLOCK / 64)), dim3(BLOCK), 0, s, d4, d6, af,
+                           targets, q, count, out_idx, out_cnt);
+    else if (count <= 8 && ((d4.flags | d6.flags) & TF_WL))
         hipLaunchKernelGGL(rt_dual_wl_kernel, dim3(grid_for(q)), dim3(BLOCK), 0, s, d4, d6, targets, af, q, count,
                            out_idx, out_cnt);
     else if (count <= 8 && ((d4.flags | d6.flags) & TF_GL))
@@ -5828,32 +6272,86 @@ static int pipe_ready(HostPipe& P) {
     return KAD_OK;
 }
 
+static int small_ready(HostPipe& P) {
+    if (!P.start) HIP_TRY(hipEventCreateWithFlags(&P.start, hipEventDisableTiming));
+    if (!P.ss) HIP_TRY(hipStreamCreateWithFlags(&P.ss, hipStreamNonBlocking));
+    if (!P.st) {
+        HIP_TRY(hipHostMalloc((void**)&P.st, 20ull * HostPipe::SMALL, hipHostMallocMapped));
+        HIP_TRY(hipHostGetDevicePointer((void**)&P.dst, P.st, 0));
+    }
+    if (!P.sc) {
+        HIP_TRY(hipHostMalloc((void**)&P.sc, HostPipe::SMALL, hipHostMallocMapped));
+        HIP_TRY(hipHostGetDevicePointer((void**)&P.dsc, P.sc, 0));
+    }
+    if (!P.si) {
+        HIP_TRY(hipHostMalloc((void**)&P.si, 4ull * HostPipe::SMALL * HostPipe::SMALL_COUNT, hipHostMallocMapped));
+        HIP_TRY(hipHostGetDevicePointer((void**)&P.dsi, P.si, 0));
+    }
+    return KAD_OK;
+}
+
+// q <= SMALL, count <= SMALL_COUNT: the kernel reads the targets from and writes the rows to mapped pinned memory.
+static int small_query(const kad_table* t, HostPipe& P, const uint8_t* targets, uint32_t q, uint32_t count,
+                       uint32_t* out_idx, uint8_t* out_cnt, bool nc) {
+    int rc = small_ready(P);
+    if (rc) return rc;
+    std::memcpy(P.st, targets, 20ull * q);
+    HIP_TRY(hipEventRecord(P.start, nullptr));  // ordered after the work issued on the null stream
+    HIP_TRY(hipStreamWaitEvent(P.ss, P.start, 0));
+    rc = nc ? kad_nc_closest_batch(t, P.dst, q, count, P.dsi, P.dsc, P.ss)
+            : kad_rt_closest_batch(t, P.dst, q, count, P.dsi, P.dsc, P.ss);
+    const hipError_t e = hipStreamSynchronize(P.ss);
+    if (rc) return rc;
+    if (e != hipSuccess) return set_err(KAD_ERR_HIP, "host batch: %s", hipGetErrorString(e));
+    if (count) std::memcpy(out_idx, P.si, 4ull * q * count);
+    if (out_cnt) std::memcpy(out_cnt, P.sc, q);
+    return KAD_OK;
+}
+
 static int host_query(const kad_table* t, const uint8_t* targets, uint32_t q, uint32_t count, uint32_t* out_idx,
                       uint8_t* out_cnt, bool nc) {
     if (!t) return set_err(KAD_ERR_INVALID, "NULL table");
     if (q == 0) return KAD_OK;
     if (!targets || (!out_idx && count)) return set_err(KAD_ERR_INVALID, "NULL buffer");
-    if (!nc && check_count(count)) return KAD_ERR_UNSUPPORTED;
+    // every check the per-chunk calls make, once, before anything is queued
+    if (nc && !(t->flags & KAD_TABLE_SORTED)) return set_err(KAD_ERR_NOT_SORTED, "NodeCache query needs a KAD_TABLE_SORTED table");
     if (nc && count > 255) return set_err(KAD_ERR_UNSUPPORTED, "count %u > 255", count);
     {
         std::lock_guard<std::mutex> lk(t->pipe_mu);
-        if (!t->pipe) t->pipe = new HostPipe();
+        if (!t->pipe) {
+            try {
+                t->pipe = new HostPipe();
+            } catch (...) {
+                return set_err(KAD_ERR_NOMEM, "host batch: out of host memory");
+            }
+        }
     }
     HostPipe& P = *t->pipe;
     std::lock_guard<std::mutex> lk(P.mu);
     DeviceGuard g(t->device);
+    if (q <= HostPipe::SMALL && count <= HostPipe::SMALL_COUNT)
+        return small_query(t, P, targets, q, count, out_idx, out_cnt, nc);
     int rc = pipe_ready(P);
     if (rc) return rc;
     // ordered after the work already issued, as a null-stream call is (a status refresh, a mirror update, ...)
     HIP_TRY(hipEventRecord(P.start, nullptr));
     for (auto& w : P.slot)
         for (HostPipe::Slot& S : w) HIP_TRY(hipStreamWaitEvent(S.s, P.start, 0));
+    if (count > 32u * HostPipe::CHUNK)
+        return set_err(KAD_ERR_UNSUPPORTED, "count %u exceeds a host-batch chunk row (%u): use the device-pointer batch",
+                       count, 32u * HostPipe::CHUNK);
     const uint32_t chunk = count <= 32 ? HostPipe::CHUNK : 32u * HostPipe::CHUNK / count;
     // worker w takes chunks [w * nch / W, (w + 1) * nch / W) of the batch
     const uint32_t nch = (q + chunk - 1) / chunk;
     const int W = (int)std::min<uint32_t>(HostPipe::WORKERS, nch);
-    std::vector<int> wrc(W, KAD_OK);
-    std::vector<std::string> werr(W);
+    std::vector<int> wrc;
+    std::vector<std::string> werr;
+    try {
+        wrc.assign(W, KAD_OK);
+        werr.resize(W);
+    } catch (...) {
+        return set_err(KAD_ERR_NOMEM, "host batch: out of host memory");
+    }
     auto work = [&](int w) {
         DeviceGuard gw(t->device);
         const uint32_t lo = (uint32_t)((uint64_t)w * nch / W * chunk);
@@ -5879,7 +6377,10 @@ static int host_query(const kad_table* t, const uint8_t* targets, uint32_t q, ui
             }
             r = nc ? kad_nc_closest_batch(t, S.dt, n, count, S.di, S.dc, S.s)
                    : kad_rt_closest_batch(t, S.dt, n, count, S.di, S.dc, S.s);
-            if (r) break;
+            if (r) {
+                (void)hipStreamSynchronize(S.s);  // the H2D copy out of the pinned slot may still run
+                break;
+            }
             if ((count && hipMemcpyAsync(S.hi, S.di, 4ull * n * count, hipMemcpyDeviceToHost, S.s) != hipSuccess) ||
                 hipMemcpyAsync(S.hc, S.dc, n, hipMemcpyDeviceToHost, S.s) != hipSuccess ||
                 hipEventRecord(S.done, S.s) != hipSuccess) {
@@ -5899,16 +6400,21 @@ static int host_query(const kad_table* t, const uint8_t* targets, uint32_t q, ui
         if (r) werr[w] = kad_last_error();
     };
     std::vector<std::thread> th;
-    std::vector<int> inline_w;  // workers whose thread could not be started run here
+    bool inline_w[HostPipe::WORKERS] = {};  // workers whose thread could not be started run here
+    try {
+        th.reserve(W);
+    } catch (...) {
+    }
     for (int w = 1; w < W; w++) {
         try {
             th.emplace_back(work, w);
         } catch (...) {
-            inline_w.push_back(w);
+            inline_w[w] = true;
         }
     }
     work(0);
-    for (int w : inline_w) work(w);
+    for (int w = 1; w < W; w++)
+        if (inline_w[w]) work(w);
     for (auto& x : th) x.join();
     for (int w = 0; w < W; w++)
         if (wrc[w]) return set_err(wrc[w], "%s", werr[w].c_str());
@@ -6153,6 +6659,7 @@ int kad_table_apply(kad_table* t, const uint32_t* ops, uint32_t n_ops, const uin
     release(t, t->wrec); t->wrec = nullptr; t->addr_len = 0;
     release(t, t->time_ns); release(t, t->reply_ns); release(t, t->expired);
     t->time_ns = nullptr; t->reply_ns = nullptr; t->expired = nullptr;
+    t->dl.invalidate();
     t->h_off.swap(off1);
     if (reshape) t->h_first.swap(first1);
     t->firsts_low_zero = t->firsts_low_zero_next;
@@ -6259,9 +6766,9 @@ int kad_nc_apply(kad_table* t, const uint32_t* erase, uint32_t n_erase, const ui
     if (n_erase)
         hipLaunchKernelGGL(flags_from_list_kernel, dim3(grid_for(n_erase)), dim3(BLOCK), 0, 0, del, n_erase, n0, deflag, dcnt);
     // erased_before[i] = erased nodes below i (exclusive scan of the flags, n0 + 1 entries)
-    hipLaunchKernelGGL(scan_tiles_kernel, dim3(tiles), dim3(BLOCK), 0, 0, dcnt, n0 + 1, dpre, dsums);
-    hipLaunchKernelGGL(scan_sums_kernel, dim3(1), dim3(BLOCK), 0, 0, dsums, tiles);
-    hipLaunchKernelGGL(scan_apply_kernel, dim3(grid_for(n0 + 1)), dim3(BLOCK), 0, 0, dpre, dsums, n0 + 1, dpre);
+    hipLaunchKernelGGL(scan_tiles_kernel, dim3(tiles), dim3(BLOCK), 0, 0, dcnt, n0 + 1, dpre, dsums, nullptr);
+    hipLaunchKernelGGL(scan_sums_kernel, dim3(1), dim3(BLOCK), 0, 0, dsums, tiles, nullptr);
+    hipLaunchKernelGGL(scan_apply_kernel, dim3(grid_for(n0 + 1)), dim3(BLOCK), 0, 0, dpre, dsums, n0 + 1, dpre, nullptr);
     if (n0)
         hipLaunchKernelGGL(nc_merge_old_kernel, dim3(grid_for(n0)), dim3(BLOCK), 0, 0, d.key, d.tail, d.status, deflag, dpre,
                            n0, dik, dit, n_ins, key1, tail1, st1, dremap);
@@ -6323,6 +6830,7 @@ int kad_nc_apply(kad_table* t, const uint32_t* erase, uint32_t n_erase, const ui
     release(t, t->wrec); t->wrec = nullptr; t->addr_len = 0;
     release(t, t->time_ns); release(t, t->reply_ns); release(t, t->expired);
     t->time_ns = nullptr; t->reply_ns = nullptr; t->expired = nullptr;
+    t->dl.invalidate();
     t->owned.insert(t->owned.end(), fresh.begin(), fresh.end());
     t->bytes += freshb;
     drop_marks(t);

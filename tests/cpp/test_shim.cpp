@@ -77,9 +77,12 @@ static void check_rt(const RoutingTable& rt, const std::vector<std::vector<std::
     orc_flat_rt_closest((uint32_t)flat.size(), ids.data(), st.data(), (uint32_t)rt.size(), first.data(), off.data(), q,
                         reinterpret_cast<const uint8_t*>(targets.data()), count, want.data(), wcnt.data(), 4);
     for (uint32_t i = 0; i < q; i++) {
-        EXPECT(got[i].size() == wcnt[i], "%s: rt count q=%u k=%u (%zu vs %u)", what, i, count, got[i].size(), wcnt[i]);
-        for (uint32_t j = 0; j < got[i].size() && j < wcnt[i]; j++)
-            EXPECT(got[i][j].get() == flat[want[i * count + j]], "%s: rt node q=%u k=%u j=%u", what, i, count, j);
+        uint32_t m = wcnt[i];  // the oracle's count byte wraps above 255: the row's padding gives the length
+        if (count > 255)
+            for (m = 0; m < count && want[(size_t)i * count + m] != 0xFFFFFFFFu; m++) {}
+        EXPECT(got[i].size() == m, "%s: rt count q=%u k=%u (%zu vs %u)", what, i, count, got[i].size(), m);
+        for (uint32_t j = 0; j < got[i].size() && j < m; j++)
+            EXPECT(got[i][j].get() == flat[want[(size_t)i * count + j]], "%s: rt node q=%u k=%u j=%u", what, i, count, j);
     }
 }
 
@@ -153,13 +156,24 @@ int main() {
                                               std::chrono::minutes(11), std::chrono::minutes(125)};
     for (auto dt : steps) {
         const time_point now = t0 + dt;
-        for (uint32_t count : {1u, 8u, 14u, 32u}) {
+        for (uint32_t count : {1u, 8u, 14u, 32u, 33u, 100u, 300u}) {
             auto got = mirror.findClosestNodesBatch(targets, now, count);
             check_rt(rt, got, targets, count, now, "moving now");
         }
         auto one = mirror.findClosestNodes(targets[3], now, 8);
         auto ref = mirror.findClosestNodesBatch(&targets[3], 1, now, 8);
         EXPECT(one == ref[0], "single query");
+    }
+    // a count above the table's size (any size_t, routing_table.h:48): every good node, closest first
+    {
+        const time_point now = t0 + std::chrono::seconds(30);
+        auto all = mirror.findClosestNodes(targets[7], now, (size_t)1 << 40);
+        size_t good = 0;
+        for (auto& nd : nodes) good += nd->isGood(now);
+        EXPECT(all.size() == good, "count > n: %zu of %zu good nodes", all.size(), good);
+        std::vector<std::vector<std::shared_ptr<Node>>> g1{all};
+        std::vector<InfoHash> t1{targets[7]};
+        check_rt(rt, g1, t1, n, now, "count > n");
     }
     // going back in time is allowed too (the status is a function of now)
     {
@@ -355,6 +369,47 @@ int main() {
             check_rt(rt, got, targets, 8, at, "dht v4");
             EXPECT(dht.findClosestNodes(targets[4], AF_INET6, 8).empty(), "dht v6 empty table");
         }
+    }
+    // latency of one call through the shim on a live-sized table (~170 nodes, the reference's per-request
+    // case): median of single findClosestNodes calls and of 64-query batches
+    {
+        const uint32_t m = 170;
+        std::vector<uint8_t> lid(20ull * m);
+        kadgpu::check(kad_synth_ids(0x1A7, m, lid.data()), "synth");
+        std::vector<uint32_t> lperm(m), loff(m + 2);
+        std::vector<uint8_t> lfirst(20ull * (m + 1));
+        uint32_t LB = 0;
+        kadgpu::check(kad_split_table(m, lid.data(), 8, lperm.data(), lfirst.data(), loff.data(), &LB), "split");
+        RoutingTable lrt;
+        std::vector<std::shared_ptr<Node>> keep;
+        for (uint32_t b = 0; b < LB; b++) {
+            Bucket bk;
+            std::memcpy(bk.first.data(), &lfirst[20ull * b], 20);
+            for (uint32_t j = loff[b]; j < loff[b + 1]; j++) {
+                auto nd = std::make_shared<Node>();
+                std::memcpy(nd->id.data(), &lid[20ull * lperm[j]], 20);
+                nd->time = nd->reply_time = t0;
+                keep.push_back(nd);
+                bk.nodes.push_back(nd);
+            }
+            lrt.push_back(bk);
+        }
+        kadgpu::RoutingTableMirror<RoutingTable> lm(lrt, t0, 0);
+        auto med = [](std::vector<double> v) { std::sort(v.begin(), v.end()); return v[v.size() / 2]; };
+        std::vector<double> one_us, b64_us;
+        for (int r = 0; r < 2000; r++) {
+            const auto a = clock::now();
+            auto res = lm.findClosestNodes(targets[r % q], t0, 8);
+            one_us.push_back(std::chrono::duration<double, std::micro>(clock::now() - a).count());
+            EXPECT(res.size() == 8, "latency table result");
+        }
+        for (int r = 0; r < 500; r++) {
+            const auto a = clock::now();
+            auto res = lm.findClosestNodesBatch(&targets[(r * 64) % (q - 64)], 64, t0, 8);
+            b64_us.push_back(std::chrono::duration<double, std::micro>(clock::now() - a).count());
+        }
+        std::printf("LATENCY {\"nodes\": %u, \"buckets\": %u, \"single_call_us\": %.2f, \"batch64_call_us\": %.2f}\n",
+                    m, LB, med(one_us), med(b64_us));
     }
     std::printf("%s (%d failures)\n", fails ? "FAIL" : "PASS", fails);
     return fails ? 1 : 0;

@@ -23,3 +23,4 @@ def test_cpp_shim_parity():
     r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "PASS" in r.stdout
+    print("\n".join(l for l in r.stdout.splitlines() if l.startswith(("LATENCY", "mirror"))))

@@ -340,3 +340,62 @@ def test_nc_lines_after_status_change(gpu):
         good = (expired == 0) & (reply_ns >= now - 120 * m) & (time_ns >= now - 10 * m)
         st3 = (good.astype(np.uint8) | (expired << 1)).astype(np.uint8)
         check_nc(T, dict(t, status=st3), targets, gpu, counts=(8, 14, 32))
+
+
+BIG_COUNTS = (33, 48, 64, 100, 255, 300, 1000)
+
+
+def _rows_len(rows):
+    """Entries before the first KAD_NO_NODE of each row (the result length for count > 255)."""
+    pad = rows == KAD_NO_NODE
+    return np.where(pad.any(axis=1), pad.argmax(axis=1), rows.shape[1])
+
+
+@pytest.mark.parametrize("t", TB.all_small_tables() + [TB.split_config(20_000, seed=0xB16)],
+                         ids=lambda t: t["name"])
+def test_rt_closest_any_count(gpu, t):
+    """RoutingTable::findClosestNodes takes any size_t count (routing_table.h:48, routing_table.cpp:67-111):
+    counts above the line kernels' 32 run one wave per query (window from the prefix sums, every good node of
+    it ranked tile against tile). Bit-exact rows for counts 33 .. 1000 on uniform, split-policy, tiny, all-bad
+    and mostly-bad tables (windows that cover the whole table); the count byte saturates at 255 and the row
+    padding gives the length beyond it. The same through the dual-family batch and the host-pointer batch."""
+    targets = TB.adversarial_targets(t, extra=600)
+    tg = dev(targets, gpu)
+    with make(t, gpu) as T:
+        for k in BIG_COUNTS:
+            idx, cnt = T.rt_closest(tg, k)
+            torch.cuda.synchronize()
+            want, _ = O.flat_rt_closest(t["ids"], t["status"], t["first"], t["off"], targets, k, nthreads=8)
+            got = u32(idx)
+            np.testing.assert_array_equal(got, want, err_msg=f"{t['name']} k={k} indices")
+            m = _rows_len(want)
+            np.testing.assert_array_equal(cnt.cpu().numpy(), np.minimum(m, 255), err_msg=f"{t['name']} k={k} counts")
+            if k in (33, 255):
+                af = torch.zeros(targets.shape[0], dtype=torch.uint8, device=gpu)
+                af[1::2] = 1
+                di, dc = rt_closest_dual(T, None, tg, af, k)
+                torch.cuda.synchronize()
+                even = np.arange(targets.shape[0]) % 2 == 0
+                np.testing.assert_array_equal(u32(di)[even], want[even], err_msg=f"{t['name']} dual k={k}")
+                assert (dc.cpu().numpy()[~even] == 0).all() and (u32(di)[~even] == KAD_NO_NODE).all()
+                hi, hc = T.rt_closest_host(targets, k)
+                np.testing.assert_array_equal(hi, want, err_msg=f"{t['name']} host k={k}")
+                np.testing.assert_array_equal(hc, np.minimum(m, 255))
+
+
+def test_host_batch_small_and_large(gpu):
+    """kad_rt_closest_batch_host: batches of 1 .. 1024 queries with count <= 64 take the one-launch path on mapped
+    pinned memory, larger ones the chunked pipeline; both equal the device batch."""
+    t = TB.uniform_config(60_000, 13, seed=0x5A11)
+    targets = TB.adversarial_targets(t, extra=5000)
+    with make(t, gpu) as T:
+        for q in (1, 2, 64, 1024, 1025, targets.shape[0]):
+            for k in (8, 14, 32, 64, 65):
+                hi, hc = T.rt_closest_host(targets[:q], k)
+                want, wcnt = O.flat_rt_closest(t["ids"], t["status"], t["first"], t["off"], targets[:q], k)
+                np.testing.assert_array_equal(hi, want, err_msg=f"q={q} k={k}")
+                np.testing.assert_array_equal(hc, wcnt, err_msg=f"q={q} k={k} counts")
+            ni, nc = T.nc_closest_host(targets[:q], 14)
+            want, wcnt = O.flat_nc_closest(t["ids"], t["status"], targets[:q], 14)
+            np.testing.assert_array_equal(ni, want, err_msg=f"nc q={q}")
+            np.testing.assert_array_equal(nc, wcnt)

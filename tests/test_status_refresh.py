@@ -144,3 +144,75 @@ def test_patch_rejects_bad_index(gpu):
             T.patch_status(np.array([t["ids"].shape[0]], np.uint32), np.array([1], np.uint8))
         with pytest.raises(KadError):  # no times uploaded yet
             T.patch_times(np.array([0], np.uint32), np.array([0]), np.array([0]), np.array([0], np.uint8))
+
+
+def test_now_walk_across_deadlines(gpu):
+    """kad_table_refresh_status follows `now` through the nodes' isGood deadlines (node.cpp:34-40: good while
+    now <= min(time + 10 min, reply_time + 120 min)): steps of 1 ns, steps landing exactly on a deadline (the
+    node is still good) and 1 ns past it, steps across thousands of deadlines, a refresh at the same `now`,
+    patch_times in between (nodes heard again turn good at the next refresh whatever `now`; setExpired), a
+    step back in time (every node re-derived) and forward again. After every step the status bytes equal
+    isGood / isExpired at that `now`, and at some steps every query equals the oracle."""
+    t = TB.uniform_config(40_000, 12, seed=0x5E8)
+    n = t["ids"].shape[0]
+    rng = np.random.default_rng(0x5E8)
+    targets = TB.adversarial_targets(t, extra=1500)
+    MIN = 60 * 10**9
+    now0 = now = 500 * 3600 * 10**9
+    time_ns = now - rng.integers(0, 10 * MIN, n)
+    reply_ns = now - rng.integers(0, 120 * MIN, n)
+    time_ns[:300] = now - 5 * MIN  # 300 nodes share one deadline
+    reply_ns[:300] = now
+    expired = (rng.random(n) < 0.05).astype(np.uint8)
+
+    def status_at(tnow):
+        good = (expired == 0) & (reply_ns >= tnow - 120 * MIN) & (time_ns >= tnow - 10 * MIN)
+        return (good.astype(np.uint8) | (expired << 1)).astype(np.uint8)
+
+    def deadlines():
+        d = np.minimum(time_ns + 10 * MIN, reply_ns + 120 * MIN)
+        return np.sort(d[(expired == 0) & (d >= now)])
+
+    def step(tnow, check_queries=False):
+        T.refresh_status(tnow)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(T.export_status(), status_at(tnow), err_msg=f"now={tnow}")
+        if check_queries:
+            _check(T, t, status_at(tnow), targets, gpu, rt=(1, 8, 14, 32), nc=(1, 14, 32))
+
+    with DeviceTable(t["ids"], status_at(now), t["first"], t["off"], device=0, sorted=True) as T:
+        T.set_times(time_ns, reply_ns, expired)
+        step(now)
+        for j in range(40):
+            d = deadlines()
+            kind = j % 5
+            if kind == 0:
+                now += 1
+            elif kind == 1:
+                now = int(d[min(len(d) - 1, 7)])  # exactly on a deadline: that node is still good
+            elif kind == 2:
+                now += 1  # ... and 1 ns later it is not
+            elif kind == 3:
+                now = int(d[min(len(d) - 1, 2000)]) + 1  # across ~2000 deadlines
+            else:
+                pass  # the same `now` again
+            step(now, check_queries=(j % 10 == 3))
+            if j == 12 and now < now0 + 5 * MIN:  # the 300 nodes sharing a deadline: on it, then past it
+                now = now0 + 5 * MIN
+                step(now)
+                now += 1
+                step(now)
+            if j in (15, 25):  # some nodes are heard again (good again at once), some expire
+                heard = rng.choice(n, size=n // 50, replace=False).astype(np.uint32)
+                time_ns[heard] = now
+                reply_ns[heard] = now - rng.integers(0, 3 * MIN, heard.shape[0])
+                gone = rng.choice(n, size=n // 400, replace=False).astype(np.uint32)
+                expired[gone] = 1
+                sel = np.unique(np.concatenate([heard, gone])).astype(np.uint32)
+                T.patch_times(sel, time_ns[sel], reply_ns[sel], expired[sel])
+                step(now, check_queries=True)
+            if j == 30:  # back in time: every node re-derived, then forward again
+                now -= 4 * MIN
+                step(now, check_queries=True)
+        now += 30 * MIN  # most good nodes age out
+        step(now, check_queries=True)

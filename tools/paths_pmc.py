@@ -1,10 +1,10 @@
-"""Workload for per-kernel PMC passes over the non-headline paths (tools/pmc.sh with
-PMC_PROG=tools/paths_pmc.py): on the bench shard (1/8 of the 100M-node U(24) table, 1M owned
-queries) each path runs REPS launches, one kernel name per path, so tools/paths_roofline.py can
-split the counters per kernel:
-  rt_wl_kernel<0> (k=8), rt_wl16_kernel (k=16), rt_wl32_kernel (k=32), rt_closest_kernel<32> (k=32,
-  KAD_RT_KERNEL=lane), nc_line_kernel (NodeCache k=14), nc_multi_kernel<2> (k=14, KAD_NC_KERNEL=multi2),
-  rt_dual_wl_kernel (dual family k=8), buffer_nodes_kernel (wire records of the k=8 rows)."""
+"""Round-2 (second session) path workload for timings and per-kernel PMC passes (tools/pmc.sh with
+PMC_PROG=tools/paths_pmc.py): every launch reads a different batch of 1M targets (8 rotated batches).
+  bench shard (1/8 of the 100M-node U(24) table): rt_ws_kernel<0> (k=8), rt_wl16_kernel<0> (k=16),
+  rt_wl32_kernel (k=32), nc_line_kernel<0, false> (NodeCache k=14), nc32_line_kernel<0, false> (NodeCache k=32);
+  split-policy table of 4M nodes: rt_sl_kernel<0> (k=8), rt_gl16_kernel (k=14), rt_gl32_kernel (k=32).
+Without a profiler it prints the per-launch times (HIP events, median of REPS) as JSON."""
+import json
 import os
 import sys
 
@@ -12,37 +12,50 @@ import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from opendht_amd import DeviceTable, rt_closest_dual  # noqa: E402
+from opendht_amd import DeviceTable  # noqa: E402
+from opendht_amd import synth as S  # noqa: E402
 from opendht_amd.sharded import build_shard, config3_spec  # noqa: E402
 
-REPS = 5
+REPS, NB, Q = 6, 8, 1 << 20
 dev = torch.device("cuda:0")
-spec = config3_spec()
-sh = build_shard(spec, 0)
-q = 1 << 20
-tg = torch.from_numpy(spec.targets_for(0, q, seed=0x0D470002)).to(dev)
+g = torch.Generator(device=dev)
+g.manual_seed(9)
+tgs = [torch.randint(0, 256, (Q, 20), dtype=torch.uint8, device=dev, generator=g) for _ in range(NB)]
+for t in tgs:
+    t[:, 0] = t[:, 0] & 0x1F  # shard 0 of the U(24) table owns the top 3 bits 000
+res = {}
+
+
+def run(name, fn):
+    ts = []
+    for j in range(REPS):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        fn(tgs[j % NB])
+        b.record()
+        torch.cuda.synchronize()
+        ts.append(a.elapsed_time(b) * 1e3)
+    res[name] = round(float(np.median(ts)), 2)
+
+
+sh = build_shard(config3_spec(), 0)
 T = DeviceTable(sh.ids, sh.status, sh.first, sh.off, device=0, index_base=sh.index_base, sorted=True)
-
-
-def run(fn, env=None):
-    if env:
-        os.environ[env[0]] = env[1]
-    for _ in range(REPS):
-        fn()
-    torch.cuda.synchronize()
-    if env:
-        os.environ.pop(env[0])
-
-
-for k in (8, 16, 32):
-    run(lambda: T.rt_closest(tg, k))
-run(lambda: T.rt_closest(tg, 32), ("KAD_RT_KERNEL", "lane"))
-run(lambda: T.nc_closest(tg, 14))
-run(lambda: T.nc_closest(tg, 14), ("KAD_NC_KERNEL", "multi2"))
-af = (torch.arange(q, device=dev) % 2).to(torch.uint8)
-run(lambda: rt_closest_dual(T, T, tg, af, 8))
-T.set_addrs(np.random.default_rng(1).integers(0, 256, (sh.ids.shape[0], 6), dtype=np.uint8))
-idx, cnt = T.rt_closest(tg, 8)
-run(lambda: T.buffer_nodes(tg, idx, cnt))
+run("U24shard_rt_k8_us", lambda t: T.rt_closest(t, 8))
+run("U24shard_rt_k16_us", lambda t: T.rt_closest(t, 16))
+run("U24shard_rt_k32_us", lambda t: T.rt_closest(t, 32))
+run("U24shard_nc_k14_us", lambda t: T.nc_closest(t, 14))
+run("U24shard_nc_k32_us", lambda t: T.nc_closest(t, 32))
 T.close()
-print("ok")
+del sh
+n = 4_000_000
+ids = S.random_ids(n, 0xB5)
+st = S.random_status(n, 0xB6)
+perm, first, off = S.split_table(ids)
+T = DeviceTable(ids[perm], st[perm], first, off, device=0)
+for t in tgs:
+    t[:, 0] = torch.randint(0, 256, (Q,), dtype=torch.uint8, device=dev, generator=g)
+run("S4M_rt_k8_us", lambda t: T.rt_closest(t, 8))
+run("S4M_rt_k14_us", lambda t: T.rt_closest(t, 14))
+run("S4M_rt_k32_us", lambda t: T.rt_closest(t, 32))
+T.close()
+print(json.dumps(res), flush=True)
