@@ -571,6 +571,18 @@ def latency_pass(dev, nodes=170, reps=2000):
     res = {"nodes": nodes, "buckets": int(first.shape[0])}
     with DeviceTable(ids, st, first, off, device=dev.index or 0) as T:
         for q in (1, 64):
+            if os.environ.get("KAD_LATENCY_AB"):  # synchronisation variants of the small host batch
+                for mode in ("noorder", "spin", "noorder,spin"):
+                    os.environ["KAD_SMALL_SYNC"] = mode
+                    ts = []
+                    oi, oc = np.zeros((q, 8), np.uint32), np.zeros((q,), np.uint8)
+                    for r in range(reps):
+                        x = np.ascontiguousarray(tg[(r * q) % (4096 - q):(r * q) % (4096 - q) + q])
+                        t0 = time.perf_counter()
+                        check(lib().kad_rt_closest_batch_host(T.handle, ptr(x), q, 8, ptr(oi), ptr(oc)), "host batch")
+                        ts.append(time.perf_counter() - t0)
+                    res[f"ab_{mode}_q{q}_us"] = float(np.median(ts)) * 1e6
+                os.environ.pop("KAD_SMALL_SYNC", None)
             oi, oc = np.zeros((q, 8), np.uint32), np.zeros((q,), np.uint8)
             ts = []
             for r in range(reps):

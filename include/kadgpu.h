@@ -147,8 +147,14 @@ int kad_table_patch_times(kad_table* t, uint32_t m, const uint32_t* nodes, const
                           const int64_t* reply_time_ns, const uint8_t* expired);
 /* Recompute the status snapshot on the device at `now_ns` from the uploaded times:
  * good = !expired && reply_time >= now-120min && time >= now-10min (node.cpp:34-40,
- * node.h:91-94): one pass over the node times; only the nodes whose status flips at this `now`
- * cause mask and line rebuilds (then the good prefix sums are re-scanned). Async on `stream`. */
+ * node.h:91-94). A good node stays good while now <= min(time + 10 min, reply_time + 120 min), so the
+ * table keeps every node's deadline sorted: the first refresh after kad_table_set_times (or after a
+ * direct status change, or with `now` earlier than the last refresh's) re-derives every node and sorts
+ * the deadlines; later ones re-derive only the nodes whose deadline `now` passed since the last refresh
+ * and the nodes patched by kad_table_patch_times, and a refresh whose `now` has not reached the next
+ * deadline (with nothing patched) returns at once without touching the GPU. Only flips cause mask and
+ * line rebuilds. Async on `stream`; later refreshes and device batches must be ordered after it by the
+ * caller (the host-pointer batches order themselves). */
 int kad_table_refresh_status(kad_table* t, int64_t now_ns, void* stream);
 
 /* ---- incremental device mirror ----------------------
@@ -199,10 +205,13 @@ int kad_table_export(const kad_table* t, uint8_t* ids, uint8_t* status, uint8_t*
  * row's entries before the first KAD_NO_NODE). */
 int kad_rt_closest_batch(const kad_table* t, const uint8_t* targets, uint32_t q, uint32_t count,
                          uint32_t* out_idx, uint8_t* out_cnt, void* stream);
-/* The same on host buffers (any memory), synchronous and ordered after the device work issued before the
- * call on the null stream. The first call gives the table ~80 MB of pinned staging and device buffers (freed
- * with it); batches run as 64k-query chunks pipelined over four host threads. One host batch per table at a
- * time. count <= 2,097,152 (one chunk row; larger counts: the device-pointer batch). */
+/* The same on host buffers (any memory), synchronous, and ordered after every change made to the table
+ * before the call (the asynchronous kad_table_refresh_status on whatever stream it ran; every other change
+ * is synchronous). Batches of up to 1024 queries with count <= 64 are one kernel launch that reads the
+ * targets from and writes the rows to mapped pinned memory (one round trip); larger ones run as 64k-query
+ * chunks pipelined over four host threads through ~80 MB of pinned staging and device buffers the table
+ * keeps (allocated on first use, freed with it). One host batch per table at a time.
+ * count <= 2,097,152 (one chunk row; larger counts: the device-pointer batch). */
 int kad_rt_closest_batch_host(const kad_table* t, const uint8_t* targets, uint32_t q, uint32_t count,
                               uint32_t* out_idx, uint8_t* out_cnt);
 

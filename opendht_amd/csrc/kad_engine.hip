@@ -1701,6 +1701,171 @@ __global__ __launch_bounds__(BLOCK) void rt_wl32_kernel(DevTable T, const uint8_
     exact_tail(T, t, act && !ok, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
 }
 
+// ---------------------------------------------------------------------------------------
+// Counts 17..32 with FOUR lanes per query (rt_wl32q_kernel, the default for TF_WL32). The one-lane form
+// ranks 58 slots in 151 VGPRs (three waves per SIMD) and stalls on its two line loads; here the quad loads
+// the 256-byte line as four 64-byte pieces (lane p: dwords 16x + 4p .. +3, x = 0..3: each instruction one
+// contiguous 64-byte segment per quad), each lane sorts its 16 slot values, and three cross-lane bitonic
+// steps over DPP quad permutes give the top 32 (lanes 0 and 1: ranks 0..15 and 16..31):
+//   B  lanes (0,1) and (2,3): half-cleaner of A ++ reverse(B) (element i against the partner's 15 - i; the
+//      high lane keeps the max at its index j = position 31 - j, still bitonic), then 8, 4, 2, 1 in-lane:
+//      P0 = lanes 0,1 ascending, P1 = lanes 2,3 ascending
+//   C  Q[i] = min(P0[i], P1[31 - i]): lane 0 against lane 3, lane 1 against lane 2 (xor 3, element 15 - i):
+//      the 32 smallest, bitonic
+//   D  half-cleaner 16 across lanes 0 and 1, then 8, 4, 2, 1 in-lane.
+// The values, masks and fallbacks are wl32_answer's, so the rows are identical.
+// ---------------------------------------------------------------------------------------
+template <int CTRL>
+__device__ __forceinline__ uint32_t qdpp(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
+}
+constexpr int QP_X1 = 0xB1, QP_X2 = 0x4E, QP_X3 = 0x1B, QP_B0 = 0x00, QP_B1 = 0x55;  // quad_perm encodings
+
+// element i against the quad partner's element (REV ? 15 - i : i); the low lane keeps the min, the other the max
+template <int CTRL, bool REV>
+__device__ __forceinline__ void quad_exchange(uint32_t (&v)[16], bool low) {
+    uint32_t w[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) w[i] = qdpp<CTRL>(v[REV ? 15 - i : i]);
+#pragma unroll
+    for (int i = 0; i < 16; i++) v[i] = low ? min(v[i], w[i]) : max(v[i], w[i]);
+}
+
+// a bitonic 16 in one lane, sorted ascending by half-cleaners 8, 4, 2, 1
+__device__ __forceinline__ void clean16(uint32_t (&v)[16]) {
+#pragma unroll
+    for (int w = 8; w >= 1; w >>= 1)
+#pragma unroll
+        for (int i = 0; i < 16; i++)
+            if ((i & w) == 0) cx(v[i], v[i + w]);
+}
+
+__device__ __forceinline__ bool wl32_answer4(const DevTable& T, const Target& t, uint32_t b, uint32_t count, bool act,
+                                             uint32_t p, uint32_t (&v)[16], uint32_t& m, uint32_t& base) {
+    uint32_t L[16];
+    if (act) {
+        const uint4* lp = T.wl32 + (WL32_STRIDE / 4) * (size_t)b;
+#pragma unroll
+        for (int x = 0; x < 4; x++) {
+            const uint4 u = lp[4 * x + p];
+            L[4 * x] = u.x; L[4 * x + 1] = u.y; L[4 * x + 2] = u.z; L[4 * x + 3] = u.w;
+        }
+    } else {
+#pragma unroll
+        for (int x = 0; x < 16; x++) L[x] = NONE;
+    }
+    // the header: dwords 0..3 are lane 0's L[0..3], dwords 4, 5 lane 1's L[0], L[1]
+    const uint32_t h = qdpp<QP_B0>(L[3]), g03 = qdpp<QP_B0>(L[1]), g47 = qdpp<QP_B0>(L[2]);
+    const uint32_t r04 = qdpp<QP_B1>(L[0]), r15 = qdpp<QP_B1>(L[1]);
+    base = qdpp<QP_B0>(L[0]);
+    const uint32_t S = (h >> 12) & 127u, R = (h >> 8) & 15u;
+    uint32_t Rc = 8, Gc = 0;
+#pragma unroll
+    for (int r = 7; r >= 0; r--) {
+        const uint32_t g = ((r < 4 ? g03 : g47) >> (8 * (r & 3))) & 255u;
+        if (g >= count || ((h >> r) & 1u)) { Rc = (uint32_t)r; Gc = g; }
+    }
+    m = min(count, Gc);
+    const bool own = (t.hi >> T.rshift) == (T.rbase >> T.rshift) + b;
+    bool ex = !act || (h & WL_DEFER) || !own || Rc > R;
+    const uint32_t tx = (uint32_t)((t.hi << (64 - T.rshift)) >> (64 - WL32_KBITS)) << 8;
+    const bool mask = __any(!ex && Rc < R);  // a smaller window: drop the later rounds' buckets
+    uint32_t inc = ~0u;
+    if (mask) {
+        inc = 0;
+#pragma unroll
+        for (int j = 0; j < 16; j++) {
+            const uint32_t rj = j < 10 ? (r04 >> (3 * j)) & 7u : (r15 >> (3 * (j - 10))) & 7u;
+            inc |= (rj <= Rc ? 1u : 0u) << j;
+        }
+    }
+    uint32_t have = 0;
+#pragma unroll
+    for (int e = 0; e < 16; e++) {
+        const uint32_t dwi = 16u * (e >> 2) + 4u * p + (e & 3), s = dwi - WL32_HDR;
+        const bool in = dwi >= WL32_HDR && s < S && ((inc >> (L[e] >> 28)) & 1u);
+        v[e] = in ? L[e] ^ tx : NONE;  // empty slots stay NONE
+        have += in;
+    }
+    have += qdpp<QP_X1>(have);
+    have += qdpp<QP_X2>(have);
+    const bool low = (p & 1u) == 0;
+    sort16(v);
+    quad_exchange<QP_X1, true>(v, low);
+    clean16(v);
+    quad_exchange<QP_X3, true>(v, true);
+    quad_exchange<QP_X1, false>(v, low);
+    clean16(v);
+    ex |= have < m;
+    return !ex;
+}
+
+// The rows of a block's BLOCK / 4 quad-form queries (lanes 0 and 1 of a quad hold entries [0, 16) and
+// [16, 32)), staged in LDS and stored as coalesced 16-byte pieces, as store_rows_block.
+__device__ __forceinline__ void store_rows_quad(uint32_t* __restrict__ out_idx, uint32_t q, uint32_t count,
+                                                const uint32_t (&o)[16], bool ok, uint32_t p) {
+    constexpr uint32_t NQ = BLOCK / 4;
+    __shared__ uint32_t rows[NQ * 32];
+    __shared__ uint32_t okm[NQ / 32];
+    const uint32_t tid = threadIdx.x, ql = tid >> 2, q0 = blockIdx.x * NQ;
+    if (tid < NQ / 32) okm[tid] = 0;
+    __syncthreads();
+    if (ok && p == 0) atomicOr(&okm[ql >> 5], 1u << (ql & 31));
+    if (p < 2)
+#pragma unroll
+        for (int k = 0; k < 16; k++)
+            if (16u * p + k < count) rows[ql * count + 16u * p + k] = o[k];
+    __syncthreads();
+    const uint32_t nq = min(NQ, q - q0), nw = nq * count;
+    uint32_t* dst = out_idx + (size_t)q0 * count;  // 16-byte aligned: NQ * count * 4 is a multiple of 16
+    for (uint32_t c = tid; 4 * c < nw; c += BLOCK) {
+        const uint32_t w0 = 4 * c;
+        const uint32_t ra = w0 / count, rb = min(w0 + 3, nw - 1) / count;
+        const bool oka = (okm[ra >> 5] >> (ra & 31)) & 1u, okb = (okm[rb >> 5] >> (rb & 31)) & 1u;
+        if (oka && okb && w0 + 4 <= nw && (((uintptr_t)out_idx & 15u) == 0)) {
+            reinterpret_cast<uint4*>(dst)[c] = make_uint4(rows[w0], rows[w0 + 1], rows[w0 + 2], rows[w0 + 3]);
+        } else {
+            for (uint32_t w = w0; w < min(w0 + 4, nw); w++) {
+                const uint32_t r = w / count;
+                if ((okm[r >> 5] >> (r & 31)) & 1u) dst[w] = rows[w];
+            }
+        }
+    }
+}
+
+template <int ABL>
+__global__ __launch_bounds__(BLOCK) void rt_wl32q_kernel(DevTable T, const uint8_t* __restrict__ targets, uint32_t q,
+                                                         uint32_t count, uint32_t* __restrict__ out_idx,
+                                                         uint8_t* __restrict__ out_cnt) {
+    const uint32_t g = blockIdx.x * BLOCK + threadIdx.x, i = g >> 2, p = g & 3u;
+    const bool act = i < q;
+    Target t{};
+    uint32_t b = 0;
+    if (act) {
+        t = load_target(targets, i);
+        b = locate_bucket(T, t);
+    }
+    uint32_t v[16], m, base;
+    const bool ok = wl32_answer4(T, t, b, count, act, p, v, m, base);
+    const uint32_t r0 = 16u * (p & 1u), bi = base + T.index_base;
+    uint32_t o[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) o[k] = r0 + k < m ? bi + (v[k] & 255u) : NONE;
+    if (act && ok && p == 0 && out_cnt) out_cnt[i] = (uint8_t)m;
+    if ((count & 3u) == 0 && ((uintptr_t)out_idx & 15u) == 0) {  // lanes 0 and 1 store 16-byte pieces
+        if (act && ok && p < 2u) {
+            uint4* row = reinterpret_cast<uint4*>(out_idx + (size_t)i * count + r0);
+#pragma unroll
+            for (int x = 0; x < 4; x++)
+                if (r0 + 4 * x < count) row[x] = make_uint4(o[4 * x], o[4 * x + 1], o[4 * x + 2], o[4 * x + 3]);
+        }
+    } else {  // staged through LDS (block-uniform branch)
+        store_rows_quad(out_idx, q, count, o, act && ok, p);
+    }
+    __shared__ uint64_t xs[BLOCK / 64][192];
+    exact_tail(T, t, act && !ok && p == 0u, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
+}
+
 // Window lines for counts 17..32 after a status change (or at creation): one thread per bucket.
 // The window's buckets are put in D order by rank (O(buckets^2), at most 16 buckets).
 __global__ __launch_bounds__(BLOCK) void wl32_build_kernel(const uint64_t* key, const uint8_t* status, const uint2* dir,
@@ -4871,11 +5036,13 @@ struct kad_table {
     mutable HostPipe* pipe = nullptr;
     Deadlines dl;                   // isGood(now) deadlines (kad_table_refresh_status)
     hipStream_t ss[2] = {nullptr, nullptr};  // side streams of an incremental rebuild (side_streams)
+    hipEvent_t mut_ev = nullptr;    // recorded after the last asynchronous status refresh (the host batches wait on it)
+    bool mut_async = false;
     hipEvent_t ev_fork = nullptr, ev_join[2] = {nullptr, nullptr};
     ~kad_table() {
         for (hipStream_t x : ss)
             if (x) { (void)hipStreamSynchronize(x); (void)hipStreamDestroy(x); }
-        for (hipEvent_t e : {ev_fork, ev_join[0], ev_join[1]})
+        for (hipEvent_t e : {ev_fork, ev_join[0], ev_join[1], mut_ev})
             if (e) (void)hipEventDestroy(e);
         delete pipe;
         for (void* p : owned) (void)hipFree(p);
@@ -5228,6 +5395,15 @@ int stage_reserve(kad_table* t, size_t bytes) {
     return KAD_OK;
 }
 
+// The table's state changed asynchronously on stream s (kad_table_refresh_status): the host batches, on their
+// own streams, wait for the event recorded here.
+int mark_async(kad_table* t, hipStream_t s) {
+    if (!t->mut_ev) HIP_TRY(hipEventCreateWithFlags(&t->mut_ev, hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(t->mut_ev, s));
+    t->mut_async = true;
+    return KAD_OK;
+}
+
 // ---- isGood(now) deadlines, host side (see deadline_kernel) ----
 NodeTimes times_of(const kad_table* t) { return NodeTimes{t->time_ns, t->reply_ns, t->expired}; }
 
@@ -5410,7 +5586,12 @@ int launch_rt(const kad_table* t, const uint8_t* targets, uint32_t q, uint32_t c
 #endif
             hipLaunchKernelGGL(rt_wl16_kernel<0>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
     } else if (K == 32 && (d.flags & TF_WL32) && !(ev && std::strcmp(ev, "lane") == 0)) {
-        hipLaunchKernelGGL(rt_wl32_kernel, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
+        // the quad form ranks faster once the rows are long; below 25 the one-lane form (tools/ab_kernels.py)
+        if ((count < 25 && !(ev && std::strcmp(ev, "wl32quad") == 0)) || (ev && std::strcmp(ev, "wl32lane") == 0))
+            hipLaunchKernelGGL(rt_wl32_kernel, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
+        else
+            hipLaunchKernelGGL(rt_wl32q_kernel<0>, dim3(grid_for(4ull * q)), dim3(BLOCK), 0, s, d, targets, q, count, out,
+                               cnt);
     } else if (K == 8 && (d.flags & TF_SL) && !(ev && (std::strcmp(ev, "lane") == 0 || std::strcmp(ev, "gl") == 0 ||
                                                         std::strcmp(ev, "sl_abl1") == 0))) {
         hipLaunchKernelGGL(rt_sl_kernel<0>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
@@ -5895,7 +6076,8 @@ int kad_table_refresh_status(kad_table* t, int64_t now_ns, void* stream) {
         D.hpend.clear();
         D.last_now = now_ns;
         if ((rc = dl_publish(t, s))) { D.invalidate(); return rc; }
-        return rebuild_good_prefix(t, s, false);
+        if ((rc = rebuild_good_prefix(t, s, false))) return rc;
+        return mark_async(t, s);
     }
     // first refresh after set_times / a status patch, or `now` moved back: every node, then the runs
     D.invalidate();
@@ -5908,7 +6090,7 @@ int kad_table_refresh_status(kad_table* t, int64_t now_ns, void* stream) {
         D.valid = true;
         D.last_now = now_ns;
     }
-    return KAD_OK;
+    return mark_async(t, s);
 }
 
 int kad_rt_closest_batch(const kad_table* t, const uint8_t* targets, uint32_t q, uint32_t count, uint32_t* out_idx,
@@ -6296,11 +6478,19 @@ static int small_query(const kad_table* t, HostPipe& P, const uint8_t* targets, 
     int rc = small_ready(P);
     if (rc) return rc;
     std::memcpy(P.st, targets, 20ull * q);
-    HIP_TRY(hipEventRecord(P.start, nullptr));  // ordered after the work issued on the null stream
-    HIP_TRY(hipStreamWaitEvent(P.ss, P.start, 0));
+    const char* mode = std::getenv("KAD_SMALL_SYNC");  // A/B of the synchronisation (tools/latency_floor.hip)
+    // ordered after the table's last asynchronous status refresh, whatever its stream (every other change to a
+    // table is synchronous); an event on the null stream would cost a whole round trip (13 us on MI355X)
+    if (t->mut_async) HIP_TRY(hipStreamWaitEvent(P.ss, t->mut_ev, 0));
     rc = nc ? kad_nc_closest_batch(t, P.dst, q, count, P.dsi, P.dsc, P.ss)
             : kad_rt_closest_batch(t, P.dst, q, count, P.dsi, P.dsc, P.ss);
-    const hipError_t e = hipStreamSynchronize(P.ss);
+    hipError_t e = hipSuccess;
+    if (mode && std::strstr(mode, "spin")) {
+        while ((e = hipStreamQuery(P.ss)) == hipErrorNotReady) {
+        }
+    } else {
+        e = hipStreamSynchronize(P.ss);
+    }
     if (rc) return rc;
     if (e != hipSuccess) return set_err(KAD_ERR_HIP, "host batch: %s", hipGetErrorString(e));
     if (count) std::memcpy(out_idx, P.si, 4ull * q * count);
@@ -6333,10 +6523,10 @@ static int host_query(const kad_table* t, const uint8_t* targets, uint32_t q, ui
         return small_query(t, P, targets, q, count, out_idx, out_cnt, nc);
     int rc = pipe_ready(P);
     if (rc) return rc;
-    // ordered after the work already issued, as a null-stream call is (a status refresh, a mirror update, ...)
-    HIP_TRY(hipEventRecord(P.start, nullptr));
-    for (auto& w : P.slot)
-        for (HostPipe::Slot& S : w) HIP_TRY(hipStreamWaitEvent(S.s, P.start, 0));
+    // ordered after the table's last asynchronous status refresh, whatever its stream
+    if (t->mut_async)
+        for (auto& w : P.slot)
+            for (HostPipe::Slot& S : w) HIP_TRY(hipStreamWaitEvent(S.s, t->mut_ev, 0));
     if (count > 32u * HostPipe::CHUNK)
         return set_err(KAD_ERR_UNSUPPORTED, "count %u exceeds a host-batch chunk row (%u): use the device-pointer batch",
                        count, 32u * HostPipe::CHUNK);

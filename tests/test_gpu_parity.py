@@ -162,10 +162,17 @@ def test_index_base_and_padding(gpu):
 
 
 def test_count_limits(gpu):
+    """Any count for findClosestNodes (test_rt_closest_any_count); the wire step still takes at most
+    KAD_MAX_COUNT candidates per query and says so."""
     t = TB.split_config(257, seed=98)
     with make(t, gpu) as T:
+        tg = dev(TB.adversarial_targets(t), gpu)
+        idx, cnt = T.rt_closest(tg, 33)
+        torch.cuda.synchronize()
+        assert idx.shape[1] == 33
+        T.set_addrs(np.zeros((t["ids"].shape[0], 6), np.uint8))
         with pytest.raises(KadError):
-            T.rt_closest(dev(TB.adversarial_targets(t), gpu), 33)
+            T.buffer_nodes(tg, torch.zeros((tg.shape[0], 33), dtype=torch.int32, device=gpu))
 
 
 def test_status_update_and_refresh_from_times(gpu):

@@ -216,3 +216,35 @@ def test_now_walk_across_deadlines(gpu):
                 step(now, check_queries=True)
         now += 30 * MIN  # most good nodes age out
         step(now, check_queries=True)
+
+
+def test_host_batch_ordered_after_async_refresh(gpu):
+    """kad_table_refresh_status on a non-blocking torch stream, then at once a host-pointer batch (which runs on the
+    table's own streams): the batch must see the refreshed status (kadgpu.h: host batches are ordered after the
+    table's last asynchronous refresh), for the one-launch small batch and the chunked pipeline."""
+    t = TB.uniform_config(60_000, 13, seed=0x5E9)
+    n = t["ids"].shape[0]
+    rng = np.random.default_rng(0x5E9)
+    targets = TB.adversarial_targets(t, extra=3000)
+    MIN = 60 * 10**9
+    now = 900 * 3600 * 10**9
+    time_ns = now - rng.integers(0, 10 * MIN, n)
+    reply_ns = now - rng.integers(0, 120 * MIN, n)
+    expired = (rng.random(n) < 0.05).astype(np.uint8)
+
+    def status_at(tnow):
+        good = (expired == 0) & (reply_ns >= tnow - 120 * MIN) & (time_ns >= tnow - 10 * MIN)
+        return (good.astype(np.uint8) | (expired << 1)).astype(np.uint8)
+
+    side = torch.cuda.Stream(gpu)
+    with DeviceTable(t["ids"], status_at(now), t["first"], t["off"], device=0, sorted=True) as T:
+        T.set_times(time_ns, reply_ns, expired)
+        for dt in (0, 4 * MIN, 3 * MIN, 2 * MIN):  # the first: every node; then ~40 % / 30 % / 20 % age out
+            now += dt
+            T.refresh_status(now, stream=side.cuda_stream)  # no synchronisation before the host batches
+            st = status_at(now)
+            for q in (7, 1024, targets.shape[0]):
+                idx, cnt = T.rt_closest_host(targets[:q], 8)
+                want, wcnt = O.flat_rt_closest(t["ids"], st, t["first"], t["off"], targets[:q], 8, nthreads=8)
+                np.testing.assert_array_equal(idx, want, err_msg=f"dt={dt} q={q}")
+                np.testing.assert_array_equal(cnt, wcnt)
