@@ -65,6 +65,15 @@ extern "C" {
 
 /* kad_table_create flags */
 #define KAD_TABLE_SORTED 0x01u      /* node array ascending by ID (enables NodeCache queries) */
+#define KAD_TABLE_EAGER 0x02u       /* build every line set at creation (default: those of count <= 8 RoutingTable
+                                       queries; the others on first use, kad_table_prepare) */
+
+/* line sets built on first use (kad_table_prepare, kad_table_line_sets) */
+#define KAD_LINES_RT16 0x01u        /* RoutingTable counts 9..16 (brings KAD_LINES_RT32, their fallback) */
+#define KAD_LINES_RT32 0x02u        /* RoutingTable counts 17..32 */
+#define KAD_LINES_NC16 0x04u        /* NodeCache counts 1..16 */
+#define KAD_LINES_NC32 0x08u        /* NodeCache counts 17..32 (brings KAD_LINES_NC16) */
+#define KAD_LINES_ALL 0x0Fu
 /* kad_table_info.flags, reported only */
 #define KAD_INFO_WINDOW_LINES 0x100u /* uniform-depth table: count <= 8 queries use one 128-byte
                                         window line per query (rt_wl_kernel) */
@@ -125,6 +134,13 @@ int kad_table_create(kad_table** out, int device,
                      uint32_t index_base, uint32_t flags);
 int kad_table_destroy(kad_table* t);
 int kad_table_get_info(const kad_table* t, kad_table_info* out);
+/* Build the line sets `sets` (KAD_LINES_*) now, if not yet: a query builds the set it needs on first use
+ * (synchronising the device once, and never inside a stream capture, where it answers on its slower exact
+ * path instead), so a caller about to capture a HIP graph prepares them first. Synchronous. */
+int kad_table_prepare(kad_table* t, uint32_t sets);
+/* Which line sets are built (KAD_LINES_* mask), and per set in bit order (RT16, RT32, NC16, NC32) the HBM
+ * bytes and the build time in ms of its first build (any output may be NULL). */
+int kad_table_line_sets(const kad_table* t, uint32_t* built, uint64_t* bytes, float* build_ms);
 
 /* Replace the status snapshot (host bytes, n_nodes). Synchronous. Incremental: only the buckets whose
  * good set changed get new masks, and only the window / NodeCache lines whose window reaches a changed

@@ -19,6 +19,8 @@ KAD_NO_NODE = 0xFFFFFFFF
 KAD_STATUS_GOOD = 0x01
 KAD_STATUS_EXPIRED = 0x02
 KAD_TABLE_SORTED = 0x01
+KAD_TABLE_EAGER = 0x02
+KAD_LINES_RT16, KAD_LINES_RT32, KAD_LINES_NC16, KAD_LINES_NC32, KAD_LINES_ALL = 0x01, 0x02, 0x04, 0x08, 0x0F
 KAD_INFO_WINDOW_LINES = 0x100
 KAD_INFO_GENERAL_LINES = 0x200
 KAD_INFO_GENERAL_LINES32 = 0x400
@@ -76,6 +78,8 @@ SIGNATURES = {
                                    C.c_uint32, C.c_uint32]),
     "kad_table_destroy": (C.c_int, [_P]),
     "kad_table_get_info": (C.c_int, [_P, _P]),
+    "kad_table_prepare": (C.c_int, [_P, C.c_uint32]),
+    "kad_table_line_sets": (C.c_int, [_P, _P, _P, _P]),
     "kad_table_update_status": (C.c_int, [_P, _P]),
     "kad_table_apply": (C.c_int, [_P, _P, C.c_uint32, _P, _P, C.c_uint32, _P, _P]),
     "kad_table_export": (C.c_int, [_P, _P, _P, _P, _P]),

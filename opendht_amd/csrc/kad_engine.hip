@@ -47,6 +47,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <atomic>
 #include <mutex>
 #include <thread>
 #include <string>
@@ -5038,6 +5039,12 @@ struct kad_table {
     hipStream_t ss[2] = {nullptr, nullptr};  // side streams of an incremental rebuild (side_streams)
     hipEvent_t mut_ev = nullptr;    // recorded after the last asynchronous status refresh (the host batches wait on it)
     bool mut_async = false;
+    // line sets built on first use (ensure_lines): the sets built or found not to apply to this table's shape,
+    // and each one's bytes and build time
+    std::atomic<uint32_t> ls_done{0};
+    std::mutex ls_mu;
+    uint64_t ls_bytes[8] = {};
+    float ls_ms[8] = {};
     hipEvent_t ev_fork = nullptr, ev_join[2] = {nullptr, nullptr};
     ~kad_table() {
         for (hipStream_t x : ss)
@@ -5190,6 +5197,8 @@ int rebuild_good_prefix_(kad_table* t, hipStream_t s, bool full) {
 // coarsest (smallest table) at which at most 1/32 of the coarse slots hold a bucket start (their queries take a
 // fallback line), provided the lines fit 512 MiB; otherwise no slot lines. Synchronous; a failure leaves the
 // table without them.
+int build_sl16(kad_table* t);
+
 int setup_slot_lines(kad_table* t) {
     DevTable& d = t->d;
     if (!(d.flags & TF_GL) || !t->gl_mut || d.B == 0 || d.rslots == 0 || t->h_first.size() < 20ull * d.B) return KAD_OK;
@@ -5249,88 +5258,124 @@ int setup_slot_lines(kad_table* t) {
     d.slshift = d.rshift + k;
     d.slslots = slslots;
     d.flags |= TF_SL;
-    // counts 9..16: copies of the gl16 lines at the same slots (optional: without them, locate + gl16)
-    if (t->gl16_mut) {
-        std::vector<void*> f16;
-        uint64_t b16 = 0;
-        uint32_t* l16 = nullptr;
-        if (dev_upload(&l16, nullptr, (size_t)GL16_STRIDE * slslots, f16, b16) == KAD_OK) {
-            hipLaunchKernelGGL(sl16_build_kernel, dim3(grid_for(8ull * slslots)), dim3(BLOCK), 0, 0, t->gl16_mut, slb,
-                               slslots, nullptr, d.rrdx, d.rslots, k, d.fkey, d.ftail, l16);
-            if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
-                for (void* p : f16) (void)hipFree(p);
-                return set_err(KAD_ERR_HIP, "slot-line (16) build failed");
-            }
-            t->owned.insert(t->owned.end(), f16.begin(), f16.end());
-            t->bytes += b16;
-            t->sl16_mut = l16;
-            d.sl16 = reinterpret_cast<const uint4*>(l16);
-            d.flags |= TF_SL16;
+    return build_sl16(t);
+}
+
+// Counts 9..16 on a table with slot lines: copies of the gl16 lines at the same slots (optional: without them,
+// locate + gl16). Synchronous.
+int build_sl16(kad_table* t) {
+    DevTable& d = t->d;
+    if (!t->gl16_mut || !t->sl_mut || t->sl16_mut) return KAD_OK;
+    std::vector<void*> f16;
+    uint64_t b16 = 0;
+    uint32_t* l16 = nullptr;
+    if (dev_upload(&l16, nullptr, (size_t)GL16_STRIDE * d.slslots, f16, b16) == KAD_OK) {
+        hipLaunchKernelGGL(sl16_build_kernel, dim3(grid_for(8ull * d.slslots)), dim3(BLOCK), 0, 0, t->gl16_mut, t->slb,
+                           d.slslots, nullptr, d.rrdx, d.rslots, d.slshift - d.rshift, d.fkey, d.ftail, l16);
+        if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+            for (void* p : f16) (void)hipFree(p);
+            return set_err(KAD_ERR_HIP, "slot-line (16) build failed");
         }
+        t->owned.insert(t->owned.end(), f16.begin(), f16.end());
+        t->bytes += b16;
+        t->sl16_mut = l16;
+        d.sl16 = reinterpret_cast<const uint4*>(l16);
+        d.flags |= TF_SL16;
     }
     return KAD_OK;
 }
 
-// General window lines (TF_GL / TF_GL32) for a table without uniform-depth lines: allocated, built from the
-// current status, and kept only when at most 1/16 of them are deferred (otherwise the lane kernel is the
-// faster path). Synchronous. A failure leaves the table without general lines (still correct).
+// General window lines for count <= 8 (TF_GL) for a table without uniform-depth lines: allocated, built from the
+// current status, and kept only when at most 1/16 of them are deferred (otherwise the lane kernel is the faster
+// path); then the slot lines. Synchronous. A failure leaves the table without general lines (still correct).
+// The count 9..32 general lines are built on first use (build_gl32, build_gl16).
+int count_deferred(const uint32_t* lines, uint32_t stride, uint32_t hdr_word, uint32_t B, uint32_t& nd) {
+    uint32_t* cnt = nullptr;
+    HIP_TRY(hipMalloc(&cnt, 4));
+    hipError_t e = hipMemset(cnt, 0, 4);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(count_deferred_kernel, dim3(grid_for(B)), dim3(BLOCK), 0, 0, lines, stride, hdr_word, B, cnt);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpy(&nd, cnt, 4, hipMemcpyDeviceToHost);
+    (void)hipFree(cnt);
+    if (e != hipSuccess) return set_err(KAD_ERR_HIP, "deferred-line count failed: %s", hipGetErrorString(e));
+    return KAD_OK;
+}
+
 int setup_general_lines(kad_table* t) {
     DevTable& d = t->d;
     if (d.B == 0 || (d.flags & TF_WL) || !d.fkey) return KAD_OK;
     const uint32_t B = d.B;
-    uint32_t *lp = nullptr, *lp16 = nullptr, *lp32 = nullptr, *cnt = nullptr;
-    int rc;
+    uint32_t* lp = nullptr;
     std::vector<void*> fresh;
     uint64_t fb = 0;
-    auto drop = [&]() { for (void* p : fresh) (void)hipFree(p); };
-    if ((rc = dev_upload(&lp, nullptr, (size_t)GL_STRIDE * B, fresh, fb)) ||
-        (rc = dev_upload(&lp16, nullptr, (size_t)GL16_STRIDE * B, fresh, fb)) ||
-        (rc = dev_upload(&lp32, nullptr, (size_t)GL32_STRIDE * B, fresh, fb)) ||
-        (rc = dev_upload(&cnt, nullptr, 3, fresh, fb))) {
-        drop();
-        return KAD_OK;
-    }
-    if (hipMemset(cnt, 0, 12) != hipSuccess) { drop(); return KAD_OK; }
+    if (dev_upload(&lp, nullptr, (size_t)GL_STRIDE * B, fresh, fb)) return KAD_OK;
     hipLaunchKernelGGL(gl_build_kernel, dim3(grid_for(B)), dim3(BLOCK), 0, 0, d.key, d.status, d.dir, d.gpre, d.fkey,
                        d.ftail, B, lp, LineSel{});
-    hipLaunchKernelGGL(gl16_build_kernel, dim3(grid_for(B)), dim3(BLOCK), 0, 0, d.key, d.status, d.dir, d.gpre, d.fkey,
-                       d.ftail, B, lp16, LineSel{});
-    hipLaunchKernelGGL(gl32_build_kernel, dim3(grid_for(B)), dim3(BLOCK), 0, 0, d.key, d.status, d.dir, d.gpre, d.fkey,
-                       d.ftail, B, lp32, LineSel{});
-    hipLaunchKernelGGL(count_deferred_kernel, dim3(grid_for(B)), dim3(BLOCK), 0, 0, lp, GL_STRIDE, 1u, B, cnt);
-    hipLaunchKernelGGL(count_deferred_kernel, dim3(grid_for(B)), dim3(BLOCK), 0, 0, lp32, GL32_STRIDE, 3u, B, cnt + 1);
-    hipLaunchKernelGGL(count_deferred_kernel, dim3(grid_for(B)), dim3(BLOCK), 0, 0, lp16, GL16_STRIDE, 1u, B, cnt + 2);
-    uint32_t nd[3] = {B, B, B};
-    if (hipGetLastError() != hipSuccess || hipMemcpy(nd, cnt, 12, hipMemcpyDeviceToHost) != hipSuccess) {
-        drop();
+    uint32_t nd = B;
+    int rc;
+    if (hipGetLastError() != hipSuccess || (rc = count_deferred(lp, GL_STRIDE, 1u, B, nd))) {
+        (void)hipFree(lp);
         return set_err(KAD_ERR_HIP, "general window-line build failed");
     }
-    (void)hipFree(cnt);
-    fresh.pop_back();
-    fb -= 16;
-    const bool keep8 = (uint64_t)nd[0] * 16 <= B, keep32 = (uint64_t)nd[1] * 16 <= B;
-    const bool keep16 = keep32 && (uint64_t)nd[2] * 16 <= B;  // counts 9..16 fall back to the 256-byte lines
-    if (std::getenv("KAD_DEBUG"))
-        std::fprintf(stderr, "general lines: B=%u deferred %u / %u / %u (8 / 32 / 16)\n", B, nd[0], nd[1], nd[2]);
-    if (keep8) {
-        t->owned.push_back(lp); t->bytes += (uint64_t)GL_STRIDE * 4 * B;
-        t->gl_mut = lp; d.gl = reinterpret_cast<const uint4*>(lp); d.flags |= TF_GL;
-    } else {
+    if (std::getenv("KAD_DEBUG")) std::fprintf(stderr, "general lines: B=%u deferred %u (count <= 8)\n", B, nd);
+    if ((uint64_t)nd * 16 > B) {
         (void)hipFree(lp);
+        return KAD_OK;
     }
-    if (keep16) {
-        t->owned.push_back(lp16); t->bytes += (uint64_t)GL16_STRIDE * 4 * B;
-        t->gl16_mut = lp16; d.gl16 = reinterpret_cast<const uint4*>(lp16); d.flags |= TF_GL16;
-    } else {
-        (void)hipFree(lp16);
-    }
-    if (keep32) {
-        t->owned.push_back(lp32); t->bytes += (uint64_t)GL32_STRIDE * 4 * B;
-        t->gl32_mut = lp32; d.gl32 = reinterpret_cast<const uint4*>(lp32); d.flags |= TF_GL32;
-    } else {
-        (void)hipFree(lp32);
-    }
+    t->owned.push_back(lp); t->bytes += fb;
+    t->gl_mut = lp; d.gl = reinterpret_cast<const uint4*>(lp); d.flags |= TF_GL;
     return setup_slot_lines(t);
+}
+
+// The 256-byte general lines (counts 9..32), kept when at most 1/16 are deferred. Synchronous.
+int build_gl32(kad_table* t) {
+    DevTable& d = t->d;
+    if (d.B == 0 || (d.flags & TF_WL) || !d.fkey || t->gl32_mut) return KAD_OK;
+    const uint32_t B = d.B;
+    uint32_t* lp = nullptr;
+    std::vector<void*> fresh;
+    uint64_t fb = 0;
+    int rc;
+    if ((rc = dev_upload(&lp, nullptr, (size_t)GL32_STRIDE * B, fresh, fb))) return rc;
+    hipLaunchKernelGGL(gl32_build_kernel, dim3(grid_for(B)), dim3(BLOCK), 0, 0, d.key, d.status, d.dir, d.gpre, d.fkey,
+                       d.ftail, B, lp, LineSel{});
+    uint32_t nd = B;
+    if (hipGetLastError() != hipSuccess || (rc = count_deferred(lp, GL32_STRIDE, 3u, B, nd))) {
+        (void)hipFree(lp);
+        return set_err(KAD_ERR_HIP, "general window-line (32) build failed");
+    }
+    if (std::getenv("KAD_DEBUG")) std::fprintf(stderr, "general lines 32: B=%u deferred %u\n", B, nd);
+    if ((uint64_t)nd * 16 > B) { (void)hipFree(lp); return KAD_OK; }
+    t->owned.push_back(lp); t->bytes += fb;
+    t->gl32_mut = lp; d.gl32 = reinterpret_cast<const uint4*>(lp); d.flags |= TF_GL32;
+    return KAD_OK;
+}
+
+// The 128-byte general lines of counts 9..16 (the 256-byte lines are their fallback, so only with those), kept
+// when at most 1/16 are deferred, and their slot-indexed copies when the table has slot lines. Synchronous.
+int build_gl16(kad_table* t) {
+    DevTable& d = t->d;
+    if (d.B == 0 || (d.flags & TF_WL) || !d.fkey || t->gl16_mut || !t->gl32_mut) return KAD_OK;
+    const uint32_t B = d.B;
+    uint32_t* lp = nullptr;
+    std::vector<void*> fresh;
+    uint64_t fb = 0;
+    int rc;
+    if ((rc = dev_upload(&lp, nullptr, (size_t)GL16_STRIDE * B, fresh, fb))) return rc;
+    hipLaunchKernelGGL(gl16_build_kernel, dim3(grid_for(B)), dim3(BLOCK), 0, 0, d.key, d.status, d.dir, d.gpre, d.fkey,
+                       d.ftail, B, lp, LineSel{});
+    uint32_t nd = B;
+    if (hipGetLastError() != hipSuccess || (rc = count_deferred(lp, GL16_STRIDE, 1u, B, nd))) {
+        (void)hipFree(lp);
+        return set_err(KAD_ERR_HIP, "general window-line (16) build failed");
+    }
+    if (std::getenv("KAD_DEBUG")) std::fprintf(stderr, "general lines 16: B=%u deferred %u\n", B, nd);
+    if ((uint64_t)nd * 16 > B) { (void)hipFree(lp); return KAD_OK; }
+    t->owned.push_back(lp); t->bytes += fb;
+    t->gl16_mut = lp; d.gl16 = reinterpret_cast<const uint4*>(lp); d.flags |= TF_GL16;
+    return build_sl16(t);
 }
 
 // Allocate (zeroed) the incremental-refresh flags for the table's current shape.
@@ -5540,6 +5585,137 @@ int dl_patch(kad_table* t, uint32_t m, const uint32_t* nodes, const int64_t* tim
     return KAD_OK;
 }
 
+// ---- line sets built on first use --------------------------------------------------------------------------
+// kad_table_create builds the count <= 8 lines (the headline path) and, with KAD_TABLE_EAGER, every other set;
+// otherwise a set is built by the first query that needs it (ensure_lines), which synchronises the device once.
+int build_wl16(kad_table* t) {
+    DevTable& d = t->d;
+    if (!(d.flags & TF_WL) || t->wl16_mut) return KAD_OK;
+    uint32_t* lp = nullptr;
+    std::vector<void*> fresh;
+    uint64_t fb = 0;
+    int rc;
+    if ((rc = dev_upload(&lp, nullptr, (size_t)WL16_STRIDE * d.B, fresh, fb))) return rc;
+    hipLaunchKernelGGL(wl16_build_kernel, dim3(grid_for(d.B)), dim3(BLOCK), 0, 0, d.key, d.status, d.dir, d.gpre, d.B,
+                       64 - d.rshift, d.rbase >> d.rshift, lp, LineSel{});
+    if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+        (void)hipFree(lp);
+        return set_err(KAD_ERR_HIP, "window-line (16) build failed");
+    }
+    t->owned.push_back(lp); t->bytes += fb;
+    d.wl16 = reinterpret_cast<const uint4*>(lp); t->wl16_mut = lp; d.flags |= TF_WL16;
+    return KAD_OK;
+}
+
+int build_wl32(kad_table* t) {
+    DevTable& d = t->d;
+    if (!(d.flags & TF_WL) || t->wl32_mut || 64 - d.rshift > 44) return KAD_OK;  // 20-bit in-bucket keys
+    uint32_t* lp = nullptr;
+    std::vector<void*> fresh;
+    uint64_t fb = 0;
+    int rc;
+    if ((rc = dev_upload(&lp, nullptr, (size_t)WL32_STRIDE * d.B, fresh, fb))) return rc;
+    hipLaunchKernelGGL(wl32_build_kernel, dim3(grid_for(d.B)), dim3(BLOCK), 0, 0, d.key, d.status, d.dir, d.gpre, d.B,
+                       64 - d.rshift, d.rbase >> d.rshift, lp, LineSel{});
+    if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+        (void)hipFree(lp);
+        return set_err(KAD_ERR_HIP, "window-line (32) build failed");
+    }
+    t->owned.push_back(lp); t->bytes += fb;
+    d.wl32 = reinterpret_cast<const uint4*>(lp); t->wl32_mut = lp; d.flags |= TF_WL32;
+    return KAD_OK;
+}
+
+int build_ncl(kad_table* t) {
+    DevTable& d = t->d;
+    if (!(t->flags & KAD_TABLE_SORTED) || !d.nrdx || d.n == 0 || t->ncl_mut) return KAD_OK;
+    uint32_t* lp = nullptr;
+    std::vector<void*> fresh;
+    uint64_t fb = 0;
+    int rc;
+    if ((rc = dev_upload(&lp, nullptr, (size_t)NCL_STRIDE * d.nslots, fresh, fb))) return rc;
+    hipLaunchKernelGGL(ncl_build_kernel, dim3(grid_for(d.nslots)), dim3(BLOCK), 0, 0, d.key, d.status, d.nrdx, d.nslots,
+                       d.n, 64 - d.nshift, lp, LineSel{});
+    if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+        (void)hipFree(lp);
+        return set_err(KAD_ERR_HIP, "NodeCache line build failed");
+    }
+    t->owned.push_back(lp); t->bytes += fb;
+    d.ncl = reinterpret_cast<const uint4*>(lp); t->ncl_mut = lp; d.flags |= TF_NCL;
+    return KAD_OK;
+}
+
+int build_ncl32(kad_table* t) {
+    DevTable& d = t->d;
+    if (!(t->flags & KAD_TABLE_SORTED) || !d.nrdx || d.n == 0 || t->ncl32_mut) return KAD_OK;
+    uint32_t* lp = nullptr;
+    std::vector<void*> fresh;
+    uint64_t fb = 0;
+    int rc;
+    if ((rc = dev_upload(&lp, nullptr, (size_t)NC32_STRIDE * d.nslots, fresh, fb))) return rc;
+    hipLaunchKernelGGL(ncl32_build_kernel, dim3(grid_for(8ull * d.nslots)), dim3(BLOCK), 0, 0, d.key, d.status, d.nrdx,
+                       d.nslots, d.n, 64 - d.nshift, lp, LineSel{});
+    if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+        (void)hipFree(lp);
+        return set_err(KAD_ERR_HIP, "NodeCache line (32) build failed");
+    }
+    t->owned.push_back(lp); t->bytes += fb;
+    d.ncl32 = reinterpret_cast<const uint4*>(lp); t->ncl32_mut = lp; d.flags |= TF_NCL32;
+    return KAD_OK;
+}
+
+constexpr uint32_t LS_WL16 = KAD_LINES_RT16, LS_WL32 = KAD_LINES_RT32, LS_NCL = KAD_LINES_NC16,
+                   LS_NCL32 = KAD_LINES_NC32, LS_ALL = KAD_LINES_ALL;
+
+// The line sets `need` (KAD_LINES_*) of a table, built now if they are not yet (the count 9..16 sets bring the
+// 17..32 ones, their fallback). Nothing is built inside a stream capture (no allocation there): the kernels
+// answer exactly without the set, on their slower paths. An allocation failure leaves the set unbuilt (the
+// same fallbacks), any other failure is returned.
+int ensure_lines(const kad_table* ct, uint32_t need, hipStream_t s) {
+    kad_table* t = const_cast<kad_table*>(ct);  // the sets are caches of the table's state
+    if (need & LS_WL16) need |= LS_WL32;
+    if (need & LS_NCL32) need |= LS_NCL;  // the refresh rebuilds the 512-byte lines along with the 256-byte ones
+    if (!(need & ~t->ls_done.load(std::memory_order_acquire))) return KAD_OK;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (s) {  // the null stream is never captured (and the query would fail with the runtime's last error set)
+        if (hipStreamIsCapturing(s, &cs) != hipSuccess) (void)hipGetLastError();
+        else if (cs != hipStreamCaptureStatusNone) return KAD_OK;
+    }
+    std::lock_guard<std::mutex> lk(t->ls_mu);
+    need &= ~t->ls_done.load(std::memory_order_relaxed);
+    if (!need) return KAD_OK;
+    DeviceGuard g(t->device);
+    HIP_TRY(hipDeviceSynchronize());  // built from the current status, whatever stream changed it last
+    const uint32_t bits[4] = {LS_WL32, LS_WL16, LS_NCL, LS_NCL32};
+    int (*uni[4])(kad_table*) = {build_wl32, build_wl16, build_ncl, build_ncl32};
+    int (*gen[4])(kad_table*) = {build_gl32, build_gl16, build_ncl, build_ncl32};
+    const bool general = !(t->d.flags & TF_WL);
+    int rc = KAD_OK;
+    for (int k = 0; k < 4 && rc == KAD_OK; k++) {
+        if (!(need & bits[k])) continue;
+        const uint64_t b0 = t->bytes;
+        const auto a = std::chrono::steady_clock::now();
+        rc = (general ? gen[k] : uni[k])(t);
+        if (rc == KAD_ERR_NOMEM) rc = KAD_OK;  // unbuilt: the fallbacks answer
+        t->ls_ms[k] = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - a).count();
+        t->ls_bytes[k] = t->bytes - b0;
+        t->ls_done.fetch_or(bits[k], std::memory_order_release);
+    }
+    drop_marks(t);  // the incremental-refresh flags are re-allocated with the new sets'
+    return rc;
+}
+
+// After a structural change (kad_table_apply, kad_nc_apply): a set the table still has stays built; the others
+// may be built again on first use.
+void reset_line_sets(kad_table* t) {
+    uint32_t done = 0;
+    if (t->wl16_mut || t->gl16_mut) done |= LS_WL16;
+    if (t->wl32_mut || t->gl32_mut) done |= LS_WL32;
+    if (t->ncl_mut) done |= LS_NCL;
+    if (t->ncl32_mut) done |= LS_NCL32;
+    t->ls_done.store(done, std::memory_order_release);
+}
+
 int check_count(uint32_t count) {
     if (count > KAD_MAX_COUNT) return set_err(KAD_ERR_UNSUPPORTED, "count %u > KAD_MAX_COUNT (%u)", count, KAD_MAX_COUNT);
     return KAD_OK;
@@ -5586,8 +5762,10 @@ int launch_rt(const kad_table* t, const uint8_t* targets, uint32_t q, uint32_t c
 #endif
             hipLaunchKernelGGL(rt_wl16_kernel<0>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
     } else if (K == 32 && (d.flags & TF_WL32) && !(ev && std::strcmp(ev, "lane") == 0)) {
-        // the quad form ranks faster once the rows are long; below 25 the one-lane form (tools/ab_kernels.py)
-        if ((count < 25 && !(ev && std::strcmp(ev, "wl32quad") == 0)) || (ev && std::strcmp(ev, "wl32lane") == 0))
+        // the quad form ranks faster for long rows stored as 16-byte pieces (counts 28 and 32), the one-lane
+        // form for the others (tools/ab_kernels.py, profiles/r03/ab_wl32.json)
+        const bool quad = count >= 28 && (count & 3u) == 0;
+        if ((!quad && !(ev && std::strcmp(ev, "wl32quad") == 0)) || (ev && std::strcmp(ev, "wl32lane") == 0))
             hipLaunchKernelGGL(rt_wl32_kernel, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
         else
             hipLaunchKernelGGL(rt_wl32q_kernel<0>, dim3(grid_for(4ull * q)), dim3(BLOCK), 0, s, d, targets, q, count, out,
@@ -5623,6 +5801,7 @@ void launch_rt_dual(const DevTable& d4, const DevTable& d6, const uint8_t* targe
 int rt_dispatch(const kad_table* t, const uint8_t* targets, uint32_t q, uint32_t count, uint32_t* out, uint8_t* cnt,
                 hipStream_t s) {
     int rc = KAD_OK;
+    if (count > 8 && count <= KAD_MAX_COUNT && (rc = ensure_lines(t, count <= 16 ? LS_WL16 : LS_WL32, s))) return rc;
     if (count > KAD_MAX_COUNT) {
         if ((uint64_t)q > 0xFFFFFFFFull / 4 * BLOCK / 64) return set_err(KAD_ERR_INVALID, "batch too large");
         hipLaunchKernelGGL(rt_wave_kernel, dim3((q + BLOCK / 64 - 1) / (BLOCK / 64)), dim3(BLOCK), 0, s, t->d, t->d,
@@ -5859,36 +6038,6 @@ int kad_table_create(kad_table** out, int device, uint32_t n_nodes, const uint8_
                 d.ws = reinterpret_cast<const uint4*>(lps);
                 t->ws_mut = lps;
                 d.flags |= TF_WS;
-                uint32_t* lp16;
-                if ((rc = dev_upload(&lp16, nullptr, (size_t)WL16_STRIDE * n_buckets, t->owned, t->bytes))) {
-                    delete t;
-                    return rc;
-                }
-                hipLaunchKernelGGL(wl16_build_kernel, dim3(grid_for(n_buckets)), dim3(BLOCK), 0, 0, d.key, d.status, d.dir,
-                                   d.gpre, n_buckets, depth, pre0, lp16, LineSel{});
-                if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
-                    delete t;
-                    return set_err(KAD_ERR_HIP, "window-line (16) build failed");
-                }
-                d.wl16 = reinterpret_cast<const uint4*>(lp16);
-                t->wl16_mut = lp16;
-                d.flags |= TF_WL16;
-                if (depth <= 44) {  // 20-bit in-bucket keys
-                    uint32_t* lp32;
-                    if ((rc = dev_upload(&lp32, nullptr, (size_t)WL32_STRIDE * n_buckets, t->owned, t->bytes))) {
-                        delete t;
-                        return rc;
-                    }
-                    hipLaunchKernelGGL(wl32_build_kernel, dim3(grid_for(n_buckets)), dim3(BLOCK), 0, 0, d.key, d.status,
-                                       d.dir, d.gpre, n_buckets, depth, pre0, lp32, LineSel{});
-                    if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
-                        delete t;
-                        return set_err(KAD_ERR_HIP, "window-line (32) build failed");
-                    }
-                    d.wl32 = reinterpret_cast<const uint4*>(lp32);
-                    t->wl32_mut = lp32;
-                    d.flags |= TF_WL32;
-                }
             }
         }
     }
@@ -5907,28 +6056,11 @@ int kad_table_create(kad_table** out, int device, uint32_t n_nodes, const uint8_
         uint32_t* dn;
         if ((rc = dev_upload(&dn, rdx.data(), rdx.size(), t->owned, t->bytes))) { delete t; return rc; }
         d.nrdx = dn; d.nbase = r.base; d.nshift = r.shift; d.nslots = r.slots; t->nbits = r.bits;
-        uint32_t* lp;
-        if ((rc = dev_upload(&lp, nullptr, (size_t)NCL_STRIDE * r.slots, t->owned, t->bytes))) { delete t; return rc; }
-        hipLaunchKernelGGL(ncl_build_kernel, dim3(grid_for(r.slots)), dim3(BLOCK), 0, 0, d.key, d.status, dn, r.slots,
-                           n_nodes, 64 - r.shift, lp, LineSel{});
-        if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
-            delete t;
-            return set_err(KAD_ERR_HIP, "NodeCache line build failed");
-        }
-        d.ncl = reinterpret_cast<const uint4*>(lp);
-        t->ncl_mut = lp;
-        d.flags |= TF_NCL;
-        uint32_t* lp32;
-        if ((rc = dev_upload(&lp32, nullptr, (size_t)NC32_STRIDE * r.slots, t->owned, t->bytes))) { delete t; return rc; }
-        hipLaunchKernelGGL(ncl32_build_kernel, dim3(grid_for(8ull * r.slots)), dim3(BLOCK), 0, 0, d.key, d.status, dn,
-                           r.slots, n_nodes, 64 - r.shift, lp32, LineSel{});
-        if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
-            delete t;
-            return set_err(KAD_ERR_HIP, "NodeCache line (32) build failed");
-        }
-        d.ncl32 = reinterpret_cast<const uint4*>(lp32);
-        t->ncl32_mut = lp32;
-        d.flags |= TF_NCL32;
+    }
+    // the line sets of counts above 8 and of NodeCache queries: now (KAD_TABLE_EAGER) or on first use
+    if ((flags & KAD_TABLE_EAGER) && (rc = ensure_lines(t, LS_ALL, nullptr))) {
+        delete t;
+        return rc;
     }
     *out = t;
     return KAD_OK;
@@ -5964,6 +6096,28 @@ int kad_table_get_info(const kad_table* t, kad_table_info* out) {
         uint32_t last;
         HIP_TRY(hipMemcpy(&last, t->d.gpre + t->d.B, sizeof last, hipMemcpyDeviceToHost));
         out->n_good = last;
+    }
+    return KAD_OK;
+}
+
+int kad_table_prepare(kad_table* t, uint32_t sets) {
+    if (!t) return set_err(KAD_ERR_INVALID, "NULL table");
+    if (sets & ~KAD_LINES_ALL) return set_err(KAD_ERR_INVALID, "unknown line sets 0x%x", sets);
+    DeviceGuard g(t->device);
+    return ensure_lines(t, sets, nullptr);
+}
+
+int kad_table_line_sets(const kad_table* t, uint32_t* built, uint64_t* bytes, float* build_ms) {
+    if (!t) return set_err(KAD_ERR_INVALID, "NULL table");
+    const uint32_t bits[4] = {LS_WL32, LS_WL16, LS_NCL, LS_NCL32};
+    if (built) {
+        *built = ((t->wl16_mut || t->gl16_mut) ? LS_WL16 : 0u) | ((t->wl32_mut || t->gl32_mut) ? LS_WL32 : 0u) |
+                 (t->ncl_mut ? LS_NCL : 0u) | (t->ncl32_mut ? LS_NCL32 : 0u);
+    }
+    for (int k = 0; k < 4; k++) {  // in the order of the KAD_LINES_* bits
+        const int j = bits[k] == LS_WL16 ? 0 : bits[k] == LS_WL32 ? 1 : bits[k] == LS_NCL ? 2 : 3;
+        if (bytes) bytes[j] = t->ls_bytes[k];
+        if (build_ms) build_ms[j] = t->ls_ms[k];
     }
     return KAD_OK;
 }
@@ -6119,6 +6273,11 @@ int kad_rt_closest_batch_dual(const kad_table* t4, const kad_table* t6, const ui
     if (count == 0) {
         if (out_cnt) HIP_TRY(hipMemsetAsync(out_cnt, 0, q, s));
         return KAD_OK;
+    }
+    if (count > 8 && count <= KAD_MAX_COUNT) {
+        const uint32_t need = count <= 16 ? LS_WL16 : LS_WL32;
+        int rc;
+        if ((t4 && (rc = ensure_lines(t4, need, s))) || (t6 && (rc = ensure_lines(t6, need, s)))) return rc;
     }
     if (count > KAD_MAX_COUNT)
         hipLaunchKernelGGL(rt_wave_kernel, dim3((q + BLOCK / 64 - 1) / (BLOCK / 64)), dim3(BLOCK), 0, s, d4, d6, af,
@@ -6345,6 +6504,10 @@ int kad_nc_closest_batch(const kad_table* t, const uint8_t* targets, uint32_t q,
     if (q == 0) return KAD_OK;
     if (!targets || (!out_idx && count)) return set_err(KAD_ERR_INVALID, "NULL buffer");
     DeviceGuard g(t->device);
+    if (count >= 1 && count <= 32) {
+        const int rc = ensure_lines(t, count <= 16 ? LS_NCL : LS_NCL32, (hipStream_t)stream);
+        if (rc) return rc;
+    }
     const char* ev = std::getenv("KAD_NC_KERNEL");
     const bool lines = (t->d.flags & TF_NCL) && !ev;  // KAD_NC_KERNEL=<kernel> picks another one (A/B timing)
 #ifdef KAD_ABLATIONS  // timing ablations with WRONG results: only in the tools build
@@ -6421,6 +6584,11 @@ int kad_nc_closest_batch_dual(const kad_table* t4, const kad_table* t6, const ui
     if (count == 0) {
         if (out_cnt) HIP_TRY(hipMemsetAsync(out_cnt, 0, q, s));
         return KAD_OK;
+    }
+    if (count <= 32) {
+        const uint32_t need = count <= 16 ? LS_NCL : LS_NCL32;
+        int rc;
+        if ((t4 && (rc = ensure_lines(t4, need, s))) || (t6 && (rc = ensure_lines(t6, need, s)))) return rc;
     }
     if (count <= 16)
         hipLaunchKernelGGL((nc_line_kernel<0, true>), dim3(grid_for(q)), dim3(BLOCK), 0, s, d4, d6, af, targets, q, count,
@@ -6893,6 +7061,7 @@ int kad_table_apply(kad_table* t, const uint32_t* ops, uint32_t n_ops, const uin
     // a table that lost (or never had) uniform-depth lines gets general ones (built from the new state)
     if (!(d.flags & TF_WL) && !t->gl_mut && !t->gl32_mut && (rc = setup_general_lines(t))) return rc;
     phase("general lines");
+    reset_line_sets(t);
     return KAD_OK;
 }
 
@@ -6935,7 +7104,8 @@ int kad_nc_apply(kad_table* t, const uint32_t* erase, uint32_t n_erase, const ui
         for (void* p : fresh) (void)hipFree(p);
         return code;
     };
-    uint64_t *dik, *key1; uint32_t *dit, *del, *dcnt, *dpre, *dsums, *dremap, *dnew, *derr, *tail1, *rdx1, *ncl1;
+    uint64_t *dik, *key1; uint32_t *dit, *del, *dcnt, *dpre, *dsums, *dremap, *dnew, *derr, *tail1, *rdx1;
+    uint32_t* ncl1 = nullptr;
     uint8_t *dist, *deflag, *st1;
     const uint32_t tiles = (n0 + 1 + SCAN_TILE - 1) / SCAN_TILE;
     int rc;
@@ -6978,17 +7148,21 @@ int kad_nc_apply(kad_table* t, const uint32_t* erase, uint32_t n_erase, const ui
     while ((1u << tb) < n1 && tb < 23) tb++;
     if (n1) r = choose_radix(kmin, kmax, tb);
     uint32_t* ncl32 = nullptr;
+    // the line sets the table has are rebuilt for the new array; the others stay unbuilt until first use
+    const bool has_ncl = t->ncl_mut != nullptr, has_ncl32 = t->ncl32_mut != nullptr;
     if (n1 && ((rc = dev_upload(&rdx1, nullptr, (size_t)r.slots + 1, fresh, freshb)) ||
-               (rc = dev_upload(&ncl1, nullptr, (size_t)NCL_STRIDE * r.slots, fresh, freshb)) ||
-               (rc = dev_upload(&ncl32, nullptr, (size_t)NC32_STRIDE * r.slots, fresh, freshb))))
+               (has_ncl && (rc = dev_upload(&ncl1, nullptr, (size_t)NCL_STRIDE * r.slots, fresh, freshb))) ||
+               (has_ncl32 && (rc = dev_upload(&ncl32, nullptr, (size_t)NC32_STRIDE * r.slots, fresh, freshb)))))
         return fail(rc);
     if (n1) {
         hipLaunchKernelGGL(nc_radix_kernel, dim3(grid_for((uint64_t)r.slots + 1)), dim3(BLOCK), 0, 0, key1, n1, r.base,
                            r.shift, r.slots, rdx1);
-        hipLaunchKernelGGL(ncl_build_kernel, dim3(grid_for(r.slots)), dim3(BLOCK), 0, 0, key1, st1, rdx1, r.slots, n1,
-                           64 - r.shift, ncl1, LineSel{});
-        hipLaunchKernelGGL(ncl32_build_kernel, dim3(grid_for(8ull * r.slots)), dim3(BLOCK), 0, 0, key1, st1, rdx1,
-                           r.slots, n1, 64 - r.shift, ncl32, LineSel{});
+        if (has_ncl)
+            hipLaunchKernelGGL(ncl_build_kernel, dim3(grid_for(r.slots)), dim3(BLOCK), 0, 0, key1, st1, rdx1, r.slots, n1,
+                               64 - r.shift, ncl1, LineSel{});
+        if (has_ncl32)
+            hipLaunchKernelGGL(ncl32_build_kernel, dim3(grid_for(8ull * r.slots)), dim3(BLOCK), 0, 0, key1, st1, rdx1,
+                               r.slots, n1, 64 - r.shift, ncl32, LineSel{});
     }
     if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess)
         return fail(set_err(KAD_ERR_HIP, "NodeCache radix / line build failed"));
@@ -7011,8 +7185,10 @@ int kad_nc_apply(kad_table* t, const uint32_t* erase, uint32_t n_erase, const ui
     d.key = key1; d.tail = tail1; d.status = st1; t->status_mut = st1; d.n = n1;
     if (n1) {
         d.nrdx = rdx1; d.nbase = r.base; d.nshift = r.shift; d.nslots = r.slots; t->nbits = r.bits;
-        d.ncl = reinterpret_cast<const uint4*>(ncl1); t->ncl_mut = ncl1; d.flags |= TF_NCL;
-        d.ncl32 = reinterpret_cast<const uint4*>(ncl32); t->ncl32_mut = ncl32; d.flags |= TF_NCL32;
+        d.ncl = reinterpret_cast<const uint4*>(ncl1); t->ncl_mut = ncl1;
+        d.flags = has_ncl ? (d.flags | TF_NCL) : (d.flags & ~TF_NCL);
+        d.ncl32 = reinterpret_cast<const uint4*>(ncl32); t->ncl32_mut = ncl32;
+        d.flags = has_ncl32 ? (d.flags | TF_NCL32) : (d.flags & ~TF_NCL32);
     } else {
         d.nrdx = nullptr; d.nslots = 0; t->nbits = 0; d.ncl = nullptr; t->ncl_mut = nullptr; d.flags &= ~TF_NCL;
         d.ncl32 = nullptr; t->ncl32_mut = nullptr; d.flags &= ~TF_NCL32;
@@ -7024,6 +7200,7 @@ int kad_nc_apply(kad_table* t, const uint32_t* erase, uint32_t n_erase, const ui
     t->owned.insert(t->owned.end(), fresh.begin(), fresh.end());
     t->bytes += freshb;
     drop_marks(t);
+    reset_line_sets(t);
     return KAD_OK;
 }
 

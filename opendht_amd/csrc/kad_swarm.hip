@@ -264,6 +264,8 @@ struct SearchDev {
     uint8_t* rn;    // [S][ALPHA]
     uint32_t* active;
     uint32_t* overflow;  // lists that hit LST entries (a bad node was dropped from the end)
+    uint32_t* xo;   // [S][XO_CAP] the search's queried peers that stayed silent: their nodes are expired
+    uint8_t* xn;    // [S] how many
     uint32_t S;
     uint32_t offline;    // peers offline per 10,000 (swarm_offline)
 };
@@ -328,13 +330,17 @@ __global__ void search_query_kernel(SwarmDev W, SearchDev X) {
     X.rn[g] = (uint8_t)m;
 }
 
-// Search::insertNode of node r (not expired) at top-64 distance rd (dht.cpp:961-1047, expired search = false):
+constexpr uint32_t XO_CAP = 64;  // silent peers remembered per lookup (4 per hop; beyond it: counted in overflow)
+
+// Search::insertNode of node r at top-64 distance rd (dht.cpp:961-1047, expired search = false); rbad: r's node
+// is expired (a peer this search queried and that stayed silent), so it joins the list as a bad node
+// (`if (node.isExpired()) bad++`, dht.cpp:1023-1025):
 // its place is after every closer entry; if the list already holds SEARCH_NODES non-bad nodes it is first cut
 // after the last prefix with SEARCH_NODES non-bad nodes (an insert beyond that point is refused), then
 // trimmed from the end while it holds more than SEARCH_NODES non-bad nodes. Static indices only.
 __device__ __forceinline__ void search_insert(const SwarmDev& W, const Tgt& t, uint32_t (&li)[LST], uint64_t (&ld)[LST],
                                               uint8_t (&q)[LST], uint8_t (&bd)[LST], uint32_t& n, uint32_t r,
-                                              uint64_t rd, bool& ovf) {
+                                              uint64_t rd, bool rbad, bool& ovf) {
     bool found = false;
     uint32_t pos = 0, bad = 0;
 #pragma unroll
@@ -372,9 +378,10 @@ __device__ __forceinline__ void search_insert(const SwarmDev& W, const Tgt& t, u
     }
 #pragma unroll
     for (uint32_t k = 0; k < LST; k++) {
-        if (k == pos) { li[k] = r; ld[k] = rd; q[k] = 0; bd[k] = 0; }
+        if (k == pos) { li[k] = r; ld[k] = rd; q[k] = 0; bd[k] = rbad ? 1 : 0; }
     }
     n++;
+    bad += rbad ? 1u : 0u;
     // while more than SEARCH_NODES non-bad nodes: drop the last one
 #pragma unroll
     for (int k = (int)LST - 1; k >= 0; k--) {
@@ -405,22 +412,30 @@ __global__ void search_merge_kernel(SwarmDev W, SearchDev X) {
         }
         const uint32_t src = X.src[s];
         bool ovf = false;
+        const uint32_t* xo = X.xo + (size_t)s * XO_CAP;
+        uint32_t xn = X.xn[s];
         for (uint32_t a = 0; a < ALPHA; a++) {
             const uint32_t g = s * ALPHA + a;
             const uint32_t rn = X.rn[g];
             for (uint32_t j = 0; j < rn; j++) {
                 const uint32_t r = X.ri[(size_t)g * BK + j];
                 if (r == src) continue;  // deserializeNodes drops our own ID (network_engine.cpp:798-799)
-                search_insert(W, t, li, ld, q, bd, n, r, X.rk[(size_t)g * BK + j] ^ t.hi, ovf);
+                bool rbad = false;
+                if (swarm_offline(r, X.offline))
+                    for (uint32_t e = 0; e < xn && !rbad; e++) rbad = xo[e] == r;
+                search_insert(W, t, li, ld, q, bd, n, r, X.rk[(size_t)g * BK + j] ^ t.hi, rbad, ovf);
             }
         }
         for (uint32_t a = 0; a < ALPHA; a++) {  // the silent ones: expired after their tries -> bad
             const uint32_t v = X.sel[(size_t)s * ALPHA + a];
             if (v == NONE || !swarm_offline(v, X.offline)) continue;
+            if (xn < XO_CAP) X.xo[(size_t)s * XO_CAP + xn++] = v;  // its node is expired from now on
+            else ovf = true;
 #pragma unroll
             for (uint32_t k = 0; k < LST; k++)
                 if (k < n && li[k] == v) bd[k] = 1;
         }
+        X.xn[s] = (uint8_t)xn;
         X.hops[s] += 1;
         // Search::isSynced: the first TARGET_NODES non-bad nodes answered; consecutive bad nodes from the front
         uint32_t good = 0, cb = 0;
@@ -619,7 +634,8 @@ int kad_search_create(kad_search** out, const kad_swarm* s, uint32_t S, const ui
         (rc = alloc(&X.hops, S, x->owned)) || (rc = alloc(&X.done, S, x->owned)) ||
         (rc = alloc(&X.sel, (size_t)S * ALPHA, x->owned)) || (rc = alloc(&X.ri, (size_t)S * ALPHA * BK, x->owned)) ||
         (rc = alloc(&X.rk, (size_t)S * ALPHA * BK, x->owned)) || (rc = alloc(&X.rn, (size_t)S * ALPHA, x->owned)) ||
-        (rc = alloc(&X.active, 1, x->owned))) {
+        (rc = alloc(&X.active, 1, x->owned)) || (rc = alloc(&X.xo, (size_t)S * XO_CAP, x->owned)) ||
+        (rc = alloc(&X.xn, S, x->owned))) {
         delete x;
         return rc;
     }
@@ -630,7 +646,8 @@ int kad_search_create(kad_search** out, const kad_swarm* s, uint32_t S, const ui
     }
     X.src = dsrc;
     X.targets = dt;
-    if (hipMemsetAsync(X.overflow, 0, 4, x->stream) != hipSuccess) {
+    if (hipMemsetAsync(X.overflow, 0, 4, x->stream) != hipSuccess ||
+        hipMemsetAsync(X.xn, 0, std::max<uint32_t>(S, 1), x->stream) != hipSuccess) {
         delete x;
         return err(KAD_ERR_HIP, "search init failed");
     }

@@ -93,8 +93,8 @@ class Search:
         return max_hops
 
     def get(self, full: bool = False):
-        """(list, queried, n, hops, done) with lists cut to SEARCH_NODES entries; full=True: (list, queried,
-        bad, n, hops, done, overflow) with the KAD_SEARCH_LIST-wide lists."""
+        """(list, queried, n, hops, done) with lists cut to SEARCH_NODES entries (n clamped to them); full=True:
+        (list, queried, bad, n, hops, done, overflow) with the KAD_SEARCH_LIST-wide lists."""
         S = self.S
         lst = np.empty((S, SEARCH_LIST), np.uint32)
         q = np.empty((S, SEARCH_LIST), np.uint8)
@@ -107,7 +107,9 @@ class Search:
               "kad_search_get")
         if full:
             return lst, q, bad, n, hops, done, ovf.value
-        return lst[:, :SEARCH_NODES].copy(), q[:, :SEARCH_NODES].copy(), n, hops, done
+        # the truncated view: n clamped to the columns returned (with offline peers a list also holds bad nodes and
+        # can be longer than SEARCH_NODES; full=True returns it whole)
+        return lst[:, :SEARCH_NODES].copy(), q[:, :SEARCH_NODES].copy(), np.minimum(n, SEARCH_NODES), hops, done
 
     def close(self):
         if getattr(self, "_h", None):

@@ -11,7 +11,7 @@ import ctypes as C
 import numpy as np
 
 from . import _lib
-from ._lib import KAD_TABLE_SORTED, check, lib, ptr
+from ._lib import KAD_TABLE_EAGER, KAD_TABLE_SORTED, check, lib, ptr
 
 
 def _as_ids(a) -> np.ndarray:
@@ -39,10 +39,11 @@ class DeviceTable:
     bucket_first   (B, 20) uint8 ascending, or None for a NodeCache-only table
     bucket_offset  (B+1,) uint32
     sorted         ids strictly ascending (enables NodeCache queries)
+    eager          build every line set now (default: the count <= 8 lines; the others on first use)
     """
 
     def __init__(self, ids, status, bucket_first=None, bucket_offset=None, *, device: int = 0,
-                 index_base: int = 0, sorted: bool = False):
+                 index_base: int = 0, sorted: bool = False, eager: bool = False):
         L = lib()
         ids = _as_ids(ids)
         status = np.ascontiguousarray(status, dtype=np.uint8)
@@ -60,7 +61,7 @@ class DeviceTable:
         h = C.c_void_p()
         rc = L.kad_table_create(C.byref(h), device, n, ptr(ids), ptr(status), B,
                                 ptr(bucket_first) if B else None, ptr(bucket_offset) if B else None,
-                                index_base, KAD_TABLE_SORTED if sorted else 0)
+                                index_base, (KAD_TABLE_SORTED if sorted else 0) | (KAD_TABLE_EAGER if eager else 0))
         check(rc, "kad_table_create")
         self._h = h
         self.device = device
@@ -92,7 +93,18 @@ class DeviceTable:
     def info(self) -> dict:
         inf = _lib.table_info()
         check(lib().kad_table_get_info(self._h, C.byref(inf)), "kad_table_get_info")
-        return {f: getattr(inf, f) for f, _ in inf._fields_}
+        out = {f: getattr(inf, f) for f, _ in inf._fields_}
+        built = C.c_uint32()
+        nb = (C.c_uint64 * 4)()
+        ms = (C.c_float * 4)()
+        check(lib().kad_table_line_sets(self._h, C.byref(built), nb, ms), "kad_table_line_sets")
+        out["line_sets"] = {name: {"built": bool(built.value & (1 << k)), "bytes": int(nb[k]), "build_ms": float(ms[k])}
+                            for k, name in enumerate(("rt16", "rt32", "nc16", "nc32"))}
+        return out
+
+    def prepare(self, sets: int = _lib.KAD_LINES_ALL) -> None:
+        """Build the line sets `sets` (KAD_LINES_*) now instead of on first use (e.g. before a graph capture)."""
+        check(lib().kad_table_prepare(self._h, sets), "kad_table_prepare")
 
     # -- status --------------------------------------------------------------------------
     def update_status(self, status) -> None:

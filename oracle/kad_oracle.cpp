@@ -762,7 +762,10 @@ int orc_swarm_search_ex(void* h, uint32_t S, const uint32_t* src, const uint8_t*
         uint32_t hops = 0;
         uint8_t done = 0;
         auto id_of = [&](uint32_t v) { return Id(s->ids + (size_t)HASH_LEN * v); };
-        // Search::insertNode(node) for a node that is not expired (dht.cpp:961-1047, expired search = false)
+        // the peers this search queried that stayed silent: their nodes are expired from then on
+        std::vector<uint32_t> silent;
+        // Search::insertNode(node) (dht.cpp:961-1047, expired search = false); an expired node joins as a bad
+        // search node (`if (node.isExpired()) bad++`, :1023-1025)
         auto insert = [&](uint32_t r) {
             const Id rid = id_of(r);
             size_t n = L.size();
@@ -785,7 +788,9 @@ int orc_swarm_search_ex(void* h, uint32_t S, const uint32_t* src, const uint8_t*
                 if (tt != L.size()) L.resize(tt);
                 if (n >= tt) return;
             }
-            L.insert(L.begin() + n, SN{r, 0, 0});
+            const bool rbad = std::find(silent.begin(), silent.end(), r) != silent.end();
+            L.insert(L.begin() + n, SN{r, 0, (uint8_t)(rbad ? 1 : 0)});
+            bad += rbad ? 1 : 0;
             while (L.size() - bad > SW_SEARCH) {
                 if (L.back().bad) bad--;
                 L.pop_back();
@@ -809,9 +814,11 @@ int orc_swarm_search_ex(void* h, uint32_t S, const uint32_t* src, const uint8_t*
                     if (r != src[i]) insert(r);  // deserializeNodes drops our own ID (network_engine.cpp:798-799)
             }
             for (uint32_t v : sel)  // the silent ones: expired after their tries, bad search nodes
-                if (swarm_offline(v, offline_per_10k))
+                if (swarm_offline(v, offline_per_10k)) {
+                    silent.push_back(v);
                     for (SN& x : L)
                         if (x.idx == v) x.bad = 1;
+                }
             uint32_t good = 0;  // Search::isSynced
             bool synced = true;
             for (const SN& x : L) {

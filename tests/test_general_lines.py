@@ -70,7 +70,7 @@ def _s_tables():
 
 @pytest.mark.parametrize("t", _s_tables(), ids=lambda t: t["name"])
 def test_general_lines_parity(gpu, t, monkeypatch):
-    with DeviceTable(t["ids"], t["status"], t["first"], t["off"], device=0) as T:
+    with DeviceTable(t["ids"], t["status"], t["first"], t["off"], device=0, eager=True) as T:
         f = T.info()["flags"]
         assert not (f & KAD_INFO_WINDOW_LINES)
         if not t.get("lane"):
@@ -101,6 +101,7 @@ def test_uniform_table_switches_to_general_lines_after_split(gpu):
         assert T.info()["flags"] & KAD_INFO_WINDOW_LINES
         T.apply(np.array([[KAD_OP_SPLIT, 100, 0], [KAD_OP_SPLIT, 7, 0]], np.uint32))
         ids, st, first, off = T.export()
+        T.prepare()  # the count 9..32 sets of the new shape (otherwise built by their first query)
         f = T.info()["flags"]
         assert not (f & KAD_INFO_WINDOW_LINES) and f & KAD_INFO_GENERAL_LINES and f & KAD_INFO_SLOT_LINES, hex(f)
         assert f & KAD_INFO_GENERAL_LINES16 and f & KAD_INFO_SLOT_LINES16, hex(f)
@@ -118,8 +119,8 @@ def test_dual_family_general_lines(gpu):
     targets = np.ascontiguousarray(np.concatenate([TB.adversarial_targets(t4, extra=3000),
                                                    TB.adversarial_targets(t6, extra=3000)]))
     af = rng.integers(0, 2, targets.shape[0]).astype(np.uint8)
-    with DeviceTable(t4["ids"], t4["status"], t4["first"], t4["off"], device=0) as T4, \
-            DeviceTable(t6["ids"], t6["status"], t6["first"], t6["off"], device=0) as T6:
+    with DeviceTable(t4["ids"], t4["status"], t4["first"], t4["off"], device=0, eager=True) as T4, \
+            DeviceTable(t6["ids"], t6["status"], t6["first"], t6["off"], device=0, eager=True) as T6:
         for T in (T4, T6):
             f = T.info()["flags"]
             assert f & KAD_INFO_GENERAL_LINES and f & KAD_INFO_GENERAL_LINES16 and f & KAD_INFO_GENERAL_LINES32, hex(f)
@@ -146,7 +147,7 @@ def test_general_lines_full_size_split_table(gpu):
     targets = tg.cpu().numpy()
     key = t["ids"][:, :8].copy().view(">u8").reshape(-1)
     th = targets[:, :8].copy().view(">u8").reshape(-1)
-    with DeviceTable(t["ids"], t["status"], t["first"], t["off"], device=0) as T:
+    with DeviceTable(t["ids"], t["status"], t["first"], t["off"], device=0, eager=True) as T:
         f = T.info()["flags"]
         assert f & KAD_INFO_SLOT_LINES and f & KAD_INFO_SLOT_LINES16 and f & KAD_INFO_GENERAL_LINES32, hex(f)
         for k in (8, 14, 16, 32):

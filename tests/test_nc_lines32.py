@@ -18,7 +18,7 @@ COUNTS = (17, 20, 24, 31, 32)
 
 def _check(t, gpu, targets, monkeypatch, counts=COUNTS):
     tg = torch.from_numpy(np.ascontiguousarray(targets)).to(gpu)
-    with DeviceTable(t["ids"], t["status"], t["first"], t["off"], device=gpu.index or 0, sorted=True) as T:
+    with DeviceTable(t["ids"], t["status"], t["first"], t["off"], device=gpu.index or 0, sorted=True, eager=True) as T:
         assert T.info()["flags"] & KAD_INFO_NODECACHE_LINES32
         for k in counts:
             idx, cnt = T.nc_closest(tg, k)

@@ -171,7 +171,9 @@ def _check_lookup_properties(ids, lst, q, bad, n, done, offline_per_10k, tg):
         assert (d[1:] >= d[:-1]).all()
         b = bad[i, :m].astype(bool)
         assert (~b).sum() <= SEARCH_NODES
-        assert (peer_off[li[b]]).all() and q[i, :m][b].all()  # bad = an offline peer that was queried
+        # bad = an offline peer this search queried: still flagged queried, or answered back into the list by
+        # another peer after it was trimmed (a new search node of an expired node, dht.cpp:1023-1025)
+        assert (peer_off[li[b]]).all()
         assert not (peer_off[li] & q[i, :m].astype(bool) & ~b).any()  # every queried offline peer turned bad
         if done[i] == 1:
             nb = np.flatnonzero(~b)[:8]
@@ -235,6 +237,9 @@ def test_swarm_gpu_offline_hop_by_hop(gpu, off):
             if active == 0:
                 break
         assert active == 0
+        # a silent peer trimmed from a list and answered back into it by another peer joins as a bad node
+        # (Search::insertNode counts an expired node as bad, dht.cpp:1023-1025): the branch is exercised
+        assert ((got[2] == 1) & (got[1] == 0)).any()
         X.close()
     M.close()
 
