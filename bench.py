@@ -591,6 +591,19 @@ def latency_pass(dev, nodes=170, reps=2000):
                 check(lib().kad_rt_closest_batch_host(T.handle, ptr(x), q, 8, ptr(oi), ptr(oc)), "host batch")
                 ts.append(time.perf_counter() - t0)
             res[f"gpu_call_q{q}_us"] = float(np.median(ts)) * 1e6
+        # the resident query service (kad_table_serve): no launch, no stream synchronise per call
+        T.serve(100_000)
+        for q in (1, 64):
+            oi, oc = np.zeros((q, 8), np.uint32), np.zeros((q,), np.uint8)
+            ts = []
+            for r in range(reps):
+                x = np.ascontiguousarray(tg[(r * q) % (4096 - q):(r * q) % (4096 - q) + q])
+                t0 = time.perf_counter()
+                check(lib().kad_rt_closest_batch_host(T.handle, ptr(x), q, 8, ptr(oi), ptr(oc)), "served batch")
+                ts.append(time.perf_counter() - t0)
+            res[f"serve_q{q}_us"] = float(np.median(ts)) * 1e6
+            res[f"serve_q{q}_p99_us"] = float(np.percentile(ts, 99)) * 1e6
+        T.serve(0)
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
 
@@ -605,6 +618,8 @@ def latency_pass(dev, nodes=170, reps=2000):
     res["cpu_port_call_us"] = float(np.median(ts)) * 1e6
     res["how"] = (f"median of {reps} synchronous calls, k=8, host buffers in and out (ctypes overhead included); "
                   "gpu: one kernel launch reading the targets from and writing the rows to mapped pinned memory; "
+                  "serve: the resident query service (kad_table_serve, 100 ms idle), a request posted to and answered "
+                  "from mapped pinned memory by a workgroup that stays on the GPU; "
                   "cpu_port: the std::list restatement of routing_table.cpp:67-135 on one thread, same table")
     return res
 

@@ -231,6 +231,31 @@ int kad_rt_closest_batch(const kad_table* t, const uint8_t* targets, uint32_t q,
 int kad_rt_closest_batch_host(const kad_table* t, const uint8_t* targets, uint32_t q, uint32_t count,
                               uint32_t* out_idx, uint8_t* out_cnt);
 
+/* Resident query service for single requests (the per-request calls of dht.cpp:3196-3217, 1650): with
+ * idle_us > 0 one workgroup stays on the GPU and answers host batches of up to KAD_SERVE_MAX_Q queries with
+ * count <= KAD_SERVE_MAX_COUNT (kad_rt_closest_batch_host, kad_nc_closest_batch_host) from a mailbox in
+ * pinned host memory: no kernel launch and no stream synchronise per call. Same results, same ordering
+ * (after the table's last asynchronous status refresh). A launch ends by itself after idle_us without a
+ * request or after one second in all, and the next request launches it again. Calls that change or free
+ * what it reads (patch/update_status, patch/set_times, apply, nc_apply, set_addrs, prepare, destroy) end it
+ * first. While it runs, device-wide synchronisation (hipDeviceSynchronize, torch.cuda.synchronize) waits for
+ * it to go idle. idle_us = 0 ends it and turns it off (the default). idle_us <= KAD_SERVE_MAX_IDLE_US. */
+#define KAD_SERVE_MAX_Q 64
+#define KAD_SERVE_MAX_COUNT 64
+#define KAD_SERVE_MAX_IDLE_US 1000000
+int kad_table_serve(kad_table* t, uint32_t idle_us);
+/* The service's counters: launches so far (the first request after an idle exit launches again), requests
+ * answered, and for the last request the header reads it took to be seen and the device time from seen to
+ * its rows fenced (the rest of a call's latency is the PCIe round trip and the host). */
+typedef struct kad_serve_stats {
+    uint32_t idle_us;
+    uint32_t last_polls;
+    uint64_t launches;
+    uint64_t requests;
+    uint64_t last_busy_ns;
+} kad_serve_stats;
+int kad_table_serve_stats(const kad_table* t, kad_serve_stats* out);
+
 /* Batched RoutingTable::findBucket (routing_table.cpp:113-135): bucket index per
  * target (0 for targets below the first bucket, as the reference's list walk). */
 int kad_rt_find_bucket_batch(const kad_table* t, const uint8_t* targets, uint32_t q,

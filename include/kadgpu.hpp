@@ -91,6 +91,9 @@ public:
     kad_table* get() const { return t_; }
     explicit operator bool() const { return t_ != nullptr; }
 
+    /* Resident query service for single requests (kad_table_serve); idle_us = 0 turns it off. */
+    void serve(uint32_t idle_us) { check(kad_table_serve(t_, idle_us), "kad_table_serve"); }
+
     /* Host-buffer batch queries (synchronous). Rows of `count` indices, KAD_NO_NODE padded. */
     void findClosestNodesBatch(const uint8_t* targets, size_t q, size_t count, std::vector<uint32_t>& idx,
                                std::vector<uint8_t>& cnt) const {

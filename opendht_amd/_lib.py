@@ -29,6 +29,7 @@ KAD_INFO_SLOT_LINES16 = 0x8000
 KAD_INFO_SHORT_LINES = 0x800
 KAD_INFO_NODECACHE_LINES32 = 0x1000
 KAD_INFO_SLOT_LINES = 0x2000
+KAD_SERVE_MAX_Q, KAD_SERVE_MAX_COUNT, KAD_SERVE_MAX_IDLE_US = 64, 64, 1000000
 KAD_OP_REMOVE, KAD_OP_REPLACE, KAD_OP_INSERT, KAD_OP_SPLIT = 1, 2, 3, 4
 
 
@@ -90,6 +91,8 @@ SIGNATURES = {
     "kad_table_patch_times": (C.c_int, [_P, C.c_uint32, _P, _P, _P, _P]),
     "kad_rt_closest_batch": (C.c_int, [_P, _P, C.c_uint32, C.c_uint32, _P, _P, _P]),
     "kad_rt_closest_batch_host": (C.c_int, [_P, _P, C.c_uint32, C.c_uint32, _P, _P]),
+    "kad_table_serve": (C.c_int, [_P, C.c_uint32]),
+    "kad_table_serve_stats": (C.c_int, [_P, _P]),
     "kad_rt_find_bucket_batch": (C.c_int, [_P, _P, C.c_uint32, _P, _P]),
     "kad_nc_closest_batch": (C.c_int, [_P, _P, C.c_uint32, C.c_uint32, _P, _P, _P]),
     "kad_nc_closest_batch_host": (C.c_int, [_P, _P, C.c_uint32, C.c_uint32, _P, _P]),
@@ -142,6 +145,13 @@ class table_info(C.Structure):
         ("n_nodes", C.c_uint32), ("n_buckets", C.c_uint32), ("index_base", C.c_uint32),
         ("flags", C.c_uint32), ("device", C.c_int32), ("rt_radix_bits", C.c_uint32),
         ("nc_radix_bits", C.c_uint32), ("n_good", C.c_uint32), ("device_bytes", C.c_uint64),
+    ]
+
+
+class serve_stats(C.Structure):
+    _fields_ = [
+        ("idle_us", C.c_uint32), ("last_polls", C.c_uint32), ("launches", C.c_uint64), ("requests", C.c_uint64),
+        ("last_busy_ns", C.c_uint64),
     ]
 
 

@@ -640,7 +640,7 @@ __device__ __forceinline__ void exact_tail(const DevTable& T, const Target& t, b
 
 // Lane-per-query RoutingTable kernel (any table shape, count <= 32).
 template <int K>
-__global__ __launch_bounds__(BLOCK) void rt_closest_kernel(DevTable T, const uint8_t* __restrict__ targets,
+__device__ __forceinline__ void rt_closest_kernel_body(const DevTable& T, const uint8_t* __restrict__ targets,
                                                            uint32_t q, uint32_t count,
                                                            uint32_t* __restrict__ out_idx,
                                                            uint8_t* __restrict__ out_cnt) {
@@ -653,6 +653,13 @@ __global__ __launch_bounds__(BLOCK) void rt_closest_kernel(DevTable T, const uin
     }
     __shared__ uint64_t xs[BLOCK / 64][192];
     exact_tail(T, t, ex, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
+}
+template <int K>
+__global__ __launch_bounds__(BLOCK) void rt_closest_kernel(DevTable T, const uint8_t* __restrict__ targets,
+                                                           uint32_t q, uint32_t count,
+                                                           uint32_t* __restrict__ out_idx,
+                                                           uint8_t* __restrict__ out_cnt) {
+    rt_closest_kernel_body<K>(T, targets, q, count, out_idx, out_cnt);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -880,7 +887,7 @@ __device__ __forceinline__ void store_row8(uint32_t* row, const uint32_t (&o)[8]
 
 // ABL 1 = no exact path, 2 = also no ranking (timing ablations only).
 template <int ABL>
-__global__ __launch_bounds__(BLOCK) void rt_wl_kernel(DevTable T, const uint8_t* __restrict__ targets, uint32_t q,
+__device__ __forceinline__ void rt_wl_kernel_body(const DevTable& T, const uint8_t* __restrict__ targets, uint32_t q,
                                                       uint32_t count, uint32_t* __restrict__ out_idx,
                                                       uint8_t* __restrict__ out_cnt) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
@@ -900,6 +907,12 @@ __global__ __launch_bounds__(BLOCK) void rt_wl_kernel(DevTable T, const uint8_t*
     }
     __shared__ uint64_t xs[BLOCK / 64][192];
     if (ABL == 0) exact_tail(T, t, act && !ok, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
+}
+template <int ABL>
+__global__ __launch_bounds__(BLOCK) void rt_wl_kernel(DevTable T, const uint8_t* __restrict__ targets, uint32_t q,
+                                                      uint32_t count, uint32_t* __restrict__ out_idx,
+                                                      uint8_t* __restrict__ out_cnt) {
+    rt_wl_kernel_body<ABL>(T, targets, q, count, out_idx, out_cnt);
 }
 
 // The good nodes of bucket x in index order: fn(node index, key). Buckets of <= 32 nodes take their good
@@ -1184,7 +1197,7 @@ __device__ __forceinline__ bool ws_answer(const DevTable& T, const Target& t, ui
 // only); 4 = path statistics: out_cnt = 100 + m for queries answered by the 128-byte line, 250 for the exact path;
 // 5 = the exact path compiled in but never taken.
 template <int ABL>
-__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) void rt_ws_kernel(DevTable T, const uint8_t* __restrict__ targets, uint32_t q,
+__device__ __forceinline__ void rt_ws_kernel_body(const DevTable& T, const uint8_t* __restrict__ targets, uint32_t q,
                                                       uint32_t count, uint32_t* __restrict__ out_idx,
                                                       uint8_t* __restrict__ out_cnt) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
@@ -1222,6 +1235,12 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) v
         }
         if (ABL == 4 && need && out_cnt) out_cnt[i] = 250;
     }
+}
+template <int ABL>
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) void rt_ws_kernel(DevTable T, const uint8_t* __restrict__ targets, uint32_t q,
+                                                      uint32_t count, uint32_t* __restrict__ out_idx,
+                                                      uint8_t* __restrict__ out_cnt) {
+    rt_ws_kernel_body<ABL>(T, targets, q, count, out_idx, out_cnt);
 }
 
 // The count <= 8 line answer for kernels that serve other paths too (dual-family, shard): lanes with `ws`
@@ -1405,7 +1424,7 @@ __device__ bool wave_wl32(const DevTable& T, const Target& t, uint32_t b, uint32
 
 // ABL 1 = no exact path (timing ablation only, KAD_RT_KERNEL=wl16_abl1; deferred rows are left unwritten).
 template <int ABL>
-__global__ __launch_bounds__(BLOCK) void rt_wl16_kernel(DevTable T, const uint8_t* __restrict__ targets, uint32_t q,
+__device__ __forceinline__ void rt_wl16_kernel_body(const DevTable& T, const uint8_t* __restrict__ targets, uint32_t q,
                                                         uint32_t count, uint32_t* __restrict__ out_idx,
                                                         uint8_t* __restrict__ out_cnt) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
@@ -1442,6 +1461,12 @@ __global__ __launch_bounds__(BLOCK) void rt_wl16_kernel(DevTable T, const uint8_
     }
     __shared__ uint64_t xs[BLOCK / 64][192];
     exact_tail(T, t, need, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
+}
+template <int ABL>
+__global__ __launch_bounds__(BLOCK) void rt_wl16_kernel(DevTable T, const uint8_t* __restrict__ targets, uint32_t q,
+                                                        uint32_t count, uint32_t* __restrict__ out_idx,
+                                                        uint8_t* __restrict__ out_cnt) {
+    rt_wl16_kernel_body<ABL>(T, targets, q, count, out_idx, out_cnt);
 }
 
 // Window lines for counts 9..16 after a status change (or at creation): one thread per bucket.
@@ -1683,7 +1708,7 @@ __device__ __forceinline__ void store_row32(uint32_t* row, const uint32_t (&o)[3
     }
 }
 
-__global__ __launch_bounds__(BLOCK) void rt_wl32_kernel(DevTable T, const uint8_t* __restrict__ targets, uint32_t q,
+__device__ __forceinline__ void rt_wl32_kernel_body(const DevTable& T, const uint8_t* __restrict__ targets, uint32_t q,
                                                         uint32_t count, uint32_t* __restrict__ out_idx,
                                                         uint8_t* __restrict__ out_cnt) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
@@ -1700,6 +1725,11 @@ __global__ __launch_bounds__(BLOCK) void rt_wl32_kernel(DevTable T, const uint8_
     store_rows_block<32>(out_idx, q, count, o, act && ok);
     __shared__ uint64_t xs[BLOCK / 64][192];
     exact_tail(T, t, act && !ok, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
+}
+__global__ __launch_bounds__(BLOCK) void rt_wl32_kernel(DevTable T, const uint8_t* __restrict__ targets, uint32_t q,
+                                                        uint32_t count, uint32_t* __restrict__ out_idx,
+                                                        uint8_t* __restrict__ out_cnt) {
+    rt_wl32_kernel_body(T, targets, q, count, out_idx, out_cnt);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -2003,7 +2033,7 @@ __device__ __forceinline__ bool gl_answer(const DevTable& T, const Target& t, ui
     return !ex;
 }
 
-__global__ __launch_bounds__(BLOCK) void rt_gl_kernel(DevTable T, const uint8_t* __restrict__ targets, uint32_t q,
+__device__ __forceinline__ void rt_gl_kernel_body(const DevTable& T, const uint8_t* __restrict__ targets, uint32_t q,
                                                       uint32_t count, uint32_t* __restrict__ out_idx,
                                                       uint8_t* __restrict__ out_cnt) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
@@ -2023,6 +2053,11 @@ __global__ __launch_bounds__(BLOCK) void rt_gl_kernel(DevTable T, const uint8_t*
     }
     __shared__ uint64_t xs[BLOCK / 64][192];
     exact_tail(T, t, act && !ok, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
+}
+__global__ __launch_bounds__(BLOCK) void rt_gl_kernel(DevTable T, const uint8_t* __restrict__ targets, uint32_t q,
+                                                      uint32_t count, uint32_t* __restrict__ out_idx,
+                                                      uint8_t* __restrict__ out_cnt) {
+    rt_gl_kernel_body(T, targets, q, count, out_idx, out_cnt);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -2169,8 +2204,8 @@ __device__ __forceinline__ bool sl_answer(const DevTable& T, uint64_t thi, uint3
 // count <= 8 on a general table with slot lines: the slot line, else locate + the 128-byte line, else exact.
 // ABL 1 (timing ablation only, results wrong): slot lines only.
 template <int ABL>
-__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) void rt_sl_kernel(
-    DevTable T, const uint8_t* __restrict__ targets, uint32_t q, uint32_t count, uint32_t* __restrict__ out_idx,
+__device__ __forceinline__ void rt_sl_kernel_body(
+    const DevTable& T, const uint8_t* __restrict__ targets, uint32_t q, uint32_t count, uint32_t* __restrict__ out_idx,
     uint8_t* __restrict__ out_cnt) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     const bool act = i < q && count > 0;
@@ -2201,6 +2236,12 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) v
         __shared__ uint64_t xs[BLOCK / 64][192];
         exact_tail(T, t, need, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
     }
+}
+template <int ABL>
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) void rt_sl_kernel(
+    DevTable T, const uint8_t* __restrict__ targets, uint32_t q, uint32_t count, uint32_t* __restrict__ out_idx,
+    uint8_t* __restrict__ out_cnt) {
+    rt_sl_kernel_body<ABL>(T, targets, q, count, out_idx, out_cnt);
 }
 
 // Fallback slot lines (dw1 == NONE) and those without a bucket (dw0 == NONE): cnt[0], cnt[1] (KAD_DEBUG).
@@ -2270,7 +2311,7 @@ __device__ __forceinline__ bool gl32_answer(const DevTable& T, const Target& t, 
     return !ex;
 }
 
-__global__ __launch_bounds__(BLOCK) void rt_gl32_kernel(DevTable T, const uint8_t* __restrict__ targets, uint32_t q,
+__device__ __forceinline__ void rt_gl32_kernel_body(const DevTable& T, const uint8_t* __restrict__ targets, uint32_t q,
                                                         uint32_t count, uint32_t* __restrict__ out_idx,
                                                         uint8_t* __restrict__ out_cnt) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
@@ -2287,6 +2328,11 @@ __global__ __launch_bounds__(BLOCK) void rt_gl32_kernel(DevTable T, const uint8_
     store_rows_block<32>(out_idx, q, count, o, act && ok);
     __shared__ uint64_t xs[BLOCK / 64][192];
     exact_tail(T, t, act && !ok, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
+}
+__global__ __launch_bounds__(BLOCK) void rt_gl32_kernel(DevTable T, const uint8_t* __restrict__ targets, uint32_t q,
+                                                        uint32_t count, uint32_t* __restrict__ out_idx,
+                                                        uint8_t* __restrict__ out_cnt) {
+    rt_gl32_kernel_body(T, targets, q, count, out_idx, out_cnt);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -2352,7 +2398,7 @@ __device__ __forceinline__ bool gl16_answer(const DevTable& T, const Target& t, 
     return ok;
 }
 
-__global__ __launch_bounds__(BLOCK) void rt_gl16_kernel(DevTable T, const uint8_t* __restrict__ targets, uint32_t q,
+__device__ __forceinline__ void rt_gl16_kernel_body(const DevTable& T, const uint8_t* __restrict__ targets, uint32_t q,
                                                         uint32_t count, uint32_t* __restrict__ out_idx,
                                                         uint8_t* __restrict__ out_cnt) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
@@ -2369,6 +2415,11 @@ __global__ __launch_bounds__(BLOCK) void rt_gl16_kernel(DevTable T, const uint8_
     store_rows_block<16>(out_idx, q, count, o, act && ok);
     __shared__ uint64_t xs[BLOCK / 64][192];
     exact_tail(T, t, act && !ok, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
+}
+__global__ __launch_bounds__(BLOCK) void rt_gl16_kernel(DevTable T, const uint8_t* __restrict__ targets, uint32_t q,
+                                                        uint32_t count, uint32_t* __restrict__ out_idx,
+                                                        uint8_t* __restrict__ out_cnt) {
+    rt_gl16_kernel_body(T, targets, q, count, out_idx, out_cnt);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -2418,7 +2469,7 @@ __global__ __launch_bounds__(BLOCK) void sl16_build_kernel(const uint32_t* __res
     }
 }
 
-__global__ __launch_bounds__(BLOCK) void rt_sl16_kernel(DevTable T, const uint8_t* __restrict__ targets, uint32_t q,
+__device__ __forceinline__ void rt_sl16_kernel_body(const DevTable& T, const uint8_t* __restrict__ targets, uint32_t q,
                                                         uint32_t count, uint32_t* __restrict__ out_idx,
                                                         uint8_t* __restrict__ out_cnt) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
@@ -2456,6 +2507,11 @@ __global__ __launch_bounds__(BLOCK) void rt_sl16_kernel(DevTable T, const uint8_
     store_rows_block<16>(out_idx, q, count, o, act && ok);
     __shared__ uint64_t xs[BLOCK / 64][192];
     exact_tail(T, t, act && !ok, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
+}
+__global__ __launch_bounds__(BLOCK) void rt_sl16_kernel(DevTable T, const uint8_t* __restrict__ targets, uint32_t q,
+                                                        uint32_t count, uint32_t* __restrict__ out_idx,
+                                                        uint8_t* __restrict__ out_cnt) {
+    rt_sl16_kernel_body(T, targets, q, count, out_idx, out_cnt);
 }
 
 // One general window line of bucket b into L (LDS, W dwords, slots from HDR): see the layout above.
@@ -3919,7 +3975,7 @@ __device__ __forceinline__ void store_rows_wave16(uint32_t* __restrict__ out_idx
 // translations (tools/nc_abl.py). The wave loads its 64 lines in two halves of 128 bytes, eight lanes per line
 // (one translation per line per instruction), and hands each lane its line through LDS.
 template <int ABL, bool DUAL>
-__global__ __launch_bounds__(BLOCK) void nc_line_kernel(DevTable T4, DevTable T6, const uint8_t* __restrict__ af,
+__device__ __forceinline__ void nc_line_kernel_body(const DevTable& T4, const DevTable& T6, const uint8_t* __restrict__ af,
                                                         const uint8_t* __restrict__ targets, uint32_t q,
                                                         uint32_t count, uint32_t* __restrict__ out_idx,
                                                         uint8_t* __restrict__ out_cnt) {
@@ -4006,6 +4062,13 @@ __global__ __launch_bounds__(BLOCK) void nc_line_kernel(DevTable T4, DevTable T6
         const NcWindow w = nc_window(T, r0, lane);
         nc_answer(T, u, r0, r1, w, lane, i - lane + l, count, out_idx, out_cnt);
     }
+}
+template <int ABL, bool DUAL>
+__global__ __launch_bounds__(BLOCK) void nc_line_kernel(DevTable T4, DevTable T6, const uint8_t* __restrict__ af,
+                                                        const uint8_t* __restrict__ targets, uint32_t q,
+                                                        uint32_t count, uint32_t* __restrict__ out_idx,
+                                                        uint8_t* __restrict__ out_cnt) {
+    nc_line_kernel_body<ABL, DUAL>(T4, T6, af, targets, q, count, out_idx, out_cnt);
 }
 
 // NodeCache counts 17..64 for two families (af per query): nc_two_pass_kernel with the table chosen per
@@ -4890,6 +4953,138 @@ std::vector<uint32_t> build_radix(const Radix& r, uint32_t m, const uint8_t* ite
     return rdx;
 }
 
+// ---------------------------------------------------------------------------------------
+// Resident query service (kad_table_serve): single Dht requests without a kernel launch. One workgroup of
+// BLOCK threads stays on the GPU and polls a mailbox in pinned host memory. The request header and the first
+// target share one 64-byte line, which wave 0 reads with one 16-lane load per poll; the host writes the
+// targets, then `seq2`, then `seq`, and a header read with seq == seq2 is whole. The workgroup then runs the
+// same kernel body the launch path would run for the table's line sets (the bodies index queries from
+// blockIdx.x = 0, so a request of up to SVC_Q <= BLOCK queries is one block of them), with the targets in LDS
+// and the rows and counts written straight into the pinned reply; counts above 32 and NodeCache queries
+// without lines take the wave paths. Every wave fences its rows to system scope before thread 0 publishes
+// the request number. A launch ends on its own: when the host sets `stop`, after `idle` ticks without a
+// request, or after `life` ticks in all (the host launches it again on the next request), so no wave
+// outlives its process.
+// ---------------------------------------------------------------------------------------
+constexpr uint32_t SVC_Q = 64, SVC_COUNT = 64;
+constexpr uint64_t KAD_SERVE_LIFE_MS = 1000;  // one launch's longest life
+static_assert(SVC_Q <= BLOCK, "a request is one block of queries");
+
+struct SvcMail {             // host writes, the service reads (system-scope loads)
+    uint32_t seq;            // dw0: request number, written last
+    uint32_t stop;           // dw1: nonzero: leave
+    uint32_t q, count, kind; // dw2-4: kind 0: RoutingTable::findClosestNodes, 1: NodeCache::getCachedNodes
+    uint32_t pad[2];
+    uint32_t seq2;           // dw7: the request number, written before seq (a torn header read shows seq != seq2)
+    uint32_t targets[SVC_Q * 5];  // from dw8: target 0 shares the header's 64-byte line
+};
+struct SvcReply {            // the service writes, the host reads
+    uint32_t done;           // the last request answered: written after the rows and counts
+    uint32_t polls;          // header reads before the last request was seen
+    uint64_t t_seen, t_done; // device wall clock: the last request seen, its rows fenced (tools/latency)
+    uint32_t pad[10];
+    uint8_t cnt[SVC_Q];
+    uint32_t idx[SVC_Q * SVC_COUNT];
+};
+
+__global__ __launch_bounds__(BLOCK) void svc_kernel(DevTable T, const SvcMail* __restrict__ mail,
+                                                     SvcReply* __restrict__ reply, uint32_t last, uint64_t idle,
+                                                     uint64_t life) {
+    __shared__ uint32_t req[4];  // go, q, count, kind
+    __shared__ uint32_t tg[SVC_Q * 5];
+    __shared__ uint64_t xs[BLOCK / 64][192];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
+    const uint32_t* mw = reinterpret_cast<const uint32_t*>(mail);
+    const uint64_t t0 = wall_clock64();
+    uint64_t heard = t0;
+    for (;;) {
+        if (w == 0) {  // wave 0 polls the header line (wave-uniform loop)
+            uint32_t v = 0, s = last, go = 0, polls = 0;
+            for (;;) {
+                polls++;
+                v = lane < 16 ? __hip_atomic_load(mw + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0u;
+                s = rdl(v, 0);
+                const uint32_t stop = rdl(v, 1), s2 = rdl(v, 7);
+                if (s != last && s == s2) { go = 1; break; }
+                const uint64_t now = wall_clock64();
+                if (stop || now - heard > idle || now - t0 > life) break;
+                __builtin_amdgcn_s_sleep(1);
+            }
+            if (lane == 0) {
+                reply->polls = polls;
+                reply->t_seen = wall_clock64();
+                req[0] = go;
+                req[1] = min(rdl(v, 2), SVC_Q);
+                req[2] = min(rdl(v, 3), SVC_COUNT);
+                req[3] = rdl(v, 4);
+            }
+            if (lane >= 8 && lane < 16) tg[lane - 8] = v;  // target 0 and the start of target 1
+            last = s;
+            heard = wall_clock64();
+        }
+        __syncthreads();
+        if (req[0] == 0) return;  // block-uniform: stop or timeout with nothing posted
+        // the other targets: system-scope loads issued after the header was seen (the host wrote them before seq)
+        const uint32_t q = req[1], count = req[2], kind = req[3];
+        for (uint32_t j = 8 + tid; j < 5 * q; j += BLOCK)  // the other targets (targets start at dw8)
+            tg[j] = __hip_atomic_load(&mail->targets[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __syncthreads();
+        const uint8_t* tq = reinterpret_cast<const uint8_t*>(tg);
+        uint32_t* idx = reply->idx;
+        uint8_t* cnt = reply->cnt;
+        // the launch path's kernel choice (launch_rt) for the line sets this table has: block-uniform branches
+        if (kind == 0 && count >= 1 && count <= 8) {
+            if (T.flags & TF_WS) rt_ws_kernel_body<0>(T, tq, q, count, idx, cnt);
+            else if (T.flags & TF_WL) rt_wl_kernel_body<0>(T, tq, q, count, idx, cnt);
+            else if (T.flags & TF_SL) rt_sl_kernel_body<0>(T, tq, q, count, idx, cnt);
+            else if (T.flags & TF_GL) rt_gl_kernel_body(T, tq, q, count, idx, cnt);
+            else rt_closest_kernel_body<8>(T, tq, q, count, idx, cnt);
+        } else if (kind == 0 && count >= 9 && count <= 16) {
+            if (T.flags & TF_WL16) rt_wl16_kernel_body<0>(T, tq, q, count, idx, cnt);
+            else if (T.flags & TF_SL16) rt_sl16_kernel_body(T, tq, q, count, idx, cnt);
+            else if (T.flags & TF_GL16) rt_gl16_kernel_body(T, tq, q, count, idx, cnt);
+            else if (T.flags & TF_GL32) rt_gl32_kernel_body(T, tq, q, count, idx, cnt);
+            else rt_closest_kernel_body<16>(T, tq, q, count, idx, cnt);
+        } else if (kind == 0 && count >= 17 && count <= 32) {
+            if (T.flags & TF_WL32) rt_wl32_kernel_body(T, tq, q, count, idx, cnt);
+            else if (T.flags & TF_GL32) rt_gl32_kernel_body(T, tq, q, count, idx, cnt);
+            else rt_closest_kernel_body<32>(T, tq, q, count, idx, cnt);
+        } else if (kind == 1 && count >= 1 && count <= 16 && (T.flags & TF_NCL)) {
+            nc_line_kernel_body<0, false>(T, T, nullptr, tq, q, count, idx, cnt);
+        } else {
+            // count 0, counts above 32, NodeCache without lines: one query per wave
+            for (uint32_t i = w; i < q; i += BLOCK / 64) {  // wave-uniform
+                const Target t = load_target(tq, i);
+                uint32_t* row = idx + (size_t)i * count;
+                uint8_t* cp = cnt + i;
+                if (count == 0) {
+                    if (lane == 0) *cp = 0;
+                } else if (kind == 0) {
+                    if (T.B == 0) {  // an empty table: an empty result (routing_table.cpp:73)
+                        if (lane < count) row[lane] = NONE;
+                        if (lane == 0) *cp = 0;
+                    } else {
+                        uint32_t lo, hi, good;
+                        wave_window(T.gpre, T.B, locate_bucket(T, t), count, lo, hi, good);
+                        wave_rank_any(T, t, T.dir[lo].x & ~WIDE, T.dir[hi + 1].x & ~WIDE, good, count, row, cp, xs[w]);
+                    }
+                } else if (T.n > 0) {
+                    // the placement rounds use all 64 lanes; the serial walk (lane 0) answers what the runs cannot
+                    nc64_query(T, t, lane, i, count, idx, cnt, true);
+                } else if (lane == 0) {
+                    nc_serial(T, t, count, row, cp);
+                }
+            }
+        }
+        __threadfence_system();  // this wave's rows and counts reach host memory before `done`
+        __syncthreads();
+        if (tid == 0) {
+            reply->t_done = wall_clock64();
+            __hip_atomic_store(&reply->done, last, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+}
+
 template <class T>
 int dev_upload(T** dptr, const void* src, size_t count, std::vector<void*>& owned, uint64_t& bytes) {
     *dptr = nullptr;
@@ -4932,7 +5127,24 @@ struct HostPipe {
     uint8_t *dst = nullptr, *dsc = nullptr;  // their device addresses
     uint32_t* dsi = nullptr;
     hipStream_t ss = nullptr;
+    // Resident query service (kad_table_serve, svc_kernel): mailbox and reply in mapped pinned memory
+    SvcMail* vm = nullptr;   // host view / device view
+    SvcMail* dvm = nullptr;
+    SvcReply* vr = nullptr;
+    SvcReply* dvr = nullptr;
+    hipStream_t vs = nullptr;
+    uint32_t vseq = 0;       // the last request number posted
+    uint64_t vlaunches = 0, vrequests = 0;  // kad_table_serve_stats
+    int vkhz = 0;            // device wall clock rate
+    uint32_t idle_us = 0;    // 0: the service is off
+    bool vrun = false;       // a launch may still be running on vs
     ~HostPipe() {
+        if (vs) {
+            if (vm) __atomic_store_n(&vm->stop, 1u, __ATOMIC_RELEASE);
+            (void)hipStreamSynchronize(vs);
+            (void)hipStreamDestroy(vs);
+        }
+        for (void* p : {(void*)vm, (void*)vr}) if (p) (void)hipHostFree(p);
         if (ss) { (void)hipStreamSynchronize(ss); (void)hipStreamDestroy(ss); }
         for (void* p : {(void*)st, (void*)sc, (void*)si}) if (p) (void)hipHostFree(p);
         for (auto& w : slot)
@@ -5057,6 +5269,8 @@ struct kad_table {
             if (p) (void)hipFree(p);
     }
 };
+
+static int svc_quiesce(const kad_table* t);  // ends the resident query service's launch (kad_table_serve)
 
 namespace {
 
@@ -6069,6 +6283,7 @@ int kad_table_create(kad_table** out, int device, uint32_t n_nodes, const uint8_
 int kad_table_destroy(kad_table* t) {
     if (!t) return KAD_OK;
     DeviceGuard g(t->device);
+    (void)svc_quiesce(t);  // the resident service ends before the device-wide synchronise
     (void)hipDeviceSynchronize();
     delete t;
     return KAD_OK;
@@ -6104,6 +6319,7 @@ int kad_table_prepare(kad_table* t, uint32_t sets) {
     if (!t) return set_err(KAD_ERR_INVALID, "NULL table");
     if (sets & ~KAD_LINES_ALL) return set_err(KAD_ERR_INVALID, "unknown line sets 0x%x", sets);
     DeviceGuard g(t->device);
+    if (int rc = svc_quiesce(t)) return rc;
     return ensure_lines(t, sets, nullptr);
 }
 
@@ -6135,6 +6351,7 @@ int kad_table_patch_status(kad_table* t, uint32_t m, const uint32_t* nodes, cons
             if (nodes[j] >= t->d.n) return set_err(KAD_ERR_INVALID, "node %u out of range (n=%u)", nodes[j], t->d.n);
     DeviceGuard g(t->device);
     int rc;
+    if ((rc = svc_quiesce(t))) return rc;
     if ((rc = ensure_marks(t))) return rc;
     t->dl.invalidate();  // status bytes set directly: the next refresh_status re-derives every node from its times
     if (m) {
@@ -6162,6 +6379,7 @@ int kad_table_patch_times(kad_table* t, uint32_t m, const uint32_t* nodes, const
     if (!m) return KAD_OK;
     DeviceGuard g(t->device);
     int rc;
+    if ((rc = svc_quiesce(t))) return rc;
     HIP_TRY(hipDeviceSynchronize());  // a refresh still running reads the staging and the deadline runs
     const size_t a = (4ull * m + 15) & ~15ull, b = 8ull * m;
     if ((rc = stage_reserve(t, a + 2 * b + m))) return rc;
@@ -6186,6 +6404,7 @@ int kad_table_set_times(kad_table* t, const int64_t* time_ns, const int64_t* rep
     if (!t || (t->d.n && (!time_ns || !reply_ns || !expired))) return set_err(KAD_ERR_INVALID, "NULL argument");
     DeviceGuard g(t->device);
     int rc;
+    if ((rc = svc_quiesce(t))) return rc;
     if (!t->time_ns) {
         if ((rc = dev_upload(&t->time_ns, nullptr, t->d.n, t->owned, t->bytes)) ||
             (rc = dev_upload(&t->reply_ns, nullptr, t->d.n, t->owned, t->bytes)) ||
@@ -6421,6 +6640,7 @@ int kad_table_set_addrs(kad_table* t, uint32_t addr_len, const uint8_t* addrs) {
     if (addr_len != KAD_ADDR4_LEN && addr_len != KAD_ADDR6_LEN)
         return set_err(KAD_ERR_INVALID, "addr_len %u: 6 (in_addr + port) or 18 (in6_addr + port)", addr_len);
     DeviceGuard g(t->device);
+    if (int rc = svc_quiesce(t)) return rc;
     if (t->wrec && t->addr_len != addr_len) return set_err(KAD_ERR_INVALID, "address length changed");
     const uint32_t rec = addr_len == KAD_ADDR4_LEN ? WREC4 : WREC6;
     int rc;
@@ -6666,6 +6886,98 @@ static int small_query(const kad_table* t, HostPipe& P, const uint8_t* targets, 
     return KAD_OK;
 }
 
+// ---- the resident query service (svc_kernel) ----
+static int svc_launch(const kad_table* t, HostPipe& P) {
+    if (!P.vs) HIP_TRY(hipStreamCreateWithFlags(&P.vs, hipStreamNonBlocking));
+    if (!P.vm) {
+        HIP_TRY(hipHostMalloc((void**)&P.vm, sizeof(SvcMail), hipHostMallocMapped));
+        std::memset((void*)P.vm, 0, sizeof(SvcMail));
+        HIP_TRY(hipHostGetDevicePointer((void**)&P.dvm, P.vm, 0));
+    }
+    if (!P.vr) {
+        HIP_TRY(hipHostMalloc((void**)&P.vr, sizeof(SvcReply), hipHostMallocMapped));
+        std::memset((void*)P.vr, 0, sizeof(SvcReply));
+        HIP_TRY(hipHostGetDevicePointer((void**)&P.dvr, P.vr, 0));
+    }
+    if (!P.vkhz) HIP_TRY(hipDeviceGetAttribute(&P.vkhz, hipDeviceAttributeWallClockRate, t->device));
+    const int khz = P.vkhz;  // the device wall clock (wall_clock64)
+    if (khz <= 0) return set_err(KAD_ERR_HIP, "no device wall clock rate");
+    const uint64_t idle = (uint64_t)P.idle_us * (uint64_t)khz / 1000u, life = (uint64_t)khz * KAD_SERVE_LIFE_MS;
+    // the first request of a launch sees the table after its last asynchronous status refresh
+    if (t->mut_async) HIP_TRY(hipStreamWaitEvent(P.vs, t->mut_ev, 0));
+    __atomic_store_n(&P.vm->stop, 0u, __ATOMIC_RELEASE);
+    hipLaunchKernelGGL(svc_kernel, dim3(1), dim3(BLOCK), 0, P.vs, t->d, P.dvm, P.dvr,
+                       __atomic_load_n(&P.vr->done, __ATOMIC_ACQUIRE), idle, life);
+    HIP_TRY(hipGetLastError());
+    P.vrun = true;
+    P.vlaunches++;
+    return KAD_OK;
+}
+
+// Ends the running launch, if any (the caller holds P.mu).
+static int svc_halt(HostPipe& P) {
+    if (!P.vrun) return KAD_OK;
+    __atomic_store_n(&P.vm->stop, 1u, __ATOMIC_RELEASE);
+    const hipError_t e = hipStreamSynchronize(P.vs);
+    __atomic_store_n(&P.vm->stop, 0u, __ATOMIC_RELEASE);
+    P.vrun = false;
+    if (e != hipSuccess) return set_err(KAD_ERR_HIP, "query service: %s", hipGetErrorString(e));
+    return KAD_OK;
+}
+
+// Before any call that changes or frees what the service reads (or synchronises the whole device).
+static int svc_quiesce(const kad_table* t) {
+    std::lock_guard<std::mutex> lk(t->pipe_mu);
+    if (!t->pipe) return KAD_OK;
+    std::lock_guard<std::mutex> lk2(t->pipe->mu);
+    DeviceGuard g(t->device);
+    return svc_halt(*t->pipe);
+}
+
+// One request of q <= SVC_Q queries, count <= SVC_COUNT (the caller holds P.mu and has validated the call).
+static int svc_query(const kad_table* t, HostPipe& P, const uint8_t* targets, uint32_t q, uint32_t count,
+                     uint32_t* out_idx, uint8_t* out_cnt, bool nc) {
+    if (t->mut_async) {  // ordered after the table's last asynchronous status refresh, whatever its stream
+        const hipError_t e = hipEventQuery(t->mut_ev);
+        if (e == hipErrorNotReady) HIP_TRY(hipEventSynchronize(t->mut_ev));
+        else if (e != hipSuccess) return set_err(KAD_ERR_HIP, "status refresh: %s", hipGetErrorString(e));
+    }
+    int rc;
+    if (!P.vrun && (rc = svc_launch(t, P))) return rc;
+    std::memcpy(P.vm->targets, targets, 20ull * q);
+    P.vm->q = q;
+    P.vm->count = count;
+    P.vm->kind = nc ? 1u : 0u;
+    const uint32_t s = ++P.vseq;
+    __atomic_store_n(&P.vm->seq2, s, __ATOMIC_RELEASE);  // the targets, then seq2, then seq (svc_kernel)
+    __atomic_store_n(&P.vm->seq, s, __ATOMIC_RELEASE);
+    const auto t0 = std::chrono::steady_clock::now();
+    int relaunched = 0;
+    for (uint64_t it = 1;; it++) {
+        if (__atomic_load_n(&P.vr->done, __ATOMIC_ACQUIRE) == s) break;
+        if ((it & 255u) == 0) {
+            const hipError_t e = hipStreamQuery(P.vs);
+            if (e == hipSuccess) {  // the launch ended (idle or life time) before it saw the request
+                P.vrun = false;
+                if (__atomic_load_n(&P.vr->done, __ATOMIC_ACQUIRE) == s) break;
+                if (++relaunched > 3) return set_err(KAD_ERR_HIP, "query service: request %u not answered", s);
+                if ((rc = svc_launch(t, P))) return rc;
+            } else if (e != hipErrorNotReady) {
+                P.vrun = false;
+                return set_err(KAD_ERR_HIP, "query service: %s", hipGetErrorString(e));
+            }
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10)) {
+                (void)svc_halt(P);
+                return set_err(KAD_ERR_HIP, "query service: request %u timed out", s);
+            }
+        }
+    }
+    if (count) std::memcpy(out_idx, (const void*)P.vr->idx, 4ull * q * count);
+    if (out_cnt) std::memcpy(out_cnt, (const void*)P.vr->cnt, q);
+    P.vrequests++;
+    return KAD_OK;
+}
+
 static int host_query(const kad_table* t, const uint8_t* targets, uint32_t q, uint32_t count, uint32_t* out_idx,
                       uint8_t* out_cnt, bool nc) {
     if (!t) return set_err(KAD_ERR_INVALID, "NULL table");
@@ -6687,6 +6999,7 @@ static int host_query(const kad_table* t, const uint8_t* targets, uint32_t q, ui
     HostPipe& P = *t->pipe;
     std::lock_guard<std::mutex> lk(P.mu);
     DeviceGuard g(t->device);
+    if (P.idle_us && q <= SVC_Q && count <= SVC_COUNT) return svc_query(t, P, targets, q, count, out_idx, out_cnt, nc);
     if (q <= HostPipe::SMALL && count <= HostPipe::SMALL_COUNT)
         return small_query(t, P, targets, q, count, out_idx, out_cnt, nc);
     int rc = pipe_ready(P);
@@ -6783,6 +7096,47 @@ int kad_rt_closest_batch_host(const kad_table* t, const uint8_t* targets, uint32
                               uint8_t* out_cnt) {
     return host_query(t, targets, q, count, out_idx, out_cnt, false);
 }
+
+int kad_table_serve_stats(const kad_table* t, kad_serve_stats* out) {
+    if (!t || !out) return set_err(KAD_ERR_INVALID, "NULL argument");
+    *out = kad_serve_stats{};
+    std::lock_guard<std::mutex> lk(t->pipe_mu);
+    if (!t->pipe) return KAD_OK;
+    HostPipe& P = *t->pipe;
+    std::lock_guard<std::mutex> lk2(P.mu);
+    out->idle_us = P.idle_us;
+    out->launches = P.vlaunches;
+    out->requests = P.vrequests;
+    if (P.vr && P.vkhz > 0 && P.vrequests) {
+        out->last_polls = P.vr->polls;
+        out->last_busy_ns = (uint64_t)((P.vr->t_done - P.vr->t_seen) * 1e6 / P.vkhz);
+    }
+    return KAD_OK;
+}
+
+int kad_table_serve(kad_table* t, uint32_t idle_us) {
+    if (!t) return set_err(KAD_ERR_INVALID, "NULL table");
+    if (idle_us > KAD_SERVE_MAX_IDLE_US)
+        return set_err(KAD_ERR_INVALID, "idle_us %u above %u", idle_us, (uint32_t)KAD_SERVE_MAX_IDLE_US);
+    {
+        std::lock_guard<std::mutex> lk(t->pipe_mu);
+        if (!t->pipe) {
+            if (!idle_us) return KAD_OK;
+            try {
+                t->pipe = new HostPipe();
+            } catch (...) {
+                return set_err(KAD_ERR_NOMEM, "query service: out of host memory");
+            }
+        }
+    }
+    HostPipe& P = *t->pipe;
+    std::lock_guard<std::mutex> lk(P.mu);
+    DeviceGuard g(t->device);
+    const int rc = svc_halt(P);  // a launch with the old idle time ends
+    P.idle_us = idle_us;
+    if (rc) return rc;
+    return idle_us ? svc_launch(t, P) : KAD_OK;  // running before the first request
+}
 int kad_nc_closest_batch_host(const kad_table* t, const uint8_t* targets, uint32_t q, uint32_t count, uint32_t* out_idx,
                               uint8_t* out_cnt) {
     return host_query(t, targets, q, count, out_idx, out_cnt, true);
@@ -6876,6 +7230,7 @@ int kad_table_apply(kad_table* t, const uint32_t* ops, uint32_t n_ops, const uin
     if (t->d.B == 0 || t->h_off.empty()) return set_err(KAD_ERR_INVALID, "the mirror needs a RoutingTable (buckets)");
     if ((uint64_t)t->d.n + n_new >= 0x7FFFFFFFull) return set_err(KAD_ERR_INVALID, "table too large");
     DeviceGuard g(t->device);
+    if (int rc = svc_quiesce(t)) return rc;  // the resident service reads the arrays this call replaces
     DevTable& d = t->d;
     const uint32_t B0 = d.B, n0 = d.n;
     // KAD_DEBUG: the phases' wall times (host plan, layout, gather, directory, line rebuild)
@@ -7097,6 +7452,7 @@ int kad_nc_apply(kad_table* t, const uint32_t* erase, uint32_t n_erase, const ui
     }
     const uint32_t n1 = n0 - n_erase + n_ins;
     DeviceGuard g(t->device);
+    if (int rc = svc_quiesce(t)) return rc;  // the resident service reads the arrays this call replaces
     std::vector<void*> tmp, fresh;
     uint64_t tmpb = 0, freshb = 0;
     auto fail = [&](int code) {

@@ -24,8 +24,8 @@ def _as_ids(a) -> np.ndarray:
 
 
 def _stream_of(t, stream):
-    if stream is not None:
-        return C.c_void_p(stream)
+    if stream is not None:  # a raw hipStream_t handle or a torch.cuda.Stream
+        return C.c_void_p(getattr(stream, "cuda_stream", stream))
     import torch
 
     return C.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
@@ -101,6 +101,17 @@ class DeviceTable:
         out["line_sets"] = {name: {"built": bool(built.value & (1 << k)), "bytes": int(nb[k]), "build_ms": float(ms[k])}
                             for k, name in enumerate(("rt16", "rt32", "nc16", "nc32"))}
         return out
+
+    def serve(self, idle_us: int = 2000) -> None:
+        """Resident query service (kad_table_serve): host batches of up to 64 queries with count <= 64 are answered
+        by a workgroup that stays on the GPU, without a launch per call. idle_us = 0 turns it off."""
+        check(lib().kad_table_serve(self._h, idle_us), "kad_table_serve")
+
+    def serve_stats(self) -> dict:
+        """kad_table_serve_stats: launches, requests, and the last request's header reads and device time."""
+        st = _lib.serve_stats()
+        check(lib().kad_table_serve_stats(self._h, C.byref(st)), "kad_table_serve_stats")
+        return {f: getattr(st, f) for f, _ in st._fields_}
 
     def prepare(self, sets: int = _lib.KAD_LINES_ALL) -> None:
         """Build the line sets `sets` (KAD_LINES_*) now instead of on first use (e.g. before a graph capture)."""

@@ -4,7 +4,7 @@ over the kernel's launch time (tools/bench_paths.py timings), VALU busy (SQ_ACTI
 1024 SIMDs x GRBM_GUI_ACTIVE / 8 cycles, the formula DESIGN.md §5 uses for the headline kernel) and
 where the waves' cycles go (WAIT_ANY parked on loads, WAIT_INST_ANY issue stalls, ACTIVE_INST_ANY).
 
-    python tools/paths_roofline.py gpurun_out/pmc_paths gpurun_out/paths.log profiles/r01_v11/paths_roofline.json
+    python tools/paths_roofline.py gpurun_out/pmc_paths gpurun_out/paths.log profiles/history/r01_v11/paths_roofline.json
 """
 import json
 import re
