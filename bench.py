@@ -57,7 +57,7 @@ def parse_args(argv=None):
                     help="headline only: no cold-cache pass, refresh, allgather variant (profiling runs)")
     ap.add_argument("--no-allgather", action="store_true")
     ap.add_argument("--no-graph", action="store_true", help="issue the K steps one by one instead of one HIP graph")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r02.json"))
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r03.json"))
     ap.add_argument("--gather-json", default=os.path.join(ROOT, "profiles", "r02_mb_gather.json"))
     ap.add_argument("--plumbing", action="store_true",
                     help="launcher/rendezvous check without a GPU: gloo ranks, barrier, max-over-ranks, one line")
@@ -595,14 +595,20 @@ def latency_pass(dev, nodes=170, reps=2000):
         T.serve(100_000)
         for q in (1, 64):
             oi, oc = np.zeros((q, 8), np.uint32), np.zeros((q,), np.uint8)
-            ts = []
+            ts, busy = [], []
             for r in range(reps):
                 x = np.ascontiguousarray(tg[(r * q) % (4096 - q):(r * q) % (4096 - q) + q])
                 t0 = time.perf_counter()
                 check(lib().kad_rt_closest_batch_host(T.handle, ptr(x), q, 8, ptr(oi), ptr(oc)), "served batch")
                 ts.append(time.perf_counter() - t0)
+            for r in range(200):  # the device side of a request, apart from the timed calls
+                x = np.ascontiguousarray(tg[(r * q) % (4096 - q):(r * q) % (4096 - q) + q])
+                check(lib().kad_rt_closest_batch_host(T.handle, ptr(x), q, 8, ptr(oi), ptr(oc)), "served batch")
+                busy.append(T.serve_stats()["last_busy_ns"])
             res[f"serve_q{q}_us"] = float(np.median(ts)) * 1e6
             res[f"serve_q{q}_p99_us"] = float(np.percentile(ts, 99)) * 1e6
+            res[f"serve_q{q}_device_us"] = float(np.median(busy)) / 1e3
+        res["serve_launches"] = int(T.serve_stats()["launches"])
         T.serve(0)
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
@@ -619,7 +625,9 @@ def latency_pass(dev, nodes=170, reps=2000):
     res["how"] = (f"median of {reps} synchronous calls, k=8, host buffers in and out (ctypes overhead included); "
                   "gpu: one kernel launch reading the targets from and writing the rows to mapped pinned memory; "
                   "serve: the resident query service (kad_table_serve, 100 ms idle), a request posted to and answered "
-                  "from mapped pinned memory by a workgroup that stays on the GPU; "
+                  "from mapped pinned memory by a workgroup that stays on the GPU (device_us: from the request seen to "
+                  "its rows fenced, device clock; the rest is the PCIe round trip and the host); "
+                  "C-level figures without ctypes: tools/latency_serve.cpp; "
                   "cpu_port: the std::list restatement of routing_table.cpp:67-135 on one thread, same table")
     return res
 

@@ -92,7 +92,7 @@ public:
     explicit operator bool() const { return t_ != nullptr; }
 
     /* Resident query service for single requests (kad_table_serve); idle_us = 0 turns it off. */
-    void serve(uint32_t idle_us) { check(kad_table_serve(t_, idle_us), "kad_table_serve"); }
+    void serve(uint32_t idle_us) const { check(kad_table_serve(t_, idle_us), "kad_table_serve"); }
 
     /* Host-buffer batch queries (synchronous). Rows of `count` indices, KAD_NO_NODE padded. */
     void findClosestNodesBatch(const uint8_t* targets, size_t q, size_t count, std::vector<uint32_t>& idx,
@@ -295,6 +295,8 @@ public:
     size_t bucketCount() const { return buckets_; }
     size_t nodeCount() const { return nodes_.size(); }
     const DeviceTable& table() const { return table_; }
+    /* Single findClosestNodes calls answered by the resident query service (kad_table_serve); 0 turns it off. */
+    void serve(uint32_t idle_us = 2000) const { table_.serve(idle_us); }
 
 private:
     // status at the query's `now`: reported liveness changes first, then the device refresh

@@ -1752,14 +1752,16 @@ __device__ __forceinline__ uint32_t qdpp(uint32_t v) {
 }
 constexpr int QP_X1 = 0xB1, QP_X2 = 0x4E, QP_X3 = 0x1B, QP_B0 = 0x00, QP_B1 = 0x55;  // quad_perm encodings
 
-// element i against the quad partner's element (REV ? 15 - i : i); the low lane keeps the min, the other the max
+// element i against the quad partner's element (REV ? 15 - i : i); the low lane keeps the min, the other the max:
+// med3(v, w, 0) = min, med3(v, w, ~0) = max, one v_med3_u32 instead of min, max and a select
 template <int CTRL, bool REV>
 __device__ __forceinline__ void quad_exchange(uint32_t (&v)[16], bool low) {
     uint32_t w[16];
+    const uint32_t c = low ? 0u : 0xFFFFFFFFu;
 #pragma unroll
     for (int i = 0; i < 16; i++) w[i] = qdpp<CTRL>(v[REV ? 15 - i : i]);
 #pragma unroll
-    for (int i = 0; i < 16; i++) v[i] = low ? min(v[i], w[i]) : max(v[i], w[i]);
+    for (int i = 0; i < 16; i++) v[i] = max(min(v[i], w[i]), min(max(v[i], w[i]), c));
 }
 
 // a bitonic 16 in one lane, sorted ascending by half-cleaners 8, 4, 2, 1
@@ -4262,65 +4264,69 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) v
         }
         const uint32_t p = NC32_LEFT + below;
         bool ex = (fl & 1u) || eq;
-        // the runs' first 64 steps: left step 8g+u = element p-1-step, right step 63-8g-u = element p+step
-        uint32_t ka[8], kb[8], runA = 0, runB = 0;
+        // the runs' first 64 steps: left step 8g+u = element p-1-step, right step 63-8g-u = element p+step. Key:
+        // distance24 << 8 | side << 7 | step << 1 | expired. A step outside the line's window is NONE: it sorts
+        // after every step inside, is never emitted (its expired bit is set), and (the outside steps are a suffix
+        // of their run) the run maxima below pass it on only to other outside steps, so no step needs a validity
+        // test after this.
+        uint32_t ka[8], kb[8];
 #pragma unroll
         for (int u = 0; u < 8; u++) {
             const uint32_t ra = 8 * g + u, rb = 63 - 8 * g - u;
             const bool va = ra < p, vb = p + rb < NC32_SLOTS;
-            const uint32_t xa = va ? W[4 + p - 1 - ra] : 0u, xb = vb ? W[4 + p + rb] : 0u;
+            const uint32_t xa = W[4 + (va ? p - 1 - ra : 0u)], xb = W[4 + (vb ? p + rb : 0u)];
             ka[u] = va ? ((((xa >> 8) ^ t24) << 8) | (ra << 1) | (xa & 1u)) : NONE;
             kb[u] = vb ? ((((xb >> 8) ^ t24) << 8) | 128u | (rb << 1) | (xb & 1u)) : NONE;
         }
-        // prefix maxima of the distances along each run: in the lane (left: u ascending, right: u descending),
-        // then the runs' earlier lanes (left: lower g, right: higher g)
-        uint32_t pa[8], pb[8];
+        // run maxima: in the lane (left: u ascending, right: u descending) over whole keys (their top 24 bits
+        // are the distance maxima), then the runs' earlier lanes (left: lower g, right: higher g); a shuffle
+        // from outside the octet returns the lane's own value, which max leaves alone
+        uint32_t pa[8], pb[8], ca = 0, cb = 0;
 #pragma unroll
-        for (int u = 0; u < 8; u++) {
-            runA = max(runA, ka[u] == NONE ? 0u : ka[u] & ~255u);
-            pa[u] = runA;
-        }
+        for (int u = 0; u < 8; u++) pa[u] = ca = max(ca, ka[u]);
 #pragma unroll
-        for (int u = 7; u >= 0; u--) {
-            runB = max(runB, kb[u] == NONE ? 0u : kb[u] & ~255u);
-            pb[u] = runB;
-        }
-        uint32_t ca = runA, cb = runB;
+        for (int u = 7; u >= 0; u--) pb[u] = cb = max(cb, kb[u]);
 #pragma unroll
         for (int o = 1; o < 8; o <<= 1) {
-            const uint32_t ya = (uint32_t)__shfl_up((int)ca, o, 8), yb = (uint32_t)__shfl_down((int)cb, o, 8);
-            if (g >= (uint32_t)o) ca = max(ca, ya);
-            if (g + o < 8) cb = max(cb, yb);
+            ca = max(ca, (uint32_t)__shfl_up((int)ca, o, 8));
+            cb = max(cb, (uint32_t)__shfl_down((int)cb, o, 8));
         }
-        // exclusive carries (the shuffles run in every lane: a lane reading a lane that skipped the read gets 0)
         const uint32_t ua = (uint32_t)__shfl_up((int)ca, 1, 8), ub = (uint32_t)__shfl_down((int)cb, 1, 8);
         const uint32_t inA = g > 0 ? ua : 0u, inB = g < 7 ? ub : 0u;
-        uint32_t endA = 0, endB = 0;
 #pragma unroll
-        for (int u = 0; u < 8; u++) {
-            if (ka[u] != NONE) { ka[u] = max(pa[u], inA) | (ka[u] & 255u); endA = max(endA, ka[u]); }
-            if (kb[u] != NONE) { kb[u] = max(pb[u], inB) | (kb[u] & 255u); endB = max(endB, kb[u]); }
+        for (int u = 0; u < 8; u++) {  // the key's distance = the run maximum up to the step (bitfield insert)
+            ka[u] = (max(pa[u], inA) & 0xFFFFFF00u) | (ka[u] & 255u);
+            kb[u] = (max(pb[u], inB) & 0xFFFFFF00u) | (kb[u] & 255u);
         }
-#pragma unroll
-        for (int o = 1; o < 8; o <<= 1) {
-            endA = max(endA, (uint32_t)__shfl_xor((int)endA, o, 8));
-            endB = max(endB, (uint32_t)__shfl_xor((int)endB, o, 8));
-        }
-        // keys beyond a truncated run end (fewer than 64 steps inside the window) are not trusted
+        // keys beyond a run cut short by the window's truncated end are not trusted: the run's last step inside
+        // the window (left: step p-1, right: step 123-p) bounds them
         uint32_t lim = NONE;
-        if ((fl & 2u) && p <= 64) lim = min(lim, endA);
-        if ((fl & 4u) && NC32_SLOTS - p <= 64) lim = min(lim, endB);
-        // the walk's first 64 steps: min(left[r], right[63-r]) is bitonic; half-cleaners sort it
+        if ((fl & 2u) && p <= 64) {
+            const uint32_t r = p - 1, ux = r & 7u;
+            uint32_t v = ka[0];
+#pragma unroll
+            for (int u = 1; u < 8; u++) v = ux == (uint32_t)u ? ka[u] : v;
+            lim = min(lim, (uint32_t)__shfl((int)v, (int)((lane & ~7u) | (r >> 3)), 64));
+        }
+        if ((fl & 4u) && NC32_SLOTS - p <= 64) {
+            const uint32_t r = 63u - (NC32_SLOTS - 1 - p), ux = r & 7u;  // step 123-p sits at u = r & 7, g = r >> 3
+            uint32_t v = kb[0];
+#pragma unroll
+            for (int u = 1; u < 8; u++) v = ux == (uint32_t)u ? kb[u] : v;
+            lim = min(lim, (uint32_t)__shfl((int)v, (int)((lane & ~7u) | (r >> 3)), 64));
+        }
+        // the walk's first 64 steps: min(left[r], right[63-r]) is bitonic; half-cleaners sort it. Across lanes
+        // the low lane of a pair keeps the min and the high one the max: med3(w, partner, 0 or ~0) in one op.
         uint32_t w[8];
 #pragma unroll
         for (int u = 0; u < 8; u++) w[u] = min(ka[u], kb[u]);
 #pragma unroll
         for (int o = 4; o >= 1; o >>= 1) {
-            const bool lo = (g & (uint32_t)o) == 0;
+            const uint32_t hi = (g & (uint32_t)o) ? 0xFFFFFFFFu : 0u;
 #pragma unroll
             for (int u = 0; u < 8; u++) {
                 const uint32_t y = (uint32_t)__shfl_xor((int)w[u], o, 8);
-                w[u] = lo ? min(w[u], y) : max(w[u], y);
+                w[u] = max(min(w[u], y), min(max(w[u], y), hi));  // v_med3_u32
             }
         }
 #pragma unroll
@@ -4328,12 +4334,13 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) v
 #pragma unroll
             for (int u = 0; u < 8; u++)
                 if ((u & h) == 0) cx(w[u], w[u + h]);
-        // emissions: non-expired steps up to lim, ranked across the octet
+        // emissions: non-expired steps up to lim (outside steps and NONE carry the expired bit), ranked across
+        // the octet
         uint32_t kept = 0;
         bool keep[8];
 #pragma unroll
         for (int u = 0; u < 8; u++) {
-            keep[u] = w[u] != NONE && w[u] <= lim && !(w[u] & 1u);
+            keep[u] = w[u] <= lim && !(w[u] & 1u);
             kept += keep[u];
         }
         uint32_t cr = kept;
@@ -4344,19 +4351,31 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) v
         }
         const uint32_t tot = (uint32_t)__shfl((int)cr, (int)((lane & ~7u) | 7u), 64);
         ok = !ex && tot >= count;
+        // the row through the octet's LDS row (the line is no longer read): entry `rank` at W[rank]
+        __builtin_amdgcn_wave_barrier();
         if (ok) {
             uint32_t rank = cr - kept;
-            uint32_t* row = out_idx + (size_t)qi * count;
-            const uint32_t base = w0 + T.index_base;
+            const uint32_t bp = w0 + T.index_base + p;
 #pragma unroll
             for (int u = 0; u < 8; u++) {
                 if (keep[u]) {
                     if (rank < count) {
                         const uint32_t st = (w[u] >> 1) & 63u;
-                        row[rank] = base + ((w[u] & 128u) ? p + st : p - 1 - st);
+                        W[rank] = (w[u] & 128u) ? bp + st : bp - 1u - st;
                     }
                     rank++;
                 }
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (ok) {
+            uint32_t* row = out_idx + (size_t)qi * count;
+            if ((count & 3u) == 0 && ((uintptr_t)out_idx & 15u) == 0) {
+                if (4 * g < count) reinterpret_cast<uint4*>(row)[g] = make_uint4(W[4 * g], W[4 * g + 1], W[4 * g + 2], W[4 * g + 3]);
+            } else {
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    if (4 * g + j < count) row[4 * g + j] = W[4 * g + j];
             }
             if (g == 0 && out_cnt) out_cnt[qi] = (uint8_t)count;
         }

@@ -408,8 +408,28 @@ int main() {
             auto res = lm.findClosestNodesBatch(&targets[(r * 64) % (q - 64)], 64, t0, 8);
             b64_us.push_back(std::chrono::duration<double, std::micro>(clock::now() - a).count());
         }
-        std::printf("LATENCY {\"nodes\": %u, \"buckets\": %u, \"single_call_us\": %.2f, \"batch64_call_us\": %.2f}\n",
-                    m, LB, med(one_us), med(b64_us));
+        // the same calls answered by the resident query service (kad_table_serve): the same nodes, in order
+        auto before = lm.findClosestNodesBatch(&targets[0], 64, t0, 14);
+        lm.serve(100000);
+        EXPECT(lm.findClosestNodesBatch(&targets[0], 64, t0, 14) == before, "served batch equals the launch path");
+        for (int j = 0; j < 64; j++)
+            EXPECT(lm.findClosestNodes(targets[j], t0, 14) == before[j], "served single call equals the launch path");
+        std::vector<double> s1_us, s64_us;
+        for (int r = 0; r < 2000; r++) {
+            const auto a = clock::now();
+            auto res = lm.findClosestNodes(targets[r % q], t0, 8);
+            s1_us.push_back(std::chrono::duration<double, std::micro>(clock::now() - a).count());
+            EXPECT(res.size() == 8, "latency table result (served)");
+        }
+        for (int r = 0; r < 500; r++) {
+            const auto a = clock::now();
+            auto res = lm.findClosestNodesBatch(&targets[(r * 64) % (q - 64)], 64, t0, 8);
+            s64_us.push_back(std::chrono::duration<double, std::micro>(clock::now() - a).count());
+        }
+        lm.serve(0);
+        std::printf("LATENCY {\"nodes\": %u, \"buckets\": %u, \"single_call_us\": %.2f, \"batch64_call_us\": %.2f, "
+                    "\"served_single_call_us\": %.2f, \"served_batch64_call_us\": %.2f}\n",
+                    m, LB, med(one_us), med(b64_us), med(s1_us), med(s64_us));
     }
     std::printf("%s (%d failures)\n", fails ? "FAIL" : "PASS", fails);
     return fails ? 1 : 0;
