@@ -1773,6 +1773,7 @@ __device__ __forceinline__ void clean16(uint32_t (&v)[16]) {
             if ((i & w) == 0) cx(v[i], v[i + w]);
 }
 
+template <bool RANK = true>  // RANK false: timing ablation only (the values unranked; results wrong)
 __device__ __forceinline__ bool wl32_answer4(const DevTable& T, const Target& t, uint32_t b, uint32_t count, bool act,
                                              uint32_t p, uint32_t (&v)[16], uint32_t& m, uint32_t& base) {
     uint32_t L[16];
@@ -1823,12 +1824,14 @@ __device__ __forceinline__ bool wl32_answer4(const DevTable& T, const Target& t,
     have += qdpp<QP_X1>(have);
     have += qdpp<QP_X2>(have);
     const bool low = (p & 1u) == 0;
-    sort16(v);
-    quad_exchange<QP_X1, true>(v, low);
-    clean16(v);
-    quad_exchange<QP_X3, true>(v, true);
-    quad_exchange<QP_X1, false>(v, low);
-    clean16(v);
+    if (RANK) {
+        sort16(v);
+        quad_exchange<QP_X1, true>(v, low);
+        clean16(v);
+        quad_exchange<QP_X3, true>(v, true);
+        quad_exchange<QP_X1, false>(v, low);
+        clean16(v);
+    }
     ex |= have < m;
     return !ex;
 }
@@ -1866,7 +1869,11 @@ __device__ __forceinline__ void store_rows_quad(uint32_t* __restrict__ out_idx, 
     }
 }
 
-template <int ABL>
+// QS: the row leaves through a per-quad LDS row, lane p storing entries [4p, 4p+4) and [16+4p, 20+4p) (16-byte pieces,
+// 64 contiguous bytes per quad and instruction) or, for rows that are not 16-byte aligned, entry 4j+p in instruction j
+// (16 contiguous bytes per quad and instruction); no block barrier. !QS: lanes 0 and 1 store their 16 entries from
+// registers (aligned rows) or the block's rows go through store_rows_quad.
+template <int ABL, bool QS>
 __global__ __launch_bounds__(BLOCK) void rt_wl32q_kernel(DevTable T, const uint8_t* __restrict__ targets, uint32_t q,
                                                          uint32_t count, uint32_t* __restrict__ out_idx,
                                                          uint8_t* __restrict__ out_cnt) {
@@ -1879,13 +1886,37 @@ __global__ __launch_bounds__(BLOCK) void rt_wl32q_kernel(DevTable T, const uint8
         b = locate_bucket(T, t);
     }
     uint32_t v[16], m, base;
-    const bool ok = wl32_answer4(T, t, b, count, act, p, v, m, base);
+    const bool ok = wl32_answer4<ABL == 0>(T, t, b, count, act, p, v, m, base);
     const uint32_t r0 = 16u * (p & 1u), bi = base + T.index_base;
     uint32_t o[16];
 #pragma unroll
     for (int k = 0; k < 16; k++) o[k] = r0 + k < m ? bi + (v[k] & 255u) : NONE;
     if (act && ok && p == 0 && out_cnt) out_cnt[i] = (uint8_t)m;
-    if ((count & 3u) == 0 && ((uintptr_t)out_idx & 15u) == 0) {  // lanes 0 and 1 store 16-byte pieces
+    if (QS) {
+        __shared__ uint4 qrow[BLOCK / 4][9];  // per quad: 32 entries + a 16-byte pad
+        uint32_t* R = reinterpret_cast<uint32_t*>(qrow[threadIdx.x >> 2]);
+        if (p < 2u) {
+#pragma unroll
+            for (int x = 0; x < 4; x++)
+                reinterpret_cast<uint4*>(R + 16u * p)[x] = make_uint4(o[4 * x], o[4 * x + 1], o[4 * x + 2], o[4 * x + 3]);
+        }
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        if (act && ok) {
+            uint32_t* row = out_idx + (size_t)i * count;
+            if ((count & 3u) == 0 && ((uintptr_t)out_idx & 15u) == 0) {
+#pragma unroll
+                for (int h = 0; h < 2; h++)
+                    if (16u * h + 4u * p < count)
+                        reinterpret_cast<uint4*>(row)[4 * h + p] = reinterpret_cast<const uint4*>(R)[4 * h + p];
+            } else {
+#pragma unroll
+                for (int j = 0; j < 8; j++)
+                    if (4u * j + p < count) row[4 * j + p] = R[4 * j + p];
+            }
+        }
+    } else if ((count & 3u) == 0 && ((uintptr_t)out_idx & 15u) == 0) {  // lanes 0 and 1 store 16-byte pieces
         if (act && ok && p < 2u) {
             uint4* row = reinterpret_cast<uint4*>(out_idx + (size_t)i * count + r0);
 #pragma unroll
@@ -5997,12 +6028,23 @@ int launch_rt(const kad_table* t, const uint8_t* targets, uint32_t q, uint32_t c
     } else if (K == 32 && (d.flags & TF_WL32) && !(ev && std::strcmp(ev, "lane") == 0)) {
         // the quad form ranks faster for long rows stored as 16-byte pieces (counts 28 and 32), the one-lane
         // form for the others (tools/ab_kernels.py, profiles/r03/ab_wl32.json)
-        const bool quad = count >= 28 && (count & 3u) == 0;
-        if ((!quad && !(ev && std::strcmp(ev, "wl32quad") == 0)) || (ev && std::strcmp(ev, "wl32lane") == 0))
+        // the quad form with its per-quad LDS row store is faster for rows of 24, 28 and 32 entries (16-byte
+        // pieces), the one-lane form for the others (tools/ab_kernels.py, profiles/r03/ab_wl32_qs.json)
+        const bool quad = count >= 24 && (count & 3u) == 0;
+#ifdef KAD_ABLATIONS
+        if (ev && std::strcmp(ev, "wl32qs_abl1") == 0) {  // no ranking: the kernel's memory floor (results wrong)
+            hipLaunchKernelGGL((rt_wl32q_kernel<1, true>), dim3(grid_for(4ull * q)), dim3(BLOCK), 0, s, d, targets, q,
+                               count, out, cnt);
+        } else
+#endif
+        if (ev && std::strcmp(ev, "wl32quad") == 0)  // A/B: the quad form with the register / block-staged stores
+            hipLaunchKernelGGL((rt_wl32q_kernel<0, false>), dim3(grid_for(4ull * q)), dim3(BLOCK), 0, s, d, targets, q,
+                               count, out, cnt);
+        else if ((!quad && !(ev && std::strcmp(ev, "wl32qs") == 0)) || (ev && std::strcmp(ev, "wl32lane") == 0))
             hipLaunchKernelGGL(rt_wl32_kernel, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
         else
-            hipLaunchKernelGGL(rt_wl32q_kernel<0>, dim3(grid_for(4ull * q)), dim3(BLOCK), 0, s, d, targets, q, count, out,
-                               cnt);
+            hipLaunchKernelGGL((rt_wl32q_kernel<0, true>), dim3(grid_for(4ull * q)), dim3(BLOCK), 0, s, d, targets, q,
+                               count, out, cnt);
     } else if (K == 8 && (d.flags & TF_SL) && !(ev && (std::strcmp(ev, "lane") == 0 || std::strcmp(ev, "gl") == 0 ||
                                                         std::strcmp(ev, "sl_abl1") == 0))) {
         hipLaunchKernelGGL(rt_sl_kernel<0>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);

@@ -1,7 +1,7 @@
 """A/B of RoutingTable kernel variants on the bench shard (1/8 of the 100M-node U(24) table): for each count,
 every variant named by KAD_RT_KERNEL (read per call by the engine; "" = the default dispatch) is timed over 16
 launches of 1M queries on 8 rotated target batches (HIP events), interleaved twice, and its rows must equal the
-default's.
+default's (except the ablations, *_abl*, whose results are wrong on purpose; RT_ABL=1 loads their build).
 
     python tools/ab_kernels.py 17,24,32 ,wl32lane
 """
@@ -13,6 +13,10 @@ import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import opendht_amd._lib as _kl  # noqa: E402
+
+if os.environ.get("RT_ABL"):  # the timing-ablation build (make -C opendht_amd/csrc ablations): *_abl variants
+    _kl.use_ablation_build()
 from opendht_amd import DeviceTable  # noqa: E402
 from opendht_amd.sharded import build_shard, config3_spec  # noqa: E402
 
@@ -51,6 +55,6 @@ for k in counts:
             res.setdefault(f"k{k}_{v or 'default'}_us", []).append(round(us, 1))
             if ref is None:
                 ref = (idx.cpu().numpy(), cnt.cpu().numpy())
-            else:
+            elif "_abl" not in v:
                 assert np.array_equal(idx.cpu().numpy(), ref[0]) and np.array_equal(cnt.cpu().numpy(), ref[1]), (k, v)
 print(json.dumps(res), flush=True)
