@@ -415,6 +415,8 @@ def main_owner(args):
         extras["other_counts"] = counts_pass(T, tgs, Q, dev, stream)
         if rank == 0:
             extras["latency"] = latency_pass(dev)
+        if rank == 0 and world == 1:
+            extras["configs"] = configs_pass(dev)
     # the rows of the last timed step (batch K-1), checked against the CPU restatement on this rank's
     # shard table (exact halo: every owned window lies inside it)
     vrows = min(Q, args.verify_rows)
@@ -629,6 +631,132 @@ def latency_pass(dev, nodes=170, reps=2000):
                   "its rows fenced, device clock; the rest is the PCIe round trip and the host); "
                   "C-level figures without ctypes: tools/latency_serve.cpp; "
                   "cpu_port: the std::list restatement of routing_table.cpp:67-135 on one thread, same table")
+    return res
+
+
+def configs_pass(dev, reps=10):
+    """BASELINE.json's other configs, measured beside the headline (config 3) on the same GPU: the launch time
+    (median of `reps` launches between HIP events, rotated target batches) and the rows checked against the CPU
+    restatement (oracle/, the checker). config 1: the reference's own CPU-runnable case, with the structure-faithful
+    port timed on the same targets; config 5: the swarm model (opendht_amd/csrc/kad_swarm.hip)."""
+    import torch
+
+    from opendht_amd import DeviceTable, nc_closest_dual, rt_closest_dual
+    from opendht_amd import synth as S
+    from opendht_amd.swarm import Swarm
+
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+
+    def med_ms(fn, n=reps):
+        ts = []
+        for r in range(n):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            fn(r)
+            b.record()
+            b.synchronize()
+            ts.append(a.elapsed_time(b))
+        return float(np.median(ts))
+
+    def uniform(n, depth, seed):
+        ids, _ = S.sort_ids(S.random_ids(n, seed))
+        st = S.random_status(n, S.SEED_STATUS ^ seed)
+        first, off = S.uniform_buckets(ids, depth)
+        return ids, st, first, off
+
+    res = {}
+    # config 1: 10k nodes in the reference split policy, 1k targets, k = 8
+    ids = S.random_ids(10_000, S.SEED_IDS)
+    st = S.random_status(10_000, S.SEED_STATUS ^ S.SEED_IDS)
+    perm, first, off = S.split_table(ids, 8)
+    ids, st = np.ascontiguousarray(ids[perm]), np.ascontiguousarray(st[perm])
+    tg = S.random_targets(1000)
+    with DeviceTable(ids, st, first, off, device=dev.index or 0) as T:
+        d = torch.from_numpy(tg).to(dev)
+        idx, cnt = T.rt_closest(d, 8)
+        ms = med_ms(lambda r: T.rt_closest(d, 8, idx, cnt))
+        want, wcnt = O.flat_rt_closest(ids, st, first, off, tg, 8)
+        bad = int((idx.cpu().numpy().view(np.uint32) != want).any(1).sum() + (cnt.cpu().numpy() != wcnt).sum())
+    F = O.FaithfulTable(ids, st, first, off)
+    t0 = time.perf_counter()
+    F.rt_closest(tg, 8, nthreads=1)
+    port_s = time.perf_counter() - t0
+    F.close()
+    res["config1"] = {"what": "10,000-node table in the reference split policy, 1,000 targets, k=8",
+                      "buckets": int(first.shape[0]), "gpu_batch_us": ms * 1e3, "cpu_port_1thread_us": port_s * 1e6,
+                      "verified": {"rows": 1000, "mismatches": bad}}
+    # config 2: 1M nodes, U(17), 64k queries, k = 8, every row checked
+    ids, st, first, off = uniform(1_000_000, 17, S.SEED_IDS)
+    with DeviceTable(ids, st, first, off, device=dev.index or 0, sorted=True) as T:
+        tgs = [S.random_targets(1 << 16, seed=S.SEED_TARGETS + j) for j in range(4)]
+        ds = [torch.from_numpy(x).to(dev) for x in tgs]
+        idx, cnt = T.rt_closest(ds[0], 8)
+        ms = med_ms(lambda r: T.rt_closest(ds[r % 4], 8, idx, cnt))
+        T.rt_closest(ds[0], 8, idx, cnt)
+        want, wcnt = O.flat_rt_closest(ids, st, first, off, tgs[0], 8, nthreads=all_cores())
+        bad = int((idx.cpu().numpy().view(np.uint32) != want).any(1).sum() + (cnt.cpu().numpy() != wcnt).sum())
+    res["config2"] = {"what": "1,000,000-node U(17) table, 65,536 queries, k=8", "us_per_launch": ms * 1e3,
+                      "queries_per_s": (1 << 16) / (ms / 1e3), "verified": {"rows": 1 << 16, "mismatches": bad}}
+    # config 4: v4 and v6 tables of 1M nodes each, 1M queries with af alternating, k = 8 / 16 / 32 and NodeCache 14
+    fam = [uniform(1_000_000, 17, seed) for seed in (0xC4F4, 0xC4F6)]
+    Q = 1 << 20
+    tg = S.random_targets(Q, seed=0x0D4704C4)
+    af = (np.arange(Q) % 2).astype(np.uint8)
+    c4 = {"what": "v4 + v6 tables of 1,000,000 nodes each (U(17), 80/10/10 good/expired/dubious), 1,048,576 queries, "
+                  "af alternating (Dht::onGetValues asks both families, dht.cpp:3216-3217)"}
+    T4 = DeviceTable(*fam[0], device=dev.index or 0, sorted=True)
+    T6 = DeviceTable(*fam[1], device=dev.index or 0, sorted=True)
+    try:
+        d, da = torch.from_numpy(tg).to(dev), torch.from_numpy(af).to(dev)
+        for k in (8, 16, 32):
+            rt_closest_dual(T4, T6, d, da, k)
+            c4[f"rt_k{k}_us"] = med_ms(lambda r: rt_closest_dual(T4, T6, d, da, k)) * 1e3
+        nc_closest_dual(T4, T6, d, da, 14)
+        c4["nc_k14_us"] = med_ms(lambda r: nc_closest_dual(T4, T6, d, da, 14)) * 1e3
+        idx, cnt = rt_closest_dual(T4, T6, d, da, 8)
+        idx, cnt = idx.cpu().numpy().view(np.uint32), cnt.cpu().numpy()
+        bad = 0
+        for a in (0, 1):
+            sel = np.flatnonzero(af[:1 << 16] == a)
+            want, wcnt = O.flat_rt_closest(*fam[a][:2], *fam[a][2:], tg[sel], 8, nthreads=all_cores())
+            bad += int((idx[sel] != want).any(1).sum() + (cnt[sel] != wcnt).sum())
+        c4["verified"] = {"rows": 1 << 16, "mismatches": bad, "what": "the first 65,536 rows of k=8"}
+    finally:
+        T4.close()
+        T6.close()
+    res["config4"] = c4
+    del fam
+    # config 5: a 10M-peer swarm of shape-K tables, 1M iterative lookups to convergence (all peers online)
+    ids, _ = S.sort_ids(S.random_ids(10_000_000, 0x0D470500))
+    t0 = time.perf_counter()
+    Wm = Swarm(ids, device=dev.index or 0)
+    torch.cuda.synchronize(dev)
+    build_s = time.perf_counter() - t0
+    try:
+        rng = np.random.default_rng(9)
+        L = 1 << 20
+        src = torch.from_numpy(rng.integers(0, ids.shape[0], L).astype(np.int32)).to(dev)
+        tgt = torch.from_numpy(S.random_targets(L, seed=0x0D470501)).to(dev)
+        X = Wm.search(src[:4096], tgt[:4096])
+        X.run()
+        X.close()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        X = Wm.search(src, tgt)
+        X.run()
+        torch.cuda.synchronize(dev)
+        run_s = time.perf_counter() - t0
+        lst, q, bad_, n, hops, done, ovf = X.get(full=True)
+        X.close()
+        res["config5"] = {"what": "10,000,000 peers (shape-K tables in HBM, dht.cpp:867-936 policy), 1,048,576 "
+                                  "lookups from random sources, alpha 4, list 14, all peers online",
+                          "table_build_s": build_s, "lookups_per_s": L / run_s, "ms": run_s * 1e3,
+                          "mean_hops": float(hops.mean()), "synced_frac": float((done == 1).mean()),
+                          "table_GB": Wm.device_bytes() / 1e9}
+    finally:
+        Wm.close()
+    torch.cuda.empty_cache()
     return res
 
 
