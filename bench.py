@@ -635,9 +635,9 @@ def latency_pass(dev, nodes=170, reps=2000):
 
 
 def configs_pass(dev, reps=10):
-    """BASELINE.json's other configs, measured beside the headline (config 3) on the same GPU: the launch time
-    (median of `reps` launches between HIP events, rotated target batches) and the rows checked against the CPU
-    restatement (oracle/, the checker). config 1: the reference's own CPU-runnable case, with the structure-faithful
+    """BASELINE.json's other configs, measured beside the headline (config 3) on the same GPU: the device time per
+    launch (`reps` launches over rotated target batches captured as one HIP graph) and the rows checked against the
+    CPU restatement (oracle/, the checker). config 1: the reference's own CPU-runnable case, with the structure-faithful
     port timed on the same targets; config 5: the swarm model (opendht_amd/csrc/kad_swarm.hip)."""
     import torch
 
@@ -649,14 +649,26 @@ def configs_pass(dev, reps=10):
     import oracle as O
 
     def med_ms(fn, n=reps):
+        """Device time per call: n calls captured as one HIP graph (no host gaps between launches; the calls'
+        line sets are built by a call before the capture), the replay timed with HIP events; the median of 3."""
+        cs = torch.cuda.Stream(dev)
+        fn(0, cs.cuda_stream)
+        torch.cuda.synchronize(dev)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=cs):
+            for r in range(n):
+                fn(r, cs.cuda_stream)
+        g.replay()
+        torch.cuda.synchronize(dev)
         ts = []
-        for r in range(n):
+        for _ in range(3):
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            a.record()
-            fn(r)
+            a.record()  # the replay runs on the current stream
+            g.replay()
             b.record()
             b.synchronize()
-            ts.append(a.elapsed_time(b))
+            ts.append(a.elapsed_time(b) / n)
+        del g
         return float(np.median(ts))
 
     def uniform(n, depth, seed):
@@ -675,7 +687,7 @@ def configs_pass(dev, reps=10):
     with DeviceTable(ids, st, first, off, device=dev.index or 0) as T:
         d = torch.from_numpy(tg).to(dev)
         idx, cnt = T.rt_closest(d, 8)
-        ms = med_ms(lambda r: T.rt_closest(d, 8, idx, cnt))
+        ms = med_ms(lambda r, st: T.rt_closest(d, 8, idx, cnt, stream=st))
         want, wcnt = O.flat_rt_closest(ids, st, first, off, tg, 8)
         bad = int((idx.cpu().numpy().view(np.uint32) != want).any(1).sum() + (cnt.cpu().numpy() != wcnt).sum())
     F = O.FaithfulTable(ids, st, first, off)
@@ -692,7 +704,7 @@ def configs_pass(dev, reps=10):
         tgs = [S.random_targets(1 << 16, seed=S.SEED_TARGETS + j) for j in range(4)]
         ds = [torch.from_numpy(x).to(dev) for x in tgs]
         idx, cnt = T.rt_closest(ds[0], 8)
-        ms = med_ms(lambda r: T.rt_closest(ds[r % 4], 8, idx, cnt))
+        ms = med_ms(lambda r, st: T.rt_closest(ds[r % 4], 8, idx, cnt, stream=st))
         T.rt_closest(ds[0], 8, idx, cnt)
         want, wcnt = O.flat_rt_closest(ids, st, first, off, tgs[0], 8, nthreads=all_cores())
         bad = int((idx.cpu().numpy().view(np.uint32) != want).any(1).sum() + (cnt.cpu().numpy() != wcnt).sum())
@@ -701,19 +713,19 @@ def configs_pass(dev, reps=10):
     # config 4: v4 and v6 tables of 1M nodes each, 1M queries with af alternating, k = 8 / 16 / 32 and NodeCache 14
     fam = [uniform(1_000_000, 17, seed) for seed in (0xC4F4, 0xC4F6)]
     Q = 1 << 20
-    tg = S.random_targets(Q, seed=0x0D4704C4)
+    tgb = [S.random_targets(Q, seed=0x0D4704C4 + j) for j in range(4)]
+    tg = tgb[0]
     af = (np.arange(Q) % 2).astype(np.uint8)
     c4 = {"what": "v4 + v6 tables of 1,000,000 nodes each (U(17), 80/10/10 good/expired/dubious), 1,048,576 queries, "
-                  "af alternating (Dht::onGetValues asks both families, dht.cpp:3216-3217)"}
+                  "af alternating (Dht::onGetValues asks both families, dht.cpp:3216-3217), 4 rotated target batches"}
     T4 = DeviceTable(*fam[0], device=dev.index or 0, sorted=True)
     T6 = DeviceTable(*fam[1], device=dev.index or 0, sorted=True)
     try:
-        d, da = torch.from_numpy(tg).to(dev), torch.from_numpy(af).to(dev)
+        db, da = [torch.from_numpy(x).to(dev) for x in tgb], torch.from_numpy(af).to(dev)
+        d = db[0]
         for k in (8, 16, 32):
-            rt_closest_dual(T4, T6, d, da, k)
-            c4[f"rt_k{k}_us"] = med_ms(lambda r: rt_closest_dual(T4, T6, d, da, k)) * 1e3
-        nc_closest_dual(T4, T6, d, da, 14)
-        c4["nc_k14_us"] = med_ms(lambda r: nc_closest_dual(T4, T6, d, da, 14)) * 1e3
+            c4[f"rt_k{k}_us"] = med_ms(lambda r, st: rt_closest_dual(T4, T6, db[r % 4], da, k, stream=st)) * 1e3
+        c4["nc_k14_us"] = med_ms(lambda r, st: nc_closest_dual(T4, T6, db[r % 4], da, 14, stream=st)) * 1e3
         idx, cnt = rt_closest_dual(T4, T6, d, da, 8)
         idx, cnt = idx.cpu().numpy().view(np.uint32), cnt.cpu().numpy()
         bad = 0

@@ -2750,9 +2750,12 @@ __global__ __launch_bounds__(BLOCK) void rt_closest_dual_kernel(DevTable T4, Dev
 
 // Dual-family batch for count <= 8 where a family has window lines: per lane the family's table,
 // its window line when it has lines, the lane fast path otherwise, then the exact path per family.
-__global__ __launch_bounds__(BLOCK) void rt_dual_wl_kernel(DevTable T4, DevTable T6, const uint8_t* __restrict__ targets,
-                                                           const uint8_t* __restrict__ af, uint32_t q, uint32_t count,
-                                                           uint32_t* __restrict__ out_idx, uint8_t* __restrict__ out_cnt) {
+// LEAN (both families have the lines or are empty, as in config 4): no lane fast path compiled in (its registers
+// cost occupancy), an empty family's queries get empty rows.
+template <bool LEAN>
+__device__ __forceinline__ void rt_dual_wl_body(const DevTable& T4, const DevTable& T6, const uint8_t* __restrict__ targets,
+                                                const uint8_t* __restrict__ af, uint32_t q, uint32_t count,
+                                                uint32_t* __restrict__ out_idx, uint8_t* __restrict__ out_cnt) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     const bool act = i < q && count > 0;
     if (i < q && count == 0 && out_cnt) out_cnt[i] = 0;
@@ -2773,11 +2776,26 @@ __global__ __launch_bounds__(BLOCK) void rt_dual_wl_kernel(DevTable T4, DevTable
         store_row8(row, o, count);
         if (out_cnt) out_cnt[i] = (uint8_t)m;
     } else if (act && !wl) {
-        ex = !rt_query_fast<8, 3>(T, t, count, row, out_cnt ? out_cnt + i : nullptr);
+        if (LEAN) {  // an empty family (routing_table.cpp:73)
+            for (uint32_t s = 0; s < count; s++) row[s] = NONE;
+            if (out_cnt) out_cnt[i] = 0;
+        } else {
+            ex = !rt_query_fast<8, 3>(T, t, count, row, out_cnt ? out_cnt + i : nullptr);
+        }
     }
     __shared__ uint64_t xs[BLOCK / 64][192];
     exact_tail(T4, t, ex && !six, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
     exact_tail(T6, t, ex && six, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
+}
+__global__ __launch_bounds__(BLOCK) void rt_dual_wl_kernel(DevTable T4, DevTable T6, const uint8_t* __restrict__ targets,
+                                                           const uint8_t* __restrict__ af, uint32_t q, uint32_t count,
+                                                           uint32_t* __restrict__ out_idx, uint8_t* __restrict__ out_cnt) {
+    rt_dual_wl_body<false>(T4, T6, targets, af, q, count, out_idx, out_cnt);
+}
+__global__ __launch_bounds__(BLOCK) void rt_dual_wl_lean_kernel(
+    DevTable T4, DevTable T6, const uint8_t* __restrict__ targets, const uint8_t* __restrict__ af, uint32_t q,
+    uint32_t count, uint32_t* __restrict__ out_idx, uint8_t* __restrict__ out_cnt) {
+    rt_dual_wl_body<true>(T4, T6, targets, af, q, count, out_idx, out_cnt);
 }
 
 // Dual-family batch (af per query) for families with general window lines (split-policy tables, the shape the
@@ -2818,12 +2836,14 @@ __global__ __launch_bounds__(BLOCK) void rt_dual_gl_kernel(DevTable T4, DevTable
     exact_tail(T6, t, ex && six, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
 }
 
-// Dual-family batch for counts 9..16 where a family has 16-slot window lines (same structure).
-__global__ __launch_bounds__(BLOCK) void rt_dual_wl16_kernel(DevTable T4, DevTable T6,
-                                                             const uint8_t* __restrict__ targets,
-                                                             const uint8_t* __restrict__ af, uint32_t q, uint32_t count,
-                                                             uint32_t* __restrict__ out_idx,
-                                                             uint8_t* __restrict__ out_cnt) {
+// Dual-family batch for counts 9..16 where a family has 16-slot window lines (same structure). LEAN: rows through
+// LDS as coalesced 16-byte stores (store_rows_block, as rt_wl16_kernel) and no lane fast path.
+template <bool LEAN>
+__device__ __forceinline__ void rt_dual_wl16_body(const DevTable& T4, const DevTable& T6,
+                                                  const uint8_t* __restrict__ targets,
+                                                  const uint8_t* __restrict__ af, uint32_t q, uint32_t count,
+                                                  uint32_t* __restrict__ out_idx,
+                                                  uint8_t* __restrict__ out_cnt) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     const bool act = i < q;
     Target t{};
@@ -2839,7 +2859,14 @@ __global__ __launch_bounds__(BLOCK) void rt_dual_wl16_kernel(DevTable T4, DevTab
     const bool ok = wl16_answer(T, t, b, count, wl, o, m);
     uint32_t* row = out_idx + (size_t)i * count;
     bool ex = wl && !ok;
-    if (wl && ok) {
+    if (LEAN) {
+        if (wl && ok && out_cnt) out_cnt[i] = (uint8_t)m;
+        store_rows_block<16>(out_idx, q, count, o, wl && ok);
+        if (act && !wl) {  // an empty family (routing_table.cpp:73)
+            for (uint32_t s = 0; s < count; s++) row[s] = NONE;
+            if (out_cnt) out_cnt[i] = 0;
+        }
+    } else if (wl && ok) {
         store_row16(row, o, count);
         if (out_cnt) out_cnt[i] = (uint8_t)m;
     } else if (act && !wl) {
@@ -2866,8 +2893,16 @@ __global__ __launch_bounds__(BLOCK) void rt_dual_wl16_kernel(DevTable T4, DevTab
     exact_tail(T4, t, ex && !six, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
     exact_tail(T6, t, ex && six, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
 }
+template <bool LEAN>
+__global__ __launch_bounds__(BLOCK) void rt_dual_wl16_kernel(DevTable T4, DevTable T6, const uint8_t* __restrict__ targets,
+                                                             const uint8_t* __restrict__ af, uint32_t q, uint32_t count,
+                                                             uint32_t* __restrict__ out_idx, uint8_t* __restrict__ out_cnt) {
+    rt_dual_wl16_body<LEAN>(T4, T6, targets, af, q, count, out_idx, out_cnt);
+}
 
-// Dual-family batch for counts 17..32 where a family has 64-slot window lines (same structure).
+// Dual-family batch for counts 17..32 where a family has 64-slot window lines (same structure). LEAN: no lane fast
+// path compiled in.
+template <bool LEAN>
 __global__ __launch_bounds__(BLOCK) void rt_dual_wl32_kernel(DevTable T4, DevTable T6,
                                                              const uint8_t* __restrict__ targets,
                                                              const uint8_t* __restrict__ af, uint32_t q, uint32_t count,
@@ -2892,8 +2927,69 @@ __global__ __launch_bounds__(BLOCK) void rt_dual_wl32_kernel(DevTable T4, DevTab
         store_row32(row, o, count);
         if (out_cnt) out_cnt[i] = (uint8_t)m;
     } else if (act && !wl) {
-        ex = !rt_query_fast<32, 6>(T, t, count, row, out_cnt ? out_cnt + i : nullptr);
+        if (LEAN) {  // an empty family (routing_table.cpp:73)
+            for (uint32_t s = 0; s < count; s++) row[s] = NONE;
+            if (out_cnt) out_cnt[i] = 0;
+        } else {
+            ex = !rt_query_fast<32, 6>(T, t, count, row, out_cnt ? out_cnt + i : nullptr);
+        }
     }
+    __shared__ uint64_t xs[BLOCK / 64][192];
+    exact_tail(T4, t, ex && !six, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
+    exact_tail(T6, t, ex && six, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
+}
+
+// Dual-family counts 24, 28, 32 (both families with 64-slot lines or empty): rt_wl32q_kernel's four lanes per
+// query and per-quad LDS row store, the family per quad.
+__global__ __launch_bounds__(BLOCK) void rt_dual_wl32q_kernel(DevTable T4, DevTable T6, const uint8_t* __restrict__ targets,
+                                                              const uint8_t* __restrict__ af, uint32_t q, uint32_t count,
+                                                              uint32_t* __restrict__ out_idx,
+                                                              uint8_t* __restrict__ out_cnt) {
+    const uint32_t g = blockIdx.x * BLOCK + threadIdx.x, i = g >> 2, p = g & 3u;
+    const bool act = i < q;
+    Target t{};
+    bool six = false;
+    if (act) {
+        t = load_target(targets, i);
+        six = af[i] != 0;
+    }
+    const DevTable& T = six ? T6 : T4;  // quad-uniform
+    const bool wl = act && (T.flags & TF_WL32);
+    const uint32_t b = wl ? locate_bucket(T, t) : 0u;
+    uint32_t v[16], m, base;
+    const bool ok = wl32_answer4<true>(T, t, b, count, wl, p, v, m, base);
+    const uint32_t r0 = 16u * (p & 1u), bi = base + T.index_base;
+    uint32_t o[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) o[k] = r0 + k < m ? bi + (v[k] & 255u) : NONE;
+    if (wl && ok && p == 0 && out_cnt) out_cnt[i] = (uint8_t)m;
+    __shared__ uint4 qrow[BLOCK / 4][9];  // per quad: 32 entries + a 16-byte pad
+    uint32_t* R = reinterpret_cast<uint32_t*>(qrow[threadIdx.x >> 2]);
+    if (p < 2u) {
+#pragma unroll
+        for (int x = 0; x < 4; x++)
+            reinterpret_cast<uint4*>(R + 16u * p)[x] = make_uint4(o[4 * x], o[4 * x + 1], o[4 * x + 2], o[4 * x + 3]);
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    uint32_t* row = out_idx + (size_t)i * count;
+    if (wl && ok) {
+        if ((count & 3u) == 0 && ((uintptr_t)out_idx & 15u) == 0) {
+#pragma unroll
+            for (int h = 0; h < 2; h++)
+                if (16u * h + 4u * p < count)
+                    reinterpret_cast<uint4*>(row)[4 * h + p] = reinterpret_cast<const uint4*>(R)[4 * h + p];
+        } else {
+#pragma unroll
+            for (int j = 0; j < 8; j++)
+                if (4u * j + p < count) row[4 * j + p] = R[4 * j + p];
+        }
+    } else if (act && !wl) {  // an empty family (routing_table.cpp:73)
+        for (uint32_t j = p; j < count; j += 4) row[j] = NONE;
+        if (p == 0 && out_cnt) out_cnt[i] = 0;
+    }
+    const bool ex = wl && !ok && p == 0u;
     __shared__ uint64_t xs[BLOCK / 64][192];
     exact_tail(T4, t, ex && !six, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
     exact_tail(T6, t, ex && six, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
@@ -6559,9 +6655,14 @@ int kad_rt_closest_batch_dual(const kad_table* t4, const kad_table* t6, const ui
         int rc;
         if ((t4 && (rc = ensure_lines(t4, need, s))) || (t6 && (rc = ensure_lines(t6, need, s)))) return rc;
     }
+    // LEAN kernels where every family has the line set the count needs or is empty (config 4's two uniform tables)
+    auto lean = [&](uint32_t f) { return (d4.B == 0 || (d4.flags & f)) && (d6.B == 0 || (d6.flags & f)); };
     if (count > KAD_MAX_COUNT)
         hipLaunchKernelGGL(rt_wave_kernel, dim3((q + BLOCK / 64 - 1) / (BLOCK / 64)), dim3(BLOCK), 0, s, d4, d6, af,
                            targets, q, count, out_idx, out_cnt);
+    else if (count <= 8 && ((d4.flags | d6.flags) & TF_WL) && lean(TF_WL))
+        hipLaunchKernelGGL(rt_dual_wl_lean_kernel, dim3(grid_for(q)), dim3(BLOCK), 0, s, d4, d6, targets, af, q, count,
+                           out_idx, out_cnt);
     else if (count <= 8 && ((d4.flags | d6.flags) & TF_WL))
         hipLaunchKernelGGL(rt_dual_wl_kernel, dim3(grid_for(q)), dim3(BLOCK), 0, s, d4, d6, targets, af, q, count,
                            out_idx, out_cnt);
@@ -6569,16 +6670,25 @@ int kad_rt_closest_batch_dual(const kad_table* t4, const kad_table* t6, const ui
         hipLaunchKernelGGL(rt_dual_gl_kernel<8>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d4, d6, targets, af, q, count,
                            out_idx, out_cnt);
     else if (count <= 8) launch_rt_dual<8>(d4, d6, targets, af, q, count, out_idx, out_cnt, s);
+    else if (count <= 16 && ((d4.flags | d6.flags) & TF_WL16) && lean(TF_WL16))
+        hipLaunchKernelGGL(rt_dual_wl16_kernel<true>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d4, d6, targets, af, q,
+                           count, out_idx, out_cnt);
     else if (count <= 16 && ((d4.flags | d6.flags) & TF_WL16))
-        hipLaunchKernelGGL(rt_dual_wl16_kernel, dim3(grid_for(q)), dim3(BLOCK), 0, s, d4, d6, targets, af, q, count,
-                           out_idx, out_cnt);
+        hipLaunchKernelGGL(rt_dual_wl16_kernel<false>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d4, d6, targets, af, q,
+                           count, out_idx, out_cnt);
     else if (count <= 16 && ((d4.flags | d6.flags) & TF_GL16))
         hipLaunchKernelGGL(rt_dual_gl_kernel<16>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d4, d6, targets, af, q, count,
                            out_idx, out_cnt);
     else if (count <= 16) launch_rt_dual<16>(d4, d6, targets, af, q, count, out_idx, out_cnt, s);
+    else if (((d4.flags | d6.flags) & TF_WL32) && lean(TF_WL32) && count >= 24 && (count & 3u) == 0)
+        hipLaunchKernelGGL(rt_dual_wl32q_kernel, dim3(grid_for(4ull * q)), dim3(BLOCK), 0, s, d4, d6, targets, af, q,
+                           count, out_idx, out_cnt);
+    else if (((d4.flags | d6.flags) & TF_WL32) && lean(TF_WL32))
+        hipLaunchKernelGGL(rt_dual_wl32_kernel<true>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d4, d6, targets, af, q,
+                           count, out_idx, out_cnt);
     else if ((d4.flags | d6.flags) & TF_WL32)
-        hipLaunchKernelGGL(rt_dual_wl32_kernel, dim3(grid_for(q)), dim3(BLOCK), 0, s, d4, d6, targets, af, q, count,
-                           out_idx, out_cnt);
+        hipLaunchKernelGGL(rt_dual_wl32_kernel<false>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d4, d6, targets, af, q,
+                           count, out_idx, out_cnt);
     else if ((d4.flags | d6.flags) & TF_GL32)
         hipLaunchKernelGGL(rt_dual_gl_kernel<32>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d4, d6, targets, af, q, count,
                            out_idx, out_cnt);
