@@ -166,6 +166,25 @@ __device__ __forceinline__ uint64_t load_target_hi(const uint8_t* targets, uint3
     return ((uint64_t)__builtin_bswap32(p[0]) << 32) | __builtin_bswap32(p[1]);
 }
 
+// Result rows leave with the non-temporal policy: written once, they would otherwise displace the line tables from
+// the Infinity Cache (the headline kernel: 32.7 -> 31.8 us per 1M, profiles/r03/ab_ws_nts/). KAD_PLAIN_STREAMS (an
+// A/B build of the tools, like KAD_ABLATIONS) keeps the plain policy.
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void st_row4(uint32_t* p, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+#ifdef KAD_PLAIN_STREAMS
+    *reinterpret_cast<uint4*>(p) = make_uint4(a, b, c, d);
+#else
+    __builtin_nontemporal_store(u32x4_t{a, b, c, d}, reinterpret_cast<u32x4_t*>(p));
+#endif
+}
+__device__ __forceinline__ void st_row1(uint32_t* p, uint32_t v) {
+#ifdef KAD_PLAIN_STREAMS
+    *p = v;
+#else
+    __builtin_nontemporal_store(v, p);
+#endif
+}
+
 // 160-bit compare of (hi, a2, a3, a4) vs (hi', b2, b3, b4): returns <0, 0, >0
 __device__ __forceinline__ int cmp160(uint64_t ah, uint32_t a2, uint32_t a3, uint32_t a4,
                                       uint64_t bh, uint32_t b2, uint32_t b3, uint32_t b4) {
@@ -1196,7 +1215,10 @@ __device__ __forceinline__ bool ws_answer(const DevTable& T, const Target& t, ui
 // ABL 1 = no fallback and no exact path, 2 = also no ranking, 3 = fallback but no exact path (timing ablations
 // only); 4 = path statistics: out_cnt = 100 + m for queries answered by the 128-byte line, 250 for the exact path;
 // 5 = the exact path compiled in but never taken.
-template <int ABL>
+// NTS: the streams (targets in, rows out) with the non-temporal policy, so that they do not displace the line table
+// from the Infinity Cache: 32.7 -> 31.8 us per 1M on the bench shard, 3 interleaved bench runs each
+// (profiles/r03/ab_ws_nts/). The launch path's default; the service (rows into host memory) keeps the plain policy.
+template <int ABL, bool NTS = false>
 __device__ __forceinline__ void rt_ws_kernel_body(const DevTable& T, const uint8_t* __restrict__ targets, uint32_t q,
                                                       uint32_t count, uint32_t* __restrict__ out_idx,
                                                       uint8_t* __restrict__ out_cnt) {
@@ -1208,13 +1230,24 @@ __device__ __forceinline__ void rt_ws_kernel_body(const DevTable& T, const uint8
     Target t{};
     uint32_t b = 0;
     if (act) {
-        t.hi = load_target_hi(targets, i);
+        if (NTS) {
+            const uint64_t w = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(targets + 20ull * i));
+            t.hi = ((uint64_t)__builtin_bswap32((uint32_t)w) << 32) | __builtin_bswap32((uint32_t)(w >> 32));
+        } else {
+            t.hi = load_target_hi(targets, i);
+        }
         b = locate_bucket(T, t);
     }
     uint32_t o[8], m;
     const bool ok = ws_answer<ABL>(T, t, b, count, act, o, m);
     if (act && ok) {
-        store_row8(out_idx + (size_t)i * count, o, count);
+        if (NTS && count == 8 && ((uintptr_t)out_idx & 15u) == 0) {
+            u32x4_t* r = reinterpret_cast<u32x4_t*>(out_idx + (size_t)i * 8u);
+            __builtin_nontemporal_store(u32x4_t{o[0], o[1], o[2], o[3]}, r);
+            __builtin_nontemporal_store(u32x4_t{o[4], o[5], o[6], o[7]}, r + 1);
+        } else {
+            store_row8(out_idx + (size_t)i * count, o, count);
+        }
         if (out_cnt) out_cnt[i] = (uint8_t)m;
     }
     bool need = (ABL == 0 || ABL >= 3) && act && !ok;
@@ -1236,11 +1269,11 @@ __device__ __forceinline__ void rt_ws_kernel_body(const DevTable& T, const uint8
         if (ABL == 4 && need && out_cnt) out_cnt[i] = 250;
     }
 }
-template <int ABL>
+template <int ABL, bool NTS = false>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) void rt_ws_kernel(DevTable T, const uint8_t* __restrict__ targets, uint32_t q,
                                                       uint32_t count, uint32_t* __restrict__ out_idx,
                                                       uint8_t* __restrict__ out_cnt) {
-    rt_ws_kernel_body<ABL>(T, targets, q, count, out_idx, out_cnt);
+    rt_ws_kernel_body<ABL, NTS>(T, targets, q, count, out_idx, out_cnt);
 }
 
 // The count <= 8 line answer for kernels that serve other paths too (dual-family, shard): lanes with `ws`
@@ -1409,11 +1442,11 @@ __device__ __forceinline__ void store_rows_block(uint32_t* __restrict__ out_idx,
         const uint32_t r0 = w0 / count, r1 = min(w0 + 3, nw - 1) / count;
         const bool ok0 = (okm[r0 >> 5] >> (r0 & 31)) & 1u, ok1 = (okm[r1 >> 5] >> (r1 & 31)) & 1u;
         if (ok0 && ok1 && w0 + 4 <= nw && (((uintptr_t)out_idx & 15u) == 0)) {
-            reinterpret_cast<uint4*>(dst)[c] = make_uint4(rows[w0], rows[w0 + 1], rows[w0 + 2], rows[w0 + 3]);
+            st_row4(dst + w0, rows[w0], rows[w0 + 1], rows[w0 + 2], rows[w0 + 3]);
         } else {
             for (uint32_t w = w0; w < min(w0 + 4, nw); w++) {
                 const uint32_t r = w / count;
-                if ((okm[r >> 5] >> (r & 31)) & 1u) dst[w] = rows[w];
+                if ((okm[r >> 5] >> (r & 31)) & 1u) st_row1(dst + w, rows[w]);
             }
         }
     }
@@ -1859,11 +1892,11 @@ __device__ __forceinline__ void store_rows_quad(uint32_t* __restrict__ out_idx, 
         const uint32_t ra = w0 / count, rb = min(w0 + 3, nw - 1) / count;
         const bool oka = (okm[ra >> 5] >> (ra & 31)) & 1u, okb = (okm[rb >> 5] >> (rb & 31)) & 1u;
         if (oka && okb && w0 + 4 <= nw && (((uintptr_t)out_idx & 15u) == 0)) {
-            reinterpret_cast<uint4*>(dst)[c] = make_uint4(rows[w0], rows[w0 + 1], rows[w0 + 2], rows[w0 + 3]);
+            st_row4(dst + w0, rows[w0], rows[w0 + 1], rows[w0 + 2], rows[w0 + 3]);
         } else {
             for (uint32_t w = w0; w < min(w0 + 4, nw); w++) {
                 const uint32_t r = w / count;
-                if ((okm[r >> 5] >> (r & 31)) & 1u) dst[w] = rows[w];
+                if ((okm[r >> 5] >> (r & 31)) & 1u) st_row1(dst + w, rows[w]);
             }
         }
     }
@@ -1909,11 +1942,12 @@ __global__ __launch_bounds__(BLOCK) void rt_wl32q_kernel(DevTable T, const uint8
 #pragma unroll
                 for (int h = 0; h < 2; h++)
                     if (16u * h + 4u * p < count)
-                        reinterpret_cast<uint4*>(row)[4 * h + p] = reinterpret_cast<const uint4*>(R)[4 * h + p];
+                        st_row4(row + 16 * h + 4 * p, R[16 * h + 4 * p], R[16 * h + 4 * p + 1], R[16 * h + 4 * p + 2],
+                                R[16 * h + 4 * p + 3]);
             } else {
 #pragma unroll
                 for (int j = 0; j < 8; j++)
-                    if (4u * j + p < count) row[4 * j + p] = R[4 * j + p];
+                    if (4u * j + p < count) st_row1(row + 4 * j + p, R[4 * j + p]);
             }
         }
     } else if ((count & 3u) == 0 && ((uintptr_t)out_idx & 15u) == 0) {  // lanes 0 and 1 store 16-byte pieces
@@ -2979,11 +3013,12 @@ __global__ __launch_bounds__(BLOCK) void rt_dual_wl32q_kernel(DevTable T4, DevTa
 #pragma unroll
             for (int h = 0; h < 2; h++)
                 if (16u * h + 4u * p < count)
-                    reinterpret_cast<uint4*>(row)[4 * h + p] = reinterpret_cast<const uint4*>(R)[4 * h + p];
+                    st_row4(row + 16 * h + 4 * p, R[16 * h + 4 * p], R[16 * h + 4 * p + 1], R[16 * h + 4 * p + 2],
+                            R[16 * h + 4 * p + 3]);
         } else {
 #pragma unroll
             for (int j = 0; j < 8; j++)
-                if (4u * j + p < count) row[4 * j + p] = R[4 * j + p];
+                if (4u * j + p < count) st_row1(row + 4 * j + p, R[4 * j + p]);
         }
     } else if (act && !wl) {  // an empty family (routing_table.cpp:73)
         for (uint32_t j = p; j < count; j += 4) row[j] = NONE;
@@ -4055,11 +4090,11 @@ __device__ __forceinline__ void store_rows_lds16(uint32_t* __restrict__ out_idx,
             if (++c == count) { c = 0; r++; }
         }
         if (al && okv[0] && okv[1] && okv[2] && okv[3]) {
-            reinterpret_cast<uint4*>(dst)[c4] = make_uint4(v[0], v[1], v[2], v[3]);
+            st_row4(dst + w0, v[0], v[1], v[2], v[3]);
         } else {
 #pragma unroll
             for (int u = 0; u < 4; u++)
-                if (okv[u]) dst[w0 + u] = v[u];
+                if (okv[u]) st_row1(dst + w0 + u, v[u]);
         }
     }
 }
@@ -4086,11 +4121,11 @@ __device__ __forceinline__ void store_rows_wave16(uint32_t* __restrict__ out_idx
             if (++c == count) { c = 0; r++; }
         }
         if (al && okv[0] && okv[1] && okv[2] && okv[3]) {
-            reinterpret_cast<uint4*>(dst)[c4] = make_uint4(v[0], v[1], v[2], v[3]);
+            st_row4(dst + w0, v[0], v[1], v[2], v[3]);
         } else {
 #pragma unroll
             for (int u = 0; u < 4; u++)
-                if (okv[u]) dst[w0 + u] = v[u];
+                if (okv[u]) st_row1(dst + w0 + u, v[u]);
         }
     }
 }
@@ -4498,11 +4533,11 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) v
         if (ok) {
             uint32_t* row = out_idx + (size_t)qi * count;
             if ((count & 3u) == 0 && ((uintptr_t)out_idx & 15u) == 0) {
-                if (4 * g < count) reinterpret_cast<uint4*>(row)[g] = make_uint4(W[4 * g], W[4 * g + 1], W[4 * g + 2], W[4 * g + 3]);
+                if (4 * g < count) st_row4(row + 4 * g, W[4 * g], W[4 * g + 1], W[4 * g + 2], W[4 * g + 3]);
             } else {
 #pragma unroll
                 for (int j = 0; j < 4; j++)
-                    if (4 * g + j < count) row[4 * g + j] = W[4 * g + j];
+                    if (4 * g + j < count) st_row1(row + 4 * g + j, W[4 * g + j]);
             }
             if (g == 0 && out_cnt) out_cnt[qi] = (uint8_t)count;
         }
@@ -6104,7 +6139,11 @@ int launch_rt(const kad_table* t, const uint8_t* targets, uint32_t q, uint32_t c
             hipLaunchKernelGGL(rt_ws_kernel<4>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
         else
 #endif
+        if (ev && std::strcmp(ev, "ws_plain") == 0)  // A/B: the streams with the plain policy
             hipLaunchKernelGGL(rt_ws_kernel<0>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
+        else
+            hipLaunchKernelGGL((rt_ws_kernel<0, true>), dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out,
+                               cnt);
     } else if (K == 8 && (d.flags & TF_WL) && !(ev && std::strcmp(ev, "lane") == 0)) {
 #ifdef KAD_ABLATIONS  // timing ablations with WRONG results: only in the tools build (Makefile target `ablations`)
         if (ev && std::strcmp(ev, "wl_abl1") == 0)
