@@ -149,21 +149,35 @@ struct LineSel {
     }
 };
 
+// Target batches are read once: non-temporal loads (as the rows, st_row4 below), two 8-byte and one 4-byte load (two
+// 4-byte non-temporal loads may be merged into one plain 8-byte load). KAD_PLAIN_STREAMS: the plain policy.
 __device__ __forceinline__ Target load_target(const uint8_t* targets, uint32_t i) {
     const uint32_t* p = reinterpret_cast<const uint32_t*>(targets + 20ull * i);
     Target t;
-    uint32_t w0 = __builtin_bswap32(p[0]), w1 = __builtin_bswap32(p[1]);
-    t.hi = ((uint64_t)w0 << 32) | w1;
-    t.t2 = __builtin_bswap32(p[2]);
-    t.t3 = __builtin_bswap32(p[3]);
-    t.t4 = __builtin_bswap32(p[4]);
+#ifdef KAD_PLAIN_STREAMS
+    const uint32_t w0 = p[0], w1 = p[1], w2 = p[2], w3 = p[3], w4 = p[4];
+#else
+    const uint64_t a = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(p));
+    const uint64_t b = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(p + 2));
+    const uint32_t w0 = (uint32_t)a, w1 = (uint32_t)(a >> 32), w2 = (uint32_t)b, w3 = (uint32_t)(b >> 32);
+    const uint32_t w4 = __builtin_nontemporal_load(p + 4);
+#endif
+    t.hi = ((uint64_t)__builtin_bswap32(w0) << 32) | __builtin_bswap32(w1);
+    t.t2 = __builtin_bswap32(w2);
+    t.t3 = __builtin_bswap32(w3);
+    t.t4 = __builtin_bswap32(w4);
     return t;
 }
 
 // The top 64 bits of target i (direct-mapped tables locate with these alone).
 __device__ __forceinline__ uint64_t load_target_hi(const uint8_t* targets, uint32_t i) {
+#ifdef KAD_PLAIN_STREAMS
     const uint32_t* p = reinterpret_cast<const uint32_t*>(targets + 20ull * i);
     return ((uint64_t)__builtin_bswap32(p[0]) << 32) | __builtin_bswap32(p[1]);
+#else
+    const uint64_t w = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(targets + 20ull * i));
+    return ((uint64_t)__builtin_bswap32((uint32_t)w) << 32) | __builtin_bswap32((uint32_t)(w >> 32));
+#endif
 }
 
 // Result rows leave with the non-temporal policy: written once, they would otherwise displace the line tables from
@@ -1230,12 +1244,7 @@ __device__ __forceinline__ void rt_ws_kernel_body(const DevTable& T, const uint8
     Target t{};
     uint32_t b = 0;
     if (act) {
-        if (NTS) {
-            const uint64_t w = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(targets + 20ull * i));
-            t.hi = ((uint64_t)__builtin_bswap32((uint32_t)w) << 32) | __builtin_bswap32((uint32_t)(w >> 32));
-        } else {
-            t.hi = load_target_hi(targets, i);
-        }
+        t.hi = load_target_hi(targets, i);
         b = locate_bucket(T, t);
     }
     uint32_t o[8], m;
