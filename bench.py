@@ -58,7 +58,7 @@ def parse_args(argv=None):
     ap.add_argument("--no-allgather", action="store_true")
     ap.add_argument("--no-graph", action="store_true", help="issue the K steps one by one instead of one HIP graph")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r03.json"))
-    ap.add_argument("--gather-json", default=os.path.join(ROOT, "profiles", "r02_mb_gather.json"))
+    ap.add_argument("--gather-json", default=os.path.join(ROOT, "profiles", "r03_mb_gather_nt.json"))
     ap.add_argument("--plumbing", action="store_true",
                     help="launcher/rendezvous check without a GPU: gloo ranks, barrier, max-over-ranks, one line")
     ap.add_argument("--mode", choices=("owner", "allgather", "allgather-child"), default="owner",
@@ -402,8 +402,9 @@ def main_owner(args):
         row = "128MB_64B" if line_b == 64 else "256MB_128B"
         a = gath.get("all", {})
         if row in a and row + "_cold" in a:
-            ceil = {"what": f"random {line_b}-byte line gather + 20 B target read + 32 B row write per query, 1M "
-                            "queries per launch, rotated batches (tools/mb_gather.py)",
+            ceil = {"what": f"random {line_b}-byte line gather + 20 B target read + 32 B row write per query (the "
+                            "streams non-temporal, as the kernel's), 1M queries per launch, rotated batches "
+                            "(tools/mb_gather_nt.py)",
                     "table_MB": int(row.split("MB")[0]), "line_bytes": line_b,
                     "us_per_1M_rotated": a[row]["us_per_1M"], "us_per_1M_cold": a[row + "_cold"]["us_per_1M"]}
 

@@ -62,17 +62,22 @@ def run(tab, nbytes, nx, reps, cold=False, coop=0):
     return ts[len(ts) // 2]
 
 
-res = {}
-for mb in (128, 256, 512, 1024, 2048, 4096):
-    tab = torch.randint(0, 1 << 30, ((mb << 20) // 4,), dtype=torch.int32, device=dev)
-    for nx, coop in ((1, 0), (2, 0), (4, 0), (8, 0), (8, 1), (16, 0)):
-        for cold in (False, True):
-            us = run(tab, mb << 20, nx, 32 if not cold else 9, cold, coop)
-            key = f"{mb}MB_{16 * nx}B{'_coop' if coop else ''}{'_cold' if cold else ''}"
-            res[key] = {
-                "us_per_1M": round(us, 2), "G_lines_s": round(n / us / 1e3, 2),
-                "line_GB_s": round(n * 16 * nx / us / 1e3, 1),
-                "all_GB_s": round(n * (16 * nx + 20 + 32) / us / 1e3, 1)}
-            print(json.dumps({key: res[key]}), flush=True)
-    del tab
-print(json.dumps(res, indent=1))
+def main():
+    res = {}
+    for mb in (128, 256, 512, 1024, 2048, 4096):
+        tab = torch.randint(0, 1 << 30, ((mb << 20) // 4,), dtype=torch.int32, device=dev)
+        for nx, coop in ((1, 0), (2, 0), (4, 0), (8, 0), (8, 1), (16, 0)):
+            for cold in (False, True):
+                us = run(tab, mb << 20, nx, 32 if not cold else 9, cold, coop)
+                key = f"{mb}MB_{16 * nx}B{'_coop' if coop else ''}{'_cold' if cold else ''}"
+                res[key] = {
+                    "us_per_1M": round(us, 2), "G_lines_s": round(n / us / 1e3, 2),
+                    "line_GB_s": round(n * 16 * nx / us / 1e3, 1),
+                    "all_GB_s": round(n * (16 * nx + 20 + 32) / us / 1e3, 1)}
+                print(json.dumps({key: res[key]}), flush=True)
+        del tab
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()

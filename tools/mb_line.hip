@@ -3,6 +3,7 @@
 //   k_lane<NX>  : per lane one random NX*16-byte piece (NX x 16-byte loads, lane-private), then with
 //                 probability p2/256 a second random piece (dependent round), plus a 20-byte target
 //                 read and a 32-byte row write per lane (the query's streaming part)
+//   k_lane_nt<NX>: k_lane<NX> with non-temporal target reads and row writes (coop = 2), the engine's stream policy
 //   k_coop      : the same 128-byte pieces, but 8 lanes x 16 B load one piece per instruction and
 //                 the piece is redistributed through LDS to its owner lane
 #include <hip/hip_runtime.h>
@@ -37,6 +38,30 @@ __global__ __launch_bounds__(256) void k_lane(const uint4* table, uint64_t npiec
     uint4 r = make_uint4(acc, acc + 1, acc + 2, acc + 3);
     reinterpret_cast<uint4*>(out + 8ull * i)[0] = r;
     reinterpret_cast<uint4*>(out + 8ull * i)[1] = r;
+}
+
+// k_lane<NX> with the streams non-temporal (the target read and the row write), as the engine's kernels do
+template <int NX>
+__global__ __launch_bounds__(256) void k_lane_nt(const uint4* table, uint64_t npieces, const uint8_t* targets,
+                                                 uint32_t n, uint32_t p2, uint32_t* out) {
+    typedef uint32_t v4 __attribute__((ext_vector_type(4)));
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t* tp = reinterpret_cast<const uint32_t*>(targets + 20ull * i);
+    const uint64_t a = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(tp));
+    const uint64_t b = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(tp + 2));
+    const uint32_t c = __builtin_nontemporal_load(tp + 4);
+    uint64_t h = mix(a ^ (b >> 32) ^ (uint32_t)b ^ c);
+    uint4 v[NX];
+    const uint64_t piece = h % npieces;
+#pragma unroll
+    for (int x = 0; x < NX; x++) v[x] = table[piece * NX + x];
+    uint32_t acc = 0;
+#pragma unroll
+    for (int x = 0; x < NX; x++) acc += v[x].x ^ v[x].w ^ v[x].y;
+    v4* o = reinterpret_cast<v4*>(out + 8ull * i);
+    __builtin_nontemporal_store(v4{acc, acc + 1, acc + 2, acc + 3}, o);
+    __builtin_nontemporal_store(v4{acc, acc + 1, acc + 2, acc + 3}, o + 1);
 }
 
 // 128-byte pieces; lane l of each 8-lane group loads 16-byte part (l & 7) of the piece of query
@@ -78,7 +103,9 @@ extern "C" int mb_line(const void* table, uint64_t bytes, const uint8_t* targets
     const uint4* t = (const uint4*)table;
     hipStream_t st = (hipStream_t)s;
     const uint64_t np = bytes / (16ull * nx);
-    if (coop) hipLaunchKernelGGL(k_coop, g, b, 0, st, t, bytes / 128, targets, n, p2, out);
+    if (coop == 2 && nx == 4) hipLaunchKernelGGL(k_lane_nt<4>, g, b, 0, st, t, np, targets, n, p2, out);
+    else if (coop == 2 && nx == 8) hipLaunchKernelGGL(k_lane_nt<8>, g, b, 0, st, t, np, targets, n, p2, out);
+    else if (coop) hipLaunchKernelGGL(k_coop, g, b, 0, st, t, bytes / 128, targets, n, p2, out);
     else if (nx == 1) hipLaunchKernelGGL(k_lane<1>, g, b, 0, st, t, np, targets, n, p2, out);
     else if (nx == 2) hipLaunchKernelGGL(k_lane<2>, g, b, 0, st, t, np, targets, n, p2, out);
     else if (nx == 4) hipLaunchKernelGGL(k_lane<4>, g, b, 0, st, t, np, targets, n, p2, out);
