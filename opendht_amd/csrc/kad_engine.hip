@@ -2387,6 +2387,107 @@ __device__ __forceinline__ bool gl32_answer(const DevTable& T, const Target& t, 
     return !ex;
 }
 
+// gl32_answer with FOUR lanes per query (rt_gl32q_kernel, counts 24 / 28 / 32 on tables with general lines: the
+// reference's split-policy shape): lane p of the quad loads 64 of the line's 256 bytes (dwords 16x + 4p .. +3), sorts
+// its 16 slot values and the quad merges them to the top 32 (as wl32_answer4). The header is lane 0's dwords 0..3
+// and lane 1's 4, 5; the values, masks and fallbacks are gl32_answer's, so the rows are identical.
+__device__ __forceinline__ bool gl32_answer4(const DevTable& T, const Target& t, uint32_t b, uint32_t count, bool act,
+                                             uint32_t p, uint32_t (&v)[16], uint32_t& m, uint32_t& base) {
+    uint32_t L[16];
+    if (act) {
+        const uint4* lp = T.gl32 + (GL32_STRIDE / 4) * (size_t)b;
+#pragma unroll
+        for (int x = 0; x < 4; x++) {
+            const uint4 u = lp[4 * x + p];
+            L[4 * x] = u.x; L[4 * x + 1] = u.y; L[4 * x + 2] = u.z; L[4 * x + 3] = u.w;
+        }
+    } else {
+#pragma unroll
+        for (int x = 0; x < 16; x++) L[x] = NONE;
+    }
+    const uint32_t h = qdpp<QP_B0>(L[3]), g03 = qdpp<QP_B0>(L[1]), g47 = qdpp<QP_B0>(L[2]);
+    const uint32_t s04 = qdpp<QP_B1>(L[0]), s56 = qdpp<QP_B1>(L[1]);  // dwords 4, 5
+    base = qdpp<QP_B0>(L[0]);
+    const uint32_t S = (h >> 12) & 127u, R = (h >> 8) & 15u;
+    uint32_t Rc = 8, Gc = 0;
+#pragma unroll
+    for (int r = 7; r >= 0; r--) {
+        const uint32_t g = ((r < 4 ? g03 : g47) >> (8 * (r & 3))) & 255u;
+        if (g >= count || ((h >> r) & 1u)) { Rc = (uint32_t)r; Gc = g; }
+    }
+    m = min(count, Gc);
+    uint32_t lim = S;
+#pragma unroll
+    for (int r = 0; r < 7; r++) {
+        const uint32_t sr = r < 5 ? (s04 >> (6 * r)) & 63u : (s56 >> (6 * (r - 5))) & 63u;
+        if ((uint32_t)r == Rc && Rc < R) lim = sr;
+    }
+    bool ex = !act || (h & WL_DEFER) || Rc > R || lim < m;
+    if (act && b == 0) ex |= below_first(T, t);
+    const uint32_t cp = (s56 >> 12) & 63u;
+    const uint32_t tx = (uint32_t)((t.hi << (cp & 63u)) >> 40) << 8;
+#pragma unroll
+    for (int e = 0; e < 16; e++) {
+        const uint32_t dwi = 16u * (e >> 2) + 4u * p + (e & 3), sl = dwi - GL32_HDR;
+        v[e] = dwi >= GL32_HDR && sl < lim ? L[e] ^ tx : NONE;  // empty slots stay NONE
+    }
+    const bool low = (p & 1u) == 0;
+    sort16(v);
+    quad_exchange<QP_X1, true>(v, low);
+    clean16(v);
+    quad_exchange<QP_X3, true>(v, true);
+    quad_exchange<QP_X1, false>(v, low);
+    clean16(v);
+    return !ex;
+}
+
+// Counts 24, 28, 32 on general lines: four lanes per query, the row through a per-quad LDS row (rt_wl32q_kernel's).
+__global__ __launch_bounds__(BLOCK) void rt_gl32q_kernel(DevTable T, const uint8_t* __restrict__ targets, uint32_t q,
+                                                         uint32_t count, uint32_t* __restrict__ out_idx,
+                                                         uint8_t* __restrict__ out_cnt) {
+    const uint32_t g = blockIdx.x * BLOCK + threadIdx.x, i = g >> 2, p = g & 3u;
+    const bool act = i < q;
+    Target t{};
+    uint32_t b = 0;
+    if (act) {
+        t = load_target(targets, i);
+        b = locate_bucket(T, t);
+    }
+    uint32_t v[16], m, base;
+    const bool ok = gl32_answer4(T, t, b, count, act, p, v, m, base);
+    const uint32_t r0 = 16u * (p & 1u), bi = base + T.index_base;
+    uint32_t o[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) o[k] = r0 + k < m ? bi + (v[k] & 255u) : NONE;
+    if (act && ok && p == 0 && out_cnt) out_cnt[i] = (uint8_t)m;
+    __shared__ uint4 qrow[BLOCK / 4][9];  // per quad: 32 entries + a 16-byte pad
+    uint32_t* R = reinterpret_cast<uint32_t*>(qrow[threadIdx.x >> 2]);
+    if (p < 2u) {
+#pragma unroll
+        for (int x = 0; x < 4; x++)
+            reinterpret_cast<uint4*>(R + 16u * p)[x] = make_uint4(o[4 * x], o[4 * x + 1], o[4 * x + 2], o[4 * x + 3]);
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    if (act && ok) {
+        uint32_t* row = out_idx + (size_t)i * count;
+        if ((count & 3u) == 0 && ((uintptr_t)out_idx & 15u) == 0) {
+#pragma unroll
+            for (int hh = 0; hh < 2; hh++)
+                if (16u * hh + 4u * p < count)
+                    st_row4(row + 16 * hh + 4 * p, R[16 * hh + 4 * p], R[16 * hh + 4 * p + 1], R[16 * hh + 4 * p + 2],
+                            R[16 * hh + 4 * p + 3]);
+        } else {
+#pragma unroll
+            for (int j = 0; j < 8; j++)
+                if (4u * j + p < count) st_row1(row + 4 * j + p, R[4 * j + p]);
+        }
+    }
+    __shared__ uint64_t xs[BLOCK / 64][192];
+    exact_tail(T, t, act && !ok && p == 0u, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
+}
+
 __device__ __forceinline__ void rt_gl32_kernel_body(const DevTable& T, const uint8_t* __restrict__ targets, uint32_t q,
                                                         uint32_t count, uint32_t* __restrict__ out_idx,
                                                         uint8_t* __restrict__ out_cnt) {
@@ -2982,8 +3083,101 @@ __global__ __launch_bounds__(BLOCK) void rt_dual_wl32_kernel(DevTable T4, DevTab
     exact_tail(T6, t, ex && six, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
 }
 
+// Dual-family batch on slot lines (both families with them or empty; the reference's split-policy shape, as
+// Dht::onGetValues asks both tables): rt_sl_kernel (count <= 8) and rt_sl16_kernel (9..16) with the table per lane,
+// the fallback line of the lane's family, the exact path per family.
+__global__ __launch_bounds__(BLOCK) void rt_dual_sl_kernel(DevTable T4, DevTable T6, const uint8_t* __restrict__ targets,
+                                                           const uint8_t* __restrict__ af, uint32_t q, uint32_t count,
+                                                           uint32_t* __restrict__ out_idx, uint8_t* __restrict__ out_cnt) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    const bool act = i < q && count > 0;
+    if (i < q && count == 0 && out_cnt) out_cnt[i] = 0;
+    const bool six = act && af[i] != 0;
+    const DevTable& T = six ? T6 : T4;
+    const bool empty = act && T.B == 0;  // an empty family (routing_table.cpp:73)
+    const uint64_t thi = act ? load_target_hi(targets, i) : 0ull;
+    const bool in = act && !empty && thi >= T.rbase && ((thi - T.rbase) >> T.slshift) < T.slslots;
+    uint32_t o[8], m, bh;
+    const bool ok = sl_answer(T, thi, in ? (uint32_t)((thi - T.rbase) >> T.slshift) : 0u, count, in, o, m, bh);
+    uint32_t* row = out_idx + (size_t)i * count;
+    if (act && ok) {
+        store_row8(row, o, count);
+        if (out_cnt) out_cnt[i] = (uint8_t)m;
+    } else if (empty) {
+        for (uint32_t c = 0; c < count; c++) row[c] = NONE;
+        if (out_cnt) out_cnt[i] = 0;
+    }
+    bool need = act && !ok && !empty;
+    if (__any(need)) {  // locate and the family's 128-byte line, then the exact path of the family
+        Target t{};
+        uint32_t b = 0;
+        if (need) {
+            t = load_target(targets, i);
+            b = bh != NONE ? bh : locate_bucket(T, t);
+        }
+        const bool ok2 = gl_answer(T, t, b, count, need, o, m);
+        if (need && ok2) {
+            store_row8(row, o, count);
+            if (out_cnt) out_cnt[i] = (uint8_t)m;
+        }
+        need = need && !ok2;
+        __shared__ uint64_t xs[BLOCK / 64][192];
+        exact_tail(T4, t, need && !six, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
+        exact_tail(T6, t, need && six, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
+    }
+}
+
+__global__ __launch_bounds__(BLOCK) void rt_dual_sl16_kernel(DevTable T4, DevTable T6, const uint8_t* __restrict__ targets,
+                                                             const uint8_t* __restrict__ af, uint32_t q, uint32_t count,
+                                                             uint32_t* __restrict__ out_idx, uint8_t* __restrict__ out_cnt) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    const bool act = i < q;
+    const bool six = act && af[i] != 0;
+    const DevTable& T = six ? T6 : T4;
+    const bool empty = act && T.B == 0;  // an empty family (routing_table.cpp:73)
+    const uint64_t thi = act ? load_target_hi(targets, i) : 0ull;
+    const bool in = act && !empty && thi >= T.rbase && ((thi - T.rbase) >> T.slshift) < T.slslots;
+    uint32_t L[GL16_STRIDE];
+    load_line32(T.sl16 + (GL16_STRIDE / 4) * (size_t)(in ? (thi - T.rbase) >> T.slshift : 0ull), in, L);
+    const bool fbl = L[1] == NONE;
+    uint32_t o[16], m;
+    bool ok = gl16_rank(L, thi, count, T.index_base, o, m) && in && !fbl;
+    const bool miss = act && !ok && !empty;
+    Target t{};
+    if (miss) t = load_target(targets, i);
+    const bool need = miss && (!in || fbl);
+    if (__any(need)) {
+        uint32_t b = 0;
+        if (need) {
+            const uint32_t bh = L[0] == NONE ? NONE
+                                             : L[0] + ((L[4] & 1u) && thi >= (((uint64_t)L[2] << 32) | L[3]) ? 1u : 0u);
+            b = in && bh != NONE ? bh : locate_bucket(T, t);
+        }
+        uint32_t o2[16], m2;
+        const bool ok2 = gl16_answer(T, t, b, count, need, o2, m2) && need;
+        if (ok2) {
+#pragma unroll
+            for (int j = 0; j < 16; j++) o[j] = o2[j];
+            m = m2;
+            ok = true;
+        }
+    }
+    if (empty) {
+#pragma unroll
+        for (int j = 0; j < 16; j++) o[j] = NONE;
+        m = 0;
+        ok = true;
+    }
+    if (act && ok && out_cnt) out_cnt[i] = (uint8_t)m;
+    store_rows_block<16>(out_idx, q, count, o, act && ok);
+    __shared__ uint64_t xs[BLOCK / 64][192];
+    exact_tail(T4, t, act && !ok && !six, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
+    exact_tail(T6, t, act && !ok && six, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
+}
+
 // Dual-family counts 24, 28, 32 (both families with 64-slot lines or empty): rt_wl32q_kernel's four lanes per
-// query and per-quad LDS row store, the family per quad.
+// query and per-quad LDS row store, the family per quad. GL: the general lines (gl32_answer4, split-policy tables).
+template <bool GL>
 __global__ __launch_bounds__(BLOCK) void rt_dual_wl32q_kernel(DevTable T4, DevTable T6, const uint8_t* __restrict__ targets,
                                                               const uint8_t* __restrict__ af, uint32_t q, uint32_t count,
                                                               uint32_t* __restrict__ out_idx,
@@ -2997,10 +3191,10 @@ __global__ __launch_bounds__(BLOCK) void rt_dual_wl32q_kernel(DevTable T4, DevTa
         six = af[i] != 0;
     }
     const DevTable& T = six ? T6 : T4;  // quad-uniform
-    const bool wl = act && (T.flags & TF_WL32);
+    const bool wl = act && (T.flags & (GL ? TF_GL32 : TF_WL32));
     const uint32_t b = wl ? locate_bucket(T, t) : 0u;
     uint32_t v[16], m, base;
-    const bool ok = wl32_answer4<true>(T, t, b, count, wl, p, v, m, base);
+    const bool ok = GL ? gl32_answer4(T, t, b, count, wl, p, v, m, base) : wl32_answer4<true>(T, t, b, count, wl, p, v, m, base);
     const uint32_t r0 = 16u * (p & 1u), bi = base + T.index_base;
     uint32_t o[16];
 #pragma unroll
@@ -6203,6 +6397,10 @@ int launch_rt(const kad_table* t, const uint8_t* targets, uint32_t q, uint32_t c
         hipLaunchKernelGGL(rt_sl16_kernel, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
     } else if (K == 16 && (d.flags & TF_GL16) && !(ev && (std::strcmp(ev, "lane") == 0 || std::strcmp(ev, "gl32") == 0))) {
         hipLaunchKernelGGL(rt_gl16_kernel, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
+    } else if (K == 32 && (d.flags & TF_GL32) && count >= 24 && (count & 3u) == 0 &&
+               !(ev && (std::strcmp(ev, "lane") == 0 || std::strcmp(ev, "gl32lane") == 0))) {
+        // four lanes per query for rows of 24, 28 and 32 entries (as the uniform lines' rt_wl32q_kernel)
+        hipLaunchKernelGGL(rt_gl32q_kernel, dim3(grid_for(4ull * q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
     } else if (K > 8 && (d.flags & TF_GL32) && !(ev && std::strcmp(ev, "lane") == 0)) {
         hipLaunchKernelGGL(rt_gl32_kernel, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
     } else {
@@ -6714,6 +6912,9 @@ int kad_rt_closest_batch_dual(const kad_table* t4, const kad_table* t6, const ui
     else if (count <= 8 && ((d4.flags | d6.flags) & TF_WL))
         hipLaunchKernelGGL(rt_dual_wl_kernel, dim3(grid_for(q)), dim3(BLOCK), 0, s, d4, d6, targets, af, q, count,
                            out_idx, out_cnt);
+    else if (count <= 8 && ((d4.flags | d6.flags) & TF_SL) && lean(TF_SL))
+        hipLaunchKernelGGL(rt_dual_sl_kernel, dim3(grid_for(q)), dim3(BLOCK), 0, s, d4, d6, targets, af, q, count,
+                           out_idx, out_cnt);
     else if (count <= 8 && ((d4.flags | d6.flags) & TF_GL))
         hipLaunchKernelGGL(rt_dual_gl_kernel<8>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d4, d6, targets, af, q, count,
                            out_idx, out_cnt);
@@ -6724,19 +6925,25 @@ int kad_rt_closest_batch_dual(const kad_table* t4, const kad_table* t6, const ui
     else if (count <= 16 && ((d4.flags | d6.flags) & TF_WL16))
         hipLaunchKernelGGL(rt_dual_wl16_kernel<false>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d4, d6, targets, af, q,
                            count, out_idx, out_cnt);
+    else if (count <= 16 && ((d4.flags | d6.flags) & TF_SL16) && lean(TF_SL16))
+        hipLaunchKernelGGL(rt_dual_sl16_kernel, dim3(grid_for(q)), dim3(BLOCK), 0, s, d4, d6, targets, af, q, count,
+                           out_idx, out_cnt);
     else if (count <= 16 && ((d4.flags | d6.flags) & TF_GL16))
         hipLaunchKernelGGL(rt_dual_gl_kernel<16>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d4, d6, targets, af, q, count,
                            out_idx, out_cnt);
     else if (count <= 16) launch_rt_dual<16>(d4, d6, targets, af, q, count, out_idx, out_cnt, s);
     else if (((d4.flags | d6.flags) & TF_WL32) && lean(TF_WL32) && count >= 24 && (count & 3u) == 0)
-        hipLaunchKernelGGL(rt_dual_wl32q_kernel, dim3(grid_for(4ull * q)), dim3(BLOCK), 0, s, d4, d6, targets, af, q,
-                           count, out_idx, out_cnt);
+        hipLaunchKernelGGL(rt_dual_wl32q_kernel<false>, dim3(grid_for(4ull * q)), dim3(BLOCK), 0, s, d4, d6, targets, af,
+                           q, count, out_idx, out_cnt);
     else if (((d4.flags | d6.flags) & TF_WL32) && lean(TF_WL32))
         hipLaunchKernelGGL(rt_dual_wl32_kernel<true>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d4, d6, targets, af, q,
                            count, out_idx, out_cnt);
     else if ((d4.flags | d6.flags) & TF_WL32)
         hipLaunchKernelGGL(rt_dual_wl32_kernel<false>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d4, d6, targets, af, q,
                            count, out_idx, out_cnt);
+    else if (((d4.flags | d6.flags) & TF_GL32) && lean(TF_GL32) && count >= 24 && (count & 3u) == 0)
+        hipLaunchKernelGGL(rt_dual_wl32q_kernel<true>, dim3(grid_for(4ull * q)), dim3(BLOCK), 0, s, d4, d6, targets, af,
+                           q, count, out_idx, out_cnt);
     else if ((d4.flags | d6.flags) & TF_GL32)
         hipLaunchKernelGGL(rt_dual_gl_kernel<32>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d4, d6, targets, af, q, count,
                            out_idx, out_cnt);

@@ -14,7 +14,8 @@ import tables as TB
 from opendht_amd import DeviceTable
 from opendht_amd import synth as S
 from opendht_amd._lib import (KAD_INFO_GENERAL_LINES, KAD_INFO_GENERAL_LINES16, KAD_INFO_GENERAL_LINES32,
-                              KAD_INFO_SLOT_LINES, KAD_INFO_SLOT_LINES16, KAD_INFO_WINDOW_LINES, KAD_OP_SPLIT)
+                              KAD_INFO_SLOT_LINES, KAD_INFO_SLOT_LINES16, KAD_INFO_WINDOW_LINES, KAD_NO_NODE,
+                              KAD_OP_SPLIT)
 
 pytestmark = pytest.mark.gpu
 
@@ -110,8 +111,10 @@ def test_uniform_table_switches_to_general_lines_after_split(gpu):
 
 
 def test_dual_family_general_lines(gpu):
-    """kad_rt_closest_batch_dual on two split-policy families (af per query) through rt_dual_gl_kernel: every
-    count range reads its family's general lines, bit-exact against the oracle per family."""
+    """kad_rt_closest_batch_dual on two split-policy families (af per query): counts <= 8 through
+    rt_dual_sl_kernel, 9..16 through rt_dual_sl16_kernel (each lane reads its family's slot line), 17..32 through
+    the general-line kernels; bit-exact against the oracle per family. Then one family empty (routing_table.cpp:73):
+    its queries get empty rows from the same slot-line kernels."""
     from opendht_amd import rt_closest_dual
     t4 = TB.split_config(100_000, seed=0x6B4)
     t6 = TB.split_config(60_000, seed=0x6B6, good=60, expired=25)
@@ -124,8 +127,9 @@ def test_dual_family_general_lines(gpu):
         for T in (T4, T6):
             f = T.info()["flags"]
             assert f & KAD_INFO_GENERAL_LINES and f & KAD_INFO_GENERAL_LINES16 and f & KAD_INFO_GENERAL_LINES32, hex(f)
+            assert f & KAD_INFO_SLOT_LINES and f & KAD_INFO_SLOT_LINES16, hex(f)
         tg, afd = torch.from_numpy(targets).to(gpu), torch.from_numpy(af).to(gpu)
-        for k in (1, 5, 8, 9, 14, 16, 17, 24, 32):
+        for k in (1, 5, 8, 9, 14, 16, 17, 24, 27, 28, 32):  # 24 / 28 / 32: the quad kernel (rt_dual_wl32q_kernel<true>)
             idx, cnt = rt_closest_dual(T4, T6, tg, afd, k)
             torch.cuda.synchronize()
             idx, cnt = idx.cpu().numpy().view(np.uint32), cnt.cpu().numpy()
@@ -134,6 +138,15 @@ def test_dual_family_general_lines(gpu):
                 want, wcnt = O.flat_rt_closest(t["ids"], t["status"], t["first"], t["off"], targets[sel], k, nthreads=8)
                 np.testing.assert_array_equal(cnt[sel], wcnt, err_msg=f"af={fam} k={k} counts")
                 np.testing.assert_array_equal(idx[sel], want, err_msg=f"af={fam} k={k}")
+        sel = np.flatnonzero(af == 0)
+        for k in (1, 8, 9, 16):
+            idx, cnt = rt_closest_dual(T4, None, tg, afd, k)
+            torch.cuda.synchronize()
+            idx, cnt = idx.cpu().numpy().view(np.uint32), cnt.cpu().numpy()
+            want, wcnt = O.flat_rt_closest(t4["ids"], t4["status"], t4["first"], t4["off"], targets[sel], k, nthreads=8)
+            np.testing.assert_array_equal(idx[sel], want, err_msg=f"empty IPv6 k={k}")
+            np.testing.assert_array_equal(cnt[sel], wcnt, err_msg=f"empty IPv6 k={k} counts")
+            assert (cnt[af == 1] == 0).all() and (idx[af == 1] == KAD_NO_NODE).all(), k
 
 
 def test_general_lines_full_size_split_table(gpu):
