@@ -325,7 +325,7 @@ def main_owner(args):
     wl = bool(flags & KAD_INFO_WINDOW_LINES)  # the shard's U(24) table carries every line set
     kk = 8 if cnt_k <= 8 else 16 if cnt_k <= 16 else 32
     ws = kk == 8 and bool(flags & KAD_INFO_SHORT_LINES) and os.environ.get("KAD_RT_KERNEL") not in ("wl", "lane")
-    kernel = ("rt_ws_kernel<0, true>" if ws else {8: "rt_wl_kernel<0>", 16: "rt_wl16_kernel<0>", 32: "rt_wl32_kernel"}[kk]
+    kernel = ("rt_ws_kernel<0, true, true>" if ws else {8: "rt_wl_kernel<0>", 16: "rt_wl16_kernel<0>", 32: "rt_wl32_kernel"}[kk]
               if wl else f"rt_closest_kernel<{kk}>")
     line_b = 64 if ws else LINE_BYTES[kk]
 

@@ -1232,7 +1232,9 @@ __device__ __forceinline__ bool ws_answer(const DevTable& T, const Target& t, ui
 // NTS: the streams (targets in, rows out) with the non-temporal policy, so that they do not displace the line table
 // from the Infinity Cache: 32.7 -> 31.8 us per 1M on the bench shard, 3 interleaved bench runs each
 // (profiles/r03/ab_ws_nts/). The launch path's default; the service (rows into host memory) keeps the plain policy.
-template <int ABL, bool NTS = false>
+// CR (with NTS, count 8, 16-byte aligned rows): the wave's 64 rows leave through LDS as two 1 KB runs of 16-byte
+// pieces at consecutive addresses (tools/mb_req.py: line + coalesced rows 27.8 against 29.4 us per 1M).
+template <int ABL, bool NTS = false, bool CR = false>
 __device__ __forceinline__ void rt_ws_kernel_body(const DevTable& T, const uint8_t* __restrict__ targets, uint32_t q,
                                                       uint32_t count, uint32_t* __restrict__ out_idx,
                                                       uint8_t* __restrict__ out_cnt) {
@@ -1249,7 +1251,24 @@ __device__ __forceinline__ void rt_ws_kernel_body(const DevTable& T, const uint8
     }
     uint32_t o[8], m;
     const bool ok = ws_answer<ABL>(T, t, b, count, act, o, m);
-    if (act && ok) {
+    if (CR && count == 8 && ((uintptr_t)out_idx & 15u) == 0) {  // count: kernel-uniform, so the branch is too
+        __shared__ uint4 wrow[BLOCK / 64][128];
+        const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6, i0 = i - lane;
+        uint4* R = wrow[w];
+        R[2 * lane] = make_uint4(o[0], o[1], o[2], o[3]);
+        R[2 * lane + 1] = make_uint4(o[4], o[5], o[6], o[7]);
+        const uint64_t okm = __ballot(act && ok);
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        u32x4_t* r = reinterpret_cast<u32x4_t*>(out_idx + (size_t)i0 * 8u);
+#pragma unroll
+        for (int h = 0; h < 2; h++) {  // piece 64h + lane = half (lane & 1) of the row of query 32h + lane / 2
+            const uint4 u = R[64 * h + lane];
+            if ((okm >> (32 * h + (lane >> 1))) & 1u) __builtin_nontemporal_store(u32x4_t{u.x, u.y, u.z, u.w}, r + 64 * h + lane);
+        }
+        if (act && ok && out_cnt) out_cnt[i] = (uint8_t)m;
+    } else if (act && ok) {
         if (NTS && count == 8 && ((uintptr_t)out_idx & 15u) == 0) {
             u32x4_t* r = reinterpret_cast<u32x4_t*>(out_idx + (size_t)i * 8u);
             __builtin_nontemporal_store(u32x4_t{o[0], o[1], o[2], o[3]}, r);
@@ -1278,11 +1297,11 @@ __device__ __forceinline__ void rt_ws_kernel_body(const DevTable& T, const uint8
         if (ABL == 4 && need && out_cnt) out_cnt[i] = 250;
     }
 }
-template <int ABL, bool NTS = false>
+template <int ABL, bool NTS = false, bool CR = false>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) void rt_ws_kernel(DevTable T, const uint8_t* __restrict__ targets, uint32_t q,
                                                       uint32_t count, uint32_t* __restrict__ out_idx,
                                                       uint8_t* __restrict__ out_cnt) {
-    rt_ws_kernel_body<ABL, NTS>(T, targets, q, count, out_idx, out_cnt);
+    rt_ws_kernel_body<ABL, NTS, CR>(T, targets, q, count, out_idx, out_cnt);
 }
 
 // The count <= 8 line answer for kernels that serve other paths too (dual-family, shard): lanes with `ws`
@@ -6344,9 +6363,12 @@ int launch_rt(const kad_table* t, const uint8_t* targets, uint32_t q, uint32_t c
 #endif
         if (ev && std::strcmp(ev, "ws_plain") == 0)  // A/B: the streams with the plain policy
             hipLaunchKernelGGL(rt_ws_kernel<0>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
-        else
+        else if (ev && std::strcmp(ev, "ws_nocr") == 0)  // A/B: rows stored by their lanes (round-3 form before CR)
             hipLaunchKernelGGL((rt_ws_kernel<0, true>), dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out,
                                cnt);
+        else  // rows through LDS as coalesced runs: 31.85 -> 31.0 us per 1M (profiles/r03/ab_ws_cr/)
+            hipLaunchKernelGGL((rt_ws_kernel<0, true, true>), dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count,
+                               out, cnt);
     } else if (K == 8 && (d.flags & TF_WL) && !(ev && std::strcmp(ev, "lane") == 0)) {
 #ifdef KAD_ABLATIONS  // timing ablations with WRONG results: only in the tools build (Makefile target `ablations`)
         if (ev && std::strcmp(ev, "wl_abl1") == 0)
