@@ -173,6 +173,45 @@ __global__ __launch_bounds__(256) void k_parts(const uint4* __restrict__ tab, ui
     }
 }
 
+// The count-32 shape: 256-byte lines read by four lanes per query (lane p: bytes 64x + 16p, x = 0..3, as
+// rt_wl32q_kernel), 128-byte rows stored as the wave's 2 KB run, the 20-byte target. F bits: 1 target, 2 line, 4 rows.
+template <int F>
+__global__ __launch_bounds__(256) void k_parts32(const uint4* __restrict__ tab, uint32_t np, const uint8_t* __restrict__ tg,
+                                                 uint32_t n, uint32_t* __restrict__ out) {
+    typedef uint32_t v4 __attribute__((ext_vector_type(4)));
+    const uint32_t lane = threadIdx.x & 63u, p = lane & 3u;
+    for (uint32_t g0 = blockIdx.x * 256 + (threadIdx.x & ~63u); (g0 >> 2) < n; g0 += gridDim.x * 256) {
+        const uint32_t i = (g0 + lane) >> 2, i0 = g0 >> 2;  // 16 queries per wave
+        uint64_t h = mix(0x9E3779B97F4A7C15ull ^ i);
+        if (F & 1) {
+            const uint32_t* tp = reinterpret_cast<const uint32_t*>(tg + 20ull * i);
+            const uint64_t a = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(tp));
+            const uint32_t c = __builtin_nontemporal_load(tp + 2 + (p < 2 ? p : 2u));  // the quad reads the rest (dwords 2..4)
+            h = mix(a ^ (uint32_t)__shfl((int)c, (int)(lane & ~3u), 64));  // one line per quad
+        }
+        uint32_t acc = (uint32_t)h;
+        if (F & 2) {
+            const uint32_t pc = piece_of(h, np / 4);
+            uint4 v[4];
+#pragma unroll
+            for (int x = 0; x < 4; x++) v[x] = tab[16ull * pc + 4 * x + p];
+#pragma unroll
+            for (int x = 0; x < 4; x++) acc += v[x].x ^ v[x].w ^ v[x].y ^ v[x].z;
+        }
+        if (F & 4) {  // piece 64h + lane of the wave's 128 pieces
+            v4* o = reinterpret_cast<v4*>(out + 32ull * i0);
+            __builtin_nontemporal_store(v4{acc, acc + 1, acc + 2, acc + 3}, o + lane);
+            __builtin_nontemporal_store(v4{acc, acc + 1, acc + 2, acc + 3}, o + 64 + lane);
+        } else if (F & 8) {  // the kernel's per-quad form: 64 contiguous bytes per quad and instruction
+            v4* o = reinterpret_cast<v4*>(out + 32ull * i);
+            __builtin_nontemporal_store(v4{acc, acc + 1, acc + 2, acc + 3}, o + p);
+            __builtin_nontemporal_store(v4{acc, acc + 1, acc + 2, acc + 3}, o + 4 + p);
+        } else if (acc == 0x9E3779B9u) {
+            out[i & 1023] = acc;
+        }
+    }
+}
+
 }  // namespace
 
 extern "C" int mb_req(const void* table, uint64_t bytes, const uint8_t* targets, uint32_t n, uint32_t mode,
@@ -189,6 +228,9 @@ extern "C" int mb_req(const void* table, uint64_t bytes, const uint8_t* targets,
 #define P(f) case f: hipLaunchKernelGGL(k_parts<f>, g, b, 0, st, t, np, targets, n, out); break;
             P(1) P(4) P(5) P(2) P(8) P(10) P(33) P(36) P(17) P(20) P(21) P(24) P(26) P(18) P(53) P(16)
 #undef P
+#define P32(f) case 100 + f: hipLaunchKernelGGL(k_parts32<f>, dim3(blocks ? blocks : (4 * n + 255) / 256), b, 0, st, t, np, targets, n, out); break;
+            P32(2) P32(4) P32(6) P32(7) P32(3) P32(8) P32(10) P32(11)
+#undef P32
             default: return -1;
         }
     } else {

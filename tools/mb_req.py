@@ -14,6 +14,7 @@ import ctypes
 import json
 import os
 import subprocess
+import sys
 
 import torch
 
@@ -30,7 +31,7 @@ N, NB, REPS = 1 << 20, 16, 8
 g = torch.Generator(device=dev)
 g.manual_seed(5)
 tgs = [torch.randint(0, 256, (N, 20), dtype=torch.uint8, device=dev, generator=g) for _ in range(NB)]
-out = torch.empty(N * 8, dtype=torch.int32, device=dev)
+out = torch.empty(N * 32, dtype=torch.int32, device=dev)
 big = torch.randint(0, 1 << 30, ((128 << 20) // 4,), dtype=torch.int32, device=dev, generator=g)
 small = big[: (64 << 10) // 4]
 st = torch.cuda.current_stream().cuda_stream
@@ -60,6 +61,14 @@ def emit(name, us):
 
 
 B = 128 << 20
+if os.environ.get("MB_REQ32"):  # the count-32 shape: 256-byte lines in a 512 MB table, 128-byte rows
+    del big
+    big = torch.randint(0, 1 << 30, ((512 << 20) // 4,), dtype=torch.int32, device=dev, generator=g)
+    for rep in range(2):
+        for f, name in {2: "line256", 4: "rows128", 6: "line256+rows128", 3: "tgt+line256", 7: "tgt+line256+rows128", 8: "rows128Q",
+                        10: "line256+rows128Q", 11: "tgt+line256+rows128Q"}.items():
+            emit(f"{name}#{rep}", run(big, 512 << 20, 2 + 100 + f, 1))
+    sys.exit(0)
 PARTS = {1: "tgt", 4: "rows", 5: "tgt+rows", 2: "tgtC", 8: "rowsC", 10: "tgtC+rowsC", 33: "tgt_plain",
          36: "rows_plain", 16: "line", 17: "tgt+line", 20: "line+rows", 21: "tgt+line+rows", 24: "line+rowsC",
          18: "tgtC+line", 26: "tgtC+line+rowsC", 53: "tgt+line+rows_plain"}
