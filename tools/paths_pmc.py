@@ -1,8 +1,8 @@
-"""Round-2 (second session) path workload for timings and per-kernel PMC passes (tools/pmc.sh with
-PMC_PROG=tools/paths_pmc.py): every launch reads a different batch of 1M targets (8 rotated batches).
-  bench shard (1/8 of the 100M-node U(24) table): rt_ws_kernel<0> (k=8), rt_wl16_kernel<0> (k=16),
-  rt_wl32_kernel (k=32), nc_line_kernel<0, false> (NodeCache k=14), nc32_line_kernel<0, false> (NodeCache k=32);
-  split-policy table of 4M nodes: rt_sl_kernel<0> (k=8), rt_gl16_kernel (k=14), rt_gl32_kernel (k=32).
+"""Path workload for timings and per-kernel PMC passes (tools/pmc.sh with PMC_PROG=tools/paths_pmc.py; round 3:
+tools/gpu_pmc_paths.sh): every launch reads a different batch of 1M targets (8 rotated batches).
+  bench shard (1/8 of the 100M-node U(24) table): rt_ws_kernel<0, true, true> (k=8), rt_wl16_kernel<0> (k=16),
+  rt_wl32q_kernel<0, true> (k=32), nc_line_kernel (NodeCache k=14), nc32_line_kernel (NodeCache k=32);
+  split-policy table of 4M nodes: rt_sl_kernel<0> (k=8), rt_gl16_kernel (k=14), rt_gl32q_kernel (k=32).
 Without a profiler it prints the per-launch times (HIP events, median of REPS) as JSON."""
 import json
 import os
