@@ -1346,15 +1346,20 @@ constexpr uint32_t WL16_SLOTS = 29, WL16_HDR = 3, WL16_STRIDE = 32;  // dwords
 #define WL16_P1 16u
 #endif
 
-// Batcher's odd-even merge sort for 16 inputs (63 comparators; tests/test_networks.py).
-constexpr int SORT16_LEN = 63;
+// A 16-input sorting network of 60 comparators in 10 layers (the best known size; one of those listed by B. Dobbelaere,
+// "SorterHunter"), 3 fewer than Batcher's odd-even merge sort; checked by the 0-1 principle in tests/test_networks.py.
+constexpr int SORT16_LEN = 60;
 __device__ constexpr uint8_t SORT16[SORT16_LEN][2] = {
-    {0, 1}, {2, 3}, {0, 2}, {1, 3}, {1, 2}, {4, 5}, {6, 7}, {4, 6}, {5, 7}, {5, 6}, {0, 4}, {2, 6}, {2, 4},
-    {1, 5}, {3, 7}, {3, 5}, {1, 2}, {3, 4}, {5, 6}, {8, 9}, {10, 11}, {8, 10}, {9, 11}, {9, 10}, {12, 13}, {14, 15},
-    {12, 14}, {13, 15}, {13, 14}, {8, 12}, {10, 14}, {10, 12}, {9, 13}, {11, 15}, {11, 13}, {9, 10}, {11, 12},
-    {13, 14}, {0, 8}, {4, 12}, {4, 8}, {2, 10}, {6, 14}, {6, 10}, {2, 4}, {6, 8}, {10, 12}, {1, 9}, {5, 13},
-    {5, 9}, {3, 11}, {7, 15}, {7, 11}, {3, 5}, {7, 9}, {11, 13}, {1, 2}, {3, 4}, {5, 6}, {7, 8}, {9, 10},
-    {11, 12}, {13, 14}};
+    {0, 13}, {1, 12}, {2, 15}, {3, 14}, {4, 8}, {5, 6}, {7, 11}, {9, 10},
+    {0, 5}, {1, 7}, {2, 9}, {3, 4}, {6, 13}, {8, 14}, {10, 15}, {11, 12},
+    {0, 1}, {2, 3}, {4, 5}, {6, 8}, {7, 9}, {10, 11}, {12, 13}, {14, 15},
+    {0, 2}, {1, 3}, {4, 10}, {5, 11}, {6, 7}, {8, 9}, {12, 14}, {13, 15},
+    {1, 2}, {3, 12}, {4, 6}, {5, 7}, {8, 10}, {9, 11}, {13, 14},
+    {1, 4}, {2, 6}, {5, 8}, {7, 10}, {9, 13}, {11, 14},
+    {2, 4}, {3, 6}, {9, 12}, {11, 13},
+    {3, 5}, {6, 8}, {7, 9}, {10, 12},
+    {3, 4}, {5, 6}, {7, 8}, {9, 10}, {11, 12},
+    {6, 7}, {8, 9}};
 
 __device__ __forceinline__ void sort16(uint32_t* v) {
 #pragma unroll
@@ -1834,6 +1839,19 @@ __device__ __forceinline__ void clean16(uint32_t (&v)[16]) {
             if ((i & w) == 0) cx(v[i], v[i + w]);
 }
 
+// A quad lane's part of its query's row (entries r0 .. r0 + 15): node index base + offset, NONE from m on. When every
+// row of the wave that is stored is full (m == count), the entries from count on are never stored: no selects.
+__device__ __forceinline__ void quad_row(const uint32_t (&v)[16], uint32_t r0, uint32_t bi, uint32_t m, uint32_t count,
+                                         bool stored, uint32_t (&o)[16]) {
+    if (__all(m == count || !stored)) {
+#pragma unroll
+        for (int k = 0; k < 16; k++) o[k] = bi + (v[k] & 255u);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 16; k++) o[k] = r0 + k < m ? bi + (v[k] & 255u) : NONE;
+    }
+}
+
 template <bool RANK = true>  // RANK false: timing ablation only (the values unranked; results wrong)
 __device__ __forceinline__ bool wl32_answer4(const DevTable& T, const Target& t, uint32_t b, uint32_t count, bool act,
                                              uint32_t p, uint32_t (&v)[16], uint32_t& m, uint32_t& base) {
@@ -1874,16 +1892,25 @@ __device__ __forceinline__ bool wl32_answer4(const DevTable& T, const Target& t,
             inc |= (rj <= Rc ? 1u : 0u) << j;
         }
     }
-    uint32_t have = 0;
+    uint32_t have = S;  // every stored slot is in unless a smaller window masks the later rounds' buckets
+    if (mask) {
+        have = 0;
 #pragma unroll
-    for (int e = 0; e < 16; e++) {
-        const uint32_t dwi = 16u * (e >> 2) + 4u * p + (e & 3), s = dwi - WL32_HDR;
-        const bool in = dwi >= WL32_HDR && s < S && ((inc >> (L[e] >> 28)) & 1u);
-        v[e] = in ? L[e] ^ tx : NONE;  // empty slots stay NONE
-        have += in;
+        for (int e = 0; e < 16; e++) {
+            const uint32_t s = 16u * (e >> 2) + 4u * p + (e & 3) - WL32_HDR;  // header dwords wrap to > S
+            const bool in = s < S && ((inc >> (L[e] >> 28)) & 1u);
+            v[e] = in ? L[e] ^ tx : NONE;  // empty slots stay NONE
+            have += in;
+        }
+        have += qdpp<QP_X1>(have);
+        have += qdpp<QP_X2>(have);
+    } else {
+#pragma unroll
+        for (int e = 0; e < 16; e++) {
+            const uint32_t s = 16u * (e >> 2) + 4u * p + (e & 3) - WL32_HDR;
+            v[e] = s < S ? L[e] ^ tx : NONE;
+        }
     }
-    have += qdpp<QP_X1>(have);
-    have += qdpp<QP_X2>(have);
     const bool low = (p & 1u) == 0;
     if (RANK) {
         sort16(v);
@@ -1950,8 +1977,7 @@ __global__ __launch_bounds__(BLOCK) void rt_wl32q_kernel(DevTable T, const uint8
     const bool ok = wl32_answer4<ABL == 0>(T, t, b, count, act, p, v, m, base);
     const uint32_t r0 = 16u * (p & 1u), bi = base + T.index_base;
     uint32_t o[16];
-#pragma unroll
-    for (int k = 0; k < 16; k++) o[k] = r0 + k < m ? bi + (v[k] & 255u) : NONE;
+    quad_row(v, r0, bi, m, count, act && ok, o);
     if (act && ok && p == 0 && out_cnt) out_cnt[i] = (uint8_t)m;
     if (QS) {
         __shared__ uint4 qrow[BLOCK / 4][9];  // per quad: 32 entries + a 16-byte pad
@@ -2476,8 +2502,7 @@ __global__ __launch_bounds__(BLOCK) void rt_gl32q_kernel(DevTable T, const uint8
     const bool ok = gl32_answer4(T, t, b, count, act, p, v, m, base);
     const uint32_t r0 = 16u * (p & 1u), bi = base + T.index_base;
     uint32_t o[16];
-#pragma unroll
-    for (int k = 0; k < 16; k++) o[k] = r0 + k < m ? bi + (v[k] & 255u) : NONE;
+    quad_row(v, r0, bi, m, count, act && ok, o);
     if (act && ok && p == 0 && out_cnt) out_cnt[i] = (uint8_t)m;
     __shared__ uint4 qrow[BLOCK / 4][9];  // per quad: 32 entries + a 16-byte pad
     uint32_t* R = reinterpret_cast<uint32_t*>(qrow[threadIdx.x >> 2]);
@@ -3216,8 +3241,7 @@ __global__ __launch_bounds__(BLOCK) void rt_dual_wl32q_kernel(DevTable T4, DevTa
     const bool ok = GL ? gl32_answer4(T, t, b, count, wl, p, v, m, base) : wl32_answer4<true>(T, t, b, count, wl, p, v, m, base);
     const uint32_t r0 = 16u * (p & 1u), bi = base + T.index_base;
     uint32_t o[16];
-#pragma unroll
-    for (int k = 0; k < 16; k++) o[k] = r0 + k < m ? bi + (v[k] & 255u) : NONE;
+    quad_row(v, r0, bi, m, count, wl && ok, o);
     if (wl && ok && p == 0 && out_cnt) out_cnt[i] = (uint8_t)m;
     __shared__ uint4 qrow[BLOCK / 4][9];  // per quad: 32 entries + a 16-byte pad
     uint32_t* R = reinterpret_cast<uint32_t*>(qrow[threadIdx.x >> 2]);

@@ -1,6 +1,6 @@
 """RoutingTable::findClosestNodes timings on the bench shard (1/8 of the 100M-node U(24) table), 1M queries per
 launch over 8 rotated target batches, HIP events around 16 launches: counts 8, 14, 16, 17, 24, 32 (the 64-byte,
-128-byte and 256-byte window lines)."""
+128-byte and 256-byte window lines). RT_SPLIT=1 adds a 4M-node split-policy table (the general lines): counts 8, 14, 32."""
 import json
 import os
 import sys
@@ -32,4 +32,26 @@ for k in (8, 14, 16, 17, 24, 32):
     b.record()
     torch.cuda.synchronize()
     res[f"rt_k{k}_us"] = round(a.elapsed_time(b) / REPS * 1e3, 1)
+if os.environ.get("RT_SPLIT"):
+    from opendht_amd import synth as S  # noqa: E402
+
+    T.close()
+    del sh
+    n = 4_000_000
+    ids, st = S.random_ids(n, 0xB5), S.random_status(n, 0xB6)
+    perm, first, off = S.split_table(ids)
+    T = DeviceTable(ids[perm], st[perm], first, off, device=0)
+    g = torch.Generator(device=dev)
+    g.manual_seed(11)
+    tgs = [torch.randint(0, 256, (Q, 20), dtype=torch.uint8, device=dev, generator=g) for _ in range(NB)]
+    for k in (8, 14, 32):
+        outs = [T.rt_closest(tgs[j], k) for j in range(NB)]
+        torch.cuda.synchronize()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for j in range(REPS):
+            T.rt_closest(tgs[j % NB], k, outs[j % NB][0], outs[j % NB][1])
+        b.record()
+        torch.cuda.synchronize()
+        res[f"split4M_k{k}_us"] = round(a.elapsed_time(b) / REPS * 1e3, 1)
 print(json.dumps(res), flush=True)
