@@ -1812,9 +1812,16 @@ __global__ __launch_bounds__(BLOCK) void rt_wl32_kernel(DevTable T, const uint8_
 //   D  half-cleaner 16 across lanes 0 and 1, then 8, 4, 2, 1 in-lane.
 // The values, masks and fallbacks are wl32_answer's, so the rows are identical.
 // ---------------------------------------------------------------------------------------
+// qdpp0: the same permute with old = 0, which the compiler folds into a following v_min (v_min_u32_dpp)
+template <int CTRL>
+__device__ __forceinline__ uint32_t qdpp0(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
+}
 template <int CTRL>
 __device__ __forceinline__ uint32_t qdpp(uint32_t v) {
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
+    // every row and bank enabled and quad_perm always names a lane of the quad, so the old value is never read:
+    // mov_dpp leaves it undefined (no v_mov to initialise it before every permute)
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, false);
 }
 constexpr int QP_X1 = 0xB1, QP_X2 = 0x4E, QP_X3 = 0x1B, QP_B0 = 0x00, QP_B1 = 0x55;  // quad_perm encodings
 
@@ -1825,7 +1832,7 @@ __device__ __forceinline__ void quad_exchange(uint32_t (&v)[16], bool low) {
     uint32_t w[16];
     const uint32_t c = low ? 0u : 0xFFFFFFFFu;
 #pragma unroll
-    for (int i = 0; i < 16; i++) w[i] = qdpp<CTRL>(v[REV ? 15 - i : i]);
+    for (int i = 0; i < 16; i++) w[i] = (CTRL == QP_X3 ? qdpp0<CTRL>(v[REV ? 15 - i : i]) : qdpp<CTRL>(v[REV ? 15 - i : i]));
 #pragma unroll
     for (int i = 0; i < 16; i++) v[i] = max(min(v[i], w[i]), min(max(v[i], w[i]), c));
 }
@@ -1852,11 +1859,14 @@ __device__ __forceinline__ void quad_row(const uint32_t (&v)[16], uint32_t r0, u
     }
 }
 
-template <bool RANK = true>  // RANK false: timing ablation only (the values unranked; results wrong)
+// RANK false: timing ablation only (the values unranked; results wrong). LOAD_ALL: the table has the line set, so
+// lanes without a query load bucket b's line too (b = 0 for them; their answer is never stored) instead of filling
+// the registers with NONE under a branch.
+template <bool RANK = true, bool LOAD_ALL = false>
 __device__ __forceinline__ bool wl32_answer4(const DevTable& T, const Target& t, uint32_t b, uint32_t count, bool act,
                                              uint32_t p, uint32_t (&v)[16], uint32_t& m, uint32_t& base) {
     uint32_t L[16];
-    if (act) {
+    if (LOAD_ALL || act) {
         const uint4* lp = T.wl32 + (WL32_STRIDE / 4) * (size_t)b;
 #pragma unroll
         for (int x = 0; x < 4; x++) {
@@ -1974,7 +1984,7 @@ __global__ __launch_bounds__(BLOCK) void rt_wl32q_kernel(DevTable T, const uint8
         b = locate_bucket(T, t);
     }
     uint32_t v[16], m, base;
-    const bool ok = wl32_answer4<ABL == 0>(T, t, b, count, act, p, v, m, base);
+    const bool ok = wl32_answer4<ABL == 0, true>(T, t, b, count, act, p, v, m, base);  // launched on TF_WL32 tables
     const uint32_t r0 = 16u * (p & 1u), bi = base + T.index_base;
     uint32_t o[16];
     quad_row(v, r0, bi, m, count, act && ok, o);
@@ -2436,10 +2446,11 @@ __device__ __forceinline__ bool gl32_answer(const DevTable& T, const Target& t, 
 // reference's split-policy shape): lane p of the quad loads 64 of the line's 256 bytes (dwords 16x + 4p .. +3), sorts
 // its 16 slot values and the quad merges them to the top 32 (as wl32_answer4). The header is lane 0's dwords 0..3
 // and lane 1's 4, 5; the values, masks and fallbacks are gl32_answer's, so the rows are identical.
+template <bool LOAD_ALL = false>  // as wl32_answer4's
 __device__ __forceinline__ bool gl32_answer4(const DevTable& T, const Target& t, uint32_t b, uint32_t count, bool act,
                                              uint32_t p, uint32_t (&v)[16], uint32_t& m, uint32_t& base) {
     uint32_t L[16];
-    if (act) {
+    if (LOAD_ALL || act) {
         const uint4* lp = T.gl32 + (GL32_STRIDE / 4) * (size_t)b;
 #pragma unroll
         for (int x = 0; x < 4; x++) {
@@ -2499,7 +2510,7 @@ __global__ __launch_bounds__(BLOCK) void rt_gl32q_kernel(DevTable T, const uint8
         b = locate_bucket(T, t);
     }
     uint32_t v[16], m, base;
-    const bool ok = gl32_answer4(T, t, b, count, act, p, v, m, base);
+    const bool ok = gl32_answer4<true>(T, t, b, count, act, p, v, m, base);  // launched on TF_GL32 tables
     const uint32_t r0 = 16u * (p & 1u), bi = base + T.index_base;
     uint32_t o[16];
     quad_row(v, r0, bi, m, count, act && ok, o);
@@ -3238,7 +3249,7 @@ __global__ __launch_bounds__(BLOCK) void rt_dual_wl32q_kernel(DevTable T4, DevTa
     const bool wl = act && (T.flags & (GL ? TF_GL32 : TF_WL32));
     const uint32_t b = wl ? locate_bucket(T, t) : 0u;
     uint32_t v[16], m, base;
-    const bool ok = GL ? gl32_answer4(T, t, b, count, wl, p, v, m, base) : wl32_answer4<true>(T, t, b, count, wl, p, v, m, base);
+    const bool ok = GL ? gl32_answer4<false>(T, t, b, count, wl, p, v, m, base) : wl32_answer4<true>(T, t, b, count, wl, p, v, m, base);
     const uint32_t r0 = 16u * (p & 1u), bi = base + T.index_base;
     uint32_t o[16];
     quad_row(v, r0, bi, m, count, wl && ok, o);
