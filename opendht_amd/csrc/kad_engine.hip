@@ -918,8 +918,32 @@ __device__ __forceinline__ void store_row8(uint32_t* row, const uint32_t (&o)[8]
     }
 }
 
-// ABL 1 = no exact path, 2 = also no ranking (timing ablations only).
-template <int ABL>
+// The wave's count-8 rows through LDS, stored as two 1 KB runs of 16-byte non-temporal pieces at consecutive addresses
+// (piece 64h + lane = half lane & 1 of the row of query 32h + lane / 2); only the rows of lanes with `st` are written
+// (the others are left to their fallbacks). Needs i = blockIdx.x * BLOCK + threadIdx.x, count 8 and a 16-byte aligned
+// out_idx; call from wave-uniform control flow. The headline's rows: 31.85 -> 31.0 us per 1M (profiles/r03/ab_ws_cr/).
+__device__ __forceinline__ void store_rows8_wave(uint32_t* __restrict__ out_idx, uint32_t i, const uint32_t (&o)[8],
+                                                 bool st) {
+    __shared__ uint4 wrow[BLOCK / 64][128];
+    const uint32_t lane = threadIdx.x & 63u, i0 = i - lane;
+    uint4* R = wrow[threadIdx.x >> 6];
+    R[2 * lane] = make_uint4(o[0], o[1], o[2], o[3]);
+    R[2 * lane + 1] = make_uint4(o[4], o[5], o[6], o[7]);
+    const uint64_t okm = __ballot(st);
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    u32x4_t* r = reinterpret_cast<u32x4_t*>(out_idx + (size_t)i0 * 8u);
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+        const uint4 u = R[64 * h + lane];
+        if ((okm >> (32 * h + (lane >> 1))) & 1u) __builtin_nontemporal_store(u32x4_t{u.x, u.y, u.z, u.w}, r + 64 * h + lane);
+    }
+}
+
+// ABL 1 = no exact path, 2 = also no ranking (timing ablations only). CR: count-8 rows as wave runs (store_rows8_wave;
+// the launch path; the resident service keeps per-lane rows).
+template <int ABL, bool CR = false>
 __device__ __forceinline__ void rt_wl_kernel_body(const DevTable& T, const uint8_t* __restrict__ targets, uint32_t q,
                                                       uint32_t count, uint32_t* __restrict__ out_idx,
                                                       uint8_t* __restrict__ out_cnt) {
@@ -934,7 +958,10 @@ __device__ __forceinline__ void rt_wl_kernel_body(const DevTable& T, const uint8
     }
     uint32_t o[8], m;
     const bool ok = wl_answer<ABL>(T, t, b, count, act, o, m);
-    if (act && ok) {
+    if (CR && count == 8 && ((uintptr_t)out_idx & 15u) == 0) {  // kernel-uniform
+        store_rows8_wave(out_idx, i, o, act && ok);
+        if (act && ok && out_cnt) out_cnt[i] = (uint8_t)m;
+    } else if (act && ok) {
         store_row8(out_idx + (size_t)i * count, o, count);
         if (out_cnt) out_cnt[i] = (uint8_t)m;
     }
@@ -945,7 +972,7 @@ template <int ABL>
 __global__ __launch_bounds__(BLOCK) void rt_wl_kernel(DevTable T, const uint8_t* __restrict__ targets, uint32_t q,
                                                       uint32_t count, uint32_t* __restrict__ out_idx,
                                                       uint8_t* __restrict__ out_cnt) {
-    rt_wl_kernel_body<ABL>(T, targets, q, count, out_idx, out_cnt);
+    rt_wl_kernel_body<ABL, true>(T, targets, q, count, out_idx, out_cnt);
 }
 
 // The good nodes of bucket x in index order: fn(node index, key). Buckets of <= 32 nodes take their good
@@ -1252,21 +1279,7 @@ __device__ __forceinline__ void rt_ws_kernel_body(const DevTable& T, const uint8
     uint32_t o[8], m;
     const bool ok = ws_answer<ABL>(T, t, b, count, act, o, m);
     if (CR && count == 8 && ((uintptr_t)out_idx & 15u) == 0) {  // count: kernel-uniform, so the branch is too
-        __shared__ uint4 wrow[BLOCK / 64][128];
-        const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6, i0 = i - lane;
-        uint4* R = wrow[w];
-        R[2 * lane] = make_uint4(o[0], o[1], o[2], o[3]);
-        R[2 * lane + 1] = make_uint4(o[4], o[5], o[6], o[7]);
-        const uint64_t okm = __ballot(act && ok);
-        __builtin_amdgcn_wave_barrier();
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_wave_barrier();
-        u32x4_t* r = reinterpret_cast<u32x4_t*>(out_idx + (size_t)i0 * 8u);
-#pragma unroll
-        for (int h = 0; h < 2; h++) {  // piece 64h + lane = half (lane & 1) of the row of query 32h + lane / 2
-            const uint4 u = R[64 * h + lane];
-            if ((okm >> (32 * h + (lane >> 1))) & 1u) __builtin_nontemporal_store(u32x4_t{u.x, u.y, u.z, u.w}, r + 64 * h + lane);
-        }
+        store_rows8_wave(out_idx, i, o, act && ok);
         if (act && ok && out_cnt) out_cnt[i] = (uint8_t)m;
     } else if (act && ok) {
         if (NTS && count == 8 && ((uintptr_t)out_idx & 15u) == 0) {
@@ -2334,7 +2347,7 @@ __device__ __forceinline__ bool sl_answer(const DevTable& T, uint64_t thi, uint3
 
 // count <= 8 on a general table with slot lines: the slot line, else locate + the 128-byte line, else exact.
 // ABL 1 (timing ablation only, results wrong): slot lines only.
-template <int ABL>
+template <int ABL, bool CR = false>  // CR: as rt_wl_kernel_body
 __device__ __forceinline__ void rt_sl_kernel_body(
     const DevTable& T, const uint8_t* __restrict__ targets, uint32_t q, uint32_t count, uint32_t* __restrict__ out_idx,
     uint8_t* __restrict__ out_cnt) {
@@ -2345,7 +2358,10 @@ __device__ __forceinline__ void rt_sl_kernel_body(
     const bool in = act && thi >= T.rbase && ((thi - T.rbase) >> T.slshift) < T.slslots;
     uint32_t o[8], m, bh;
     const bool ok = sl_answer(T, thi, in ? (uint32_t)((thi - T.rbase) >> T.slshift) : 0u, count, in, o, m, bh);
-    if (act && ok) {
+    if (CR && count == 8 && ((uintptr_t)out_idx & 15u) == 0) {  // kernel-uniform
+        store_rows8_wave(out_idx, i, o, act && ok);
+        if (act && ok && out_cnt) out_cnt[i] = (uint8_t)m;
+    } else if (act && ok) {
         store_row8(out_idx + (size_t)i * count, o, count);
         if (out_cnt) out_cnt[i] = (uint8_t)m;
     }
@@ -2372,7 +2388,7 @@ template <int ABL>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) void rt_sl_kernel(
     DevTable T, const uint8_t* __restrict__ targets, uint32_t q, uint32_t count, uint32_t* __restrict__ out_idx,
     uint8_t* __restrict__ out_cnt) {
-    rt_sl_kernel_body<ABL>(T, targets, q, count, out_idx, out_cnt);
+    rt_sl_kernel_body<ABL, true>(T, targets, q, count, out_idx, out_cnt);
 }
 
 // Fallback slot lines (dw1 == NONE) and those without a bucket (dw0 == NONE): cnt[0], cnt[1] (KAD_DEBUG).
