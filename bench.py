@@ -861,6 +861,7 @@ def refresh_pass(T, sh, tgs, outs, ocnt, cnt_k, Q, avg_kernel_s, dev, stream, re
         flips = int(np.searchsorted(D, now, "left") - np.searchsorted(D, t0, "left"))
         g_ms, h_ms = timed(lambda: T.refresh_status(now, stream=stream.cuda_stream))
         ticks[f"{dt_ms}ms"] = {"gpu_ms": g_ms, "host_call_ms": h_ms, "aged_nodes": flips}
+    live, now = live_pass(T, sh, tgs, outs, ocnt, cnt_k, Q, dev, stream, now, t, rt, ex, D)
     rng = np.random.default_rng(0xF11)
     st_now = T.export_status()
     good = np.flatnonzero(st_now & 1).astype(np.uint32)
@@ -894,7 +895,7 @@ def refresh_pass(T, sh, tgs, outs, ocnt, cnt_k, Q, avg_kernel_s, dev, stream, re
             "refresh_ageing_ms": ageing,
             "patch_status_ms": patch,
             "nodes": int(n),
-            "refresh_plus_query_queries_per_s": Q / (no_flip_gpu * 1e-3 + avg_kernel_s),
+            "live": live,
             "how": "refresh_no_flip: kad_table_refresh_status(now) with `now` moved by 1 ns .. 5 ns (below the next "
                    "isGood deadline: the call returns without GPU work), median of 5: GPU time between HIP events and "
                    "the host time of the call; refresh_first: the first refresh after set_times (every node, the "
@@ -903,7 +904,68 @@ def refresh_pass(T, sh, tgs, outs, ocnt, cnt_k, Q, avg_kernel_s, dev, stream, re
                    "refresh_ageing: patch_times of that share of the good nodes as last heard 10 min + 1 ns ago, "
                    "then the refresh (GPU ms); patch_status: kad_table_patch_status of a random changed-node list of "
                    "that share of the nodes (host list, synchronous, wall clock incl. the H2D copy); "
-                   "refresh_plus_query: one no-flip refresh + one step"}
+                   "live: see its own `how`"}
+
+
+def live_pass(T, sh, tgs, outs, ocnt, cnt_k, Q, dev, stream, now, t, rt, ex, D, K=400, W=20, vrows=65536):
+    """The query rate with `now` following the clock, as a live node calls the table (routing_table.cpp:77 and
+    node.cpp:34-40 evaluate isGood(now) on every call): each step is kad_table_refresh_status(now) with `now` =
+    the start time + the wall-clock time elapsed since, then one batch of Q queries on the same stream (a
+    distinct batch per step). The node times are a live table's (good nodes heard over the last 10 minutes:
+    a deadline passes every ~60 us on a 1/8 shard), so most refreshes return at once and the others re-derive
+    the nodes whose deadline passed (the small path). Eager issue from Python, HIP events around every refresh
+    for its GPU time. The last step's first `vrows` rows are checked against the CPU restatement at that
+    step's `now`."""
+    import torch
+
+    MIN = 60 * 10**9
+    NB = len(tgs)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+    base = now
+    for j in range(W):  # warm-up: the same loop, untimed
+        now = base + j * 30_000
+        T.refresh_status(now, stream=stream.cuda_stream)
+        T.rt_closest(tgs[j % NB], cnt_k, outs[j % NB], ocnt[j % NB], stream=stream.cuda_stream)
+    torch.cuda.synchronize(dev)
+    start = now
+    nows = []
+    t0 = time.perf_counter()
+    for j in range(K):
+        now = start + int((time.perf_counter() - t0) * 1e9)
+        nows.append(now)
+        a, b = evs[j]
+        a.record(stream)
+        T.refresh_status(now, stream=stream.cuda_stream)
+        b.record(stream)
+        T.rt_closest(tgs[j % NB], cnt_k, outs[j % NB], ocnt[j % NB], stream=stream.cuda_stream)
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t0
+    rf = np.array([a.elapsed_time(b) for a, b in evs])
+    passed = int(np.searchsorted(D, nows[-1], "left") - np.searchsorted(D, start, "left"))
+    # the last step at its `now`: isGood / isExpired from the host copies of the times
+    st = (((ex == 0) & (rt >= nows[-1] - 120 * MIN) & (t >= nows[-1] - 10 * MIN)).astype(np.uint8) |
+          (ex << 1)).astype(np.uint8)
+    last = (K - 1) % NB
+    vr = min(Q, vrows)
+    bad = verify_rows(sh.ids, st, sh.first, sh.off, sh.index_base, tgs[last][:vr].cpu().numpy(),
+                      outs[last][:vr].cpu().numpy(), ocnt[last][:vr].cpu().numpy(), cnt_k)
+    work = rf > 0.003
+    live = {"queries_per_s": Q * K / wall,
+            "ms_per_step": wall / K * 1e3,
+            "steps": K,
+            "now_advanced_ms": (nows[-1] - start) / 1e6,
+            "deadlines_passed": passed,
+            "refreshes_with_gpu_work": int(work.sum()),
+            "refresh_gpu_ms_mean": float(rf.mean()),
+            "refresh_gpu_ms_median_with_work": float(np.median(rf[work])) if work.any() else 0.0,
+            "refresh_gpu_ms_max": float(rf.max()),
+            "refresh_share": float(rf.sum() / (wall * 1e3)),
+            "verified": {"rows": vr, "mismatches": bad,
+                         "what": "the first rows of the last step against the CPU restatement at that step's `now`"},
+            "how": "K steps of refresh_status(now = start + elapsed wall time) + one Q-query batch on one stream, "
+                   "eager; queries_per_s = K*Q / wall; refresh GPU time between HIP events around each refresh "
+                   "(a refresh below the next deadline launches nothing: ~0 ms)"}
+    return live, nows[-1] + 1
 
 
 # ---------------------------------------------------------------------------------------------

@@ -168,9 +168,14 @@ int kad_table_patch_times(kad_table* t, uint32_t m, const uint32_t* nodes, const
  * direct status change, or with `now` earlier than the last refresh's) re-derives every node and sorts
  * the deadlines; later ones re-derive only the nodes whose deadline `now` passed since the last refresh
  * and the nodes patched by kad_table_patch_times, and a refresh whose `now` has not reached the next
- * deadline (with nothing patched) returns at once without touching the GPU. Only flips cause mask and
- * line rebuilds. Async on `stream`; later refreshes and device batches must be ordered after it by the
- * caller (the host-pointer batches order themselves). */
+ * deadline (with nothing patched) returns at once without touching the GPU. The host keeps a copy of the
+ * sorted deadlines (8 bytes per node) and finds the passed ones itself. Up to 2,048 such nodes take the
+ * small path: one kernel re-derives them and lists the changed buckets and the lines whose windows reach
+ * them, then the line builders rebuild only those (no pass over the buckets or the lines); more take the
+ * flag-and-compact path. Async on `stream` (the first refresh after set_times waits for the sort);
+ * later refreshes and device batches must be ordered after it by the caller (the host-pointer batches
+ * order themselves). A refresh that changes anything ends the table's resident query service launch
+ * (kad_table_serve) first. */
 int kad_table_refresh_status(kad_table* t, int64_t now_ns, void* stream);
 
 /* ---- incremental device mirror ----------------------
@@ -236,10 +241,16 @@ int kad_rt_closest_batch_host(const kad_table* t, const uint8_t* targets, uint32
  * count <= KAD_SERVE_MAX_COUNT (kad_rt_closest_batch_host, kad_nc_closest_batch_host) from a mailbox in
  * pinned host memory: no kernel launch and no stream synchronise per call. Same results, same ordering
  * (after the table's last asynchronous status refresh). A launch ends by itself after idle_us without a
- * request or after one second in all, and the next request launches it again. Calls that change or free
- * what it reads (patch/update_status, patch/set_times, apply, nc_apply, set_addrs, prepare, destroy) end it
- * first. While it runs, device-wide synchronisation (hipDeviceSynchronize, torch.cuda.synchronize) waits for
- * it to go idle. idle_us = 0 ends it and turns it off (the default). idle_us <= KAD_SERVE_MAX_IDLE_US. */
+ * request or after 50 ms in all, and the next request launches it again. Calls that change or free what
+ * it reads (patch/update_status, patch/set_times, a refresh_status that changes anything, apply, nc_apply,
+ * set_addrs, prepare, destroy) end it first. While it runs it holds one CU, and:
+ *   - device-wide synchronisation (hipDeviceSynchronize, torch.cuda.synchronize) waits for it to go idle
+ *     (up to idle_us after the last request, or the rest of its 50 ms life);
+ *   - HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues (4 by default): work queued on a stream that
+ *     shares the service's queue waits behind the resident launch the same way. With more than four
+ *     streams in the process, keep idle_us short (a few hundred microseconds) or call kad_table_serve(t, 0)
+ *     before long device work.
+ * idle_us = 0 ends it and turns it off (the default). idle_us <= KAD_SERVE_MAX_IDLE_US. */
 #define KAD_SERVE_MAX_Q 64
 #define KAD_SERVE_MAX_COUNT 64
 #define KAD_SERVE_MAX_IDLE_US 1000000
@@ -264,7 +275,10 @@ int kad_rt_find_bucket_batch(const kad_table* t, const uint8_t* targets, uint32_
 /* ---- queries: NodeCache::getCachedNodes --------------------------------- */
 /* Batched NodeCache::getCachedNodes(target, af, count) (node_cache.cpp:36-66) over
  * one family's map, snapshotted as a KAD_TABLE_SORTED table. Emits non-expired
- * nodes in the reference's two-pointer walk order (NOT sorted by distance). */
+ * nodes in the reference's two-pointer walk order (NOT sorted by distance). Any count, as the
+ * reference's size_t count (node_cache.h:32): counts up to 16 / 32 run the NodeCache line kernels,
+ * 33..64 one wave per query, larger ones the serial walk (a lane per query); out_cnt saturates at 255
+ * (for count > 255 the result length is the row's entries before the first KAD_NO_NODE). */
 int kad_nc_closest_batch(const kad_table* t, const uint8_t* targets, uint32_t q, uint32_t count,
                          uint32_t* out_idx, uint8_t* out_cnt, void* stream);
 int kad_nc_closest_batch_host(const kad_table* t, const uint8_t* targets, uint32_t q, uint32_t count,
@@ -279,7 +293,8 @@ int kad_rt_closest_batch_dual(const kad_table* table4, const kad_table* table6,
 
 /* Per-query family select for NodeCache::getCachedNodes(id, sa_family, count) (node_cache.cpp:36-66:
  * cache_4 or cache_6 by family; Dht::refill asks the search's family, dht.cpp:1650): af[i] = 0 -> table4,
- * 1 -> table6 (KAD_TABLE_SORTED tables; either may be NULL = an empty map). count <= 64. Device pointers. */
+ * 1 -> table6 (KAD_TABLE_SORTED tables; either may be NULL = an empty map). Any count (as kad_nc_closest_batch).
+ * Device pointers. */
 int kad_nc_closest_batch_dual(const kad_table* table4, const kad_table* table6,
                               const uint8_t* targets, const uint8_t* af, uint32_t q, uint32_t count,
                               uint32_t* out_idx, uint8_t* out_cnt, void* stream);

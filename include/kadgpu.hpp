@@ -448,6 +448,9 @@ public:
     template <class InfoHashT>
     std::vector<std::vector<NodePtr>> getCachedNodesBatch(const InfoHashT* ids, size_t q, size_t count) const {
         std::vector<std::vector<NodePtr>> out(q);
+        // any size_t count, as node_cache.h:32: a result never holds more than the map's nodes
+        count = std::min(count, nodes_.size());
+        if (count == 0 || q == 0) return out;
         std::vector<size_t> todo(q);
         for (size_t i = 0; i < q; i++) todo[i] = i;
         while (!todo.empty()) {
@@ -462,7 +465,10 @@ public:
                 std::vector<NodePtr>& o = out[todo[k]];
                 o.clear();
                 bool ok = true;
-                for (size_t j = 0; j < cnt[k]; j++) {
+                size_t m = cnt[k];
+                if (count > 255)  // the count byte saturates: the row's padding gives the length
+                    for (m = 0; m < count && idx[k * count + m] != KAD_NO_NODE; m++) {}
+                for (size_t j = 0; j < m; j++) {
                     const uint32_t x = idx[k * count + j];
                     NodePtr n = nodes_[x].lock();
                     if (!n || n->isExpired()) { stale.push_back(x); ok = false; continue; }

@@ -16,7 +16,7 @@
 //   status[n]   u8   bit0 isGood(now), bit1 isExpired()   (NodeCache walk, wide-bucket fallback)
 //   dir[B+1]    u32x2 {first node of bucket b (bit31: bucket wider than 32 nodes), good bitmask of
 //                      b's nodes}: 8 bytes per bucket, good counts are popcounts
-//   gpre[B+1]   u32  good nodes in buckets < b (slow path / deferred queries)
+//   gcnt[B+1]   u32  good nodes of bucket b (gcnt[B] = 0): window sizes for the slow path and the line builders
 //   dmask[B]    u32  "top 64 ID bits shared with another node" bitmask (only if any node has one)
 //   fkey[B], ftail[B][3]   bucket `first` IDs (read only when the radix slot is ambiguous)
 //   rrdx[S+1]   u32  #bucket firsts below radix slot s (bit31: bucket starts exactly at slot)
@@ -92,7 +92,7 @@ struct DevTable {
     const uint32_t* tail;
     const uint8_t* status;
     const uint2* dir;
-    const uint32_t* gpre;
+    const uint32_t* gcnt;  // good nodes per bucket, B + 1 entries (the last 0)
     const uint32_t* dmask;
     const uint64_t* fkey;
     const uint32_t* ftail;
@@ -619,11 +619,46 @@ __device__ void wave_rank(const DevTable& T, const Target& t, uint32_t beg, uint
     }
 }
 
-// W(R) of a wave-uniform target on one table (routing_table.cpp:89-104 closed form): lane l tests
-// round r0 + l from the good prefix sums, a ballot gives the least R; 64 rounds per probe.
-// Returns the window's buckets [lo, hi] and good count.
-__device__ __forceinline__ void wave_window(const uint32_t* gpre, uint32_t B, uint32_t b, uint32_t count,
+// Good nodes that round r adds to the window of bucket b: W(0) = [b-1, b], round r >= 1 adds b-1-r and b+r
+// (each only if it exists; routing_table.cpp:89-104 closed form).
+__device__ __forceinline__ uint32_t ring_good(const uint32_t* gcnt, uint32_t B, uint32_t b, uint32_t r) {
+    if (r == 0) return gcnt[b] + (b ? gcnt[b - 1] : 0u);
+    return (b > r ? gcnt[b - 1 - r] : 0u) + ((uint64_t)b + r < (uint64_t)B ? gcnt[b + r] : 0u);
+}
+
+// W(R) of a wave-uniform target on one table (routing_table.cpp:89-104 closed form): lane l takes round
+// r0 + l, a wave scan of the per-round good counts gives each round's window size and a ballot the least R;
+// 64 rounds per probe. Returns the window's buckets [lo, hi] and good count.
+__device__ __forceinline__ void wave_window(const uint32_t* gcnt, uint32_t B, uint32_t b, uint32_t count,
                                             uint32_t& lo, uint32_t& hi, uint32_t& good) {
+    const uint32_t lane = threadIdx.x & 63u;
+    uint32_t carry = 0;
+    for (uint32_t r0 = 0;; r0 += 64) {
+        const uint32_t r = r0 + lane;
+        const uint32_t l_ = b > r ? b - 1 - r : 0u;
+        const uint32_t h_ = (uint64_t)b + r >= (uint64_t)B - 1 ? B - 1 : b + r;
+        uint32_t g_ = ring_good(gcnt, B, b, r);
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(g_, o, 64);
+            if (lane >= (uint32_t)o) g_ += y;
+        }
+        g_ += carry;
+        const uint64_t ok = __ballot(g_ >= count || (l_ == 0 && h_ == B - 1));
+        if (ok) {
+            const uint32_t R = (uint32_t)__builtin_ctzll(ok);
+            lo = rdl(l_, R);
+            hi = rdl(h_, R);
+            good = rdl(g_, R);
+            return;
+        }
+        carry = rdl(g_, 63);
+    }
+}
+
+// wave_window over good prefix sums (the north-star shard's replicated global directory, GB + 1 entries).
+__device__ __forceinline__ void wave_window_pre(const uint32_t* gpre, uint32_t B, uint32_t b, uint32_t count,
+                                                uint32_t& lo, uint32_t& hi, uint32_t& good) {
     const uint32_t lane = threadIdx.x & 63u;
     for (uint32_t r0 = 0;; r0 += 64) {
         const uint32_t r = r0 + lane;
@@ -641,6 +676,16 @@ __device__ __forceinline__ void wave_window(const uint32_t* gpre, uint32_t B, ui
     }
 }
 
+// Sum of gcnt[a, e) by the whole wave (wave-uniform arguments).
+__device__ __forceinline__ uint32_t wave_good_sum(const uint32_t* gcnt, uint32_t a, uint32_t e) {
+    const uint32_t lane = threadIdx.x & 63u;
+    uint32_t s = 0;
+    for (uint32_t x = a + lane; x < e; x += 64) s += gcnt[x];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    return s;
+}
+
 __device__ void wave_exact(const DevTable& T, const Target& t, uint32_t count, uint32_t* row, uint8_t* cp,
                            uint64_t* xs /* this wave's 64 x 3 LDS words */) {
     const uint32_t lane = threadIdx.x & 63u, B = T.B;
@@ -650,7 +695,7 @@ __device__ void wave_exact(const DevTable& T, const Target& t, uint32_t count, u
         return;
     }
     uint32_t lo, hi, good;
-    wave_window(T.gpre, B, locate_bucket(T, t), count, lo, hi, good);
+    wave_window(T.gcnt, B, locate_bucket(T, t), count, lo, hi, good);
     wave_rank(T, t, T.dir[lo].x & ~WIDE, T.dir[hi + 1].x & ~WIDE, good, count, row, nullptr, xs);
     if (lane == 0 && cp) *cp = (uint8_t)min(count, good);
 }
@@ -761,7 +806,7 @@ __global__ __launch_bounds__(BLOCK) void rt_wave_kernel(DevTable T4, DevTable T6
         return;
     }
     uint32_t lo, hi, good;
-    wave_window(T.gpre, T.B, locate_bucket(T, t), count, lo, hi, good);
+    wave_window(T.gcnt, T.B, locate_bucket(T, t), count, lo, hi, good);
     wave_rank_any(T, t, T.dir[lo].x & ~WIDE, T.dir[hi + 1].x & ~WIDE, good, count, row, cp, xs[w]);
 }
 
@@ -1004,10 +1049,10 @@ __device__ __forceinline__ void for_good(const uint64_t* key, const uint8_t* sta
     }
 }
 
-// The good-node count of bucket x (popcount of its mask; gpre for wide buckets).
-__device__ __forceinline__ uint32_t good_of(const uint2* dir, const uint32_t* gpre, uint32_t x) {
+// The good-node count of bucket x (popcount of its mask; gcnt for wide buckets).
+__device__ __forceinline__ uint32_t good_of(const uint2* dir, const uint32_t* gcnt, uint32_t x) {
     const uint2 a = dir[x];
-    return (a.x & WIDE) ? gpre[x + 1] - gpre[x] : (uint32_t)__popc(a.y);
+    return (a.x & WIDE) ? gcnt[x] : (uint32_t)__popc(a.y);
 }
 
 // A line assembled in the thread's LDS row (odd stride: conflict-free), then stored as 16-byte pieces.
@@ -1018,24 +1063,16 @@ __device__ __forceinline__ void store_line(const uint32_t* L, uint32_t* dst) {
         *reinterpret_cast<uint4*>(dst + k) = make_uint4(L[k], L[k + 1], L[k + 2], L[k + 3]);
 }
 
-// Window lines after a status change (or at table creation): one thread per bucket (d = depth).
-// sel: every bucket's line, or only the listed ones (incremental status refresh).
-__global__ __launch_bounds__(BLOCK) void wl_build_kernel(const uint64_t* key, const uint8_t* status, const uint2* dir,
-                                                          const uint32_t* gpre, uint32_t B, uint32_t d, uint64_t pre0,
-                                                          uint32_t* lines, LineSel sel) {
-    __shared__ uint32_t lds[BLOCK][33];
-    // one item per thread, grid-stride (an incremental rebuild launches a capped grid)
-    for (uint32_t j_ = blockIdx.x * BLOCK + threadIdx.x;; j_ += gridDim.x * BLOCK) {
-        uint32_t b;
-        if (!sel.pick(j_, B, b)) return;
-        [&] {
-    uint32_t* L = lds[threadIdx.x];
+// Window line b after a status change (or at table creation), assembled in L (an LDS row of 33 dwords) and
+// stored (d = depth).
+__device__ void wl_build_line(const uint64_t* key, const uint8_t* status, const uint2* dir, const uint32_t* gcnt,
+                              uint32_t B, uint32_t d, uint64_t pre0, uint32_t* lines, uint32_t b, uint32_t* L) {
     for (int k = 0; k < 32; k++) L[k] = NONE;
     // R_8 and the per-round good counts (routing_table.cpp:89-104 closed form)
-    uint32_t h = 0, R8 = 3;
+    uint32_t h = 0, R8 = 3, g = 0;
     for (uint32_t r = 0; r < 3; r++) {
         const uint32_t lo = b > r ? b - 1 - r : 0u, hi = min(B - 1, b + r);
-        const uint32_t g = gpre[hi + 1] - gpre[lo];
+        g += ring_good(gcnt, B, b, r);
         const bool whole = lo == 0 && hi == B - 1;
         h |= (min(g, 63u) << (6 * r)) | ((whole ? 1u : 0u) << (18 + r));
         if (R8 == 3 && (g >= 8 || whole)) R8 = r;
@@ -1058,7 +1095,7 @@ __global__ __launch_bounds__(BLOCK) void wl_build_kernel(const uint64_t* key, co
             if (rk == j) x = y;
         }
         rounds |= (x >= b ? x - b : b - 1 - x) << (2 * j);
-        const uint32_t g = good_of(dir, gpre, x);
+        const uint32_t g = good_of(dir, gcnt, x);
         if (full || S + g > WL_SLOTS) { full = true; continue; }  // whole buckets only
         const uint32_t s0 = S;
         for_good(key, status, dir, x, [&](uint32_t n, uint64_t kn) {
@@ -1086,8 +1123,6 @@ __global__ __launch_bounds__(BLOCK) void wl_build_kernel(const uint64_t* key, co
     L[2] = rounds;
     L[3] = tie;
     store_line<32>(L, lines + 32ull * b);
-        }();
-    }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1138,30 +1173,8 @@ __device__ __forceinline__ void put_bits(uint32_t* L, uint32_t p, uint32_t w, ui
     L[k + 1] = (uint32_t)(x >> 32);
 }
 
-// One thread per bucket: short line b from 128-byte line b (sel as the 128-byte builder's). The source line is
-// staged in the thread's LDS row with eight 16-byte loads, the short line assembled in another (odd strides),
-// then stored as 16-byte pieces.
-__global__ __launch_bounds__(BLOCK) void ws_build_kernel(const uint32_t* __restrict__ wl, uint32_t B,
-                                                          uint32_t* __restrict__ ws, LineSel sel) {
-    __shared__ uint32_t lds[BLOCK][17];
-    __shared__ uint32_t src[BLOCK][33];
-    // one item per thread, grid-stride (an incremental rebuild launches a capped grid)
-    for (uint32_t j_ = blockIdx.x * BLOCK + threadIdx.x;; j_ += gridDim.x * BLOCK) {
-        uint32_t b;
-        if (!sel.pick(j_, B, b)) return;
-        [&] {
-    uint32_t* W = src[threadIdx.x];
-    {
-        const uint4* g = reinterpret_cast<const uint4*>(wl + 32ull * b);
-        uint4 v[8];
-#pragma unroll
-        for (int x = 0; x < 8; x++) v[x] = g[x];
-#pragma unroll
-        for (int x = 0; x < 8; x++) {
-            W[4 * x] = v[x].x; W[4 * x + 1] = v[x].y; W[4 * x + 2] = v[x].z; W[4 * x + 3] = v[x].w;
-        }
-    }
-    uint32_t* L = lds[threadIdx.x];
+// Short line b transcoded from its 128-byte line W (an LDS row), assembled in L (an LDS row of 17 dwords).
+__device__ void ws_build_line(const uint32_t* W, uint32_t* __restrict__ ws, uint32_t b, uint32_t* L) {
     const uint32_t h = W[1], rounds = W[2], S = (h >> 23) & 31u;
     bool fb = (h & WL_DEFER) != 0;
     // the longest whole-bucket prefix of the 128-byte line's slots that fits
@@ -1189,7 +1202,22 @@ __global__ __launch_bounds__(BLOCK) void ws_build_kernel(const uint32_t* __restr
     put_bits(L, WS_HDR, 23, hw);
     put_bits(L, WS_ROUNDS, 12, rk);
     store_line<16>(L, ws + 16ull * b);
-        }();
+}
+
+// Window lines, one thread per bucket: every bucket's line, or only the listed ones (sel: incremental status
+// refresh), grid-stride (an incremental rebuild launches a capped grid). WS: the short line of each bucket is
+// transcoded from the 128-byte line while it is still in the thread's LDS row.
+template <bool WS>
+__global__ __launch_bounds__(BLOCK) void wl_build_kernel(const uint64_t* key, const uint8_t* status, const uint2* dir,
+                                                          const uint32_t* gcnt, uint32_t B, uint32_t d, uint64_t pre0,
+                                                          uint32_t* lines, uint32_t* ws, LineSel sel) {
+    __shared__ uint32_t lds[BLOCK][33];
+    __shared__ uint32_t lds_s[WS ? BLOCK : 1][17];
+    for (uint32_t j_ = blockIdx.x * BLOCK + threadIdx.x;; j_ += gridDim.x * BLOCK) {
+        uint32_t b;
+        if (!sel.pick(j_, B, b)) return;
+        wl_build_line(key, status, dir, gcnt, B, d, pre0, lines, b, lds[threadIdx.x]);
+        if (WS) ws_build_line(lds[threadIdx.x], ws, b, lds_s[WS ? threadIdx.x : 0]);
     }
 }
 
@@ -1550,7 +1578,7 @@ __global__ __launch_bounds__(BLOCK) void rt_wl16_kernel(DevTable T, const uint8_
 
 // Window lines for counts 9..16 after a status change (or at creation): one thread per bucket.
 __global__ __launch_bounds__(BLOCK) void wl16_build_kernel(const uint64_t* key, const uint8_t* status, const uint2* dir,
-                                                            const uint32_t* gpre, uint32_t B, uint32_t d, uint64_t pre0,
+                                                            const uint32_t* gcnt, uint32_t B, uint32_t d, uint64_t pre0,
                                                             uint32_t* lines, LineSel sel) {
     __shared__ uint32_t lds[BLOCK][33];
     // one item per thread, grid-stride (an incremental rebuild launches a capped grid)
@@ -1560,10 +1588,11 @@ __global__ __launch_bounds__(BLOCK) void wl16_build_kernel(const uint64_t* key, 
         [&] {
     uint32_t* L = lds[threadIdx.x];
     for (uint32_t k = 0; k < WL16_STRIDE; k++) L[k] = NONE;
-    uint32_t h = 0, R = 4;
+    uint32_t h = 0, R = 4, g = 0, Gr[4];
     for (uint32_t r = 0; r < 4; r++) {
         const uint32_t lo = b > r ? b - 1 - r : 0u, hi = min(B - 1, b + r);
-        const uint32_t g = gpre[hi + 1] - gpre[lo];
+        g += ring_good(gcnt, B, b, r);
+        Gr[r] = g;
         const bool whole = lo == 0 && hi == B - 1;
         h |= (min(g, 31u) << (5 * r)) | ((whole ? 1u : 0u) << (20 + r));
         if (R == 4 && (g >= 16 || whole)) R = r;
@@ -1585,7 +1614,7 @@ __global__ __launch_bounds__(BLOCK) void wl16_build_kernel(const uint64_t* key, 
             if (rk == j) x = y;
         }
         xj[j] = x;
-        gj[j] = good_of(dir, gpre, x);
+        gj[j] = good_of(dir, gcnt, x);
         rounds |= (x >= b ? x - b : b - 1 - x) << (2 * j);
     }
     // Whole buckets, in four passes: (0) the D-rank prefix of W(R_14) up to its 14th good node (count 14 =
@@ -1607,7 +1636,7 @@ __global__ __launch_bounds__(BLOCK) void wl16_build_kernel(const uint64_t* key, 
     uint32_t R14 = R;
     for (int r = (int)R; r >= 0; r--) {
         const uint32_t lo_r = b > (uint32_t)r ? b - 1 - r : 0u, hi_r = min(B - 1, b + r);
-        if (gpre[hi_r + 1] - gpre[lo_r] >= 14u || (lo_r == 0 && hi_r == B - 1)) R14 = (uint32_t)r;
+        if (Gr[r] >= 14u || (lo_r == 0 && hi_r == B - 1)) R14 = (uint32_t)r;
     }
     for (uint32_t j = 0, cum = 0; j < nb && cum < 14u; j++)
         if (((rounds >> (2 * j)) & 3u) <= R14) {
@@ -2044,7 +2073,7 @@ __global__ __launch_bounds__(BLOCK) void rt_wl32q_kernel(DevTable T, const uint8
 // Window lines for counts 17..32 after a status change (or at creation): one thread per bucket.
 // The window's buckets are put in D order by rank (O(buckets^2), at most 16 buckets).
 __global__ __launch_bounds__(BLOCK) void wl32_build_kernel(const uint64_t* key, const uint8_t* status, const uint2* dir,
-                                                            const uint32_t* gpre, uint32_t B, uint32_t d, uint64_t pre0,
+                                                            const uint32_t* gcnt, uint32_t B, uint32_t d, uint64_t pre0,
                                                             uint32_t* lines, LineSel sel) {
     __shared__ uint32_t lds[BLOCK][WL32_STRIDE + 1];
     // one item per thread, grid-stride (an incremental rebuild launches a capped grid)
@@ -2054,10 +2083,11 @@ __global__ __launch_bounds__(BLOCK) void wl32_build_kernel(const uint64_t* key, 
         [&] {
     uint32_t* L = lds[threadIdx.x];
     for (uint32_t k = 0; k < WL32_STRIDE; k++) L[k] = NONE;
-    uint32_t g01 = 0, g23 = 0, whole = 0, R = 8;
+    uint32_t g01 = 0, g23 = 0, whole = 0, R = 8, gs = 0;
     for (uint32_t r = 0; r < 8; r++) {
         const uint32_t lo = b > r ? b - 1 - r : 0u, hi = min(B - 1, b + r);
-        const uint32_t g = min(gpre[hi + 1] - gpre[lo], 255u);
+        gs += ring_good(gcnt, B, b, r);
+        const uint32_t g = min(gs, 255u);
         const bool w = lo == 0 && hi == B - 1;
         if (r < 4) g01 |= g << (8 * r); else g23 |= g << (8 * (r - 4));
         whole |= (w ? 1u : 0u) << r;
@@ -2082,7 +2112,7 @@ __global__ __launch_bounds__(BLOCK) void wl32_build_kernel(const uint64_t* key, 
         const uint32_t x = ord[j];
         const uint32_t rd = x >= b ? x - b : b - 1 - x;
         if (j < 10) r04 |= rd << (3 * j); else r15 |= rd << (3 * (j - 10));
-        const uint32_t g = good_of(dir, gpre, x);
+        const uint32_t g = good_of(dir, gcnt, x);
         if (full || S + g > WL32_SLOTS) { full = true; continue; }  // whole buckets only
         const uint32_t s0 = S;
         for_good(key, status, dir, x, [&](uint32_t n, uint64_t kn) {
@@ -2770,14 +2800,15 @@ struct GlInfo {
 };
 
 template <int RMAX, uint32_t NEED, uint32_t SLOTS, uint32_t HDR>
-__device__ void gl_build_line(const uint64_t* key, const uint8_t* status, const uint2* dir, const uint32_t* gpre,
+__device__ void gl_build_line(const uint64_t* key, const uint8_t* status, const uint2* dir, const uint32_t* gcnt,
                               const uint64_t* fkey, const uint32_t* ftail, uint32_t B, uint32_t b, uint32_t* L,
                               GlInfo& I) {
     I.R = RMAX + 1; I.S = 0; I.cp = 0; I.base = 0; I.whole = 0; I.defer = false;
     for (int r = 0; r < 8; r++) { I.G[r] = 0; I.Sr[r] = 0; }
-    for (uint32_t r = 0; r <= (uint32_t)RMAX; r++) {
+    for (uint32_t r = 0, g = 0; r <= (uint32_t)RMAX; r++) {
         const uint32_t lo = b > r ? b - 1 - r : 0u, hi = min(B - 1, b + r);
-        I.G[r] = gpre[hi + 1] - gpre[lo];
+        g += ring_good(gcnt, B, b, r);
+        I.G[r] = g;
         const bool w = lo == 0 && hi == B - 1;
         I.whole |= (w ? 1u : 0u) << r;
         if (I.R > (uint32_t)RMAX && (I.G[r] >= NEED || w)) I.R = r;
@@ -2829,7 +2860,7 @@ __device__ void gl_build_line(const uint64_t* key, const uint8_t* status, const 
     uint32_t stored = 0, used = 0;  // bit (c - lo)
     bool full = false;
     for (uint32_t j = 0; j < nb; j++) {
-        const uint32_t x = ord[j], g = good_of(dir, gpre, x);
+        const uint32_t x = ord[j], g = good_of(dir, gcnt, x);
         if (full || used + g > SLOTS) { full = true; continue; }
         used += g;
         stored |= 1u << (x - lo);
@@ -2857,7 +2888,7 @@ __device__ void gl_build_line(const uint64_t* key, const uint8_t* status, const 
 }
 
 __global__ __launch_bounds__(BLOCK) void gl_build_kernel(const uint64_t* key, const uint8_t* status, const uint2* dir,
-                                                         const uint32_t* gpre, const uint64_t* fkey, const uint32_t* ftail,
+                                                         const uint32_t* gcnt, const uint64_t* fkey, const uint32_t* ftail,
                                                          uint32_t B, uint32_t* lines, LineSel sel) {
     __shared__ uint32_t lds[BLOCK][GL_STRIDE + 1];
     // one item per thread, grid-stride (an incremental rebuild launches a capped grid)
@@ -2868,7 +2899,7 @@ __global__ __launch_bounds__(BLOCK) void gl_build_kernel(const uint64_t* key, co
     uint32_t* L = lds[threadIdx.x];
     for (uint32_t k = 0; k < GL_STRIDE; k++) L[k] = NONE;
     GlInfo I;
-    gl_build_line<2, 8, GL_SLOTS, GL_HDR>(key, status, dir, gpre, fkey, ftail, B, b, L, I);
+    gl_build_line<2, 8, GL_SLOTS, GL_HDR>(key, status, dir, gcnt, fkey, ftail, B, b, L, I);
     uint32_t h = 0;
     for (int r = 0; r < 3; r++) h |= min(I.G[r], 63u) << (6 * r);
     h |= (I.whole & 7u) << 18;
@@ -2882,7 +2913,7 @@ __global__ __launch_bounds__(BLOCK) void gl_build_kernel(const uint64_t* key, co
 }
 
 __global__ __launch_bounds__(BLOCK) void gl16_build_kernel(const uint64_t* key, const uint8_t* status, const uint2* dir,
-                                                           const uint32_t* gpre, const uint64_t* fkey,
+                                                           const uint32_t* gcnt, const uint64_t* fkey,
                                                            const uint32_t* ftail, uint32_t B, uint32_t* lines,
                                                            LineSel sel) {
     __shared__ uint32_t lds[BLOCK][GL16_STRIDE + 1];
@@ -2892,7 +2923,7 @@ __global__ __launch_bounds__(BLOCK) void gl16_build_kernel(const uint64_t* key, 
         uint32_t* L = lds[threadIdx.x];
         for (uint32_t k = 0; k < GL16_STRIDE; k++) L[k] = NONE;
         GlInfo I;
-        gl_build_line<3, 16, GL16_SLOTS, GL16_HDR>(key, status, dir, gpre, fkey, ftail, B, b, L, I);
+        gl_build_line<3, 16, GL16_SLOTS, GL16_HDR>(key, status, dir, gcnt, fkey, ftail, B, b, L, I);
         uint32_t h = 0;
         for (int r = 0; r < 4; r++) h |= min(I.G[r], 63u) << (6 * r);
         L[0] = I.base;
@@ -2904,7 +2935,7 @@ __global__ __launch_bounds__(BLOCK) void gl16_build_kernel(const uint64_t* key, 
 }
 
 __global__ __launch_bounds__(BLOCK) void gl32_build_kernel(const uint64_t* key, const uint8_t* status, const uint2* dir,
-                                                           const uint32_t* gpre, const uint64_t* fkey,
+                                                           const uint32_t* gcnt, const uint64_t* fkey,
                                                            const uint32_t* ftail, uint32_t B, uint32_t* lines,
                                                            LineSel sel) {
     __shared__ uint32_t lds[BLOCK][GL32_STRIDE + 1];
@@ -2916,7 +2947,7 @@ __global__ __launch_bounds__(BLOCK) void gl32_build_kernel(const uint64_t* key, 
     uint32_t* L = lds[threadIdx.x];
     for (uint32_t k = 0; k < GL32_STRIDE; k++) L[k] = NONE;
     GlInfo I;
-    gl_build_line<7, 32, GL32_SLOTS, GL32_HDR>(key, status, dir, gpre, fkey, ftail, B, b, L, I);
+    gl_build_line<7, 32, GL32_SLOTS, GL32_HDR>(key, status, dir, gcnt, fkey, ftail, B, b, L, I);
     uint32_t g01 = 0, g23 = 0;
     for (int r = 0; r < 8; r++) {
         const uint32_t g = min(I.G[r], 255u);
@@ -3350,12 +3381,12 @@ __device__ void wave_shard(const DevTable& T, const ShardCtx& S, const Target& t
                            uint64_t* xs) {
     const uint32_t lane = threadIdx.x & 63u;
     uint32_t lo, hi, good;
-    wave_window(S.gpre, S.GB, shard_bucket(S, t), count, lo, hi, good);
+    wave_window_pre(S.gpre, S.GB, shard_bucket(S, t), count, lo, hi, good);
     const uint32_t a = max(lo, S.s_lo), e = min(hi + 1, S.s_hi);
     if (a >= e) return;
     const bool complete = lo >= S.s_lo && hi < S.s_hi;
     const uint32_t al = a - S.s_lo, el = e - S.s_lo;
-    const uint32_t lgood = T.gpre[el] - T.gpre[al];
+    const uint32_t lgood = wave_good_sum(T.gcnt, al, el);
     uint32_t slot = 0;
     const uint32_t region = blockIdx.x & 7u;
     if (lane == 0) slot = atomicAdd(S.ctr + KAD_SHARD_COUNTER_STRIDE * (complete ? region : 8u), 1u);
@@ -3765,7 +3796,7 @@ __device__ void nc_serial(const DevTable& T, const Target& t, uint32_t count, ui
         if (!(T.status[it] & KAD_STATUS_EXPIRED)) row[m++] = it + T.index_base;
     }
     for (uint32_t s = m; s < count; s++) row[s] = NONE;
-    if (cp) *cp = (uint8_t)m;
+    if (cp) *cp = (uint8_t)min(m, 255u);  // saturates (a count above 255 reads the length off the padding)
 }
 
 __global__ __launch_bounds__(BLOCK) void nc_closest_kernel(DevTable T, const uint8_t* __restrict__ targets,
@@ -3775,6 +3806,16 @@ __global__ __launch_bounds__(BLOCK) void nc_closest_kernel(DevTable T, const uin
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (i >= q) return;
     nc_serial(T, load_target(targets, i), count, out_idx + (size_t)i * count, out_cnt ? out_cnt + i : nullptr);
+}
+
+// Any count on the dual-family batch (counts above 64): the serial walk, one lane per query on its family's map.
+__global__ __launch_bounds__(BLOCK) void nc_closest_dual_kernel(DevTable T4, DevTable T6, const uint8_t* __restrict__ af,
+                                                                const uint8_t* __restrict__ targets, uint32_t q,
+                                                                uint32_t count, uint32_t* __restrict__ out_idx,
+                                                                uint8_t* __restrict__ out_cnt) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= q) return;
+    nc_serial(af[i] ? T6 : T4, load_target(targets, i), count, out_idx + (size_t)i * count, out_cnt ? out_cnt + i : nullptr);
 }
 
 // NodeCache::getCachedNodes, one wave per query (count <= 32). The walk is a greedy merge of the
@@ -5119,45 +5160,247 @@ __global__ void deadline_kernel(NodeTimes N, uint32_t n, uint64_t* __restrict__ 
     node[i] = i;
 }
 
-// lower_bound of x in the ascending k[lo, n), by the whole wave: each round 64 lanes probe evenly spaced
-// points and a ballot keeps the one interval that holds the answer (4 dependent loads for 12.5M keys).
-__device__ uint32_t wave_lower_bound(const uint64_t* k, uint32_t lo, uint32_t n, uint64_t x) {
-    const uint32_t lane = threadIdx.x & 63u;
-    uint32_t hi = n;  // the answer lies in [lo, hi]
-    while (hi - lo > 64) {
-        const uint32_t p = lo + (uint32_t)(((uint64_t)(hi - lo) * (lane + 1)) / 65);
-        const uint32_t c = (uint32_t)__builtin_popcountll(__ballot(k[p] < x));  // monotone in the lane
-        const uint32_t nlo = c ? rdl(p, c - 1) + 1 : lo;
-        const uint32_t nhi = c < 64 ? rdl(p, c) : hi;
-        lo = nlo;
-        hi = nhi;
-    }
-    const uint32_t j = lo + lane;
-    return lo + (uint32_t)__builtin_popcountll(__ballot(j < hi && k[j] < x));
-}
-
-// One wave. cur: [0] main cursor, [1] side cursor, [2..3] the main range passed now, [4..5] the side range.
-__global__ void dl_search_kernel(const uint64_t* __restrict__ km, uint32_t nm, const uint64_t* __restrict__ ks,
-                                 uint32_t ns, uint64_t nowk, uint32_t* __restrict__ cur, uint64_t* __restrict__ next) {
-    const uint32_t cm = cur[0], cs = cur[1];
-    const uint32_t hm = wave_lower_bound(km, cm, nm, nowk), hs = wave_lower_bound(ks, cs, ns, nowk);
-    if (threadIdx.x == 0) {
-        cur[2] = cm; cur[3] = hm; cur[4] = cs; cur[5] = hs;
-        cur[0] = hm; cur[1] = hs;
-        *next = min(hm < nm ? km[hm] : DL_NEVER, hs < ns ? ks[hs] : DL_NEVER);
-    }
-}
-
-// The nodes whose deadline `now` passed (both runs' ranges from dl_search_kernel) and the patched nodes:
-// status re-derived from their times. A node listed twice gets the same status twice.
-__global__ void dl_process_kernel(NodeTimes N, const uint32_t* __restrict__ mnode, const uint32_t* __restrict__ snode,
-                                  const uint32_t* __restrict__ cur, const uint32_t* __restrict__ pend, uint32_t np,
-                                  uint32_t n, int64_t now, uint8_t* status, StatusMarks M) {
-    const uint32_t a = cur[3] - cur[2], b = cur[5] - cur[4];
-    const uint64_t total = (uint64_t)a + b + np;
+// The nodes whose deadline `now` passed (main run [ma, ma + mc), side run [sa, sa + sc), both found by the host
+// on its copy of the run keys) and the patched nodes: status re-derived from their times (the large-refresh path:
+// flags, then the O(buckets) passes of rebuild_good_prefix). A node listed twice gets the same status twice.
+__global__ void dl_process_kernel(NodeTimes N, const uint32_t* __restrict__ mnode, uint32_t mc,
+                                  const uint32_t* __restrict__ snode, uint32_t sc, const uint32_t* __restrict__ pend,
+                                  uint32_t np, uint32_t n, int64_t now, uint8_t* status, StatusMarks M) {
+    const uint64_t total = (uint64_t)mc + sc + np;
     for (uint64_t j = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; j < total; j += (uint64_t)gridDim.x * BLOCK) {
-        const uint32_t i = j < a ? mnode[cur[2] + j] : j < (uint64_t)a + b ? snode[cur[4] + (j - a)] : pend[j - a - b];
+        const uint32_t i = j < mc ? mnode[j] : j < (uint64_t)mc + sc ? snode[j - mc] : pend[j - mc - sc];
         if (i < n) refresh_node(N, i, now, status, M);
+    }
+}
+
+__device__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* lds, uint32_t& total);
+
+// ---------------------------------------------------------------------------------------
+// Small refresh (at most RF_CAP nodes to re-derive: the steady state of a table whose `now` follows the
+// clock, where a few deadlines pass between two query batches). No pass over the buckets or the lines:
+//   rf_nodes_kernel  phase 1, every block: each listed node's status from its times (or a given value);
+//                    a good-bit change appends the node's bucket, an expired-bit change the NodeCache slot
+//                    range whose lines hold the node (wave-aggregated appends);
+//                    phase 2, the last block to finish (a completion counter, no grid barrier): the buckets
+//                    sorted and made unique in LDS, their masks and good counts recounted, and per line set
+//                    the union of the windows that can read them ([b-2, b+3] / [b-3, b+4] / [b-7, b+8]) written
+//                    as a sorted list, and the union of the NodeCache ranges
+//   line builders    the listed lines only (LineSel over those lists), grids sized by the host's bound.
+// The window good counts come from the per-bucket counts (gcnt), so nothing is O(buckets).
+// ---------------------------------------------------------------------------------------
+constexpr uint32_t RF_CAP = 2048;
+constexpr uint32_t RF_NB = 0, RF_NR = 1, RF_DONE = 2, RF_L8 = 3, RF_L16 = 4, RF_L32 = 5, RF_LNC = 6, RF_CTRS = 8;
+
+struct RfCtx {
+    NodeTimes N;
+    const uint32_t* mnode; uint32_t mc;  // main-run nodes whose deadline passed
+    const uint32_t* snode; uint32_t sc;  // side-run nodes whose deadline passed
+    const uint32_t* pend; uint32_t np;   // patched nodes
+    const uint8_t* vals;                 // NULL: every status from the times at `now`; else pend[j] gets vals[j]
+    int64_t now;
+    DevTable T;                          // locate (key, tail, radix, firsts), B, n
+    uint8_t* status;
+    uint2* dir;
+    uint32_t* gcnt;
+    uint32_t* blist;                     // RF_CAP appended buckets
+    uint32_t* nrange;                    // RF_CAP NodeCache slot ranges (first, last)
+    uint32_t* ctr;                       // RF_CTRS words
+    uint32_t* list[4];                   // lines of the count <= 8, 9..16, 17..32 sets and NodeCache slots (NULL: none)
+    uint32_t nback, nfwd;                // NodeCache windows, as StatusMarks
+};
+
+// One atomic per wave for the lanes with `want` (wave-uniform call); returns each wanting lane's slot.
+__device__ __forceinline__ uint32_t wave_append(uint32_t* ctr, bool want) {
+    const uint64_t m = __ballot(want);
+    if (!m) return 0;
+    const uint32_t lane = threadIdx.x & 63u, leader = (uint32_t)__builtin_ctzll(m);
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(ctr, (uint32_t)__builtin_popcountll(m));
+    base = __shfl(base, (int)leader, 64);
+    return base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// The bucket holding node i: the locate of its own ID (findBucket), checked against the directory; a table
+// whose node lies outside its bucket's range falls back to the search over the bucket starts.
+__device__ uint32_t node_bucket(const DevTable& T, const uint2* dir, uint32_t i) {
+    Target t;
+    t.hi = T.key[i];
+    const uint32_t* tl = T.tail + 3ull * i;
+    t.t2 = tl[0]; t.t3 = tl[1]; t.t4 = tl[2];
+    const uint32_t b = locate_bucket(T, t);
+    if ((dir[b].x & ~WIDE) <= i && i < (dir[b + 1].x & ~WIDE)) return b;
+    uint32_t lo = 0, hi = T.B;  // the last bucket whose first node is <= i
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if ((dir[mid].x & ~WIDE) <= i) lo = mid + 1; else hi = mid;
+    }
+    return lo ? lo - 1 : 0u;
+}
+
+// Ascending bitonic sort of a[0, P) in LDS by the block (P a power of two, block-uniform).
+__device__ void block_sort_u64(uint64_t* a, uint32_t P) {
+    for (uint32_t k = 2; k <= P; k <<= 1)
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t x = threadIdx.x; x < P; x += BLOCK) {
+                const uint32_t y = x ^ j;
+                if (y > x) {
+                    const uint64_t u = a[x], v = a[y];
+                    if ((x & k) == 0 ? u > v : u < v) { a[x] = v; a[y] = u; }
+                }
+            }
+            __syncthreads();
+        }
+}
+
+// Union of the sorted intervals [lo(u), hi(u)] (u < m, ascending lo) written as one sorted list of indices;
+// returns its length. iv(u) gives the interval; the ends need not ascend (a running maximum covers them).
+template <class IV>
+__device__ uint32_t block_union(uint32_t m, IV iv, uint32_t* out, uint32_t* lds4) {
+    uint32_t written = 0;
+    int64_t reach = -1;  // the largest end so far (block-uniform between chunks)
+    __shared__ int64_t chunk_end;
+    for (uint32_t c = 0; c < m; c += BLOCK) {  // block-uniform
+        const uint32_t u = c + threadIdx.x;
+        int64_t lo = 0, hi = -1;
+        if (u < m) { uint32_t a, e; iv(u, a, e); lo = a; hi = e; }
+        // the running maximum of the ends before u: an inclusive max-scan over the chunk, shifted by one
+        int64_t x = hi;
+        const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int64_t y = __shfl_up(x, o, 64);
+            if (lane >= (uint32_t)o) x = max(x, y);
+        }
+        __shared__ int64_t wmax[BLOCK / 64];
+        if (lane == 63) wmax[wid] = x;
+        __syncthreads();
+        int64_t before = reach;
+        for (uint32_t w = 0; w < wid; w++) before = max(before, wmax[w]);
+        const int64_t incl = max(before, x);
+        int64_t prev = __shfl_up(incl, 1, 64);
+        if (lane == 0) prev = before;
+        const int64_t s0 = max(lo, prev + 1);
+        const uint32_t cnt = (u < m && hi >= s0) ? (uint32_t)(hi - s0 + 1) : 0u;
+        uint32_t tot;
+        const uint32_t off = block_exclusive_scan(cnt, lds4, tot);
+        for (uint32_t k = 0; k < cnt; k++) out[written + off + k] = (uint32_t)(s0 + k);
+        written += tot;
+        if (threadIdx.x == BLOCK - 1) chunk_end = incl;
+        __syncthreads();
+        reach = chunk_end;
+        __syncthreads();
+    }
+    return written;
+}
+
+__global__ __launch_bounds__(BLOCK) void rf_nodes_kernel(RfCtx C) {
+    const DevTable& T = C.T;
+    const uint32_t total = C.mc + C.sc + C.np;
+    for (uint32_t base = blockIdx.x * BLOCK; base < total; base += gridDim.x * BLOCK) {  // block-uniform
+        const uint32_t j = base + threadIdx.x;
+        bool act = j < total;
+        uint32_t i = 0, st = 0, old = 0;
+        if (act) {
+            i = j < C.mc ? C.mnode[j] : j < C.mc + C.sc ? C.snode[j - C.mc] : C.pend[j - C.mc - C.sc];
+            act = i < T.n;
+        }
+        if (act) {
+            st = (C.vals && j >= C.mc + C.sc) ? (uint32_t)(C.vals[j - C.mc - C.sc] & (KAD_STATUS_GOOD | KAD_STATUS_EXPIRED))
+                                               : status_at(C.N, i, C.now);
+            old = C.status[i];
+            if (st != old) C.status[i] = (uint8_t)st;
+        }
+        const bool gchg = act && T.B && ((st ^ old) & KAD_STATUS_GOOD);
+        const uint32_t b = gchg ? node_bucket(T, C.dir, i) : 0u;
+        const uint32_t ob = wave_append(C.ctr + RF_NB, gchg);
+        if (gchg && ob < RF_CAP) C.blist[ob] = b;
+        const bool echg = act && C.list[3] && ((st ^ old) & KAD_STATUS_EXPIRED);
+        uint32_t sa = 0, se = 0;
+        if (echg) {  // every NodeCache slot from that of node i - nback to that of node i + nfwd (as mark_status_change)
+            const uint32_t a = i >= C.nback ? i - C.nback : 0u, e = min(T.n - 1, i + C.nfwd);
+            const uint64_t ka = T.key[a], ke = T.key[e];
+            sa = ka < T.nbase ? 0u : (uint32_t)min<uint64_t>((ka - T.nbase) >> T.nshift, T.nslots - 1);
+            se = ke < T.nbase ? 0u : (uint32_t)min<uint64_t>((ke - T.nbase) >> T.nshift, T.nslots - 1);
+        }
+        const uint32_t orr = wave_append(C.ctr + RF_NR, echg);
+        if (echg && orr < RF_CAP) { C.nrange[2 * orr] = sa; C.nrange[2 * orr + 1] = se; }
+    }
+    // the last block to finish takes phase 2 (every other block's appends are visible after the acquire)
+    __shared__ uint32_t last;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __syncthreads();
+    if (threadIdx.x == 0) last = atomicAdd(C.ctr + RF_DONE, 1u) == gridDim.x - 1;
+    __syncthreads();
+    if (!last) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    __shared__ uint64_t srt[RF_CAP];
+    __shared__ uint32_t ub[RF_CAP];
+    __shared__ uint32_t lds4[4];
+    __shared__ uint32_t nu_s;
+    const uint32_t nb = min(__hip_atomic_load(C.ctr + RF_NB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), RF_CAP);
+    const uint32_t nr = min(__hip_atomic_load(C.ctr + RF_NR, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), RF_CAP);
+    // buckets: sort, unique
+    uint32_t P = 1;
+    while (P < nb) P <<= 1;
+    for (uint32_t x = threadIdx.x; x < P; x += BLOCK) srt[x] = x < nb ? C.blist[x] : ~0ull;
+    __syncthreads();
+    block_sort_u64(srt, P);
+    uint32_t nu = 0;
+    for (uint32_t c = 0; c < nb; c += BLOCK) {
+        const uint32_t x = c + threadIdx.x;
+        const bool keep = x < nb && (x == 0 || srt[x] != srt[x - 1]);
+        uint32_t tot;
+        const uint32_t off = block_exclusive_scan(keep ? 1u : 0u, lds4, tot);
+        if (keep) ub[nu + off] = (uint32_t)srt[x];
+        nu += tot;
+    }
+    __syncthreads();
+    // their masks and good counts (bucket_good_kernel for these buckets)
+    for (uint32_t u = threadIdx.x; u < nu; u += BLOCK) {
+        const uint32_t b = ub[u];
+        const uint32_t j0 = C.dir[b].x & ~WIDE, j1 = C.dir[b + 1].x & ~WIDE;
+        uint32_t g = 0, mask = 0;
+        for (uint32_t jj = j0; jj < j1; jj++) {
+            const uint32_t gb = C.status[jj] & KAD_STATUS_GOOD;
+            g += gb;
+            if (jj - j0 < 32) mask |= gb << (jj - j0);
+        }
+        C.gcnt[b] = g;
+        C.dir[b].y = (j1 - j0 <= 32) ? mask : 0u;
+    }
+    // per line set: the union of the windows that can read a changed bucket
+    const uint32_t B = T.B;
+    const uint32_t below[3] = {2, 3, 7}, above[3] = {3, 4, 8};
+    for (int k = 0; k < 3; k++) {
+        if (!C.list[k]) continue;  // block-uniform
+        const uint32_t lb = below[k], la = above[k];
+        const uint32_t n = block_union(nu, [&](uint32_t u, uint32_t& a, uint32_t& e) {
+            const uint32_t b = ub[u];
+            a = b > lb ? b - lb : 0u;
+            e = min(B - 1, b + la);
+        }, C.list[k], lds4);
+        if (threadIdx.x == 0) C.ctr[RF_L8 + k] = n;
+    }
+    // NodeCache slots: the union of the ranges, sorted by first slot
+    if (C.list[3]) {
+        __syncthreads();
+        P = 1;
+        while (P < nr) P <<= 1;
+        for (uint32_t x = threadIdx.x; x < P; x += BLOCK)
+            srt[x] = x < nr ? ((uint64_t)C.nrange[2 * x] << 32) | C.nrange[2 * x + 1] : ~0ull;
+        __syncthreads();
+        block_sort_u64(srt, P);
+        const uint32_t n = block_union(nr, [&](uint32_t u, uint32_t& a, uint32_t& e) {
+            a = (uint32_t)(srt[u] >> 32);
+            e = (uint32_t)srt[u];
+        }, C.list[3], lds4);
+        if (threadIdx.x == 0) C.ctr[RF_LNC] = n;
+    }
+    (void)nu_s;
+    if (threadIdx.x == 0) {  // the next refresh starts from empty appends
+        C.ctr[RF_NB] = 0;
+        C.ctr[RF_NR] = 0;
+        C.ctr[RF_DONE] = 0;
     }
 }
 
@@ -5228,6 +5471,15 @@ __global__ void bucket_good_kernel(const uint8_t* status, uint2* dir, uint32_t B
     }
     cnt[b] = g;
     dir[b].y = (j1 - j0 <= 32) ? mask : 0u;
+}
+
+// *acc += sum of a[0, m) (grid-stride; *acc zeroed by the caller).
+__global__ __launch_bounds__(BLOCK) void sum_u32_kernel(const uint32_t* a, uint32_t m, uint32_t* acc) {
+    uint32_t s = 0;
+    for (uint32_t j = blockIdx.x * BLOCK + threadIdx.x; j < m; j += gridDim.x * BLOCK) s += a[j];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    if ((threadIdx.x & 63u) == 0 && s) atomicAdd(acc, s);
 }
 
 constexpr int SCAN_ITEMS = 4;
@@ -5421,7 +5673,7 @@ std::vector<uint32_t> build_radix(const Radix& r, uint32_t m, const uint8_t* ite
 // outlives its process.
 // ---------------------------------------------------------------------------------------
 constexpr uint32_t SVC_Q = 64, SVC_COUNT = 64;
-constexpr uint64_t KAD_SERVE_LIFE_MS = 1000;  // one launch's longest life
+constexpr uint64_t KAD_SERVE_LIFE_MS = 50;  // one launch's longest life (bounds head-of-line blocking)
 static_assert(SVC_Q <= BLOCK, "a request is one block of queries");
 
 struct SvcMail {             // host writes, the service reads (system-scope loads)
@@ -5464,9 +5716,18 @@ __global__ __launch_bounds__(BLOCK) void svc_kernel(DevTable T, const SvcMail* _
                 if (stop || now - heard > idle || now - t0 > life) break;
                 __builtin_amdgcn_s_sleep(1);
             }
+            if (go) {
+                // seq == seq2 shows the header words were read together, not that the rest of the line was: after an
+                // acquire at system scope (synchronising with the host's release of seq) the line is read again, and
+                // holds the request the host wrote before seq (it writes no other until this one is answered)
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+                v = lane < 16 ? __hip_atomic_load(mw + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0u;
+            }
             if (lane == 0) {
-                reply->polls = polls;
-                reply->t_seen = wall_clock64();
+                if (go) {  // the statistics of a request (an idle or stop exit leaves them alone)
+                    reply->polls = polls;
+                    reply->t_seen = wall_clock64();
+                }
                 req[0] = go;
                 req[1] = min(rdl(v, 2), SVC_Q);
                 req[2] = min(rdl(v, 3), SVC_COUNT);
@@ -5519,7 +5780,7 @@ __global__ __launch_bounds__(BLOCK) void svc_kernel(DevTable T, const SvcMail* _
                         if (lane == 0) *cp = 0;
                     } else {
                         uint32_t lo, hi, good;
-                        wave_window(T.gpre, T.B, locate_bucket(T, t), count, lo, hi, good);
+                        wave_window(T.gcnt, T.B, locate_bucket(T, t), count, lo, hi, good);
                         wave_rank_any(T, t, T.dir[lo].x & ~WIDE, T.dir[hi + 1].x & ~WIDE, good, count, row, cp, xs[w]);
                     }
                 } else if (T.n > 0) {
@@ -5614,13 +5875,17 @@ struct HostPipe {
 };
 
 // isGood(now) deadlines of a table with node times (kad_table_refresh_status; the device side is at
-// deadline_kernel). valid: the runs, cursors and status bytes agree with the device times at last_now.
+// deadline_kernel). valid: the runs, cursors and status bytes agree with the device times at last_now. The host
+// keeps a copy of both runs' keys, so it finds the passed ranges itself (no device search, no read-back) and
+// knows the next deadline at once.
 struct Deadlines {
     bool valid = false;
     int64_t last_now = INT64_MIN;
     uint64_t* km = nullptr;        // main run: keys and nodes, n entries (device)
     uint32_t* kn = nullptr;
     uint32_t nm = 0, mcap = 0;
+    std::vector<uint64_t> hkm;     // the main run's keys (host copy)
+    uint32_t cm = 0, cs = 0;       // cursors: the first unpassed entry of each run
     uint64_t* ks = nullptr;        // side run: deadlines of patched nodes (device), kept sorted on the host
     uint32_t* sn = nullptr;
     uint32_t ns = 0, scap = 0;
@@ -5629,28 +5894,25 @@ struct Deadlines {
     uint32_t* pend = nullptr;      // nodes patched since the last refresh (device), re-derived at the next one
     uint32_t np = 0, pcap = 0;
     std::vector<uint32_t> hpend;
-    uint32_t* cur = nullptr;       // 8 words: cursors and the ranges passed (dl_search_kernel)
-    uint64_t* next_dev = nullptr;  // the smallest unpassed key after the last refresh
-    uint64_t* next_host = nullptr; // its pinned copy, valid once `ev` completed
-    hipEvent_t ev = nullptr;
-    bool ev_pending = false, next_known = false;
-    uint64_t next = 0;
+    uint64_t next = 0;             // the smallest unpassed key (valid runs)
     void* tmp = nullptr;           // radix-sort scratch: keys, nodes, hipcub temp storage
     size_t tmp_bytes = 0;
     ~Deadlines() {
-        for (void* p : {(void*)km, (void*)kn, (void*)ks, (void*)sn, (void*)pend, (void*)cur, (void*)next_dev, tmp})
+        for (void* p : {(void*)km, (void*)kn, (void*)ks, (void*)sn, (void*)pend, tmp})
             if (p) (void)hipFree(p);
-        if (next_host) (void)hipHostFree(next_host);
-        if (ev) (void)hipEventDestroy(ev);
     }
     void invalidate() {
         valid = false;
         np = 0;
         ns = 0;
+        cs = 0;
         hpend.clear();
         hks.clear();
         hsn.clear();
-        next_known = false;
+    }
+    void set_next() {
+        const uint64_t a = cm < hkm.size() ? hkm[cm] : ~0ull, b = cs < hks.size() ? hks[cs] : ~0ull;
+        next = std::min(a, b);
     }
 };
 
@@ -5663,7 +5925,6 @@ struct kad_table {
     uint32_t rbits = 0, nbits = 0;
     uint8_t* status_mut = nullptr;
     uint2* dir_mut = nullptr;
-    uint32_t* gpre_mut = nullptr;
     uint32_t* wl_mut = nullptr;
     uint32_t* ws_mut = nullptr;
     uint32_t* wl16_mut = nullptr;
@@ -5686,9 +5947,7 @@ struct kad_table {
     int64_t* time_ns = nullptr;
     int64_t* reply_ns = nullptr;
     uint8_t* expired = nullptr;
-    uint32_t* scan_cnt = nullptr;   // B+1 (after every rebuild: the per-bucket good counts)
-    uint32_t* scan_part = nullptr;  // B+1
-    uint32_t* scan_sums = nullptr;  // tiles
+    uint32_t* gcnt_mut = nullptr;   // B+1: the per-bucket good counts (d.gcnt), kept current by every rebuild
     // incremental status refresh (allocated on first use, see StatusMarks)
     uint8_t* bdirty = nullptr;      // B
     uint8_t* ld8 = nullptr;         // B each, per line set present: lines to rebuild
@@ -5702,6 +5961,9 @@ struct kad_table {
     mutable std::mutex pipe_mu;     // creates `pipe` on the first host-pointer batch
     mutable HostPipe* pipe = nullptr;
     Deadlines dl;                   // isGood(now) deadlines (kad_table_refresh_status)
+    uint32_t* rf_ctr = nullptr;     // small refresh (rf_nodes_kernel): counters, appended buckets, NodeCache ranges
+    uint32_t* rf_blist = nullptr;
+    uint32_t* rf_nrange = nullptr;
     hipStream_t ss[2] = {nullptr, nullptr};  // side streams of an incremental rebuild (side_streams)
     hipEvent_t mut_ev = nullptr;    // recorded after the last asynchronous status refresh (the host batches wait on it)
     bool mut_async = false;
@@ -5712,14 +5974,17 @@ struct kad_table {
     uint64_t ls_bytes[8] = {};
     float ls_ms[8] = {};
     hipEvent_t ev_fork = nullptr, ev_join[2] = {nullptr, nullptr};
+    hipStream_t bs = nullptr;       // line-set builds (ensure_lines): a non-blocking stream of the table's own
     ~kad_table() {
+        if (bs) { (void)hipStreamSynchronize(bs); (void)hipStreamDestroy(bs); }
         for (hipStream_t x : ss)
             if (x) { (void)hipStreamSynchronize(x); (void)hipStreamDestroy(x); }
         for (hipEvent_t e : {ev_fork, ev_join[0], ev_join[1], mut_ev})
             if (e) (void)hipEventDestroy(e);
         delete pipe;
         for (void* p : owned) (void)hipFree(p);
-        for (void* p : {(void*)bdirty, (void*)ld8, (void*)ld16, (void*)ld32, (void*)ndirty, (void*)dlist, (void*)dctr, stage})
+        for (void* p : {(void*)bdirty, (void*)ld8, (void*)ld16, (void*)ld32, (void*)ndirty, (void*)dlist, (void*)dctr, stage,
+                        (void*)rf_ctr, (void*)rf_blist, (void*)rf_nrange})
             if (p) (void)hipFree(p);
     }
 };
@@ -5746,6 +6011,16 @@ int side_streams(kad_table* t) {
     for (hipEvent_t& e : t->ev_join)
         if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     return KAD_OK;
+}
+
+// The table's build stream (created on first use; the null stream if that fails). Line-set builds run there and
+// wait for it alone, not for the whole device (a resident service or another thread's graph capture).
+hipStream_t build_stream(kad_table* t) {
+    if (!t->bs && hipStreamCreateWithFlags(&t->bs, hipStreamNonBlocking) != hipSuccess) {
+        (void)hipGetLastError();
+        t->bs = nullptr;
+    }
+    return t->bs;
 }
 
 int rebuild_good_prefix_(kad_table* t, hipStream_t s, bool full);
@@ -5780,19 +6055,14 @@ int rebuild_good_prefix_(kad_table* t, hipStream_t s, bool full) {
     }
     if (B == 0) return KAD_OK;
     const uint32_t m = B + 1;
-    const uint32_t tiles = (m + SCAN_TILE - 1) / SCAN_TILE;
     if (full)
         hipLaunchKernelGGL(bucket_good_kernel, dim3(grid_for(m)), dim3(BLOCK), 0, s, t->d.status, t->dir_mut, B,
-                           t->scan_cnt);
+                           t->gcnt_mut);
     else
         hipLaunchKernelGGL(bucket_good_dirty_kernel, dim3(grid_for(B)), dim3(BLOCK), 0, s, t->d.status, t->dir_mut, B,
-                           t->scan_cnt, t->bdirty, (t->wl_mut || t->gl_mut) ? t->ld8 : nullptr,
+                           t->gcnt_mut, t->bdirty, (t->wl_mut || t->gl_mut) ? t->ld8 : nullptr,
                            (t->wl16_mut || t->gl16_mut) ? t->ld16 : nullptr, (t->wl32_mut || t->gl32_mut) ? t->ld32 : nullptr,
                            any);
-    hipLaunchKernelGGL(scan_tiles_kernel, dim3(tiles), dim3(BLOCK), 0, s, t->scan_cnt, m, t->scan_part, t->scan_sums, any);
-    hipLaunchKernelGGL(scan_sums_kernel, dim3(1), dim3(BLOCK), 0, s, t->scan_sums, tiles, any);
-    hipLaunchKernelGGL(scan_apply_kernel, dim3(grid_for(m)), dim3(BLOCK), 0, s, t->scan_part, t->scan_sums, m, t->gpre_mut,
-                       any);
     // the lines of every bucket (full) or only the compacted dirty ones
     auto sel_for = [&](uint8_t* flags, uint32_t k, hipStream_t st) -> LineSel {
         if (full) return LineSel{};
@@ -5815,23 +6085,24 @@ int rebuild_good_prefix_(kad_table* t, hipStream_t s, bool full) {
     }
     if (t->wl16_mut)
         hipLaunchKernelGGL(wl16_build_kernel, lgrid(B), dim3(BLOCK), 0, sB, t->d.key, t->d.status, t->d.dir,
-                           t->d.gpre, B, 64 - t->d.rshift, t->d.rbase >> t->d.rshift, t->wl16_mut, sel_for(t->ld16, 1, sB));
+                           t->d.gcnt, B, 64 - t->d.rshift, t->d.rbase >> t->d.rshift, t->wl16_mut, sel_for(t->ld16, 1, sB));
     if (t->wl32_mut)
         hipLaunchKernelGGL(wl32_build_kernel, lgrid(B), dim3(BLOCK), 0, sC, t->d.key, t->d.status, t->d.dir,
-                           t->d.gpre, B, 64 - t->d.rshift, t->d.rbase >> t->d.rshift, t->wl32_mut, sel_for(t->ld32, 2, sC));
+                           t->d.gcnt, B, 64 - t->d.rshift, t->d.rbase >> t->d.rshift, t->wl32_mut, sel_for(t->ld32, 2, sC));
     if (t->gl32_mut)
         hipLaunchKernelGGL(gl32_build_kernel, lgrid(B), dim3(BLOCK), 0, sC, t->d.key, t->d.status, t->d.dir,
-                           t->d.gpre, t->d.fkey, t->d.ftail, B, t->gl32_mut, sel_for(t->ld32, 2, sC));
+                           t->d.gcnt, t->d.fkey, t->d.ftail, B, t->gl32_mut, sel_for(t->ld32, 2, sC));
     LineSel s8{};
     if (t->wl_mut || t->gl_mut) s8 = sel_for(t->ld8, 0, s);
-    if (t->wl_mut)
-        hipLaunchKernelGGL(wl_build_kernel, lgrid(B), dim3(BLOCK), 0, s, t->d.key, t->d.status, t->d.dir,
-                           t->d.gpre, B, 64 - t->d.rshift, t->d.rbase >> t->d.rshift, t->wl_mut, s8);
-    if (t->ws_mut)  // transcoded from the 128-byte lines just rebuilt, the same selection
-        hipLaunchKernelGGL(ws_build_kernel, lgrid(B), dim3(BLOCK), 0, s, t->wl_mut, B, t->ws_mut, s8);
+    if (t->wl_mut && t->ws_mut)  // the short lines transcoded from the 128-byte lines in the same thread
+        hipLaunchKernelGGL(wl_build_kernel<true>, lgrid(B), dim3(BLOCK), 0, s, t->d.key, t->d.status, t->d.dir,
+                           t->d.gcnt, B, 64 - t->d.rshift, t->d.rbase >> t->d.rshift, t->wl_mut, t->ws_mut, s8);
+    else if (t->wl_mut)
+        hipLaunchKernelGGL(wl_build_kernel<false>, lgrid(B), dim3(BLOCK), 0, s, t->d.key, t->d.status, t->d.dir,
+                           t->d.gcnt, B, 64 - t->d.rshift, t->d.rbase >> t->d.rshift, t->wl_mut, nullptr, s8);
     if (t->gl_mut)
         hipLaunchKernelGGL(gl_build_kernel, lgrid(B), dim3(BLOCK), 0, s, t->d.key, t->d.status, t->d.dir,
-                           t->d.gpre, t->d.fkey, t->d.ftail, B, t->gl_mut, s8);
+                           t->d.gcnt, t->d.fkey, t->d.ftail, B, t->gl_mut, s8);
     if (t->sl_mut) {  // slot lines: transcoded from the general lines just rebuilt (all, or the flagged buckets')
         if (!full) hipLaunchKernelGGL(mark_sel_kernel, lgrid(B), dim3(BLOCK), 0, s, s8, B, t->gdirty, (uint8_t)1);
         hipLaunchKernelGGL(sl_build_kernel, lgrid(t->d.slslots), dim3(BLOCK), 0, s, t->gl_mut, t->slb, t->d.slslots,
@@ -5842,7 +6113,7 @@ int rebuild_good_prefix_(kad_table* t, hipStream_t s, bool full) {
     if (t->gl16_mut) {
         const LineSel s16 = sel_for(t->ld16, 1, s);
         hipLaunchKernelGGL(gl16_build_kernel, lgrid(B), dim3(BLOCK), 0, s, t->d.key, t->d.status, t->d.dir,
-                           t->d.gpre, t->d.fkey, t->d.ftail, B, t->gl16_mut, s16);
+                           t->d.gcnt, t->d.fkey, t->d.ftail, B, t->gl16_mut, s16);
         if (t->sl16_mut) {  // their slot-indexed copies: all, or the flagged buckets'
             if (!full) hipLaunchKernelGGL(mark_sel_kernel, lgrid(B), dim3(BLOCK), 0, s, s16, B, t->gdirty, (uint8_t)1);
             hipLaunchKernelGGL(sl16_build_kernel, lgrid(8ull * t->d.slslots), dim3(BLOCK), 0, s, t->gl16_mut, t->slb,
@@ -5902,10 +6173,10 @@ int setup_slot_lines(kad_table* t) {
         drop();
         return KAD_OK;
     }
-    hipLaunchKernelGGL(sl_index_kernel, dim3(grid_for(slslots)), dim3(BLOCK), 0, 0, d.rrdx, d.rslots, k, slslots, slb);
-    hipLaunchKernelGGL(sl_build_kernel, dim3(grid_for(slslots)), dim3(BLOCK), 0, 0, t->gl_mut, slb, slslots, nullptr,
+    hipLaunchKernelGGL(sl_index_kernel, dim3(grid_for(slslots)), dim3(BLOCK), 0, build_stream(t), d.rrdx, d.rslots, k, slslots, slb);
+    hipLaunchKernelGGL(sl_build_kernel, dim3(grid_for(slslots)), dim3(BLOCK), 0, build_stream(t), t->gl_mut, slb, slslots, nullptr,
                        d.rrdx, d.rslots, k, d.fkey, d.ftail, lines);
-    if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+    if (hipGetLastError() != hipSuccess || hipStreamSynchronize(build_stream(t)) != hipSuccess) {
         drop();
         return set_err(KAD_ERR_HIP, "slot-line build failed");
     }
@@ -5913,7 +6184,7 @@ int setup_slot_lines(kad_table* t) {
         uint32_t* dc = nullptr;
         uint32_t hc[2] = {0, 0};
         if (hipMalloc(&dc, 8) == hipSuccess && hipMemset(dc, 0, 8) == hipSuccess) {
-            hipLaunchKernelGGL(sl_count_kernel, dim3(grid_for(slslots)), dim3(BLOCK), 0, 0, lines, slslots, dc);
+            hipLaunchKernelGGL(sl_count_kernel, dim3(grid_for(slslots)), dim3(BLOCK), 0, build_stream(t), lines, slslots, dc);
             (void)hipMemcpy(hc, dc, 8, hipMemcpyDeviceToHost);
         }
         if (dc) (void)hipFree(dc);
@@ -5938,9 +6209,9 @@ int build_sl16(kad_table* t) {
     uint64_t b16 = 0;
     uint32_t* l16 = nullptr;
     if (dev_upload(&l16, nullptr, (size_t)GL16_STRIDE * d.slslots, f16, b16) == KAD_OK) {
-        hipLaunchKernelGGL(sl16_build_kernel, dim3(grid_for(8ull * d.slslots)), dim3(BLOCK), 0, 0, t->gl16_mut, t->slb,
+        hipLaunchKernelGGL(sl16_build_kernel, dim3(grid_for(8ull * d.slslots)), dim3(BLOCK), 0, build_stream(t), t->gl16_mut, t->slb,
                            d.slslots, nullptr, d.rrdx, d.rslots, d.slshift - d.rshift, d.fkey, d.ftail, l16);
-        if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+        if (hipGetLastError() != hipSuccess || hipStreamSynchronize(build_stream(t)) != hipSuccess) {
             for (void* p : f16) (void)hipFree(p);
             return set_err(KAD_ERR_HIP, "slot-line (16) build failed");
         }
@@ -5957,15 +6228,17 @@ int build_sl16(kad_table* t) {
 // current status, and kept only when at most 1/16 of them are deferred (otherwise the lane kernel is the faster
 // path); then the slot lines. Synchronous. A failure leaves the table without general lines (still correct).
 // The count 9..32 general lines are built on first use (build_gl32, build_gl16).
-int count_deferred(const uint32_t* lines, uint32_t stride, uint32_t hdr_word, uint32_t B, uint32_t& nd) {
+int count_deferred(const uint32_t* lines, uint32_t stride, uint32_t hdr_word, uint32_t B, uint32_t& nd,
+                   hipStream_t s) {
     uint32_t* cnt = nullptr;
     HIP_TRY(hipMalloc(&cnt, 4));
-    hipError_t e = hipMemset(cnt, 0, 4);
+    hipError_t e = hipMemsetAsync(cnt, 0, 4, s);
     if (e == hipSuccess) {
-        hipLaunchKernelGGL(count_deferred_kernel, dim3(grid_for(B)), dim3(BLOCK), 0, 0, lines, stride, hdr_word, B, cnt);
+        hipLaunchKernelGGL(count_deferred_kernel, dim3(grid_for(B)), dim3(BLOCK), 0, s, lines, stride, hdr_word, B, cnt);
         e = hipGetLastError();
     }
-    if (e == hipSuccess) e = hipMemcpy(&nd, cnt, 4, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpyAsync(&nd, cnt, 4, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
     (void)hipFree(cnt);
     if (e != hipSuccess) return set_err(KAD_ERR_HIP, "deferred-line count failed: %s", hipGetErrorString(e));
     return KAD_OK;
@@ -5979,11 +6252,11 @@ int setup_general_lines(kad_table* t) {
     std::vector<void*> fresh;
     uint64_t fb = 0;
     if (dev_upload(&lp, nullptr, (size_t)GL_STRIDE * B, fresh, fb)) return KAD_OK;
-    hipLaunchKernelGGL(gl_build_kernel, dim3(grid_for(B)), dim3(BLOCK), 0, 0, d.key, d.status, d.dir, d.gpre, d.fkey,
+    hipLaunchKernelGGL(gl_build_kernel, dim3(grid_for(B)), dim3(BLOCK), 0, build_stream(t), d.key, d.status, d.dir, d.gcnt, d.fkey,
                        d.ftail, B, lp, LineSel{});
     uint32_t nd = B;
     int rc;
-    if (hipGetLastError() != hipSuccess || (rc = count_deferred(lp, GL_STRIDE, 1u, B, nd))) {
+    if (hipGetLastError() != hipSuccess || (rc = count_deferred(lp, GL_STRIDE, 1u, B, nd, build_stream(t)))) {
         (void)hipFree(lp);
         return set_err(KAD_ERR_HIP, "general window-line build failed");
     }
@@ -6007,10 +6280,10 @@ int build_gl32(kad_table* t) {
     uint64_t fb = 0;
     int rc;
     if ((rc = dev_upload(&lp, nullptr, (size_t)GL32_STRIDE * B, fresh, fb))) return rc;
-    hipLaunchKernelGGL(gl32_build_kernel, dim3(grid_for(B)), dim3(BLOCK), 0, 0, d.key, d.status, d.dir, d.gpre, d.fkey,
+    hipLaunchKernelGGL(gl32_build_kernel, dim3(grid_for(B)), dim3(BLOCK), 0, build_stream(t), d.key, d.status, d.dir, d.gcnt, d.fkey,
                        d.ftail, B, lp, LineSel{});
     uint32_t nd = B;
-    if (hipGetLastError() != hipSuccess || (rc = count_deferred(lp, GL32_STRIDE, 3u, B, nd))) {
+    if (hipGetLastError() != hipSuccess || (rc = count_deferred(lp, GL32_STRIDE, 3u, B, nd, build_stream(t)))) {
         (void)hipFree(lp);
         return set_err(KAD_ERR_HIP, "general window-line (32) build failed");
     }
@@ -6032,10 +6305,10 @@ int build_gl16(kad_table* t) {
     uint64_t fb = 0;
     int rc;
     if ((rc = dev_upload(&lp, nullptr, (size_t)GL16_STRIDE * B, fresh, fb))) return rc;
-    hipLaunchKernelGGL(gl16_build_kernel, dim3(grid_for(B)), dim3(BLOCK), 0, 0, d.key, d.status, d.dir, d.gpre, d.fkey,
+    hipLaunchKernelGGL(gl16_build_kernel, dim3(grid_for(B)), dim3(BLOCK), 0, build_stream(t), d.key, d.status, d.dir, d.gcnt, d.fkey,
                        d.ftail, B, lp, LineSel{});
     uint32_t nd = B;
-    if (hipGetLastError() != hipSuccess || (rc = count_deferred(lp, GL16_STRIDE, 1u, B, nd))) {
+    if (hipGetLastError() != hipSuccess || (rc = count_deferred(lp, GL16_STRIDE, 1u, B, nd, build_stream(t)))) {
         (void)hipFree(lp);
         return set_err(KAD_ERR_HIP, "general window-line (16) build failed");
     }
@@ -6117,8 +6390,130 @@ int mark_async(kad_table* t, hipStream_t s) {
     return KAD_OK;
 }
 
-// ---- isGood(now) deadlines, host side (see deadline_kernel) ----
+// ---- small refresh (rf_nodes_kernel) ----
 NodeTimes times_of(const kad_table* t) { return NodeTimes{t->time_ns, t->reply_ns, t->expired}; }
+
+int rf_ready(kad_table* t) {
+    if (t->rf_ctr) return KAD_OK;
+    void *c = nullptr, *bl = nullptr, *nr = nullptr;
+    hipError_t e = hipMalloc(&c, RF_CTRS * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMalloc(&bl, RF_CAP * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMalloc(&nr, 2 * RF_CAP * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMemset(c, 0, RF_CTRS * sizeof(uint32_t));
+    if (e != hipSuccess) {
+        for (void* p : {c, bl, nr}) if (p) (void)hipFree(p);
+        return set_err(KAD_ERR_NOMEM, "small refresh buffers: %s", hipGetErrorString(e));
+    }
+    t->rf_ctr = static_cast<uint32_t*>(c);
+    t->rf_blist = static_cast<uint32_t*>(bl);
+    t->rf_nrange = static_cast<uint32_t*>(nr);
+    return KAD_OK;
+}
+
+// Re-derive the status of at most RF_CAP listed nodes (main-run, side-run and patched nodes; vals: the patched
+// nodes' new status bytes instead of their times) and rebuild only what they change: rf_nodes_kernel, then the
+// line builders over its lists. ensure_marks must have run (the lists live in dlist). Async on s.
+int small_refresh(kad_table* t, hipStream_t s, const uint32_t* mnode, uint32_t mc, const uint32_t* snode, uint32_t sc,
+                  const uint32_t* pend, uint32_t np, const uint8_t* vals, int64_t now) {
+    const uint32_t total = mc + sc + np;
+    if (total == 0) return KAD_OK;
+    int rc;
+    if ((rc = rf_ready(t))) return rc;
+    const DevTable& d = t->d;
+    const uint32_t B = d.B;
+    const bool has8 = t->wl_mut || t->gl_mut, has16 = t->wl16_mut || t->gl16_mut, has32 = t->wl32_mut || t->gl32_mut;
+    RfCtx C{};
+    C.N = times_of(t);
+    C.mnode = mnode; C.mc = mc;
+    C.snode = snode; C.sc = sc;
+    C.pend = pend; C.np = np;
+    C.vals = vals;
+    C.now = now;
+    C.T = d;
+    C.status = t->status_mut;
+    C.dir = t->dir_mut;
+    C.gcnt = t->gcnt_mut;
+    C.blist = t->rf_blist;
+    C.nrange = t->rf_nrange;
+    C.ctr = t->rf_ctr;
+    C.list[0] = B && has8 ? t->dlist : nullptr;
+    C.list[1] = B && has16 ? t->dlist + (size_t)B : nullptr;
+    C.list[2] = B && has32 ? t->dlist + 2ull * B : nullptr;
+    C.list[3] = t->ncl_mut ? t->dlist + 3ull * B : nullptr;
+    C.nback = t->ncl32_mut ? NC32_SLOTS - NC32_LEFT : NCL_SLOTS - NCL_LEFT;
+    C.nfwd = t->ncl32_mut ? NC32_LEFT : NCL_LEFT;
+    hipLaunchKernelGGL(rf_nodes_kernel, dim3(std::min<uint32_t>((total + BLOCK - 1) / BLOCK, 64u)), dim3(BLOCK), 0, s, C);
+    HIP_TRY(hipGetLastError());
+    // the builders over the lists; grids from the host's bound on each list
+    auto grid = [&](uint64_t items) { return dim3((uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((items + BLOCK - 1) / BLOCK, 2048))); };
+    const uint64_t u8 = std::min<uint64_t>(B, 6ull * total), u16 = std::min<uint64_t>(B, 8ull * total),
+                   u32 = std::min<uint64_t>(B, 16ull * total), unc = d.nslots;
+    const LineSel s8{C.list[0], t->rf_ctr + RF_L8}, s16{C.list[1], t->rf_ctr + RF_L16}, s32{C.list[2], t->rf_ctr + RF_L32};
+    if (t->ncl_mut) {
+        const LineSel snc{C.list[3], t->rf_ctr + RF_LNC};
+        hipLaunchKernelGGL(ncl_build_kernel, grid(unc), dim3(BLOCK), 0, s, d.key, d.status, d.nrdx, d.nslots, d.n,
+                           64 - d.nshift, t->ncl_mut, snc);
+        if (t->ncl32_mut)
+            hipLaunchKernelGGL(ncl32_build_kernel, grid(8 * unc), dim3(BLOCK), 0, s, d.key, d.status, d.nrdx, d.nslots,
+                               d.n, 64 - d.nshift, t->ncl32_mut, snc);
+    }
+    if (B == 0) return KAD_OK;
+    // the count 9..16 and 17..32 sets on the side streams (independent of the count <= 8 chain), joined back
+    hipStream_t sB = s, sC = s;
+    const bool fork = (has16 || has32) && side_streams(t) == KAD_OK;
+    if (fork) {
+        HIP_TRY(hipEventRecord(t->ev_fork, s));
+        sB = t->ss[0];
+        sC = t->ss[1];
+        HIP_TRY(hipStreamWaitEvent(sB, t->ev_fork, 0));
+        HIP_TRY(hipStreamWaitEvent(sC, t->ev_fork, 0));
+    }
+    if (t->wl16_mut)
+        hipLaunchKernelGGL(wl16_build_kernel, grid(u16), dim3(BLOCK), 0, sB, d.key, d.status, d.dir, d.gcnt, B,
+                           64 - d.rshift, d.rbase >> d.rshift, t->wl16_mut, s16);
+    if (t->wl32_mut)
+        hipLaunchKernelGGL(wl32_build_kernel, grid(u32), dim3(BLOCK), 0, sC, d.key, d.status, d.dir, d.gcnt, B,
+                           64 - d.rshift, d.rbase >> d.rshift, t->wl32_mut, s32);
+    if (t->gl32_mut)
+        hipLaunchKernelGGL(gl32_build_kernel, grid(u32), dim3(BLOCK), 0, sC, d.key, d.status, d.dir, d.gcnt, d.fkey,
+                           d.ftail, B, t->gl32_mut, s32);
+    if (t->wl_mut && t->ws_mut)
+        hipLaunchKernelGGL(wl_build_kernel<true>, grid(u8), dim3(BLOCK), 0, s, d.key, d.status, d.dir, d.gcnt, B,
+                           64 - d.rshift, d.rbase >> d.rshift, t->wl_mut, t->ws_mut, s8);
+    else if (t->wl_mut)
+        hipLaunchKernelGGL(wl_build_kernel<false>, grid(u8), dim3(BLOCK), 0, s, d.key, d.status, d.dir, d.gcnt, B,
+                           64 - d.rshift, d.rbase >> d.rshift, t->wl_mut, nullptr, s8);
+    if (t->gl_mut) {
+        hipLaunchKernelGGL(gl_build_kernel, grid(u8), dim3(BLOCK), 0, s, d.key, d.status, d.dir, d.gcnt, d.fkey, d.ftail,
+                           B, t->gl_mut, s8);
+        if (t->sl_mut) {  // slot lines: transcoded from the general lines just rebuilt (the flagged buckets')
+            hipLaunchKernelGGL(mark_sel_kernel, grid(u8), dim3(BLOCK), 0, s, s8, B, t->gdirty, (uint8_t)1);
+            hipLaunchKernelGGL(sl_build_kernel, grid(d.slslots), dim3(BLOCK), 0, s, t->gl_mut, t->slb, d.slslots,
+                               t->gdirty, d.rrdx, d.rslots, d.slshift - d.rshift, d.fkey, d.ftail, t->sl_mut);
+            hipLaunchKernelGGL(mark_sel_kernel, grid(u8), dim3(BLOCK), 0, s, s8, B, t->gdirty, (uint8_t)0);
+        }
+    }
+    if (t->gl16_mut) {  // on s: its slot copies share the gdirty flags with the count <= 8 slot lines
+        hipLaunchKernelGGL(gl16_build_kernel, grid(u16), dim3(BLOCK), 0, s, d.key, d.status, d.dir, d.gcnt, d.fkey,
+                           d.ftail, B, t->gl16_mut, s16);
+        if (t->sl16_mut) {
+            hipLaunchKernelGGL(mark_sel_kernel, grid(u16), dim3(BLOCK), 0, s, s16, B, t->gdirty, (uint8_t)1);
+            hipLaunchKernelGGL(sl16_build_kernel, grid(8ull * d.slslots), dim3(BLOCK), 0, s, t->gl16_mut, t->slb,
+                               d.slslots, t->gdirty, d.rrdx, d.rslots, d.slshift - d.rshift, d.fkey, d.ftail, t->sl16_mut);
+            hipLaunchKernelGGL(mark_sel_kernel, grid(u16), dim3(BLOCK), 0, s, s16, B, t->gdirty, (uint8_t)0);
+        }
+    }
+    if (fork) {
+        HIP_TRY(hipEventRecord(t->ev_join[0], sB));
+        HIP_TRY(hipEventRecord(t->ev_join[1], sC));
+        HIP_TRY(hipStreamWaitEvent(s, t->ev_join[0], 0));
+        HIP_TRY(hipStreamWaitEvent(s, t->ev_join[1], 0));
+    }
+    HIP_TRY(hipGetLastError());
+    return KAD_OK;
+}
+
+// ---- isGood(now) deadlines, host side (see deadline_kernel) ----
 
 int dl_alloc(void** p, size_t bytes) {
     hipError_t e = hipMalloc(p, std::max<size_t>(bytes, 16));
@@ -6126,27 +6521,26 @@ int dl_alloc(void** p, size_t bytes) {
     return KAD_OK;
 }
 
-// The next deadline to the host: an async copy into pinned memory and an event (read by the next refresh).
-int dl_publish(kad_table* t, hipStream_t s) {
-    Deadlines& D = t->dl;
-    HIP_TRY(hipMemcpyAsync(D.next_host, D.next_dev, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipEventRecord(D.ev, s));
-    D.ev_pending = true;
-    D.next_known = false;
-    return KAD_OK;
+// lower_bound of x in k[from, n) by galloping from the cursor (a refresh passes few deadlines).
+uint32_t gallop_lower_bound(const std::vector<uint64_t>& k, uint32_t from, uint64_t x) {
+    const uint32_t n = (uint32_t)k.size();
+    if (from >= n || k[from] >= x) return from;
+    uint32_t lo = from, step = 1;  // k[lo] < x
+    while (lo + step < n && k[lo + step] < x) {
+        lo += step;
+        step <<= 1;
+    }
+    const uint32_t hi = std::min<uint64_t>(n, (uint64_t)lo + step);
+    return (uint32_t)(std::lower_bound(k.begin() + lo + 1, k.begin() + hi, x) - k.begin());
 }
 
-// Main run of every node's deadline from the device times (radix sort by key), the side run emptied, the
-// cursors at the first deadline >= nowk (everything before it counts as passed). Async on s.
+// Main run of every node's deadline from the device times (radix sort by key), its keys copied to the host
+// (synchronous on s), the side run emptied, the cursors at the first deadline >= nowk (everything before it
+// counts as passed).
 int dl_build_main(kad_table* t, hipStream_t s, uint64_t nowk) {
     Deadlines& D = t->dl;
     const uint32_t n = t->d.n;
     int rc;
-    if (!D.cur) {
-        if ((rc = dl_alloc((void**)&D.cur, 8 * sizeof(uint32_t))) || (rc = dl_alloc((void**)&D.next_dev, 8))) return rc;
-        HIP_TRY(hipHostMalloc((void**)&D.next_host, sizeof(uint64_t), hipHostMallocDefault));
-        HIP_TRY(hipEventCreateWithFlags(&D.ev, hipEventDisableTiming));
-    }
     if (D.mcap < n) {
         if (D.km) { (void)hipFree(D.km); D.km = nullptr; }
         if (D.kn) { (void)hipFree(D.kn); D.kn = nullptr; }
@@ -6161,6 +6555,11 @@ int dl_build_main(kad_table* t, hipStream_t s, uint64_t nowk) {
         D.tmp_bytes = kb + nb + cub;
         D.mcap = n;
     }
+    try {
+        D.hkm.resize(n);
+    } catch (...) {
+        return set_err(KAD_ERR_NOMEM, "deadline keys: out of host memory");
+    }
     const size_t kb = (8ull * n + 255) & ~255ull, nb = (4ull * n + 255) & ~255ull;
     uint64_t* tk = static_cast<uint64_t*>(D.tmp);
     uint32_t* tn = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(D.tmp) + kb);
@@ -6169,14 +6568,16 @@ int dl_build_main(kad_table* t, hipStream_t s, uint64_t nowk) {
     hipLaunchKernelGGL(deadline_kernel, dim3(grid_for(n)), dim3(BLOCK), 0, s, times_of(t), n, tk, tn);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipcub::DeviceRadixSort::SortPairs(ct, cb, tk, D.km, tn, D.kn, (int)n, 0, 64, s));
+    HIP_TRY(hipMemcpyAsync(D.hkm.data(), D.km, 8ull * n, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
     D.nm = n;
     D.ns = 0;
     D.hks.clear();
     D.hsn.clear();
-    HIP_TRY(hipMemsetAsync(D.cur, 0, 8 * sizeof(uint32_t), s));
-    hipLaunchKernelGGL(dl_search_kernel, dim3(1), dim3(64), 0, s, D.km, D.nm, D.ks, 0u, nowk, D.cur, D.next_dev);
-    HIP_TRY(hipGetLastError());
-    return dl_publish(t, s);
+    D.cm = (uint32_t)(std::lower_bound(D.hkm.begin(), D.hkm.end(), nowk) - D.hkm.begin());
+    D.cs = 0;
+    D.set_next();
+    return KAD_OK;
 }
 
 // patch_times on the deadline runs (synchronous; the device times are already updated): the patched nodes
@@ -6248,8 +6649,8 @@ int dl_patch(kad_table* t, uint32_t m, const uint32_t* nodes, const int64_t* tim
         HIP_TRY(hipMemcpy(D.sn, D.hsn.data(), 4ull * D.hsn.size(), hipMemcpyHostToDevice));
     }
     D.ns = (uint32_t)D.hks.size();
-    const uint32_t zero = 0;
-    HIP_TRY(hipMemcpy(D.cur + 1, &zero, sizeof zero, hipMemcpyHostToDevice));  // every side entry is unpassed
+    D.cs = 0;  // every side entry is unpassed
+    D.set_next();
     return KAD_OK;
 }
 
@@ -6264,9 +6665,9 @@ int build_wl16(kad_table* t) {
     uint64_t fb = 0;
     int rc;
     if ((rc = dev_upload(&lp, nullptr, (size_t)WL16_STRIDE * d.B, fresh, fb))) return rc;
-    hipLaunchKernelGGL(wl16_build_kernel, dim3(grid_for(d.B)), dim3(BLOCK), 0, 0, d.key, d.status, d.dir, d.gpre, d.B,
+    hipLaunchKernelGGL(wl16_build_kernel, dim3(grid_for(d.B)), dim3(BLOCK), 0, build_stream(t), d.key, d.status, d.dir, d.gcnt, d.B,
                        64 - d.rshift, d.rbase >> d.rshift, lp, LineSel{});
-    if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+    if (hipGetLastError() != hipSuccess || hipStreamSynchronize(build_stream(t)) != hipSuccess) {
         (void)hipFree(lp);
         return set_err(KAD_ERR_HIP, "window-line (16) build failed");
     }
@@ -6283,9 +6684,9 @@ int build_wl32(kad_table* t) {
     uint64_t fb = 0;
     int rc;
     if ((rc = dev_upload(&lp, nullptr, (size_t)WL32_STRIDE * d.B, fresh, fb))) return rc;
-    hipLaunchKernelGGL(wl32_build_kernel, dim3(grid_for(d.B)), dim3(BLOCK), 0, 0, d.key, d.status, d.dir, d.gpre, d.B,
+    hipLaunchKernelGGL(wl32_build_kernel, dim3(grid_for(d.B)), dim3(BLOCK), 0, build_stream(t), d.key, d.status, d.dir, d.gcnt, d.B,
                        64 - d.rshift, d.rbase >> d.rshift, lp, LineSel{});
-    if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+    if (hipGetLastError() != hipSuccess || hipStreamSynchronize(build_stream(t)) != hipSuccess) {
         (void)hipFree(lp);
         return set_err(KAD_ERR_HIP, "window-line (32) build failed");
     }
@@ -6302,9 +6703,9 @@ int build_ncl(kad_table* t) {
     uint64_t fb = 0;
     int rc;
     if ((rc = dev_upload(&lp, nullptr, (size_t)NCL_STRIDE * d.nslots, fresh, fb))) return rc;
-    hipLaunchKernelGGL(ncl_build_kernel, dim3(grid_for(d.nslots)), dim3(BLOCK), 0, 0, d.key, d.status, d.nrdx, d.nslots,
+    hipLaunchKernelGGL(ncl_build_kernel, dim3(grid_for(d.nslots)), dim3(BLOCK), 0, build_stream(t), d.key, d.status, d.nrdx, d.nslots,
                        d.n, 64 - d.nshift, lp, LineSel{});
-    if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+    if (hipGetLastError() != hipSuccess || hipStreamSynchronize(build_stream(t)) != hipSuccess) {
         (void)hipFree(lp);
         return set_err(KAD_ERR_HIP, "NodeCache line build failed");
     }
@@ -6321,9 +6722,9 @@ int build_ncl32(kad_table* t) {
     uint64_t fb = 0;
     int rc;
     if ((rc = dev_upload(&lp, nullptr, (size_t)NC32_STRIDE * d.nslots, fresh, fb))) return rc;
-    hipLaunchKernelGGL(ncl32_build_kernel, dim3(grid_for(8ull * d.nslots)), dim3(BLOCK), 0, 0, d.key, d.status, d.nrdx,
+    hipLaunchKernelGGL(ncl32_build_kernel, dim3(grid_for(8ull * d.nslots)), dim3(BLOCK), 0, build_stream(t), d.key, d.status, d.nrdx,
                        d.nslots, d.n, 64 - d.nshift, lp, LineSel{});
-    if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+    if (hipGetLastError() != hipSuccess || hipStreamSynchronize(build_stream(t)) != hipSuccess) {
         (void)hipFree(lp);
         return set_err(KAD_ERR_HIP, "NodeCache line (32) build failed");
     }
@@ -6353,7 +6754,11 @@ int ensure_lines(const kad_table* ct, uint32_t need, hipStream_t s) {
     need &= ~t->ls_done.load(std::memory_order_relaxed);
     if (!need) return KAD_OK;
     DeviceGuard g(t->device);
-    HIP_TRY(hipDeviceSynchronize());  // built from the current status, whatever stream changed it last
+    // built from the current status: after the last asynchronous refresh (every other change is synchronous);
+    // the table's own streams only, never the whole device
+    if (t->mut_async) HIP_TRY(hipEventSynchronize(t->mut_ev));
+    for (hipStream_t x : t->ss)
+        if (x) HIP_TRY(hipStreamSynchronize(x));
     const uint32_t bits[4] = {LS_WL32, LS_WL16, LS_NCL, LS_NCL32};
     int (*uni[4])(kad_table*) = {build_wl32, build_wl16, build_ncl, build_ncl32};
     int (*gen[4])(kad_table*) = {build_gl32, build_gl16, build_ncl, build_ncl32};
@@ -6619,18 +7024,16 @@ int kad_table_create(kad_table** out, int device, uint32_t n_nodes, const uint8_
     // bucket directory
     if (n_buckets) {
         std::vector<uint2> dir(n_buckets + 1);
-        std::vector<uint32_t> gpre(n_buckets + 1), dmask(any_dup ? n_buckets : 0);
-        uint32_t g = 0;
+        std::vector<uint32_t> cnt(n_buckets + 1, 0), dmask(any_dup ? n_buckets : 0);
         for (uint32_t b = 0; b <= n_buckets; b++) {
             dir[b].x = bucket_offset[b];
             dir[b].y = 0;
-            gpre[b] = g;
             if (b < n_buckets) {
                 const uint32_t j0 = bucket_offset[b], j1 = bucket_offset[b + 1];
                 if (j1 - j0 > 32) dir[b].x |= WIDE;
                 for (uint32_t j = j0; j < j1; j++) {
                     const uint32_t gb = status[j] & KAD_STATUS_GOOD;
-                    g += gb;
+                    cnt[b] += gb;
                     if (j1 - j0 <= 32) {
                         dir[b].y |= gb << (j - j0);
                         if (any_dup) dmask[b] |= (uint32_t)dup[j] << (j - j0);
@@ -6639,9 +7042,6 @@ int kad_table_create(kad_table** out, int device, uint32_t n_nodes, const uint8_
                 // a wide bucket's dup nodes are handled by the slow path (wide -> deferred)
             }
         }
-        // per-bucket good counts: the scan input, kept current by every rebuild (incremental refresh)
-        std::vector<uint32_t> cnt(n_buckets + 1, 0);
-        for (uint32_t b = 0; b < n_buckets; b++) cnt[b] = gpre[b + 1] - gpre[b];
         std::vector<uint64_t> fkey(n_buckets);
         std::vector<uint32_t> ftail(3ull * n_buckets);
         for (uint32_t b = 0; b < n_buckets; b++) {
@@ -6676,20 +7076,17 @@ int kad_table_create(kad_table** out, int device, uint32_t n_nodes, const uint8_
         for (uint32_t sl = 0; sl < r.slots && direct; sl++) direct = rdx[sl] == (sl | RDX_EXACT);
         if (direct) d.flags |= TF_DIRECT;
         const uint32_t depth = 64 - r.shift;
-        uint2* ddir; uint64_t* dfk; uint32_t *dft, *drdx, *dgp, *ddm = nullptr;
+        uint2* ddir; uint64_t* dfk; uint32_t *dft, *drdx, *ddm = nullptr;
         if ((rc = dev_upload(&ddir, dir.data(), n_buckets + 1, t->owned, t->bytes)) ||
-            (rc = dev_upload(&dgp, gpre.data(), n_buckets + 1, t->owned, t->bytes)) ||
             (any_dup && (rc = dev_upload(&ddm, dmask.data(), n_buckets, t->owned, t->bytes))) ||
             (rc = dev_upload(&dfk, fkey.data(), n_buckets, t->owned, t->bytes)) ||
             (rc = dev_upload(&dft, ftail.data(), 3ull * n_buckets, t->owned, t->bytes)) ||
             (rc = dev_upload(&drdx, rdx.data(), rdx.size(), t->owned, t->bytes)) ||
-            (rc = dev_upload(&t->scan_cnt, cnt.data(), n_buckets + 1, t->owned, t->bytes)) ||
-            (rc = dev_upload(&t->scan_part, nullptr, n_buckets + 1, t->owned, t->bytes)) ||
-            (rc = dev_upload(&t->scan_sums, nullptr, (n_buckets + 1 + SCAN_TILE - 1) / SCAN_TILE, t->owned, t->bytes))) {
+            (rc = dev_upload(&t->gcnt_mut, cnt.data(), n_buckets + 1, t->owned, t->bytes))) {
             delete t;
             return rc;
         }
-        d.dir = ddir; t->dir_mut = ddir; d.gpre = dgp; t->gpre_mut = dgp; d.dmask = ddm; d.fkey = dfk; d.ftail = dft; d.rrdx = drdx;
+        d.dir = ddir; t->dir_mut = ddir; d.gcnt = t->gcnt_mut; d.dmask = ddm; d.fkey = dfk; d.ftail = dft; d.rrdx = drdx;
         d.rbase = r.base; d.rshift = r.shift; d.rslots = r.slots; t->rbits = r.bits;
         // window lines (rt_wl_kernel): direct-mapped, uniform depth 1..43, every node inside its
         // bucket's dyadic range
@@ -6700,13 +7097,14 @@ int kad_table_create(kad_table** out, int device, uint32_t n_nodes, const uint8_
                 for (uint32_t j = bucket_offset[b]; j < bucket_offset[b + 1] && inside; j++)
                     inside = (id_hi(ids + 20ull * j) >> r.shift) == pre0 + b;
             if (inside) {
-                uint32_t* lp;
-                if ((rc = dev_upload(&lp, nullptr, 32ull * n_buckets, t->owned, t->bytes))) {
+                uint32_t *lp, *lps;
+                if ((rc = dev_upload(&lp, nullptr, 32ull * n_buckets, t->owned, t->bytes)) ||
+                    (rc = dev_upload(&lps, nullptr, 16ull * n_buckets, t->owned, t->bytes))) {
                     delete t;
                     return rc;
                 }
-                hipLaunchKernelGGL(wl_build_kernel, dim3(grid_for(n_buckets)), dim3(BLOCK), 0, 0, d.key, d.status, d.dir,
-                                   d.gpre, n_buckets, depth, pre0, lp, LineSel{});
+                hipLaunchKernelGGL(wl_build_kernel<true>, dim3(grid_for(n_buckets)), dim3(BLOCK), 0, 0, d.key, d.status,
+                                   d.dir, d.gcnt, n_buckets, depth, pre0, lp, lps, LineSel{});
                 if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
                     delete t;
                     return set_err(KAD_ERR_HIP, "window-line build failed");
@@ -6714,17 +7112,6 @@ int kad_table_create(kad_table** out, int device, uint32_t n_nodes, const uint8_
                 d.wl = reinterpret_cast<const uint4*>(lp);
                 t->wl_mut = lp;
                 d.flags |= TF_WL;
-                uint32_t* lps;
-                if ((rc = dev_upload(&lps, nullptr, 16ull * n_buckets, t->owned, t->bytes))) {
-                    delete t;
-                    return rc;
-                }
-                hipLaunchKernelGGL(ws_build_kernel, dim3(grid_for(n_buckets)), dim3(BLOCK), 0, 0, lp, n_buckets, lps,
-                                   LineSel{});
-                if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
-                    delete t;
-                    return set_err(KAD_ERR_HIP, "short window-line build failed");
-                }
                 d.ws = reinterpret_cast<const uint4*>(lps);
                 t->ws_mut = lps;
                 d.flags |= TF_WS;
@@ -6782,10 +7169,21 @@ int kad_table_get_info(const kad_table* t, kad_table_info* out) {
     out->nc_radix_bits = t->nbits;
     out->device_bytes = t->bytes;
     out->n_good = 0;
-    if (t->d.B) {
+    if (t->d.B) {  // the sum of the per-bucket good counts
         DeviceGuard g(t->device);
-        uint32_t last;
-        HIP_TRY(hipMemcpy(&last, t->d.gpre + t->d.B, sizeof last, hipMemcpyDeviceToHost));
+        if (t->mut_async) HIP_TRY(hipEventSynchronize(t->mut_ev));  // after the last asynchronous refresh
+        uint32_t* acc = nullptr;
+        HIP_TRY(hipMalloc(&acc, sizeof(uint32_t)));
+        uint32_t last = 0;
+        hipError_t e = hipMemset(acc, 0, sizeof(uint32_t));
+        if (e == hipSuccess) {
+            hipLaunchKernelGGL(sum_u32_kernel, dim3(std::min(grid_for(t->d.B), 1024u)), dim3(BLOCK), 0, 0, t->d.gcnt,
+                               t->d.B, acc);
+            e = hipGetLastError();
+        }
+        if (e == hipSuccess) e = hipMemcpy(&last, acc, sizeof last, hipMemcpyDeviceToHost);  // after the table's refreshes
+        (void)hipFree(acc);
+        if (e != hipSuccess) return set_err(KAD_ERR_HIP, "good count: %s", hipGetErrorString(e));
         out->n_good = last;
     }
     return KAD_OK;
@@ -6836,6 +7234,13 @@ int kad_table_patch_status(kad_table* t, uint32_t m, const uint32_t* nodes, cons
         uint8_t* st = static_cast<uint8_t*>(t->stage);
         if (nodes) HIP_TRY(hipMemcpy(st, nodes, 4ull * m, hipMemcpyHostToDevice));
         HIP_TRY(hipMemcpy(st + ib, status, m, hipMemcpyHostToDevice));
+        if (nodes && m <= RF_CAP) {  // a few nodes: the small refresh (no pass over the buckets or the lines)
+            if ((rc = small_refresh(t, nullptr, nullptr, 0, nullptr, 0, reinterpret_cast<const uint32_t*>(st), m, st + ib,
+                                    0)))
+                return rc;
+            HIP_TRY(hipDeviceSynchronize());
+            return KAD_OK;
+        }
         hipLaunchKernelGGL(status_patch_kernel, dim3(grid_for(m)), dim3(BLOCK), 0, 0,
                            nodes ? reinterpret_cast<const uint32_t*>(st) : nullptr, st + ib, m, t->status_mut,
                            marks_of(t));
@@ -6902,33 +7307,39 @@ int kad_table_refresh_status(kad_table* t, int64_t now_ns, void* stream) {
     DeviceGuard g(t->device);
     hipStream_t s = (hipStream_t)stream;
     int rc;
-    if ((rc = ensure_marks(t))) return rc;
     Deadlines& D = t->dl;
     const uint32_t n = t->d.n;
     const uint64_t nowk = dl_key(now_ns);
     if (D.valid && now_ns >= D.last_now) {
-        if (D.ev_pending && hipEventQuery(D.ev) == hipSuccess) {
-            D.next = *D.next_host;
-            D.next_known = true;
-            D.ev_pending = false;
-        }
-        if (D.np == 0 && D.next_known && nowk <= D.next) {  // no deadline passed, nothing patched: no status can change
+        if (D.np == 0 && nowk <= D.next) {  // no deadline passed, nothing patched: no status can change
             D.last_now = now_ns;
             return KAD_OK;
         }
-        // the nodes whose deadline `now` passes, and the patched ones
-        hipLaunchKernelGGL(dl_search_kernel, dim3(1), dim3(64), 0, s, D.km, D.nm, D.ks, D.ns, nowk, D.cur, D.next_dev);
-        hipLaunchKernelGGL(dl_process_kernel, dim3(512), dim3(BLOCK), 0, s, times_of(t), D.kn, D.sn, D.cur, D.pend, D.np,
-                           n, now_ns, t->status_mut, marks_of(t));
-        HIP_TRY(hipGetLastError());
+        // the nodes whose deadline `now` passes (both runs, found on the host copies of their keys) and the patched ones
+        const uint32_t hm = gallop_lower_bound(D.hkm, D.cm, nowk);
+        const uint32_t hs = (uint32_t)(std::lower_bound(D.hks.begin() + D.cs, D.hks.end(), nowk) - D.hks.begin());
+        const uint32_t mc = hm - D.cm, sc = hs - D.cs;
+        // the resident service reads what changes: its launch ends (the next one waits for mut_ev)
+        if ((rc = svc_quiesce(t)) || (rc = ensure_marks(t))) return rc;
+        if ((uint64_t)mc + sc + D.np <= RF_CAP) {
+            rc = small_refresh(t, s, D.kn + D.cm, mc, D.sn + D.cs, sc, D.pend, D.np, nullptr, now_ns);
+        } else {
+            hipLaunchKernelGGL(dl_process_kernel, dim3(512), dim3(BLOCK), 0, s, times_of(t), D.kn + D.cm, mc, D.sn + D.cs,
+                               sc, D.pend, D.np, n, now_ns, t->status_mut, marks_of(t));
+            rc = hipGetLastError() == hipSuccess ? rebuild_good_prefix(t, s, false)
+                                                 : set_err(KAD_ERR_HIP, "status refresh launch failed");
+        }
+        if (rc) { D.invalidate(); return rc; }
+        D.cm = hm;
+        D.cs = hs;
         D.np = 0;
         D.hpend.clear();
         D.last_now = now_ns;
-        if ((rc = dl_publish(t, s))) { D.invalidate(); return rc; }
-        if ((rc = rebuild_good_prefix(t, s, false))) return rc;
+        D.set_next();
         return mark_async(t, s);
     }
     // first refresh after set_times / a status patch, or `now` moved back: every node, then the runs
+    if ((rc = svc_quiesce(t)) || (rc = ensure_marks(t))) return rc;
     D.invalidate();
     if (n)
         hipLaunchKernelGGL(status_from_times_kernel, dim3(grid_for(n)), dim3(BLOCK), 0, s, times_of(t), n, now_ns,
@@ -7219,7 +7630,6 @@ int kad_nc_closest_batch(const kad_table* t, const uint8_t* targets, uint32_t q,
                          uint8_t* out_cnt, void* stream) {
     if (!t) return set_err(KAD_ERR_INVALID, "NULL table");
     if (!(t->flags & KAD_TABLE_SORTED)) return set_err(KAD_ERR_NOT_SORTED, "NodeCache query needs a KAD_TABLE_SORTED table");
-    if (count > 255) return set_err(KAD_ERR_UNSUPPORTED, "count %u > 255", count);
     if (q == 0) return KAD_OK;
     if (!targets || (!out_idx && count)) return set_err(KAD_ERR_INVALID, "NULL buffer");
     DeviceGuard g(t->device);
@@ -7292,7 +7702,6 @@ int kad_nc_closest_batch_dual(const kad_table* t4, const kad_table* t6, const ui
     for (const kad_table* t : {t4, t6})
         if (t && t->d.n && !(t->flags & KAD_TABLE_SORTED))
             return set_err(KAD_ERR_NOT_SORTED, "NodeCache query needs KAD_TABLE_SORTED tables");
-    if (count > 64) return set_err(KAD_ERR_UNSUPPORTED, "count %u > 64 (dual-family NodeCache batch)", count);
     if (q == 0) return KAD_OK;
     if (!targets || !af || (!out_idx && count)) return set_err(KAD_ERR_INVALID, "NULL buffer");
     DevTable empty{};  // a missing family behaves as an empty map (no results)
@@ -7315,9 +7724,12 @@ int kad_nc_closest_batch_dual(const kad_table* t4, const kad_table* t6, const ui
     else if (count <= 32 && ((d4.flags | d6.flags) & TF_NCL32))  // a family without the lines takes the wave path
         hipLaunchKernelGGL((nc32_line_kernel<0, true>), dim3(grid_for(8ull * q)), dim3(BLOCK), 0, s, d4, d6, af, targets,
                            q, count, out_idx, out_cnt);
-    else
+    else if (count <= 64)
         hipLaunchKernelGGL(nc_two_pass_dual_kernel, dim3((q + BLOCK / 64 - 1) / (BLOCK / 64)), dim3(BLOCK), 0, s, d4, d6,
                            af, targets, q, count, out_idx, out_cnt);
+    else  // any larger count (node_cache.h:32 takes a size_t): the serial walk
+        hipLaunchKernelGGL(nc_closest_dual_kernel, dim3(grid_for(q)), dim3(BLOCK), 0, s, d4, d6, af, targets, q, count,
+                           out_idx, out_cnt);
     HIP_TRY(hipGetLastError());
     return KAD_OK;
 }
@@ -7484,7 +7896,6 @@ static int host_query(const kad_table* t, const uint8_t* targets, uint32_t q, ui
     if (!targets || (!out_idx && count)) return set_err(KAD_ERR_INVALID, "NULL buffer");
     // every check the per-chunk calls make, once, before anything is queued
     if (nc && !(t->flags & KAD_TABLE_SORTED)) return set_err(KAD_ERR_NOT_SORTED, "NodeCache query needs a KAD_TABLE_SORTED table");
-    if (nc && count > 255) return set_err(KAD_ERR_UNSUPPORTED, "count %u > 255", count);
     {
         std::lock_guard<std::mutex> lk(t->pipe_mu);
         if (!t->pipe) {
@@ -7608,7 +8019,8 @@ int kad_table_serve_stats(const kad_table* t, kad_serve_stats* out) {
     out->requests = P.vrequests;
     if (P.vr && P.vkhz > 0 && P.vrequests) {
         out->last_polls = P.vr->polls;
-        out->last_busy_ns = (uint64_t)((P.vr->t_done - P.vr->t_seen) * 1e6 / P.vkhz);
+        const uint64_t a = P.vr->t_seen, b = P.vr->t_done;
+        out->last_busy_ns = b > a ? (uint64_t)((double)(b - a) * 1e6 / P.vkhz) : 0u;
     }
     return KAD_OK;
 }
@@ -7816,15 +8228,12 @@ int kad_table_apply(kad_table* t, const uint32_t* ops, uint32_t n_ops, const uin
         dir[c].x = off1[c] | (c < B1 && off1[c + 1] - off1[c] > 32 ? WIDE : 0u);
         dir[c].y = 0;
     }
-    uint2* ddir; uint32_t *dgp = nullptr, *scnt = nullptr, *spart = nullptr, *ssums = nullptr, *ddm, *dany;
+    uint2* ddir; uint32_t *scnt = nullptr, *ddm, *dany;
     if ((rc = dev_upload(&ddir, dir.data(), B1 + 1, fresh, freshb))) return fail(rc);
     const bool reshape = B1 != B0;
     BucketIndex bix;
     if (reshape &&
-        ((rc = dev_upload(&dgp, nullptr, B1 + 1, fresh, freshb)) ||
-         (rc = dev_upload(&scnt, nullptr, B1 + 1, fresh, freshb)) ||
-         (rc = dev_upload(&spart, nullptr, B1 + 1, fresh, freshb)) ||
-         (rc = dev_upload(&ssums, nullptr, (B1 + 1 + SCAN_TILE - 1) / SCAN_TILE, fresh, freshb))))
+        (rc = dev_upload(&scnt, nullptr, B1 + 1, fresh, freshb)))
         return fail(rc);
     std::vector<uint8_t>& first1 = plan.first1;  // the new bucket firsts (only splits change them)
     if (reshape && (rc = make_bucket_index(first1, B1, bix, fresh, freshb))) return fail(rc);
@@ -7878,9 +8287,8 @@ int kad_table_apply(kad_table* t, const uint32_t* ops, uint32_t n_ops, const uin
     release(t, t->dir_mut);
     d.dir = ddir; t->dir_mut = ddir;
     if (reshape) {
-        release(t, t->gpre_mut);
-        release(t, t->scan_cnt); release(t, t->scan_part); release(t, t->scan_sums);
-        d.gpre = dgp; t->gpre_mut = dgp; t->scan_cnt = scnt; t->scan_part = spart; t->scan_sums = ssums; d.B = B1;
+        release(t, t->gcnt_mut);
+        d.gcnt = scnt; t->gcnt_mut = scnt; d.B = B1;
         release(t, const_cast<uint64_t*>(d.fkey));
         release(t, const_cast<uint32_t*>(d.ftail));
         release(t, const_cast<uint32_t*>(d.rrdx));

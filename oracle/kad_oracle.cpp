@@ -27,6 +27,7 @@
 #include <list>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <random>
 #include <thread>
 #include <vector>
@@ -619,8 +620,12 @@ struct Swarm {
     uint32_t n;
     const uint8_t* ids;
     std::vector<uint64_t> key;
-    std::vector<uint8_t> depth, counts;  // counts[p*SW_LEVELS + level]
-    std::vector<uint32_t> ent;           // ent[(p*SW_LEVELS + level)*SW_BUCKET + j]
+    std::unique_ptr<uint8_t[]> depth, counts;  // counts[p*SW_LEVELS + level]
+    std::unique_ptr<uint32_t[]> ent;           // ent[(p*SW_LEVELS + level)*SW_BUCKET + j]
+    std::unique_ptr<std::once_flag[]> once;    // lazy model: each peer's table built on first use
+    void ensure(uint32_t p) const {
+        if (once) std::call_once(once[p], [&] { const_cast<Swarm*>(this)->build(p); });
+    }
     // peers whose top-64 key starts with the L-bit prefix P: [lo, hi)
     void range(uint64_t P, uint32_t L, uint32_t& lo, uint32_t& hi) const {
         if (L == 0) { lo = 0; hi = n; return; }
@@ -637,7 +642,10 @@ struct Swarm {
             if (hi - lo - 1 <= SW_BUCKET || D == SW_LEVELS - 1) break;
         }
         depth[p] = (uint8_t)D;
-        for (uint32_t d = 0; d < SW_LEVELS; d++) counts[(size_t)p * SW_LEVELS + d] = 0;
+        for (uint32_t d = 0; d < SW_LEVELS; d++) {
+            counts[(size_t)p * SW_LEVELS + d] = 0;
+            for (uint32_t j = 0; j < SW_BUCKET; j++) ent[((size_t)p * SW_LEVELS + d) * SW_BUCKET + j] = 0xFFFFFFFFu;
+        }
         for (uint32_t d = 0; d < D; d++) {
             uint32_t a, e;
             range((k >> (63 - d)) ^ 1ull, d + 1, a, e);
@@ -655,6 +663,7 @@ struct Swarm {
     }
     // p's table as a RoutingTable (buckets sorted by first) -> findClosestNodes(t, count)
     void closest(uint32_t p, const Id& t, uint32_t count, std::vector<uint32_t>& out) const {
+        ensure(p);
         out.clear();
         const Id me(ids + (size_t)HASH_LEN * p);
         const uint32_t D = depth[p];
@@ -691,7 +700,7 @@ struct Swarm {
 };
 
 extern "C" {
-void* orc_swarm_build(uint32_t n, const uint8_t* sorted_ids, int nthreads) {
+static Swarm* swarm_alloc(uint32_t n, const uint8_t* sorted_ids) {
     Swarm* s = new Swarm;
     s->n = n;
     s->ids = sorted_ids;
@@ -701,15 +710,28 @@ void* orc_swarm_build(uint32_t n, const uint8_t* sorted_ids, int nthreads) {
         for (int b = 0; b < 8; b++) k = (k << 8) | sorted_ids[(size_t)HASH_LEN * i + b];
         s->key[i] = k;
     }
-    s->depth.resize(n);
-    s->counts.resize((size_t)n * SW_LEVELS);
-    s->ent.assign((size_t)n * SW_LEVELS * SW_BUCKET, 0xFFFFFFFFu);
+    // not value-initialised: a lazy model touches only the pages of the peers it builds
+    s->depth.reset(new uint8_t[n]);
+    s->counts.reset(new uint8_t[(size_t)n * SW_LEVELS]);
+    s->ent.reset(new uint32_t[(size_t)n * SW_LEVELS * SW_BUCKET]);
+    return s;
+}
+void* orc_swarm_build(uint32_t n, const uint8_t* sorted_ids, int nthreads) {
+    Swarm* s = swarm_alloc(n, sorted_ids);
     parallel_for(n, nthreads, [&](uint32_t a, uint32_t e) { for (uint32_t p = a; p < e; p++) s->build(p); });
+    return s;
+}
+// The same model with each peer's table built when a query first reaches it (swarms of 10M peers, of which a
+// sample of lookups touches a few thousand).
+void* orc_swarm_build_lazy(uint32_t n, const uint8_t* sorted_ids) {
+    Swarm* s = swarm_alloc(n, sorted_ids);
+    s->once.reset(new std::once_flag[n]);
     return s;
 }
 void orc_swarm_free(void* h) { delete (Swarm*)h; }
 void orc_swarm_table(void* h, uint32_t p, uint32_t* depth, uint8_t* counts, uint32_t* ent) {
     const Swarm* s = (const Swarm*)h;
+    s->ensure(p);
     *depth = s->depth[p];
     std::memcpy(counts, &s->counts[(size_t)p * SW_LEVELS], SW_LEVELS);
     std::memcpy(ent, &s->ent[(size_t)p * SW_LEVELS * SW_BUCKET], 4ull * SW_LEVELS * SW_BUCKET);

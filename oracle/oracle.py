@@ -43,6 +43,7 @@ _SIG = {
     "orc_infohash_get": (C.c_int, [C.c_uint32, _P, _P, _P]),
     "orc_table_apply": (C.c_int, [_P, C.c_uint32, _P, C.c_uint32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "orc_swarm_build": (_P, [C.c_uint32, _P, C.c_int]),
+    "orc_swarm_build_lazy": (_P, [C.c_uint32, _P]),
     "orc_swarm_free": (None, [_P]),
     "orc_swarm_table": (None, [_P, C.c_uint32, _P, _P, _P]),
     "orc_swarm_closest": (C.c_int, [_P, C.c_uint32, _P, _P, C.c_uint32, _P, _P, C.c_int]),
@@ -254,10 +255,12 @@ class SwarmModel:
     """Config 5 swarm model (kad_oracle.cpp "Config 5 swarm model"): shape-K peer tables over sorted
     IDs, per-peer findClosestNodes, synchronous iterative lookups."""
 
-    def __init__(self, sorted_ids, nthreads=8):
+    def __init__(self, sorted_ids, nthreads=8, lazy=False):
+        """lazy: each peer's table is built when a query first reaches it (10M-peer swarms)."""
         self.ids = _ids(sorted_ids)
         self.n = self.ids.shape[0]
-        self._h = lib().orc_swarm_build(self.n, _p(self.ids), nthreads)
+        self._h = (lib().orc_swarm_build_lazy(self.n, _p(self.ids)) if lazy
+                   else lib().orc_swarm_build(self.n, _p(self.ids), nthreads))
 
     def close(self):
         if self._h:

@@ -87,7 +87,7 @@ static void check_rt(const RoutingTable& rt, const std::vector<std::vector<std::
 }
 
 static void check_nc(const NodeMap& nm, const std::vector<std::vector<std::shared_ptr<Node>>>& got,
-                     const std::vector<InfoHash>& targets, uint32_t count, const char* what) {
+                     const std::vector<InfoHash>& targets, size_t count_in, const char* what) {
     std::vector<uint8_t> ids, st;
     std::vector<const Node*> flat;
     for (auto& kv : nm) {
@@ -97,14 +97,22 @@ static void check_nc(const NodeMap& nm, const std::vector<std::vector<std::share
         flat.push_back(n.get());
     }
     const uint32_t q = (uint32_t)targets.size();
-    std::vector<uint32_t> want(q * count);
+    const uint32_t count = (uint32_t)std::min<size_t>(count_in, flat.size());  // a result holds at most the map
+    EXPECT(got.size() == q, "%s: nc rows", what);
+    if (count == 0) {
+        for (uint32_t i = 0; i < q; i++) EXPECT(got[i].empty(), "%s: nc empty q=%u", what, i);
+        return;
+    }
+    std::vector<uint32_t> want((size_t)q * count);
     std::vector<uint8_t> wcnt(q);
     orc_flat_nc_closest((uint32_t)flat.size(), ids.data(), st.data(), q, reinterpret_cast<const uint8_t*>(targets.data()),
                         count, want.data(), wcnt.data(), 4);
     for (uint32_t i = 0; i < q; i++) {
-        EXPECT(got[i].size() == wcnt[i], "%s: nc count q=%u k=%u", what, i, count);
-        for (uint32_t j = 0; j < got[i].size() && j < wcnt[i]; j++)
-            EXPECT(got[i][j].get() == flat[want[i * count + j]], "%s: nc node q=%u j=%u", what, i, j);
+        uint32_t m = 0;  // the row's entries before the padding (the count byte wraps above 255)
+        while (m < count && want[(size_t)i * count + m] != 0xFFFFFFFFu) m++;
+        EXPECT(got[i].size() == m, "%s: nc count q=%u k=%zu", what, i, count_in);
+        for (uint32_t j = 0; j < got[i].size() && j < m; j++)
+            EXPECT(got[i][j].get() == flat[want[(size_t)i * count + j]], "%s: nc node q=%u j=%u", what, i, j);
     }
 }
 
@@ -259,6 +267,14 @@ int main() {
             check_nc(c6, b6, targets, count, "nc v6 after sync");
         }
         EXPECT(nc.family(AF_INET).size() == c4.size() && nc.family(AF_INET6).size() == c6.size(), "nc sizes after sync");
+        // any size_t count (node_cache.h:32): above the kernels' 64, above the count byte's 255, above the map's size
+        for (size_t count : {size_t(300), c6.size() + 5, size_t(1) << 40}) {
+            std::vector<InfoHash> few(targets.begin(), targets.begin() + 40);
+            auto b4 = nc.family(AF_INET).getCachedNodesBatch(few, count);
+            auto b6 = nc.family(AF_INET6).getCachedNodesBatch(few, count);
+            check_nc(c4, b4, few, count, "nc v4 large count");
+            check_nc(c6, b6, few, count, "nc v6 large count");
+        }
     }
 
     // Incremental mirror: Dht::onNewNode (replace an expired node / emplace_front / split my bucket)

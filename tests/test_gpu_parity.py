@@ -390,6 +390,38 @@ def test_rt_closest_any_count(gpu, t):
                 np.testing.assert_array_equal(hc, np.minimum(m, 255))
 
 
+@pytest.mark.parametrize("t", [x for x in TB.all_small_tables() if x["sorted"]] + [TB.uniform_config(20_000, 11, seed=0xB17)],
+                         ids=lambda t: t["name"])
+def test_nc_closest_any_count(gpu, t):
+    """NodeCache::getCachedNodes takes any size_t count (node_cache.h:32, node_cache.cpp:36-66): counts above 64
+    run the serial walk (a lane per query). Bit-exact rows for counts 65 .. 1000 and one above the map's size; the
+    count byte saturates at 255 and the row padding gives the length beyond it. The same through the dual-family
+    batch and the host-pointer batch."""
+    from opendht_amd import nc_closest_dual
+
+    targets = TB.adversarial_targets(t, extra=400)
+    tg = dev(targets, gpu)
+    with make(t, gpu) as T:
+        for k in (65, 100, 255, 300, 1000, t["ids"].shape[0] + 3):
+            idx, cnt = T.nc_closest(tg, k)
+            torch.cuda.synchronize()
+            want, _ = O.flat_nc_closest(t["ids"], t["status"], targets, k, nthreads=8)
+            np.testing.assert_array_equal(u32(idx), want, err_msg=f"{t['name']} nc k={k} indices")
+            m = _rows_len(want)
+            np.testing.assert_array_equal(cnt.cpu().numpy(), np.minimum(m, 255), err_msg=f"{t['name']} nc k={k} counts")
+            if k in (65, 300):
+                af = torch.zeros(targets.shape[0], dtype=torch.uint8, device=gpu)
+                af[1::2] = 1
+                di, dc = nc_closest_dual(T, None, tg, af, k)
+                torch.cuda.synchronize()
+                even = np.arange(targets.shape[0]) % 2 == 0
+                np.testing.assert_array_equal(u32(di)[even], want[even], err_msg=f"{t['name']} nc dual k={k}")
+                assert (dc.cpu().numpy()[~even] == 0).all() and (u32(di)[~even] == KAD_NO_NODE).all()
+                hi, hc = T.nc_closest_host(targets, k)
+                np.testing.assert_array_equal(hi, want, err_msg=f"{t['name']} nc host k={k}")
+                np.testing.assert_array_equal(hc, np.minimum(m, 255))
+
+
 def test_host_batch_small_and_large(gpu):
     """kad_rt_closest_batch_host: batches of 1 .. 1024 queries with count <= 64 take the one-launch path on mapped
     pinned memory, larger ones the chunked pipeline; both equal the device batch."""

@@ -132,3 +132,11 @@ def test_split_builder_matches_faithful():
         b = O.split_table(ids)
         for x, y in zip(a, b):
             np.testing.assert_array_equal(x, y)
+
+
+@pytest.mark.parametrize("t", [x for x in TB.all_small_tables() if x["sorted"] and x["first"] is not None],
+                         ids=lambda t: t["name"])
+def test_restatements_agree_large_counts(t):
+    """Both restatements for counts above the line kernels' (RoutingTable and NodeCache take any size_t count,
+    routing_table.h:48, node_cache.h:32), up to counts larger than the table."""
+    _check_restatements(t, TB.adversarial_targets(t, extra=64), counts=(65, 300, 1000, t["ids"].shape[0] + 7))

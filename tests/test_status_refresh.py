@@ -248,3 +248,68 @@ def test_host_batch_ordered_after_async_refresh(gpu):
                 want, wcnt = O.flat_rt_closest(t["ids"], st, t["first"], t["off"], targets[:q], 8, nthreads=8)
                 np.testing.assert_array_equal(idx, want, err_msg=f"dt={dt} q={q}")
                 np.testing.assert_array_equal(cnt, wcnt)
+
+
+@pytest.mark.parametrize("t", [TB.uniform_config(50_000, 12, seed=0x5EA), TB.split_config(30_000, seed=0x5EB)],
+                         ids=lambda t: t["name"])
+def test_small_refresh_every_line_set(gpu, t):
+    """The small refresh path (at most 2,048 nodes to re-derive: rf_nodes_kernel lists the changed buckets and the
+    lines whose windows reach them, the builders rebuild only those) on tables holding every line set (uniform:
+    short, 128-byte, 9..16, 17..32 and NodeCache lines; split policy: slot, general 8 / 16 / 32 lines and their
+    slot copies), then across the 2,048 boundary to the flag path: `now` passes exactly k deadlines for
+    k = 1, 2, 7, 100, 2047, 2048, 2049, 5000; patch_times of a few nodes (heard again, expired: NodeCache ranges)
+    refreshed at the same `now`; patch_status of a few nodes, including the first and last buckets' (windows
+    clamped at the table's ends). After every step the status bytes equal isGood / isExpired and every query
+    equals the oracle."""
+    n = t["ids"].shape[0]
+    off = t["off"]
+    rng = np.random.default_rng(n)
+    targets = TB.adversarial_targets(t, extra=2500)
+    MIN = 60 * 10**9
+    now = 700 * 3600 * 10**9
+    time_ns = now - rng.integers(0, 10 * MIN, n)
+    reply_ns = now - rng.integers(0, 120 * MIN, n)
+    expired = (rng.random(n) < 0.05).astype(np.uint8)
+
+    def status_at(tnow):
+        good = (expired == 0) & (reply_ns >= tnow - 120 * MIN) & (time_ns >= tnow - 10 * MIN)
+        return (good.astype(np.uint8) | (expired << 1)).astype(np.uint8)
+
+    def passed_after(k):  # the `now` at which exactly k more (distinct) deadlines have passed
+        d = np.minimum(time_ns + 10 * MIN, reply_ns + 120 * MIN)
+        d = np.unique(d[(expired == 0) & (d >= now)])
+        return int(d[min(len(d) - 1, k - 1)]) + 1
+
+    rt, nc = (1, 8, 14, 16, 32), (1, 14, 32)
+    with DeviceTable(t["ids"], status_at(now), t["first"], t["off"], device=0, sorted=t["sorted"], eager=True) as T:
+        T.set_times(time_ns, reply_ns, expired)
+        T.refresh_status(now)
+        for k in (1, 2, 7, 100, 2047, 2048, 2049, 5000):
+            now = passed_after(k)
+            T.refresh_status(now)
+            torch.cuda.synchronize()
+            st = status_at(now)
+            np.testing.assert_array_equal(T.export_status(), st, err_msg=f"k={k}")
+            if k in (1, 7, 2048, 2049):
+                _check(T, t, st, targets, gpu, rt=rt, nc=nc)
+        # a few nodes heard again or expired (the NodeCache lines' ranges), refreshed at the same `now`
+        sel = np.unique(np.concatenate([rng.choice(n, 40, replace=False), [0, n - 1]])).astype(np.uint32)
+        time_ns[sel[::2]] = now
+        reply_ns[sel[::2]] = now
+        expired[sel[1::2]] = 1
+        T.patch_times(sel, time_ns[sel], reply_ns[sel], expired[sel])
+        T.refresh_status(now)
+        torch.cuda.synchronize()
+        st = status_at(now)
+        np.testing.assert_array_equal(T.export_status(), st)
+        _check(T, t, st, targets, gpu, rt=rt, nc=nc)
+        # direct status patches of a few nodes: the first and last buckets' nodes and random ones
+        nodes = np.unique(np.concatenate([np.arange(off[0], off[2]), np.arange(off[-3], off[-1]),
+                                          rng.choice(n, 60, replace=False)])).astype(np.uint32)
+        vals = rng.choice(np.array([0, 1, 1, 2, 3], np.uint8), size=nodes.shape[0])
+        st = st.copy()
+        st[nodes] = vals
+        T.patch_status(nodes, vals)
+        np.testing.assert_array_equal(T.export_status(), st)
+        assert T.info()["n_good"] == int((st & 1).sum())
+        _check(T, t, st, targets, gpu, rt=rt, nc=nc)

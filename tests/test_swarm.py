@@ -202,6 +202,7 @@ def test_swarm_search_offline_peers_oracle(off):
     tg = S.random_targets(src.shape[0], seed=9)
     lst, q, bad, nn, hops, done = M.search_ex(src, tg, off)
     _check_lookup_properties(ids, lst, q, bad, nn, done, off, tg)
+    _check_lookup_properties_vec(ids, lst, q, bad, nn, done, off, tg)
     assert set(np.unique(done)) <= {1, 2, 3}
     if off == 0:
         a = M.search(src, tg)
@@ -272,5 +273,81 @@ def test_swarm_gpu_1m_peers(gpu):
         assert active == 0 and ovf == 0
         _check_lookup_properties(ids, lst, q, bad, nn, done, off, tg)
         assert (done == 1).mean() > 0.97 and hops.max() < 30
+        X.close()
+    M.close()
+
+
+def _check_lookup_properties_vec(ids, lst, q, bad, n, done, offline_per_10k, tg):
+    """_check_lookup_properties over every lookup at once (numpy), for batches of a million lookups."""
+    from opendht_amd.swarm import SEARCH_NODES
+
+    key, tk = _key(ids), _key(tg)
+    peer_off = _offline(np.arange(ids.shape[0]), offline_per_10k)
+    valid = np.arange(lst.shape[1])[None, :] < n.astype(np.int64)[:, None]
+    assert (lst[~valid] == O.NO_NODE).all()
+    li = np.where(valid, lst, 0).astype(np.int64)
+    d = key[li] ^ tk[:, None]
+    assert ((d[:, 1:] >= d[:, :-1]) | ~valid[:, 1:]).all()  # ascending XOR distance
+    b = bad.astype(bool) & valid
+    nb = ~b & valid
+    assert (nb.sum(axis=1) <= SEARCH_NODES).all()
+    off = peer_off[li]
+    assert (off | ~b).all()  # bad nodes are offline peers
+    assert not (off & q.astype(bool) & nb).any()  # every queried offline peer turned bad
+    first8 = nb & (np.cumsum(nb, axis=1) <= 8)
+    syn = done == 1
+    assert nb[syn].any(axis=1).all() and (q.astype(bool)[syn] | ~first8[syn]).all()
+
+
+def test_swarm_lazy_model_equals_eager():
+    """The lazy oracle model (each peer's table built when a query first reaches it, for 10M-peer swarms) gives
+    the eager model's tables and lookups."""
+    n, off = 30_000, 1000
+    ids = _swarm_ids(n, 0x5AA)
+    A, Bm = O.SwarmModel(ids), O.SwarmModel(ids, lazy=True)
+    rng = np.random.default_rng(0x5AA)
+    src = rng.integers(0, n, 500).astype(np.uint32)
+    src = src[~_offline(src, off)]
+    tg = S.random_targets(src.shape[0], seed=0x5AA)
+    for a, b in zip(A.search_ex(src, tg, off), Bm.search_ex(src, tg, off)):
+        np.testing.assert_array_equal(a, b)
+    for p in rng.integers(0, n, 50):
+        for a, b in zip(A.table(int(p)), Bm.table(int(p))):
+            np.testing.assert_array_equal(a, b)
+    A.close()
+    Bm.close()
+
+
+@pytest.mark.gpu
+def test_swarm_gpu_10m_peers(gpu):
+    """Config 5 at its stated size (BASELINE config 5: a 10M-node swarm): 10,000,000 peers, 1,048,576 lookups from
+    random online sources with 10 % of the peers offline, run to the end on the GPU. The model's invariants on
+    every lookup (Search::insertNode with bad-node accounting, dht.cpp:961-1047; synced per Search::isSynced,
+    dht.cpp:1467-1478), convergence, and a sample of 1,000 lookups hop by hop against the oracle (lazy model:
+    the tables of the peers the sample reaches)."""
+    from opendht_amd.swarm import Swarm
+    n, off = 10_000_000, 1000
+    ids = _swarm_ids(n, 0x5A9)
+    rng = np.random.default_rng(0x10A)
+    src = rng.integers(0, n, 1 << 20).astype(np.uint32)
+    src = src[~_offline(src, off)]
+    tg = S.random_targets(src.shape[0], seed=0x10B)
+    samp = rng.choice(src.shape[0], 1000, replace=False)
+    M = O.SwarmModel(ids, lazy=True)
+    with Swarm(ids, device=gpu.index or 0) as W:
+        X = W.search(torch.from_numpy(src.view(np.int32)).to(gpu), torch.from_numpy(tg).to(gpu), off)
+        for h in range(1, 64):
+            active = X.hop()
+            if h in (1, 3, 6) or active == 0:
+                lst, q, bad, nn, hops, done, ovf = X.get(full=True)
+                want = M.search_ex(src[samp], tg[samp], off, max_hops=h, nthreads=16)
+                for a, b, name in zip((lst, q, bad, nn, hops, done), want, ("list", "queried", "bad", "n", "hops", "done")):
+                    np.testing.assert_array_equal(a[samp], b, err_msg=f"hop {h}: {name}")
+            if active == 0:
+                break
+        assert active == 0 and ovf == 0
+        _check_lookup_properties_vec(ids, lst, q, bad, nn, done, off, tg)
+        assert (done == 1).mean() > 0.97 and hops.max() < 30
+        assert bad.any()
         X.close()
     M.close()
