@@ -408,6 +408,16 @@ def main_owner(args):
                     "table_MB": int(row.split("MB")[0]), "line_bytes": line_b,
                     "us_per_1M_rotated": a[row]["us_per_1M"], "us_per_1M_cold": a[row + "_cold"]["us_per_1M"]}
 
+    # the rows of the last timed step (batch K-1; before the extras, which reuse the buffers and change the
+    # status), checked against the CPU restatement on this rank's
+    # shard table (exact halo: every owned window lies inside it)
+    vrows = min(Q, args.verify_rows)
+    vt = tgs[(K - 1) % NB][:vrows].cpu().numpy()
+    bad = verify_rows(sh.ids, sh.status, sh.first, sh.off, sh.index_base, vt,
+                      outs[(K - 1) % NB][:vrows].cpu().numpy(), ocnt[(K - 1) % NB][:vrows].cpu().numpy(), cnt_k)
+    verified = {"rows": sum_over_ranks(dist, vrows), "mismatches": sum_over_ranks(dist, bad),
+                "what": f"the first {vrows} rows (indices, counts) of every rank's last timed step, against the "
+                        "closed-form CPU restatement (oracle/) on the rank's shard table"}
     extras = {}
     if not args.no_extras:
         extras["cold"] = cold_pass(T, tgs, outs, ocnt, cnt_k, Q, moved_q, dev, stream)
@@ -418,15 +428,6 @@ def main_owner(args):
             extras["latency"] = latency_pass(dev)
         if rank == 0 and world == 1:
             extras["configs"] = configs_pass(dev)
-    # the rows of the last timed step (batch K-1), checked against the CPU restatement on this rank's
-    # shard table (exact halo: every owned window lies inside it)
-    vrows = min(Q, args.verify_rows)
-    vt = tgs[(K - 1) % NB][:vrows].cpu().numpy()
-    bad = verify_rows(sh.ids, sh.status, sh.first, sh.off, sh.index_base, vt,
-                      outs[(K - 1) % NB][:vrows].cpu().numpy(), ocnt[(K - 1) % NB][:vrows].cpu().numpy(), cnt_k)
-    verified = {"rows": sum_over_ranks(dist, vrows), "mismatches": sum_over_ranks(dist, bad),
-                "what": f"the first {vrows} rows (indices, counts) of every rank's last timed step, against the "
-                        "closed-form CPU restatement (oracle/) on the rank's shard table"}
     cpu = fast = None
     if rank == 0 and world == 1 and not args.no_cpu:
         host_t = tgs[0][:1 << 17].cpu().numpy()
@@ -907,41 +908,55 @@ def refresh_pass(T, sh, tgs, outs, ocnt, cnt_k, Q, avg_kernel_s, dev, stream, re
                    "live: see its own `how`"}
 
 
-def live_pass(T, sh, tgs, outs, ocnt, cnt_k, Q, dev, stream, now, t, rt, ex, D, K=400, W=20, vrows=65536):
+def live_pass(T, sh, tgs, outs, ocnt, cnt_k, Q, dev, stream, now, t, rt, ex, D, K=1000, W=50, vrows=65536):
     """The query rate with `now` following the clock, as a live node calls the table (routing_table.cpp:77 and
     node.cpp:34-40 evaluate isGood(now) on every call): each step is kad_table_refresh_status(now) with `now` =
     the start time + the wall-clock time elapsed since, then one batch of Q queries on the same stream (a
     distinct batch per step). The node times are a live table's (good nodes heard over the last 10 minutes:
     a deadline passes every ~60 us on a 1/8 shard), so most refreshes return at once and the others re-derive
-    the nodes whose deadline passed (the small path). Eager issue from Python, HIP events around every refresh
-    for its GPU time. The last step's first `vrows` rows are checked against the CPU restatement at that
+    the nodes whose deadline passed (the small refresh: one launch that also rebuilds the lines). Eager issue
+    through direct C-ABI calls (ctypes, no per-step events); the same loop without the refresh gives the share
+    the refreshes take. The last step's first `vrows` rows are checked against the CPU restatement at that
     step's `now`."""
+    import ctypes as C
+
     import torch
+
+    from opendht_amd._lib import lib
 
     MIN = 60 * 10**9
     NB = len(tgs)
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
-    base = now
-    for j in range(W):  # warm-up: the same loop, untimed
-        now = base + j * 30_000
-        T.refresh_status(now, stream=stream.cuda_stream)
-        T.rt_closest(tgs[j % NB], cnt_k, outs[j % NB], ocnt[j % NB], stream=stream.cuda_stream)
+    L = lib()
+    h, s = T._h, C.c_void_p(stream.cuda_stream)
+    rt_fn, rf_fn = L.kad_rt_closest_batch, L.kad_table_refresh_status
+    P = [(C.c_void_p(tgs[j].data_ptr()), C.c_void_p(outs[j].data_ptr()), C.c_void_p(ocnt[j].data_ptr()))
+         for j in range(NB)]
+
+    def loop(refresh, start):
+        nows = []
+        t0 = time.perf_counter()
+        for j in range(K):
+            if refresh:
+                nw = start + int((time.perf_counter() - t0) * 1e9)
+                nows.append(nw)
+                if rf_fn(h, C.c_int64(nw), s):
+                    raise RuntimeError("kad_table_refresh_status failed")
+            tp, op, cp = P[j % NB]
+            if rt_fn(h, tp, Q, cnt_k, op, cp, s):
+                raise RuntimeError("kad_rt_closest_batch failed")
+        torch.cuda.synchronize(dev)
+        return time.perf_counter() - t0, nows
+
+    for j in range(W):  # warm-up: the same loop, untimed, `now` moving 30 us per step
+        now += 30_000
+        rf_fn(h, C.c_int64(now), s)
+        tp, op, cp = P[j % NB]
+        rt_fn(h, tp, Q, cnt_k, op, cp, s)
     torch.cuda.synchronize(dev)
-    start = now
-    nows = []
-    t0 = time.perf_counter()
-    for j in range(K):
-        now = start + int((time.perf_counter() - t0) * 1e9)
-        nows.append(now)
-        a, b = evs[j]
-        a.record(stream)
-        T.refresh_status(now, stream=stream.cuda_stream)
-        b.record(stream)
-        T.rt_closest(tgs[j % NB], cnt_k, outs[j % NB], ocnt[j % NB], stream=stream.cuda_stream)
-    torch.cuda.synchronize(dev)
-    wall = time.perf_counter() - t0
-    rf = np.array([a.elapsed_time(b) for a, b in evs])
-    passed = int(np.searchsorted(D, nows[-1], "left") - np.searchsorted(D, start, "left"))
+    wall0, _ = loop(False, now)
+    start = now + 1
+    wall, nows = loop(True, start)
+    passed = np.diff(np.searchsorted(D, np.array([start] + nows), "left"))
     # the last step at its `now`: isGood / isExpired from the host copies of the times
     st = (((ex == 0) & (rt >= nows[-1] - 120 * MIN) & (t >= nows[-1] - 10 * MIN)).astype(np.uint8) |
           (ex << 1)).astype(np.uint8)
@@ -949,23 +964,39 @@ def live_pass(T, sh, tgs, outs, ocnt, cnt_k, Q, dev, stream, now, t, rt, ex, D, 
     vr = min(Q, vrows)
     bad = verify_rows(sh.ids, st, sh.first, sh.off, sh.index_base, tgs[last][:vr].cpu().numpy(),
                       outs[last][:vr].cpu().numpy(), ocnt[last][:vr].cpu().numpy(), cnt_k)
-    work = rf > 0.003
+    # single refreshes passing k deadlines, each alone between two events (the events' own floor: k = 0)
+    ticks = {}
+    now = nows[-1]
+    for k in (0, 1, 4, 16, 64):
+        i0 = int(np.searchsorted(D, now, "left"))
+        nxt = now + 1 if k == 0 else int(D[min(D.shape[0] - 1, i0 + k - 1)]) + 1
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize(dev)
+        a.record(stream)
+        h0 = time.perf_counter()
+        rf_fn(h, C.c_int64(nxt), s)
+        h1 = time.perf_counter()
+        b.record(stream)
+        torch.cuda.synchronize(dev)
+        ticks[str(k)] = {"gpu_us": a.elapsed_time(b) * 1e3, "host_us": (h1 - h0) * 1e6,
+                         "passed": int(np.searchsorted(D, nxt, "left") - i0)}
+        now = nxt
     live = {"queries_per_s": Q * K / wall,
             "ms_per_step": wall / K * 1e3,
+            "ms_per_step_without_refresh": wall0 / K * 1e3,
+            "refresh_share": max(0.0, 1.0 - wall0 / wall),
             "steps": K,
             "now_advanced_ms": (nows[-1] - start) / 1e6,
-            "deadlines_passed": passed,
-            "refreshes_with_gpu_work": int(work.sum()),
-            "refresh_gpu_ms_mean": float(rf.mean()),
-            "refresh_gpu_ms_median_with_work": float(np.median(rf[work])) if work.any() else 0.0,
-            "refresh_gpu_ms_max": float(rf.max()),
-            "refresh_share": float(rf.sum() / (wall * 1e3)),
+            "deadlines_passed": int(passed.sum()),
+            "refreshes_with_gpu_work": int((passed > 0).sum()),
+            "single_refresh_us": ticks,
             "verified": {"rows": vr, "mismatches": bad,
                          "what": "the first rows of the last step against the CPU restatement at that step's `now`"},
             "how": "K steps of refresh_status(now = start + elapsed wall time) + one Q-query batch on one stream, "
-                   "eager; queries_per_s = K*Q / wall; refresh GPU time between HIP events around each refresh "
-                   "(a refresh below the next deadline launches nothing: ~0 ms)"}
-    return live, nows[-1] + 1
+                   "eager through direct C-ABI calls; queries_per_s = K*Q / wall; refresh_share = 1 - (the same loop "
+                   "without the refresh) / wall; single_refresh_us: one refresh passing k deadlines between two HIP "
+                   "events (k = 0: the events' floor, no GPU work) and the host time of the call"}
+    return live, now + 1
 
 
 # ---------------------------------------------------------------------------------------------
@@ -1019,11 +1050,12 @@ def graph_steps(step, K, W, dev, dist, use_graph=True):
 
 def allgather_pass(args, world, rank, local, dev, dist):
     """The north-star variant: the 100M-node table in `world` halo-free shards, the same
-    1M-query batch on every rank, each rank's part of every window, one all-gather of fixed-size blocks,
-    the device scatter + merge; no host read inside the K steps (the overflow word is read after them)."""
+    1M-query batch on every rank, each rank's part of every window into the send block of the query's home
+    rank, one all_to_all of fixed-size blocks (each rank receives its ~Q/world home queries' rows), the device
+    scatter + merge; no host read inside the K steps (the overflow word is combined and read after them)."""
     import torch
 
-    from opendht_amd.global_shard import GlobalShard, build_plain_shard, global_good_prefix
+    from opendht_amd.global_shard import GlobalShard, build_plain_shard, global_good_prefix, home_range
     from opendht_amd.sharded import build_shard, config3_spec
     from opendht_amd.synth import bucket_firsts
 
@@ -1038,7 +1070,7 @@ def allgather_pass(args, world, rank, local, dev, dist):
     Q, K, cnt_k = args.queries, max(4, min(args.steps, 20)), args.count
     NB = K + 2
     tgs = device_targets(NB, Q, 0, 0, 0x0D470002, dev)  # the same global batches on every rank
-    out_idx = torch.empty((Q, cnt_k), dtype=torch.int32, device=dev)
+    out_idx = torch.empty((Q, cnt_k), dtype=torch.int32, device=dev)  # (home rows first at N > 1)
     out_cnt = torch.empty((Q,), dtype=torch.uint8, device=dev)
     setup = time.perf_counter() - t0
     vrows = min(Q, args.verify_rows)
@@ -1055,7 +1087,7 @@ def allgather_pass(args, world, rank, local, dev, dist):
                     "workload": f"100M-node U(24) table whole on one GPU ({n_local} nodes), {Q} queries per step "
                                 f"(a distinct batch per step), k={cnt_k}: the plain batch",
                     "verified": {"rows": vrows, "mismatches": bad}})
-        # what each rank runs at N > 1 minus the collective: shard kernel + kad_rt_gather_finish, as a graph
+        # what each rank runs at N > 1 minus the collective: shard kernel + kad_rt_home_finish, as a graph
         ex = G.exchange(Q, cnt_k, 1)
         t_sh, kern_sh, how_sh = graph_steps(lambda j: G.step(tgs[j % NB], ex, out_idx, out_cnt), K, 2, dev, None)
         ovf = ex.overflowed()
@@ -1063,45 +1095,71 @@ def allgather_pass(args, world, rank, local, dev, dist):
                              out_cnt[:vrows].cpu().numpy(), cnt_k)
         res["shard_kernel_path"] = {"ms_per_step": t_sh / K * 1e3, "avg_kernel_ms": kern_sh, "launch": how_sh,
                                     "overflow": ovf, "verified": {"rows": vrows, "mismatches": bad_sh},
-                                    "how": "N = 1 through kad_rt_shard_batch + kad_rt_gather_finish (device-only "
+                                    "how": "N = 1 through kad_rt_shard_batch_home + kad_rt_home_finish (device-only "
                                            "step) instead of the plain batch"}
+        # the exchange each rank would receive at N = 2, 4, 8 for this Q and count (layouts only, nothing sent)
+        res["exchange_model"] = exchange_model(Q, cnt_k, dev)
     else:
         ex = G.exchange(Q, cnt_k, world)
-        for _ in range(4):  # capacities: grow until a step fits (every rank reads the same gathered counters)
-            G.step(tgs[K], ex, out_idx, out_cnt)
+        lo, hi = home_range(Q, world, rank)
+        oi, oc = out_idx[:hi - lo], out_cnt[:hi - lo]
+        for _ in range(4):  # capacities: grow until a step fits (the counters combined over the ranks)
+            G.step(tgs[K], ex, oi, oc, rank=rank)
             if not ex.overflowed():
                 break
-            ex = G._ex[(Q, cnt_k, world)] = ex.grown()
+            ex = G._ex[(Q, cnt_k, world, True)] = ex.grown()
         for _ in range(3):
-            t_max, kern_ms, how = graph_steps(lambda j: G.step(tgs[j % NB], ex, out_idx, out_cnt), K, 1, dev, dist,
+            t_max, kern_ms, how = graph_steps(lambda j: G.step(tgs[j % NB], ex, oi, oc, rank=rank), K, 1, dev, dist,
                                               use_graph=False)
             if not ex.overflowed():
                 break
-            ex = G._ex[(Q, cnt_k, world)] = ex.grown()
+            ex = G._ex[(Q, cnt_k, world, True)] = ex.grown()
         else:
             raise RuntimeError("exchange buffers kept overflowing")
-        # verification: the rows of the last step whose targets this rank owns, against the restatement on
-        # this rank's shard WITH its exact halo (owner-routing shard: every owned window lies inside it)
+        # verification: this rank's home rows (queries [lo, hi)) among the first vrows whose targets this rank
+        # owns, against the restatement on this rank's shard WITH its exact halo (every owned window lies inside)
         G.close()
         del ids, st
-        vt = tgs[(K - 1) % NB][:vrows].cpu().numpy()
+        vh = min(hi, vrows) - lo if lo < vrows else 0
+        vt = tgs[(K - 1) % NB][lo:lo + max(vh, 0)].cpu().numpy()
         own = (vt[:, 0].astype(np.int64) >> (8 - spec.shard_bits)) == rank
         sh = build_shard(spec, rank)
         bad = verify_rows(sh.ids, sh.status, sh.first, sh.off, sh.index_base, vt[own],
-                          out_idx[:vrows].cpu().numpy()[own], out_cnt[:vrows].cpu().numpy()[own], cnt_k)
+                          oi[:vt.shape[0]].cpu().numpy()[own], oc[:vt.shape[0]].cpu().numpy()[own], cnt_k)
         res.update({"value": Q * K / t_max, "ms_per_step": t_max / K * 1e3, "avg_step_ms_events": kern_ms,
                     "launch": how,
                     "workload": f"100M-node U(24) table, 1/{world} per GPU without halo ({n_local} nodes on rank 0), "
                                 f"{Q} global queries per step (a distinct batch per step, replicated on every rank), "
-                                f"k={cnt_k}; kad_rt_shard_batch into a fixed-size block, RCCL all_gather_into_tensor of "
-                                "the blocks, kad_rt_gather_finish (scatter + merge on the device)",
+                                f"k={cnt_k}; kad_rt_shard_batch_home into `world` fixed-size blocks (one per home "
+                                "rank), RCCL all_to_all_single of the blocks, kad_rt_home_finish (scatter + merge of "
+                                "the rank's home queries on the device)",
                     "gathered_bytes_per_step": ex.gathered_bytes,
+                    "xgmi_bytes_per_step": ex.xgmi_bytes,
                     "row_cap": ex.row_cap, "part_cap": ex.part_cap,
                     "verified": {"rows": sum_over_ranks(dist, int(own.sum()), dev),
                                  "mismatches": sum_over_ranks(dist, bad, dev)}})
         return res
     G.close()
     return res
+
+
+def exchange_model(Q, count, dev, link_gbs=64.0):
+    """The home exchange's per-rank bytes at N = 2, 4, 8 for a Q-query step (the default layouts, nothing sent),
+    and a modelled all_to_all time: each rank receives world - 1 blocks, each over its own xGMI link, at
+    link_gbs GB/s per link (a conservative one-direction rate for one of the 7 links of an MI355X), plus ~10 us of
+    collective latency. The all-gather layout's bytes beside it."""
+    from opendht_amd.global_shard import Exchange
+
+    out = {"link_GBps_assumed": link_gbs, "latency_us_assumed": 10.0}
+    for n in (2, 4, 8):
+        h = Exchange(Q, count, n, dev, home=True)
+        g = Exchange(Q, count, n, dev, home=False)
+        out[str(n)] = {"home_gathered_bytes": h.gathered_bytes, "home_xgmi_bytes": h.xgmi_bytes,
+                       "home_modelled_us": 10.0 + 4 * h.block / (link_gbs * 1e3),
+                       "allgather_gathered_bytes": g.gathered_bytes,
+                       "allgather_modelled_us": 10.0 + 4 * g.block / (link_gbs * 1e3)}
+        del h, g
+    return out
 
 
 def allgather_child(args, world, rank, local, dist) -> dict:

@@ -214,6 +214,22 @@ int kad_nc_apply(kad_table* t, const uint32_t* erase, uint32_t n_erase, const ui
  * firsts B x 20 and offsets B+1 (sizes from kad_table_get_info). */
 int kad_table_export(const kad_table* t, uint8_t* ids, uint8_t* status, uint8_t* bucket_first,
                      uint32_t* bucket_offset);
+/* A derived array of the table as raw bytes (tests: an incrementally maintained set must equal the one a fresh
+ * table builds from the same status). out == NULL: *bytes = the size (0 if the table has no such set). */
+#define KAD_LINESET_WL 0u     /* 128-byte window lines (count <= 8) */
+#define KAD_LINESET_WS 1u     /* 64-byte short window lines */
+#define KAD_LINESET_WL16 2u
+#define KAD_LINESET_WL32 3u
+#define KAD_LINESET_GL 4u     /* general lines */
+#define KAD_LINESET_GL16 5u
+#define KAD_LINESET_GL32 6u
+#define KAD_LINESET_SL 7u     /* slot lines */
+#define KAD_LINESET_SL16 8u
+#define KAD_LINESET_NCL 9u    /* NodeCache lines */
+#define KAD_LINESET_NCL32 10u
+#define KAD_LINESET_GCNT 11u  /* per-bucket good counts */
+#define KAD_LINESET_DIR 12u   /* bucket directory: first node (bit 31: wide), good mask */
+int kad_table_export_lines(const kad_table* t, uint32_t set, void* out, uint64_t* bytes);
 
 /* ---- queries: RoutingTable::findClosestNodes ---------------------------- */
 /* Batched RoutingTable::findClosestNodes(target, now, count) (routing_table.cpp:67-111)
@@ -362,6 +378,26 @@ int kad_rt_merge_parts(const uint32_t* parts, uint32_t n_parts, uint32_t count, 
 int kad_rt_gather_finish(const uint32_t* recv, uint32_t world, uint32_t row_cap, uint32_t part_cap, uint32_t q,
                          uint32_t count, uint32_t* scratch, uint32_t* out_idx, uint8_t* out_cnt,
                          uint32_t* overflow, int device, void* stream);
+/* The home-rank exchange (the default north-star step; the all-gather above moves every row to every rank).
+ * Query block k (KAD_SHARD_QUERY_BLOCK queries of the replicated batch) has the home rank k * world / nblk:
+ * kad_home_range gives rank r's queries [lo, hi). A rank's rows and parts go only to their query's home rank,
+ * so one all_to_all of fixed-size blocks (RCCL) moves ~q/world rows into each rank instead of q:
+ *   send     device, world blocks of KAD_SHARD_BLOCK_WORDS(count, row_cap, part_cap) words: block d holds what
+ *            goes to rank d (its regions, parts and counters; the counters are zeroed by the call first)
+ *   recv     after all_to_all_single(recv, send) with equal splits: block s = what rank s sent here
+ * kad_rt_home_finish then writes rank `rank`'s rows: out_idx (hi - lo) x count and out_cnt (hi - lo) for qids
+ * lo + i. scratch: (hi - lo) + world*part_cap words, the first (hi - lo) KAD_NO_NODE before the first call (every
+ * call leaves them so). overflow: set to 1 when a block sent here was full; it only sees this rank's blocks, so
+ * callers combine it over the ranks (all_reduce MAX) before deciding to grow and run again. */
+#define KAD_SHARD_QUERY_BLOCK 256u
+void kad_home_range(uint32_t q, uint32_t world, uint32_t rank, uint32_t* lo, uint32_t* hi);
+int kad_rt_shard_batch_home(const kad_table* shard, const uint32_t* global_good_prefix, uint32_t global_buckets,
+                            uint64_t global_base_hi, uint32_t depth, uint32_t shard_first_bucket, uint32_t reach_lo,
+                            uint32_t reach_hi, const uint8_t* targets, uint32_t q, uint32_t count, uint32_t world,
+                            uint32_t* send, uint32_t row_cap, uint32_t part_cap, void* stream);
+int kad_rt_home_finish(const uint32_t* recv, uint32_t world, uint32_t rank, uint32_t row_cap, uint32_t part_cap,
+                       uint32_t q, uint32_t count, uint32_t* scratch, uint32_t* out_idx, uint8_t* out_cnt,
+                       uint32_t* overflow, int device, void* stream);
 
 /* ---- wire step after the query ------------------------ */
 #define KAD_SEND_NODES 8u           /* reference network_engine.cpp:59 SEND_NODES */

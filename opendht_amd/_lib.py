@@ -21,6 +21,9 @@ KAD_STATUS_EXPIRED = 0x02
 KAD_TABLE_SORTED = 0x01
 KAD_TABLE_EAGER = 0x02
 KAD_LINES_RT16, KAD_LINES_RT32, KAD_LINES_NC16, KAD_LINES_NC32, KAD_LINES_ALL = 0x01, 0x02, 0x04, 0x08, 0x0F
+# kad_table_export_lines sets
+(KAD_LINESET_WL, KAD_LINESET_WS, KAD_LINESET_WL16, KAD_LINESET_WL32, KAD_LINESET_GL, KAD_LINESET_GL16, KAD_LINESET_GL32,
+ KAD_LINESET_SL, KAD_LINESET_SL16, KAD_LINESET_NCL, KAD_LINESET_NCL32, KAD_LINESET_GCNT, KAD_LINESET_DIR) = range(13)
 KAD_INFO_WINDOW_LINES = 0x100
 KAD_INFO_GENERAL_LINES = 0x200
 KAD_INFO_GENERAL_LINES32 = 0x400
@@ -84,6 +87,7 @@ SIGNATURES = {
     "kad_table_update_status": (C.c_int, [_P, _P]),
     "kad_table_apply": (C.c_int, [_P, _P, C.c_uint32, _P, _P, C.c_uint32, _P, _P]),
     "kad_table_export": (C.c_int, [_P, _P, _P, _P, _P]),
+    "kad_table_export_lines": (C.c_int, [_P, C.c_uint32, _P, _P]),
     "kad_nc_apply": (C.c_int, [_P, _P, C.c_uint32, _P, _P, C.c_uint32, _P, _P]),
     "kad_table_set_times": (C.c_int, [_P, _P, _P, _P]),
     "kad_table_refresh_status": (C.c_int, [_P, C.c_int64, _P]),
@@ -106,6 +110,11 @@ SIGNATURES = {
     "kad_rt_merge_parts": (C.c_int, [_P, C.c_uint32, C.c_uint32, _P, _P, C.c_int, _P]),
     "kad_rt_gather_finish": (C.c_int, [_P, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, _P, _P, _P,
                                        _P, C.c_int, _P]),
+    "kad_home_range": (None, [C.c_uint32, C.c_uint32, C.c_uint32, _P, _P]),
+    "kad_rt_shard_batch_home": (C.c_int, [_P, _P, C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
+                                          _P, C.c_uint32, C.c_uint32, C.c_uint32, _P, C.c_uint32, C.c_uint32, _P]),
+    "kad_rt_home_finish": (C.c_int, [_P, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, _P,
+                                     _P, _P, _P, C.c_int, _P]),
     "kad_table_set_addrs": (C.c_int, [_P, C.c_uint32, _P]),
     "kad_buffer_nodes_batch": (C.c_int, [_P, _P, C.c_uint32, _P, _P, C.c_uint32, _P, _P, _P]),
     "kad_parse_nodes_batch": (C.c_int, [_P, C.c_uint32, C.c_uint32, _P, _P, C.c_int, _P]),

@@ -2887,16 +2887,10 @@ __device__ void gl_build_line(const uint64_t* key, const uint8_t* status, const 
     I.S = S;
 }
 
-__global__ __launch_bounds__(BLOCK) void gl_build_kernel(const uint64_t* key, const uint8_t* status, const uint2* dir,
-                                                         const uint32_t* gcnt, const uint64_t* fkey, const uint32_t* ftail,
-                                                         uint32_t B, uint32_t* lines, LineSel sel) {
-    __shared__ uint32_t lds[BLOCK][GL_STRIDE + 1];
-    // one item per thread, grid-stride (an incremental rebuild launches a capped grid)
-    for (uint32_t j_ = blockIdx.x * BLOCK + threadIdx.x;; j_ += gridDim.x * BLOCK) {
-        uint32_t b;
-        if (!sel.pick(j_, B, b)) return;
-        [&] {
-    uint32_t* L = lds[threadIdx.x];
+// General line b (count <= 8) assembled in L (an LDS row of GL_STRIDE + 1 dwords) and stored.
+__device__ void gl8_build_line(const uint64_t* key, const uint8_t* status, const uint2* dir, const uint32_t* gcnt,
+                               const uint64_t* fkey, const uint32_t* ftail, uint32_t B, uint32_t* lines, uint32_t b,
+                               uint32_t* L) {
     for (uint32_t k = 0; k < GL_STRIDE; k++) L[k] = NONE;
     GlInfo I;
     gl_build_line<2, 8, GL_SLOTS, GL_HDR>(key, status, dir, gcnt, fkey, ftail, B, b, L, I);
@@ -2908,7 +2902,17 @@ __global__ __launch_bounds__(BLOCK) void gl_build_kernel(const uint64_t* key, co
     L[2] = I.Sr[0] | (I.Sr[1] << 5) | (I.cp << 10);
     L[3] = 0;
     store_line<GL_STRIDE>(L, lines + (size_t)GL_STRIDE * b);
-        }();
+}
+
+__global__ __launch_bounds__(BLOCK) void gl_build_kernel(const uint64_t* key, const uint8_t* status, const uint2* dir,
+                                                         const uint32_t* gcnt, const uint64_t* fkey, const uint32_t* ftail,
+                                                         uint32_t B, uint32_t* lines, LineSel sel) {
+    __shared__ uint32_t lds[BLOCK][GL_STRIDE + 1];
+    // one item per thread, grid-stride (an incremental rebuild launches a capped grid)
+    for (uint32_t j_ = blockIdx.x * BLOCK + threadIdx.x;; j_ += gridDim.x * BLOCK) {
+        uint32_t b;
+        if (!sel.pick(j_, B, b)) return;
+        gl8_build_line(key, status, dir, gcnt, fkey, ftail, B, lines, b, lds[threadIdx.x]);
     }
 }
 
@@ -3364,7 +3368,19 @@ struct ShardCtx {
     uint32_t* ctr;  // counter k at word KAD_SHARD_COUNTER_STRIDE*k (own 128-byte line): [0..7] rows appended
                     // per region, [8] parts appended, [9] overflow flag
     uint32_t row_cap, part_cap, rs, ps;
+    // home-rank exchange (kad_rt_shard_batch_home): rows and parts of query block k go to the send block of rank
+    // home(k) = k * dests / nblk (dest_words apart); dests = 1: one block for every query (the all-gather layout)
+    uint32_t dests, nblk;
+    uint64_t dest_words;
 };
+
+// The rank a query's rows and parts go to: query blocks of BLOCK queries split evenly over the ranks, in order.
+__host__ __device__ __forceinline__ uint32_t home_of_block(uint32_t k, uint32_t dests, uint32_t nblk) {
+    return (uint32_t)(((uint64_t)k * dests) / nblk);
+}
+__device__ __forceinline__ uint64_t dest_off(const ShardCtx& S, uint32_t qid) {
+    return S.dests > 1 ? (uint64_t)home_of_block(qid / BLOCK, S.dests, S.nblk) * S.dest_words : 0ull;
+}
 
 __device__ __forceinline__ uint32_t shard_bucket(const ShardCtx& S, const Target& t) {
     if (t.hi < S.gbase) return 0;
@@ -3389,13 +3405,16 @@ __device__ void wave_shard(const DevTable& T, const ShardCtx& S, const Target& t
     const uint32_t lgood = wave_good_sum(T.gcnt, al, el);
     uint32_t slot = 0;
     const uint32_t region = blockIdx.x & 7u;
-    if (lane == 0) slot = atomicAdd(S.ctr + KAD_SHARD_COUNTER_STRIDE * (complete ? region : 8u), 1u);
+    const uint64_t dof = dest_off(S, qid);
+    uint32_t* ctr = S.ctr + dof;
+    if (lane == 0) slot = atomicAdd(ctr + KAD_SHARD_COUNTER_STRIDE * (complete ? region : 8u), 1u);
     slot = rdl(slot, 0);
     if (slot >= (complete ? S.row_cap : S.part_cap)) {
-        if (lane == 0) atomicOr(S.ctr + KAD_SHARD_COUNTER_STRIDE * 9u, 1u);
+        if (lane == 0) atomicOr(ctr + KAD_SHARD_COUNTER_STRIDE * 9u, 1u);
         return;
     }
-    uint32_t* row = complete ? S.rows + ((size_t)region * S.row_cap + slot) * S.rs : S.parts + (size_t)slot * S.ps;
+    uint32_t* row = complete ? S.rows + dof + ((size_t)region * S.row_cap + slot) * S.rs
+                             : S.parts + dof + (size_t)slot * S.ps;
     if (lane == 0) {
         row[0] = qid;
         row[1] = min(count, lgood);
@@ -3429,22 +3448,24 @@ __global__ __launch_bounds__(BLOCK) void rt_shard_kernel(DevTable T, ShardCtx S,
         const uint32_t w = threadIdx.x >> 6;
         if ((threadIdx.x & 63u) == 0) wcnt[w] = (uint32_t)__builtin_popcountll(want);
         __syncthreads();
+        // the block's queries share one home rank (home_of_block): one atomic per block
+        const uint64_t dof = dest_off(S, blockIdx.x * BLOCK);
         if (threadIdx.x == 0) {
             uint32_t tot = 0;
             for (uint32_t k = 0; k < BLOCK / 64; k++) tot += wcnt[k];
-            wcnt[BLOCK / 64] = tot ? atomicAdd(S.ctr + KAD_SHARD_COUNTER_STRIDE * (blockIdx.x & 7u), tot) : 0u;
+            wcnt[BLOCK / 64] = tot ? atomicAdd(S.ctr + dof + KAD_SHARD_COUNTER_STRIDE * (blockIdx.x & 7u), tot) : 0u;
         }
         __syncthreads();
         uint32_t slot = wcnt[BLOCK / 64] + lanes_below(want);
         for (uint32_t k = 0; k < w; k++) slot += wcnt[k];
         if (ok) {
             if (slot < S.row_cap) {
-                uint32_t* row = S.rows + ((size_t)(blockIdx.x & 7u) * S.row_cap + slot) * S.rs;
+                uint32_t* row = S.rows + dof + ((size_t)(blockIdx.x & 7u) * S.row_cap + slot) * S.rs;
                 reinterpret_cast<uint4*>(row)[0] = make_uint4(i, m, 0u, 0u);
                 store_row8(row + 4, o, count);
                 edge = false;
             } else {
-                atomicOr(S.ctr + KAD_SHARD_COUNTER_STRIDE * 9u, 1u);
+                atomicOr(S.ctr + dof + KAD_SHARD_COUNTER_STRIDE * 9u, 1u);
             }
         }
     }
@@ -3537,6 +3558,7 @@ struct GatherCtx {
     uint64_t block;               // words per rank block
     uint64_t parts_off, ctr_off;  // word offsets of the parts and the counters inside a block
     uint32_t world, row_cap, part_cap, rs, ps, count, q;
+    uint32_t qbase;               // rows of qids [qbase, qbase + q) (the home range; 0 for the all-gather)
 };
 
 __device__ __forceinline__ const uint32_t* gather_ctr(const GatherCtx& G, uint32_t r) {
@@ -3554,7 +3576,7 @@ __global__ void gather_scatter_kernel(GatherCtx G, uint32_t* __restrict__ out_id
     if (rem == 0 && ctr[KAD_SHARD_COUNTER_STRIDE * 9u] && overflow) atomicOr(overflow, 1u);
     if (k >= min(ctr[KAD_SHARD_COUNTER_STRIDE * region], G.row_cap)) return;
     const uint32_t* src = G.recv + (size_t)r * G.block + ((size_t)region * G.row_cap + k) * G.rs;
-    const uint32_t qid = src[0];
+    const uint32_t qid = src[0] - G.qbase;
     if (qid >= G.q) return;
     if (out_cnt) out_cnt[qid] = (uint8_t)src[1];
     uint32_t* dst = out_idx + (size_t)qid * G.count;
@@ -3564,6 +3586,14 @@ __global__ void gather_scatter_kernel(GatherCtx G, uint32_t* __restrict__ out_id
     } else {
         for (uint32_t j = 0; j < G.count; j++) dst[j] = src[4 + j];
     }
+}
+
+// The counters of `n` send blocks (block_words apart, the counters at ctr_off) zeroed before a step.
+__global__ void zero_counters_kernel(uint32_t* send, uint32_t n, uint64_t block_words, uint64_t ctr_off) {
+    const uint32_t j = blockIdx.x * BLOCK + threadIdx.x;
+    const uint32_t words = KAD_SHARD_COUNTERS * KAD_SHARD_COUNTER_STRIDE;
+    if (j >= n * words) return;
+    send[(uint64_t)(j / words) * block_words + ctr_off + j % words] = 0;
 }
 
 // Part x = (rank r, slot p) of the gathered buffer, or NULL if the slot is empty.
@@ -3576,8 +3606,8 @@ __device__ __forceinline__ const uint32_t* gather_part(const GatherCtx& G, uint6
 __global__ void gather_link_kernel(GatherCtx G, uint32_t* __restrict__ head, uint32_t* __restrict__ next) {
     const uint64_t x = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
     const uint32_t* part = gather_part(G, x);
-    if (!part || part[0] >= G.q) return;
-    next[x] = atomicExch(head + part[0], (uint32_t)x);
+    if (!part || part[0] - G.qbase >= G.q) return;
+    next[x] = atomicExch(head + (part[0] - G.qbase), (uint32_t)x);
 }
 
 // The thread of a query's chain head merges its parts (at most one per rank, KAD_SHARD_MAX_WORLD) by
@@ -3587,7 +3617,7 @@ __global__ void gather_merge_kernel(GatherCtx G, uint32_t* __restrict__ head, co
     const uint64_t x = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
     const uint32_t* part = gather_part(G, x);
     if (!part) return;
-    const uint32_t qid = part[0];
+    const uint32_t qid = part[0] - G.qbase;
     if (qid >= G.q || head[qid] != (uint32_t)x) return;
     constexpr uint32_t MAXSEG = KAD_SHARD_MAX_WORLD;
     const uint32_t* seg[MAXSEG];
@@ -5207,7 +5237,13 @@ struct RfCtx {
     uint32_t* ctr;                       // RF_CTRS words
     uint32_t* list[4];                   // lines of the count <= 8, 9..16, 17..32 sets and NodeCache slots (NULL: none)
     uint32_t nback, nfwd;                // NodeCache windows, as StatusMarks
+    uint32_t* wl;                        // fused count <= 8 builds (rf_nodes_kernel FUSE): the line sets written
+    uint32_t* ws;
+    uint32_t* gl;
+    uint32_t ninl;                       // > 0: the nodes are inl[0, ninl) (the host's copies of the runs), no lists
+    uint32_t inl[16];
 };
+constexpr uint32_t RF_INLINE = 16;
 
 // One atomic per wave for the lanes with `want` (wave-uniform call); returns each wanting lane's slot.
 __device__ __forceinline__ uint32_t wave_append(uint32_t* ctr, bool want) {
@@ -5222,9 +5258,13 @@ __device__ __forceinline__ uint32_t wave_append(uint32_t* ctr, bool want) {
 
 // The bucket holding node i: the locate of its own ID (findBucket), checked against the directory; a table
 // whose node lies outside its bucket's range falls back to the search over the bucket starts.
-__device__ uint32_t node_bucket(const DevTable& T, const uint2* dir, uint32_t i) {
+__device__ uint32_t node_bucket(const DevTable& T, const uint2* dir, uint32_t i, uint64_t key_i) {
     Target t;
-    t.hi = T.key[i];
+    t.hi = key_i;
+    if (T.flags & TF_WL) {  // window-line tables: every node lies in its bucket's dyadic range (checked at creation)
+        t.t2 = t.t3 = t.t4 = 0;
+        return locate_bucket(T, t);
+    }
     const uint32_t* tl = T.tail + 3ull * i;
     t.t2 = tl[0]; t.t3 = tl[1]; t.t4 = tl[2];
     const uint32_t b = locate_bucket(T, t);
@@ -5293,27 +5333,255 @@ __device__ uint32_t block_union(uint32_t m, IV iv, uint32_t* out, uint32_t* lds4
     return written;
 }
 
+// ---------------------------------------------------------------------------------------
+// Window line b and its short copy built by a whole wave (the small refresh's few lines: one lane building
+// a line serially waits on hundreds of dependent LDS and memory accesses, ~20 us). Bit for bit the lines
+// of wl_build_line + ws_build_line, for windows W(2) = [b-3, b+2] of at most 64 nodes: lane l holds node
+// n0 + l (key and status staged by the caller in the wave's registers), the bucket good counts are ballots
+// over the status bytes, each stored good node finds its slot from the D ranks of the buckets and its rank
+// in its bucket, and the key collisions the serial build resolves in processing order (D rank, node,
+// earlier node) are found lane against lane in LDS:
+//   pairs >= 2 or a pair equal in all 64 bits -> defer; the first pair (in that order) whose keys differ
+//   -> the tie word. The short line's 23-bit slot fields are OR-ed into LDS words.
+// ---------------------------------------------------------------------------------------
+struct WaveLds {
+    uint64_t key[64];
+    uint32_t pk[64];   // per lane: stored bit 31 | D rank << 24 | key21
+    uint32_t L[32];    // the 128-byte line
+    uint32_t S16[16];  // the short line
+    uint32_t dx[8];    // first nodes of the staged buckets
+    uint32_t R[33 + 17];  // rows of the serial fallback (a window of more than 64 nodes)
+};
+
+__device__ void wl_ws_build_wave(uint32_t b, uint32_t B, uint32_t d, uint64_t pre0, uint32_t db, const uint32_t* dx,
+                                 uint32_t n0, uint32_t n1, uint64_t key, uint32_t stat, uint32_t* wl_out,
+                                 uint32_t* ws_out, WaveLds& W) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t below = (1ull << lane) - 1ull;
+    const uint32_t n = n0 + lane;
+    const bool have = n < n1;
+    const uint32_t e = min(B, b + 3);  // buckets [db, e) staged; dx[i] = first node of bucket db + i (i <= e - db)
+    uint32_t x = NONE;
+    if (have)
+        for (uint32_t i = 0; db + i < e; i++)
+            if (dx[i] <= n) x = db + i;
+    const bool good = have && (stat & KAD_STATUS_GOOD);
+    // good nodes per staged bucket (as gcnt / the masks: the same status bytes)
+    uint32_t cnt[7];
+#pragma unroll
+    for (uint32_t i = 0; i < 7; i++)
+        cnt[i] = db + i < e ? (uint32_t)__builtin_popcountll(__ballot(good && x == db + i)) : 0u;
+    auto cnt_of = [&](uint32_t y) {  // y in [db, e)
+        uint32_t c = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < 7; i++) c = (db + i == y) ? cnt[i] : c;
+        return c;
+    };
+    for (uint32_t k = lane; k < 32; k += 64) W.L[k] = NONE;
+    uint32_t h = 0, R8 = 3, g = 0;
+    for (uint32_t r = 0; r < 3; r++) {
+        const uint32_t lo = b > r ? b - 1 - r : 0u, hi = min(B - 1, b + r);
+        g += r == 0 ? cnt_of(b) + (b ? cnt_of(b - 1) : 0u)
+                    : (b > r ? cnt_of(b - 1 - r) : 0u) + ((uint64_t)b + r < (uint64_t)B ? cnt_of(b + r) : 0u);
+        const bool whole = lo == 0 && hi == B - 1;
+        h |= (min(g, 63u) << (6 * r)) | ((whole ? 1u : 0u) << (18 + r));
+        if (R8 == 3 && (g >= 8 || whole)) R8 = r;
+    }
+    uint32_t S = 0, rounds = 0, tie = 0, base = NONE;
+    bool defer = false;
+    if (R8 == 3) {
+        if (lane == 0) { W.L[1] = WL_DEFER; W.L[3] = 0; }
+    } else {
+        const uint32_t lo = b > R8 ? b - 1 - R8 : 0u, hi = min(B - 1, b + R8), nb = hi - lo + 1;
+        base = dx[lo - db];
+        // D rank of every window bucket, the stored prefix (whole buckets in D order while they fit)
+        uint32_t rank_of[6], start_of[6];
+        bool stored_of[6];
+        bool full = false;
+        for (uint32_t j = 0; j < nb; j++) {
+            uint32_t xj = lo;
+            for (uint32_t y = lo; y <= hi; y++) {
+                uint32_t rk = 0;
+                for (uint32_t z = lo; z <= hi; z++) rk += ((pre0 + z) ^ (pre0 + b)) < ((pre0 + y) ^ (pre0 + b));
+                if (rk == j) xj = y;
+            }
+            rounds |= (xj >= b ? xj - b : b - 1 - xj) << (2 * j);
+            const uint32_t gj = cnt_of(xj);
+            rank_of[xj - lo] = j;
+            stored_of[xj - lo] = false;
+            start_of[xj - lo] = 0;
+            if (full || S + gj > WL_SLOTS) { full = true; continue; }
+            stored_of[xj - lo] = true;
+            start_of[xj - lo] = S;
+            S += gj;
+        }
+        // my slot
+        const bool inw = good && x >= lo && x <= hi;
+        uint32_t rj = 0, st0 = 0;
+        bool sto = false;
+        for (uint32_t i = 0; i < nb; i++)
+            if (inw && x == lo + i) { rj = rank_of[i]; st0 = start_of[i]; sto = stored_of[i]; }
+        const bool mine = inw && sto;
+        const uint32_t k21 = (uint32_t)((key << d) >> (64 - WL_KBITS)), off = n - base;
+        uint32_t inb = 0;  // stored good nodes of my bucket below me (index order)
+        for (uint32_t i = 0; i < nb; i++) {
+            const uint64_t m = __ballot(mine && x == lo + i);
+            if (mine && x == lo + i) inb = (uint32_t)__builtin_popcountll(m & below);
+        }
+        defer = __any(mine && off > 255u);
+        W.pk[lane] = mine ? (0x80000000u | (rj << 24) | k21) : 0u;
+        W.key[lane] = key;
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        // pairs: earlier stored nodes of my bucket (lower lanes, same D rank) with my key21
+        uint32_t pairs = 0, my_tie = 0;
+        bool zero = false, have_tie = false;
+        if (mine) {
+            for (uint32_t l2 = 0; l2 < lane; l2++) {
+                const uint32_t v = W.pk[l2];
+                if (v != (0x80000000u | (rj << 24) | k21)) continue;
+                pairs++;
+                const uint64_t x64 = key ^ W.key[l2];
+                if (x64 == 0) { zero = true; continue; }
+                if (!have_tie) {
+                    const uint32_t p = (uint32_t)__builtin_clzll(x64), bn = (uint32_t)(key >> (63 - p)) & 1u;
+                    my_tie = WL_DEFER | (bn << 30) | (p << 16) | (((n0 + l2 - base) & 255u) << 8) | (off & 255u);
+                    have_tie = true;
+                }
+            }
+        }
+        uint32_t tp = pairs;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) tp += __shfl_xor(tp, o, 64);
+        defer = defer || tp >= 2 || __any(zero);
+        // the tie of the first pair in processing order (D rank, then node index)
+        const uint32_t keyt = have_tie ? (rj << 8) | lane : NONE;
+        uint32_t mk = keyt;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) mk = min(mk, (uint32_t)__shfl_xor(mk, o, 64));
+        if (mk != NONE) tie = rdl(my_tie, mk & 255u);
+        if (mine) W.L[WL_SLOT0 + st0 + inb] = (rj << 29) | (k21 << 8) | (off & 255u);
+        if (lane == 0) {
+            W.L[0] = base;
+            W.L[2] = rounds;
+            W.L[3] = tie;
+        }
+    }
+    if (lane == 0 && R8 != 3) W.L[1] = h | (R8 << 21) | (S << 23) | (defer ? WL_DEFER : 0u);
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    if (lane < 8) reinterpret_cast<uint4*>(wl_out + 32ull * b)[lane] =
+        make_uint4(W.L[4 * lane], W.L[4 * lane + 1], W.L[4 * lane + 2], W.L[4 * lane + 3]);
+    if (!ws_out) return;
+    // the short line (ws_build_line over W.L)
+    const uint32_t hh = W.L[1], rnd = W.L[2], SS = (hh >> 23) & 31u;
+    bool fb = (hh & WL_DEFER) != 0;
+    const uint32_t vs = lane < SS ? W.L[WL_SLOT0 + lane] : 0u;
+    const bool endb = lane < SS && lane < WS_SLOTS && (lane + 1 == SS || (W.L[WL_SLOT0 + lane + 1] >> 29) != (vs >> 29));
+    uint32_t keep = endb ? lane + 1 : 0u;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) keep = max(keep, (uint32_t)__shfl_xor(keep, o, 64));
+    constexpr uint32_t KSH = 8 + WL_KBITS - WS_KBITS;
+    const bool ks = lane < keep;
+    const uint32_t jj = vs >> 29, k16 = (vs >> KSH) & 0xFFFFu, offs = vs & 255u;
+    bool f = ks && offs >= 64u;
+    if (ks)
+        for (uint32_t r = 0; r < lane; r++) {
+            const uint32_t u = W.L[WL_SLOT0 + r];
+            f |= (u >> 29) == jj && ((u >> KSH) & 0xFFFFu) == k16;
+        }
+    fb = fb || __any(f);
+    const bool start = ks && (lane == 0 || (W.L[WL_SLOT0 + lane - 1] >> 29) != jj);
+    const uint64_t sm = __ballot(start);
+    uint32_t rk = start ? ((rnd >> (2 * jj)) & 3u) << (2 * (uint32_t)__builtin_popcountll(sm & below)) : 0u;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) rk |= __shfl_xor(rk, o, 64);
+    if (lane < 16) W.S16[lane] = 0;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    if (ks) {  // the slot's 23 bits at bit WS_SLOT0 + 23 * lane
+        const uint32_t v = (start ? 1u << 22 : 0u) | (k16 << 6) | offs, p = WS_SLOT0 + WS_SBITS * lane;
+        const uint64_t w = (uint64_t)v << (p & 31);
+        atomicOr(&W.S16[p >> 5], (uint32_t)w);
+        if ((p & 31) + WS_SBITS > 32) atomicOr(&W.S16[(p >> 5) + 1], (uint32_t)(w >> 32));
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    if (lane < 16) {
+        const uint32_t G0 = min(hh & 63u, 15u), G1 = min((hh >> 6) & 63u, 15u), G2 = min((hh >> 12) & 63u, 15u);
+        const uint32_t hw = G0 | (G1 << 4) | (G2 << 8) | (((hh >> 18) & 7u) << 12) | (((hh >> 21) & 3u) << 15) |
+                            (keep << 17) | ((fb ? 1u : 0u) << 22);
+        // bits [0, 32) base, [32, 55) hw, [55, 67) rk, slots from 67, ones from the first unused slot on
+        const uint64_t hdr = (uint64_t)hw | ((uint64_t)rk << 23);  // bits 32 .. 66
+        uint32_t v = W.S16[lane];
+        if (lane == 0) v = W.L[0];
+        if (lane == 1) v |= (uint32_t)hdr;
+        if (lane == 2) v |= (uint32_t)(hdr >> 32);
+        const uint32_t u0 = WS_SLOT0 + WS_SBITS * keep, lo_bit = 32 * lane;  // ones from bit u0
+        if (lo_bit + 32 <= u0) {
+        } else if (lo_bit >= u0) {
+            v = NONE;
+        } else {
+            v |= NONE << (u0 - lo_bit);
+        }
+        W.S16[lane] = v;
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    if (lane < 4) reinterpret_cast<uint4*>(ws_out + 16ull * b)[lane] =
+        make_uint4(W.S16[4 * lane], W.S16[4 * lane + 1], W.S16[4 * lane + 2], W.S16[4 * lane + 3]);
+}
+
+// SINGLE: one block (at most BLOCK listed nodes): the appends go to LDS and there is no completion counter.
+// FUSE: the count <= 8 lines of the changed buckets are rebuilt by this block too (1: window lines and their
+// short copies, 2: general lines; the host fuses when at most RF_FUSE_LINES can be listed), so a refresh
+// that passes a few deadlines is one launch.
+constexpr uint32_t RF_FUSE_LINES = 64;
+
+// p - n as a generic (flat) pointer: p[n + i] is then p[i] for the callee, whatever the address space of p.
+template <class T>
+__device__ __forceinline__ const T* flat_shift(const T* p, uint32_t n) {
+    return reinterpret_cast<const T*>(reinterpret_cast<uintptr_t>(static_cast<const void*>(p)) - (uintptr_t)n * sizeof(T));
+}
+constexpr uint32_t RF_POOL = BLOCK * (33 + 17);  // dwords: phase 2's sort buffers, then phase 3's line rows
+
+template <bool SINGLE, int FUSE>
 __global__ __launch_bounds__(BLOCK) void rf_nodes_kernel(RfCtx C) {
     const DevTable& T = C.T;
-    const uint32_t total = C.mc + C.sc + C.np;
+    __shared__ __attribute__((aligned(16))) uint32_t pool[RF_POOL];
+    __shared__ uint32_t lctr[2];
+    uint64_t* srt = reinterpret_cast<uint64_t*>(pool);  // RF_CAP (phase 2)
+    uint32_t* ub = pool + 2 * RF_CAP;                     // RF_CAP (phase 2)
+    uint32_t* lb_ = SINGLE ? pool + 3 * RF_CAP : nullptr; // BLOCK appended buckets (phase 1, single block)
+    uint32_t* lr_ = SINGLE ? pool + 3 * RF_CAP + BLOCK : nullptr;  // 2 x BLOCK NodeCache ranges
+    static_assert(3 * RF_CAP + 3 * BLOCK <= RF_POOL, "pool");
+    if (SINGLE && threadIdx.x < 2) lctr[threadIdx.x] = 0;
+    if (SINGLE) __syncthreads();
+    const uint32_t total = C.ninl ? C.ninl : C.mc + C.sc + C.np;
     for (uint32_t base = blockIdx.x * BLOCK; base < total; base += gridDim.x * BLOCK) {  // block-uniform
         const uint32_t j = base + threadIdx.x;
         bool act = j < total;
         uint32_t i = 0, st = 0, old = 0;
         if (act) {
-            i = j < C.mc ? C.mnode[j] : j < C.mc + C.sc ? C.snode[j - C.mc] : C.pend[j - C.mc - C.sc];
+            i = C.ninl ? C.inl[j] : j < C.mc ? C.mnode[j] : j < C.mc + C.sc ? C.snode[j - C.mc] : C.pend[j - C.mc - C.sc];
             act = i < T.n;
         }
+        uint64_t key_i = 0;
         if (act) {
-            st = (C.vals && j >= C.mc + C.sc) ? (uint32_t)(C.vals[j - C.mc - C.sc] & (KAD_STATUS_GOOD | KAD_STATUS_EXPIRED))
-                                               : status_at(C.N, i, C.now);
+            if (T.B) key_i = T.key[i];  // issued with the times: the locate needs it only if the good bit flips
+            st = (!C.ninl && C.vals && j >= C.mc + C.sc)
+                     ? (uint32_t)(C.vals[j - C.mc - C.sc] & (KAD_STATUS_GOOD | KAD_STATUS_EXPIRED))
+                     : status_at(C.N, i, C.now);
             old = C.status[i];
             if (st != old) C.status[i] = (uint8_t)st;
         }
         const bool gchg = act && T.B && ((st ^ old) & KAD_STATUS_GOOD);
-        const uint32_t b = gchg ? node_bucket(T, C.dir, i) : 0u;
-        const uint32_t ob = wave_append(C.ctr + RF_NB, gchg);
-        if (gchg && ob < RF_CAP) C.blist[ob] = b;
+        const uint32_t b = gchg ? node_bucket(T, C.dir, i, key_i) : 0u;
         const bool echg = act && C.list[3] && ((st ^ old) & KAD_STATUS_EXPIRED);
         uint32_t sa = 0, se = 0;
         if (echg) {  // every NodeCache slot from that of node i - nback to that of node i + nfwd (as mark_status_change)
@@ -5322,27 +5590,66 @@ __global__ __launch_bounds__(BLOCK) void rf_nodes_kernel(RfCtx C) {
             sa = ka < T.nbase ? 0u : (uint32_t)min<uint64_t>((ka - T.nbase) >> T.nshift, T.nslots - 1);
             se = ke < T.nbase ? 0u : (uint32_t)min<uint64_t>((ke - T.nbase) >> T.nshift, T.nslots - 1);
         }
-        const uint32_t orr = wave_append(C.ctr + RF_NR, echg);
-        if (echg && orr < RF_CAP) { C.nrange[2 * orr] = sa; C.nrange[2 * orr + 1] = se; }
+        if (SINGLE) {  // LDS appends (total <= BLOCK)
+            if (gchg) lb_[atomicAdd(&lctr[0], 1u)] = b;
+            if (echg) { const uint32_t o = atomicAdd(&lctr[1], 1u); lr_[2 * o] = sa; lr_[2 * o + 1] = se; }
+        } else {
+            const uint32_t ob = wave_append(C.ctr + RF_NB, gchg);
+            if (gchg && ob < RF_CAP) C.blist[ob] = b;
+            const uint32_t orr = wave_append(C.ctr + RF_NR, echg);
+            if (echg && orr < RF_CAP) { C.nrange[2 * orr] = sa; C.nrange[2 * orr + 1] = se; }
+        }
     }
-    // the last block to finish takes phase 2 (every other block's appends are visible after the acquire)
-    __shared__ uint32_t last;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    __syncthreads();
-    if (threadIdx.x == 0) last = atomicAdd(C.ctr + RF_DONE, 1u) == gridDim.x - 1;
-    __syncthreads();
-    if (!last) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    __shared__ uint64_t srt[RF_CAP];
-    __shared__ uint32_t ub[RF_CAP];
+    uint32_t nb, nr;
+    const uint32_t* blist;
+    const uint32_t* nrange;
+    if (SINGLE) {
+        __syncthreads();
+        nb = lctr[0];
+        nr = lctr[1];
+        blist = lb_;
+        nrange = lr_;
+    } else {
+        // the last block to finish takes phase 2 (every other block's appends are visible after the acquire)
+        __shared__ uint32_t last;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        __syncthreads();
+        if (threadIdx.x == 0) last = atomicAdd(C.ctr + RF_DONE, 1u) == gridDim.x - 1;
+        __syncthreads();
+        if (!last) return;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        nb = min(__hip_atomic_load(C.ctr + RF_NB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), RF_CAP);
+        nr = min(__hip_atomic_load(C.ctr + RF_NR, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), RF_CAP);
+        blist = C.blist;
+        nrange = C.nrange;
+    }
     __shared__ uint32_t lds4[4];
-    __shared__ uint32_t nu_s;
-    const uint32_t nb = min(__hip_atomic_load(C.ctr + RF_NB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), RF_CAP);
-    const uint32_t nr = min(__hip_atomic_load(C.ctr + RF_NR, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), RF_CAP);
+    __shared__ uint32_t l8[FUSE ? RF_FUSE_LINES : 1];
+    __shared__ uint32_t n8_s;
+    // NodeCache ranges first (sorted in the same buffer as the buckets next)
+    uint32_t nrs = 0;
+    uint64_t* rsrt = srt;
+    if (C.list[3]) {  // block-uniform
+        uint32_t P = 1;
+        while (P < nr) P <<= 1;
+        __syncthreads();
+        for (uint32_t x = threadIdx.x; x < P; x += BLOCK)  // (single mode: the appends lie above the sort buffer)
+            rsrt[x] = x < nr ? ((uint64_t)nrange[2 * x] << 32) | nrange[2 * x + 1] : ~0ull;
+        __syncthreads();
+        block_sort_u64(rsrt, P);
+        const uint32_t n = block_union(nr, [&](uint32_t u, uint32_t& a, uint32_t& e) {
+            a = (uint32_t)(rsrt[u] >> 32);
+            e = (uint32_t)rsrt[u];
+        }, C.list[3], lds4);
+        if (threadIdx.x == 0) C.ctr[RF_LNC] = n;
+        nrs = n;
+    }
+    (void)nrs;
     // buckets: sort, unique
     uint32_t P = 1;
     while (P < nb) P <<= 1;
-    for (uint32_t x = threadIdx.x; x < P; x += BLOCK) srt[x] = x < nb ? C.blist[x] : ~0ull;
+    __syncthreads();
+    for (uint32_t x = threadIdx.x; x < P; x += BLOCK) srt[x] = x < nb ? (uint64_t)blist[x] : ~0ull;
     __syncthreads();
     block_sort_u64(srt, P);
     uint32_t nu = 0;
@@ -5368,39 +5675,108 @@ __global__ __launch_bounds__(BLOCK) void rf_nodes_kernel(RfCtx C) {
         C.gcnt[b] = g;
         C.dir[b].y = (j1 - j0 <= 32) ? mask : 0u;
     }
-    // per line set: the union of the windows that can read a changed bucket
+    // per line set: the union of the windows that can read a changed bucket (the count <= 8 set into LDS when fused)
     const uint32_t B = T.B;
     const uint32_t below[3] = {2, 3, 7}, above[3] = {3, 4, 8};
     for (int k = 0; k < 3; k++) {
-        if (!C.list[k]) continue;  // block-uniform
+        if (!C.list[k] && !(FUSE && k == 0)) continue;  // block-uniform
         const uint32_t lb = below[k], la = above[k];
         const uint32_t n = block_union(nu, [&](uint32_t u, uint32_t& a, uint32_t& e) {
             const uint32_t b = ub[u];
             a = b > lb ? b - lb : 0u;
             e = min(B - 1, b + la);
-        }, C.list[k], lds4);
-        if (threadIdx.x == 0) C.ctr[RF_L8 + k] = n;
+        }, (FUSE && k == 0) ? l8 : C.list[k], lds4);
+        if (threadIdx.x == 0) {
+            if (FUSE && k == 0) n8_s = n; else C.ctr[RF_L8 + k] = n;
+        }
     }
-    // NodeCache slots: the union of the ranges, sorted by first slot
-    if (C.list[3]) {
-        __syncthreads();
-        P = 1;
-        while (P < nr) P <<= 1;
-        for (uint32_t x = threadIdx.x; x < P; x += BLOCK)
-            srt[x] = x < nr ? ((uint64_t)C.nrange[2 * x] << 32) | C.nrange[2 * x + 1] : ~0ull;
-        __syncthreads();
-        block_sort_u64(srt, P);
-        const uint32_t n = block_union(nr, [&](uint32_t u, uint32_t& a, uint32_t& e) {
-            a = (uint32_t)(srt[u] >> 32);
-            e = (uint32_t)srt[u];
-        }, C.list[3], lds4);
-        if (threadIdx.x == 0) C.ctr[RF_LNC] = n;
-    }
-    (void)nu_s;
-    if (threadIdx.x == 0) {  // the next refresh starts from empty appends
+    if (!SINGLE && threadIdx.x == 0) {  // the next refresh starts from empty appends
         C.ctr[RF_NB] = 0;
         C.ctr[RF_NR] = 0;
         C.ctr[RF_DONE] = 0;
+    }
+    if (FUSE == 1) {
+        // phase 3: the count <= 8 window lines of the list and their short copies, one wave per line
+        // (wl_ws_build_wave) from W(2)'s nodes loaded in one round; a window of more than 64 nodes is built by
+        // the wave's first lane (wl_build_line, ws_build_line)
+        static_assert(4 * sizeof(WaveLds) <= 4 * RF_POOL, "phase 3 wave buffers");
+        WaveLds& WV = reinterpret_cast<WaveLds*>(pool)[threadIdx.x >> 6];
+        const uint32_t lane = threadIdx.x & 63u;
+        __syncthreads();
+        const uint32_t n8 = n8_s;
+        for (uint32_t x = threadIdx.x >> 6; x < n8; x += BLOCK / 64) {  // wave-uniform
+            const uint32_t b = l8[x], db = b >= 3 ? b - 3 : 0u, e = min(B, b + 3);
+            if (db + lane <= e && lane < 8) WV.dx[lane] = C.dir[db + lane].x & ~WIDE;
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+            __builtin_amdgcn_wave_barrier();
+            const uint32_t n0 = WV.dx[0], n1 = WV.dx[e - db];
+            if (n1 - n0 <= 64) {
+                const bool have = n0 + lane < n1;
+                const uint64_t kk = have ? T.key[n0 + lane] : 0ull;
+                const uint32_t sv = have ? C.status[n0 + lane] : 0u;
+                wl_ws_build_wave(b, B, 64 - T.rshift, T.rbase >> T.rshift, db, WV.dx, n0, n1, kk, sv, C.wl, C.ws, WV);
+            } else if (lane == 0) {
+                wl_build_line(T.key, C.status, C.dir, C.gcnt, B, 64 - T.rshift, T.rbase >> T.rshift, C.wl, b, WV.R);
+                if (C.ws) ws_build_line(WV.R, C.ws, b, WV.R + 33);
+            }
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+    if (FUSE == 2) {
+        // phase 3: the count <= 8 general lines of the list, RF_GROUP lanes per line (the pool's sort buffers are free now).
+        // A line reads only W(2) = [b-3, b+2] (its bucket counts, directory entries up to b+3 and their nodes),
+        // which the group stages in LDS in two rounds of parallel loads; its first lane then builds the line from
+        // there (a window larger than RF_WCAP nodes is read from HBM). A line built straight from HBM waits
+        // for ~10 dependent loads (one per bucket of its window, and the keys eight at a time).
+        constexpr uint32_t RF_GROUP = 16, NG = BLOCK / RF_GROUP, RF_WCAP = 128;
+        static_assert(NG * (2 * RF_WCAP + RF_WCAP / 4 + 16 + 8 + 33 + 17) <= RF_POOL, "phase 3 staging");
+        uint64_t* skey = reinterpret_cast<uint64_t*>(pool);                        // NG x RF_WCAP keys
+        uint8_t* sst = reinterpret_cast<uint8_t*>(pool + NG * 2 * RF_WCAP);        // NG x RF_WCAP status bytes
+        uint2* sdir = reinterpret_cast<uint2*>(pool + NG * (2 * RF_WCAP + RF_WCAP / 4));  // NG x 8
+        uint32_t* sgc = pool + NG * (2 * RF_WCAP + RF_WCAP / 4 + 16);               // NG x 8
+        uint32_t* rows = sgc + NG * 8;                                              // NG x (33 + 17)
+        const uint32_t g = threadIdx.x / RF_GROUP, gl = threadIdx.x % RF_GROUP;
+        __syncthreads();
+        const uint32_t n8 = n8_s;
+        for (uint32_t x0 = 0; x0 < n8; x0 += NG) {  // block-uniform
+            const uint32_t x = x0 + g;
+            const bool act = x < n8;
+            const uint32_t b = act ? l8[x] : 0u, db = b >= 3 ? b - 3 : 0u;
+            // round 1: the counts of [db, db + 6) and the directory entries [db, db + 7)
+            if (act && gl < 6 && db + gl < B) sgc[8 * g + gl] = C.gcnt[db + gl];
+            if (act && gl >= 6 && gl < 13 && db + gl - 6 <= B) sdir[8 * g + gl - 6] = C.dir[db + gl - 6];
+            __syncthreads();
+            // round 2: the keys and status bytes of the nodes of buckets [db, min(B - 1, b + 2)]
+            const uint32_t e = min(B, b + 3);
+            const uint32_t n0 = sdir[8 * g].x & ~WIDE, n1 = sdir[8 * g + (e - db)].x & ~WIDE;
+            const bool staged = act && n1 - n0 <= RF_WCAP;
+            if (staged) {
+#pragma unroll
+                for (uint32_t k = 0; k < RF_WCAP / RF_GROUP; k++) {
+                    const uint32_t o = gl + RF_GROUP * k;
+                    if (o < n1 - n0) {
+                        skey[RF_WCAP * g + o] = T.key[n0 + o];
+                        sst[RF_WCAP * g + o] = C.status[n0 + o];
+                    }
+                }
+            }
+            __syncthreads();
+            if (act && gl == 0) {
+                // the staged copies as views indexed like the arrays (every index the build uses lies in W(2)):
+                // the shift is applied to the generic address (an LDS-space pointer shifted below its base would
+                // wrap in 32 bits and leave the LDS aperture once converted)
+                const uint64_t* kp = staged ? flat_shift(skey + RF_WCAP * g, n0) : T.key;
+                const uint8_t* sp = staged ? flat_shift(sst + RF_WCAP * g, n0) : C.status;
+                const uint2* dp = flat_shift(sdir + 8 * g, db);
+                const uint32_t* gp = flat_shift(sgc + 8 * g, db);
+                uint32_t* rowA = rows + 50 * g;
+                gl8_build_line(kp, sp, dp, gp, T.fkey, T.ftail, B, C.gl, b, rowA);
+            }
+            __syncthreads();
+        }
     }
 }
 
@@ -5884,7 +6260,8 @@ struct Deadlines {
     uint64_t* km = nullptr;        // main run: keys and nodes, n entries (device)
     uint32_t* kn = nullptr;
     uint32_t nm = 0, mcap = 0;
-    std::vector<uint64_t> hkm;     // the main run's keys (host copy)
+    std::vector<uint64_t> hkm;     // the main run's keys and nodes (host copies)
+    std::vector<uint32_t> hkn;
     uint32_t cm = 0, cs = 0;       // cursors: the first unpassed entry of each run
     uint64_t* ks = nullptr;        // side run: deadlines of patched nodes (device), kept sorted on the host
     uint32_t* sn = nullptr;
@@ -6414,8 +6791,9 @@ int rf_ready(kad_table* t) {
 // nodes' new status bytes instead of their times) and rebuild only what they change: rf_nodes_kernel, then the
 // line builders over its lists. ensure_marks must have run (the lists live in dlist). Async on s.
 int small_refresh(kad_table* t, hipStream_t s, const uint32_t* mnode, uint32_t mc, const uint32_t* snode, uint32_t sc,
-                  const uint32_t* pend, uint32_t np, const uint8_t* vals, int64_t now) {
-    const uint32_t total = mc + sc + np;
+                  const uint32_t* pend, uint32_t np, const uint8_t* vals, int64_t now, const uint32_t* inl = nullptr,
+                  uint32_t ninl = 0) {
+    const uint32_t total = ninl ? ninl : mc + sc + np;
     if (total == 0) return KAD_OK;
     int rc;
     if ((rc = rf_ready(t))) return rc;
@@ -6442,7 +6820,27 @@ int small_refresh(kad_table* t, hipStream_t s, const uint32_t* mnode, uint32_t m
     C.list[3] = t->ncl_mut ? t->dlist + 3ull * B : nullptr;
     C.nback = t->ncl32_mut ? NC32_SLOTS - NC32_LEFT : NCL_SLOTS - NCL_LEFT;
     C.nfwd = t->ncl32_mut ? NC32_LEFT : NCL_LEFT;
-    hipLaunchKernelGGL(rf_nodes_kernel, dim3(std::min<uint32_t>((total + BLOCK - 1) / BLOCK, 64u)), dim3(BLOCK), 0, s, C);
+    if (ninl) {  // the node ids as kernel arguments (host copies of the runs): no list load before the times
+        C.ninl = std::min(ninl, RF_INLINE);
+        std::memcpy(C.inl, inl, 4ull * C.ninl);
+    }
+    // one block when it holds every listed node; the count <= 8 lines built by it when at most RF_FUSE_LINES can
+    // be listed (6 per changed bucket) and no slot lines depend on them
+    const bool single = total <= BLOCK;
+    const int fuse = (!B || 6ull * total > RF_FUSE_LINES || t->sl_mut) ? 0 : t->wl_mut ? 1 : t->gl_mut ? 2 : 0;
+    if (fuse) {
+        C.list[0] = nullptr;
+        C.wl = t->wl_mut;
+        C.ws = t->ws_mut;
+        C.gl = t->gl_mut;
+    }
+    const dim3 g1(std::min<uint32_t>((total + BLOCK - 1) / BLOCK, 64u));
+    if (single && fuse == 1) hipLaunchKernelGGL((rf_nodes_kernel<true, 1>), g1, dim3(BLOCK), 0, s, C);
+    else if (single && fuse == 2) hipLaunchKernelGGL((rf_nodes_kernel<true, 2>), g1, dim3(BLOCK), 0, s, C);
+    else if (single) hipLaunchKernelGGL((rf_nodes_kernel<true, 0>), g1, dim3(BLOCK), 0, s, C);
+    else if (fuse == 1) hipLaunchKernelGGL((rf_nodes_kernel<false, 1>), g1, dim3(BLOCK), 0, s, C);
+    else if (fuse == 2) hipLaunchKernelGGL((rf_nodes_kernel<false, 2>), g1, dim3(BLOCK), 0, s, C);
+    else hipLaunchKernelGGL((rf_nodes_kernel<false, 0>), g1, dim3(BLOCK), 0, s, C);
     HIP_TRY(hipGetLastError());
     // the builders over the lists; grids from the host's bound on each list
     auto grid = [&](uint64_t items) { return dim3((uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((items + BLOCK - 1) / BLOCK, 2048))); };
@@ -6477,13 +6875,15 @@ int small_refresh(kad_table* t, hipStream_t s, const uint32_t* mnode, uint32_t m
     if (t->gl32_mut)
         hipLaunchKernelGGL(gl32_build_kernel, grid(u32), dim3(BLOCK), 0, sC, d.key, d.status, d.dir, d.gcnt, d.fkey,
                            d.ftail, B, t->gl32_mut, s32);
-    if (t->wl_mut && t->ws_mut)
+    if (fuse) {
+        // built by rf_nodes_kernel
+    } else if (t->wl_mut && t->ws_mut)
         hipLaunchKernelGGL(wl_build_kernel<true>, grid(u8), dim3(BLOCK), 0, s, d.key, d.status, d.dir, d.gcnt, B,
                            64 - d.rshift, d.rbase >> d.rshift, t->wl_mut, t->ws_mut, s8);
     else if (t->wl_mut)
         hipLaunchKernelGGL(wl_build_kernel<false>, grid(u8), dim3(BLOCK), 0, s, d.key, d.status, d.dir, d.gcnt, B,
                            64 - d.rshift, d.rbase >> d.rshift, t->wl_mut, nullptr, s8);
-    if (t->gl_mut) {
+    if (t->gl_mut && !fuse) {
         hipLaunchKernelGGL(gl_build_kernel, grid(u8), dim3(BLOCK), 0, s, d.key, d.status, d.dir, d.gcnt, d.fkey, d.ftail,
                            B, t->gl_mut, s8);
         if (t->sl_mut) {  // slot lines: transcoded from the general lines just rebuilt (the flagged buckets')
@@ -6557,6 +6957,7 @@ int dl_build_main(kad_table* t, hipStream_t s, uint64_t nowk) {
     }
     try {
         D.hkm.resize(n);
+        D.hkn.resize(n);
     } catch (...) {
         return set_err(KAD_ERR_NOMEM, "deadline keys: out of host memory");
     }
@@ -6569,6 +6970,7 @@ int dl_build_main(kad_table* t, hipStream_t s, uint64_t nowk) {
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipcub::DeviceRadixSort::SortPairs(ct, cb, tk, D.km, tn, D.kn, (int)n, 0, 64, s));
     HIP_TRY(hipMemcpyAsync(D.hkm.data(), D.km, 8ull * n, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(D.hkn.data(), D.kn, 4ull * n, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     D.nm = n;
     D.ns = 0;
@@ -7321,7 +7723,13 @@ int kad_table_refresh_status(kad_table* t, int64_t now_ns, void* stream) {
         const uint32_t mc = hm - D.cm, sc = hs - D.cs;
         // the resident service reads what changes: its launch ends (the next one waits for mut_ev)
         if ((rc = svc_quiesce(t)) || (rc = ensure_marks(t))) return rc;
-        if ((uint64_t)mc + sc + D.np <= RF_CAP) {
+        if ((uint64_t)mc + sc + D.np <= RF_INLINE && D.hkn.size() == D.hkm.size()) {
+            uint32_t inl[RF_INLINE], k = 0;
+            for (uint32_t x = D.cm; x < hm; x++) inl[k++] = D.hkn[x];
+            for (uint32_t x = D.cs; x < hs; x++) inl[k++] = D.hsn[x];
+            for (uint32_t x : D.hpend) inl[k++] = x;
+            rc = small_refresh(t, s, nullptr, 0, nullptr, 0, nullptr, 0, nullptr, now_ns, inl, k);
+        } else if ((uint64_t)mc + sc + D.np <= RF_CAP) {
             rc = small_refresh(t, s, D.kn + D.cm, mc, D.sn + D.cs, sc, D.pend, D.np, nullptr, now_ns);
         } else {
             hipLaunchKernelGGL(dl_process_kernel, dim3(512), dim3(BLOCK), 0, s, times_of(t), D.kn + D.cm, mc, D.sn + D.cs,
@@ -7436,10 +7844,11 @@ int kad_rt_closest_batch_dual(const kad_table* t4, const kad_table* t6, const ui
     return KAD_OK;
 }
 
-int kad_rt_shard_batch(const kad_table* t, const uint32_t* global_good_prefix, uint32_t global_buckets,
+static int shard_batch(const kad_table* t, const uint32_t* global_good_prefix, uint32_t global_buckets,
                        uint64_t global_base_hi, uint32_t depth, uint32_t shard_first_bucket, uint32_t reach_lo,
                        uint32_t reach_hi, const uint8_t* targets, uint32_t q, uint32_t count, uint32_t* rows,
-                       uint32_t row_cap, uint32_t* parts, uint32_t part_cap, uint32_t* counters, void* stream) {
+                       uint32_t row_cap, uint32_t* parts, uint32_t part_cap, uint32_t* counters, uint32_t dests,
+                       uint64_t dest_words, void* stream) {
     if (!t) return set_err(KAD_ERR_INVALID, "NULL table");
     int rc = check_count(count);
     if (rc) return rc;
@@ -7467,6 +7876,9 @@ int kad_rt_shard_batch(const kad_table* t, const uint32_t* global_good_prefix, u
     S.part_cap = part_cap;
     S.rs = KAD_ROW_WORDS(count);
     S.ps = KAD_PART_WORDS(count);
+    S.dests = dests;
+    S.nblk = (q + BLOCK - 1) / BLOCK;
+    S.dest_words = dest_words;
     // the window line is valid for a shard of a uniform table of the same depth
     const bool wl = count <= 8 && (t->d.flags & TF_WL) && (64 - t->d.rshift) == depth;
     DeviceGuard g(t->device);
@@ -7478,6 +7890,44 @@ int kad_rt_shard_batch(const kad_table* t, const uint32_t* global_good_prefix, u
                            targets, q, count);
     HIP_TRY(hipGetLastError());
     return KAD_OK;
+}
+
+int kad_rt_shard_batch(const kad_table* t, const uint32_t* global_good_prefix, uint32_t global_buckets,
+                       uint64_t global_base_hi, uint32_t depth, uint32_t shard_first_bucket, uint32_t reach_lo,
+                       uint32_t reach_hi, const uint8_t* targets, uint32_t q, uint32_t count, uint32_t* rows,
+                       uint32_t row_cap, uint32_t* parts, uint32_t part_cap, uint32_t* counters, void* stream) {
+    return shard_batch(t, global_good_prefix, global_buckets, global_base_hi, depth, shard_first_bucket, reach_lo,
+                       reach_hi, targets, q, count, rows, row_cap, parts, part_cap, counters, 1, 0, stream);
+}
+
+void kad_home_range(uint32_t q, uint32_t world, uint32_t rank, uint32_t* lo, uint32_t* hi) {
+    // the query blocks k with home_of_block(k) == rank: k in [ceil(rank * nblk / world), ceil((rank+1) * nblk / world))
+    const uint32_t nblk = (q + BLOCK - 1) / BLOCK;
+    auto first = [&](uint32_t r) { return (uint32_t)(((uint64_t)r * nblk + world - 1) / world); };
+    const uint64_t a = (uint64_t)first(rank) * BLOCK, e = (uint64_t)first(rank + 1) * BLOCK;
+    *lo = (uint32_t)std::min<uint64_t>(a, q);
+    *hi = (uint32_t)std::min<uint64_t>(e, q);
+}
+
+int kad_rt_shard_batch_home(const kad_table* t, const uint32_t* global_good_prefix, uint32_t global_buckets,
+                            uint64_t global_base_hi, uint32_t depth, uint32_t shard_first_bucket, uint32_t reach_lo,
+                            uint32_t reach_hi, const uint8_t* targets, uint32_t q, uint32_t count, uint32_t world,
+                            uint32_t* send, uint32_t row_cap, uint32_t part_cap, void* stream) {
+    if (!t) return set_err(KAD_ERR_INVALID, "NULL table");
+    if (world == 0 || world > KAD_SHARD_MAX_WORLD)
+        return set_err(KAD_ERR_INVALID, "world %u outside 1..%u", world, KAD_SHARD_MAX_WORLD);
+    if (row_cap == 0 || part_cap == 0) return set_err(KAD_ERR_INVALID, "row_cap and part_cap must be > 0");
+    if (!send) return set_err(KAD_ERR_INVALID, "NULL buffer");
+    const uint64_t bw = KAD_SHARD_BLOCK_WORDS(count, row_cap, part_cap);
+    const uint64_t parts_off = (uint64_t)KAD_SHARD_REGIONS * row_cap * KAD_ROW_WORDS(count);
+    const uint64_t ctr_off = parts_off + (uint64_t)part_cap * KAD_PART_WORDS(count);
+    DeviceGuard g(t->device);
+    hipLaunchKernelGGL(zero_counters_kernel, dim3(grid_for((uint64_t)world * KAD_SHARD_COUNTERS * KAD_SHARD_COUNTER_STRIDE)),
+                       dim3(BLOCK), 0, (hipStream_t)stream, send, world, bw, ctr_off);
+    HIP_TRY(hipGetLastError());
+    return shard_batch(t, global_good_prefix, global_buckets, global_base_hi, depth, shard_first_bucket, reach_lo,
+                       reach_hi, targets, q, count, send, row_cap, send + parts_off, part_cap, send + ctr_off, world, bw,
+                       stream);
 }
 
 int kad_rt_scatter_rows(const uint32_t* rows, const uint32_t* n_rows, uint32_t n_rows_stride, uint32_t n_blocks,
@@ -7509,9 +7959,9 @@ int kad_rt_merge_parts(const uint32_t* parts, uint32_t n_parts, uint32_t count, 
     return KAD_OK;
 }
 
-int kad_rt_gather_finish(const uint32_t* recv, uint32_t world, uint32_t row_cap, uint32_t part_cap, uint32_t q,
-                         uint32_t count, uint32_t* scratch, uint32_t* out_idx, uint8_t* out_cnt, uint32_t* overflow,
-                         int device, void* stream) {
+static int gather_finish(const uint32_t* recv, uint32_t world, uint32_t row_cap, uint32_t part_cap, uint32_t qbase,
+                         uint32_t q, uint32_t count, uint32_t* scratch, uint32_t* out_idx, uint8_t* out_cnt,
+                         uint32_t* overflow, int device, void* stream) {
     int rc = check_count(count);
     if (rc) return rc;
     if (count == 0) return set_err(KAD_ERR_INVALID, "count 0: nothing to answer (the caller writes empty rows)");
@@ -7532,6 +7982,7 @@ int kad_rt_gather_finish(const uint32_t* recv, uint32_t world, uint32_t row_cap,
     G.part_cap = part_cap;
     G.count = count;
     G.q = q;
+    G.qbase = qbase;
     uint32_t* head = scratch;
     uint32_t* next = scratch + q;
     DeviceGuard g(device);
@@ -7543,6 +7994,23 @@ int kad_rt_gather_finish(const uint32_t* recv, uint32_t world, uint32_t row_cap,
     hipLaunchKernelGGL(gather_merge_kernel, dim3(grid_for(nparts)), dim3(BLOCK), 0, s, G, head, next, out_idx, out_cnt);
     HIP_TRY(hipGetLastError());
     return KAD_OK;
+}
+
+int kad_rt_gather_finish(const uint32_t* recv, uint32_t world, uint32_t row_cap, uint32_t part_cap, uint32_t q,
+                         uint32_t count, uint32_t* scratch, uint32_t* out_idx, uint8_t* out_cnt, uint32_t* overflow,
+                         int device, void* stream) {
+    return gather_finish(recv, world, row_cap, part_cap, 0, q, count, scratch, out_idx, out_cnt, overflow, device,
+                         stream);
+}
+
+int kad_rt_home_finish(const uint32_t* recv, uint32_t world, uint32_t rank, uint32_t row_cap, uint32_t part_cap,
+                       uint32_t q, uint32_t count, uint32_t* scratch, uint32_t* out_idx, uint8_t* out_cnt,
+                       uint32_t* overflow, int device, void* stream) {
+    if (world == 0 || rank >= world) return set_err(KAD_ERR_INVALID, "rank %u of world %u", rank, world);
+    uint32_t lo, hi;
+    kad_home_range(q, world, rank, &lo, &hi);
+    return gather_finish(recv, world, row_cap, part_cap, lo, hi - lo, count, scratch, out_idx, out_cnt, overflow,
+                         device, stream);
 }
 
 int kad_table_set_addrs(kad_table* t, uint32_t addr_len, const uint8_t* addrs) {
@@ -8483,9 +8951,45 @@ int kad_table_export(const kad_table* t, uint8_t* ids, uint8_t* status, uint8_t*
                 for (int x = 0; x < 4; x++) b[8 + 4 * w + x] = (uint8_t)(tl[3ull * i + w] >> (24 - 8 * x));
         }
     }
-    if (status && n) HIP_TRY(hipMemcpy(status, t->d.status, n, hipMemcpyDeviceToHost));
+    if (status && n) {
+        if (t->mut_async) HIP_TRY(hipEventSynchronize(t->mut_ev));  // after the last asynchronous refresh
+        HIP_TRY(hipMemcpy(status, t->d.status, n, hipMemcpyDeviceToHost));
+    }
     if (bucket_first && B) std::memcpy(bucket_first, t->h_first.data(), 20ull * B);
     if (bucket_offset && B) std::memcpy(bucket_offset, t->h_off.data(), 4ull * (B + 1));
+    return KAD_OK;
+}
+
+int kad_table_export_lines(const kad_table* t, uint32_t set, void* out, uint64_t* bytes) {
+    if (!t || !bytes) return set_err(KAD_ERR_INVALID, "NULL argument");
+    const DevTable& d = t->d;
+    const void* src = nullptr;
+    uint64_t nb = 0;
+    switch (set) {
+        case KAD_LINESET_WL: src = d.wl; nb = 128ull * d.B; break;
+        case KAD_LINESET_WS: src = d.ws; nb = 64ull * d.B; break;
+        case KAD_LINESET_WL16: src = d.wl16; nb = 4ull * WL16_STRIDE * d.B; break;
+        case KAD_LINESET_WL32: src = d.wl32; nb = 4ull * WL32_STRIDE * d.B; break;
+        case KAD_LINESET_GL: src = d.gl; nb = 4ull * GL_STRIDE * d.B; break;
+        case KAD_LINESET_GL16: src = d.gl16; nb = 4ull * GL16_STRIDE * d.B; break;
+        case KAD_LINESET_GL32: src = d.gl32; nb = 4ull * GL32_STRIDE * d.B; break;
+        case KAD_LINESET_SL: src = d.sl; nb = 64ull * d.slslots; break;
+        case KAD_LINESET_SL16: src = d.sl16; nb = 128ull * d.slslots; break;
+        case KAD_LINESET_NCL: src = d.ncl; nb = 4ull * NCL_STRIDE * d.nslots; break;
+        case KAD_LINESET_NCL32: src = d.ncl32; nb = 4ull * NC32_STRIDE * d.nslots; break;
+        case KAD_LINESET_GCNT: src = d.gcnt; nb = 4ull * d.B; break;
+        case KAD_LINESET_DIR: src = d.dir; nb = 8ull * (d.B + 1); break;
+        default: return set_err(KAD_ERR_INVALID, "unknown line set %u", set);
+    }
+    if (!src) nb = 0;
+    if (!out) { *bytes = nb; return KAD_OK; }
+    if (*bytes < nb) return set_err(KAD_ERR_INVALID, "buffer of %llu bytes for %llu", (unsigned long long)*bytes,
+                                    (unsigned long long)nb);
+    *bytes = nb;
+    if (!nb) return KAD_OK;
+    DeviceGuard g(t->device);
+    if (t->mut_async) HIP_TRY(hipEventSynchronize(t->mut_ev));
+    HIP_TRY(hipMemcpy(out, src, nb, hipMemcpyDeviceToHost));
     return KAD_OK;
 }
 

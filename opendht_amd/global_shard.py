@@ -1,19 +1,22 @@
 """North-star multi-GPU variant: the table is sharded across the GPUs of one node
-with NO halo; every GPU answers its part of every query's window, the parts are all-gathered over
-RCCL and merged on the device.
+with NO halo; every GPU answers its part of every query's window, the parts are exchanged over RCCL
+and merged on the device.
 
 Per rank s (one process per GPU):
   * the shard table holds global buckets [lo, hi) of a global U(depth) table, with global node
     indices (index_base = nodes below lo); window lines make its interior queries one line each;
   * the GLOBAL good prefix sums (4 bytes per global bucket) are all-gathered once at setup, so the
     rank can compute any query's global window W(R) (routing_table.cpp:89-104);
-  * a step is device-only: kad_rt_shard_batch over the replicated batch appends complete rows (W(R)
+  * a step is device-only: kad_rt_shard_batch_home over the replicated batch appends complete rows (W(R)
     inside the shard) and partial rows (W(R) crossing an edge, with XOR distances) straight into the
-    rank's fixed-size send block; one all_gather_into_tensor of the blocks (RCCL over xGMI);
-    kad_rt_gather_finish scatters the complete rows by qid and merges each query's parts, reading every
-    count on the device. Every rank ends with every query's result, bit-exact with
+    send block of the query's HOME rank (query block k of 256 queries: rank k * world / nblk); one
+    all_to_all_single of the fixed-size blocks (RCCL over xGMI) delivers to every rank only the rows of its
+    own home range, ~q / world rows instead of q; kad_rt_home_finish scatters them and merges each query's
+    parts, reading every count on the device. Every rank ends with its home range's results, bit-exact with
     RoutingTable::findClosestNodes on the whole table. No host read per step (a full buffer sets a
-    sticky overflow word checked once per batch), so steps can be captured in a HIP graph.
+    sticky overflow word, combined over the ranks once per batch), so steps can be captured in a HIP graph.
+  * the all-gather form (kad_rt_shard_batch + kad_rt_gather_finish: every rank ends with every result, q
+    rows into every rank) is kept as Exchange(home=False).
 
 The owner-routed halo variant (sharded.py) moves only results a client asked for; this variant
 is the one the north star describes and config 3 names ("RCCL all-gather + top-k merge").
@@ -71,60 +74,116 @@ def allgather_padded(x, n: int, group=None):
     return torch.stack(out), counts
 
 
+def home_range(q: int, world: int, rank: int) -> tuple[int, int]:
+    """Rank `rank`'s home queries [lo, hi) of a q-query batch (kad_home_range: query blocks of 256 split evenly)."""
+    lo, hi = C.c_uint32(), C.c_uint32()
+    lib().kad_home_range(q, world, rank, C.byref(lo), C.byref(hi))
+    return lo.value, hi.value
+
+
 class Exchange:
-    """Fixed-size send / receive blocks of one step shape (q queries, count, world ranks): the layout of
-    kad_rt_gather_finish (include/kadgpu.h). A rank's send block is its kad_rt_shard_batch output in place
-    (REGIONS regions of row_cap complete rows, part_cap partial rows, the counters); one all-gather of the
-    blocks, then the device scatter + merge. The capacities are the same on every rank (they depend on
-    q, count and world only), so the collective is always matched. No host read per step: a region or
-    part buffer that fills sets the sticky overflow word, which the caller checks once per batch (query)
-    or once per K steps (bench.py) and then runs again with grown(); every rank reads the same gathered
-    counters, so every rank grows the same way."""
+    """Fixed-size send / receive blocks of one step shape (q queries, count, world ranks).
+
+    home=True (the default step): the send buffer is `world` blocks, block d holding what goes to rank d (the
+    rows and parts of rank d's home queries: REGIONS regions of row_cap complete rows, part_cap partial rows, the
+    counters); one all_to_all_single, then kad_rt_home_finish on the received blocks. A rank receives ~q / world
+    rows per step.
+    home=False: the all-gather layout of kad_rt_gather_finish: one block with the rows of every query, one
+    all_gather_into_tensor; every rank receives every row.
+    The capacities are the same on every rank (they depend on q, count and world only, or on counters combined
+    over the ranks), so the collective is always matched. No host read per step: a region or part buffer that
+    fills sets the sticky overflow word, which the caller checks (combined over the ranks) once per batch or once
+    per K steps and then runs again with grown()."""
 
     def __init__(self, q: int, count: int, world: int, device, row_cap: int | None = None,
-                 part_cap: int | None = None):
+                 part_cap: int | None = None, home: bool = True):
         import torch
 
-        self.q, self.count, self.world, self.dev = q, count, world, device
-        # rows of query block k go to region k % 8, so this capacity can never overflow
-        self.row_cap_max = -(-(-(-q // 256)) // 8) * 256
-        est = -(-q // (REGIONS * world)) * 5 // 4 + 256  # uniform targets: ~q / world rows per rank
+        self.q, self.count, self.world, self.dev, self.home = q, count, world, device, home
+        nblk = -(-q // 256)
+        if home:
+            # region k % 8 of a home range of ceil(nblk / world) query blocks: this capacity can never overflow
+            self.row_cap_max = -(-(-(-nblk // world)) // REGIONS) * 256
+            # uniform targets: a source shard answers ~1/world of a home rank's ~q/world queries, ~exp per region
+            exp = -(-q // (REGIONS * world * world))
+            est = exp + 6 * int(np.sqrt(exp)) + 32
+            part_def = 256
+        else:
+            self.row_cap_max = -(-nblk // REGIONS) * 256  # rows of query block k go to region k % 8
+            est = -(-q // (REGIONS * world)) * 5 // 4 + 256  # ~q / world rows per rank
+            part_def = 1024
         self.row_cap = max(1, min(self.row_cap_max, row_cap or est))
-        self.part_cap = max(1, part_cap or 1024)
+        self.part_cap = max(1, part_cap or part_def)
         rw, pw = row_words(count), part_words(count)
         self.parts_off = REGIONS * self.row_cap * rw
         self.ctr_off = self.parts_off + self.part_cap * pw
         self.block = shard_block_words(count, self.row_cap, self.part_cap)
-        self.send = torch.empty((self.block,), dtype=torch.int32, device=device)
+        nsend = world if home else 1
+        self.send = torch.zeros((nsend * self.block,), dtype=torch.int32, device=device)
         self.recv = self.send if world == 1 else torch.empty((world * self.block,), dtype=torch.int32, device=device)
-        self.scratch = torch.full((q + world * self.part_cap,), -1, dtype=torch.int32, device=device)
+        qh = max(home_range(q, world, r)[1] - home_range(q, world, r)[0] for r in range(world)) if home else q
+        self.scratch = torch.full((qh + world * self.part_cap,), -1, dtype=torch.int32, device=device)
         self.overflow = torch.zeros((1,), dtype=torch.int32, device=device)
 
     @property
     def gathered_bytes(self) -> int:
-        """Bytes every rank receives per step (world fixed-size blocks)."""
+        """Bytes every rank receives per step (world fixed-size blocks, its own included)."""
         return 4 * self.world * self.block
 
+    @property
+    def xgmi_bytes(self) -> int:
+        """Bytes every rank receives from the other ranks per step (over xGMI)."""
+        return 4 * (self.world - 1) * self.block
+
     def counters(self):
-        """This rank's counter words (a view of the send block)."""
+        """This rank's counter words (a view of the send block; the all-gather layout)."""
         return self.send[self.ctr_off:self.ctr_off + COUNTERS * CSTRIDE]
 
-    def overflowed(self) -> bool:
-        """Host read of the sticky overflow word (synchronises), cleared."""
+    def overflowed(self, group=None, combine: bool = True) -> bool:
+        """Host read of the sticky overflow word (synchronises), cleared. The home exchange combines it over the
+        ranks first (each rank sees only the blocks sent to it), so every rank decides the same (combine=False:
+        one process simulating the ranks)."""
+        if combine and self.home and self.world > 1:
+            import torch.distributed as dist
+
+            dist.all_reduce(self.overflow, op=dist.ReduceOp.MAX, group=group)
         v = bool(int(self.overflow.item()))
         if v:
             self.overflow.zero_()
         return v
 
-    def grown(self) -> "Exchange":
-        """A new layout sized from the gathered counters of the last step (the same on every rank)."""
+    def parts_received(self) -> int:
+        """Partial rows in the received blocks of the last step."""
+        c = self.recv.view(self.world, self.block)[:, self.ctr_off:self.ctr_off + COUNTERS * CSTRIDE]
+        return int(c.cpu().numpy().reshape(self.world, COUNTERS, CSTRIDE)[:, 8, 0].astype(np.int64).sum())
+
+    def needs(self) -> tuple[int, int]:
+        """The largest region and part counts in the received blocks of the last step."""
         c = self.recv.view(self.world, self.block)[:, self.ctr_off:self.ctr_off + COUNTERS * CSTRIDE]
         c = c.cpu().numpy().reshape(self.world, COUNTERS, CSTRIDE)[:, :, 0].astype(np.int64)
-        need_r, need_p = int(c[:, :REGIONS].max()), int(c[:, 8].max())
+        return int(c[:, :REGIONS].max()), int(c[:, 8].max())
+
+    def grown(self, group=None, needs: tuple[int, int] | None = None) -> "Exchange":
+        """A new layout sized from the counters of the last step, combined over the ranks (the same on every
+        rank). needs: the (rows, parts) counts to fit, if known (query_simulated)."""
+        need_r, need_p = needs if needs is not None else self.needs()
+        if needs is None and self.home and self.world > 1:
+            import torch
+            import torch.distributed as dist
+
+            t = torch.tensor([need_r, need_p], dtype=torch.int64, device=self.dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+            need_r, need_p = (int(x) for x in t.cpu())
         row_cap = self.row_cap if need_r <= self.row_cap else max(2 * self.row_cap, need_r * 5 // 4)
         part_cap = self.part_cap if need_p <= self.part_cap else max(2 * self.part_cap, need_p * 5 // 4)
         return Exchange(self.q, self.count, self.world, self.dev, row_cap=min(row_cap, self.row_cap_max),
-                        part_cap=part_cap)
+                        part_cap=part_cap, home=self.home)
+
+    def home_finish(self, rank: int, out_idx, out_cnt, stream):
+        """kad_rt_home_finish over the received blocks: rank `rank`'s rows (device only)."""
+        check(lib().kad_rt_home_finish(ptr(self.recv), self.world, rank, self.row_cap, self.part_cap, self.q,
+                                       self.count, ptr(self.scratch), ptr(out_idx), ptr(out_cnt), ptr(self.overflow),
+                                       self.dev.index or 0, stream), "kad_rt_home_finish")
 
     def finish(self, out_idx, out_cnt, stream):
         """kad_rt_gather_finish over the received blocks (device only)."""
@@ -154,12 +213,23 @@ class GlobalShard:
     def close(self):
         self.table.close()
 
-    def exchange(self, q: int, count: int, world: int) -> Exchange:
-        """The cached step layout for (q, count, world)."""
-        key = (q, count, world)
+    def exchange(self, q: int, count: int, world: int, home: bool = True) -> Exchange:
+        """The cached step layout for (q, count, world, home)."""
+        key = (q, count, world, home)
         if key not in self._ex:
-            self._ex[key] = Exchange(q, count, world, self.dev)
+            self._ex[key] = Exchange(q, count, world, self.dev, home=home)
         return self._ex[key]
+
+    def home_block(self, targets, ex: Exchange, stream=None):
+        """kad_rt_shard_batch_home over a replicated (q, 20) device batch into ex's `world` send blocks (their
+        counters zeroed by the call); async on `stream` (a raw hipStream_t; default: the current torch stream)."""
+        import torch
+
+        s = stream if stream is not None else torch.cuda.current_stream(self.dev).cuda_stream
+        check(lib().kad_rt_shard_batch_home(self.table.handle, ptr(self.gpre), self.GB, C.c_uint64(self.base_hi),
+                                            self.depth, self.lo, self.reach[0], self.reach[1], ptr(targets), ex.q,
+                                            ex.count, ex.world, ptr(ex.send), ex.row_cap, ex.part_cap, C.c_void_p(s)),
+              "kad_rt_shard_batch_home")
 
     def local_block(self, targets, ex: Exchange, stream=None):
         """kad_rt_shard_batch over a replicated (q, 20) device batch into ex's send block (counters zeroed
@@ -180,14 +250,25 @@ class GlobalShard:
                                        ex.count, C.c_void_p(base), ex.row_cap, C.c_void_p(base + 4 * ex.parts_off),
                                        ex.part_cap, ptr(ctr), C.c_void_p(s)), "kad_rt_shard_batch")
 
-    def step(self, targets, ex: Exchange, out_idx, out_cnt, group=None, stream=None):
-        """One device-only step: local block, all-gather of the fixed-size blocks (RCCL; gloo lists in the
-        CPU-rank tests; nothing at world 1), scatter + merge. No host read: check ex.overflowed() after.
-        `stream`: a raw hipStream_t, default the current torch stream (what graph capture uses)."""
+    def step(self, targets, ex: Exchange, out_idx, out_cnt, group=None, stream=None, rank: int | None = None):
+        """One device-only step: the send blocks, the collective (home: all_to_all_single of the world blocks;
+        else all_gather_into_tensor; RCCL, gloo through the host in the CPU-rank tests; nothing at world 1), the
+        scatter + merge. home: out_idx / out_cnt get this rank's home range (home_range) only. No host read:
+        check ex.overflowed(group) after. `stream`: a raw hipStream_t, default the current torch stream (what
+        graph capture uses)."""
         import torch
 
-        self.local_block(targets, ex, stream)
         s = stream if stream is not None else torch.cuda.current_stream(self.dev).cuda_stream
+        if ex.home:
+            if rank is None:
+                rank = rank_of(group) if ex.world > 1 else 0
+            self.home_block(targets, ex, s)
+            if ex.world > 1:
+                with torch.cuda.stream(torch.cuda.ExternalStream(s, device=self.dev)):
+                    exchange_into(ex.recv, ex.send, group)
+            ex.home_finish(rank, out_idx, out_cnt, C.c_void_p(s))
+            return
+        self.local_block(targets, ex, stream)
         if ex.world > 1:
             if stream is None:
                 gather_into(ex.recv, ex.send, group)
@@ -196,42 +277,50 @@ class GlobalShard:
                     gather_into(ex.recv, ex.send, group)
         ex.finish(out_idx, out_cnt, C.c_void_p(s))
 
-    def query(self, targets, count: int, group=None, out_idx=None, out_cnt=None, single_rank_shard_kernel=False):
-        """Every query's RoutingTable::findClosestNodes result on every rank: local rows and parts,
-        all-gather (RCCL / gloo), device scatter and merge; one host read of the overflow word per call
-        (a full buffer grows the layout and runs the batch again on every rank). A single rank holds the
-        whole table: the plain kad_rt_closest_batch (single_rank_shard_kernel: the shard kernel and the
-        finish instead, what each rank runs at N > 1 minus the collective)."""
+    def query(self, targets, count: int, group=None, out_idx=None, out_cnt=None, single_rank_shard_kernel=False,
+              home: bool = True):
+        """RoutingTable::findClosestNodes over a replicated batch: local rows and parts, the exchange (RCCL /
+        gloo), device scatter and merge; one combined host read of the overflow word per call (a full buffer
+        grows the layout and runs the batch again on every rank). home (default): returns (lo, out_idx, out_cnt)
+        with this rank's home queries [lo, lo + len(out_idx)); home=False: (0, every query's rows) on every rank
+        (the all-gather). A single rank holds the whole table: the plain kad_rt_closest_batch
+        (single_rank_shard_kernel: the shard kernel and the finish instead, what each rank runs at N > 1 minus
+        the collective)."""
         import torch
         import torch.distributed as dist
 
         q = targets.shape[0]
+        world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+        rank = rank_of(group) if world > 1 else 0
+        lo, hi = home_range(q, world, rank) if home else (0, q)
         if out_idx is None:
-            out_idx = torch.empty((q, count), dtype=torch.int32, device=self.dev)
+            out_idx = torch.empty((hi - lo, count), dtype=torch.int32, device=self.dev)
         if out_cnt is None:
-            out_cnt = torch.empty((q,), dtype=torch.uint8, device=self.dev)
+            out_cnt = torch.empty((hi - lo,), dtype=torch.uint8, device=self.dev)
         if count == 0 or q == 0:
             out_cnt.zero_()
-            return out_idx, out_cnt
-        world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+            return lo, out_idx, out_cnt
         if world == 1:
             if (self.lo, self.hi) != (0, self.GB):
                 raise ValueError("a single rank must hold the whole table")
             if not single_rank_shard_kernel:
-                return self.table.rt_closest(targets, count, out_idx=out_idx, out_cnt=out_cnt)
+                return 0, *self.table.rt_closest(targets, count, out_idx=out_idx, out_cnt=out_cnt)
         while True:
-            ex = self.exchange(q, count, world)
-            self.step(targets, ex, out_idx, out_cnt, group)
-            if not ex.overflowed():
-                return out_idx, out_cnt
-            self._ex[(q, count, world)] = ex.grown()
+            ex = self.exchange(q, count, world, home)
+            self.step(targets, ex, out_idx, out_cnt, group, rank=rank)
+            if not ex.overflowed(group):
+                return lo, out_idx, out_cnt
+            self._ex[(q, count, world, home)] = ex.grown(group)
 
 
-def query_simulated(shards, targets, count: int, out_idx=None, out_cnt=None, row_cap=None, part_cap=None):
-    """Every shard of a global table in ONE process (one GPU, no collective): each shard's send block, the
-    blocks concatenated in rank order (exactly what all_gather_into_tensor delivers to every rank), the same
-    kad_rt_gather_finish. How the tests drive the exchange of N ranks on one GPU. Returns (out_idx, out_cnt,
-    the last Exchange)."""
+def query_simulated(shards, targets, count: int, out_idx=None, out_cnt=None, row_cap=None, part_cap=None,
+                    home: bool = True):
+    """Every shard of a global table in ONE process (one GPU, no collective), the N ranks' step:
+    home (default): each shard's `world` send blocks; for every rank r the blocks the shards address to r,
+    concatenated in source order (exactly what all_to_all_single delivers to rank r), then kad_rt_home_finish
+    for r into r's home range of the output; home=False: each shard's block, the blocks concatenated (what
+    all_gather_into_tensor delivers to every rank), kad_rt_gather_finish. How the tests drive the exchange of N
+    ranks on one GPU. Returns (out_idx, out_cnt, the last Exchange) with every query's row."""
     import torch
 
     q, world = targets.shape[0], len(shards)
@@ -240,8 +329,29 @@ def query_simulated(shards, targets, count: int, out_idx=None, out_cnt=None, row
         out_idx = torch.empty((q, count), dtype=torch.int32, device=dev)
     if out_cnt is None:
         out_cnt = torch.empty((q,), dtype=torch.uint8, device=dev)
-    while True:
+    s = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    while home:
         exs = [Exchange(q, count, world, dev, row_cap=row_cap, part_cap=part_cap) for _ in shards]
+        for sh, ex in zip(shards, exs):
+            sh.home_block(targets, ex)
+        ex0 = exs[0]
+        ovf, need_r, need_p, ptot = False, 0, 0, 0
+        for r in range(world):
+            if world > 1:
+                torch.cat([e.send[r * e.block:(r + 1) * e.block] for e in exs], out=ex0.recv)
+            lo, hi = home_range(q, world, r)
+            ex0.home_finish(r, out_idx[lo:hi], out_cnt[lo:hi], s)
+            nr, npt = ex0.needs()
+            need_r, need_p = max(need_r, nr), max(need_p, npt)
+            ptot += ex0.parts_received()
+            ovf = ex0.overflowed(combine=False) or ovf
+        if not ovf:
+            ex0.parts_total = ptot
+            return out_idx, out_cnt, ex0
+        g = ex0.grown(needs=(need_r, need_p))
+        row_cap, part_cap = g.row_cap, g.part_cap
+    while True:
+        exs = [Exchange(q, count, world, dev, row_cap=row_cap, part_cap=part_cap, home=False) for _ in shards]
         for sh, ex in zip(shards, exs):
             sh.local_block(targets, ex)
         ex0 = exs[0]
@@ -249,9 +359,32 @@ def query_simulated(shards, targets, count: int, out_idx=None, out_cnt=None, row
             torch.cat([e.send for e in exs], out=ex0.recv)
         ex0.finish(out_idx, out_cnt, C.c_void_p(torch.cuda.current_stream(dev).cuda_stream))
         if not ex0.overflowed():
+            ex0.parts_total = ex0.parts_received()
             return out_idx, out_cnt, ex0
         g = ex0.grown()
         row_cap, part_cap = g.row_cap, g.part_cap
+
+
+def exchange_into(recv, send, group=None):
+    """recv (world blocks) <- block r of every rank's send, in rank order: one all_to_all_single with equal
+    splits on RCCL; elsewhere (gloo) through host tensors (gloo's all_to_all on CPU, else an all-gather of the
+    whole send buffers)."""
+    import torch
+    import torch.distributed as dist
+
+    if dist.get_backend(group) == "nccl":
+        dist.all_to_all_single(recv, send, group=group)
+        return
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    cs = send.cpu()
+    try:
+        cr = torch.empty_like(cs)
+        dist.all_to_all_single(cr, cs, group=group)
+    except (RuntimeError, NotImplementedError):
+        full = [torch.empty_like(cs) for _ in range(world)]
+        dist.all_gather(full, cs, group=group)
+        cr = torch.cat([f.view(world, -1)[rank] for f in full])
+    recv.copy_(cr.to(recv.device))
 
 
 def gather_into(recv, send, group=None):

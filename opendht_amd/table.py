@@ -192,6 +192,16 @@ class DeviceTable:
         check(lib().kad_table_export(self._h, ptr(ids), ptr(st), ptr(first), ptr(off)), "kad_table_export")
         return ids[:n], st[:n], first[:B], off
 
+    def export_lines(self, which: int):
+        """A derived array (KAD_LINESET_*) as host bytes (kad_table_export_lines), or None if absent."""
+        nb = C.c_uint64(0)
+        check(lib().kad_table_export_lines(self._h, which, None, C.byref(nb)), "kad_table_export_lines")
+        if nb.value == 0:
+            return None
+        out = np.empty(nb.value, np.uint8)
+        check(lib().kad_table_export_lines(self._h, which, ptr(out), C.byref(nb)), "kad_table_export_lines")
+        return out
+
     def export_status(self):
         """The device's status bytes (n,), e.g. after refresh_status."""
         st = np.zeros(max(self.n, 1), np.uint8)

@@ -313,3 +313,106 @@ def test_small_refresh_every_line_set(gpu, t):
         np.testing.assert_array_equal(T.export_status(), st)
         assert T.info()["n_good"] == int((st & 1).sum())
         _check(T, t, st, targets, gpu, rt=rt, nc=nc)
+
+
+@pytest.mark.parametrize("t", [x for x in TB.all_small_tables() if x["ids"].shape[0] >= 50], ids=lambda t: t["name"])
+def test_small_refresh_shapes(gpu, t):
+    """The one-launch small refresh (rf_nodes_kernel with the count <= 8 lines built in the same block: window lines
+    and their short copies, or general lines where no slot lines exist) and its multi-block form on every small
+    table shape: `now` passes 1, 3, 40 and 300 deadlines, then nodes are heard again and refreshed at the same
+    `now`."""
+    n = t["ids"].shape[0]
+    rng = np.random.default_rng(n + 17)
+    targets = TB.adversarial_targets(t, extra=500)
+    MIN = 60 * 10**9
+    now = 300 * 3600 * 10**9
+    time_ns = now - rng.integers(0, 10 * MIN, n)
+    reply_ns = now - rng.integers(0, 120 * MIN, n)
+    expired = (rng.random(n) < 0.05).astype(np.uint8)
+
+    def status_at(tnow):
+        good = (expired == 0) & (reply_ns >= tnow - 120 * MIN) & (time_ns >= tnow - 10 * MIN)
+        return (good.astype(np.uint8) | (expired << 1)).astype(np.uint8)
+
+    with DeviceTable(t["ids"], status_at(now), t["first"], t["off"], device=0, sorted=t["sorted"]) as T:
+        T.set_times(time_ns, reply_ns, expired)
+        T.refresh_status(now)
+        for k in (1, 3, 40, 300):
+            d = np.unique(np.minimum(time_ns + 10 * MIN, reply_ns + 120 * MIN)[expired == 0])
+            d = d[d >= now]
+            if d.size == 0:
+                break
+            now = int(d[min(d.size - 1, k - 1)]) + 1
+            T.refresh_status(now)
+            torch.cuda.synchronize()
+            st = status_at(now)
+            np.testing.assert_array_equal(T.export_status(), st, err_msg=f"k={k}")
+            _check(T, t, st, targets, gpu, rt=(1, 8, 16, 32), nc=(1, 14, 32))
+        sel = rng.choice(n, min(n, 30), replace=False).astype(np.uint32)
+        time_ns[sel] = now
+        reply_ns[sel] = now
+        T.patch_times(sel, time_ns[sel], reply_ns[sel], expired[sel])
+        T.refresh_status(now)
+        torch.cuda.synchronize()
+        st = status_at(now)
+        np.testing.assert_array_equal(T.export_status(), st)
+        _check(T, t, st, targets, gpu, rt=(1, 8, 16, 32), nc=(1, 14, 32))
+
+
+LINESETS = ("WL", "WS", "WL16", "WL32", "GL", "GL16", "GL32", "SL", "SL16", "NCL", "NCL32", "GCNT", "DIR")
+
+
+@pytest.mark.parametrize("t", [TB.uniform_config(40_000, 12, seed=0x5EC), TB.split_config(20_000, seed=0x5ED),
+                               TB.uniform_config(6_000, 12, seed=0x5EE)], ids=lambda t: t["name"])
+def test_incremental_lines_equal_fresh_build(gpu, t):
+    """Every derived array an incremental refresh maintains (window, short, general and slot lines of every count,
+    NodeCache lines, per-bucket good counts, the directory's masks) is bit for bit what a table built from scratch
+    on the same status holds: after refreshes passing 1, 2, 5, 9, 30 and 3000 deadlines (the one-launch path whose
+    lines a wave builds, the single-block and multi-block lists, the flag path), a patch of times and one of status
+    bytes. The U(12) 6,000-node table has sparse buckets (windows of several rounds, deferred lines)."""
+    from opendht_amd import _lib
+
+    n = t["ids"].shape[0]
+    rng = np.random.default_rng(n ^ 0x5EC)
+    MIN = 60 * 10**9
+    now = 800 * 3600 * 10**9
+    time_ns = now - rng.integers(0, 10 * MIN, n)
+    reply_ns = now - rng.integers(0, 120 * MIN, n)
+    expired = (rng.random(n) < 0.05).astype(np.uint8)
+
+    def status_at(tnow):
+        good = (expired == 0) & (reply_ns >= tnow - 120 * MIN) & (time_ns >= tnow - 10 * MIN)
+        return (good.astype(np.uint8) | (expired << 1)).astype(np.uint8)
+
+    def compare(T, st, what):
+        with DeviceTable(t["ids"], st, t["first"], t["off"], device=0, sorted=t["sorted"], eager=True) as F:
+            for name in LINESETS:
+                k = getattr(_lib, f"KAD_LINESET_{name}")
+                a, b = T.export_lines(k), F.export_lines(k)
+                assert (a is None) == (b is None), f"{what}: {name} present in one table only"
+                if a is not None:
+                    np.testing.assert_array_equal(a, b, err_msg=f"{what}: {name}")
+
+    with DeviceTable(t["ids"], status_at(now), t["first"], t["off"], device=0, sorted=t["sorted"], eager=True) as T:
+        T.set_times(time_ns, reply_ns, expired)
+        T.refresh_status(now)
+        for k in (1, 2, 5, 9, 30, 3000):
+            d = np.unique(np.minimum(time_ns + 10 * MIN, reply_ns + 120 * MIN)[expired == 0])
+            d = d[d >= now]
+            now = int(d[min(d.size - 1, k - 1)]) + 1
+            T.refresh_status(now)
+            torch.cuda.synchronize()
+            compare(T, status_at(now), f"k={k}")
+        sel = rng.choice(n, 8, replace=False).astype(np.uint32)
+        time_ns[sel[:4]] = now
+        reply_ns[sel[:4]] = now
+        expired[sel[4:]] = 1
+        T.patch_times(sel, time_ns[sel], reply_ns[sel], expired[sel])
+        T.refresh_status(now)
+        torch.cuda.synchronize()
+        compare(T, status_at(now), "patch_times")
+        st = status_at(now).copy()
+        nodes = rng.choice(n, 5, replace=False).astype(np.uint32)
+        st[nodes] ^= np.uint8(1)
+        T.patch_status(nodes, st[nodes])
+        compare(T, st, "patch_status")
