@@ -188,6 +188,8 @@ public:
         off.push_back((uint32_t)nodes_.size());
         buckets_ = (uint32_t)(off.size() - 1);
         table_ = DeviceTable(device, ids, status, first, off);
+        first_.swap(first);
+        off_.swap(off);
         reindex();
         syncTimes();
         now_ns_ = to_ns(now);
@@ -205,6 +207,11 @@ public:
     template <class InfoHashT, class TimePoint>
     std::vector<std::vector<NodePtr>> findClosestNodesBatch(const InfoHashT* ids, size_t q, TimePoint now,
                                                             size_t count = KAD_TARGET_NODES) const {
+        if (q <= host_q_ && count <= host_count_) {  // a few single requests: the host path (no device round trip)
+            std::vector<std::vector<NodePtr>> out(q);
+            for (size_t i = 0; i < q; i++) out[i] = findClosestNodesHost(ids[i], now, count);
+            return out;
+        }
         advance(to_ns(now));
         std::vector<std::vector<NodePtr>> out(q);
         // any size_t count, as routing_table.h:48: a result never holds more than the table's nodes
@@ -284,12 +291,68 @@ public:
             if (idx[s] != KAD_NO_NODE) next[idx[s]] = added_[s];
         nodes_.swap(next);
         buckets_ = inf.n_buckets;
+        first_.assign((size_t)KAD_HASH_LEN * buckets_, 0);
+        off_.assign(buckets_ + 1, 0);
+        check(kad_table_export(table_.get(), nullptr, nullptr, buckets_ ? first_.data() : nullptr, off_.data()),
+              "kad_table_export");
         ops_.clear();
         added_.clear();
         reindex();
         syncTimes();  // kad_table_apply drops the node times (the layout moved)
         now_ns_ = to_ns(now);
         refresh_ = true;
+    }
+
+    /* RoutingTable::findClosestNodes(id, now, count) on the host, over the mirror's bucket directory and the
+     * table's own Node objects (isGood(now) read from them, as routing_table.cpp:77 does): the closed form of
+     * routing_table.cpp:67-111 -- findBucket by binary search over the bucket firsts, the window W(r) grown ring
+     * by ring until it holds `count` good nodes or the whole table, its good nodes ordered by (XOR distance,
+     * index) -- no pass over the table and no device round trip. For a few single requests it answers faster
+     * than a launch or the resident service (the crossover, tools/crossover.cpp); batches go to the device. */
+    template <class InfoHashT, class TimePoint>
+    std::vector<NodePtr> findClosestNodesHost(const InfoHashT& id, TimePoint now, size_t count = KAD_TARGET_NODES) const {
+        std::vector<NodePtr> out;
+        const uint32_t B = (uint32_t)(off_.size() ? off_.size() - 1 : 0);
+        if (B == 0 || count == 0) return out;
+        const uint8_t* t = id_bytes(id);
+        // findBucket (routing_table.cpp:113-127): the last bucket whose first is <= t, the first if none
+        uint32_t lo = 0, hi = B;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) / 2;
+            if (std::memcmp(&first_[(size_t)KAD_HASH_LEN * mid], t, KAD_HASH_LEN) <= 0) lo = mid + 1; else hi = mid;
+        }
+        const uint32_t b = lo ? lo - 1 : 0;
+        // the window: W(0) = [b-1, b], each round one bucket more on either side (routing_table.cpp:89-104)
+        struct Cand { uint32_t idx; const uint8_t* id; };
+        std::vector<Cand> cand;
+        size_t good = 0;
+        auto take = [&](uint32_t x) {
+            for (uint32_t j = off_[x]; j < off_[x + 1]; j++)
+                if (nodes_[j]->isGood(now)) { cand.push_back(Cand{j, id_bytes(nodes_[j]->id)}); good++; }
+        };
+        uint32_t wl = b ? b - 1 : 0, wh = b;
+        for (uint32_t x = wl; x <= wh; x++) take(x);
+        while (good < count && !(wl == 0 && wh == B - 1)) {
+            if (wh + 1 < B) take(++wh);
+            if (wl > 0) take(--wl);
+        }
+        auto closer = [&](const Cand& a, const Cand& c) {  // InfoHash::xorCmp (infohash.h:131-146), then index
+            for (unsigned k = 0; k < KAD_HASH_LEN; k++) {
+                const uint8_t da = a.id[k] ^ t[k], dc = c.id[k] ^ t[k];
+                if (da != dc) return da < dc;
+            }
+            return a.idx < c.idx;
+        };
+        const size_t m = std::min(count, cand.size());
+        std::partial_sort(cand.begin(), cand.begin() + m, cand.end(), closer);
+        out.reserve(m);
+        for (size_t k = 0; k < m; k++) out.push_back(nodes_[cand[k].idx]);
+        return out;
+    }
+    /* Batches of at most q requests with count <= max_count take the host path (0: never). */
+    void setHostPath(size_t q, size_t max_count = 64) {
+        host_q_ = q;
+        host_count_ = max_count;
     }
 
     size_t bucketCount() const { return buckets_; }
@@ -346,6 +409,9 @@ private:
     std::vector<NodePtr> nodes_;
     std::unordered_map<const void*, uint32_t> index_;
     uint32_t buckets_ = 0;
+    std::vector<uint8_t> first_;  // the bucket directory on the host (the host path)
+    std::vector<uint32_t> off_;
+    size_t host_q_ = 1, host_count_ = 64;  // single requests take the host path (tools/crossover.cpp)
     std::vector<uint32_t> ops_;
     std::vector<NodePtr> added_;
     mutable std::vector<uint32_t> updated_;

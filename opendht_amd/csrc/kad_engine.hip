@@ -5537,6 +5537,40 @@ __device__ void wl_ws_build_wave(uint32_t b, uint32_t B, uint32_t d, uint64_t pr
         make_uint4(W.S16[4 * lane], W.S16[4 * lane + 1], W.S16[4 * lane + 2], W.S16[4 * lane + 3]);
 }
 
+// The listed window lines (and their short copies) built by one wave each (wl_ws_build_wave): an incremental
+// rebuild's lines are few and scattered, so a line's latency (not the throughput of a thread per line) sets the
+// time. Windows of more than 64 nodes are built by the wave's first lane.
+__global__ __launch_bounds__(BLOCK) void wl_ws_wave_kernel(const uint64_t* __restrict__ key, const uint8_t* status,
+                                                            const uint2* dir, const uint32_t* gcnt, uint32_t B,
+                                                            uint32_t d, uint64_t pre0, uint32_t* wl, uint32_t* ws,
+                                                            LineSel sel) {
+    __shared__ WaveLds wv[BLOCK / 64];
+    WaveLds& WV = wv[threadIdx.x >> 6];
+    const uint32_t lane = threadIdx.x & 63u;
+    for (uint32_t x = (blockIdx.x * BLOCK + threadIdx.x) >> 6;; x += (gridDim.x * BLOCK) >> 6) {  // wave-uniform
+        uint32_t b;
+        if (!sel.pick(x, B, b)) return;
+        const uint32_t db = b >= 3 ? b - 3 : 0u, e = min(B, b + 3);
+        if (db + lane <= e && lane < 8) WV.dx[lane] = dir[db + lane].x & ~WIDE;
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t n0 = WV.dx[0], n1 = WV.dx[e - db];
+        if (n1 - n0 <= 64) {
+            const bool have = n0 + lane < n1;
+            const uint64_t kk = have ? key[n0 + lane] : 0ull;
+            const uint32_t sv = have ? status[n0 + lane] : 0u;
+            wl_ws_build_wave(b, B, d, pre0, db, WV.dx, n0, n1, kk, sv, wl, ws, WV);
+        } else if (lane == 0) {
+            wl_build_line(key, status, dir, gcnt, B, d, pre0, wl, b, WV.R);
+            if (ws) ws_build_line(WV.R, ws, b, WV.R + 33);
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
 // SINGLE: one block (at most BLOCK listed nodes): the appends go to LDS and there is no completion counter.
 // FUSE: the count <= 8 lines of the changed buckets are rebuilt by this block too (1: window lines and their
 // short copies, 2: general lines; the host fuses when at most RF_FUSE_LINES can be listed), so a refresh
@@ -6471,7 +6505,10 @@ int rebuild_good_prefix_(kad_table* t, hipStream_t s, bool full) {
                            t->d.gcnt, t->d.fkey, t->d.ftail, B, t->gl32_mut, sel_for(t->ld32, 2, sC));
     LineSel s8{};
     if (t->wl_mut || t->gl_mut) s8 = sel_for(t->ld8, 0, s);
-    if (t->wl_mut && t->ws_mut)  // the short lines transcoded from the 128-byte lines in the same thread
+    if (t->wl_mut && !full)  // a few scattered lines: a wave per line (wl_ws_wave_kernel), the short copies with it
+        hipLaunchKernelGGL(wl_ws_wave_kernel, lgrid(64ull * B), dim3(BLOCK), 0, s, t->d.key, t->d.status, t->d.dir,
+                           t->d.gcnt, B, 64 - t->d.rshift, t->d.rbase >> t->d.rshift, t->wl_mut, t->ws_mut, s8);
+    else if (t->wl_mut && t->ws_mut)  // the short lines transcoded from the 128-byte lines in the same thread
         hipLaunchKernelGGL(wl_build_kernel<true>, lgrid(B), dim3(BLOCK), 0, s, t->d.key, t->d.status, t->d.dir,
                            t->d.gcnt, B, 64 - t->d.rshift, t->d.rbase >> t->d.rshift, t->wl_mut, t->ws_mut, s8);
     else if (t->wl_mut)
@@ -6877,12 +6914,10 @@ int small_refresh(kad_table* t, hipStream_t s, const uint32_t* mnode, uint32_t m
                            d.ftail, B, t->gl32_mut, s32);
     if (fuse) {
         // built by rf_nodes_kernel
-    } else if (t->wl_mut && t->ws_mut)
-        hipLaunchKernelGGL(wl_build_kernel<true>, grid(u8), dim3(BLOCK), 0, s, d.key, d.status, d.dir, d.gcnt, B,
+    } else if (t->wl_mut) {  // a wave per listed line
+        hipLaunchKernelGGL(wl_ws_wave_kernel, grid(64ull * u8), dim3(BLOCK), 0, s, d.key, d.status, d.dir, d.gcnt, B,
                            64 - d.rshift, d.rbase >> d.rshift, t->wl_mut, t->ws_mut, s8);
-    else if (t->wl_mut)
-        hipLaunchKernelGGL(wl_build_kernel<false>, grid(u8), dim3(BLOCK), 0, s, d.key, d.status, d.dir, d.gcnt, B,
-                           64 - d.rshift, d.rbase >> d.rshift, t->wl_mut, nullptr, s8);
+    }
     if (t->gl_mut && !fuse) {
         hipLaunchKernelGGL(gl_build_kernel, grid(u8), dim3(BLOCK), 0, s, d.key, d.status, d.dir, d.gcnt, d.fkey, d.ftail,
                            B, t->gl_mut, s8);

@@ -169,8 +169,14 @@ int main() {
             check_rt(rt, got, targets, count, now, "moving now");
         }
         auto one = mirror.findClosestNodes(targets[3], now, 8);
-        auto ref = mirror.findClosestNodesBatch(&targets[3], 1, now, 8);
-        EXPECT(one == ref[0], "single query");
+        auto ref = mirror.findClosestNodesBatch(&targets[3], 2, now, 8);  // two requests: the device path
+        EXPECT(one == ref[0], "single query (host path) equals the device batch");
+        // the host path (single requests below the crossover) for every target and count, against the oracle
+        for (uint32_t count : {1u, 8u, 14u, 33u, 300u}) {
+            std::vector<std::vector<std::shared_ptr<Node>>> hg;
+            for (auto& t : targets) hg.push_back(mirror.findClosestNodesHost(t, now, count));
+            check_rt(rt, hg, targets, count, now, "host path");
+        }
     }
     // a count above the table's size (any size_t, routing_table.h:48): every good node, closest first
     {
@@ -412,6 +418,14 @@ int main() {
         }
         kadgpu::RoutingTableMirror<RoutingTable> lm(lrt, t0, 0);
         auto med = [](std::vector<double> v) { std::sort(v.begin(), v.end()); return v[v.size() / 2]; };
+        std::vector<double> host_us;
+        for (int r = 0; r < 2000; r++) {  // single requests on the host path (the default below the crossover)
+            const auto a = clock::now();
+            auto res = lm.findClosestNodes(targets[r % q], t0, 8);
+            host_us.push_back(std::chrono::duration<double, std::micro>(clock::now() - a).count());
+            EXPECT(res.size() == 8, "latency table result (host)");
+        }
+        lm.setHostPath(0);  // the device paths from here
         std::vector<double> one_us, b64_us;
         for (int r = 0; r < 2000; r++) {
             const auto a = clock::now();
@@ -443,9 +457,9 @@ int main() {
             s64_us.push_back(std::chrono::duration<double, std::micro>(clock::now() - a).count());
         }
         lm.serve(0);
-        std::printf("LATENCY {\"nodes\": %u, \"buckets\": %u, \"single_call_us\": %.2f, \"batch64_call_us\": %.2f, "
-                    "\"served_single_call_us\": %.2f, \"served_batch64_call_us\": %.2f}\n",
-                    m, LB, med(one_us), med(b64_us), med(s1_us), med(s64_us));
+        std::printf("LATENCY {\"nodes\": %u, \"buckets\": %u, \"host_single_call_us\": %.2f, \"single_call_us\": %.2f, "
+                    "\"batch64_call_us\": %.2f, \"served_single_call_us\": %.2f, \"served_batch64_call_us\": %.2f}\n",
+                    m, LB, med(host_us), med(one_us), med(b64_us), med(s1_us), med(s64_us));
     }
     std::printf("%s (%d failures)\n", fails ? "FAIL" : "PASS", fails);
     return fails ? 1 : 0;
