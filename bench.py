@@ -768,6 +768,19 @@ def configs_pass(dev, reps=10):
                           "table_build_s": build_s, "lookups_per_s": L / run_s, "ms": run_s * 1e3,
                           "mean_hops": float(hops.mean()), "synced_frac": float((done == 1).mean()),
                           "table_GB": Wm.device_bytes() / 1e9}
+        # the same lookups with 10% of the peers offline (a deterministic hash of the peer index; requests to them
+        # time out and mark the node expired in the search list, search.cpp's expire path)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        X = Wm.search(src, tgt, offline_per_10k=1000)
+        X.run()
+        torch.cuda.synchronize(dev)
+        run_s = time.perf_counter() - t0
+        lst, q, bad_, n, hops, done, ovf = X.get(full=True)
+        X.close()
+        res["config5"]["offline_10pct"] = {"lookups_per_s": L / run_s, "ms": run_s * 1e3,
+                                           "mean_hops": float(hops.mean()),
+                                           "synced_frac": float((done == 1).mean())}
     finally:
         Wm.close()
     torch.cuda.empty_cache()

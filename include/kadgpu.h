@@ -386,8 +386,9 @@ int kad_rt_gather_finish(const uint32_t* recv, uint32_t world, uint32_t row_cap,
  *            goes to rank d (its regions, parts and counters; the counters are zeroed by the call first)
  *   recv     after all_to_all_single(recv, send) with equal splits: block s = what rank s sent here
  * kad_rt_home_finish then writes rank `rank`'s rows: out_idx (hi - lo) x count and out_cnt (hi - lo) for qids
- * lo + i. scratch: (hi - lo) + world*part_cap words, the first (hi - lo) KAD_NO_NODE before the first call (every
- * call leaves them so). overflow: set to 1 when a block sent here was full; it only sees this rank's blocks, so
+ * lo + i. scratch: H + world*part_cap words, H = the size of rank 0's range (the largest; the same for every rank,
+ * so one scratch can serve the ranks of a step one after the other), the first H KAD_NO_NODE before the first call
+ * (every call leaves them so). overflow: set to 1 when a block sent here was full; it only sees this rank's blocks, so
  * callers combine it over the ranks (all_reduce MAX) before deciding to grow and run again. */
 #define KAD_SHARD_QUERY_BLOCK 256u
 void kad_home_range(uint32_t q, uint32_t world, uint32_t rank, uint32_t* lo, uint32_t* hi);

@@ -2724,7 +2724,10 @@ __global__ __launch_bounds__(BLOCK) void sl16_build_kernel(const uint32_t* __res
             dst[g] = reinterpret_cast<const uint4*>(gl16 + (size_t)GL16_STRIDE * b)[g];
             continue;
         }
-        if (g > 1) continue;
+        if (g > 1) {  // the unused rest of a fallback line: zero, so a line's bytes are a function of the table
+            dst[g] = make_uint4(0u, 0u, 0u, 0u);
+            continue;
+        }
         const uint32_t r0 = rrdx[j << k], r1 = rrdx[min((j + 1) << k, rslots)];
         const uint32_t lo = r0 & RDX_MASK, hi = r1 & RDX_MASK;
         const bool exact = (r0 & RDX_EXACT) != 0;
@@ -7995,8 +7998,8 @@ int kad_rt_merge_parts(const uint32_t* parts, uint32_t n_parts, uint32_t count, 
 }
 
 static int gather_finish(const uint32_t* recv, uint32_t world, uint32_t row_cap, uint32_t part_cap, uint32_t qbase,
-                         uint32_t q, uint32_t count, uint32_t* scratch, uint32_t* out_idx, uint8_t* out_cnt,
-                         uint32_t* overflow, int device, void* stream) {
+                         uint32_t q, uint32_t head_words, uint32_t count, uint32_t* scratch, uint32_t* out_idx,
+                         uint8_t* out_cnt, uint32_t* overflow, int device, void* stream) {
     int rc = check_count(count);
     if (rc) return rc;
     if (count == 0) return set_err(KAD_ERR_INVALID, "count 0: nothing to answer (the caller writes empty rows)");
@@ -8019,7 +8022,7 @@ static int gather_finish(const uint32_t* recv, uint32_t world, uint32_t row_cap,
     G.q = q;
     G.qbase = qbase;
     uint32_t* head = scratch;
-    uint32_t* next = scratch + q;
+    uint32_t* next = scratch + head_words;  // the same offset for every rank of a step: one scratch can serve them all
     DeviceGuard g(device);
     hipStream_t s = (hipStream_t)stream;
     const uint64_t nrows = (uint64_t)world * KAD_SHARD_REGIONS * row_cap, nparts = (uint64_t)world * part_cap;
@@ -8034,7 +8037,7 @@ static int gather_finish(const uint32_t* recv, uint32_t world, uint32_t row_cap,
 int kad_rt_gather_finish(const uint32_t* recv, uint32_t world, uint32_t row_cap, uint32_t part_cap, uint32_t q,
                          uint32_t count, uint32_t* scratch, uint32_t* out_idx, uint8_t* out_cnt, uint32_t* overflow,
                          int device, void* stream) {
-    return gather_finish(recv, world, row_cap, part_cap, 0, q, count, scratch, out_idx, out_cnt, overflow, device,
+    return gather_finish(recv, world, row_cap, part_cap, 0, q, q, count, scratch, out_idx, out_cnt, overflow, device,
                          stream);
 }
 
@@ -8042,10 +8045,11 @@ int kad_rt_home_finish(const uint32_t* recv, uint32_t world, uint32_t rank, uint
                        uint32_t q, uint32_t count, uint32_t* scratch, uint32_t* out_idx, uint8_t* out_cnt,
                        uint32_t* overflow, int device, void* stream) {
     if (world == 0 || rank >= world) return set_err(KAD_ERR_INVALID, "rank %u of world %u", rank, world);
-    uint32_t lo, hi;
+    uint32_t lo, hi, lo0, hi0;
     kad_home_range(q, world, rank, &lo, &hi);
-    return gather_finish(recv, world, row_cap, part_cap, lo, hi - lo, count, scratch, out_idx, out_cnt, overflow,
-                         device, stream);
+    kad_home_range(q, world, 0, &lo0, &hi0);  // rank 0's range is the largest
+    return gather_finish(recv, world, row_cap, part_cap, lo, hi - lo, hi0 - lo0, count, scratch, out_idx, out_cnt,
+                         overflow, device, stream);
 }
 
 int kad_table_set_addrs(kad_table* t, uint32_t addr_len, const uint8_t* addrs) {

@@ -253,7 +253,7 @@ def _gather_worker(rank, world, port, q):
     sys.path[:0] = [os.path.dirname(here), here]
     import torch.distributed as dist
 
-    from opendht_amd.global_shard import allgather_padded, gather_into, global_good_prefix
+    from opendht_amd.global_shard import allgather_padded, exchange_into, gather_into, global_good_prefix
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -269,6 +269,12 @@ def _gather_worker(rank, world, port, q):
         recv = torch.full((world * 7,), -1, dtype=torch.int32)
         gather_into(recv, torch.arange(7, dtype=torch.int32) + 100 * rank)
         ok = ok and torch.equal(recv, torch.cat([torch.arange(7, dtype=torch.int32) + 100 * r for r in range(world)]))
+        # the home exchange's collective: block d of every rank's send buffer lands in rank d's recv, in rank order
+        send = torch.arange(world * 5, dtype=torch.int32) + 1000 * rank
+        recv = torch.full((world * 5,), -1, dtype=torch.int32)
+        exchange_into(recv, send)
+        ok = ok and torch.equal(recv, torch.cat([torch.arange(5 * rank, 5 * rank + 5, dtype=torch.int32) + 1000 * r
+                                                 for r in range(world)]))
         gp = global_good_prefix(np.full(5, rank + 1))
         ok = ok and np.array_equal(gp, np.concatenate([[0], np.cumsum(np.repeat(np.arange(1, world + 1), 5))]))
         q.put((rank, bool(ok)))
@@ -305,7 +311,7 @@ def _query_worker(rank, world, port, q):
     os.environ["MASTER_PORT"] = str(port)
     # both ranks share cuda:0 (one GPU box): gloo stages the gathers through the host
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    ok = False
+    ok, why = False, "did not finish"
     try:
         dev = torch.device("cuda:0")
         spec = ShardSpec(n_shards=world, depth=9, mean_per_bucket=6.0, seed=0x5A, good_pct=40, expired_pct=30)
@@ -323,12 +329,20 @@ def _query_worker(rank, world, port, q):
                 lo, idx, cnt = G.query(tg, count, home=home)
                 torch.cuda.synchronize()
                 m = idx.shape[0]
-                ok = ok and (m < targets.shape[0] if home else m == targets.shape[0])
-                ok = ok and np.array_equal(idx.cpu().numpy().view(np.uint32), want[lo:lo + m])
-                ok = ok and np.array_equal(cnt.cpu().numpy(), wcnt[lo:lo + m])
+                what = f"rank {rank} count {count} home {home} lo {lo} m {m}"
+                if not (m < targets.shape[0] if home else m == targets.shape[0]):
+                    ok, why = False, f"{what}: wrong row count"
+                bad_i = int((idx.cpu().numpy().view(np.uint32) != want[lo:lo + m]).any(1).sum())
+                bad_c = int((cnt.cpu().numpy() != wcnt[lo:lo + m]).sum())
+                if ok and (bad_i or bad_c):
+                    ok, why = False, f"{what}: {bad_i} rows and {bad_c} counts differ"
         G.close()
+        if ok:
+            why = ""
+    except Exception as e:  # reported through the queue
+        ok, why = False, f"rank {rank}: {type(e).__name__}: {e}"
     finally:
-        q.put((rank, bool(ok)))
+        q.put((rank, (bool(ok), why)))
         dist.destroy_process_group()
 
 
@@ -346,4 +360,4 @@ def test_global_shard_query_world2_gloo_gpu(gpu):
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    assert res == {0: True, 1: True}
+    assert res == {0: (True, ""), 1: (True, "")}, res

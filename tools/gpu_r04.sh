@@ -6,7 +6,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/$T
 mkdir -p $O
 cd $R
-timeout -k 10 400 python -u -m pytest tests/test_status_refresh.py tests/test_serve.py -x -v --timeout 200 --timeout-method thread > $O/pytest_focus.log 2>&1 || exit $?
+timeout -k 10 400 python -u -m pytest tests/test_status_refresh.py tests/test_global_shard.py tests/test_serve.py -x -v --timeout 200 --timeout-method thread > $O/pytest_focus.log 2>&1 || exit $?
 if [ "$2" != "quick" ]; then
   timeout -k 10 700 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread > $O/pytest_gpu.log 2>&1 || exit $?
 fi
