@@ -104,8 +104,10 @@ class Exchange:
         if home:
             # region k % 8 of a home range of ceil(nblk / world) query blocks: this capacity can never overflow
             self.row_cap_max = -(-(-(-nblk // world)) // REGIONS) * 256
-            # uniform targets: a source shard answers ~1/world of a home rank's ~q/world queries, ~exp per region
-            exp = -(-q // (REGIONS * world * world))
+            # uniform targets: a region holds the home range's blocks k with k % 8 == region (ceil(hb / 8) of
+            # them), a source shard answers ~1/world of each block's 256 queries
+            hb = -(-nblk // world)
+            exp = -(-(-(-hb // REGIONS) * 256) // world)
             est = exp + 6 * int(np.sqrt(exp)) + 32
             part_def = 256
         else:
@@ -146,7 +148,12 @@ class Exchange:
         if combine and self.home and self.world > 1:
             import torch.distributed as dist
 
-            dist.all_reduce(self.overflow, op=dist.ReduceOp.MAX, group=group)
+            if dist.get_backend(group) == "nccl":
+                dist.all_reduce(self.overflow, op=dist.ReduceOp.MAX, group=group)
+            else:  # gloo: through a host tensor (its device-tensor path does not order after the finish kernel)
+                h = self.overflow.cpu()
+                dist.all_reduce(h, op=dist.ReduceOp.MAX, group=group)
+                self.overflow.copy_(h)
         v = bool(int(self.overflow.item()))
         if v:
             self.overflow.zero_()
@@ -171,7 +178,8 @@ class Exchange:
             import torch
             import torch.distributed as dist
 
-            t = torch.tensor([need_r, need_p], dtype=torch.int64, device=self.dev)
+            nccl = dist.get_backend(group) == "nccl"
+            t = torch.tensor([need_r, need_p], dtype=torch.int64, device=self.dev if nccl else "cpu")
             dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
             need_r, need_p = (int(x) for x in t.cpu())
         row_cap = self.row_cap if need_r <= self.row_cap else max(2 * self.row_cap, need_r * 5 // 4)
@@ -305,8 +313,10 @@ class GlobalShard:
                 raise ValueError("a single rank must hold the whole table")
             if not single_rank_shard_kernel:
                 return 0, *self.table.rt_closest(targets, count, out_idx=out_idx, out_cnt=out_cnt)
+        self.tries = []  # (row_cap, part_cap) of every step of the last call
         while True:
             ex = self.exchange(q, count, world, home)
+            self.tries.append((ex.row_cap, ex.part_cap))
             self.step(targets, ex, out_idx, out_cnt, group, rank=rank)
             if not ex.overflowed(group):
                 return lo, out_idx, out_cnt

@@ -335,7 +335,18 @@ def _query_worker(rank, world, port, q):
                 bad_i = int((idx.cpu().numpy().view(np.uint32) != want[lo:lo + m]).any(1).sum())
                 bad_c = int((cnt.cpu().numpy() != wcnt[lo:lo + m]).sum())
                 if ok and (bad_i or bad_c):
-                    ok, why = False, f"{what}: {bad_i} rows and {bad_c} counts differ"
+                    j = int(np.flatnonzero((idx.cpu().numpy().view(np.uint32) != want[lo:lo + m]).any(1))[0])
+                    ok, why = False, (f"{what}: {bad_i} rows and {bad_c} counts differ; steps {G.tries}; row {j}: "
+                                      f"{idx[j].cpu().numpy().view(np.uint32)[:6].tolist()} cnt {int(cnt[j])} against "
+                                      f"{want[lo + j][:6].tolist()} cnt {int(wcnt[lo + j])}")
+                    # the same batch again with room for everything from the start (no growth)
+                    from opendht_amd.global_shard import Exchange
+                    G._ex[(targets.shape[0], count, world, home)] = Exchange(targets.shape[0], count, world, dev,
+                                                                             row_cap=1 << 20, part_cap=4096, home=home)
+                    _, idx2, cnt2 = G.query(tg, count, home=home)
+                    torch.cuda.synchronize()
+                    bad2 = int((idx2.cpu().numpy().view(np.uint32) != want[lo:lo + m]).any(1).sum())
+                    why += f"; with room from the start: {bad2} rows differ, steps {G.tries}"
         G.close()
         if ok:
             why = ""

@@ -146,3 +146,41 @@ def test_serve_limits_and_close(gpu):
         T.serve(2_000_000)  # idle above the limit
     check(T, t, targets[:64], (8,), tag=" after refused serve")
     T.close()  # ends the running launch, then frees the table
+
+
+def test_serve_refresh_latency_many_streams(gpu):
+    """A refresh that flips many nodes, then a served request, with more streams alive than the process has
+    hardware queues (GPU_MAX_HW_QUEUES = 4): the refresh ends the resident launch first, so neither the refresh nor
+    the request waits behind it for its idle period (50 ms here); the answers follow the refreshed table."""
+    t = TB.uniform_config(20_000, 11, seed=0x5E7)
+    n = t["ids"].shape[0]
+    targets = TB.adversarial_targets(t, extra=32)[:64]
+    rng = np.random.default_rng(7)
+    streams = [torch.cuda.Stream(device=gpu) for _ in range(8)]
+    for s in streams:  # every stream used once, so each holds a hardware queue slot
+        with torch.cuda.stream(s):
+            torch.ones(1024, device=gpu).sum()
+    torch.cuda.synchronize()
+    with make(t, gpu) as T:
+        now = 10**15
+        age = rng.integers(0, 20 * 60 * 10**9, n)
+        tm, rp, ex = now - age, np.full(n, now, np.int64), np.zeros(n, np.uint8)
+        T.set_times(tm, rp, ex)
+        T.refresh_status(now)
+        good = (tm >= now - 600 * 10**9) & (rp >= now - 7200 * 10**9)
+        t = dict(t, status=good.astype(np.uint8))
+        T.serve(50_000)
+        check(T, t, targets, (8,))
+        worst = 0.0
+        for dt in (60, 120, 300):  # seconds of ageing: thousands of nodes flip each time
+            now2 = now + dt * 10**9
+            t0 = time.perf_counter()
+            T.refresh_status(now2)
+            good = (tm >= now2 - 600 * 10**9) & (rp >= now2 - 7200 * 10**9)
+            t = dict(t, status=good.astype(np.uint8))
+            idx, cnt = served(T, targets, 8)
+            worst = max(worst, time.perf_counter() - t0)
+            want, wcnt = O.flat_rt_closest(t["ids"], t["status"], t["first"], t["off"], targets, 8)
+            np.testing.assert_array_equal(cnt, wcnt, err_msg=f"now+{dt}s counts")
+            np.testing.assert_array_equal(idx, want, err_msg=f"now+{dt}s indices")
+        assert worst < 0.030, f"refresh + served request took {worst * 1e3:.1f} ms (idle period 50 ms)"
