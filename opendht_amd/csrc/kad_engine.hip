@@ -5222,7 +5222,7 @@ __device__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* lds, uint32_t& to
 // The window good counts come from the per-bucket counts (gcnt), so nothing is O(buckets).
 // ---------------------------------------------------------------------------------------
 constexpr uint32_t RF_CAP = 2048;
-constexpr uint32_t RF_NB = 0, RF_NR = 1, RF_DONE = 2, RF_L8 = 3, RF_L16 = 4, RF_L32 = 5, RF_LNC = 6, RF_CTRS = 8;
+constexpr uint32_t RF_NB = 0, RF_NR = 1, RF_DONE = 2, RF_L8 = 3, RF_L16 = 4, RF_L32 = 5, RF_LNC = 6, RF_GO = 7, RF_CTRS = 8;
 
 struct RfCtx {
     NodeTimes N;
@@ -5243,10 +5243,19 @@ struct RfCtx {
     uint32_t* wl;                        // fused count <= 8 builds (rf_nodes_kernel FUSE): the line sets written
     uint32_t* ws;
     uint32_t* gl;
+    uint32_t* fl;                        // FUSE: the line list block 0 publishes to the builder blocks
+    uint32_t epoch;                      // FUSE: this refresh's value of ctr[RF_GO] (the list is published)
     uint32_t ninl;                       // > 0: the nodes are inl[0, ninl) (the host's copies of the runs), no lists
     uint32_t inl[16];
+    // with inline nodes, derived on the host from its copy of the bucket offsets (0: derived on the device):
+    uint32_t nhb;                        // the listed nodes' buckets, sorted and distinct
+    uint32_t hb[16];
+    uint32_t nhl;                        // FUSE 1: the window lines to rebuild, as nhr runs of consecutive lines:
+    uint32_t nhr;                        //   run r = lines hr[3r] .. hr[3r] + hr[3r+1] - 1, whose windows' bucket
+    uint32_t hr[3 * 16];                 //   offsets h_off[max(0, first - 3) ..] start at hoff[hr[3r+2]]
+    uint32_t hoff[256];
 };
-constexpr uint32_t RF_INLINE = 16;
+constexpr uint32_t RF_INLINE = 16, RF_HOFF = 256;
 
 // One atomic per wave for the lanes with `want` (wave-uniform call); returns each wanting lane's slot.
 __device__ __forceinline__ uint32_t wave_append(uint32_t* ctr, bool want) {
@@ -5347,16 +5356,24 @@ __device__ uint32_t block_union(uint32_t m, IV iv, uint32_t* out, uint32_t* lds4
 //   pairs >= 2 or a pair equal in all 64 bits -> defer; the first pair (in that order) whose keys differ
 //   -> the tie word. The short line's 23-bit slot fields are OR-ed into LDS words.
 // ---------------------------------------------------------------------------------------
+// LDS written by some lanes of a wave and read by others of the same wave: one wave's LDS accesses complete in
+// order, so only the compiler must not move accesses across this point (no hardware wait, in particular none on
+// the wave's outstanding global stores, which a workgroup-scope fence would drain).
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
 struct WaveLds {
-    uint64_t key[64];
-    uint32_t pk[64];   // per lane: stored bit 31 | D rank << 24 | key21
     uint32_t L[32];    // the 128-byte line
     uint32_t S16[16];  // the short line
     uint32_t dx[8];    // first nodes of the staged buckets
     uint32_t R[33 + 17];  // rows of the serial fallback (a window of more than 64 nodes)
 };
 
-__device__ void wl_ws_build_wave(uint32_t b, uint32_t B, uint32_t d, uint64_t pre0, uint32_t db, const uint32_t* dx,
+__device__ __attribute__((always_inline)) void wl_ws_build_wave(uint32_t b, uint32_t B, uint32_t d, uint64_t pre0,
+                                                                  uint32_t db, const uint32_t* dx,
                                  uint32_t n0, uint32_t n1, uint64_t key, uint32_t stat, uint32_t* wl_out,
                                  uint32_t* ws_out, WaveLds& W) {
     const uint32_t lane = threadIdx.x & 63u;
@@ -5395,75 +5412,64 @@ __device__ void wl_ws_build_wave(uint32_t b, uint32_t B, uint32_t d, uint64_t pr
     if (R8 == 3) {
         if (lane == 0) { W.L[1] = WL_DEFER; W.L[3] = 0; }
     } else {
-        const uint32_t lo = b > R8 ? b - 1 - R8 : 0u, hi = min(B - 1, b + R8), nb = hi - lo + 1;
+        const uint32_t lo = b > R8 ? b - 1 - R8 : 0u, hi = min(B - 1, b + R8), nb = hi - lo + 1;  // nb <= 6
         base = dx[lo - db];
-        // D rank of every window bucket, the stored prefix (whole buckets in D order while they fit)
-        uint32_t rank_of[6], start_of[6];
-        bool stored_of[6];
-        bool full = false;
-        for (uint32_t j = 0; j < nb; j++) {
-            uint32_t xj = lo;
-            for (uint32_t y = lo; y <= hi; y++) {
-                uint32_t rk = 0;
-                for (uint32_t z = lo; z <= hi; z++) rk += ((pre0 + z) ^ (pre0 + b)) < ((pre0 + y) ^ (pre0 + b));
-                if (rk == j) xj = y;
-            }
-            rounds |= (xj >= b ? xj - b : b - 1 - xj) << (2 * j);
-            const uint32_t gj = cnt_of(xj);
-            rank_of[xj - lo] = j;
-            stored_of[xj - lo] = false;
-            start_of[xj - lo] = 0;
-            if (full || S + gj > WL_SLOTS) { full = true; continue; }
-            stored_of[xj - lo] = true;
-            start_of[xj - lo] = S;
-            S += gj;
+        // lane y < nb holds window bucket lo + y: its D rank (the order of (pre0 + y) ^ (pre0 + b)), its good
+        // count, and the stored prefix in D order (whole buckets while the cumulative count fits WL_SLOTS)
+        const uint32_t yb = lo + min(lane, nb - 1);
+        const uint64_t dy = (pre0 + yb) ^ (pre0 + b);
+        uint32_t ry = 0;
+        for (uint32_t z = 0; z < nb; z++) ry += ((pre0 + lo + z) ^ (pre0 + b)) < dy;
+        const uint32_t cy = cnt_of(yb);
+        uint32_t excl = 0;
+        for (uint32_t z = 0; z < nb; z++) excl += rdl(ry, z) < ry ? rdl(cy, z) : 0u;
+        const bool sty = lane < nb && excl + cy <= WL_SLOTS;
+        const uint32_t rb = lane < nb ? (yb >= b ? yb - b : b - 1 - yb) << (2 * ry) : 0u, sS = sty ? excl + cy : 0u;
+        for (uint32_t z = 0; z < nb; z++) {  // (wave-uniform reads of the nb bucket lanes)
+            rounds |= rdl(rb, z);
+            S = max(S, rdl(sS, z));
         }
-        // my slot
+        const uint32_t info_y = (sty ? 0x80000000u : 0u) | (ry << 24) | excl;
+        // my slot: my bucket's rank and start, my rank among its stored nodes (its nodes are consecutive lanes)
         const bool inw = good && x >= lo && x <= hi;
-        uint32_t rj = 0, st0 = 0;
-        bool sto = false;
-        for (uint32_t i = 0; i < nb; i++)
-            if (inw && x == lo + i) { rj = rank_of[i]; st0 = start_of[i]; sto = stored_of[i]; }
-        const bool mine = inw && sto;
+        const uint32_t info = (uint32_t)__shfl((int)info_y, (int)(inw ? x - lo : 0u), 64);
+        const bool mine = inw && (info >> 31);
+        const uint32_t rj = (info >> 24) & 7u, st0 = info & 0xFFFFFFu;
         const uint32_t k21 = (uint32_t)((key << d) >> (64 - WL_KBITS)), off = n - base;
-        uint32_t inb = 0;  // stored good nodes of my bucket below me (index order)
-        for (uint32_t i = 0; i < nb; i++) {
-            const uint64_t m = __ballot(mine && x == lo + i);
-            if (mine && x == lo + i) inb = (uint32_t)__builtin_popcountll(m & below);
-        }
+        const uint64_t mm = __ballot(mine);
+        const uint32_t fl = inw ? dx[x - db] - n0 : 0u;  // first lane of my bucket
+        const uint32_t inb = (uint32_t)__builtin_popcountll(mm & below & ~((1ull << fl) - 1ull));
         defer = __any(mine && off > 255u);
-        W.pk[lane] = mine ? (0x80000000u | (rj << 24) | k21) : 0u;
-        W.key[lane] = key;
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
-        __builtin_amdgcn_wave_barrier();
-        // pairs: earlier stored nodes of my bucket (lower lanes, same D rank) with my key21
+        // pairs: earlier stored nodes of my bucket (lower lanes, same D rank) with my key21, in lane order
+        const uint32_t mypk = mine ? (0x80000000u | (rj << 24) | k21) : 0u;
         uint32_t pairs = 0, my_tie = 0;
         bool zero = false, have_tie = false;
-        if (mine) {
-            for (uint32_t l2 = 0; l2 < lane; l2++) {
-                const uint32_t v = W.pk[l2];
-                if (v != (0x80000000u | (rj << 24) | k21)) continue;
+        for (uint64_t m = mm; m; m &= m - 1) {  // wave-uniform, at most WL_SLOTS stored lanes
+            const uint32_t l2 = (uint32_t)__builtin_ctzll(m);
+            const uint32_t v = rdl(mypk, l2);
+            const uint64_t k2 = rdl64(key, l2);
+            if (mine && l2 < lane && v == mypk) {
                 pairs++;
-                const uint64_t x64 = key ^ W.key[l2];
-                if (x64 == 0) { zero = true; continue; }
-                if (!have_tie) {
+                const uint64_t x64 = key ^ k2;
+                if (x64 == 0) {
+                    zero = true;
+                } else if (!have_tie) {
                     const uint32_t p = (uint32_t)__builtin_clzll(x64), bn = (uint32_t)(key >> (63 - p)) & 1u;
                     my_tie = WL_DEFER | (bn << 30) | (p << 16) | (((n0 + l2 - base) & 255u) << 8) | (off & 255u);
                     have_tie = true;
                 }
             }
         }
-        uint32_t tp = pairs;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) tp += __shfl_xor(tp, o, 64);
-        defer = defer || tp >= 2 || __any(zero);
+        // two pairs or more in the line, or a pair equal in all 64 bits: defer
+        defer = defer || __any(zero) || __any(pairs >= 2) || __builtin_popcountll(__ballot(pairs >= 1)) >= 2;
         // the tie of the first pair in processing order (D rank, then node index)
-        const uint32_t keyt = have_tie ? (rj << 8) | lane : NONE;
-        uint32_t mk = keyt;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) mk = min(mk, (uint32_t)__shfl_xor(mk, o, 64));
-        if (mk != NONE) tie = rdl(my_tie, mk & 255u);
+        for (uint32_t r = 0; r < nb; r++) {  // wave-uniform
+            const uint64_t tm = __ballot(have_tie && rj == r);
+            if (tm) {
+                tie = rdl(my_tie, (uint32_t)__builtin_ctzll(tm));
+                break;
+            }
+        }
         if (mine) W.L[WL_SLOT0 + st0 + inb] = (rj << 29) | (k21 << 8) | (off & 255u);
         if (lane == 0) {
             W.L[0] = base;
@@ -5472,9 +5478,7 @@ __device__ void wl_ws_build_wave(uint32_t b, uint32_t B, uint32_t d, uint64_t pr
         }
     }
     if (lane == 0 && R8 != 3) W.L[1] = h | (R8 << 21) | (S << 23) | (defer ? WL_DEFER : 0u);
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
-    __builtin_amdgcn_wave_barrier();
+    wave_lds_sync();
     if (lane < 8) reinterpret_cast<uint4*>(wl_out + 32ull * b)[lane] =
         make_uint4(W.L[4 * lane], W.L[4 * lane + 1], W.L[4 * lane + 2], W.L[4 * lane + 3]);
     if (!ws_out) return;
@@ -5482,38 +5486,33 @@ __device__ void wl_ws_build_wave(uint32_t b, uint32_t B, uint32_t d, uint64_t pr
     const uint32_t hh = W.L[1], rnd = W.L[2], SS = (hh >> 23) & 31u;
     bool fb = (hh & WL_DEFER) != 0;
     const uint32_t vs = lane < SS ? W.L[WL_SLOT0 + lane] : 0u;
-    const bool endb = lane < SS && lane < WS_SLOTS && (lane + 1 == SS || (W.L[WL_SLOT0 + lane + 1] >> 29) != (vs >> 29));
-    uint32_t keep = endb ? lane + 1 : 0u;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) keep = max(keep, (uint32_t)__shfl_xor(keep, o, 64));
+    const uint32_t vnext = (uint32_t)__shfl_down((int)vs, 1, 64), vprev = (uint32_t)__shfl_up((int)vs, 1, 64);
+    const bool endb = lane < SS && lane < WS_SLOTS && (lane + 1 == SS || (vnext >> 29) != (vs >> 29));
+    const uint64_t em = __ballot(endb);
+    const uint32_t keep = em ? 64u - (uint32_t)__builtin_clzll(em) : 0u;  // the last bucket end + 1
     constexpr uint32_t KSH = 8 + WL_KBITS - WS_KBITS;
     const bool ks = lane < keep;
     const uint32_t jj = vs >> 29, k16 = (vs >> KSH) & 0xFFFFu, offs = vs & 255u;
     bool f = ks && offs >= 64u;
-    if (ks)
-        for (uint32_t r = 0; r < lane; r++) {
-            const uint32_t u = W.L[WL_SLOT0 + r];
-            f |= (u >> 29) == jj && ((u >> KSH) & 0xFFFFu) == k16;
-        }
+    for (uint32_t r = 0; r < keep; r++) {  // wave-uniform: an earlier slot of the same bucket with my key16
+        const uint32_t u = rdl(vs, r);
+        f |= ks && r < lane && (u >> 29) == jj && ((u >> KSH) & 0xFFFFu) == k16;
+    }
     fb = fb || __any(f);
-    const bool start = ks && (lane == 0 || (W.L[WL_SLOT0 + lane - 1] >> 29) != jj);
+    const bool start = ks && (lane == 0 || (vprev >> 29) != jj);
     const uint64_t sm = __ballot(start);
-    uint32_t rk = start ? ((rnd >> (2 * jj)) & 3u) << (2 * (uint32_t)__builtin_popcountll(sm & below)) : 0u;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) rk |= __shfl_xor(rk, o, 64);
+    uint32_t rk = 0, kb = 0;
+    for (uint64_t m = sm; m; m &= m - 1, kb++)  // wave-uniform: the rounds of the kept buckets, in slot order
+        rk |= ((rnd >> (2 * rdl(jj, (uint32_t)__builtin_ctzll(m)))) & 3u) << (2 * kb);
     if (lane < 16) W.S16[lane] = 0;
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
-    __builtin_amdgcn_wave_barrier();
+    wave_lds_sync();
     if (ks) {  // the slot's 23 bits at bit WS_SLOT0 + 23 * lane
         const uint32_t v = (start ? 1u << 22 : 0u) | (k16 << 6) | offs, p = WS_SLOT0 + WS_SBITS * lane;
         const uint64_t w = (uint64_t)v << (p & 31);
         atomicOr(&W.S16[p >> 5], (uint32_t)w);
         if ((p & 31) + WS_SBITS > 32) atomicOr(&W.S16[(p >> 5) + 1], (uint32_t)(w >> 32));
     }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
-    __builtin_amdgcn_wave_barrier();
+    wave_lds_sync();
     if (lane < 16) {
         const uint32_t G0 = min(hh & 63u, 15u), G1 = min((hh >> 6) & 63u, 15u), G2 = min((hh >> 12) & 63u, 15u);
         const uint32_t hw = G0 | (G1 << 4) | (G2 << 8) | (((hh >> 18) & 7u) << 12) | (((hh >> 21) & 3u) << 15) |
@@ -5533,9 +5532,7 @@ __device__ void wl_ws_build_wave(uint32_t b, uint32_t B, uint32_t d, uint64_t pr
         }
         W.S16[lane] = v;
     }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
-    __builtin_amdgcn_wave_barrier();
+    wave_lds_sync();
     if (lane < 4) reinterpret_cast<uint4*>(ws_out + 16ull * b)[lane] =
         make_uint4(W.S16[4 * lane], W.S16[4 * lane + 1], W.S16[4 * lane + 2], W.S16[4 * lane + 3]);
 }
@@ -5555,9 +5552,7 @@ __global__ __launch_bounds__(BLOCK) void wl_ws_wave_kernel(const uint64_t* __res
         if (!sel.pick(x, B, b)) return;
         const uint32_t db = b >= 3 ? b - 3 : 0u, e = min(B, b + 3);
         if (db + lane <= e && lane < 8) WV.dx[lane] = dir[db + lane].x & ~WIDE;
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
-        __builtin_amdgcn_wave_barrier();
+        wave_lds_sync();
         const uint32_t n0 = WV.dx[0], n1 = WV.dx[e - db];
         if (n1 - n0 <= 64) {
             const bool have = n0 + lane < n1;
@@ -5568,17 +5563,18 @@ __global__ __launch_bounds__(BLOCK) void wl_ws_wave_kernel(const uint64_t* __res
             wl_build_line(key, status, dir, gcnt, B, d, pre0, wl, b, WV.R);
             if (ws) ws_build_line(WV.R, ws, b, WV.R + 33);
         }
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
-        __builtin_amdgcn_wave_barrier();
+        wave_lds_sync();
     }
 }
 
 // SINGLE: one block (at most BLOCK listed nodes): the appends go to LDS and there is no completion counter.
-// FUSE: the count <= 8 lines of the changed buckets are rebuilt by this block too (1: window lines and their
-// short copies, 2: general lines; the host fuses when at most RF_FUSE_LINES can be listed), so a refresh
-// that passes a few deadlines is one launch.
-constexpr uint32_t RF_FUSE_LINES = 64;
+// FUSE (implies SINGLE): the count <= 8 lines of the changed buckets are rebuilt in the same launch (1: window
+// lines and their short copies, a wave per line; 2: general lines, a 16-lane group per line; the host fuses
+// when at most RF_FUSE_LINES can be listed), so a refresh that passes a few deadlines is one launch. Block 0
+// derives the nodes and the list, publishes it (ctr[RF_GO] = epoch, release at agent scope) and builds its share;
+// blocks 1.. wait for the epoch (dispatched after block 0, so it is always resident) and build the rest, all
+// lines in one round.
+constexpr uint32_t RF_FUSE_LINES = 256;
 
 // p - n as a generic (flat) pointer: p[n + i] is then p[i] for the callee, whatever the address space of p.
 template <class T>
@@ -5587,11 +5583,268 @@ __device__ __forceinline__ const T* flat_shift(const T* p, uint32_t n) {
 }
 constexpr uint32_t RF_POOL = BLOCK * (33 + 17);  // dwords: phase 2's sort buffers, then phase 3's line rows
 
+// KAD_RF_TRACE (diagnostic builds only): thread 0 of the phase-2 block stamps the device wall clock at the phase
+// boundaries and prints them (tools/rf_trace.py).
+#ifdef KAD_RF_TRACE
+#define RF_STAMP(k) do { if (threadIdx.x == 0) rf_ts[k] = wall_clock64(); } while (0)
+#else
+#define RF_STAMP(k) do { } while (0)
+#endif
+
+// Builder blocks of a fused window-line refresh (FUSE 1, blocks 1..): independent of block 0. Wave 0 derives
+// the listed nodes' new statuses itself (as phase 1 does) and the lines that can read their buckets (the union of
+// [b-2, b+3], as phase 2's list: sorted and merged across the wave); every wave then builds lines of that list
+// (wl_ws_build_wave) with the listed nodes' statuses taken from the derived values, so no line waits for block 0's
+// status writes. Only a window of more than 64 nodes (the serial builder, which reads the table's statuses and
+// good counts) waits for block 0's epoch (published after its good counts). Unchanged nodes in the list rebuild
+// lines that come out identical.
+__device__ void rf_wl_builders(const RfCtx& C, uint32_t* pool) {
+    const DevTable& T = C.T;
+    const uint32_t B = T.B, lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
+    const uint32_t total = C.ninl ? C.ninl : C.mc + C.sc + C.np;  // <= 64 (the host fuses at 6 * total <= 256)
+    static_assert(4 * sizeof(WaveLds) <= 4 * RF_POOL, "builder wave buffers");
+    if (C.nhl) {  // the host's lines and offsets: one round of loads (window keys and statuses, listed nodes' times)
+        WaveLds& WV = reinterpret_cast<WaveLds*>(pool)[wid];
+        for (uint32_t x = (blockIdx.x - 1) * (BLOCK / 64) + wid; x < C.nhl; x += (gridDim.x - 1) * (BLOCK / 64)) {
+            uint32_t r = 0, k = x;  // the run of line x (wave-uniform)
+            while (r + 1 < C.nhr && k >= C.hr[3 * r + 1]) k -= C.hr[3 * r + 1], r++;
+            const uint32_t first = C.hr[3 * r], b = first + k, db = b >= 3 ? b - 3 : 0u, e = min(B, b + 3);
+            const uint32_t* hl = C.hoff + C.hr[3 * r + 2] + (db - (first >= 3 ? first - 3 : 0u));  // offsets of db ..
+            const uint32_t n0 = hl[0], n1 = hl[e - db];
+            if (n1 - n0 <= 64) {
+                if (lane < 8) WV.dx[lane] = hl[min(lane, e - db)];
+                const uint32_t n = n0 + lane;
+                const bool have = n < n1;
+                bool listed = false;
+                for (uint32_t j = 0; j < C.ninl; j++) listed |= C.inl[j] == n;
+#ifdef KAD_RF_TRACE
+                const uint64_t tb0 = wall_clock64();
+#endif
+                const uint64_t kk = have ? T.key[n] : 0ull;
+                const uint32_t sv = !have ? 0u : listed ? status_at(C.N, n, C.now) : (uint32_t)C.status[n];
+                wave_lds_sync();
+#ifdef KAD_RF_TRACE
+                __builtin_amdgcn_s_waitcnt(0);
+                const uint64_t tb1 = wall_clock64();
+#endif
+                wl_ws_build_wave(b, B, 64 - T.rshift, T.rbase >> T.rshift, db, WV.dx, n0, n1, kk, sv, C.wl, C.ws, WV);
+#ifdef KAD_RF_TRACE
+                const uint64_t tb2 = wall_clock64();
+                __builtin_amdgcn_s_waitcnt(0);
+                const uint64_t tb3 = wall_clock64();
+                if (lane == 0)
+                    printf("RFWAVE blk=%u wave=%u line=%u nodes=%u loads=%llu build=%llu drain=%llu at=%llu\n", blockIdx.x,
+                           wid, b, n1 - n0, (unsigned long long)(tb1 - tb0), (unsigned long long)(tb2 - tb1),
+                           (unsigned long long)(tb3 - tb2), (unsigned long long)tb0);
+#endif
+            } else if (lane == 0) {  // serial build from the table: wait for block 0's statuses and good counts
+                const uint64_t t0 = wall_clock64();
+                bool go = true;
+                while (__hip_atomic_load(C.ctr + RF_GO, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != C.epoch) {
+                    __builtin_amdgcn_s_sleep(1);
+                    if (wall_clock64() - t0 > 100000000ull) { go = false; break; }
+                }
+                if (go) {
+                    wl_build_line(T.key, C.status, C.dir, C.gcnt, B, 64 - T.rshift, T.rbase >> T.rshift, C.wl, b, WV.R);
+                    if (C.ws) ws_build_line(WV.R, C.ws, b, WV.R + 33);
+                }
+            }
+            wave_lds_sync();
+        }
+        return;
+    }
+    __shared__ uint32_t s_node[64];
+    __shared__ uint32_t s_st[64];
+    __shared__ uint32_t s_lines[RF_FUSE_LINES];
+    __shared__ uint32_t s_nl;
+    if (wid == 0) {
+        const bool act = lane < total;
+        uint32_t i = NONE, st = 0, b = NONE;
+        if (act)
+            i = C.ninl ? C.inl[lane] : lane < C.mc ? C.mnode[lane] : lane < C.mc + C.sc ? C.snode[lane - C.mc]
+                                                                                       : C.pend[lane - C.mc - C.sc];
+        if (act && i < T.n) {
+            const uint64_t key_i = T.key[i];
+            st = (!C.ninl && C.vals && lane >= C.mc + C.sc)
+                     ? (uint32_t)(C.vals[lane - C.mc - C.sc] & (KAD_STATUS_GOOD | KAD_STATUS_EXPIRED))
+                     : status_at(C.N, i, C.now);
+            b = node_bucket(T, C.dir, i, key_i);
+        } else {
+            i = NONE;
+        }
+        s_node[lane] = i;
+        s_st[lane] = st;
+        // the buckets sorted across the wave (bitonic; NONE last), then each distinct one's [b-2, b+3] merged
+        uint32_t v = b;
+#pragma unroll
+        for (uint32_t k = 2; k <= 64; k <<= 1)
+#pragma unroll
+            for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+                const uint32_t u = (uint32_t)__shfl_xor((int)v, (int)j, 64);
+                v = (((lane & j) == 0) == ((lane & k) == 0)) ? min(v, u) : max(v, u);
+            }
+        const uint32_t pv = (uint32_t)__shfl_up((int)v, 1, 64);
+        const bool keep = v != NONE && (lane == 0 || v != pv);
+        const uint32_t a0 = keep ? (v > 2 ? v - 2 : 0u) : 0u, e1 = keep ? min(B - 1, v + 3) + 1 : 0u;
+        uint32_t mx = e1;  // inclusive running max of the interval ends (+1) in lane order
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)mx, o, 64);
+            if (lane >= (uint32_t)o) mx = max(mx, y);
+        }
+        uint32_t before = (uint32_t)__shfl_up((int)mx, 1, 64);
+        if (lane == 0) before = 0;
+        const uint32_t s0 = max(a0, before), cnt = keep && e1 > s0 ? e1 - s0 : 0u;
+        uint32_t off = cnt;  // inclusive sum, then exclusive
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)off, o, 64);
+            if (lane >= (uint32_t)o) off += y;
+        }
+        const uint32_t nl = rdl(off, 63);
+        off -= cnt;
+        for (uint32_t k = 0; k < cnt; k++)
+            if (off + k < RF_FUSE_LINES) s_lines[off + k] = s0 + k;
+        if (lane == 0) s_nl = min(nl, RF_FUSE_LINES);
+    }
+    __syncthreads();
+    const uint32_t nl = s_nl;
+    WaveLds& WV = reinterpret_cast<WaveLds*>(pool)[wid];
+    const uint32_t nbuild = gridDim.x - 1;
+    for (uint32_t x = (blockIdx.x - 1) * (BLOCK / 64) + wid; x < nl; x += nbuild * (BLOCK / 64)) {  // wave-uniform
+        const uint32_t b = s_lines[x], db = b >= 3 ? b - 3 : 0u, e = min(B, b + 3);
+        if (db + lane <= e && lane < 8) WV.dx[lane] = C.dir[db + lane].x & ~WIDE;
+        wave_lds_sync();
+        const uint32_t n0 = WV.dx[0], n1 = WV.dx[e - db];
+        if (n1 - n0 <= 64) {
+            const bool have = n0 + lane < n1;
+            const uint64_t kk = have ? T.key[n0 + lane] : 0ull;
+            uint32_t sv = have ? C.status[n0 + lane] : 0u;
+            for (uint32_t j = 0; j < total; j++) {  // the listed nodes' derived statuses
+                const uint32_t nj = s_node[j];
+                if (nj != NONE && nj - n0 == lane) sv = s_st[j];
+            }
+            wl_ws_build_wave(b, B, 64 - T.rshift, T.rbase >> T.rshift, db, WV.dx, n0, n1, kk, sv, C.wl, C.ws, WV);
+        } else if (lane == 0) {  // serial build from the table: wait for block 0's statuses and good counts
+            const uint64_t t0 = wall_clock64();
+            bool go = true;
+            while (__hip_atomic_load(C.ctr + RF_GO, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != C.epoch) {
+                __builtin_amdgcn_s_sleep(1);
+                if (wall_clock64() - t0 > 100000000ull) { go = false; break; }
+            }
+            if (go) {
+                wl_build_line(T.key, C.status, C.dir, C.gcnt, B, 64 - T.rshift, T.rbase >> T.rshift, C.wl, b, WV.R);
+                if (C.ws) ws_build_line(WV.R, C.ws, b, WV.R + 33);
+            }
+        }
+        wave_lds_sync();
+    }
+}
+
+// Phase 3 of a fused general-line refresh (FUSE 2): lines l8[x] for x = this block's share (blockIdx.x, stride
+// gridDim.x), after block 0 published the list.
+template <int FUSE>
+__device__ void rf_fused_lines(const RfCtx& C, uint32_t* pool, uint32_t n8, const uint32_t* l8) {
+    const DevTable& T = C.T;
+    const uint32_t B = T.B;
+    if (FUSE == 2) {
+        // phase 3: the count <= 8 general lines of the list, RF_GROUP lanes per line (the pool's sort buffers are free now).
+        // A line reads only W(2) = [b-3, b+2] (its bucket counts, directory entries up to b+3 and their nodes),
+        // which the group stages in LDS in two rounds of parallel loads; its first lane then builds the line from
+        // there (a window larger than RF_WCAP nodes is read from HBM). A line built straight from HBM waits
+        // for ~10 dependent loads (one per bucket of its window, and the keys eight at a time).
+        constexpr uint32_t RF_GROUP = 16, NG = BLOCK / RF_GROUP, RF_WCAP = 128;
+        static_assert(NG * (2 * RF_WCAP + RF_WCAP / 4 + 16 + 8 + 33 + 17) <= RF_POOL, "phase 3 staging");
+        uint64_t* skey = reinterpret_cast<uint64_t*>(pool);                        // NG x RF_WCAP keys
+        uint8_t* sst = reinterpret_cast<uint8_t*>(pool + NG * 2 * RF_WCAP);        // NG x RF_WCAP status bytes
+        uint2* sdir = reinterpret_cast<uint2*>(pool + NG * (2 * RF_WCAP + RF_WCAP / 4));  // NG x 8
+        uint32_t* sgc = pool + NG * (2 * RF_WCAP + RF_WCAP / 4 + 16);               // NG x 8
+        uint32_t* rows = sgc + NG * 8;                                              // NG x (33 + 17)
+        const uint32_t g = threadIdx.x / RF_GROUP, gl = threadIdx.x % RF_GROUP;
+        for (uint32_t x0 = blockIdx.x * NG; x0 < n8; x0 += gridDim.x * NG) {  // block-uniform
+            const uint32_t x = x0 + g;
+            const bool act = x < n8;
+            const uint32_t b = act ? l8[x] : 0u, db = b >= 3 ? b - 3 : 0u;
+            // round 1: the counts of [db, db + 6) and the directory entries [db, db + 7)
+            if (act && gl < 6 && db + gl < B) sgc[8 * g + gl] = C.gcnt[db + gl];
+            if (act && gl >= 6 && gl < 13 && db + gl - 6 <= B) sdir[8 * g + gl - 6] = C.dir[db + gl - 6];
+            __syncthreads();
+            // round 2: the keys and status bytes of the nodes of buckets [db, min(B - 1, b + 2)]
+            const uint32_t e = min(B, b + 3);
+            const uint32_t n0 = sdir[8 * g].x & ~WIDE, n1 = sdir[8 * g + (e - db)].x & ~WIDE;
+            const bool staged = act && n1 - n0 <= RF_WCAP;
+            if (staged) {
+#pragma unroll
+                for (uint32_t k = 0; k < RF_WCAP / RF_GROUP; k++) {
+                    const uint32_t o = gl + RF_GROUP * k;
+                    if (o < n1 - n0) {
+                        skey[RF_WCAP * g + o] = T.key[n0 + o];
+                        sst[RF_WCAP * g + o] = C.status[n0 + o];
+                    }
+                }
+            }
+            __syncthreads();
+            if (act && gl == 0) {
+                // the staged copies as views indexed like the arrays (every index the build uses lies in W(2)):
+                // the shift is applied to the generic address (an LDS-space pointer shifted below its base would
+                // wrap in 32 bits and leave the LDS aperture once converted)
+                const uint64_t* kp = staged ? flat_shift(skey + RF_WCAP * g, n0) : T.key;
+                const uint8_t* sp = staged ? flat_shift(sst + RF_WCAP * g, n0) : C.status;
+                const uint2* dp = flat_shift(sdir + 8 * g, db);
+                const uint32_t* gp = flat_shift(sgc + 8 * g, db);
+                uint32_t* rowA = rows + 50 * g;
+                gl8_build_line(kp, sp, dp, gp, T.fkey, T.ftail, B, C.gl, b, rowA);
+            }
+            __syncthreads();
+        }
+    }
+}
+
 template <bool SINGLE, int FUSE>
 __global__ __launch_bounds__(BLOCK) void rf_nodes_kernel(RfCtx C) {
+    static_assert(!FUSE || SINGLE, "a fused refresh derives its nodes in block 0");
     const DevTable& T = C.T;
+#ifdef KAD_RF_TRACE
+    uint64_t rf_ts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
+    RF_STAMP(0);
     __shared__ __attribute__((aligned(16))) uint32_t pool[RF_POOL];
     __shared__ uint32_t lctr[2];
+    if (FUSE == 1 && blockIdx.x > 0) {  // a window-line builder block (independent of block 0)
+        rf_wl_builders(C, pool);
+#ifdef KAD_RF_TRACE
+        __syncthreads();
+        RF_STAMP(2);
+        if (threadIdx.x == 0)
+            printf("RFBUILD blk=%u start=%llu go=%llu end=%llu\n", blockIdx.x, (unsigned long long)rf_ts[0],
+                   (unsigned long long)rf_ts[0], (unsigned long long)rf_ts[2]);
+#endif
+        return;
+    }
+    if (FUSE == 2 && blockIdx.x > 0) {  // a general-line builder block: wait for block 0's list (block-uniform)
+        if (threadIdx.x == 0) {
+            // bounded (1 s of the 100 MHz wall clock): a list that never comes leaves the lines alone, no hang
+            const uint64_t t0 = wall_clock64();
+            bool go = true;
+            while (__hip_atomic_load(C.ctr + RF_GO, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != C.epoch) {
+                __builtin_amdgcn_s_sleep(1);
+                if (wall_clock64() - t0 > 100000000ull) { go = false; break; }
+            }
+            lctr[0] = go ? __hip_atomic_load(C.ctr + RF_L8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+        }
+        __syncthreads();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        RF_STAMP(1);
+        rf_fused_lines<FUSE>(C, pool, lctr[0], C.fl);
+#ifdef KAD_RF_TRACE
+        __syncthreads();
+        RF_STAMP(2);
+        if (threadIdx.x == 0)
+            printf("RFBUILD blk=%u start=%llu go=%llu end=%llu\n", blockIdx.x, (unsigned long long)rf_ts[0],
+                   (unsigned long long)rf_ts[1], (unsigned long long)rf_ts[2]);
+#endif
+        return;
+    }
     uint64_t* srt = reinterpret_cast<uint64_t*>(pool);  // RF_CAP (phase 2)
     uint32_t* ub = pool + 2 * RF_CAP;                     // RF_CAP (phase 2)
     uint32_t* lb_ = SINGLE ? pool + 3 * RF_CAP : nullptr; // BLOCK appended buckets (phase 1, single block)
@@ -5610,14 +5863,14 @@ __global__ __launch_bounds__(BLOCK) void rf_nodes_kernel(RfCtx C) {
         }
         uint64_t key_i = 0;
         if (act) {
-            if (T.B) key_i = T.key[i];  // issued with the times: the locate needs it only if the good bit flips
+            if (T.B && !C.nhb) key_i = T.key[i];  // issued with the times: the locate needs it only if the good bit flips
             st = (!C.ninl && C.vals && j >= C.mc + C.sc)
                      ? (uint32_t)(C.vals[j - C.mc - C.sc] & (KAD_STATUS_GOOD | KAD_STATUS_EXPIRED))
                      : status_at(C.N, i, C.now);
             old = C.status[i];
             if (st != old) C.status[i] = (uint8_t)st;
         }
-        const bool gchg = act && T.B && ((st ^ old) & KAD_STATUS_GOOD);
+        const bool gchg = act && T.B && !C.nhb && ((st ^ old) & KAD_STATUS_GOOD);  // (nhb: the host's buckets)
         const uint32_t b = gchg ? node_bucket(T, C.dir, i, key_i) : 0u;
         const bool echg = act && C.list[3] && ((st ^ old) & KAD_STATUS_EXPIRED);
         uint32_t sa = 0, se = 0;
@@ -5660,6 +5913,7 @@ __global__ __launch_bounds__(BLOCK) void rf_nodes_kernel(RfCtx C) {
         blist = C.blist;
         nrange = C.nrange;
     }
+    RF_STAMP(1);
     __shared__ uint32_t lds4[4];
     __shared__ uint32_t l8[FUSE ? RF_FUSE_LINES : 1];
     __shared__ uint32_t n8_s;
@@ -5682,23 +5936,33 @@ __global__ __launch_bounds__(BLOCK) void rf_nodes_kernel(RfCtx C) {
         nrs = n;
     }
     (void)nrs;
-    // buckets: sort, unique
-    uint32_t P = 1;
-    while (P < nb) P <<= 1;
-    __syncthreads();
-    for (uint32_t x = threadIdx.x; x < P; x += BLOCK) srt[x] = x < nb ? (uint64_t)blist[x] : ~0ull;
-    __syncthreads();
-    block_sort_u64(srt, P);
+    RF_STAMP(2);
+    // buckets: sort, unique (or the host's list: every listed node's bucket, changed or not; a recount of an
+    // unchanged bucket and a rebuild of its lines give the same values)
     uint32_t nu = 0;
-    for (uint32_t c = 0; c < nb; c += BLOCK) {
-        const uint32_t x = c + threadIdx.x;
-        const bool keep = x < nb && (x == 0 || srt[x] != srt[x - 1]);
-        uint32_t tot;
-        const uint32_t off = block_exclusive_scan(keep ? 1u : 0u, lds4, tot);
-        if (keep) ub[nu + off] = (uint32_t)srt[x];
-        nu += tot;
+    if (C.nhb) {  // block-uniform
+        __syncthreads();
+        if (threadIdx.x < C.nhb) ub[threadIdx.x] = C.hb[threadIdx.x];
+        nu = C.nhb;
+        __syncthreads();
+    } else {
+        uint32_t P = 1;
+        while (P < nb) P <<= 1;
+        __syncthreads();
+        for (uint32_t x = threadIdx.x; x < P; x += BLOCK) srt[x] = x < nb ? (uint64_t)blist[x] : ~0ull;
+        __syncthreads();
+        block_sort_u64(srt, P);
+        for (uint32_t c = 0; c < nb; c += BLOCK) {
+            const uint32_t x = c + threadIdx.x;
+            const bool keep = x < nb && (x == 0 || srt[x] != srt[x - 1]);
+            uint32_t tot;
+            const uint32_t off = block_exclusive_scan(keep ? 1u : 0u, lds4, tot);
+            if (keep) ub[nu + off] = (uint32_t)srt[x];
+            nu += tot;
+        }
+        __syncthreads();
     }
-    __syncthreads();
+    RF_STAMP(3);
     // their masks and good counts (bucket_good_kernel for these buckets)
     for (uint32_t u = threadIdx.x; u < nu; u += BLOCK) {
         const uint32_t b = ub[u];
@@ -5712,19 +5976,26 @@ __global__ __launch_bounds__(BLOCK) void rf_nodes_kernel(RfCtx C) {
         C.gcnt[b] = g;
         C.dir[b].y = (j1 - j0 <= 32) ? mask : 0u;
     }
+    if (FUSE == 1) {  // statuses and good counts written: a builder's serial fallback may read them
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        __syncthreads();
+        if (threadIdx.x == 0 && gridDim.x > 1)
+            __hip_atomic_store(C.ctr + RF_GO, C.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    RF_STAMP(4);
     // per line set: the union of the windows that can read a changed bucket (the count <= 8 set into LDS when fused)
     const uint32_t B = T.B;
     const uint32_t below[3] = {2, 3, 7}, above[3] = {3, 4, 8};
     for (int k = 0; k < 3; k++) {
-        if (!C.list[k] && !(FUSE && k == 0)) continue;  // block-uniform
+        if (!C.list[k] && !(FUSE == 2 && k == 0)) continue;  // block-uniform (FUSE 1: the builders list their own)
         const uint32_t lb = below[k], la = above[k];
         const uint32_t n = block_union(nu, [&](uint32_t u, uint32_t& a, uint32_t& e) {
             const uint32_t b = ub[u];
             a = b > lb ? b - lb : 0u;
             e = min(B - 1, b + la);
-        }, (FUSE && k == 0) ? l8 : C.list[k], lds4);
+        }, (FUSE == 2 && k == 0) ? l8 : C.list[k], lds4);
         if (threadIdx.x == 0) {
-            if (FUSE && k == 0) n8_s = n; else C.ctr[RF_L8 + k] = n;
+            if (FUSE == 2 && k == 0) n8_s = n; else C.ctr[RF_L8 + k] = n;
         }
     }
     if (!SINGLE && threadIdx.x == 0) {  // the next refresh starts from empty appends
@@ -5732,89 +6003,31 @@ __global__ __launch_bounds__(BLOCK) void rf_nodes_kernel(RfCtx C) {
         C.ctr[RF_NR] = 0;
         C.ctr[RF_DONE] = 0;
     }
-    if (FUSE == 1) {
-        // phase 3: the count <= 8 window lines of the list and their short copies, one wave per line
-        // (wl_ws_build_wave) from W(2)'s nodes loaded in one round; a window of more than 64 nodes is built by
-        // the wave's first lane (wl_build_line, ws_build_line)
-        static_assert(4 * sizeof(WaveLds) <= 4 * RF_POOL, "phase 3 wave buffers");
-        WaveLds& WV = reinterpret_cast<WaveLds*>(pool)[threadIdx.x >> 6];
-        const uint32_t lane = threadIdx.x & 63u;
-        __syncthreads();
-        const uint32_t n8 = n8_s;
-        for (uint32_t x = threadIdx.x >> 6; x < n8; x += BLOCK / 64) {  // wave-uniform
-            const uint32_t b = l8[x], db = b >= 3 ? b - 3 : 0u, e = min(B, b + 3);
-            if (db + lane <= e && lane < 8) WV.dx[lane] = C.dir[db + lane].x & ~WIDE;
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
-            __builtin_amdgcn_wave_barrier();
-            const uint32_t n0 = WV.dx[0], n1 = WV.dx[e - db];
-            if (n1 - n0 <= 64) {
-                const bool have = n0 + lane < n1;
-                const uint64_t kk = have ? T.key[n0 + lane] : 0ull;
-                const uint32_t sv = have ? C.status[n0 + lane] : 0u;
-                wl_ws_build_wave(b, B, 64 - T.rshift, T.rbase >> T.rshift, db, WV.dx, n0, n1, kk, sv, C.wl, C.ws, WV);
-            } else if (lane == 0) {
-                wl_build_line(T.key, C.status, C.dir, C.gcnt, B, 64 - T.rshift, T.rbase >> T.rshift, C.wl, b, WV.R);
-                if (C.ws) ws_build_line(WV.R, C.ws, b, WV.R + 33);
-            }
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
-            __builtin_amdgcn_wave_barrier();
-        }
-    }
+    RF_STAMP(5);
     if (FUSE == 2) {
-        // phase 3: the count <= 8 general lines of the list, RF_GROUP lanes per line (the pool's sort buffers are free now).
-        // A line reads only W(2) = [b-3, b+2] (its bucket counts, directory entries up to b+3 and their nodes),
-        // which the group stages in LDS in two rounds of parallel loads; its first lane then builds the line from
-        // there (a window larger than RF_WCAP nodes is read from HBM). A line built straight from HBM waits
-        // for ~10 dependent loads (one per bucket of its window, and the keys eight at a time).
-        constexpr uint32_t RF_GROUP = 16, NG = BLOCK / RF_GROUP, RF_WCAP = 128;
-        static_assert(NG * (2 * RF_WCAP + RF_WCAP / 4 + 16 + 8 + 33 + 17) <= RF_POOL, "phase 3 staging");
-        uint64_t* skey = reinterpret_cast<uint64_t*>(pool);                        // NG x RF_WCAP keys
-        uint8_t* sst = reinterpret_cast<uint8_t*>(pool + NG * 2 * RF_WCAP);        // NG x RF_WCAP status bytes
-        uint2* sdir = reinterpret_cast<uint2*>(pool + NG * (2 * RF_WCAP + RF_WCAP / 4));  // NG x 8
-        uint32_t* sgc = pool + NG * (2 * RF_WCAP + RF_WCAP / 4 + 16);               // NG x 8
-        uint32_t* rows = sgc + NG * 8;                                              // NG x (33 + 17)
-        const uint32_t g = threadIdx.x / RF_GROUP, gl = threadIdx.x % RF_GROUP;
+        // publish the list to the builder blocks, then build this block's share
         __syncthreads();
         const uint32_t n8 = n8_s;
-        for (uint32_t x0 = 0; x0 < n8; x0 += NG) {  // block-uniform
-            const uint32_t x = x0 + g;
-            const bool act = x < n8;
-            const uint32_t b = act ? l8[x] : 0u, db = b >= 3 ? b - 3 : 0u;
-            // round 1: the counts of [db, db + 6) and the directory entries [db, db + 7)
-            if (act && gl < 6 && db + gl < B) sgc[8 * g + gl] = C.gcnt[db + gl];
-            if (act && gl >= 6 && gl < 13 && db + gl - 6 <= B) sdir[8 * g + gl - 6] = C.dir[db + gl - 6];
-            __syncthreads();
-            // round 2: the keys and status bytes of the nodes of buckets [db, min(B - 1, b + 2)]
-            const uint32_t e = min(B, b + 3);
-            const uint32_t n0 = sdir[8 * g].x & ~WIDE, n1 = sdir[8 * g + (e - db)].x & ~WIDE;
-            const bool staged = act && n1 - n0 <= RF_WCAP;
-            if (staged) {
-#pragma unroll
-                for (uint32_t k = 0; k < RF_WCAP / RF_GROUP; k++) {
-                    const uint32_t o = gl + RF_GROUP * k;
-                    if (o < n1 - n0) {
-                        skey[RF_WCAP * g + o] = T.key[n0 + o];
-                        sst[RF_WCAP * g + o] = C.status[n0 + o];
-                    }
-                }
-            }
-            __syncthreads();
-            if (act && gl == 0) {
-                // the staged copies as views indexed like the arrays (every index the build uses lies in W(2)):
-                // the shift is applied to the generic address (an LDS-space pointer shifted below its base would
-                // wrap in 32 bits and leave the LDS aperture once converted)
-                const uint64_t* kp = staged ? flat_shift(skey + RF_WCAP * g, n0) : T.key;
-                const uint8_t* sp = staged ? flat_shift(sst + RF_WCAP * g, n0) : C.status;
-                const uint2* dp = flat_shift(sdir + 8 * g, db);
-                const uint32_t* gp = flat_shift(sgc + 8 * g, db);
-                uint32_t* rowA = rows + 50 * g;
-                gl8_build_line(kp, sp, dp, gp, T.fkey, T.ftail, B, C.gl, b, rowA);
-            }
-            __syncthreads();
-        }
+        for (uint32_t x = threadIdx.x; x < n8; x += BLOCK) C.fl[x] = l8[x];
+        if (threadIdx.x == 0) C.ctr[RF_L8] = n8;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        __syncthreads();
+        if (threadIdx.x == 0 && gridDim.x > 1)
+            __hip_atomic_store(C.ctr + RF_GO, C.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        RF_STAMP(6);
+        rf_fused_lines<FUSE>(C, pool, n8, l8);
     }
+#ifdef KAD_RF_TRACE
+    __syncthreads();
+    RF_STAMP(7);
+    if (threadIdx.x == 0)
+        printf("RFTRACE single=%d fuse=%d total=%u nb=%u nu=%u n8=%u grid=%u ts=%llu %llu %llu %llu %llu %llu %llu %llu\n",
+               (int)SINGLE, FUSE, total, nb, nu, FUSE == 2 ? n8_s : 0u, gridDim.x, (unsigned long long)rf_ts[0],
+               (unsigned long long)(rf_ts[1] - rf_ts[0]), (unsigned long long)(rf_ts[2] - rf_ts[0]),
+               (unsigned long long)(rf_ts[3] - rf_ts[0]), (unsigned long long)(rf_ts[4] - rf_ts[0]),
+               (unsigned long long)(rf_ts[5] - rf_ts[0]), (unsigned long long)(rf_ts[6] - rf_ts[0]),
+               (unsigned long long)(rf_ts[7] - rf_ts[0]));
+#endif
 }
 
 // New status bytes: all n nodes (nodes == NULL) or the m listed ones; only changes are written and marked.
@@ -6376,6 +6589,7 @@ struct kad_table {
     mutable HostPipe* pipe = nullptr;
     Deadlines dl;                   // isGood(now) deadlines (kad_table_refresh_status)
     uint32_t* rf_ctr = nullptr;     // small refresh (rf_nodes_kernel): counters, appended buckets, NodeCache ranges
+    uint32_t rf_epoch = 0;          // the last fused refresh's list epoch (rf_ctr[RF_GO])
     uint32_t* rf_blist = nullptr;
     uint32_t* rf_nrange = nullptr;
     hipStream_t ss[2] = {nullptr, nullptr};  // side streams of an incremental rebuild (side_streams)
@@ -6863,23 +7077,71 @@ int small_refresh(kad_table* t, hipStream_t s, const uint32_t* mnode, uint32_t m
     if (ninl) {  // the node ids as kernel arguments (host copies of the runs): no list load before the times
         C.ninl = std::min(ninl, RF_INLINE);
         std::memcpy(C.inl, inl, 4ull * C.ninl);
+        // their buckets from the host's copy of the bucket offsets (no locate on the device), and for the window
+        // lines the lines to rebuild with the offsets their builders read (no directory load before the keys)
+        if (B && t->h_off.size() == (size_t)B + 1) {
+            uint32_t nh = 0;
+            for (uint32_t j = 0; j < C.ninl; j++) {
+                if (C.inl[j] >= d.n) continue;
+                C.hb[nh++] = (uint32_t)(std::upper_bound(t->h_off.begin(), t->h_off.end(), C.inl[j]) - t->h_off.begin()) - 1;
+            }
+            std::sort(C.hb, C.hb + nh);
+            C.nhb = (uint32_t)(std::unique(C.hb, C.hb + nh) - C.hb);
+            if (C.nhb == 0) C.hb[C.nhb++] = 0;  // (no valid node: one harmless recount)
+            // the union of [b-2, b+3] (ascending) as runs of consecutive lines, with the bucket offsets their
+            // windows [l-3, l+3] read
+            uint32_t nl = 0, nr = 0, no = 0;
+            bool fits = true;
+            for (uint32_t u = 0; u < C.nhb && fits; u++) {
+                const uint32_t b = C.hb[u], lo = b > 2 ? b - 2 : 0u, hi = std::min(B - 1, b + 3);
+                if (nr && lo <= C.hr[3 * (nr - 1)] + C.hr[3 * (nr - 1) + 1]) {  // extends the last run
+                    uint32_t* R = C.hr + 3 * (nr - 1);
+                    const uint32_t end = std::max(R[0] + R[1], hi + 1), add = end - (R[0] + R[1]);
+                    const uint32_t o_end = std::min(B, end - 1 + 3) + 1;  // offsets [.., min(B, last + 3)]
+                    const uint32_t have = R[2] + ((std::min(B, R[0] + R[1] - 1 + 3) + 1) - (R[0] >= 3 ? R[0] - 3 : 0u));
+                    const uint32_t want = R[2] + (o_end - (R[0] >= 3 ? R[0] - 3 : 0u));
+                    if (want > RF_HOFF) { fits = false; break; }
+                    for (uint32_t o = have; o < want; o++) C.hoff[o] = t->h_off[(R[0] >= 3 ? R[0] - 3 : 0u) + (o - R[2])];
+                    no = want;
+                    R[1] += add;
+                    nl += add;
+                } else {
+                    if (nr == 16) { fits = false; break; }
+                    const uint32_t o0 = lo >= 3 ? lo - 3 : 0u, o1 = std::min(B, hi + 3) + 1;
+                    if (no + (o1 - o0) > RF_HOFF) { fits = false; break; }
+                    uint32_t* R = C.hr + 3 * nr++;
+                    R[0] = lo;
+                    R[1] = hi - lo + 1;
+                    R[2] = no;
+                    for (uint32_t o = o0; o < o1; o++) C.hoff[no++] = t->h_off[o];
+                    nl += R[1];
+                }
+            }
+            C.nhl = fits ? nl : 0;
+            C.nhr = fits ? nr : 0;
+        }
     }
     // one block when it holds every listed node; the count <= 8 lines built by it when at most RF_FUSE_LINES can
     // be listed (6 per changed bucket) and no slot lines depend on them
     const bool single = total <= BLOCK;
     const int fuse = (!B || 6ull * total > RF_FUSE_LINES || t->sl_mut) ? 0 : t->wl_mut ? 1 : t->gl_mut ? 2 : 0;
-    if (fuse) {
+    dim3 g1(std::min<uint32_t>((total + BLOCK - 1) / BLOCK, 64u));
+    if (fuse) {  // (6 * total <= RF_FUSE_LINES: one block derives every node) + builder blocks, all lines in one round
         C.list[0] = nullptr;
         C.wl = t->wl_mut;
         C.ws = t->ws_mut;
         C.gl = t->gl_mut;
+        C.fl = t->dlist;
+        if (++t->rf_epoch == 0) t->rf_epoch = 1;  // ctr[RF_GO] starts at 0
+        C.epoch = t->rf_epoch;
+        // FUSE 1: block 0 + builder blocks of one line per wave; FUSE 2: 16 lines per block, block 0 included
+        const uint32_t lines = C.nhl ? C.nhl : std::min<uint32_t>(B, 6u * total);
+        g1 = fuse == 1 ? dim3(1 + (lines + BLOCK / 64 - 1) / (BLOCK / 64))
+                       : dim3(std::max<uint32_t>(1, (lines + BLOCK / 16 - 1) / (BLOCK / 16)));
     }
-    const dim3 g1(std::min<uint32_t>((total + BLOCK - 1) / BLOCK, 64u));
-    if (single && fuse == 1) hipLaunchKernelGGL((rf_nodes_kernel<true, 1>), g1, dim3(BLOCK), 0, s, C);
-    else if (single && fuse == 2) hipLaunchKernelGGL((rf_nodes_kernel<true, 2>), g1, dim3(BLOCK), 0, s, C);
+    if (fuse == 1) hipLaunchKernelGGL((rf_nodes_kernel<true, 1>), g1, dim3(BLOCK), 0, s, C);
+    else if (fuse == 2) hipLaunchKernelGGL((rf_nodes_kernel<true, 2>), g1, dim3(BLOCK), 0, s, C);
     else if (single) hipLaunchKernelGGL((rf_nodes_kernel<true, 0>), g1, dim3(BLOCK), 0, s, C);
-    else if (fuse == 1) hipLaunchKernelGGL((rf_nodes_kernel<false, 1>), g1, dim3(BLOCK), 0, s, C);
-    else if (fuse == 2) hipLaunchKernelGGL((rf_nodes_kernel<false, 2>), g1, dim3(BLOCK), 0, s, C);
     else hipLaunchKernelGGL((rf_nodes_kernel<false, 0>), g1, dim3(BLOCK), 0, s, C);
     HIP_TRY(hipGetLastError());
     // the builders over the lists; grids from the host's bound on each list
