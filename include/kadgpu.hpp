@@ -207,7 +207,7 @@ public:
     template <class InfoHashT, class TimePoint>
     std::vector<std::vector<NodePtr>> findClosestNodesBatch(const InfoHashT* ids, size_t q, TimePoint now,
                                                             size_t count = KAD_TARGET_NODES) const {
-        if (q <= host_q_ && count <= host_count_) {  // a few single requests: the host path (no device round trip)
+        if (q <= hostBatchLimit() && count <= host_count_) {  // a few requests: the host path (no device round trip)
             std::vector<std::vector<NodePtr>> out(q);
             for (size_t i = 0; i < q; i++) out[i] = findClosestNodesHost(ids[i], now, count);
             return out;
@@ -349,10 +349,19 @@ public:
         for (size_t k = 0; k < m; k++) out.push_back(nodes_[cand[k].idx]);
         return out;
     }
-    /* Batches of at most q requests with count <= max_count take the host path (0: never). */
+    /* Batches of at most q requests with count <= max_count take the host path (0: never; the default picks q from
+       the table size, below). */
     void setHostPath(size_t q, size_t max_count = 64) {
         host_q_ = q;
         host_count_ = max_count;
+    }
+    /* The largest batch the host path answers: set by setHostPath, else the crossover measured on MI355X
+       (tools/crossover.cpp, profiles/r04/r04j/crossover.json: the host path beats both device paths up to 32
+       requests on tables of up to 10k nodes, 16 at 100k, 8 at 1M). */
+    size_t hostBatchLimit() const {
+        if (host_q_ != kHostAuto) return host_q_;
+        const size_t n = nodes_.size();
+        return n <= 20000 ? 32 : n <= 200000 ? 16 : 8;
     }
 
     size_t bucketCount() const { return buckets_; }
@@ -411,7 +420,8 @@ private:
     uint32_t buckets_ = 0;
     std::vector<uint8_t> first_;  // the bucket directory on the host (the host path)
     std::vector<uint32_t> off_;
-    size_t host_q_ = 1, host_count_ = 64;  // single requests take the host path (tools/crossover.cpp)
+    static constexpr size_t kHostAuto = ~size_t(0);
+    size_t host_q_ = kHostAuto, host_count_ = 64;  // small batches take the host path (hostBatchLimit)
     std::vector<uint32_t> ops_;
     std::vector<NodePtr> added_;
     mutable std::vector<uint32_t> updated_;

@@ -5245,17 +5245,17 @@ struct RfCtx {
     uint32_t* gl;
     uint32_t* fl;                        // FUSE: the line list block 0 publishes to the builder blocks
     uint32_t epoch;                      // FUSE: this refresh's value of ctr[RF_GO] (the list is published)
-    uint32_t ninl;                       // > 0: the nodes are inl[0, ninl) (the host's copies of the runs), no lists
-    uint32_t inl[16];
+    uint32_t ninl;                       // > 0: the nodes are inl[0, ninl) (the host's copies of the runs, sorted), no lists
+    uint32_t inl[128];
     // with inline nodes, derived on the host from its copy of the bucket offsets (0: derived on the device):
     uint32_t nhb;                        // the listed nodes' buckets, sorted and distinct
-    uint32_t hb[16];
+    uint32_t hb[128];
     uint32_t nhl;                        // FUSE 1: the window lines to rebuild, as nhr runs of consecutive lines:
     uint32_t nhr;                        //   run r = lines hr[3r] .. hr[3r] + hr[3r+1] - 1, whose windows' bucket
     uint32_t hr[3 * 16];                 //   offsets h_off[max(0, first - 3) ..] start at hoff[hr[3r+2]]
     uint32_t hoff[256];
 };
-constexpr uint32_t RF_INLINE = 16, RF_HOFF = 256;
+constexpr uint32_t RF_INLINE = 128, RF_HOFF = 256;
 
 // One atomic per wave for the lanes with `want` (wave-uniform call); returns each wanting lane's slot.
 __device__ __forceinline__ uint32_t wave_append(uint32_t* ctr, bool want) {
@@ -5369,6 +5369,10 @@ struct WaveLds {
     uint32_t L[32];    // the 128-byte line
     uint32_t S16[16];  // the short line
     uint32_t dx[8];    // first nodes of the staged buckets
+    uint32_t hlo[32];  // collision prefilter: lanes (0..31, 32..63) per 5-bit hash
+    uint32_t hhi[32];
+    uint32_t pk[64];   // per lane: stored bit 31 | D rank << 24 | key21 (read by the lanes it may collide with)
+    uint64_t key[64];
     uint32_t R[33 + 17];  // rows of the serial fallback (a window of more than 64 nodes)
 };
 
@@ -5381,10 +5385,12 @@ __device__ __attribute__((always_inline)) void wl_ws_build_wave(uint32_t b, uint
     const uint32_t n = n0 + lane;
     const bool have = n < n1;
     const uint32_t e = min(B, b + 3);  // buckets [db, e) staged; dx[i] = first node of bucket db + i (i <= e - db)
-    uint32_t x = NONE;
-    if (have)
-        for (uint32_t i = 0; db + i < e; i++)
-            if (dx[i] <= n) x = db + i;
+    const uint32_t dxv = lane < 8 ? dx[lane] : 0u;  // dx in registers: uniform reads by readlane
+    uint32_t x = NONE, xfirst = 0;
+    for (uint32_t i = 0; db + i < e; i++) {  // wave-uniform
+        const uint32_t di = rdl(dxv, i);
+        if (have && di <= n) { x = db + i; xfirst = di; }
+    }
     const bool good = have && (stat & KAD_STATUS_GOOD);
     // good nodes per staged bucket (as gcnt / the masks: the same status bytes)
     uint32_t cnt[7];
@@ -5413,7 +5419,7 @@ __device__ __attribute__((always_inline)) void wl_ws_build_wave(uint32_t b, uint
         if (lane == 0) { W.L[1] = WL_DEFER; W.L[3] = 0; }
     } else {
         const uint32_t lo = b > R8 ? b - 1 - R8 : 0u, hi = min(B - 1, b + R8), nb = hi - lo + 1;  // nb <= 6
-        base = dx[lo - db];
+        base = rdl(dxv, lo - db);
         // lane y < nb holds window bucket lo + y: its D rank (the order of (pre0 + y) ^ (pre0 + b)), its good
         // count, and the stored prefix in D order (whole buckets while the cumulative count fits WL_SLOTS)
         const uint32_t yb = lo + min(lane, nb - 1);
@@ -5437,18 +5443,29 @@ __device__ __attribute__((always_inline)) void wl_ws_build_wave(uint32_t b, uint
         const uint32_t rj = (info >> 24) & 7u, st0 = info & 0xFFFFFFu;
         const uint32_t k21 = (uint32_t)((key << d) >> (64 - WL_KBITS)), off = n - base;
         const uint64_t mm = __ballot(mine);
-        const uint32_t fl = inw ? dx[x - db] - n0 : 0u;  // first lane of my bucket
+        const uint32_t fl = inw ? xfirst - n0 : 0u;  // first lane of my bucket
         const uint32_t inb = (uint32_t)__builtin_popcountll(mm & below & ~((1ull << fl) - 1ull));
         defer = __any(mine && off > 255u);
-        // pairs: earlier stored nodes of my bucket (lower lanes, same D rank) with my key21, in lane order
+        // pairs: earlier stored nodes of my bucket (lower lanes, same D rank) with my key21, in lane order. A 5-bit
+        // hash of (rank, key21) in LDS names the earlier lanes that can be equal; usually none, and the exact
+        // comparison runs over those only.
         const uint32_t mypk = mine ? (0x80000000u | (rj << 24) | k21) : 0u;
+        if (lane < 32) { W.hlo[lane] = 0; W.hhi[lane] = 0; }
+        W.pk[lane] = mypk;
+        W.key[lane] = key;
+        wave_lds_sync();
+        const uint32_t hs = (mypk * 0x9E3779B1u) >> 27;
+        if (mine) atomicOr(lane < 32 ? &W.hlo[hs] : &W.hhi[hs], 1u << (lane & 31u));
+        wave_lds_sync();
+        uint64_t same = 0;
+        if (mine) same = (((uint64_t)W.hhi[hs] << 32) | W.hlo[hs]) & below;
         uint32_t pairs = 0, my_tie = 0;
         bool zero = false, have_tie = false;
-        for (uint64_t m = mm; m; m &= m - 1) {  // wave-uniform, at most WL_SLOTS stored lanes
+        for (uint64_t m = same; m; m &= m - 1) {  // per lane, ascending
             const uint32_t l2 = (uint32_t)__builtin_ctzll(m);
-            const uint32_t v = rdl(mypk, l2);
-            const uint64_t k2 = rdl64(key, l2);
-            if (mine && l2 < lane && v == mypk) {
+            const uint32_t v = W.pk[l2];  // (LDS: the lane l2 need not be active here)
+            const uint64_t k2 = W.key[l2];
+            if (v == mypk) {
                 pairs++;
                 const uint64_t x64 = key ^ k2;
                 if (x64 == 0) {
@@ -5494,9 +5511,17 @@ __device__ __attribute__((always_inline)) void wl_ws_build_wave(uint32_t b, uint
     const bool ks = lane < keep;
     const uint32_t jj = vs >> 29, k16 = (vs >> KSH) & 0xFFFFu, offs = vs & 255u;
     bool f = ks && offs >= 64u;
-    for (uint32_t r = 0; r < keep; r++) {  // wave-uniform: an earlier slot of the same bucket with my key16
-        const uint32_t u = rdl(vs, r);
-        f |= ks && r < lane && (u >> 29) == jj && ((u >> KSH) & 0xFFFFu) == k16;
+    {  // an earlier kept slot of the same bucket with my key16 (the same hash prefilter; kept slots are lanes < 19)
+        const uint32_t jk = (jj << 16) | k16, hk = (jk * 0x9E3779B1u) >> 27;
+        if (lane < 32) W.hlo[lane] = 0;
+        wave_lds_sync();
+        if (ks) atomicOr(&W.hlo[hk], 1u << lane);
+        wave_lds_sync();
+        uint32_t same = ks ? W.hlo[hk] & (uint32_t)below : 0u;
+        for (; same; same &= same - 1) {
+            const uint32_t u = W.L[WL_SLOT0 + __builtin_ctz(same)];
+            f |= (u >> 29) == jj && ((u >> KSH) & 0xFFFFu) == k16;
+        }
     }
     fb = fb || __any(f);
     const bool start = ks && (lane == 0 || (vprev >> 29) != jj);
@@ -5574,7 +5599,7 @@ __global__ __launch_bounds__(BLOCK) void wl_ws_wave_kernel(const uint64_t* __res
 // derives the nodes and the list, publishes it (ctr[RF_GO] = epoch, release at agent scope) and builds its share;
 // blocks 1.. wait for the epoch (dispatched after block 0, so it is always resident) and build the rest, all
 // lines in one round.
-constexpr uint32_t RF_FUSE_LINES = 256;
+constexpr uint32_t RF_FUSE_LINES = 6 * 128;
 
 // p - n as a generic (flat) pointer: p[n + i] is then p[i] for the callee, whatever the address space of p.
 template <class T>
@@ -5591,140 +5616,170 @@ constexpr uint32_t RF_POOL = BLOCK * (33 + 17);  // dwords: phase 2's sort buffe
 #define RF_STAMP(k) do { } while (0)
 #endif
 
-// Builder blocks of a fused window-line refresh (FUSE 1, blocks 1..): independent of block 0. Wave 0 derives
-// the listed nodes' new statuses itself (as phase 1 does) and the lines that can read their buckets (the union of
-// [b-2, b+3], as phase 2's list: sorted and merged across the wave); every wave then builds lines of that list
-// (wl_ws_build_wave) with the listed nodes' statuses taken from the derived values, so no line waits for block 0's
-// status writes. Only a window of more than 64 nodes (the serial builder, which reads the table's statuses and
-// good counts) waits for block 0's epoch (published after its good counts). Unchanged nodes in the list rebuild
-// lines that come out identical.
+// Builder blocks of a fused window-line refresh (FUSE 1, blocks 1..): independent of block 0. The lines to build
+// are the union of [b-2, b+3] over the listed nodes' buckets (phase 2's count <= 8 list): given by the host with
+// the bucket offsets their windows read (C.nhl), derived here from the host's buckets (C.nhb: a merge across the
+// wave, then the directory), or, for nodes in device lists, derived from the nodes (their buckets located and
+// sorted across wave 0). Every wave builds lines of that list (wl_ws_build_wave) with the listed nodes' statuses
+// derived here as phase 1 derives them, so no line waits for block 0's status writes. Only a window of more than
+// 64 nodes (the serial builder, which reads the table's statuses and good counts) waits for block 0's epoch
+// (published after its good counts). A listed node whose status did not change rebuilds lines that come out the same.
 __device__ void rf_wl_builders(const RfCtx& C, uint32_t* pool) {
     const DevTable& T = C.T;
     const uint32_t B = T.B, lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
-    const uint32_t total = C.ninl ? C.ninl : C.mc + C.sc + C.np;  // <= 64 (the host fuses at 6 * total <= 256)
+    const uint32_t total = C.ninl ? C.ninl : C.mc + C.sc + C.np;  // inline <= RF_INLINE, lists <= 64
     static_assert(4 * sizeof(WaveLds) <= 4 * RF_POOL, "builder wave buffers");
-    if (C.nhl) {  // the host's lines and offsets: one round of loads (window keys and statuses, listed nodes' times)
-        WaveLds& WV = reinterpret_cast<WaveLds*>(pool)[wid];
-        for (uint32_t x = (blockIdx.x - 1) * (BLOCK / 64) + wid; x < C.nhl; x += (gridDim.x - 1) * (BLOCK / 64)) {
-            uint32_t r = 0, k = x;  // the run of line x (wave-uniform)
-            while (r + 1 < C.nhr && k >= C.hr[3 * r + 1]) k -= C.hr[3 * r + 1], r++;
-            const uint32_t first = C.hr[3 * r], b = first + k, db = b >= 3 ? b - 3 : 0u, e = min(B, b + 3);
-            const uint32_t* hl = C.hoff + C.hr[3 * r + 2] + (db - (first >= 3 ? first - 3 : 0u));  // offsets of db ..
-            const uint32_t n0 = hl[0], n1 = hl[e - db];
-            if (n1 - n0 <= 64) {
-                if (lane < 8) WV.dx[lane] = hl[min(lane, e - db)];
-                const uint32_t n = n0 + lane;
-                const bool have = n < n1;
-                bool listed = false;
-                for (uint32_t j = 0; j < C.ninl; j++) listed |= C.inl[j] == n;
-#ifdef KAD_RF_TRACE
-                const uint64_t tb0 = wall_clock64();
-#endif
-                const uint64_t kk = have ? T.key[n] : 0ull;
-                const uint32_t sv = !have ? 0u : listed ? status_at(C.N, n, C.now) : (uint32_t)C.status[n];
-                wave_lds_sync();
-#ifdef KAD_RF_TRACE
-                __builtin_amdgcn_s_waitcnt(0);
-                const uint64_t tb1 = wall_clock64();
-#endif
-                wl_ws_build_wave(b, B, 64 - T.rshift, T.rbase >> T.rshift, db, WV.dx, n0, n1, kk, sv, C.wl, C.ws, WV);
-#ifdef KAD_RF_TRACE
-                const uint64_t tb2 = wall_clock64();
-                __builtin_amdgcn_s_waitcnt(0);
-                const uint64_t tb3 = wall_clock64();
-                if (lane == 0)
-                    printf("RFWAVE blk=%u wave=%u line=%u nodes=%u loads=%llu build=%llu drain=%llu at=%llu\n", blockIdx.x,
-                           wid, b, n1 - n0, (unsigned long long)(tb1 - tb0), (unsigned long long)(tb2 - tb1),
-                           (unsigned long long)(tb3 - tb2), (unsigned long long)tb0);
-#endif
-            } else if (lane == 0) {  // serial build from the table: wait for block 0's statuses and good counts
-                const uint64_t t0 = wall_clock64();
-                bool go = true;
-                while (__hip_atomic_load(C.ctr + RF_GO, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != C.epoch) {
-                    __builtin_amdgcn_s_sleep(1);
-                    if (wall_clock64() - t0 > 100000000ull) { go = false; break; }
-                }
-                if (go) {
-                    wl_build_line(T.key, C.status, C.dir, C.gcnt, B, 64 - T.rshift, T.rbase >> T.rshift, C.wl, b, WV.R);
-                    if (C.ws) ws_build_line(WV.R, C.ws, b, WV.R + 33);
-                }
-            }
-            wave_lds_sync();
-        }
-        return;
-    }
     __shared__ uint32_t s_node[64];
     __shared__ uint32_t s_st[64];
     __shared__ uint32_t s_lines[RF_FUSE_LINES];
     __shared__ uint32_t s_nl;
-    if (wid == 0) {
-        const bool act = lane < total;
-        uint32_t i = NONE, st = 0, b = NONE;
-        if (act)
-            i = C.ninl ? C.inl[lane] : lane < C.mc ? C.mnode[lane] : lane < C.mc + C.sc ? C.snode[lane - C.mc]
-                                                                                       : C.pend[lane - C.mc - C.sc];
-        if (act && i < T.n) {
-            const uint64_t key_i = T.key[i];
-            st = (!C.ninl && C.vals && lane >= C.mc + C.sc)
-                     ? (uint32_t)(C.vals[lane - C.mc - C.sc] & (KAD_STATUS_GOOD | KAD_STATUS_EXPIRED))
-                     : status_at(C.N, i, C.now);
-            b = node_bucket(T, C.dir, i, key_i);
-        } else {
-            i = NONE;
-        }
-        s_node[lane] = i;
-        s_st[lane] = st;
-        // the buckets sorted across the wave (bitonic; NONE last), then each distinct one's [b-2, b+3] merged
-        uint32_t v = b;
+    const bool host_lines = C.nhl != 0;
+    if (!host_lines) {  // block-uniform
+        if (wid == 0 && C.nhb) {
+            // the host's buckets (sorted, distinct, <= RF_INLINE): merge [b-2, b+3] in passes of 64
+            uint32_t carry = 0, base = 0;
+            for (uint32_t p0 = 0; p0 < C.nhb; p0 += 64) {  // wave-uniform
+                const uint32_t idx = p0 + lane;
+                const bool keep = idx < C.nhb;
+                const uint32_t v = keep ? C.hb[idx] : 0u;
+                const uint32_t a0 = keep ? (v > 2 ? v - 2 : 0u) : 0u, e1 = keep ? min(B - 1, v + 3) + 1 : 0u;
+                uint32_t mx = e1;  // inclusive running max of the interval ends (+1)
 #pragma unroll
-        for (uint32_t k = 2; k <= 64; k <<= 1)
+                for (int o = 1; o < 64; o <<= 1) {
+                    const uint32_t y = (uint32_t)__shfl_up((int)mx, o, 64);
+                    if (lane >= (uint32_t)o) mx = max(mx, y);
+                }
+                uint32_t before = (uint32_t)__shfl_up((int)mx, 1, 64);
+                before = max(lane == 0 ? 0u : before, carry);
+                const uint32_t s0 = max(a0, before), cnt = keep && e1 > s0 ? e1 - s0 : 0u;
+                uint32_t off = cnt;
 #pragma unroll
-            for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-                const uint32_t u = (uint32_t)__shfl_xor((int)v, (int)j, 64);
-                v = (((lane & j) == 0) == ((lane & k) == 0)) ? min(v, u) : max(v, u);
+                for (int o = 1; o < 64; o <<= 1) {
+                    const uint32_t y = (uint32_t)__shfl_up((int)off, o, 64);
+                    if (lane >= (uint32_t)o) off += y;
+                }
+                const uint32_t tot = rdl(off, 63);
+                off = base + off - cnt;
+                for (uint32_t k = 0; k < cnt; k++)
+                    if (off + k < RF_FUSE_LINES) s_lines[off + k] = s0 + k;
+                carry = max(carry, rdl(mx, 63));
+                base += tot;
             }
-        const uint32_t pv = (uint32_t)__shfl_up((int)v, 1, 64);
-        const bool keep = v != NONE && (lane == 0 || v != pv);
-        const uint32_t a0 = keep ? (v > 2 ? v - 2 : 0u) : 0u, e1 = keep ? min(B - 1, v + 3) + 1 : 0u;
-        uint32_t mx = e1;  // inclusive running max of the interval ends (+1) in lane order
+            if (lane == 0) s_nl = min(base, RF_FUSE_LINES);
+        } else if (wid == 0) {
+            // nodes from device lists (<= 64): locate, derive, sort the buckets across the wave, merge
+            const bool act = lane < total;
+            uint32_t i = NONE, st = 0, b = NONE;
+            if (act)
+                i = C.ninl ? C.inl[lane] : lane < C.mc ? C.mnode[lane] : lane < C.mc + C.sc ? C.snode[lane - C.mc]
+                                                                                           : C.pend[lane - C.mc - C.sc];
+            if (act && i < T.n) {
+                const uint64_t key_i = T.key[i];
+                st = (!C.ninl && C.vals && lane >= C.mc + C.sc)
+                         ? (uint32_t)(C.vals[lane - C.mc - C.sc] & (KAD_STATUS_GOOD | KAD_STATUS_EXPIRED))
+                         : status_at(C.N, i, C.now);
+                b = node_bucket(T, C.dir, i, key_i);
+            } else {
+                i = NONE;
+            }
+            s_node[lane] = i;
+            s_st[lane] = st;
+            uint32_t v = b;  // bitonic across the wave, NONE last
 #pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = (uint32_t)__shfl_up((int)mx, o, 64);
-            if (lane >= (uint32_t)o) mx = max(mx, y);
-        }
-        uint32_t before = (uint32_t)__shfl_up((int)mx, 1, 64);
-        if (lane == 0) before = 0;
-        const uint32_t s0 = max(a0, before), cnt = keep && e1 > s0 ? e1 - s0 : 0u;
-        uint32_t off = cnt;  // inclusive sum, then exclusive
+            for (uint32_t k = 2; k <= 64; k <<= 1)
 #pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = (uint32_t)__shfl_up((int)off, o, 64);
-            if (lane >= (uint32_t)o) off += y;
+                for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+                    const uint32_t u = (uint32_t)__shfl_xor((int)v, (int)j, 64);
+                    v = (((lane & j) == 0) == ((lane & k) == 0)) ? min(v, u) : max(v, u);
+                }
+            const uint32_t pv = (uint32_t)__shfl_up((int)v, 1, 64);
+            const bool keep = v != NONE && (lane == 0 || v != pv);
+            const uint32_t a0 = keep ? (v > 2 ? v - 2 : 0u) : 0u, e1 = keep ? min(B - 1, v + 3) + 1 : 0u;
+            uint32_t mx = e1;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = (uint32_t)__shfl_up((int)mx, o, 64);
+                if (lane >= (uint32_t)o) mx = max(mx, y);
+            }
+            uint32_t before = (uint32_t)__shfl_up((int)mx, 1, 64);
+            if (lane == 0) before = 0;
+            const uint32_t s0 = max(a0, before), cnt = keep && e1 > s0 ? e1 - s0 : 0u;
+            uint32_t off = cnt;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = (uint32_t)__shfl_up((int)off, o, 64);
+                if (lane >= (uint32_t)o) off += y;
+            }
+            const uint32_t nl = rdl(off, 63);
+            off -= cnt;
+            for (uint32_t k = 0; k < cnt; k++)
+                if (off + k < RF_FUSE_LINES) s_lines[off + k] = s0 + k;
+            if (lane == 0) s_nl = min(nl, RF_FUSE_LINES);
         }
-        const uint32_t nl = rdl(off, 63);
-        off -= cnt;
-        for (uint32_t k = 0; k < cnt; k++)
-            if (off + k < RF_FUSE_LINES) s_lines[off + k] = s0 + k;
-        if (lane == 0) s_nl = min(nl, RF_FUSE_LINES);
+        __syncthreads();
     }
-    __syncthreads();
-    const uint32_t nl = s_nl;
+    const uint32_t nl = host_lines ? C.nhl : s_nl;
     WaveLds& WV = reinterpret_cast<WaveLds*>(pool)[wid];
-    const uint32_t nbuild = gridDim.x - 1;
-    for (uint32_t x = (blockIdx.x - 1) * (BLOCK / 64) + wid; x < nl; x += nbuild * (BLOCK / 64)) {  // wave-uniform
-        const uint32_t b = s_lines[x], db = b >= 3 ? b - 3 : 0u, e = min(B, b + 3);
-        if (db + lane <= e && lane < 8) WV.dx[lane] = C.dir[db + lane].x & ~WIDE;
-        wave_lds_sync();
-        const uint32_t n0 = WV.dx[0], n1 = WV.dx[e - db];
+    for (uint32_t x = (blockIdx.x - 1) * (BLOCK / 64) + wid; x < nl; x += (gridDim.x - 1) * (BLOCK / 64)) {
+        uint32_t b, n0, n1;  // (wave-uniform)
+        if (host_lines) {  // the run of line x and its offsets (kernel arguments)
+            uint32_t r = 0, k = x;
+            while (r + 1 < C.nhr && k >= C.hr[3 * r + 1]) k -= C.hr[3 * r + 1], r++;
+            const uint32_t first = C.hr[3 * r];
+            b = first + k;
+            const uint32_t db = b >= 3 ? b - 3 : 0u, e = min(B, b + 3);
+            const uint32_t* hl = C.hoff + C.hr[3 * r + 2] + (db - (first >= 3 ? first - 3 : 0u));
+            if (lane < 8) WV.dx[lane] = hl[min(lane, e - db)];
+            n0 = hl[0];
+            n1 = hl[e - db];
+        } else {
+            b = s_lines[x];
+            const uint32_t db = b >= 3 ? b - 3 : 0u, e = min(B, b + 3);
+            if (db + lane <= e && lane < 8) WV.dx[lane] = C.dir[db + lane].x & ~WIDE;
+            wave_lds_sync();
+            n0 = WV.dx[0];
+            n1 = WV.dx[e - db];
+        }
+        const uint32_t db = b >= 3 ? b - 3 : 0u;
         if (n1 - n0 <= 64) {
-            const bool have = n0 + lane < n1;
-            const uint64_t kk = have ? T.key[n0 + lane] : 0ull;
-            uint32_t sv = have ? C.status[n0 + lane] : 0u;
-            for (uint32_t j = 0; j < total; j++) {  // the listed nodes' derived statuses
-                const uint32_t nj = s_node[j];
-                if (nj != NONE && nj - n0 == lane) sv = s_st[j];
+            const uint32_t n = n0 + lane;
+            const bool have = n < n1;
+            uint32_t sv;
+#ifdef KAD_RF_TRACE
+            const uint64_t tb0 = wall_clock64();
+#endif
+            const uint64_t kk = have ? T.key[n] : 0ull;
+            if (C.ninl) {  // inline nodes (sorted by the host): those in [n0, n1) take their derived status
+                uint32_t lo = 0, hi = C.ninl;
+                while (lo < hi) {  // wave-uniform lower_bound of n0
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (C.inl[mid] < n0) lo = mid + 1; else hi = mid;
+                }
+                bool listed = false;
+                for (uint32_t j = lo; j < C.ninl && C.inl[j] < n1; j++) listed |= C.inl[j] == n;
+                sv = !have ? 0u : listed ? status_at(C.N, n, C.now) : (uint32_t)C.status[n];
+            } else {  // device lists: the statuses wave 0 derived
+                sv = have ? C.status[n] : 0u;
+                for (uint32_t j = 0; j < total; j++) {
+                    const uint32_t nj = s_node[j];
+                    if (nj != NONE && nj - n0 == lane) sv = s_st[j];
+                }
             }
+            wave_lds_sync();
+#ifdef KAD_RF_TRACE
+            __builtin_amdgcn_s_waitcnt(0);
+            const uint64_t tb1 = wall_clock64();
+#endif
             wl_ws_build_wave(b, B, 64 - T.rshift, T.rbase >> T.rshift, db, WV.dx, n0, n1, kk, sv, C.wl, C.ws, WV);
+#ifdef KAD_RF_TRACE
+            const uint64_t tb2 = wall_clock64();
+            __builtin_amdgcn_s_waitcnt(0);
+            const uint64_t tb3 = wall_clock64();
+            if (lane == 0)
+                printf("RFWAVE blk=%u wave=%u line=%u nodes=%u loads=%llu build=%llu drain=%llu at=%llu\n", blockIdx.x,
+                       wid, b, n1 - n0, (unsigned long long)(tb1 - tb0), (unsigned long long)(tb2 - tb1),
+                       (unsigned long long)(tb3 - tb2), (unsigned long long)tb0);
+#endif
         } else if (lane == 0) {  // serial build from the table: wait for block 0's statuses and good counts
             const uint64_t t0 = wall_clock64();
             bool go = true;
@@ -7044,6 +7099,31 @@ int rf_ready(kad_table* t) {
 // Re-derive the status of at most RF_CAP listed nodes (main-run, side-run and patched nodes; vals: the patched
 // nodes' new status bytes instead of their times) and rebuild only what they change: rf_nodes_kernel, then the
 // line builders over its lists. ensure_marks must have run (the lists live in dlist). Async on s.
+// The bucket holding node i (the last b with off[b] <= i; off = the B + 1 bucket offsets, off[B] = n): a galloping
+// search from the proportional guess i * B / n, so a few cache lines of the 4 (B + 1)-byte array per node.
+uint32_t bucket_of_node(const std::vector<uint32_t>& off, uint32_t n, uint32_t i) {
+    const uint32_t B = (uint32_t)off.size() - 1;
+    uint64_t lo, hi;  // off[lo] <= i < off[hi] (hi may be B + 1: past the end)
+    uint64_t g = n ? std::min<uint64_t>((uint64_t)i * B / n, B - 1) : 0;
+    if (off[g] <= i) {
+        uint64_t step = 1;
+        lo = g;
+        while (lo + step <= B && off[lo + step] <= i) { lo += step; step <<= 1; }
+        hi = std::min<uint64_t>(lo + step, B + 1);
+    } else {
+        uint64_t step = 1;
+        hi = g;
+        while (hi >= step && off[hi - step] > i) { hi -= step; step <<= 1; }
+        lo = hi >= step ? hi - step : 0;
+        if (off[lo] > i) return 0;  // (i below every offset: bucket 0)
+    }
+    while (hi - lo > 1) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (off[mid] <= i) lo = mid; else hi = mid;
+    }
+    return (uint32_t)std::min<uint64_t>(lo, B - 1);
+}
+
 int small_refresh(kad_table* t, hipStream_t s, const uint32_t* mnode, uint32_t mc, const uint32_t* snode, uint32_t sc,
                   const uint32_t* pend, uint32_t np, const uint8_t* vals, int64_t now, const uint32_t* inl = nullptr,
                   uint32_t ninl = 0) {
@@ -7077,14 +7157,13 @@ int small_refresh(kad_table* t, hipStream_t s, const uint32_t* mnode, uint32_t m
     if (ninl) {  // the node ids as kernel arguments (host copies of the runs): no list load before the times
         C.ninl = std::min(ninl, RF_INLINE);
         std::memcpy(C.inl, inl, 4ull * C.ninl);
+        std::sort(C.inl, C.inl + C.ninl);  // (the builders search them by node)
         // their buckets from the host's copy of the bucket offsets (no locate on the device), and for the window
         // lines the lines to rebuild with the offsets their builders read (no directory load before the keys)
         if (B && t->h_off.size() == (size_t)B + 1) {
             uint32_t nh = 0;
-            for (uint32_t j = 0; j < C.ninl; j++) {
-                if (C.inl[j] >= d.n) continue;
-                C.hb[nh++] = (uint32_t)(std::upper_bound(t->h_off.begin(), t->h_off.end(), C.inl[j]) - t->h_off.begin()) - 1;
-            }
+            for (uint32_t j = 0; j < C.ninl; j++)
+                if (C.inl[j] < d.n) C.hb[nh++] = bucket_of_node(t->h_off, d.n, C.inl[j]);
             std::sort(C.hb, C.hb + nh);
             C.nhb = (uint32_t)(std::unique(C.hb, C.hb + nh) - C.hb);
             if (C.nhb == 0) C.hb[C.nhb++] = 0;  // (no valid node: one harmless recount)
@@ -7124,7 +7203,9 @@ int small_refresh(kad_table* t, hipStream_t s, const uint32_t* mnode, uint32_t m
     // one block when it holds every listed node; the count <= 8 lines built by it when at most RF_FUSE_LINES can
     // be listed (6 per changed bucket) and no slot lines depend on them
     const bool single = total <= BLOCK;
-    const int fuse = (!B || 6ull * total > RF_FUSE_LINES || t->sl_mut) ? 0 : t->wl_mut ? 1 : t->gl_mut ? 2 : 0;
+    // (window-line builders derive the lines of nodes in device lists with one wave: at most 64 of them)
+    int fuse = (!B || 6ull * total > RF_FUSE_LINES || t->sl_mut) ? 0 : t->wl_mut ? 1 : t->gl_mut ? 2 : 0;
+    if (fuse == 1 && !C.nhb && total > 64) fuse = 0;
     dim3 g1(std::min<uint32_t>((total + BLOCK - 1) / BLOCK, 64u));
     if (fuse) {  // (6 * total <= RF_FUSE_LINES: one block derives every node) + builder blocks, all lines in one round
         C.list[0] = nullptr;

@@ -100,7 +100,7 @@ def main():
     res["live_ev"] = eager(True, True)
     # single refreshes passing k deadlines: GPU time between events, host time of the call
     ticks = {}
-    for k in (0, 1, 4, 16, 64, 256, 2048):
+    for k in (0, 1, 4, 16, 64, 100, 128, 256, 2048):
         i0 = int(np.searchsorted(D, now, "right"))
         target = now + 1 if k == 0 else int(D[i0 + k - 1]) + 1
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

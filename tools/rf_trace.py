@@ -41,7 +41,7 @@ def main():
     MIN = 60 * 10**9
     D = np.unique(np.minimum(t + 10 * MIN, r + 120 * MIN)[ex == 0])
     for rep in range(3):
-        for k in (1, 2, 4, 8, 16, 64):
+        for k in (1, 2, 4, 8, 16, 64, 100, 128):
             i0 = int(np.searchsorted(D, now, "right"))
             target = int(D[i0 + k - 1]) + 1
             L.kad_rt_closest_batch(h, C.c_void_p(tg.data_ptr()), Q, 8, C.c_void_p(out.data_ptr()),
