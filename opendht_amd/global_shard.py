@@ -250,7 +250,7 @@ class GlobalShard:
             ctr.zero_()
         else:
             s = stream
-            with torch.cuda.stream(torch.cuda.ExternalStream(s, device=self.dev)):
+            with torch.cuda.stream(_torch_stream(s, self.dev)):
                 ctr.zero_()
         base = ex.send.data_ptr()
         check(lib().kad_rt_shard_batch(self.table.handle, ptr(self.gpre), self.GB, C.c_uint64(self.base_hi),
@@ -272,7 +272,7 @@ class GlobalShard:
                 rank = rank_of(group) if ex.world > 1 else 0
             self.home_block(targets, ex, s)
             if ex.world > 1:
-                with torch.cuda.stream(torch.cuda.ExternalStream(s, device=self.dev)):
+                with torch.cuda.stream(_torch_stream(s, self.dev)):
                     exchange_into(ex.recv, ex.send, group)
             ex.home_finish(rank, out_idx, out_cnt, C.c_void_p(s))
             return
@@ -281,7 +281,7 @@ class GlobalShard:
             if stream is None:
                 gather_into(ex.recv, ex.send, group)
             else:
-                with torch.cuda.stream(torch.cuda.ExternalStream(s, device=self.dev)):
+                with torch.cuda.stream(_torch_stream(s, self.dev)):
                     gather_into(ex.recv, ex.send, group)
         ex.finish(out_idx, out_cnt, C.c_void_p(s))
 
@@ -411,6 +411,17 @@ def gather_into(recv, send, group=None):
         dist.all_gather(tmp, send, group=group)
         for o, t in zip(out, tmp):
             o.copy_(t)
+
+
+def _torch_stream(s, dev):
+    """The torch stream object for a raw hipStream_t handle. 0 is the null (legacy default) stream, which is torch's
+    default stream: that stream itself, never ExternalStream(0), which does not name the null stream (work on it
+    would not be ordered after the kernels the library launched on the null stream)."""
+    import torch
+
+    if not s:
+        return torch.cuda.default_stream(dev)
+    return torch.cuda.ExternalStream(s, device=dev)
 
 
 def rank_of(group=None) -> int:

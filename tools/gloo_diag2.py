@@ -35,14 +35,34 @@ def worker(rank, world, port, out):
     log = []
     orig = GS.exchange_into
 
+    mode = os.environ.get("GLOO_DIAG_MODE", "both")
+
     def wrapped(recv, send, group=None):
         ex_block = recv.numel() // world
-        torch.cuda.synchronize()
-        sc = [send[d * ex_block:(d + 1) * ex_block][-320:].cpu().numpy().reshape(10, 32)[:, 0].tolist() for d in range(world)]
+        if mode == "inspect":  # exchange_into's gloo path, logging what the host copy of `send` held
+            import ctypes as C
+            hip = C.CDLL("libamdhip64.so")
+            cur = torch.cuda.current_stream()
+            q0 = hip.hipStreamQuery(C.c_void_p(cur.cuda_stream))
+            cs = send.cpu()
+            ctr_cs = [cs[d * ex_block:(d + 1) * ex_block][-320:].numpy().reshape(10, 32)[:, 0].tolist() for d in range(world)]
+            torch.cuda.synchronize()
+            cs2 = send.cpu()
+            ctr_cs2 = [cs2[d * ex_block:(d + 1) * ex_block][-320:].numpy().reshape(10, 32)[:, 0].tolist() for d in range(world)]
+            orig(recv, send, group)
+            log.append({"block": ex_block, "stream": cur.cuda_stream, "query_before": q0, "ctr_first_copy": ctr_cs,
+                        "ctr_after_sync": ctr_cs2, "same": bool(torch.equal(cs, cs2))})
+            return
+        if mode in ("before", "both"):
+            torch.cuda.synchronize()
+        if mode == "stream":  # the current (torch) stream only: the stream the step's kernels were launched on
+            torch.cuda.current_stream().synchronize()
+        if mode == "null":  # the legacy null stream only
+            torch.cuda.Stream(stream_ptr=0).synchronize() if hasattr(torch.cuda, "Stream") else None
         orig(recv, send, group)
-        torch.cuda.synchronize()
-        rc = [recv[d * ex_block:(d + 1) * ex_block][-320:].cpu().numpy().reshape(10, 32)[:, 0].tolist() for d in range(world)]
-        log.append({"block": ex_block, "send_ctr": sc, "recv_ctr": rc, "stream": torch.cuda.current_stream().cuda_stream})
+        if mode in ("after", "both"):
+            torch.cuda.synchronize()
+        log.append({"block": ex_block, "stream": torch.cuda.current_stream().cuda_stream})
 
     GS.exchange_into = wrapped
     rec = {"rank": rank}
