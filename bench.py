@@ -977,14 +977,18 @@ def live_pass(T, sh, tgs, outs, ocnt, cnt_k, Q, dev, stream, now, t, rt, ex, D, 
     vr = min(Q, vrows)
     bad = verify_rows(sh.ids, st, sh.first, sh.off, sh.index_base, tgs[last][:vr].cpu().numpy(),
                       outs[last][:vr].cpu().numpy(), ocnt[last][:vr].cpu().numpy(), cnt_k)
-    # single refreshes passing k deadlines, each alone between two events (the events' own floor: k = 0)
+    # single refreshes passing k deadlines, as in the loop: queued behind a query batch, so the device runs the
+    # refresh as soon as the batch ends (event a) and b - a is its device time (k = 0: the events' own floor);
+    # host_us: the call's host time
     ticks = {}
     now = nows[-1]
-    for k in (0, 1, 4, 16, 64):
+    for k in (0, 1, 4, 16, 64, 100):
         i0 = int(np.searchsorted(D, now, "left"))
         nxt = now + 1 if k == 0 else int(D[min(D.shape[0] - 1, i0 + k - 1)]) + 1
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         torch.cuda.synchronize(dev)
+        tp, op, cp = P[k % NB]
+        rt_fn(h, tp, Q, cnt_k, op, cp, s)
         a.record(stream)
         h0 = time.perf_counter()
         rf_fn(h, C.c_int64(nxt), s)
@@ -1007,8 +1011,9 @@ def live_pass(T, sh, tgs, outs, ocnt, cnt_k, Q, dev, stream, now, t, rt, ex, D, 
                          "what": "the first rows of the last step against the CPU restatement at that step's `now`"},
             "how": "K steps of refresh_status(now = start + elapsed wall time) + one Q-query batch on one stream, "
                    "eager through direct C-ABI calls; queries_per_s = K*Q / wall; refresh_share = 1 - (the same loop "
-                   "without the refresh) / wall; single_refresh_us: one refresh passing k deadlines between two HIP "
-                   "events (k = 0: the events' floor, no GPU work) and the host time of the call"}
+                   "without the refresh) / wall; single_refresh_us: one refresh passing k deadlines queued behind a query "
+                   "batch, its device time between an event after the batch and one after the refresh (k = 0: the "
+                   "events' floor, no GPU work), and the host time of the call"}
     return live, now + 1
 
 

@@ -6827,6 +6827,7 @@ int build_sl16(kad_table* t);
 int setup_slot_lines(kad_table* t) {
     DevTable& d = t->d;
     if (!(d.flags & TF_GL) || !t->gl_mut || d.B == 0 || d.rslots == 0 || t->h_first.size() < 20ull * d.B) return KAD_OK;
+    if (std::getenv("KAD_NO_SLOT_LINES")) return KAD_OK;  // test hook: general lines alone (the fused general-line refresh)
     const uint32_t B = d.B;
     const uint8_t* f = t->h_first.data();
     int pick = -1;

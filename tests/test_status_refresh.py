@@ -250,9 +250,10 @@ def test_host_batch_ordered_after_async_refresh(gpu):
                 np.testing.assert_array_equal(cnt, wcnt)
 
 
+@pytest.mark.parametrize("nosl", [False, True], ids=["", "nosl"])
 @pytest.mark.parametrize("t", [TB.uniform_config(50_000, 12, seed=0x5EA), TB.split_config(30_000, seed=0x5EB)],
                          ids=lambda t: t["name"])
-def test_small_refresh_every_line_set(gpu, t):
+def test_small_refresh_every_line_set(gpu, t, nosl, monkeypatch):
     """The small refresh path (at most 2,048 nodes to re-derive: rf_nodes_kernel lists the changed buckets and the
     lines whose windows reach them, the builders rebuild only those) on tables holding every line set (uniform:
     short, 128-byte, 9..16, 17..32 and NodeCache lines; split policy: slot, general 8 / 16 / 32 lines and their
@@ -261,6 +262,10 @@ def test_small_refresh_every_line_set(gpu, t):
     refreshed at the same `now`; patch_status of a few nodes, including the first and last buckets' (windows
     clamped at the table's ends). After every step the status bytes equal isGood / isExpired and every query
     equals the oracle."""
+    if nosl:  # the split table without slot lines: the fused general-line refresh (KAD_NO_SLOT_LINES)
+        if t["sorted"]:
+            pytest.skip("uniform tables have no slot lines")
+        monkeypatch.setenv("KAD_NO_SLOT_LINES", "1")
     n = t["ids"].shape[0]
     off = t["off"]
     rng = np.random.default_rng(n)
@@ -362,15 +367,23 @@ def test_small_refresh_shapes(gpu, t):
 LINESETS = ("WL", "WS", "WL16", "WL32", "GL", "GL16", "GL32", "SL", "SL16", "NCL", "NCL32", "GCNT", "DIR")
 
 
+@pytest.mark.parametrize("nosl", [False, True], ids=["", "nosl"])
 @pytest.mark.parametrize("t", [TB.uniform_config(40_000, 12, seed=0x5EC), TB.split_config(20_000, seed=0x5ED),
                                TB.uniform_config(6_000, 12, seed=0x5EE)], ids=lambda t: t["name"])
-def test_incremental_lines_equal_fresh_build(gpu, t):
+def test_incremental_lines_equal_fresh_build(gpu, t, nosl, monkeypatch):
     """Every derived array an incremental refresh maintains (window, short, general and slot lines of every count,
     NodeCache lines, per-bucket good counts, the directory's masks) is bit for bit what a table built from scratch
     on the same status holds: after refreshes passing 1, 2, 5, 9, 30 and 3000 deadlines (the one-launch path whose
     lines a wave builds, the single-block and multi-block lists, the flag path), a patch of times and one of status
-    bytes. The U(12) 6,000-node table has sparse buckets (windows of several rounds, deferred lines)."""
+    bytes. The U(12) 6,000-node table has sparse buckets (windows of several rounds, deferred lines). nosl: the
+    split table without slot lines (KAD_NO_SLOT_LINES), so the count <= 8 general lines are rebuilt in the fused
+    launch (block 0 publishes the list to the builder blocks)."""
     from opendht_amd import _lib
+
+    if nosl:
+        if t["sorted"]:
+            pytest.skip("uniform tables have no slot lines")
+        monkeypatch.setenv("KAD_NO_SLOT_LINES", "1")
 
     n = t["ids"].shape[0]
     rng = np.random.default_rng(n ^ 0x5EC)

@@ -105,6 +105,8 @@ def main():
         target = now + 1 if k == 0 else int(D[i0 + k - 1]) + 1
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         torch.cuda.synchronize()
+        tp, op, cp = P[k % NB]  # queued behind a query batch: the events bracket the refresh's device time
+        assert rt(h, tp, Q, 8, op, cp, s) == 0
         a.record(stream)
         h0 = time.perf_counter()
         assert rf(h, C.c_int64(target), s) == 0
