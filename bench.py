@@ -1117,6 +1117,15 @@ def allgather_pass(args, world, rank, local, dev, dist):
                                            "step) instead of the plain batch"}
         # the exchange each rank would receive at N = 2, 4, 8 for this Q and count (layouts only, nothing sent)
         res["exchange_model"] = exchange_model(Q, cnt_k, dev)
+        # rank 0's device work at N = 8, timed here on its shard of the same table: the shard kernel over the
+        # replicated batch into 8 home blocks, and the finish over 8 blocks of its rows (copies of its own block
+        # to itself: the other ranks' blocks have the same shape); with the modelled all_to_all, a step's time and
+        # the aggregate rate N = 8 ranks would reach on this replicated batch
+        try:
+            res["n8_step_model"] = n8_step_model(ids, st, off, gp if world == 1 else None, spec, tgs, Q, cnt_k, K, NB,
+                                                 dev, res["exchange_model"]["8"]["home_modelled_us"])
+        except Exception as e:  # a model, never the line's failure
+            res["n8_step_model"] = {"error": f"{type(e).__name__}: {e}"}
     else:
         ex = G.exchange(Q, cnt_k, world)
         lo, hi = home_range(Q, world, rank)
@@ -1159,6 +1168,56 @@ def allgather_pass(args, world, rank, local, dev, dist):
         return res
     G.close()
     return res
+
+
+def n8_step_model(ids, st, off, gp, spec, tgs, Q, cnt_k, K, NB, dev, xchg_us):
+    """Rank 0's kernels at N = 8 (see allgather_pass), HIP events around K eager launches each."""
+    import torch
+
+    from opendht_amd.global_shard import GlobalShard
+
+    B = off.shape[0] - 1
+    hi = B // 8
+    n0 = int(off[hi])
+    G0 = GlobalShard(ids[:n0], st[:n0], off[:hi + 1], 0, hi, spec.depth, 0, gp, device=dev.index or 0)
+    try:
+        ex = G0.exchange(Q, cnt_k, 8)
+        stream = torch.cuda.current_stream(dev)
+        for j in range(2):
+            G0.home_block(tgs[j % NB], ex)
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize(dev)
+        a.record(stream)
+        for j in range(K):
+            G0.home_block(tgs[j % NB], ex)
+        b.record(stream)
+        torch.cuda.synchronize(dev)
+        shard_us = a.elapsed_time(b) / K * 1e3
+        blk = ex.send[:ex.block]
+        ex.recv = torch.cat([blk] * 8)
+        lo, hi_q = 0, -(-(-(-Q // 256)) // 8) * 256
+        oi = torch.empty((min(hi_q, Q), cnt_k), dtype=torch.int32, device=dev)
+        oc = torch.empty((min(hi_q, Q),), dtype=torch.uint8, device=dev)
+        import ctypes as C
+        s = C.c_void_p(stream.cuda_stream)
+        ex.home_finish(0, oi, oc, s)
+        torch.cuda.synchronize(dev)
+        a.record(stream)
+        for j in range(K):
+            ex.home_finish(0, oi, oc, s)
+        b.record(stream)
+        torch.cuda.synchronize(dev)
+        fin_us = a.elapsed_time(b) / K * 1e3
+        step_us = shard_us + xchg_us + fin_us
+        return {"shard_kernel_us": shard_us, "finish_us": fin_us, "exchange_modelled_us": xchg_us,
+                "step_modelled_us": step_us, "aggregate_queries_per_s_modelled": Q / (step_us * 1e-6),
+                "shard_nodes": n0,
+                "how": "rank 0 of 8 (global buckets [0, B/8), no halo) on this GPU: kad_rt_shard_batch_home over "
+                       "the whole replicated batch into 8 home blocks, kad_rt_home_finish over 8 blocks (copies of "
+                       "the block it sends itself: timing only); + the modelled all_to_all at N = 8. The eight ranks "
+                       "answer the one batch together, so the aggregate is Q / step"}
+    finally:
+        G0.close()
 
 
 def exchange_model(Q, count, dev, link_gbs=64.0):
