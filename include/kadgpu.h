@@ -143,8 +143,8 @@ int kad_table_prepare(kad_table* t, uint32_t sets);
 int kad_table_line_sets(const kad_table* t, uint32_t* built, uint64_t* bytes, float* build_ms);
 
 /* Replace the status snapshot (host bytes, n_nodes). Synchronous. Incremental: only the buckets whose
- * good set changed get new masks, and only the window / NodeCache lines whose window reaches a changed
- * node are rebuilt (the good prefix sums are re-scanned). */
+ * good set changed get new masks and good counts, and only the window / NodeCache lines whose window reaches
+ * a changed node are rebuilt. */
 int kad_table_update_status(kad_table* t, const uint8_t* status);
 /* Incremental status update for a changed-node list (reference: the isGood/isExpired flips that
  * Node::received / setExpired cause, node.cpp:82-108; network_engine.cpp:245): node nodes[j] gets
@@ -171,8 +171,10 @@ int kad_table_patch_times(kad_table* t, uint32_t m, const uint32_t* nodes, const
  * deadline (with nothing patched) returns at once without touching the GPU. The host keeps a copy of the
  * sorted deadlines (8 bytes per node) and finds the passed ones itself. Up to 2,048 such nodes take the
  * small path: one kernel re-derives them and lists the changed buckets and the lines whose windows reach
- * them, then the line builders rebuild only those (no pass over the buckets or the lines); more take the
- * flag-and-compact path. Async on `stream` (the first refresh after set_times waits for the sort);
+ * them, then the line builders rebuild only those (no pass over the buckets or the lines); up to 128 of them
+ * on a table with window lines are one launch in all (block 0 re-derives the nodes, the other blocks rebuild
+ * the count <= 8 lines at the same time, the host having found the nodes' buckets and the lines). More take
+ * the flag-and-compact path. Async on `stream` (the first refresh after set_times waits for the sort);
  * later refreshes and device batches must be ordered after it by the caller (the host-pointer batches
  * order themselves). A refresh that changes anything ends the table's resident query service launch
  * (kad_table_serve) first. */
