@@ -3428,10 +3428,19 @@ __device__ void wave_shard(const DevTable& T, const ShardCtx& S, const Target& t
               complete ? nullptr : row + (S.rs), xs);
 }
 
-template <bool WL>
+// LK: the window-line set the shard's uniform table answers from (8: counts <= 8, 16: 9..16, 32: 17..32; 0: none).
+// A window of that set spans at most LK / 2 buckets on either side, so a query whose bucket lies that far inside the
+// shard has the same window locally as globally.
+template <int LK>
 __global__ __launch_bounds__(BLOCK) void rt_shard_kernel(DevTable T, ShardCtx S, const uint8_t* __restrict__ targets,
                                                          uint32_t q, uint32_t count) {
-    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    constexpr uint32_t MARGIN = LK == 8 ? 4u : LK == 16 ? 8u : 16u;
+    // The block's queries within the shard's reach, compacted to its first lanes (at N ranks a shard reaches ~1/N of
+    // the replicated batch: the waves that would hold only out-of-reach lanes then do no line or wave work)
+    __shared__ uint64_t c_hi[BLOCK];
+    __shared__ uint32_t c_t2[BLOCK], c_t3[BLOCK], c_t4[BLOCK], c_i[BLOCK], c_b[BLOCK];
+    __shared__ uint32_t c_w[BLOCK / 64 + 1];
+    uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     Target t{};
     bool near = false, line = false;
     uint32_t b = 0;
@@ -3439,14 +3448,43 @@ __global__ __launch_bounds__(BLOCK) void rt_shard_kernel(DevTable T, ShardCtx S,
         t = load_target(targets, i);
         b = shard_bucket(S, t);
         near = b >= S.reach_lo && b < S.reach_hi;
-        line = WL && near && b >= S.s_lo + 4 && b + 4 <= S.s_hi;
+    }
+    {
+        const uint64_t nm = __ballot(near);
+        const uint32_t w = threadIdx.x >> 6;
+        if ((threadIdx.x & 63u) == 0) c_w[w] = (uint32_t)__builtin_popcountll(nm);
+        __syncthreads();
+        uint32_t pos = lanes_below(nm), tot = 0;
+        for (uint32_t k = 0; k < BLOCK / 64; k++) {
+            pos += k < w ? c_w[k] : 0u;
+            tot += c_w[k];
+        }
+        if (near) {
+            c_hi[pos] = t.hi; c_t2[pos] = t.t2; c_t3[pos] = t.t3; c_t4[pos] = t.t4; c_i[pos] = i; c_b[pos] = b;
+        }
+        __syncthreads();
+        near = threadIdx.x < tot;
+        if (near) {
+            t.hi = c_hi[threadIdx.x]; t.t2 = c_t2[threadIdx.x]; t.t3 = c_t3[threadIdx.x]; t.t4 = c_t4[threadIdx.x];
+            i = c_i[threadIdx.x];
+            b = c_b[threadIdx.x];
+        }
+        line = LK && near && b >= S.s_lo + MARGIN && b + MARGIN <= S.s_hi;
     }
     bool edge = near;
     __shared__ uint64_t xs[BLOCK / 64][192];
     __shared__ uint32_t wcnt[BLOCK / 64 + 1];
-    if (WL && __syncthreads_or(line)) {  // block-uniform
-        uint32_t o[8], m;
-        const bool ok = line8_answer(T, t, line ? b - S.s_lo : 0u, count, line, line && (T.flags & TF_WS), o, m);
+    if (LK && __syncthreads_or(line)) {  // block-uniform
+        uint32_t o[LK ? LK : 1], m = 0;
+        // (a wave whose lanes are all past the compacted queries skips the line work: a wave-uniform branch)
+        bool ok = false;
+        if (__any(line)) {
+            const uint32_t bl = line ? b - S.s_lo : 0u;
+            if constexpr (LK == 8) ok = line8_answer(T, t, bl, count, line, line && (T.flags & TF_WS), o, m);
+            else if constexpr (LK == 16) ok = wl16_answer(T, t, bl, count, line, o, m);
+            else if constexpr (LK == 32) ok = wl32_answer(T, t, bl, count, line, o, m);
+            ok = ok && line;
+        }
         const uint64_t want = __ballot(ok);
         const uint32_t w = threadIdx.x >> 6;
         if ((threadIdx.x & 63u) == 0) wcnt[w] = (uint32_t)__builtin_popcountll(want);
@@ -3465,7 +3503,9 @@ __global__ __launch_bounds__(BLOCK) void rt_shard_kernel(DevTable T, ShardCtx S,
             if (slot < S.row_cap) {
                 uint32_t* row = S.rows + dof + ((size_t)(blockIdx.x & 7u) * S.row_cap + slot) * S.rs;
                 reinterpret_cast<uint4*>(row)[0] = make_uint4(i, m, 0u, 0u);
-                store_row8(row + 4, o, count);
+                if constexpr (LK == 8) store_row8(row + 4, o, count);
+                else if constexpr (LK == 16) store_row16(row + 4, o, count);
+                else if constexpr (LK == 32) store_row32(row + 4, o, count);
                 edge = false;
             } else {
                 atomicOr(S.ctr + dof + KAD_SHARD_COUNTER_STRIDE * 9u, 1u);
@@ -8261,15 +8301,16 @@ static int shard_batch(const kad_table* t, const uint32_t* global_good_prefix, u
     S.dests = dests;
     S.nblk = (q + BLOCK - 1) / BLOCK;
     S.dest_words = dest_words;
-    // the window line is valid for a shard of a uniform table of the same depth
-    const bool wl = count <= 8 && (t->d.flags & TF_WL) && (64 - t->d.rshift) == depth;
+    // the window lines are valid for a shard of a uniform table of the same depth (built on first use for
+    // counts 9..32, as for the unsharded query)
+    const bool uni = (t->d.flags & TF_WL) && (64 - t->d.rshift) == depth;
+    if (uni && count > 8 && (rc = ensure_lines(t, count <= 16 ? LS_WL16 : LS_WL32, (hipStream_t)stream))) return rc;
+    const uint32_t fl = t->d.flags;
+    const int lk = !uni ? 0 : count <= 8 ? 8 : count <= 16 ? ((fl & TF_WL16) ? 16 : 0) : ((fl & TF_WL32) ? 32 : 0);
     DeviceGuard g(t->device);
-    if (wl)
-        hipLaunchKernelGGL(rt_shard_kernel<true>, dim3(grid_for(q)), dim3(BLOCK), 0, (hipStream_t)stream, t->d, S,
-                           targets, q, count);
-    else
-        hipLaunchKernelGGL(rt_shard_kernel<false>, dim3(grid_for(q)), dim3(BLOCK), 0, (hipStream_t)stream, t->d, S,
-                           targets, q, count);
+    void (*kern)(DevTable, ShardCtx, const uint8_t*, uint32_t, uint32_t) =
+        lk == 8 ? rt_shard_kernel<8> : lk == 16 ? rt_shard_kernel<16> : lk == 32 ? rt_shard_kernel<32> : rt_shard_kernel<0>;
+    hipLaunchKernelGGL(kern, dim3(grid_for(q)), dim3(BLOCK), 0, (hipStream_t)stream, t->d, S, targets, q, count);
     HIP_TRY(hipGetLastError());
     return KAD_OK;
 }
