@@ -5290,12 +5290,18 @@ struct RfCtx {
     // with inline nodes, derived on the host from its copy of the bucket offsets (0: derived on the device):
     uint32_t nhb;                        // the listed nodes' buckets, sorted and distinct
     uint32_t hb[128];
+    uint32_t inb[128];                   // nhb: node inl[j]'s bucket hb[inb[j] & 127] and, when that bucket holds at
+                                         // most 32 nodes (a directory mask), 1 + its place in it (inb[j] >> 8)
     uint32_t nhl;                        // FUSE 1: the window lines to rebuild, as nhr runs of consecutive lines:
     uint32_t nhr;                        //   run r = lines hr[3r] .. hr[3r] + hr[3r+1] - 1, whose windows' bucket
     uint32_t hr[3 * 16];                 //   offsets h_off[max(0, first - 3) ..] start at hoff[hr[3r+2]]
     uint32_t hoff[256];
+#ifdef KAD_ABLATIONS
+    uint32_t abl;  // tools build (KAD_RF_ABL): 1 = builder blocks return at once, 2 = block 0 returns at once
+#endif
 };
 constexpr uint32_t RF_INLINE = 128, RF_HOFF = 256;
+static_assert(sizeof(RfCtx) <= 4096, "rf_nodes_kernel's arguments must fit the 4 KB kernel-argument limit");
 
 // One atomic per wave for the lanes with `want` (wave-uniform call); returns each wanting lane's slot.
 __device__ __forceinline__ uint32_t wave_append(uint32_t* ctr, bool want) {
@@ -5664,7 +5670,7 @@ constexpr uint32_t RF_POOL = BLOCK * (33 + 17);  // dwords: phase 2's sort buffe
 // derived here as phase 1 derives them, so no line waits for block 0's status writes. Only a window of more than
 // 64 nodes (the serial builder, which reads the table's statuses and good counts) waits for block 0's epoch
 // (published after its good counts). A listed node whose status did not change rebuilds lines that come out the same.
-__device__ void rf_wl_builders(const RfCtx& C, uint32_t* pool) {
+__device__ __attribute__((always_inline)) void rf_wl_builders(const RfCtx& C, uint32_t* pool) {
     const DevTable& T = C.T;
     const uint32_t B = T.B, lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
     const uint32_t total = C.ninl ? C.ninl : C.mc + C.sc + C.np;  // inline <= RF_INLINE, lists <= 64
@@ -5673,7 +5679,19 @@ __device__ void rf_wl_builders(const RfCtx& C, uint32_t* pool) {
     __shared__ uint32_t s_st[64];
     __shared__ uint32_t s_lines[RF_FUSE_LINES];
     __shared__ uint32_t s_nl;
+    // the kernel arguments the line loop searches (inline nodes, runs, offsets), staged in LDS in one round of
+    // independent loads: a wave-uniform search of them in the argument segment was a chain of dependent scalar loads
+    __shared__ uint32_t s_inl[RF_INLINE], s_hr[3 * 16], s_hoff[RF_HOFF];
     const bool host_lines = C.nhl != 0;
+    {
+        const uint32_t tid = threadIdx.x;
+        if (tid < C.ninl) s_inl[tid] = C.inl[tid];
+        if (host_lines) {
+            if (tid < 3 * C.nhr) s_hr[tid] = C.hr[tid];
+            for (uint32_t o = tid; o < RF_HOFF; o += BLOCK) s_hoff[o] = C.hoff[o];
+        }
+        __syncthreads();
+    }
     if (!host_lines) {  // block-uniform
         if (wid == 0 && C.nhb) {
             // the host's buckets (sorted, distinct, <= RF_INLINE): merge [b-2, b+3] in passes of 64
@@ -5764,11 +5782,11 @@ __device__ void rf_wl_builders(const RfCtx& C, uint32_t* pool) {
         uint32_t b, n0, n1;  // (wave-uniform)
         if (host_lines) {  // the run of line x and its offsets (kernel arguments)
             uint32_t r = 0, k = x;
-            while (r + 1 < C.nhr && k >= C.hr[3 * r + 1]) k -= C.hr[3 * r + 1], r++;
-            const uint32_t first = C.hr[3 * r];
+            while (r + 1 < C.nhr && k >= s_hr[3 * r + 1]) k -= s_hr[3 * r + 1], r++;
+            const uint32_t first = s_hr[3 * r];
             b = first + k;
             const uint32_t db = b >= 3 ? b - 3 : 0u, e = min(B, b + 3);
-            const uint32_t* hl = C.hoff + C.hr[3 * r + 2] + (db - (first >= 3 ? first - 3 : 0u));
+            const uint32_t* hl = s_hoff + s_hr[3 * r + 2] + (db - (first >= 3 ? first - 3 : 0u));
             if (lane < 8) WV.dx[lane] = hl[min(lane, e - db)];
             n0 = hl[0];
             n1 = hl[e - db];
@@ -5793,10 +5811,10 @@ __device__ void rf_wl_builders(const RfCtx& C, uint32_t* pool) {
                 uint32_t lo = 0, hi = C.ninl;
                 while (lo < hi) {  // wave-uniform lower_bound of n0
                     const uint32_t mid = (lo + hi) >> 1;
-                    if (C.inl[mid] < n0) lo = mid + 1; else hi = mid;
+                    if (s_inl[mid] < n0) lo = mid + 1; else hi = mid;
                 }
                 bool listed = false;
-                for (uint32_t j = lo; j < C.ninl && C.inl[j] < n1; j++) listed |= C.inl[j] == n;
+                for (uint32_t j = lo; j < C.ninl && s_inl[j] < n1; j++) listed |= s_inl[j] == n;
                 sv = !have ? 0u : listed ? status_at(C.N, n, C.now) : (uint32_t)C.status[n];
             } else {  // device lists: the statuses wave 0 derived
                 sv = have ? C.status[n] : 0u;
@@ -5896,8 +5914,16 @@ __device__ void rf_fused_lines(const RfCtx& C, uint32_t* pool, uint32_t n8, cons
 }
 
 template <bool SINGLE, int FUSE>
-__global__ __launch_bounds__(BLOCK) void rf_nodes_kernel(RfCtx C) {
+__global__ __launch_bounds__(BLOCK) void rf_nodes_kernel(RfCtx C_arg) {
     static_assert(!FUSE || SINGLE, "a fused refresh derives its nodes in block 0");
+    // the argument read in place through the segment pointer (it is the only one): indexed per lane, the by-value
+    // argument was copied to scratch whole (3.2 KB per lane)
+#if __HIP_DEVICE_COMPILE__
+    const RfCtx& C = *(const RfCtx*)__builtin_amdgcn_kernarg_segment_ptr();
+    (void)C_arg;
+#else
+    const RfCtx& C = C_arg;
+#endif
     const DevTable& T = C.T;
 #ifdef KAD_RF_TRACE
     uint64_t rf_ts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -5905,6 +5931,9 @@ __global__ __launch_bounds__(BLOCK) void rf_nodes_kernel(RfCtx C) {
     RF_STAMP(0);
     __shared__ __attribute__((aligned(16))) uint32_t pool[RF_POOL];
     __shared__ uint32_t lctr[2];
+#ifdef KAD_ABLATIONS
+    if ((C.abl == 1 && blockIdx.x > 0) || (C.abl == 2 && blockIdx.x == 0)) return;
+#endif
     if (FUSE == 1 && blockIdx.x > 0) {  // a window-line builder block (independent of block 0)
         rf_wl_builders(C, pool);
 #ifdef KAD_RF_TRACE
@@ -5966,6 +5995,13 @@ __global__ __launch_bounds__(BLOCK) void rf_nodes_kernel(RfCtx C) {
             if (st != old) C.status[i] = (uint8_t)st;
         }
         const bool gchg = act && T.B && !C.nhb && ((st ^ old) & KAD_STATUS_GOOD);  // (nhb: the host's buckets)
+        if (act && T.B && C.nhb && ((st ^ old) & KAD_STATUS_GOOD)) {
+            // the host's buckets: the flip patches its bucket's good count and mask in place (no recount: the
+            // nodes are distinct, the atomics return nothing, block 0's release below orders them before RF_GO)
+            const uint32_t e = C.inb[j], hbk = C.hb[e & 127u];
+            atomicAdd(C.gcnt + hbk, (st & KAD_STATUS_GOOD) ? 1u : ~0u);
+            if (e >> 8) atomicXor(reinterpret_cast<uint32_t*>(C.dir + hbk) + 1, 1u << ((e >> 8) - 1));
+        }
         const uint32_t b = gchg ? node_bucket(T, C.dir, i, key_i) : 0u;
         const bool echg = act && C.list[3] && ((st ^ old) & KAD_STATUS_EXPIRED);
         uint32_t sa = 0, se = 0;
@@ -6058,8 +6094,8 @@ __global__ __launch_bounds__(BLOCK) void rf_nodes_kernel(RfCtx C) {
         __syncthreads();
     }
     RF_STAMP(3);
-    // their masks and good counts (bucket_good_kernel for these buckets)
-    for (uint32_t u = threadIdx.x; u < nu; u += BLOCK) {
+    // their masks and good counts (bucket_good_kernel for these buckets; the host's buckets were patched in phase 1)
+    for (uint32_t u = threadIdx.x; u < (C.nhb ? 0u : nu); u += BLOCK) {
         const uint32_t b = ub[u];
         const uint32_t j0 = C.dir[b].x & ~WIDE, j1 = C.dir[b + 1].x & ~WIDE;
         uint32_t g = 0, mask = 0;
@@ -7199,15 +7235,22 @@ int small_refresh(kad_table* t, hipStream_t s, const uint32_t* mnode, uint32_t m
         C.ninl = std::min(ninl, RF_INLINE);
         std::memcpy(C.inl, inl, 4ull * C.ninl);
         std::sort(C.inl, C.inl + C.ninl);  // (the builders search them by node)
+        C.ninl = (uint32_t)(std::unique(C.inl, C.inl + C.ninl) - C.inl);  // (each flip patches its bucket once)
         // their buckets from the host's copy of the bucket offsets (no locate on the device), and for the window
         // lines the lines to rebuild with the offsets their builders read (no directory load before the keys)
         if (B && t->h_off.size() == (size_t)B + 1) {
-            uint32_t nh = 0;
+            uint32_t nh = 0, nb_[RF_INLINE];
             for (uint32_t j = 0; j < C.ninl; j++)
-                if (C.inl[j] < d.n) C.hb[nh++] = bucket_of_node(t->h_off, d.n, C.inl[j]);
+                if (C.inl[j] < d.n) C.hb[nh++] = nb_[j] = bucket_of_node(t->h_off, d.n, C.inl[j]);
             std::sort(C.hb, C.hb + nh);
             C.nhb = (uint32_t)(std::unique(C.hb, C.hb + nh) - C.hb);
             if (C.nhb == 0) C.hb[C.nhb++] = 0;  // (no valid node: one harmless recount)
+            for (uint32_t j = 0; j < C.ninl; j++) {
+                if (C.inl[j] >= d.n) continue;
+                const uint32_t b = nb_[j], u = (uint32_t)(std::lower_bound(C.hb, C.hb + C.nhb, b) - C.hb);
+                const uint32_t a = t->h_off[b], sz = t->h_off[b + 1] - a;
+                C.inb[j] = u | (sz <= 32 ? (C.inl[j] - a + 1) << 8 : 0u);
+            }
             // the union of [b-2, b+3] (ascending) as runs of consecutive lines, with the bucket offsets their
             // windows [l-3, l+3] read
             uint32_t nl = 0, nr = 0, no = 0;
@@ -7261,6 +7304,9 @@ int small_refresh(kad_table* t, hipStream_t s, const uint32_t* mnode, uint32_t m
         g1 = fuse == 1 ? dim3(1 + (lines + BLOCK / 64 - 1) / (BLOCK / 64))
                        : dim3(std::max<uint32_t>(1, (lines + BLOCK / 16 - 1) / (BLOCK / 16)));
     }
+#ifdef KAD_ABLATIONS
+    if (const char* e = std::getenv("KAD_RF_ABL")) C.abl = (uint32_t)std::atoi(e);
+#endif
     if (fuse == 1) hipLaunchKernelGGL((rf_nodes_kernel<true, 1>), g1, dim3(BLOCK), 0, s, C);
     else if (fuse == 2) hipLaunchKernelGGL((rf_nodes_kernel<true, 2>), g1, dim3(BLOCK), 0, s, C);
     else if (single) hipLaunchKernelGGL((rf_nodes_kernel<true, 0>), g1, dim3(BLOCK), 0, s, C);
