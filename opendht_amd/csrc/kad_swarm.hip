@@ -206,13 +206,35 @@ __device__ uint32_t peer_closest(const SwarmDev& W, uint32_t p, const Tgt& t, ui
 #pragma unroll
     for (uint32_t s = 0; s < K; s++) { L0[s] = ~0ull; LI[s] = NONE; }
     uint32_t nl = 0;
+    static_assert(BK == 8, "a level's slots are two 16-byte index loads and four 16-byte key loads");
     for (uint32_t P = lo; P <= hi; P++) {
         const uint32_t d = level(P), nb = cp[d];
-        const uint32_t* ep = W.ent + ((size_t)p * L + d) * BK;
-        const uint64_t* kp = W.ekey + ((size_t)p * L + d) * BK;
+        // the level's 8 slots in one round of 16-byte loads (the slots from nb on are padding, skipped)
+        const uint4* ep4 = reinterpret_cast<const uint4*>(W.ent + ((size_t)p * L + d) * BK);
+        const uint4* kp4 = reinterpret_cast<const uint4*>(W.ekey + ((size_t)p * L + d) * BK);
+        uint32_t ei[BK];
+        uint64_t ek[BK];
+#pragma unroll
+        for (int x = 0; x < 2; x++) {
+            const uint4 u = ep4[x];
+            ei[4 * x] = u.x; ei[4 * x + 1] = u.y; ei[4 * x + 2] = u.z; ei[4 * x + 3] = u.w;
+        }
+#pragma unroll
+        for (int x = 0; x < 4; x++) {
+            const uint4 u = kp4[x];
+            ek[2 * x] = ((uint64_t)u.y << 32) | u.x;
+            ek[2 * x + 1] = ((uint64_t)u.w << 32) | u.z;
+        }
+#pragma unroll 1
         for (uint32_t j = 0; j < nb; j++) {
-            uint64_t cd = kp[j] ^ t.hi;
-            uint32_t ci = ep[j];
+            uint64_t cd = ek[0];
+            uint32_t ci = ei[0];
+#pragma unroll
+            for (uint32_t y = 1; y < BK; y++) {  // (a select chain: the slots stay in registers)
+                cd = j == y ? ek[y] : cd;
+                ci = j == y ? ei[y] : ci;
+            }
+            cd ^= t.hi;
             bool sh = false;
 #pragma unroll
             for (uint32_t s = 0; s < K; s++) {
@@ -235,7 +257,7 @@ __device__ uint32_t peer_closest(const SwarmDev& W, uint32_t p, const Tgt& t, ui
     return m;
 }
 
-__global__ void swarm_closest_kernel(SwarmDev W, const uint32_t* peers, const uint8_t* targets, uint32_t q, uint32_t count,
+__global__ __launch_bounds__(BLOCK) void swarm_closest_kernel(SwarmDev W, const uint32_t* peers, const uint8_t* targets, uint32_t q, uint32_t count,
                                      uint32_t* out_idx, uint8_t* out_cnt) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (i >= q) return;
@@ -283,38 +305,88 @@ __device__ __forceinline__ bool swarm_offline(uint32_t p, uint32_t per10k) {
 }
 
 // first <= ALPHA nodes in list order that are neither queried nor bad (searchSendGetValues / canGet,
-// dht.cpp:302-304, 1171-1235) -> sel, marked queried; none -> stalled
-__device__ __forceinline__ void select_next(const SearchDev& X, uint32_t s, uint32_t n, uint8_t* q, const uint8_t* bd,
-                                            const uint32_t* li) {
-    uint32_t k = 0;
-    for (uint32_t j = 0; j < n && k < ALPHA; j++)
-        if (!q[j] && !bd[j]) { X.sel[(size_t)s * ALPHA + k++] = li[j]; q[j] = 1; }
-    for (uint32_t j = k; j < ALPHA; j++) X.sel[(size_t)s * ALPHA + j] = NONE;
-    if (k == 0) X.done[s] = 2;
+// dht.cpp:302-304, 1171-1235) -> sel, marked queried; none -> stalled. The queried and bad flags are bit masks (bit k:
+// list entry k; bits from n on are don't-care) and every list index is static, so the lists stay in registers.
+__device__ __forceinline__ uint32_t lo_mask(uint32_t n) { return n >= 32 ? ~0u : (1u << n) - 1u; }
+
+template <uint32_t N>
+__device__ __forceinline__ void select_next(const SearchDev& X, uint32_t s, uint32_t n, uint32_t& qm, uint32_t bm,
+                                            const uint32_t (&li)[N]) {
+    uint32_t rest = ~(qm | bm) & lo_mask(min(n, N)), pick = 0;
+#pragma unroll
+    for (uint32_t a = 0; a < ALPHA; a++) {
+        pick |= rest & (0u - rest);
+        rest &= rest - 1u;
+    }
+    qm |= pick;
+    uint32_t sel[ALPHA] = {NONE, NONE, NONE, NONE};
+#pragma unroll
+    for (uint32_t j = 0; j < N; j++) {
+        const uint32_t rk = (uint32_t)__builtin_popcount(pick & ((1u << j) - 1u));
+        if ((pick >> j) & 1u)
+#pragma unroll
+            for (uint32_t a = 0; a < ALPHA; a++)
+                if (a == rk) sel[a] = li[j];
+    }
+    reinterpret_cast<uint4*>(X.sel)[s] = make_uint4(sel[0], sel[1], sel[2], sel[3]);  // (ALPHA = 4)
+    if (!pick) X.done[s] = 2;
 }
 
-__global__ void search_init_kernel(SwarmDev W, SearchDev X) {
+// the list's flag bytes (queried or bad) of search s as a bit mask, and back (entries from n on: 0)
+__device__ __forceinline__ uint32_t load_flags(const uint8_t* f, uint32_t s) {
+    const uint4* p = reinterpret_cast<const uint4*>(f + (size_t)s * LST);
+    uint32_t m = 0;
+#pragma unroll
+    for (int x = 0; x < (int)LST / 16; x++) {
+        const uint4 u = p[x];
+        const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+        for (int y = 0; y < 4; y++)
+#pragma unroll
+            for (int z = 0; z < 4; z++) m |= (((w[y] >> (8 * z)) & 255u) ? 1u : 0u) << (16 * x + 4 * y + z);
+    }
+    return m;
+}
+__device__ __forceinline__ void store_flags(uint8_t* f, uint32_t s, uint32_t m, uint32_t n) {
+    m &= lo_mask(n);
+    uint4* p = reinterpret_cast<uint4*>(f + (size_t)s * LST);
+#pragma unroll
+    for (int x = 0; x < (int)LST / 16; x++) {
+        uint32_t w[4];
+#pragma unroll
+        for (int y = 0; y < 4; y++) {
+            w[y] = 0;
+#pragma unroll
+            for (int z = 0; z < 4; z++) w[y] |= ((m >> (16 * x + 4 * y + z)) & 1u) << (8 * z);
+        }
+        p[x] = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+}
+static_assert(LST == 32 && ALPHA == 4, "the flag masks are 32 bits, the selection one 16-byte store");
+
+__global__ __launch_bounds__(BLOCK) void search_init_kernel(SwarmDev W, SearchDev X) {
     const uint32_t s = blockIdx.x * BLOCK + threadIdx.x;
     if (s >= X.S) return;
     uint32_t li[SNP];
     uint64_t lk[SNP];
-    uint8_t q[SNP] = {0}, bd[SNP] = {0};
+    uint32_t qm = 0;
     const uint32_t p = X.src[s];
     const uint32_t n = p < W.n ? peer_closest<SNP>(W, p, load_tgt(X.targets, s), SN, li, lk) : 0u;
     X.done[s] = n ? 0 : 2;
     X.hops[s] = 0;
     X.ln[s] = (uint8_t)n;
-    if (n) select_next(X, s, n, q, bd, li);
+    if (n) select_next(X, s, n, qm, 0u, li);
+#pragma unroll
     for (uint32_t j = 0; j < LST; j++) {
-        X.li[(size_t)s * LST + j] = j < n ? li[j] : NONE;
-        X.lk[(size_t)s * LST + j] = j < n ? lk[j] : ~0ull;
-        X.lq[(size_t)s * LST + j] = j < n ? q[j] : 0;
-        X.lb[(size_t)s * LST + j] = 0;
+        X.li[(size_t)s * LST + j] = j < SNP && j < n ? li[j < SNP ? j : 0] : NONE;
+        X.lk[(size_t)s * LST + j] = j < SNP && j < n ? lk[j < SNP ? j : 0] : ~0ull;
     }
+    store_flags(X.lq, s, qm, n);
+    store_flags(X.lb, s, 0u, n);
 }
 
 // one lane per (search, queried node): its findClosestNodes(t, 8), or nothing if it is offline
-__global__ void search_query_kernel(SwarmDev W, SearchDev X) {
+__global__ __launch_bounds__(BLOCK) void search_query_kernel(SwarmDev W, SearchDev X) {
     const uint32_t g = blockIdx.x * BLOCK + threadIdx.x;
     if (g >= X.S * ALPHA) return;
     const uint32_t s = g / ALPHA;
@@ -337,56 +409,68 @@ constexpr uint32_t XO_CAP = 64;  // silent peers remembered per lookup (4 per ho
 // (`if (node.isExpired()) bad++`, dht.cpp:1023-1025):
 // its place is after every closer entry; if the list already holds SEARCH_NODES non-bad nodes it is first cut
 // after the last prefix with SEARCH_NODES non-bad nodes (an insert beyond that point is refused), then
-// trimmed from the end while it holds more than SEARCH_NODES non-bad nodes. Static indices only.
+// trimmed from the end while it holds more than SEARCH_NODES non-bad nodes. Static indices only; the queried and
+// bad flags are bit masks (qm, bm).
 __device__ __forceinline__ void search_insert(const SwarmDev& W, const Tgt& t, uint32_t (&li)[LST], uint64_t (&ld)[LST],
-                                              uint8_t (&q)[LST], uint8_t (&bd)[LST], uint32_t& n, uint32_t r,
-                                              uint64_t rd, bool rbad, bool& ovf) {
+                                              uint32_t& qm, uint32_t& bm, uint32_t& n, uint32_t r, uint64_t rd, bool rbad,
+                                              bool& ovf) {
     bool found = false;
-    uint32_t pos = 0, bad = 0;
+    uint32_t pos = 0, tie = 0;
 #pragma unroll
     for (uint32_t k = 0; k < LST; k++) {
         if (k < n) {
             found |= li[k] == r;
-            pos += ld[k] < rd || (ld[k] == rd && li[k] != r && tail_less(W, t, li[k], r));
-            bad += bd[k];
+            pos += ld[k] < rd;
+            tie |= (ld[k] == rd && li[k] != r ? 1u : 0u) << k;
         }
     }
     if (found) return;
-    const bool full = n - bad >= SN;
-    // tt = the largest t <= n whose prefix [0, t) holds at most SEARCH_NODES non-bad nodes
-    uint32_t tt = 0, nb = 0, badt = 0, bb = 0;
+    while (tie) {  // equal top 64 bits (rare): the full 160-bit order (a select chain keeps the index static)
+        const uint32_t k = (uint32_t)__builtin_ctz(tie);
+        tie &= tie - 1u;
+        uint32_t lk = 0;
 #pragma unroll
-    for (uint32_t k = 0; k <= LST; k++) {
-        if (k <= n && nb <= SN) { tt = k; badt = bb; }
-        if (k < n && k < LST) { nb += bd[k] ? 0u : 1u; bb += bd[k]; }
+        for (uint32_t x = 0; x < LST; x++) lk = x == k ? li[x] : lk;
+        pos += tail_less(W, t, lk, r);
     }
+    uint32_t bad = (uint32_t)__builtin_popcount(bm & lo_mask(n));
+    const bool full = n - bad >= SN;
     if (full) {
+        // tt = the largest t <= n whose prefix [0, t) holds at most SEARCH_NODES non-bad nodes: the prefix ends
+        // just before the (SN + 1)-th non-bad entry (or at n)
+        uint32_t good = ~bm & lo_mask(n);
+#pragma unroll
+        for (uint32_t k = 0; k < SN; k++) good &= good - 1u;  // drop the first SN non-bad entries
+        const uint32_t tt = good ? (uint32_t)__builtin_ctz(good) : n;
         n = tt;
-        bad = badt;
+        bad = (uint32_t)__builtin_popcount(bm & lo_mask(n));
         if (pos >= tt) return;
     }
     if (n == LST) {  // capacity: drop the farthest entry (counted; never reached in the tests)
-        bad -= bd[LST - 1];
+        bad -= (bm >> (LST - 1)) & 1u;
         n--;
         ovf = true;
         if (pos >= n) return;
     }
-    // insert at pos
+    // insert at pos: entries from pos on move up one (selects, not conditional stores: those became stores through
+    // a selected pointer and put the lists in scratch); entries from n + 1 on are don't-care
 #pragma unroll
     for (uint32_t k = LST - 1; k > 0; k--) {
-        if (k > pos && k <= n) { li[k] = li[k - 1]; ld[k] = ld[k - 1]; q[k] = q[k - 1]; bd[k] = bd[k - 1]; }
+        li[k] = k > pos ? li[k - 1] : k == pos ? r : li[k];
+        ld[k] = k > pos ? ld[k - 1] : k == pos ? rd : ld[k];
     }
-#pragma unroll
-    for (uint32_t k = 0; k < LST; k++) {
-        if (k == pos) { li[k] = r; ld[k] = rd; q[k] = 0; bd[k] = rbad ? 1 : 0; }
-    }
+    li[0] = pos == 0 ? r : li[0];
+    ld[0] = pos == 0 ? rd : ld[0];
+    const uint32_t low = lo_mask(pos), bit = 1u << pos;
+    qm = (qm & low) | ((qm & ~low) << 1);
+    bm = (bm & low) | ((bm & ~low) << 1) | (rbad ? bit : 0u);
     n++;
     bad += rbad ? 1u : 0u;
     // while more than SEARCH_NODES non-bad nodes: drop the last one
 #pragma unroll
     for (int k = (int)LST - 1; k >= 0; k--) {
         if ((uint32_t)k == n - 1 && n - bad > SN) {
-            bad -= bd[k];
+            bad -= (bm >> k) & 1u;
             n--;
         }
     }
@@ -394,22 +478,30 @@ __device__ __forceinline__ void search_insert(const SwarmDev& W, const Tgt& t, u
 
 // one lane per search: Search::insertNode of every answer in the order of the queried nodes, then the
 // offline queried nodes turn bad (expired), then the isSynced / expired checks and the next hop's selection
-__global__ void search_merge_kernel(SwarmDev W, SearchDev X) {
+__global__ __launch_bounds__(BLOCK) void search_merge_kernel(SwarmDev W, SearchDev X) {
     const uint32_t s = blockIdx.x * BLOCK + threadIdx.x;
     bool running = false;
     if (s < X.S && !X.done[s]) {
         const Tgt t = load_tgt(X.targets, s);
         uint32_t li[LST];
         uint64_t ld[LST];  // top-64 XOR distances
-        uint8_t q[LST], bd[LST];
         uint32_t n = X.ln[s];
+        {
+            const uint4* pi = reinterpret_cast<const uint4*>(X.li + (size_t)s * LST);
+            const uint4* pk = reinterpret_cast<const uint4*>(X.lk + (size_t)s * LST);
 #pragma unroll
-        for (uint32_t j = 0; j < LST; j++) {
-            li[j] = X.li[(size_t)s * LST + j];
-            ld[j] = X.lk[(size_t)s * LST + j] ^ t.hi;
-            q[j] = X.lq[(size_t)s * LST + j];
-            bd[j] = X.lb[(size_t)s * LST + j];
+            for (uint32_t x = 0; x < LST / 4; x++) {
+                const uint4 u = pi[x];
+                li[4 * x] = u.x; li[4 * x + 1] = u.y; li[4 * x + 2] = u.z; li[4 * x + 3] = u.w;
+            }
+#pragma unroll
+            for (uint32_t x = 0; x < LST / 2; x++) {
+                const uint4 u = pk[x];
+                ld[2 * x] = (((uint64_t)u.y << 32) | u.x) ^ t.hi;
+                ld[2 * x + 1] = (((uint64_t)u.w << 32) | u.z) ^ t.hi;
+            }
         }
+        uint32_t qm = load_flags(X.lq, s), bm = load_flags(X.lb, s);
         const uint32_t src = X.src[s];
         bool ovf = false;
         const uint32_t* xo = X.xo + (size_t)s * XO_CAP;
@@ -423,45 +515,53 @@ __global__ void search_merge_kernel(SwarmDev W, SearchDev X) {
                 bool rbad = false;
                 if (swarm_offline(r, X.offline))
                     for (uint32_t e = 0; e < xn && !rbad; e++) rbad = xo[e] == r;
-                search_insert(W, t, li, ld, q, bd, n, r, X.rk[(size_t)g * BK + j] ^ t.hi, rbad, ovf);
+                search_insert(W, t, li, ld, qm, bm, n, r, X.rk[(size_t)g * BK + j] ^ t.hi, rbad, ovf);
             }
         }
+        const uint4 sv = reinterpret_cast<const uint4*>(X.sel)[s];
+        const uint32_t sel[ALPHA] = {sv.x, sv.y, sv.z, sv.w};
+#pragma unroll
         for (uint32_t a = 0; a < ALPHA; a++) {  // the silent ones: expired after their tries -> bad
-            const uint32_t v = X.sel[(size_t)s * ALPHA + a];
+            const uint32_t v = sel[a];
             if (v == NONE || !swarm_offline(v, X.offline)) continue;
             if (xn < XO_CAP) X.xo[(size_t)s * XO_CAP + xn++] = v;  // its node is expired from now on
             else ovf = true;
 #pragma unroll
             for (uint32_t k = 0; k < LST; k++)
-                if (k < n && li[k] == v) bd[k] = 1;
+                if (k < n && li[k] == v) bm |= 1u << k;
         }
         X.xn[s] = (uint8_t)xn;
         X.hops[s] += 1;
         // Search::isSynced: the first TARGET_NODES non-bad nodes answered; consecutive bad nodes from the front
-        uint32_t good = 0, cb = 0;
-        bool synced = true, stop = false, lead = true;
+        const uint32_t nm = lo_mask(n), good = ~bm & nm;
+        uint32_t first8 = good;  // the first BK non-bad entries
+        {
+            uint32_t rest = good;
 #pragma unroll
-        for (uint32_t k = 0; k < LST; k++) {
-            if (k < n) {
-                lead &= bd[k] != 0;
-                cb += lead ? 1u : 0u;
-                if (!stop && !bd[k]) {
-                    if (!q[k]) { synced = false; stop = true; }
-                    else if (++good == BK) stop = true;
-                }
+            for (uint32_t k = 0; k < BK; k++) rest &= rest - 1u;
+            first8 &= ~rest;
+        }
+        const bool synced = (first8 & ~qm) == 0;
+        const uint32_t lead = ~(bm & nm), cb = lead ? (uint32_t)__builtin_ctz(lead) : 32u;  // leading bad entries
+        if (synced && first8) X.done[s] = 1;
+        else if (n > 0 && cb >= min(n, MAX_BAD)) X.done[s] = 3;
+        else select_next(X, s, n, qm, bm, li);
+        X.ln[s] = (uint8_t)n;
+        {
+            uint4* pi = reinterpret_cast<uint4*>(X.li + (size_t)s * LST);
+            uint4* pk = reinterpret_cast<uint4*>(X.lk + (size_t)s * LST);
+#pragma unroll
+            for (uint32_t x = 0; x < LST / 4; x++)
+                pi[x] = make_uint4(4 * x < n ? li[4 * x] : NONE, 4 * x + 1 < n ? li[4 * x + 1] : NONE,
+                                   4 * x + 2 < n ? li[4 * x + 2] : NONE, 4 * x + 3 < n ? li[4 * x + 3] : NONE);
+#pragma unroll
+            for (uint32_t x = 0; x < LST / 2; x++) {
+                const uint64_t k0 = 2 * x < n ? ld[2 * x] ^ t.hi : ~0ull, k1 = 2 * x + 1 < n ? ld[2 * x + 1] ^ t.hi : ~0ull;
+                pk[x] = make_uint4((uint32_t)k0, (uint32_t)(k0 >> 32), (uint32_t)k1, (uint32_t)(k1 >> 32));
             }
         }
-        if (synced && good > 0) X.done[s] = 1;
-        else if (n > 0 && cb >= min(n, MAX_BAD)) X.done[s] = 3;
-        else select_next(X, s, n, q, bd, li);
-        X.ln[s] = (uint8_t)n;
-#pragma unroll
-        for (uint32_t j = 0; j < LST; j++) {
-            X.li[(size_t)s * LST + j] = j < n ? li[j] : NONE;
-            X.lk[(size_t)s * LST + j] = j < n ? ld[j] ^ t.hi : ~0ull;
-            X.lq[(size_t)s * LST + j] = j < n ? q[j] : 0;
-            X.lb[(size_t)s * LST + j] = j < n ? bd[j] : 0;
-        }
+        store_flags(X.lq, s, qm, n);
+        store_flags(X.lb, s, bm, n);
         if (ovf) atomicAdd(X.overflow, 1u);
         running = !X.done[s];
     }
