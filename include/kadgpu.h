@@ -336,7 +336,9 @@ int kad_nc_closest_batch_dual(const kad_table* table4, const kad_table* table6,
  * never overflows.
  * The ranks' rows and parts are all-gathered by the caller (RCCL); kad_rt_scatter_rows and
  * kad_rt_merge_parts (parts sorted by qid) then give every query's findClosestNodes result.
- * All pointers are device pointers; count in 1..KAD_MAX_COUNT. */
+ * All pointers are device pointers; count in 1..KAD_MAX_COUNT. Queries far enough inside the shard
+ * answer from the window lines of their count (counts 9..32: the 16/32-count sets, built on first
+ * use as for kad_rt_closest_batch; kad_table_prepare builds them ahead of a stream capture). */
 #define KAD_ROW_WORDS(count) (4u + (((count) + 3u) & ~3u))
 #define KAD_PART_WORDS(count) (KAD_ROW_WORDS(count) + 5u * (count))
 #define KAD_SHARD_REGIONS 8u
