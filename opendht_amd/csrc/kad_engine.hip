@@ -4699,6 +4699,27 @@ __global__ void ncl_build_kernel(const uint64_t* key, const uint8_t* status, con
 // ---------------------------------------------------------------------------------------
 constexpr uint32_t NC32_SLOTS = 124, NC32_LEFT = 56, NC32_XMAX = 15, NC32_STRIDE = 128;  // dwords
 
+// Octet (8-lane group) cross-lane moves without address arithmetic: quad permutes and row shifts by DPP, the lane-4
+// exchange and the octet broadcast by ds_swizzle's bit-mask mode (lane' = ((lane & and) | or) ^ xor within 32 lanes).
+// __shfl_xor / __shfl_up with width 8 compiled to ds_bpermute with a per-lane address (several VALU ops each).
+template <int O>  // the value of lane g ^ O of the octet (O = 1, 2, 4)
+__device__ __forceinline__ uint32_t oct_xor(uint32_t v) {
+    if constexpr (O == 1) return qdpp<QP_X1>(v);
+    else if constexpr (O == 2) return qdpp<QP_X2>(v);
+    else return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x1F | (4 << 10));
+}
+template <int O>  // the value of lane g - O (row_shr; the caller masks g < O, which read another octet or 0)
+__device__ __forceinline__ uint32_t oct_up(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x110 | O, 0xF, 0xF, true);
+}
+template <int O>  // the value of lane g + O (row_shl; the caller masks g + O > 7)
+__device__ __forceinline__ uint32_t oct_down(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x100 | O, 0xF, 0xF, true);
+}
+__device__ __forceinline__ uint32_t oct_last(uint32_t v) {  // lane 7 of the octet
+    return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x18 | (0x07 << 5));
+}
+
 // One octet per radix slot: lane g builds dwords [16g, 16g + 16) of line s.
 __global__ __launch_bounds__(BLOCK) void ncl32_build_kernel(const uint64_t* key, const uint8_t* status,
                                                              const uint32_t* nrdx, uint32_t nslots, uint32_t n,
@@ -4806,11 +4827,12 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) v
                 eq |= k24 == t24 ? 1u : 0u;
             }
         }
-#pragma unroll
-        for (int o = 1; o < 8; o <<= 1) {
-            below += (uint32_t)__shfl_xor((int)below, o, 8);
-            eq |= (uint32_t)__shfl_xor((int)eq, o, 8);
-        }
+        below += oct_xor<1>(below);
+        eq |= oct_xor<1>(eq);
+        below += oct_xor<2>(below);
+        eq |= oct_xor<2>(eq);
+        below += oct_xor<4>(below);
+        eq |= oct_xor<4>(eq);
         const uint32_t p = NC32_LEFT + below;
         bool ex = (fl & 1u) || eq;
         // the runs' first 64 steps: left step 8g+u = element p-1-step, right step 63-8g-u = element p+step. Key:
@@ -4835,12 +4857,23 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) v
         for (int u = 0; u < 8; u++) pa[u] = ca = max(ca, ka[u]);
 #pragma unroll
         for (int u = 7; u >= 0; u--) pb[u] = cb = max(cb, kb[u]);
-#pragma unroll
-        for (int o = 1; o < 8; o <<= 1) {
-            ca = max(ca, (uint32_t)__shfl_up((int)ca, o, 8));
-            cb = max(cb, (uint32_t)__shfl_down((int)cb, o, 8));
+        // (lanes whose partner lies outside the octet take 0, which max leaves alone). Every lane runs the move and
+        // then selects: a move under `cond ? move : 0` runs with the other lanes off, and a DPP read of an inactive
+        // lane returns 0.
+        {
+            uint32_t ya = oct_up<1>(ca), yb = oct_down<1>(cb);
+            ca = max(ca, g >= 1 ? ya : 0u);
+            cb = max(cb, g + 1 <= 7 ? yb : 0u);
+            ya = oct_up<2>(ca);
+            yb = oct_down<2>(cb);
+            ca = max(ca, g >= 2 ? ya : 0u);
+            cb = max(cb, g + 2 <= 7 ? yb : 0u);
+            ya = oct_up<4>(ca);
+            yb = oct_down<4>(cb);
+            ca = max(ca, g >= 4 ? ya : 0u);
+            cb = max(cb, g + 4 <= 7 ? yb : 0u);
         }
-        const uint32_t ua = (uint32_t)__shfl_up((int)ca, 1, 8), ub = (uint32_t)__shfl_down((int)cb, 1, 8);
+        const uint32_t ua = oct_up<1>(ca), ub = oct_down<1>(cb);
         const uint32_t inA = g > 0 ? ua : 0u, inB = g < 7 ? ub : 0u;
 #pragma unroll
         for (int u = 0; u < 8; u++) {  // the key's distance = the run maximum up to the step (bitfield insert)
@@ -4869,13 +4902,23 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) v
         uint32_t w[8];
 #pragma unroll
         for (int u = 0; u < 8; u++) w[u] = min(ka[u], kb[u]);
-#pragma unroll
-        for (int o = 4; o >= 1; o >>= 1) {
-            const uint32_t hi = (g & (uint32_t)o) ? 0xFFFFFFFFu : 0u;
+        {
+            const uint32_t hi4 = (g & 4u) ? 0xFFFFFFFFu : 0u, hi2 = (g & 2u) ? 0xFFFFFFFFu : 0u,
+                           hi1 = (g & 1u) ? 0xFFFFFFFFu : 0u;
 #pragma unroll
             for (int u = 0; u < 8; u++) {
-                const uint32_t y = (uint32_t)__shfl_xor((int)w[u], o, 8);
-                w[u] = max(min(w[u], y), min(max(w[u], y), hi));  // v_med3_u32
+                const uint32_t y = oct_xor<4>(w[u]);
+                w[u] = max(min(w[u], y), min(max(w[u], y), hi4));  // v_med3_u32
+            }
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                const uint32_t y = oct_xor<2>(w[u]);
+                w[u] = max(min(w[u], y), min(max(w[u], y), hi2));
+            }
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                const uint32_t y = oct_xor<1>(w[u]);
+                w[u] = max(min(w[u], y), min(max(w[u], y), hi1));
             }
         }
 #pragma unroll
@@ -4893,12 +4936,15 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) v
             kept += keep[u];
         }
         uint32_t cr = kept;
-#pragma unroll
-        for (int o = 1; o < 8; o <<= 1) {
-            const uint32_t y = (uint32_t)__shfl_up((int)cr, o, 8);
-            if (g >= (uint32_t)o) cr += y;
+        {
+            uint32_t y = oct_up<1>(cr);  // (moves outside the select, as above)
+            cr += g >= 1 ? y : 0u;
+            y = oct_up<2>(cr);
+            cr += g >= 2 ? y : 0u;
+            y = oct_up<4>(cr);
+            cr += g >= 4 ? y : 0u;
         }
-        const uint32_t tot = (uint32_t)__shfl((int)cr, (int)((lane & ~7u) | 7u), 64);
+        const uint32_t tot = oct_last(cr);
         ok = !ex && tot >= count;
         // the row through the octet's LDS row (the line is no longer read): entry `rank` at W[rank]
         __builtin_amdgcn_wave_barrier();
