@@ -3608,9 +3608,8 @@ __device__ __forceinline__ const uint32_t* gather_ctr(const GatherCtx& G, uint32
     return G.recv + (size_t)r * G.block + G.ctr_off;
 }
 
-__global__ void gather_scatter_kernel(GatherCtx G, uint32_t* __restrict__ out_idx, uint8_t* __restrict__ out_cnt,
-                                      uint32_t* __restrict__ overflow) {
-    const uint64_t g = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+__device__ __forceinline__ void gather_scatter(const GatherCtx& G, uint64_t g, uint32_t* __restrict__ out_idx,
+                                               uint8_t* __restrict__ out_cnt, uint32_t* __restrict__ overflow) {
     const uint64_t per = (uint64_t)KAD_SHARD_REGIONS * G.row_cap;
     const uint32_t r = (uint32_t)(g / per);
     if (r >= G.world) return;
@@ -3646,8 +3645,19 @@ __device__ __forceinline__ const uint32_t* gather_part(const GatherCtx& G, uint6
     return G.recv + (size_t)r * G.block + G.parts_off + (size_t)p * G.ps;
 }
 
-__global__ void gather_link_kernel(GatherCtx G, uint32_t* __restrict__ head, uint32_t* __restrict__ next) {
-    const uint64_t x = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+// One launch for the two independent passes of a finish: blocks [0, sblocks) scatter the complete rows, the others
+// link each part into its query's chain (the merge that walks the chains is the next launch).
+__global__ __launch_bounds__(BLOCK) void gather_scatter_link_kernel(GatherCtx G, uint32_t sblocks,
+                                                                    uint32_t* __restrict__ out_idx,
+                                                                    uint8_t* __restrict__ out_cnt,
+                                                                    uint32_t* __restrict__ overflow,
+                                                                    uint32_t* __restrict__ head,
+                                                                    uint32_t* __restrict__ next) {
+    if (blockIdx.x < sblocks) {  // block-uniform
+        gather_scatter(G, (uint64_t)blockIdx.x * BLOCK + threadIdx.x, out_idx, out_cnt, overflow);
+        return;
+    }
+    const uint64_t x = (uint64_t)(blockIdx.x - sblocks) * BLOCK + threadIdx.x;
     const uint32_t* part = gather_part(G, x);
     if (!part || part[0] - G.qbase >= G.q) return;
     next[x] = atomicExch(head + (part[0] - G.qbase), (uint32_t)x);
@@ -8504,8 +8514,10 @@ static int gather_finish(const uint32_t* recv, uint32_t world, uint32_t row_cap,
     hipStream_t s = (hipStream_t)stream;
     const uint64_t nrows = (uint64_t)world * KAD_SHARD_REGIONS * row_cap, nparts = (uint64_t)world * part_cap;
     if (nrows > 0xFFFFFFFFull * BLOCK || nparts >= 0xFFFFFFFFull) return set_err(KAD_ERR_INVALID, "buffers too large");
-    hipLaunchKernelGGL(gather_scatter_kernel, dim3(grid_for(nrows)), dim3(BLOCK), 0, s, G, out_idx, out_cnt, overflow);
-    hipLaunchKernelGGL(gather_link_kernel, dim3(grid_for(nparts)), dim3(BLOCK), 0, s, G, head, next);
+    const uint32_t sb = grid_for(nrows), lb = grid_for(nparts);
+    if ((uint64_t)sb + lb > 0x7FFFFFFFull) return set_err(KAD_ERR_INVALID, "buffers too large");
+    hipLaunchKernelGGL(gather_scatter_link_kernel, dim3(sb + lb), dim3(BLOCK), 0, s, G, sb, out_idx, out_cnt, overflow,
+                       head, next);
     hipLaunchKernelGGL(gather_merge_kernel, dim3(grid_for(nparts)), dim3(BLOCK), 0, s, G, head, next, out_idx, out_cnt);
     HIP_TRY(hipGetLastError());
     return KAD_OK;
