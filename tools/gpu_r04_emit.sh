@@ -1,6 +1,7 @@
 # A/B of a parked NodeCache count <= 16 variant (opendht_amd/libkadgpu_emit.so: branch-free emission in ncl_answer)
 # against the product library: its parity tests, then tools/nc_time.py on both.
 # Usage (on the GPU box): bash tools/gpu_r04_emit.sh [tag]; output under gpurun_out/<tag>/.
+# (The variant library was built from profiles/r04/parked/emit/nc_emit_variant.patch and removed after the A/B.)
 set -o pipefail
 T=${1:-r04emit}
 R=${GRAFT_REPO_ROOT:-$(pwd)}

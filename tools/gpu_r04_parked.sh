@@ -3,6 +3,7 @@
 # per-bucket offsets for up to 128 host buckets (libkadgpu_rf.so, libkadgpu_rf_abl.so). Each variant's parity tests
 # run against it, then the timing tools against it and against the product library.
 # Usage (on the GPU box): bash tools/gpu_r04_parked.sh [tag]; output under gpurun_out/<tag>/.
+# (The variant libraries were built from the patches under profiles/r04/parked/ and removed after the A/B.)
 set -o pipefail
 T=${1:-r04parked}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
