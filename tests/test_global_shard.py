@@ -104,7 +104,7 @@ def test_global_shards_simulated_gather(gpu, case):
     shards = _build(spec, gpu.index or 0)
     grew = False
     try:
-        for count in (1, 3, 8, 9, 14, 32):
+        for count in (1, 3, 8, 9, 14, 16, 24, 32):
             want, wcnt = O.flat_rt_closest(gids, gst, gfirst, goff, targets, count, nthreads=8)
             for home in (True, False):
                 for caps in ((None, None), (1, 1)):
