@@ -61,7 +61,7 @@ def parse_args(argv=None):
     ap.add_argument("--gather-json", default=os.path.join(ROOT, "profiles", "r03_mb_gather_nt.json"))
     ap.add_argument("--plumbing", action="store_true",
                     help="launcher/rendezvous check without a GPU: gloo ranks, barrier, max-over-ranks, one line")
-    ap.add_argument("--mode", choices=("owner", "allgather", "allgather-child"), default="owner",
+    ap.add_argument("--mode", choices=("owner", "allgather", "allgather-child", "rccl1-child"), default="owner",
                     help="owner: the headline (allgather measured as a sub-object); allgather: only the "
                          "north-star variant, as its own line; allgather-child: internal (allgather_child)")
     ap.add_argument("--verify-rows", type=int, default=1 << 16,
@@ -69,6 +69,8 @@ def parse_args(argv=None):
     ap.add_argument("--ag-timeout", type=float, default=240.0,
                     help="seconds before the north-star child processes (N > 1) are killed")
     ap.add_argument("--ag-out", default="", help="internal: where an allgather child writes its result")
+    ap.add_argument("--no-rccl1", action="store_true",
+                    help="N = 1: skip the one-rank RCCL step (allgather.rccl_world1, a child process)")
     return ap.parse_args(argv)
 
 
@@ -1126,6 +1128,9 @@ def allgather_pass(args, world, rank, local, dev, dist):
                                                  dev, res["exchange_model"]["8"]["home_modelled_us"])
         except Exception as e:  # a model, never the line's failure
             res["n8_step_model"] = {"error": f"{type(e).__name__}: {e}"}
+        if not args.no_rccl1:
+            G.close()
+            res["rccl_world1"] = rccl_world1_child(args)
     else:
         ex = G.exchange(Q, cnt_k, world)
         lo, hi = home_range(Q, world, rank)
@@ -1134,13 +1139,13 @@ def allgather_pass(args, world, rank, local, dev, dist):
             G.step(tgs[K], ex, oi, oc, rank=rank)
             if not ex.overflowed():
                 break
-            ex = G._ex[(Q, cnt_k, world, True)] = ex.grown()
+            ex = G._ex[(Q, cnt_k, world, True, world > 1)] = ex.grown()
         for _ in range(3):
             t_max, kern_ms, how = graph_steps(lambda j: G.step(tgs[j % NB], ex, oi, oc, rank=rank), K, 1, dev, dist,
                                               use_graph=False)
             if not ex.overflowed():
                 break
-            ex = G._ex[(Q, cnt_k, world, True)] = ex.grown()
+            ex = G._ex[(Q, cnt_k, world, True, world > 1)] = ex.grown()
         else:
             raise RuntimeError("exchange buffers kept overflowing")
         # verification: this rank's home rows (queries [lo, hi)) among the first vrows whose targets this rank
@@ -1273,6 +1278,119 @@ def allgather_child(args, world, rank, local, dist) -> dict:
     return res
 
 
+def rccl_world1_child(args) -> dict:
+    """The north-star step through a real one-rank RCCL group (rccl1_pass), in a child process with a timeout so
+    that a failing RCCL initialisation costs only this object."""
+    import tempfile
+
+    out = os.path.join(tempfile.gettempdir(), f"kadgpu_rccl1_{os.getpid()}.json")
+    argv = [sys.executable, "-u", os.path.abspath(__file__), "--mode", "rccl1-child", "--ag-out", out, "--queries",
+            str(args.queries), "--steps", str(args.steps), "--verify-rows", str(args.verify_rows)]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    p = subprocess.Popen(argv, env=env, stdout=sys.stderr)
+    try:
+        rc = p.wait(timeout=args.ag_timeout)
+    except subprocess.TimeoutExpired:
+        p.kill()
+        p.wait()
+        return {"error": f"the one-rank RCCL child was killed after {args.ag_timeout:.0f} s"}
+    try:
+        with open(out) as f:
+            res = json.load(f)
+        os.unlink(out)
+    except (OSError, ValueError):
+        res = {"error": f"the one-rank RCCL child exited with {rc} and no result"}
+    return res
+
+
+def rccl1_pass(args) -> dict:
+    """One rank, one real RCCL ("nccl") process group on this GPU: the north-star step with its collective forced
+    on (kad_rt_shard_batch_home, all_to_all_single of the send block through RCCL, kad_rt_home_finish) beside the
+    same step without it, on config 3's rank-0 shard as a table of its own (2^21 U(24) buckets, 12.5M nodes: the
+    per-GPU table size, targets in its range). HIP events around K eager steps each, and around the collective
+    alone; the last step's rows checked against the CPU restatement."""
+    import ctypes as C
+    from datetime import timedelta
+
+    import torch
+    import torch.distributed as dist
+
+    from opendht_amd.global_shard import GlobalShard, build_plain_shard, exchange_into
+    from opendht_amd.sharded import config3_spec
+    from opendht_amd.synth import bucket_firsts
+
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1, device_id=dev,
+                            timeout=timedelta(seconds=60))
+    try:
+        spec = config3_spec(8)
+        ids, st, off, lo, hi, base, good = build_plain_shard(spec, 0)
+        gp = np.concatenate([[0], np.cumsum(good.astype(np.int64))])
+        G = GlobalShard(ids, st, off, 0, hi, spec.depth, 0, gp, device=0)
+        Q, K, cnt_k = args.queries, max(4, min(args.steps, 20)), 8
+        NB = K + 2
+        tgs = device_targets(NB, Q, spec.shard_bits, 0, 0x0D470005, dev)
+        oi = torch.empty((Q, cnt_k), dtype=torch.int32, device=dev)
+        oc = torch.empty((Q,), dtype=torch.uint8, device=dev)
+        stream = torch.cuda.current_stream(dev)
+        res = {"workload": f"config 3's rank-0 shard as a table of its own ({ids.shape[0]} nodes, {hi} U(24) buckets), "
+                           f"{Q} queries per step, k={cnt_k}, one-rank RCCL group on this GPU",
+               "backend": dist.get_backend()}
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        for coll in (False, True):
+            ex = G.exchange(Q, cnt_k, 1, True, coll)
+            for _ in range(4):
+                G.step(tgs[K], ex, oi, oc, rank=0)
+                if not ex.overflowed():
+                    break
+                ex = G._ex[(Q, cnt_k, 1, True, coll)] = ex.grown()
+            torch.cuda.synchronize(dev)
+            a.record(stream)
+            for j in range(K):
+                G.step(tgs[j % NB], ex, oi, oc, rank=0)
+            b.record(stream)
+            torch.cuda.synchronize(dev)
+            key = "rccl" if coll else "no_collective"
+            res[f"step_us_{key}"] = a.elapsed_time(b) / K * 1e3
+            res[f"overflow_{key}"] = ex.overflowed()
+            vrows = min(Q, args.verify_rows)
+            first = bucket_firsts(spec.depth, 0, hi)
+            res[f"verified_{key}"] = {"rows": vrows, "mismatches": verify_rows(
+                ids, st, first, off, 0, tgs[(K - 1) % NB][:vrows].cpu().numpy(), oi[:vrows].cpu().numpy(),
+                oc[:vrows].cpu().numpy(), cnt_k)}
+            if coll:
+                res["block_bytes"] = 4 * ex.block
+                torch.cuda.synchronize(dev)
+                a.record(stream)
+                for j in range(K):
+                    exchange_into(ex.recv, ex.send)
+                b.record(stream)
+                torch.cuda.synchronize(dev)
+                res["all_to_all_us"] = a.elapsed_time(b) / K * 1e3
+        G.close()
+        res["how"] = ("Exchange(world=1, collective=True): the all_to_all_single of the one send block runs through "
+                      "RCCL (a device copy at world 1); the difference to step_us_no_collective is its cost")
+        return res
+    finally:
+        dist.destroy_process_group()
+
+
+def main_rccl1_child(args):
+    try:
+        res = rccl1_pass(args)
+    except Exception as e:
+        res = {"error": f"{type(e).__name__}: {e}"}
+    with open(args.ag_out, "w") as f:
+        json.dump(res, f)
+    return 0 if "error" not in res else 1
+
+
 def main_allgather_child(args):
     import torch
 
@@ -1351,6 +1469,8 @@ def main(argv=None):
         return main_allgather_line(args)
     if args.mode == "allgather-child":
         return main_allgather_child(args)
+    if args.mode == "rccl1-child":
+        return main_rccl1_child(args)
     return main_owner(args)
 
 

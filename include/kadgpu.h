@@ -67,6 +67,9 @@ extern "C" {
 #define KAD_TABLE_SORTED 0x01u      /* node array ascending by ID (enables NodeCache queries) */
 #define KAD_TABLE_EAGER 0x02u       /* build every line set at creation (default: those of count <= 8 RoutingTable
                                        queries; the others on first use, kad_table_prepare) */
+#define KAD_TABLE_NO_SLOT_LINES 0x04u /* general-line tables: no slot lines (count <= 8 / 9..16 queries locate
+                                         their bucket and read its general line; a status refresh then rebuilds
+                                         the count <= 8 general lines in its one fused launch) */
 
 /* line sets built on first use (kad_table_prepare, kad_table_line_sets) */
 #define KAD_LINES_RT16 0x01u        /* RoutingTable counts 9..16 (brings KAD_LINES_RT32, their fallback) */
@@ -179,6 +182,20 @@ int kad_table_patch_times(kad_table* t, uint32_t m, const uint32_t* nodes, const
  * order themselves). A refresh that changes anything ends the table's resident query service launch
  * (kad_table_serve) first. */
 int kad_table_refresh_status(kad_table* t, int64_t now_ns, void* stream);
+/* Counters of the small refresh since the table was created (synchronises the device):
+ *   spin_timeouts     builder blocks of a fused general-line refresh that waited RF_SPIN_TICKS (1 s) for the
+ *                     line list block 0 publishes and gave up (block 0 not running: the GPU busy with other
+ *                     work); their lines were then built by the launch's last block, so results stay exact
+ *   last_block_lines  lines built by a fused launch's last block (windows of more than 64 nodes, and the lists
+ *                     of timed-out builders)
+ *   guard_errors      bounds guards of the kernel that fired (bit mask; the host validates every inline
+ *                     argument before a launch, so this is 0 unless the engine has a bug) */
+typedef struct kad_refresh_diag {
+    uint32_t spin_timeouts;
+    uint32_t last_block_lines;
+    uint32_t guard_errors;
+} kad_refresh_diag;
+int kad_table_refresh_diag(const kad_table* t, kad_refresh_diag* out);
 
 /* ---- incremental device mirror ----------------------
  * Replays the table mutations of a live Dht on the device instead of re-snapshotting. Ops are rows

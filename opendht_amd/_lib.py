@@ -20,6 +20,7 @@ KAD_STATUS_GOOD = 0x01
 KAD_STATUS_EXPIRED = 0x02
 KAD_TABLE_SORTED = 0x01
 KAD_TABLE_EAGER = 0x02
+KAD_TABLE_NO_SLOT_LINES = 0x04
 KAD_LINES_RT16, KAD_LINES_RT32, KAD_LINES_NC16, KAD_LINES_NC32, KAD_LINES_ALL = 0x01, 0x02, 0x04, 0x08, 0x0F
 # kad_table_export_lines sets
 (KAD_LINESET_WL, KAD_LINESET_WS, KAD_LINESET_WL16, KAD_LINESET_WL32, KAD_LINESET_GL, KAD_LINESET_GL16, KAD_LINESET_GL32,
@@ -91,6 +92,7 @@ SIGNATURES = {
     "kad_nc_apply": (C.c_int, [_P, _P, C.c_uint32, _P, _P, C.c_uint32, _P, _P]),
     "kad_table_set_times": (C.c_int, [_P, _P, _P, _P]),
     "kad_table_refresh_status": (C.c_int, [_P, C.c_int64, _P]),
+    "kad_table_refresh_diag": (C.c_int, [_P, _P]),
     "kad_table_patch_status": (C.c_int, [_P, C.c_uint32, _P, _P]),
     "kad_table_patch_times": (C.c_int, [_P, C.c_uint32, _P, _P, _P, _P]),
     "kad_rt_closest_batch": (C.c_int, [_P, _P, C.c_uint32, C.c_uint32, _P, _P, _P]),
@@ -162,6 +164,10 @@ class serve_stats(C.Structure):
         ("idle_us", C.c_uint32), ("last_polls", C.c_uint32), ("launches", C.c_uint64), ("requests", C.c_uint64),
         ("last_busy_ns", C.c_uint64),
     ]
+
+
+class refresh_diag(C.Structure):
+    _fields_ = [("spin_timeouts", C.c_uint32), ("last_block_lines", C.c_uint32), ("guard_errors", C.c_uint32)]
 
 
 _lib = None

@@ -5318,7 +5318,15 @@ __device__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* lds, uint32_t& to
 // The window good counts come from the per-bucket counts (gcnt), so nothing is O(buckets).
 // ---------------------------------------------------------------------------------------
 constexpr uint32_t RF_CAP = 2048;
-constexpr uint32_t RF_NB = 0, RF_NR = 1, RF_DONE = 2, RF_L8 = 3, RF_L16 = 4, RF_L32 = 5, RF_LNC = 6, RF_GO = 7, RF_CTRS = 8;
+constexpr uint32_t RF_NB = 0, RF_NR = 1, RF_DONE = 2, RF_L8 = 3, RF_L16 = 4, RF_L32 = 5, RF_LNC = 6, RF_GO = 7;
+// fused launches (FUSE 1 / 2): RF_NDEF window lines left to the last block (windows of more than 64 nodes);
+// RF_REDO set by a builder block that gave up waiting for block 0's list (the last block rebuilds the list);
+// sticky diagnostics, never reset by the device (kad_table_refresh_diag): RF_SPIN spin waits that timed out,
+// RF_DEFB lines the last block built, RF_ERR bounds guards that fired (RF_ERR_* bits; zero unless a bug)
+constexpr uint32_t RF_NDEF = 8, RF_REDO = 9, RF_SPIN = 10, RF_DEFB = 11, RF_ERR = 12, RF_CTRS = 13;
+constexpr uint32_t RF_ERR_INB = 1, RF_ERR_RUN = 2, RF_ERR_LINE = 4, RF_ERR_NHR = 8, RF_ERR_DEF = 16;
+// a builder's wait for block 0's list: 1 s of the 100 MHz wall clock, then the last block does its work
+constexpr uint64_t RF_SPIN_TICKS = 100000000ull;
 
 struct RfCtx {
     NodeTimes N;
@@ -5353,7 +5361,8 @@ struct RfCtx {
     uint32_t hr[3 * 16];                 //   offsets h_off[max(0, first - 3) ..] start at hoff[hr[3r+2]]
     uint32_t hoff[256];
 #ifdef KAD_ABLATIONS
-    uint32_t abl;  // tools build (KAD_RF_ABL): 1 = builder blocks return at once, 2 = block 0 returns at once
+    uint32_t abl;  // tools build (KAD_RF_ABL): 1 = builder blocks skip their work, 2 = block 0 skips its work,
+                   // 3 = block 0 starts RF_SPIN_TICKS + 0.2 s late (the builders' wait times out)
 #endif
 };
 constexpr uint32_t RF_INLINE = 128, RF_HOFF = 256;
@@ -5738,10 +5747,13 @@ __device__ __attribute__((always_inline)) void rf_wl_builders(const RfCtx& C, ui
     // the kernel arguments the line loop searches (inline nodes, runs, offsets), staged in LDS in one round of
     // independent loads: a wave-uniform search of them in the argument segment was a chain of dependent scalar loads
     __shared__ uint32_t s_inl[RF_INLINE], s_hr[3 * 16], s_hoff[RF_HOFF];
-    const bool host_lines = C.nhl != 0;
+    // (the host checks every inline limit before the launch, rf_check_inline; the guards here only record a
+    // violation in the sticky error word and skip the access)
+    const bool host_lines = C.nhl != 0 && C.nhr <= 16;
     {
         const uint32_t tid = threadIdx.x;
-        if (tid < C.ninl) s_inl[tid] = C.inl[tid];
+        if (tid == 0 && C.nhl != 0 && C.nhr > 16) atomicOr(C.ctr + RF_ERR, RF_ERR_NHR);
+        if (tid < min(C.ninl, RF_INLINE)) s_inl[tid] = C.inl[tid];
         if (host_lines) {
             if (tid < 3 * C.nhr) s_hr[tid] = C.hr[tid];
             for (uint32_t o = tid; o < RF_HOFF; o += BLOCK) s_hoff[o] = C.hoff[o];
@@ -5842,7 +5854,12 @@ __device__ __attribute__((always_inline)) void rf_wl_builders(const RfCtx& C, ui
             const uint32_t first = s_hr[3 * r];
             b = first + k;
             const uint32_t db = b >= 3 ? b - 3 : 0u, e = min(B, b + 3);
-            const uint32_t* hl = s_hoff + s_hr[3 * r + 2] + (db - (first >= 3 ? first - 3 : 0u));
+            const uint32_t o0 = s_hr[3 * r + 2] + (db - (first >= 3 ? first - 3 : 0u));
+            if (b >= B || db < (first >= 3 ? first - 3 : 0u) || o0 + (e - db) >= RF_HOFF) {  // (never: rf_check_inline)
+                if (lane == 0) atomicOr(C.ctr + RF_ERR, b >= B ? RF_ERR_LINE : RF_ERR_RUN);
+                continue;
+            }
+            const uint32_t* hl = s_hoff + o0;
             if (lane < 8) WV.dx[lane] = hl[min(lane, e - db)];
             n0 = hl[0];
             n1 = hl[e - db];
@@ -5894,26 +5911,70 @@ __device__ __attribute__((always_inline)) void rf_wl_builders(const RfCtx& C, ui
                        wid, b, n1 - n0, (unsigned long long)(tb1 - tb0), (unsigned long long)(tb2 - tb1),
                        (unsigned long long)(tb3 - tb2), (unsigned long long)tb0);
 #endif
-        } else if (lane == 0) {  // serial build from the table: wait for block 0's statuses and good counts
-            const uint64_t t0 = wall_clock64();
-            bool go = true;
-            while (__hip_atomic_load(C.ctr + RF_GO, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != C.epoch) {
-                __builtin_amdgcn_s_sleep(1);
-                if (wall_clock64() - t0 > 100000000ull) { go = false; break; }
-            }
-            if (go) {
-                wl_build_line(T.key, C.status, C.dir, C.gcnt, B, 64 - T.rshift, T.rbase >> T.rshift, C.wl, b, WV.R);
-                if (C.ws) ws_build_line(WV.R, C.ws, b, WV.R + 33);
-            }
+        } else if (lane == 0) {
+            // a window of more than 64 nodes: the serial build reads the table's statuses and good counts, which
+            // block 0 writes; the line goes to the last block to finish (rf_fused_finish), after block 0's writes
+            const uint32_t o = atomicAdd(C.ctr + RF_NDEF, 1u);
+            if (o < RF_FUSE_LINES) C.blist[o] = b;
+            else atomicOr(C.ctr + RF_ERR, RF_ERR_DEF);  // (never: at most RF_FUSE_LINES lines per launch)
         }
         wave_lds_sync();
     }
 }
 
-// Phase 3 of a fused general-line refresh (FUSE 2): lines l8[x] for x = this block's share (blockIdx.x, stride
-// gridDim.x), after block 0 published the list.
+// End of a fused launch (FUSE 1 / 2), every block: the last block to finish (a completion counter, after
+// every other block's release; no block waits for another) builds what no builder could without block 0's
+// statuses and good counts: FUSE 1, the window lines of more than 64 nodes the builders listed; FUSE 2, the
+// whole line list again if a builder block gave up waiting for it (RF_REDO: its wait timed out, so block 0
+// was not running; rebuilding a line gives the same line). Then it resets the counters for the next refresh.
 template <int FUSE>
-__device__ void rf_fused_lines(const RfCtx& C, uint32_t* pool, uint32_t n8, const uint32_t* l8) {
+__device__ void rf_fused_lines(const RfCtx& C, uint32_t* pool, uint32_t n8, const uint32_t* l8, uint32_t bx,
+                               uint32_t nbx);
+
+template <int FUSE>
+__device__ void rf_fused_finish(const RfCtx& C, uint32_t* pool) {
+    __shared__ uint32_t last, s_ndef, s_redo, s_n8;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __syncthreads();
+    if (threadIdx.x == 0) last = atomicAdd(C.ctr + RF_DONE, 1u) == gridDim.x - 1;
+    __syncthreads();
+    if (!last) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    if (threadIdx.x == 0) {
+        s_ndef = __hip_atomic_load(C.ctr + RF_NDEF, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_redo = __hip_atomic_load(C.ctr + RF_REDO, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_n8 = __hip_atomic_load(C.ctr + RF_L8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    const DevTable& T = C.T;
+    if (FUSE == 1 && s_ndef) {
+        const uint32_t nd = min(s_ndef, RF_FUSE_LINES), lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
+        WaveLds& WV = reinterpret_cast<WaveLds*>(pool)[wid];
+        for (uint32_t x = wid; x < nd; x += BLOCK / 64) {  // wave-uniform
+            if (lane == 0) {
+                const uint32_t b = C.blist[x];
+                wl_build_line(T.key, C.status, C.dir, C.gcnt, T.B, 64 - T.rshift, T.rbase >> T.rshift, C.wl, b, WV.R);
+                if (C.ws) ws_build_line(WV.R, C.ws, b, WV.R + 33);
+            }
+            wave_lds_sync();
+        }
+    }
+    if (FUSE == 2 && s_redo) rf_fused_lines<FUSE>(C, pool, s_n8, C.fl, 0u, 1u);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (s_ndef) atomicAdd(C.ctr + RF_DEFB, s_ndef);
+        if (s_redo) atomicAdd(C.ctr + RF_DEFB, s_n8);
+        C.ctr[RF_NDEF] = 0;
+        C.ctr[RF_REDO] = 0;
+        C.ctr[RF_DONE] = 0;
+    }
+}
+
+// Phase 3 of a fused general-line refresh (FUSE 2): lines l8[x] for x = this block's share (block bx of nbx:
+// blockIdx.x of gridDim.x, or 0 of 1 for the last block's rebuild), after block 0 published the list.
+template <int FUSE>
+__device__ void rf_fused_lines(const RfCtx& C, uint32_t* pool, uint32_t n8, const uint32_t* l8, uint32_t bx,
+                               uint32_t nbx) {
     const DevTable& T = C.T;
     const uint32_t B = T.B;
     if (FUSE == 2) {
@@ -5930,7 +5991,7 @@ __device__ void rf_fused_lines(const RfCtx& C, uint32_t* pool, uint32_t n8, cons
         uint32_t* sgc = pool + NG * (2 * RF_WCAP + RF_WCAP / 4 + 16);               // NG x 8
         uint32_t* rows = sgc + NG * 8;                                              // NG x (33 + 17)
         const uint32_t g = threadIdx.x / RF_GROUP, gl = threadIdx.x % RF_GROUP;
-        for (uint32_t x0 = blockIdx.x * NG; x0 < n8; x0 += gridDim.x * NG) {  // block-uniform
+        for (uint32_t x0 = bx * NG; x0 < n8; x0 += nbx * NG) {  // block-uniform
             const uint32_t x = x0 + g;
             const bool act = x < n8;
             const uint32_t b = act ? l8[x] : 0u, db = b >= 3 ? b - 3 : 0u;
@@ -5988,10 +6049,17 @@ __global__ __launch_bounds__(BLOCK) void rf_nodes_kernel(RfCtx C_arg) {
     __shared__ __attribute__((aligned(16))) uint32_t pool[RF_POOL];
     __shared__ uint32_t lctr[2];
 #ifdef KAD_ABLATIONS
-    if ((C.abl == 1 && blockIdx.x > 0) || (C.abl == 2 && blockIdx.x == 0)) return;
+    const bool skip = (C.abl == 1 && blockIdx.x > 0) || (C.abl == 2 && blockIdx.x == 0);
+    if (skip && !FUSE) return;
+    if (C.abl == 3 && blockIdx.x == 0) {  // block 0 starts late: the builders' wait for its list times out
+        const uint64_t t0 = wall_clock64();
+        while (wall_clock64() - t0 < RF_SPIN_TICKS + 20000000ull) __builtin_amdgcn_s_sleep(127);
+    }
+#else
+    constexpr bool skip = false;
 #endif
     if (FUSE == 1 && blockIdx.x > 0) {  // a window-line builder block (independent of block 0)
-        rf_wl_builders(C, pool);
+        if (!skip) rf_wl_builders(C, pool);
 #ifdef KAD_RF_TRACE
         __syncthreads();
         RF_STAMP(2);
@@ -5999,23 +6067,29 @@ __global__ __launch_bounds__(BLOCK) void rf_nodes_kernel(RfCtx C_arg) {
             printf("RFBUILD blk=%u start=%llu go=%llu end=%llu\n", blockIdx.x, (unsigned long long)rf_ts[0],
                    (unsigned long long)rf_ts[0], (unsigned long long)rf_ts[2]);
 #endif
+        rf_fused_finish<FUSE>(C, pool);
         return;
     }
     if (FUSE == 2 && blockIdx.x > 0) {  // a general-line builder block: wait for block 0's list (block-uniform)
         if (threadIdx.x == 0) {
-            // bounded (1 s of the 100 MHz wall clock): a list that never comes leaves the lines alone, no hang
+            // bounded: a list that does not come within RF_SPIN_TICKS (block 0 not running) is left to the last
+            // block to finish (RF_REDO), which runs after block 0 whatever the order the blocks ran in
             const uint64_t t0 = wall_clock64();
-            bool go = true;
-            while (__hip_atomic_load(C.ctr + RF_GO, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != C.epoch) {
+            bool go = !skip;
+            while (go && __hip_atomic_load(C.ctr + RF_GO, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != C.epoch) {
                 __builtin_amdgcn_s_sleep(1);
-                if (wall_clock64() - t0 > 100000000ull) { go = false; break; }
+                if (wall_clock64() - t0 > RF_SPIN_TICKS) {
+                    go = false;
+                    atomicAdd(C.ctr + RF_SPIN, 1u);
+                    atomicOr(C.ctr + RF_REDO, 1u);
+                }
             }
             lctr[0] = go ? __hip_atomic_load(C.ctr + RF_L8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
         }
         __syncthreads();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         RF_STAMP(1);
-        rf_fused_lines<FUSE>(C, pool, lctr[0], C.fl);
+        rf_fused_lines<FUSE>(C, pool, lctr[0], C.fl, blockIdx.x, gridDim.x);
 #ifdef KAD_RF_TRACE
         __syncthreads();
         RF_STAMP(2);
@@ -6023,6 +6097,11 @@ __global__ __launch_bounds__(BLOCK) void rf_nodes_kernel(RfCtx C_arg) {
             printf("RFBUILD blk=%u start=%llu go=%llu end=%llu\n", blockIdx.x, (unsigned long long)rf_ts[0],
                    (unsigned long long)rf_ts[1], (unsigned long long)rf_ts[2]);
 #endif
+        rf_fused_finish<FUSE>(C, pool);
+        return;
+    }
+    if (FUSE && skip) {  // (tools build) block 0 skips its work
+        rf_fused_finish<FUSE>(C, pool);
         return;
     }
     uint64_t* srt = reinterpret_cast<uint64_t*>(pool);  // RF_CAP (phase 2)
@@ -6054,9 +6133,14 @@ __global__ __launch_bounds__(BLOCK) void rf_nodes_kernel(RfCtx C_arg) {
         if (act && T.B && C.nhb && ((st ^ old) & KAD_STATUS_GOOD)) {
             // the host's buckets: the flip patches its bucket's good count and mask in place (no recount: the
             // nodes are distinct, the atomics return nothing, block 0's release below orders them before RF_GO)
-            const uint32_t e = C.inb[j], hbk = C.hb[e & 127u];
-            atomicAdd(C.gcnt + hbk, (st & KAD_STATUS_GOOD) ? 1u : ~0u);
-            if (e >> 8) atomicXor(reinterpret_cast<uint32_t*>(C.dir + hbk) + 1, 1u << ((e >> 8) - 1));
+            const uint32_t e = C.inb[j];
+            if ((e & 127u) < min(C.nhb, RF_INLINE) && C.hb[e & 127u] < T.B && (e >> 8) <= 32) {  // (rf_check_inline)
+                const uint32_t hbk = C.hb[e & 127u];
+                atomicAdd(C.gcnt + hbk, (st & KAD_STATUS_GOOD) ? 1u : ~0u);
+                if (e >> 8) atomicXor(reinterpret_cast<uint32_t*>(C.dir + hbk) + 1, 1u << ((e >> 8) - 1));
+            } else {
+                atomicOr(C.ctr + RF_ERR, RF_ERR_INB);
+            }
         }
         const uint32_t b = gchg ? node_bucket(T, C.dir, i, key_i) : 0u;
         const bool echg = act && C.list[3] && ((st ^ old) & KAD_STATUS_EXPIRED);
@@ -6129,8 +6213,8 @@ __global__ __launch_bounds__(BLOCK) void rf_nodes_kernel(RfCtx C_arg) {
     uint32_t nu = 0;
     if (C.nhb) {  // block-uniform
         __syncthreads();
-        if (threadIdx.x < C.nhb) ub[threadIdx.x] = C.hb[threadIdx.x];
-        nu = C.nhb;
+        nu = min(C.nhb, RF_INLINE);
+        if (threadIdx.x < nu) ub[threadIdx.x] = C.hb[threadIdx.x];
         __syncthreads();
     } else {
         uint32_t P = 1;
@@ -6162,12 +6246,6 @@ __global__ __launch_bounds__(BLOCK) void rf_nodes_kernel(RfCtx C_arg) {
         }
         C.gcnt[b] = g;
         C.dir[b].y = (j1 - j0 <= 32) ? mask : 0u;
-    }
-    if (FUSE == 1) {  // statuses and good counts written: a builder's serial fallback may read them
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        __syncthreads();
-        if (threadIdx.x == 0 && gridDim.x > 1)
-            __hip_atomic_store(C.ctr + RF_GO, C.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     }
     RF_STAMP(4);
     // per line set: the union of the windows that can read a changed bucket (the count <= 8 set into LDS when fused)
@@ -6202,7 +6280,7 @@ __global__ __launch_bounds__(BLOCK) void rf_nodes_kernel(RfCtx C_arg) {
         if (threadIdx.x == 0 && gridDim.x > 1)
             __hip_atomic_store(C.ctr + RF_GO, C.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         RF_STAMP(6);
-        rf_fused_lines<FUSE>(C, pool, n8, l8);
+        rf_fused_lines<FUSE>(C, pool, n8, l8, blockIdx.x, gridDim.x);
     }
 #ifdef KAD_RF_TRACE
     __syncthreads();
@@ -6215,6 +6293,7 @@ __global__ __launch_bounds__(BLOCK) void rf_nodes_kernel(RfCtx C_arg) {
                (unsigned long long)(rf_ts[5] - rf_ts[0]), (unsigned long long)(rf_ts[6] - rf_ts[0]),
                (unsigned long long)(rf_ts[7] - rf_ts[0]));
 #endif
+    if (FUSE) rf_fused_finish<FUSE>(C, pool);
 }
 
 // New status bytes: all n nodes (nodes == NULL) or the m listed ones; only changes are written and marked.
@@ -6959,7 +7038,7 @@ int build_sl16(kad_table* t);
 int setup_slot_lines(kad_table* t) {
     DevTable& d = t->d;
     if (!(d.flags & TF_GL) || !t->gl_mut || d.B == 0 || d.rslots == 0 || t->h_first.size() < 20ull * d.B) return KAD_OK;
-    if (std::getenv("KAD_NO_SLOT_LINES")) return KAD_OK;  // test hook: general lines alone (the fused general-line refresh)
+    if (t->flags & KAD_TABLE_NO_SLOT_LINES) return KAD_OK;  // general lines alone (the caller's choice)
     const uint32_t B = d.B;
     const uint8_t* f = t->h_first.data();
     int pick = -1;
@@ -7257,6 +7336,48 @@ uint32_t bucket_of_node(const std::vector<uint32_t>& off, uint32_t n, uint32_t i
     return (uint32_t)std::min<uint64_t>(lo, B - 1);
 }
 
+// Every index the kernel derives from its inline arguments, checked on the host before the launch (at most
+// RF_INLINE nodes, 16 runs and RF_HOFF offsets: a few hundred compares). The kernel's guards only record a
+// violation (RF_ERR); this check refuses the launch, so a wrong argument never reaches the device.
+int rf_check_inline(const RfCtx& C, const std::vector<uint32_t>& off, uint32_t n, uint32_t B) {
+    auto bad = [](const char* what, uint32_t a, uint32_t b) {
+        return set_err(KAD_ERR_INVALID, "small refresh: inline argument out of range (%s: %u, %u)", what, a, b);
+    };
+    if (C.ninl > RF_INLINE) return bad("ninl", C.ninl, RF_INLINE);
+    for (uint32_t j = 1; j < C.ninl; j++)
+        if (C.inl[j] <= C.inl[j - 1]) return bad("inl order", j, C.inl[j]);
+    if (C.nhb == 0) return C.nhl ? bad("nhl without nhb", C.nhl, 0) : KAD_OK;
+    if (C.nhb > RF_INLINE) return bad("nhb", C.nhb, RF_INLINE);
+    if (off.size() != (size_t)B + 1) return bad("offsets", (uint32_t)off.size(), B);
+    for (uint32_t u = 0; u < C.nhb; u++)
+        if (C.hb[u] >= B || (u && C.hb[u] <= C.hb[u - 1])) return bad("hb", u, C.hb[u]);
+    for (uint32_t j = 0; j < C.ninl; j++) {
+        const uint32_t i = C.inl[j];
+        if (i >= n) continue;
+        const uint32_t u = C.inb[j] & 127u, p = C.inb[j] >> 8;
+        if ((C.inb[j] & 0xFFu) >= C.nhb || u >= C.nhb) return bad("inb bucket", j, C.inb[j]);
+        const uint32_t b = C.hb[u];
+        if (!(off[b] <= i && i < off[b + 1])) return bad("inb not the node's bucket", j, b);
+        if (p > 32 || (p && off[b] + p - 1 != i) || (!p && off[b + 1] - off[b] <= 32)) return bad("inb place", j, p);
+    }
+    if (C.nhl == 0) return C.nhr ? bad("nhr without nhl", C.nhr, 0) : KAD_OK;
+    if (C.nhr == 0 || C.nhr > 16) return bad("nhr", C.nhr, 16);
+    uint32_t lines = 0, next = 0, prev_end = 0;
+    for (uint32_t r = 0; r < C.nhr; r++) {
+        const uint32_t first = C.hr[3 * r], len = C.hr[3 * r + 1], o = C.hr[3 * r + 2];
+        if (len == 0 || (uint64_t)first + len > B || (r && first <= prev_end)) return bad("run lines", r, first);
+        const uint32_t o0 = first >= 3 ? first - 3 : 0u, o1 = std::min(B, first + len - 1 + 3) + 1;
+        if (o != next || (uint64_t)o + (o1 - o0) > RF_HOFF) return bad("run offsets", r, o);
+        for (uint32_t k = o0; k < o1; k++)
+            if (C.hoff[o + (k - o0)] != off[k]) return bad("hoff", r, k);
+        next = o + (o1 - o0);
+        lines += len;
+        prev_end = first + len;
+    }
+    if (lines != C.nhl) return bad("nhl", C.nhl, lines);
+    return KAD_OK;
+}
+
 int small_refresh(kad_table* t, hipStream_t s, const uint32_t* mnode, uint32_t mc, const uint32_t* snode, uint32_t sc,
                   const uint32_t* pend, uint32_t np, const uint8_t* vals, int64_t now, const uint32_t* inl = nullptr,
                   uint32_t ninl = 0) {
@@ -7339,6 +7460,7 @@ int small_refresh(kad_table* t, hipStream_t s, const uint32_t* mnode, uint32_t m
             C.nhl = fits ? nl : 0;
             C.nhr = fits ? nr : 0;
         }
+        if ((rc = rf_check_inline(C, t->h_off, d.n, B))) return rc;
     }
     // one block when it holds every listed node; the count <= 8 lines built by it when at most RF_FUSE_LINES can
     // be listed (6 per changed bucket) and no slot lines depend on them
@@ -9018,6 +9140,20 @@ int kad_table_serve_stats(const kad_table* t, kad_serve_stats* out) {
         const uint64_t a = P.vr->t_seen, b = P.vr->t_done;
         out->last_busy_ns = b > a ? (uint64_t)((double)(b - a) * 1e6 / P.vkhz) : 0u;
     }
+    return KAD_OK;
+}
+
+int kad_table_refresh_diag(const kad_table* t, kad_refresh_diag* out) {
+    if (!t || !out) return set_err(KAD_ERR_INVALID, "NULL argument");
+    *out = kad_refresh_diag{};
+    if (!t->rf_ctr) return KAD_OK;
+    DeviceGuard g(t->device);
+    uint32_t c[RF_CTRS];
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(c, t->rf_ctr, sizeof(c), hipMemcpyDeviceToHost));
+    out->spin_timeouts = c[RF_SPIN];
+    out->last_block_lines = c[RF_DEFB];
+    out->guard_errors = c[RF_ERR];
     return KAD_OK;
 }
 

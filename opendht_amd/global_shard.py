@@ -96,10 +96,13 @@ class Exchange:
     per K steps and then runs again with grown()."""
 
     def __init__(self, q: int, count: int, world: int, device, row_cap: int | None = None,
-                 part_cap: int | None = None, home: bool = True):
+                 part_cap: int | None = None, home: bool = True, collective: bool | None = None):
         import torch
 
         self.q, self.count, self.world, self.dev, self.home = q, count, world, device, home
+        # the step runs the collective (and the overflow combine) at world > 1; collective=True forces it at
+        # world 1 too (a one-rank RCCL group: the same calls on the same buffers, tests/rccl_world1_worker.py)
+        self.collective = world > 1 if collective is None else bool(collective)
         nblk = -(-q // 256)
         if home:
             # region k % 8 of a home range of ceil(nblk / world) query blocks: this capacity can never overflow
@@ -122,7 +125,8 @@ class Exchange:
         self.block = shard_block_words(count, self.row_cap, self.part_cap)
         nsend = world if home else 1
         self.send = torch.zeros((nsend * self.block,), dtype=torch.int32, device=device)
-        self.recv = self.send if world == 1 else torch.empty((world * self.block,), dtype=torch.int32, device=device)
+        self.recv = self.send if not self.collective else torch.empty((world * self.block,), dtype=torch.int32,
+                                                                      device=device)
         qh = max(home_range(q, world, r)[1] - home_range(q, world, r)[0] for r in range(world)) if home else q
         self.scratch = torch.full((qh + world * self.part_cap,), -1, dtype=torch.int32, device=device)
         self.overflow = torch.zeros((1,), dtype=torch.int32, device=device)
@@ -145,7 +149,7 @@ class Exchange:
         """Host read of the sticky overflow word (synchronises), cleared. The home exchange combines it over the
         ranks first (each rank sees only the blocks sent to it), so every rank decides the same (combine=False:
         one process simulating the ranks)."""
-        if combine and self.home and self.world > 1:
+        if combine and self.home and self.collective:
             import torch.distributed as dist
 
             if dist.get_backend(group) == "nccl":
@@ -174,7 +178,7 @@ class Exchange:
         """A new layout sized from the counters of the last step, combined over the ranks (the same on every
         rank). needs: the (rows, parts) counts to fit, if known (query_simulated)."""
         need_r, need_p = needs if needs is not None else self.needs()
-        if needs is None and self.home and self.world > 1:
+        if needs is None and self.home and self.collective:
             import torch
             import torch.distributed as dist
 
@@ -185,7 +189,7 @@ class Exchange:
         row_cap = self.row_cap if need_r <= self.row_cap else max(2 * self.row_cap, need_r * 5 // 4)
         part_cap = self.part_cap if need_p <= self.part_cap else max(2 * self.part_cap, need_p * 5 // 4)
         return Exchange(self.q, self.count, self.world, self.dev, row_cap=min(row_cap, self.row_cap_max),
-                        part_cap=part_cap, home=self.home)
+                        part_cap=part_cap, home=self.home, collective=self.collective)
 
     def home_finish(self, rank: int, out_idx, out_cnt, stream):
         """kad_rt_home_finish over the received blocks: rank `rank`'s rows (device only)."""
@@ -221,11 +225,12 @@ class GlobalShard:
     def close(self):
         self.table.close()
 
-    def exchange(self, q: int, count: int, world: int, home: bool = True) -> Exchange:
-        """The cached step layout for (q, count, world, home)."""
-        key = (q, count, world, home)
+    def exchange(self, q: int, count: int, world: int, home: bool = True, collective: bool | None = None) -> Exchange:
+        """The cached step layout for (q, count, world, home, collective)."""
+        coll = world > 1 if collective is None else bool(collective)
+        key = (q, count, world, home, coll)
         if key not in self._ex:
-            self._ex[key] = Exchange(q, count, world, self.dev, home=home)
+            self._ex[key] = Exchange(q, count, world, self.dev, home=home, collective=coll)
         return self._ex[key]
 
     def home_block(self, targets, ex: Exchange, stream=None):
@@ -271,13 +276,13 @@ class GlobalShard:
             if rank is None:
                 rank = rank_of(group) if ex.world > 1 else 0
             self.home_block(targets, ex, s)
-            if ex.world > 1:
+            if ex.collective:
                 with torch.cuda.stream(_torch_stream(s, self.dev)):
                     exchange_into(ex.recv, ex.send, group)
             ex.home_finish(rank, out_idx, out_cnt, C.c_void_p(s))
             return
         self.local_block(targets, ex, stream)
-        if ex.world > 1:
+        if ex.collective:
             if stream is None:
                 gather_into(ex.recv, ex.send, group)
             else:
@@ -286,14 +291,14 @@ class GlobalShard:
         ex.finish(out_idx, out_cnt, C.c_void_p(s))
 
     def query(self, targets, count: int, group=None, out_idx=None, out_cnt=None, single_rank_shard_kernel=False,
-              home: bool = True):
+              home: bool = True, force_collective: bool = False):
         """RoutingTable::findClosestNodes over a replicated batch: local rows and parts, the exchange (RCCL /
         gloo), device scatter and merge; one combined host read of the overflow word per call (a full buffer
         grows the layout and runs the batch again on every rank). home (default): returns (lo, out_idx, out_cnt)
         with this rank's home queries [lo, lo + len(out_idx)); home=False: (0, every query's rows) on every rank
         (the all-gather). A single rank holds the whole table: the plain kad_rt_closest_batch
         (single_rank_shard_kernel: the shard kernel and the finish instead, what each rank runs at N > 1 minus
-        the collective)."""
+        the collective; force_collective: and the collective too, through the one-rank process group)."""
         import torch
         import torch.distributed as dist
 
@@ -311,16 +316,17 @@ class GlobalShard:
         if world == 1:
             if (self.lo, self.hi) != (0, self.GB):
                 raise ValueError("a single rank must hold the whole table")
-            if not single_rank_shard_kernel:
+            if not (single_rank_shard_kernel or force_collective):
                 return 0, *self.table.rt_closest(targets, count, out_idx=out_idx, out_cnt=out_cnt)
+        coll = world > 1 or force_collective
         self.tries = []  # (row_cap, part_cap) of every step of the last call
         while True:
-            ex = self.exchange(q, count, world, home)
+            ex = self.exchange(q, count, world, home, coll)
             self.tries.append((ex.row_cap, ex.part_cap))
             self.step(targets, ex, out_idx, out_cnt, group, rank=rank)
             if not ex.overflowed(group):
                 return lo, out_idx, out_cnt
-            self._ex[(q, count, world, home)] = ex.grown(group)
+            self._ex[(q, count, world, home, coll)] = ex.grown(group)
 
 
 def query_simulated(shards, targets, count: int, out_idx=None, out_cnt=None, row_cap=None, part_cap=None,

@@ -11,7 +11,7 @@ import ctypes as C
 import numpy as np
 
 from . import _lib
-from ._lib import KAD_TABLE_EAGER, KAD_TABLE_SORTED, check, lib, ptr
+from ._lib import KAD_TABLE_EAGER, KAD_TABLE_NO_SLOT_LINES, KAD_TABLE_SORTED, check, lib, ptr
 
 
 def _as_ids(a) -> np.ndarray:
@@ -40,10 +40,12 @@ class DeviceTable:
     bucket_offset  (B+1,) uint32
     sorted         ids strictly ascending (enables NodeCache queries)
     eager          build every line set now (default: the count <= 8 lines; the others on first use)
+    slot_lines     general-line tables: build slot lines (KAD_TABLE_NO_SLOT_LINES when False)
     """
 
     def __init__(self, ids, status, bucket_first=None, bucket_offset=None, *, device: int = 0,
-                 index_base: int = 0, sorted: bool = False, eager: bool = False):
+                 index_base: int = 0, sorted: bool = False, eager: bool = False,
+                 slot_lines: bool = True):
         L = lib()
         ids = _as_ids(ids)
         status = np.ascontiguousarray(status, dtype=np.uint8)
@@ -61,7 +63,8 @@ class DeviceTable:
         h = C.c_void_p()
         rc = L.kad_table_create(C.byref(h), device, n, ptr(ids), ptr(status), B,
                                 ptr(bucket_first) if B else None, ptr(bucket_offset) if B else None,
-                                index_base, (KAD_TABLE_SORTED if sorted else 0) | (KAD_TABLE_EAGER if eager else 0))
+                                index_base, (KAD_TABLE_SORTED if sorted else 0) | (KAD_TABLE_EAGER if eager else 0)
+                                | (0 if slot_lines else KAD_TABLE_NO_SLOT_LINES))
         check(rc, "kad_table_create")
         self._h = h
         self.device = device
@@ -150,6 +153,12 @@ class DeviceTable:
     def refresh_status(self, now_ns: int, stream=None) -> None:
         check(lib().kad_table_refresh_status(self._h, C.c_int64(now_ns), _stream_of(self, stream)),
               "kad_table_refresh_status")
+
+    def refresh_diag(self) -> dict:
+        """kad_table_refresh_diag: the small refresh's spin timeouts, lines its last block built, guard errors."""
+        d = _lib.refresh_diag()
+        check(lib().kad_table_refresh_diag(self._h, C.byref(d)), "kad_table_refresh_diag")
+        return {f: getattr(d, f) for f, _ in d._fields_}
 
     def apply(self, ops, new_ids=None, new_status=None, remap=None):
         """Incremental mirror (kad_table_apply): ops (m, 3) uint32 rows (kind, a, b). Returns the new

@@ -341,7 +341,7 @@ def _query_worker(rank, world, port, q):
                                       f"{want[lo + j][:6].tolist()} cnt {int(wcnt[lo + j])}")
                     # the same batch again with room for everything from the start (no growth)
                     from opendht_amd.global_shard import Exchange
-                    G._ex[(targets.shape[0], count, world, home)] = Exchange(targets.shape[0], count, world, dev,
+                    G._ex[(targets.shape[0], count, world, home, world > 1)] = Exchange(targets.shape[0], count, world, dev,
                                                                              row_cap=1 << 20, part_cap=4096, home=home)
                     _, idx2, cnt2 = G.query(tg, count, home=home)
                     torch.cuda.synchronize()

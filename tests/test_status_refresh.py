@@ -253,7 +253,7 @@ def test_host_batch_ordered_after_async_refresh(gpu):
 @pytest.mark.parametrize("nosl", [False, True], ids=["", "nosl"])
 @pytest.mark.parametrize("t", [TB.uniform_config(50_000, 12, seed=0x5EA), TB.split_config(30_000, seed=0x5EB)],
                          ids=lambda t: t["name"])
-def test_small_refresh_every_line_set(gpu, t, nosl, monkeypatch):
+def test_small_refresh_every_line_set(gpu, t, nosl):
     """The small refresh path (at most 2,048 nodes to re-derive: rf_nodes_kernel lists the changed buckets and the
     lines whose windows reach them, the builders rebuild only those) on tables holding every line set (uniform:
     short, 128-byte, 9..16, 17..32 and NodeCache lines; split policy: slot, general 8 / 16 / 32 lines and their
@@ -262,10 +262,8 @@ def test_small_refresh_every_line_set(gpu, t, nosl, monkeypatch):
     refreshed at the same `now`; patch_status of a few nodes, including the first and last buckets' (windows
     clamped at the table's ends). After every step the status bytes equal isGood / isExpired and every query
     equals the oracle."""
-    if nosl:  # the split table without slot lines: the fused general-line refresh (KAD_NO_SLOT_LINES)
-        if t["sorted"]:
-            pytest.skip("uniform tables have no slot lines")
-        monkeypatch.setenv("KAD_NO_SLOT_LINES", "1")
+    if nosl and t["sorted"]:  # the split table without slot lines: the fused general-line refresh
+        pytest.skip("uniform tables have no slot lines")
     n = t["ids"].shape[0]
     off = t["off"]
     rng = np.random.default_rng(n)
@@ -286,7 +284,8 @@ def test_small_refresh_every_line_set(gpu, t, nosl, monkeypatch):
         return int(d[min(len(d) - 1, k - 1)]) + 1
 
     rt, nc = (1, 8, 14, 16, 32), (1, 14, 32)
-    with DeviceTable(t["ids"], status_at(now), t["first"], t["off"], device=0, sorted=t["sorted"], eager=True) as T:
+    with DeviceTable(t["ids"], status_at(now), t["first"], t["off"], device=0, sorted=t["sorted"], eager=True,
+                     slot_lines=not nosl) as T:
         T.set_times(time_ns, reply_ns, expired)
         T.refresh_status(now)
         for k in (1, 2, 7, 100, 2047, 2048, 2049, 5000):
@@ -370,20 +369,18 @@ LINESETS = ("WL", "WS", "WL16", "WL32", "GL", "GL16", "GL32", "SL", "SL16", "NCL
 @pytest.mark.parametrize("nosl", [False, True], ids=["", "nosl"])
 @pytest.mark.parametrize("t", [TB.uniform_config(40_000, 12, seed=0x5EC), TB.split_config(20_000, seed=0x5ED),
                                TB.uniform_config(6_000, 12, seed=0x5EE)], ids=lambda t: t["name"])
-def test_incremental_lines_equal_fresh_build(gpu, t, nosl, monkeypatch):
+def test_incremental_lines_equal_fresh_build(gpu, t, nosl):
     """Every derived array an incremental refresh maintains (window, short, general and slot lines of every count,
     NodeCache lines, per-bucket good counts, the directory's masks) is bit for bit what a table built from scratch
     on the same status holds: after refreshes passing 1, 2, 5, 9, 30 and 3000 deadlines (the one-launch path whose
     lines a wave builds, the single-block and multi-block lists, the flag path), a patch of times and one of status
     bytes. The U(12) 6,000-node table has sparse buckets (windows of several rounds, deferred lines). nosl: the
-    split table without slot lines (KAD_NO_SLOT_LINES), so the count <= 8 general lines are rebuilt in the fused
+    split table without slot lines (KAD_TABLE_NO_SLOT_LINES), so the count <= 8 general lines are rebuilt in the fused
     launch (block 0 publishes the list to the builder blocks)."""
     from opendht_amd import _lib
 
-    if nosl:
-        if t["sorted"]:
-            pytest.skip("uniform tables have no slot lines")
-        monkeypatch.setenv("KAD_NO_SLOT_LINES", "1")
+    if nosl and t["sorted"]:
+        pytest.skip("uniform tables have no slot lines")
 
     n = t["ids"].shape[0]
     rng = np.random.default_rng(n ^ 0x5EC)
@@ -398,7 +395,8 @@ def test_incremental_lines_equal_fresh_build(gpu, t, nosl, monkeypatch):
         return (good.astype(np.uint8) | (expired << 1)).astype(np.uint8)
 
     def compare(T, st, what):
-        with DeviceTable(t["ids"], st, t["first"], t["off"], device=0, sorted=t["sorted"], eager=True) as F:
+        with DeviceTable(t["ids"], st, t["first"], t["off"], device=0, sorted=t["sorted"], eager=True,
+                         slot_lines=not nosl) as F:
             for name in LINESETS:
                 k = getattr(_lib, f"KAD_LINESET_{name}")
                 a, b = T.export_lines(k), F.export_lines(k)
@@ -406,7 +404,8 @@ def test_incremental_lines_equal_fresh_build(gpu, t, nosl, monkeypatch):
                 if a is not None:
                     np.testing.assert_array_equal(a, b, err_msg=f"{what}: {name}")
 
-    with DeviceTable(t["ids"], status_at(now), t["first"], t["off"], device=0, sorted=t["sorted"], eager=True) as T:
+    with DeviceTable(t["ids"], status_at(now), t["first"], t["off"], device=0, sorted=t["sorted"], eager=True,
+                     slot_lines=not nosl) as T:
         T.set_times(time_ns, reply_ns, expired)
         T.refresh_status(now)
         for k in (1, 2, 5, 9, 30, 3000):
