@@ -427,6 +427,11 @@ def main_owner(args):
         extras["host_buffers"] = host_pass(T, tgs, cnt_k, Q, dev)
         extras["other_counts"] = counts_pass(T, tgs, Q, dev, stream)
         if rank == 0:
+            try:
+                extras["owner_step_model"] = owner_step_model(T, Q, cnt_k, dev, stream, avg_kernel_s)
+            except Exception as e:  # a model, never the line's failure
+                extras["owner_step_model"] = {"error": f"{type(e).__name__}: {e}"}
+        if rank == 0:
             extras["latency"] = latency_pass(dev)
         if rank == 0 and world == 1:
             extras["configs"] = configs_pass(dev)
@@ -510,6 +515,67 @@ def main_owner(args):
     if dist:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def owner_step_model(T, Q, cnt_k, dev, stream, avg_kernel_s, link_gbs=64.0, lat_us=10.0, reps=20):
+    """The headline form's multi-GPU data path priced: a serving front end holding Q arbitrary
+    targets per rank at N = 2, 4, 8 routes each to the rank owning its shard and gets the rows back
+    (sharded.OwnerRoute). Timed on this GPU, on rank 0's shard table: kad_route_pack of Q targets spread over the N
+    shards into N blocks, the query over the N blocks rank 0 receives (N x cap owned targets, cap = Q / N + 6 sigma +
+    256), kad_route_unpack of the rows. Modelled: the two all_to_all_single exchanges, each rank sending one block
+    to every other rank over its own xGMI link at link_gbs GB/s, lat_us per collective (targets: one; rows and
+    counts: two). serial = pack + targets + query + rows + unpack; overlapped = the compute and the exchanges of
+    consecutive batches on two streams, max(pack + query + unpack, exchanges)."""
+    import torch
+
+    from opendht_amd.sharded import OwnerRoute
+
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+
+    def timed(fn):
+        fn()
+        torch.cuda.synchronize(dev)
+        a.record(stream)
+        for _ in range(reps):
+            fn()
+        b.record(stream)
+        torch.cuda.synchronize(dev)
+        return a.elapsed_time(b) / reps * 1e3
+
+    g = torch.Generator(device=dev)
+    g.manual_seed(0x0D470777)
+    s = stream.cuda_stream
+    out = {"link_GBps_assumed": link_gbs, "latency_us_per_collective_assumed": lat_us, "queries_per_rank": Q,
+           "headline_kernel_us": avg_kernel_s * 1e6}
+    for n in (2, 4, 8):
+        t = torch.randint(0, 256, (Q, 20), dtype=torch.uint8, device=dev, generator=g)
+        sh = torch.randint(0, n, (Q,), dtype=torch.uint8, device=dev, generator=g)
+        t[:, 0] = (t[:, 0] & 0x1F) | (sh << 5)  # targets spread over the N held shards of the 8-shard table
+        R = OwnerRoute(Q, cnt_k, n, 3, dev, collective=False)
+        pack_us = timed(lambda: R.pack(t, s))
+        over = R.overflowed(combine=False)
+        recv = torch.randint(0, 256, (n * R.cap, 20), dtype=torch.uint8, device=dev, generator=g)
+        recv[:, 0] &= 0x1F  # what rank 0 receives: targets of its own shard
+        query_us = timed(lambda: T.rt_closest(recv, cnt_k, out_idx=R.rows, out_cnt=R.cnt, stream=s))
+        oi = torch.empty((Q, cnt_k), dtype=torch.int32, device=dev)
+        oc = torch.empty((Q,), dtype=torch.uint8, device=dev)
+        unpack_us = timed(lambda: R.unpack(oi, oc, s))
+        xb = R.xgmi_bytes
+        x_t = lat_us + 20 * R.cap / (link_gbs * 1e3)
+        x_r = 2 * lat_us + (4 * cnt_k + 1) * R.cap / (link_gbs * 1e3)
+        serial = pack_us + x_t + query_us + x_r + unpack_us
+        overlap = max(pack_us + query_us + unpack_us, x_t + x_r)
+        out[str(n)] = {"cap": R.cap, "overflow": over, "pack_us": pack_us, "query_us": query_us,
+                       "unpack_us": unpack_us, "xgmi_targets_bytes": xb["targets"], "xgmi_rows_bytes": xb["rows"],
+                       "exchange_targets_modelled_us": x_t, "exchange_rows_modelled_us": x_r,
+                       "step_serial_us": serial, "step_overlapped_us": overlap,
+                       "aggregate_queries_per_s_serial": n * Q / (serial * 1e-6),
+                       "aggregate_queries_per_s_overlapped": n * Q / (overlap * 1e-6)}
+        del R, t, recv, oi, oc
+    out["how"] = ("rank 0 of N on this GPU (its 1/8 shard of the 100M-node table): the pack, the query over the "
+                  "blocks it receives and the unpack timed with HIP events (eager, 20 launches each); the exchanges "
+                  "modelled from the block bytes (nothing sent)")
+    return out
 
 
 def cold_pass(T, tgs, outs, ocnt, cnt_k, Q, moved_q, dev, stream, reps=8):

@@ -421,6 +421,27 @@ int kad_rt_home_finish(const uint32_t* recv, uint32_t world, uint32_t rank, uint
                        uint32_t q, uint32_t count, uint32_t* scratch, uint32_t* out_idx, uint8_t* out_cnt,
                        uint32_t* overflow, int device, void* stream);
 
+/* ---- owner routing of a serving front end ----
+ * The headline form shards the table by ID range, one GPU per range, and answers every query on the GPU owning its
+ * target (the reference answers each request where it arrives: Dht::onFindNode / onGetValues, dht.cpp:3189-3217).
+ * A front end spreading arbitrary targets over N GPUs sends each target to its owner and the rows back, as
+ * all_to_all_single of fixed-size blocks (no host read per batch):
+ * kad_route_pack: targets (device, q x 20 bytes) into `world` send blocks of `cap` records of 20 bytes (send:
+ *   world * cap * 20 bytes): target i goes to block d = (byte 0 >> (8 - shard_bits)) % world (d = 0 when
+ *   shard_bits = 0); slot[i] = d * cap + its record (KAD_NO_NODE when block d is full, which sets the sticky word
+ *   ctr[world * KAD_ROUTE_CSTRIDE]). ctr: (world + 1) * KAD_ROUTE_CSTRIDE words, zeroed by the call;
+ *   ctr[d * KAD_ROUTE_CSTRIDE] ends as block d's record count (it may exceed cap). The order of the records inside
+ *   a block is unspecified; records past a block's count are left as they were. Async on stream.
+ * kad_route_unpack: rows returned in the send layout (back_idx: world * cap rows of `count` uint32, back_cnt: world *
+ *   cap bytes) back to each query's position: out_idx row i = back_idx row slot[i], out_cnt[i] = back_cnt[slot[i]]
+ *   (KAD_NO_NODE and 0 for slot KAD_NO_NODE). Async on stream. All pointers are device pointers. */
+#define KAD_ROUTE_CSTRIDE 32u
+#define KAD_ROUTE_MAX_WORLD 16u
+int kad_route_pack(const uint8_t* targets, uint32_t q, uint32_t world, uint32_t shard_bits, uint32_t cap,
+                   uint8_t* send, uint32_t* slot, uint32_t* ctr, int device, void* stream);
+int kad_route_unpack(const uint32_t* slot, uint32_t q, uint32_t count, const uint32_t* back_idx,
+                     const uint8_t* back_cnt, uint32_t* out_idx, uint8_t* out_cnt, int device, void* stream);
+
 /* ---- wire step after the query ------------------------ */
 #define KAD_SEND_NODES 8u           /* reference network_engine.cpp:59 SEND_NODES */
 #define KAD_ADDR4_LEN 6u            /* sin_addr (4) + sin_port (2), bytes as stored in sockaddr_in */

@@ -51,6 +51,8 @@ KAD_SHARD_REGIONS = 8
 KAD_SHARD_COUNTERS = 10
 KAD_SHARD_COUNTER_STRIDE = 32
 KAD_SHARD_MAX_WORLD = 16
+KAD_ROUTE_CSTRIDE = 32
+KAD_ROUTE_MAX_WORLD = 16
 
 
 def shard_block_words(count: int, row_cap: int, part_cap: int) -> int:
@@ -117,6 +119,8 @@ SIGNATURES = {
                                           _P, C.c_uint32, C.c_uint32, C.c_uint32, _P, C.c_uint32, C.c_uint32, _P]),
     "kad_rt_home_finish": (C.c_int, [_P, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, _P,
                                      _P, _P, _P, C.c_int, _P]),
+    "kad_route_pack": (C.c_int, [_P, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, _P, _P, _P, C.c_int, _P]),
+    "kad_route_unpack": (C.c_int, [_P, C.c_uint32, C.c_uint32, _P, _P, _P, _P, C.c_int, _P]),
     "kad_table_set_addrs": (C.c_int, [_P, C.c_uint32, _P]),
     "kad_buffer_nodes_batch": (C.c_int, [_P, _P, C.c_uint32, _P, _P, C.c_uint32, _P, _P, _P]),
     "kad_parse_nodes_batch": (C.c_int, [_P, C.c_uint32, C.c_uint32, _P, _P, C.c_int, _P]),

@@ -1,0 +1,153 @@
+// kad_route.hip — owner routing of a serving front end: the headline form shards
+// the table by ID range, one GPU per range, and every query is answered by the GPU that owns its target. The
+// reference answers each request on the node it arrives at (Dht::onFindNode / onGetValues, dht.cpp:3189-3217); a
+// front end that spreads lookups over N shard GPUs must send each target to its owner and the rows back. Device-only
+// pieces of that exchange, so that it needs no host read per batch:
+//   route_pack_kernel   targets -> `world` fixed-size send blocks (the owner's block), each query's place recorded;
+//                       per-workgroup counts in LDS, one global atomic per (workgroup, owner); a full block sets a
+//                       sticky overflow word (the caller grows the blocks and runs the batch again)
+//   route_unpack_kernel rows that came back in the send layout -> each query's original position
+// The blocks travel with all_to_all_single (RCCL over xGMI), equal splits: opendht_amd/sharded.py OwnerRoute.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "../../include/kadgpu.h"
+
+namespace kadgpu_internal {
+int set_error(int code, const char* msg);
+}  // namespace kadgpu_internal
+
+namespace {
+
+constexpr uint32_t BLOCK = 256, QPT = 4;  // queries per thread: a workgroup packs 1,024 targets
+constexpr uint32_t NONE = 0xFFFFFFFFu;
+
+__global__ __launch_bounds__(BLOCK) void route_pack_kernel(const uint8_t* __restrict__ targets, uint32_t q,
+                                                            uint32_t world, uint32_t shard_bits, uint32_t cap,
+                                                            uint8_t* __restrict__ send, uint32_t* __restrict__ slot,
+                                                            uint32_t* __restrict__ ctr) {
+    __shared__ uint32_t hcnt[KAD_ROUTE_MAX_WORLD], hbase[KAD_ROUTE_MAX_WORLD];
+    const uint32_t tid = threadIdx.x;
+    if (tid < KAD_ROUTE_MAX_WORLD) hcnt[tid] = 0;
+    __syncthreads();
+    uint32_t w[QPT][5], dst[QPT], pos[QPT];
+    const uint64_t base = (uint64_t)blockIdx.x * BLOCK * QPT;
+#pragma unroll
+    for (uint32_t r = 0; r < QPT; r++) {
+        const uint64_t i = base + r * BLOCK + tid;  // consecutive lanes, consecutive 20-byte records
+        dst[r] = NONE;
+        if (i < q) {
+            const uint32_t* p = reinterpret_cast<const uint32_t*>(targets + 20 * i);
+#pragma unroll
+            for (int x = 0; x < 5; x++) w[r][x] = __builtin_nontemporal_load(p + x);
+            const uint32_t b0 = w[r][0] & 0xFFu;  // InfoHash byte 0: the most significant
+            dst[r] = shard_bits ? (b0 >> (8 - shard_bits)) % world : 0u;
+            pos[r] = atomicAdd(&hcnt[dst[r]], 1u);
+        }
+    }
+    __syncthreads();
+    if (tid < world) hbase[tid] = hcnt[tid] ? atomicAdd(ctr + tid * KAD_ROUTE_CSTRIDE, hcnt[tid]) : 0u;
+    __syncthreads();
+#pragma unroll
+    for (uint32_t r = 0; r < QPT; r++) {
+        const uint64_t i = base + r * BLOCK + tid;
+        if (dst[r] == NONE) continue;
+        const uint32_t s = hbase[dst[r]] + pos[r];
+        uint32_t out = NONE;
+        if (s < cap) {
+            out = dst[r] * cap + s;
+            uint32_t* o = reinterpret_cast<uint32_t*>(send + 20ull * out);
+#pragma unroll
+            for (int x = 0; x < 5; x++) o[x] = w[r][x];
+        } else {
+            atomicOr(ctr + world * KAD_ROUTE_CSTRIDE, 1u);
+        }
+        __builtin_nontemporal_store(out, slot + i);
+    }
+}
+
+// One thread per 16-byte piece of a row when count is a multiple of 4 (the common counts 8, 16, 32), else per
+// word; the row of query i comes from place slot[i] of the returned blocks.
+template <bool VEC>
+__global__ __launch_bounds__(BLOCK) void route_unpack_kernel(const uint32_t* __restrict__ slot, uint32_t q,
+                                                             uint32_t count, const uint32_t* __restrict__ back_idx,
+                                                             const uint8_t* __restrict__ back_cnt,
+                                                             uint32_t* __restrict__ out_idx,
+                                                             uint8_t* __restrict__ out_cnt) {
+    const uint32_t per = VEC ? count / 4 : count;  // pieces per row
+    const uint64_t t = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    const uint64_t i = per ? t / per : t;
+    if (i >= q) return;
+    const uint32_t c = per ? (uint32_t)(t - i * per) : 0u;
+    const uint32_t p = slot[i];
+    if (per) {
+        if (VEC) {
+            uint4 v = make_uint4(NONE, NONE, NONE, NONE);
+            if (p != NONE) v = *reinterpret_cast<const uint4*>(back_idx + (uint64_t)p * count + 4 * c);
+            __builtin_nontemporal_store(v.x, out_idx + i * count + 4 * c);
+            __builtin_nontemporal_store(v.y, out_idx + i * count + 4 * c + 1);
+            __builtin_nontemporal_store(v.z, out_idx + i * count + 4 * c + 2);
+            __builtin_nontemporal_store(v.w, out_idx + i * count + 4 * c + 3);
+        } else {
+            out_idx[i * count + c] = p != NONE ? back_idx[(uint64_t)p * count + c] : NONE;
+        }
+    }
+    if (c == 0) out_cnt[i] = p != NONE ? back_cnt[p] : (uint8_t)0;
+}
+
+struct DevSwitch {
+    int prev = -1;
+    explicit DevSwitch(int device) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != device) (void)hipSetDevice(device);
+    }
+    ~DevSwitch() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+}  // namespace
+
+extern "C" int kad_route_pack(const uint8_t* targets, uint32_t q, uint32_t world, uint32_t shard_bits, uint32_t cap,
+                              uint8_t* send, uint32_t* slot, uint32_t* ctr, int device, void* stream) {
+    using kadgpu_internal::set_error;
+    if (world == 0 || world > KAD_ROUTE_MAX_WORLD) return set_error(KAD_ERR_INVALID, "world must be 1..16");
+    if (shard_bits > 8) return set_error(KAD_ERR_INVALID, "shard_bits must be 0..8");
+    if (cap == 0 || (uint64_t)world * cap >= NONE) return set_error(KAD_ERR_INVALID, "cap must be >= 1 and world * cap < 2^32 - 1");
+    if (!ctr || (q && (!targets || !send || !slot))) return set_error(KAD_ERR_INVALID, "NULL buffer");
+    DevSwitch g(device);
+    hipStream_t s = (hipStream_t)stream;
+    hipError_t e = hipMemsetAsync(ctr, 0, 4ull * (world + 1) * KAD_ROUTE_CSTRIDE, s);
+    if (e == hipSuccess && q) {
+        const uint32_t nb = (uint32_t)(((uint64_t)q + BLOCK * QPT - 1) / (BLOCK * QPT));
+        hipLaunchKernelGGL(route_pack_kernel, dim3(nb), dim3(BLOCK), 0, s, targets, q, world, shard_bits, cap, send,
+                           slot, ctr);
+        e = hipGetLastError();
+    }
+    if (e != hipSuccess) return set_error(KAD_ERR_HIP, hipGetErrorString(e));
+    return KAD_OK;
+}
+
+extern "C" int kad_route_unpack(const uint32_t* slot, uint32_t q, uint32_t count, const uint32_t* back_idx,
+                                const uint8_t* back_cnt, uint32_t* out_idx, uint8_t* out_cnt, int device,
+                                void* stream) {
+    using kadgpu_internal::set_error;
+    if (q == 0) return KAD_OK;
+    if (!slot || !back_cnt || !out_cnt || (count && (!back_idx || !out_idx))) return set_error(KAD_ERR_INVALID, "NULL buffer");
+    DevSwitch g(device);
+    const bool vec = count && count % 4 == 0 && ((uintptr_t)back_idx % 16 == 0) && ((uintptr_t)out_idx % 16 == 0);
+    const uint64_t per = count == 0 ? 1 : vec ? count / 4 : count;
+    const uint64_t threads = (uint64_t)q * per;
+    const dim3 grid((uint32_t)((threads + BLOCK - 1) / BLOCK));
+    if (vec)
+        hipLaunchKernelGGL(route_unpack_kernel<true>, grid, dim3(BLOCK), 0, (hipStream_t)stream, slot, q, count,
+                           back_idx, back_cnt, out_idx, out_cnt);
+    else
+        hipLaunchKernelGGL(route_unpack_kernel<false>, grid, dim3(BLOCK), 0, (hipStream_t)stream, slot, q, count,
+                           back_idx, back_cnt, out_idx, out_cnt);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return set_error(KAD_ERR_HIP, hipGetErrorString(e));
+    return KAD_OK;
+}

@@ -269,3 +269,190 @@ def return_results(local_idx, local_cnt, ctx, group=None):
     out_idx[order] = back_idx
     out_cnt[order] = back_cnt.to(torch.uint8)
     return out_idx, out_cnt
+
+
+class OwnerRoute:
+    """Device-only owner routing of one step shape (q targets per rank, count, world ranks): the serving front end's
+    exchange without a host read per batch and without sorting.
+
+      pack    kad_route_pack: every target into the fixed-size send block of its owner (rank (byte 0 >> (8 -
+              shard_bits)) % world), its place recorded per query
+      send    all_to_all_single of the target blocks (equal splits; RCCL over xGMI, gloo through the host)
+      answer  the owner's table answers every record of the received blocks (padding records included: their rows
+              are never read back)
+      return  all_to_all_single of the row and count blocks, back to the senders
+      unpack  kad_route_unpack: each query's row to its original position
+
+    cap: records per block; default q / world + 6 sigma + 256 of uniform targets. A block that fills sets a sticky
+    word; overflowed() combines it over the ranks (one host read per batch, or per K steps), grown() sizes the
+    blocks from the counts, and the batch runs again. collective=True forces the collectives at world 1 (a one-rank
+    RCCL group)."""
+
+    def __init__(self, q: int, count: int, world: int, shard_bits: int, device, cap: int | None = None,
+                 collective: bool | None = None):
+        import torch
+
+        self.q, self.count, self.world, self.shard_bits, self.dev = q, count, world, shard_bits, device
+        self.collective = world > 1 if collective is None else bool(collective)
+        nominal = -(-q // world)
+        self.cap_max = max(1, q)
+        self.cap = max(1, min(self.cap_max, cap or nominal + 6 * int(np.sqrt(nominal)) + 256))
+        n = world * self.cap
+        self.send = torch.empty((n, 20), dtype=torch.uint8, device=device)
+        self.recv = torch.empty_like(self.send) if self.collective else self.send
+        self.slot = torch.empty((max(q, 1),), dtype=torch.int32, device=device)
+        self.ctr = torch.zeros(((world + 1) * 32,), dtype=torch.int32, device=device)
+        self.rows = torch.empty((n, max(count, 1)), dtype=torch.int32, device=device)
+        self.cnt = torch.empty((n,), dtype=torch.uint8, device=device)
+        self.back_rows = torch.empty_like(self.rows) if self.collective else self.rows
+        self.back_cnt = torch.empty_like(self.cnt) if self.collective else self.cnt
+
+    @property
+    def xgmi_bytes(self) -> dict:
+        """Bytes a rank sends to the other ranks per step: targets out, rows + counts back."""
+        return {"targets": 20 * (self.world - 1) * self.cap, "rows": (4 * self.count + 1) * (self.world - 1) * self.cap}
+
+    def pack(self, targets, stream):
+        import ctypes as C
+
+        from ._lib import check, lib, ptr
+
+        check(lib().kad_route_pack(ptr(targets), self.q, self.world, self.shard_bits, self.cap, ptr(self.send),
+                                   ptr(self.slot), ptr(self.ctr), self.dev.index or 0, C.c_void_p(stream)),
+              "kad_route_pack")
+
+    def unpack(self, out_idx, out_cnt, stream):
+        import ctypes as C
+
+        from ._lib import check, lib, ptr
+
+        check(lib().kad_route_unpack(ptr(self.slot), self.q, self.count, ptr(self.back_rows), ptr(self.back_cnt),
+                                     ptr(out_idx), ptr(out_cnt), self.dev.index or 0, C.c_void_p(stream)),
+              "kad_route_unpack")
+
+    def answer(self, table, stream):
+        """The owner's rows for every record of the received blocks (table: a DeviceTable)."""
+        table.rt_closest(self.recv, self.count, out_idx=self.rows, out_cnt=self.cnt, stream=stream)
+
+    def step(self, table, targets, out_idx, out_cnt, group=None, stream=None):
+        """pack, send, answer, return, unpack: device-only (check overflowed() after)."""
+        import torch
+
+        from .global_shard import _torch_stream
+
+        s = stream if stream is not None else torch.cuda.current_stream(self.dev).cuda_stream
+        self.pack(targets, s)
+        if self.collective:
+            with torch.cuda.stream(_torch_stream(s, self.dev)):
+                _all_to_all(self.recv, self.send, group)
+        self.answer(table, s)
+        if self.collective:
+            with torch.cuda.stream(_torch_stream(s, self.dev)):
+                _all_to_all(self.back_rows, self.rows, group)
+                _all_to_all(self.back_cnt, self.cnt, group)
+        self.unpack(out_idx, out_cnt, s)
+
+    def overflowed(self, group=None, combine: bool = True) -> bool:
+        """Host read of the sticky overflow word, combined over the ranks (every rank decides the same)."""
+        ov = self.ctr[self.world * 32:self.world * 32 + 1]
+        if combine and self.collective:
+            import torch.distributed as dist
+
+            if dist.get_backend(group) == "nccl":
+                dist.all_reduce(ov, op=dist.ReduceOp.MAX, group=group)
+            else:
+                h = ov.cpu()
+                dist.all_reduce(h, op=dist.ReduceOp.MAX, group=group)
+                ov.copy_(h)
+        return bool(int(ov.item()))
+
+    def need(self, group=None) -> int:
+        """The largest block count of the last pack, combined over the ranks."""
+        import torch
+
+        n = int(self.ctr.view(self.world + 1, 32)[:self.world, 0].max().item())
+        if self.collective:
+            import torch.distributed as dist
+
+            nccl = dist.get_backend(group) == "nccl"
+            t = torch.tensor([n], dtype=torch.int64, device=self.dev if nccl else "cpu")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+            n = int(t.item())
+        return n
+
+    def grown(self, group=None, need: int | None = None) -> "OwnerRoute":
+        n = self.need(group) if need is None else need
+        return OwnerRoute(self.q, self.count, self.world, self.shard_bits, self.dev,
+                          cap=min(self.cap_max, max(2 * self.cap, n * 5 // 4)), collective=self.collective)
+
+
+def _all_to_all(recv, send, group=None):
+    """recv <- block r of every rank's send, equal splits (dim 0): RCCL on device tensors; gloo through the host."""
+    import torch.distributed as dist
+
+    if dist.get_backend(group) == "nccl":
+        dist.all_to_all_single(recv, send, group=group)
+        return
+    from .global_shard import exchange_into
+
+    exchange_into(recv.view(-1), send.view(-1), group)
+
+
+def serve_owner(table, targets, count: int, route: OwnerRoute | None = None, group=None, stream=None):
+    """Answer a batch of arbitrary targets through the owner-routed shards (every rank calls it with its own batch):
+    returns (out_idx, out_cnt, route) with each query's row at its position. Grows the blocks and runs again when
+    one overflowed (the decision combined over the ranks)."""
+    import torch
+    import torch.distributed as dist
+
+    q = targets.shape[0]
+    world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+    if route is None:
+        shard_bits = (world.bit_length() - 1) if world > 1 else 0
+        route = OwnerRoute(q, count, world, shard_bits, targets.device)
+    out_idx = torch.empty((q, count), dtype=torch.int32, device=targets.device)
+    out_cnt = torch.empty((q,), dtype=torch.uint8, device=targets.device)
+    while True:
+        route.step(table, targets, out_idx, out_cnt, group, stream)
+        if not route.overflowed(group):
+            return out_idx, out_cnt, route
+        route = route.grown(group)
+
+
+def route_simulated(tables, batches, count: int, shard_bits: int, cap: int | None = None):
+    """Every rank of the owner-routed exchange in ONE process (one GPU): rank r packs batches[r]; rank d receives
+    block d of every rank's send buffer, concatenated in rank order (what all_to_all_single delivers), answers it
+    with tables[d]; rank s receives block s of every rank's rows; rank s unpacks. Grows and reruns on overflow.
+    Returns ([(out_idx, out_cnt)] per rank, the last OwnerRoute of rank 0)."""
+    import torch
+
+    world = len(tables)
+    dev = batches[0].device
+    s = torch.cuda.current_stream(dev).cuda_stream
+    while True:
+        routes = [OwnerRoute(b.shape[0], count, world, shard_bits, dev, cap=cap, collective=False) for b in batches]
+        if len({r.cap for r in routes}) != 1:
+            raise ValueError("every rank's batch must give the same block size")
+        c = routes[0].cap
+        for r, b in zip(routes, batches):
+            r.pack(b, s)
+        over = any(bool(int(r.ctr[world * 32].item())) for r in routes)
+        if over:
+            cap = max(2 * c, max(int(r.ctr.view(world + 1, 32)[:world, 0].max().item()) for r in routes) * 5 // 4)
+            continue
+        answered = []
+        for d in range(world):
+            recv = torch.cat([r.send[d * c:(d + 1) * c] for r in routes])
+            rows = torch.empty((world * c, count), dtype=torch.int32, device=dev)
+            cnt = torch.empty((world * c,), dtype=torch.uint8, device=dev)
+            tables[d].rt_closest(recv, count, out_idx=rows, out_cnt=cnt)
+            answered.append((rows, cnt))
+        out = []
+        for src, r in enumerate(routes):
+            r.back_rows = torch.cat([answered[d][0][src * c:(src + 1) * c] for d in range(world)])
+            r.back_cnt = torch.cat([answered[d][1][src * c:(src + 1) * c] for d in range(world)])
+            oi = torch.empty((r.q, count), dtype=torch.int32, device=dev)
+            oc = torch.empty((r.q,), dtype=torch.uint8, device=dev)
+            r.unpack(oi, oc, s)
+            out.append((oi, oc))
+        return out, routes[0]

@@ -6,7 +6,8 @@ so that the multi-GPU code's RCCL branches run on the device at least once (the 
     all_gather_into_tensor; both started with capacities of 1, so the sticky overflow word is combined with a
     device-tensor all_reduce(MAX) and the needed capacities with another, the layout grows and the batch reruns;
   * owner routing (sharded.route_queries / return_results): all_to_all_single of the split sizes, the targets,
-    the rows and the counts, on device tensors.
+    the rows and the counts, on device tensors; and its device-only form (sharded.OwnerRoute through serve_owner:
+    kad_route_pack, all_to_all_single of the fixed-size blocks, kad_route_unpack, the overflow combine).
 
 Every row is compared with the oracle on the whole table (routing_table.cpp:67-111; the windows of
 routing_table.cpp:89-104). Prints RCCL_WORLD1_OK and one JSON line of step timings."""
@@ -30,7 +31,7 @@ import torch.distributed as dist  # noqa: E402
 import oracle as O  # noqa: E402
 from opendht_amd import synth as S  # noqa: E402
 from opendht_amd.global_shard import Exchange, GlobalShard, build_plain_shard  # noqa: E402
-from opendht_amd.sharded import ShardSpec, return_results, route_queries  # noqa: E402
+from opendht_amd.sharded import OwnerRoute, ShardSpec, return_results, route_queries, serve_owner  # noqa: E402
 from opendht_amd.table import DeviceTable  # noqa: E402
 
 
@@ -95,6 +96,14 @@ def main():
             torch.cuda.synchronize()
             np.testing.assert_array_equal(oc.cpu().numpy(), wcnt, err_msg=f"routed k={count} counts")
             np.testing.assert_array_equal(oi.cpu().numpy().view(np.uint32), want, err_msg=f"routed k={count}")
+            # the device-only owner routing (kad_route_pack / unpack) with its all_to_alls through RCCL, started
+            # with blocks of one record: the overflow and the block counts are combined through RCCL all_reduces
+            route = OwnerRoute(q, count, 1, 0, dev, cap=1, collective=True)
+            oi, oc, route = serve_owner(T, tg, count, route=route)
+            torch.cuda.synchronize()
+            assert route.cap > 1
+            np.testing.assert_array_equal(oc.cpu().numpy(), wcnt, err_msg=f"owner route k={count} counts")
+            np.testing.assert_array_equal(oi.cpu().numpy().view(np.uint32), want, err_msg=f"owner route k={count}")
         T.close()
     finally:
         G.close()

@@ -1,0 +1,150 @@
+"""Owner routing of a serving front end, device-only (kad_route_pack / kad_route_unpack, sharded.OwnerRoute;
+DESIGN.md §6.1): every rank sends its batch's targets to the ranks owning them, the owners answer from their
+halo shards, the rows come back to the senders' positions. The reference answers each request where it arrives
+(Dht::onFindNode / onGetValues, dht.cpp:3189-3217), every answer the whole table's findClosestNodes
+(routing_table.cpp:67-111). Checked bit-exact against the oracle on the whole table: N = 1, 2, 4, 8 ranks simulated
+on one GPU (blocks concatenated as all_to_all_single delivers them), capacities of 1 (overflow, growth, rerun), and
+two real gloo ranks sharing the GPU."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+import oracle as O
+from opendht_amd import DeviceTable
+from opendht_amd import synth as S
+from opendht_amd.sharded import OwnerRoute, ShardSpec, build_shard, route_simulated
+
+pytestmark = pytest.mark.gpu
+
+
+def _batch(spec, n, seed):
+    """Targets over the whole ID space plus node IDs and bucket firsts next to every shard edge."""
+    rng = np.random.default_rng(seed)
+    parts = [S.random_targets(n, seed=seed)]
+    per = spec.n_buckets // spec.n_shards
+    for e in range(0, spec.n_buckets + 1, per):
+        for b in (e - 1, e):
+            if 0 <= b < spec.n_buckets:
+                f = S.bucket_firsts(spec.depth, b, b + 1).copy()
+                f[0, 8:] = rng.integers(0, 256, 12, dtype=np.uint8)
+                parts.append(f)
+    return np.ascontiguousarray(np.concatenate(parts), np.uint8)
+
+
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+@pytest.mark.parametrize("small_cap", [False, True], ids=["", "cap1"])
+def test_owner_route_simulated(gpu, world, small_cap):
+    spec = ShardSpec(n_shards=world, depth=10, mean_per_bucket=6.0, seed=0x0A0 + world, good_pct=60, expired_pct=20)
+    gids, gst, goff = spec.bucket_range(0, spec.n_buckets)
+    gfirst = S.bucket_firsts(spec.depth, 0, spec.n_buckets)
+    shards = [build_shard(spec, s) for s in range(world)]
+    tables = [DeviceTable(sh.ids, sh.status, sh.first, sh.off, device=0, index_base=sh.index_base, sorted=True)
+              for sh in shards]
+    try:
+        batches = [_batch(spec, 3000, seed=world * 16 + r) for r in range(world)]
+        n = min(b.shape[0] for b in batches)
+        batches = [b[:n] for b in batches]
+        tgs = [torch.from_numpy(b).to(gpu) for b in batches]
+        for count in (1, 8, 14, 32):
+            out, r0 = route_simulated(tables, tgs, count, spec.shard_bits, cap=1 if small_cap else None)
+            torch.cuda.synchronize()
+            if small_cap:
+                assert r0.cap > 1  # it grew
+            for r, (oi, oc) in enumerate(out):
+                want, wcnt = O.flat_rt_closest(gids, gst, gfirst, goff, batches[r], count, nthreads=8)
+                np.testing.assert_array_equal(oc.cpu().numpy(), wcnt, err_msg=f"N={world} rank {r} k={count} counts")
+                np.testing.assert_array_equal(oi.cpu().numpy().view(np.uint32), want,
+                                              err_msg=f"N={world} rank {r} k={count}")
+    finally:
+        for T in tables:
+            T.close()
+
+
+def test_route_pack_layout(gpu):
+    """kad_route_pack places every target in its owner's block once, counts each block, flags a full block."""
+    q, world, bits = 5000, 4, 2
+    t = torch.randint(0, 256, (q, 20), dtype=torch.uint8, device=gpu)
+    R = OwnerRoute(q, 8, world, bits, gpu, cap=q)
+    s = torch.cuda.current_stream(gpu).cuda_stream
+    R.pack(t, s)
+    torch.cuda.synchronize()
+    owner = (t[:, 0].to(torch.int64) >> (8 - bits)) % world
+    slot = R.slot.cpu().numpy().view(np.uint32).astype(np.int64)
+    cnts = R.ctr.view(world + 1, 32)[:, 0].cpu().numpy()
+    assert cnts[world] == 0
+    np.testing.assert_array_equal(cnts[:world], torch.bincount(owner, minlength=world).cpu().numpy())
+    np.testing.assert_array_equal(slot // q, owner.cpu().numpy())
+    assert np.unique(slot).size == q
+    np.testing.assert_array_equal(R.send[torch.from_numpy(slot).to(gpu)].cpu().numpy(), t.cpu().numpy())
+    R2 = OwnerRoute(q, 8, world, bits, gpu, cap=q // world // 2)
+    R2.pack(t, s)
+    torch.cuda.synchronize()
+    assert R2.overflowed(combine=False)
+    assert int((R2.slot.cpu().numpy().view(np.uint32) == 0xFFFFFFFF).sum()) > 0
+
+
+def _free_port():
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def _serve_worker(rank, world, port, q):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path[:0] = [os.path.dirname(here), os.path.join(os.path.dirname(here), "oracle"), here]
+    import torch.distributed as dist
+
+    import oracle as O
+    from opendht_amd import DeviceTable
+    from opendht_amd import synth as S
+    from opendht_amd.sharded import OwnerRoute, ShardSpec, build_shard, serve_owner
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)  # both ranks on cuda:0: gloo through the host
+    ok, why = False, "did not finish"
+    try:
+        dev = torch.device("cuda:0")
+        spec = ShardSpec(n_shards=world, depth=9, mean_per_bucket=6.0, seed=0x5B, good_pct=50, expired_pct=25)
+        sh = build_shard(spec, rank)
+        T = DeviceTable(sh.ids, sh.status, sh.first, sh.off, device=0, index_base=sh.index_base, sorted=True)
+        gids, gst, goff = spec.bucket_range(0, spec.n_buckets)
+        gfirst = S.bucket_firsts(spec.depth, 0, spec.n_buckets)
+        targets = _batch(spec, 1500, seed=40 + rank)[:1500]
+        tg = torch.from_numpy(targets).to(dev)
+        ok, why = True, ""
+        for count in (1, 8, 14, 32):
+            for cap in (None, 1):
+                route = OwnerRoute(tg.shape[0], count, world, spec.shard_bits, dev, cap=cap)
+                oi, oc, route = serve_owner(T, tg, count, route=route)
+                torch.cuda.synchronize()
+                want, wcnt = O.flat_rt_closest(gids, gst, gfirst, goff, targets, count)
+                if not (np.array_equal(oi.cpu().numpy().view(np.uint32), want) and np.array_equal(oc.cpu().numpy(), wcnt)):
+                    ok, why = False, f"rank {rank} k={count} cap={cap}"
+        T.close()
+    except Exception as e:  # reported through the queue
+        ok, why = False, f"{type(e).__name__}: {e}"
+    finally:
+        q.put((rank, ok, why))
+        dist.destroy_process_group()
+
+
+def test_serve_owner_gloo_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_serve_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in procs:
+        r, ok, why = q.get(timeout=240)
+        res[r] = (ok, why)
+    for p in procs:
+        p.join(timeout=60)
+    assert res == {0: (True, ""), 1: (True, "")}, res
