@@ -393,10 +393,14 @@ def main_owner(args):
     ref = [rt_algorithmic_bytes(sh.status, sh.off, T.find_bucket(tgs[j]).cpu().numpy().view(np.uint32)
                                 .astype(np.int64), cnt_k) for j in range(min(4, NB))]
     ref_bytes = float(np.mean([r[0] for r in ref]))
-    traffic = None
+    traffic = traffic_src = None
     tj = load_json(args.traffic_json)
     if tj and tj.get("kernel", "") in kernel and tj.get("count") == cnt_k:
         traffic = tj.get("hbm_bytes_per_launch")
+        traffic_src = {"file": os.path.relpath(args.traffic_json, ROOT), "date": tj.get("date"),
+                       "source": tj.get("source"), "correction": tj.get("correction"),
+                       "note": "rocprofv3 PMC of a separate run of this command (counters cannot be collected in the "
+                               "timed run); not measured by this run"}
     gath = load_json(args.gather_json)
     # the ceiling row for this line size and table footprint (64-byte lines: 134 MB; 128-byte: 268 MB)
     ceil = None
@@ -485,6 +489,7 @@ def main_owner(args):
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
+                "traffic_source": traffic_src,
                 "kernel": kernel,
                 "bytes_per_query": moved_q,
                 "bytes_basis": f"bytes the kernel must move per query: 20 target + {line_b} window line "

@@ -349,8 +349,13 @@ public:
         for (size_t k = 0; k < m; k++) out.push_back(nodes_[cand[k].idx]);
         return out;
     }
-    /* Batches of at most q requests with count <= max_count take the host path (0: never; the default picks q from
-       the table size, below). */
+    /* Batches of at most q requests with count <= max_count take the host path (0: never; kHostPathAuto, the
+       default: q from the table size, below).
+       The two paths read liveness differently: the host path evaluates isGood(now) on the table's own Node objects
+       (as routing_table.cpp:77 does), the device path the liveness mirrored through nodeUpdated / syncTimes. They
+       agree when every change is reported (the mirror's contract); a change that is not reported shows up only in
+       the answers of device batches (more than hostBatchLimit() requests, or count above max_count). */
+    static constexpr size_t kHostPathAuto = ~size_t(0);
     void setHostPath(size_t q, size_t max_count = 64) {
         host_q_ = q;
         host_count_ = max_count;

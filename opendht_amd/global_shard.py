@@ -393,14 +393,37 @@ def exchange_into(recv, send, group=None):
         return
     world, rank = dist.get_world_size(group), dist.get_rank(group)
     cs = send.cpu()
-    try:
+    if _host_all_to_all(group, world):
         cr = torch.empty_like(cs)
-        dist.all_to_all_single(cr, cs, group=group)
-    except (RuntimeError, NotImplementedError):
+        dist.all_to_all_single(cr, cs, group=group)  # a real failure (timeout, dead peer) raises
+    else:
         full = [torch.empty_like(cs) for _ in range(world)]
         dist.all_gather(full, cs, group=group)
         cr = torch.cat([f.view(world, -1)[rank] for f in full])
     recv.copy_(cr.to(recv.device))
+
+
+_A2A_OK: dict = {}
+
+
+def _host_all_to_all(group, world: int) -> bool:
+    """Whether this (gloo) group runs all_to_all_single on host tensors: probed once per group with a tiny
+    collective that every rank reaches at the same call (so all ranks then take the same collective), cached.
+    Only the probe's own "unsupported" errors select the all-gather fallback."""
+    import torch
+    import torch.distributed as dist
+
+    key = id(group) if group is not None else None
+    if key not in _A2A_OK:
+        try:
+            x = torch.zeros(world, dtype=torch.int32)
+            dist.all_to_all_single(torch.empty_like(x), x, group=group)
+            _A2A_OK[key] = True
+        except (RuntimeError, NotImplementedError) as e:
+            if "not supported" not in str(e).lower() and "not implemented" not in str(e).lower():
+                raise
+            _A2A_OK[key] = False
+    return _A2A_OK[key]
 
 
 def gather_into(recv, send, group=None):

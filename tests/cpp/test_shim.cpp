@@ -168,8 +168,10 @@ int main() {
             auto got = mirror.findClosestNodesBatch(targets, now, count);
             check_rt(rt, got, targets, count, now, "moving now");
         }
-        auto one = mirror.findClosestNodes(targets[3], now, 8);
-        auto ref = mirror.findClosestNodesBatch(&targets[3], 2, now, 8);  // two requests: the device path
+        auto one = mirror.findClosestNodes(targets[3], now, 8);  // one request: the host path
+        mirror.setHostPath(0);  // every batch to the device
+        auto ref = mirror.findClosestNodesBatch(&targets[3], 2, now, 8);
+        mirror.setHostPath(kadgpu::RoutingTableMirror<RoutingTable>::kHostPathAuto);
         EXPECT(one == ref[0], "single query (host path) equals the device batch");
         // the host path (single requests below the crossover) for every target and count, against the oracle
         for (uint32_t count : {1u, 8u, 14u, 33u, 300u}) {
