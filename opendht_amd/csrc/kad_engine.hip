@@ -5735,7 +5735,7 @@ constexpr uint32_t RF_POOL = BLOCK * (33 + 17);  // dwords: phase 2's sort buffe
 // derived here as phase 1 derives them, so no line waits for block 0's status writes. Only a window of more than
 // 64 nodes (the serial builder, which reads the table's statuses and good counts) waits for block 0's epoch
 // (published after its good counts). A listed node whose status did not change rebuilds lines that come out the same.
-__device__ __attribute__((always_inline)) void rf_wl_builders(const RfCtx& C, uint32_t* pool) {
+__device__ __attribute__((always_inline)) bool rf_wl_builders(const RfCtx& C, uint32_t* pool) {
     const DevTable& T = C.T;
     const uint32_t B = T.B, lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
     const uint32_t total = C.ninl ? C.ninl : C.mc + C.sc + C.np;  // inline <= RF_INLINE, lists <= 64
@@ -5846,6 +5846,7 @@ __device__ __attribute__((always_inline)) void rf_wl_builders(const RfCtx& C, ui
     }
     const uint32_t nl = host_lines ? C.nhl : s_nl;
     WaveLds& WV = reinterpret_cast<WaveLds*>(pool)[wid];
+    bool deferred = false;  // (lane 0 of a wave that listed a line for the last block)
     for (uint32_t x = (blockIdx.x - 1) * (BLOCK / 64) + wid; x < nl; x += (gridDim.x - 1) * (BLOCK / 64)) {
         uint32_t b, n0, n1;  // (wave-uniform)
         if (host_lines) {  // the run of line x and its offsets (kernel arguments)
@@ -5917,35 +5918,44 @@ __device__ __attribute__((always_inline)) void rf_wl_builders(const RfCtx& C, ui
             const uint32_t o = atomicAdd(C.ctr + RF_NDEF, 1u);
             if (o < RF_FUSE_LINES) C.blist[o] = b;
             else atomicOr(C.ctr + RF_ERR, RF_ERR_DEF);  // (never: at most RF_FUSE_LINES lines per launch)
+            deferred = true;
         }
         wave_lds_sync();
     }
+    return deferred;
 }
 
-// End of a fused launch (FUSE 1 / 2), every block: the last block to finish (a completion counter, after
-// every other block's release; no block waits for another) builds what no builder could without block 0's
-// statuses and good counts: FUSE 1, the window lines of more than 64 nodes the builders listed; FUSE 2, the
-// whole line list again if a builder block gave up waiting for it (RF_REDO: its wait timed out, so block 0
-// was not running; rebuilding a line gives the same line). Then it resets the counters for the next refresh.
 template <int FUSE>
 __device__ void rf_fused_lines(const RfCtx& C, uint32_t* pool, uint32_t n8, const uint32_t* l8, uint32_t bx,
                                uint32_t nbx);
 
+// End of a fused launch (FUSE 1 / 2), every block: the last block to finish (a completion counter; no block
+// waits for another) builds what no builder could without block 0's statuses and good counts: FUSE 1, the
+// window lines of more than 64 nodes the builders listed; FUSE 2, the whole line list again if a builder block
+// gave up waiting for it (RF_REDO: its wait timed out, so block 0 was not running; rebuilding a line gives the
+// same line). Then it resets the counters for the next refresh. Only the blocks whose writes the last block may
+// read release them (block 0: statuses, counts, masks; a builder that listed a deferred line: the list): an
+// agent-scope release writes back the XCD's L2 (buffer_wbl2), and one per builder block cost 2-6 us per
+// refresh. The last block acquires (an L2 invalidate, buffer_inv) only when it has something to build.
 template <int FUSE>
-__device__ void rf_fused_finish(const RfCtx& C, uint32_t* pool) {
-    __shared__ uint32_t last, s_ndef, s_redo, s_n8;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+__device__ void rf_fused_finish(const RfCtx& C, uint32_t* pool, bool publish) {
+    __shared__ uint32_t last, s_ndef, s_redo, s_n8, s_pub;
+    if (threadIdx.x == 0) s_pub = 0;
+    __syncthreads();
+    if (publish) s_pub = 1;
+    __syncthreads();
+    if (s_pub) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // (block-uniform)
     __syncthreads();
     if (threadIdx.x == 0) last = atomicAdd(C.ctr + RF_DONE, 1u) == gridDim.x - 1;
     __syncthreads();
     if (!last) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     if (threadIdx.x == 0) {
         s_ndef = __hip_atomic_load(C.ctr + RF_NDEF, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         s_redo = __hip_atomic_load(C.ctr + RF_REDO, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         s_n8 = __hip_atomic_load(C.ctr + RF_L8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
+    if ((FUSE == 1 && s_ndef) || (FUSE == 2 && s_redo)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     const DevTable& T = C.T;
     if (FUSE == 1 && s_ndef) {
         const uint32_t nd = min(s_ndef, RF_FUSE_LINES), lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
@@ -6059,7 +6069,7 @@ __global__ __launch_bounds__(BLOCK) void rf_nodes_kernel(RfCtx C_arg) {
     constexpr bool skip = false;
 #endif
     if (FUSE == 1 && blockIdx.x > 0) {  // a window-line builder block (independent of block 0)
-        if (!skip) rf_wl_builders(C, pool);
+        const bool deferred = !skip && rf_wl_builders(C, pool);
 #ifdef KAD_RF_TRACE
         __syncthreads();
         RF_STAMP(2);
@@ -6067,7 +6077,7 @@ __global__ __launch_bounds__(BLOCK) void rf_nodes_kernel(RfCtx C_arg) {
             printf("RFBUILD blk=%u start=%llu go=%llu end=%llu\n", blockIdx.x, (unsigned long long)rf_ts[0],
                    (unsigned long long)rf_ts[0], (unsigned long long)rf_ts[2]);
 #endif
-        rf_fused_finish<FUSE>(C, pool);
+        rf_fused_finish<FUSE>(C, pool, deferred);
         return;
     }
     if (FUSE == 2 && blockIdx.x > 0) {  // a general-line builder block: wait for block 0's list (block-uniform)
@@ -6097,11 +6107,11 @@ __global__ __launch_bounds__(BLOCK) void rf_nodes_kernel(RfCtx C_arg) {
             printf("RFBUILD blk=%u start=%llu go=%llu end=%llu\n", blockIdx.x, (unsigned long long)rf_ts[0],
                    (unsigned long long)rf_ts[1], (unsigned long long)rf_ts[2]);
 #endif
-        rf_fused_finish<FUSE>(C, pool);
+        rf_fused_finish<FUSE>(C, pool, false);
         return;
     }
     if (FUSE && skip) {  // (tools build) block 0 skips its work
-        rf_fused_finish<FUSE>(C, pool);
+        rf_fused_finish<FUSE>(C, pool, false);
         return;
     }
     uint64_t* srt = reinterpret_cast<uint64_t*>(pool);  // RF_CAP (phase 2)
@@ -6293,7 +6303,8 @@ __global__ __launch_bounds__(BLOCK) void rf_nodes_kernel(RfCtx C_arg) {
                (unsigned long long)(rf_ts[5] - rf_ts[0]), (unsigned long long)(rf_ts[6] - rf_ts[0]),
                (unsigned long long)(rf_ts[7] - rf_ts[0]));
 #endif
-    if (FUSE) rf_fused_finish<FUSE>(C, pool);
+    // block 0's statuses, counts and masks, for the last block: FUSE 2 released them before publishing the list
+    if (FUSE) rf_fused_finish<FUSE>(C, pool, FUSE == 1);
 }
 
 // New status bytes: all n nodes (nodes == NULL) or the m listed ones; only changes are written and marked.

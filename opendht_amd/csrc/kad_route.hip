@@ -4,8 +4,9 @@
 // front end that spreads lookups over N shard GPUs must send each target to its owner and the rows back. Device-only
 // pieces of that exchange, so that it needs no host read per batch:
 //   route_pack_kernel   targets -> `world` fixed-size send blocks (the owner's block), each query's place recorded;
-//                       per-workgroup counts in LDS, one global atomic per (workgroup, owner); a full block sets a
-//                       sticky overflow word (the caller grows the blocks and runs the batch again)
+//                       per-workgroup counts in LDS (one LDS atomic per wave and owner), one global atomic per
+//                       (workgroup, owner); a full block sets a sticky overflow word (the caller grows the blocks
+//                       and runs the batch again)
 //   route_unpack_kernel rows that came back in the send layout -> each query's original position
 // The blocks travel with all_to_all_single (RCCL over xGMI), equal splits: opendht_amd/sharded.py OwnerRoute.
 #include <hip/hip_runtime.h>
@@ -43,7 +44,19 @@ __global__ __launch_bounds__(BLOCK) void route_pack_kernel(const uint8_t* __rest
             for (int x = 0; x < 5; x++) w[r][x] = __builtin_nontemporal_load(p + x);
             const uint32_t b0 = w[r][0] & 0xFFu;  // InfoHash byte 0: the most significant
             dst[r] = shard_bits ? (b0 >> (8 - shard_bits)) % world : 0u;
-            pos[r] = atomicAdd(&hcnt[dst[r]], 1u);
+        }
+        // places in the workgroup's count of each owner: one LDS atomic per (wave, owner), the wave's lanes of
+        // one owner at consecutive places (their records then leave as contiguous runs)
+        const uint32_t lane = tid & 63u;
+        for (uint32_t d = 0; d < world; d++) {  // (wave-uniform)
+            const uint64_t m = __ballot(dst[r] == d);
+            if (!m) continue;
+            const uint32_t leader = (uint32_t)__builtin_ctzll(m);
+            uint32_t b = 0;
+            if (lane == leader) b = atomicAdd(&hcnt[d], (uint32_t)__builtin_popcountll(m));
+            b = __shfl(b, (int)leader, 64);
+            if (dst[r] == d)
+                pos[r] = b + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
         }
     }
     __syncthreads();
