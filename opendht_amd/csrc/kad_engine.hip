@@ -5319,12 +5319,14 @@ __device__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* lds, uint32_t& to
 // ---------------------------------------------------------------------------------------
 constexpr uint32_t RF_CAP = 2048;
 constexpr uint32_t RF_NB = 0, RF_NR = 1, RF_DONE = 2, RF_L8 = 3, RF_L16 = 4, RF_L32 = 5, RF_LNC = 6, RF_GO = 7;
-// fused launches (FUSE 1 / 2): RF_NDEF window lines left to the last block (windows of more than 64 nodes);
-// RF_REDO set by a builder block that gave up waiting for block 0's list (the last block rebuilds the list);
+// fused launches (FUSE 1 / 2): RF_DONE the completion word (blocks done, blocks that listed deferred lines,
+// blocks that gave up waiting for block 0's list: RF_DONE_*); RF_NDEF window lines left to the last block
+// (windows of more than 64 nodes); word 9 unused;
 // sticky diagnostics, never reset by the device (kad_table_refresh_diag): RF_SPIN spin waits that timed out,
 // RF_DEFB lines the last block built, RF_ERR bounds guards that fired (RF_ERR_* bits; zero unless a bug)
-constexpr uint32_t RF_NDEF = 8, RF_REDO = 9, RF_SPIN = 10, RF_DEFB = 11, RF_ERR = 12, RF_CTRS = 13;
+constexpr uint32_t RF_NDEF = 8, RF_SPIN = 10, RF_DEFB = 11, RF_ERR = 12, RF_CTRS = 13;
 constexpr uint32_t RF_ERR_INB = 1, RF_ERR_RUN = 2, RF_ERR_LINE = 4, RF_ERR_NHR = 8, RF_ERR_DEF = 16;
+constexpr uint32_t RF_DONE_BLOCK = 1u, RF_DONE_DEF = 1u << 12, RF_DONE_REDO = 1u << 22;  // fields of 12 / 10 / 10 bits
 // a builder's wait for block 0's list: 1 s of the 100 MHz wall clock, then the last block does its work
 constexpr uint64_t RF_SPIN_TICKS = 100000000ull;
 
@@ -5932,30 +5934,44 @@ __device__ void rf_fused_lines(const RfCtx& C, uint32_t* pool, uint32_t n8, cons
 // End of a fused launch (FUSE 1 / 2), every block: the last block to finish (a completion counter; no block
 // waits for another) builds what no builder could without block 0's statuses and good counts: FUSE 1, the
 // window lines of more than 64 nodes the builders listed; FUSE 2, the whole line list again if a builder block
-// gave up waiting for it (RF_REDO: its wait timed out, so block 0 was not running; rebuilding a line gives the
+// gave up waiting for it (RF_DONE_REDO: its wait timed out, so block 0 was not running; rebuilding a line gives the
 // same line). Then it resets the counters for the next refresh. Only the blocks whose writes the last block may
 // read release them (block 0: statuses, counts, masks; a builder that listed a deferred line: the list): an
 // agent-scope release writes back the XCD's L2 (buffer_wbl2), and one per builder block cost 2-6 us per
 // refresh. The last block acquires (an L2 invalidate, buffer_inv) only when it has something to build.
 template <int FUSE>
-__device__ void rf_fused_finish(const RfCtx& C, uint32_t* pool, bool publish) {
-    __shared__ uint32_t last, s_ndef, s_redo, s_n8, s_pub;
+__device__ void rf_fused_finish(const RfCtx& C, uint32_t* pool, bool deferred, bool redo) {
+    // one atomic per block: the returned word (plus this block's part) tells the last block whether any block
+    // listed deferred lines or gave up waiting, so the common case reads nothing more
+    __shared__ uint32_t s_last, s_ndef, s_redo, s_n8, s_pub;
     if (threadIdx.x == 0) s_pub = 0;
     __syncthreads();
-    if (publish) s_pub = 1;
+    if (deferred) s_pub = 1;
     __syncthreads();
-    if (s_pub) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // (block-uniform)
+    const bool publish = s_pub || (FUSE == 1 && blockIdx.x == 0);  // block 0: statuses, counts, masks (FUSE 2
+                                                                       // released them before its list)
+    if (publish) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // (block-uniform)
     __syncthreads();
-    if (threadIdx.x == 0) last = atomicAdd(C.ctr + RF_DONE, 1u) == gridDim.x - 1;
-    __syncthreads();
-    if (!last) return;
     if (threadIdx.x == 0) {
-        s_ndef = __hip_atomic_load(C.ctr + RF_NDEF, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_redo = __hip_atomic_load(C.ctr + RF_REDO, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_n8 = __hip_atomic_load(C.ctr + RF_L8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t mine = RF_DONE_BLOCK + (s_pub ? RF_DONE_DEF : 0u) + (redo ? RF_DONE_REDO : 0u);
+        const uint32_t v = atomicAdd(C.ctr + RF_DONE, mine) + mine;
+        s_last = (v & (RF_DONE_DEF - 1)) == gridDim.x;
+        s_ndef = (v / RF_DONE_DEF) & 1023u;
+        s_redo = v / RF_DONE_REDO;
     }
     __syncthreads();
-    if ((FUSE == 1 && s_ndef) || (FUSE == 2 && s_redo)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    if (!s_last) return;
+    if ((FUSE == 1 && s_ndef) || (FUSE == 2 && s_redo)) {  // (block-uniform)
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        if (threadIdx.x == 0) {
+            s_ndef = __hip_atomic_load(C.ctr + RF_NDEF, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_n8 = __hip_atomic_load(C.ctr + RF_L8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __syncthreads();
+    } else {
+        if (threadIdx.x == 0) s_ndef = s_redo = 0;
+        __syncthreads();
+    }
     const DevTable& T = C.T;
     if (FUSE == 1 && s_ndef) {
         const uint32_t nd = min(s_ndef, RF_FUSE_LINES), lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
@@ -5972,10 +5988,11 @@ __device__ void rf_fused_finish(const RfCtx& C, uint32_t* pool, bool publish) {
     if (FUSE == 2 && s_redo) rf_fused_lines<FUSE>(C, pool, s_n8, C.fl, 0u, 1u);
     __syncthreads();
     if (threadIdx.x == 0) {
-        if (s_ndef) atomicAdd(C.ctr + RF_DEFB, s_ndef);
+        if (s_ndef) {
+            atomicAdd(C.ctr + RF_DEFB, s_ndef);
+            C.ctr[RF_NDEF] = 0;
+        }
         if (s_redo) atomicAdd(C.ctr + RF_DEFB, s_n8);
-        C.ctr[RF_NDEF] = 0;
-        C.ctr[RF_REDO] = 0;
         C.ctr[RF_DONE] = 0;
     }
 }
@@ -6077,13 +6094,13 @@ __global__ __launch_bounds__(BLOCK) void rf_nodes_kernel(RfCtx C_arg) {
             printf("RFBUILD blk=%u start=%llu go=%llu end=%llu\n", blockIdx.x, (unsigned long long)rf_ts[0],
                    (unsigned long long)rf_ts[0], (unsigned long long)rf_ts[2]);
 #endif
-        rf_fused_finish<FUSE>(C, pool, deferred);
+        rf_fused_finish<FUSE>(C, pool, deferred, false);
         return;
     }
     if (FUSE == 2 && blockIdx.x > 0) {  // a general-line builder block: wait for block 0's list (block-uniform)
         if (threadIdx.x == 0) {
             // bounded: a list that does not come within RF_SPIN_TICKS (block 0 not running) is left to the last
-            // block to finish (RF_REDO), which runs after block 0 whatever the order the blocks ran in
+            // block to finish (RF_DONE_REDO), which runs after block 0 whatever the order the blocks ran in
             const uint64_t t0 = wall_clock64();
             bool go = !skip;
             while (go && __hip_atomic_load(C.ctr + RF_GO, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != C.epoch) {
@@ -6091,10 +6108,10 @@ __global__ __launch_bounds__(BLOCK) void rf_nodes_kernel(RfCtx C_arg) {
                 if (wall_clock64() - t0 > RF_SPIN_TICKS) {
                     go = false;
                     atomicAdd(C.ctr + RF_SPIN, 1u);
-                    atomicOr(C.ctr + RF_REDO, 1u);
                 }
             }
             lctr[0] = go ? __hip_atomic_load(C.ctr + RF_L8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+            lctr[1] = go || skip ? 0u : 1u;  // redo: the last block builds the list
         }
         __syncthreads();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -6107,11 +6124,11 @@ __global__ __launch_bounds__(BLOCK) void rf_nodes_kernel(RfCtx C_arg) {
             printf("RFBUILD blk=%u start=%llu go=%llu end=%llu\n", blockIdx.x, (unsigned long long)rf_ts[0],
                    (unsigned long long)rf_ts[1], (unsigned long long)rf_ts[2]);
 #endif
-        rf_fused_finish<FUSE>(C, pool, false);
+        rf_fused_finish<FUSE>(C, pool, false, lctr[1] != 0);
         return;
     }
     if (FUSE && skip) {  // (tools build) block 0 skips its work
-        rf_fused_finish<FUSE>(C, pool, false);
+        rf_fused_finish<FUSE>(C, pool, false, false);
         return;
     }
     uint64_t* srt = reinterpret_cast<uint64_t*>(pool);  // RF_CAP (phase 2)
@@ -6304,7 +6321,7 @@ __global__ __launch_bounds__(BLOCK) void rf_nodes_kernel(RfCtx C_arg) {
                (unsigned long long)(rf_ts[7] - rf_ts[0]));
 #endif
     // block 0's statuses, counts and masks, for the last block: FUSE 2 released them before publishing the list
-    if (FUSE) rf_fused_finish<FUSE>(C, pool, FUSE == 1);
+    if (FUSE) rf_fused_finish<FUSE>(C, pool, false, false);
 }
 
 // New status bytes: all n nodes (nodes == NULL) or the m listed ones; only changes are written and marked.
