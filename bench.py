@@ -1257,41 +1257,82 @@ def n8_step_model(ids, st, off, gp, spec, tgs, Q, cnt_k, K, NB, dev, xchg_us):
     n0 = int(off[hi])
     G0 = GlobalShard(ids[:n0], st[:n0], off[:hi + 1], 0, hi, spec.depth, 0, gp, device=dev.index or 0)
     try:
-        ex = G0.exchange(Q, cnt_k, 8)
-        stream = torch.cuda.current_stream(dev)
-        for j in range(2):
-            G0.home_block(tgs[j % NB], ex)
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        torch.cuda.synchronize(dev)
-        a.record(stream)
-        for j in range(K):
-            G0.home_block(tgs[j % NB], ex)
-        b.record(stream)
-        torch.cuda.synchronize(dev)
-        shard_us = a.elapsed_time(b) / K * 1e3
-        blk = ex.send[:ex.block]
-        ex.recv = torch.cat([blk] * 8)
-        lo, hi_q = 0, -(-(-(-Q // 256)) // 8) * 256
-        oi = torch.empty((min(hi_q, Q), cnt_k), dtype=torch.int32, device=dev)
-        oc = torch.empty((min(hi_q, Q),), dtype=torch.uint8, device=dev)
         import ctypes as C
+
+        stream = torch.cuda.current_stream(dev)
         s = C.c_void_p(stream.cuda_stream)
-        ex.home_finish(0, oi, oc, s)
-        torch.cuda.synchronize(dev)
-        a.record(stream)
+        out = {"shard_nodes": n0}
+        for k in sorted({cnt_k, 32}):
+            ex = G0.exchange(Q, k, 8, True, True)
+            ctr = ex.send.view(8, ex.block)[:, ex.ctr_off:ex.ctr_off + 10 * 32]
+            for j in range(2):
+                ctr.zero_()
+                G0.home_block(tgs[j % NB], ex, zeroed=True)
+            # per launch, the counters zeroed between launches outside the timed interval (the step's own finish
+            # zeroes them: kad_rt_home_finish_reset)
+            ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+            for j in range(K):
+                ctr.zero_()
+                ev[j][0].record(stream)
+                G0.home_block(tgs[j % NB], ex, zeroed=True)
+                ev[j][1].record(stream)
+            torch.cuda.synchronize(dev)
+            shard_us = float(np.median([a.elapsed_time(b) for a, b in ev])) * 1e3
+            over = ex.overflowed(combine=False)
+            G0.home_block(tgs[0], ex, zeroed=False)  # (the old form with its zeroing launch, for comparison)
+            torch.cuda.synchronize(dev)
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(stream)
+            for j in range(K):
+                G0.home_block(tgs[j % NB], ex, zeroed=False)
+            b.record(stream)
+            torch.cuda.synchronize(dev)
+            shard_zeroing_us = a.elapsed_time(b) / K * 1e3
+            blk = ex.send[:ex.block]
+            ex.recv = torch.cat([blk] * 8)
+            hi_q = -(-(-(-Q // 256)) // 8) * 256
+            oi = torch.empty((min(hi_q, Q), k), dtype=torch.int32, device=dev)
+            oc = torch.empty((min(hi_q, Q),), dtype=torch.uint8, device=dev)
+            ex.home_finish(0, oi, oc, s, reset=True)
+            torch.cuda.synchronize(dev)
+            a.record(stream)
+            for j in range(K):
+                ex.home_finish(0, oi, oc, s, reset=True)
+            b.record(stream)
+            torch.cuda.synchronize(dev)
+            fin_us = a.elapsed_time(b) / K * 1e3
+            xm = exchange_model(Q, k, dev)["8"]["home_modelled_us"] if k != cnt_k else xchg_us
+            step_us = shard_us + xm + fin_us
+            out[f"k{k}"] = {"shard_kernel_us": shard_us, "shard_kernel_with_zeroing_launch_us": shard_zeroing_us,
+                            "overflow": over, "finish_us": fin_us, "exchange_modelled_us": xm,
+                            "step_modelled_us": step_us, "aggregate_queries_per_s_modelled": Q / (step_us * 1e-6)}
+            del ex, blk, oi, oc
+        # the reach-0 floor: the same kernel on a batch none of whose targets this shard can reach (reading and
+        # testing the batch is all it does)
+        ex = G0.exchange(Q, cnt_k, 8, True, True)
+        far = [t.clone() for t in tgs[:4]]
+        for t in far:
+            t[:, 0] = t[:, 0] | 0x80  # buckets in the upper half of the table: beyond rank 0's reach
+        ctr = ex.send.view(8, ex.block)[:, ex.ctr_off:ex.ctr_off + 10 * 32]
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
         for j in range(K):
-            ex.home_finish(0, oi, oc, s)
-        b.record(stream)
+            ctr.zero_()
+            ev[j][0].record(stream)
+            G0.home_block(far[j % 4], ex, zeroed=True)
+            ev[j][1].record(stream)
         torch.cuda.synchronize(dev)
-        fin_us = a.elapsed_time(b) / K * 1e3
-        step_us = shard_us + xchg_us + fin_us
-        return {"shard_kernel_us": shard_us, "finish_us": fin_us, "exchange_modelled_us": xchg_us,
-                "step_modelled_us": step_us, "aggregate_queries_per_s_modelled": Q / (step_us * 1e-6),
-                "shard_nodes": n0,
-                "how": "rank 0 of 8 (global buckets [0, B/8), no halo) on this GPU: kad_rt_shard_batch_home over "
-                       "the whole replicated batch into 8 home blocks, kad_rt_home_finish over 8 blocks (copies of "
-                       "the block it sends itself: timing only); + the modelled all_to_all at N = 8. The eight ranks "
-                       "answer the one batch together, so the aggregate is Q / step"}
+        out["reach0_shard_kernel_us"] = float(np.median([a.elapsed_time(b) for a, b in ev])) * 1e3
+        top = out[f"k{cnt_k}"]
+        out.update({"shard_kernel_us": top["shard_kernel_us"], "finish_us": top["finish_us"],
+                    "exchange_modelled_us": xchg_us, "step_modelled_us": top["step_modelled_us"],
+                    "aggregate_queries_per_s_modelled": top["aggregate_queries_per_s_modelled"]})
+        out["how"] = ("rank 0 of 8 (global buckets [0, B/8), no halo) on this GPU: kad_rt_shard_step_home over the "
+                      "whole replicated batch into 8 home blocks (HIP events around each launch, median; the "
+                      "counters zeroed between launches outside them, as kad_rt_home_finish_reset leaves them), "
+                      "kad_rt_home_finish_reset over 8 blocks (copies of the block it sends itself: timing only); + "
+                      "the modelled all_to_all at N = 8. The eight ranks answer the one batch together, so the "
+                      "aggregate is Q / step")
+        return out
     finally:
         G0.close()
 

@@ -420,6 +420,18 @@ int kad_rt_shard_batch_home(const kad_table* shard, const uint32_t* global_good_
 int kad_rt_home_finish(const uint32_t* recv, uint32_t world, uint32_t rank, uint32_t row_cap, uint32_t part_cap,
                        uint32_t q, uint32_t count, uint32_t* scratch, uint32_t* out_idx, uint8_t* out_cnt,
                        uint32_t* overflow, int device, void* stream);
+/* The same step without the counter-zeroing launch: kad_rt_shard_step_home is kad_rt_shard_batch_home on send blocks
+ * whose counters are already zero (a zero-filled buffer, or the previous step's kad_rt_home_finish_reset);
+ * kad_rt_home_finish_reset is kad_rt_home_finish that also zeroes the counters of the `world` send blocks in its last
+ * launch (the exchange has delivered them by then). send must not be recv (at world 1 without a collective, use the
+ * zeroing pair above). */
+int kad_rt_shard_step_home(const kad_table* shard, const uint32_t* global_good_prefix, uint32_t global_buckets,
+                           uint64_t global_base_hi, uint32_t depth, uint32_t shard_first_bucket, uint32_t reach_lo,
+                           uint32_t reach_hi, const uint8_t* targets, uint32_t q, uint32_t count, uint32_t world,
+                           uint32_t* send, uint32_t row_cap, uint32_t part_cap, void* stream);
+int kad_rt_home_finish_reset(const uint32_t* recv, uint32_t* send, uint32_t world, uint32_t rank, uint32_t row_cap,
+                             uint32_t part_cap, uint32_t q, uint32_t count, uint32_t* scratch, uint32_t* out_idx,
+                             uint8_t* out_cnt, uint32_t* overflow, int device, void* stream);
 
 /* ---- owner routing of a serving front end ----
  * The headline form shards the table by ID range, one GPU per range, and answers every query on the GPU owning its

@@ -119,6 +119,10 @@ SIGNATURES = {
                                           _P, C.c_uint32, C.c_uint32, C.c_uint32, _P, C.c_uint32, C.c_uint32, _P]),
     "kad_rt_home_finish": (C.c_int, [_P, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, _P,
                                      _P, _P, _P, C.c_int, _P]),
+    "kad_rt_shard_step_home": (C.c_int, [_P, _P, C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
+                                         _P, C.c_uint32, C.c_uint32, C.c_uint32, _P, C.c_uint32, C.c_uint32, _P]),
+    "kad_rt_home_finish_reset": (C.c_int, [_P, _P, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
+                                           C.c_uint32, _P, _P, _P, _P, C.c_int, _P]),
     "kad_route_pack": (C.c_int, [_P, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, _P, _P, _P, C.c_int, _P]),
     "kad_route_unpack": (C.c_int, [_P, C.c_uint32, C.c_uint32, _P, _P, _P, _P, C.c_int, _P]),
     "kad_table_set_addrs": (C.c_int, [_P, C.c_uint32, _P]),

@@ -3407,7 +3407,7 @@ __device__ void wave_shard(const DevTable& T, const ShardCtx& S, const Target& t
     const uint32_t al = a - S.s_lo, el = e - S.s_lo;
     const uint32_t lgood = wave_good_sum(T.gcnt, al, el);
     uint32_t slot = 0;
-    const uint32_t region = blockIdx.x & 7u;
+    const uint32_t region = (qid / BLOCK) & 7u;  // (the region of the query's 256-query block, as its line rows')
     const uint64_t dof = dest_off(S, qid);
     uint32_t* ctr = S.ctr + dof;
     if (lane == 0) slot = atomicAdd(ctr + KAD_SHARD_COUNTER_STRIDE * (complete ? region : 8u), 1u);
@@ -3431,95 +3431,150 @@ __device__ void wave_shard(const DevTable& T, const ShardCtx& S, const Target& t
 // LK: the window-line set the shard's uniform table answers from (8: counts <= 8, 16: 9..16, 32: 17..32; 0: none).
 // A window of that set spans at most LK / 2 buckets on either side, so a query whose bucket lies that far inside the
 // shard has the same window locally as globally.
+// A workgroup takes SHARD_QB = 1,024 queries of the replicated batch: their 20 KB of targets come in as coalesced
+// 16-byte non-temporal loads into LDS (five per thread, all in flight at once: a lane-per-query form had only three
+// small loads in flight per lane and read the batch at ~2 TB/s, 10.6 us per 1M with nothing in reach), the in-reach
+// ones are compacted (at N ranks a shard reaches ~1/N of the batch), then answered BLOCK at a time: the window line of
+// the count's set for queries far enough inside the shard, the wave path on the global window for the rest.
+// Complete rows of 256-query block k go to region k % 8 of home rank home_of_block(k) (one atomic per 256-query
+// block that has rows, as before), so a region's capacity bound is unchanged.
+constexpr uint32_t SHARD_QB = 4 * BLOCK;
+
 template <int LK>
 __global__ __launch_bounds__(BLOCK) void rt_shard_kernel(DevTable T, ShardCtx S, const uint8_t* __restrict__ targets,
-                                                         uint32_t q, uint32_t count) {
+                                                         uint32_t q, uint32_t count, uint32_t aligned16) {
     constexpr uint32_t MARGIN = LK == 8 ? 4u : LK == 16 ? 8u : 16u;
-    // The block's queries within the shard's reach, compacted to its first lanes (at N ranks a shard reaches ~1/N of
-    // the replicated batch: the waves that would hold only out-of-reach lanes then do no line or wave work)
-    __shared__ uint64_t c_hi[BLOCK];
-    __shared__ uint32_t c_t2[BLOCK], c_t3[BLOCK], c_t4[BLOCK], c_i[BLOCK], c_b[BLOCK];
+    __shared__ __attribute__((aligned(16))) uint32_t st[SHARD_QB * 5];  // the block's targets, as stored (20 KB)
+    __shared__ uint16_t cq[SHARD_QB];                                   // in-reach queries (block-local index)
     __shared__ uint32_t c_w[BLOCK / 64 + 1];
-    uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
-    Target t{};
-    bool near = false, line = false;
-    uint32_t b = 0;
-    if (i < q) {
-        t = load_target(targets, i);
-        b = shard_bucket(S, t);
-        near = b >= S.reach_lo && b < S.reach_hi;
+    __shared__ uint64_t xs[BLOCK / 64][192];
+    __shared__ uint32_t wcnt[SHARD_QB / BLOCK][BLOCK / 64], qbase_slot[SHARD_QB / BLOCK];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
+    const uint64_t base = (uint64_t)blockIdx.x * SHARD_QB;
+    const uint32_t nq = (uint32_t)min<uint64_t>(SHARD_QB, q - base);
+    {  // the block's 20 * nq bytes
+        const uint32_t nw = 5 * nq;
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(targets) + 5 * base;
+        uint32_t o = 0;
+        if (aligned16) {  // (targets 16-byte aligned; 5 * base dwords is a multiple of 4)
+            const uint32_t n4 = nw / 4;
+            const u32x4_t* s4 = reinterpret_cast<const u32x4_t*>(src);
+            u32x4_t* d4 = reinterpret_cast<u32x4_t*>(st);
+#pragma unroll
+            for (uint32_t k = 0; k < 5; k++) {
+                const uint32_t x = tid + k * BLOCK;
+                if (x < n4) d4[x] = __builtin_nontemporal_load(s4 + x);
+            }
+            o = 4 * n4;
+        }
+        for (uint32_t x = o + tid; x < nw; x += BLOCK) st[x] = __builtin_nontemporal_load(src + x);
     }
-    {
+    __syncthreads();
+    // the queries within the shard's reach, compacted in query order (a ballot per wave and a block prefix per round)
+    uint32_t nnear = 0;  // (block-uniform)
+    for (uint32_t r = 0; r < SHARD_QB / BLOCK; r++) {
+        const uint32_t j = r * BLOCK + tid;
+        bool near = false;
+        if (j < nq) {
+            const uint64_t hi = ((uint64_t)__builtin_bswap32(st[5 * j]) << 32) | __builtin_bswap32(st[5 * j + 1]);
+            Target th;
+            th.hi = hi;
+            const uint32_t b = shard_bucket(S, th);
+            near = b >= S.reach_lo && b < S.reach_hi;
+        }
         const uint64_t nm = __ballot(near);
-        const uint32_t w = threadIdx.x >> 6;
-        if ((threadIdx.x & 63u) == 0) c_w[w] = (uint32_t)__builtin_popcountll(nm);
+        if (lane == 0) c_w[w] = (uint32_t)__builtin_popcountll(nm);
         __syncthreads();
-        uint32_t pos = lanes_below(nm), tot = 0;
+        uint32_t pos = nnear + lanes_below(nm), tot = 0;
         for (uint32_t k = 0; k < BLOCK / 64; k++) {
             pos += k < w ? c_w[k] : 0u;
             tot += c_w[k];
         }
-        if (near) {
-            c_hi[pos] = t.hi; c_t2[pos] = t.t2; c_t3[pos] = t.t3; c_t4[pos] = t.t4; c_i[pos] = i; c_b[pos] = b;
-        }
+        if (near) cq[pos] = (uint16_t)j;
+        nnear += tot;
         __syncthreads();
-        near = threadIdx.x < tot;
-        if (near) {
-            t.hi = c_hi[threadIdx.x]; t.t2 = c_t2[threadIdx.x]; t.t3 = c_t3[threadIdx.x]; t.t4 = c_t4[threadIdx.x];
-            i = c_i[threadIdx.x];
-            b = c_b[threadIdx.x];
-        }
-        line = LK && near && b >= S.s_lo + MARGIN && b + MARGIN <= S.s_hi;
     }
-    bool edge = near;
-    __shared__ uint64_t xs[BLOCK / 64][192];
-    __shared__ uint32_t wcnt[BLOCK / 64 + 1];
-    if (LK && __syncthreads_or(line)) {  // block-uniform
-        uint32_t o[LK ? LK : 1], m = 0;
-        // (a wave whose lanes are all past the compacted queries skips the line work: a wave-uniform branch)
-        bool ok = false;
-        if (__any(line)) {
-            const uint32_t bl = line ? b - S.s_lo : 0u;
-            if constexpr (LK == 8) ok = line8_answer(T, t, bl, count, line, line && (T.flags & TF_WS), o, m);
-            else if constexpr (LK == 16) ok = wl16_answer(T, t, bl, count, line, o, m);
-            else if constexpr (LK == 32) ok = wl32_answer(T, t, bl, count, line, o, m);
-            ok = ok && line;
+    // the compacted queries, BLOCK at a time (block-uniform loop)
+    for (uint32_t c0 = 0; c0 < nnear; c0 += BLOCK) {
+        const uint32_t k = c0 + tid;
+        const bool act = k < nnear;
+        const uint32_t j = act ? cq[k] : 0u;
+        Target t{};
+        uint32_t b = 0, i = 0;
+        if (act) {
+            const uint32_t* p = st + 5 * j;
+            t.hi = ((uint64_t)__builtin_bswap32(p[0]) << 32) | __builtin_bswap32(p[1]);
+            t.t2 = __builtin_bswap32(p[2]);
+            t.t3 = __builtin_bswap32(p[3]);
+            t.t4 = __builtin_bswap32(p[4]);
+            b = shard_bucket(S, t);
+            i = (uint32_t)base + j;
         }
-        const uint64_t want = __ballot(ok);
-        const uint32_t w = threadIdx.x >> 6;
-        if ((threadIdx.x & 63u) == 0) wcnt[w] = (uint32_t)__builtin_popcountll(want);
-        __syncthreads();
-        // the block's queries share one home rank (home_of_block): one atomic per block
-        const uint64_t dof = dest_off(S, blockIdx.x * BLOCK);
-        if (threadIdx.x == 0) {
-            uint32_t tot = 0;
-            for (uint32_t k = 0; k < BLOCK / 64; k++) tot += wcnt[k];
-            wcnt[BLOCK / 64] = tot ? atomicAdd(S.ctr + dof + KAD_SHARD_COUNTER_STRIDE * (blockIdx.x & 7u), tot) : 0u;
-        }
-        __syncthreads();
-        uint32_t slot = wcnt[BLOCK / 64] + lanes_below(want);
-        for (uint32_t k = 0; k < w; k++) slot += wcnt[k];
-        if (ok) {
-            if (slot < S.row_cap) {
-                uint32_t* row = S.rows + dof + ((size_t)(blockIdx.x & 7u) * S.row_cap + slot) * S.rs;
-                reinterpret_cast<uint4*>(row)[0] = make_uint4(i, m, 0u, 0u);
-                if constexpr (LK == 8) store_row8(row + 4, o, count);
-                else if constexpr (LK == 16) store_row16(row + 4, o, count);
-                else if constexpr (LK == 32) store_row32(row + 4, o, count);
-                edge = false;
-            } else {
-                atomicOr(S.ctr + dof + KAD_SHARD_COUNTER_STRIDE * 9u, 1u);
+        const bool line = LK && act && b >= S.s_lo + MARGIN && b + MARGIN <= S.s_hi;
+        bool edge = act;
+        if (LK && __syncthreads_or(line)) {  // block-uniform
+            uint32_t o[LK ? LK : 1], m = 0;
+            bool ok = false;
+            if (__any(line)) {  // (a wave of idle lanes skips the line work)
+                const uint32_t bl = line ? b - S.s_lo : 0u;
+                if constexpr (LK == 8) ok = line8_answer(T, t, bl, count, line, line && (T.flags & TF_WS), o, m);
+                else if constexpr (LK == 16) ok = wl16_answer(T, t, bl, count, line, o, m);
+                else if constexpr (LK == 32) ok = wl32_answer(T, t, bl, count, line, o, m);
+                ok = ok && line;
             }
+            // one atomic per 256-query block (sb) with rows in this round: the rows of block sb go to region sb % 8
+            // of its home rank; lanes are grouped by their query's block (compaction keeps query order)
+            const uint32_t sb = act ? j / BLOCK : 0u;
+#pragma unroll
+            for (uint32_t r = 0; r < SHARD_QB / BLOCK; r++) {
+                const uint64_t mb = __ballot(ok && sb == r);
+                if (lane == 0) wcnt[r][w] = (uint32_t)__builtin_popcountll(mb);
+            }
+            __syncthreads();
+            if (tid < SHARD_QB / BLOCK) {
+                uint32_t tot = 0;
+                for (uint32_t x = 0; x < BLOCK / 64; x++) tot += wcnt[tid][x];
+                const uint32_t kb = (uint32_t)(base / BLOCK) + tid;
+                const uint64_t dof = S.dests > 1 ? (uint64_t)home_of_block(kb, S.dests, S.nblk) * S.dest_words : 0ull;
+                qbase_slot[tid] = tot ? atomicAdd(S.ctr + dof + KAD_SHARD_COUNTER_STRIDE * (kb & 7u), tot) : 0u;
+            }
+            __syncthreads();
+            {
+                // the slot of each row: its block's base + the rows of the same block in earlier waves and lanes
+                uint32_t slot = 0;
+                for (uint32_t r = 0; r < SHARD_QB / BLOCK; r++) {
+                    const uint64_t mb = __ballot(ok && sb == r);
+                    if (ok && sb == r) {
+                        slot = qbase_slot[r] + lanes_below(mb);
+                        for (uint32_t x = 0; x < w; x++) slot += wcnt[r][x];
+                    }
+                }
+                if (ok) {
+                    const uint32_t kb = (uint32_t)(base / BLOCK) + sb;
+                    const uint64_t dof = S.dests > 1 ? (uint64_t)home_of_block(kb, S.dests, S.nblk) * S.dest_words : 0ull;
+                    if (slot < S.row_cap) {
+                        uint32_t* row = S.rows + dof + ((size_t)(kb & 7u) * S.row_cap + slot) * S.rs;
+                        reinterpret_cast<uint4*>(row)[0] = make_uint4(i, m, 0u, 0u);
+                        if constexpr (LK == 8) store_row8(row + 4, o, count);
+                        else if constexpr (LK == 16) store_row16(row + 4, o, count);
+                        else if constexpr (LK == 32) store_row32(row + 4, o, count);
+                        edge = false;
+                    } else {
+                        atomicOr(S.ctr + dof + KAD_SHARD_COUNTER_STRIDE * 9u, 1u);
+                    }
+                }
+            }
+            __syncthreads();  // (wcnt / qbase_slot reused by the next round)
         }
-    }
-    for (uint64_t mm = __ballot(edge); mm; mm &= mm - 1) {
-        const uint32_t l = (uint32_t)__builtin_ctzll(mm);
-        Target u;
-        u.hi = rdl64(t.hi, l);
-        u.t2 = rdl(t.t2, l);
-        u.t3 = rdl(t.t3, l);
-        u.t4 = rdl(t.t4, l);
-        wave_shard(T, S, u, rdl(i, l), count, xs[threadIdx.x >> 6]);
+        for (uint64_t mm = __ballot(edge); mm; mm &= mm - 1) {
+            const uint32_t l = (uint32_t)__builtin_ctzll(mm);
+            Target u;
+            u.hi = rdl64(t.hi, l);
+            u.t2 = rdl(t.t2, l);
+            u.t3 = rdl(t.t3, l);
+            u.t4 = rdl(t.t4, l);
+            wave_shard(T, S, u, rdl(i, l), count, xs[w]);
+        }
     }
 }
 
@@ -3666,7 +3721,13 @@ __global__ __launch_bounds__(BLOCK) void gather_scatter_link_kernel(GatherCtx G,
 // The thread of a query's chain head merges its parts (at most one per rank, KAD_SHARD_MAX_WORLD) by
 // (XOR distance, global index), as merge_parts_kernel, and resets the head.
 __global__ void gather_merge_kernel(GatherCtx G, uint32_t* __restrict__ head, const uint32_t* __restrict__ next,
-                                    uint32_t* __restrict__ out_idx, uint8_t* __restrict__ out_cnt) {
+                                    uint32_t* __restrict__ out_idx, uint8_t* __restrict__ out_cnt, uint32_t mblocks,
+                                    uint32_t* __restrict__ zsend) {
+    if (blockIdx.x >= mblocks) {  // kad_rt_home_finish_reset: the send blocks' counters for the next step
+        const uint32_t j = (blockIdx.x - mblocks) * BLOCK + threadIdx.x, words = KAD_SHARD_COUNTERS * KAD_SHARD_COUNTER_STRIDE;
+        if (j < G.world * words) zsend[(uint64_t)(j / words) * G.block + G.ctr_off + j % words] = 0;
+        return;
+    }
     const uint64_t x = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
     const uint32_t* part = gather_part(G, x);
     if (!part) return;
@@ -5362,6 +5423,8 @@ struct RfCtx {
     uint32_t nhr;                        //   run r = lines hr[3r] .. hr[3r] + hr[3r+1] - 1, whose windows' bucket
     uint32_t hr[3 * 16];                 //   offsets h_off[max(0, first - 3) ..] start at hoff[hr[3r+2]]
     uint32_t hoff[256];
+    uint32_t fin;                        // FUSE 1: 1 = some line's window may exceed RF_WCAP1 nodes (the host could
+                                         // not rule it out): the blocks run the completion protocol (rf_fused_finish)
 #ifdef KAD_ABLATIONS
     uint32_t abl;  // tools build (KAD_RF_ABL): 1 = builder blocks skip their work, 2 = block 0 skips its work,
                    // 3 = block 0 starts RF_SPIN_TICKS + 0.2 s late (the builders' wait times out)
@@ -5713,6 +5776,16 @@ __global__ __launch_bounds__(BLOCK) void wl_ws_wave_kernel(const uint64_t* __res
 // blocks 1.. wait for the epoch (dispatched after block 0, so it is always resident) and build the rest, all
 // lines in one round.
 constexpr uint32_t RF_FUSE_LINES = 6 * 128;
+// FUSE 1: a window of 65 .. RF_WCAP1 nodes is staged by its builder wave in LDS (keys, statuses derived as block 0
+// derives them, the window's good counts and masks) and built from there by one lane (wl_build_line on the staged
+// views), without waiting for block 0; only a larger one is left to the launch's last block.
+constexpr uint32_t RF_WCAP1 = 1024;
+struct RfStage {
+    uint64_t key[RF_WCAP1];
+    uint2 dir[8];
+    uint32_t gc[8];
+    uint8_t st[RF_WCAP1];
+};
 
 // p - n as a generic (flat) pointer: p[n + i] is then p[i] for the callee, whatever the address space of p.
 template <class T>
@@ -5741,7 +5814,7 @@ __device__ __attribute__((always_inline)) bool rf_wl_builders(const RfCtx& C, ui
     const DevTable& T = C.T;
     const uint32_t B = T.B, lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
     const uint32_t total = C.ninl ? C.ninl : C.mc + C.sc + C.np;  // inline <= RF_INLINE, lists <= 64
-    static_assert(4 * sizeof(WaveLds) <= 4 * RF_POOL, "builder wave buffers");
+    static_assert(4 * sizeof(WaveLds) + 4 * sizeof(RfStage) <= 4 * RF_POOL, "builder wave buffers");
     __shared__ uint32_t s_node[64];
     __shared__ uint32_t s_st[64];
     __shared__ uint32_t s_lines[RF_FUSE_LINES];
@@ -5848,7 +5921,23 @@ __device__ __attribute__((always_inline)) bool rf_wl_builders(const RfCtx& C, ui
     }
     const uint32_t nl = host_lines ? C.nhl : s_nl;
     WaveLds& WV = reinterpret_cast<WaveLds*>(pool)[wid];
+    RfStage& SG = reinterpret_cast<RfStage*>(pool + (4 * sizeof(WaveLds) + 15) / 16 * 4)[wid];
     bool deferred = false;  // (lane 0 of a wave that listed a line for the last block)
+    // node n's status as this refresh derives it (the listed nodes: from their times or given values)
+    auto derived = [&](uint32_t n) -> uint32_t {
+        if (C.ninl) {
+            uint32_t lo = 0, hi = C.ninl;
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (s_inl[mid] < n) lo = mid + 1; else hi = mid;
+            }
+            return lo < C.ninl && s_inl[lo] == n ? status_at(C.N, n, C.now) : (uint32_t)C.status[n];
+        }
+        uint32_t sv = C.status[n];
+        for (uint32_t j = 0; j < total; j++)
+            if (s_node[j] == n) sv = s_st[j];
+        return sv;
+    };
     for (uint32_t x = (blockIdx.x - 1) * (BLOCK / 64) + wid; x < nl; x += (gridDim.x - 1) * (BLOCK / 64)) {
         uint32_t b, n0, n1;  // (wave-uniform)
         if (host_lines) {  // the run of line x and its offsets (kernel arguments)
@@ -5914,12 +6003,39 @@ __device__ __attribute__((always_inline)) bool rf_wl_builders(const RfCtx& C, ui
                        wid, b, n1 - n0, (unsigned long long)(tb1 - tb0), (unsigned long long)(tb2 - tb1),
                        (unsigned long long)(tb3 - tb2), (unsigned long long)tb0);
 #endif
+        } else if (n1 - n0 <= RF_WCAP1) {
+            // 65 .. RF_WCAP1 nodes: W(2) staged with this refresh's statuses, its buckets' good counts and masks
+            // recounted from them, then the serial build over the staged views (no wait for block 0)
+            const uint32_t e = min(B, b + 3), nbk = e - db;
+            if (lane <= nbk) {
+                const uint32_t f = WV.dx[lane], sz = lane < nbk ? WV.dx[lane + 1] - f : 0u;
+                SG.dir[lane] = make_uint2(f | (sz > 32 ? WIDE : 0u), 0u);
+                SG.gc[lane] = 0;
+            }
+            wave_lds_sync();
+            for (uint32_t o = lane; o < n1 - n0; o += 64) {
+                const uint32_t n = n0 + o, sv = derived(n);
+                SG.key[o] = T.key[n];
+                SG.st[o] = (uint8_t)sv;
+                if (sv & KAD_STATUS_GOOD) {
+                    uint32_t x = 0;
+                    for (uint32_t y = 1; y < nbk; y++) x = WV.dx[y] <= n ? y : x;
+                    atomicAdd(&SG.gc[x], 1u);
+                    if (WV.dx[x + 1] - WV.dx[x] <= 32) atomicOr(&SG.dir[x].y, 1u << (n - WV.dx[x]));
+                }
+            }
+            wave_lds_sync();
+            if (lane == 0) {
+                wl_build_line(flat_shift(SG.key, n0), flat_shift(SG.st, n0), flat_shift(SG.dir, db),
+                              flat_shift(SG.gc, db), B, 64 - T.rshift, T.rbase >> T.rshift, C.wl, b, WV.R);
+                if (C.ws) ws_build_line(WV.R, C.ws, b, WV.R + 33);
+            }
         } else if (lane == 0) {
-            // a window of more than 64 nodes: the serial build reads the table's statuses and good counts, which
-            // block 0 writes; the line goes to the last block to finish (rf_fused_finish), after block 0's writes
+            // more: the serial build reads the table's statuses and good counts, which block 0 writes; the line goes
+            // to the last block to finish (rf_fused_finish, which runs when the host could not rule this out: C.fin)
             const uint32_t o = atomicAdd(C.ctr + RF_NDEF, 1u);
-            if (o < RF_FUSE_LINES) C.blist[o] = b;
-            else atomicOr(C.ctr + RF_ERR, RF_ERR_DEF);  // (never: at most RF_FUSE_LINES lines per launch)
+            if (o < RF_FUSE_LINES && C.fin) C.blist[o] = b;
+            else atomicOr(C.ctr + RF_ERR, RF_ERR_DEF);  // (never)
             deferred = true;
         }
         wave_lds_sync();
@@ -6094,7 +6210,7 @@ __global__ __launch_bounds__(BLOCK) void rf_nodes_kernel(RfCtx C_arg) {
             printf("RFBUILD blk=%u start=%llu go=%llu end=%llu\n", blockIdx.x, (unsigned long long)rf_ts[0],
                    (unsigned long long)rf_ts[0], (unsigned long long)rf_ts[2]);
 #endif
-        rf_fused_finish<FUSE>(C, pool, deferred, false);
+        if (C.fin) rf_fused_finish<FUSE>(C, pool, deferred, false);
         return;
     }
     if (FUSE == 2 && blockIdx.x > 0) {  // a general-line builder block: wait for block 0's list (block-uniform)
@@ -6128,7 +6244,7 @@ __global__ __launch_bounds__(BLOCK) void rf_nodes_kernel(RfCtx C_arg) {
         return;
     }
     if (FUSE && skip) {  // (tools build) block 0 skips its work
-        rf_fused_finish<FUSE>(C, pool, false, false);
+        if (FUSE == 2 || C.fin) rf_fused_finish<FUSE>(C, pool, false, false);
         return;
     }
     uint64_t* srt = reinterpret_cast<uint64_t*>(pool);  // RF_CAP (phase 2)
@@ -6321,7 +6437,7 @@ __global__ __launch_bounds__(BLOCK) void rf_nodes_kernel(RfCtx C_arg) {
                (unsigned long long)(rf_ts[7] - rf_ts[0]));
 #endif
     // block 0's statuses, counts and masks, for the last block: FUSE 2 released them before publishing the list
-    if (FUSE) rf_fused_finish<FUSE>(C, pool, false, false);
+    if (FUSE == 2 || (FUSE == 1 && C.fin)) rf_fused_finish<FUSE>(C, pool, false, false);
 }
 
 // New status bytes: all n nodes (nodes == NULL) or the m listed ones; only changes are written and marked.
@@ -7507,6 +7623,16 @@ int small_refresh(kad_table* t, hipStream_t s, const uint32_t* mnode, uint32_t m
         C.epoch = t->rf_epoch;
         // FUSE 1: block 0 + builder blocks of one line per wave; FUSE 2: 16 lines per block, block 0 included
         const uint32_t lines = C.nhl ? C.nhl : std::min<uint32_t>(B, 6u * total);
+        // FUSE 1: the completion protocol only if some window may exceed RF_WCAP1 nodes (the largest W(2) of the
+        // lines around the host's buckets, from its copy of the offsets; unknown without them)
+        C.fin = 1;
+        if (fuse == 1 && C.nhb && t->h_off.size() == (size_t)B + 1) {
+            uint32_t wmax = 0;
+            for (uint32_t u = 0; u < C.nhb; u++)
+                for (uint32_t l = C.hb[u] > 2 ? C.hb[u] - 2 : 0u; l <= std::min(B - 1, C.hb[u] + 3); l++)
+                    wmax = std::max(wmax, t->h_off[std::min(B, l + 3)] - t->h_off[l >= 3 ? l - 3 : 0u]);
+            C.fin = wmax > RF_WCAP1;
+        }
         g1 = fuse == 1 ? dim3(1 + (lines + BLOCK / 64 - 1) / (BLOCK / 64))
                        : dim3(std::max<uint32_t>(1, (lines + BLOCK / 16 - 1) / (BLOCK / 16)));
     }
@@ -8560,9 +8686,11 @@ static int shard_batch(const kad_table* t, const uint32_t* global_good_prefix, u
     const uint32_t fl = t->d.flags;
     const int lk = !uni ? 0 : count <= 8 ? 8 : count <= 16 ? ((fl & TF_WL16) ? 16 : 0) : ((fl & TF_WL32) ? 32 : 0);
     DeviceGuard g(t->device);
-    void (*kern)(DevTable, ShardCtx, const uint8_t*, uint32_t, uint32_t) =
+    void (*kern)(DevTable, ShardCtx, const uint8_t*, uint32_t, uint32_t, uint32_t) =
         lk == 8 ? rt_shard_kernel<8> : lk == 16 ? rt_shard_kernel<16> : lk == 32 ? rt_shard_kernel<32> : rt_shard_kernel<0>;
-    hipLaunchKernelGGL(kern, dim3(grid_for(q)), dim3(BLOCK), 0, (hipStream_t)stream, t->d, S, targets, q, count);
+    const uint32_t aligned16 = ((uintptr_t)targets & 15u) == 0;
+    hipLaunchKernelGGL(kern, dim3((uint32_t)(((uint64_t)q + SHARD_QB - 1) / SHARD_QB)), dim3(BLOCK), 0,
+                       (hipStream_t)stream, t->d, S, targets, q, count, aligned16);
     HIP_TRY(hipGetLastError());
     return KAD_OK;
 }
@@ -8584,10 +8712,10 @@ void kad_home_range(uint32_t q, uint32_t world, uint32_t rank, uint32_t* lo, uin
     *hi = (uint32_t)std::min<uint64_t>(e, q);
 }
 
-int kad_rt_shard_batch_home(const kad_table* t, const uint32_t* global_good_prefix, uint32_t global_buckets,
-                            uint64_t global_base_hi, uint32_t depth, uint32_t shard_first_bucket, uint32_t reach_lo,
-                            uint32_t reach_hi, const uint8_t* targets, uint32_t q, uint32_t count, uint32_t world,
-                            uint32_t* send, uint32_t row_cap, uint32_t part_cap, void* stream) {
+static int shard_home(const kad_table* t, const uint32_t* global_good_prefix, uint32_t global_buckets,
+                      uint64_t global_base_hi, uint32_t depth, uint32_t shard_first_bucket, uint32_t reach_lo,
+                      uint32_t reach_hi, const uint8_t* targets, uint32_t q, uint32_t count, uint32_t world,
+                      uint32_t* send, uint32_t row_cap, uint32_t part_cap, void* stream, bool zero) {
     if (!t) return set_err(KAD_ERR_INVALID, "NULL table");
     if (world == 0 || world > KAD_SHARD_MAX_WORLD)
         return set_err(KAD_ERR_INVALID, "world %u outside 1..%u", world, KAD_SHARD_MAX_WORLD);
@@ -8597,12 +8725,30 @@ int kad_rt_shard_batch_home(const kad_table* t, const uint32_t* global_good_pref
     const uint64_t parts_off = (uint64_t)KAD_SHARD_REGIONS * row_cap * KAD_ROW_WORDS(count);
     const uint64_t ctr_off = parts_off + (uint64_t)part_cap * KAD_PART_WORDS(count);
     DeviceGuard g(t->device);
-    hipLaunchKernelGGL(zero_counters_kernel, dim3(grid_for((uint64_t)world * KAD_SHARD_COUNTERS * KAD_SHARD_COUNTER_STRIDE)),
-                       dim3(BLOCK), 0, (hipStream_t)stream, send, world, bw, ctr_off);
-    HIP_TRY(hipGetLastError());
+    if (zero) {
+        hipLaunchKernelGGL(zero_counters_kernel, dim3(grid_for((uint64_t)world * KAD_SHARD_COUNTERS * KAD_SHARD_COUNTER_STRIDE)),
+                           dim3(BLOCK), 0, (hipStream_t)stream, send, world, bw, ctr_off);
+        HIP_TRY(hipGetLastError());
+    }
     return shard_batch(t, global_good_prefix, global_buckets, global_base_hi, depth, shard_first_bucket, reach_lo,
                        reach_hi, targets, q, count, send, row_cap, send + parts_off, part_cap, send + ctr_off, world, bw,
                        stream);
+}
+
+int kad_rt_shard_batch_home(const kad_table* t, const uint32_t* global_good_prefix, uint32_t global_buckets,
+                            uint64_t global_base_hi, uint32_t depth, uint32_t shard_first_bucket, uint32_t reach_lo,
+                            uint32_t reach_hi, const uint8_t* targets, uint32_t q, uint32_t count, uint32_t world,
+                            uint32_t* send, uint32_t row_cap, uint32_t part_cap, void* stream) {
+    return shard_home(t, global_good_prefix, global_buckets, global_base_hi, depth, shard_first_bucket, reach_lo,
+                      reach_hi, targets, q, count, world, send, row_cap, part_cap, stream, true);
+}
+
+int kad_rt_shard_step_home(const kad_table* t, const uint32_t* global_good_prefix, uint32_t global_buckets,
+                           uint64_t global_base_hi, uint32_t depth, uint32_t shard_first_bucket, uint32_t reach_lo,
+                           uint32_t reach_hi, const uint8_t* targets, uint32_t q, uint32_t count, uint32_t world,
+                           uint32_t* send, uint32_t row_cap, uint32_t part_cap, void* stream) {
+    return shard_home(t, global_good_prefix, global_buckets, global_base_hi, depth, shard_first_bucket, reach_lo,
+                      reach_hi, targets, q, count, world, send, row_cap, part_cap, stream, false);
 }
 
 int kad_rt_scatter_rows(const uint32_t* rows, const uint32_t* n_rows, uint32_t n_rows_stride, uint32_t n_blocks,
@@ -8636,7 +8782,7 @@ int kad_rt_merge_parts(const uint32_t* parts, uint32_t n_parts, uint32_t count, 
 
 static int gather_finish(const uint32_t* recv, uint32_t world, uint32_t row_cap, uint32_t part_cap, uint32_t qbase,
                          uint32_t q, uint32_t head_words, uint32_t count, uint32_t* scratch, uint32_t* out_idx,
-                         uint8_t* out_cnt, uint32_t* overflow, int device, void* stream) {
+                         uint8_t* out_cnt, uint32_t* overflow, int device, void* stream, uint32_t* zsend = nullptr) {
     int rc = check_count(count);
     if (rc) return rc;
     if (count == 0) return set_err(KAD_ERR_INVALID, "count 0: nothing to answer (the caller writes empty rows)");
@@ -8668,7 +8814,8 @@ static int gather_finish(const uint32_t* recv, uint32_t world, uint32_t row_cap,
     if ((uint64_t)sb + lb > 0x7FFFFFFFull) return set_err(KAD_ERR_INVALID, "buffers too large");
     hipLaunchKernelGGL(gather_scatter_link_kernel, dim3(sb + lb), dim3(BLOCK), 0, s, G, sb, out_idx, out_cnt, overflow,
                        head, next);
-    hipLaunchKernelGGL(gather_merge_kernel, dim3(grid_for(nparts)), dim3(BLOCK), 0, s, G, head, next, out_idx, out_cnt);
+    const uint32_t mb = grid_for(nparts), zb = zsend ? grid_for((uint64_t)world * KAD_SHARD_COUNTERS * KAD_SHARD_COUNTER_STRIDE) : 0u;
+    hipLaunchKernelGGL(gather_merge_kernel, dim3(mb + zb), dim3(BLOCK), 0, s, G, head, next, out_idx, out_cnt, mb, zsend);
     HIP_TRY(hipGetLastError());
     return KAD_OK;
 }
@@ -8689,6 +8836,28 @@ int kad_rt_home_finish(const uint32_t* recv, uint32_t world, uint32_t rank, uint
     kad_home_range(q, world, 0, &lo0, &hi0);  // rank 0's range is the largest
     return gather_finish(recv, world, row_cap, part_cap, lo, hi - lo, hi0 - lo0, count, scratch, out_idx, out_cnt,
                          overflow, device, stream);
+}
+
+int kad_rt_home_finish_reset(const uint32_t* recv, uint32_t* send, uint32_t world, uint32_t rank, uint32_t row_cap,
+                             uint32_t part_cap, uint32_t q, uint32_t count, uint32_t* scratch, uint32_t* out_idx,
+                             uint8_t* out_cnt, uint32_t* overflow, int device, void* stream) {
+    if (world == 0 || rank >= world) return set_err(KAD_ERR_INVALID, "rank %u of world %u", rank, world);
+    if (!send || send == recv) return set_err(KAD_ERR_INVALID, "send must be a buffer of its own (not recv)");
+    uint32_t lo, hi, lo0, hi0;
+    kad_home_range(q, world, rank, &lo, &hi);
+    kad_home_range(q, world, 0, &lo0, &hi0);
+    if (q == 0) {  // (nothing to finish: the counters are zeroed all the same)
+        const uint64_t bw = KAD_SHARD_BLOCK_WORDS(count, row_cap, part_cap);
+        const uint64_t ctr_off = (uint64_t)KAD_SHARD_REGIONS * row_cap * KAD_ROW_WORDS(count) +
+                                 (uint64_t)part_cap * KAD_PART_WORDS(count);
+        DeviceGuard g(device);
+        hipLaunchKernelGGL(zero_counters_kernel, dim3(grid_for((uint64_t)world * KAD_SHARD_COUNTERS * KAD_SHARD_COUNTER_STRIDE)),
+                           dim3(BLOCK), 0, (hipStream_t)stream, send, world, bw, ctr_off);
+        HIP_TRY(hipGetLastError());
+        return KAD_OK;
+    }
+    return gather_finish(recv, world, row_cap, part_cap, lo, hi - lo, hi0 - lo0, count, scratch, out_idx, out_cnt,
+                         overflow, device, stream, send);
 }
 
 int kad_table_set_addrs(kad_table* t, uint32_t addr_len, const uint8_t* addrs) {

@@ -191,8 +191,15 @@ class Exchange:
         return Exchange(self.q, self.count, self.world, self.dev, row_cap=min(row_cap, self.row_cap_max),
                         part_cap=part_cap, home=self.home, collective=self.collective)
 
-    def home_finish(self, rank: int, out_idx, out_cnt, stream):
-        """kad_rt_home_finish over the received blocks: rank `rank`'s rows (device only)."""
+    def home_finish(self, rank: int, out_idx, out_cnt, stream, reset: bool = False):
+        """kad_rt_home_finish over the received blocks: rank `rank`'s rows (device only). reset: also zero the send
+        blocks' counters for the next step (kad_rt_home_finish_reset; the send buffer must not be the receive one)."""
+        if reset:
+            check(lib().kad_rt_home_finish_reset(ptr(self.recv), ptr(self.send), self.world, rank, self.row_cap,
+                                                 self.part_cap, self.q, self.count, ptr(self.scratch), ptr(out_idx),
+                                                 ptr(out_cnt), ptr(self.overflow), self.dev.index or 0, stream),
+                  "kad_rt_home_finish_reset")
+            return
         check(lib().kad_rt_home_finish(ptr(self.recv), self.world, rank, self.row_cap, self.part_cap, self.q,
                                        self.count, ptr(self.scratch), ptr(out_idx), ptr(out_cnt), ptr(self.overflow),
                                        self.dev.index or 0, stream), "kad_rt_home_finish")
@@ -233,16 +240,18 @@ class GlobalShard:
             self._ex[key] = Exchange(q, count, world, self.dev, home=home, collective=coll)
         return self._ex[key]
 
-    def home_block(self, targets, ex: Exchange, stream=None):
+    def home_block(self, targets, ex: Exchange, stream=None, zeroed: bool = False):
         """kad_rt_shard_batch_home over a replicated (q, 20) device batch into ex's `world` send blocks (their
-        counters zeroed by the call); async on `stream` (a raw hipStream_t; default: the current torch stream)."""
+        counters zeroed by the call; zeroed=True: kad_rt_shard_step_home, the counters already zero, as the
+        previous step's finish with reset leaves them); async on `stream` (a raw hipStream_t; default: the current
+        torch stream)."""
         import torch
 
         s = stream if stream is not None else torch.cuda.current_stream(self.dev).cuda_stream
-        check(lib().kad_rt_shard_batch_home(self.table.handle, ptr(self.gpre), self.GB, C.c_uint64(self.base_hi),
-                                            self.depth, self.lo, self.reach[0], self.reach[1], ptr(targets), ex.q,
-                                            ex.count, ex.world, ptr(ex.send), ex.row_cap, ex.part_cap, C.c_void_p(s)),
-              "kad_rt_shard_batch_home")
+        fn = lib().kad_rt_shard_step_home if zeroed else lib().kad_rt_shard_batch_home
+        check(fn(self.table.handle, ptr(self.gpre), self.GB, C.c_uint64(self.base_hi), self.depth, self.lo,
+                 self.reach[0], self.reach[1], ptr(targets), ex.q, ex.count, ex.world, ptr(ex.send), ex.row_cap,
+                 ex.part_cap, C.c_void_p(s)), "kad_rt_shard_batch_home")
 
     def local_block(self, targets, ex: Exchange, stream=None):
         """kad_rt_shard_batch over a replicated (q, 20) device batch into ex's send block (counters zeroed
@@ -275,11 +284,13 @@ class GlobalShard:
         if ex.home:
             if rank is None:
                 rank = rank_of(group) if ex.world > 1 else 0
-            self.home_block(targets, ex, s)
+            # with a collective the send blocks are a buffer of their own: their counters start zero (a new layout
+            # is zero-filled) and each finish zeroes them for the next step, so the step has no zeroing launch
+            self.home_block(targets, ex, s, zeroed=ex.collective)
             if ex.collective:
                 with torch.cuda.stream(_torch_stream(s, self.dev)):
                     exchange_into(ex.recv, ex.send, group)
-            ex.home_finish(rank, out_idx, out_cnt, C.c_void_p(s))
+            ex.home_finish(rank, out_idx, out_cnt, C.c_void_p(s), reset=ex.collective)
             return
         self.local_block(targets, ex, stream)
         if ex.collective:

@@ -75,7 +75,8 @@ def _case(gpu, t, runs, slot_lines=True, seed=1):
 @pytest.mark.parametrize("layout", [0, 1, 2], ids=["16runs_256off", "17runs", "257off"])
 def test_inline_limits_window_lines(gpu, n, layout):
     """Uniform U(12) tables (window lines, the FUSE 1 launch). At ~10 nodes per bucket about a third of the
-    W(2) windows exceed 64 nodes, at ~15 most do: those lines are built by the launch's last block."""
+    W(2) windows exceed 64 nodes, at ~15 most do: their builder waves stage them (up to 1,024 nodes) with this
+    refresh's statuses and build them without waiting for block 0."""
     t = TB.uniform_config(n, 12, seed=0x1A0 + n)
     B = t["off"].shape[0] - 1
     name, runs, want_off = _layouts(B)[layout]
@@ -85,8 +86,18 @@ def test_inline_limits_window_lines(gpu, n, layout):
     d = _case(gpu, t, runs, seed=layout)
     assert d["guard_errors"] == 0, d
     assert d["spin_timeouts"] == 0, d
-    if n == 60_000:
-        assert d["last_block_lines"] > 0, d  # windows of more than 64 nodes were listed and built
+    # windows of 65 .. 1,024 nodes (most of them at n = 60,000) are staged and built by their builder waves
+    assert d["last_block_lines"] == 0, d
+
+
+def test_huge_windows_last_block(gpu):
+    """U(6) at 60,000 nodes: ~940 nodes per bucket, so every W(2) exceeds the builders' 1,024-node staging and the
+    host turns the completion protocol on; the launch's last block builds those lines."""
+    t = TB.uniform_config(60_000, 6, seed=0x1A9)
+    runs = [(0, 2), (30, 2), (62, 2)]
+    d = _case(gpu, t, runs, seed=3)
+    assert d["guard_errors"] == 0 and d["spin_timeouts"] == 0, d
+    assert d["last_block_lines"] > 0, d
 
 
 @pytest.mark.parametrize("layout", [0, 1], ids=["16runs_256off", "17runs"])
