@@ -87,6 +87,15 @@ def mode_shard():
     del ids, st
     tgs = batches(seed=11)
     s = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    far = batches(seed=13)
+    for t in far:
+        t[:, 0] |= 0x80  # beyond rank 0's reach: reading and testing the batch is all the kernel does
+    ex = G0.exchange(Q, 8, 8)
+    run("shard_reach0_us", lambda t: G0.home_block(t, ex), far)
+    own = batches(top3=0, seed=14)  # every query in reach (what one rank holding its own queries would see)
+    ex1 = G0.exchange(Q, 8, 1)
+    run("shard_allreach_k8_us", lambda t: G0.home_block(t, ex1), own)
+    del far, own, ex1
     for k in (8, 32):
         ex = G0.exchange(Q, k, 8)
         run(f"shard_k{k}_us", lambda t: G0.home_block(t, ex), tgs)
