@@ -3358,7 +3358,8 @@ __global__ __launch_bounds__(BLOCK) void rt_dual_wl32q_kernel(DevTable T4, DevTa
 // Complete rows of block k go to region k % 8 of KAD_SHARD_REGIONS regions of row_cap rows: one
 // atomic per block for the window-line rows, eight counters (a single counter hit by every wave cost
 // ~10 ns per wave, 160 us per 1M queries). A region can hold every query of its blocks, so
-// row_cap >= ceil(ceil(q / 256) / 8) * 256 never overflows.
+// row_cap >= 2 * ceil(ceil(q / 256) / 8) * 256 never overflows (a query takes at most two rows: a tombstone and
+// its wave-path row).
 // ---------------------------------------------------------------------------------------
 struct ShardCtx {
     const uint32_t* gpre;  // global good prefix sums, GB + 1
@@ -3470,28 +3471,39 @@ __global__ __launch_bounds__(BLOCK) void rt_shard_kernel(DevTable T, ShardCtx S,
         for (uint32_t x = o + tid; x < nw; x += BLOCK) st[x] = __builtin_nontemporal_load(src + x);
     }
     __syncthreads();
-    // the queries within the shard's reach, compacted in query order (a ballot per wave and a block prefix per round)
-    uint32_t nnear = 0;  // (block-uniform)
-    for (uint32_t r = 0; r < SHARD_QB / BLOCK; r++) {
-        const uint32_t j = r * BLOCK + tid;
-        bool near = false;
-        if (j < nq) {
-            const uint64_t hi = ((uint64_t)__builtin_bswap32(st[5 * j]) << 32) | __builtin_bswap32(st[5 * j + 1]);
-            Target th;
-            th.hi = hi;
-            const uint32_t b = shard_bucket(S, th);
-            near = b >= S.reach_lo && b < S.reach_hi;
+    // the queries within the shard's reach, compacted: thread tid tests queries tid + r * BLOCK, one block scan of
+    // the per-thread counts places them (the order is free: rows carry their qid)
+    uint32_t nnear;  // (block-uniform)
+    {
+        uint32_t nm = 0;
+#pragma unroll
+        for (uint32_t r = 0; r < SHARD_QB / BLOCK; r++) {
+            const uint32_t j = r * BLOCK + tid;
+            if (j < nq) {
+                Target th;
+                th.hi = ((uint64_t)__builtin_bswap32(st[5 * j]) << 32) | __builtin_bswap32(st[5 * j + 1]);
+                const uint32_t b = shard_bucket(S, th);
+                nm |= (b >= S.reach_lo && b < S.reach_hi ? 1u : 0u) << r;
+            }
         }
-        const uint64_t nm = __ballot(near);
-        if (lane == 0) c_w[w] = (uint32_t)__builtin_popcountll(nm);
+        const uint32_t c = (uint32_t)__builtin_popcount(nm);
+        uint32_t inc = c;  // inclusive scan across the wave
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)inc, o, 64);
+            if (lane >= (uint32_t)o) inc += y;
+        }
+        if (lane == 63) c_w[w] = inc;
         __syncthreads();
-        uint32_t pos = nnear + lanes_below(nm), tot = 0;
+        uint32_t pos = inc - c;
+        nnear = 0;
         for (uint32_t k = 0; k < BLOCK / 64; k++) {
             pos += k < w ? c_w[k] : 0u;
-            tot += c_w[k];
+            nnear += c_w[k];
         }
-        if (near) cq[pos] = (uint16_t)j;
-        nnear += tot;
+#pragma unroll
+        for (uint32_t r = 0; r < SHARD_QB / BLOCK; r++)
+            if (nm >> r & 1u) cq[pos++] = (uint16_t)(r * BLOCK + tid);
         __syncthreads();
     }
     // the compacted queries, BLOCK at a time (block-uniform loop)
@@ -3513,22 +3525,17 @@ __global__ __launch_bounds__(BLOCK) void rt_shard_kernel(DevTable T, ShardCtx S,
         const bool line = LK && act && b >= S.s_lo + MARGIN && b + MARGIN <= S.s_hi;
         bool edge = act;
         if (LK && __syncthreads_or(line)) {  // block-uniform
-            uint32_t o[LK ? LK : 1], m = 0;
-            bool ok = false;
-            if (__any(line)) {  // (a wave of idle lanes skips the line work)
-                const uint32_t bl = line ? b - S.s_lo : 0u;
-                if constexpr (LK == 8) ok = line8_answer(T, t, bl, count, line, line && (T.flags & TF_WS), o, m);
-                else if constexpr (LK == 16) ok = wl16_answer(T, t, bl, count, line, o, m);
-                else if constexpr (LK == 32) ok = wl32_answer(T, t, bl, count, line, o, m);
-                ok = ok && line;
-            }
-            // one atomic per 256-query block (sb) with rows in this round: the rows of block sb go to region sb % 8
-            // of its home rank; lanes are grouped by their query's block (compaction keeps query order)
+            // the row slots are reserved before the lines are read (one atomic per 256-query block sb with line
+            // queries in this round: its rows go to region sb % 8 of its home rank), so the atomic's round trip
+            // overlaps the line loads; a query its line cannot answer leaves a tombstone row (qid KAD_NO_NODE, skipped
+            // by the finish) and takes the wave path
             const uint32_t sb = act ? j / BLOCK : 0u;
+            uint32_t slot = 0;
 #pragma unroll
             for (uint32_t r = 0; r < SHARD_QB / BLOCK; r++) {
-                const uint64_t mb = __ballot(ok && sb == r);
+                const uint64_t mb = __ballot(line && sb == r);
                 if (lane == 0) wcnt[r][w] = (uint32_t)__builtin_popcountll(mb);
+                if (line && sb == r) slot = lanes_below(mb);
             }
             __syncthreads();
             if (tid < SHARD_QB / BLOCK) {
@@ -3538,30 +3545,34 @@ __global__ __launch_bounds__(BLOCK) void rt_shard_kernel(DevTable T, ShardCtx S,
                 const uint64_t dof = S.dests > 1 ? (uint64_t)home_of_block(kb, S.dests, S.nblk) * S.dest_words : 0ull;
                 qbase_slot[tid] = tot ? atomicAdd(S.ctr + dof + KAD_SHARD_COUNTER_STRIDE * (kb & 7u), tot) : 0u;
             }
+            uint32_t o[LK ? LK : 1], m = 0;
+            bool ok = false;
+            if (__any(line)) {  // (a wave of idle lanes skips the line work)
+                const uint32_t bl = line ? b - S.s_lo : 0u;
+                if constexpr (LK == 8) ok = line8_answer(T, t, bl, count, line, line && (T.flags & TF_WS), o, m);
+                else if constexpr (LK == 16) ok = wl16_answer(T, t, bl, count, line, o, m);
+                else if constexpr (LK == 32) ok = wl32_answer(T, t, bl, count, line, o, m);
+                ok = ok && line;
+            }
             __syncthreads();
-            {
-                // the slot of each row: its block's base + the rows of the same block in earlier waves and lanes
-                uint32_t slot = 0;
-                for (uint32_t r = 0; r < SHARD_QB / BLOCK; r++) {
-                    const uint64_t mb = __ballot(ok && sb == r);
-                    if (ok && sb == r) {
-                        slot = qbase_slot[r] + lanes_below(mb);
-                        for (uint32_t x = 0; x < w; x++) slot += wcnt[r][x];
-                    }
-                }
-                if (ok) {
-                    const uint32_t kb = (uint32_t)(base / BLOCK) + sb;
-                    const uint64_t dof = S.dests > 1 ? (uint64_t)home_of_block(kb, S.dests, S.nblk) * S.dest_words : 0ull;
-                    if (slot < S.row_cap) {
-                        uint32_t* row = S.rows + dof + ((size_t)(kb & 7u) * S.row_cap + slot) * S.rs;
+            if (line) {
+                for (uint32_t x = 0; x < w; x++) slot += wcnt[sb][x];
+                slot += qbase_slot[sb];
+                const uint32_t kb = (uint32_t)(base / BLOCK) + sb;
+                const uint64_t dof = S.dests > 1 ? (uint64_t)home_of_block(kb, S.dests, S.nblk) * S.dest_words : 0ull;
+                if (slot < S.row_cap) {
+                    uint32_t* row = S.rows + dof + ((size_t)(kb & 7u) * S.row_cap + slot) * S.rs;
+                    if (ok) {
                         reinterpret_cast<uint4*>(row)[0] = make_uint4(i, m, 0u, 0u);
                         if constexpr (LK == 8) store_row8(row + 4, o, count);
                         else if constexpr (LK == 16) store_row16(row + 4, o, count);
                         else if constexpr (LK == 32) store_row32(row + 4, o, count);
                         edge = false;
                     } else {
-                        atomicOr(S.ctr + dof + KAD_SHARD_COUNTER_STRIDE * 9u, 1u);
+                        reinterpret_cast<uint4*>(row)[0] = make_uint4(NONE, 0u, 0u, 0u);  // tombstone
                     }
+                } else {
+                    atomicOr(S.ctr + dof + KAD_SHARD_COUNTER_STRIDE * 9u, 1u);
                 }
             }
             __syncthreads();  // (wcnt / qbase_slot reused by the next round)
@@ -3589,6 +3600,7 @@ __global__ void scatter_rows_kernel(const uint32_t* __restrict__ rows, const uin
     if (r >= n_blocks || k >= min(n_rows[(size_t)r * n_rows_stride], block_cap)) return;
     const uint32_t* src = rows + ((size_t)r * block_cap + k) * stride;
     const uint32_t qid = src[0];
+    if (qid == NONE) return;  // (a tombstone: the query's row comes from the wave path)
     if (out_cnt) out_cnt[qid] = (uint8_t)src[1];
     uint32_t* dst = out_idx + (size_t)qid * count;
     if (count == 8 && ((uintptr_t)dst & 15u) == 0) {
