@@ -3443,7 +3443,9 @@ constexpr uint32_t SHARD_QB = 4 * BLOCK;
 
 template <int LK>
 __global__ __launch_bounds__(BLOCK) void rt_shard_kernel(DevTable T, ShardCtx S, const uint8_t* __restrict__ targets,
-                                                         uint32_t q, uint32_t count, uint32_t aligned16) {
+                                                         uint32_t q, uint32_t count, uint32_t aligned16, uint32_t abl) {
+    // abl (tools build only, KAD_SHARD_ABL; results wrong on purpose): 1 = no wave path (edge queries dropped),
+    // 2 = no line work either (the load and the reach compaction alone)
     constexpr uint32_t MARGIN = LK == 8 ? 4u : LK == 16 ? 8u : 16u;
     __shared__ __attribute__((aligned(16))) uint32_t st[SHARD_QB * 5];  // the block's targets, as stored (20 KB)
     __shared__ uint16_t cq[SHARD_QB];                                   // in-reach queries (block-local index)
@@ -3522,8 +3524,8 @@ __global__ __launch_bounds__(BLOCK) void rt_shard_kernel(DevTable T, ShardCtx S,
             b = shard_bucket(S, t);
             i = (uint32_t)base + j;
         }
-        const bool line = LK && act && b >= S.s_lo + MARGIN && b + MARGIN <= S.s_hi;
-        bool edge = act;
+        const bool line = LK && act && b >= S.s_lo + MARGIN && b + MARGIN <= S.s_hi && !(abl & 2);
+        bool edge = act && !(abl & 3);
         if (LK && __syncthreads_or(line)) {  // block-uniform
             // the row slots are reserved before the lines are read (one atomic per 256-query block sb with line
             // queries in this round: its rows go to region sb % 8 of its home rank), so the atomic's round trip
@@ -8698,11 +8700,15 @@ static int shard_batch(const kad_table* t, const uint32_t* global_good_prefix, u
     const uint32_t fl = t->d.flags;
     const int lk = !uni ? 0 : count <= 8 ? 8 : count <= 16 ? ((fl & TF_WL16) ? 16 : 0) : ((fl & TF_WL32) ? 32 : 0);
     DeviceGuard g(t->device);
-    void (*kern)(DevTable, ShardCtx, const uint8_t*, uint32_t, uint32_t, uint32_t) =
+    void (*kern)(DevTable, ShardCtx, const uint8_t*, uint32_t, uint32_t, uint32_t, uint32_t) =
         lk == 8 ? rt_shard_kernel<8> : lk == 16 ? rt_shard_kernel<16> : lk == 32 ? rt_shard_kernel<32> : rt_shard_kernel<0>;
     const uint32_t aligned16 = ((uintptr_t)targets & 15u) == 0;
+    uint32_t abl = 0;
+#ifdef KAD_ABLATIONS
+    if (const char* e = std::getenv("KAD_SHARD_ABL")) abl = (uint32_t)std::atoi(e);
+#endif
     hipLaunchKernelGGL(kern, dim3((uint32_t)(((uint64_t)q + SHARD_QB - 1) / SHARD_QB)), dim3(BLOCK), 0,
-                       (hipStream_t)stream, t->d, S, targets, q, count, aligned16);
+                       (hipStream_t)stream, t->d, S, targets, q, count, aligned16, abl);
     HIP_TRY(hipGetLastError());
     return KAD_OK;
 }
