@@ -3476,6 +3476,8 @@ __global__ __launch_bounds__(BLOCK) void rt_shard_kernel(DevTable T, ShardCtx S,
     // the queries within the shard's reach, compacted: thread tid tests queries tid + r * BLOCK, one block scan of
     // the per-thread counts places them (the order is free: rows carry their qid)
     uint32_t nnear;  // (block-uniform)
+    uint32_t pf = 0;  // prefetch: a load of each line query's window line, issued here so that the line is in the
+                      // L2 when the compaction has moved the query to its lane (its value is never used)
     {
         uint32_t nm = 0;
 #pragma unroll
@@ -3485,7 +3487,14 @@ __global__ __launch_bounds__(BLOCK) void rt_shard_kernel(DevTable T, ShardCtx S,
                 Target th;
                 th.hi = ((uint64_t)__builtin_bswap32(st[5 * j]) << 32) | __builtin_bswap32(st[5 * j + 1]);
                 const uint32_t b = shard_bucket(S, th);
-                nm |= (b >= S.reach_lo && b < S.reach_hi ? 1u : 0u) << r;
+                const bool in = b >= S.reach_lo && b < S.reach_hi;
+                nm |= (in ? 1u : 0u) << r;
+                if (LK && in && b >= S.s_lo + MARGIN && b + MARGIN <= S.s_hi && !abl) {
+                    const size_t bl = b - S.s_lo;
+                    if constexpr (LK == 8) pf ^= (T.flags & TF_WS) ? T.ws[4 * bl].x : T.wl[8 * bl].x;
+                    else if constexpr (LK == 16) pf ^= T.wl16[(WL16_STRIDE / 4) * bl].x;
+                    else pf ^= T.wl32[(WL32_STRIDE / 4) * bl].x ^ T.wl32[(WL32_STRIDE / 4) * bl + 8].x;
+                }
             }
         }
         const uint32_t c = (uint32_t)__builtin_popcount(nm);
@@ -3508,36 +3517,42 @@ __global__ __launch_bounds__(BLOCK) void rt_shard_kernel(DevTable T, ShardCtx S,
             if (nm >> r & 1u) cq[pos++] = (uint16_t)(r * BLOCK + tid);
         __syncthreads();
     }
-    // the compacted queries, BLOCK at a time (block-uniform loop)
-    for (uint32_t c0 = 0; c0 < nnear; c0 += BLOCK) {
-        const uint32_t k = c0 + tid;
+    // the compacted queries, QN at a time (block-uniform loop): one lane per query, or for count 17..32 four lanes per
+    // query on the 256-byte line (rt_wl32q_kernel's form, ~60 VGPRs instead of ~150, so the load phase above keeps
+    // four workgroups per CU)
+    constexpr bool QUAD = LK == 32;
+    constexpr uint32_t QN = QUAD ? BLOCK / 4 : BLOCK;
+    const uint32_t p = QUAD ? tid & 3u : 0u;
+    for (uint32_t c0 = 0; c0 < nnear; c0 += QN) {
+        const uint32_t k = c0 + (QUAD ? tid >> 2 : tid);
         const bool act = k < nnear;
         const uint32_t j = act ? cq[k] : 0u;
         Target t{};
         uint32_t b = 0, i = 0;
         if (act) {
-            const uint32_t* p = st + 5 * j;
-            t.hi = ((uint64_t)__builtin_bswap32(p[0]) << 32) | __builtin_bswap32(p[1]);
-            t.t2 = __builtin_bswap32(p[2]);
-            t.t3 = __builtin_bswap32(p[3]);
-            t.t4 = __builtin_bswap32(p[4]);
+            const uint32_t* sp = st + 5 * j;
+            t.hi = ((uint64_t)__builtin_bswap32(sp[0]) << 32) | __builtin_bswap32(sp[1]);
+            t.t2 = __builtin_bswap32(sp[2]);
+            t.t3 = __builtin_bswap32(sp[3]);
+            t.t4 = __builtin_bswap32(sp[4]);
             b = shard_bucket(S, t);
             i = (uint32_t)base + j;
         }
         const bool line = LK && act && b >= S.s_lo + MARGIN && b + MARGIN <= S.s_hi && !(abl & 2);
-        bool edge = act && !(abl & 3);
+        const bool lead = !QUAD || p == 0;  // the lane that reserves, stores the header and takes the wave path
+        bool edge = act && lead && !(abl & 3);
         if (LK && __syncthreads_or(line)) {  // block-uniform
             // the row slots are reserved before the lines are read (one atomic per 256-query block sb with line
             // queries in this round: its rows go to region sb % 8 of its home rank), so the atomic's round trip
-            // overlaps the line loads; a query its line cannot answer leaves a tombstone row (qid KAD_NO_NODE, skipped
-            // by the finish) and takes the wave path
+            // overlaps the line loads; a query its line cannot answer leaves a tombstone row (qid KAD_NO_NODE,
+            // skipped by the finish) and takes the wave path
             const uint32_t sb = act ? j / BLOCK : 0u;
             uint32_t slot = 0;
 #pragma unroll
             for (uint32_t r = 0; r < SHARD_QB / BLOCK; r++) {
-                const uint64_t mb = __ballot(line && sb == r);
+                const uint64_t mb = __ballot(line && lead && sb == r);
                 if (lane == 0) wcnt[r][w] = (uint32_t)__builtin_popcountll(mb);
-                if (line && sb == r) slot = lanes_below(mb);
+                if (line && lead && sb == r) slot = lanes_below(mb);
             }
             __syncthreads();
             if (tid < SHARD_QB / BLOCK) {
@@ -3547,17 +3562,24 @@ __global__ __launch_bounds__(BLOCK) void rt_shard_kernel(DevTable T, ShardCtx S,
                 const uint64_t dof = S.dests > 1 ? (uint64_t)home_of_block(kb, S.dests, S.nblk) * S.dest_words : 0ull;
                 qbase_slot[tid] = tot ? atomicAdd(S.ctr + dof + KAD_SHARD_COUNTER_STRIDE * (kb & 7u), tot) : 0u;
             }
-            uint32_t o[LK ? LK : 1], m = 0;
+            uint32_t o[QUAD ? 16 : (LK ? LK : 1)], m = 0;
             bool ok = false;
             if (__any(line)) {  // (a wave of idle lanes skips the line work)
                 const uint32_t bl = line ? b - S.s_lo : 0u;
-                if constexpr (LK == 8) ok = line8_answer(T, t, bl, count, line, line && (T.flags & TF_WS), o, m);
-                else if constexpr (LK == 16) ok = wl16_answer(T, t, bl, count, line, o, m);
-                else if constexpr (LK == 32) ok = wl32_answer(T, t, bl, count, line, o, m);
+                if constexpr (LK == 8) {
+                    ok = line8_answer(T, t, bl, count, line, line && (T.flags & TF_WS), o, m);
+                } else if constexpr (LK == 16) {
+                    ok = wl16_answer(T, t, bl, count, line, o, m);
+                } else if constexpr (QUAD) {
+                    uint32_t v[16], bs;
+                    ok = wl32_answer4<true, false>(T, t, bl, count, line, p, v, m, bs);
+                    quad_row(v, 16u * (p & 1u), bs + T.index_base, m, count, line && ok, o);
+                }
                 ok = ok && line;
             }
             __syncthreads();
             if (line) {
+                if (QUAD) slot = (uint32_t)__shfl((int)slot, (int)(lane & ~3u), 64);
                 for (uint32_t x = 0; x < w; x++) slot += wcnt[sb][x];
                 slot += qbase_slot[sb];
                 const uint32_t kb = (uint32_t)(base / BLOCK) + sb;
@@ -3565,15 +3587,20 @@ __global__ __launch_bounds__(BLOCK) void rt_shard_kernel(DevTable T, ShardCtx S,
                 if (slot < S.row_cap) {
                     uint32_t* row = S.rows + dof + ((size_t)(kb & 7u) * S.row_cap + slot) * S.rs;
                     if (ok) {
-                        reinterpret_cast<uint4*>(row)[0] = make_uint4(i, m, 0u, 0u);
+                        if (lead) reinterpret_cast<uint4*>(row)[0] = make_uint4(i, m, 0u, 0u);
                         if constexpr (LK == 8) store_row8(row + 4, o, count);
                         else if constexpr (LK == 16) store_row16(row + 4, o, count);
-                        else if constexpr (LK == 32) store_row32(row + 4, o, count);
+                        else if constexpr (QUAD) {
+                            if (p < 2u)
+#pragma unroll
+                                for (int e = 0; e < 16; e++)
+                                    if (16u * p + e < count) row[4 + 16 * p + e] = o[e];
+                        }
                         edge = false;
-                    } else {
+                    } else if (lead) {
                         reinterpret_cast<uint4*>(row)[0] = make_uint4(NONE, 0u, 0u, 0u);  // tombstone
                     }
-                } else {
+                } else if (lead) {
                     atomicOr(S.ctr + dof + KAD_SHARD_COUNTER_STRIDE * 9u, 1u);
                 }
             }
@@ -3589,6 +3616,7 @@ __global__ __launch_bounds__(BLOCK) void rt_shard_kernel(DevTable T, ShardCtx S,
             wave_shard(T, S, u, rdl(i, l), count, xs[w]);
         }
     }
+    if (pf == 0x5EEDF00Du && abl == 0xFFFFFFFFu) st[tid] = pf;  // (never: keeps the prefetch loads)
 }
 
 // Gathered complete rows -> out rows. Block r of n_blocks holds n_rows[r] rows of `stride` words at
