@@ -3355,11 +3355,11 @@ __global__ __launch_bounds__(BLOCK) void rt_dual_wl32q_kernel(DevTable T4, DevTa
 // global one); the others take the wave-cooperative path on the global window.
 // Row layout (uint32): qid, m, 0, 0, idx[count] (padded to 4): KAD_ROW_WORDS(count).
 // Part layout: the row, then dist[count][5]: KAD_PART_WORDS(count).
-// Complete rows of block k go to region k % 8 of KAD_SHARD_REGIONS regions of row_cap rows: one
-// atomic per block for the window-line rows, eight counters (a single counter hit by every wave cost
-// ~10 ns per wave, 160 us per 1M queries). A region can hold every query of its blocks, so
-// row_cap >= 2 * ceil(ceil(q / 256) / 8) * 256 never overflows (a query takes at most two rows: a tombstone and
-// its wave-path row).
+// Complete rows of workgroup w (SHARD_QB = 1,024 queries) go to region w % 8 of KAD_SHARD_REGIONS regions of
+// row_cap rows: one atomic per workgroup and home rank for the window-line rows, eight counters per home (a single
+// counter hit by every wave cost ~10 ns per wave, 160 us per 1M queries). A query takes at most two rows (a
+// tombstone and its wave-path row), so row_cap >= 2 * ceil(W / 8) * 1024 never overflows, W = the workgroups
+// holding a home range's queries (ceil(q / 1024) for one home; ceil(ceil(q / 256) / world / 4) + 1 per home).
 // ---------------------------------------------------------------------------------------
 struct ShardCtx {
     const uint32_t* gpre;  // global good prefix sums, GB + 1
@@ -3396,6 +3396,8 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
+constexpr uint32_t SHARD_QB = 4 * BLOCK;  // queries per workgroup of rt_shard_kernel
+
 // One query, wave-uniform: global window, intersection with the shard, wave_rank, append.
 __device__ void wave_shard(const DevTable& T, const ShardCtx& S, const Target& t, uint32_t qid, uint32_t count,
                            uint64_t* xs) {
@@ -3408,7 +3410,7 @@ __device__ void wave_shard(const DevTable& T, const ShardCtx& S, const Target& t
     const uint32_t al = a - S.s_lo, el = e - S.s_lo;
     const uint32_t lgood = wave_good_sum(T.gcnt, al, el);
     uint32_t slot = 0;
-    const uint32_t region = (qid / BLOCK) & 7u;  // (the region of the query's 256-query block, as its line rows')
+    const uint32_t region = (qid / SHARD_QB) & 7u;  // (the region of the query's workgroup, as its line rows')
     const uint64_t dof = dest_off(S, qid);
     uint32_t* ctr = S.ctr + dof;
     if (lane == 0) slot = atomicAdd(ctr + KAD_SHARD_COUNTER_STRIDE * (complete ? region : 8u), 1u);
@@ -3437,10 +3439,8 @@ __device__ void wave_shard(const DevTable& T, const ShardCtx& S, const Target& t
 // small loads in flight per lane and read the batch at ~2 TB/s, 10.6 us per 1M with nothing in reach), the in-reach
 // ones are compacted (at N ranks a shard reaches ~1/N of the batch), then answered BLOCK at a time: the window line of
 // the count's set for queries far enough inside the shard, the wave path on the global window for the rest.
-// Complete rows of 256-query block k go to region k % 8 of home rank home_of_block(k) (one atomic per 256-query
-// block that has rows, as before), so a region's capacity bound is unchanged.
-constexpr uint32_t SHARD_QB = 4 * BLOCK;
-
+// Complete rows of the workgroup's queries go to region (workgroup index) % 8 of their home rank home_of_block(k):
+// one atomic per workgroup and home rank (usually one per workgroup).
 template <int LK>
 __global__ __launch_bounds__(BLOCK) void rt_shard_kernel(DevTable T, ShardCtx S, const uint8_t* __restrict__ targets,
                                                          uint32_t q, uint32_t count, uint32_t aligned16, uint32_t abl) {
@@ -3476,8 +3476,6 @@ __global__ __launch_bounds__(BLOCK) void rt_shard_kernel(DevTable T, ShardCtx S,
     // the queries within the shard's reach, compacted: thread tid tests queries tid + r * BLOCK, one block scan of
     // the per-thread counts places them (the order is free: rows carry their qid)
     uint32_t nnear;  // (block-uniform)
-    uint32_t pf = 0;  // prefetch: a load of each line query's window line, issued here so that the line is in the
-                      // L2 when the compaction has moved the query to its lane (its value is never used)
     {
         uint32_t nm = 0;
 #pragma unroll
@@ -3487,14 +3485,7 @@ __global__ __launch_bounds__(BLOCK) void rt_shard_kernel(DevTable T, ShardCtx S,
                 Target th;
                 th.hi = ((uint64_t)__builtin_bswap32(st[5 * j]) << 32) | __builtin_bswap32(st[5 * j + 1]);
                 const uint32_t b = shard_bucket(S, th);
-                const bool in = b >= S.reach_lo && b < S.reach_hi;
-                nm |= (in ? 1u : 0u) << r;
-                if (LK && in && b >= S.s_lo + MARGIN && b + MARGIN <= S.s_hi && !abl) {
-                    const size_t bl = b - S.s_lo;
-                    if constexpr (LK == 8) pf ^= (T.flags & TF_WS) ? T.ws[4 * bl].x : T.wl[8 * bl].x;
-                    else if constexpr (LK == 16) pf ^= T.wl16[(WL16_STRIDE / 4) * bl].x;
-                    else pf ^= T.wl32[(WL32_STRIDE / 4) * bl].x ^ T.wl32[(WL32_STRIDE / 4) * bl + 8].x;
-                }
+                nm |= (b >= S.reach_lo && b < S.reach_hi ? 1u : 0u) << r;
             }
         }
         const uint32_t c = (uint32_t)__builtin_popcount(nm);
@@ -3517,90 +3508,86 @@ __global__ __launch_bounds__(BLOCK) void rt_shard_kernel(DevTable T, ShardCtx S,
             if (nm >> r & 1u) cq[pos++] = (uint16_t)(r * BLOCK + tid);
         __syncthreads();
     }
-    // the compacted queries, QN at a time (block-uniform loop): one lane per query, or for count 17..32 four lanes per
-    // query on the 256-byte line (rt_wl32q_kernel's form, ~60 VGPRs instead of ~150, so the load phase above keeps
-    // four workgroups per CU)
-    constexpr bool QUAD = LK == 32;
-    constexpr uint32_t QN = QUAD ? BLOCK / 4 : BLOCK;
-    const uint32_t p = QUAD ? tid & 3u : 0u;
-    for (uint32_t c0 = 0; c0 < nnear; c0 += QN) {
-        const uint32_t k = c0 + (QUAD ? tid >> 2 : tid);
+    // the compacted queries, BLOCK at a time (block-uniform loop)
+    for (uint32_t c0 = 0; c0 < nnear; c0 += BLOCK) {
+        const uint32_t k = c0 + tid;
         const bool act = k < nnear;
         const uint32_t j = act ? cq[k] : 0u;
         Target t{};
         uint32_t b = 0, i = 0;
         if (act) {
-            const uint32_t* sp = st + 5 * j;
-            t.hi = ((uint64_t)__builtin_bswap32(sp[0]) << 32) | __builtin_bswap32(sp[1]);
-            t.t2 = __builtin_bswap32(sp[2]);
-            t.t3 = __builtin_bswap32(sp[3]);
-            t.t4 = __builtin_bswap32(sp[4]);
+            const uint32_t* p = st + 5 * j;
+            t.hi = ((uint64_t)__builtin_bswap32(p[0]) << 32) | __builtin_bswap32(p[1]);
+            t.t2 = __builtin_bswap32(p[2]);
+            t.t3 = __builtin_bswap32(p[3]);
+            t.t4 = __builtin_bswap32(p[4]);
             b = shard_bucket(S, t);
             i = (uint32_t)base + j;
         }
         const bool line = LK && act && b >= S.s_lo + MARGIN && b + MARGIN <= S.s_hi && !(abl & 2);
-        const bool lead = !QUAD || p == 0;  // the lane that reserves, stores the header and takes the wave path
-        bool edge = act && lead && !(abl & 3);
+        bool edge = act && !(abl & 3);
         if (LK && __syncthreads_or(line)) {  // block-uniform
             // the row slots are reserved before the lines are read (one atomic per 256-query block sb with line
             // queries in this round: its rows go to region sb % 8 of its home rank), so the atomic's round trip
-            // overlaps the line loads; a query its line cannot answer leaves a tombstone row (qid KAD_NO_NODE,
-            // skipped by the finish) and takes the wave path
+            // overlaps the line loads; a query its line cannot answer leaves a tombstone row (qid KAD_NO_NODE, skipped
+            // by the finish) and takes the wave path
             const uint32_t sb = act ? j / BLOCK : 0u;
             uint32_t slot = 0;
 #pragma unroll
             for (uint32_t r = 0; r < SHARD_QB / BLOCK; r++) {
-                const uint64_t mb = __ballot(line && lead && sb == r);
+                const uint64_t mb = __ballot(line && sb == r);
                 if (lane == 0) wcnt[r][w] = (uint32_t)__builtin_popcountll(mb);
-                if (line && lead && sb == r) slot = lanes_below(mb);
+                if (line && sb == r) slot = lanes_below(mb);
             }
             __syncthreads();
-            if (tid < SHARD_QB / BLOCK) {
-                uint32_t tot = 0;
-                for (uint32_t x = 0; x < BLOCK / 64; x++) tot += wcnt[tid][x];
-                const uint32_t kb = (uint32_t)(base / BLOCK) + tid;
-                const uint64_t dof = S.dests > 1 ? (uint64_t)home_of_block(kb, S.dests, S.nblk) * S.dest_words : 0ull;
-                qbase_slot[tid] = tot ? atomicAdd(S.ctr + dof + KAD_SHARD_COUNTER_STRIDE * (kb & 7u), tot) : 0u;
+            if (tid == 0) {  // one atomic per home rank among the workgroup's four 256-query blocks (usually one)
+                uint32_t tot[SHARD_QB / BLOCK], hm[SHARD_QB / BLOCK];
+#pragma unroll
+                for (uint32_t r = 0; r < SHARD_QB / BLOCK; r++) {
+                    tot[r] = 0;
+                    for (uint32_t x = 0; x < BLOCK / 64; x++) tot[r] += wcnt[r][x];
+                    hm[r] = S.dests > 1 ? home_of_block((uint32_t)(base / BLOCK) + r, S.dests, S.nblk) : 0u;
+                }
+                uint32_t acc = 0;
+#pragma unroll
+                for (uint32_t r = 0; r < SHARD_QB / BLOCK; r++) {
+                    if (r == 0 || hm[r] != hm[r - 1]) {  // (homes ascend with the block)
+                        uint32_t run = 0;
+                        for (uint32_t y = r; y < SHARD_QB / BLOCK; y++) run += hm[y] == hm[r] ? tot[y] : 0u;
+                        acc = run ? atomicAdd(S.ctr + (uint64_t)hm[r] * S.dest_words + KAD_SHARD_COUNTER_STRIDE *
+                                              (blockIdx.x & 7u), run) : 0u;
+                    }
+                    qbase_slot[r] = acc;
+                    acc += tot[r];
+                }
             }
-            uint32_t o[QUAD ? 16 : (LK ? LK : 1)], m = 0;
+            uint32_t o[LK ? LK : 1], m = 0;
             bool ok = false;
             if (__any(line)) {  // (a wave of idle lanes skips the line work)
                 const uint32_t bl = line ? b - S.s_lo : 0u;
-                if constexpr (LK == 8) {
-                    ok = line8_answer(T, t, bl, count, line, line && (T.flags & TF_WS), o, m);
-                } else if constexpr (LK == 16) {
-                    ok = wl16_answer(T, t, bl, count, line, o, m);
-                } else if constexpr (QUAD) {
-                    uint32_t v[16], bs;
-                    ok = wl32_answer4<true, false>(T, t, bl, count, line, p, v, m, bs);
-                    quad_row(v, 16u * (p & 1u), bs + T.index_base, m, count, line && ok, o);
-                }
+                if constexpr (LK == 8) ok = line8_answer(T, t, bl, count, line, line && (T.flags & TF_WS), o, m);
+                else if constexpr (LK == 16) ok = wl16_answer(T, t, bl, count, line, o, m);
+                else if constexpr (LK == 32) ok = wl32_answer(T, t, bl, count, line, o, m);
                 ok = ok && line;
             }
             __syncthreads();
             if (line) {
-                if (QUAD) slot = (uint32_t)__shfl((int)slot, (int)(lane & ~3u), 64);
                 for (uint32_t x = 0; x < w; x++) slot += wcnt[sb][x];
                 slot += qbase_slot[sb];
                 const uint32_t kb = (uint32_t)(base / BLOCK) + sb;
                 const uint64_t dof = S.dests > 1 ? (uint64_t)home_of_block(kb, S.dests, S.nblk) * S.dest_words : 0ull;
                 if (slot < S.row_cap) {
-                    uint32_t* row = S.rows + dof + ((size_t)(kb & 7u) * S.row_cap + slot) * S.rs;
+                    uint32_t* row = S.rows + dof + ((size_t)(blockIdx.x & 7u) * S.row_cap + slot) * S.rs;
                     if (ok) {
-                        if (lead) reinterpret_cast<uint4*>(row)[0] = make_uint4(i, m, 0u, 0u);
+                        reinterpret_cast<uint4*>(row)[0] = make_uint4(i, m, 0u, 0u);
                         if constexpr (LK == 8) store_row8(row + 4, o, count);
                         else if constexpr (LK == 16) store_row16(row + 4, o, count);
-                        else if constexpr (QUAD) {
-                            if (p < 2u)
-#pragma unroll
-                                for (int e = 0; e < 16; e++)
-                                    if (16u * p + e < count) row[4 + 16 * p + e] = o[e];
-                        }
+                        else if constexpr (LK == 32) store_row32(row + 4, o, count);
                         edge = false;
-                    } else if (lead) {
+                    } else {
                         reinterpret_cast<uint4*>(row)[0] = make_uint4(NONE, 0u, 0u, 0u);  // tombstone
                     }
-                } else if (lead) {
+                } else {
                     atomicOr(S.ctr + dof + KAD_SHARD_COUNTER_STRIDE * 9u, 1u);
                 }
             }
@@ -3616,7 +3603,6 @@ __global__ __launch_bounds__(BLOCK) void rt_shard_kernel(DevTable T, ShardCtx S,
             wave_shard(T, S, u, rdl(i, l), count, xs[w]);
         }
     }
-    if (pf == 0x5EEDF00Du && abl == 0xFFFFFFFFu) st[tid] = pf;  // (never: keeps the prefetch loads)
 }
 
 // Gathered complete rows -> out rows. Block r of n_blocks holds n_rows[r] rows of `stride` words at

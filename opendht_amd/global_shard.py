@@ -105,10 +105,11 @@ class Exchange:
         self.collective = world > 1 if collective is None else bool(collective)
         nblk = -(-q // 256)
         if home:
-            # region k % 8 of a home range of ceil(nblk / world) query blocks, two rows per query at most (a line
-            # query its line cannot answer leaves a tombstone row, then its wave-path row): this capacity can never
-            # overflow
-            self.row_cap_max = 2 * -(-(-(-nblk // world)) // REGIONS) * 256
+            # region w % 8 of the workgroups (1,024 queries) holding a home range's queries, two rows per query at
+            # most (a line query its line cannot answer leaves a tombstone row, then its wave-path row): this
+            # capacity can never overflow
+            wg = -(-(-(-nblk // world)) // 4) + 1  # workgroups of 1,024 queries touching a home range
+            self.row_cap_max = 2 * -(-wg // REGIONS) * 1024
             # uniform targets: a region holds the home range's blocks k with k % 8 == region (ceil(hb / 8) of
             # them), a source shard answers ~1/world of each block's 256 queries
             hb = -(-nblk // world)
@@ -116,7 +117,8 @@ class Exchange:
             est = exp + 6 * int(np.sqrt(exp)) + 32
             part_def = 256
         else:
-            self.row_cap_max = 2 * -(-nblk // REGIONS) * 256  # rows of query block k go to region k % 8 (tombstones)
+            # rows of workgroup w (1,024 queries) go to region w % 8 (two per query at most: tombstones)
+            self.row_cap_max = 2 * -(-(-(-nblk // 4)) // REGIONS) * 1024
             est = -(-q // (REGIONS * world)) * 5 // 4 + 256  # ~q / world rows per rank
             part_def = 1024
         self.row_cap = max(1, min(self.row_cap_max, row_cap or est))
