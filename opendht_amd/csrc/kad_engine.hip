@@ -3445,7 +3445,8 @@ template <int LK>
 __global__ __launch_bounds__(BLOCK) void rt_shard_kernel(DevTable T, ShardCtx S, const uint8_t* __restrict__ targets,
                                                          uint32_t q, uint32_t count, uint32_t aligned16, uint32_t abl) {
     // abl (tools build only, KAD_SHARD_ABL; results wrong on purpose): 1 = no wave path (edge queries dropped),
-    // 2 = no line work either (the load and the reach compaction alone)
+    // 2 = no line work either (the load and the reach compaction alone), 4 = plain (not non-temporal) target loads,
+    // 8 = the target load alone
     constexpr uint32_t MARGIN = LK == 8 ? 4u : LK == 16 ? 8u : 16u;
     __shared__ __attribute__((aligned(16))) uint32_t st[SHARD_QB * 5];  // the block's targets, as stored (20 KB)
     __shared__ uint16_t cq[SHARD_QB];                                   // in-reach queries (block-local index)
@@ -3463,16 +3464,28 @@ __global__ __launch_bounds__(BLOCK) void rt_shard_kernel(DevTable T, ShardCtx S,
             const uint32_t n4 = nw / 4;
             const u32x4_t* s4 = reinterpret_cast<const u32x4_t*>(src);
             u32x4_t* d4 = reinterpret_cast<u32x4_t*>(st);
+            if (abl & 4) {
 #pragma unroll
-            for (uint32_t k = 0; k < 5; k++) {
-                const uint32_t x = tid + k * BLOCK;
-                if (x < n4) d4[x] = __builtin_nontemporal_load(s4 + x);
+                for (uint32_t k = 0; k < 5; k++) {
+                    const uint32_t x = tid + k * BLOCK;
+                    if (x < n4) d4[x] = s4[x];
+                }
+            } else {
+#pragma unroll
+                for (uint32_t k = 0; k < 5; k++) {
+                    const uint32_t x = tid + k * BLOCK;
+                    if (x < n4) d4[x] = __builtin_nontemporal_load(s4 + x);
+                }
             }
             o = 4 * n4;
         }
         for (uint32_t x = o + tid; x < nw; x += BLOCK) st[x] = __builtin_nontemporal_load(src + x);
     }
     __syncthreads();
+    if (abl & 8) {
+        if (st[tid] == 0x5EEDF00Du && st[tid + 1] == 0x5EEDF00Du) S.ctr[KAD_SHARD_COUNTER_STRIDE * 9u] = 1u;  // (keeps the load)
+        return;
+    }
     // the queries within the shard's reach, compacted: thread tid tests queries tid + r * BLOCK, one block scan of
     // the per-thread counts places them (the order is free: rows carry their qid)
     uint32_t nnear;  // (block-uniform)

@@ -1,6 +1,7 @@
 """Where the north-star shard kernel's time goes (round 5): rank 0 of 8 of the 100M-node table, the replicated 1M
 batch, k = 8 and 32, run on the tools build (libkadgpu_abl.so) with KAD_SHARD_ABL = 0 (the product kernel), 1 (no
-wave path: the edge queries dropped) and 2 (no line work either: the target load and the reach compaction alone).
+wave path: the edge queries dropped), 2 (no line work either: the target load and the reach compaction alone), 6 (2
+with plain target loads), 8 (the target load alone), 12 (8 with plain loads).
 Results are wrong on purpose for 1 and 2. Run under rocprofv3 --kernel-trace for the kernel durations; prints the
 event times as JSON."""
 import json
@@ -33,7 +34,7 @@ tgs = [torch.randint(0, 256, (Q, 20), dtype=torch.uint8, device=dev, generator=g
 res = {}
 for k in (8, 32):
     ex = G0.exchange(Q, k, 8)
-    for abl in ("0", "1", "2"):
+    for abl in (("0", "1", "2", "6", "8", "12") if k == 8 else ("0", "1", "2")):
         os.environ["KAD_SHARD_ABL"] = abl
         ts = []
         for j in range(REPS):
