@@ -4,10 +4,9 @@
 // front end that spreads lookups over N shard GPUs must send each target to its owner and the rows back. Device-only
 // pieces of that exchange, so that it needs no host read per batch:
 //   route_pack_kernel   targets -> `world` fixed-size send blocks (the owner's block), each query's place recorded;
-//                       a workgroup's 1,024 targets come in as coalesced 16-byte loads into LDS, are grouped by owner
-//                       there (one LDS atomic per wave and owner; one global atomic per workgroup and owner) and leave
-//                       as contiguous dword runs; a full block sets a sticky overflow word (the caller grows the
-//                       blocks and runs the batch again)
+//                       per-workgroup counts in LDS (one LDS atomic per wave and owner), one global atomic per
+//                       (workgroup, owner); a full block sets a sticky overflow word (the caller grows the blocks
+//                       and runs the batch again)
 //   route_unpack_kernel rows that came back in the send layout -> each query's original position
 // The blocks travel with all_to_all_single (RCCL over xGMI), equal splits: opendht_amd/sharded.py OwnerRoute.
 #include <hip/hip_runtime.h>
@@ -28,43 +27,27 @@ constexpr uint32_t NONE = 0xFFFFFFFFu;
 __global__ __launch_bounds__(BLOCK) void route_pack_kernel(const uint8_t* __restrict__ targets, uint32_t q,
                                                             uint32_t world, uint32_t shard_bits, uint32_t cap,
                                                             uint8_t* __restrict__ send, uint32_t* __restrict__ slot,
-                                                            uint32_t* __restrict__ ctr, uint32_t aligned16) {
-    constexpr uint32_t QB = BLOCK * QPT;
-    __shared__ __attribute__((aligned(16))) uint32_t st[QB * 5];  // the workgroup's targets, as stored (20 KB)
-    __shared__ __attribute__((aligned(16))) uint32_t ob[QB * 5];  // the same records grouped by owner
-    __shared__ uint32_t hcnt[KAD_ROUTE_MAX_WORLD], hbase[KAD_ROUTE_MAX_WORLD], lpre[KAD_ROUTE_MAX_WORLD + 1];
-    const uint32_t tid = threadIdx.x, lane = tid & 63u;
+                                                            uint32_t* __restrict__ ctr) {
+    __shared__ uint32_t hcnt[KAD_ROUTE_MAX_WORLD], hbase[KAD_ROUTE_MAX_WORLD];
+    const uint32_t tid = threadIdx.x;
     if (tid < KAD_ROUTE_MAX_WORLD) hcnt[tid] = 0;
-    const uint64_t base = (uint64_t)blockIdx.x * QB;
-    const uint32_t nq = (uint32_t)min<uint64_t>(QB, q - base), nw = 5 * nq;
-    {  // coalesced 16-byte loads of the 20 * nq bytes (5 * base dwords is a multiple of 4)
-        const uint32_t* src = reinterpret_cast<const uint32_t*>(targets) + 5 * base;
-        uint32_t o = 0;
-        if (aligned16) {
-            const uint32_t n4 = nw / 4;
-            typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-            const u32x4* s4 = reinterpret_cast<const u32x4*>(src);
-            u32x4* d4 = reinterpret_cast<u32x4*>(st);
-#pragma unroll
-            for (uint32_t k = 0; k < 5; k++) {
-                const uint32_t x = tid + k * BLOCK;
-                if (x < n4) d4[x] = __builtin_nontemporal_load(s4 + x);
-            }
-            o = 4 * n4;
-        }
-        for (uint32_t x = o + tid; x < nw; x += BLOCK) st[x] = __builtin_nontemporal_load(src + x);
-    }
     __syncthreads();
-    // owners and places: one LDS atomic per (wave, owner), the wave's lanes of one owner at consecutive places
-    uint32_t dst[QPT], pos[QPT];
+    uint32_t w[QPT][5], dst[QPT], pos[QPT];
+    const uint64_t base = (uint64_t)blockIdx.x * BLOCK * QPT;
 #pragma unroll
     for (uint32_t r = 0; r < QPT; r++) {
-        const uint32_t j = r * BLOCK + tid;
+        const uint64_t i = base + r * BLOCK + tid;  // consecutive lanes, consecutive 20-byte records
         dst[r] = NONE;
-        if (j < nq) {
-            const uint32_t b0 = st[5 * j] & 0xFFu;  // InfoHash byte 0: the most significant
+        if (i < q) {
+            const uint32_t* p = reinterpret_cast<const uint32_t*>(targets + 20 * i);
+#pragma unroll
+            for (int x = 0; x < 5; x++) w[r][x] = __builtin_nontemporal_load(p + x);
+            const uint32_t b0 = w[r][0] & 0xFFu;  // InfoHash byte 0: the most significant
             dst[r] = shard_bits ? (b0 >> (8 - shard_bits)) % world : 0u;
         }
+        // places in the workgroup's count of each owner: one LDS atomic per (wave, owner), the wave's lanes of
+        // one owner at consecutive places (their records then leave as contiguous runs)
+        const uint32_t lane = tid & 63u;
         for (uint32_t d = 0; d < world; d++) {  // (wave-uniform)
             const uint64_t m = __ballot(dst[r] == d);
             if (!m) continue;
@@ -78,33 +61,23 @@ __global__ __launch_bounds__(BLOCK) void route_pack_kernel(const uint8_t* __rest
     }
     __syncthreads();
     if (tid < world) hbase[tid] = hcnt[tid] ? atomicAdd(ctr + tid * KAD_ROUTE_CSTRIDE, hcnt[tid]) : 0u;
-    if (tid == 0) {
-        uint32_t a = 0;
-        for (uint32_t d = 0; d < world; d++) { lpre[d] = a; a += hcnt[d]; }
-        lpre[world] = a;
-    }
     __syncthreads();
-    // each record into its owner's group (LDS), each query's place
 #pragma unroll
     for (uint32_t r = 0; r < QPT; r++) {
-        const uint32_t j = r * BLOCK + tid;
+        const uint64_t i = base + r * BLOCK + tid;
         if (dst[r] == NONE) continue;
-        const uint32_t g = lpre[dst[r]] + pos[r];
-#pragma unroll
-        for (int x = 0; x < 5; x++) ob[5 * g + x] = st[5 * j + x];
         const uint32_t s = hbase[dst[r]] + pos[r];
-        __builtin_nontemporal_store(s < cap ? dst[r] * cap + s : NONE, slot + base + j);
+        uint32_t out = NONE;
+        if (s < cap) {
+            out = dst[r] * cap + s;
+            uint32_t* o = reinterpret_cast<uint32_t*>(send + 20ull * out);
+#pragma unroll
+            for (int x = 0; x < 5; x++) o[x] = w[r][x];
+        } else {
+            atomicOr(ctr + world * KAD_ROUTE_CSTRIDE, 1u);
+        }
+        __builtin_nontemporal_store(out, slot + i);
     }
-    __syncthreads();
-    // the groups leave as contiguous runs of dwords (consecutive lanes, consecutive addresses within a group)
-    for (uint32_t x = tid; x < nw; x += BLOCK) {
-        const uint32_t g = x / 5;
-        uint32_t d = 0;
-        for (uint32_t y = 1; y < world; y++) d = lpre[y] <= g ? y : d;
-        const uint32_t s = hbase[d] + (g - lpre[d]);
-        if (s < cap) reinterpret_cast<uint32_t*>(send)[5ull * ((uint64_t)d * cap + s) + x % 5] = ob[x];
-    }
-    if (tid < world && hbase[tid] + hcnt[tid] > cap) atomicOr(ctr + world * KAD_ROUTE_CSTRIDE, 1u);
 }
 
 // One thread per 16-byte piece of a row when count is a multiple of 4 (the common counts 8, 16, 32), else per
@@ -163,7 +136,7 @@ extern "C" int kad_route_pack(const uint8_t* targets, uint32_t q, uint32_t world
     if (e == hipSuccess && q) {
         const uint32_t nb = (uint32_t)(((uint64_t)q + BLOCK * QPT - 1) / (BLOCK * QPT));
         hipLaunchKernelGGL(route_pack_kernel, dim3(nb), dim3(BLOCK), 0, s, targets, q, world, shard_bits, cap, send,
-                           slot, ctr, ((uintptr_t)targets & 15u) == 0 ? 1u : 0u);
+                           slot, ctr);
         e = hipGetLastError();
     }
     if (e != hipSuccess) return set_error(KAD_ERR_HIP, hipGetErrorString(e));
