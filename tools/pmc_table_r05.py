@@ -26,8 +26,11 @@ KERNELS = [  # (label, mode, kernel-name substring, what)
     ("rt_sl", "lines", "rt_sl_kernel", "RoutingTable k=8, split-policy 4M nodes"),
     ("rt_sl16", "lines", "rt_sl16_kernel", "RoutingTable k=14, split-policy 4M nodes"),
     ("rt_gl32q", "lines", "rt_gl32q_kernel", "RoutingTable k=32, split-policy 4M nodes"),
-    ("rt_shard<8>", "shard", "rt_shard_kernel<8>", "north-star shard kernel, rank 0 of 8, k=8 (and the reach-0 / "
-                                                   "all-in-reach runs of the same kernel)"),
+    ("rt_shard<8> reach 0", "shard", "rt_shard_kernel<8>#0", "north-star shard kernel, a batch none of whose targets "
+                                                             "rank 0 can reach"),
+    ("rt_shard<8> all in reach", "shard", "rt_shard_kernel<8>#1", "north-star shard kernel, every target in reach "
+                                                                  "(world 1)"),
+    ("rt_shard<8>", "shard", "rt_shard_kernel<8>#2", "north-star shard kernel, rank 0 of 8, replicated batch, k=8"),
     ("rt_shard<32>", "shard", "rt_shard_kernel<32>", "north-star shard kernel, rank 0 of 8, k=32"),
     ("gather_scatter_link", "shard", "gather_scatter_link_kernel", "north-star finish over 8 blocks (k=8 and 32)"),
     ("gather_merge", "shard", "gather_merge_kernel", "north-star finish: part merge"),
@@ -39,23 +42,38 @@ KERNELS = [  # (label, mode, kernel-name substring, what)
 ]
 
 
+GROUP = 6  # tools/paths_pmc_r05.py runs REPS = 6 launches per case; "name#k" picks the k-th case of that kernel
+
+
+def _pick(sub):
+    name, _, k = sub.partition("#")
+    return name, (int(k) if k else None)
+
+
 def counters(pmc_dirs, mode, sub):
+    name, k = _pick(sub)
     per = defaultdict(lambda: defaultdict(float))
     for d in pmc_dirs:
         for f in glob.glob(os.path.join(d, f"pmc_{mode}", "**", "*counter_collection.csv"), recursive=True):
-            for r in csv.DictReader(open(f)):
-                if sub in r.get("Kernel_Name", ""):
+            rows = [r for r in csv.DictReader(open(f)) if name in r.get("Kernel_Name", "")]
+            ids = sorted({int(r["Dispatch_Id"]) for r in rows})
+            keep = set(ids[GROUP * k:GROUP * (k + 1)]) if k is not None else set(ids)
+            for r in rows:
+                if int(r["Dispatch_Id"]) in keep:
                     per[r["Counter_Name"]][(r["Dispatch_Id"], f)] += float(r["Counter_Value"])
     return {c: sum(v.values()) / len(v) for c, v in per.items() if v}
 
 
 def durations(pmc_dirs, mode, sub):
+    name, k = _pick(sub)
     out = []
     for d in pmc_dirs:
         for f in glob.glob(os.path.join(d, f"stats_{mode}", "*kernel_trace.csv")):
-            for r in csv.DictReader(open(f)):
-                if sub in r["Kernel_Name"]:
-                    out.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+            rows = [r for r in csv.DictReader(open(f)) if name in r["Kernel_Name"]]
+            rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+            if k is not None:
+                rows = rows[GROUP * k:GROUP * (k + 1)]
+            out += [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows]
     return out
 
 
