@@ -4888,13 +4888,16 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) v
                                                           const uint8_t* __restrict__ targets, uint32_t q,
                                                           uint32_t count, uint32_t* __restrict__ out_idx,
                                                           uint8_t* __restrict__ out_cnt) {
-    __shared__ uint32_t lds[BLOCK / 8][NC32_STRIDE + 4];
+    // the octets' rows of NC32_STRIDE + 4 dwords, with 8 dwords of padding before the first and 16 after the last: the
+    // run steps below read their elements at unclamped indices (-4 .. 138 of a row) and mask the ones outside
+    constexpr uint32_t NC32_ROW = NC32_STRIDE + 4;
+    __shared__ uint32_t ldsf[8 + (BLOCK / 8) * NC32_ROW + 16];
     const uint32_t lane = threadIdx.x & 63u, g = threadIdx.x & 7u;
     const uint32_t qi = (blockIdx.x * BLOCK + threadIdx.x) >> 3;
     const bool act = qi < q;
     const bool fam = DUAL && act && af[qi] != 0;
     const DevTable& T = fam ? T6 : T4;  // octet-uniform
-    uint32_t* W = lds[threadIdx.x >> 3];
+    uint32_t* W = ldsf + 8 + (threadIdx.x >> 3) * NC32_ROW;
     bool ok = false, line = false;
     uint64_t thi = 0;
     uint32_t s = 0;
@@ -4952,14 +4955,27 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) v
         // after every step inside, is never emitted (its expired bit is set), and (the outside steps are a suffix
         // of their run) the run maxima below pass it on only to other outside steps, so no step needs a validity
         // test after this.
+        // (all 16 elements read first at unclamped indices — one base per side and constant offsets — then masked:
+        // a clamped index per element had compiled to a branch and an LDS round trip per element)
         uint32_t ka[8], kb[8];
+        {
+            const uint32_t* Wa = W + 4 + (int)p - 1 - 8 * (int)g;   // element p-1-ra = Wa[-u]
+            const uint32_t* Wb = W + 4 + (int)p + 63 - 8 * (int)g;  // element p+rb = Wb[-u]
+            uint32_t xa[8], xb[8];
 #pragma unroll
-        for (int u = 0; u < 8; u++) {
-            const uint32_t ra = 8 * g + u, rb = 63 - 8 * g - u;
-            const bool va = ra < p, vb = p + rb < NC32_SLOTS;
-            const uint32_t xa = W[4 + (va ? p - 1 - ra : 0u)], xb = W[4 + (vb ? p + rb : 0u)];
-            ka[u] = va ? ((((xa >> 8) ^ t24) << 8) | (ra << 1) | (xa & 1u)) : NONE;
-            kb[u] = vb ? ((((xb >> 8) ^ t24) << 8) | 128u | (rb << 1) | (xb & 1u)) : NONE;
+            for (int u = 0; u < 8; u++) {
+                xa[u] = Wa[-u];
+                xb[u] = Wb[-u];
+            }
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                const uint32_t ra = 8 * g + u, rb = 63 - 8 * g - u;
+                const bool va = ra < p, vb = p + rb < NC32_SLOTS;
+                const uint32_t a = (((xa[u] >> 8) ^ t24) << 8) | (ra << 1) | (xa[u] & 1u);
+                const uint32_t b = (((xb[u] >> 8) ^ t24) << 8) | 128u | (rb << 1) | (xb[u] & 1u);
+                ka[u] = va ? a : NONE;
+                kb[u] = vb ? b : NONE;
+            }
         }
         // run maxima: in the lane (left: u ascending, right: u descending) over whole keys (their top 24 bits
         // are the distance maxima), then the runs' earlier lanes (left: lower g, right: higher g); a shuffle
@@ -5060,18 +5076,15 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) v
         ok = !ex && tot >= count;
         // the row through the octet's LDS row (the line is no longer read): entry `rank` at W[rank]
         __builtin_amdgcn_wave_barrier();
-        if (ok) {
+        if (ok) {  // (every step written: the ones not emitted into a dummy dword past the row's entries)
             uint32_t rank = cr - kept;
             const uint32_t bp = w0 + T.index_base + p;
 #pragma unroll
             for (int u = 0; u < 8; u++) {
-                if (keep[u]) {
-                    if (rank < count) {
-                        const uint32_t st = (w[u] >> 1) & 63u;
-                        W[rank] = (w[u] & 128u) ? bp + st : bp - 1u - st;
-                    }
-                    rank++;
-                }
+                const uint32_t st = (w[u] >> 1) & 63u;
+                const uint32_t val = (w[u] & 128u) ? bp + st : bp - 1u - st;
+                W[keep[u] && rank < count ? rank : NC32_ROW - 1] = val;
+                rank += keep[u] ? 1u : 0u;
             }
         }
         __builtin_amdgcn_wave_barrier();
