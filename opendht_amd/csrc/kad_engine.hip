@@ -109,6 +109,7 @@ struct DevTable {
     const uint4* sl;    // slot lines, count <= 8 (TF_SL, with TF_GL): 64 bytes per coarse radix slot
     const uint4* gl16;  // general window lines, counts 9..16 (TF_GL16): 128 bytes per bucket
     const uint4* sl16;  // slot lines, counts 9..16 (TF_SL16, with TF_SL): 128 bytes per coarse radix slot
+    const uint32_t* slb;  // (TF_SL) the bucket of every coarse radix slot, NONE where a bucket starts inside it
     uint32_t slshift, slslots;
     uint64_t rbase, nbase;
     uint32_t rshift, rslots, nshift, nslots;
@@ -215,6 +216,15 @@ __device__ __forceinline__ uint32_t locate_bucket(const DevTable& T, const Targe
         if (t.hi < T.rbase) return 0;
         const uint64_t s = (t.hi - T.rbase) >> T.rshift;
         return s >= T.B ? T.B - 1 : (uint32_t)s;
+    }
+    // tables with slot lines: the coarse slot's bucket, one load, unless a bucket starts inside the slot (~1 %); the
+    // radix below otherwise (one or two loads, and a search of the bucket firsts where a radix slot holds several)
+    if ((T.flags & TF_SL) && t.hi >= T.rbase) {
+        const uint64_t j = (t.hi - T.rbase) >> T.slshift;
+        if (j < T.slslots) {
+            const uint32_t b = T.slb[j];
+            if (b != NONE) return b;
+        }
     }
     uint32_t ub;
     if (t.hi < T.rbase) {
@@ -7290,6 +7300,7 @@ int setup_slot_lines(kad_table* t) {
     t->bytes += fb;
     t->sl_mut = lines; t->slb = slb; t->gdirty = gd;
     d.sl = reinterpret_cast<const uint4*>(lines);
+    d.slb = slb;
     d.slshift = d.rshift + k;
     d.slslots = slslots;
     d.flags |= TF_SL;
@@ -9694,7 +9705,8 @@ int kad_table_apply(kad_table* t, const uint32_t* ops, uint32_t n_ops, const uin
         release(t, t->gl32_mut); t->gl32_mut = nullptr; d.gl32 = nullptr; d.flags &= ~TF_GL32;
         release(t, t->gl16_mut); t->gl16_mut = nullptr; d.gl16 = nullptr; d.flags &= ~TF_GL16;
         release(t, t->sl_mut); release(t, t->slb); release(t, t->gdirty);
-        t->sl_mut = nullptr; t->slb = nullptr; t->gdirty = nullptr; d.sl = nullptr; d.slslots = 0; d.flags &= ~TF_SL;
+        t->sl_mut = nullptr; t->slb = nullptr; t->gdirty = nullptr; d.sl = nullptr; d.slb = nullptr; d.slslots = 0;
+        d.flags &= ~TF_SL;
         release(t, t->sl16_mut); t->sl16_mut = nullptr; d.sl16 = nullptr; d.flags &= ~TF_SL16;
     }
     release(t, const_cast<uint32_t*>(d.dmask));
