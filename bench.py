@@ -1246,6 +1246,27 @@ def allgather_pass(args, world, rank, local, dev, dist):
     return res
 
 
+def home0_recv(G0, ex, tg, Q, dev):
+    """The blocks rank 0 receives at N = 8, in shape: 8 blocks addressed to home 0, block c holding this shard's rows
+    of the home-0 queries i = c (mod 8) (their targets moved into this shard, every other target beyond its reach), so
+    that each home query is answered in exactly one block with the row volume of a uniform batch."""
+    import torch
+
+    ctr = ex.send.view(8, ex.block)[:, ex.ctr_off:ex.ctr_off + 10 * 32]
+    sel = torch.arange(Q, device=dev) % 8
+    blocks = []
+    for c in range(8):
+        t = tg.clone()
+        t[:, 0] = torch.where(sel == c, t[:, 0] & 0x1F, t[:, 0] | 0x80)
+        ctr.zero_()
+        G0.home_block(t, ex, zeroed=True)
+        blocks.append(ex.send[:ex.block].clone())
+    recv = torch.cat(blocks)
+    if bool((recv.view(8, ex.block)[:, ex.ctr_off + 9 * 32] != 0).any()):  # a block's sticky overflow word
+        raise RuntimeError("home-0 blocks overflowed their capacities")
+    return recv
+
+
 def n8_step_model(ids, st, off, gp, spec, tgs, Q, cnt_k, K, NB, dev, xchg_us):
     """Rank 0's kernels at N = 8 (see allgather_pass), HIP events around K eager launches each."""
     import torch
@@ -1288,8 +1309,7 @@ def n8_step_model(ids, st, off, gp, spec, tgs, Q, cnt_k, K, NB, dev, xchg_us):
             b.record(stream)
             torch.cuda.synchronize(dev)
             shard_zeroing_us = a.elapsed_time(b) / K * 1e3
-            blk = ex.send[:ex.block]
-            ex.recv = torch.cat([blk] * 8)
+            ex.recv = home0_recv(G0, ex, tgs[0], Q, dev)
             hi_q = -(-(-(-Q // 256)) // 8) * 256
             oi = torch.empty((min(hi_q, Q), k), dtype=torch.int32, device=dev)
             oc = torch.empty((min(hi_q, Q),), dtype=torch.uint8, device=dev)
@@ -1306,7 +1326,7 @@ def n8_step_model(ids, st, off, gp, spec, tgs, Q, cnt_k, K, NB, dev, xchg_us):
             out[f"k{k}"] = {"shard_kernel_us": shard_us, "shard_kernel_with_zeroing_launch_us": shard_zeroing_us,
                             "overflow": over, "finish_us": fin_us, "exchange_modelled_us": xm,
                             "step_modelled_us": step_us, "aggregate_queries_per_s_modelled": Q / (step_us * 1e-6)}
-            del ex, blk, oi, oc
+            del ex, oi, oc
         # the reach-0 floor: the same kernel on a batch none of whose targets this shard can reach (reading and
         # testing the batch is all it does)
         ex = G0.exchange(Q, cnt_k, 8, True, True)
@@ -1329,7 +1349,9 @@ def n8_step_model(ids, st, off, gp, spec, tgs, Q, cnt_k, K, NB, dev, xchg_us):
         out["how"] = ("rank 0 of 8 (global buckets [0, B/8), no halo) on this GPU: kad_rt_shard_step_home over the "
                       "whole replicated batch into 8 home blocks (HIP events around each launch, median; the "
                       "counters zeroed between launches outside them, as kad_rt_home_finish_reset leaves them), "
-                      "kad_rt_home_finish_reset over 8 blocks (copies of the block it sends itself: timing only); + "
+                      "kad_rt_home_finish_reset over 8 blocks addressed to home 0 (block c: this shard's rows of the "
+                      "home-0 queries i = c mod 8, so that every home query is answered once, as when 8 shards "
+                      "answer it); + "
                       "the modelled all_to_all at N = 8. The eight ranks answer the one batch together, so the "
                       "aggregate is Q / step")
         return out

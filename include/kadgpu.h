@@ -349,10 +349,11 @@ int kad_nc_closest_batch_dual(const kad_table* table4, const kad_table* table6,
  * counters (device, KAD_SHARD_COUNTERS x KAD_SHARD_COUNTER_STRIDE uint32, zeroed by the caller;
  * counter k at word k*KAD_SHARD_COUNTER_STRIDE): rows appended per region (k < 8), parts appended
  * (k = 8), overflow flag (k = 9: a region or the parts buffer was full: grow and run again).
- * Rows of the queries [1024 w, 1024 w + 1024) go to region w % 8. A query takes at most two rows: a query
- * whose window line cannot answer it leaves a tombstone row (qid KAD_NO_NODE, skipped by every finish) beside
- * its wave-path row or part, so row_cap >= 2*ceil(ceil(q/1024)/8)*1024 never overflows (home layout:
- * W = ceil(ceil(q/256)/world/4) + 1 workgroups per home range, row_cap >= 2*ceil(W/8)*1024).
+ * Rows of the queries [QB w, QB w + QB) go to region w % 8 (QB = 1024; 2048 in a tools-build A/B). A
+ * query takes at most two rows: a query whose window line cannot answer it leaves a tombstone row (qid
+ * KAD_NO_NODE, skipped by every finish) beside its wave-path row or part, so row_cap >= 2*ceil(ceil(q/QB)/8)*QB
+ * never overflows (home layout: W = ceil(ceil(q/256)/world/(QB/256)) + 1 workgroups per home range,
+ * row_cap >= 2*ceil(W/8)*QB).
  * The ranks' rows and parts are all-gathered by the caller (RCCL); kad_rt_scatter_rows and
  * kad_rt_merge_parts (parts sorted by qid) then give every query's findClosestNodes result.
  * All pointers are device pointers; count in 1..KAD_MAX_COUNT. Queries far enough inside the shard

@@ -3365,11 +3365,11 @@ __global__ __launch_bounds__(BLOCK) void rt_dual_wl32q_kernel(DevTable T4, DevTa
 // global one); the others take the wave-cooperative path on the global window.
 // Row layout (uint32): qid, m, 0, 0, idx[count] (padded to 4): KAD_ROW_WORDS(count).
 // Part layout: the row, then dist[count][5]: KAD_PART_WORDS(count).
-// Complete rows of workgroup w (SHARD_QB = 1,024 queries) go to region w % 8 of KAD_SHARD_REGIONS regions of
-// row_cap rows: one atomic per workgroup and home rank for the window-line rows, eight counters per home (a single
-// counter hit by every wave cost ~10 ns per wave, 160 us per 1M queries). A query takes at most two rows (a
-// tombstone and its wave-path row), so row_cap >= 2 * ceil(W / 8) * 1024 never overflows, W = the workgroups
-// holding a home range's queries (ceil(q / 1024) for one home; ceil(ceil(q / 256) / world / 4) + 1 per home).
+// Complete rows of workgroup w (QB = 1,024 or 2,048 queries, shard_qb) go to region w % 8 of KAD_SHARD_REGIONS
+// regions of row_cap rows: one atomic per workgroup and home rank for the window-line rows, eight counters per home
+// (a single counter hit by every wave cost ~10 ns per wave, 160 us per 1M queries). A query takes at most two rows (a
+// tombstone and its wave-path row), so row_cap >= 2 * ceil(W / 8) * QB never overflows, W = the workgroups holding
+// a home range's queries (ceil(q / QB) for one home; ceil(ceil(q / 256) / world / (QB / 256)) + 1 per home).
 // ---------------------------------------------------------------------------------------
 struct ShardCtx {
     const uint32_t* gpre;  // global good prefix sums, GB + 1
@@ -3406,11 +3406,15 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
-constexpr uint32_t SHARD_QB = 4 * BLOCK;  // queries per workgroup of rt_shard_kernel
+// Queries per workgroup of rt_shard_kernel<LK>: 1,024. (The count 17..32 kernel holds 193 VGPRs, two waves per SIMD,
+// so 1,024 workgroups of 1,024 take two rounds; 512 of 2,048 fit one round but measured the same at N = 8, 35.5
+// against 35.0 us, and 2,048 cost k = 8 / 16 5 / 4 us: tools/shard_abl_r05.py, KAD_SHARD_ABL=16, tools build.)
+__host__ __device__ constexpr uint32_t shard_qb(int) { return 4u * BLOCK; }
 
-// One query, wave-uniform: global window, intersection with the shard, wave_rank, append.
+// One query, wave-uniform: global window, intersection with the shard, wave_rank, append (complete rows to `region`,
+// the region of the query's workgroup, as its line rows').
 __device__ void wave_shard(const DevTable& T, const ShardCtx& S, const Target& t, uint32_t qid, uint32_t count,
-                           uint64_t* xs) {
+                           uint32_t region, uint64_t* xs) {
     const uint32_t lane = threadIdx.x & 63u;
     uint32_t lo, hi, good;
     wave_window_pre(S.gpre, S.GB, shard_bucket(S, t), count, lo, hi, good);
@@ -3420,7 +3424,6 @@ __device__ void wave_shard(const DevTable& T, const ShardCtx& S, const Target& t
     const uint32_t al = a - S.s_lo, el = e - S.s_lo;
     const uint32_t lgood = wave_good_sum(T.gcnt, al, el);
     uint32_t slot = 0;
-    const uint32_t region = (qid / SHARD_QB) & 7u;  // (the region of the query's workgroup, as its line rows')
     const uint64_t dof = dest_off(S, qid);
     uint32_t* ctr = S.ctr + dof;
     if (lane == 0) slot = atomicAdd(ctr + KAD_SHARD_COUNTER_STRIDE * (complete ? region : 8u), 1u);
@@ -3444,28 +3447,29 @@ __device__ void wave_shard(const DevTable& T, const ShardCtx& S, const Target& t
 // LK: the window-line set the shard's uniform table answers from (8: counts <= 8, 16: 9..16, 32: 17..32; 0: none).
 // A window of that set spans at most LK / 2 buckets on either side, so a query whose bucket lies that far inside the
 // shard has the same window locally as globally.
-// A workgroup takes SHARD_QB = 1,024 queries of the replicated batch: their 20 KB of targets come in as coalesced
-// 16-byte non-temporal loads into LDS (five per thread, all in flight at once: a lane-per-query form had only three
+// A workgroup takes QB = 1,024 (2,048) queries of the replicated batch: their 20 (40) KB of targets come in as coalesced
+// 16-byte non-temporal loads into LDS (five (ten) per thread, all in flight at once: a lane-per-query form had only three
 // small loads in flight per lane and read the batch at ~2 TB/s, 10.6 us per 1M with nothing in reach), the in-reach
 // ones are compacted (at N ranks a shard reaches ~1/N of the batch), then answered BLOCK at a time: the window line of
 // the count's set for queries far enough inside the shard, the wave path on the global window for the rest.
 // Complete rows of the workgroup's queries go to region (workgroup index) % 8 of their home rank home_of_block(k):
 // one atomic per workgroup and home rank (usually one per workgroup).
-template <int LK>
+template <int LK, uint32_t QB>
 __global__ __launch_bounds__(BLOCK) void rt_shard_kernel(DevTable T, ShardCtx S, const uint8_t* __restrict__ targets,
                                                          uint32_t q, uint32_t count, uint32_t aligned16, uint32_t abl) {
     // abl (tools build only, KAD_SHARD_ABL; results wrong on purpose): 1 = no wave path (edge queries dropped),
     // 2 = no line work either (the load and the reach compaction alone), 4 = plain (not non-temporal) target loads,
     // 8 = the target load alone
     constexpr uint32_t MARGIN = LK == 8 ? 4u : LK == 16 ? 8u : 16u;
-    __shared__ __attribute__((aligned(16))) uint32_t st[SHARD_QB * 5];  // the block's targets, as stored (20 KB)
-    __shared__ uint16_t cq[SHARD_QB];                                   // in-reach queries (block-local index)
+    constexpr uint32_t NR = QB / BLOCK;  // 256-query blocks per workgroup
+    __shared__ __attribute__((aligned(16))) uint32_t st[QB * 5];  // the block's targets, as stored
+    __shared__ uint16_t cq[QB];                                   // in-reach queries (block-local index)
     __shared__ uint32_t c_w[BLOCK / 64 + 1];
     __shared__ uint64_t xs[BLOCK / 64][192];
-    __shared__ uint32_t wcnt[SHARD_QB / BLOCK][BLOCK / 64], qbase_slot[SHARD_QB / BLOCK];
+    __shared__ uint32_t wcnt[NR][BLOCK / 64], qbase_slot[NR];
     const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
-    const uint64_t base = (uint64_t)blockIdx.x * SHARD_QB;
-    const uint32_t nq = (uint32_t)min<uint64_t>(SHARD_QB, q - base);
+    const uint64_t base = (uint64_t)blockIdx.x * QB;
+    const uint32_t nq = (uint32_t)min<uint64_t>(QB, q - base);
     {  // the block's 20 * nq bytes
         const uint32_t nw = 5 * nq;
         const uint32_t* src = reinterpret_cast<const uint32_t*>(targets) + 5 * base;
@@ -3476,13 +3480,13 @@ __global__ __launch_bounds__(BLOCK) void rt_shard_kernel(DevTable T, ShardCtx S,
             u32x4_t* d4 = reinterpret_cast<u32x4_t*>(st);
             if (abl & 4) {
 #pragma unroll
-                for (uint32_t k = 0; k < 5; k++) {
+                for (uint32_t k = 0; k < 5 * NR / 4; k++) {
                     const uint32_t x = tid + k * BLOCK;
                     if (x < n4) d4[x] = s4[x];
                 }
             } else {
 #pragma unroll
-                for (uint32_t k = 0; k < 5; k++) {
+                for (uint32_t k = 0; k < 5 * NR / 4; k++) {
                     const uint32_t x = tid + k * BLOCK;
                     if (x < n4) d4[x] = __builtin_nontemporal_load(s4 + x);
                 }
@@ -3502,7 +3506,7 @@ __global__ __launch_bounds__(BLOCK) void rt_shard_kernel(DevTable T, ShardCtx S,
     {
         uint32_t nm = 0;
 #pragma unroll
-        for (uint32_t r = 0; r < SHARD_QB / BLOCK; r++) {
+        for (uint32_t r = 0; r < NR; r++) {
             const uint32_t j = r * BLOCK + tid;
             if (j < nq) {
                 Target th;
@@ -3527,7 +3531,7 @@ __global__ __launch_bounds__(BLOCK) void rt_shard_kernel(DevTable T, ShardCtx S,
             nnear += c_w[k];
         }
 #pragma unroll
-        for (uint32_t r = 0; r < SHARD_QB / BLOCK; r++)
+        for (uint32_t r = 0; r < NR; r++)
             if (nm >> r & 1u) cq[pos++] = (uint16_t)(r * BLOCK + tid);
         __syncthreads();
     }
@@ -3557,26 +3561,26 @@ __global__ __launch_bounds__(BLOCK) void rt_shard_kernel(DevTable T, ShardCtx S,
             const uint32_t sb = act ? j / BLOCK : 0u;
             uint32_t slot = 0;
 #pragma unroll
-            for (uint32_t r = 0; r < SHARD_QB / BLOCK; r++) {
+            for (uint32_t r = 0; r < NR; r++) {
                 const uint64_t mb = __ballot(line && sb == r);
                 if (lane == 0) wcnt[r][w] = (uint32_t)__builtin_popcountll(mb);
                 if (line && sb == r) slot = lanes_below(mb);
             }
             __syncthreads();
             if (tid == 0) {  // one atomic per home rank among the workgroup's four 256-query blocks (usually one)
-                uint32_t tot[SHARD_QB / BLOCK], hm[SHARD_QB / BLOCK];
+                uint32_t tot[NR], hm[NR];
 #pragma unroll
-                for (uint32_t r = 0; r < SHARD_QB / BLOCK; r++) {
+                for (uint32_t r = 0; r < NR; r++) {
                     tot[r] = 0;
                     for (uint32_t x = 0; x < BLOCK / 64; x++) tot[r] += wcnt[r][x];
                     hm[r] = S.dests > 1 ? home_of_block((uint32_t)(base / BLOCK) + r, S.dests, S.nblk) : 0u;
                 }
                 uint32_t acc = 0;
 #pragma unroll
-                for (uint32_t r = 0; r < SHARD_QB / BLOCK; r++) {
+                for (uint32_t r = 0; r < NR; r++) {
                     if (r == 0 || hm[r] != hm[r - 1]) {  // (homes ascend with the block)
                         uint32_t run = 0;
-                        for (uint32_t y = r; y < SHARD_QB / BLOCK; y++) run += hm[y] == hm[r] ? tot[y] : 0u;
+                        for (uint32_t y = r; y < NR; y++) run += hm[y] == hm[r] ? tot[y] : 0u;
                         acc = run ? atomicAdd(S.ctr + (uint64_t)hm[r] * S.dest_words + KAD_SHARD_COUNTER_STRIDE *
                                               (blockIdx.x & 7u), run) : 0u;
                     }
@@ -3623,31 +3627,45 @@ __global__ __launch_bounds__(BLOCK) void rt_shard_kernel(DevTable T, ShardCtx S,
             u.t2 = rdl(t.t2, l);
             u.t3 = rdl(t.t3, l);
             u.t4 = rdl(t.t4, l);
-            wave_shard(T, S, u, rdl(i, l), count, xs[w]);
+            wave_shard(T, S, u, rdl(i, l), count, blockIdx.x & 7u, xs[w]);
         }
     }
 }
 
+// A complete row's `count` indices (at src + 4) copied to dst by `lpr` lanes: lane `sub` moves the row's 16-byte
+// pieces sub, sub + lpr, ... (counts that are multiples of 4, both ends 16-byte aligned), or its words sub, sub + lpr,
+// ... otherwise. A row of k = 32 leaves as eight lanes' 16-byte stores instead of one lane's 32 dword stores into
+// 64 different lines per instruction.
+__host__ __device__ constexpr uint32_t scatter_lpr(uint32_t count) {
+    return count <= 4 ? 1u : count <= 8 ? 2u : count <= 16 ? 4u : 8u;
+}
+
+__device__ __forceinline__ void copy_row(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst, uint32_t count,
+                                         uint32_t sub, uint32_t lpr) {
+    if ((count & 3u) == 0 && (((uintptr_t)(src + 4) | (uintptr_t)dst) & 15u) == 0) {
+        for (uint32_t j = 4 * sub; j < count; j += 4 * lpr)
+            *reinterpret_cast<uint4*>(dst + j) = *reinterpret_cast<const uint4*>(src + 4 + j);
+    } else {
+        for (uint32_t j = sub; j < count; j += lpr) dst[j] = src[4 + j];
+    }
+}
+
 // Gathered complete rows -> out rows. Block r of n_blocks holds n_rows[r] rows of `stride` words at
-// rows + r * block_cap * stride.
+// rows + r * block_cap * stride; scatter_lpr(count) lanes per row.
 __global__ void scatter_rows_kernel(const uint32_t* __restrict__ rows, const uint32_t* __restrict__ n_rows,
                                     uint32_t n_rows_stride, uint32_t n_blocks, uint32_t block_cap, uint32_t stride,
                                     uint32_t count,
                                     uint32_t* __restrict__ out_idx, uint8_t* __restrict__ out_cnt) {
-    const uint64_t g = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    const uint32_t lpr = scatter_lpr(count);
+    const uint64_t t = (uint64_t)blockIdx.x * BLOCK + threadIdx.x, g = t / lpr;
+    const uint32_t sub = (uint32_t)(t % lpr);
     const uint32_t r = (uint32_t)(g / block_cap), k = (uint32_t)(g % block_cap);
     if (r >= n_blocks || k >= min(n_rows[(size_t)r * n_rows_stride], block_cap)) return;
     const uint32_t* src = rows + ((size_t)r * block_cap + k) * stride;
     const uint32_t qid = src[0];
     if (qid == NONE) return;  // (a tombstone: the query's row comes from the wave path)
-    if (out_cnt) out_cnt[qid] = (uint8_t)src[1];
-    uint32_t* dst = out_idx + (size_t)qid * count;
-    if (count == 8 && ((uintptr_t)dst & 15u) == 0) {
-        reinterpret_cast<uint4*>(dst)[0] = reinterpret_cast<const uint4*>(src)[1];
-        reinterpret_cast<uint4*>(dst)[1] = reinterpret_cast<const uint4*>(src)[2];
-    } else {
-        for (uint32_t j = 0; j < count; j++) dst[j] = src[4 + j];
-    }
+    if (out_cnt && sub == 0) out_cnt[qid] = (uint8_t)src[1];
+    copy_row(src, out_idx + (size_t)qid * count, count, sub, lpr);
 }
 
 // Partial rows sorted by qid: the thread of a qid segment's first row merges the segment's sorted
@@ -3714,26 +3732,21 @@ __device__ __forceinline__ const uint32_t* gather_ctr(const GatherCtx& G, uint32
     return G.recv + (size_t)r * G.block + G.ctr_off;
 }
 
-__device__ __forceinline__ void gather_scatter(const GatherCtx& G, uint64_t g, uint32_t* __restrict__ out_idx,
+__device__ __forceinline__ void gather_scatter(const GatherCtx& G, uint64_t t, uint32_t* __restrict__ out_idx,
                                                uint8_t* __restrict__ out_cnt, uint32_t* __restrict__ overflow) {
-    const uint64_t per = (uint64_t)KAD_SHARD_REGIONS * G.row_cap;
+    const uint32_t lpr = scatter_lpr(G.count), sub = (uint32_t)(t % lpr);
+    const uint64_t g = t / lpr, per = (uint64_t)KAD_SHARD_REGIONS * G.row_cap;
     const uint32_t r = (uint32_t)(g / per);
     if (r >= G.world) return;
     const uint32_t rem = (uint32_t)(g % per), region = rem / G.row_cap, k = rem % G.row_cap;
     const uint32_t* ctr = gather_ctr(G, r);
-    if (rem == 0 && ctr[KAD_SHARD_COUNTER_STRIDE * 9u] && overflow) atomicOr(overflow, 1u);
+    if (rem == 0 && sub == 0 && ctr[KAD_SHARD_COUNTER_STRIDE * 9u] && overflow) atomicOr(overflow, 1u);
     if (k >= min(ctr[KAD_SHARD_COUNTER_STRIDE * region], G.row_cap)) return;
     const uint32_t* src = G.recv + (size_t)r * G.block + ((size_t)region * G.row_cap + k) * G.rs;
     const uint32_t qid = src[0] - G.qbase;
-    if (qid >= G.q) return;
-    if (out_cnt) out_cnt[qid] = (uint8_t)src[1];
-    uint32_t* dst = out_idx + (size_t)qid * G.count;
-    if (G.count == 8 && ((uintptr_t)dst & 15u) == 0) {
-        reinterpret_cast<uint4*>(dst)[0] = reinterpret_cast<const uint4*>(src)[1];
-        reinterpret_cast<uint4*>(dst)[1] = reinterpret_cast<const uint4*>(src)[2];
-    } else {
-        for (uint32_t j = 0; j < G.count; j++) dst[j] = src[4 + j];
-    }
+    if (qid >= G.q) return;  // (tombstones too: NONE - qbase >= q)
+    if (out_cnt && sub == 0) out_cnt[qid] = (uint8_t)src[1];
+    copy_row(src, out_idx + (size_t)qid * G.count, G.count, sub, lpr);
 }
 
 // The counters of `n` send blocks (block_words apart, the counters at ctr_off) zeroed before a step.
@@ -4977,14 +4990,17 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) v
                 xa[u] = Wa[-u];
                 xb[u] = Wb[-u];
             }
+            // an element is key24 << 8 | expired (bits 1..7 clear), so x ^ t24 << 8 is the distance key with its expired
+            // bit, and the step goes into bits 1..6 by an OR: ra << 1 = 16g | 2u, rb << 1 = 16(7 - g) | (14 - 2u).
+            // Valid: ra < p <=> u < p - 8g; p + rb < NC32_SLOTS <=> u > p - 61 - 8g (four ops per element)
+            const uint32_t T8 = t24 << 8, ga = 16u * g, gb = 128u | (16u * (7u - g));
+            const int dA = (int)p - 8 * (int)g, dB = (int)p - 61 - 8 * (int)g;
 #pragma unroll
             for (int u = 0; u < 8; u++) {
-                const uint32_t ra = 8 * g + u, rb = 63 - 8 * g - u;
-                const bool va = ra < p, vb = p + rb < NC32_SLOTS;
-                const uint32_t a = (((xa[u] >> 8) ^ t24) << 8) | (ra << 1) | (xa[u] & 1u);
-                const uint32_t b = (((xb[u] >> 8) ^ t24) << 8) | 128u | (rb << 1) | (xb[u] & 1u);
-                ka[u] = va ? a : NONE;
-                kb[u] = vb ? b : NONE;
+                const uint32_t a = (xa[u] ^ T8) | ga | (2u * u);
+                const uint32_t b = (xb[u] ^ T8) | gb | (14u - 2u * u);
+                ka[u] = u < dA ? a : NONE;
+                kb[u] = u > dB ? b : NONE;
             }
         }
         // run maxima: in the lane (left: u ascending, right: u descending) over whole keys (their top 24 bits
@@ -5012,7 +5028,8 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) v
             cb = max(cb, g + 4 <= 7 ? yb : 0u);
         }
         const uint32_t ua = oct_up<1>(ca), ub = oct_down<1>(cb);
-        const uint32_t inA = g > 0 ? ua : 0u, inB = g < 7 ? ub : 0u;
+        uint32_t inA = g > 0 ? ua : 0u, inB = g < 7 ? ub : 0u;
+        asm volatile("" : "+v"(inA), "+v"(inB));  // (kept as values: folded into each max, the select ran per element)
 #pragma unroll
         for (int u = 0; u < 8; u++) {  // the key's distance = the run maximum up to the step (bitfield insert)
             ka[u] = (max(pa[u], inA) & 0xFFFFFF00u) | (ka[u] & 255u);
@@ -5093,7 +5110,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) v
             for (int u = 0; u < 8; u++) {
                 const uint32_t st = (w[u] >> 1) & 63u;
                 const uint32_t val = (w[u] & 128u) ? bp + st : bp - 1u - st;
-                W[keep[u] && rank < count ? rank : NC32_ROW - 1] = val;
+                W[keep[u] ? rank : NC32_ROW - 1] = val;  // (rank < 64: entries past `count` are never read)
                 rank += keep[u] ? 1u : 0u;
             }
         }
@@ -8752,13 +8769,21 @@ static int shard_batch(const kad_table* t, const uint32_t* global_good_prefix, u
     const int lk = !uni ? 0 : count <= 8 ? 8 : count <= 16 ? ((fl & TF_WL16) ? 16 : 0) : ((fl & TF_WL32) ? 32 : 0);
     DeviceGuard g(t->device);
     void (*kern)(DevTable, ShardCtx, const uint8_t*, uint32_t, uint32_t, uint32_t, uint32_t) =
-        lk == 8 ? rt_shard_kernel<8> : lk == 16 ? rt_shard_kernel<16> : lk == 32 ? rt_shard_kernel<32> : rt_shard_kernel<0>;
+        lk == 8 ? rt_shard_kernel<8, shard_qb(8)> : lk == 16 ? rt_shard_kernel<16, shard_qb(16)>
+        : lk == 32 ? rt_shard_kernel<32, shard_qb(32)> : rt_shard_kernel<0, shard_qb(0)>;
+    uint32_t qb = shard_qb(lk);
     const uint32_t aligned16 = ((uintptr_t)targets & 15u) == 0;
     uint32_t abl = 0;
 #ifdef KAD_ABLATIONS
     if (const char* e = std::getenv("KAD_SHARD_ABL")) abl = (uint32_t)std::atoi(e);
+    if (abl & 16) {  // the other workgroup size (A/B)
+        qb = qb == 4u * BLOCK ? 8u * BLOCK : 4u * BLOCK;
+        kern = qb == 4u * BLOCK ? kern
+                                : (lk == 8 ? rt_shard_kernel<8, 8u * BLOCK> : lk == 16 ? rt_shard_kernel<16, 8u * BLOCK>
+                                   : lk == 32 ? rt_shard_kernel<32, 8u * BLOCK> : rt_shard_kernel<0, 8u * BLOCK>);
+    }
 #endif
-    hipLaunchKernelGGL(kern, dim3((uint32_t)(((uint64_t)q + SHARD_QB - 1) / SHARD_QB)), dim3(BLOCK), 0,
+    hipLaunchKernelGGL(kern, dim3((uint32_t)(((uint64_t)q + qb - 1) / qb)), dim3(BLOCK), 0,
                        (hipStream_t)stream, t->d, S, targets, q, count, aligned16, abl);
     HIP_TRY(hipGetLastError());
     return KAD_OK;
@@ -8828,7 +8853,7 @@ int kad_rt_scatter_rows(const uint32_t* rows, const uint32_t* n_rows, uint32_t n
     if (n_blocks == 0 || block_cap == 0) return KAD_OK;
     if (!rows || !n_rows || !out_idx) return set_err(KAD_ERR_INVALID, "NULL buffer");
     DeviceGuard g(device);
-    hipLaunchKernelGGL(scatter_rows_kernel, dim3(grid_for((uint64_t)n_blocks * block_cap)), dim3(BLOCK), 0,
+    hipLaunchKernelGGL(scatter_rows_kernel, dim3(grid_for((uint64_t)n_blocks * block_cap * scatter_lpr(count))), dim3(BLOCK), 0,
                        (hipStream_t)stream, rows, n_rows, n_rows_stride ? n_rows_stride : 1u, n_blocks, block_cap,
                        (uint32_t)KAD_ROW_WORDS(count), count,
                        out_idx, out_cnt);
@@ -8878,8 +8903,9 @@ static int gather_finish(const uint32_t* recv, uint32_t world, uint32_t row_cap,
     DeviceGuard g(device);
     hipStream_t s = (hipStream_t)stream;
     const uint64_t nrows = (uint64_t)world * KAD_SHARD_REGIONS * row_cap, nparts = (uint64_t)world * part_cap;
-    if (nrows > 0xFFFFFFFFull * BLOCK || nparts >= 0xFFFFFFFFull) return set_err(KAD_ERR_INVALID, "buffers too large");
-    const uint32_t sb = grid_for(nrows), lb = grid_for(nparts);
+    if (nrows * scatter_lpr(count) > 0xFFFFFFFFull * BLOCK || nparts >= 0xFFFFFFFFull)
+        return set_err(KAD_ERR_INVALID, "buffers too large");
+    const uint32_t sb = grid_for(nrows * scatter_lpr(count)), lb = grid_for(nparts);
     if ((uint64_t)sb + lb > 0x7FFFFFFFull) return set_err(KAD_ERR_INVALID, "buffers too large");
     hipLaunchKernelGGL(gather_scatter_link_kernel, dim3(sb + lb), dim3(BLOCK), 0, s, G, sb, out_idx, out_cnt, overflow,
                        head, next);

@@ -81,6 +81,24 @@ def home_range(q: int, world: int, rank: int) -> tuple[int, int]:
     return lo.value, hi.value
 
 
+SHARD_QB = (1024, 2048)  # queries per workgroup of rt_shard_kernel (csrc shard_qb: 1,024; 2,048 in a tools-build A/B)
+
+
+def region_queries(q: int, world: int, qb: int) -> int:
+    """The most queries of one home range (kad_home_range's split of 256-query blocks) that fall in one row region:
+    workgroup w of the shard kernel (qb queries) appends its rows to region w % REGIONS."""
+    nblk = -(-q // 256)
+    worst = 0
+    for d in range(world):
+        lo = -(-(d * nblk) // world) * 256
+        hi = min(q, -(-((d + 1) * nblk) // world) * 256)
+        per = [0] * REGIONS
+        for w in range(lo // qb, -(-hi // qb)):
+            per[w % REGIONS] += max(0, min(hi, (w + 1) * qb) - max(lo, w * qb))
+        worst = max(worst, max(per))
+    return worst
+
+
 class Exchange:
     """Fixed-size send / receive blocks of one step shape (q queries, count, world ranks).
 
@@ -105,20 +123,18 @@ class Exchange:
         self.collective = world > 1 if collective is None else bool(collective)
         nblk = -(-q // 256)
         if home:
-            # region w % 8 of the workgroups (1,024 queries) holding a home range's queries, two rows per query at
-            # most (a line query its line cannot answer leaves a tombstone row, then its wave-path row): this
-            # capacity can never overflow
-            wg = -(-(-(-nblk // world)) // 4) + 1  # workgroups of 1,024 queries touching a home range
-            self.row_cap_max = 2 * -(-wg // REGIONS) * 1024
-            # uniform targets: a region holds the home range's blocks k with k % 8 == region (ceil(hb / 8) of
-            # them), a source shard answers ~1/world of each block's 256 queries
-            hb = -(-nblk // world)
-            exp = -(-(-(-hb // REGIONS) * 256) // world)
+            # region w % 8 of the workgroups (QB = 1,024 or 2,048 queries, the shard kernel's shard_qb) holding a
+            # home range's queries, two rows per query at most (a line query its line cannot answer leaves a
+            # tombstone row, then its wave-path row): this capacity can never overflow, for either QB
+            worst = max(region_queries(q, world, qb) for qb in SHARD_QB)
+            self.row_cap_max = 2 * worst
+            # uniform targets: a source shard answers ~1/world of a region's queries
+            exp = -(-worst // world)
             est = exp + 6 * int(np.sqrt(exp)) + 32
             part_def = 256
         else:
-            # rows of workgroup w (1,024 queries) go to region w % 8 (two per query at most: tombstones)
-            self.row_cap_max = 2 * -(-(-(-nblk // 4)) // REGIONS) * 1024
+            # rows of workgroup w (QB queries) go to region w % 8 (two per query at most: tombstones)
+            self.row_cap_max = 2 * max(region_queries(q, 1, qb) for qb in SHARD_QB)
             est = -(-q // (REGIONS * world)) * 5 // 4 + 256  # ~q / world rows per rank
             part_def = 1024
         self.row_cap = max(1, min(self.row_cap_max, row_cap or est))

@@ -61,7 +61,7 @@ def _compact_path(shards, tg, count, gpu):
     rw, pw = row_words(count), part_words(count)
     rows, parts = [], []
     for sh in shards:
-        ex = Exchange(q, count, len(shards), gpu, row_cap=2 * -(-(-(-q // 1024)) // 8) * 1024, part_cap=max(4096, 8 * q),
+        ex = Exchange(q, count, len(shards), gpu, row_cap=2 * -(-(-(-q // 2048)) // 8) * 2048, part_cap=max(4096, 8 * q),
                       home=False)
         sh.local_block(tg, ex)
         c = ex.counters().cpu().numpy().reshape(-1, 32)[:, 0]

@@ -75,6 +75,7 @@ def mode_lines():
 
 
 def mode_shard():
+    import bench
     from opendht_amd.global_shard import GlobalShard, build_plain_shard
 
     spec = config3_spec(1)  # the whole 100M-node table, then rank 0's eighth of it (as bench.n8_step_model)
@@ -99,8 +100,7 @@ def mode_shard():
     for k in (8, 32):
         ex = G0.exchange(Q, k, 8)
         run(f"shard_k{k}_us", lambda t: G0.home_block(t, ex), tgs)
-        blk = ex.send[:ex.block]
-        ex.recv = torch.cat([blk] * 8)
+        ex.recv = bench.home0_recv(G0, ex, tgs[0], Q, dev)
         hq = -(-(-(-Q // 256)) // 8) * 256
         oi = torch.empty((hq, k), dtype=torch.int32, device=dev)
         oc = torch.empty((hq,), dtype=torch.uint8, device=dev)
