@@ -3422,11 +3422,14 @@ __device__ void wave_shard(const DevTable& T, const ShardCtx& S, const Target& t
     if (a >= e) return;
     const bool complete = lo >= S.s_lo && hi < S.s_hi;
     const uint32_t al = a - S.s_lo, el = e - S.s_lo;
-    const uint32_t lgood = wave_good_sum(T.gcnt, al, el);
+    // the window's node range, the row slot and (parts only) the local good count: independent round trips, issued
+    // together (a complete window's good count is the global one)
+    const uint32_t beg = T.dir[al].x & ~WIDE, end = T.dir[el].x & ~WIDE;
     uint32_t slot = 0;
     const uint64_t dof = dest_off(S, qid);
     uint32_t* ctr = S.ctr + dof;
     if (lane == 0) slot = atomicAdd(ctr + KAD_SHARD_COUNTER_STRIDE * (complete ? region : 8u), 1u);
+    const uint32_t lgood = complete ? good : wave_good_sum(T.gcnt, al, el);
     slot = rdl(slot, 0);
     if (slot >= (complete ? S.row_cap : S.part_cap)) {
         if (lane == 0) atomicOr(ctr + KAD_SHARD_COUNTER_STRIDE * 9u, 1u);
@@ -3440,8 +3443,7 @@ __device__ void wave_shard(const DevTable& T, const ShardCtx& S, const Target& t
         row[2] = 0;
         row[3] = 0;
     }
-    wave_rank(T, t, T.dir[al].x & ~WIDE, T.dir[el].x & ~WIDE, lgood, count, row + 4,
-              complete ? nullptr : row + (S.rs), xs);
+    wave_rank(T, t, beg, end, lgood, count, row + 4, complete ? nullptr : row + (S.rs), xs);
 }
 
 // LK: the window-line set the shard's uniform table answers from (8: counts <= 8, 16: 9..16, 32: 17..32; 0: none).
@@ -3782,8 +3784,97 @@ __global__ __launch_bounds__(BLOCK) void gather_scatter_link_kernel(GatherCtx G,
     next[x] = atomicExch(head + (part[0] - G.qbase), (uint32_t)x);
 }
 
-// The thread of a query's chain head merges its parts (at most one per rank, KAD_SHARD_MAX_WORLD) by
-// (XOR distance, global index), as merge_parts_kernel, and resets the head.
+// (a, ai) < (b, bi): 160-bit XOR distance, then global index
+__device__ __forceinline__ bool dist_idx_less(const uint32_t* a, uint32_t ai, const uint32_t* b, uint32_t bi) {
+#pragma unroll
+    for (int w = 0; w < 5; w++)
+        if (a[w] != b[w]) return a[w] < b[w];
+    return ai < bi;
+}
+
+// One query's parts (the chain from part xh: at most one per rank, KAD_SHARD_MAX_WORLD) merged by (XOR distance,
+// global index) by the whole wave (wave-uniform arguments). Up to 64 entries in all: lane e loads entry e (one round
+// of independent loads) and counts the entries before it, 6 words broadcast per entry; the row entry at that rank is
+// the lane's. More entries: lane 0 merges the sorted parts serially, as merge_parts_kernel.
+__device__ void wave_merge_chain(const GatherCtx& G, const uint32_t* __restrict__ next, uint32_t xh, uint32_t qid,
+                                 uint32_t* __restrict__ out_idx, uint8_t* __restrict__ out_cnt) {
+    constexpr uint32_t MAXSEG = KAD_SHARD_MAX_WORLD;
+    const uint32_t lane = threadIdx.x & 63u, count = G.count;
+    uint32_t ys = NONE, nseg = 0;  // lane s < nseg: part slot of segment s
+    for (uint32_t y = xh; y != NONE && nseg < MAXSEG; y = next[y]) {
+        if (lane == nseg) ys = y;
+        nseg++;
+    }
+    const uint32_t* myseg = lane < nseg ? gather_part(G, ys) : nullptr;
+    const uint32_t cnt = myseg ? myseg[1] : 0u;
+    uint32_t off = cnt;  // inclusive scan over the segments (nseg <= 16 lanes)
+#pragma unroll
+    for (int o = 1; o < (int)MAXSEG; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)off, o, 64);
+        if (lane >= (uint32_t)o) off += y;
+    }
+    const uint32_t total = rdl(off, MAXSEG - 1), m = min(count, total);
+    uint32_t* dst = out_idx + (size_t)qid * count;
+    if (total <= 64) {
+        // lane e: entry e of segment s (off[s-1] <= e < off[s])
+        uint32_t s = 0;
+        for (uint32_t k = 0; k + 1 < nseg; k++) s += rdl(off, k) <= lane ? 1u : 0u;
+        const bool has = lane < total;
+        const uintptr_t sp = (uintptr_t)myseg;  // (the shuffles run in every lane)
+        const uint32_t* sg = reinterpret_cast<const uint32_t*>(
+            (uintptr_t)(uint32_t)__shfl((int)(uint32_t)sp, (int)s, 64) |
+            ((uintptr_t)(uint32_t)__shfl((int)(uint32_t)(sp >> 32), (int)s, 64) << 32));
+        const uint32_t ofs = (uint32_t)__shfl((int)off, (int)(s ? s - 1 : 0), 64);
+        const uint32_t e = lane - (s ? ofs : 0u);
+        uint32_t d[5] = {0, 0, 0, 0, 0}, idx = NONE;
+        if (has) {
+            idx = sg[4 + e];
+#pragma unroll
+            for (int w = 0; w < 5; w++) d[w] = sg[G.rs + 5 * e + w];
+        }
+        uint32_t rank = 0;
+        for (uint32_t j = 0; j < total; j++) {
+            uint32_t b[5];
+#pragma unroll
+            for (int w = 0; w < 5; w++) b[w] = rdl(d[w], j);
+            rank += dist_idx_less(b, rdl(idx, j), d, idx) ? 1u : 0u;
+        }
+        if (has && rank < m) dst[rank] = idx;
+        if (lane >= m && lane < count) dst[lane] = NONE;
+        if (count > 64)
+            for (uint32_t p = 64 + lane; p < count; p += 64) dst[p] = NONE;
+    } else if (lane == 0) {
+        const uint32_t* seg[MAXSEG];
+        uint32_t at[MAXSEG];
+        {
+            uint32_t k = 0;
+            for (uint32_t y = xh; y != NONE && k < MAXSEG; y = next[y]) {
+                seg[k] = gather_part(G, y);
+                at[k++] = 0;
+            }
+        }
+        for (uint32_t p = 0; p < count; p++) {
+            if (p >= m) {
+                dst[p] = NONE;
+                continue;
+            }
+            uint32_t best = NONE;
+            for (uint32_t k = 0; k < nseg; k++) {
+                if (at[k] >= seg[k][1]) continue;
+                if (best == NONE ||
+                    dist_idx_less(seg[k] + G.rs + 5 * at[k], seg[k][4 + at[k]], seg[best] + G.rs + 5 * at[best],
+                                  seg[best][4 + at[best]]))
+                    best = k;
+            }
+            dst[p] = seg[best][4 + at[best]];
+            at[best]++;
+        }
+    }
+    if (lane == 0 && out_cnt) out_cnt[qid] = (uint8_t)m;
+}
+
+// The chain heads (the first part of each query's chain) merge their query's parts (wave_merge_chain) and reset the
+// head.
 __global__ void gather_merge_kernel(GatherCtx G, uint32_t* __restrict__ head, const uint32_t* __restrict__ next,
                                     uint32_t* __restrict__ out_idx, uint8_t* __restrict__ out_cnt, uint32_t mblocks,
                                     uint32_t* __restrict__ zsend) {
@@ -3794,40 +3885,15 @@ __global__ void gather_merge_kernel(GatherCtx G, uint32_t* __restrict__ head, co
     }
     const uint64_t x = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
     const uint32_t* part = gather_part(G, x);
-    if (!part) return;
-    const uint32_t qid = part[0] - G.qbase;
-    if (qid >= G.q || head[qid] != (uint32_t)x) return;
-    constexpr uint32_t MAXSEG = KAD_SHARD_MAX_WORLD;
-    const uint32_t* seg[MAXSEG];
-    uint32_t at[MAXSEG], nseg = 0, total = 0;
-    for (uint32_t y = (uint32_t)x; y != NONE && nseg < MAXSEG; y = next[y]) {
-        seg[nseg] = gather_part(G, y);
-        at[nseg] = 0;
-        total += seg[nseg][1];
-        nseg++;
+    const uint32_t qid = part ? part[0] - G.qbase : NONE;
+    const bool mine = part && qid < G.q && head[qid] == (uint32_t)x;
+    // the wave merges its chain heads one at a time, all 64 lanes on each (parts are rare: queries whose window
+    // crosses a shard edge)
+    for (uint64_t mm = __ballot(mine); mm; mm &= mm - 1) {
+        const uint32_t l = (uint32_t)__builtin_ctzll(mm);
+        wave_merge_chain(G, next, rdl((uint32_t)x, l), rdl(qid, l), out_idx, out_cnt);
     }
-    const uint32_t count = G.count, m = min(count, total);
-    uint32_t* dst = out_idx + (size_t)qid * count;
-    for (uint32_t p = 0; p < count; p++) {
-        if (p >= m) {
-            dst[p] = NONE;
-            continue;
-        }
-        uint32_t best = NONE;
-        for (uint32_t s = 0; s < nseg; s++) {
-            if (at[s] >= seg[s][1]) continue;
-            if (best == NONE) { best = s; continue; }
-            const uint32_t* da = seg[s] + G.rs + 5 * at[s];
-            const uint32_t* db = seg[best] + G.rs + 5 * at[best];
-            int c = 0;
-            for (int w = 0; w < 5 && c == 0; w++) c = da[w] < db[w] ? -1 : da[w] > db[w] ? 1 : 0;
-            if (c < 0 || (c == 0 && seg[s][4 + at[s]] < seg[best][4 + at[best]])) best = s;
-        }
-        dst[p] = seg[best][4 + at[best]];
-        at[best]++;
-    }
-    if (out_cnt) out_cnt[qid] = (uint8_t)m;
-    head[qid] = NONE;
+    if (mine) head[qid] = NONE;
 }
 
 // ---------------------------------------------------------------------------------------
