@@ -26,12 +26,12 @@ KERNELS = [  # (label, mode, kernel-name substring, what)
     ("rt_sl", "lines", "rt_sl_kernel", "RoutingTable k=8, split-policy 4M nodes"),
     ("rt_sl16", "lines", "rt_sl16_kernel", "RoutingTable k=14, split-policy 4M nodes"),
     ("rt_gl32q", "lines", "rt_gl32q_kernel", "RoutingTable k=32, split-policy 4M nodes"),
-    ("rt_shard<8> reach 0", "shard", "rt_shard_kernel<8>#0", "north-star shard kernel, a batch none of whose targets "
+    ("rt_shard<8> reach 0", "shard", "rt_shard_kernel<8,#0", "north-star shard kernel, a batch none of whose targets "
                                                              "rank 0 can reach"),
-    ("rt_shard<8> all in reach", "shard", "rt_shard_kernel<8>#1", "north-star shard kernel, every target in reach "
+    ("rt_shard<8> all in reach", "shard", "rt_shard_kernel<8,#1", "north-star shard kernel, every target in reach "
                                                                   "(world 1)"),
-    ("rt_shard<8>", "shard", "rt_shard_kernel<8>#2", "north-star shard kernel, rank 0 of 8, replicated batch, k=8"),
-    ("rt_shard<32>", "shard", "rt_shard_kernel<32>", "north-star shard kernel, rank 0 of 8, k=32"),
+    ("rt_shard<8>", "shard", "rt_shard_kernel<8,#2", "north-star shard kernel, rank 0 of 8, replicated batch, k=8"),
+    ("rt_shard<32>", "shard", "rt_shard_kernel<32,#0", "north-star shard kernel, rank 0 of 8, k=32"),
     ("gather_scatter_link", "shard", "gather_scatter_link_kernel", "north-star finish over 8 blocks (k=8 and 32)"),
     ("gather_merge", "shard", "gather_merge_kernel", "north-star finish: part merge"),
     ("search_query", "swarm", "search_query_kernel", "config 5 hop: queried peers' windows (2M peers, 256k lookups)"),
