@@ -191,6 +191,15 @@ def use_ablation_build() -> None:
     LIB_PATH = os.path.join(_HERE, "libkadgpu_abl.so")
 
 
+def use_library(path: str) -> None:
+    """Tools only (tools/nc32_ab.py): load a variant build of the engine (an A/B against the product library).
+    Must run before the first lib() call."""
+    global LIB_PATH
+    if _lib is not None:
+        raise RuntimeError("libkadgpu.so is already loaded")
+    LIB_PATH = os.path.abspath(path)
+
+
 def lib() -> C.CDLL:
     """Load libkadgpu.so, raising loudly (no fallback) if it is not built."""
     global _lib
