@@ -427,6 +427,8 @@ def main_owner(args):
     extras = {}
     if not args.no_extras:
         extras["cold"] = cold_pass(T, tgs, outs, ocnt, cnt_k, Q, moved_q, dev, stream)
+        # (before refresh_pass, which moves `now` and so the statuses the rows are checked against)
+        extras["owner_routed"] = owner_routed_pass(T, sh, spec, Q, cnt_k, K, W, dev, dist, world, rank)
         extras["refresh"] = refresh_pass(T, sh, tgs, outs, ocnt, cnt_k, Q, avg_kernel_s, dev, stream)
         extras["host_buffers"] = host_pass(T, tgs, cnt_k, Q, dev)
         extras["other_counts"] = counts_pass(T, tgs, Q, dev, stream)
@@ -522,6 +524,62 @@ def main_owner(args):
         dist.destroy_process_group()
 
 
+def owner_routed_pass(T, sh, spec, Q, cnt_k, K, W, dev, dist, world, rank, NB=4):
+    """The headline form as a serving front end, measured at this N: every rank holds Q arbitrary
+    targets per step (uniform over the N shards), routes each to its owner and gets the rows back
+    (sharded.OwnerRoute.step: kad_route_pack, all_to_all_single of the target blocks — RCCL over xGMI at N > 1 —,
+    the owner's kad_rt_closest_batch over the blocks it received, kad_route_compress, all_to_all_single of the packed
+    rows back, kad_route_unpack_packed). W + K eager steps (collectives are not captured), barrier + synchronize on both sides, the
+    max over ranks; a distinct batch per step (NB rotated). At N = 1 there is no exchange (the local pack / query /
+    unpack)."""
+    import torch
+
+    from opendht_amd.sharded import OwnerRoute
+
+    try:
+        g = torch.Generator(device=dev)
+        g.manual_seed(0x0D470600 + rank)
+        tgs = []
+        for _ in range(NB):
+            t = torch.randint(0, 256, (Q, 20), dtype=torch.uint8, device=dev, generator=g)
+            own = torch.randint(0, world, (Q,), dtype=torch.int32, device=dev, generator=g)
+            t[:, 0] = ((t[:, 0].to(torch.int32) & 0x1F) | (own << 5)).to(torch.uint8)
+            tgs.append(t)
+        s = torch.cuda.current_stream(dev).cuda_stream
+        R = OwnerRoute(Q, cnt_k, world, spec.shard_bits, dev)
+        oi = torch.empty((Q, cnt_k), dtype=torch.int32, device=dev)
+        oc = torch.empty((Q,), dtype=torch.uint8, device=dev)
+        for _ in range(6):  # block capacities: grow until a step fits (decided together over the ranks)
+            R.step(T, tgs[0], oi, oc, None, s)
+            if not R.overflowed():
+                break
+            R = R.grown()
+        t_max, ev_ms, how = graph_steps(lambda j: R.step(T, tgs[j % NB], oi, oc, None, s), K, W, dev, dist,
+                                        use_graph=False)
+        over = R.overflowed()
+        esc = R.escaped()  # (a row too wide to pack in some step: the last batch's way back again, unpacked)
+        last = tgs[(K - 1) % NB]
+        if esc:
+            R.back(oi, oc, None, s, packed=False)
+            torch.cuda.synchronize(dev)
+        # the rows of this rank's own targets in the last step, against the restatement on its shard table
+        vt = last[:65536].cpu().numpy()
+        mine = (vt[:, 0].astype(np.int64) >> (8 - spec.shard_bits)) == rank
+        bad = verify_rows(sh.ids, sh.status, sh.first, sh.off, sh.index_base, vt[mine],
+                          oi[:65536].cpu().numpy()[mine], oc[:65536].cpu().numpy()[mine], cnt_k)
+        xb = R.xgmi_bytes
+        return {"queries_per_s": world * Q * K / t_max, "ms_per_step": t_max / K * 1e3, "n_gpus": world,
+                "collective": "RCCL all_to_all_single" if world > 1 else None, "cap": R.cap, "overflow": over,
+                "rows_back": f"packed, {4 * R.pw} bytes per row" if R.packed else "plain", "escaped": esc,
+                "xgmi_bytes_per_rank_step": xb, "launch": how,
+                "verified": {"rows": sum_over_ranks(dist, int(mine.sum()), dev),
+                             "mismatches": sum_over_ranks(dist, bad, dev),
+                             "what": "each rank's own-shard targets among the first 65,536 of its last step"},
+                "how": owner_routed_pass.__doc__.split("\n\n")[0].replace("\n", " ")}
+    except Exception as e:  # the headline line is printed whatever happens here
+        return {"error": f"{type(e).__name__}: {e}"}
+
+
 def owner_step_model(T, Q, cnt_k, dev, stream, avg_kernel_s, link_gbs=64.0, lat_us=10.0, reps=20):
     """The headline form's multi-GPU data path priced: a serving front end holding Q arbitrary
     targets per rank at N = 2, 4, 8 routes each to the rank owning its shard and gets the rows back
@@ -530,7 +588,9 @@ def owner_step_model(T, Q, cnt_k, dev, stream, avg_kernel_s, link_gbs=64.0, lat_
     256), kad_route_unpack of the rows. Modelled: the two all_to_all_single exchanges, each rank sending one block
     to every other rank over its own xGMI link at link_gbs GB/s, lat_us per collective (targets: one; rows and
     counts: two). serial = pack + targets + query + rows + unpack; overlapped = the compute and the exchanges of
-    consecutive batches on two streams, max(pack + query + unpack, exchanges)."""
+    consecutive batches on two streams, max(pack + query + unpack, exchanges). `packed`: the same with the rows
+    back packed (kad_route_compress, one collective of KAD_ROUTE_PACKED_WORDS(k) words per row,
+    kad_route_unpack_packed)."""
     import torch
 
     from opendht_amd.sharded import OwnerRoute
@@ -565,17 +625,31 @@ def owner_step_model(T, Q, cnt_k, dev, stream, avg_kernel_s, link_gbs=64.0, lat_
         oi = torch.empty((Q, cnt_k), dtype=torch.int32, device=dev)
         oc = torch.empty((Q,), dtype=torch.uint8, device=dev)
         unpack_us = timed(lambda: R.unpack(oi, oc, s))
-        xb = R.xgmi_bytes
         x_t = lat_us + 20 * R.cap / (link_gbs * 1e3)
         x_r = 2 * lat_us + (4 * cnt_k + 1) * R.cap / (link_gbs * 1e3)
         serial = pack_us + x_t + query_us + x_r + unpack_us
         overlap = max(pack_us + query_us + unpack_us, x_t + x_r)
-        out[str(n)] = {"cap": R.cap, "overflow": over, "pack_us": pack_us, "query_us": query_us,
-                       "unpack_us": unpack_us, "xgmi_targets_bytes": xb["targets"], "xgmi_rows_bytes": xb["rows"],
-                       "exchange_targets_modelled_us": x_t, "exchange_rows_modelled_us": x_r,
-                       "step_serial_us": serial, "step_overlapped_us": overlap,
-                       "aggregate_queries_per_s_serial": n * Q / (serial * 1e-6),
-                       "aggregate_queries_per_s_overlapped": n * Q / (overlap * 1e-6)}
+        e = {"cap": R.cap, "overflow": over, "pack_us": pack_us, "query_us": query_us,
+             "unpack_us": unpack_us, "xgmi_targets_bytes": 20 * (n - 1) * R.cap,
+             "xgmi_rows_bytes": (4 * cnt_k + 1) * (n - 1) * R.cap,
+             "exchange_targets_modelled_us": x_t, "exchange_rows_modelled_us": x_r,
+             "step_serial_us": serial, "step_overlapped_us": overlap,
+             "aggregate_queries_per_s_serial": n * Q / (serial * 1e-6),
+             "aggregate_queries_per_s_overlapped": n * Q / (overlap * 1e-6)}
+        if R.packed:  # the rows back packed: kad_route_compress + one collective + kad_route_unpack_packed
+            compress_us = timed(lambda: R.compress(s))
+            esc = R.escaped(combine=False)
+            unpack_p_us = timed(lambda: R.unpack_packed(oi, oc, s))
+            x_p = lat_us + 4 * R.pw * R.cap / (link_gbs * 1e3)
+            serial_p = pack_us + x_t + query_us + compress_us + x_p + unpack_p_us
+            overlap_p = max(pack_us + query_us + compress_us + unpack_p_us, x_t + x_p)
+            e["packed"] = {"row_bytes": 4 * R.pw, "escaped": esc, "compress_us": compress_us,
+                           "unpack_us": unpack_p_us, "xgmi_rows_bytes": 4 * R.pw * (n - 1) * R.cap,
+                           "exchange_rows_modelled_us": x_p, "step_serial_us": serial_p,
+                           "step_overlapped_us": overlap_p,
+                           "aggregate_queries_per_s_serial": n * Q / (serial_p * 1e-6),
+                           "aggregate_queries_per_s_overlapped": n * Q / (overlap_p * 1e-6)}
+        out[str(n)] = e
         del R, t, recv, oi, oc
     out["how"] = ("rank 0 of N on this GPU (its 1/8 shard of the 100M-node table): the pack, the query over the "
                   "blocks it receives and the unpack timed with HIP events (eager, 20 launches each); the exchanges "

@@ -456,6 +456,21 @@ int kad_route_pack(const uint8_t* targets, uint32_t q, uint32_t world, uint32_t 
                    uint8_t* send, uint32_t* slot, uint32_t* ctr, int device, void* stream);
 int kad_route_unpack(const uint32_t* slot, uint32_t q, uint32_t count, const uint32_t* back_idx,
                      const uint8_t* back_cnt, uint32_t* out_idx, uint8_t* out_cnt, int device, void* stream);
+/* Packed rows for the way back (count <= KAD_ROUTE_PACKED_MAX_COUNT): a row's indices lie in one window of the
+ * sorted table, so they travel as word 0 = the row's smallest index (KAD_NO_NODE for an empty row) and one byte
+ * per entry = the entry's index minus word 0 (0xFF past the row's count), KAD_ROUTE_PACKED_WORDS(count) words
+ * (count 8: 12 bytes instead of 33).
+ * kad_route_compress: n rows (idx: n x count uint32, cnt: n bytes, the send layout) -> packed (n x
+ *   KAD_ROUTE_PACKED_WORDS(count) uint32). A row whose indices span more than 254 cannot be packed: it sets the
+ *   sticky word *escape (not cleared by the call; kad_route_pack's ctr[world * KAD_ROUTE_CSTRIDE + 1] is meant for
+ *   it), and the caller runs the batch's way back unpacked.
+ * kad_route_unpack_packed: as kad_route_unpack, from packed rows in the send layout. Async on stream. */
+#define KAD_ROUTE_PACKED_MAX_COUNT 32u
+#define KAD_ROUTE_PACKED_WORDS(count) (1u + ((count) + 3u) / 4u)
+int kad_route_compress(const uint32_t* idx, const uint8_t* cnt, uint32_t n, uint32_t count, uint32_t* packed,
+                       uint32_t* escape, int device, void* stream);
+int kad_route_unpack_packed(const uint32_t* slot, uint32_t q, uint32_t count, const uint32_t* back_packed,
+                            uint32_t* out_idx, uint8_t* out_cnt, int device, void* stream);
 
 /* ---- wire step after the query ------------------------ */
 #define KAD_SEND_NODES 8u           /* reference network_engine.cpp:59 SEND_NODES */

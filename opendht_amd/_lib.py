@@ -53,6 +53,12 @@ KAD_SHARD_COUNTER_STRIDE = 32
 KAD_SHARD_MAX_WORLD = 16
 KAD_ROUTE_CSTRIDE = 32
 KAD_ROUTE_MAX_WORLD = 16
+KAD_ROUTE_PACKED_MAX_COUNT = 32
+
+
+def route_packed_words(count: int) -> int:
+    """KAD_ROUTE_PACKED_WORDS(count)"""
+    return 1 + (count + 3) // 4
 
 
 def shard_block_words(count: int, row_cap: int, part_cap: int) -> int:
@@ -125,6 +131,8 @@ SIGNATURES = {
                                            C.c_uint32, _P, _P, _P, _P, C.c_int, _P]),
     "kad_route_pack": (C.c_int, [_P, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, _P, _P, _P, C.c_int, _P]),
     "kad_route_unpack": (C.c_int, [_P, C.c_uint32, C.c_uint32, _P, _P, _P, _P, C.c_int, _P]),
+    "kad_route_compress": (C.c_int, [_P, _P, C.c_uint32, C.c_uint32, _P, _P, C.c_int, _P]),
+    "kad_route_unpack_packed": (C.c_int, [_P, C.c_uint32, C.c_uint32, _P, _P, _P, C.c_int, _P]),
     "kad_table_set_addrs": (C.c_int, [_P, C.c_uint32, _P]),
     "kad_buffer_nodes_batch": (C.c_int, [_P, _P, C.c_uint32, _P, _P, C.c_uint32, _P, _P, _P]),
     "kad_parse_nodes_batch": (C.c_int, [_P, C.c_uint32, C.c_uint32, _P, _P, C.c_int, _P]),

@@ -8,6 +8,9 @@
 //                       (workgroup, owner); a full block sets a sticky overflow word (the caller grows the blocks
 //                       and runs the batch again)
 //   route_unpack_kernel rows that came back in the send layout -> each query's original position
+//   route_compress_kernel / route_unpack_packed_kernel: the rows travel back packed (the smallest index + one byte
+//                       per entry: 12 bytes for count 8 instead of 33); a row spanning more than 254 indices sets a
+//                       sticky word and the caller sends that batch's rows unpacked
 // The blocks travel with all_to_all_single (RCCL over xGMI), equal splits: opendht_amd/sharded.py OwnerRoute.
 #include <hip/hip_runtime.h>
 
@@ -23,6 +26,7 @@ namespace {
 
 constexpr uint32_t BLOCK = 256, QPT = 4;  // queries per thread: a workgroup packs 1,024 targets
 constexpr uint32_t NONE = 0xFFFFFFFFu;
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
 
 __global__ __launch_bounds__(BLOCK) void route_pack_kernel(const uint8_t* __restrict__ targets, uint32_t q,
                                                             uint32_t world, uint32_t shard_bits, uint32_t cap,
@@ -109,6 +113,147 @@ __global__ __launch_bounds__(BLOCK) void route_unpack_kernel(const uint32_t* __r
     if (c == 0) out_cnt[i] = p != NONE ? back_cnt[p] : (uint8_t)0;
 }
 
+// One thread per row: the row's smallest index, then each entry's offset from it in a byte (0xFF past the count).
+// W = KAD_ROUTE_PACKED_WORDS(count) words per packed row.
+__global__ __launch_bounds__(BLOCK) void route_compress_kernel(const uint32_t* __restrict__ idx,
+                                                               const uint8_t* __restrict__ cnt, uint32_t n,
+                                                               uint32_t count, uint32_t* __restrict__ packed,
+                                                               uint32_t* __restrict__ escape) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t c = min((uint32_t)cnt[i], count), W = KAD_ROUTE_PACKED_WORDS(count);
+    const uint32_t* r = idx + (uint64_t)i * count;
+    uint32_t lo = NONE, hi = 0;
+    for (uint32_t j = 0; j < c; j++) {
+        const uint32_t v = r[j];
+        lo = min(lo, v);
+        hi = max(hi, v);
+    }
+    uint32_t* o = packed + (uint64_t)i * W;
+    o[0] = lo;
+    if (c && hi - lo > 254u) atomicOr(escape, 1u);
+    for (uint32_t w = 1; w < W; w++) {
+        uint32_t b = 0;
+#pragma unroll
+        for (uint32_t x = 0; x < 4; x++) {
+            const uint32_t j = 4 * (w - 1) + x;
+            const uint32_t off = j < c ? min(r[j] - lo, 254u) : 255u;
+            b |= off << (8 * x);
+        }
+        o[w] = b;
+    }
+}
+
+// One thread per query: its packed row (slot[i]) expanded into out_idx row i and out_cnt[i].
+__global__ __launch_bounds__(BLOCK) void route_unpack_packed_kernel(const uint32_t* __restrict__ slot, uint32_t q,
+                                                                    uint32_t count,
+                                                                    const uint32_t* __restrict__ back_packed,
+                                                                    uint32_t* __restrict__ out_idx,
+                                                                    uint8_t* __restrict__ out_cnt) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= q) return;
+    const uint32_t p = slot[i], W = KAD_ROUTE_PACKED_WORDS(count);
+    const uint32_t* pr = p != NONE ? back_packed + (uint64_t)p * W : nullptr;
+    const uint32_t lo = pr ? pr[0] : NONE;
+    uint32_t* row = out_idx + (uint64_t)i * count;
+    uint32_t c = 0;
+    for (uint32_t w = 1; w < W; w++) {
+        const uint32_t b = pr ? pr[w] : 0xFFFFFFFFu;
+        uint32_t v[4];
+#pragma unroll
+        for (uint32_t x = 0; x < 4; x++) {
+            const uint32_t off = (b >> (8 * x)) & 255u;
+            v[x] = off == 255u ? NONE : lo + off;
+            c += off != 255u ? 1u : 0u;
+        }
+        const uint32_t j = 4 * (w - 1);
+        if (j + 4 <= count && (count & 3u) == 0 && ((uintptr_t)row & 15u) == 0) {
+            __builtin_nontemporal_store(v[0], row + j);
+            __builtin_nontemporal_store(v[1], row + j + 1);
+            __builtin_nontemporal_store(v[2], row + j + 2);
+            __builtin_nontemporal_store(v[3], row + j + 3);
+        } else {
+#pragma unroll
+            for (uint32_t x = 0; x < 4; x++)
+                if (j + x < count) row[j + x] = v[x];
+        }
+    }
+    out_cnt[i] = (uint8_t)c;
+}
+
+// Counts that are multiples of 4 (the common 8, 16, 32): L = count / 4 lanes per row (a power-of-two group G >= L),
+// lane j moving entries 4j..4j+3 as one 16-byte load and one packed dword; the group's min / max by shuffles.
+template <uint32_t G>
+__global__ __launch_bounds__(BLOCK) void route_compress4_kernel(const uint32_t* __restrict__ idx,
+                                                                const uint8_t* __restrict__ cnt, uint32_t n,
+                                                                uint32_t count, uint32_t* __restrict__ packed,
+                                                                uint32_t* __restrict__ escape) {
+    const uint64_t t = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    const uint64_t i = t / G;
+    const uint32_t j = (uint32_t)(t % G), L = count / 4;
+    const bool row = i < n, mine = row && j < L;
+    const uint32_t c = row ? min((uint32_t)cnt[i], count) : 0u;
+    u32x4_t v = {NONE, NONE, NONE, NONE};
+    if (mine) v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(idx + i * count) + j);
+    const uint32_t e[4] = {v.x, v.y, v.z, v.w};
+    uint32_t lo = NONE, hi = 0;
+#pragma unroll
+    for (uint32_t x = 0; x < 4; x++)
+        if (4 * j + x < c) {
+            lo = min(lo, e[x]);
+            hi = max(hi, e[x]);
+        }
+#pragma unroll
+    for (uint32_t o = 1; o < G; o <<= 1) {
+        lo = min(lo, (uint32_t)__shfl_xor((int)lo, (int)o, 64));
+        hi = max(hi, (uint32_t)__shfl_xor((int)hi, (int)o, 64));
+    }
+    if (!mine) return;
+    uint32_t b = 0;
+#pragma unroll
+    for (uint32_t x = 0; x < 4; x++) b |= (4 * j + x < c ? min(e[x] - lo, 254u) : 255u) << (8 * x);
+    uint32_t* o = packed + i * (1 + L);
+    o[1 + j] = b;
+    if (j == 0) {
+        o[0] = lo;
+        if (c && hi - lo > 254u) atomicOr(escape, 1u);
+    }
+}
+
+template <uint32_t G>
+__global__ __launch_bounds__(BLOCK) void route_unpack_packed4_kernel(const uint32_t* __restrict__ slot, uint32_t q,
+                                                                     uint32_t count,
+                                                                     const uint32_t* __restrict__ back_packed,
+                                                                     uint32_t* __restrict__ out_idx,
+                                                                     uint8_t* __restrict__ out_cnt) {
+    const uint64_t t = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    const uint64_t i = t / G;
+    const uint32_t j = (uint32_t)(t % G), L = count / 4;
+    const bool mine = i < q && j < L;
+    uint32_t lo = NONE, b = 0xFFFFFFFFu;
+    if (mine) {
+        const uint32_t p = slot[i];
+        if (p != NONE) {
+            const uint32_t* pr = back_packed + (uint64_t)p * (1 + L);
+            lo = pr[0];
+            b = pr[1 + j];
+        }
+    }
+    uint32_t v[4], c = 0;
+#pragma unroll
+    for (uint32_t x = 0; x < 4; x++) {
+        const uint32_t off = (b >> (8 * x)) & 255u;
+        v[x] = off == 255u ? NONE : lo + off;
+        c += off != 255u ? 1u : 0u;
+    }
+#pragma unroll
+    for (uint32_t o = 1; o < G; o <<= 1) c += (uint32_t)__shfl_xor((int)c, (int)o, 64);
+    if (!mine) return;
+    const u32x4_t w = {v[0], v[1], v[2], v[3]};
+    __builtin_nontemporal_store(w, reinterpret_cast<u32x4_t*>(out_idx + i * count) + j);
+    if (j == 0) out_cnt[i] = (uint8_t)c;
+}
+
 struct DevSwitch {
     int prev = -1;
     explicit DevSwitch(int device) {
@@ -160,6 +305,54 @@ extern "C" int kad_route_unpack(const uint32_t* slot, uint32_t q, uint32_t count
     else
         hipLaunchKernelGGL(route_unpack_kernel<false>, grid, dim3(BLOCK), 0, (hipStream_t)stream, slot, q, count,
                            back_idx, back_cnt, out_idx, out_cnt);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return set_error(KAD_ERR_HIP, hipGetErrorString(e));
+    return KAD_OK;
+}
+
+extern "C" int kad_route_compress(const uint32_t* idx, const uint8_t* cnt, uint32_t n, uint32_t count,
+                                  uint32_t* packed, uint32_t* escape, int device, void* stream) {
+    using kadgpu_internal::set_error;
+    if (count == 0 || count > KAD_ROUTE_PACKED_MAX_COUNT) return set_error(KAD_ERR_INVALID, "count must be 1..32");
+    if (n == 0) return KAD_OK;
+    if (!idx || !cnt || !packed || !escape) return set_error(KAD_ERR_INVALID, "NULL buffer");
+    DevSwitch g(device);
+    hipStream_t s = (hipStream_t)stream;
+    if (count % 4 == 0 && (uintptr_t)idx % 16 == 0) {
+        const uint32_t L = count / 4, G = L <= 1 ? 1u : L <= 2 ? 2u : L <= 4 ? 4u : 8u;
+        const dim3 grid((uint32_t)(((uint64_t)n * G + BLOCK - 1) / BLOCK));
+        if (G == 1) hipLaunchKernelGGL(route_compress4_kernel<1>, grid, dim3(BLOCK), 0, s, idx, cnt, n, count, packed, escape);
+        else if (G == 2) hipLaunchKernelGGL(route_compress4_kernel<2>, grid, dim3(BLOCK), 0, s, idx, cnt, n, count, packed, escape);
+        else if (G == 4) hipLaunchKernelGGL(route_compress4_kernel<4>, grid, dim3(BLOCK), 0, s, idx, cnt, n, count, packed, escape);
+        else hipLaunchKernelGGL(route_compress4_kernel<8>, grid, dim3(BLOCK), 0, s, idx, cnt, n, count, packed, escape);
+    } else {
+        hipLaunchKernelGGL(route_compress_kernel, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, idx, cnt, n, count,
+                           packed, escape);
+    }
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return set_error(KAD_ERR_HIP, hipGetErrorString(e));
+    return KAD_OK;
+}
+
+extern "C" int kad_route_unpack_packed(const uint32_t* slot, uint32_t q, uint32_t count, const uint32_t* back_packed,
+                                       uint32_t* out_idx, uint8_t* out_cnt, int device, void* stream) {
+    using kadgpu_internal::set_error;
+    if (count == 0 || count > KAD_ROUTE_PACKED_MAX_COUNT) return set_error(KAD_ERR_INVALID, "count must be 1..32");
+    if (q == 0) return KAD_OK;
+    if (!slot || !back_packed || !out_idx || !out_cnt) return set_error(KAD_ERR_INVALID, "NULL buffer");
+    DevSwitch g(device);
+    hipStream_t s = (hipStream_t)stream;
+    if (count % 4 == 0 && (uintptr_t)out_idx % 16 == 0) {
+        const uint32_t L = count / 4, G = L <= 1 ? 1u : L <= 2 ? 2u : L <= 4 ? 4u : 8u;
+        const dim3 grid((uint32_t)(((uint64_t)q * G + BLOCK - 1) / BLOCK));
+        if (G == 1) hipLaunchKernelGGL(route_unpack_packed4_kernel<1>, grid, dim3(BLOCK), 0, s, slot, q, count, back_packed, out_idx, out_cnt);
+        else if (G == 2) hipLaunchKernelGGL(route_unpack_packed4_kernel<2>, grid, dim3(BLOCK), 0, s, slot, q, count, back_packed, out_idx, out_cnt);
+        else if (G == 4) hipLaunchKernelGGL(route_unpack_packed4_kernel<4>, grid, dim3(BLOCK), 0, s, slot, q, count, back_packed, out_idx, out_cnt);
+        else hipLaunchKernelGGL(route_unpack_packed4_kernel<8>, grid, dim3(BLOCK), 0, s, slot, q, count, back_packed, out_idx, out_cnt);
+    } else {
+        hipLaunchKernelGGL(route_unpack_packed_kernel, dim3((q + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, slot, q, count,
+                           back_packed, out_idx, out_cnt);
+    }
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return set_error(KAD_ERR_HIP, hipGetErrorString(e));
     return KAD_OK;

@@ -282,6 +282,10 @@ class OwnerRoute:
               are never read back)
       return  all_to_all_single of the row and count blocks, back to the senders
       unpack  kad_route_unpack: each query's row to its original position
+    packed (the default for counts 4, 8, ..., 32): the rows go back packed (kad_route_compress: the row's smallest index and a
+    byte per entry, 12 bytes for count 8 instead of 33; one collective instead of two) and kad_route_unpack_packed
+    expands them; a row spanning more than 254 indices sets a sticky word (escaped()), and the batch's way back
+    runs again unpacked.
 
     cap: records per block; default q / world + 6 sigma + 256 of uniform targets. A block that fills sets a sticky
     word; overflowed() combines it over the ranks (one host read per batch, or per K steps), grown() sizes the
@@ -289,10 +293,15 @@ class OwnerRoute:
     RCCL group)."""
 
     def __init__(self, q: int, count: int, world: int, shard_bits: int, device, cap: int | None = None,
-                 collective: bool | None = None):
+                 collective: bool | None = None, packed: bool | None = None):
         import torch
 
+        from ._lib import KAD_ROUTE_PACKED_MAX_COUNT, route_packed_words
+
         self.q, self.count, self.world, self.shard_bits, self.dev = q, count, world, shard_bits, device
+        # packed by default for the counts the vector kernels take (multiples of 4 up to 32: count 8 packs in 11.7 us
+        # and unpacks in 8.3 us per 1M rows, against 13.1 us for the plain unpack; tools/route_packed_check.py)
+        self.packed = (count % 4 == 0 and 1 <= count <= KAD_ROUTE_PACKED_MAX_COUNT) if packed is None else bool(packed)
         self.collective = world > 1 if collective is None else bool(collective)
         nominal = -(-q // world)
         self.cap_max = max(1, q)
@@ -306,11 +315,15 @@ class OwnerRoute:
         self.cnt = torch.empty((n,), dtype=torch.uint8, device=device)
         self.back_rows = torch.empty_like(self.rows) if self.collective else self.rows
         self.back_cnt = torch.empty_like(self.cnt) if self.collective else self.cnt
+        self.pw = route_packed_words(count) if self.packed else 0
+        self.prow = torch.empty((n, self.pw), dtype=torch.int32, device=device) if self.packed else None
+        self.back_prow = (torch.empty_like(self.prow) if self.collective else self.prow) if self.packed else None
 
     @property
     def xgmi_bytes(self) -> dict:
         """Bytes a rank sends to the other ranks per step: targets out, rows + counts back."""
-        return {"targets": 20 * (self.world - 1) * self.cap, "rows": (4 * self.count + 1) * (self.world - 1) * self.cap}
+        per = 4 * self.pw if self.packed else 4 * self.count + 1
+        return {"targets": 20 * (self.world - 1) * self.cap, "rows": per * (self.world - 1) * self.cap}
 
     def pack(self, targets, stream):
         import ctypes as C
@@ -330,12 +343,33 @@ class OwnerRoute:
                                      ptr(out_idx), ptr(out_cnt), self.dev.index or 0, C.c_void_p(stream)),
               "kad_route_unpack")
 
+    def compress(self, stream):
+        """The answered rows packed for the way back (escape word: ctr[world * 32 + 1])."""
+        import ctypes as C
+
+        from ._lib import check, lib, ptr
+
+        n = self.world * self.cap
+        check(lib().kad_route_compress(ptr(self.rows), ptr(self.cnt), n, self.count, ptr(self.prow),
+                                       C.c_void_p(self.ctr.data_ptr() + 4 * (self.world * 32 + 1)),
+                                       self.dev.index or 0, C.c_void_p(stream)), "kad_route_compress")
+
+    def unpack_packed(self, out_idx, out_cnt, stream):
+        import ctypes as C
+
+        from ._lib import check, lib, ptr
+
+        check(lib().kad_route_unpack_packed(ptr(self.slot), self.q, self.count, ptr(self.back_prow), ptr(out_idx),
+                                            ptr(out_cnt), self.dev.index or 0, C.c_void_p(stream)),
+              "kad_route_unpack_packed")
+
     def answer(self, table, stream):
         """The owner's rows for every record of the received blocks (table: a DeviceTable)."""
         table.rt_closest(self.recv, self.count, out_idx=self.rows, out_cnt=self.cnt, stream=stream)
 
-    def step(self, table, targets, out_idx, out_cnt, group=None, stream=None):
-        """pack, send, answer, return, unpack: device-only (check overflowed() after)."""
+    def step(self, table, targets, out_idx, out_cnt, group=None, stream=None, packed: bool | None = None):
+        """pack, send, answer, return, unpack: device-only (check overflowed(), then escaped(), after).
+        packed=False: the way back unpacked (the rerun of a batch whose rows escaped packing)."""
         import torch
 
         from .global_shard import _torch_stream
@@ -346,15 +380,39 @@ class OwnerRoute:
             with torch.cuda.stream(_torch_stream(s, self.dev)):
                 _all_to_all(self.recv, self.send, group)
         self.answer(table, s)
+        self.back(out_idx, out_cnt, group, s, self.packed if packed is None else packed)
+
+    def back(self, out_idx, out_cnt, group, s, packed: bool):
+        """The way back of the answered rows: return + unpack (packed or not)."""
+        import torch
+
+        from .global_shard import _torch_stream
+
+        if packed:
+            self.compress(s)
+            if self.collective:
+                with torch.cuda.stream(_torch_stream(s, self.dev)):
+                    _all_to_all(self.back_prow, self.prow, group)
+            self.unpack_packed(out_idx, out_cnt, s)
+            return
         if self.collective:
             with torch.cuda.stream(_torch_stream(s, self.dev)):
                 _all_to_all(self.back_rows, self.rows, group)
                 _all_to_all(self.back_cnt, self.cnt, group)
         self.unpack(out_idx, out_cnt, s)
 
+    def escaped(self, group=None, combine: bool = True) -> bool:
+        """Host read of the packing escape word (a row spanning more than 254 indices), combined over the ranks."""
+        if not self.packed:
+            return False
+        return self._flag(self.world * 32 + 1, group, combine)
+
     def overflowed(self, group=None, combine: bool = True) -> bool:
         """Host read of the sticky overflow word, combined over the ranks (every rank decides the same)."""
-        ov = self.ctr[self.world * 32:self.world * 32 + 1]
+        return self._flag(self.world * 32, group, combine)
+
+    def _flag(self, w: int, group, combine: bool) -> bool:
+        ov = self.ctr[w:w + 1]
         if combine and self.collective:
             import torch.distributed as dist
 
@@ -383,7 +441,8 @@ class OwnerRoute:
     def grown(self, group=None, need: int | None = None) -> "OwnerRoute":
         n = self.need(group) if need is None else need
         return OwnerRoute(self.q, self.count, self.world, self.shard_bits, self.dev,
-                          cap=min(self.cap_max, max(2 * self.cap, n * 5 // 4)), collective=self.collective)
+                          cap=min(self.cap_max, max(2 * self.cap, n * 5 // 4)), collective=self.collective,
+                          packed=self.packed)
 
 
 def _all_to_all(recv, send, group=None):
@@ -415,11 +474,16 @@ def serve_owner(table, targets, count: int, route: OwnerRoute | None = None, gro
     while True:
         route.step(table, targets, out_idx, out_cnt, group, stream)
         if not route.overflowed(group):
+            if route.escaped(group):  # a row too wide to pack: this batch's rows go back unpacked
+                import torch as _t
+
+                s = stream if stream is not None else _t.cuda.current_stream(targets.device).cuda_stream
+                route.back(out_idx, out_cnt, group, s, packed=False)
             return out_idx, out_cnt, route
         route = route.grown(group)
 
 
-def route_simulated(tables, batches, count: int, shard_bits: int, cap: int | None = None):
+def route_simulated(tables, batches, count: int, shard_bits: int, cap: int | None = None, packed: bool = False):
     """Every rank of the owner-routed exchange in ONE process (one GPU): rank r packs batches[r]; rank d receives
     block d of every rank's send buffer, concatenated in rank order (what all_to_all_single delivers), answers it
     with tables[d]; rank s receives block s of every rank's rows; rank s unpacks. Grows and reruns on overflow.
@@ -430,7 +494,8 @@ def route_simulated(tables, batches, count: int, shard_bits: int, cap: int | Non
     dev = batches[0].device
     s = torch.cuda.current_stream(dev).cuda_stream
     while True:
-        routes = [OwnerRoute(b.shape[0], count, world, shard_bits, dev, cap=cap, collective=False) for b in batches]
+        routes = [OwnerRoute(b.shape[0], count, world, shard_bits, dev, cap=cap, collective=False, packed=packed)
+                  for b in batches]
         if len({r.cap for r in routes}) != 1:
             raise ValueError("every rank's batch must give the same block size")
         c = routes[0].cap
@@ -447,12 +512,26 @@ def route_simulated(tables, batches, count: int, shard_bits: int, cap: int | Non
             cnt = torch.empty((world * c,), dtype=torch.uint8, device=dev)
             tables[d].rt_closest(recv, count, out_idx=rows, out_cnt=cnt)
             answered.append((rows, cnt))
+        escaped = False
+        if packed:  # owner d packs its rows (its route object's buffers hold them), the escape words combined
+            packs = []
+            for d in range(world):
+                R = routes[d]
+                R.rows, R.cnt = answered[d]
+                R.compress(s)
+                packs.append(R.prow.clone())
+            escaped = any(bool(int(R.ctr[world * 32 + 1].item())) for R in routes)
         out = []
         for src, r in enumerate(routes):
-            r.back_rows = torch.cat([answered[d][0][src * c:(src + 1) * c] for d in range(world)])
-            r.back_cnt = torch.cat([answered[d][1][src * c:(src + 1) * c] for d in range(world)])
             oi = torch.empty((r.q, count), dtype=torch.int32, device=dev)
             oc = torch.empty((r.q,), dtype=torch.uint8, device=dev)
-            r.unpack(oi, oc, s)
+            if packed and not escaped:
+                r.back_prow = torch.cat([packs[d][src * c:(src + 1) * c] for d in range(world)])
+                r.unpack_packed(oi, oc, s)
+            else:
+                r.back_rows = torch.cat([answered[d][0][src * c:(src + 1) * c] for d in range(world)])
+                r.back_cnt = torch.cat([answered[d][1][src * c:(src + 1) * c] for d in range(world)])
+                r.unpack(oi, oc, s)
             out.append((oi, oc))
+        routes[0].sim_escaped = escaped
         return out, routes[0]

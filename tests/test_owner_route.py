@@ -3,8 +3,9 @@ DESIGN.md §6.1): every rank sends its batch's targets to the ranks owning them,
 halo shards, the rows come back to the senders' positions. The reference answers each request where it arrives
 (Dht::onFindNode / onGetValues, dht.cpp:3189-3217), every answer the whole table's findClosestNodes
 (routing_table.cpp:67-111). Checked bit-exact against the oracle on the whole table: N = 1, 2, 4, 8 ranks simulated
-on one GPU (blocks concatenated as all_to_all_single delivers them), capacities of 1 (overflow, growth, rerun), and
-two real gloo ranks sharing the GPU."""
+on one GPU (blocks concatenated as all_to_all_single delivers them), capacities of 1 (overflow, growth, rerun), rows
+back plain and packed (kad_route_compress, and the unpacked rerun when a row cannot be packed), and two real gloo
+ranks sharing the GPU."""
 import os
 import socket
 
@@ -37,7 +38,8 @@ def _batch(spec, n, seed):
 
 @pytest.mark.parametrize("world", [1, 2, 4, 8])
 @pytest.mark.parametrize("small_cap", [False, True], ids=["", "cap1"])
-def test_owner_route_simulated(gpu, world, small_cap):
+@pytest.mark.parametrize("packed", [False, True], ids=["rows", "packed"])
+def test_owner_route_simulated(gpu, world, small_cap, packed):
     spec = ShardSpec(n_shards=world, depth=10, mean_per_bucket=6.0, seed=0x0A0 + world, good_pct=60, expired_pct=20)
     gids, gst, goff = spec.bucket_range(0, spec.n_buckets)
     gfirst = S.bucket_firsts(spec.depth, 0, spec.n_buckets)
@@ -50,10 +52,13 @@ def test_owner_route_simulated(gpu, world, small_cap):
         batches = [b[:n] for b in batches]
         tgs = [torch.from_numpy(b).to(gpu) for b in batches]
         for count in (1, 8, 14, 32):
-            out, r0 = route_simulated(tables, tgs, count, spec.shard_bits, cap=1 if small_cap else None)
+            out, r0 = route_simulated(tables, tgs, count, spec.shard_bits, cap=1 if small_cap else None,
+                                      packed=packed)
             torch.cuda.synchronize()
             if small_cap:
                 assert r0.cap > 1  # it grew
+            if packed:
+                assert not r0.sim_escaped  # (60 % good: every window spans far fewer than 255 nodes)
             for r, (oi, oc) in enumerate(out):
                 want, wcnt = O.flat_rt_closest(gids, gst, gfirst, goff, batches[r], count, nthreads=8)
                 np.testing.assert_array_equal(oc.cpu().numpy(), wcnt, err_msg=f"N={world} rank {r} k={count} counts")
@@ -85,6 +90,35 @@ def test_route_pack_layout(gpu):
     torch.cuda.synchronize()
     assert R2.overflowed(combine=False)
     assert int((R2.slot.cpu().numpy().view(np.uint32) == 0xFFFFFFFF).sum()) > 0
+
+
+def test_owner_route_packed_escape(gpu):
+    """A mostly-bad table: count-32 windows span more than 254 nodes, so the packed rows escape and the way back
+    runs unpacked; every row still equals the whole table's answer. kad_route_compress / kad_route_unpack_packed
+    round trip on rows that do pack."""
+    world = 2
+    spec = ShardSpec(n_shards=world, depth=8, mean_per_bucket=12.0, seed=0xE5C, good_pct=2, expired_pct=90)
+    gids, gst, goff = spec.bucket_range(0, spec.n_buckets)
+    gfirst = S.bucket_firsts(spec.depth, 0, spec.n_buckets)
+    shards = [build_shard(spec, s) for s in range(world)]
+    tables = [DeviceTable(sh.ids, sh.status, sh.first, sh.off, device=0, index_base=sh.index_base, sorted=True)
+              for sh in shards]
+    try:
+        batches = [_batch(spec, 800, seed=70 + r)[:800] for r in range(world)]
+        tgs = [torch.from_numpy(b).to(gpu) for b in batches]
+        seen = set()
+        for count in (4, 32):
+            out, r0 = route_simulated(tables, tgs, count, spec.shard_bits, packed=True)
+            torch.cuda.synchronize()
+            seen.add(r0.sim_escaped)
+            for r, (oi, oc) in enumerate(out):
+                want, wcnt = O.flat_rt_closest(gids, gst, gfirst, goff, batches[r], count, nthreads=8)
+                np.testing.assert_array_equal(oc.cpu().numpy(), wcnt, err_msg=f"rank {r} k={count} counts")
+                np.testing.assert_array_equal(oi.cpu().numpy().view(np.uint32), want, err_msg=f"rank {r} k={count}")
+        assert True in seen  # count 32 escaped
+    finally:
+        for T in tables:
+            T.close()
 
 
 def _free_port():
@@ -119,13 +153,13 @@ def _serve_worker(rank, world, port, q):
         tg = torch.from_numpy(targets).to(dev)
         ok, why = True, ""
         for count in (1, 8, 14, 32):
-            for cap in (None, 1):
-                route = OwnerRoute(tg.shape[0], count, world, spec.shard_bits, dev, cap=cap)
+            for cap, packed in ((None, True), (1, True), (None, False)):
+                route = OwnerRoute(tg.shape[0], count, world, spec.shard_bits, dev, cap=cap, packed=packed)
                 oi, oc, route = serve_owner(T, tg, count, route=route)
                 torch.cuda.synchronize()
                 want, wcnt = O.flat_rt_closest(gids, gst, gfirst, goff, targets, count)
                 if not (np.array_equal(oi.cpu().numpy().view(np.uint32), want) and np.array_equal(oc.cpu().numpy(), wcnt)):
-                    ok, why = False, f"rank {rank} k={count} cap={cap}"
+                    ok, why = False, f"rank {rank} k={count} cap={cap} packed={packed}"
         T.close()
     except Exception as e:  # reported through the queue
         ok, why = False, f"{type(e).__name__}: {e}"
