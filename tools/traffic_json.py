@@ -10,6 +10,7 @@ import json
 import os
 import subprocess
 import sys
+import time
 
 d, ksub, tag = sys.argv[1], sys.argv[2], sys.argv[3]
 count = int(sys.argv[4]) if len(sys.argv) > 4 else 8
@@ -30,7 +31,8 @@ out = {"kernel": ksub, "count": count, "hbm_bytes_per_launch": fetch + write, "r
        "raw_kib": {"FETCH_SIZE": pm["FETCH_SIZE"], "WRITE_SIZE": pm["WRITE_SIZE"]},
        "l2_hit_rate": pm["TCC_HIT_sum"] / (pm["TCC_HIT_sum"] + pm["TCC_MISS_sum"]) if "TCC_HIT_sum" in pm else None,
        "correction": basis,
-       "source": f"rocprofv3 --pmc passes over bench.py {args} ({d})"}
+       "source": f"rocprofv3 --pmc passes over bench.py {args} ({d})",
+       "date": time.strftime("%Y-%m-%d")}
 p = os.path.join(root, "profiles", f"traffic_{tag}.json")
 json.dump(out, open(p, "w"), indent=1)
 print(json.dumps(out, indent=1))
