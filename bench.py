@@ -569,7 +569,8 @@ def owner_routed_pass(T, sh, spec, Q, cnt_k, K, W, dev, dist, world, rank, NB=4)
                           oi[:65536].cpu().numpy()[mine], oc[:65536].cpu().numpy()[mine], cnt_k)
         xb = R.xgmi_bytes
         return {"queries_per_s": world * Q * K / t_max, "ms_per_step": t_max / K * 1e3, "n_gpus": world,
-                "collective": "RCCL all_to_all_single" if world > 1 else None, "cap": R.cap, "overflow": over,
+                "collective": (f"all_to_all_single ({'RCCL' if dist.get_backend() == 'nccl' else dist.get_backend()})"
+                               if world > 1 else None), "cap": R.cap, "overflow": over,
                 "rows_back": f"packed, {4 * R.pw} bytes per row" if R.packed else "plain", "escaped": esc,
                 "xgmi_bytes_per_rank_step": xb, "launch": how,
                 "verified": {"rows": sum_over_ranks(dist, int(mine.sum()), dev),

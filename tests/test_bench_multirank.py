@@ -1,7 +1,8 @@
 """bench.py's N-rank flow on one GPU (a rehearsal of the driver's `bench.py --gpus N` on an 8-GPU node):
 `python bench.py --gpus 2` starts two ranks itself; with KADGPU_BENCH_ONE_GPU=1 both use cuda:0 and gloo
 (RCCL needs a GPU per rank). Both variants must complete: owner routing (weak scaling, 2 shards of the
-100M-node table) and the north-star all-gather (the 100M-node table split in two, gathered rows and
+100M-node table), the owner-routed serving step (targets to their owners and packed rows back through
+all_to_all_single) and the north-star all-gather (the 100M-node table split in two, gathered rows and
 parts, device merge), and rank 0 prints one line with n_gpus = 2."""
 import json
 import os
@@ -30,3 +31,7 @@ def test_bench_two_ranks_on_one_gpu():
     assert "error" not in ag, ag
     assert ag["n_gpus"] == 2 and ag["value"] > 0 and ag["gathered_bytes_per_step"] > 0
     assert ag["verified"]["rows"] > 0 and ag["verified"]["mismatches"] == 0
+    ow = d["owner_routed"]  # the owner-routed serving step at N = 2 (all_to_alls through gloo here)
+    assert "error" not in ow, ow
+    assert ow["n_gpus"] == 2 and ow["queries_per_s"] > 0 and not ow["overflow"]
+    assert ow["verified"]["rows"] > 0 and ow["verified"]["mismatches"] == 0
