@@ -4535,11 +4535,13 @@ __global__ __launch_bounds__(BLOCK) void nc_two_pass_kernel(DevTable T, const ui
 // where [r0, r1) are the slot's nodes:
 //   dw0      w0
 //   dw1      ns = r1 - r0 | sh << 8
-//   dw2      defer | truncated left (w0 > 0) << 1 | truncated right (w0 + 60 < n) << 2
+//   dw2      defer (clamped window / wide slot) | truncated left (w0 > 0) << 1 | truncated right (w0 + 60 < n) << 2
 //   dw4..63  slot j: key24(node w0+j) << 8 | expired
 // key24 = ID bits [40-sh, 64-sh) = (key >> sh) & 0xFFFFFF, starting at or above the window's common
 // prefix: all window nodes share the bits above, so every XOR comparison between them (the walk's
-// xorCmp) is decided inside those 24 bits (a line is deferred when two adjacent nodes share them).
+// xorCmp) is decided inside those 24 bits unless the two nodes share them; key24 is monotone over the window,
+// so a left-run and a right-run node can only share one if the two nodes either side of lb do, and only that
+// pair sends the query to the exact path (round 4 deferred the whole line for any equal neighbours).
 // The start is also at or above the slot's prefix, so "node < target" for the slot's nodes is a
 // key24 comparison (equal key24: exact path). Windows clamped at the array ends and
 // slots of more than 15 nodes are deferred (exact path): lb = r0 + x with x <= 15.
@@ -4595,6 +4597,9 @@ __device__ __forceinline__ bool ncl_answer(const uint4 (&Lq)[16], uint32_t index
 #pragma unroll
         for (int j = 0; j < 64; j++) v[j] = (x & 8u) ? (j < 56 ? u[j + 8] : NONE) : u[j];
     }
+    // equal key24 either side of lb: the runs may tie at 24 bits (the window's key24 values are monotone, so a
+    // left and a right element can only share one if these two do); only the full IDs order them -> exact path
+    ex |= (v[NCL_LEFT - 1] >> 8) == (v[NCL_LEFT] >> 8);
     const uint32_t nv = NCL_SLOTS - x;  // valid slots after the shift
     // keys: (M along the run) << 8 | side << 7 | steps from lb << 1 | expired. Each run's keys ascend
     // outward from lb (M never decreases, the steps grow), and the expired bit is below the steps.
@@ -4863,17 +4868,13 @@ __global__ void ncl_build_kernel(const uint64_t* key, const uint8_t* status, con
     const uint32_t w0 = r0 - NCL_LEFT;
     const uint32_t P = (uint32_t)__builtin_clzll((key[w0] ^ key[w0 + NCL_SLOTS - 1]) | 1ull);
     const uint32_t Pp = min(min(P, slot_prefix), 40u), sh = 40 - Pp;
-    bool defer = false;
-    uint32_t prev = 0;
-    for (uint32_t j = 0; j < NCL_SLOTS; j++) {
+    for (uint32_t j = 0; j < NCL_SLOTS; j++) {  // (equal neighbours: ncl_answer checks the pair around lb)
         const uint32_t k24 = (uint32_t)(key[w0 + j] >> sh) & 0xFFFFFFu;
-        defer |= j > 0 && k24 == prev;
-        prev = k24;
         L[4 + j] = (k24 << 8) | ((status[w0 + j] & KAD_STATUS_EXPIRED) ? 1u : 0u);
     }
     L[0] = w0;
     L[1] = ns | (sh << 8);
-    L[2] = (defer ? 1u : 0u) | (w0 > 0 ? 2u : 0u) | (w0 + NCL_SLOTS < n ? 4u : 0u);
+    L[2] = (w0 > 0 ? 2u : 0u) | (w0 + NCL_SLOTS < n ? 4u : 0u);
     L[3] = 0;
         }();
     }
@@ -4884,7 +4885,7 @@ __global__ void ncl_build_kernel(const uint64_t* key, const uint8_t* status, con
 // w0 = r0-56 .. r0+67 of the sorted node array ([r0, r1) = the slot's nodes, at most 15):
 //   dw0      w0
 //   dw1      ns = r1 - r0 | sh << 8
-//   dw2      defer | truncated left (w0 > 0) << 1 | truncated right (w0 + 124 < n) << 2
+//   dw2      defer (a clamped or wide slot) | truncated left (w0 > 0) << 1 | truncated right (w0 + 124 < n) << 2
 //   dw4..127 element e (node w0 + e): key24 << 8 | expired, key24 as in the 256-byte lines
 // A query is answered by 8 lanes (an octet; 8 queries per wave). The octet stages its line in LDS with
 // 16-byte loads, counts the slot's nodes below the target (lb = w0 + p, p = 56 + x), and reads the
@@ -4895,8 +4896,8 @@ __global__ void ncl_build_kernel(const uint64_t* key, const uint8_t* status, con
 // lines), so the walk's first 64 steps are min(left[r], right[63-r]) followed by a bitonic half-cleaner
 // cascade (three stages across lanes, three inside). The first `count` non-expired steps are the answer;
 // a run cut by the window's truncated end limits the trusted keys to that end's key. A query with fewer
-// than `count` trusted emissions, a deferred line, or a target equal in key24 to a slot node takes the
-// two-pass wave path (nc_answer, then nc64_query / the serial walk).
+// than `count` trusted emissions, a deferred line, a target equal in key24 to a slot node, or equal key24
+// either side of its position takes the two-pass wave path (nc_answer, then nc64_query / the serial walk).
 // ---------------------------------------------------------------------------------------
 constexpr uint32_t NC32_SLOTS = 124, NC32_LEFT = 56, NC32_XMAX = 15, NC32_STRIDE = 128;  // dwords
 
@@ -4940,27 +4941,20 @@ __global__ __launch_bounds__(BLOCK) void ncl32_build_kernel(const uint64_t* key,
     const uint32_t w0 = r0 - NC32_LEFT;
     const uint32_t P = (uint32_t)__builtin_clzll((key[w0] ^ key[w0 + NC32_SLOTS - 1]) | 1ull);
     const uint32_t Pp = min(min(P, slot_prefix), 40u), sh = 40 - Pp;
+    // (equal key24 between neighbours no longer defers the line: nc32_line_kernel checks the one pair that can change
+    // the walk's order, the two elements either side of the target's position)
     uint32_t v[16];
-    bool defer = false;
-    uint32_t prev = 0;
-    if (g > 0) prev = (uint32_t)(key[w0 + 16 * g - 5] >> sh) & 0xFFFFFFu;  // element 16g - 5
 #pragma unroll
     for (int u = 0; u < 16; u++) {
         const int j = 16 * (int)g + u, e = j - 4;
         if (e < 0) { v[u] = 0; continue; }
         const uint32_t k24 = (uint32_t)(key[w0 + e] >> sh) & 0xFFFFFFu;
-        defer |= e > 0 && k24 == prev;
-        prev = k24;
         v[u] = (k24 << 8) | ((status[w0 + e] & KAD_STATUS_EXPIRED) ? 1u : 0u);
     }
-    uint32_t df = defer ? 1u : 0u;
-    df |= (uint32_t)__shfl_xor((int)df, 1, 8);
-    df |= (uint32_t)__shfl_xor((int)df, 2, 8);
-    df |= (uint32_t)__shfl_xor((int)df, 4, 8);
     if (g == 0) {
         v[0] = w0;
         v[1] = ns | (sh << 8);
-        v[2] = df | (w0 > 0 ? 2u : 0u) | (w0 + NC32_SLOTS < n ? 4u : 0u);
+        v[2] = (w0 > 0 ? 2u : 0u) | (w0 + NC32_SLOTS < n ? 4u : 0u);
         v[3] = 0;
     }
 #pragma unroll
@@ -5038,7 +5032,11 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) v
         below += oct_xor<4>(below);
         eq |= oct_xor<4>(eq);
         const uint32_t p = NC32_LEFT + below;
-        bool ex = (fl & 1u) || eq;
+        // the window's key24 values are monotone (its nodes share the top Pp bits), so equal ones are neighbours, and
+        // a left-run and a right-run element can share one (a tie at 24 bits between the runs, which only the full IDs
+        // order) only if elements p-1 and p do: then the exact path (the builder no longer defers a line for equal
+        // neighbours elsewhere in the window: 0.5 % of count-32 queries took the wave path for that)
+        bool ex = (fl & 1u) || eq || (W[4 + p - 1] >> 8) == (W[4 + p] >> 8);
         // the runs' first 64 steps: left step 8g+u = element p-1-step, right step 63-8g-u = element p+step. Key:
         // distance24 << 8 | side << 7 | step << 1 | expired. A step outside the line's window is NONE: it sorts
         // after every step inside, is never emitted (its expired bit is set), and (the outside steps are a suffix
