@@ -2554,6 +2554,9 @@ __device__ __forceinline__ bool gl32_answer4(const DevTable& T, const Target& t,
 }
 
 // Counts 24, 28, 32 on general lines: four lanes per query, the row through a per-quad LDS row (rt_wl32q_kernel's).
+// ABL (tools build only, KAD_RT_KERNEL=gl32q_abl1 / gl32q_stats): 1 = no exact path (those rows left unwritten);
+// 3 = path statistics (out_cnt = 250 for the queries the exact path answers).
+template <int ABL>
 __global__ __launch_bounds__(BLOCK) void rt_gl32q_kernel(DevTable T, const uint8_t* __restrict__ targets, uint32_t q,
                                                          uint32_t count, uint32_t* __restrict__ out_idx,
                                                          uint8_t* __restrict__ out_cnt) {
@@ -2595,8 +2598,10 @@ __global__ __launch_bounds__(BLOCK) void rt_gl32q_kernel(DevTable T, const uint8
                 if (4u * j + p < count) st_row1(row + 4 * j + p, R[4 * j + p]);
         }
     }
+    if (ABL == 1) return;
     __shared__ uint64_t xs[BLOCK / 64][192];
     exact_tail(T, t, act && !ok && p == 0u, i, count, out_idx, out_cnt, xs[threadIdx.x >> 6]);
+    if (ABL == 3 && act && !ok && p == 0u && out_cnt) out_cnt[i] = 250;
 }
 
 __device__ __forceinline__ void rt_gl32_kernel_body(const DevTable& T, const uint8_t* __restrict__ targets, uint32_t q,
@@ -8226,7 +8231,12 @@ int launch_rt(const kad_table* t, const uint8_t* targets, uint32_t q, uint32_t c
     } else if (K == 32 && (d.flags & TF_GL32) && count >= 24 && (count & 3u) == 0 &&
                !(ev && (std::strcmp(ev, "lane") == 0 || std::strcmp(ev, "gl32lane") == 0))) {
         // four lanes per query for rows of 24, 28 and 32 entries (as the uniform lines' rt_wl32q_kernel)
-        hipLaunchKernelGGL(rt_gl32q_kernel, dim3(grid_for(4ull * q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
+        void (*kq)(DevTable, const uint8_t*, uint32_t, uint32_t, uint32_t*, uint8_t*) = rt_gl32q_kernel<0>;
+#ifdef KAD_ABLATIONS
+        if (ev && std::strcmp(ev, "gl32q_abl1") == 0) kq = rt_gl32q_kernel<1>;
+        if (ev && std::strcmp(ev, "gl32q_stats") == 0) kq = rt_gl32q_kernel<3>;
+#endif
+        hipLaunchKernelGGL(kq, dim3(grid_for(4ull * q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
     } else if (K > 8 && (d.flags & TF_GL32) && !(ev && std::strcmp(ev, "lane") == 0)) {
         hipLaunchKernelGGL(rt_gl32_kernel, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
     } else {
