@@ -1539,7 +1539,8 @@ __device__ __forceinline__ void store_rows_block(uint32_t* __restrict__ out_idx,
 __device__ bool wave_wl32(const DevTable& T, const Target& t, uint32_t b, uint32_t count, uint32_t lane, uint32_t* row,
                           uint8_t* cp);  // below, with the 32-count lines
 
-// ABL 1 = no exact path (timing ablation only, KAD_RT_KERNEL=wl16_abl1; deferred rows are left unwritten).
+// ABL 1 = no exact path (timing ablation only, KAD_RT_KERNEL=wl16_abl1; deferred rows are left unwritten); 3 = path
+// statistics (wl16_stats: out_cnt 250 where the line could not answer).
 template <int ABL>
 __device__ __forceinline__ void rt_wl16_kernel_body(const DevTable& T, const uint8_t* __restrict__ targets, uint32_t q,
                                                         uint32_t count, uint32_t* __restrict__ out_idx,
@@ -1556,7 +1557,11 @@ __device__ __forceinline__ void rt_wl16_kernel_body(const DevTable& T, const uin
     bool ok = wl16_answer(T, t, b, count, act, o, m);
     if (act && ok && out_cnt) out_cnt[i] = (uint8_t)m;
     store_rows_block<16>(out_idx, q, count, o, act && ok);
-    if (ABL) return;
+    if (ABL == 1) return;
+    if (ABL == 3) {  // path statistics (tools build): 250 = the 16-count line could not answer
+        if (act && !ok && out_cnt) out_cnt[i] = 250;
+        return;
+    }
     // the queries the 16-count line cannot answer (its 29 slots could not hold both the count 14 and the count 16
     // D-rank prefixes, a deferred line): the 32-count line of the same bucket (58 slots) by the wave, one query at a
     // time, then the exact path
@@ -8191,6 +8196,8 @@ int launch_rt(const kad_table* t, const uint8_t* targets, uint32_t q, uint32_t c
 #ifdef KAD_ABLATIONS
         if (ev && std::strcmp(ev, "wl16_abl1") == 0)
             hipLaunchKernelGGL(rt_wl16_kernel<1>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
+        else if (ev && std::strcmp(ev, "wl16_stats") == 0)
+            hipLaunchKernelGGL(rt_wl16_kernel<3>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
         else
 #endif
             hipLaunchKernelGGL(rt_wl16_kernel<0>, dim3(grid_for(q)), dim3(BLOCK), 0, s, d, targets, q, count, out, cnt);
