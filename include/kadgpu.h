@@ -443,15 +443,24 @@ int kad_rt_home_finish_reset(const uint32_t* recv, uint32_t* send, uint32_t worl
  * all_to_all_single of fixed-size blocks (no host read per batch):
  * kad_route_pack: targets (device, q x 20 bytes) into `world` send blocks of `cap` records of 20 bytes (send:
  *   world * cap * 20 bytes): target i goes to block d = (byte 0 >> (8 - shard_bits)) % world (d = 0 when
- *   shard_bits = 0); slot[i] = d * cap + its record (KAD_NO_NODE when block d is full, which sets the sticky word
- *   ctr[world * KAD_ROUTE_CSTRIDE]). ctr: (world + 1) * KAD_ROUTE_CSTRIDE words, zeroed by the call;
- *   ctr[d * KAD_ROUTE_CSTRIDE] ends as block d's record count (it may exceed cap). The order of the records inside
- *   a block is unspecified; records past a block's count are left as they were. Async on stream.
+ *   shard_bits = 0). A block is KAD_ROUTE_SUBS sub-blocks of cap / KAD_ROUTE_SUBS records (cap a multiple of
+ *   KAD_ROUTE_SUBS): the targets of workgroup w (KAD_ROUTE_QPW queries) go to sub-block w % KAD_ROUTE_SUBS, so that
+ *   the workgroups' appends spread over KAD_ROUTE_SUBS counters per block (one counter hit by every workgroup
+ *   serialised them: 24 us against 15 per 1M targets). slot[i] = d * cap + its record (KAD_NO_NODE when its
+ *   sub-block is full, which sets the sticky word ctr[KAD_ROUTE_OVERFLOW_WORD(world)]). ctr:
+ *   KAD_ROUTE_CTR_WORDS(world) words, zeroed by the call; ctr[(d * KAD_ROUTE_SUBS + r) * KAD_ROUTE_CSTRIDE] ends as
+ *   sub-block r of block d's record count (it may exceed its capacity). The order of the records inside a sub-block
+ *   is unspecified; records past a sub-block's count are left as they were (the owner answers them too; their rows
+ *   are never read back). Async on stream.
  * kad_route_unpack: rows returned in the send layout (back_idx: world * cap rows of `count` uint32, back_cnt: world *
  *   cap bytes) back to each query's position: out_idx row i = back_idx row slot[i], out_cnt[i] = back_cnt[slot[i]]
  *   (KAD_NO_NODE and 0 for slot KAD_NO_NODE). Async on stream. All pointers are device pointers. */
 #define KAD_ROUTE_CSTRIDE 32u
 #define KAD_ROUTE_MAX_WORLD 16u
+#define KAD_ROUTE_SUBS 8u
+#define KAD_ROUTE_QPW 1024u
+#define KAD_ROUTE_CTR_WORDS(world) (((world) * KAD_ROUTE_SUBS + 1u) * KAD_ROUTE_CSTRIDE)
+#define KAD_ROUTE_OVERFLOW_WORD(world) ((world) * KAD_ROUTE_SUBS * KAD_ROUTE_CSTRIDE)
 int kad_route_pack(const uint8_t* targets, uint32_t q, uint32_t world, uint32_t shard_bits, uint32_t cap,
                    uint8_t* send, uint32_t* slot, uint32_t* ctr, int device, void* stream);
 int kad_route_unpack(const uint32_t* slot, uint32_t q, uint32_t count, const uint32_t* back_idx,
@@ -462,8 +471,8 @@ int kad_route_unpack(const uint32_t* slot, uint32_t q, uint32_t count, const uin
  * (count 8: 12 bytes instead of 33).
  * kad_route_compress: n rows (idx: n x count uint32, cnt: n bytes, the send layout) -> packed (n x
  *   KAD_ROUTE_PACKED_WORDS(count) uint32). A row whose indices span more than 254 cannot be packed: it sets the
- *   sticky word *escape (not cleared by the call; kad_route_pack's ctr[world * KAD_ROUTE_CSTRIDE + 1] is meant for
- *   it), and the caller runs the batch's way back unpacked.
+ *   sticky word *escape (not cleared by the call; kad_route_pack's ctr[KAD_ROUTE_OVERFLOW_WORD(world) + 1] is meant
+ *   for it), and the caller runs the batch's way back unpacked.
  * kad_route_unpack_packed: as kad_route_unpack, from packed rows in the send layout. Async on stream. */
 #define KAD_ROUTE_PACKED_MAX_COUNT 32u
 #define KAD_ROUTE_PACKED_WORDS(count) (1u + ((count) + 3u) / 4u)

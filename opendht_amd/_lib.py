@@ -54,6 +54,18 @@ KAD_SHARD_MAX_WORLD = 16
 KAD_ROUTE_CSTRIDE = 32
 KAD_ROUTE_MAX_WORLD = 16
 KAD_ROUTE_PACKED_MAX_COUNT = 32
+KAD_ROUTE_SUBS = 8
+KAD_ROUTE_QPW = 1024
+
+
+def route_ctr_words(world: int) -> int:
+    """KAD_ROUTE_CTR_WORDS(world)"""
+    return (world * KAD_ROUTE_SUBS + 1) * KAD_ROUTE_CSTRIDE
+
+
+def route_overflow_word(world: int) -> int:
+    """KAD_ROUTE_OVERFLOW_WORD(world)"""
+    return world * KAD_ROUTE_SUBS * KAD_ROUTE_CSTRIDE
 
 
 def route_packed_words(count: int) -> int:

@@ -5,8 +5,8 @@
 // pieces of that exchange, so that it needs no host read per batch:
 //   route_pack_kernel   targets -> `world` fixed-size send blocks (the owner's block), each query's place recorded;
 //                       per-workgroup counts in LDS (one LDS atomic per wave and owner), one global atomic per
-//                       (workgroup, owner); a full block sets a sticky overflow word (the caller grows the blocks
-//                       and runs the batch again)
+//                       (workgroup, owner) on the counter of the workgroup's sub-block (8 per block); a full
+//                       sub-block sets a sticky overflow word (the caller grows the blocks and runs the batch again)
 //   route_unpack_kernel rows that came back in the send layout -> each query's original position
 //   route_compress_kernel / route_unpack_packed_kernel: the rows travel back packed (the smallest index + one byte
 //                       per entry: 12 bytes for count 8 instead of 33); a row spanning more than 254 indices sets a
@@ -24,7 +24,7 @@ int set_error(int code, const char* msg);
 
 namespace {
 
-constexpr uint32_t BLOCK = 256, QPT = 4;  // queries per thread: a workgroup packs 1,024 targets
+constexpr uint32_t BLOCK = 256, QPT = KAD_ROUTE_QPW / BLOCK;  // queries per thread: a workgroup packs 1,024 targets
 constexpr uint32_t NONE = 0xFFFFFFFFu;
 typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
 
@@ -64,7 +64,10 @@ __global__ __launch_bounds__(BLOCK) void route_pack_kernel(const uint8_t* __rest
         }
     }
     __syncthreads();
-    if (tid < world) hbase[tid] = hcnt[tid] ? atomicAdd(ctr + tid * KAD_ROUTE_CSTRIDE, hcnt[tid]) : 0u;
+    // the workgroup's sub-block of each block: KAD_ROUTE_SUBS counters per block instead of one for every workgroup
+    const uint32_t sub = cap / KAD_ROUTE_SUBS, rg = blockIdx.x % KAD_ROUTE_SUBS;
+    if (tid < world)
+        hbase[tid] = hcnt[tid] ? atomicAdd(ctr + (tid * KAD_ROUTE_SUBS + rg) * KAD_ROUTE_CSTRIDE, hcnt[tid]) : 0u;
     __syncthreads();
 #pragma unroll
     for (uint32_t r = 0; r < QPT; r++) {
@@ -72,13 +75,13 @@ __global__ __launch_bounds__(BLOCK) void route_pack_kernel(const uint8_t* __rest
         if (dst[r] == NONE) continue;
         const uint32_t s = hbase[dst[r]] + pos[r];
         uint32_t out = NONE;
-        if (s < cap) {
-            out = dst[r] * cap + s;
+        if (s < sub) {
+            out = dst[r] * cap + rg * sub + s;
             uint32_t* o = reinterpret_cast<uint32_t*>(send + 20ull * out);
 #pragma unroll
             for (int x = 0; x < 5; x++) o[x] = w[r][x];
         } else {
-            atomicOr(ctr + world * KAD_ROUTE_CSTRIDE, 1u);
+            atomicOr(ctr + KAD_ROUTE_OVERFLOW_WORD(world), 1u);
         }
         __builtin_nontemporal_store(out, slot + i);
     }
@@ -273,11 +276,12 @@ extern "C" int kad_route_pack(const uint8_t* targets, uint32_t q, uint32_t world
     using kadgpu_internal::set_error;
     if (world == 0 || world > KAD_ROUTE_MAX_WORLD) return set_error(KAD_ERR_INVALID, "world must be 1..16");
     if (shard_bits > 8) return set_error(KAD_ERR_INVALID, "shard_bits must be 0..8");
-    if (cap == 0 || (uint64_t)world * cap >= NONE) return set_error(KAD_ERR_INVALID, "cap must be >= 1 and world * cap < 2^32 - 1");
+    if (cap == 0 || cap % KAD_ROUTE_SUBS || (uint64_t)world * cap >= NONE)
+        return set_error(KAD_ERR_INVALID, "cap must be a positive multiple of KAD_ROUTE_SUBS and world * cap < 2^32 - 1");
     if (!ctr || (q && (!targets || !send || !slot))) return set_error(KAD_ERR_INVALID, "NULL buffer");
     DevSwitch g(device);
     hipStream_t s = (hipStream_t)stream;
-    hipError_t e = hipMemsetAsync(ctr, 0, 4ull * (world + 1) * KAD_ROUTE_CSTRIDE, s);
+    hipError_t e = hipMemsetAsync(ctr, 0, 4ull * KAD_ROUTE_CTR_WORDS(world), s);
     if (e == hipSuccess && q) {
         const uint32_t nb = (uint32_t)(((uint64_t)q + BLOCK * QPT - 1) / (BLOCK * QPT));
         hipLaunchKernelGGL(route_pack_kernel, dim3(nb), dim3(BLOCK), 0, s, targets, q, world, shard_bits, cap, send,

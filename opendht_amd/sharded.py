@@ -287,30 +287,36 @@ class OwnerRoute:
     expands them; a row spanning more than 254 indices sets a sticky word (escaped()), and the batch's way back
     runs again unpacked.
 
-    cap: records per block; default q / world + 6 sigma + 256 of uniform targets. A block that fills sets a sticky
-    word; overflowed() combines it over the ranks (one host read per batch, or per K steps), grown() sizes the
-    blocks from the counts, and the batch runs again. collective=True forces the collectives at world 1 (a one-rank
+    cap: records per block, a multiple of KAD_ROUTE_SUBS: a block is 8 sub-blocks, workgroup w (1,024 targets)
+    appending to sub-block w % 8; default 8 x (the most targets one sub-block's workgroups hold / world + 6 sigma +
+    32) for uniform targets. A sub-block that fills sets a sticky word; overflowed() combines it over the ranks (one
+    host read per batch, or per K steps), grown() sizes the blocks from the counts, and the batch runs again. collective=True forces the collectives at world 1 (a one-rank
     RCCL group)."""
 
     def __init__(self, q: int, count: int, world: int, shard_bits: int, device, cap: int | None = None,
                  collective: bool | None = None, packed: bool | None = None):
         import torch
 
-        from ._lib import KAD_ROUTE_PACKED_MAX_COUNT, route_packed_words
+        from ._lib import KAD_ROUTE_PACKED_MAX_COUNT, KAD_ROUTE_QPW, KAD_ROUTE_SUBS, route_ctr_words, route_packed_words
 
         self.q, self.count, self.world, self.shard_bits, self.dev = q, count, world, shard_bits, device
         # packed by default for the counts the vector kernels take (multiples of 4 up to 32: count 8 packs in 11.7 us
         # and unpacks in 8.3 us per 1M rows, against 13.1 us for the plain unpack; tools/route_packed_check.py)
         self.packed = (count % 4 == 0 and 1 <= count <= KAD_ROUTE_PACKED_MAX_COUNT) if packed is None else bool(packed)
         self.collective = world > 1 if collective is None else bool(collective)
-        nominal = -(-q // world)
-        self.cap_max = max(1, q)
-        self.cap = max(1, min(self.cap_max, cap or nominal + 6 * int(np.sqrt(nominal)) + 256))
+        # the most targets the workgroups of one sub-block hold (workgroup w -> sub-block w % 8): a sub-block can never
+        # receive more, so 8 x that is the capacity that never overflows
+        S = KAD_ROUTE_SUBS
+        qs = min(max(q, 1), -(-(-(-q // KAD_ROUTE_QPW)) // S) * KAD_ROUTE_QPW)
+        self.cap_max = S * max(1, qs)
+        nominal = -(-qs // world)
+        sub = cap if cap is None else -(-cap // S)
+        self.cap = S * max(1, min(qs, sub or nominal + 6 * int(np.sqrt(nominal)) + 32))
         n = world * self.cap
         self.send = torch.empty((n, 20), dtype=torch.uint8, device=device)
         self.recv = torch.empty_like(self.send) if self.collective else self.send
         self.slot = torch.empty((max(q, 1),), dtype=torch.int32, device=device)
-        self.ctr = torch.zeros(((world + 1) * 32,), dtype=torch.int32, device=device)
+        self.ctr = torch.zeros((route_ctr_words(world),), dtype=torch.int32, device=device)
         self.rows = torch.empty((n, max(count, 1)), dtype=torch.int32, device=device)
         self.cnt = torch.empty((n,), dtype=torch.uint8, device=device)
         self.back_rows = torch.empty_like(self.rows) if self.collective else self.rows
@@ -344,14 +350,14 @@ class OwnerRoute:
               "kad_route_unpack")
 
     def compress(self, stream):
-        """The answered rows packed for the way back (escape word: ctr[world * 32 + 1])."""
+        """The answered rows packed for the way back (escape word: ctr[KAD_ROUTE_OVERFLOW_WORD(world) + 1])."""
         import ctypes as C
 
-        from ._lib import check, lib, ptr
+        from ._lib import check, lib, ptr, route_overflow_word
 
         n = self.world * self.cap
         check(lib().kad_route_compress(ptr(self.rows), ptr(self.cnt), n, self.count, ptr(self.prow),
-                                       C.c_void_p(self.ctr.data_ptr() + 4 * (self.world * 32 + 1)),
+                                       C.c_void_p(self.ctr.data_ptr() + 4 * (route_overflow_word(self.world) + 1)),
                                        self.dev.index or 0, C.c_void_p(stream)), "kad_route_compress")
 
     def unpack_packed(self, out_idx, out_cnt, stream):
@@ -405,11 +411,15 @@ class OwnerRoute:
         """Host read of the packing escape word (a row spanning more than 254 indices), combined over the ranks."""
         if not self.packed:
             return False
-        return self._flag(self.world * 32 + 1, group, combine)
+        from ._lib import route_overflow_word
+
+        return self._flag(route_overflow_word(self.world) + 1, group, combine)
 
     def overflowed(self, group=None, combine: bool = True) -> bool:
         """Host read of the sticky overflow word, combined over the ranks (every rank decides the same)."""
-        return self._flag(self.world * 32, group, combine)
+        from ._lib import route_overflow_word
+
+        return self._flag(route_overflow_word(self.world), group, combine)
 
     def _flag(self, w: int, group, combine: bool) -> bool:
         ov = self.ctr[w:w + 1]
@@ -425,10 +435,10 @@ class OwnerRoute:
         return bool(int(ov.item()))
 
     def need(self, group=None) -> int:
-        """The largest block count of the last pack, combined over the ranks."""
+        """The block capacity the last pack needed (8 x its fullest sub-block), combined over the ranks."""
         import torch
 
-        n = int(self.ctr.view(self.world + 1, 32)[:self.world, 0].max().item())
+        n = need_of(self.ctr, self.world)
         if self.collective:
             import torch.distributed as dist
 
@@ -443,6 +453,14 @@ class OwnerRoute:
         return OwnerRoute(self.q, self.count, self.world, self.shard_bits, self.dev,
                           cap=min(self.cap_max, max(2 * self.cap, n * 5 // 4)), collective=self.collective,
                           packed=self.packed)
+
+
+def need_of(ctr, world: int) -> int:
+    """The block capacity a pack needed: KAD_ROUTE_SUBS x the fullest sub-block's record count."""
+    from ._lib import KAD_ROUTE_CSTRIDE, KAD_ROUTE_SUBS
+
+    c = ctr[:world * KAD_ROUTE_SUBS * KAD_ROUTE_CSTRIDE].view(world * KAD_ROUTE_SUBS, KAD_ROUTE_CSTRIDE)[:, 0]
+    return KAD_ROUTE_SUBS * int(c.max().item())
 
 
 def _all_to_all(recv, send, group=None):
@@ -501,9 +519,9 @@ def route_simulated(tables, batches, count: int, shard_bits: int, cap: int | Non
         c = routes[0].cap
         for r, b in zip(routes, batches):
             r.pack(b, s)
-        over = any(bool(int(r.ctr[world * 32].item())) for r in routes)
+        over = any(r.overflowed(combine=False) for r in routes)
         if over:
-            cap = max(2 * c, max(int(r.ctr.view(world + 1, 32)[:world, 0].max().item()) for r in routes) * 5 // 4)
+            cap = max(2 * c, max(need_of(r.ctr, world) for r in routes) * 5 // 4)
             continue
         answered = []
         for d in range(world):
@@ -520,7 +538,7 @@ def route_simulated(tables, batches, count: int, shard_bits: int, cap: int | Non
                 R.rows, R.cnt = answered[d]
                 R.compress(s)
                 packs.append(R.prow.clone())
-            escaped = any(bool(int(R.ctr[world * 32 + 1].item())) for R in routes)
+            escaped = any(R.escaped(combine=False) for R in routes)
         out = []
         for src, r in enumerate(routes):
             oi = torch.empty((r.q, count), dtype=torch.int32, device=dev)

@@ -56,7 +56,7 @@ def test_owner_route_simulated(gpu, world, small_cap, packed):
                                       packed=packed)
             torch.cuda.synchronize()
             if small_cap:
-                assert r0.cap > 1  # it grew
+                assert r0.cap > 8  # it grew (cap 1 -> one record per sub-block)
             if packed:
                 assert not r0.sim_escaped  # (60 % good: every window spans far fewer than 255 nodes)
             for r, (oi, oc) in enumerate(out):
@@ -70,22 +70,27 @@ def test_owner_route_simulated(gpu, world, small_cap, packed):
 
 
 def test_route_pack_layout(gpu):
-    """kad_route_pack places every target in its owner's block once, counts each block, flags a full block."""
+    """kad_route_pack places every target in its owner's block once (in its workgroup's sub-block), counts each
+    sub-block, flags a full one."""
     q, world, bits = 5000, 4, 2
     t = torch.randint(0, 256, (q, 20), dtype=torch.uint8, device=gpu)
-    R = OwnerRoute(q, 8, world, bits, gpu, cap=q)
+    R = OwnerRoute(q, 8, world, bits, gpu, cap=8 * 1024)
     s = torch.cuda.current_stream(gpu).cuda_stream
     R.pack(t, s)
     torch.cuda.synchronize()
     owner = (t[:, 0].to(torch.int64) >> (8 - bits)) % world
     slot = R.slot.cpu().numpy().view(np.uint32).astype(np.int64)
-    cnts = R.ctr.view(world + 1, 32)[:, 0].cpu().numpy()
-    assert cnts[world] == 0
-    np.testing.assert_array_equal(cnts[:world], torch.bincount(owner, minlength=world).cpu().numpy())
-    np.testing.assert_array_equal(slot // q, owner.cpu().numpy())
+    subs = R.ctr[:world * 8 * 32].view(world * 8, 32)[:, 0].cpu().numpy().reshape(world, 8)
+    assert not R.overflowed(combine=False)
+    np.testing.assert_array_equal(subs.sum(1), torch.bincount(owner, minlength=world).cpu().numpy())
+    cap = R.cap
+    np.testing.assert_array_equal(slot // cap, owner.cpu().numpy())
+    # workgroup w (1,024 targets) appends to sub-block w % 8 of its owner's block
+    np.testing.assert_array_equal((slot % cap) // (cap // 8), (np.arange(q) // 1024) % 8)
+    assert int(subs[:, 5:].sum()) == 0  # (5,000 targets: workgroups 0..4)
     assert np.unique(slot).size == q
     np.testing.assert_array_equal(R.send[torch.from_numpy(slot).to(gpu)].cpu().numpy(), t.cpu().numpy())
-    R2 = OwnerRoute(q, 8, world, bits, gpu, cap=q // world // 2)
+    R2 = OwnerRoute(q, 8, world, bits, gpu, cap=8 * 100)
     R2.pack(t, s)
     torch.cuda.synchronize()
     assert R2.overflowed(combine=False)
