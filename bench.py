@@ -560,6 +560,7 @@ def owner_routed_pass(T, sh, spec, Q, cnt_k, K, W, dev, dist, world, rank, NB=4)
         esc = R.escaped()  # (a row too wide to pack in some step: the last batch's way back again, unpacked)
         last = tgs[(K - 1) % NB]
         if esc:
+            R.answer(T, s, packed=False)
             R.back(oi, oc, None, s, packed=False)
             torch.cuda.synchronize(dev)
         # the rows of this rank's own targets in the last step, against the restatement on its shard table
@@ -590,8 +591,8 @@ def owner_step_model(T, Q, cnt_k, dev, stream, avg_kernel_s, link_gbs=64.0, lat_
     to every other rank over its own xGMI link at link_gbs GB/s, lat_us per collective (targets: one; rows and
     counts: two). serial = pack + targets + query + rows + unpack; overlapped = the compute and the exchanges of
     consecutive batches on two streams, max(pack + query + unpack, exchanges). `packed`: the same with the rows
-    back packed (kad_route_compress, one collective of KAD_ROUTE_PACKED_WORDS(k) words per row,
-    kad_route_unpack_packed)."""
+    back packed (written packed by the query kernel at count 8 — kad_rt_closest_batch_packed —, by kad_route_compress
+    otherwise; one collective of KAD_ROUTE_PACKED_WORDS(k) words per row; kad_route_unpack_packed)."""
     import torch
 
     from opendht_amd.sharded import OwnerRoute
@@ -637,15 +638,21 @@ def owner_step_model(T, Q, cnt_k, dev, stream, avg_kernel_s, link_gbs=64.0, lat_
              "step_serial_us": serial, "step_overlapped_us": overlap,
              "aggregate_queries_per_s_serial": n * Q / (serial * 1e-6),
              "aggregate_queries_per_s_overlapped": n * Q / (overlap * 1e-6)}
-        if R.packed:  # the rows back packed: kad_route_compress + one collective + kad_route_unpack_packed
-            compress_us = timed(lambda: R.compress(s))
+        if R.packed:  # the rows back packed: one collective of packed rows + kad_route_unpack_packed
+            R.send, R.recv = recv, recv  # (answer() reads the received block from recv)
+            query_p_us = timed(lambda: R.answer(T, s))  # count 8: the query kernel writes packed rows
+            fused = R.fused
+            compress_us = 0.0 if fused else timed(lambda: R.compress(s))
             esc = R.escaped(combine=False)
             unpack_p_us = timed(lambda: R.unpack_packed(oi, oc, s))
             x_p = lat_us + 4 * R.pw * R.cap / (link_gbs * 1e3)
-            serial_p = pack_us + x_t + query_us + compress_us + x_p + unpack_p_us
-            overlap_p = max(pack_us + query_us + compress_us + unpack_p_us, x_t + x_p)
-            e["packed"] = {"row_bytes": 4 * R.pw, "escaped": esc, "compress_us": compress_us,
-                           "unpack_us": unpack_p_us, "xgmi_rows_bytes": 4 * R.pw * (n - 1) * R.cap,
+            qp = (query_p_us if fused else query_us) + compress_us
+            serial_p = pack_us + x_t + qp + x_p + unpack_p_us
+            overlap_p = max(pack_us + qp + unpack_p_us, x_t + x_p)
+            e["packed"] = {"row_bytes": 4 * R.pw, "escaped": esc,
+                           "query_us": query_p_us if fused else None, "fused": fused,
+                           "compress_us": compress_us, "unpack_us": unpack_p_us,
+                           "xgmi_rows_bytes": 4 * R.pw * (n - 1) * R.cap,
                            "exchange_rows_modelled_us": x_p, "step_serial_us": serial_p,
                            "step_overlapped_us": overlap_p,
                            "aggregate_queries_per_s_serial": n * Q / (serial_p * 1e-6),

@@ -480,6 +480,13 @@ int kad_route_compress(const uint32_t* idx, const uint8_t* cnt, uint32_t n, uint
                        uint32_t* escape, int device, void* stream);
 int kad_route_unpack_packed(const uint32_t* slot, uint32_t q, uint32_t count, const uint32_t* back_packed,
                             uint32_t* out_idx, uint8_t* out_cnt, int device, void* stream);
+/* kad_rt_closest_batch_packed: kad_rt_closest_batch with each row written packed (the layout above, word 0 a base
+ * no larger than any entry) by the query kernel itself: no full row is written and read back by kad_route_compress.
+ * Count 8 on tables with short window lines only (KAD_ERR_UNSUPPORTED otherwise: use kad_rt_closest_batch +
+ * kad_route_compress). A row whose indices span more than 254 sets *escape and writes nothing for it: the caller
+ * answers the batch again unpacked. Async on stream. */
+int kad_rt_closest_batch_packed(const kad_table* t, const uint8_t* targets, uint32_t q, uint32_t count,
+                                uint32_t* packed, uint32_t* escape, void* stream);
 
 /* ---- wire step after the query ------------------------ */
 #define KAD_SEND_NODES 8u           /* reference network_engine.cpp:59 SEND_NODES */

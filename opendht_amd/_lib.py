@@ -80,6 +80,7 @@ def shard_block_words(count: int, row_cap: int, part_cap: int) -> int:
 
 
 KAD_ERR_NOMEM = -3
+KAD_ERR_UNSUPPORTED = -4
 
 ERRORS = {
     -1: "KAD_ERR_INVALID",
@@ -144,6 +145,7 @@ SIGNATURES = {
     "kad_route_pack": (C.c_int, [_P, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, _P, _P, _P, C.c_int, _P]),
     "kad_route_unpack": (C.c_int, [_P, C.c_uint32, C.c_uint32, _P, _P, _P, _P, C.c_int, _P]),
     "kad_route_compress": (C.c_int, [_P, _P, C.c_uint32, C.c_uint32, _P, _P, C.c_int, _P]),
+    "kad_rt_closest_batch_packed": (C.c_int, [_P, _P, C.c_uint32, C.c_uint32, _P, _P, _P]),
     "kad_route_unpack_packed": (C.c_int, [_P, C.c_uint32, C.c_uint32, _P, _P, _P, C.c_int, _P]),
     "kad_table_set_addrs": (C.c_int, [_P, C.c_uint32, _P]),
     "kad_buffer_nodes_batch": (C.c_int, [_P, _P, C.c_uint32, _P, _P, C.c_uint32, _P, _P, _P]),

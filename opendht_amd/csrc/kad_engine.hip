@@ -1355,6 +1355,86 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     rt_ws_kernel_body<ABL, NTS, CR>(T, targets, q, count, out_idx, out_cnt);
 }
 
+// Count 8 with the row written packed for owner routing's way back (kad_rt_closest_batch_packed; KAD_ROUTE_PACKED_WORDS
+// (8) = 3 words: a base index, then one byte per entry, index - base, 0xFF past the count): the short line's answer,
+// else the 128-byte line's, else the exact path's (by the wave, into LDS), packed in the kernel, so that no row of 33
+// bytes is written and read again. A row wider than 254 indices sets *escape and writes nothing: the caller answers
+// that batch again unpacked.
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) void rt_ws_packed_kernel(
+    DevTable T, const uint8_t* __restrict__ targets, uint32_t q, uint32_t* __restrict__ packed,
+    uint32_t* __restrict__ escape) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    const bool act = i < q;
+    Target t{};
+    uint32_t b = 0;
+    if (act) {
+        t.hi = load_target_hi(targets, i);
+        b = locate_bucket(T, t);
+    }
+    uint32_t o[8], m;
+    bool ok = ws_answer<0>(T, t, b, 8u, act, o, m);
+    bool need = act && !ok;
+    if (__any(need)) {  // the 128-byte line of the (few) queries the short line cannot answer
+        uint32_t o2[8], m2;
+        const bool ok2 = wl_answer<0>(T, t, b, 8u, need, o2, m2);
+        if (need && ok2) {
+#pragma unroll
+            for (int j = 0; j < 8; j++) o[j] = o2[j];
+            m = m2;
+            ok = true;
+        }
+        need = need && !ok2;
+    }
+    if (__any(need)) {  // the exact path, one query at a time by the wave, its row in LDS
+        __shared__ uint64_t xs[BLOCK / 64][192];
+        __shared__ uint32_t xrow[BLOCK / 64][8];
+        __shared__ uint8_t xcnt[BLOCK / 64];
+        const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+        if (need) t = load_target(targets, i);
+        for (uint64_t mm = __ballot(need); mm; mm &= mm - 1) {
+            const uint32_t l = (uint32_t)__builtin_ctzll(mm);
+            Target u;
+            u.hi = rdl64(t.hi, l);
+            u.t2 = rdl(t.t2, l);
+            u.t3 = rdl(t.t3, l);
+            u.t4 = rdl(t.t4, l);
+            wave_exact(T, u, 8u, xrow[w], &xcnt[w], xs[w]);
+            __builtin_amdgcn_wave_barrier();
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_wave_barrier();
+            if (lane == l) {
+#pragma unroll
+                for (int j = 0; j < 8; j++) o[j] = xrow[w][j];
+                m = xcnt[w];
+                ok = true;
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+    if (!act) return;
+    uint32_t lo = NONE, hi = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++)
+        if ((uint32_t)j < m) {
+            lo = min(lo, o[j]);
+            hi = max(hi, o[j]);
+        }
+    if (!ok || (m && hi - lo > 254u)) {
+        atomicOr(escape, 1u);
+        return;
+    }
+    uint32_t w1 = 0, w2 = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        w1 |= ((uint32_t)j < m ? o[j] - lo : 255u) << (8 * j);
+        w2 |= ((uint32_t)j + 4 < m ? o[j + 4] - lo : 255u) << (8 * j);
+    }
+    uint32_t* pr = packed + 3ull * i;
+    __builtin_nontemporal_store(lo, pr);
+    __builtin_nontemporal_store(w1, pr + 1);
+    __builtin_nontemporal_store(w2, pr + 2);
+}
+
 // The count <= 8 line answer for kernels that serve other paths too (dual-family, shard): lanes with `ws`
 // (their table has short lines) try the 64-byte line, lanes with `act` it did not answer read the 128-byte
 // line. Same contract as wl_answer; call from uniform control flow.
@@ -8733,6 +8813,21 @@ int kad_rt_closest_batch(const kad_table* t, const uint8_t* targets, uint32_t q,
     if (((uintptr_t)targets & 3) || ((uintptr_t)out_idx & 3)) return set_err(KAD_ERR_INVALID, "device buffers must be 4-byte aligned");
     DeviceGuard g(t->device);
     return rt_dispatch(t, targets, q, count, out_idx, out_cnt, (hipStream_t)stream);
+}
+
+int kad_rt_closest_batch_packed(const kad_table* t, const uint8_t* targets, uint32_t q, uint32_t count,
+                                uint32_t* packed, uint32_t* escape, void* stream) {
+    if (!t) return set_err(KAD_ERR_INVALID, "NULL table");
+    if (count != 8 || !(t->d.flags & TF_WS) || std::getenv("KAD_RT_KERNEL"))
+        return set_err(KAD_ERR_UNSUPPORTED, "packed rows: count 8 on tables with short window lines only");
+    if (q == 0) return KAD_OK;
+    if (!targets || !packed || !escape) return set_err(KAD_ERR_INVALID, "NULL buffer");
+    if (((uintptr_t)targets & 3) || ((uintptr_t)packed & 3)) return set_err(KAD_ERR_INVALID, "device buffers must be 4-byte aligned");
+    DeviceGuard g(t->device);
+    hipLaunchKernelGGL(rt_ws_packed_kernel, dim3(grid_for(q)), dim3(BLOCK), 0, (hipStream_t)stream, t->d, targets, q,
+                       packed, escape);
+    HIP_TRY(hipGetLastError());
+    return KAD_OK;
 }
 
 int kad_rt_closest_batch_dual(const kad_table* t4, const kad_table* t6, const uint8_t* targets, const uint8_t* af,

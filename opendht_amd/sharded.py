@@ -282,9 +282,10 @@ class OwnerRoute:
               are never read back)
       return  all_to_all_single of the row and count blocks, back to the senders
       unpack  kad_route_unpack: each query's row to its original position
-    packed (the default for counts 4, 8, ..., 32): the rows go back packed (kad_route_compress: the row's smallest index and a
-    byte per entry, 12 bytes for count 8 instead of 33; one collective instead of two) and kad_route_unpack_packed
-    expands them; a row spanning more than 254 indices sets a sticky word (escaped()), and the batch's way back
+    packed (the default for counts 4, 8, ..., 32): the rows go back packed (a base index and a byte per entry, 12 bytes
+    for count 8 instead of 33; one collective instead of two) — written packed by the query kernel itself at count 8
+    on tables with short window lines (kad_rt_closest_batch_packed), by kad_route_compress otherwise — and
+    kad_route_unpack_packed expands them; a row spanning more than 254 indices sets a sticky word (escaped()), and the batch's way back
     runs again unpacked.
 
     cap: records per block, a multiple of KAD_ROUTE_SUBS: a block is 8 sub-blocks, workgroup w (1,024 targets)
@@ -369,8 +370,23 @@ class OwnerRoute:
                                             ptr(out_cnt), self.dev.index or 0, C.c_void_p(stream)),
               "kad_route_unpack_packed")
 
-    def answer(self, table, stream):
-        """The owner's rows for every record of the received blocks (table: a DeviceTable)."""
+    def answer(self, table, stream, packed: bool | None = None):
+        """The owner's rows for every record of the received blocks (table: a DeviceTable). Packed rows at count 8 on
+        a table with short window lines come packed out of the query kernel itself (kad_rt_closest_batch_packed:
+        `fused`); otherwise full rows, packed by compress() on the way back."""
+        import ctypes as C
+
+        from ._lib import KAD_ERR_UNSUPPORTED, check, lib, ptr, route_overflow_word
+
+        self.fused = False
+        if (self.packed if packed is None else packed) and self.count == 8:
+            rc = lib().kad_rt_closest_batch_packed(
+                table._h, ptr(self.recv), self.world * self.cap, self.count, ptr(self.prow),
+                C.c_void_p(self.ctr.data_ptr() + 4 * (route_overflow_word(self.world) + 1)), C.c_void_p(stream))
+            if rc != KAD_ERR_UNSUPPORTED:
+                check(rc, "kad_rt_closest_batch_packed")
+                self.fused = True
+                return
         table.rt_closest(self.recv, self.count, out_idx=self.rows, out_cnt=self.cnt, stream=stream)
 
     def step(self, table, targets, out_idx, out_cnt, group=None, stream=None, packed: bool | None = None):
@@ -381,12 +397,13 @@ class OwnerRoute:
         from .global_shard import _torch_stream
 
         s = stream if stream is not None else torch.cuda.current_stream(self.dev).cuda_stream
+        packed = self.packed if packed is None else packed
         self.pack(targets, s)
         if self.collective:
             with torch.cuda.stream(_torch_stream(s, self.dev)):
                 _all_to_all(self.recv, self.send, group)
-        self.answer(table, s)
-        self.back(out_idx, out_cnt, group, s, self.packed if packed is None else packed)
+        self.answer(table, s, packed)
+        self.back(out_idx, out_cnt, group, s, packed)
 
     def back(self, out_idx, out_cnt, group, s, packed: bool):
         """The way back of the answered rows: return + unpack (packed or not)."""
@@ -395,7 +412,8 @@ class OwnerRoute:
         from .global_shard import _torch_stream
 
         if packed:
-            self.compress(s)
+            if not getattr(self, "fused", False):
+                self.compress(s)
             if self.collective:
                 with torch.cuda.stream(_torch_stream(s, self.dev)):
                     _all_to_all(self.back_prow, self.prow, group)
@@ -496,6 +514,7 @@ def serve_owner(table, targets, count: int, route: OwnerRoute | None = None, gro
                 import torch as _t
 
                 s = stream if stream is not None else _t.cuda.current_stream(targets.device).cuda_stream
+                route.answer(table, s, packed=False)  # (the received targets are still in place)
                 route.back(out_idx, out_cnt, group, s, packed=False)
             return out_idx, out_cnt, route
         route = route.grown(group)

@@ -126,6 +126,36 @@ def test_owner_route_packed_escape(gpu):
             T.close()
 
 
+@pytest.mark.parametrize("good_pct", [80, 2], ids=["u80", "mostly_bad"])
+def test_owner_route_fused_packed_rows(gpu, good_pct):
+    """Count 8 on a table with short window lines: the query kernel writes the rows packed
+    (kad_rt_closest_batch_packed, no compress pass). On a 2 %-good table most windows span hundreds of nodes, the
+    rows escape packing and serve_owner answers the batch again unpacked. One rank, every row against the oracle."""
+    from opendht_amd.sharded import serve_owner
+
+    spec = ShardSpec(n_shards=1, depth=10, mean_per_bucket=6.0, seed=0xF5 + good_pct, good_pct=good_pct,
+                     expired_pct=(100 - good_pct) // 2)
+    gids, gst, goff = spec.bucket_range(0, spec.n_buckets)
+    gfirst = S.bucket_firsts(spec.depth, 0, spec.n_buckets)
+    sh = build_shard(spec, 0)
+    T = DeviceTable(sh.ids, sh.status, sh.first, sh.off, device=0, index_base=sh.index_base, sorted=True)
+    try:
+        targets = _batch(spec, 3000, seed=90 + good_pct)
+        tg = torch.from_numpy(targets).to(gpu)
+        R = OwnerRoute(tg.shape[0], 8, 1, 0, gpu)
+        oi, oc, R = serve_owner(T, tg, 8, route=R)
+        torch.cuda.synchronize()
+        if good_pct == 2:
+            assert R.escaped(combine=False) and not R.fused  # could not pack them: answered again unpacked
+        else:
+            assert R.fused and not R.escaped(combine=False)  # the kernel wrote the packed rows
+        want, wcnt = O.flat_rt_closest(gids, gst, gfirst, goff, targets, 8, nthreads=8)
+        np.testing.assert_array_equal(oc.cpu().numpy(), wcnt)
+        np.testing.assert_array_equal(oi.cpu().numpy().view(np.uint32), want)
+    finally:
+        T.close()
+
+
 def _free_port():
     with socket.socket() as so:
         so.bind(("127.0.0.1", 0))
