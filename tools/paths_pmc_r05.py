@@ -7,7 +7,8 @@ per run, so that each rocprofv3 --pmc pass stays short:
            1M batch into 8 home blocks (k = 8 and 32), gather_scatter_link_kernel + gather_merge_kernel over 8 blocks
   swarm    config 5 at 2M peers: search_init / search_query / search_merge over 256k lookups to convergence
   refresh  the live refresh: rf_nodes_kernel over 300 refreshes of the bench shard at a moving `now`
-  route    the owner-routed serving form: route_pack_kernel (N = 8), route_unpack_kernel (k = 8)
+  route    the owner-routed serving form: route_pack_kernel (N = 8), route_unpack_kernel (k = 8), the owner's query with
+           packed rows (rt_ws_packed_kernel) over 8 received blocks, route_unpack_packed4_kernel
 Every launch reads a different batch (8 rotated batches of 1M targets). Prints the per-launch times (HIP events,
 median of REPS) as one JSON object."""
 import ctypes as C
@@ -169,6 +170,15 @@ def mode_route():
     R.rows.random_(0, 1 << 20)
     R.cnt.fill_(8)
     run("route_unpack_k8_us", lambda t: R.unpack(oi, oc, s), tgs)
+    # the owner's query with packed rows (rt_ws_packed_kernel) over the 8 blocks it receives, and the packed unpack
+    sh = build_shard(config3_spec(), 0)
+    T = DeviceTable(sh.ids, sh.status, sh.first, sh.off, device=0, index_base=sh.index_base, sorted=True)
+    own = batches(top3=0, seed=15)
+    R.recv = R.send = torch.cat([t[:R.cap] for t in own])[:8 * R.cap]
+    run("route_answer_packed_k8_us", lambda t: R.answer(T, s), tgs)
+    res["route_answer_fused"] = bool(R.fused)
+    run("route_unpack_packed_k8_us", lambda t: R.unpack_packed(oi, oc, s), tgs)
+    T.close()
 
 
 if __name__ == "__main__":

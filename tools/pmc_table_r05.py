@@ -38,7 +38,9 @@ KERNELS = [  # (label, mode, kernel-name substring, what)
     ("search_merge", "swarm", "search_merge_kernel", "config 5 hop: insertNode merge per lookup"),
     ("rf_nodes<true,1>", "refresh", "rf_nodes_kernel<true, 1>", "fused small refresh, 1..100 deadlines"),
     ("route_pack", "route", "route_pack_kernel", "owner routing: pack 1M targets into 8 blocks"),
-    ("route_unpack", "route", "route_unpack_kernel", "owner routing: rows back, k=8"),
+    ("route_unpack", "route", "route_unpack_kernel<", "owner routing: rows back, k=8"),
+    ("rt_ws_packed", "route", "rt_ws_packed_kernel", "owner routing: the owner's k=8 query, rows written packed"),
+    ("route_unpack_packed", "route", "route_unpack_packed4_kernel", "owner routing: packed rows back, k=8"),
 ]
 
 
