@@ -2,8 +2,8 @@
 // "nothing in reach" case (not product code).
 // Build: hipcc --offload-arch=gfx950 -O3 tools/mb_stream.hip -o tools/mb_stream.bin
 //   empty      : the shard kernel's grid (q / 1,024 workgroups of 256), no memory work: dispatch + drain
-//   lds<NR>    : the shard kernel's load: 256 * NR targets per workgroup as 16-byte non-temporal loads into LDS, one
-//                compare per target (the reach test), NR = 4 (1,024 per workgroup) or 8
+//   lds<NR,PAD>: the shard kernel's load: 256 * NR targets per workgroup as 16-byte non-temporal loads into LDS, one
+//                compare per target (the reach test), NR = 2, 4 (1,024 per workgroup) or 8; PAD more LDS words held
 //   reg<U>     : grid-stride 16-byte loads into registers, U per thread in flight, folded; grid = G workgroups
 // Each case: `bufs` distinct batches rotated (so the Infinity Cache holds some, as in the shard runs), 200 launches
 // timed between two events, plus each launch alone between events (median), µs per launch.
@@ -29,10 +29,10 @@ __global__ __launch_bounds__(256) void k_empty(uint32_t* flag, uint32_t v) {
     if (v == 0x5EEDF00Du && threadIdx.x == 0) flag[blockIdx.x] = v;
 }
 
-template <uint32_t NR>
+template <uint32_t NR, uint32_t PAD = 0>
 __global__ __launch_bounds__(256) void k_lds(const uint8_t* __restrict__ tg, uint32_t q, uint64_t lo, uint64_t hi,
                                              uint32_t* flag) {
-    __shared__ __attribute__((aligned(16))) uint32_t st[256 * NR * 5];
+    __shared__ __attribute__((aligned(16))) uint32_t st[256 * NR * 5 + PAD];
     const uint32_t tid = threadIdx.x;
     const uint64_t base = (uint64_t)blockIdx.x * 256 * NR;
     const uint32_t nq = (uint32_t)std::min<uint64_t>(256 * NR, q - base);
@@ -48,6 +48,35 @@ __global__ __launch_bounds__(256) void k_lds(const uint8_t* __restrict__ tg, uin
     uint32_t hit = 0;
 #pragma unroll
     for (uint32_t r = 0; r < NR; r++) {
+        const uint32_t j = r * 256 + tid;
+        if (j < nq) {
+            const uint64_t h = ((uint64_t)__builtin_bswap32(st[5 * j]) << 32) | __builtin_bswap32(st[5 * j + 1]);
+            hit += h >= lo && h < hi;
+        }
+    }
+    if (PAD && hit == 0x5EEDF00Du) hit += st[256 * NR * 5 + PAD - 1 - tid];  // (keeps the pad)
+    if (hit) flag[blockIdx.x] = hit;
+}
+
+// k_lds<4> with at most 4 waves per SIMD (the occupancy of the shard kernel's 105 VGPRs)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 4))) void k_lds4_occ4(
+    const uint8_t* __restrict__ tg, uint32_t q, uint64_t lo, uint64_t hi, uint32_t* flag) {
+    __shared__ __attribute__((aligned(16))) uint32_t st[256 * 4 * 5];
+    const uint32_t tid = threadIdx.x;
+    const uint64_t base = (uint64_t)blockIdx.x * 1024;
+    const uint32_t nq = (uint32_t)std::min<uint64_t>(1024, q - base);
+    const u32x4_t* s4 = reinterpret_cast<const u32x4_t*>(tg + 20 * base);
+    u32x4_t* d4 = reinterpret_cast<u32x4_t*>(st);
+    const uint32_t n4 = 5 * nq / 4;
+#pragma unroll
+    for (uint32_t k = 0; k < 5; k++) {
+        const uint32_t x = tid + k * 256;
+        if (x < n4) d4[x] = __builtin_nontemporal_load(s4 + x);
+    }
+    __syncthreads();
+    uint32_t hit = 0;
+#pragma unroll
+    for (uint32_t r = 0; r < 4; r++) {
         const uint32_t j = r * 256 + tid;
         if (j < nq) {
             const uint64_t h = ((uint64_t)__builtin_bswap32(st[5 * j]) << 32) | __builtin_bswap32(st[5 * j + 1]);
@@ -123,6 +152,12 @@ int main(int argc, char** argv) {
     timeit("empty, q/1024 workgroups", bufs, [&](int) { k_empty<<<(q + 1023) / 1024, 256>>>(flag, 0); });
     timeit("lds NR=4 (the shard kernel's load)", bufs,
            [&](int i) { k_lds<4><<<(q + 1023) / 1024, 256>>>(tg[i], q, lo, hi, flag); });
+    timeit("lds NR=4 + 9 KB LDS (the shard kernel's 29 KB)", bufs,
+           [&](int i) { k_lds<4, 2304><<<(q + 1023) / 1024, 256>>>(tg[i], q, lo, hi, flag); });
+    timeit("lds NR=4 + 20 KB LDS", bufs,
+           [&](int i) { k_lds<4, 5120><<<(q + 1023) / 1024, 256>>>(tg[i], q, lo, hi, flag); });
+    timeit("lds NR=4, at most 4 waves per SIMD", bufs,
+           [&](int i) { k_lds4_occ4<<<(q + 1023) / 1024, 256>>>(tg[i], q, lo, hi, flag); });
     timeit("lds NR=8", bufs, [&](int i) { k_lds<8><<<(q + 2047) / 2048, 256>>>(tg[i], q, lo, hi, flag); });
     timeit("lds NR=2", bufs, [&](int i) { k_lds<2><<<(q + 511) / 512, 256>>>(tg[i], q, lo, hi, flag); });
     const uint64_t n4 = nb / 16;
