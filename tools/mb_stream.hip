@@ -40,7 +40,7 @@ __global__ __launch_bounds__(256) void k_lds(const uint8_t* __restrict__ tg, uin
     u32x4_t* d4 = reinterpret_cast<u32x4_t*>(st);
     const uint32_t n4 = 5 * nq / 4;
 #pragma unroll
-    for (uint32_t k = 0; k < 5 * NR / 4; k++) {
+    for (uint32_t k = 0; k < (5 * NR + 3) / 4; k++) {
         const uint32_t x = tid + k * 256;
         if (x < n4) d4[x] = __builtin_nontemporal_load(s4 + x);
     }
