@@ -349,8 +349,8 @@ int kad_nc_closest_batch_dual(const kad_table* table4, const kad_table* table6,
  * counters (device, KAD_SHARD_COUNTERS x KAD_SHARD_COUNTER_STRIDE uint32, zeroed by the caller;
  * counter k at word k*KAD_SHARD_COUNTER_STRIDE): rows appended per region (k < 8), parts appended
  * (k = 8), overflow flag (k = 9: a region or the parts buffer was full: grow and run again).
- * Rows of the queries [QB w, QB w + QB) go to region w % 8 (QB = 1024; 2048 in a tools-build A/B). A
- * query takes at most two rows: a query whose window line cannot answer it leaves a tombstone row (qid
+ * Rows of the queries [QB w, QB w + QB) go to region w % 8 (QB = 1024, or 256 for counts 17..32; 2048 in a
+ * tools-build A/B). A query takes at most two rows: a query whose window line cannot answer it leaves a tombstone row (qid
  * KAD_NO_NODE, skipped by every finish) beside its wave-path row or part, so row_cap >= 2*ceil(ceil(q/QB)/8)*QB
  * never overflows (home layout: W = ceil(ceil(q/256)/world/(QB/256)) + 1 workgroups per home range,
  * row_cap >= 2*ceil(W/8)*QB).

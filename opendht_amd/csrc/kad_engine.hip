@@ -3455,7 +3455,7 @@ __global__ __launch_bounds__(BLOCK) void rt_dual_wl32q_kernel(DevTable T4, DevTa
 // global one); the others take the wave-cooperative path on the global window.
 // Row layout (uint32): qid, m, 0, 0, idx[count] (padded to 4): KAD_ROW_WORDS(count).
 // Part layout: the row, then dist[count][5]: KAD_PART_WORDS(count).
-// Complete rows of workgroup w (QB = 1,024 or 2,048 queries, shard_qb) go to region w % 8 of KAD_SHARD_REGIONS
+// Complete rows of workgroup w (QB = 256, 1,024 or 2,048 queries, shard_qb) go to region w % 8 of KAD_SHARD_REGIONS
 // regions of row_cap rows: one atomic per workgroup and home rank for the window-line rows, eight counters per home
 // (a single counter hit by every wave cost ~10 ns per wave, 160 us per 1M queries). A query takes at most two rows (a
 // tombstone and its wave-path row), so row_cap >= 2 * ceil(W / 8) * QB never overflows, W = the workgroups holding
@@ -3496,10 +3496,25 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
-// Queries per workgroup of rt_shard_kernel<LK>: 1,024. (The count 17..32 kernel holds 193 VGPRs, two waves per SIMD,
-// so 1,024 workgroups of 1,024 take two rounds; 512 of 2,048 fit one round but measured the same at N = 8, 35.5
-// against 35.0 us, and 2,048 cost k = 8 / 16 5 / 4 us: tools/shard_abl_r05.py, KAD_SHARD_ABL=16, tools build.)
-__host__ __device__ constexpr uint32_t shard_qb(int) { return 4u * BLOCK; }
+// Queries and threads per workgroup of rt_shard_kernel<LK>: 1,024 and 256 for LK 0 / 8 / 16; 256 and 64 for LK 32,
+// whose 193 VGPRs hold two waves per SIMD: one-wave workgroups wait at no barrier for the other waves' line work
+// (rank 0 of 8, k = 32: 33.6 -> 30.7 us; k = 8 and 16 measured slower with 64- or 128-thread workgroups:
+// tools/shard_ab.py, profiles/r05/shard_shape/). (2,048 per workgroup measured no faster at N = 8 and costs k = 8 /
+// 16 5 / 4 us: KAD_SHARD_ABL=16, tools build.) The tools-build A/B libraries set the KAD_SHARD_* macros.
+#ifndef KAD_SHARD_QB8
+#define KAD_SHARD_QB8 1024u
+#endif
+#ifndef KAD_SHARD_WG8
+#define KAD_SHARD_WG8 256u
+#endif
+#ifndef KAD_SHARD_QB32
+#define KAD_SHARD_QB32 256u
+#endif
+#ifndef KAD_SHARD_WG32
+#define KAD_SHARD_WG32 64u
+#endif
+__host__ __device__ constexpr uint32_t shard_qb(int lk) { return lk == 32 ? KAD_SHARD_QB32 : KAD_SHARD_QB8; }
+__host__ __device__ constexpr uint32_t shard_wg(int lk) { return lk == 32 ? KAD_SHARD_WG32 : KAD_SHARD_WG8; }
 
 // One query, wave-uniform: global window, intersection with the shard, wave_rank, append (complete rows to `region`,
 // the region of the query's workgroup, as its line rows').
@@ -3539,26 +3554,30 @@ __device__ void wave_shard(const DevTable& T, const ShardCtx& S, const Target& t
 // LK: the window-line set the shard's uniform table answers from (8: counts <= 8, 16: 9..16, 32: 17..32; 0: none).
 // A window of that set spans at most LK / 2 buckets on either side, so a query whose bucket lies that far inside the
 // shard has the same window locally as globally.
-// A workgroup takes QB = 1,024 (2,048) queries of the replicated batch: their 20 (40) KB of targets come in as coalesced
-// 16-byte non-temporal loads into LDS (five (ten) per thread, all in flight at once: a lane-per-query form had only three
+// A workgroup of WG threads takes QB queries of the replicated batch (shard_qb / shard_wg: 1,024 over 256 threads, or 256
+// over one wave for LK 32): their 20 * QB bytes of targets come in as coalesced 16-byte non-temporal loads into LDS
+// (5 * QB / (4 * WG) per thread, all in flight at once: a lane-per-query form had only three
 // small loads in flight per lane and read the batch at ~2 TB/s, 10.6 us per 1M with nothing in reach), the in-reach
-// ones are compacted (at N ranks a shard reaches ~1/N of the batch), then answered BLOCK at a time: the window line of
+// ones are compacted (at N ranks a shard reaches ~1/N of the batch), then answered WG at a time: the window line of
 // the count's set for queries far enough inside the shard, the wave path on the global window for the rest.
 // Complete rows of the workgroup's queries go to region (workgroup index) % 8 of their home rank home_of_block(k):
 // one atomic per workgroup and home rank (usually one per workgroup).
-template <int LK, uint32_t QB>
-__global__ __launch_bounds__(BLOCK) void rt_shard_kernel(DevTable T, ShardCtx S, const uint8_t* __restrict__ targets,
-                                                         uint32_t q, uint32_t count, uint32_t aligned16, uint32_t abl) {
+template <int LK, uint32_t QB, uint32_t WG>
+__global__ __launch_bounds__(WG) void rt_shard_kernel(DevTable T, ShardCtx S, const uint8_t* __restrict__ targets,
+                                                      uint32_t q, uint32_t count, uint32_t aligned16, uint32_t abl) {
     // abl (tools build only, KAD_SHARD_ABL; results wrong on purpose): 1 = no wave path (edge queries dropped),
     // 2 = no line work either (the load and the reach compaction alone), 4 = plain (not non-temporal) target loads,
     // 8 = the target load alone
     constexpr uint32_t MARGIN = LK == 8 ? 4u : LK == 16 ? 8u : 16u;
-    constexpr uint32_t NR = QB / BLOCK;  // 256-query blocks per workgroup
+    constexpr uint32_t NR = QB / WG;     // WG-query chunks per workgroup (the reach test)
+    constexpr uint32_t NH = QB / BLOCK;  // 256-query home blocks per workgroup (the row slots)
+    constexpr uint32_t NW = WG / 64;     // waves
+    static_assert(QB % BLOCK == 0 && QB % WG == 0 && (5 * QB) % (4 * WG) == 0, "shard workgroup shape");
     __shared__ __attribute__((aligned(16))) uint32_t st[QB * 5];  // the block's targets, as stored
     __shared__ uint16_t cq[QB];                                   // in-reach queries (block-local index)
-    __shared__ uint32_t c_w[BLOCK / 64 + 1];
-    __shared__ uint64_t xs[BLOCK / 64][192];
-    __shared__ uint32_t wcnt[NR][BLOCK / 64], qbase_slot[NR];
+    __shared__ uint32_t c_w[NW + 1];
+    __shared__ uint64_t xs[NW][192];
+    __shared__ uint32_t wcnt[NH][NW], qbase_slot[NH];
     const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
     const uint64_t base = (uint64_t)blockIdx.x * QB;
     const uint32_t nq = (uint32_t)min<uint64_t>(QB, q - base);
@@ -3572,63 +3591,64 @@ __global__ __launch_bounds__(BLOCK) void rt_shard_kernel(DevTable T, ShardCtx S,
             u32x4_t* d4 = reinterpret_cast<u32x4_t*>(st);
             if (abl & 4) {
 #pragma unroll
-                for (uint32_t k = 0; k < 5 * NR / 4; k++) {
-                    const uint32_t x = tid + k * BLOCK;
+                for (uint32_t k = 0; k < 5 * QB / (4 * WG); k++) {
+                    const uint32_t x = tid + k * WG;
                     if (x < n4) d4[x] = s4[x];
                 }
             } else {
 #pragma unroll
-                for (uint32_t k = 0; k < 5 * NR / 4; k++) {
-                    const uint32_t x = tid + k * BLOCK;
+                for (uint32_t k = 0; k < 5 * QB / (4 * WG); k++) {
+                    const uint32_t x = tid + k * WG;
                     if (x < n4) d4[x] = __builtin_nontemporal_load(s4 + x);
                 }
             }
             o = 4 * n4;
         }
-        for (uint32_t x = o + tid; x < nw; x += BLOCK) st[x] = __builtin_nontemporal_load(src + x);
+        for (uint32_t x = o + tid; x < nw; x += WG) st[x] = __builtin_nontemporal_load(src + x);
     }
     __syncthreads();
     if (abl & 8) {
         if (st[tid] == 0x5EEDF00Du && st[tid + 1] == 0x5EEDF00Du) S.ctr[KAD_SHARD_COUNTER_STRIDE * 9u] = 1u;  // (keeps the load)
         return;
     }
-    // the queries within the shard's reach, compacted: thread tid tests queries tid + r * BLOCK, one block scan of
-    // the per-thread counts places them (the order is free: rows carry their qid)
+    // the queries within the shard's reach, compacted: thread tid tests queries tid + r * WG; a ballot per r
+    // places them within the wave, the waves' totals (one barrier) place the waves (the order is free: rows carry
+    // their qid). A workgroup with none in reach is done.
     uint32_t nnear;  // (block-uniform)
     {
-        uint32_t nm = 0;
+        uint64_t mr[NR];
+        uint32_t tw = 0;
 #pragma unroll
         for (uint32_t r = 0; r < NR; r++) {
-            const uint32_t j = r * BLOCK + tid;
+            const uint32_t j = r * WG + tid;
+            bool in = false;
             if (j < nq) {
                 Target th;
                 th.hi = ((uint64_t)__builtin_bswap32(st[5 * j]) << 32) | __builtin_bswap32(st[5 * j + 1]);
                 const uint32_t b = shard_bucket(S, th);
-                nm |= (b >= S.reach_lo && b < S.reach_hi ? 1u : 0u) << r;
+                in = b >= S.reach_lo && b < S.reach_hi;
             }
+            mr[r] = __ballot(in);
+            tw += (uint32_t)__builtin_popcountll(mr[r]);
         }
-        const uint32_t c = (uint32_t)__builtin_popcount(nm);
-        uint32_t inc = c;  // inclusive scan across the wave
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = (uint32_t)__shfl_up((int)inc, o, 64);
-            if (lane >= (uint32_t)o) inc += y;
-        }
-        if (lane == 63) c_w[w] = inc;
+        if (lane == 0) c_w[w] = tw;
         __syncthreads();
-        uint32_t pos = inc - c;
+        uint32_t pos = 0;
         nnear = 0;
-        for (uint32_t k = 0; k < BLOCK / 64; k++) {
+        for (uint32_t k = 0; k < NW; k++) {
             pos += k < w ? c_w[k] : 0u;
             nnear += c_w[k];
         }
+        if (nnear == 0) return;
 #pragma unroll
-        for (uint32_t r = 0; r < NR; r++)
-            if (nm >> r & 1u) cq[pos++] = (uint16_t)(r * BLOCK + tid);
+        for (uint32_t r = 0; r < NR; r++) {
+            if (mr[r] >> lane & 1u) cq[pos + lanes_below(mr[r])] = (uint16_t)(r * WG + tid);
+            pos += (uint32_t)__builtin_popcountll(mr[r]);
+        }
         __syncthreads();
     }
-    // the compacted queries, BLOCK at a time (block-uniform loop)
-    for (uint32_t c0 = 0; c0 < nnear; c0 += BLOCK) {
+    // the compacted queries, WG at a time (block-uniform loop)
+    for (uint32_t c0 = 0; c0 < nnear; c0 += WG) {
         const uint32_t k = c0 + tid;
         const bool act = k < nnear;
         const uint32_t j = act ? cq[k] : 0u;
@@ -3646,38 +3666,40 @@ __global__ __launch_bounds__(BLOCK) void rt_shard_kernel(DevTable T, ShardCtx S,
         const bool line = LK && act && b >= S.s_lo + MARGIN && b + MARGIN <= S.s_hi && !(abl & 2);
         bool edge = act && !(abl & 3);
         if (LK && __syncthreads_or(line)) {  // block-uniform
-            // the row slots are reserved before the lines are read (one atomic per 256-query block sb with line
+            // the row slots are reserved before the lines are read (one atomic per home block sb with line
             // queries in this round: its rows go to region sb % 8 of its home rank), so the atomic's round trip
             // overlaps the line loads; a query its line cannot answer leaves a tombstone row (qid KAD_NO_NODE, skipped
             // by the finish) and takes the wave path
             const uint32_t sb = act ? j / BLOCK : 0u;
             uint32_t slot = 0;
 #pragma unroll
-            for (uint32_t r = 0; r < NR; r++) {
+            for (uint32_t r = 0; r < NH; r++) {
                 const uint64_t mb = __ballot(line && sb == r);
                 if (lane == 0) wcnt[r][w] = (uint32_t)__builtin_popcountll(mb);
                 if (line && sb == r) slot = lanes_below(mb);
             }
             __syncthreads();
-            if (tid == 0) {  // one atomic per home rank among the workgroup's four 256-query blocks (usually one)
-                uint32_t tot[NR], hm[NR];
+            // one atomic per home rank among the workgroup's 256-query blocks (usually one), issued by thread 0
+            // before its wave's line work; the bases are written to LDS after it, so that the atomic's round trip
+            // overlaps the line loads of wave 0 too
+            uint32_t tot[NH], hm[NH], ab[NH];
+            if (tid == 0) {
 #pragma unroll
-                for (uint32_t r = 0; r < NR; r++) {
+                for (uint32_t r = 0; r < NH; r++) {
                     tot[r] = 0;
-                    for (uint32_t x = 0; x < BLOCK / 64; x++) tot[r] += wcnt[r][x];
+                    for (uint32_t x = 0; x < NW; x++) tot[r] += wcnt[r][x];
                     hm[r] = S.dests > 1 ? home_of_block((uint32_t)(base / BLOCK) + r, S.dests, S.nblk) : 0u;
                 }
-                uint32_t acc = 0;
 #pragma unroll
-                for (uint32_t r = 0; r < NR; r++) {
+                for (uint32_t r = 0; r < NH; r++) {
+                    ab[r] = 0;
                     if (r == 0 || hm[r] != hm[r - 1]) {  // (homes ascend with the block)
                         uint32_t run = 0;
-                        for (uint32_t y = r; y < NR; y++) run += hm[y] == hm[r] ? tot[y] : 0u;
-                        acc = run ? atomicAdd(S.ctr + (uint64_t)hm[r] * S.dest_words + KAD_SHARD_COUNTER_STRIDE *
-                                              (blockIdx.x & 7u), run) : 0u;
+                        for (uint32_t y = r; y < NH; y++) run += hm[y] == hm[r] ? tot[y] : 0u;
+                        if (run)
+                            ab[r] = atomicAdd(S.ctr + (uint64_t)hm[r] * S.dest_words +
+                                              KAD_SHARD_COUNTER_STRIDE * (blockIdx.x & 7u), run);
                     }
-                    qbase_slot[r] = acc;
-                    acc += tot[r];
                 }
             }
             uint32_t o[LK ? LK : 1], m = 0;
@@ -3688,6 +3710,15 @@ __global__ __launch_bounds__(BLOCK) void rt_shard_kernel(DevTable T, ShardCtx S,
                 else if constexpr (LK == 16) ok = wl16_answer(T, t, bl, count, line, o, m);
                 else if constexpr (LK == 32) ok = wl32_answer(T, t, bl, count, line, o, m);
                 ok = ok && line;
+            }
+            if (tid == 0) {
+                uint32_t acc = 0;
+#pragma unroll
+                for (uint32_t r = 0; r < NH; r++) {
+                    if (r == 0 || hm[r] != hm[r - 1]) acc = ab[r];
+                    qbase_slot[r] = acc;
+                    acc += tot[r];
+                }
             }
             __syncthreads();
             if (line) {
@@ -8945,21 +8976,21 @@ static int shard_batch(const kad_table* t, const uint32_t* global_good_prefix, u
     const int lk = !uni ? 0 : count <= 8 ? 8 : count <= 16 ? ((fl & TF_WL16) ? 16 : 0) : ((fl & TF_WL32) ? 32 : 0);
     DeviceGuard g(t->device);
     void (*kern)(DevTable, ShardCtx, const uint8_t*, uint32_t, uint32_t, uint32_t, uint32_t) =
-        lk == 8 ? rt_shard_kernel<8, shard_qb(8)> : lk == 16 ? rt_shard_kernel<16, shard_qb(16)>
-        : lk == 32 ? rt_shard_kernel<32, shard_qb(32)> : rt_shard_kernel<0, shard_qb(0)>;
-    uint32_t qb = shard_qb(lk);
+        lk == 8 ? rt_shard_kernel<8, shard_qb(8), shard_wg(8)> : lk == 16 ? rt_shard_kernel<16, shard_qb(16), shard_wg(16)>
+        : lk == 32 ? rt_shard_kernel<32, shard_qb(32), shard_wg(32)> : rt_shard_kernel<0, shard_qb(0), shard_wg(0)>;
+    uint32_t qb = shard_qb(lk), wg = shard_wg(lk);
     const uint32_t aligned16 = ((uintptr_t)targets & 15u) == 0;
     uint32_t abl = 0;
 #ifdef KAD_ABLATIONS
     if (const char* e = std::getenv("KAD_SHARD_ABL")) abl = (uint32_t)std::atoi(e);
-    if (abl & 16) {  // the other workgroup size (A/B)
-        qb = qb == 4u * BLOCK ? 8u * BLOCK : 4u * BLOCK;
-        kern = qb == 4u * BLOCK ? kern
-                                : (lk == 8 ? rt_shard_kernel<8, 8u * BLOCK> : lk == 16 ? rt_shard_kernel<16, 8u * BLOCK>
-                                   : lk == 32 ? rt_shard_kernel<32, 8u * BLOCK> : rt_shard_kernel<0, 8u * BLOCK>);
+    if (abl & 16) {  // 2,048 queries per workgroup of 256 threads (A/B)
+        qb = 8u * BLOCK;
+        wg = BLOCK;
+        kern = lk == 8 ? rt_shard_kernel<8, 8u * BLOCK, BLOCK> : lk == 16 ? rt_shard_kernel<16, 8u * BLOCK, BLOCK>
+               : lk == 32 ? rt_shard_kernel<32, 8u * BLOCK, BLOCK> : rt_shard_kernel<0, 8u * BLOCK, BLOCK>;
     }
 #endif
-    hipLaunchKernelGGL(kern, dim3((uint32_t)(((uint64_t)q + qb - 1) / qb)), dim3(BLOCK), 0,
+    hipLaunchKernelGGL(kern, dim3((uint32_t)(((uint64_t)q + qb - 1) / qb)), dim3(wg), 0,
                        (hipStream_t)stream, t->d, S, targets, q, count, aligned16, abl);
     HIP_TRY(hipGetLastError());
     return KAD_OK;

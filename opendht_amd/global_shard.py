@@ -81,7 +81,8 @@ def home_range(q: int, world: int, rank: int) -> tuple[int, int]:
     return lo.value, hi.value
 
 
-SHARD_QB = (1024, 2048)  # queries per workgroup of rt_shard_kernel (csrc shard_qb: 1,024; 2,048 in a tools-build A/B)
+SHARD_QB = (256, 512, 1024, 2048)  # queries per workgroup of rt_shard_kernel (csrc KAD_SHARD_QB; 2,048 in a
+# tools-build A/B)
 
 
 def region_queries(q: int, world: int, qb: int) -> int:
@@ -123,9 +124,9 @@ class Exchange:
         self.collective = world > 1 if collective is None else bool(collective)
         nblk = -(-q // 256)
         if home:
-            # region w % 8 of the workgroups (QB = 1,024 or 2,048 queries, the shard kernel's shard_qb) holding a
+            # region w % 8 of the workgroups (QB = 256 ... 2,048 queries, the shard kernel's shard_qb) holding a
             # home range's queries, two rows per query at most (a line query its line cannot answer leaves a
-            # tombstone row, then its wave-path row): this capacity can never overflow, for either QB
+            # tombstone row, then its wave-path row): this capacity can never overflow, for any QB of SHARD_QB
             worst = max(region_queries(q, world, qb) for qb in SHARD_QB)
             self.row_cap_max = 2 * worst
             # uniform targets: a source shard answers ~1/world of a region's queries
