@@ -211,6 +211,13 @@ __device__ __forceinline__ int cmp160(uint64_t ah, uint32_t a2, uint32_t a3, uin
 }
 
 // RoutingTable::findBucket (routing_table.cpp:113-127) = upper_bound(first, t) - 1, clamped to 0.
+// (A/B builds only: KAD_Q32_OCC8 caps the quad count-32 kernels at 64 VGPRs, eight waves per SIMD)
+#ifdef KAD_Q32_OCC8
+#define KAD_Q32_OCC __attribute__((amdgpu_waves_per_eu(8, 8)))
+#else
+#define KAD_Q32_OCC
+#endif
+
 __device__ __forceinline__ uint32_t locate_bucket(const DevTable& T, const Target& t) {
     if (T.flags & TF_DIRECT) {
         if (t.hi < T.rbase) return 0;
@@ -2109,7 +2116,7 @@ __device__ __forceinline__ void store_rows_quad(uint32_t* __restrict__ out_idx, 
 // (16 contiguous bytes per quad and instruction); no block barrier. !QS: lanes 0 and 1 store their 16 entries from
 // registers (aligned rows) or the block's rows go through store_rows_quad.
 template <int ABL, bool QS>
-__global__ __launch_bounds__(BLOCK) void rt_wl32q_kernel(DevTable T, const uint8_t* __restrict__ targets, uint32_t q,
+__global__ __launch_bounds__(BLOCK) KAD_Q32_OCC void rt_wl32q_kernel(DevTable T, const uint8_t* __restrict__ targets, uint32_t q,
                                                          uint32_t count, uint32_t* __restrict__ out_idx,
                                                          uint8_t* __restrict__ out_cnt) {
     const uint32_t g = blockIdx.x * BLOCK + threadIdx.x, i = g >> 2, p = g & 3u;
@@ -2642,7 +2649,7 @@ __device__ __forceinline__ bool gl32_answer4(const DevTable& T, const Target& t,
 // ABL (tools build only, KAD_RT_KERNEL=gl32q_abl1 / gl32q_stats): 1 = no exact path (those rows left unwritten);
 // 3 = path statistics (out_cnt = 250 for the queries the exact path answers).
 template <int ABL>
-__global__ __launch_bounds__(BLOCK) void rt_gl32q_kernel(DevTable T, const uint8_t* __restrict__ targets, uint32_t q,
+__global__ __launch_bounds__(BLOCK) KAD_Q32_OCC void rt_gl32q_kernel(DevTable T, const uint8_t* __restrict__ targets, uint32_t q,
                                                          uint32_t count, uint32_t* __restrict__ out_idx,
                                                          uint8_t* __restrict__ out_cnt) {
     const uint32_t g = blockIdx.x * BLOCK + threadIdx.x, i = g >> 2, p = g & 3u;
