@@ -211,13 +211,6 @@ __device__ __forceinline__ int cmp160(uint64_t ah, uint32_t a2, uint32_t a3, uin
 }
 
 // RoutingTable::findBucket (routing_table.cpp:113-127) = upper_bound(first, t) - 1, clamped to 0.
-// (A/B builds only: KAD_Q32_OCC8 caps the quad count-32 kernels at 64 VGPRs, eight waves per SIMD)
-#ifdef KAD_Q32_OCC8
-#define KAD_Q32_OCC __attribute__((amdgpu_waves_per_eu(8, 8)))
-#else
-#define KAD_Q32_OCC
-#endif
-
 __device__ __forceinline__ uint32_t locate_bucket(const DevTable& T, const Target& t) {
     if (T.flags & TF_DIRECT) {
         if (t.hi < T.rbase) return 0;
@@ -2116,7 +2109,7 @@ __device__ __forceinline__ void store_rows_quad(uint32_t* __restrict__ out_idx, 
 // (16 contiguous bytes per quad and instruction); no block barrier. !QS: lanes 0 and 1 store their 16 entries from
 // registers (aligned rows) or the block's rows go through store_rows_quad.
 template <int ABL, bool QS>
-__global__ __launch_bounds__(BLOCK) KAD_Q32_OCC void rt_wl32q_kernel(DevTable T, const uint8_t* __restrict__ targets, uint32_t q,
+__global__ __launch_bounds__(BLOCK) void rt_wl32q_kernel(DevTable T, const uint8_t* __restrict__ targets, uint32_t q,
                                                          uint32_t count, uint32_t* __restrict__ out_idx,
                                                          uint8_t* __restrict__ out_cnt) {
     const uint32_t g = blockIdx.x * BLOCK + threadIdx.x, i = g >> 2, p = g & 3u;
@@ -2646,10 +2639,12 @@ __device__ __forceinline__ bool gl32_answer4(const DevTable& T, const Target& t,
 }
 
 // Counts 24, 28, 32 on general lines: four lanes per query, the row through a per-quad LDS row (rt_wl32q_kernel's).
+// Held to 64 VGPRs (eight waves per SIMD instead of seven; no spill): 79.2-81.0 -> 78.1-78.5 us per 1M on the 4M-node
+// split-policy table (profiles/r05/q32_occ8/; rt_wl32q_kernel measured the same either way).
 // ABL (tools build only, KAD_RT_KERNEL=gl32q_abl1 / gl32q_stats): 1 = no exact path (those rows left unwritten);
 // 3 = path statistics (out_cnt = 250 for the queries the exact path answers).
 template <int ABL>
-__global__ __launch_bounds__(BLOCK) KAD_Q32_OCC void rt_gl32q_kernel(DevTable T, const uint8_t* __restrict__ targets, uint32_t q,
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) void rt_gl32q_kernel(DevTable T, const uint8_t* __restrict__ targets, uint32_t q,
                                                          uint32_t count, uint32_t* __restrict__ out_idx,
                                                          uint8_t* __restrict__ out_cnt) {
     const uint32_t g = blockIdx.x * BLOCK + threadIdx.x, i = g >> 2, p = g & 3u;
@@ -3569,8 +3564,13 @@ __device__ void wave_shard(const DevTable& T, const ShardCtx& S, const Target& t
 // the count's set for queries far enough inside the shard, the wave path on the global window for the rest.
 // Complete rows of the workgroup's queries go to region (workgroup index) % 8 of their home rank home_of_block(k):
 // one atomic per workgroup and home rank (usually one per workgroup).
+#ifdef KAD_SHARD_OCC4  // (A/B builds only: at most 128 VGPRs, four waves per SIMD)
+#define KAD_SHARD_OCC __attribute__((amdgpu_waves_per_eu(4)))
+#else
+#define KAD_SHARD_OCC
+#endif
 template <int LK, uint32_t QB, uint32_t WG>
-__global__ __launch_bounds__(WG) void rt_shard_kernel(DevTable T, ShardCtx S, const uint8_t* __restrict__ targets,
+__global__ __launch_bounds__(WG) KAD_SHARD_OCC void rt_shard_kernel(DevTable T, ShardCtx S, const uint8_t* __restrict__ targets,
                                                       uint32_t q, uint32_t count, uint32_t aligned16, uint32_t abl) {
     // abl (tools build only, KAD_SHARD_ABL; results wrong on purpose): 1 = no wave path (edge queries dropped),
     // 2 = no line work either (the load and the reach compaction alone), 4 = plain (not non-temporal) target loads,
