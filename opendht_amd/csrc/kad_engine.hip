@@ -3500,7 +3500,8 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
 
 // Queries and threads per workgroup of rt_shard_kernel<LK>: 1,024 and 256 for LK 0 / 8 / 16; 256 and 64 for LK 32,
 // whose 193 VGPRs hold two waves per SIMD: one-wave workgroups wait at no barrier for the other waves' line work
-// (rank 0 of 8, k = 32: 33.6 -> 30.7 us; k = 8 and 16 measured slower with 64- or 128-thread workgroups:
+// (rank 0 of 8, k = 32: 33.6 -> 30.7 us; held to 128 VGPRs for four waves per SIMD it spills 36 and takes 33.0;
+// k = 8 and 16 measured slower with 64- or 128-thread workgroups:
 // tools/shard_ab.py, profiles/r05/shard_shape/). (2,048 per workgroup measured no faster at N = 8 and costs k = 8 /
 // 16 5 / 4 us: KAD_SHARD_ABL=16, tools build.) The tools-build A/B libraries set the KAD_SHARD_* macros.
 #ifndef KAD_SHARD_QB8
@@ -3564,13 +3565,8 @@ __device__ void wave_shard(const DevTable& T, const ShardCtx& S, const Target& t
 // the count's set for queries far enough inside the shard, the wave path on the global window for the rest.
 // Complete rows of the workgroup's queries go to region (workgroup index) % 8 of their home rank home_of_block(k):
 // one atomic per workgroup and home rank (usually one per workgroup).
-#ifdef KAD_SHARD_OCC4  // (A/B builds only: at most 128 VGPRs, four waves per SIMD)
-#define KAD_SHARD_OCC __attribute__((amdgpu_waves_per_eu(4)))
-#else
-#define KAD_SHARD_OCC
-#endif
 template <int LK, uint32_t QB, uint32_t WG>
-__global__ __launch_bounds__(WG) KAD_SHARD_OCC void rt_shard_kernel(DevTable T, ShardCtx S, const uint8_t* __restrict__ targets,
+__global__ __launch_bounds__(WG) void rt_shard_kernel(DevTable T, ShardCtx S, const uint8_t* __restrict__ targets,
                                                       uint32_t q, uint32_t count, uint32_t aligned16, uint32_t abl) {
     // abl (tools build only, KAD_SHARD_ABL; results wrong on purpose): 1 = no wave path (edge queries dropped),
     // 2 = no line work either (the load and the reach compaction alone), 4 = plain (not non-temporal) target loads,
