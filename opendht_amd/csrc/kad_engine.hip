@@ -5023,7 +5023,13 @@ __global__ void ncl_build_kernel(const uint64_t* key, const uint8_t* status, con
 // than `count` trusted emissions, a deferred line, a target equal in key24 to a slot node, or equal key24
 // either side of its position takes the two-pass wave path (nc_answer, then nc64_query / the serial walk).
 // ---------------------------------------------------------------------------------------
-constexpr uint32_t NC32_SLOTS = 124, NC32_LEFT = 56, NC32_XMAX = 15, NC32_STRIDE = 128;  // dwords
+#ifndef KAD_NC32_STRIDE
+#define KAD_NC32_STRIDE 128u
+#define KAD_NC32_LEFT 56u
+#endif
+constexpr uint32_t NC32_STRIDE = KAD_NC32_STRIDE, NC32_SLOTS = NC32_STRIDE - 4, NC32_LEFT = KAD_NC32_LEFT,
+                   NC32_XMAX = 15;  // dwords
+static_assert(NC32_STRIDE % 32 == 0 && NC32_STRIDE <= 128 && NC32_LEFT + NC32_XMAX < NC32_SLOTS, "NodeCache-32 line");
 
 // Octet (8-lane group) cross-lane moves without address arithmetic: quad permutes and row shifts by DPP, the lane-4
 // exchange and the octet broadcast by ds_swizzle's bit-mask mode (lane' = ((lane & and) | or) ^ xor within 32 lanes).
@@ -5067,6 +5073,7 @@ __global__ __launch_bounds__(BLOCK) void ncl32_build_kernel(const uint64_t* key,
     const uint32_t Pp = min(min(P, slot_prefix), 40u), sh = 40 - Pp;
     // (equal key24 between neighbours no longer defers the line: nc32_line_kernel checks the one pair that can change
     // the walk's order, the two elements either side of the target's position)
+    if (16 * g >= NC32_STRIDE) return;  // (a line of fewer than 128 dwords: its first NC32_STRIDE / 16 lanes)
     uint32_t v[16];
 #pragma unroll
     for (int u = 0; u < 16; u++) {
@@ -5095,16 +5102,18 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) v
                                                           const uint8_t* __restrict__ targets, uint32_t q,
                                                           uint32_t count, uint32_t* __restrict__ out_idx,
                                                           uint8_t* __restrict__ out_cnt) {
-    // the octets' rows of NC32_STRIDE + 4 dwords, with 8 dwords of padding before the first and 16 after the last: the
-    // run steps below read their elements at unclamped indices (-4 .. 138 of a row) and mask the ones outside
+    // the octets' rows of NC32_STRIDE + 4 dwords, with padding before the first and after the last: the run steps
+    // below read their elements at unclamped indices (NC32_LEFT - 60 .. NC32_LEFT + NC32_XMAX + 67 of a row) and mask
+    // the ones outside
     constexpr uint32_t NC32_ROW = NC32_STRIDE + 4;
-    __shared__ uint32_t ldsf[8 + (BLOCK / 8) * NC32_ROW + 16];
+    constexpr uint32_t PADF = (64u - NC32_LEFT + 7u) & ~7u, PADB = NC32_LEFT + NC32_XMAX + 68u - NC32_ROW + 8u;
+    __shared__ uint32_t ldsf[PADF + (BLOCK / 8) * NC32_ROW + PADB];
     const uint32_t lane = threadIdx.x & 63u, g = threadIdx.x & 7u;
     const uint32_t qi = (blockIdx.x * BLOCK + threadIdx.x) >> 3;
     const bool act = qi < q;
     const bool fam = DUAL && act && af[qi] != 0;
     const DevTable& T = fam ? T6 : T4;  // octet-uniform
-    uint32_t* W = ldsf + 8 + (threadIdx.x >> 3) * NC32_ROW;
+    uint32_t* W = ldsf + PADF + (threadIdx.x >> 3) * NC32_ROW;
     bool ok = false, line = false;
     uint64_t thi = 0;
     uint32_t s = 0;
@@ -5121,18 +5130,18 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     }
     if (line) {  // load x: the octet reads 128 contiguous bytes, lane g the 16 at 128x + 16g
         const uint4* src = T.ncl32 + (size_t)(NC32_STRIDE / 4) * s + g;
-        uint4 x4[4];
+        uint4 x4[NC32_STRIDE / 32];
 #pragma unroll
-        for (int x = 0; x < 4; x++) x4[x] = src[8 * x];
+        for (int x = 0; x < (int)NC32_STRIDE / 32; x++) x4[x] = src[8 * x];
 #pragma unroll
-        for (int x = 0; x < 4; x++) {
+        for (int x = 0; x < (int)NC32_STRIDE / 32; x++) {
             W[32 * x + 4 * g] = x4[x].x; W[32 * x + 4 * g + 1] = x4[x].y;
             W[32 * x + 4 * g + 2] = x4[x].z; W[32 * x + 4 * g + 3] = x4[x].w;
         }
     }
     __syncthreads();
     if (ABL == 2) {
-        if (line) out_idx[(size_t)qi * count + g] = W[g] ^ W[64 + g] ^ W[127 - g];
+        if (line) out_idx[(size_t)qi * count + g] = W[g] ^ W[64 + g] ^ W[NC32_STRIDE - 1 - g];
         return;
     }
     if (line) {
@@ -5180,9 +5189,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) v
             }
             // an element is key24 << 8 | expired (bits 1..7 clear), so x ^ t24 << 8 is the distance key with its expired
             // bit, and the step goes into bits 1..6 by an OR: ra << 1 = 16g | 2u, rb << 1 = 16(7 - g) | (14 - 2u).
-            // Valid: ra < p <=> u < p - 8g; p + rb < NC32_SLOTS <=> u > p - 61 - 8g (four ops per element)
+            // Valid: ra < p <=> u < p - 8g; p + rb < NC32_SLOTS <=> u > p + 63 - NC32_SLOTS - 8g (four ops per element)
             const uint32_t T8 = t24 << 8, ga = 16u * g, gb = 128u | (16u * (7u - g));
-            const int dA = (int)p - 8 * (int)g, dB = (int)p - 61 - 8 * (int)g;
+            const int dA = (int)p - 8 * (int)g, dB = (int)p + 63 - (int)NC32_SLOTS - 8 * (int)g;
 #pragma unroll
             for (int u = 0; u < 8; u++) {
                 const uint32_t a = (xa[u] ^ T8) | ga | (2u * u);
