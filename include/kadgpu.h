@@ -88,7 +88,7 @@ extern "C" {
 #define KAD_INFO_SLOT_LINES 0x2000u /* other bucket shapes: count <= 8 queries read one 64-byte line indexed by
                                        the target's top bits (rt_sl_kernel), the locate + 128-byte line only
                                        as fallback */
-#define KAD_INFO_NODECACHE_LINES32 0x1000u /* sorted table: NodeCache counts 17..32 read one 512-byte line
+#define KAD_INFO_NODECACHE_LINES32 0x1000u /* sorted table: NodeCache counts 17..32 read one 384-byte line
                                              per query, 8 lanes per query (nc32_line_kernel) */
 #define KAD_INFO_SHORT_LINES 0x800u /* uniform-depth table: count <= 8 queries read one 64-byte short
                                        window line (rt_ws_kernel), the 128-byte line only as fallback */

@@ -5005,14 +5005,14 @@ __global__ void ncl_build_kernel(const uint64_t* key, const uint8_t* status, con
 }
 
 // ---------------------------------------------------------------------------------------
-// NodeCache lines for counts 17..32 (TF_NCL32): one 512-byte line per node radix slot s, the 124-node window
-// w0 = r0-56 .. r0+67 of the sorted node array ([r0, r1) = the slot's nodes, at most 15):
+// NodeCache lines for counts 17..32 (TF_NCL32): one 384-byte line per node radix slot s, the 92-node window
+// w0 = r0-44 .. r0+47 of the sorted node array ([r0, r1) = the slot's nodes, at most 15):
 //   dw0      w0
 //   dw1      ns = r1 - r0 | sh << 8
-//   dw2      defer (a clamped or wide slot) | truncated left (w0 > 0) << 1 | truncated right (w0 + 124 < n) << 2
-//   dw4..127 element e (node w0 + e): key24 << 8 | expired, key24 as in the 256-byte lines
+//   dw2      defer (a clamped or wide slot) | truncated left (w0 > 0) << 1 | truncated right (w0 + 92 < n) << 2
+//   dw4..95  element e (node w0 + e): key24 << 8 | expired, key24 as in the 256-byte lines
 // A query is answered by 8 lanes (an octet; 8 queries per wave). The octet stages its line in LDS with
-// 16-byte loads, counts the slot's nodes below the target (lb = w0 + p, p = 56 + x), and reads the
+// 16-byte loads, counts the slot's nodes below the target (lb = w0 + p, p = 44 + x), and reads the
 // first 64 steps of each run: lane g holds left steps 8g..8g+7 (element p-1-step) and right steps
 // 63-8g-u (element p+step). A run's prefix maxima of the XOR distance (in-lane, then across the octet)
 // give each element the key (M << 8 | side << 7 | step << 1 | expired); each run's keys ascend with the
@@ -5023,9 +5023,12 @@ __global__ void ncl_build_kernel(const uint64_t* key, const uint8_t* status, con
 // than `count` trusted emissions, a deferred line, a target equal in key24 to a slot node, or equal key24
 // either side of its position takes the two-pass wave path (nc_answer, then nc64_query / the serial walk).
 // ---------------------------------------------------------------------------------------
+// 384-byte lines, 44 nodes left of the slot: the count-32 walk rarely goes past 40 steps on a side
+// (tools/nc32_walk_extent.py: p99 37, max 44 in 20k walks), and the 512-byte form (124 slots, 56 left) read a third more
+// bytes for nothing: 121.9-122.9 -> 116.9-119.2 us at k = 32, 130-134 -> 119-122 at k = 24 (profiles/r05/nc96/)
 #ifndef KAD_NC32_STRIDE
-#define KAD_NC32_STRIDE 128u
-#define KAD_NC32_LEFT 56u
+#define KAD_NC32_STRIDE 96u
+#define KAD_NC32_LEFT 44u
 #endif
 constexpr uint32_t NC32_STRIDE = KAD_NC32_STRIDE, NC32_SLOTS = NC32_STRIDE - 4, NC32_LEFT = KAD_NC32_LEFT,
                    NC32_XMAX = 15;  // dwords
@@ -5147,7 +5150,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     if (line) {
         const uint32_t w0 = W[0], ns = W[1] & 255u, sh = (W[1] >> 8) & 63u, fl = W[2];
         const uint32_t t24 = (uint32_t)(thi >> sh) & 0xFFFFFFu;
-        // lb: the slot's nodes below the target (elements 56 .. 56+ns-1, two per lane)
+        // lb: the slot's nodes below the target (elements NC32_LEFT .. NC32_LEFT+ns-1, two per lane)
         uint32_t below = 0, eq = 0;
 #pragma unroll
         for (int u = 0; u < 2; u++) {
@@ -5233,7 +5236,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) v
             kb[u] = (max(pb[u], inB) & 0xFFFFFF00u) | (kb[u] & 255u);
         }
         // keys beyond a run cut short by the window's truncated end are not trusted: the run's last step inside
-        // the window (left: step p-1, right: step 123-p) bounds them
+        // the window (left: step p-1, right: step NC32_SLOTS-1-p) bounds them
         uint32_t lim = NONE;
         if ((fl & 2u) && p <= 64) {
             const uint32_t r = p - 1, ux = r & 7u;
@@ -5243,7 +5246,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) v
             lim = min(lim, (uint32_t)__shfl((int)v, (int)((lane & ~7u) | (r >> 3)), 64));
         }
         if ((fl & 4u) && NC32_SLOTS - p <= 64) {
-            const uint32_t r = 63u - (NC32_SLOTS - 1 - p), ux = r & 7u;  // step 123-p sits at u = r & 7, g = r >> 3
+            const uint32_t r = 63u - (NC32_SLOTS - 1 - p), ux = r & 7u;  // that step sits at u = r & 7, g = r >> 3
             uint32_t v = kb[0];
 #pragma unroll
             for (int u = 1; u < 8; u++) v = ux == (uint32_t)u ? kb[u] : v;

@@ -1,4 +1,4 @@
-"""512-byte NodeCache lines, counts 17..32 (nc32_line_kernel): 8 lanes per query, the walk's
+"""384-byte NodeCache lines, counts 17..32 (nc32_line_kernel): 8 lanes per query, the walk's
 first 64 steps as one bitonic merge, the two-pass wave path for the rest. Every test compares with the oracle
 (NodeCache::getCachedNodes, node_cache.cpp:36-66) bit for bit, and with the wave path (KAD_NC_KERNEL=two_pass)."""
 import numpy as np
@@ -59,7 +59,7 @@ def test_clustered(gpu, monkeypatch):
 
 
 def test_after_status_patch(gpu):
-    """The 512-byte lines carry expired bits: incremental patches rebuild the slots whose window holds a node."""
+    """The 384-byte lines carry expired bits: incremental patches rebuild the slots whose window holds a node."""
     t = TB.uniform_config(60_000, 12, seed=0x3277)
     rng = np.random.default_rng(9)
     targets = TB.adversarial_targets(t, extra=8192)
@@ -79,7 +79,7 @@ def test_after_status_patch(gpu):
 
 
 def test_dual(gpu):
-    """Dual-family batch (af per query) with the 512-byte lines in both families."""
+    """Dual-family batch (af per query) with the 384-byte lines in both families."""
     t4 = TB.uniform_config(30_000, 10, seed=0x3241)
     t6 = TB.uniform_config(20_000, 10, seed=0x3261, good=60, expired=30)
     targets = TB.adversarial_targets(t4, extra=4096)
