@@ -3668,7 +3668,7 @@ __global__ __launch_bounds__(WG) void rt_shard_kernel(DevTable T, ShardCtx S, co
         }
         const bool line = LK && act && b >= S.s_lo + MARGIN && b + MARGIN <= S.s_hi && !(abl & 2);
         bool edge = act && !(abl & 3);
-        if (LK && __syncthreads_or(line)) {  // block-uniform
+        if (LK) {  // (a round without line queries reserves nothing: its counts are zero and no wave has line work)
             // the row slots are reserved before the lines are read (one atomic per home block sb with line
             // queries in this round: its rows go to region sb % 8 of its home rank), so the atomic's round trip
             // overlaps the line loads; a query its line cannot answer leaves a tombstone row (qid KAD_NO_NODE, skipped
@@ -3744,7 +3744,7 @@ __global__ __launch_bounds__(WG) void rt_shard_kernel(DevTable T, ShardCtx S, co
                     atomicOr(S.ctr + dof + KAD_SHARD_COUNTER_STRIDE * 9u, 1u);
                 }
             }
-            __syncthreads();  // (wcnt / qbase_slot reused by the next round)
+            if (c0 + WG < nnear) __syncthreads();  // (wcnt / qbase_slot reused by the next round; block-uniform)
         }
         for (uint64_t mm = __ballot(edge); mm; mm &= mm - 1) {
             const uint32_t l = (uint32_t)__builtin_ctzll(mm);
