@@ -4681,20 +4681,28 @@ __global__ __launch_bounds__(BLOCK) void nc_two_pass_kernel(DevTable T, const ui
 // of them means the walk leaves the window: the wave answers those lanes' queries one by one with
 // nc_answer (32-node runs each side of lb, wave-cooperative).
 // ---------------------------------------------------------------------------------------
-constexpr uint32_t NCL_SLOTS = 60, NCL_LEFT = 28, NCL_XMAX = 15, NCL_STRIDE = 64;  // dwords
+#ifndef KAD_NCL_STRIDE
+#define KAD_NCL_STRIDE 64u
+#define KAD_NCL_LEFT 28u
+#endif
+constexpr uint32_t NCL_STRIDE = KAD_NCL_STRIDE, NCL_SLOTS = NCL_STRIDE - 4, NCL_LEFT = KAD_NCL_LEFT,
+                   NCL_XMAX = 15;                 // dwords
+constexpr uint32_t NCL_PIECES = NCL_STRIDE / 4;  // 16-byte pieces of a line
+constexpr int NCL_NV = (int)NCL_SLOTS + 4;        // a lane's slot array (the slots, then NONE)
+static_assert(NCL_STRIDE % 16 == 0 && NCL_STRIDE <= 64 && NCL_LEFT + NCL_XMAX < NCL_SLOTS, "NodeCache line");
 
 // The answer from the lane's line (Lq: its 16 pieces, loaded by the wave): the node indices go to lrow[0..m) (the
 // lane's LDS row) by emission rank.
 __device__ __forceinline__ bool ncl_answer(const uint4 (&Lq)[16], uint32_t index_base, const Target& t,
                                            uint32_t count, uint32_t* lrow, uint32_t& m) {
-    uint32_t v[64];
+    uint32_t v[NCL_NV];
     const uint4 hd = Lq[0];
 #pragma unroll
-    for (int x = 1; x < (int)NCL_STRIDE / 4; x++) {
+    for (int x = 1; x < (int)NCL_PIECES; x++) {
         const uint4 u = Lq[x];
         v[4 * x - 4] = u.x; v[4 * x - 3] = u.y; v[4 * x - 2] = u.z; v[4 * x - 1] = u.w;
     }
-    v[60] = v[61] = v[62] = v[63] = NONE;
+    v[NCL_NV - 4] = v[NCL_NV - 3] = v[NCL_NV - 2] = v[NCL_NV - 1] = NONE;
     const uint32_t w0 = hd.x, ns = hd.y & 255u, sh = (hd.y >> 8) & 63u, fl = hd.z;
     const uint32_t tx = ((uint32_t)(t.hi >> sh) & 0xFFFFFFu) << 8;
     bool ex = fl & 1u;
@@ -4709,17 +4717,17 @@ __device__ __forceinline__ bool ncl_answer(const uint4 (&Lq)[16], uint32_t index
         }
         v[j] ^= tx;
     }
-    // shift the window by x: lb at slot 28, the left run 27..0, the right run 28..59-x
+    // shift the window by x: lb at slot NCL_LEFT, the left run NCL_LEFT-1..0, the right run NCL_LEFT..NCL_SLOTS-1-x
     {
-        uint32_t u[64];
+        uint32_t u[NCL_NV];
 #pragma unroll
-        for (int j = 0; j < 64; j++) u[j] = (x & 1u) ? (j < 63 ? v[j + 1] : NONE) : v[j];
+        for (int j = 0; j < NCL_NV; j++) u[j] = (x & 1u) ? (j < NCL_NV - 1 ? v[j + 1] : NONE) : v[j];
 #pragma unroll
-        for (int j = 0; j < 64; j++) v[j] = (x & 2u) ? (j < 62 ? u[j + 2] : NONE) : u[j];
+        for (int j = 0; j < NCL_NV; j++) v[j] = (x & 2u) ? (j < NCL_NV - 2 ? u[j + 2] : NONE) : u[j];
 #pragma unroll
-        for (int j = 0; j < 64; j++) u[j] = (x & 4u) ? (j < 60 ? v[j + 4] : NONE) : v[j];
+        for (int j = 0; j < NCL_NV; j++) u[j] = (x & 4u) ? (j < NCL_NV - 4 ? v[j + 4] : NONE) : v[j];
 #pragma unroll
-        for (int j = 0; j < 64; j++) v[j] = (x & 8u) ? (j < 56 ? u[j + 8] : NONE) : u[j];
+        for (int j = 0; j < NCL_NV; j++) v[j] = (x & 8u) ? (j < NCL_NV - 8 ? u[j + 8] : NONE) : u[j];
     }
     // equal key24 either side of lb: the runs may tie at 24 bits (the window's key24 values are monotone, so a
     // left and a right element can only share one if these two do); only the full IDs order them -> exact path
@@ -4745,13 +4753,14 @@ __device__ __forceinline__ bool ncl_answer(const uint4 (&Lq)[16], uint32_t index
     }
     if (!(fl & 4u)) endR = NONE;  // the window reaches the array end
     const uint32_t lim = min(endL, endR);  // keys <= lim are the walk's first steps
-    // the walk's first 32 steps: top-32 merge of the two ascending runs (left 28 reversed + 4 NONE,
-    // right 32), then a bitonic half-cleaner cascade
+    // the walk's first 32 steps: top-32 merge of the two ascending runs (left NCL_LEFT reversed + NONE,
+    // right up to 32 + NONE), then a bitonic half-cleaner cascade
     uint32_t w[32];
 #pragma unroll
     for (int r = 0; r < 32; r++) {
-        const uint32_t a = r < (int)NCL_LEFT ? v[NCL_LEFT - 1 - r] : NONE;  // left, ascending
-        w[r] = min(a, v[NCL_LEFT + 31 - r]);                              // right, descending
+        const uint32_t a = r < (int)NCL_LEFT ? v[NCL_LEFT - 1 - r] : NONE;              // left, ascending
+        const int jr = (int)NCL_LEFT + 31 - r;
+        w[r] = min(a, jr < (int)NCL_SLOTS ? v[jr < NCL_NV ? jr : 0] : NONE);              // right, descending
     }
 #pragma unroll
     for (int h = 16; h >= 1; h >>= 1)
@@ -4890,9 +4899,9 @@ __device__ __forceinline__ void nc_line_kernel_body(const DevTable& T4, const De
         const uint32_t so = (uint32_t)__shfl((int)sl, 8 * r + (int)(lane >> 3), 64);
         uint4 a = make_uint4(0u, 0u, 0u, 0u), b = a;
         if (so != NONE) {
-            const uint4* lp = ((DUAL && (so >> 31)) ? T6.ncl : T4.ncl) + (NCL_STRIDE / 4) * (size_t)(so & 0x7FFFFFFFu);
+            const uint4* lp = ((DUAL && (so >> 31)) ? T6.ncl : T4.ncl) + (size_t)NCL_PIECES * (so & 0x7FFFFFFFu);
             a = lp[lane & 7];
-            b = lp[8 + (lane & 7)];
+            if (NCL_PIECES == 16 || 8 + (lane & 7) < NCL_PIECES) b = lp[8 + (lane & 7)];
         }
         ld[r] = a;
         ld[8 + r] = b;

@@ -29,7 +29,7 @@ sh = build_shard(spec, 0)
 T = DeviceTable(sh.ids, sh.status, sh.first, sh.off, device=0, index_base=sh.index_base, sorted=True)
 tgs = [torch.from_numpy(spec.targets_for(0, Q, seed=0x0D470100 + j)).to(dev) for j in range(NB)]
 res = {"lib": _kl.LIB_PATH}
-for k in (32, 24, 20):
+for k in (32, 24, 20, 14, 16):
     outs = [T.nc_closest(tgs[j], k) for j in range(NB)]
     torch.cuda.synchronize()
     ts = []
