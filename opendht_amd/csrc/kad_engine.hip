@@ -5151,7 +5151,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) v
             W[32 * x + 4 * g + 2] = x4[x].z; W[32 * x + 4 * g + 3] = x4[x].w;
         }
     }
-    __syncthreads();
+    // (the octet's row is its own: its wave's LDS order suffices — reads past the row into a neighbour's, which
+    // another wave may still be writing, are masked out below)
+    wave_sync();
     if (ABL == 2) {
         if (line) out_idx[(size_t)qi * count + g] = W[g] ^ W[64 + g] ^ W[NC32_STRIDE - 1 - g];
         return;
