@@ -61,7 +61,8 @@ def parse_args(argv=None):
     ap.add_argument("--gather-json", default=os.path.join(ROOT, "profiles", "r03_mb_gather_nt.json"))
     ap.add_argument("--plumbing", action="store_true",
                     help="launcher/rendezvous check without a GPU: gloo ranks, barrier, max-over-ranks, one line")
-    ap.add_argument("--mode", choices=("owner", "allgather", "allgather-child", "rccl1-child"), default="owner",
+    ap.add_argument("--mode", choices=("owner", "allgather", "allgather-child", "owner-child", "rccl1-child"),
+                    default="owner",
                     help="owner: the headline (allgather measured as a sub-object); allgather: only the "
                          "north-star variant, as its own line; allgather-child: internal (allgather_child)")
     ap.add_argument("--verify-rows", type=int, default=1 << 16,
@@ -428,7 +429,10 @@ def main_owner(args):
     if not args.no_extras:
         extras["cold"] = cold_pass(T, tgs, outs, ocnt, cnt_k, Q, moved_q, dev, stream)
         # (before refresh_pass, which moves `now` and so the statuses the rows are checked against)
-        extras["owner_routed"] = owner_routed_pass(T, sh, spec, Q, cnt_k, K, W, dev, dist, world, rank)
+        # N > 1: in child processes whose data path runs on an RCCL group (owner_child); N = 1: no exchange here,
+        # and the same pass through a one-rank RCCL group in the rccl1 child (owner_routed.rccl_world1)
+        extras["owner_routed"] = (owner_routed_pass(T, sh, spec, Q, cnt_k, K, W, dev, dist, world, rank) if world == 1
+                                  else owner_child(args, world, rank, local, dist))
         extras["refresh"] = refresh_pass(T, sh, tgs, outs, ocnt, cnt_k, Q, avg_kernel_s, dev, stream)
         extras["host_buffers"] = host_pass(T, tgs, cnt_k, Q, dev)
         extras["other_counts"] = counts_pass(T, tgs, Q, dev, stream)
@@ -458,6 +462,10 @@ def main_owner(args):
         else:
             ag = allgather_child(args, world, rank, local, dist)
 
+    if isinstance(ag, dict) and isinstance(ag.get("rccl_world1"), dict) and "owner_routed" in ag["rccl_world1"]:
+        ow = extras.get("owner_routed")
+        if isinstance(ow, dict):
+            ow["rccl_world1"] = ag["rccl_world1"].pop("owner_routed")
     if rank == 0:
         line = {
             "metric": METRIC,
@@ -524,62 +532,210 @@ def main_owner(args):
         dist.destroy_process_group()
 
 
-def owner_routed_pass(T, sh, spec, Q, cnt_k, K, W, dev, dist, world, rank, NB=4):
+def data_backend(world: int, dev) -> str | None:
+    """The backend of owner routing's data-path group (the all_to_alls of the target blocks and the rows): RCCL over
+    xGMI whenever the ranks have a GPU each (world > 1 on CUDA devices); gloo only in the one-GPU rehearsal
+    (KADGPU_BENCH_ONE_GPU, every rank on cuda:0) and on CPU; none at world 1."""
+    if world <= 1:
+        return None
+    return "nccl" if dev.type == "cuda" and not REHEARSE_ONE_GPU else "gloo"
+
+
+def verify_routed(dist, sh, spec, rank, world, tg, idx, cnt, cnt_k, rows=65536) -> dict:
+    """Rows that came back through owner routing, checked by the ranks that own them: every rank's first `rows`
+    (target, row, count) triples are all-gathered over the default group (gloo, host tensors), and each rank checks
+    the triples whose target it owns against the CPU restatement (oracle/) on its own shard table. So the rows answered
+    by another rank and returned over the links ((N-1)/N of them) are checked as well as the rank's own."""
+    import torch
+
+    v = min(rows, tg.shape[0])
+    rec = np.concatenate([tg[:v].cpu().numpy(), idx[:v].cpu().numpy().view(np.uint8).reshape(v, -1),
+                          cnt[:v].cpu().numpy().reshape(v, 1)], axis=1)
+    src = np.full(v, rank, np.int64)
+    if world > 1:
+        parts = [torch.empty(rec.shape, dtype=torch.uint8) for _ in range(world)]
+        dist.all_gather(parts, torch.from_numpy(np.ascontiguousarray(rec)))
+        rec = np.concatenate([p.numpy() for p in parts])
+        src = np.repeat(np.arange(world), v)
+    own = (rec[:, 0].astype(np.int64) >> (8 - spec.shard_bits)) == rank if spec.shard_bits else np.ones(len(rec), bool)
+    r = rec[own]
+    bad = verify_rows(sh.ids, sh.status, sh.first, sh.off, sh.index_base, np.ascontiguousarray(r[:, :20]),
+                      np.ascontiguousarray(r[:, 20:20 + 4 * cnt_k]).view(np.int32),
+                      np.ascontiguousarray(r[:, 20 + 4 * cnt_k]), cnt_k)
+    cross = int((src[own] != rank).sum())
+    if world == 1:
+        dist = None  # (a one-rank group: nothing to sum)
+    return {"rows": sum_over_ranks(dist, int(own.sum())), "mismatches": sum_over_ranks(dist, bad),
+            "rows_answered_by_another_rank": sum_over_ranks(dist, cross),
+            "what": f"the first {v} rows of every rank's last batch, all-gathered; each row checked by the rank owning "
+                    "its target against the CPU restatement on that rank's shard table"}
+
+
+def routed_targets(Q, world, rank, dev, NB, seed=0x0D470600):
+    """NB batches of Q arbitrary targets per rank, spread uniformly over the `world` shards of the 8-shard layout's
+    first `world` shards (top three bits = a random rank < world)."""
+    import torch
+
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed + rank)
+    tgs = []
+    for _ in range(NB):
+        t = torch.randint(0, 256, (Q, 20), dtype=torch.uint8, device=dev, generator=g)
+        own = torch.randint(0, world, (Q,), dtype=torch.int32, device=dev, generator=g)
+        t[:, 0] = ((t[:, 0].to(torch.int32) & 0x1F) | (own << 5)).to(torch.uint8)
+        tgs.append(t)
+    return tgs
+
+
+def owner_routed_pass(T, sh, spec, Q, cnt_k, K, W, dev, dist, world, rank, NB=4, group=None, collective=None,
+                      pipelined=None):
     """The headline form as a serving front end, measured at this N: every rank holds Q arbitrary
     targets per step (uniform over the N shards), routes each to its owner and gets the rows back
-    (sharded.OwnerRoute.step: kad_route_pack, all_to_all_single of the target blocks — RCCL over xGMI at N > 1 —,
-    the owner's kad_rt_closest_batch over the blocks it received, kad_route_compress, all_to_all_single of the packed
-    rows back, kad_route_unpack_packed). W + K eager steps (collectives are not captured), barrier + synchronize on both sides, the
-    max over ranks; a distinct batch per step (NB rotated). At N = 1 there is no exchange (the local pack / query /
-    unpack)."""
+    (sharded.OwnerRoute.step: kad_route_pack, all_to_all_single of the target blocks on `group` — RCCL over xGMI at
+    N > 1 —, the owner's kad_rt_closest_batch_packed over the blocks it received, all_to_all_single of the packed
+    rows back, kad_route_unpack_packed). W + K eager steps (collectives are not captured), barrier + synchronize on
+    both sides, the max over ranks; a distinct batch per step (NB rotated); each step's overflow and escape words
+    folded on the device and read once after. `pipelined`: the same K batches through sharded.OwnerPipeline (batch
+    i's exchanges on a comm stream under batch i+1's pack and batch i's answer). At N = 1 without `collective` there
+    is no exchange (the local pack / query / unpack)."""
     import torch
 
     from opendht_amd.sharded import OwnerRoute
 
+    want = data_backend(world, dev)
+    coll = world > 1 if collective is None else bool(collective)
+    if world > 1 and dist.get_backend(group) != want:
+        raise RuntimeError(f"owner routing's data path must run on {want} at N = {world} "
+                           f"(got {dist.get_backend(group)})")
+    if pipelined is None:
+        pipelined = coll
     try:
-        g = torch.Generator(device=dev)
-        g.manual_seed(0x0D470600 + rank)
-        tgs = []
-        for _ in range(NB):
-            t = torch.randint(0, 256, (Q, 20), dtype=torch.uint8, device=dev, generator=g)
-            own = torch.randint(0, world, (Q,), dtype=torch.int32, device=dev, generator=g)
-            t[:, 0] = ((t[:, 0].to(torch.int32) & 0x1F) | (own << 5)).to(torch.uint8)
-            tgs.append(t)
+        tgs = routed_targets(Q, world, rank, dev, NB)
         s = torch.cuda.current_stream(dev).cuda_stream
-        R = OwnerRoute(Q, cnt_k, world, spec.shard_bits, dev)
-        oi = torch.empty((Q, cnt_k), dtype=torch.int32, device=dev)
-        oc = torch.empty((Q,), dtype=torch.uint8, device=dev)
+        R = OwnerRoute(Q, cnt_k, world, spec.shard_bits, dev, collective=coll)
+        outs = [(torch.empty((Q, cnt_k), dtype=torch.int32, device=dev), torch.empty((Q,), dtype=torch.uint8, device=dev))
+                for _ in range(NB)]
+        acc = torch.zeros((2,), dtype=torch.int32, device=dev)
         for _ in range(6):  # block capacities: grow until a step fits (decided together over the ranks)
-            R.step(T, tgs[0], oi, oc, None, s)
-            if not R.overflowed():
+            R.step(T, tgs[0], *outs[0], group, s)
+            if not R.overflowed(group):
                 break
-            R = R.grown()
-        t_max, ev_ms, how = graph_steps(lambda j: R.step(T, tgs[j % NB], oi, oc, None, s), K, W, dev, dist,
-                                        use_graph=False)
-        over = R.overflowed()
-        esc = R.escaped()  # (a row too wide to pack in some step: the last batch's way back again, unpacked)
-        last = tgs[(K - 1) % NB]
-        if esc:
+            R = R.grown(group)
+
+        def step(j):
+            R.step(T, tgs[j % NB], *outs[j % NB], group, s)
+            R.fold_flags(acc, s)
+
+        t_max, ev_ms, how = graph_steps(step, K, W, dev, dist, use_graph=False)
+        from opendht_amd.sharded import combine_max
+
+        over, esc = (bool(x) for x in combine_max(acc, group, coll))
+        last = (K - 1) % NB
+        if esc:  # (a row too wide to pack in some step: the last batch's way back again, unpacked)
             R.answer(T, s, packed=False)
-            R.back(oi, oc, None, s, packed=False)
+            R.back(*outs[last], group, s, packed=False)
             torch.cuda.synchronize(dev)
-        # the rows of this rank's own targets in the last step, against the restatement on its shard table
-        vt = last[:65536].cpu().numpy()
-        mine = (vt[:, 0].astype(np.int64) >> (8 - spec.shard_bits)) == rank
-        bad = verify_rows(sh.ids, sh.status, sh.first, sh.off, sh.index_base, vt[mine],
-                          oi[:65536].cpu().numpy()[mine], oc[:65536].cpu().numpy()[mine], cnt_k)
+        verified = verify_routed(dist, sh, spec, rank, world, tgs[last], *outs[last], cnt_k)
         xb = R.xgmi_bytes
-        return {"queries_per_s": world * Q * K / t_max, "ms_per_step": t_max / K * 1e3, "n_gpus": world,
-                "collective": (f"all_to_all_single ({'RCCL' if dist.get_backend() == 'nccl' else dist.get_backend()})"
-                               if world > 1 else None), "cap": R.cap, "overflow": over,
-                "rows_back": f"packed, {4 * R.pw} bytes per row" if R.packed else "plain", "escaped": esc,
-                "xgmi_bytes_per_rank_step": xb, "launch": how,
-                "verified": {"rows": sum_over_ranks(dist, int(mine.sum()), dev),
-                             "mismatches": sum_over_ranks(dist, bad, dev),
-                             "what": "each rank's own-shard targets among the first 65,536 of its last step"},
-                "how": owner_routed_pass.__doc__.split("\n\n")[0].replace("\n", " ")}
+        backend = dist.get_backend(group) if coll else None
+        res = {"queries_per_s": world * Q * K / t_max, "ms_per_step": t_max / K * 1e3, "n_gpus": world,
+               "collective": (f"all_to_all_single ({'RCCL' if backend == 'nccl' else backend})" if coll else None),
+               "cap": R.cap, "overflow": over,
+               "rows_back": f"packed, {4 * R.pw} bytes per row" if R.packed else "plain", "escaped": esc,
+               "xgmi_bytes_per_rank_step": xb, "launch": how, "verified": verified,
+               "how": owner_routed_pass.__doc__.split("\n\n")[0].replace("\n", " ")}
+        if pipelined:
+            res["pipelined"] = pipelined_pass(T, sh, spec, tgs, outs, Q, cnt_k, K, W, dev, dist, world, rank, R.cap,
+                                              group, coll)
+        return res
     except Exception as e:  # the headline line is printed whatever happens here
         return {"error": f"{type(e).__name__}: {e}"}
+
+
+def issue_timed(issue, K, dev, dist, graph_ok):
+    """Time K batches issued by issue(): eager (the wall time and the host's issue time alone), then — when graph_ok
+    (RCCL or no collective: gloo stages through the host and cannot be captured) — the same issue captured once as
+    one HIP graph (fork/join of the compute and comm streams by events, the RCCL collectives as graph nodes) and
+    replayed. Barrier + synchronize on both sides, max over ranks. Returns {mode: (max wall s, host issue s)}."""
+    import torch
+
+    out = {}
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    issue()
+    t1 = time.perf_counter()
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    out["eager"] = (max_over_ranks(dist, time.perf_counter() - t0, dev), max_over_ranks(dist, t1 - t0, dev))
+    if graph_ok:
+        try:
+            g = torch.cuda.CUDAGraph()
+            cur = torch.cuda.current_stream(dev)
+            cap = torch.cuda.Stream(dev)
+            cap.wait_stream(cur)
+            with torch.cuda.graph(g, stream=cap):
+                issue()
+            cur.wait_stream(cap)
+            g.replay()  # the first replay uploads the graph
+            torch.cuda.synchronize(dev)
+            if dist:
+                dist.barrier()
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            g.replay()
+            torch.cuda.synchronize(dev)
+            if dist:
+                dist.barrier()
+            out["graph"] = (max_over_ranks(dist, time.perf_counter() - t0, dev), 0.0)
+            del g
+        except Exception as e:
+            out["graph_error"] = f"{type(e).__name__}: {e}"
+    return out
+
+
+def pipelined_pass(T, sh, spec, tgs, outs, Q, cnt_k, K, W, dev, dist, world, rank, cap, group, coll):
+    """owner_routed_pass's K batches through sharded.OwnerPipeline (three buffer sets, compute and comm streams): the
+    same barrier + synchronize on both sides and max over ranks, the overflow / escape words folded on the device
+    and combined after; eager (with the host's issue time) and as one HIP graph of the K batches; the last batch's
+    rows checked by their owners."""
+    import torch
+
+    from opendht_amd.sharded import OwnerPipeline
+
+    NB = len(tgs)
+    P = OwnerPipeline(Q, cnt_k, world, spec.shard_bits, dev, cap=cap, collective=coll)
+    for _ in range(6):
+        P.run(T, tgs[:2], outs[:2], group)
+        over, esc = P.flags(group)
+        if not over:
+            break
+        P = P.grown(group)
+    P.run(T, [tgs[j % NB] for j in range(W)], [outs[j % NB] for j in range(W)], group)
+    torch.cuda.synchronize(dev)
+    P.flags(group)
+    # (no HIP graph around the torch RCCL collectives: capturing them crashed the one-rank RCCL child on this image,
+    # gpurun_out/r06b; the native executor, kad_comm, issues the pipeline from C++ instead)
+    tm = issue_timed(lambda: P.run(T, [tgs[j % NB] for j in range(K)], [outs[j % NB] for j in range(K)], group), K,
+                     dev, dist, graph_ok=not coll)
+    over, esc = P.flags(group)
+    last = (K - 1) % NB
+    if esc:
+        P.run(T, [tgs[last]], [outs[last]], group, packed=False)
+        torch.cuda.synchronize(dev)
+        P.flags(group)
+    best = "graph" if "graph" in tm else "eager"
+    t_max = tm[best][0]
+    res = {"queries_per_s": world * Q * K / t_max, "ms_per_step": t_max / K * 1e3, "launch": best,
+           "eager_ms_per_step": tm["eager"][0] / K * 1e3, "eager_host_issue_ms_per_step": tm["eager"][1] / K * 1e3,
+           "cap": P.cap, "overflow": over, "escaped": esc,
+           "verified": verify_routed(dist, sh, spec, rank, world, tgs[last], *outs[last], cnt_k),
+           "how": OwnerPipeline.__doc__.split("\n\n")[0].replace("\n", " ")}
+    if "graph_error" in tm:
+        res["graph_error"] = tm["graph_error"]
+    return res
 
 
 def owner_step_model(T, Q, cnt_k, dev, stream, avg_kernel_s, link_gbs=64.0, lat_us=10.0, reps=20):
@@ -1301,6 +1457,10 @@ def allgather_pass(args, world, rank, local, dev, dist):
             ex = G._ex[(Q, cnt_k, world, True, world > 1)] = ex.grown()
         else:
             raise RuntimeError("exchange buffers kept overflowing")
+        try:
+            pipe, pi, pc = north_star_pipelined(G, ex, tgs, Q, cnt_k, K, NB, dev, dist, world, rank)
+        except Exception as e:
+            pipe, pi = {"error": f"{type(e).__name__}: {e}"}, None
         # verification: this rank's home rows (queries [lo, hi)) among the first vrows whose targets this rank
         # owns, against the restatement on this rank's shard WITH its exact halo (every owned window lies inside)
         G.close()
@@ -1311,6 +1471,12 @@ def allgather_pass(args, world, rank, local, dev, dist):
         sh = build_shard(spec, rank)
         bad = verify_rows(sh.ids, sh.status, sh.first, sh.off, sh.index_base, vt[own],
                           oi[:vt.shape[0]].cpu().numpy()[own], oc[:vt.shape[0]].cpu().numpy()[own], cnt_k)
+        if pi is not None:
+            pbad = verify_rows(sh.ids, sh.status, sh.first, sh.off, sh.index_base, vt[own],
+                               pi[:vt.shape[0]].cpu().numpy()[own], pc[:vt.shape[0]].cpu().numpy()[own], cnt_k)
+            pipe["verified"] = {"rows": sum_over_ranks(dist, int(own.sum()), dev),
+                                "mismatches": sum_over_ranks(dist, pbad, dev)}
+        res["pipelined"] = pipe
         res.update({"value": Q * K / t_max, "ms_per_step": t_max / K * 1e3, "avg_step_ms_events": kern_ms,
                     "launch": how,
                     "workload": f"100M-node U(24) table, 1/{world} per GPU without halo ({n_local} nodes on rank 0), "
@@ -1326,6 +1492,36 @@ def allgather_pass(args, world, rank, local, dev, dist):
         return res
     G.close()
     return res
+
+
+def north_star_pipelined(G, ex, tgs, Q, cnt_k, K, NB, dev, dist, world, rank):
+    """The north-star step over K consecutive batches through GlobalShard.run_pipelined (three exchange buffer sets
+    with ex's grown capacities; batch i+1's all_to_all under batch i's finish and batch i+2's shard kernel): eager
+    and as one HIP graph of the K batches (issue_timed; RCCL only), the sticky overflow words of the three sets
+    combined after. Returns (the object, this rank's home rows of the last batch)."""
+    import torch
+
+    from opendht_amd.global_shard import home_range
+
+    lo, hi = home_range(Q, world, rank)
+    exs = G.pipeline(Q, cnt_k, world, like=ex)
+    outs = [(torch.empty((hi - lo, cnt_k), dtype=torch.int32, device=dev),
+             torch.empty((hi - lo,), dtype=torch.uint8, device=dev)) for _ in range(NB)]
+    G.run_pipelined([tgs[j % NB] for j in range(3)], exs, [outs[j % NB] for j in range(3)], None, rank)
+    torch.cuda.synchronize(dev)
+    over0 = any(e.overflowed() for e in exs)
+    tm = issue_timed(lambda: G.run_pipelined([tgs[j % NB] for j in range(K)], exs, [outs[j % NB] for j in range(K)],
+                                             None, rank), K, dev, dist, graph_ok=False)
+    over = any(e.overflowed() for e in exs)
+    oi, oc = outs[(K - 1) % NB]
+    best = "graph" if "graph" in tm else "eager"
+    res = {"value": Q * K / tm[best][0], "ms_per_step": tm[best][0] / K * 1e3, "launch": best,
+           "eager_ms_per_step": tm["eager"][0] / K * 1e3, "eager_host_issue_ms_per_step": tm["eager"][1] / K * 1e3,
+           "overflow": over or over0,
+           "how": "GlobalShard.run_pipelined: " + G.run_pipelined.__doc__.split("\n\n")[0].replace("\n", " ")}
+    if "graph_error" in tm:
+        res["graph_error"] = tm["graph_error"]
+    return res, oi, oc
 
 
 def home0_recv(G0, ex, tg, Q, dev):
@@ -1461,9 +1657,20 @@ def exchange_model(Q, count, dev, link_gbs=64.0):
 
 
 def allgather_child(args, world, rank, local, dist) -> dict:
-    """The north-star variant at N > 1 in child processes (one per rank, the same GPU), so that a failing or
-    hanging RCCL collective can cost only the `allgather` object, never the headline line: each rank starts
-    its child with a shared fresh port and waits at most --ag-timeout seconds."""
+    """The north-star variant at N > 1 in child processes (rank_child)."""
+    return rank_child(args, world, rank, local, dist, "allgather-child")
+
+
+def owner_child(args, world, rank, local, dist) -> dict:
+    """The owner-routed serving step at N > 1 in child processes (rank_child, main_owner_child): its data path runs on
+    an RCCL group, and a failing or hanging RCCL collective can cost only the `owner_routed` object."""
+    return rank_child(args, world, rank, local, dist, "owner-child")
+
+
+def rank_child(args, world, rank, local, dist, mode) -> dict:
+    """A part of the line measured at N > 1 in child processes (one per rank, the same GPU), so that a failing or
+    hanging RCCL collective can cost only that object, never the headline line: each rank starts its child with a
+    shared fresh port and waits at most --ag-timeout seconds."""
     import tempfile
 
     port = [0]
@@ -1472,26 +1679,65 @@ def allgather_child(args, world, rank, local, dist) -> dict:
             so.bind(("127.0.0.1", 0))
             port[0] = so.getsockname()[1]
     dist.broadcast_object_list(port, src=0)
-    out = os.path.join(tempfile.gettempdir(), f"kadgpu_ag_{port[0]}_{rank}.json")
+    out = os.path.join(tempfile.gettempdir(), f"kadgpu_{mode}_{port[0]}_{rank}.json")
     env = dict(os.environ, RANK=str(rank), LOCAL_RANK=str(local), WORLD_SIZE=str(world),
                LOCAL_WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port[0]))
-    argv = [sys.executable, "-u", os.path.abspath(__file__), "--gpus", str(world), "--mode", "allgather-child",
-            "--ag-out", out, "--queries", str(args.queries), "--steps", str(args.steps), "--count", str(args.count),
-            "--verify-rows", str(args.verify_rows)]
+    argv = [sys.executable, "-u", os.path.abspath(__file__), "--gpus", str(world), "--mode", mode,
+            "--ag-out", out, "--queries", str(args.queries), "--steps", str(args.steps), "--warmup", str(args.warmup),
+            "--count", str(args.count), "--verify-rows", str(args.verify_rows)]
     p = subprocess.Popen(argv, env=env, stdout=sys.stderr)  # the child's output never reaches the JSON line
     try:
         rc = p.wait(timeout=args.ag_timeout)
     except subprocess.TimeoutExpired:
         p.kill()
         p.wait()
-        return {"error": f"rank {rank}: the north-star child was killed after {args.ag_timeout:.0f} s"}
+        return {"error": f"rank {rank}: the {mode} process was killed after {args.ag_timeout:.0f} s"}
     try:
         with open(out) as f:
             res = json.load(f)
         os.unlink(out)
     except (OSError, ValueError):
-        res = {"error": f"rank {rank}: the north-star child exited with {rc} and no result"}
+        res = {"error": f"rank {rank}: the {mode} process exited with {rc} and no result"}
     return res
+
+
+def main_owner_child(args):
+    """owner_routed_pass at N > 1 (owner_child): the default group is gloo (barriers, max over ranks, the verification
+    gather), the data path's all_to_alls run on a second group of data_backend() — RCCL over xGMI on the driver's
+    node, one GPU per rank."""
+    from datetime import timedelta
+
+    import torch
+    import torch.distributed as dist
+
+    from opendht_amd import DeviceTable
+    from opendht_amd.sharded import build_shard, config3_spec
+
+    world, rank, local = dist_env()
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist.init_process_group("gloo", timeout=timedelta(seconds=600))
+    res = {}
+    try:
+        be = data_backend(world, dev)
+        group = dist.new_group(backend=be, timeout=timedelta(seconds=120)) if be == "nccl" else None
+        spec = config3_spec()
+        sh = build_shard(spec, rank)
+        T = DeviceTable(sh.ids, sh.status, sh.first, sh.off, device=local, index_base=sh.index_base, sorted=True)
+        try:
+            res = owner_routed_pass(T, sh, spec, args.queries, args.count, args.steps, args.warmup, dev, dist, world,
+                                    rank, group=group)
+        finally:
+            T.close()
+    except Exception as e:
+        res = {"error": f"rank {rank}: {type(e).__name__}: {e}"}
+    with open(args.ag_out, "w") as f:
+        json.dump(res, f)
+    try:
+        dist.destroy_process_group()
+    except Exception:
+        pass
+    return 0 if "error" not in res else 1
 
 
 def rccl_world1_child(args) -> dict:
@@ -1589,7 +1835,31 @@ def rccl1_pass(args) -> dict:
                 b.record(stream)
                 torch.cuda.synchronize(dev)
                 res["all_to_all_us"] = a.elapsed_time(b) / K * 1e3
+                # the same K batches pipelined (the all_to_all on a comm stream under the next shard kernel)
+                try:
+                    pipe, pi, pc = north_star_pipelined(G, ex, tgs, Q, cnt_k, K, NB, dev, dist, 1, 0)
+                    pipe["step_us"] = pipe.pop("ms_per_step") * 1e3
+                    pipe["verified"] = {"rows": vrows, "mismatches": verify_rows(
+                        ids, st, first, off, 0, tgs[(K - 1) % NB][:vrows].cpu().numpy(), pi[:vrows].cpu().numpy(),
+                        pc[:vrows].cpu().numpy(), cnt_k)}
+                    res["pipelined"] = pipe
+                except Exception as e:
+                    res["pipelined"] = {"error": f"{type(e).__name__}: {e}"}
         G.close()
+        del ids, st
+        # owner routing through the one-rank RCCL group: config 3's rank-0 shard with its halo,
+        # the targets (all owned by shard 0) through kad_route_pack, the RCCL all_to_all of the target blocks, the
+        # packed query, the RCCL all_to_all of the packed rows, the unpack; then the same batches pipelined
+        from opendht_amd import DeviceTable
+        from opendht_amd.sharded import build_shard
+
+        sh = build_shard(spec, 0)
+        T = DeviceTable(sh.ids, sh.status, sh.first, sh.off, device=0, index_base=sh.index_base, sorted=True)
+        try:
+            res["owner_routed"] = owner_routed_pass(T, sh, spec, Q, cnt_k, K, 2, dev, dist, 1, 0, group=None,
+                                                    collective=True, pipelined=True)
+        finally:
+            T.close()
         res["how"] = ("Exchange(world=1, collective=True): the all_to_all_single of the one send block runs through "
                       "RCCL (a device copy at world 1); the difference to step_us_no_collective is its cost")
         return res
@@ -1685,6 +1955,8 @@ def main(argv=None):
         return main_allgather_line(args)
     if args.mode == "allgather-child":
         return main_allgather_child(args)
+    if args.mode == "owner-child":
+        return main_owner_child(args)
     if args.mode == "rccl1-child":
         return main_rccl1_child(args)
     return main_owner(args)

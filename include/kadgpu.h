@@ -451,7 +451,8 @@ int kad_rt_home_finish_reset(const uint32_t* recv, uint32_t* send, uint32_t worl
  *   KAD_ROUTE_CTR_WORDS(world) words, zeroed by the call; ctr[(d * KAD_ROUTE_SUBS + r) * KAD_ROUTE_CSTRIDE] ends as
  *   sub-block r of block d's record count (it may exceed its capacity). The order of the records inside a sub-block
  *   is unspecified; records past a sub-block's count are left as they were (the owner answers them too; their rows
- *   are never read back). Async on stream.
+ *   are never read back). targets, send, slot and ctr must be 4-byte aligned (KAD_ERR_INVALID otherwise). Async on
+ *   stream.
  * kad_route_unpack: rows returned in the send layout (back_idx: world * cap rows of `count` uint32, back_cnt: world *
  *   cap bytes) back to each query's position: out_idx row i = back_idx row slot[i], out_cnt[i] = back_cnt[slot[i]]
  *   (KAD_NO_NODE and 0 for slot KAD_NO_NODE). Async on stream. All pointers are device pointers. */

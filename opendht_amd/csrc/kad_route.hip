@@ -279,6 +279,9 @@ extern "C" int kad_route_pack(const uint8_t* targets, uint32_t q, uint32_t world
     if (cap == 0 || cap % KAD_ROUTE_SUBS || (uint64_t)world * cap >= NONE)
         return set_error(KAD_ERR_INVALID, "cap must be a positive multiple of KAD_ROUTE_SUBS and world * cap < 2^32 - 1");
     if (!ctr || (q && (!targets || !send || !slot))) return set_error(KAD_ERR_INVALID, "NULL buffer");
+    // the kernel moves the 20-byte records as five dwords, the slots and counters as dwords
+    if (((uintptr_t)targets | (uintptr_t)send | (uintptr_t)slot | (uintptr_t)ctr) & 3u)
+        return set_error(KAD_ERR_INVALID, "targets, send, slot and ctr must be 4-byte aligned");
     DevSwitch g(device);
     hipStream_t s = (hipStream_t)stream;
     hipError_t e = hipMemsetAsync(ctr, 0, 4ull * KAD_ROUTE_CTR_WORDS(world), s);

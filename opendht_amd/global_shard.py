@@ -322,6 +322,58 @@ class GlobalShard:
                     gather_into(ex.recv, ex.send, group)
         ex.finish(out_idx, out_cnt, C.c_void_p(s))
 
+    def pipeline(self, q: int, count: int, world: int, like: Exchange | None = None) -> list:
+        """Three home-exchange buffer sets (collective) for run_pipelined, with the capacities of `like` (a grown
+        exchange of the same shape) or the defaults."""
+        rc, pc = (like.row_cap, like.part_cap) if like is not None else (None, None)
+        return [Exchange(q, count, world, self.dev, row_cap=rc, part_cap=pc, collective=True) for _ in range(3)]
+
+    def run_pipelined(self, batches, exs, outs, group=None, rank: int = 0):
+        """The north-star step over consecutive batches with the exchange overlapped: three Exchange
+        buffer sets, a compute stream (kad_rt_shard_step_home, kad_rt_home_finish_reset) and a comm stream (the
+        all_to_all_single), ordered by events. For batch i the host issues
+
+            compute:  shard kernel(i+1)                    finish(i)
+            comm:                      all_to_all(i+1)
+
+        so the all_to_all of batch i+1 runs under batch i's finish and batch i+2's shard kernel. A set is reused by
+        batch i+3 only after batch i's finish (which zeroed its send counters, on the same compute stream); batch i+1's
+        all_to_all writes its receive blocks only after batch i-2's finish read them. outs[i] = (out_idx, out_cnt):
+        this rank's home rows of batch i. No host read: check overflowed() on every set after (any(...))."""
+        import torch
+
+        if not all(ex.collective and ex.home for ex in exs) or len(exs) != 3:
+            raise ValueError("run_pipelined takes three collective home exchanges (GlobalShard.pipeline)")
+        cur = torch.cuda.current_stream(self.dev)
+        if not hasattr(self, "_streams"):
+            self._streams = (torch.cuda.Stream(self.dev), torch.cuda.Stream(self.dev))
+        cs, xs = self._streams
+        cs.wait_stream(cur)
+        xs.wait_stream(cur)
+        n = len(batches)
+        sent = [None] * n
+
+        def shard(i):
+            ex = exs[i % 3]
+            self.home_block(batches[i], ex, cs.cuda_stream, zeroed=True)
+            e = torch.cuda.Event()
+            e.record(cs)
+            xs.wait_event(e)
+            with torch.cuda.stream(xs):
+                exchange_into(ex.recv, ex.send, group)
+            sent[i] = torch.cuda.Event()
+            sent[i].record(xs)
+
+        if n:
+            shard(0)
+        for i in range(n):
+            if i + 1 < n:
+                shard(i + 1)
+            cs.wait_event(sent[i])
+            exs[i % 3].home_finish(rank, outs[i][0], outs[i][1], C.c_void_p(cs.cuda_stream), reset=True)
+        cur.wait_stream(cs)
+        cur.wait_stream(xs)
+
     def query(self, targets, count: int, group=None, out_idx=None, out_cnt=None, single_rank_shard_kernel=False,
               home: bool = True, force_collective: bool = False):
         """RoutingTable::findClosestNodes over a replicated batch: local rows and parts, the exchange (RCCL /
@@ -425,37 +477,18 @@ def exchange_into(recv, send, group=None):
         return
     world, rank = dist.get_world_size(group), dist.get_rank(group)
     cs = send.cpu()
-    if _host_all_to_all(group, world):
-        cr = torch.empty_like(cs)
+    cr = torch.empty_like(cs)
+    try:
         dist.all_to_all_single(cr, cs, group=group)  # a real failure (timeout, dead peer) raises
-    else:
+    except (RuntimeError, NotImplementedError) as e:
+        # a backend without all_to_all refuses it locally, before any communication, and the same way on every
+        # rank (same backend), so every rank takes the all-gather together; nothing is cached per group
+        if "not supported" not in str(e).lower() and "not implemented" not in str(e).lower():
+            raise
         full = [torch.empty_like(cs) for _ in range(world)]
         dist.all_gather(full, cs, group=group)
         cr = torch.cat([f.view(world, -1)[rank] for f in full])
     recv.copy_(cr.to(recv.device))
-
-
-_A2A_OK: dict = {}
-
-
-def _host_all_to_all(group, world: int) -> bool:
-    """Whether this (gloo) group runs all_to_all_single on host tensors: probed once per group with a tiny
-    collective that every rank reaches at the same call (so all ranks then take the same collective), cached.
-    Only the probe's own "unsupported" errors select the all-gather fallback."""
-    import torch
-    import torch.distributed as dist
-
-    key = id(group) if group is not None else None
-    if key not in _A2A_OK:
-        try:
-            x = torch.zeros(world, dtype=torch.int32)
-            dist.all_to_all_single(torch.empty_like(x), x, group=group)
-            _A2A_OK[key] = True
-        except (RuntimeError, NotImplementedError) as e:
-            if "not supported" not in str(e).lower() and "not implemented" not in str(e).lower():
-                raise
-            _A2A_OK[key] = False
-    return _A2A_OK[key]
 
 
 def gather_into(recv, send, group=None):

@@ -315,6 +315,7 @@ class OwnerRoute:
         self.cap = S * max(1, min(qs, sub or nominal + 6 * int(np.sqrt(nominal)) + 32))
         n = world * self.cap
         self.send = torch.empty((n, 20), dtype=torch.uint8, device=device)
+        pad_blocks(self.send, world, shard_bits, self.cap)
         self.recv = torch.empty_like(self.send) if self.collective else self.send
         self.slot = torch.empty((max(q, 1),), dtype=torch.int32, device=device)
         self.ctr = torch.zeros((route_ctr_words(world),), dtype=torch.int32, device=device)
@@ -394,36 +395,63 @@ class OwnerRoute:
         packed=False: the way back unpacked (the rerun of a batch whose rows escaped packing)."""
         import torch
 
-        from .global_shard import _torch_stream
-
         s = stream if stream is not None else torch.cuda.current_stream(self.dev).cuda_stream
         packed = self.packed if packed is None else packed
         self.pack(targets, s)
-        if self.collective:
-            with torch.cuda.stream(_torch_stream(s, self.dev)):
-                _all_to_all(self.recv, self.send, group)
+        self.send_targets(group, s)
         self.answer(table, s, packed)
         self.back(out_idx, out_cnt, group, s, packed)
 
     def back(self, out_idx, out_cnt, group, s, packed: bool):
         """The way back of the answered rows: return + unpack (packed or not)."""
+        if packed and not getattr(self, "fused", False):
+            self.compress(s)
+        self.send_back(group, s, packed)
+        self.unpack_rows(out_idx, out_cnt, s, packed)
+
+    def send_targets(self, group, s):
+        """The target blocks to their owners (all_to_all_single on stream s; nothing without a collective)."""
         import torch
 
         from .global_shard import _torch_stream
 
-        if packed:
-            if not getattr(self, "fused", False):
-                self.compress(s)
-            if self.collective:
-                with torch.cuda.stream(_torch_stream(s, self.dev)):
-                    _all_to_all(self.back_prow, self.prow, group)
-            self.unpack_packed(out_idx, out_cnt, s)
-            return
         if self.collective:
             with torch.cuda.stream(_torch_stream(s, self.dev)):
+                _all_to_all(self.recv, self.send, group)
+
+    def send_back(self, group, s, packed: bool):
+        """The answered rows back to their senders (packed: one all_to_all_single of the packed rows, already
+        written; else the rows and the counts)."""
+        import torch
+
+        from .global_shard import _torch_stream
+
+        if not self.collective:
+            return
+        with torch.cuda.stream(_torch_stream(s, self.dev)):
+            if packed:
+                _all_to_all(self.back_prow, self.prow, group)
+            else:
                 _all_to_all(self.back_rows, self.rows, group)
                 _all_to_all(self.back_cnt, self.cnt, group)
-        self.unpack(out_idx, out_cnt, s)
+
+    def unpack_rows(self, out_idx, out_cnt, s, packed: bool):
+        if packed:
+            self.unpack_packed(out_idx, out_cnt, s)
+        else:
+            self.unpack(out_idx, out_cnt, s)
+
+    def fold_flags(self, acc, s):
+        """acc (2 int32, device) |= this batch's overflow and escape words, on stream s: kad_route_pack zeroes both
+        with the counters, so a caller running many batches folds them after each one and reads acc once."""
+        import torch
+
+        from ._lib import route_overflow_word
+        from .global_shard import _torch_stream
+
+        w = route_overflow_word(self.world)
+        with torch.cuda.stream(_torch_stream(s, self.dev)):
+            torch.maximum(acc, self.ctr[w:w + 2], out=acc)
 
     def escaped(self, group=None, combine: bool = True) -> bool:
         """Host read of the packing escape word (a row spanning more than 254 indices), combined over the ranks."""
@@ -440,23 +468,13 @@ class OwnerRoute:
         return self._flag(route_overflow_word(self.world), group, combine)
 
     def _flag(self, w: int, group, combine: bool) -> bool:
-        ov = self.ctr[w:w + 1]
-        if combine and self.collective:
-            import torch.distributed as dist
+        return bool(combine_max(self.ctr[w:w + 1], group, combine and self.collective)[0])
 
-            if dist.get_backend(group) == "nccl":
-                dist.all_reduce(ov, op=dist.ReduceOp.MAX, group=group)
-            else:
-                h = ov.cpu()
-                dist.all_reduce(h, op=dist.ReduceOp.MAX, group=group)
-                ov.copy_(h)
-        return bool(int(ov.item()))
-
-    def need(self, group=None) -> int:
-        """The block capacity the last pack needed (8 x its fullest sub-block), combined over the ranks."""
+    def need(self, group=None, local: int | None = None) -> int:
+        """The block capacity the last pack needed (8 x its fullest sub-block; or `local`), combined over the ranks."""
         import torch
 
-        n = need_of(self.ctr, self.world)
+        n = need_of(self.ctr, self.world) if local is None else int(local)
         if self.collective:
             import torch.distributed as dist
 
@@ -471,6 +489,39 @@ class OwnerRoute:
         return OwnerRoute(self.q, self.count, self.world, self.shard_bits, self.dev,
                           cap=min(self.cap_max, max(2 * self.cap, n * 5 // 4)), collective=self.collective,
                           packed=self.packed)
+
+
+def combine_max(words, group=None, combine: bool = True) -> list[int]:
+    """Host read of a few device int32 words, each the MAX over the ranks when `combine` (RCCL: a device-tensor
+    all_reduce on the group; gloo: through a host tensor), so that every rank decides the same."""
+    if combine:
+        import torch.distributed as dist
+
+        if dist.get_backend(group) == "nccl":
+            dist.all_reduce(words, op=dist.ReduceOp.MAX, group=group)
+        else:
+            h = words.cpu()
+            dist.all_reduce(h, op=dist.ReduceOp.MAX, group=group)
+            words.copy_(h)
+    return [int(x) for x in words.cpu()]
+
+
+def pad_blocks(send, world: int, shard_bits: int, cap: int):
+    """Fill every record of the `world` send blocks with a padding target owned by the block's rank, in the middle of
+    its shard (byte 0 = d << (8 - shard_bits) | half of the rest, the other 19 bytes zero). The owner answers the
+    whole of every block it receives, so records past a sub-block's count are answered too: before their first use
+    they would otherwise be uninitialised memory whose rows could span more than 254 indices and set the packing
+    escape word for the whole batch (then stale targets of the same owner, which pack like any other)."""
+    import torch
+
+    send.zero_()
+    b = torch.arange(world, dtype=torch.int32, device=send.device)
+    v = send.view(world, cap, 20)
+    if shard_bits >= 8:
+        v[:, :, 0] = b.to(torch.uint8)[:, None]
+        v[:, :, 1] = 0x80
+    else:
+        v[:, :, 0] = ((b << (8 - shard_bits)) | (1 << (7 - shard_bits))).to(torch.uint8)[:, None]
 
 
 def need_of(ctr, world: int) -> int:
@@ -493,18 +544,32 @@ def _all_to_all(recv, send, group=None):
     exchange_into(recv.view(-1), send.view(-1), group)
 
 
-def serve_owner(table, targets, count: int, route: OwnerRoute | None = None, group=None, stream=None):
+def owner_shard_bits(world: int, spec: ShardSpec | None = None) -> int:
+    """The routing bits of owner routing over `world` ranks, one shard per rank: kad_route_pack sends a target to rank
+    (byte 0 >> (8 - shard_bits)) % world, which is the rank holding its shard only when the table has exactly `world`
+    shards and `world` is a power of two. Anything else raises instead of answering from the wrong shard."""
+    if world < 1 or world & (world - 1):
+        raise ValueError(f"owner routing needs a power-of-two world size, got {world}")
+    if spec is not None and spec.n_shards != world:
+        raise ValueError(f"the table has {spec.n_shards} shards but the group {world} ranks: one shard per rank")
+    return world.bit_length() - 1
+
+
+def serve_owner(table, targets, count: int, route: OwnerRoute | None = None, group=None, stream=None,
+                spec: ShardSpec | None = None):
     """Answer a batch of arbitrary targets through the owner-routed shards (every rank calls it with its own batch):
     returns (out_idx, out_cnt, route) with each query's row at its position. Grows the blocks and runs again when
-    one overflowed (the decision combined over the ranks)."""
+    one overflowed (the decision combined over the ranks). spec: the ShardSpec the tables were built from (checked
+    against the group: one shard per rank)."""
     import torch
     import torch.distributed as dist
 
     q = targets.shape[0]
     world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
     if route is None:
-        shard_bits = (world.bit_length() - 1) if world > 1 else 0
-        route = OwnerRoute(q, count, world, shard_bits, targets.device)
+        route = OwnerRoute(q, count, world, owner_shard_bits(world, spec), targets.device)
+    elif route.world != world:
+        raise ValueError(f"route built for {route.world} ranks, group has {world}")
     out_idx = torch.empty((q, count), dtype=torch.int32, device=targets.device)
     out_cnt = torch.empty((q,), dtype=torch.uint8, device=targets.device)
     while True:
@@ -518,6 +583,133 @@ def serve_owner(table, targets, count: int, route: OwnerRoute | None = None, gro
                 route.back(out_idx, out_cnt, group, s, packed=False)
             return out_idx, out_cnt, route
         route = route.grown(group)
+
+
+class OwnerPipeline:
+    """Owner routing of consecutive batches with the exchanges overlapped: three OwnerRoute buffer
+    sets, a compute stream (pack, answer, unpack: the kernels) and a comm stream (the all_to_alls), ordered by events.
+    The host issues, for batch i,
+
+        compute:  pack(i+1)                answer(i)                 unpack(i-1)
+        comm:                 targets(i+1)             rows back(i)
+
+    so batch i+1's pack and batch i's answer run while batch i's and i-1's blocks are on the links. A buffer set is
+    reused by batch i+3 only after batch i's unpack (same compute stream, issued before): three sets, never two
+    (pack(i+1) would overwrite the slots unpack(i-1) still reads). No host read inside run(): each batch's overflow
+    and escape words are folded into one device accumulator; check overflowed() / escaped() after (combined over the
+    ranks), and run the batches again grown() / unpacked when set."""
+
+    DEPTH = 3
+
+    def __init__(self, q: int, count: int, world: int, shard_bits: int, device, cap: int | None = None,
+                 collective: bool | None = None, packed: bool | None = None):
+        import torch
+
+        self.routes = [OwnerRoute(q, count, world, shard_bits, device, cap=cap, collective=collective, packed=packed)
+                       for _ in range(self.DEPTH)]
+        r = self.routes[0]
+        self.q, self.count, self.world, self.shard_bits, self.dev = q, count, world, shard_bits, device
+        self.cap, self.packed, self.collective = r.cap, r.packed, r.collective
+        self.compute = torch.cuda.Stream(device)
+        self.comm = torch.cuda.Stream(device)
+        self.acc = torch.zeros((2,), dtype=torch.int32, device=device)  # [overflow, escape] over the batches run
+
+    def run(self, table, batches, outs, group=None, packed: bool | None = None):
+        """Route every batch of `batches` ((q, 20) device targets) and unpack its rows into outs[i] = (out_idx,
+        out_cnt). Returns when everything is issued; the caller's current stream waits for the last unpack."""
+        import torch
+
+        packed = self.packed if packed is None else bool(packed)
+        cur = torch.cuda.current_stream(self.dev)
+        cs, xs = self.compute, self.comm
+        cs.wait_stream(cur)
+        xs.wait_stream(cur)
+        n = len(batches)
+        sent, back = [None] * n, [None] * n
+        c, x = cs.cuda_stream, xs.cuda_stream
+        R = lambda i: self.routes[i % self.DEPTH]  # noqa: E731
+
+        def pack(i):
+            R(i).pack(batches[i], c)
+            e = torch.cuda.Event()
+            e.record(cs)
+            xs.wait_event(e)
+            R(i).send_targets(group, x)
+            sent[i] = torch.cuda.Event()
+            sent[i].record(xs)
+
+        def answer(i):
+            r = R(i)
+            cs.wait_event(sent[i])
+            r.answer(table, c, packed)
+            if packed and not r.fused:
+                r.compress(c)
+            e = torch.cuda.Event()
+            e.record(cs)
+            xs.wait_event(e)
+            r.send_back(group, x, packed)
+            back[i] = torch.cuda.Event()
+            back[i].record(xs)
+
+        def unpack(i):
+            r = R(i)
+            cs.wait_event(back[i])
+            r.unpack_rows(outs[i][0], outs[i][1], c, packed)
+            r.fold_flags(self.acc, c)
+
+        if n:
+            pack(0)
+        for i in range(n):
+            if i + 1 < n:
+                pack(i + 1)
+            answer(i)
+            if i >= 1:
+                unpack(i - 1)
+        if n:
+            unpack(n - 1)
+        cur.wait_stream(cs)
+        cur.wait_stream(xs)
+
+    def flags(self, group=None, combine: bool = True) -> tuple[bool, bool]:
+        """(overflowed, escaped) over every batch run since the last call, combined over the ranks; cleared."""
+        ov, esc = combine_max(self.acc, group, combine and self.collective)
+        self.acc.zero_()
+        return bool(ov), bool(esc) and self.packed
+
+    def grown(self, group=None) -> "OwnerPipeline":
+        """Larger blocks, sized from the fullest sub-block of the last batch each buffer set packed (combined)."""
+        n = max(need_of(r.ctr, self.world) for r in self.routes)
+        n = self.routes[0].need(group, local=n) if self.collective else n
+        cap = min(self.routes[0].cap_max, max(2 * self.cap, n * 5 // 4))
+        return OwnerPipeline(self.q, self.count, self.world, self.shard_bits, self.dev, cap=cap,
+                             collective=self.collective, packed=self.packed)
+
+
+def serve_pipelined(table, batches, count: int, pipe: OwnerPipeline | None = None, group=None, outs=None):
+    """serve_owner for a run of batches through the overlapped OwnerPipeline: grows the blocks and runs everything
+    again when some batch overflowed, and again with the rows back unpacked when some row escaped packing (both
+    decisions combined over the ranks). Returns (outs, pipe)."""
+    import torch
+    import torch.distributed as dist
+
+    q = batches[0].shape[0]
+    dev = batches[0].device
+    world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+    if pipe is None:
+        pipe = OwnerPipeline(q, count, world, owner_shard_bits(world), dev)
+    if outs is None:
+        outs = [(torch.empty((q, count), dtype=torch.int32, device=dev), torch.empty((q,), dtype=torch.uint8,
+                                                                                     device=dev)) for _ in batches]
+    while True:
+        pipe.run(table, batches, outs, group)
+        over, esc = pipe.flags(group)
+        if over:
+            pipe = pipe.grown(group)
+            continue
+        if esc:
+            pipe.run(table, batches, outs, group, packed=False)
+            pipe.flags(group)
+        return outs, pipe
 
 
 def route_simulated(tables, batches, count: int, shard_bits: int, cap: int | None = None, packed: bool = False):

@@ -31,7 +31,8 @@ import torch.distributed as dist  # noqa: E402
 import oracle as O  # noqa: E402
 from opendht_amd import synth as S  # noqa: E402
 from opendht_amd.global_shard import Exchange, GlobalShard, build_plain_shard  # noqa: E402
-from opendht_amd.sharded import OwnerRoute, ShardSpec, return_results, route_queries, serve_owner  # noqa: E402
+from opendht_amd.sharded import (OwnerPipeline, OwnerRoute, ShardSpec, return_results, route_queries,  # noqa: E402
+                                 serve_owner, serve_pipelined)
 from opendht_amd.table import DeviceTable  # noqa: E402
 
 
@@ -104,6 +105,30 @@ def main():
             assert route.cap > 1
             np.testing.assert_array_equal(oc.cpu().numpy(), wcnt, err_msg=f"owner route k={count} counts")
             np.testing.assert_array_equal(oi.cpu().numpy().view(np.uint32), want, err_msg=f"owner route k={count}")
+        # the overlapped forms through RCCL: 5 consecutive distinct batches each
+        batches = [np.ascontiguousarray(S.random_targets(6000, seed=300 + j), np.uint8) for j in range(5)]
+        dbs = [torch.from_numpy(b).to(dev) for b in batches]
+        for count in (8, 14):
+            wants = [O.flat_rt_closest(ids, st, first, off, b, count, nthreads=8) for b in batches]
+            pipe = OwnerPipeline(6000, count, 1, 0, dev, cap=8, collective=True)
+            outs, pipe = serve_pipelined(T, dbs, count, pipe=pipe)
+            torch.cuda.synchronize()
+            assert pipe.cap > 8 and pipe.collective
+            for j, (want, wcnt) in enumerate(wants):
+                np.testing.assert_array_equal(outs[j][1].cpu().numpy(), wcnt, err_msg=f"owner pipe k={count} b{j}")
+                np.testing.assert_array_equal(outs[j][0].cpu().numpy().view(np.uint32), want,
+                                              err_msg=f"owner pipe k={count} b{j}")
+            like = Exchange(6000, count, 1, dev, row_cap=1 << 20, part_cap=4096, collective=True)
+            exs = G.pipeline(6000, count, 1, like=like)
+            outs = [(torch.empty((6000, count), dtype=torch.int32, device=dev),
+                     torch.empty((6000,), dtype=torch.uint8, device=dev)) for _ in dbs]
+            G.run_pipelined(dbs, exs, outs, rank=0)
+            torch.cuda.synchronize()
+            assert not any(e.overflowed() for e in exs)
+            for j, (want, wcnt) in enumerate(wants):
+                np.testing.assert_array_equal(outs[j][1].cpu().numpy(), wcnt, err_msg=f"ns pipe k={count} b{j}")
+                np.testing.assert_array_equal(outs[j][0].cpu().numpy().view(np.uint32), want,
+                                              err_msg=f"ns pipe k={count} b{j}")
         T.close()
     finally:
         G.close()

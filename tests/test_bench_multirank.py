@@ -35,3 +35,12 @@ def test_bench_two_ranks_on_one_gpu():
     assert "error" not in ow, ow
     assert ow["n_gpus"] == 2 and ow["queries_per_s"] > 0 and not ow["overflow"]
     assert ow["verified"]["rows"] > 0 and ow["verified"]["mismatches"] == 0
+    # every rank's returned rows are checked by their owners, the ones answered by the other rank included
+    assert ow["verified"]["rows"] == 2 * (1 << 16) and ow["verified"]["rows_answered_by_another_rank"] > 0
+    assert ow["collective"] == "all_to_all_single (gloo)"  # the rehearsal: RCCL needs a GPU per rank
+    pw = ow["pipelined"]  # the overlapped OwnerPipeline, same batches
+    assert "error" not in pw and not pw["overflow"], pw
+    assert pw["verified"]["rows"] == 2 * (1 << 16) and pw["verified"]["mismatches"] == 0
+    ap = ag["pipelined"]  # the north-star step pipelined
+    assert "error" not in ap and not ap["overflow"], ap
+    assert ap["verified"]["rows"] > 0 and ap["verified"]["mismatches"] == 0

@@ -347,6 +347,26 @@ def _query_worker(rank, world, port, q):
                     torch.cuda.synchronize()
                     bad2 = int((idx2.cpu().numpy().view(np.uint32) != want[lo:lo + m]).any(1).sum())
                     why += f"; with room from the start: {bad2} rows differ, steps {G.tries}"
+        # the pipelined step (GlobalShard.run_pipelined: three buffer sets, the all_to_all of batch i+1 on a comm
+        # stream under batch i's finish) over 5 consecutive distinct batches, every home row against the oracle
+        from opendht_amd.global_shard import Exchange, home_range
+        batches = [_targets(spec, 2000, seed=50 + j)[:2000] for j in range(5)]
+        nq = batches[0].shape[0]
+        hlo, hhi = home_range(nq, world, rank)
+        for count in (8, 14):
+            like = Exchange(nq, count, world, dev, row_cap=1 << 20, part_cap=4096, collective=True)
+            exs = G.pipeline(nq, count, world, like=like)
+            outs = [(torch.empty((hhi - hlo, count), dtype=torch.int32, device=dev),
+                     torch.empty((hhi - hlo,), dtype=torch.uint8, device=dev)) for _ in batches]
+            G.run_pipelined([torch.from_numpy(b).to(dev) for b in batches], exs, outs, rank=rank)
+            torch.cuda.synchronize()
+            if any(e.overflowed() for e in exs) and ok:
+                ok, why = False, f"rank {rank} pipelined count {count}: overflow"
+            for j, b in enumerate(batches):
+                want, wcnt = O.flat_rt_closest(gids, gst, gfirst, goff, b, count)
+                if ok and not (np.array_equal(outs[j][0].cpu().numpy().view(np.uint32), want[hlo:hhi]) and
+                               np.array_equal(outs[j][1].cpu().numpy(), wcnt[hlo:hhi])):
+                    ok, why = False, f"rank {rank} pipelined count {count} batch {j}: rows differ"
         G.close()
         if ok:
             why = ""

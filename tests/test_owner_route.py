@@ -156,6 +156,49 @@ def test_owner_route_fused_packed_rows(gpu, good_pct):
         T.close()
 
 
+@pytest.mark.parametrize("good_pct", [60, 2], ids=["u60", "mostly_bad"])
+def test_owner_pipeline_one_rank(gpu, good_pct):
+    """sharded.OwnerPipeline without a collective (one rank): 6 consecutive distinct batches through three buffer
+    sets on two streams, blocks of one record first (the folded overflow word makes every batch run again grown);
+    on the 2 %-good table rows escape packing and the batches run again unpacked. Every row against the oracle."""
+    from opendht_amd.sharded import OwnerPipeline, serve_pipelined
+
+    spec = ShardSpec(n_shards=1, depth=10, mean_per_bucket=6.0, seed=0x91 + good_pct, good_pct=good_pct,
+                     expired_pct=(100 - good_pct) // 2)
+    gids, gst, goff = spec.bucket_range(0, spec.n_buckets)
+    gfirst = S.bucket_firsts(spec.depth, 0, spec.n_buckets)
+    sh = build_shard(spec, 0)
+    T = DeviceTable(sh.ids, sh.status, sh.first, sh.off, device=0, index_base=sh.index_base, sorted=True)
+    try:
+        batches = [_batch(spec, 2500, seed=200 + j)[:2500] for j in range(6)]
+        for count in (8, 14, 32):
+            pipe = OwnerPipeline(2500, count, 1, 0, gpu, cap=8)
+            outs, pipe = serve_pipelined(T, [torch.from_numpy(b).to(gpu) for b in batches], count, pipe=pipe)
+            torch.cuda.synchronize()
+            assert pipe.cap > 8
+            for j, b in enumerate(batches):
+                want, wcnt = O.flat_rt_closest(gids, gst, gfirst, goff, b, count, nthreads=8)
+                np.testing.assert_array_equal(outs[j][1].cpu().numpy(), wcnt, err_msg=f"k={count} batch {j} counts")
+                np.testing.assert_array_equal(outs[j][0].cpu().numpy().view(np.uint32), want,
+                                              err_msg=f"k={count} batch {j}")
+    finally:
+        T.close()
+
+
+def test_padding_records_pack(gpu):
+    """The send blocks start filled with a padding target of each block's owner: an owner answering
+    whole blocks never meets uninitialised records, so the rows of the padding pack (no escape)."""
+    from opendht_amd.sharded import pad_blocks
+
+    R = OwnerRoute(3000, 8, 4, 2, gpu)
+    v = R.send.view(4, R.cap, 20).cpu().numpy()
+    for d in range(4):
+        assert (v[d, :, 0] == ((d << 6) | 0x20)).all() and not v[d, :, 1:].any()
+    t = torch.empty((2, 8, 20), dtype=torch.uint8, device=gpu)
+    pad_blocks(t.view(16, 20), 2, 8, 8)
+    assert t[1, :, 0].eq(1).all() and t[1, :, 1].eq(0x80).all()
+
+
 def _free_port():
     with socket.socket() as so:
         so.bind(("127.0.0.1", 0))
@@ -171,7 +214,7 @@ def _serve_worker(rank, world, port, q):
     import oracle as O
     from opendht_amd import DeviceTable
     from opendht_amd import synth as S
-    from opendht_amd.sharded import OwnerRoute, ShardSpec, build_shard, serve_owner
+    from opendht_amd.sharded import OwnerPipeline, OwnerRoute, ShardSpec, build_shard, serve_owner, serve_pipelined
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -195,6 +238,20 @@ def _serve_worker(rank, world, port, q):
                 want, wcnt = O.flat_rt_closest(gids, gst, gfirst, goff, targets, count)
                 if not (np.array_equal(oi.cpu().numpy().view(np.uint32), want) and np.array_equal(oc.cpu().numpy(), wcnt)):
                     ok, why = False, f"rank {rank} k={count} cap={cap} packed={packed}"
+        # the overlapped pipeline (sharded.OwnerPipeline: gloo all_to_alls on the comm stream), 5 consecutive
+        # distinct batches, blocks of one record first (overflow combined over the ranks, grown, all run again)
+        batches = [_batch(spec, 1200, seed=100 + 7 * rank + j)[:1200] for j in range(5)]
+        for count in (8, 14):
+            pipe = OwnerPipeline(1200, count, world, spec.shard_bits, dev, cap=8)
+            outs, pipe = serve_pipelined(T, [torch.from_numpy(b).to(dev) for b in batches], count, pipe=pipe)
+            torch.cuda.synchronize()
+            if pipe.cap <= 8:
+                ok, why = False, f"rank {rank} pipelined k={count}: did not grow"
+            for j, b in enumerate(batches):
+                want, wcnt = O.flat_rt_closest(gids, gst, gfirst, goff, b, count)
+                if not (np.array_equal(outs[j][0].cpu().numpy().view(np.uint32), want) and
+                        np.array_equal(outs[j][1].cpu().numpy(), wcnt)):
+                    ok, why = False, f"rank {rank} pipelined k={count} batch {j}"
         T.close()
     except Exception as e:  # reported through the queue
         ok, why = False, f"{type(e).__name__}: {e}"
