@@ -588,7 +588,7 @@ def routed_targets(Q, world, rank, dev, NB, seed=0x0D470600):
 
 
 def owner_routed_pass(T, sh, spec, Q, cnt_k, K, W, dev, dist, world, rank, NB=4, group=None, collective=None,
-                      pipelined=None):
+                      pipelined=None, comm=None):
     """The headline form as a serving front end, measured at this N: every rank holds Q arbitrary
     targets per step (uniform over the N shards), routes each to its owner and gets the rows back
     (sharded.OwnerRoute.step: kad_route_pack, all_to_all_single of the target blocks on `group` — RCCL over xGMI at
@@ -596,8 +596,9 @@ def owner_routed_pass(T, sh, spec, Q, cnt_k, K, W, dev, dist, world, rank, NB=4,
     rows back, kad_route_unpack_packed). W + K eager steps (collectives are not captured), barrier + synchronize on
     both sides, the max over ranks; a distinct batch per step (NB rotated); each step's overflow and escape words
     folded on the device and read once after. `pipelined`: the same K batches through sharded.OwnerPipeline (batch
-    i's exchanges on a comm stream under batch i+1's pack and batch i's answer). At N = 1 without `collective` there
-    is no exchange (the local pack / query / unpack)."""
+    i's exchanges on a comm stream under batch i+1's pack and batch i's answer). `comm` (an opendht_amd.comm.Comm):
+    the same batches through the native executor too (native_pass). At N = 1 without `collective` there is no
+    exchange (the local pack / query / unpack)."""
     import torch
 
     from opendht_amd.sharded import OwnerRoute
@@ -615,7 +616,7 @@ def owner_routed_pass(T, sh, spec, Q, cnt_k, K, W, dev, dist, world, rank, NB=4,
         R = OwnerRoute(Q, cnt_k, world, spec.shard_bits, dev, collective=coll)
         outs = [(torch.empty((Q, cnt_k), dtype=torch.int32, device=dev), torch.empty((Q,), dtype=torch.uint8, device=dev))
                 for _ in range(NB)]
-        acc = torch.zeros((2,), dtype=torch.int32, device=dev)
+        acc = torch.zeros((3,), dtype=torch.int32, device=dev)
         for _ in range(6):  # block capacities: grow until a step fits (decided together over the ranks)
             R.step(T, tgs[0], *outs[0], group, s)
             if not R.overflowed(group):
@@ -629,11 +630,10 @@ def owner_routed_pass(T, sh, spec, Q, cnt_k, K, W, dev, dist, world, rank, NB=4,
         t_max, ev_ms, how = graph_steps(step, K, W, dev, dist, use_graph=False)
         from opendht_amd.sharded import combine_max
 
-        over, esc = (bool(x) for x in combine_max(acc, group, coll))
+        over, esc, tail = (bool(x) for x in combine_max(acc, group, coll))
         last = (K - 1) % NB
-        if esc:  # (a row too wide to pack in some step: the last batch's way back again, unpacked)
-            R.answer(T, s, packed=False)
-            R.back(*outs[last], group, s, packed=False)
+        if tail or esc:  # (some step needed full targets or unpacked rows: the last batch again, that way)
+            R.step(T, tgs[last], *outs[last], group, s, packed=not esc, keys=False)
             torch.cuda.synchronize(dev)
         verified = verify_routed(dist, sh, spec, rank, world, tgs[last], *outs[last], cnt_k)
         xb = R.xgmi_bytes
@@ -641,12 +641,20 @@ def owner_routed_pass(T, sh, spec, Q, cnt_k, K, W, dev, dist, world, rank, NB=4,
         res = {"queries_per_s": world * Q * K / t_max, "ms_per_step": t_max / K * 1e3, "n_gpus": world,
                "collective": (f"all_to_all_single ({'RCCL' if backend == 'nccl' else backend})" if coll else None),
                "cap": R.cap, "overflow": over,
+               "targets_out": f"{R.record_bytes} bytes per query" + (" (key-only: the top 64 bits)" if R.keys else ""),
                "rows_back": f"packed, {4 * R.pw} bytes per row" if R.packed else "plain", "escaped": esc,
+               "tailed": tail,
                "xgmi_bytes_per_rank_step": xb, "launch": how, "verified": verified,
                "how": owner_routed_pass.__doc__.split("\n\n")[0].replace("\n", " ")}
         if pipelined:
             res["pipelined"] = pipelined_pass(T, sh, spec, tgs, outs, Q, cnt_k, K, W, dev, dist, world, rank, R.cap,
                                               group, coll)
+        if comm is not None:
+            try:
+                res["native"] = native_pass(T, sh, spec, tgs, outs, Q, cnt_k, K, W, dev, dist, world, rank, R.cap,
+                                            comm, group)
+            except Exception as e:
+                res["native"] = {"error": f"{type(e).__name__}: {e}"}
         return res
     except Exception as e:  # the headline line is printed whatever happens here
         return {"error": f"{type(e).__name__}: {e}"}
@@ -709,7 +717,7 @@ def pipelined_pass(T, sh, spec, tgs, outs, Q, cnt_k, K, W, dev, dist, world, ran
     P = OwnerPipeline(Q, cnt_k, world, spec.shard_bits, dev, cap=cap, collective=coll)
     for _ in range(6):
         P.run(T, tgs[:2], outs[:2], group)
-        over, esc = P.flags(group)
+        over, esc, tail = P.flags(group)
         if not over:
             break
         P = P.grown(group)
@@ -720,21 +728,62 @@ def pipelined_pass(T, sh, spec, tgs, outs, Q, cnt_k, K, W, dev, dist, world, ran
     # gpurun_out/r06b; the native executor, kad_comm, issues the pipeline from C++ instead)
     tm = issue_timed(lambda: P.run(T, [tgs[j % NB] for j in range(K)], [outs[j % NB] for j in range(K)], group), K,
                      dev, dist, graph_ok=not coll)
-    over, esc = P.flags(group)
+    over, esc, tail = P.flags(group)
     last = (K - 1) % NB
-    if esc:
-        P.run(T, [tgs[last]], [outs[last]], group, packed=False)
+    if tail or esc:
+        P.run(T, [tgs[last]], [outs[last]], group, packed=not esc, keys=False)
         torch.cuda.synchronize(dev)
         P.flags(group)
     best = "graph" if "graph" in tm else "eager"
     t_max = tm[best][0]
     res = {"queries_per_s": world * Q * K / t_max, "ms_per_step": t_max / K * 1e3, "launch": best,
            "eager_ms_per_step": tm["eager"][0] / K * 1e3, "eager_host_issue_ms_per_step": tm["eager"][1] / K * 1e3,
-           "cap": P.cap, "overflow": over, "escaped": esc,
+           "cap": P.cap, "overflow": over, "escaped": esc, "tailed": tail,
            "verified": verify_routed(dist, sh, spec, rank, world, tgs[last], *outs[last], cnt_k),
            "how": OwnerPipeline.__doc__.split("\n\n")[0].replace("\n", " ")}
     if "graph_error" in tm:
         res["graph_error"] = tm["graph_error"]
+    return res
+
+
+def native_pass(T, sh, spec, tgs, outs, Q, cnt_k, K, W, dev, dist, world, rank, cap, comm, group):
+    """owner_routed_pass's K batches through the native executor (opendht_amd.comm.NativeRoute, kad_route_run over the
+    engine's own RCCL communicator, one C call per run of batches): `serial` (one buffer set, each batch in order on
+    one stream) and `pipelined` (three sets: batch i+1's pack and batch i's query on the compute stream while batch i's
+    targets and batch i-1's rows are on the links). Barrier + synchronize on both sides, max over ranks; the host's
+    issue time beside; the last batch's rows checked by their owners."""
+    import torch
+
+    from opendht_amd.comm import NativeRoute
+
+    NB = len(tgs)
+    res = {}
+    for name, n_sets in (("serial", 1), ("pipelined", 3)):
+        R = NativeRoute(Q, cnt_k, world, spec.shard_bits, dev, cap=cap, n_sets=n_sets, comm=comm)
+        for _ in range(6):
+            R.run(T, tgs[:2], outs[:2])
+            over, esc, tail = R.flags(group)
+            if not over:
+                break
+            R = R.grown(group)
+        R.run(T, [tgs[j % NB] for j in range(W)], [outs[j % NB] for j in range(W)])
+        torch.cuda.synchronize(dev)
+        R.flags(group)
+        tm = issue_timed(lambda: R.run(T, [tgs[j % NB] for j in range(K)], [outs[j % NB] for j in range(K)]), K, dev,
+                         dist, graph_ok=False)
+        over, esc, tail = R.flags(group)
+        last = (K - 1) % NB
+        if tail or esc:
+            R.run(T, [tgs[last]], [outs[last]], packed=not esc, keys=False)
+            torch.cuda.synchronize(dev)
+            R.flags(group)
+        t_max, host = tm["eager"]
+        res[name] = {"queries_per_s": world * Q * K / t_max, "ms_per_step": t_max / K * 1e3,
+                     "host_issue_ms_per_step": host / K * 1e3, "cap": R.cap, "overflow": over, "escaped": esc,
+                     "tailed": tail, "targets_bytes_per_query": 8 if R.keys else 20,
+                     "verified": verify_routed(dist, sh, spec, rank, world, tgs[last], *outs[last], cnt_k)}
+        del R
+    res["how"] = native_pass.__doc__.split("\n\n")[0].replace("\n", " ")
     return res
 
 
@@ -748,7 +797,9 @@ def owner_step_model(T, Q, cnt_k, dev, stream, avg_kernel_s, link_gbs=64.0, lat_
     counts: two). serial = pack + targets + query + rows + unpack; overlapped = the compute and the exchanges of
     consecutive batches on two streams, max(pack + query + unpack, exchanges). `packed`: the same with the rows
     back packed (written packed by the query kernel at count 8 — kad_rt_closest_batch_packed —, by kad_route_compress
-    otherwise; one collective of KAD_ROUTE_PACKED_WORDS(k) words per row; kad_route_unpack_packed)."""
+    otherwise; one collective of KAD_ROUTE_PACKED_WORDS(k) words per row; kad_route_unpack_packed). `keys` (count 8,
+    the default route): the targets out as 8-byte keys (kad_route_pack_keys, kad_rt_closest_keys_packed), the rows
+    back packed: 20 bytes per query on the links instead of 32."""
     import torch
 
     from opendht_amd.sharded import OwnerRoute
@@ -774,7 +825,7 @@ def owner_step_model(T, Q, cnt_k, dev, stream, avg_kernel_s, link_gbs=64.0, lat_
         t = torch.randint(0, 256, (Q, 20), dtype=torch.uint8, device=dev, generator=g)
         sh = torch.randint(0, n, (Q,), dtype=torch.uint8, device=dev, generator=g)
         t[:, 0] = (t[:, 0] & 0x1F) | (sh << 5)  # targets spread over the N held shards of the 8-shard table
-        R = OwnerRoute(Q, cnt_k, n, 3, dev, collective=False)
+        R = OwnerRoute(Q, cnt_k, n, 3, dev, collective=False, keys=False)
         pack_us = timed(lambda: R.pack(t, s))
         over = R.overflowed(combine=False)
         recv = torch.randint(0, 256, (n * R.cap, 20), dtype=torch.uint8, device=dev, generator=g)
@@ -813,6 +864,24 @@ def owner_step_model(T, Q, cnt_k, dev, stream, avg_kernel_s, link_gbs=64.0, lat_
                            "step_overlapped_us": overlap_p,
                            "aggregate_queries_per_s_serial": n * Q / (serial_p * 1e-6),
                            "aggregate_queries_per_s_overlapped": n * Q / (overlap_p * 1e-6)}
+            if cnt_k == 8:  # key-only targets (8 bytes out) + packed rows (12 back): kad_route_pack_keys,
+                # kad_rt_closest_keys_packed, kad_route_unpack_packed
+                RK = OwnerRoute(Q, cnt_k, n, 3, dev, collective=False, keys=True)
+                pack_k_us = timed(lambda: RK.pack(t, s))
+                RK.recv_keys = recv[:, :8].flip(1).contiguous().view(torch.int64).view(-1)  # big-endian top 64 bits
+                query_k_us = timed(lambda: RK.answer(T, s))
+                tail = RK.tailed(combine=False)
+                x_k = lat_us + 8 * RK.cap / (link_gbs * 1e3)
+                serial_k = pack_k_us + x_k + query_k_us + x_p + unpack_p_us
+                overlap_k = max(pack_k_us + query_k_us + unpack_p_us, x_k + x_p)
+                e["keys"] = {"target_bytes": 8, "row_bytes": 4 * R.pw, "tailed": tail, "pack_us": pack_k_us,
+                             "query_us": query_k_us, "unpack_us": unpack_p_us,
+                             "xgmi_targets_bytes": 8 * (n - 1) * RK.cap, "xgmi_rows_bytes": 4 * R.pw * (n - 1) * RK.cap,
+                             "exchange_targets_modelled_us": x_k, "exchange_rows_modelled_us": x_p,
+                             "step_serial_us": serial_k, "step_overlapped_us": overlap_k,
+                             "aggregate_queries_per_s_serial": n * Q / (serial_k * 1e-6),
+                             "aggregate_queries_per_s_overlapped": n * Q / (overlap_k * 1e-6)}
+                del RK
         out[str(n)] = e
         del R, t, recv, oi, oc
     out["how"] = ("rank 0 of N on this GPU (its 1/8 shard of the 100M-node table): the pack, the query over the "
@@ -1461,6 +1530,15 @@ def allgather_pass(args, world, rank, local, dev, dist):
             pipe, pi, pc = north_star_pipelined(G, ex, tgs, Q, cnt_k, K, NB, dev, dist, world, rank)
         except Exception as e:
             pipe, pi = {"error": f"{type(e).__name__}: {e}"}, None
+        nat, nrows = None, {}
+        if dist.get_backend() == "nccl":  # the native executor (its own communicator; the id over this group)
+            try:
+                from opendht_amd.comm import Comm
+
+                with Comm(local, world, rank) as comm:
+                    nat, nrows = north_star_native(G, ex, tgs, Q, cnt_k, K, NB, dev, dist, world, rank, comm)
+            except Exception as e:
+                nat = {"error": f"{type(e).__name__}: {e}"}
         # verification: this rank's home rows (queries [lo, hi)) among the first vrows whose targets this rank
         # owns, against the restatement on this rank's shard WITH its exact halo (every owned window lies inside)
         G.close()
@@ -1477,6 +1555,13 @@ def allgather_pass(args, world, rank, local, dev, dist):
             pipe["verified"] = {"rows": sum_over_ranks(dist, int(own.sum()), dev),
                                 "mismatches": sum_over_ranks(dist, pbad, dev)}
         res["pipelined"] = pipe
+        for m, (ni, nc) in nrows.items():
+            nb = verify_rows(sh.ids, sh.status, sh.first, sh.off, sh.index_base, vt[own],
+                             ni[:vt.shape[0]].cpu().numpy()[own], nc[:vt.shape[0]].cpu().numpy()[own], cnt_k)
+            nat[m]["verified"] = {"rows": sum_over_ranks(dist, int(own.sum()), dev),
+                                  "mismatches": sum_over_ranks(dist, nb, dev)}
+        if nat is not None:
+            res["native"] = nat
         res.update({"value": Q * K / t_max, "ms_per_step": t_max / K * 1e3, "avg_step_ms_events": kern_ms,
                     "launch": how,
                     "workload": f"100M-node U(24) table, 1/{world} per GPU without halo ({n_local} nodes on rank 0), "
@@ -1522,6 +1607,34 @@ def north_star_pipelined(G, ex, tgs, Q, cnt_k, K, NB, dev, dist, world, rank):
     if "graph_error" in tm:
         res["graph_error"] = tm["graph_error"]
     return res, oi, oc
+
+
+def north_star_native(G, ex, tgs, Q, cnt_k, K, NB, dev, dist, world, rank, comm):
+    """The north-star step over K batches through the native executor (opendht_amd.comm.shard_run: kad_shard_run over
+    the engine's own RCCL communicator, one C call per run): one exchange set (serial) and three (pipelined), with ex's
+    grown capacities. Returns ({mode: object}, {mode: this rank's home rows of the last batch})."""
+    import torch
+
+    from opendht_amd.comm import shard_run
+    from opendht_amd.global_shard import home_range
+
+    lo, hi = home_range(Q, world, rank)
+    res, rows = {}, {}
+    for name, n in (("serial", 1), ("pipelined", 3)):
+        exs = G.pipeline(Q, cnt_k, world, like=ex)[:n]
+        outs = [(torch.empty((hi - lo, cnt_k), dtype=torch.int32, device=dev),
+                 torch.empty((hi - lo,), dtype=torch.uint8, device=dev)) for _ in range(NB)]
+        shard_run(G, comm, [tgs[j % NB] for j in range(3)], exs, [outs[j % NB] for j in range(3)])
+        torch.cuda.synchronize(dev)
+        over0 = exs[0].overflowed()
+        tm = issue_timed(lambda: shard_run(G, comm, [tgs[j % NB] for j in range(K)], exs,
+                                           [outs[j % NB] for j in range(K)]), K, dev, dist, graph_ok=False)
+        t_max, host = tm["eager"]
+        res[name] = {"value": Q * K / t_max, "ms_per_step": t_max / K * 1e3, "host_issue_ms_per_step": host / K * 1e3,
+                     "overflow": over0 or exs[0].overflowed()}
+        rows[name] = outs[(K - 1) % NB]
+    res["how"] = north_star_native.__doc__.split("\n\n")[0].replace("\n", " ")
+    return res, rows
 
 
 def home0_recv(G0, ex, tg, Q, dev):
@@ -1724,11 +1837,18 @@ def main_owner_child(args):
         spec = config3_spec()
         sh = build_shard(spec, rank)
         T = DeviceTable(sh.ids, sh.status, sh.first, sh.off, device=local, index_base=sh.index_base, sorted=True)
+        comm = None
+        if be == "nccl":
+            from opendht_amd.comm import Comm
+
+            comm = Comm(local, world, rank)  # the native executor's communicator (id over the gloo default group)
         try:
             res = owner_routed_pass(T, sh, spec, args.queries, args.count, args.steps, args.warmup, dev, dist, world,
-                                    rank, group=group)
+                                    rank, group=group, comm=comm)
         finally:
             T.close()
+            if comm is not None:
+                comm.close()
     except Exception as e:
         res = {"error": f"rank {rank}: {type(e).__name__}: {e}"}
     with open(args.ag_out, "w") as f:
@@ -1845,6 +1965,18 @@ def rccl1_pass(args) -> dict:
                     res["pipelined"] = pipe
                 except Exception as e:
                     res["pipelined"] = {"error": f"{type(e).__name__}: {e}"}
+                try:
+                    from opendht_amd.comm import Comm
+
+                    with Comm(0, 1, 0) as comm:
+                        nat, nrows = north_star_native(G, ex, tgs, Q, cnt_k, K, NB, dev, dist, 1, 0, comm)
+                        for m, (ni, nc) in nrows.items():
+                            nat[m]["verified"] = {"rows": vrows, "mismatches": verify_rows(
+                                ids, st, first, off, 0, tgs[(K - 1) % NB][:vrows].cpu().numpy(),
+                                ni[:vrows].cpu().numpy(), nc[:vrows].cpu().numpy(), cnt_k)}
+                    res["native"] = nat
+                except Exception as e:
+                    res["native"] = {"error": f"{type(e).__name__}: {e}"}
         G.close()
         del ids, st
         # owner routing through the one-rank RCCL group: config 3's rank-0 shard with its halo,
@@ -1855,11 +1987,15 @@ def rccl1_pass(args) -> dict:
 
         sh = build_shard(spec, 0)
         T = DeviceTable(sh.ids, sh.status, sh.first, sh.off, device=0, index_base=sh.index_base, sorted=True)
+        from opendht_amd.comm import Comm
+
+        comm = Comm(0, 1, 0)
         try:
             res["owner_routed"] = owner_routed_pass(T, sh, spec, Q, cnt_k, K, 2, dev, dist, 1, 0, group=None,
-                                                    collective=True, pipelined=True)
+                                                    collective=True, pipelined=True, comm=comm)
         finally:
             T.close()
+            comm.close()
         res["how"] = ("Exchange(world=1, collective=True): the all_to_all_single of the one send block runs through "
                       "RCCL (a device copy at world 1); the difference to step_us_no_collective is its cost")
         return res

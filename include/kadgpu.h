@@ -464,6 +464,11 @@ int kad_rt_home_finish_reset(const uint32_t* recv, uint32_t* send, uint32_t worl
 #define KAD_ROUTE_OVERFLOW_WORD(world) ((world) * KAD_ROUTE_SUBS * KAD_ROUTE_CSTRIDE)
 int kad_route_pack(const uint8_t* targets, uint32_t q, uint32_t world, uint32_t shard_bits, uint32_t cap,
                    uint8_t* send, uint32_t* slot, uint32_t* ctr, int device, void* stream);
+/* kad_route_pack_keys: kad_route_pack with each record the target's top 64 bits as one native uint64 key (send_keys:
+ * world * cap keys, 8-byte aligned) instead of its 20 bytes: owner routing's key-only exchange, 8 bytes per query on
+ * the links instead of 20 (answered by kad_rt_closest_keys_packed). */
+int kad_route_pack_keys(const uint8_t* targets, uint32_t q, uint32_t world, uint32_t shard_bits, uint32_t cap,
+                        uint64_t* send_keys, uint32_t* slot, uint32_t* ctr, int device, void* stream);
 int kad_route_unpack(const uint32_t* slot, uint32_t q, uint32_t count, const uint32_t* back_idx,
                      const uint8_t* back_cnt, uint32_t* out_idx, uint8_t* out_cnt, int device, void* stream);
 /* Packed rows for the way back (count <= KAD_ROUTE_PACKED_MAX_COUNT): a row's indices lie in one window of the
@@ -488,6 +493,80 @@ int kad_route_unpack_packed(const uint32_t* slot, uint32_t q, uint32_t count, co
  * answers the batch again unpacked. Async on stream. */
 int kad_rt_closest_batch_packed(const kad_table* t, const uint8_t* targets, uint32_t q, uint32_t count,
                                 uint32_t* packed, uint32_t* escape, void* stream);
+/* kad_rt_closest_keys_packed: kad_rt_closest_batch_packed from 8-byte keys (the targets' top 64 bits, native uint64:
+ * kad_route_pack_keys' records), which is all the short and 128-byte window lines read. The exact path (the few queries
+ * no line answers) runs with the targets' low 96 bits taken as zero: the same rows as from the full targets unless two
+ * nodes of its window share their top 64 bits (XOR order then depends on the low bits, infohash.h:131-146), which sets
+ * the sticky word *tail (not cleared; ctr[KAD_ROUTE_OVERFLOW_WORD(world) + 2] is meant for it): the caller answers
+ * that batch again from full targets. keys 8-byte aligned. Count 8 on tables with short window lines only. */
+int kad_rt_closest_keys_packed(const kad_table* t, const uint64_t* keys, uint32_t q, uint32_t count, uint32_t* packed,
+                               uint32_t* escape, uint32_t* tail, void* stream);
+/* kad_route_fold_flags: flags[0..2] |= ctr[KAD_ROUTE_OVERFLOW_WORD(world) + 0..2] — overflow, packing escape, key-only
+ * tail — (device words; kad_route_pack zeroes them, so a caller running many batches folds them after each). Async on
+ * stream. */
+int kad_route_fold_flags(const uint32_t* ctr, uint32_t world, uint32_t* flags, int device, void* stream);
+
+/* ---- native multi-GPU executor (csrc/kad_comm.hip) ----
+ * The two multi-GPU steps issued from C++ over an RCCL communicator of the engine's own (RCCL is loaded at run time:
+ * the librccl.so.1 already in the process, else /opt/rocm/lib's; KAD_ERR_UNSUPPORTED without one).
+ * kad_comm_unique_id: a new communicator id (KAD_COMM_ID_BYTES bytes) on rank 0; the caller hands it to every rank.
+ * kad_comm_create: this rank's communicator on `device` (collective: every rank calls it at once), plus a compute
+ *   and a comm stream of its own for the pipelined forms. kad_comm_all_to_all: ncclAllToAll of bytes_per_rank bytes
+ *   per rank on stream.
+ * kad_route_run: owner routing (sharded.OwnerRoute; reference callers dht.cpp:3189-3217) over n_batches batches of
+ *   q targets: kad_route_pack into `world` blocks of `cap` records, all_to_all of the blocks, the owner's query of
+ *   every received record (packed != 0: the rows go back packed — count 8 on tables with short window lines through
+ *   kad_rt_closest_batch_packed, else kad_rt_closest_batch + kad_route_compress —; packed = 0: rows and counts), the
+ *   all_to_all back, the unpack of batch i into out_idx[i] / out_cnt[i], and kad_route_fold_flags into flags (3 device
+ *   words: [0] a block overflowed — grow cap and run again —, [1] a row escaped packing — run again unpacked —, [2] a
+ *   key-only query needed the target's low bits — run again with KAD_ROUTE_KEYS off). `packed` is a mask:
+ *   KAD_ROUTE_PACKED (rows back packed), KAD_ROUTE_KEYS (with it, count 8 on tables with short window lines: the
+ *   targets travel as 8-byte keys, kad_route_pack_keys + kad_rt_closest_keys_packed; send / recv then hold world *
+ *   cap keys; a table without short lines sets flags[2]).
+ *   n_sets = 1: every batch in order on `stream` (comm may be NULL at world 1: no collective, recv == send and
+ *   back_* == the answer buffers allowed). n_sets >= 3 (comm required): pipelined on the communicator's streams —
+ *   batch i+1's pack and batch i's query on the compute stream while batch i's targets and batch i-1's rows are on the
+ *   links —, forked from and joined back to `stream`. Pointers in `targets`, `out_idx`, `out_cnt` (host arrays of
+ *   n_batches device pointers) and in the sets are device pointers; a set's buffers: send / recv world * cap * 20
+ *   bytes, slot q words, ctr KAD_ROUTE_CTR_WORDS(world) words, rows / back_rows world * cap * count words and cnt /
+ *   back_cnt world * cap bytes (packed = 0), prow / back_prow world * cap * KAD_ROUTE_PACKED_WORDS(count) words.
+ * kad_shard_run: the north-star step (global_shard.GlobalShard.step) over n_batches replicated batches:
+ *   kad_rt_shard_step_home into the `world` home blocks of send[k], all_to_all into recv[k],
+ *   kad_rt_home_finish_reset into out_idx[i] / out_cnt[i] (this rank's home range), set k = i % n_sets; the send
+ *   counters must start zero (each finish zeroes its set's). n_sets = 1 serial on `stream`, >= 3 pipelined (batch
+ *   i+1's all_to_all under batch i's finish and batch i+2's shard kernel). overflow: the sticky word of
+ *   kad_rt_home_finish. */
+#define KAD_COMM_ID_BYTES 128u
+#define KAD_ROUTE_PACKED 1u
+#define KAD_ROUTE_KEYS 2u
+typedef struct kad_comm kad_comm;
+typedef struct kad_route_set {
+    uint8_t* send;
+    uint8_t* recv;
+    uint32_t* slot;
+    uint32_t* ctr;
+    uint32_t* rows;
+    uint8_t* cnt;
+    uint32_t* back_rows;
+    uint8_t* back_cnt;
+    uint32_t* prow;
+    uint32_t* back_prow;
+} kad_route_set;
+int kad_comm_unique_id(uint8_t* out_id);
+int kad_comm_create(kad_comm** out, int device, uint32_t world, uint32_t rank, const uint8_t* id);
+int kad_comm_destroy(kad_comm* comm);
+int kad_comm_info(const kad_comm* comm, uint32_t* world, uint32_t* rank, int* device);
+int kad_comm_all_to_all(kad_comm* comm, const void* send, void* recv, uint64_t bytes_per_rank, void* stream);
+int kad_route_run(kad_comm* comm, const kad_table* t, uint32_t n_batches, const uint8_t* const* targets, uint32_t q,
+                  uint32_t count, uint32_t world, uint32_t shard_bits, uint32_t cap, uint32_t packed, uint32_t n_sets,
+                  const kad_route_set* sets, uint32_t* const* out_idx, uint8_t* const* out_cnt, uint32_t* flags,
+                  void* stream);
+int kad_shard_run(kad_comm* comm, const kad_table* shard, const uint32_t* global_good_prefix, uint32_t global_buckets,
+                  uint64_t global_base_hi, uint32_t depth, uint32_t shard_first_bucket, uint32_t reach_lo,
+                  uint32_t reach_hi, uint32_t n_batches, const uint8_t* const* targets, uint32_t q, uint32_t count,
+                  uint32_t row_cap, uint32_t part_cap, uint32_t n_sets, uint32_t* const* send, uint32_t* const* recv,
+                  uint32_t* const* scratch, uint32_t* overflow, uint32_t* const* out_idx, uint8_t* const* out_cnt,
+                  void* stream);
 
 /* ---- wire step after the query ------------------------ */
 #define KAD_SEND_NODES 8u           /* reference network_engine.cpp:59 SEND_NODES */

@@ -147,6 +147,19 @@ SIGNATURES = {
     "kad_route_compress": (C.c_int, [_P, _P, C.c_uint32, C.c_uint32, _P, _P, C.c_int, _P]),
     "kad_rt_closest_batch_packed": (C.c_int, [_P, _P, C.c_uint32, C.c_uint32, _P, _P, _P]),
     "kad_route_unpack_packed": (C.c_int, [_P, C.c_uint32, C.c_uint32, _P, _P, _P, C.c_int, _P]),
+    "kad_route_fold_flags": (C.c_int, [_P, C.c_uint32, _P, C.c_int, _P]),
+    "kad_route_pack_keys": (C.c_int, [_P, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, _P, _P, _P, C.c_int, _P]),
+    "kad_rt_closest_keys_packed": (C.c_int, [_P, _P, C.c_uint32, C.c_uint32, _P, _P, _P, _P]),
+    "kad_comm_unique_id": (C.c_int, [_P]),
+    "kad_comm_create": (C.c_int, [C.POINTER(_P), C.c_int, C.c_uint32, C.c_uint32, _P]),
+    "kad_comm_destroy": (C.c_int, [_P]),
+    "kad_comm_info": (C.c_int, [_P, _P, _P, _P]),
+    "kad_comm_all_to_all": (C.c_int, [_P, _P, _P, C.c_uint64, _P]),
+    "kad_route_run": (C.c_int, [_P, _P, C.c_uint32, _P, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
+                                C.c_uint32, C.c_uint32, _P, _P, _P, _P, _P]),
+    "kad_shard_run": (C.c_int, [_P, _P, _P, C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
+                                C.c_uint32, _P, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, _P, _P, _P,
+                                _P, _P, _P, _P]),
     "kad_table_set_addrs": (C.c_int, [_P, C.c_uint32, _P]),
     "kad_buffer_nodes_batch": (C.c_int, [_P, _P, C.c_uint32, _P, _P, C.c_uint32, _P, _P, _P]),
     "kad_parse_nodes_batch": (C.c_int, [_P, C.c_uint32, C.c_uint32, _P, _P, C.c_int, _P]),
@@ -187,6 +200,16 @@ class table_info(C.Structure):
         ("flags", C.c_uint32), ("device", C.c_int32), ("rt_radix_bits", C.c_uint32),
         ("nc_radix_bits", C.c_uint32), ("n_good", C.c_uint32), ("device_bytes", C.c_uint64),
     ]
+
+
+KAD_COMM_ID_BYTES = 128
+KAD_ROUTE_PACKED, KAD_ROUTE_KEYS = 1, 2
+
+
+class route_set(C.Structure):
+    """kad_route_set: one buffer set of kad_route_run (device pointers)."""
+    _fields_ = [(n, C.c_void_p) for n in ("send", "recv", "slot", "ctr", "rows", "cnt", "back_rows", "back_cnt", "prow",
+                                          "back_prow")]
 
 
 class serve_stats(C.Structure):

@@ -522,10 +522,18 @@ __device__ __forceinline__ bool lt3(uint64_t a0, uint64_t a1, uint64_t a2, uint6
 // the first min(count, good) good nodes by (160-bit XOR distance, index), + index_base, padded with
 // NONE. If `dist` is given, dist[5*r .. 5*r+4] = the XOR distance of row entry r as five native
 // words (most significant first): the merge key of kad_rt_merge_parts.
+// tie (key-only queries, kad_rt_closest_keys_packed: the target's low 96 bits unknown, taken as zero): the order is
+// that of the full target unless two nodes of [beg, end) share their top 64 bits (equal keys are adjacent in a sorted
+// table), which sets *tie: the caller answers the batch again from full targets.
 __device__ void wave_rank(const DevTable& T, const Target& t, uint32_t beg, uint32_t end, uint32_t good,
-                          uint32_t count, uint32_t* row, uint32_t* dist, uint64_t* xs) {
+                          uint32_t count, uint32_t* row, uint32_t* dist, uint64_t* xs, uint32_t* tie = nullptr) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t m = min(count, good);
+    if (tie) {
+        bool eq = false;
+        for (uint32_t j = beg + lane; j + 1 < end; j += 64) eq |= T.key[j] == T.key[j + 1];
+        if (__any(eq) && lane == 0) atomicOr(tie, 1u);
+    }
     if (end - beg <= 64) {  // one tile (nearly every case): rank by broadcast LDS reads
         const uint32_t j = beg + lane;
         uint64_t V0 = ~0ull, V1 = ~0ull, V2 = ~0ull;
@@ -697,7 +705,7 @@ __device__ __forceinline__ uint32_t wave_good_sum(const uint32_t* gcnt, uint32_t
 }
 
 __device__ void wave_exact(const DevTable& T, const Target& t, uint32_t count, uint32_t* row, uint8_t* cp,
-                           uint64_t* xs /* this wave's 64 x 3 LDS words */) {
+                           uint64_t* xs /* this wave's 64 x 3 LDS words */, uint32_t* tie = nullptr) {
     const uint32_t lane = threadIdx.x & 63u, B = T.B;
     if (B == 0 || count == 0) {
         if (lane < count) row[lane] = NONE;
@@ -706,7 +714,7 @@ __device__ void wave_exact(const DevTable& T, const Target& t, uint32_t count, u
     }
     uint32_t lo, hi, good;
     wave_window(T.gcnt, B, locate_bucket(T, t), count, lo, hi, good);
-    wave_rank(T, t, T.dir[lo].x & ~WIDE, T.dir[hi + 1].x & ~WIDE, good, count, row, nullptr, xs);
+    wave_rank(T, t, T.dir[lo].x & ~WIDE, T.dir[hi + 1].x & ~WIDE, good, count, row, nullptr, xs, tie);
     if (lane == 0 && cp) *cp = (uint8_t)min(count, good);
 }
 
@@ -1360,15 +1368,21 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) v
 // else the 128-byte line's, else the exact path's (by the wave, into LDS), packed in the kernel, so that no row of 33
 // bytes is written and read again. A row wider than 254 indices sets *escape and writes nothing: the caller answers
 // that batch again unpacked.
+// KEYS (kad_rt_closest_keys_packed, owner routing's key-only exchange): the batch is the targets' top 64 bits alone
+// (8-byte keys, native order), which is all the short and 128-byte lines read; the exact path runs with the low 96
+// bits taken as zero, exact unless two nodes of its window share their top 64 bits — then *tail is set and the caller
+// answers the batch again from full targets (wave_rank).
+template <bool KEYS = false>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) void rt_ws_packed_kernel(
     DevTable T, const uint8_t* __restrict__ targets, uint32_t q, uint32_t* __restrict__ packed,
-    uint32_t* __restrict__ escape) {
+    uint32_t* __restrict__ escape, uint32_t* __restrict__ tail = nullptr) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     const bool act = i < q;
     Target t{};
     uint32_t b = 0;
     if (act) {
-        t.hi = load_target_hi(targets, i);
+        t.hi = KEYS ? __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(targets) + i)
+                    : load_target_hi(targets, i);
         b = locate_bucket(T, t);
     }
     uint32_t o[8], m;
@@ -1390,15 +1404,15 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) v
         __shared__ uint32_t xrow[BLOCK / 64][8];
         __shared__ uint8_t xcnt[BLOCK / 64];
         const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-        if (need) t = load_target(targets, i);
+        if (need && !KEYS) t = load_target(targets, i);
         for (uint64_t mm = __ballot(need); mm; mm &= mm - 1) {
             const uint32_t l = (uint32_t)__builtin_ctzll(mm);
             Target u;
             u.hi = rdl64(t.hi, l);
-            u.t2 = rdl(t.t2, l);
-            u.t3 = rdl(t.t3, l);
-            u.t4 = rdl(t.t4, l);
-            wave_exact(T, u, 8u, xrow[w], &xcnt[w], xs[w]);
+            u.t2 = KEYS ? 0u : rdl(t.t2, l);
+            u.t3 = KEYS ? 0u : rdl(t.t3, l);
+            u.t4 = KEYS ? 0u : rdl(t.t4, l);
+            wave_exact(T, u, 8u, xrow[w], &xcnt[w], xs[w], KEYS ? tail : nullptr);
             __builtin_amdgcn_wave_barrier();
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_wave_barrier();
@@ -8881,8 +8895,23 @@ int kad_rt_closest_batch_packed(const kad_table* t, const uint8_t* targets, uint
     if (!targets || !packed || !escape) return set_err(KAD_ERR_INVALID, "NULL buffer");
     if (((uintptr_t)targets & 3) || ((uintptr_t)packed & 3)) return set_err(KAD_ERR_INVALID, "device buffers must be 4-byte aligned");
     DeviceGuard g(t->device);
-    hipLaunchKernelGGL(rt_ws_packed_kernel, dim3(grid_for(q)), dim3(BLOCK), 0, (hipStream_t)stream, t->d, targets, q,
-                       packed, escape);
+    hipLaunchKernelGGL(rt_ws_packed_kernel<false>, dim3(grid_for(q)), dim3(BLOCK), 0, (hipStream_t)stream, t->d, targets,
+                       q, packed, escape, nullptr);
+    HIP_TRY(hipGetLastError());
+    return KAD_OK;
+}
+
+int kad_rt_closest_keys_packed(const kad_table* t, const uint64_t* keys, uint32_t q, uint32_t count, uint32_t* packed,
+                               uint32_t* escape, uint32_t* tail, void* stream) {
+    if (!t) return set_err(KAD_ERR_INVALID, "NULL table");
+    if (count != 8 || !(t->d.flags & TF_WS) || std::getenv("KAD_RT_KERNEL"))
+        return set_err(KAD_ERR_UNSUPPORTED, "key-only rows: count 8 on tables with short window lines only");
+    if (q == 0) return KAD_OK;
+    if (!keys || !packed || !escape || !tail) return set_err(KAD_ERR_INVALID, "NULL buffer");
+    if (((uintptr_t)keys & 7) || ((uintptr_t)packed & 3)) return set_err(KAD_ERR_INVALID, "keys must be 8-byte aligned, rows 4-byte");
+    DeviceGuard g(t->device);
+    hipLaunchKernelGGL(rt_ws_packed_kernel<true>, dim3(grid_for(q)), dim3(BLOCK), 0, (hipStream_t)stream, t->d,
+                       reinterpret_cast<const uint8_t*>(keys), q, packed, escape, tail);
     HIP_TRY(hipGetLastError());
     return KAD_OK;
 }

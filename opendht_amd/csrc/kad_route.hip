@@ -28,6 +28,9 @@ constexpr uint32_t BLOCK = 256, QPT = KAD_ROUTE_QPW / BLOCK;  // queries per thr
 constexpr uint32_t NONE = 0xFFFFFFFFu;
 typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
 
+// KEYS (kad_route_pack_keys): each record is the target's top 64 bits as one native 8-byte key instead of its 20 bytes
+// (owner routing's key-only exchange: the owner's line paths read nothing else).
+template <bool KEYS>
 __global__ __launch_bounds__(BLOCK) void route_pack_kernel(const uint8_t* __restrict__ targets, uint32_t q,
                                                             uint32_t world, uint32_t shard_bits, uint32_t cap,
                                                             uint8_t* __restrict__ send, uint32_t* __restrict__ slot,
@@ -77,9 +80,15 @@ __global__ __launch_bounds__(BLOCK) void route_pack_kernel(const uint8_t* __rest
         uint32_t out = NONE;
         if (s < sub) {
             out = dst[r] * cap + rg * sub + s;
-            uint32_t* o = reinterpret_cast<uint32_t*>(send + 20ull * out);
+            if (KEYS) {
+                uint32_t* o = reinterpret_cast<uint32_t*>(send + 8ull * out);
+                o[0] = __builtin_bswap32(w[r][1]);  // (InfoHash bytes 4..7: the key's low word)
+                o[1] = __builtin_bswap32(w[r][0]);
+            } else {
+                uint32_t* o = reinterpret_cast<uint32_t*>(send + 20ull * out);
 #pragma unroll
-            for (int x = 0; x < 5; x++) o[x] = w[r][x];
+                for (int x = 0; x < 5; x++) o[x] = w[r][x];
+            }
         } else {
             atomicOr(ctr + KAD_ROUTE_OVERFLOW_WORD(world), 1u);
         }
@@ -271,8 +280,8 @@ struct DevSwitch {
 
 }  // namespace
 
-extern "C" int kad_route_pack(const uint8_t* targets, uint32_t q, uint32_t world, uint32_t shard_bits, uint32_t cap,
-                              uint8_t* send, uint32_t* slot, uint32_t* ctr, int device, void* stream) {
+static int route_pack(bool keys, const uint8_t* targets, uint32_t q, uint32_t world, uint32_t shard_bits, uint32_t cap,
+                      uint8_t* send, uint32_t* slot, uint32_t* ctr, int device, void* stream) {
     using kadgpu_internal::set_error;
     if (world == 0 || world > KAD_ROUTE_MAX_WORLD) return set_error(KAD_ERR_INVALID, "world must be 1..16");
     if (shard_bits > 8) return set_error(KAD_ERR_INVALID, "shard_bits must be 0..8");
@@ -287,12 +296,29 @@ extern "C" int kad_route_pack(const uint8_t* targets, uint32_t q, uint32_t world
     hipError_t e = hipMemsetAsync(ctr, 0, 4ull * KAD_ROUTE_CTR_WORDS(world), s);
     if (e == hipSuccess && q) {
         const uint32_t nb = (uint32_t)(((uint64_t)q + BLOCK * QPT - 1) / (BLOCK * QPT));
-        hipLaunchKernelGGL(route_pack_kernel, dim3(nb), dim3(BLOCK), 0, s, targets, q, world, shard_bits, cap, send,
-                           slot, ctr);
+        if (keys)
+            hipLaunchKernelGGL(route_pack_kernel<true>, dim3(nb), dim3(BLOCK), 0, s, targets, q, world, shard_bits, cap,
+                               send, slot, ctr);
+        else
+            hipLaunchKernelGGL(route_pack_kernel<false>, dim3(nb), dim3(BLOCK), 0, s, targets, q, world, shard_bits, cap,
+                               send, slot, ctr);
         e = hipGetLastError();
     }
     if (e != hipSuccess) return set_error(KAD_ERR_HIP, hipGetErrorString(e));
     return KAD_OK;
+}
+
+extern "C" int kad_route_pack(const uint8_t* targets, uint32_t q, uint32_t world, uint32_t shard_bits, uint32_t cap,
+                              uint8_t* send, uint32_t* slot, uint32_t* ctr, int device, void* stream) {
+    return route_pack(false, targets, q, world, shard_bits, cap, send, slot, ctr, device, stream);
+}
+
+extern "C" int kad_route_pack_keys(const uint8_t* targets, uint32_t q, uint32_t world, uint32_t shard_bits,
+                                   uint32_t cap, uint64_t* send_keys, uint32_t* slot, uint32_t* ctr, int device,
+                                   void* stream) {
+    if ((uintptr_t)send_keys & 7u) return kadgpu_internal::set_error(KAD_ERR_INVALID, "send_keys must be 8-byte aligned");
+    return route_pack(true, targets, q, world, shard_bits, cap, reinterpret_cast<uint8_t*>(send_keys), slot, ctr, device,
+                      stream);
 }
 
 extern "C" int kad_route_unpack(const uint32_t* slot, uint32_t q, uint32_t count, const uint32_t* back_idx,

@@ -291,11 +291,18 @@ class OwnerRoute:
     cap: records per block, a multiple of KAD_ROUTE_SUBS: a block is 8 sub-blocks, workgroup w (1,024 targets)
     appending to sub-block w % 8; default 8 x (the most targets one sub-block's workgroups hold / world + 6 sigma +
     32) for uniform targets. A sub-block that fills sets a sticky word; overflowed() combines it over the ranks (one
-    host read per batch, or per K steps), grown() sizes the blocks from the counts, and the batch runs again. collective=True forces the collectives at world 1 (a one-rank
-    RCCL group)."""
+    host read per batch, or per K steps), grown() sizes the blocks from the counts, and the batch runs again.
+    collective=True forces the collectives at world 1 (a one-rank RCCL group).
+
+    keys (the default at count 8 with packed rows): the targets travel as 8-byte keys, their top 64 bits
+    (kad_route_pack_keys), which is all the owner's short and 128-byte window lines read; the owner answers with
+    kad_rt_closest_keys_packed, whose exact path (the ~0.001 % of queries no line answers) is exact from the key alone
+    unless two nodes of its window share their top 64 bits — then a sticky tail word (tailed()) asks for the batch
+    again from full targets (keys=False), as does an owner table without short lines. 8 + 12 bytes per query on the
+    links instead of 20 + 12."""
 
     def __init__(self, q: int, count: int, world: int, shard_bits: int, device, cap: int | None = None,
-                 collective: bool | None = None, packed: bool | None = None):
+                 collective: bool | None = None, packed: bool | None = None, keys: bool | None = None):
         import torch
 
         from ._lib import KAD_ROUTE_PACKED_MAX_COUNT, KAD_ROUTE_QPW, KAD_ROUTE_SUBS, route_ctr_words, route_packed_words
@@ -305,6 +312,9 @@ class OwnerRoute:
         # and unpacks in 8.3 us per 1M rows, against 13.1 us for the plain unpack; tools/route_packed_check.py)
         self.packed = (count % 4 == 0 and 1 <= count <= KAD_ROUTE_PACKED_MAX_COUNT) if packed is None else bool(packed)
         self.collective = world > 1 if collective is None else bool(collective)
+        self.keys = (count == 8 and self.packed) if keys is None else bool(keys)
+        if self.keys and not (count == 8 and self.packed):
+            raise ValueError("key-only routing needs count 8 and packed rows")
         # the most targets the workgroups of one sub-block hold (workgroup w -> sub-block w % 8): a sub-block can never
         # receive more, so 8 x that is the capacity that never overflows
         S = KAD_ROUTE_SUBS
@@ -317,6 +327,11 @@ class OwnerRoute:
         self.send = torch.empty((n, 20), dtype=torch.uint8, device=device)
         pad_blocks(self.send, world, shard_bits, self.cap)
         self.recv = torch.empty_like(self.send) if self.collective else self.send
+        self.send_keys = self.recv_keys = None
+        if self.keys:
+            self.send_keys = torch.empty((n,), dtype=torch.int64, device=device)
+            pad_keys(self.send_keys, world, shard_bits, self.cap)
+            self.recv_keys = torch.empty_like(self.send_keys) if self.collective else self.send_keys
         self.slot = torch.empty((max(q, 1),), dtype=torch.int32, device=device)
         self.ctr = torch.zeros((route_ctr_words(world),), dtype=torch.int32, device=device)
         self.rows = torch.empty((n, max(count, 1)), dtype=torch.int32, device=device)
@@ -331,13 +346,23 @@ class OwnerRoute:
     def xgmi_bytes(self) -> dict:
         """Bytes a rank sends to the other ranks per step: targets out, rows + counts back."""
         per = 4 * self.pw if self.packed else 4 * self.count + 1
-        return {"targets": 20 * (self.world - 1) * self.cap, "rows": per * (self.world - 1) * self.cap}
+        return {"targets": self.record_bytes * (self.world - 1) * self.cap, "rows": per * (self.world - 1) * self.cap}
 
-    def pack(self, targets, stream):
+    @property
+    def record_bytes(self) -> int:
+        """Bytes per target record on the links: an 8-byte key, or the 20-byte target."""
+        return 8 if self.keys else 20
+
+    def pack(self, targets, stream, keys: bool | None = None):
         import ctypes as C
 
         from ._lib import check, lib, ptr
 
+        if self.keys if keys is None else keys:
+            check(lib().kad_route_pack_keys(ptr(targets), self.q, self.world, self.shard_bits, self.cap,
+                                            ptr(self.send_keys), ptr(self.slot), ptr(self.ctr), self.dev.index or 0,
+                                            C.c_void_p(stream)), "kad_route_pack_keys")
+            return
         check(lib().kad_route_pack(ptr(targets), self.q, self.world, self.shard_bits, self.cap, ptr(self.send),
                                    ptr(self.slot), ptr(self.ctr), self.dev.index or 0, C.c_void_p(stream)),
               "kad_route_pack")
@@ -371,15 +396,33 @@ class OwnerRoute:
                                             ptr(out_cnt), self.dev.index or 0, C.c_void_p(stream)),
               "kad_route_unpack_packed")
 
-    def answer(self, table, stream, packed: bool | None = None):
+    def answer(self, table, stream, packed: bool | None = None, keys: bool | None = None):
         """The owner's rows for every record of the received blocks (table: a DeviceTable). Packed rows at count 8 on
         a table with short window lines come packed out of the query kernel itself (kad_rt_closest_batch_packed:
-        `fused`); otherwise full rows, packed by compress() on the way back."""
+        `fused`); otherwise full rows, packed by compress() on the way back. keys: from the received 8-byte keys
+        (kad_rt_closest_keys_packed; an owner table without short lines sets the tail word)."""
         import ctypes as C
 
         from ._lib import KAD_ERR_UNSUPPORTED, check, lib, ptr, route_overflow_word
 
         self.fused = False
+        if self.keys if keys is None else keys:
+            esc = self.ctr.data_ptr() + 4 * (route_overflow_word(self.world) + 1)
+            rc = lib().kad_rt_closest_keys_packed(table._h, ptr(self.recv_keys), self.world * self.cap, self.count,
+                                                  ptr(self.prow), C.c_void_p(esc), C.c_void_p(esc + 4),
+                                                  C.c_void_p(stream))
+            self.fused = True
+            if rc == KAD_ERR_UNSUPPORTED:
+                import torch
+
+                from .global_shard import _torch_stream
+
+                w = route_overflow_word(self.world) + 2
+                with torch.cuda.stream(_torch_stream(stream, self.dev)):
+                    self.ctr[w:w + 1].fill_(1)
+                return
+            check(rc, "kad_rt_closest_keys_packed")
+            return
         if (self.packed if packed is None else packed) and self.count == 8:
             rc = lib().kad_rt_closest_batch_packed(
                 table._h, ptr(self.recv), self.world * self.cap, self.count, ptr(self.prow),
@@ -390,16 +433,19 @@ class OwnerRoute:
                 return
         table.rt_closest(self.recv, self.count, out_idx=self.rows, out_cnt=self.cnt, stream=stream)
 
-    def step(self, table, targets, out_idx, out_cnt, group=None, stream=None, packed: bool | None = None):
-        """pack, send, answer, return, unpack: device-only (check overflowed(), then escaped(), after).
-        packed=False: the way back unpacked (the rerun of a batch whose rows escaped packing)."""
+    def step(self, table, targets, out_idx, out_cnt, group=None, stream=None, packed: bool | None = None,
+             keys: bool | None = None):
+        """pack, send, answer, return, unpack: device-only (check overflowed(), then tailed(), then escaped(), after).
+        packed=False: the way back unpacked (the rerun of a batch whose rows escaped packing); keys=False: full
+        targets (the rerun of a batch whose key-only answer needed the targets' low bits)."""
         import torch
 
         s = stream if stream is not None else torch.cuda.current_stream(self.dev).cuda_stream
         packed = self.packed if packed is None else packed
-        self.pack(targets, s)
-        self.send_targets(group, s)
-        self.answer(table, s, packed)
+        keys = (self.keys if keys is None else keys) and packed
+        self.pack(targets, s, keys)
+        self.send_targets(group, s, keys)
+        self.answer(table, s, packed, keys)
         self.back(out_idx, out_cnt, group, s, packed)
 
     def back(self, out_idx, out_cnt, group, s, packed: bool):
@@ -409,7 +455,7 @@ class OwnerRoute:
         self.send_back(group, s, packed)
         self.unpack_rows(out_idx, out_cnt, s, packed)
 
-    def send_targets(self, group, s):
+    def send_targets(self, group, s, keys: bool | None = None):
         """The target blocks to their owners (all_to_all_single on stream s; nothing without a collective)."""
         import torch
 
@@ -417,7 +463,10 @@ class OwnerRoute:
 
         if self.collective:
             with torch.cuda.stream(_torch_stream(s, self.dev)):
-                _all_to_all(self.recv, self.send, group)
+                if self.keys if keys is None else keys:
+                    _all_to_all(self.recv_keys, self.send_keys, group)
+                else:
+                    _all_to_all(self.recv, self.send, group)
 
     def send_back(self, group, s, packed: bool):
         """The answered rows back to their senders (packed: one all_to_all_single of the packed rows, already
@@ -442,8 +491,8 @@ class OwnerRoute:
             self.unpack(out_idx, out_cnt, s)
 
     def fold_flags(self, acc, s):
-        """acc (2 int32, device) |= this batch's overflow and escape words, on stream s: kad_route_pack zeroes both
-        with the counters, so a caller running many batches folds them after each one and reads acc once."""
+        """acc (3 int32, device) |= this batch's overflow, escape and tail words, on stream s: kad_route_pack zeroes
+        them with the counters, so a caller running many batches folds them after each one and reads acc once."""
         import torch
 
         from ._lib import route_overflow_word
@@ -451,7 +500,15 @@ class OwnerRoute:
 
         w = route_overflow_word(self.world)
         with torch.cuda.stream(_torch_stream(s, self.dev)):
-            torch.maximum(acc, self.ctr[w:w + 2], out=acc)
+            torch.maximum(acc, self.ctr[w:w + 3], out=acc)
+
+    def tailed(self, group=None, combine: bool = True) -> bool:
+        """Host read of the key-only tail word (a batch answered from keys needs the full targets), combined."""
+        if not self.keys:
+            return False
+        from ._lib import route_overflow_word
+
+        return self._flag(route_overflow_word(self.world) + 2, group, combine)
 
     def escaped(self, group=None, combine: bool = True) -> bool:
         """Host read of the packing escape word (a row spanning more than 254 indices), combined over the ranks."""
@@ -488,7 +545,7 @@ class OwnerRoute:
         n = self.need(group) if need is None else need
         return OwnerRoute(self.q, self.count, self.world, self.shard_bits, self.dev,
                           cap=min(self.cap_max, max(2 * self.cap, n * 5 // 4)), collective=self.collective,
-                          packed=self.packed)
+                          packed=self.packed, keys=self.keys)
 
 
 def combine_max(words, group=None, combine: bool = True) -> list[int]:
@@ -522,6 +579,18 @@ def pad_blocks(send, world: int, shard_bits: int, cap: int):
         v[:, :, 1] = 0x80
     else:
         v[:, :, 0] = ((b << (8 - shard_bits)) | (1 << (7 - shard_bits))).to(torch.uint8)[:, None]
+
+
+def pad_keys(keys, world: int, shard_bits: int, cap: int):
+    """pad_blocks for key-only blocks: every key the padding target's top 64 bits."""
+    import torch
+
+    b = torch.arange(world, dtype=torch.int64, device=keys.device)
+    if shard_bits >= 8:
+        k = (b << 56) | (0x80 << 48)
+    else:
+        k = ((b << (8 - shard_bits)) | (1 << (7 - shard_bits))) << 56
+    keys.view(world, cap)[:] = k[:, None]
 
 
 def need_of(ctr, world: int) -> int:
@@ -575,11 +644,16 @@ def serve_owner(table, targets, count: int, route: OwnerRoute | None = None, gro
     while True:
         route.step(table, targets, out_idx, out_cnt, group, stream)
         if not route.overflowed(group):
-            if route.escaped(group):  # a row too wide to pack: this batch's rows go back unpacked
-                import torch as _t
+            import torch as _t
 
-                s = stream if stream is not None else _t.cuda.current_stream(targets.device).cuda_stream
-                route.answer(table, s, packed=False)  # (the received targets are still in place)
+            s = stream if stream is not None else _t.cuda.current_stream(targets.device).cuda_stream
+            if route.tailed(group):  # a key-only answer needed the low bits: the batch again from full targets
+                route.step(table, targets, out_idx, out_cnt, group, stream, keys=False)
+            if route.escaped(group):  # a row too wide to pack: this batch's rows go back unpacked
+                if route.keys:  # (the received keys cannot answer unpacked: the full targets travel)
+                    route.pack(targets, s, keys=False)
+                    route.send_targets(group, s, keys=False)
+                route.answer(table, s, packed=False, keys=False)  # (the received targets are in place)
                 route.back(out_idx, out_cnt, group, s, packed=False)
             return out_idx, out_cnt, route
         route = route.grown(group)
@@ -602,24 +676,27 @@ class OwnerPipeline:
     DEPTH = 3
 
     def __init__(self, q: int, count: int, world: int, shard_bits: int, device, cap: int | None = None,
-                 collective: bool | None = None, packed: bool | None = None):
+                 collective: bool | None = None, packed: bool | None = None, keys: bool | None = None):
         import torch
 
-        self.routes = [OwnerRoute(q, count, world, shard_bits, device, cap=cap, collective=collective, packed=packed)
-                       for _ in range(self.DEPTH)]
+        self.routes = [OwnerRoute(q, count, world, shard_bits, device, cap=cap, collective=collective, packed=packed,
+                                  keys=keys) for _ in range(self.DEPTH)]
         r = self.routes[0]
         self.q, self.count, self.world, self.shard_bits, self.dev = q, count, world, shard_bits, device
         self.cap, self.packed, self.collective = r.cap, r.packed, r.collective
         self.compute = torch.cuda.Stream(device)
         self.comm = torch.cuda.Stream(device)
-        self.acc = torch.zeros((2,), dtype=torch.int32, device=device)  # [overflow, escape] over the batches run
+        self.keys = r.keys
+        self.acc = torch.zeros((3,), dtype=torch.int32, device=device)  # [overflow, escape, tail] over the batches
 
-    def run(self, table, batches, outs, group=None, packed: bool | None = None):
+    def run(self, table, batches, outs, group=None, packed: bool | None = None, keys: bool | None = None):
         """Route every batch of `batches` ((q, 20) device targets) and unpack its rows into outs[i] = (out_idx,
-        out_cnt). Returns when everything is issued; the caller's current stream waits for the last unpack."""
+        out_cnt). Returns when everything is issued; the caller's current stream waits for the last unpack.
+        packed=False / keys=False: the reruns (rows back unpacked / full targets on the links)."""
         import torch
 
         packed = self.packed if packed is None else bool(packed)
+        keys = (self.keys if keys is None else bool(keys)) and packed
         cur = torch.cuda.current_stream(self.dev)
         cs, xs = self.compute, self.comm
         cs.wait_stream(cur)
@@ -630,18 +707,18 @@ class OwnerPipeline:
         R = lambda i: self.routes[i % self.DEPTH]  # noqa: E731
 
         def pack(i):
-            R(i).pack(batches[i], c)
+            R(i).pack(batches[i], c, keys)
             e = torch.cuda.Event()
             e.record(cs)
             xs.wait_event(e)
-            R(i).send_targets(group, x)
+            R(i).send_targets(group, x, keys)
             sent[i] = torch.cuda.Event()
             sent[i].record(xs)
 
         def answer(i):
             r = R(i)
             cs.wait_event(sent[i])
-            r.answer(table, c, packed)
+            r.answer(table, c, packed, keys)
             if packed and not r.fused:
                 r.compress(c)
             e = torch.cuda.Event()
@@ -670,11 +747,12 @@ class OwnerPipeline:
         cur.wait_stream(cs)
         cur.wait_stream(xs)
 
-    def flags(self, group=None, combine: bool = True) -> tuple[bool, bool]:
-        """(overflowed, escaped) over every batch run since the last call, combined over the ranks; cleared."""
-        ov, esc = combine_max(self.acc, group, combine and self.collective)
+    def flags(self, group=None, combine: bool = True) -> tuple[bool, bool, bool]:
+        """(overflowed, escaped, tailed) over every batch run since the last call, combined over the ranks;
+        cleared."""
+        ov, esc, tail = combine_max(self.acc, group, combine and self.collective)
         self.acc.zero_()
-        return bool(ov), bool(esc) and self.packed
+        return bool(ov), bool(esc) and self.packed, bool(tail) and self.keys
 
     def grown(self, group=None) -> "OwnerPipeline":
         """Larger blocks, sized from the fullest sub-block of the last batch each buffer set packed (combined)."""
@@ -682,13 +760,13 @@ class OwnerPipeline:
         n = self.routes[0].need(group, local=n) if self.collective else n
         cap = min(self.routes[0].cap_max, max(2 * self.cap, n * 5 // 4))
         return OwnerPipeline(self.q, self.count, self.world, self.shard_bits, self.dev, cap=cap,
-                             collective=self.collective, packed=self.packed)
+                             collective=self.collective, packed=self.packed, keys=self.keys)
 
 
 def serve_pipelined(table, batches, count: int, pipe: OwnerPipeline | None = None, group=None, outs=None):
     """serve_owner for a run of batches through the overlapped OwnerPipeline: grows the blocks and runs everything
-    again when some batch overflowed, and again with the rows back unpacked when some row escaped packing (both
-    decisions combined over the ranks). Returns (outs, pipe)."""
+    again when some batch overflowed, from full targets when some key-only answer needed them, and with the rows back
+    unpacked when some row escaped packing (every decision combined over the ranks). Returns (outs, pipe)."""
     import torch
     import torch.distributed as dist
 
@@ -702,10 +780,13 @@ def serve_pipelined(table, batches, count: int, pipe: OwnerPipeline | None = Non
                                                                                      device=dev)) for _ in batches]
     while True:
         pipe.run(table, batches, outs, group)
-        over, esc = pipe.flags(group)
+        over, esc, tail = pipe.flags(group)
         if over:
             pipe = pipe.grown(group)
             continue
+        if tail:  # some key-only answer needed the targets' low bits: everything again from full targets
+            pipe.run(table, batches, outs, group, keys=False)
+            _, esc, _ = pipe.flags(group)
         if esc:
             pipe.run(table, batches, outs, group, packed=False)
             pipe.flags(group)
@@ -723,8 +804,8 @@ def route_simulated(tables, batches, count: int, shard_bits: int, cap: int | Non
     dev = batches[0].device
     s = torch.cuda.current_stream(dev).cuda_stream
     while True:
-        routes = [OwnerRoute(b.shape[0], count, world, shard_bits, dev, cap=cap, collective=False, packed=packed)
-                  for b in batches]
+        routes = [OwnerRoute(b.shape[0], count, world, shard_bits, dev, cap=cap, collective=False, packed=packed,
+                             keys=False) for b in batches]
         if len({r.cap for r in routes}) != 1:
             raise ValueError("every rank's batch must give the same block size")
         c = routes[0].cap

@@ -129,6 +129,41 @@ def main():
                 np.testing.assert_array_equal(outs[j][1].cpu().numpy(), wcnt, err_msg=f"ns pipe k={count} b{j}")
                 np.testing.assert_array_equal(outs[j][0].cpu().numpy().view(np.uint32), want,
                                               err_msg=f"ns pipe k={count} b{j}")
+        # the native executor (opendht_amd.comm: kad_route_run / kad_shard_run over the engine's own RCCL
+        # communicator), serial and pipelined, blocks of one record first for the owner routing
+        from opendht_amd.comm import Comm, NativeRoute, serve_native, shard_run
+
+        with Comm(0, 1, 0) as comm:
+            for count in (8, 14, 32):
+                wants = [O.flat_rt_closest(ids, st, first, off, b, count, nthreads=8) for b in batches]
+                for n_sets in (1, 3):
+                    route = NativeRoute(6000, count, 1, 0, dev, cap=8, n_sets=n_sets, comm=comm)
+                    outs, route = serve_native(T, dbs, count, route)
+                    torch.cuda.synchronize()
+                    assert route.cap > 8
+                    for j, (want, wcnt) in enumerate(wants):
+                        np.testing.assert_array_equal(outs[j][1].cpu().numpy(), wcnt, err_msg=f"native k={count} "
+                                                      f"sets={n_sets} b{j} counts")
+                        np.testing.assert_array_equal(outs[j][0].cpu().numpy().view(np.uint32), want,
+                                                      err_msg=f"native k={count} sets={n_sets} b{j}")
+                    like = Exchange(6000, count, 1, dev, row_cap=1 << 20, part_cap=4096, collective=True)
+                    exs = G.pipeline(6000, count, 1, like=like)[:n_sets]
+                    outs = [(torch.empty((6000, count), dtype=torch.int32, device=dev),
+                             torch.empty((6000,), dtype=torch.uint8, device=dev)) for _ in dbs]
+                    shard_run(G, comm, dbs, exs, outs)
+                    torch.cuda.synchronize()
+                    assert not exs[0].overflowed()
+                    for j, (want, wcnt) in enumerate(wants):
+                        np.testing.assert_array_equal(outs[j][1].cpu().numpy(), wcnt, err_msg=f"native ns k={count} "
+                                                      f"sets={n_sets} b{j} counts")
+                        np.testing.assert_array_equal(outs[j][0].cpu().numpy().view(np.uint32), want,
+                                                      err_msg=f"native ns k={count} sets={n_sets} b{j}")
+            # kad_comm_all_to_all at world 1: a copy
+            x = torch.randint(0, 1 << 30, (4096,), dtype=torch.int32, device=dev)
+            y = torch.empty_like(x)
+            comm.all_to_all(y, x)
+            torch.cuda.synchronize()
+            assert torch.equal(x, y)
         T.close()
     finally:
         G.close()

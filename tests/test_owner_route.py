@@ -185,6 +185,78 @@ def test_owner_pipeline_one_rank(gpu, good_pct):
         T.close()
 
 
+def test_native_route_one_rank_no_comm(gpu):
+    """kad_route_run without a communicator (world 1, one buffer set, every batch in order on the stream): rows
+    packed (count 8, 32) and plain (14), blocks of one record first; every row against the oracle."""
+    from opendht_amd.comm import NativeRoute, serve_native
+
+    spec = ShardSpec(n_shards=1, depth=10, mean_per_bucket=6.0, seed=0x93, good_pct=70, expired_pct=15)
+    gids, gst, goff = spec.bucket_range(0, spec.n_buckets)
+    gfirst = S.bucket_firsts(spec.depth, 0, spec.n_buckets)
+    sh = build_shard(spec, 0)
+    T = DeviceTable(sh.ids, sh.status, sh.first, sh.off, device=0, index_base=sh.index_base, sorted=True)
+    try:
+        batches = [_batch(spec, 2500, seed=300 + j)[:2500] for j in range(4)]
+        for count in (8, 14, 32):
+            route = NativeRoute(2500, count, 1, 0, gpu, cap=8, n_sets=1)
+            outs, route = serve_native(T, [torch.from_numpy(b).to(gpu) for b in batches], count, route)
+            torch.cuda.synchronize()
+            assert route.cap > 8
+            for j, b in enumerate(batches):
+                want, wcnt = O.flat_rt_closest(gids, gst, gfirst, goff, b, count, nthreads=8)
+                np.testing.assert_array_equal(outs[j][1].cpu().numpy(), wcnt, err_msg=f"k={count} batch {j} counts")
+                np.testing.assert_array_equal(outs[j][0].cpu().numpy().view(np.uint32), want,
+                                              err_msg=f"k={count} batch {j}")
+        with pytest.raises(ValueError):
+            NativeRoute(2500, 8, 1, 0, gpu, n_sets=3)  # the pipelined form needs a communicator
+    finally:
+        T.close()
+
+
+def _tie_tables():
+    import tables as TB
+
+    return TB.tie_table() + TB.tie_table(groups=24, per=48, seed=8, tag="48") + [TB.uniform_config(20_000, 10),
+                                                                              TB.split_config(4000)]
+
+
+@pytest.mark.parametrize("ti", range(6), ids=["ties", "dups", "ties48", "dups48", "uniform", "split"])
+def test_owner_route_keys_ties(gpu, ti):
+    """Key-only owner routing (8-byte keys on the links, kad_rt_closest_keys_packed): on tables whose nodes share
+    their top 64 bits (tests/tables.py tie_table: ties / ties48, and the unsorted dups tables without short lines)
+    the key-only answer cannot order the window, sets the tail word, and serve_owner answers the batch again from
+    full targets; on a uniform table the keys answer every query. Every row bit-exact against the oracle
+    (infohash.h:131-146: xorCmp reads all 20 bytes)."""
+    import tables as TB
+    from opendht_amd.sharded import serve_owner
+
+    t = _tie_tables()[ti]
+    rng = np.random.default_rng(40 + ti)
+    tg = TB.adversarial_targets(t, extra=2000, seed=ti)
+    heads = t["ids"][rng.integers(0, t["ids"].shape[0], 300)].copy()
+    heads[:, 8:] = rng.integers(0, 256, (300, 12), dtype=np.uint8)  # the tied heads with other tails
+    tg = np.ascontiguousarray(np.concatenate([tg, heads]), np.uint8)
+    tg = tg[:tg.shape[0] // 8 * 8]
+    T = DeviceTable(t["ids"], t["status"], t["first"], t["off"], device=0, sorted=t.get("sorted", False))
+    try:
+        d = torch.from_numpy(tg).to(gpu)
+        R = OwnerRoute(tg.shape[0], 8, 1, 0, gpu)
+        assert R.keys and R.record_bytes == 8
+        oi = torch.empty((tg.shape[0], 8), dtype=torch.int32, device=gpu)
+        oc = torch.empty((tg.shape[0],), dtype=torch.uint8, device=gpu)
+        R.step(T, d, oi, oc)
+        tailed = R.tailed(combine=False)
+        if ti != 4:
+            assert tailed, "a top-64 tie (or a table without short lines) must ask for the full targets"
+        oi, oc, R = serve_owner(T, d, 8, route=R)
+        torch.cuda.synchronize()
+        want, wcnt = O.flat_rt_closest(t["ids"], t["status"], t["first"], t["off"], tg, 8, nthreads=8)
+        np.testing.assert_array_equal(oc.cpu().numpy(), wcnt)
+        np.testing.assert_array_equal(oi.cpu().numpy().view(np.uint32), want)
+    finally:
+        T.close()
+
+
 def test_padding_records_pack(gpu):
     """The send blocks start filled with a padding target of each block's owner: an owner answering
     whole blocks never meets uninitialised records, so the rows of the padding pack (no escape)."""
