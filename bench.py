@@ -798,8 +798,9 @@ def owner_step_model(T, Q, cnt_k, dev, stream, avg_kernel_s, link_gbs=64.0, lat_
     consecutive batches on two streams, max(pack + query + unpack, exchanges). `packed`: the same with the rows
     back packed (written packed by the query kernel at count 8 — kad_rt_closest_batch_packed —, by kad_route_compress
     otherwise; one collective of KAD_ROUTE_PACKED_WORDS(k) words per row; kad_route_unpack_packed). `keys` (count 8,
-    the default route): the targets out as 8-byte keys (kad_route_pack_keys, kad_rt_closest_keys_packed), the rows
-    back packed: 20 bytes per query on the links instead of 32."""
+    the default route): the targets out as 8-byte keys, the rows back packed (20 bytes per query on the links instead
+    of 32), the kernels as the native executor issues them (kad_route_pack_ex without a memset,
+    kad_rt_closest_keys_packed, kad_route_unpack_packed_fold)."""
     import torch
 
     from opendht_amd.sharded import OwnerRoute
@@ -866,16 +867,41 @@ def owner_step_model(T, Q, cnt_k, dev, stream, avg_kernel_s, link_gbs=64.0, lat_
                            "aggregate_queries_per_s_overlapped": n * Q / (overlap_p * 1e-6)}
             if cnt_k == 8:  # key-only targets (8 bytes out) + packed rows (12 back): kad_route_pack_keys,
                 # kad_rt_closest_keys_packed, kad_route_unpack_packed
+                import ctypes as C
+
+                from opendht_amd._lib import KAD_ROUTE_KEYS, KAD_ROUTE_ZEROED, check, lib, ptr, route_ctr_words
+
                 RK = OwnerRoute(Q, cnt_k, n, 3, dev, collective=False, keys=True)
-                pack_k_us = timed(lambda: RK.pack(t, s))
+                # as the native executor runs them (kad_route_run): the pack without a memset (KAD_ROUTE_ZEROED, a
+                # fresh zeroed counter set per launch), the unpack folding and zeroing the counters in its launch
+                cw = route_ctr_words(n)
+                ctrs = torch.zeros((reps + 1, cw), dtype=torch.int32, device=dev)
+                flags = torch.zeros((4,), dtype=torch.int32, device=dev)
+                it = iter(range(10**9))
+
+                def pack_z():
+                    j = next(it) % (reps + 1)
+                    check(lib().kad_route_pack_ex(ptr(t), Q, n, 3, RK.cap, ptr(RK.send_keys), ptr(RK.slot),
+                                                  ptr(ctrs[j]), KAD_ROUTE_KEYS | KAD_ROUTE_ZEROED, dev.index or 0,
+                                                  C.c_void_p(s)), "kad_route_pack_ex")
+
+                pack_k_us = timed(pack_z)
                 RK.recv_keys = recv[:, :8].flip(1).contiguous().view(torch.int64).view(-1)  # big-endian top 64 bits
                 query_k_us = timed(lambda: RK.answer(T, s))
                 tail = RK.tailed(combine=False)
+                RK.back_prow = R.prow  # (rows of the packed answer above: the unpack's input)
+
+                def unpack_f():
+                    check(lib().kad_route_unpack_packed_fold(ptr(RK.slot), Q, cnt_k, ptr(RK.back_prow), ptr(oi),
+                                                             ptr(oc), ptr(RK.ctr), n, ptr(flags), dev.index or 0,
+                                                             C.c_void_p(s)), "kad_route_unpack_packed_fold")
+
+                unpack_k_us = timed(unpack_f)
                 x_k = lat_us + 8 * RK.cap / (link_gbs * 1e3)
-                serial_k = pack_k_us + x_k + query_k_us + x_p + unpack_p_us
-                overlap_k = max(pack_k_us + query_k_us + unpack_p_us, x_k + x_p)
+                serial_k = pack_k_us + x_k + query_k_us + x_p + unpack_k_us
+                overlap_k = max(pack_k_us + query_k_us + unpack_k_us, x_k + x_p)
                 e["keys"] = {"target_bytes": 8, "row_bytes": 4 * R.pw, "tailed": tail, "pack_us": pack_k_us,
-                             "query_us": query_k_us, "unpack_us": unpack_p_us,
+                             "query_us": query_k_us, "unpack_us": unpack_k_us,
                              "xgmi_targets_bytes": 8 * (n - 1) * RK.cap, "xgmi_rows_bytes": 4 * R.pw * (n - 1) * RK.cap,
                              "exchange_targets_modelled_us": x_k, "exchange_rows_modelled_us": x_p,
                              "step_serial_us": serial_k, "step_overlapped_us": overlap_k,

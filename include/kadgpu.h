@@ -436,6 +436,10 @@ int kad_rt_home_finish_reset(const uint32_t* recv, uint32_t* send, uint32_t worl
                              uint32_t part_cap, uint32_t q, uint32_t count, uint32_t* scratch, uint32_t* out_idx,
                              uint8_t* out_cnt, uint32_t* overflow, int device, void* stream);
 
+#define KAD_ROUTE_PACKED 1u /* mode bits of kad_route_run / kad_route_pack_ex */
+#define KAD_ROUTE_KEYS 2u
+#define KAD_ROUTE_ZEROED 4u
+
 /* ---- owner routing of a serving front end ----
  * The headline form shards the table by ID range, one GPU per range, and answers every query on the GPU owning its
  * target (the reference answers each request where it arrives: Dht::onFindNode / onGetValues, dht.cpp:3189-3217).
@@ -469,6 +473,11 @@ int kad_route_pack(const uint8_t* targets, uint32_t q, uint32_t world, uint32_t 
  * the links instead of 20 (answered by kad_rt_closest_keys_packed). */
 int kad_route_pack_keys(const uint8_t* targets, uint32_t q, uint32_t world, uint32_t shard_bits, uint32_t cap,
                         uint64_t* send_keys, uint32_t* slot, uint32_t* ctr, int device, void* stream);
+/* kad_route_pack_ex: kad_route_pack / kad_route_pack_keys by `mode`: KAD_ROUTE_KEYS (8-byte key records),
+ * KAD_ROUTE_ZEROED (ctr is already zero — kad_route_unpack_packed_fold of the buffer set's previous batch leaves it so
+ * — and is not zeroed by the call: no memset before the kernel). */
+int kad_route_pack_ex(const uint8_t* targets, uint32_t q, uint32_t world, uint32_t shard_bits, uint32_t cap, void* send,
+                      uint32_t* slot, uint32_t* ctr, uint32_t mode, int device, void* stream);
 int kad_route_unpack(const uint32_t* slot, uint32_t q, uint32_t count, const uint32_t* back_idx,
                      const uint8_t* back_cnt, uint32_t* out_idx, uint8_t* out_cnt, int device, void* stream);
 /* Packed rows for the way back (count <= KAD_ROUTE_PACKED_MAX_COUNT): a row's indices lie in one window of the
@@ -486,6 +495,13 @@ int kad_route_compress(const uint32_t* idx, const uint8_t* cnt, uint32_t n, uint
                        uint32_t* escape, int device, void* stream);
 int kad_route_unpack_packed(const uint32_t* slot, uint32_t q, uint32_t count, const uint32_t* back_packed,
                             uint32_t* out_idx, uint8_t* out_cnt, int device, void* stream);
+/* kad_route_unpack_packed_fold: kad_route_unpack_packed, and in the same launch the batch's counters folded and zeroed
+ * for the next KAD_ROUTE_ZEROED pack: flags[0..2] |= ctr[KAD_ROUTE_OVERFLOW_WORD(world) + 0..2] (overflow, escape,
+ * tail), flags[3] = max(flags[3], KAD_ROUTE_SUBS x the fullest sub-block count: the capacity the batch needed), then
+ * ctr[0 .. KAD_ROUTE_CTR_WORDS(world)) = 0. q = 0: the fold and reset alone. */
+int kad_route_unpack_packed_fold(const uint32_t* slot, uint32_t q, uint32_t count, const uint32_t* back_packed,
+                                 uint32_t* out_idx, uint8_t* out_cnt, uint32_t* ctr, uint32_t world, uint32_t* flags,
+                                 int device, void* stream);
 /* kad_rt_closest_batch_packed: kad_rt_closest_batch with each row written packed (the layout above, word 0 a base
  * no larger than any entry) by the query kernel itself: no full row is written and read back by kad_route_compress.
  * Count 8 on tables with short window lines only (KAD_ERR_UNSUPPORTED otherwise: use kad_rt_closest_batch +
@@ -517,9 +533,11 @@ int kad_route_fold_flags(const uint32_t* ctr, uint32_t world, uint32_t* flags, i
  *   q targets: kad_route_pack into `world` blocks of `cap` records, all_to_all of the blocks, the owner's query of
  *   every received record (packed != 0: the rows go back packed — count 8 on tables with short window lines through
  *   kad_rt_closest_batch_packed, else kad_rt_closest_batch + kad_route_compress —; packed = 0: rows and counts), the
- *   all_to_all back, the unpack of batch i into out_idx[i] / out_cnt[i], and kad_route_fold_flags into flags (3 device
- *   words: [0] a block overflowed — grow cap and run again —, [1] a row escaped packing — run again unpacked —, [2] a
- *   key-only query needed the target's low bits — run again with KAD_ROUTE_KEYS off). `packed` is a mask:
+ *   all_to_all back, the unpack of batch i into out_idx[i] / out_cnt[i] with its counters folded into flags and zeroed
+ *   (kad_route_unpack_packed_fold; 4 device words: [0] a block overflowed — grow cap and run again —, [1] a row
+ *   escaped packing — run again unpacked —, [2] a key-only query needed the target's low bits — run again with
+ *   KAD_ROUTE_KEYS off —, [3] the largest block capacity a batch needed). Every set's ctr must be zero on entry (a new
+ *   zeroed buffer, or a previous kad_route_run's) and is left zero. `packed` is a mask:
  *   KAD_ROUTE_PACKED (rows back packed), KAD_ROUTE_KEYS (with it, count 8 on tables with short window lines: the
  *   targets travel as 8-byte keys, kad_route_pack_keys + kad_rt_closest_keys_packed; send / recv then hold world *
  *   cap keys; a table without short lines sets flags[2]).
@@ -537,8 +555,6 @@ int kad_route_fold_flags(const uint32_t* ctr, uint32_t world, uint32_t* flags, i
  *   i+1's all_to_all under batch i's finish and batch i+2's shard kernel). overflow: the sticky word of
  *   kad_rt_home_finish. */
 #define KAD_COMM_ID_BYTES 128u
-#define KAD_ROUTE_PACKED 1u
-#define KAD_ROUTE_KEYS 2u
 typedef struct kad_comm kad_comm;
 typedef struct kad_route_set {
     uint8_t* send;

@@ -150,6 +150,10 @@ SIGNATURES = {
     "kad_route_fold_flags": (C.c_int, [_P, C.c_uint32, _P, C.c_int, _P]),
     "kad_route_pack_keys": (C.c_int, [_P, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, _P, _P, _P, C.c_int, _P]),
     "kad_rt_closest_keys_packed": (C.c_int, [_P, _P, C.c_uint32, C.c_uint32, _P, _P, _P, _P]),
+    "kad_route_pack_ex": (C.c_int, [_P, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, _P, _P, _P, C.c_uint32, C.c_int,
+                                    _P]),
+    "kad_route_unpack_packed_fold": (C.c_int, [_P, C.c_uint32, C.c_uint32, _P, _P, _P, _P, C.c_uint32, _P, C.c_int,
+                                               _P]),
     "kad_comm_unique_id": (C.c_int, [_P]),
     "kad_comm_create": (C.c_int, [C.POINTER(_P), C.c_int, C.c_uint32, C.c_uint32, _P]),
     "kad_comm_destroy": (C.c_int, [_P]),
@@ -203,7 +207,7 @@ class table_info(C.Structure):
 
 
 KAD_COMM_ID_BYTES = 128
-KAD_ROUTE_PACKED, KAD_ROUTE_KEYS = 1, 2
+KAD_ROUTE_PACKED, KAD_ROUTE_KEYS, KAD_ROUTE_ZEROED = 1, 2, 4
 
 
 class route_set(C.Structure):

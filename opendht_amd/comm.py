@@ -100,7 +100,8 @@ class NativeRoute:
 
         self._sets = sets(False)
         self._sets_keys = sets(True) if self.keys else None
-        self.acc = torch.zeros((3,), dtype=torch.int32, device=device)
+        # [overflow, escape, tail, capacity needed], folded by every batch's unpack (kad_route_unpack_packed_fold)
+        self.acc = torch.zeros((4,), dtype=torch.int32, device=device)
 
     def run(self, table, batches, outs, stream=None, packed: bool | None = None, keys: bool | None = None):
         """Route batches[i] ((q, 20) device targets) and unpack its rows into outs[i] = (out_idx, out_cnt); the
@@ -124,16 +125,15 @@ class NativeRoute:
         group); cleared."""
         from .sharded import combine_max
 
-        ov, esc, tail = combine_max(self.acc, group, self.world > 1)
+        ov, esc, tail, need = combine_max(self.acc, group, self.world > 1)
         self.acc.zero_()
+        self.need = need
         return bool(ov), bool(esc) and self.packed, bool(tail) and self.keys
 
     def grown(self, group=None) -> "NativeRoute":
-        from .sharded import need_of
-
-        n = max(need_of(r.ctr, self.world) for r in self.sets)
-        if self.world > 1:
-            n = self.sets[0].need(group, local=n)
+        """Larger blocks: from the largest capacity a batch of the last run needed (flags(), combined over the ranks
+        already; the counters themselves are zeroed by every unpack)."""
+        n = getattr(self, "need", 0)
         cap = min(self.sets[0].cap_max, max(2 * self.cap, n * 5 // 4))
         return NativeRoute(self.q, self.count, self.world, self.shard_bits, self.dev, cap=cap, n_sets=self.n_sets,
                            packed=self.packed, comm=self.comm, keys=self.keys)

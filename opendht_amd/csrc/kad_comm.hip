@@ -282,19 +282,22 @@ int kad_route_run(kad_comm* c, const kad_table* t, uint32_t n_batches, const uin
         KAD_TRY(a2a(c, S.rows, S.back_rows, 4ull * cap * count, xs));
         return a2a(c, S.cnt, S.back_cnt, cap, xs);
     };
+    // the unpack folds the set's counters into flags and zeroes them, so that its next pack needs no memset
     auto unpack = [&](uint32_t i) -> int {
         const kad_route_set& S = sets[i % n_sets];
-        if (packed) KAD_TRY(kad_route_unpack_packed(S.slot, q, count, S.back_prow, out_idx[i], out_cnt[i], info.device, cs));
-        else KAD_TRY(kad_route_unpack(S.slot, q, count, S.back_rows, S.back_cnt, out_idx[i], out_cnt[i], info.device, cs));
-        return kad_route_fold_flags(S.ctr, world, flags, info.device, cs);
+        if (packed)
+            return kad_route_unpack_packed_fold(S.slot, q, count, S.back_prow, out_idx[i], out_cnt[i], S.ctr, world, flags,
+                                                info.device, cs);
+        KAD_TRY(kad_route_unpack(S.slot, q, count, S.back_rows, S.back_cnt, out_idx[i], out_cnt[i], info.device, cs));
+        return kad_route_unpack_packed_fold(S.slot, 0, count, nullptr, nullptr, nullptr, S.ctr, world, flags, info.device,
+                                            cs);
     };
+    const uint32_t pmode = (keys ? KAD_ROUTE_KEYS : 0u) | KAD_ROUTE_ZEROED;
     if (!pipe) {  // one set: every batch in order on the caller's stream
         const kad_route_set& S = sets[0];
         for (uint32_t i = 0; i < n_batches; i++) {
-            KAD_TRY(keys ? kad_route_pack_keys(targets[i], q, world, shard_bits, cap, reinterpret_cast<uint64_t*>(S.send),
-                                               S.slot, S.ctr, info.device, caller)
-                         : kad_route_pack(targets[i], q, world, shard_bits, cap, S.send, S.slot, S.ctr, info.device,
-                                          caller));
+            KAD_TRY(kad_route_pack_ex(targets[i], q, world, shard_bits, cap, S.send, S.slot, S.ctr, pmode, info.device,
+                                      caller));
             if (c) KAD_TRY(a2a(c, S.send, S.recv, rec * cap, caller));
             KAD_TRY(answer(S));
             KAD_TRY(back(S));
@@ -307,9 +310,7 @@ int kad_route_run(kad_comm* c, const kad_table* t, uint32_t n_batches, const uin
     KAD_TRY_HIP(order(c, caller, xs));
     auto pack = [&](uint32_t i) -> int {
         const kad_route_set& S = sets[i % n_sets];
-        KAD_TRY(keys ? kad_route_pack_keys(targets[i], q, world, shard_bits, cap, reinterpret_cast<uint64_t*>(S.send),
-                                           S.slot, S.ctr, info.device, cs)
-                     : kad_route_pack(targets[i], q, world, shard_bits, cap, S.send, S.slot, S.ctr, info.device, cs));
+        KAD_TRY(kad_route_pack_ex(targets[i], q, world, shard_bits, cap, S.send, S.slot, S.ctr, pmode, info.device, cs));
         KAD_TRY_HIP(order(c, cs, xs));
         return a2a(c, S.send, S.recv, rec * cap, xs);
     };

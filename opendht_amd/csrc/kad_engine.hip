@@ -3872,21 +3872,33 @@ __device__ __forceinline__ const uint32_t* gather_ctr(const GatherCtx& G, uint32
     return G.recv + (size_t)r * G.block + G.ctr_off;
 }
 
-__device__ __forceinline__ void gather_scatter(const GatherCtx& G, uint64_t t, uint32_t* __restrict__ out_idx,
-                                               uint8_t* __restrict__ out_cnt, uint32_t* __restrict__ overflow) {
-    const uint32_t lpr = scatter_lpr(G.count), sub = (uint32_t)(t % lpr);
-    const uint64_t g = t / lpr, per = (uint64_t)KAD_SHARD_REGIONS * G.row_cap;
-    const uint32_t r = (uint32_t)(g / per);
+// The complete rows of (rank r, region g) = pair p, by the spb workgroups of that pair: each reads the region's count
+// once and strides over its rows only, instead of one thread per row CAPACITY (a launch sized for the worst case, most
+// of whose workgroups found nothing to copy: 8.4 us for ~131k rows at N = 8).
+__device__ __forceinline__ void gather_scatter_pair(const GatherCtx& G, uint32_t b, uint32_t spb,
+                                                    uint32_t* __restrict__ out_idx, uint8_t* __restrict__ out_cnt,
+                                                    uint32_t* __restrict__ overflow) {
+    const uint32_t lpr = scatter_lpr(G.count), p = b / spb, j = b % spb;
+    const uint32_t r = p / KAD_SHARD_REGIONS, region = p % KAD_SHARD_REGIONS;
     if (r >= G.world) return;
-    const uint32_t rem = (uint32_t)(g % per), region = rem / G.row_cap, k = rem % G.row_cap;
     const uint32_t* ctr = gather_ctr(G, r);
-    if (rem == 0 && sub == 0 && ctr[KAD_SHARD_COUNTER_STRIDE * 9u] && overflow) atomicOr(overflow, 1u);
-    if (k >= min(ctr[KAD_SHARD_COUNTER_STRIDE * region], G.row_cap)) return;
-    const uint32_t* src = G.recv + (size_t)r * G.block + ((size_t)region * G.row_cap + k) * G.rs;
-    const uint32_t qid = src[0] - G.qbase;
-    if (qid >= G.q) return;  // (tombstones too: NONE - qbase >= q)
-    if (out_cnt && sub == 0) out_cnt[qid] = (uint8_t)src[1];
-    copy_row(src, out_idx + (size_t)qid * G.count, G.count, sub, lpr);
+    if (region == 0 && j == 0 && threadIdx.x == 0 && ctr[KAD_SHARD_COUNTER_STRIDE * 9u] && overflow) atomicOr(overflow, 1u);
+    const uint32_t n = min(ctr[KAD_SHARD_COUNTER_STRIDE * region], G.row_cap), rpb = BLOCK / lpr;
+    const uint32_t sub = threadIdx.x % lpr;
+    const uint32_t* base = G.recv + (size_t)r * G.block + (size_t)region * G.row_cap * G.rs;
+    for (uint32_t k = j * rpb + threadIdx.x / lpr; k < n; k += spb * rpb) {
+        const uint32_t* src = base + (size_t)k * G.rs;
+        const uint32_t qid = src[0] - G.qbase;
+        if (qid >= G.q) continue;  // (tombstones too: NONE - qbase >= q)
+        if (out_cnt && sub == 0) out_cnt[qid] = (uint8_t)src[1];
+        copy_row(src, out_idx + (size_t)qid * G.count, G.count, sub, lpr);
+    }
+}
+
+// Workgroups per (rank, region) pair of gather_scatter_pair: about two rows per thread at a full region.
+inline uint32_t scatter_spb(uint32_t row_cap, uint32_t count) {
+    const uint64_t threads = (uint64_t)row_cap * scatter_lpr(count);
+    return (uint32_t)std::min<uint64_t>(1024, std::max<uint64_t>(1, (threads + 2 * BLOCK - 1) / (2 * BLOCK)));
 }
 
 // The counters of `n` send blocks (block_words apart, the counters at ctr_off) zeroed before a step.
@@ -3906,14 +3918,14 @@ __device__ __forceinline__ const uint32_t* gather_part(const GatherCtx& G, uint6
 
 // One launch for the two independent passes of a finish: blocks [0, sblocks) scatter the complete rows, the others
 // link each part into its query's chain (the merge that walks the chains is the next launch).
-__global__ __launch_bounds__(BLOCK) void gather_scatter_link_kernel(GatherCtx G, uint32_t sblocks,
+__global__ __launch_bounds__(BLOCK) void gather_scatter_link_kernel(GatherCtx G, uint32_t sblocks, uint32_t spb,
                                                                     uint32_t* __restrict__ out_idx,
                                                                     uint8_t* __restrict__ out_cnt,
                                                                     uint32_t* __restrict__ overflow,
                                                                     uint32_t* __restrict__ head,
                                                                     uint32_t* __restrict__ next) {
     if (blockIdx.x < sblocks) {  // block-uniform
-        gather_scatter(G, (uint64_t)blockIdx.x * BLOCK + threadIdx.x, out_idx, out_cnt, overflow);
+        gather_scatter_pair(G, blockIdx.x, spb, out_idx, out_cnt, overflow);
         return;
     }
     const uint64_t x = (uint64_t)(blockIdx.x - sblocks) * BLOCK + threadIdx.x;
@@ -4012,26 +4024,27 @@ __device__ void wave_merge_chain(const GatherCtx& G, const uint32_t* __restrict_
 }
 
 // The chain heads (the first part of each query's chain) merge their query's parts (wave_merge_chain) and reset the
-// head.
-__global__ void gather_merge_kernel(GatherCtx G, uint32_t* __restrict__ head, const uint32_t* __restrict__ next,
-                                    uint32_t* __restrict__ out_idx, uint8_t* __restrict__ out_cnt, uint32_t mblocks,
-                                    uint32_t* __restrict__ zsend) {
+// head. One WAVE per part slot (wave-uniform x): the chains merge side by side, each a few dependent memory round
+// trips, instead of a wave walking the ~64 chain heads of its 64 slots one after another (8.5 us at N = 8 for a
+// few thousand parts; profiles/r06/merge/).
+constexpr uint32_t MERGE_WPB = BLOCK / 64;  // part slots per workgroup
+__global__ __launch_bounds__(BLOCK) void gather_merge_kernel(GatherCtx G, uint32_t* __restrict__ head,
+                                                             const uint32_t* __restrict__ next,
+                                                             uint32_t* __restrict__ out_idx,
+                                                             uint8_t* __restrict__ out_cnt, uint32_t mblocks,
+                                                             uint32_t* __restrict__ zsend) {
     if (blockIdx.x >= mblocks) {  // kad_rt_home_finish_reset: the send blocks' counters for the next step
         const uint32_t j = (blockIdx.x - mblocks) * BLOCK + threadIdx.x, words = KAD_SHARD_COUNTERS * KAD_SHARD_COUNTER_STRIDE;
         if (j < G.world * words) zsend[(uint64_t)(j / words) * G.block + G.ctr_off + j % words] = 0;
         return;
     }
-    const uint64_t x = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    const uint64_t x = (uint64_t)blockIdx.x * MERGE_WPB + (threadIdx.x >> 6);  // wave-uniform
     const uint32_t* part = gather_part(G, x);
-    const uint32_t qid = part ? part[0] - G.qbase : NONE;
-    const bool mine = part && qid < G.q && head[qid] == (uint32_t)x;
-    // the wave merges its chain heads one at a time, all 64 lanes on each (parts are rare: queries whose window
-    // crosses a shard edge)
-    for (uint64_t mm = __ballot(mine); mm; mm &= mm - 1) {
-        const uint32_t l = (uint32_t)__builtin_ctzll(mm);
-        wave_merge_chain(G, next, rdl((uint32_t)x, l), rdl(qid, l), out_idx, out_cnt);
-    }
-    if (mine) head[qid] = NONE;
+    if (!part) return;
+    const uint32_t qid = part[0] - G.qbase;
+    if (qid >= G.q || head[qid] != (uint32_t)x) return;  // (parts are rare: queries whose window crosses a shard edge)
+    wave_merge_chain(G, next, (uint32_t)x, qid, out_idx, out_cnt);
+    if ((threadIdx.x & 63u) == 0) head[qid] = NONE;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -9164,14 +9177,14 @@ static int gather_finish(const uint32_t* recv, uint32_t world, uint32_t row_cap,
     uint32_t* next = scratch + head_words;  // the same offset for every rank of a step: one scratch can serve them all
     DeviceGuard g(device);
     hipStream_t s = (hipStream_t)stream;
-    const uint64_t nrows = (uint64_t)world * KAD_SHARD_REGIONS * row_cap, nparts = (uint64_t)world * part_cap;
-    if (nrows * scatter_lpr(count) > 0xFFFFFFFFull * BLOCK || nparts >= 0xFFFFFFFFull)
-        return set_err(KAD_ERR_INVALID, "buffers too large");
-    const uint32_t sb = grid_for(nrows * scatter_lpr(count)), lb = grid_for(nparts);
+    const uint64_t nparts = (uint64_t)world * part_cap;
+    if (nparts >= 0xFFFFFFFFull) return set_err(KAD_ERR_INVALID, "buffers too large");
+    const uint32_t spb = scatter_spb(row_cap, count), sb = world * KAD_SHARD_REGIONS * spb, lb = grid_for(nparts);
     if ((uint64_t)sb + lb > 0x7FFFFFFFull) return set_err(KAD_ERR_INVALID, "buffers too large");
-    hipLaunchKernelGGL(gather_scatter_link_kernel, dim3(sb + lb), dim3(BLOCK), 0, s, G, sb, out_idx, out_cnt, overflow,
-                       head, next);
-    const uint32_t mb = grid_for(nparts), zb = zsend ? grid_for((uint64_t)world * KAD_SHARD_COUNTERS * KAD_SHARD_COUNTER_STRIDE) : 0u;
+    hipLaunchKernelGGL(gather_scatter_link_kernel, dim3(sb + lb), dim3(BLOCK), 0, s, G, sb, spb, out_idx, out_cnt,
+                       overflow, head, next);
+    const uint32_t mb = (uint32_t)((nparts + MERGE_WPB - 1) / MERGE_WPB),
+                   zb = zsend ? grid_for((uint64_t)world * KAD_SHARD_COUNTERS * KAD_SHARD_COUNTER_STRIDE) : 0u;
     hipLaunchKernelGGL(gather_merge_kernel, dim3(mb + zb), dim3(BLOCK), 0, s, G, head, next, out_idx, out_cnt, mb, zsend);
     HIP_TRY(hipGetLastError());
     return KAD_OK;

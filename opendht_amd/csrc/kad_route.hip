@@ -14,6 +14,7 @@
 // The blocks travel with all_to_all_single (RCCL over xGMI), equal splits: opendht_amd/sharded.py OwnerRoute.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 
 #include "../../include/kadgpu.h"
@@ -156,12 +157,38 @@ __global__ __launch_bounds__(BLOCK) void route_compress_kernel(const uint32_t* _
     }
 }
 
+// kad_route_unpack_packed_fold: the batch's counters folded into the caller's flags and zeroed for the next
+// kad_route_pack_ex(KAD_ROUTE_ZEROED), by workgroup 0 of the unpack (which runs after the pack, the answer and the
+// compress that write them): flags[0..2] |= the overflow / escape / tail words, flags[3] = max(flags[3], KAD_ROUTE_SUBS
+// x the fullest sub-block count). No memset before the next pack, no fold launch after this one.
+struct RouteFold {
+    uint32_t* ctr;  // NULL: no fold
+    uint32_t world;
+    uint32_t* flags;
+};
+
+__device__ void fold_reset(const RouteFold& F) {
+    __shared__ uint32_t mx;
+    const uint32_t tid = threadIdx.x, nsub = F.world * KAD_ROUTE_SUBS, ov = KAD_ROUTE_OVERFLOW_WORD(F.world);
+    if (tid == 0) mx = 0;
+    __syncthreads();
+    uint32_t m = 0;
+    for (uint32_t j = tid; j < nsub; j += BLOCK) m = max(m, F.ctr[j * KAD_ROUTE_CSTRIDE]);
+    if (m) atomicMax(&mx, m);
+    const uint32_t w = tid < 3 ? F.ctr[ov + tid] : 0u;
+    __syncthreads();
+    if (tid < 3 && w) F.flags[tid] |= w;
+    if (tid == 0) F.flags[3] = max(F.flags[3], KAD_ROUTE_SUBS * mx);
+    for (uint32_t j = tid; j < KAD_ROUTE_CTR_WORDS(F.world); j += BLOCK) F.ctr[j] = 0;  // (every read is done)
+}
+
 // One thread per query: its packed row (slot[i]) expanded into out_idx row i and out_cnt[i].
 __global__ __launch_bounds__(BLOCK) void route_unpack_packed_kernel(const uint32_t* __restrict__ slot, uint32_t q,
                                                                     uint32_t count,
                                                                     const uint32_t* __restrict__ back_packed,
                                                                     uint32_t* __restrict__ out_idx,
-                                                                    uint8_t* __restrict__ out_cnt) {
+                                                                    uint8_t* __restrict__ out_cnt, RouteFold F) {
+    if (F.ctr && blockIdx.x == 0) fold_reset(F);
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (i >= q) return;
     const uint32_t p = slot[i], W = KAD_ROUTE_PACKED_WORDS(count);
@@ -237,7 +264,8 @@ __global__ __launch_bounds__(BLOCK) void route_unpack_packed4_kernel(const uint3
                                                                      uint32_t count,
                                                                      const uint32_t* __restrict__ back_packed,
                                                                      uint32_t* __restrict__ out_idx,
-                                                                     uint8_t* __restrict__ out_cnt) {
+                                                                     uint8_t* __restrict__ out_cnt, RouteFold F) {
+    if (F.ctr && blockIdx.x == 0) fold_reset(F);
     const uint64_t t = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
     const uint64_t i = t / G;
     const uint32_t j = (uint32_t)(t % G), L = count / 4;
@@ -280,8 +308,8 @@ struct DevSwitch {
 
 }  // namespace
 
-static int route_pack(bool keys, const uint8_t* targets, uint32_t q, uint32_t world, uint32_t shard_bits, uint32_t cap,
-                      uint8_t* send, uint32_t* slot, uint32_t* ctr, int device, void* stream) {
+static int route_pack(bool keys, bool zeroed, const uint8_t* targets, uint32_t q, uint32_t world, uint32_t shard_bits,
+                      uint32_t cap, uint8_t* send, uint32_t* slot, uint32_t* ctr, int device, void* stream) {
     using kadgpu_internal::set_error;
     if (world == 0 || world > KAD_ROUTE_MAX_WORLD) return set_error(KAD_ERR_INVALID, "world must be 1..16");
     if (shard_bits > 8) return set_error(KAD_ERR_INVALID, "shard_bits must be 0..8");
@@ -293,7 +321,7 @@ static int route_pack(bool keys, const uint8_t* targets, uint32_t q, uint32_t wo
         return set_error(KAD_ERR_INVALID, "targets, send, slot and ctr must be 4-byte aligned");
     DevSwitch g(device);
     hipStream_t s = (hipStream_t)stream;
-    hipError_t e = hipMemsetAsync(ctr, 0, 4ull * KAD_ROUTE_CTR_WORDS(world), s);
+    hipError_t e = zeroed ? hipSuccess : hipMemsetAsync(ctr, 0, 4ull * KAD_ROUTE_CTR_WORDS(world), s);
     if (e == hipSuccess && q) {
         const uint32_t nb = (uint32_t)(((uint64_t)q + BLOCK * QPT - 1) / (BLOCK * QPT));
         if (keys)
@@ -310,15 +338,24 @@ static int route_pack(bool keys, const uint8_t* targets, uint32_t q, uint32_t wo
 
 extern "C" int kad_route_pack(const uint8_t* targets, uint32_t q, uint32_t world, uint32_t shard_bits, uint32_t cap,
                               uint8_t* send, uint32_t* slot, uint32_t* ctr, int device, void* stream) {
-    return route_pack(false, targets, q, world, shard_bits, cap, send, slot, ctr, device, stream);
+    return route_pack(false, false, targets, q, world, shard_bits, cap, send, slot, ctr, device, stream);
+}
+
+extern "C" int kad_route_pack_ex(const uint8_t* targets, uint32_t q, uint32_t world, uint32_t shard_bits, uint32_t cap,
+                                 void* send, uint32_t* slot, uint32_t* ctr, uint32_t mode, int device, void* stream) {
+    if (mode & ~(KAD_ROUTE_KEYS | KAD_ROUTE_ZEROED)) return kadgpu_internal::set_error(KAD_ERR_INVALID, "unknown mode bits");
+    if ((mode & KAD_ROUTE_KEYS) && ((uintptr_t)send & 7u))
+        return kadgpu_internal::set_error(KAD_ERR_INVALID, "send keys must be 8-byte aligned");
+    return route_pack(mode & KAD_ROUTE_KEYS, mode & KAD_ROUTE_ZEROED, targets, q, world, shard_bits, cap,
+                      reinterpret_cast<uint8_t*>(send), slot, ctr, device, stream);
 }
 
 extern "C" int kad_route_pack_keys(const uint8_t* targets, uint32_t q, uint32_t world, uint32_t shard_bits,
                                    uint32_t cap, uint64_t* send_keys, uint32_t* slot, uint32_t* ctr, int device,
                                    void* stream) {
     if ((uintptr_t)send_keys & 7u) return kadgpu_internal::set_error(KAD_ERR_INVALID, "send_keys must be 8-byte aligned");
-    return route_pack(true, targets, q, world, shard_bits, cap, reinterpret_cast<uint8_t*>(send_keys), slot, ctr, device,
-                      stream);
+    return route_pack(true, false, targets, q, world, shard_bits, cap, reinterpret_cast<uint8_t*>(send_keys), slot, ctr,
+                      device, stream);
 }
 
 extern "C" int kad_route_unpack(const uint32_t* slot, uint32_t q, uint32_t count, const uint32_t* back_idx,
@@ -367,26 +404,39 @@ extern "C" int kad_route_compress(const uint32_t* idx, const uint8_t* cnt, uint3
     return KAD_OK;
 }
 
-extern "C" int kad_route_unpack_packed(const uint32_t* slot, uint32_t q, uint32_t count, const uint32_t* back_packed,
-                                       uint32_t* out_idx, uint8_t* out_cnt, int device, void* stream) {
+static int unpack_packed(const uint32_t* slot, uint32_t q, uint32_t count, const uint32_t* back_packed,
+                         uint32_t* out_idx, uint8_t* out_cnt, RouteFold F, int device, void* stream) {
     using kadgpu_internal::set_error;
     if (count == 0 || count > KAD_ROUTE_PACKED_MAX_COUNT) return set_error(KAD_ERR_INVALID, "count must be 1..32");
-    if (q == 0) return KAD_OK;
-    if (!slot || !back_packed || !out_idx || !out_cnt) return set_error(KAD_ERR_INVALID, "NULL buffer");
+    if (q == 0 && !F.ctr) return KAD_OK;
+    if (q && (!slot || !back_packed || !out_idx || !out_cnt)) return set_error(KAD_ERR_INVALID, "NULL buffer");
     DevSwitch g(device);
     hipStream_t s = (hipStream_t)stream;
     if (count % 4 == 0 && (uintptr_t)out_idx % 16 == 0) {
         const uint32_t L = count / 4, G = L <= 1 ? 1u : L <= 2 ? 2u : L <= 4 ? 4u : 8u;
-        const dim3 grid((uint32_t)(((uint64_t)q * G + BLOCK - 1) / BLOCK));
-        if (G == 1) hipLaunchKernelGGL(route_unpack_packed4_kernel<1>, grid, dim3(BLOCK), 0, s, slot, q, count, back_packed, out_idx, out_cnt);
-        else if (G == 2) hipLaunchKernelGGL(route_unpack_packed4_kernel<2>, grid, dim3(BLOCK), 0, s, slot, q, count, back_packed, out_idx, out_cnt);
-        else if (G == 4) hipLaunchKernelGGL(route_unpack_packed4_kernel<4>, grid, dim3(BLOCK), 0, s, slot, q, count, back_packed, out_idx, out_cnt);
-        else hipLaunchKernelGGL(route_unpack_packed4_kernel<8>, grid, dim3(BLOCK), 0, s, slot, q, count, back_packed, out_idx, out_cnt);
+        const dim3 grid((uint32_t)std::max<uint64_t>(1, ((uint64_t)q * G + BLOCK - 1) / BLOCK));
+        if (G == 1) hipLaunchKernelGGL(route_unpack_packed4_kernel<1>, grid, dim3(BLOCK), 0, s, slot, q, count, back_packed, out_idx, out_cnt, F);
+        else if (G == 2) hipLaunchKernelGGL(route_unpack_packed4_kernel<2>, grid, dim3(BLOCK), 0, s, slot, q, count, back_packed, out_idx, out_cnt, F);
+        else if (G == 4) hipLaunchKernelGGL(route_unpack_packed4_kernel<4>, grid, dim3(BLOCK), 0, s, slot, q, count, back_packed, out_idx, out_cnt, F);
+        else hipLaunchKernelGGL(route_unpack_packed4_kernel<8>, grid, dim3(BLOCK), 0, s, slot, q, count, back_packed, out_idx, out_cnt, F);
     } else {
-        hipLaunchKernelGGL(route_unpack_packed_kernel, dim3((q + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, slot, q, count,
-                           back_packed, out_idx, out_cnt);
+        hipLaunchKernelGGL(route_unpack_packed_kernel, dim3(std::max<uint32_t>(1, (q + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0,
+                           s, slot, q, count, back_packed, out_idx, out_cnt, F);
     }
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return set_error(KAD_ERR_HIP, hipGetErrorString(e));
     return KAD_OK;
+}
+
+extern "C" int kad_route_unpack_packed(const uint32_t* slot, uint32_t q, uint32_t count, const uint32_t* back_packed,
+                                       uint32_t* out_idx, uint8_t* out_cnt, int device, void* stream) {
+    return unpack_packed(slot, q, count, back_packed, out_idx, out_cnt, RouteFold{nullptr, 0, nullptr}, device, stream);
+}
+
+extern "C" int kad_route_unpack_packed_fold(const uint32_t* slot, uint32_t q, uint32_t count,
+                                            const uint32_t* back_packed, uint32_t* out_idx, uint8_t* out_cnt,
+                                            uint32_t* ctr, uint32_t world, uint32_t* flags, int device, void* stream) {
+    if (!ctr || !flags) return kadgpu_internal::set_error(KAD_ERR_INVALID, "NULL ctr or flags");
+    if (world == 0 || world > KAD_ROUTE_MAX_WORLD) return kadgpu_internal::set_error(KAD_ERR_INVALID, "world must be 1..16");
+    return unpack_packed(slot, q, count, back_packed, out_idx, out_cnt, RouteFold{ctr, world, flags}, device, stream);
 }

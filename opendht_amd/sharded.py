@@ -647,9 +647,11 @@ def serve_owner(table, targets, count: int, route: OwnerRoute | None = None, gro
             import torch as _t
 
             s = stream if stream is not None else _t.cuda.current_stream(targets.device).cuda_stream
-            if route.tailed(group):  # a key-only answer needed the low bits: the batch again from full targets
+            route.last_tailed = route.tailed(group)
+            if route.last_tailed:  # a key-only answer needed the low bits: the batch again from full targets
                 route.step(table, targets, out_idx, out_cnt, group, stream, keys=False)
-            if route.escaped(group):  # a row too wide to pack: this batch's rows go back unpacked
+            route.last_escaped = route.escaped(group)
+            if route.last_escaped:  # a row too wide to pack: this batch's rows go back unpacked
                 if route.keys:  # (the received keys cannot answer unpacked: the full targets travel)
                     route.pack(targets, s, keys=False)
                     route.send_targets(group, s, keys=False)

@@ -74,7 +74,7 @@ def test_route_pack_layout(gpu):
     sub-block, flags a full one."""
     q, world, bits = 5000, 4, 2
     t = torch.randint(0, 256, (q, 20), dtype=torch.uint8, device=gpu)
-    R = OwnerRoute(q, 8, world, bits, gpu, cap=8 * 1024)
+    R = OwnerRoute(q, 8, world, bits, gpu, cap=8 * 1024, keys=False)
     s = torch.cuda.current_stream(gpu).cuda_stream
     R.pack(t, s)
     torch.cuda.synchronize()
@@ -90,6 +90,16 @@ def test_route_pack_layout(gpu):
     assert int(subs[:, 5:].sum()) == 0  # (5,000 targets: workgroups 0..4)
     assert np.unique(slot).size == q
     np.testing.assert_array_equal(R.send[torch.from_numpy(slot).to(gpu)].cpu().numpy(), t.cpu().numpy())
+    # kad_route_pack_keys: the same places, each record the target's top 64 bits as one native key
+    RK = OwnerRoute(q, 8, world, bits, gpu, cap=8 * 1024, keys=True)
+    RK.pack(t, s)
+    torch.cuda.synchronize()
+    kslot = RK.slot.cpu().numpy().view(np.uint32).astype(np.int64)  # (the order inside a sub-block is unspecified)
+    np.testing.assert_array_equal(kslot // cap, owner.cpu().numpy())
+    assert np.unique(kslot).size == q
+    want = t.cpu().numpy()[:, :8].copy().view(">u8").reshape(-1)
+    got = RK.send_keys[torch.from_numpy(kslot).to(gpu)].cpu().numpy().view(np.uint64)
+    np.testing.assert_array_equal(got, want)
     R2 = OwnerRoute(q, 8, world, bits, gpu, cap=8 * 100)
     R2.pack(t, s)
     torch.cuda.synchronize()
@@ -146,9 +156,9 @@ def test_owner_route_fused_packed_rows(gpu, good_pct):
         oi, oc, R = serve_owner(T, tg, 8, route=R)
         torch.cuda.synchronize()
         if good_pct == 2:
-            assert R.escaped(combine=False) and not R.fused  # could not pack them: answered again unpacked
+            assert R.last_escaped and not R.fused  # could not pack them: answered again unpacked
         else:
-            assert R.fused and not R.escaped(combine=False)  # the kernel wrote the packed rows
+            assert R.fused and not R.last_escaped  # the kernel wrote the packed rows
         want, wcnt = O.flat_rt_closest(gids, gst, gfirst, goff, targets, 8, nthreads=8)
         np.testing.assert_array_equal(oc.cpu().numpy(), wcnt)
         np.testing.assert_array_equal(oi.cpu().numpy().view(np.uint32), want)
