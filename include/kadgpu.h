@@ -185,7 +185,9 @@ int kad_table_refresh_status(kad_table* t, int64_t now_ns, void* stream);
 /* Counters of the small refresh since the table was created (synchronises the device):
  *   spin_timeouts     builder blocks of a fused general-line refresh that waited RF_SPIN_TICKS (1 s) for the
  *                     line list block 0 publishes and gave up (block 0 not running: the GPU busy with other
- *                     work); their lines were then built by the launch's last block, so results stay exact
+ *                     work); their lines were then built by the launch's last block, so results stay exact. After
+ *                     the first timeout the table stops fusing those builds (they go out as stream-ordered
+ *                     launches after the node kernel), so the wait cannot recur
  *   last_block_lines  lines built by a fused launch's last block (windows of more than 64 nodes, and the lists
  *                     of timed-out builders)
  *   guard_errors      bounds guards of the kernel that fired (bit mask; the host validates every inline

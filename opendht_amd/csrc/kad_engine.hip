@@ -7319,6 +7319,12 @@ struct kad_table {
     Deadlines dl;                   // isGood(now) deadlines (kad_table_refresh_status)
     uint32_t* rf_ctr = nullptr;     // small refresh (rf_nodes_kernel): counters, appended buckets, NodeCache ranges
     uint32_t rf_epoch = 0;          // the last fused refresh's list epoch (rf_ctr[RF_GO])
+    // FUSE 2's builder blocks spin for block 0's list; when other work holds the CUs that spin can time out (a
+    // latency cliff of up to RF_SPIN_TICKS). rf_spin_host: pinned mirror of rf_ctr[RF_SPIN],
+    // copied after every fused general-line refresh and read by the next one; once non-zero the table never fuses
+    // the general-line builds again (rf_no_fuse2: they go out as stream-ordered launches after the node kernel).
+    uint32_t* rf_spin_host = nullptr;
+    bool rf_no_fuse2 = false;
     uint32_t* rf_blist = nullptr;
     uint32_t* rf_nrange = nullptr;
     hipStream_t ss[2] = {nullptr, nullptr};  // side streams of an incremental rebuild (side_streams)
@@ -7343,6 +7349,7 @@ struct kad_table {
         for (void* p : {(void*)bdirty, (void*)ld8, (void*)ld16, (void*)ld32, (void*)ndirty, (void*)dlist, (void*)dctr, stage,
                         (void*)rf_ctr, (void*)rf_blist, (void*)rf_nrange})
             if (p) (void)hipFree(p);
+        if (rf_spin_host) (void)hipHostFree(rf_spin_host);
     }
 };
 
@@ -7762,10 +7769,15 @@ int rf_ready(kad_table* t) {
     if (e == hipSuccess) e = hipMalloc(&bl, RF_CAP * sizeof(uint32_t));
     if (e == hipSuccess) e = hipMalloc(&nr, 2 * RF_CAP * sizeof(uint32_t));
     if (e == hipSuccess) e = hipMemset(c, 0, RF_CTRS * sizeof(uint32_t));
+    void* sh = nullptr;
+    if (e == hipSuccess) e = hipHostMalloc(&sh, sizeof(uint32_t), hipHostMallocDefault);
     if (e != hipSuccess) {
         for (void* p : {c, bl, nr}) if (p) (void)hipFree(p);
+        if (sh) (void)hipHostFree(sh);
         return set_err(KAD_ERR_NOMEM, "small refresh buffers: %s", hipGetErrorString(e));
     }
+    *static_cast<uint32_t*>(sh) = 0;
+    t->rf_spin_host = static_cast<uint32_t*>(sh);
     t->rf_ctr = static_cast<uint32_t*>(c);
     t->rf_blist = static_cast<uint32_t*>(bl);
     t->rf_nrange = static_cast<uint32_t*>(nr);
@@ -7932,6 +7944,10 @@ int small_refresh(kad_table* t, hipStream_t s, const uint32_t* mnode, uint32_t m
     // (window-line builders derive the lines of nodes in device lists with one wave: at most 64 of them)
     int fuse = (!B || 6ull * total > RF_FUSE_LINES || t->sl_mut) ? 0 : t->wl_mut ? 1 : t->gl_mut ? 2 : 0;
     if (fuse == 1 && !C.nhb && total > 64) fuse = 0;
+    // (the mirror of an earlier fused refresh's spin-timeout count: a copy that has not landed yet reads as the one
+    // before it, so the demotion can come one refresh late, never wrongly)
+    if (t->rf_spin_host && __atomic_load_n(t->rf_spin_host, __ATOMIC_RELAXED)) t->rf_no_fuse2 = true;
+    if (fuse == 2 && t->rf_no_fuse2) fuse = 0;
     dim3 g1(std::min<uint32_t>((total + BLOCK - 1) / BLOCK, 64u));
     if (fuse) {  // (6 * total <= RF_FUSE_LINES: one block derives every node) + builder blocks, all lines in one round
         C.list[0] = nullptr;
@@ -7960,7 +7976,10 @@ int small_refresh(kad_table* t, hipStream_t s, const uint32_t* mnode, uint32_t m
     if (const char* e = std::getenv("KAD_RF_ABL")) C.abl = (uint32_t)std::atoi(e);
 #endif
     if (fuse == 1) hipLaunchKernelGGL((rf_nodes_kernel<true, 1>), g1, dim3(BLOCK), 0, s, C);
-    else if (fuse == 2) hipLaunchKernelGGL((rf_nodes_kernel<true, 2>), g1, dim3(BLOCK), 0, s, C);
+    else if (fuse == 2) {
+        hipLaunchKernelGGL((rf_nodes_kernel<true, 2>), g1, dim3(BLOCK), 0, s, C);
+        HIP_TRY(hipMemcpyAsync(t->rf_spin_host, t->rf_ctr + RF_SPIN, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    }
     else if (single) hipLaunchKernelGGL((rf_nodes_kernel<true, 0>), g1, dim3(BLOCK), 0, s, C);
     else hipLaunchKernelGGL((rf_nodes_kernel<false, 0>), g1, dim3(BLOCK), 0, s, C);
     HIP_TRY(hipGetLastError());

@@ -207,24 +207,38 @@ __device__ uint32_t peer_closest(const SwarmDev& W, uint32_t p, const Tgt& t, ui
     for (uint32_t s = 0; s < K; s++) { L0[s] = ~0ull; LI[s] = NONE; }
     uint32_t nl = 0;
     static_assert(BK == 8, "a level's slots are two 16-byte index loads and four 16-byte key loads");
-    for (uint32_t P = lo; P <= hi; P++) {
-        const uint32_t d = level(P), nb = cp[d];
-        // the level's 8 slots in one round of 16-byte loads (the slots from nb on are padding, skipped)
+    // a level's 8 slots in one round of 16-byte loads (the slots from its count on are padding, skipped); the next
+    // window bucket's slots are loaded before the current one's are ranked, so the window costs one round trip, not
+    // one per bucket
+    struct Slots {
+        uint32_t i[BK];
+        uint64_t k[BK];
+        uint32_t nb;
+    };
+    auto load_level = [&](uint32_t P, Slots& S) {
+        const uint32_t d = level(P);
+        S.nb = cp[d];
         const uint4* ep4 = reinterpret_cast<const uint4*>(W.ent + ((size_t)p * L + d) * BK);
         const uint4* kp4 = reinterpret_cast<const uint4*>(W.ekey + ((size_t)p * L + d) * BK);
-        uint32_t ei[BK];
-        uint64_t ek[BK];
 #pragma unroll
         for (int x = 0; x < 2; x++) {
             const uint4 u = ep4[x];
-            ei[4 * x] = u.x; ei[4 * x + 1] = u.y; ei[4 * x + 2] = u.z; ei[4 * x + 3] = u.w;
+            S.i[4 * x] = u.x; S.i[4 * x + 1] = u.y; S.i[4 * x + 2] = u.z; S.i[4 * x + 3] = u.w;
         }
 #pragma unroll
         for (int x = 0; x < 4; x++) {
             const uint4 u = kp4[x];
-            ek[2 * x] = ((uint64_t)u.y << 32) | u.x;
-            ek[2 * x + 1] = ((uint64_t)u.w << 32) | u.z;
+            S.k[2 * x] = ((uint64_t)u.y << 32) | u.x;
+            S.k[2 * x + 1] = ((uint64_t)u.w << 32) | u.z;
         }
+    };
+    Slots cur, nxt;
+    load_level(lo, cur);
+    for (uint32_t P = lo; P <= hi; P++) {
+        if (P < hi) load_level(P + 1, nxt);
+        const uint32_t nb = cur.nb;
+        const uint32_t* ei = cur.i;
+        const uint64_t* ek = cur.k;
 #pragma unroll 1
         for (uint32_t j = 0; j < nb; j++) {
             uint64_t cd = ek[0];
@@ -248,9 +262,11 @@ __device__ uint32_t peer_closest(const SwarmDev& W, uint32_t p, const Tgt& t, ui
             }
             nl = min(nl + 1, K);
         }
+        if (P < hi) cur = nxt;
     }
     const uint32_t m = min(nl, count);
-    for (uint32_t s = 0; s < m; s++) {
+#pragma unroll
+    for (uint32_t s = 0; s < K; s++) {  // (every slot, statically: entries from m on are padding)
         oi[s] = LI[s];
         ok[s] = L0[s] ^ t.hi;
     }
@@ -332,13 +348,14 @@ __device__ __forceinline__ void select_next(const SearchDev& X, uint32_t s, uint
     if (!pick) X.done[s] = 2;
 }
 
-// the list's flag bytes (queried or bad) of search s as a bit mask, and back (entries from n on: 0)
-__device__ __forceinline__ uint32_t load_flags(const uint8_t* f, uint32_t s) {
+// the list's flag bytes (queried or bad) of search s as a bit mask, and back (entries from n on: 0); only the 16-byte
+// pieces holding entries below n are read (a list is ~14-17 entries: one piece of two)
+__device__ __forceinline__ uint32_t load_flags(const uint8_t* f, uint32_t s, uint32_t n = LST) {
     const uint4* p = reinterpret_cast<const uint4*>(f + (size_t)s * LST);
     uint32_t m = 0;
 #pragma unroll
     for (int x = 0; x < (int)LST / 16; x++) {
-        const uint4 u = p[x];
+        const uint4 u = 16u * x < n ? p[x] : make_uint4(0, 0, 0, 0);
         const uint32_t w[4] = {u.x, u.y, u.z, u.w};
 #pragma unroll
         for (int y = 0; y < 4; y++)
@@ -347,11 +364,13 @@ __device__ __forceinline__ uint32_t load_flags(const uint8_t* f, uint32_t s) {
     }
     return m;
 }
-__device__ __forceinline__ void store_flags(uint8_t* f, uint32_t s, uint32_t m, uint32_t n) {
+// w: the pieces to write are those below max(n, the previous length): the ones above hold zeros already
+__device__ __forceinline__ void store_flags(uint8_t* f, uint32_t s, uint32_t m, uint32_t n, uint32_t w = LST) {
     m &= lo_mask(n);
     uint4* p = reinterpret_cast<uint4*>(f + (size_t)s * LST);
 #pragma unroll
     for (int x = 0; x < (int)LST / 16; x++) {
+        if (16u * x >= w) continue;
         uint32_t w[4];
 #pragma unroll
         for (int y = 0; y < 4; y++) {
@@ -395,9 +414,18 @@ __global__ __launch_bounds__(BLOCK) void search_query_kernel(SwarmDev W, SearchD
     uint64_t ok[BK];
     const bool up = v < W.n && !swarm_offline(v, X.offline);
     const uint32_t m = up ? peer_closest<BK>(W, v, load_tgt(X.targets, s), BK, oi, ok) : 0u;
-    for (uint32_t j = 0; j < m; j++) {
-        X.ri[(size_t)g * BK + j] = oi[j];
-        X.rk[(size_t)g * BK + j] = ok[j];
+    // the answers as whole 16-byte pieces (entries from m on are never read: the merge reads rn of them)
+    if (m) {
+        uint4* pi = reinterpret_cast<uint4*>(X.ri + (size_t)g * BK);
+        uint4* pk = reinterpret_cast<uint4*>(X.rk + (size_t)g * BK);
+#pragma unroll
+        for (uint32_t x = 0; x < BK / 4; x++)
+            if (4 * x < m) pi[x] = make_uint4(oi[4 * x], oi[4 * x + 1], oi[4 * x + 2], oi[4 * x + 3]);
+#pragma unroll
+        for (uint32_t x = 0; x < BK / 2; x++)
+            if (2 * x < m)
+                pk[x] = make_uint4((uint32_t)ok[2 * x], (uint32_t)(ok[2 * x] >> 32), (uint32_t)ok[2 * x + 1],
+                                   (uint32_t)(ok[2 * x + 1] >> 32));
     }
     X.rn[g] = (uint8_t)m;
 }
@@ -476,8 +504,33 @@ __device__ __forceinline__ void search_insert(const SwarmDev& W, const Tgt& t, u
     }
 }
 
+// One queried node's answers (<= BK peer indices and keys), loaded as whole 16-byte pieces (predicated on its count)
+struct Answers {
+    uint32_t r[BK];
+    uint64_t k[BK];
+};
+__device__ __forceinline__ void load_answers(const SearchDev& X, uint32_t g, uint32_t rn, Answers& A) {
+    const uint4* pi = reinterpret_cast<const uint4*>(X.ri + (size_t)g * BK);
+    const uint4* pk = reinterpret_cast<const uint4*>(X.rk + (size_t)g * BK);
+#pragma unroll
+    for (uint32_t x = 0; x < BK / 4; x++) {
+        const uint4 u = 4 * x < rn ? pi[x] : make_uint4(NONE, NONE, NONE, NONE);
+        A.r[4 * x] = u.x; A.r[4 * x + 1] = u.y; A.r[4 * x + 2] = u.z; A.r[4 * x + 3] = u.w;
+    }
+#pragma unroll
+    for (uint32_t x = 0; x < BK / 2; x++) {
+        const uint4 u = 2 * x < rn ? pk[x] : make_uint4(0, 0, 0, 0);
+        A.k[2 * x] = ((uint64_t)u.y << 32) | u.x;
+        A.k[2 * x + 1] = ((uint64_t)u.w << 32) | u.z;
+    }
+}
+
 // one lane per search: Search::insertNode of every answer in the order of the queried nodes, then the
-// offline queried nodes turn bad (expired), then the isSynced / expired checks and the next hop's selection
+// offline queried nodes turn bad (expired), then the isSynced / expired checks and the next hop's selection.
+// Memory: the list, its flags and the answers are read as 16-byte pieces below their lengths only, all of them before
+// the inserts (the next queried node's answers in flight while the current one's are inserted), and the list is
+// written back below max(new, old length): the round-5 form read every answer by a dependent 4 + 8-byte load inside
+// the insert loop (32 round trips per lookup) and moved whole 32-entry lists.
 __global__ __launch_bounds__(BLOCK) void search_merge_kernel(SwarmDev W, SearchDev X) {
     const uint32_t s = blockIdx.x * BLOCK + threadIdx.x;
     bool running = false;
@@ -485,37 +538,49 @@ __global__ __launch_bounds__(BLOCK) void search_merge_kernel(SwarmDev W, SearchD
         const Tgt t = load_tgt(X.targets, s);
         uint32_t li[LST];
         uint64_t ld[LST];  // top-64 XOR distances
-        uint32_t n = X.ln[s];
+        const uint32_t n0 = X.ln[s];
+        uint32_t n = n0;
+        const uint32_t rn4 = *reinterpret_cast<const uint32_t*>(X.rn + (size_t)s * ALPHA);  // (ALPHA = 4 counts)
+        Answers A[2];
+        load_answers(X, s * ALPHA, rn4 & 255u, A[0]);
         {
             const uint4* pi = reinterpret_cast<const uint4*>(X.li + (size_t)s * LST);
             const uint4* pk = reinterpret_cast<const uint4*>(X.lk + (size_t)s * LST);
 #pragma unroll
             for (uint32_t x = 0; x < LST / 4; x++) {
-                const uint4 u = pi[x];
+                const uint4 u = 4 * x < n0 ? pi[x] : make_uint4(NONE, NONE, NONE, NONE);
                 li[4 * x] = u.x; li[4 * x + 1] = u.y; li[4 * x + 2] = u.z; li[4 * x + 3] = u.w;
             }
 #pragma unroll
             for (uint32_t x = 0; x < LST / 2; x++) {
-                const uint4 u = pk[x];
+                const uint4 u = 2 * x < n0 ? pk[x] : make_uint4(~0u, ~0u, ~0u, ~0u);
                 ld[2 * x] = (((uint64_t)u.y << 32) | u.x) ^ t.hi;
                 ld[2 * x + 1] = (((uint64_t)u.w << 32) | u.z) ^ t.hi;
             }
         }
-        uint32_t qm = load_flags(X.lq, s), bm = load_flags(X.lb, s);
+        uint32_t qm = load_flags(X.lq, s, n0), bm = load_flags(X.lb, s, n0);
         const uint32_t src = X.src[s];
         bool ovf = false;
         const uint32_t* xo = X.xo + (size_t)s * XO_CAP;
         uint32_t xn = X.xn[s];
+#pragma unroll
         for (uint32_t a = 0; a < ALPHA; a++) {
-            const uint32_t g = s * ALPHA + a;
-            const uint32_t rn = X.rn[g];
+            if (a + 1 < ALPHA) load_answers(X, s * ALPHA + a + 1, (rn4 >> (8 * (a + 1))) & 255u, A[(a + 1) & 1]);
+            const Answers& C = A[a & 1];
+            const uint32_t rn = (rn4 >> (8 * a)) & 255u;
             for (uint32_t j = 0; j < rn; j++) {
-                const uint32_t r = X.ri[(size_t)g * BK + j];
+                uint32_t r = C.r[0];
+                uint64_t rk = C.k[0];
+#pragma unroll
+                for (uint32_t x = 1; x < BK; x++) {  // (a select chain: the answers stay in registers)
+                    r = j == x ? C.r[x] : r;
+                    rk = j == x ? C.k[x] : rk;
+                }
                 if (r == src) continue;  // deserializeNodes drops our own ID (network_engine.cpp:798-799)
                 bool rbad = false;
                 if (swarm_offline(r, X.offline))
                     for (uint32_t e = 0; e < xn && !rbad; e++) rbad = xo[e] == r;
-                search_insert(W, t, li, ld, qm, bm, n, r, X.rk[(size_t)g * BK + j] ^ t.hi, rbad, ovf);
+                search_insert(W, t, li, ld, qm, bm, n, r, rk ^ t.hi, rbad, ovf);
             }
         }
         const uint4 sv = reinterpret_cast<const uint4*>(X.sel)[s];
@@ -547,21 +612,24 @@ __global__ __launch_bounds__(BLOCK) void search_merge_kernel(SwarmDev W, SearchD
         else if (n > 0 && cb >= min(n, MAX_BAD)) X.done[s] = 3;
         else select_next(X, s, n, qm, bm, li);
         X.ln[s] = (uint8_t)n;
+        const uint32_t wn = max(n, n0);  // pieces above it hold the padding already
         {
             uint4* pi = reinterpret_cast<uint4*>(X.li + (size_t)s * LST);
             uint4* pk = reinterpret_cast<uint4*>(X.lk + (size_t)s * LST);
 #pragma unroll
             for (uint32_t x = 0; x < LST / 4; x++)
-                pi[x] = make_uint4(4 * x < n ? li[4 * x] : NONE, 4 * x + 1 < n ? li[4 * x + 1] : NONE,
-                                   4 * x + 2 < n ? li[4 * x + 2] : NONE, 4 * x + 3 < n ? li[4 * x + 3] : NONE);
+                if (4 * x < wn)
+                    pi[x] = make_uint4(4 * x < n ? li[4 * x] : NONE, 4 * x + 1 < n ? li[4 * x + 1] : NONE,
+                                       4 * x + 2 < n ? li[4 * x + 2] : NONE, 4 * x + 3 < n ? li[4 * x + 3] : NONE);
 #pragma unroll
             for (uint32_t x = 0; x < LST / 2; x++) {
+                if (2 * x >= wn) continue;
                 const uint64_t k0 = 2 * x < n ? ld[2 * x] ^ t.hi : ~0ull, k1 = 2 * x + 1 < n ? ld[2 * x + 1] ^ t.hi : ~0ull;
                 pk[x] = make_uint4((uint32_t)k0, (uint32_t)(k0 >> 32), (uint32_t)k1, (uint32_t)(k1 >> 32));
             }
         }
-        store_flags(X.lq, s, qm, n);
-        store_flags(X.lb, s, bm, n);
+        store_flags(X.lq, s, qm, n, wn);
+        store_flags(X.lb, s, bm, n, wn);
         if (ovf) atomicAdd(X.overflow, 1u);
         running = !X.done[s];
     }

@@ -48,6 +48,19 @@ def run(t, runs, slot_lines, expect_timeouts):
         assert d["guard_errors"] == 0, d
         if expect_timeouts:
             assert d["spin_timeouts"] > 0 and d["last_block_lines"] > 0, d
+            # after a timeout the table no longer fuses its general-line builds: the same delay
+            # again spins nowhere (the count stays), and the rows are still exact
+            os.environ["KAD_RF_ABL"] = "3"
+            now2 = now1 + 10**4
+            T.refresh_status(now2)
+            torch.cuda.synchronize()
+            os.environ.pop("KAD_RF_ABL")
+            st2 = R.status_at(time_ns, reply_ns, expired, now2)
+            np.testing.assert_array_equal(T.export_status(), st2)
+            R.compare_fresh(DeviceTable, _lib, T, t, st2, f"{t['name']} delayed block 0, demoted", slot_lines=slot_lines)
+            d2 = T.refresh_diag()
+            print(t["name"], "after demotion", d2, flush=True)
+            assert d2["spin_timeouts"] == d["spin_timeouts"] and d2["guard_errors"] == 0, (d, d2)
         else:
             assert d["spin_timeouts"] == 0, d
 
