@@ -42,14 +42,23 @@ __global__ __launch_bounds__(BLOCK) void route_pack_kernel(const uint8_t* __rest
     __syncthreads();
     uint32_t w[QPT][5], dst[QPT], pos[QPT];
     const uint64_t base = (uint64_t)blockIdx.x * BLOCK * QPT;
+    // every target's loads first (QPT x 5 in flight per lane): the LDS atomics below would otherwise order each
+    // round's loads after the previous round's placement, QPT dependent memory round trips per workgroup
+    // (only the words the record carries: the top 8 bytes for a key)
 #pragma unroll
     for (uint32_t r = 0; r < QPT; r++) {
         const uint64_t i = base + r * BLOCK + tid;  // consecutive lanes, consecutive 20-byte records
-        dst[r] = NONE;
         if (i < q) {
             const uint32_t* p = reinterpret_cast<const uint32_t*>(targets + 20 * i);
 #pragma unroll
-            for (int x = 0; x < 5; x++) w[r][x] = __builtin_nontemporal_load(p + x);
+            for (int x = 0; x < (KEYS ? 2 : 5); x++) w[r][x] = __builtin_nontemporal_load(p + x);
+        }
+    }
+#pragma unroll
+    for (uint32_t r = 0; r < QPT; r++) {
+        const uint64_t i = base + r * BLOCK + tid;
+        dst[r] = NONE;
+        if (i < q) {
             const uint32_t b0 = w[r][0] & 0xFFu;  // InfoHash byte 0: the most significant
             dst[r] = shard_bits ? (b0 >> (8 - shard_bits)) % world : 0u;
         }

@@ -43,7 +43,11 @@ def med(fn):
 
 
 for n in (2, 4, 8):
-    R = OwnerRoute(Q, 8, n, 3, dev, collective=False)
+    RK = OwnerRoute(Q, 8, n, 3, dev, collective=False, keys=True)
+    res[f"pack_keys_n{n}_us"] = med(lambda r: RK.pack(tgs[r % NB], s))
+    assert not RK.overflowed(combine=False)
+    del RK
+    R = OwnerRoute(Q, 8, n, 3, dev, collective=False, keys=False)
     res[f"pack_n{n}_us"] = med(lambda r: R.pack(tgs[r % NB], s))
     assert not R.overflowed(combine=False)
 R.rows.random_(0, 1 << 20)
