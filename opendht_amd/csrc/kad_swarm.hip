@@ -26,6 +26,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstdarg>
 #include <cstdint>
 #include <cstdio>
@@ -531,6 +532,10 @@ __device__ __forceinline__ void load_answers(const SearchDev& X, uint32_t g, uin
 // the inserts (the next queried node's answers in flight while the current one's are inserted), and the list is
 // written back below max(new, old length): the round-5 form read every answer by a dependent 4 + 8-byte load inside
 // the insert loop (32 round trips per lookup) and moved whole 32-entry lists.
+// FUSED (search_hop_kernel): the hop in one lane per lookup — each queried node's findClosestNodes(t, 8) computed in
+// place (peer_closest, the query kernel's code) and inserted at once, so the answers never go through HBM (the split
+// form writes and reads 4 x 96 bytes per lookup and hop) and the hop is one launch.
+template <bool FUSED>
 __global__ __launch_bounds__(BLOCK) void search_merge_kernel(SwarmDev W, SearchDev X) {
     const uint32_t s = blockIdx.x * BLOCK + threadIdx.x;
     bool running = false;
@@ -540,9 +545,11 @@ __global__ __launch_bounds__(BLOCK) void search_merge_kernel(SwarmDev W, SearchD
         uint64_t ld[LST];  // top-64 XOR distances
         const uint32_t n0 = X.ln[s];
         uint32_t n = n0;
-        const uint32_t rn4 = *reinterpret_cast<const uint32_t*>(X.rn + (size_t)s * ALPHA);  // (ALPHA = 4 counts)
+        const uint4 sv = reinterpret_cast<const uint4*>(X.sel)[s];
+        const uint32_t sel[ALPHA] = {sv.x, sv.y, sv.z, sv.w};
+        const uint32_t rn4 = FUSED ? 0u : *reinterpret_cast<const uint32_t*>(X.rn + (size_t)s * ALPHA);  // (ALPHA = 4)
         Answers A[2];
-        load_answers(X, s * ALPHA, rn4 & 255u, A[0]);
+        if (!FUSED) load_answers(X, s * ALPHA, rn4 & 255u, A[0]);
         {
             const uint4* pi = reinterpret_cast<const uint4*>(X.li + (size_t)s * LST);
             const uint4* pk = reinterpret_cast<const uint4*>(X.lk + (size_t)s * LST);
@@ -565,9 +572,16 @@ __global__ __launch_bounds__(BLOCK) void search_merge_kernel(SwarmDev W, SearchD
         uint32_t xn = X.xn[s];
 #pragma unroll
         for (uint32_t a = 0; a < ALPHA; a++) {
-            if (a + 1 < ALPHA) load_answers(X, s * ALPHA + a + 1, (rn4 >> (8 * (a + 1))) & 255u, A[(a + 1) & 1]);
+            uint32_t rn;
+            if (FUSED) {
+                const uint32_t v = sel[a];
+                const bool up = v < W.n && !swarm_offline(v, X.offline);
+                rn = up ? peer_closest<BK>(W, v, t, BK, A[a & 1].r, A[a & 1].k) : 0u;
+            } else {
+                if (a + 1 < ALPHA) load_answers(X, s * ALPHA + a + 1, (rn4 >> (8 * (a + 1))) & 255u, A[(a + 1) & 1]);
+                rn = (rn4 >> (8 * a)) & 255u;
+            }
             const Answers& C = A[a & 1];
-            const uint32_t rn = (rn4 >> (8 * a)) & 255u;
             for (uint32_t j = 0; j < rn; j++) {
                 uint32_t r = C.r[0];
                 uint64_t rk = C.k[0];
@@ -583,8 +597,6 @@ __global__ __launch_bounds__(BLOCK) void search_merge_kernel(SwarmDev W, SearchD
                 search_insert(W, t, li, ld, qm, bm, n, r, rk ^ t.hi, rbad, ovf);
             }
         }
-        const uint4 sv = reinterpret_cast<const uint4*>(X.sel)[s];
-        const uint32_t sel[ALPHA] = {sv.x, sv.y, sv.z, sv.w};
 #pragma unroll
         for (uint32_t a = 0; a < ALPHA; a++) {  // the silent ones: expired after their tries -> bad
             const uint32_t v = sel[a];
@@ -834,8 +846,17 @@ int kad_search_hop(kad_search* x, uint32_t* n_active) {
     const SearchDev& X = x->X;
     SW_TRY(hipMemsetAsync(X.active, 0, 4, x->stream));
     if (X.S) {
-        hipLaunchKernelGGL(search_query_kernel, dim3(grid_for((uint64_t)X.S * ALPHA)), dim3(BLOCK), 0, x->stream, x->sw->W, X);
-        hipLaunchKernelGGL(search_merge_kernel, dim3(grid_for(X.S)), dim3(BLOCK), 0, x->stream, x->sw->W, X);
+        // the two-kernel hop (query kernel, answers through HBM, merge kernel). KAD_SWARM_FUSED=1 (tools): the fused
+        // kernel, measured slower — 48-50 against 73 M lookups/s at 10M peers (profiles/r06/swarm_fused/): the peer
+        // walks run on a quarter of the lanes, behind the merge's registers, with their round trips no longer hidden
+        static const bool split = std::getenv("KAD_SWARM_FUSED") == nullptr;
+        if (split) {
+            hipLaunchKernelGGL(search_query_kernel, dim3(grid_for((uint64_t)X.S * ALPHA)), dim3(BLOCK), 0, x->stream,
+                               x->sw->W, X);
+            hipLaunchKernelGGL(search_merge_kernel<false>, dim3(grid_for(X.S)), dim3(BLOCK), 0, x->stream, x->sw->W, X);
+        } else {
+            hipLaunchKernelGGL(search_merge_kernel<true>, dim3(grid_for(X.S)), dim3(BLOCK), 0, x->stream, x->sw->W, X);
+        }
     }
     SW_TRY(hipGetLastError());
     if (n_active) {
