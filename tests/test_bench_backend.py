@@ -86,3 +86,59 @@ def test_owner_shard_bits_refuses_mismatch(world, n_shards):
 
     with pytest.raises(ValueError):
         owner_shard_bits(world, ShardSpec(n_shards=n_shards) if n_shards & (n_shards - 1) == 0 else None)
+
+
+def _verify_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import numpy as np
+    import torch.distributed as dist
+
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "oracle")]
+    import oracle as O
+    from opendht_amd import synth as S
+    from opendht_amd.sharded import ShardSpec, build_shard
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        b = _bench(False)
+        spec = ShardSpec(n_shards=world, depth=8, mean_per_bucket=6.0, seed=0xA11 + 3, good_pct=70, expired_pct=15)
+        sh = build_shard(spec, rank)
+        gids, gst, goff = spec.bucket_range(0, spec.n_buckets)
+        gfirst = S.bucket_firsts(spec.depth, 0, spec.n_buckets)
+        tg = S.random_targets(600, seed=50 + rank)  # targets of both shards: half answered by the other rank
+        want, wcnt = O.flat_rt_closest(gids, gst, gfirst, goff, tg, 8)
+        idx = torch.from_numpy(want.view(np.int32).copy())
+        cnt = torch.from_numpy(wcnt.copy())
+        good = b.verify_routed(dist, sh, spec, rank, world, torch.from_numpy(tg), idx, cnt, 8)
+        # rank 1 corrupts one returned row whose target rank 0 owns: rank 0 must be the one to catch it
+        if rank == 1:
+            j = int(np.flatnonzero((tg[:, 0] >> 7) == 0)[0])
+            idx[j, 0] = idx[j, 0] + 1
+        bad = b.verify_routed(dist, sh, spec, rank, world, torch.from_numpy(tg), idx, cnt, 8)
+        q.put((rank, good, bad))
+    except Exception as e:  # reported through the queue
+        q.put((rank, {"error": repr(e)}, None))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_verify_routed_checks_rows_answered_elsewhere():
+    """bench.verify_routed: every rank's returned rows are all-gathered and each is checked by the rank
+    owning its target, so a wrong row that came back from another rank is counted. Two gloo ranks on the CPU, rows
+    from the oracle on the whole table, then one row of a rank-0 target corrupted on rank 1."""
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_verify_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    got = {r: (g, b) for r, g, b in (q.get(timeout=180) for _ in ps)}
+    for p in ps:
+        p.join(timeout=60)
+    for r in (0, 1):
+        g, b = got[r]
+        assert "error" not in g, g
+        assert g["rows"] == 1200 and g["mismatches"] == 0 and g["rows_answered_by_another_rank"] > 0, g
+        assert b["mismatches"] == 1, b
