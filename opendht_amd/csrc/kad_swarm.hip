@@ -443,18 +443,24 @@ constexpr uint32_t XO_CAP = 64;  // silent peers remembered per lookup (4 per ho
 __device__ __forceinline__ void search_insert(const SwarmDev& W, const Tgt& t, uint32_t (&li)[LST], uint64_t (&ld)[LST],
                                               uint32_t& qm, uint32_t& bm, uint32_t& n, uint32_t r, uint64_t rd, bool rbad,
                                               bool& ovf) {
-    bool found = false;
-    uint32_t pos = 0, tie = 0;
+    bool found = false, anyeq = false;
+    uint32_t pos = 0;
 #pragma unroll
     for (uint32_t k = 0; k < LST; k++) {
         if (k < n) {
             found |= li[k] == r;
             pos += ld[k] < rd;
-            tie |= (ld[k] == rd && li[k] != r ? 1u : 0u) << k;
+            anyeq |= ld[k] == rd;
         }
     }
     if (found) return;
-    while (tie) {  // equal top 64 bits (rare): the full 160-bit order (a select chain keeps the index static)
+    uint32_t tie = 0;
+    if (anyeq) {  // equal top 64 bits (rare): which entries, for the full 160-bit order below
+#pragma unroll
+        for (uint32_t k = 0; k < LST; k++)
+            if (k < n) tie |= (ld[k] == rd && li[k] != r ? 1u : 0u) << k;
+    }
+    while (tie) {  // the full 160-bit order (a select chain keeps the index static)
         const uint32_t k = (uint32_t)__builtin_ctz(tie);
         tie &= tie - 1u;
         uint32_t lk = 0;
@@ -495,13 +501,15 @@ __device__ __forceinline__ void search_insert(const SwarmDev& W, const Tgt& t, u
     bm = (bm & low) | ((bm & ~low) << 1) | (rbad ? bit : 0u);
     n++;
     bad += rbad ? 1u : 0u;
-    // while more than SEARCH_NODES non-bad nodes: drop the last one
+    // while more than SEARCH_NODES non-bad nodes: drop the last one (dropping from the end stops right after the
+    // (SN + 1)-th non-bad entry goes: the list ends just before it, the bad entries ahead of it kept). In closed form
+    // from the masks instead of a 32-step loop over the entries (~190 of the insert's ~600 VALU instructions)
+    if (n - bad > SN) {
+        uint32_t good = ~bm & lo_mask(n);
 #pragma unroll
-    for (int k = (int)LST - 1; k >= 0; k--) {
-        if ((uint32_t)k == n - 1 && n - bad > SN) {
-            bad -= (bm >> k) & 1u;
-            n--;
-        }
+        for (uint32_t k = 0; k < SN; k++) good &= good - 1u;  // drop the first SN non-bad entries
+        n = (uint32_t)__builtin_ctz(good);                    // (non-empty: n - bad > SN)
+        bad = (uint32_t)__builtin_popcount(bm & lo_mask(n));
     }
 }
 

@@ -13,6 +13,10 @@ import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+if os.environ.get("KADGPU_LIB"):  # (an A/B against another engine build, e.g. tools/gpu_swarm_ab.sh)
+    from opendht_amd import _lib  # noqa: E402
+
+    _lib.use_library(os.environ["KADGPU_LIB"])
 from opendht_amd import synth as S  # noqa: E402
 from opendht_amd.swarm import Swarm  # noqa: E402
 
