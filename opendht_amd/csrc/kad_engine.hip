@@ -4717,6 +4717,13 @@ constexpr uint32_t NCL_STRIDE = KAD_NCL_STRIDE, NCL_SLOTS = NCL_STRIDE - 4, NCL_
 constexpr uint32_t NCL_PIECES = NCL_STRIDE / 4;  // 16-byte pieces of a line
 constexpr int NCL_NV = (int)NCL_SLOTS + 4;        // a lane's slot array (the slots, then NONE)
 static_assert(NCL_STRIDE % 16 == 0 && NCL_STRIDE <= 64 && NCL_LEFT + NCL_XMAX < NCL_SLOTS, "NodeCache line");
+// The 128-byte line of slot s (after all the 256-byte lines: dword NCL_STRIDE * nslots + NCL2_DWORDS * s), the 37-node
+// window centred on the slot, read first (ncl2_build_line).
+constexpr uint32_t NCL2_DWORDS = 32, NCL2_SLOTS = 37, NCL2_MID = 18, NCL2_XMAX = 15, NCL2_PMIN = NCL2_MID - NCL2_XMAX / 2,
+                   NCL2_PMAX = NCL2_MID + (NCL2_XMAX + 1) / 2;
+// counts up to 14 (SEARCH_NODES) read the 128-byte line and send its misses to the wave path; 15 and 16 walk past
+// its 37 nodes for 1.6 % of the queries (k = 16) and read the 256-byte line instead
+constexpr uint32_t NCL2_COUNT_MAX = 14;
 
 // The answer from the lane's line (Lq: its 16 pieces, loaded by the wave): the node indices go to lrow[0..m) (the
 // lane's LDS row) by emission rank.
@@ -4811,6 +4818,96 @@ __device__ __forceinline__ bool ncl_answer(const uint4 (&Lq)[16], uint32_t index
     return !ex;
 }
 
+// The answer from the lane's 128-byte line (Lq: its 8 pieces; layout at ncl2_build_line). The line's 37 nodes sit
+// around the middle of the slot, so lb lies at window position p in [11, 26]: nodes before 11 are below every target of
+// the slot, nodes from 26 on above it, and p = 11 + the nodes of positions 11..25 below the target. The window is
+// shifted right by 26 - p (lb at 26; the left run 25..0 holds all p window nodes left of lb, then NONE; the right run
+// 26.. the 37 - p others), then walked as ncl_answer walks the 256-byte line.
+__device__ __forceinline__ bool ncl2_answer(const uint4 (&Lq)[8], uint32_t index_base, const Target& t,
+                                            uint32_t count, uint32_t* lrow, uint32_t& m) {
+    constexpr int S = (int)NCL2_SLOTS, PMIN = (int)NCL2_PMIN, PMAX = (int)NCL2_PMAX, NV = S + PMAX - PMIN;
+    uint32_t d[32], v[NV];
+#pragma unroll
+    for (int x = 0; x < 8; x++) {
+        d[4 * x] = Lq[x].x; d[4 * x + 1] = Lq[x].y; d[4 * x + 2] = Lq[x].z; d[4 * x + 3] = Lq[x].w;
+    }
+    const uint32_t w0 = d[0], sh = (d[1] >> 8) & 63u, fl = d[1] >> 16;
+    const uint32_t tx = ((uint32_t)(t.hi >> sh) & 0xFFFFFFu) << 8;
+    bool ex = fl & 1u;
+    uint32_t p = PMIN;
+#pragma unroll
+    for (int e = 0; e < S; e++) {  // key24 of node w0 + e at byte 16 + 3e, its expired bit at bit e of dw2..3
+        const int o = 3 * e, w = 4 + o / 4, b = 8 * (o % 4);
+        const uint32_t k = b <= 8 ? d[w] >> b : __builtin_amdgcn_alignbit(d[w + 1], d[w], (uint32_t)b);
+        const uint32_t val = (k << 8) | ((d[2 + e / 32] >> (e % 32)) & 1u);
+        if (e >= PMIN && e < PMAX) {  // the slot's nodes and their neighbours: key24 < t24 iff val < t24 << 8
+            ex |= (val ^ tx) < 256u;
+            p += val < tx ? 1u : 0u;
+        }
+        v[e] = val ^ tx;
+    }
+#pragma unroll
+    for (int e = S; e < NV; e++) v[e] = NONE;
+    const uint32_t s = (uint32_t)PMAX - p;  // 0..15
+    {
+        uint32_t u[NV];
+#pragma unroll
+        for (int j = 0; j < NV; j++) u[j] = (s & 1u) ? (j >= 1 ? v[j - 1] : NONE) : v[j];
+#pragma unroll
+        for (int j = 0; j < NV; j++) v[j] = (s & 2u) ? (j >= 2 ? u[j - 2] : NONE) : u[j];
+#pragma unroll
+        for (int j = 0; j < NV; j++) u[j] = (s & 4u) ? (j >= 4 ? v[j - 4] : NONE) : v[j];
+#pragma unroll
+        for (int j = 0; j < NV; j++) v[j] = (s & 8u) ? (j >= 8 ? u[j - 8] : NONE) : u[j];
+    }
+    ex |= (v[PMAX - 1] >> 8) == (v[PMAX] >> 8);  // equal key24 either side of lb (ncl_answer)
+    uint32_t run = 0, endL = NONE, endR = NONE;
+#pragma unroll
+    for (int j = PMAX - 1; j >= 0; j--) {
+        const bool in = (uint32_t)j >= s;
+        run = max(run, in ? v[j] & ~255u : 0u);
+        v[j] = in ? run | ((uint32_t)(PMAX - 1 - j) << 1) | (v[j] & 1u) : NONE;
+        if (j <= PMAX - PMIN && (uint32_t)j == s) endL = v[j];
+    }
+    if (!(fl & 2u)) endL = NONE;  // the window starts at node 0
+    run = 0;
+#pragma unroll
+    for (int j = PMAX; j < NV; j++) {
+        const bool in = (uint32_t)j < (uint32_t)S + s;
+        run = max(run, in ? v[j] & ~255u : 0u);
+        v[j] = in ? run | 128u | ((uint32_t)(j - PMAX) << 1) | (v[j] & 1u) : NONE;
+        if (j >= S - 1 && (uint32_t)j == (uint32_t)S - 1 + s) endR = v[j];
+    }
+    if (!(fl & 4u)) endR = NONE;  // the window reaches the array end
+    const uint32_t lim = min(endL, endR);
+    uint32_t w[32];
+#pragma unroll
+    for (int r = 0; r < 32; r++) {
+        const uint32_t a = r < PMAX ? v[PMAX - 1 - r] : NONE;
+        const int jr = PMAX + 31 - r;
+        w[r] = min(a, jr < NV ? v[jr] : NONE);
+    }
+#pragma unroll
+    for (int h = 16; h >= 1; h >>= 1)
+#pragma unroll
+        for (int r = 0; r < 32; r++)
+            if ((r & h) == 0) cx(w[r], w[r + h]);
+    const uint32_t lbn = w0 + p + index_base;
+    uint32_t have = 0;
+#pragma unroll
+    for (int r = 0; r < 32; r++) {
+        const bool keep = w[r] <= lim && !(w[r] & 1u);
+        if (keep && have < count) {
+            const uint32_t st = (w[r] >> 1) & 63u;
+            lrow[have] = (w[r] & 128u) ? lbn + st : lbn - 1 - st;
+        }
+        have += keep ? 1u : 0u;
+    }
+    m = min(count, have);
+    ex |= have < count && (lim != NONE || w[31] != NONE);
+    return !ex;
+}
+
 // Wave-level LDS ordering (the rocPRIM wave barrier): the wave's LDS writes before it are seen by its reads after.
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -4883,15 +4980,18 @@ __device__ __forceinline__ void store_rows_wave16(uint32_t* __restrict__ out_idx
     }
 }
 
-// ABL 1 (timing ablation only, KAD_NC_KERNEL=lines_abl1; results wrong): no exact path. ABL 2 (lines_abl2): the
-// line load and the row store only (every word of the line folded into one value), the memory floor.
+// ABL 1 (timing ablation only, KAD_NC_KERNEL=lines_abl1; results wrong): the 256-byte lines alone (round 5's
+// kernel), no exact path. ABL 2 (lines_abl2): the 256-byte line load and the row store only (every word of the line
+// folded into one value), round 5's memory floor. ABL 3 (lines_abl3): the 128-byte lines alone (no second line, no
+// exact path). ABL 5 (lines_stats): the product kernel with out_cnt = the step that answered (1: the 128-byte line,
+// 2: the 256-byte line, 3: the wave path).
 // DUAL: per-query family (af[i] = 0 -> T4, 1 -> T6; NodeCache::getCachedNodes picks cache_4 / cache_6 by
 // sa_family, node_cache.cpp:37); an empty family map (n = 0) gives zero results.
 // The lines are loaded by the wave, not by their lanes: a lane-private 256-byte line is 16 random 16-byte loads,
 // each instruction touching 64 lines (64 address translations), and a 2 GB line table is bound by those
 // translations (tools/nc_abl.py). The wave loads its 64 lines in two halves of 128 bytes, eight lanes per line
 // (one translation per line per instruction), and hands each lane its line through LDS.
-template <int ABL, bool DUAL>
+template <int ABL, bool DUAL, bool HALF>
 __device__ __forceinline__ void nc_line_kernel_body(const DevTable& T4, const DevTable& T6, const uint8_t* __restrict__ af,
                                                         const uint8_t* __restrict__ targets, uint32_t q,
                                                         uint32_t count, uint32_t* __restrict__ out_idx,
@@ -4919,6 +5019,43 @@ __device__ __forceinline__ void nc_line_kernel_body(const DevTable& T4, const De
                 sl = (uint32_t)((t.hi - nbase) >> nshift) | (fam ? 0x80000000u : 0u);
         }
     }
+    uint4 (*S)[8] = stg[tid >> 6];  // this wave's region: only wave-level ordering is needed
+    // the wave's rows (64 x 16 words) reuse its region: row r of the block at rows + ncl_wrow(r)
+    uint32_t* rows = reinterpret_cast<uint32_t*>(&stg[0][0][0]);
+    uint32_t stage = 3;  // ABL 5: which step answered (1: the 128-byte line, 2: the 256-byte line, 3: the wave)
+    if ((ABL == 0 && HALF) || ABL == 3 || ABL == 5 || ABL == 6) {
+        // the 128-byte lines first: round r, lane L loads piece (L & 7) of the line of query 8r + (L >> 3)
+        uint4 ld[8], L2[8];
+#pragma unroll
+        for (int r = 0; r < 8; r++) {
+            const uint32_t so = (uint32_t)__shfl((int)sl, 8 * r + (int)(lane >> 3), 64);
+            uint4 a = make_uint4(0u, 0u, 0u, 0u);
+            if (so != NONE) {
+                const DevTable& T = (DUAL && (so >> 31)) ? T6 : T4;
+                a = T.ncl[(size_t)NCL_PIECES * T.nslots + 8ull * (so & 0x7FFFFFFFu) + (lane & 7)];
+            }
+            ld[r] = a;
+        }
+#pragma unroll
+        for (int r = 0; r < 8; r++) S[8 * r + (lane >> 3)][(lane & 7) ^ ((lane >> 3) & 7)] = ld[r];
+        wave_sync();
+#pragma unroll
+        for (int x = 0; x < 8; x++) L2[x] = S[lane][x ^ (lane & 7)];
+        wave_sync();
+        const uint32_t ib = fam ? T6.index_base : T4.index_base;
+        if (sl != NONE) ok = ncl2_answer(L2, ib, t, count, rows + ncl_wrow(tid), m);
+        if (ok) stage = 1;
+        // the walks that leave the 37-node window (about one query in 150 at k = 14), deferred lines: the 256-byte
+        // line, loaded by its lane
+        if (ABL == 6 && sl != NONE && !ok) {
+            const uint4* lp = (fam ? T6.ncl : T4.ncl) + (size_t)NCL_PIECES * (sl & 0x7FFFFFFFu);
+            uint4 L[16];
+#pragma unroll
+            for (int x = 0; x < 16; x++) L[x] = x < (int)NCL_PIECES ? lp[x] : make_uint4(0u, 0u, 0u, 0u);
+            ok = ncl_answer(L, ib, t, count, rows + ncl_wrow(tid), m);
+            if (ok) stage = 2;
+        }
+    } else {
     // round r: lane L loads pieces (L & 7) and 8 + (L & 7) of the line of query 8r + (L >> 3)
     uint4 ld[16], L[16];
 #pragma unroll
@@ -4933,7 +5070,6 @@ __device__ __forceinline__ void nc_line_kernel_body(const DevTable& T4, const De
         ld[r] = a;
         ld[8 + r] = b;
     }
-    uint4 (*S)[8] = stg[tid >> 6];  // this wave's region: only wave-level ordering is needed
 #pragma unroll
     for (int h = 0; h < 2; h++) {
 #pragma unroll
@@ -4943,8 +5079,6 @@ __device__ __forceinline__ void nc_line_kernel_body(const DevTable& T4, const De
         for (int x = 0; x < 8; x++) L[8 * h + x] = S[lane][x ^ (lane & 7)];
         wave_sync();
     }
-    // the wave's rows (64 x 16 words) reuse its region: row r of the block at rows + NCL_WROWS(r)
-    uint32_t* rows = reinterpret_cast<uint32_t*>(&stg[0][0][0]);
     if (sl != NONE) {
         if (ABL == 2) {
             uint32_t f = 0;
@@ -4957,13 +5091,14 @@ __device__ __forceinline__ void nc_line_kernel_body(const DevTable& T4, const De
             ok = ncl_answer(L, fam ? T6.index_base : T4.index_base, t, count, rows + ncl_wrow(tid), m);
         }
     }
+    }
     if (act && ok && out_cnt) out_cnt[i] = (uint8_t)m;
     rows[(tid >> 6) * 2048u + 1024u + lane] = m | (ok ? 256u : 0u);  // the row's meta word (its wave's region)
     __syncthreads();
     store_rows_wave16(out_idx, q, count, rows);
     // the lanes the lines could not answer: one query at a time by the whole wave (nc_answer: 32-node
     // runs each side of lb, itself falling back to lane 0's serial walk)
-    uint64_t pend = ABL ? 0ull : __ballot(act && !ok);
+    uint64_t pend = (ABL == 0 || ABL == 5 || ABL == 6) ? __ballot(act && !ok) : 0ull;
     const uint64_t fm = DUAL ? __ballot(fam) : 0ull;
     while (pend) {
         const uint32_t l = (uint32_t)__builtin_ctzll(pend);
@@ -4979,13 +5114,14 @@ __device__ __forceinline__ void nc_line_kernel_body(const DevTable& T4, const De
         const NcWindow w = nc_window(T, r0, lane);
         nc_answer(T, u, r0, r1, w, lane, i - lane + l, count, out_idx, out_cnt);
     }
+    if (ABL == 5 && act && out_cnt) out_cnt[i] = (uint8_t)stage;
 }
-template <int ABL, bool DUAL>
+template <int ABL, bool DUAL, bool HALF>
 __global__ __launch_bounds__(BLOCK) void nc_line_kernel(DevTable T4, DevTable T6, const uint8_t* __restrict__ af,
                                                         const uint8_t* __restrict__ targets, uint32_t q,
                                                         uint32_t count, uint32_t* __restrict__ out_idx,
                                                         uint8_t* __restrict__ out_cnt) {
-    nc_line_kernel_body<ABL, DUAL>(T4, T6, af, targets, q, count, out_idx, out_cnt);
+    nc_line_kernel_body<ABL, DUAL, HALF>(T4, T6, af, targets, q, count, out_idx, out_cnt);
 }
 
 // NodeCache counts 17..64 for two families (af per query): nc_two_pass_kernel with the table chosen per
@@ -5011,7 +5147,43 @@ __global__ __launch_bounds__(BLOCK) void nc_two_pass_dual_kernel(DevTable T4, De
         nc64_query(T, t, lane, qi, count, out_idx, out_cnt, true);
 }
 
-// NodeCache lines after a status change (or at creation): one thread per radix slot.
+// The 128-byte line of a slot ([r0, r1) its nodes, ns = r1 - r0 <= 15), the 37 nodes w0 = r0 + ns / 2 - 18 ..:
+//   dw0      w0
+//   dw1      ns | sh << 8 | (defer | truncated left << 1 | truncated right << 2) << 16
+//   dw2..3   the expired bits of the 37 window nodes (node w0 + e at bit e)
+//   bytes 16 + 3e .. 18 + 3e   key24 of node w0 + e (little-endian; key24 as in the 256-byte lines, from the window's
+//            own common prefix)
+// The slot's nodes sit at positions 18 - ns / 2 .. 17 + ns - ns / 2, inside [11, 26). A clamped window or a slot of
+// more than 15 nodes is deferred (the 256-byte line answers).
+__device__ __forceinline__ void ncl2_build_line(const uint64_t* key, const uint8_t* status, uint32_t r0, uint32_t r1,
+                                                uint32_t n, uint32_t slot_prefix, uint4* L2) {
+    const uint32_t ns = r1 - r0, c = r0 + ns / 2;
+    if (ns > NCL2_XMAX || c < NCL2_MID || (uint64_t)c - NCL2_MID + NCL2_SLOTS > n) {
+        L2[0] = make_uint4(0u, 1u << 16, 0u, 0u);
+        return;
+    }
+    const uint32_t w0 = c - NCL2_MID;
+    const uint32_t P = (uint32_t)__builtin_clzll((key[w0] ^ key[w0 + NCL2_SLOTS - 1]) | 1ull);
+    const uint32_t Pp = min(min(P, slot_prefix), 40u), sh = 40 - Pp;
+    uint32_t d[32];
+#pragma unroll
+    for (int x = 0; x < 32; x++) d[x] = 0;
+#pragma unroll
+    for (int e = 0; e < (int)NCL2_SLOTS; e++) {
+        const uint32_t k24 = (uint32_t)(key[w0 + e] >> sh) & 0xFFFFFFu;
+        const int o = 3 * e, w = 4 + o / 4, b = 8 * (o % 4);
+        d[w] |= k24 << b;
+        if (b > 8) d[w + 1] |= k24 >> (32 - b);
+        d[2 + e / 32] |= ((status[w0 + e] & KAD_STATUS_EXPIRED) ? 1u : 0u) << (e % 32);
+    }
+    d[0] = w0;
+    d[1] = ns | (sh << 8) | ((w0 > 0 ? 2u : 0u) | (w0 + NCL2_SLOTS < n ? 4u : 0u)) << 16;
+#pragma unroll
+    for (int x = 0; x < 8; x++) L2[x] = make_uint4(d[4 * x], d[4 * x + 1], d[4 * x + 2], d[4 * x + 3]);
+}
+
+// NodeCache lines after a status change (or at creation): one thread per radix slot, its 256-byte and its 128-byte
+// line (lines: the 256-byte lines of all slots, then the 128-byte ones).
 __global__ void ncl_build_kernel(const uint64_t* key, const uint8_t* status, const uint32_t* nrdx, uint32_t nslots,
                                  uint32_t n, uint32_t slot_prefix, uint32_t* lines, LineSel sel) {
     // one item per thread, grid-stride (an incremental rebuild launches a capped grid)
@@ -5021,6 +5193,8 @@ __global__ void ncl_build_kernel(const uint64_t* key, const uint8_t* status, con
         [&] {
     uint32_t* L = lines + (size_t)NCL_STRIDE * s;
     const uint32_t r0 = nrdx[s], r1 = nrdx[s + 1], ns = r1 - r0;
+    ncl2_build_line(key, status, r0, r1, n, slot_prefix,
+                    reinterpret_cast<uint4*>(lines + (size_t)NCL_STRIDE * nslots + (size_t)NCL2_DWORDS * s));
     if (r0 < NCL_LEFT || (uint64_t)r0 - NCL_LEFT + NCL_SLOTS > n || ns > NCL_XMAX) {  // clamped window / wide slot
         L[0] = 0; L[1] = 0; L[2] = 1u; L[3] = 0;
         return;
@@ -7120,7 +7294,7 @@ __global__ __launch_bounds__(BLOCK) void svc_kernel(DevTable T, const SvcMail* _
             else if (T.flags & TF_GL32) rt_gl32_kernel_body(T, tq, q, count, idx, cnt);
             else rt_closest_kernel_body<32>(T, tq, q, count, idx, cnt);
         } else if (kind == 1 && count >= 1 && count <= 16 && (T.flags & TF_NCL)) {
-            nc_line_kernel_body<0, false>(T, T, nullptr, tq, q, count, idx, cnt);
+            nc_line_kernel_body<0, false, false>(T, T, nullptr, tq, q, count, idx, cnt);
         } else {
             // count 0, counts above 32, NodeCache without lines: one query per wave
             for (uint32_t i = w; i < q; i += BLOCK / 64) {  // wave-uniform
@@ -8243,7 +8417,7 @@ int build_ncl(kad_table* t) {
     std::vector<void*> fresh;
     uint64_t fb = 0;
     int rc;
-    if ((rc = dev_upload(&lp, nullptr, (size_t)NCL_STRIDE * d.nslots, fresh, fb))) return rc;
+    if ((rc = dev_upload(&lp, nullptr, (size_t)(NCL_STRIDE + NCL2_DWORDS) * d.nslots, fresh, fb))) return rc;
     hipLaunchKernelGGL(ncl_build_kernel, dim3(grid_for(d.nslots)), dim3(BLOCK), 0, build_stream(t), d.key, d.status, d.nrdx, d.nslots,
                        d.n, 64 - d.nshift, lp, LineSel{});
     if (hipGetLastError() != hipSuccess || hipStreamSynchronize(build_stream(t)) != hipSuccess) {
@@ -9345,10 +9519,10 @@ int kad_nc_closest_batch(const kad_table* t, const uint8_t* targets, uint32_t q,
     const bool lines = (t->d.flags & TF_NCL) && !ev;  // KAD_NC_KERNEL=<kernel> picks another one (A/B timing)
 #ifdef KAD_ABLATIONS  // timing ablations with WRONG results: only in the tools build
     if ((t->d.flags & TF_NCL) && ev && std::strcmp(ev, "lines_abl1") == 0 && count >= 1 && count <= 16)
-        hipLaunchKernelGGL((nc_line_kernel<1, false>), dim3(grid_for(q)), dim3(BLOCK), 0, (hipStream_t)stream, t->d,
+        hipLaunchKernelGGL((nc_line_kernel<1, false, false>), dim3(grid_for(q)), dim3(BLOCK), 0, (hipStream_t)stream, t->d,
                            t->d, nullptr, targets, q, count, out_idx, out_cnt);
     else if ((t->d.flags & TF_NCL) && ev && std::strcmp(ev, "lines_abl2") == 0 && count >= 1 && count <= 16)
-        hipLaunchKernelGGL((nc_line_kernel<2, false>), dim3(grid_for(q)), dim3(BLOCK), 0, (hipStream_t)stream, t->d,
+        hipLaunchKernelGGL((nc_line_kernel<2, false, false>), dim3(grid_for(q)), dim3(BLOCK), 0, (hipStream_t)stream, t->d,
                            t->d, nullptr, targets, q, count, out_idx, out_cnt);
     else if ((t->d.flags & TF_NCL32) && ev && std::strcmp(ev, "l32_abl1") == 0 && count > 16 && count <= 32)
         hipLaunchKernelGGL((nc32_line_kernel<1, false>), dim3(grid_for(8ull * q)), dim3(BLOCK), 0, (hipStream_t)stream,
@@ -9362,11 +9536,26 @@ int kad_nc_closest_batch(const kad_table* t, const uint8_t* targets, uint32_t q,
     else if (count > 16 && count <= 64 && t->d.n > 0 && ev && std::strcmp(ev, "w64_abl1") == 0)
         hipLaunchKernelGGL(nc_wave64_kernel<1>, dim3((q + BLOCK / 64 - 1) / (BLOCK / 64)), dim3(BLOCK), 0,
                            (hipStream_t)stream, t->d, targets, q, count, out_idx, out_cnt);
+    else if ((t->d.flags & TF_NCL) && ev && std::strcmp(ev, "lines_abl3") == 0 && count >= 1 && count <= 16)
+        hipLaunchKernelGGL((nc_line_kernel<3, false, true>), dim3(grid_for(q)), dim3(BLOCK), 0, (hipStream_t)stream, t->d,
+                           t->d, nullptr, targets, q, count, out_idx, out_cnt);
+    else if ((t->d.flags & TF_NCL) && ev && std::strcmp(ev, "lines_stats") == 0 && count >= 1 && count <= 16)
+        hipLaunchKernelGGL((nc_line_kernel<5, false, true>), dim3(grid_for(q)), dim3(BLOCK), 0, (hipStream_t)stream, t->d,
+                           t->d, nullptr, targets, q, count, out_idx, out_cnt);
+    else if ((t->d.flags & TF_NCL) && ev && std::strcmp(ev, "lines_p2") == 0 && count >= 1 && count <= 16)
+        hipLaunchKernelGGL((nc_line_kernel<6, false, true>), dim3(grid_for(q)), dim3(BLOCK), 0, (hipStream_t)stream,
+                           t->d, t->d, nullptr, targets, q, count, out_idx, out_cnt);
+    else if ((t->d.flags & TF_NCL) && ev && std::strcmp(ev, "lines_one") == 0 && count >= 1 && count <= 16)
+        hipLaunchKernelGGL((nc_line_kernel<0, false, false>), dim3(grid_for(q)), dim3(BLOCK), 0, (hipStream_t)stream,
+                           t->d, t->d, nullptr, targets, q, count, out_idx, out_cnt);
     else
 #endif
-    if (lines && count >= 1 && count <= 16)
-        hipLaunchKernelGGL((nc_line_kernel<0, false>), dim3(grid_for(q)), dim3(BLOCK), 0, (hipStream_t)stream, t->d,
-                           t->d, nullptr, targets, q, count, out_idx, out_cnt);
+    if (lines && count >= 1 && count <= NCL2_COUNT_MAX)
+        hipLaunchKernelGGL((nc_line_kernel<0, false, true>), dim3(grid_for(q)), dim3(BLOCK), 0, (hipStream_t)stream,
+                           t->d, t->d, nullptr, targets, q, count, out_idx, out_cnt);
+    else if (lines && count > NCL2_COUNT_MAX && count <= 16)
+        hipLaunchKernelGGL((nc_line_kernel<0, false, false>), dim3(grid_for(q)), dim3(BLOCK), 0, (hipStream_t)stream,
+                           t->d, t->d, nullptr, targets, q, count, out_idx, out_cnt);
     else if ((t->d.flags & TF_NCL32) && !ev && count > 16 && count <= 32)
         hipLaunchKernelGGL((nc32_line_kernel<0, false>), dim3(grid_for(8ull * q)), dim3(BLOCK), 0, (hipStream_t)stream,
                            t->d, t->d, nullptr, targets, q, count, out_idx, out_cnt);
@@ -9422,9 +9611,12 @@ int kad_nc_closest_batch_dual(const kad_table* t4, const kad_table* t6, const ui
         int rc;
         if ((t4 && (rc = ensure_lines(t4, need, s))) || (t6 && (rc = ensure_lines(t6, need, s)))) return rc;
     }
-    if (count <= 16)
-        hipLaunchKernelGGL((nc_line_kernel<0, true>), dim3(grid_for(q)), dim3(BLOCK), 0, s, d4, d6, af, targets, q, count,
-                           out_idx, out_cnt);
+    if (count <= NCL2_COUNT_MAX)
+        hipLaunchKernelGGL((nc_line_kernel<0, true, true>), dim3(grid_for(q)), dim3(BLOCK), 0, s, d4, d6, af, targets, q,
+                           count, out_idx, out_cnt);
+    else if (count <= 16)
+        hipLaunchKernelGGL((nc_line_kernel<0, true, false>), dim3(grid_for(q)), dim3(BLOCK), 0, s, d4, d6, af, targets, q,
+                           count, out_idx, out_cnt);
     else if (count <= 32 && ((d4.flags | d6.flags) & TF_NCL32))  // a family without the lines takes the wave path
         hipLaunchKernelGGL((nc32_line_kernel<0, true>), dim3(grid_for(8ull * q)), dim3(BLOCK), 0, s, d4, d6, af, targets,
                            q, count, out_idx, out_cnt);
@@ -10133,7 +10325,7 @@ int kad_nc_apply(kad_table* t, const uint32_t* erase, uint32_t n_erase, const ui
     // the line sets the table has are rebuilt for the new array; the others stay unbuilt until first use
     const bool has_ncl = t->ncl_mut != nullptr, has_ncl32 = t->ncl32_mut != nullptr;
     if (n1 && ((rc = dev_upload(&rdx1, nullptr, (size_t)r.slots + 1, fresh, freshb)) ||
-               (has_ncl && (rc = dev_upload(&ncl1, nullptr, (size_t)NCL_STRIDE * r.slots, fresh, freshb))) ||
+               (has_ncl && (rc = dev_upload(&ncl1, nullptr, (size_t)(NCL_STRIDE + NCL2_DWORDS) * r.slots, fresh, freshb))) ||
                (has_ncl32 && (rc = dev_upload(&ncl32, nullptr, (size_t)NC32_STRIDE * r.slots, fresh, freshb)))))
         return fail(rc);
     if (n1) {
@@ -10226,7 +10418,7 @@ int kad_table_export_lines(const kad_table* t, uint32_t set, void* out, uint64_t
         case KAD_LINESET_GL32: src = d.gl32; nb = 4ull * GL32_STRIDE * d.B; break;
         case KAD_LINESET_SL: src = d.sl; nb = 64ull * d.slslots; break;
         case KAD_LINESET_SL16: src = d.sl16; nb = 128ull * d.slslots; break;
-        case KAD_LINESET_NCL: src = d.ncl; nb = 4ull * NCL_STRIDE * d.nslots; break;
+        case KAD_LINESET_NCL: src = d.ncl; nb = 4ull * (NCL_STRIDE + NCL2_DWORDS) * d.nslots; break;
         case KAD_LINESET_NCL32: src = d.ncl32; nb = 4ull * NC32_STRIDE * d.nslots; break;
         case KAD_LINESET_GCNT: src = d.gcnt; nb = 4ull * d.B; break;
         case KAD_LINESET_DIR: src = d.dir; nb = 8ull * (d.B + 1); break;
