@@ -5023,6 +5023,7 @@ __device__ __forceinline__ void nc_line_kernel_body(const DevTable& T4, const De
     // the wave's rows (64 x 16 words) reuse its region: row r of the block at rows + ncl_wrow(r)
     uint32_t* rows = reinterpret_cast<uint32_t*>(&stg[0][0][0]);
     uint32_t stage = 3;  // ABL 5: which step answered (1: the 128-byte line, 2: the 256-byte line, 3: the wave)
+    uint32_t hr0 = NONE, hns = 0;  // the slot's first node and node count from a 128-byte line header (NONE: none)
     if ((ABL == 0 && HALF) || ABL == 3 || ABL == 5 || ABL == 6) {
         // the 128-byte lines first: round r, lane L loads piece (L & 7) of the line of query 8r + (L >> 3)
         uint4 ld[8], L2[8];
@@ -5043,6 +5044,10 @@ __device__ __forceinline__ void nc_line_kernel_body(const DevTable& T4, const De
         for (int x = 0; x < 8; x++) L2[x] = S[lane][x ^ (lane & 7)];
         wave_sync();
         const uint32_t ib = fam ? T6.index_base : T4.index_base;
+        if (sl != NONE && !((L2[0].y >> 16) & 1u)) {  // the slot's node range from the line header (the wave path's)
+            hns = L2[0].y & 255u;
+            hr0 = L2[0].x + NCL2_MID - hns / 2;
+        }
         if (sl != NONE) ok = ncl2_answer(L2, ib, t, count, rows + ncl_wrow(tid), m);
         if (ok) stage = 1;
         // the walks that leave the 37-node window (about one query in 150 at k = 14), deferred lines: the 256-byte
@@ -5109,8 +5114,9 @@ __device__ __forceinline__ void nc_line_kernel_body(const DevTable& T4, const De
         u.t3 = (uint32_t)__shfl((int)t.t3, (int)l, 64);
         u.t4 = (uint32_t)__shfl((int)t.t4, (int)l, 64);
         const DevTable& T = (DUAL && ((fm >> l) & 1ull)) ? T6 : T4;  // wave-uniform
-        uint32_t r0, r1;
-        nc_slot(T, u, r0, r1);
+        uint32_t r0 = (uint32_t)__shfl((int)hr0, (int)l, 64), r1;
+        if (r0 != NONE) r1 = r0 + (uint32_t)__shfl((int)hns, (int)l, 64);  // no radix load
+        else nc_slot(T, u, r0, r1);
         const NcWindow w = nc_window(T, r0, lane);
         nc_answer(T, u, r0, r1, w, lane, i - lane + l, count, out_idx, out_cnt);
     }
