@@ -5130,6 +5130,204 @@ __global__ __launch_bounds__(BLOCK) void nc_line_kernel(DevTable T4, DevTable T6
     nc_line_kernel_body<ABL, DUAL, HALF>(T4, T6, af, targets, q, count, out_idx, out_cnt);
 }
 
+// ---------------------------------------------------------------------------------------
+// NodeCache counts <= NCL2_COUNT_MAX, one lane per query reading its own 128-byte line (layout at ncl2_build_line).
+// The line region of the bench shard is 1 GB (8M radix slots): at that size eight 16-byte loads per lane reach 37 us
+// per 1M lines where the wave-loaded form (eight lanes per line, handed over through LDS) holds 45, and
+// with no line staging the block's LDS is its rows alone, so eight waves per SIMD fit.
+//
+// The walk without shifting the window: along the line's positions e = 0..36 the left run's keys descend (each key
+// ascends outward from lb) and the right run's ascend, so the 37 keys followed by NONE form a bitonic sequence of 64
+// whatever lb is. One half-cleaner at h = 32 (five mins) keeps the 32 smallest as a bitonic 32, and five more levels
+// sort them: the walk's first 32 steps, with no position-dependent indexing anywhere. The tie-break field is (63 - e)
+// on the left and e on the right (the same order as the steps from lb), so the node of a key is w0 + e read straight
+// from the key; the lane writes raw keys into its LDS row and the block's store decodes them.
+// ---------------------------------------------------------------------------------------
+constexpr uint32_t NCL2_RS = 17;  // LDS row stride in words (16 keys + 1: the lanes' rows fall into different banks)
+
+__device__ __forceinline__ uint32_t ncl2_key24x(const uint32_t (&d)[32], int e) {
+    // key24 of line position e (bytes 16 + 3e .. 18 + 3e) as key24 << 8, low byte zero: one byte permute
+    const int o = 3 * e, w = 4 + o / 4, b = o % 4;
+    const uint32_t sel = 0x0Cu | ((uint32_t)b << 8) | ((uint32_t)(b + 1) << 16) | ((uint32_t)(b + 2) << 24);
+    return __builtin_amdgcn_perm(w + 1 < 32 ? d[w + 1] : 0u, d[w], sel);
+}
+
+// The answer from the lane's 128-byte line d: raw walk keys (run max << 8 | side << 7 | tie-break << 1) into lrow[0..m),
+// the row's node base (w0 + index_base) into *rbase. False: the walk leaves the line (or a tie needs the full IDs).
+__device__ __forceinline__ bool ncl2_lane_answer(const uint32_t (&d)[32], uint64_t thi, uint32_t count, uint32_t* lrow,
+                                                 uint32_t& m) {
+    constexpr int S = (int)NCL2_SLOTS, PMIN = (int)NCL2_PMIN, PMAX = (int)NCL2_PMAX;
+    const uint32_t sh = (d[1] >> 8) & 63u, fl = d[1] >> 16;
+    const uint32_t tx = ((uint32_t)(thi >> sh) & 0xFFFFFFu) << 8;
+    uint32_t k[S];
+    uint32_t p = PMIN, z = NONE;
+#pragma unroll
+    for (int e = 0; e < S; e++) {
+        const uint32_t val = ncl2_key24x(d, e);
+        if (e >= PMIN && e < PMAX) p += val < tx ? 1u : 0u;  // the slot's nodes below the target (at 24 bits)
+        // the distance's 24 bits << 8 | expired (node w0 + e at bit e of dw2..3), taken in here so that the header
+        // dies with the line
+        k[e] = (val ^ tx) | ((d[2 + e / 32] >> (e % 32)) & 1u);
+        // a distance of zero at 24 bits in the slot (lb needs the full IDs) or just left of it (the runs may tie)
+        if (e >= PMIN - 1 && e < PMAX) z = min(z, k[e]);
+    }
+    bool ex = (fl & 1u) || z < 256u;
+    // runs: the left one from position PMAX - 1 down over the positions below p, the right one from PMIN up over the
+    // others. The two sets are disjoint, so each position's distance turns into its side's key in place (the line's
+    // keys and the walk fit in 64 VGPRs).
+    uint32_t runL = 0, runR = 0, endL = NONE, endR = NONE;
+#pragma unroll
+    for (int e = PMAX - 1; e >= 0; e--) {
+        const bool L = e < PMIN || (uint32_t)e < p;
+        runL = max(runL, L ? k[e] : 0u);  // (the run's low byte is some node's expired bit: masked below)
+        if (L) k[e] = (runL & ~255u) | ((uint32_t)(63 - e) << 1) | (k[e] & 1u);
+    }
+    if (fl & 2u) endL = k[0] | 1u;  // more nodes left of the line (the end node itself, expired or not, is in it)
+#pragma unroll
+    for (int e = PMIN; e < S; e++) {
+        const bool R = e >= PMAX || (uint32_t)e >= p;
+        runR = max(runR, R ? k[e] : 0u);
+        if (R) k[e] = (runR & ~255u) | 128u | ((uint32_t)e << 1) | (k[e] & 1u);
+    }
+    if (fl & 4u) endR = k[S - 1] | 1u;  // more nodes right of the line
+    const uint32_t lim = min(endL, endR);
+    // the 32 smallest of the bitonic 64 (k, then NONE), sorted
+#pragma unroll
+    for (int r = 0; r + 32 < S; r++) k[r] = min(k[r], k[r + 32]);
+#pragma unroll
+    for (int h = 16; h >= 1; h >>= 1)
+#pragma unroll
+        for (int r = 0; r < 32; r++)
+            if ((r & h) == 0) cx(k[r], k[r + h]);
+    uint32_t have = 0;
+#pragma unroll
+    for (int r = 0; r < 32; r++) {
+        const bool keep = k[r] <= lim && !(k[r] & 1u);
+        if (keep && have < count) lrow[have] = k[r];
+        have += keep ? 1u : 0u;
+    }
+    m = min(count, have);
+    ex |= have < count && (lim != NONE || k[31] != NONE);  // the walk goes on past the line / step 32
+    return !ex;
+}
+
+// The block's rows from raw walk keys (row r's keys at rows[r * NCL2_RS ..], its meta word m | answered << 8 and its
+// node base at meta[r] / base[r]) as one run of 16-byte stores; rows not answered are skipped dword by dword.
+template <int NT>
+__device__ __forceinline__ void store_rows_keys16(uint32_t* __restrict__ out_idx, uint32_t q, uint32_t count,
+                                                  const uint32_t* rows, const uint32_t* meta, const uint32_t* base) {
+    const uint32_t tid = threadIdx.x, q0 = blockIdx.x * NT;
+    const uint32_t nq = min((uint32_t)NT, q - q0), nw = nq * count;
+    uint32_t* dst = out_idx + (size_t)q0 * count;
+    const bool al = ((uintptr_t)out_idx & 15u) == 0;  // NT * count * 4 is a multiple of 16
+    for (uint32_t c4 = tid; 4 * c4 < nw; c4 += NT) {
+        const uint32_t w0 = 4 * c4;
+        uint32_t r = w0 / count, c = w0 - r * count, v[4];
+        bool okv[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const bool in = w0 + u < nw;
+            const uint32_t mt = in ? meta[r] : 0u;
+            okv[u] = in && ((mt >> 8) & 1u);
+            v[u] = NONE;
+            if (in && c < (mt & 255u)) {
+                const uint32_t key = rows[r * NCL2_RS + c], f = (key >> 1) & 63u;
+                v[u] = base[r] + ((key & 128u) ? f : 63u - f);
+            }
+            if (++c == count) { c = 0; r++; }
+        }
+        if (al && okv[0] && okv[1] && okv[2] && okv[3]) {
+            st_row4(dst + w0, v[0], v[1], v[2], v[3]);
+        } else {
+#pragma unroll
+            for (int u = 0; u < 4; u++)
+                if (okv[u]) st_row1(dst + w0 + u, v[u]);
+        }
+    }
+}
+
+// ABL 1 (timing ablation only, KAD_NC_KERNEL=lane_abl1; results wrong): the lines and the answer, no wave path. ABL 5
+// (lane_stats): out_cnt = the step that answered (1: the line, 2: the wave path, 3: the wave path's serial fallback).
+// WPE: the waves per SIMD the register allocation aims at (5: 85 VGPRs, no spill; 6 and 8 spill: A/B only). NT: threads
+// per workgroup (64: a wave that runs the wave path for a missed query holds only its own slot, not its block's).
+template <int ABL, bool DUAL, int WPE, int NT>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void ncl2_lane_kernel(
+    DevTable T4, DevTable T6, const uint8_t* __restrict__ af, const uint8_t* __restrict__ targets, uint32_t q,
+    uint32_t count, uint32_t* __restrict__ out_idx, uint8_t* __restrict__ out_cnt) {
+    const uint32_t i = blockIdx.x * NT + threadIdx.x, lane = threadIdx.x & 63u, tid = threadIdx.x;
+    const bool act = i < q;
+    const bool fam = DUAL && act && af[i] != 0;
+    // 76 bytes per query. meta[r] = m | answered << 8 | header valid << 9 | the slot's node count << 16
+    __shared__ uint32_t rows[NT * NCL2_RS], meta[NT], base[NT];
+    bool ok = false;
+    uint32_t m = 0, hv = 0;  // hv: header valid << 9 | the slot's node count << 16 (from the line header)
+    if (act) {
+        const uint64_t thi = load_target_hi(targets, i);  // the line path reads the top 64 bits alone
+        const DevTable& T = fam ? T6 : T4;
+        if (T.n == 0) {  // empty map: no nodes
+            ok = true;
+        } else if ((T.flags & TF_NCL) && thi >= T.nbase && ((thi - T.nbase) >> T.nshift) < T.nslots) {
+            // below the first slot / past the last: lb = 0 / n, windows clamped at the ends (the wave path)
+            const uint4* lp = T.ncl + (size_t)NCL_PIECES * T.nslots + 8ull * ((thi - T.nbase) >> T.nshift);
+            uint32_t d[32];
+#pragma unroll
+            for (int x = 0; x < 8; x++) {
+                uint4 u;
+                if (ABL == 7) {
+                    const u32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(lp + x));
+                    u = make_uint4(v.x, v.y, v.z, v.w);
+                } else {
+                    u = lp[x];
+                }
+                d[4 * x] = u.x; d[4 * x + 1] = u.y; d[4 * x + 2] = u.z; d[4 * x + 3] = u.w;
+            }
+            if (!((d[1] >> 16) & 1u)) hv = 512u | ((d[1] & 255u) << 16);
+            base[tid] = d[0] + T.index_base;
+            ok = ncl2_lane_answer(d, thi, count, rows + tid * NCL2_RS, m);
+        }
+    }
+    if (act && ok && out_cnt) out_cnt[i] = (uint8_t)m;
+    meta[tid] = m | (ok ? 256u : 0u) | hv;
+    if (NT > 64) __syncthreads(); else wave_sync();
+    // the lanes the line could not answer (0.11 % of the queries at k = 14): one query at a time by the whole wave,
+    // its target read again (wave-uniform) and its slot range from the line header when there is one. The first
+    // one's target and window loads go out before the row store, each next one's before the current one's answer.
+    uint64_t pend = ABL == 1 ? 0ull : __ballot(act && !ok);
+    const uint64_t fm = DUAL ? __ballot(fam) : 0ull;
+    Target u{};
+    NcWindow w{0, 0, 0};
+    uint32_t qi = 0, r0 = 0, r1 = 0;
+    bool f6 = false;
+    auto fetch = [&](uint32_t l) {
+        qi = i - lane + l;
+        u = load_target(targets, qi);
+        f6 = DUAL && ((fm >> l) & 1ull);  // wave-uniform
+        const DevTable& T = f6 ? T6 : T4;
+        const uint32_t mt = meta[tid - lane + l];
+        if (mt & 512u) {  // no radix load
+            const uint32_t ns = (mt >> 16) & 255u;
+            r0 = base[tid - lane + l] - T.index_base + NCL2_MID - ns / 2;
+            r1 = r0 + ns;
+        } else {
+            nc_slot(T, u, r0, r1);
+        }
+        w = nc_window(T, r0, lane);
+    };
+    if (pend) fetch((uint32_t)__builtin_ctzll(pend));
+    store_rows_keys16<NT>(out_idx, q, count, rows, meta, base);
+    while (pend) {
+        pend &= pend - 1;
+        const Target uc = u;
+        const NcWindow wc = w;
+        const uint32_t qc = qi, a0 = r0, a1 = r1;
+        const bool c6 = f6;
+        if (pend) fetch((uint32_t)__builtin_ctzll(pend));
+        const bool wok = nc_answer(c6 ? T6 : T4, uc, a0, a1, wc, lane, qc, count, out_idx, out_cnt);
+        if (ABL == 5 && lane == 0 && out_cnt) out_cnt[qc] = wok ? 2 : 3;
+    }
+    if (ABL == 5 && act && ok && out_cnt) out_cnt[i] = 1;
+}
+
 // NodeCache counts 17..64 for two families (af per query): nc_two_pass_kernel with the table chosen per
 // wave (one query per wave); an empty family map gives zero results.
 __global__ __launch_bounds__(BLOCK) void nc_two_pass_dual_kernel(DevTable T4, DevTable T6, const uint8_t* __restrict__ af,
@@ -7110,6 +7308,7 @@ __global__ void scan_apply_kernel(const uint32_t* part, const uint32_t* sums, ui
 }
 
 inline uint32_t grid_for(uint64_t n) { return (uint32_t)((n + BLOCK - 1) / BLOCK); }
+inline uint32_t grid64(uint64_t n) { return (uint32_t)((n + 63) / 64); }  // one-wave workgroups
 
 
 // ---------------------------------------------------------------------------------------
@@ -9510,6 +9709,13 @@ int kad_rt_find_bucket_batch(const kad_table* t, const uint8_t* targets, uint32_
     return KAD_OK;
 }
 
+// The count <= 14 NodeCache kernel's form for A/B (KAD_NCL2_WPE = 6: aimed at six waves per SIMD, spills; 7: the line
+// read with non-temporal loads; 256: blocks of four waves; default: five waves per SIMD, one-wave blocks).
+static int ncl2_wpe() {
+    const char* e = std::getenv("KAD_NCL2_WPE");
+    return e ? std::atoi(e) : 5;
+}
+
 int kad_nc_closest_batch(const kad_table* t, const uint8_t* targets, uint32_t q, uint32_t count, uint32_t* out_idx,
                          uint8_t* out_cnt, void* stream) {
     if (!t) return set_err(KAD_ERR_INVALID, "NULL table");
@@ -9551,14 +9757,35 @@ int kad_nc_closest_batch(const kad_table* t, const uint8_t* targets, uint32_t q,
     else if ((t->d.flags & TF_NCL) && ev && std::strcmp(ev, "lines_p2") == 0 && count >= 1 && count <= 16)
         hipLaunchKernelGGL((nc_line_kernel<6, false, true>), dim3(grid_for(q)), dim3(BLOCK), 0, (hipStream_t)stream,
                            t->d, t->d, nullptr, targets, q, count, out_idx, out_cnt);
+    else if ((t->d.flags & TF_NCL) && ev && std::strcmp(ev, "lines_wave") == 0 && count >= 1 && count <= NCL2_COUNT_MAX)
+        hipLaunchKernelGGL((nc_line_kernel<0, false, true>), dim3(grid_for(q)), dim3(BLOCK), 0, (hipStream_t)stream,
+                           t->d, t->d, nullptr, targets, q, count, out_idx, out_cnt);
+    else if ((t->d.flags & TF_NCL) && ev && std::strcmp(ev, "lane_abl1") == 0 && count >= 1 && count <= NCL2_COUNT_MAX)
+        hipLaunchKernelGGL((ncl2_lane_kernel<1, false, 5, 64>), dim3(grid64(q)), dim3(64), 0, (hipStream_t)stream,
+                           t->d, t->d, nullptr, targets, q, count, out_idx, out_cnt);
+    else if ((t->d.flags & TF_NCL) && ev && std::strcmp(ev, "lane_stats") == 0 && count >= 1 && count <= NCL2_COUNT_MAX)
+        hipLaunchKernelGGL((ncl2_lane_kernel<5, false, 5, 64>), dim3(grid64(q)), dim3(64), 0, (hipStream_t)stream,
+                           t->d, t->d, nullptr, targets, q, count, out_idx, out_cnt);
     else if ((t->d.flags & TF_NCL) && ev && std::strcmp(ev, "lines_one") == 0 && count >= 1 && count <= 16)
         hipLaunchKernelGGL((nc_line_kernel<0, false, false>), dim3(grid_for(q)), dim3(BLOCK), 0, (hipStream_t)stream,
                            t->d, t->d, nullptr, targets, q, count, out_idx, out_cnt);
     else
 #endif
-    if (lines && count >= 1 && count <= NCL2_COUNT_MAX)
-        hipLaunchKernelGGL((nc_line_kernel<0, false, true>), dim3(grid_for(q)), dim3(BLOCK), 0, (hipStream_t)stream,
-                           t->d, t->d, nullptr, targets, q, count, out_idx, out_cnt);
+    if (lines && count >= 1 && count <= NCL2_COUNT_MAX) {
+        const int wpe = ncl2_wpe();
+        if (wpe == 6)
+            hipLaunchKernelGGL((ncl2_lane_kernel<0, false, 6, 64>), dim3(grid64(q)), dim3(64), 0,
+                               (hipStream_t)stream, t->d, t->d, nullptr, targets, q, count, out_idx, out_cnt);
+        else if (wpe == 7)  // non-temporal line loads
+            hipLaunchKernelGGL((ncl2_lane_kernel<7, false, 5, 64>), dim3(grid64(q)), dim3(64), 0,
+                               (hipStream_t)stream, t->d, t->d, nullptr, targets, q, count, out_idx, out_cnt);
+        else if (wpe == 256)
+            hipLaunchKernelGGL((ncl2_lane_kernel<0, false, 5, 256>), dim3(grid_for(q)), dim3(256), 0,
+                               (hipStream_t)stream, t->d, t->d, nullptr, targets, q, count, out_idx, out_cnt);
+        else
+            hipLaunchKernelGGL((ncl2_lane_kernel<0, false, 5, 64>), dim3(grid64(q)), dim3(64), 0,
+                               (hipStream_t)stream, t->d, t->d, nullptr, targets, q, count, out_idx, out_cnt);
+    }
     else if (lines && count > NCL2_COUNT_MAX && count <= 16)
         hipLaunchKernelGGL((nc_line_kernel<0, false, false>), dim3(grid_for(q)), dim3(BLOCK), 0, (hipStream_t)stream,
                            t->d, t->d, nullptr, targets, q, count, out_idx, out_cnt);
@@ -9618,7 +9845,7 @@ int kad_nc_closest_batch_dual(const kad_table* t4, const kad_table* t6, const ui
         if ((t4 && (rc = ensure_lines(t4, need, s))) || (t6 && (rc = ensure_lines(t6, need, s)))) return rc;
     }
     if (count <= NCL2_COUNT_MAX)
-        hipLaunchKernelGGL((nc_line_kernel<0, true, true>), dim3(grid_for(q)), dim3(BLOCK), 0, s, d4, d6, af, targets, q,
+        hipLaunchKernelGGL((ncl2_lane_kernel<0, true, 5, 64>), dim3(grid64(q)), dim3(64), 0, s, d4, d6, af, targets, q,
                            count, out_idx, out_cnt);
     else if (count <= 16)
         hipLaunchKernelGGL((nc_line_kernel<0, true, false>), dim3(grid_for(q)), dim3(BLOCK), 0, s, d4, d6, af, targets, q,
