@@ -5246,8 +5246,10 @@ __device__ __forceinline__ void store_rows_keys16(uint32_t* __restrict__ out_idx
     }
 }
 
-// ABL 1 (timing ablation only, KAD_NC_KERNEL=lane_abl1; results wrong): the lines and the answer, no wave path. ABL 5
-// (lane_stats): out_cnt = the step that answered (1: the line, 2: the wave path, 3: the wave path's serial fallback).
+// ABL 1 (timing ablation only, KAD_NC_KERNEL=lane_abl1; results wrong): the lines and the answer, no wave path. ABL 9
+// (lane_abl9): the wave path's loads without its answers; ABL 11 (lane_abl11): the same and a whole row of plain stores
+// per missed query. ABL 5 (lane_stats): out_cnt = the step that answered (1: the line, 2: the wave path, 3: the wave
+// path's serial fallback).
 // WPE: the waves per SIMD the register allocation aims at (5: 85 VGPRs, no spill; 6 and 8 spill: A/B only). NT: threads
 // per workgroup (64: a wave that runs the wave path for a missed query holds only its own slot, not its block's).
 template <int ABL, bool DUAL, int WPE, int NT>
@@ -5272,13 +5274,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
             uint32_t d[32];
 #pragma unroll
             for (int x = 0; x < 8; x++) {
-                uint4 u;
-                if (ABL == 7) {
-                    const u32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(lp + x));
-                    u = make_uint4(v.x, v.y, v.z, v.w);
-                } else {
-                    u = lp[x];
-                }
+                const uint4 u = lp[x];
                 d[4 * x] = u.x; d[4 * x + 1] = u.y; d[4 * x + 2] = u.z; d[4 * x + 3] = u.w;
             }
             if (!((d[1] >> 16) & 1u)) hv = 512u | ((d[1] & 255u) << 16);
@@ -5322,6 +5318,14 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
         const uint32_t qc = qi, a0 = r0, a1 = r1;
         const bool c6 = f6;
         if (pend) fetch((uint32_t)__builtin_ctzll(pend));
+        if (ABL == 9) {  // the misses' loads without their answers (results wrong)
+            if (lane == 0) out_idx[(size_t)qc * count] = (uint32_t)(wc.k0 ^ wc.k1 ^ uc.hi) + a0 + a1 + c6;
+            continue;
+        }
+        if (ABL == 11) {  // the misses' loads and a whole row of plain stores, no answer (results wrong)
+            if (lane < count) out_idx[(size_t)qc * count + lane] = (uint32_t)(wc.k0 ^ wc.k1 ^ uc.hi) + a0 + a1 + c6;
+            continue;
+        }
         const bool wok = nc_answer(c6 ? T6 : T4, uc, a0, a1, wc, lane, qc, count, out_idx, out_cnt);
         if (ABL == 5 && lane == 0 && out_cnt) out_cnt[qc] = wok ? 2 : 3;
     }
@@ -9709,8 +9713,8 @@ int kad_rt_find_bucket_batch(const kad_table* t, const uint8_t* targets, uint32_
     return KAD_OK;
 }
 
-// The count <= 14 NodeCache kernel's form for A/B (KAD_NCL2_WPE = 6: aimed at six waves per SIMD, spills; 7: the line
-// read with non-temporal loads; 256: blocks of four waves; default: five waves per SIMD, one-wave blocks).
+// The count <= 14 NodeCache kernel's form for A/B (KAD_NCL2_WPE = 6: aimed at six waves per SIMD, spills; 256: blocks of
+// four waves; default: five waves per SIMD, one-wave blocks).
 static int ncl2_wpe() {
     const char* e = std::getenv("KAD_NCL2_WPE");
     return e ? std::atoi(e) : 5;
@@ -9763,6 +9767,12 @@ int kad_nc_closest_batch(const kad_table* t, const uint8_t* targets, uint32_t q,
     else if ((t->d.flags & TF_NCL) && ev && std::strcmp(ev, "lane_abl1") == 0 && count >= 1 && count <= NCL2_COUNT_MAX)
         hipLaunchKernelGGL((ncl2_lane_kernel<1, false, 5, 64>), dim3(grid64(q)), dim3(64), 0, (hipStream_t)stream,
                            t->d, t->d, nullptr, targets, q, count, out_idx, out_cnt);
+    else if ((t->d.flags & TF_NCL) && ev && std::strcmp(ev, "lane_abl9") == 0 && count >= 1 && count <= NCL2_COUNT_MAX)
+        hipLaunchKernelGGL((ncl2_lane_kernel<9, false, 5, 64>), dim3(grid64(q)), dim3(64), 0, (hipStream_t)stream,
+                           t->d, t->d, nullptr, targets, q, count, out_idx, out_cnt);
+    else if ((t->d.flags & TF_NCL) && ev && std::strcmp(ev, "lane_abl11") == 0 && count >= 1 && count <= NCL2_COUNT_MAX)
+        hipLaunchKernelGGL((ncl2_lane_kernel<11, false, 5, 64>), dim3(grid64(q)), dim3(64), 0, (hipStream_t)stream,
+                           t->d, t->d, nullptr, targets, q, count, out_idx, out_cnt);
     else if ((t->d.flags & TF_NCL) && ev && std::strcmp(ev, "lane_stats") == 0 && count >= 1 && count <= NCL2_COUNT_MAX)
         hipLaunchKernelGGL((ncl2_lane_kernel<5, false, 5, 64>), dim3(grid64(q)), dim3(64), 0, (hipStream_t)stream,
                            t->d, t->d, nullptr, targets, q, count, out_idx, out_cnt);
@@ -9775,9 +9785,6 @@ int kad_nc_closest_batch(const kad_table* t, const uint8_t* targets, uint32_t q,
         const int wpe = ncl2_wpe();
         if (wpe == 6)
             hipLaunchKernelGGL((ncl2_lane_kernel<0, false, 6, 64>), dim3(grid64(q)), dim3(64), 0,
-                               (hipStream_t)stream, t->d, t->d, nullptr, targets, q, count, out_idx, out_cnt);
-        else if (wpe == 7)  // non-temporal line loads
-            hipLaunchKernelGGL((ncl2_lane_kernel<7, false, 5, 64>), dim3(grid64(q)), dim3(64), 0,
                                (hipStream_t)stream, t->d, t->d, nullptr, targets, q, count, out_idx, out_cnt);
         else if (wpe == 256)
             hipLaunchKernelGGL((ncl2_lane_kernel<0, false, 5, 256>), dim3(grid_for(q)), dim3(256), 0,

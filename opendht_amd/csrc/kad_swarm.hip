@@ -51,6 +51,9 @@ constexpr uint32_t SNP = 16; // per-peer answer width (count <= 16)
 constexpr uint32_t LST = KAD_SEARCH_LIST;  // search list capacity: SEARCH_NODES non-bad nodes + the bad ones
 constexpr uint32_t MAX_BAD = 25;           // SEARCH_MAX_BAD_NODES (dht.h:316-324)
 constexpr uint32_t ALPHA = 4;
+#ifndef SW_NARROW_WPE
+#define SW_NARROW_WPE 1
+#endif
 constexpr int BLOCK = 256;
 
 int err(int code, const char* fmt, ...) {
@@ -440,13 +443,16 @@ constexpr uint32_t XO_CAP = 64;  // silent peers remembered per lookup (4 per ho
 // after the last prefix with SEARCH_NODES non-bad nodes (an insert beyond that point is refused), then
 // trimmed from the end while it holds more than SEARCH_NODES non-bad nodes. Static indices only; the queried and
 // bad flags are bit masks (qm, bm).
-__device__ __forceinline__ void search_insert(const SwarmDev& W, const Tgt& t, uint32_t (&li)[LST], uint64_t (&ld)[LST],
+// N: the list's register width (LST, or 16 for a wave whose lists hold no bad node and no silent peer: at most
+// SEARCH_NODES + 1 entries then, so the capacity branch is never taken).
+template <uint32_t N>
+__device__ __forceinline__ void search_insert(const SwarmDev& W, const Tgt& t, uint32_t (&li)[N], uint64_t (&ld)[N],
                                               uint32_t& qm, uint32_t& bm, uint32_t& n, uint32_t r, uint64_t rd, bool rbad,
                                               bool& ovf) {
     bool found = false, anyeq = false;
     uint32_t pos = 0;
 #pragma unroll
-    for (uint32_t k = 0; k < LST; k++) {
+    for (uint32_t k = 0; k < N; k++) {
         if (k < n) {
             found |= li[k] == r;
             pos += ld[k] < rd;
@@ -457,7 +463,7 @@ __device__ __forceinline__ void search_insert(const SwarmDev& W, const Tgt& t, u
     uint32_t tie = 0;
     if (anyeq) {  // equal top 64 bits (rare): which entries, for the full 160-bit order below
 #pragma unroll
-        for (uint32_t k = 0; k < LST; k++)
+        for (uint32_t k = 0; k < N; k++)
             if (k < n) tie |= (ld[k] == rd && li[k] != r ? 1u : 0u) << k;
     }
     while (tie) {  // the full 160-bit order (a select chain keeps the index static)
@@ -465,7 +471,7 @@ __device__ __forceinline__ void search_insert(const SwarmDev& W, const Tgt& t, u
         tie &= tie - 1u;
         uint32_t lk = 0;
 #pragma unroll
-        for (uint32_t x = 0; x < LST; x++) lk = x == k ? li[x] : lk;
+        for (uint32_t x = 0; x < N; x++) lk = x == k ? li[x] : lk;
         pos += tail_less(W, t, lk, r);
     }
     uint32_t bad = (uint32_t)__builtin_popcount(bm & lo_mask(n));
@@ -481,8 +487,8 @@ __device__ __forceinline__ void search_insert(const SwarmDev& W, const Tgt& t, u
         bad = (uint32_t)__builtin_popcount(bm & lo_mask(n));
         if (pos >= tt) return;
     }
-    if (n == LST) {  // capacity: drop the farthest entry (counted; never reached in the tests)
-        bad -= (bm >> (LST - 1)) & 1u;
+    if (n == N) {  // capacity: drop the farthest entry (counted; never reached in the tests)
+        bad -= (bm >> (N - 1)) & 1u;
         n--;
         ovf = true;
         if (pos >= n) return;
@@ -490,7 +496,7 @@ __device__ __forceinline__ void search_insert(const SwarmDev& W, const Tgt& t, u
     // insert at pos: entries from pos on move up one (selects, not conditional stores: those became stores through
     // a selected pointer and put the lists in scratch); entries from n + 1 on are don't-care
 #pragma unroll
-    for (uint32_t k = LST - 1; k > 0; k--) {
+    for (uint32_t k = N - 1; k > 0; k--) {
         li[k] = k > pos ? li[k - 1] : k == pos ? r : li[k];
         ld[k] = k > pos ? ld[k - 1] : k == pos ? rd : ld[k];
     }
@@ -543,15 +549,14 @@ __device__ __forceinline__ void load_answers(const SearchDev& X, uint32_t g, uin
 // FUSED (search_hop_kernel): the hop in one lane per lookup — each queried node's findClosestNodes(t, 8) computed in
 // place (peer_closest, the query kernel's code) and inserted at once, so the answers never go through HBM (the split
 // form writes and reads 4 x 96 bytes per lookup and hop) and the hop is one launch.
-template <bool FUSED>
-__global__ __launch_bounds__(BLOCK) void search_merge_kernel(SwarmDev W, SearchDev X) {
-    const uint32_t s = blockIdx.x * BLOCK + threadIdx.x;
-    bool running = false;
-    if (s < X.S && !X.done[s]) {
+// N: the list's register width (search_insert); n0, bm0, xn: the list length, its bad flags and the silent-peer count.
+template <uint32_t N, bool FUSED>
+__device__ __forceinline__ bool merge_lookup(const SwarmDev& W, const SearchDev& X, uint32_t s, uint32_t n0, uint32_t bm0,
+                                             uint32_t xn) {
+    {
         const Tgt t = load_tgt(X.targets, s);
-        uint32_t li[LST];
-        uint64_t ld[LST];  // top-64 XOR distances
-        const uint32_t n0 = X.ln[s];
+        uint32_t li[N];
+        uint64_t ld[N];  // top-64 XOR distances
         uint32_t n = n0;
         const uint4 sv = reinterpret_cast<const uint4*>(X.sel)[s];
         const uint32_t sel[ALPHA] = {sv.x, sv.y, sv.z, sv.w};
@@ -562,22 +567,21 @@ __global__ __launch_bounds__(BLOCK) void search_merge_kernel(SwarmDev W, SearchD
             const uint4* pi = reinterpret_cast<const uint4*>(X.li + (size_t)s * LST);
             const uint4* pk = reinterpret_cast<const uint4*>(X.lk + (size_t)s * LST);
 #pragma unroll
-            for (uint32_t x = 0; x < LST / 4; x++) {
+            for (uint32_t x = 0; x < N / 4; x++) {
                 const uint4 u = 4 * x < n0 ? pi[x] : make_uint4(NONE, NONE, NONE, NONE);
                 li[4 * x] = u.x; li[4 * x + 1] = u.y; li[4 * x + 2] = u.z; li[4 * x + 3] = u.w;
             }
 #pragma unroll
-            for (uint32_t x = 0; x < LST / 2; x++) {
+            for (uint32_t x = 0; x < N / 2; x++) {
                 const uint4 u = 2 * x < n0 ? pk[x] : make_uint4(~0u, ~0u, ~0u, ~0u);
                 ld[2 * x] = (((uint64_t)u.y << 32) | u.x) ^ t.hi;
                 ld[2 * x + 1] = (((uint64_t)u.w << 32) | u.z) ^ t.hi;
             }
         }
-        uint32_t qm = load_flags(X.lq, s, n0), bm = load_flags(X.lb, s, n0);
+        uint32_t qm = load_flags(X.lq, s, n0), bm = bm0;
         const uint32_t src = X.src[s];
         bool ovf = false;
         const uint32_t* xo = X.xo + (size_t)s * XO_CAP;
-        uint32_t xn = X.xn[s];
 #pragma unroll
         for (uint32_t a = 0; a < ALPHA; a++) {
             uint32_t rn;
@@ -612,7 +616,7 @@ __global__ __launch_bounds__(BLOCK) void search_merge_kernel(SwarmDev W, SearchD
             if (xn < XO_CAP) X.xo[(size_t)s * XO_CAP + xn++] = v;  // its node is expired from now on
             else ovf = true;
 #pragma unroll
-            for (uint32_t k = 0; k < LST; k++)
+            for (uint32_t k = 0; k < N; k++)
                 if (k < n && li[k] == v) bm |= 1u << k;
         }
         X.xn[s] = (uint8_t)xn;
@@ -637,12 +641,12 @@ __global__ __launch_bounds__(BLOCK) void search_merge_kernel(SwarmDev W, SearchD
             uint4* pi = reinterpret_cast<uint4*>(X.li + (size_t)s * LST);
             uint4* pk = reinterpret_cast<uint4*>(X.lk + (size_t)s * LST);
 #pragma unroll
-            for (uint32_t x = 0; x < LST / 4; x++)
+            for (uint32_t x = 0; x < N / 4; x++)
                 if (4 * x < wn)
                     pi[x] = make_uint4(4 * x < n ? li[4 * x] : NONE, 4 * x + 1 < n ? li[4 * x + 1] : NONE,
                                        4 * x + 2 < n ? li[4 * x + 2] : NONE, 4 * x + 3 < n ? li[4 * x + 3] : NONE);
 #pragma unroll
-            for (uint32_t x = 0; x < LST / 2; x++) {
+            for (uint32_t x = 0; x < N / 2; x++) {
                 if (2 * x >= wn) continue;
                 const uint64_t k0 = 2 * x < n ? ld[2 * x] ^ t.hi : ~0ull, k1 = 2 * x + 1 < n ? ld[2 * x + 1] ^ t.hi : ~0ull;
                 pk[x] = make_uint4((uint32_t)k0, (uint32_t)(k0 >> 32), (uint32_t)k1, (uint32_t)(k1 >> 32));
@@ -651,7 +655,21 @@ __global__ __launch_bounds__(BLOCK) void search_merge_kernel(SwarmDev W, SearchD
         store_flags(X.lq, s, qm, n, wn);
         store_flags(X.lb, s, bm, n, wn);
         if (ovf) atomicAdd(X.overflow, 1u);
-        running = !X.done[s];
+        return !X.done[s];
+    }
+}
+
+// N = 16 (the narrow form): for runs where every peer answers (swarm_offline never true), so that no list holds a bad
+// node and no lookup meets a silent peer: a list keeps at most SEARCH_NODES + 1 entries through a hop, in 16
+// registers instead of LST (and the kernel in a quarter of the VGPRs). N = LST: any run.
+template <bool FUSED, uint32_t N>
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(N == 16 ? SW_NARROW_WPE : 1, 8))) void search_merge_kernel(SwarmDev W, SearchDev X) {
+    const uint32_t s = blockIdx.x * BLOCK + threadIdx.x;
+    const bool live = s < X.S && !X.done[s];
+    bool running = false;
+    if (live) {
+        const uint32_t n0 = X.ln[s];
+        running = merge_lookup<N, FUSED>(W, X, s, n0, N == LST ? load_flags(X.lb, s, n0) : 0u, N == LST ? X.xn[s] : 0u);
     }
     const uint64_t m = __ballot(running);
     if ((threadIdx.x & 63u) == 0 && m) atomicAdd(X.active, (uint32_t)__builtin_popcountll(m));
@@ -848,6 +866,12 @@ int kad_search_create(kad_search** out, const kad_swarm* s, uint32_t S, const ui
     return KAD_OK;
 }
 
+// KAD_SWARM_WIDE=1 (A/B): the LST-wide merge even where every peer answers.
+static bool narrow_off() {
+    static const bool off = std::getenv("KAD_SWARM_WIDE") != nullptr;
+    return off;
+}
+
 int kad_search_hop(kad_search* x, uint32_t* n_active) {
     if (!x) return err(KAD_ERR_INVALID, "NULL search");
     Guard g(x->device);
@@ -861,9 +885,14 @@ int kad_search_hop(kad_search* x, uint32_t* n_active) {
         if (split) {
             hipLaunchKernelGGL(search_query_kernel, dim3(grid_for((uint64_t)X.S * ALPHA)), dim3(BLOCK), 0, x->stream,
                                x->sw->W, X);
-            hipLaunchKernelGGL(search_merge_kernel<false>, dim3(grid_for(X.S)), dim3(BLOCK), 0, x->stream, x->sw->W, X);
+            if (X.offline == 0 && !narrow_off())
+                hipLaunchKernelGGL((search_merge_kernel<false, 16>), dim3(grid_for(X.S)), dim3(BLOCK), 0, x->stream,
+                                   x->sw->W, X);
+            else
+                hipLaunchKernelGGL((search_merge_kernel<false, LST>), dim3(grid_for(X.S)), dim3(BLOCK), 0, x->stream,
+                                   x->sw->W, X);
         } else {
-            hipLaunchKernelGGL(search_merge_kernel<true>, dim3(grid_for(X.S)), dim3(BLOCK), 0, x->stream, x->sw->W, X);
+            hipLaunchKernelGGL((search_merge_kernel<true, LST>), dim3(grid_for(X.S)), dim3(BLOCK), 0, x->stream, x->sw->W, X);
         }
     }
     SW_TRY(hipGetLastError());
