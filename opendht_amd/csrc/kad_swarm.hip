@@ -18,8 +18,9 @@
 //
 // HBM layout (n peers, L = KAD_SWARM_LEVELS levels, 8 entries per bucket):
 //   key[n] u64 (ID bits 0..63 of the sorted peer IDs), tail[n][3] u32 (bits 64..159, exact ties only)
-//   depth[n] u8, cnt[n][L] u8, ent[n][L][8] u32 (peer indices), ekey[n][L][8] u64 (their keys inline:
-//   one 64-byte line per bucket, so a window of buckets costs a few lines and no per-node gathers)
+//   hdr[n]: one 64-byte line (key, depth D, the L level counts); lvl[n][L]: one 128-byte line per bucket (the 8
+//   entries' peer indices, then their keys inline), so a findClosestNodes reads the header and one line per window
+//   bucket and does no per-node gathers
 // A peer's buckets sorted by `first` (the RoutingTable order) follow from k's bits: the levels whose
 // bit of k is 1 (their bucket lies below k) in ascending d, my bucket, then the levels whose bit is
 // 0 in descending d. The bucket holding a target is level commonBits(k, t) (or my bucket).
@@ -31,6 +32,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -54,6 +56,9 @@ constexpr uint32_t ALPHA = 4;
 #ifndef SW_NARROW_WPE
 #define SW_NARROW_WPE 1
 #endif
+#ifndef SW_QUERY_WPE
+#define SW_QUERY_WPE 1
+#endif
 constexpr int BLOCK = 256;
 
 int err(int code, const char* fmt, ...) {
@@ -73,13 +78,16 @@ int err(int code, const char* fmt, ...) {
 
 inline uint32_t grid_for(uint64_t n) { return (uint32_t)((n + BLOCK - 1) / BLOCK); }
 
+// A peer's table as one 64-byte header line (HDR_WORDS: its key, depth and the L level counts) and one 128-byte line
+// per level (LVL_WORDS: the 8 entries' peer indices, then their keys): a findClosestNodes on a peer's table reads
+// the header and one line per window bucket, 3 random lines for the usual 2-bucket window, where separate key,
+// depth, count, index and key arrays took 7 (the query kernel is bound by its random line requests).
+constexpr uint32_t HDR_WORDS = 16, LVL_WORDS = 32;  // header: dw0-1 key, byte 8 depth, bytes 16.. counts
 struct SwarmDev {
     const uint64_t* key;
     const uint32_t* tail;
-    uint8_t* depth;
-    uint8_t* cnt;
-    uint32_t* ent;
-    uint64_t* ekey;
+    uint32_t* hdr;  // [n][HDR_WORDS]
+    uint32_t* lvl;  // [n][L][LVL_WORDS]: dw 0-7 indices, dw 8-23 keys (lo, hi), dw 24-31 zero
     uint32_t n;
 };
 
@@ -131,31 +139,50 @@ __global__ void swarm_build_kernel(SwarmDev W) {
         prefix_range(W, D ? k >> (64 - D) : 0ull, D, lo, hi);
         if (hi - lo - 1 <= BK || D == L - 1) break;
     }
-    W.depth[p] = (uint8_t)D;
-    uint8_t* cp = W.cnt + (size_t)p * L;
+    uint32_t* hp = W.hdr + (size_t)p * HDR_WORDS;
+    uint8_t cp[L];
     for (uint32_t d = 0; d < L; d++) cp[d] = 0;
-    for (uint32_t d = 0; d < D; d++) {
-        uint32_t a, e;
-        prefix_range(W, (k >> (63 - d)) ^ 1ull, d + 1, a, e);
-        const uint32_t m = e - a, c = min(m, BK);
-        const uint64_t off = m > BK ? mix(k ^ ((uint64_t)(d + 1) * 0x9E3779B97F4A7C15ull)) % m : 0ull;
-        uint32_t* ep = W.ent + ((size_t)p * L + d) * BK;
-        uint64_t* kp = W.ekey + ((size_t)p * L + d) * BK;
+    // a level line: 8 indices, 8 keys, padding
+    auto put = [&](uint32_t d, const uint32_t (&ei)[BK]) {
+        uint32_t* lp = W.lvl + ((size_t)p * L + d) * LVL_WORDS;
         for (uint32_t j = 0; j < BK; j++) {
-            const uint32_t x = j < c ? (m > BK ? a + (uint32_t)((off + (uint64_t)j * m / BK) % m) : a + j) : NONE;
-            ep[j] = x;
-            kp[j] = x != NONE ? W.key[x] : ~0ull;
+            const uint64_t kk = ei[j] != NONE ? W.key[ei[j]] : ~0ull;
+            lp[j] = ei[j];
+            lp[BK + 2 * j] = (uint32_t)kk;
+            lp[BK + 2 * j + 1] = (uint32_t)(kk >> 32);
         }
-        cp[d] = (uint8_t)c;
+        for (uint32_t j = 3 * BK; j < LVL_WORDS; j++) lp[j] = 0;
+    };
+    for (uint32_t d = 0; d < L; d++) {
+        uint32_t ei[BK];
+        for (uint32_t j = 0; j < BK; j++) ei[j] = NONE;
+        if (d < D) {
+            uint32_t a, e;
+            prefix_range(W, (k >> (63 - d)) ^ 1ull, d + 1, a, e);
+            const uint32_t m = e - a, c = min(m, BK);
+            const uint64_t off = m > BK ? mix(k ^ ((uint64_t)(d + 1) * 0x9E3779B97F4A7C15ull)) % m : 0ull;
+            for (uint32_t j = 0; j < c; j++) ei[j] = m > BK ? a + (uint32_t)((off + (uint64_t)j * m / BK) % m) : a + j;
+            cp[d] = (uint8_t)c;
+        } else if (d == D) {
+            uint32_t c = 0;
+            for (uint32_t x = lo; x < hi && c < BK; x++)
+                if (x != p) ei[c++] = x;
+            cp[D] = (uint8_t)c;
+        }
+        put(d, ei);  // (levels past my bucket: empty lines)
     }
-    uint32_t* ep = W.ent + ((size_t)p * L + D) * BK;
-    uint64_t* kp = W.ekey + ((size_t)p * L + D) * BK;
-    uint32_t c = 0;
-    for (uint32_t x = lo; x < hi && c < BK; x++)
-        if (x != p) { ep[c] = x; kp[c] = W.key[x]; c++; }
-    for (uint32_t j = c; j < BK; j++) { ep[j] = NONE; kp[j] = ~0ull; }
-    cp[D] = (uint8_t)c;
+    hp[0] = (uint32_t)k;
+    hp[1] = (uint32_t)(k >> 32);
+    hp[2] = D;
+    hp[3] = 0;
+    for (uint32_t w = 0; w < HDR_WORDS - 4; w++) {
+        uint32_t v = 0;
+        for (uint32_t b = 0; b < 4; b++)
+            if (4 * w + b < L) v |= (uint32_t)cp[4 * w + b] << (8 * b);
+        hp[4 + w] = v;
+    }
 }
+static_assert(L <= 4 * (HDR_WORDS - 4), "the level counts fit the header line");
 
 // The i-th set bit (ascending) of m (i < popcount(m)).
 __device__ __forceinline__ uint32_t nth_bit(uint32_t m, uint32_t i) {
@@ -178,9 +205,11 @@ __device__ __forceinline__ bool tail_less(const SwarmDev& W, const Tgt& t, uint3
 // indices and keys (sorted by XOR distance) and returns their number.
 template <uint32_t K>
 __device__ uint32_t peer_closest(const SwarmDev& W, uint32_t p, const Tgt& t, uint32_t count, uint32_t* oi, uint64_t* ok) {
-    const uint64_t k = W.key[p];
-    const uint32_t D = W.depth[p];
-    const uint8_t* cp = W.cnt + (size_t)p * L;
+    const uint32_t* hp = W.hdr + (size_t)p * HDR_WORDS;
+    const uint4 h0 = *reinterpret_cast<const uint4*>(hp);  // key, depth (the counts: the same line, cached)
+    const uint64_t k = ((uint64_t)h0.y << 32) | h0.x;
+    const uint32_t D = h0.z;
+    const uint8_t* cp = reinterpret_cast<const uint8_t*>(hp + 4);
     const uint32_t lv = (uint32_t)(__builtin_bitreverse64(k) & ((1ull << D) - 1));  // bit d = bit d of k from the top
     const uint32_t m1 = lv, m0 = ~lv & (uint32_t)((1ull << D) - 1);
     const uint32_t M = (uint32_t)__builtin_popcount(m1), B = D + 1;
@@ -222,8 +251,8 @@ __device__ uint32_t peer_closest(const SwarmDev& W, uint32_t p, const Tgt& t, ui
     auto load_level = [&](uint32_t P, Slots& S) {
         const uint32_t d = level(P);
         S.nb = cp[d];
-        const uint4* ep4 = reinterpret_cast<const uint4*>(W.ent + ((size_t)p * L + d) * BK);
-        const uint4* kp4 = reinterpret_cast<const uint4*>(W.ekey + ((size_t)p * L + d) * BK);
+        const uint4* ep4 = reinterpret_cast<const uint4*>(W.lvl + ((size_t)p * L + d) * LVL_WORDS);
+        const uint4* kp4 = ep4 + BK / 4;
 #pragma unroll
         for (int x = 0; x < 2; x++) {
             const uint4 u = ep4[x];
@@ -409,7 +438,7 @@ __global__ __launch_bounds__(BLOCK) void search_init_kernel(SwarmDev W, SearchDe
 }
 
 // one lane per (search, queried node): its findClosestNodes(t, 8), or nothing if it is offline
-__global__ __launch_bounds__(BLOCK) void search_query_kernel(SwarmDev W, SearchDev X) {
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(SW_QUERY_WPE, 8))) void search_query_kernel(SwarmDev W, SearchDev X) {
     const uint32_t g = blockIdx.x * BLOCK + threadIdx.x;
     if (g >= X.S * ALPHA) return;
     const uint32_t s = g / ALPHA;
@@ -677,12 +706,31 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(N == 16 ?
 
 }  // namespace
 
+// A search's device state (lists, flags, answers, its copies of the sources and targets) for up to `cap` lookups.
+// The swarm keeps the largest one a destroyed search left (kad_search_destroy) and the next kad_search_create of at
+// most that many lookups takes it instead of making its ~700 bytes per lookup of hipMalloc calls again (17 of them:
+// ~2.5 ms of a 1M-lookup run that converges in ~8 ms of kernels, tools/bench_swarm.py).
+struct SearchBufs {
+    std::vector<void*> owned;
+    SearchDev X{};
+    uint32_t* src = nullptr;
+    uint8_t* targets = nullptr;
+    uint32_t cap = 0;
+    void release() {
+        for (void* p : owned) (void)hipFree(p);
+        owned.clear();
+        cap = 0;
+    }
+};
 struct kad_swarm {
     int device = 0;
     SwarmDev W{};
     std::vector<void*> owned;
     uint64_t bytes = 0;
+    mutable std::mutex pool_mu;
+    mutable SearchBufs pool;  // (searches must not outlive their swarm: they read its tables)
     ~kad_swarm() {
+        pool.release();
         for (void* p : owned) (void)hipFree(p);
     }
 };
@@ -692,10 +740,8 @@ struct kad_search {
     const kad_swarm* sw = nullptr;
     SearchDev X{};
     hipStream_t stream = nullptr;
-    std::vector<void*> owned;
-    ~kad_search() {
-        for (void* p : owned) (void)hipFree(p);
-    }
+    SearchBufs bufs;
+    ~kad_search() { bufs.release(); }
 };
 
 namespace {
@@ -751,9 +797,8 @@ int kad_swarm_create(kad_swarm** out, int device, uint32_t n, const uint8_t* sor
     uint32_t* dt;
     int rc;
     if ((rc = alloc(&dk, n, s->owned, &s->bytes)) || (rc = alloc(&dt, 3ull * n, s->owned, &s->bytes)) ||
-        (rc = alloc(&s->W.depth, n, s->owned, &s->bytes)) || (rc = alloc(&s->W.cnt, (size_t)n * L, s->owned, &s->bytes)) ||
-        (rc = alloc(&s->W.ent, (size_t)n * L * BK, s->owned, &s->bytes)) ||
-        (rc = alloc(&s->W.ekey, (size_t)n * L * BK, s->owned, &s->bytes))) {
+        (rc = alloc(&s->W.hdr, (size_t)n * HDR_WORDS, s->owned, &s->bytes)) ||
+        (rc = alloc(&s->W.lvl, (size_t)n * L * LVL_WORDS, s->owned, &s->bytes))) {
         delete s;
         return rc;
     }
@@ -793,11 +838,15 @@ int kad_swarm_get_table(const kad_swarm* s, uint32_t peer, uint32_t* depth, uint
     if (!s || !depth || !counts || !entries) return err(KAD_ERR_INVALID, "NULL argument");
     if (peer >= s->W.n) return err(KAD_ERR_INVALID, "peer %u >= %u", peer, s->W.n);
     Guard g(s->device);
-    uint8_t d;
-    SW_TRY(hipMemcpy(&d, s->W.depth + peer, 1, hipMemcpyDeviceToHost));
-    SW_TRY(hipMemcpy(counts, s->W.cnt + (size_t)peer * L, L, hipMemcpyDeviceToHost));
-    SW_TRY(hipMemcpy(entries, s->W.ent + (size_t)peer * L * BK, 4ull * L * BK, hipMemcpyDeviceToHost));
-    *depth = d;
+    uint32_t h[HDR_WORDS];
+    std::vector<uint32_t> lv((size_t)L * LVL_WORDS);
+    SW_TRY(hipMemcpy(h, s->W.hdr + (size_t)peer * HDR_WORDS, sizeof h, hipMemcpyDeviceToHost));
+    SW_TRY(hipMemcpy(lv.data(), s->W.lvl + (size_t)peer * L * LVL_WORDS, 4 * lv.size(), hipMemcpyDeviceToHost));
+    *depth = h[2];
+    for (uint32_t d = 0; d < L; d++) {
+        counts[d] = (uint8_t)(h[4 + d / 4] >> (8 * (d % 4)));
+        for (uint32_t j = 0; j < BK; j++) entries[d * BK + j] = lv[(size_t)d * LVL_WORDS + j];
+    }
     return KAD_OK;
 }
 
@@ -830,21 +879,37 @@ int kad_search_create(kad_search** out, const kad_swarm* s, uint32_t S, const ui
         return err(KAD_ERR_INVALID, "offline_per_10k %u > 10000", offline_per_10k);
     }
     X.offline = offline_per_10k;
-    uint32_t* dsrc;
-    uint8_t* dt;
-    int rc;
-    if ((rc = alloc(&dsrc, S, x->owned)) || (rc = alloc(&dt, 20ull * S, x->owned)) ||
-        (rc = alloc(&X.li, (size_t)S * LST, x->owned)) || (rc = alloc(&X.lk, (size_t)S * LST, x->owned)) ||
-        (rc = alloc(&X.lq, (size_t)S * LST, x->owned)) || (rc = alloc(&X.lb, (size_t)S * LST, x->owned)) ||
-        (rc = alloc(&X.ln, S, x->owned)) || (rc = alloc(&X.overflow, 1, x->owned)) ||
-        (rc = alloc(&X.hops, S, x->owned)) || (rc = alloc(&X.done, S, x->owned)) ||
-        (rc = alloc(&X.sel, (size_t)S * ALPHA, x->owned)) || (rc = alloc(&X.ri, (size_t)S * ALPHA * BK, x->owned)) ||
-        (rc = alloc(&X.rk, (size_t)S * ALPHA * BK, x->owned)) || (rc = alloc(&X.rn, (size_t)S * ALPHA, x->owned)) ||
-        (rc = alloc(&X.active, 1, x->owned)) || (rc = alloc(&X.xo, (size_t)S * XO_CAP, x->owned)) ||
-        (rc = alloc(&X.xn, S, x->owned))) {
-        delete x;
-        return rc;
+    {
+        std::lock_guard<std::mutex> lk(s->pool_mu);
+        if (S && s->pool.cap >= S) std::swap(x->bufs, s->pool);  // (the pool is left empty)
     }
+    SearchBufs& B = x->bufs;
+    if (!B.cap) {
+        SearchDev& Y = B.X;
+        std::vector<void*>& o = B.owned;
+        const uint32_t C = S;
+        int rc;
+        if ((rc = alloc(&B.src, C, o)) || (rc = alloc(&B.targets, 20ull * C, o)) ||
+            (rc = alloc(&Y.li, (size_t)C * LST, o)) || (rc = alloc(&Y.lk, (size_t)C * LST, o)) ||
+            (rc = alloc(&Y.lq, (size_t)C * LST, o)) || (rc = alloc(&Y.lb, (size_t)C * LST, o)) ||
+            (rc = alloc(&Y.ln, C, o)) || (rc = alloc(&Y.overflow, 1, o)) || (rc = alloc(&Y.hops, C, o)) ||
+            (rc = alloc(&Y.done, C, o)) || (rc = alloc(&Y.sel, (size_t)C * ALPHA, o)) ||
+            (rc = alloc(&Y.ri, (size_t)C * ALPHA * BK, o)) || (rc = alloc(&Y.rk, (size_t)C * ALPHA * BK, o)) ||
+            (rc = alloc(&Y.rn, (size_t)C * ALPHA, o)) || (rc = alloc(&Y.active, 1, o)) ||
+            (rc = alloc(&Y.xo, (size_t)C * XO_CAP, o)) || (rc = alloc(&Y.xn, C, o))) {
+            delete x;
+            return rc;
+        }
+        B.cap = std::max<uint32_t>(C, 1);
+    }
+    {
+        const uint32_t S0 = X.S, off0 = X.offline;
+        X = B.X;
+        X.S = S0;
+        X.offline = off0;
+    }
+    uint32_t* dsrc = B.src;
+    uint8_t* dt = B.targets;
     if (S && (hipMemcpyAsync(dsrc, src, 4ull * S, hipMemcpyDefault, x->stream) != hipSuccess ||
               hipMemcpyAsync(dt, targets, 20ull * S, hipMemcpyDefault, x->stream) != hipSuccess)) {
         delete x;
@@ -923,7 +988,11 @@ int kad_search_get(const kad_search* x, uint32_t* list, uint8_t* queried, uint8_
 int kad_search_destroy(kad_search* x) {
     if (!x) return KAD_OK;
     Guard g(x->device);
-    (void)hipStreamSynchronize(x->stream);
+    if (hipStreamSynchronize(x->stream) == hipSuccess && x->sw && x->bufs.cap) {
+        // the buffers back to the swarm's pool (the larger of the two stays)
+        std::lock_guard<std::mutex> lk(x->sw->pool_mu);
+        if (x->bufs.cap > x->sw->pool.cap) std::swap(x->bufs, x->sw->pool);
+    }
     delete x;
     return KAD_OK;
 }
