@@ -4184,7 +4184,8 @@ __global__ __launch_bounds__(BLOCK) void find_bucket_kernel(DevTable T, const ui
 // NodeCache::getCachedNodes, one query per lane (node_cache.cpp:36-66): two-pointer walk from
 // lower_bound(t): p = lb-1 (or lb at begin), n = lb; take the closer (xorCmp(p, n) < 0 -> p);
 // taking begin() exhausts p; emit non-expired nodes, stop at count. (Serial form: counts > 16 and
-// the group kernel's rare fallback.)
+// the group kernel's rare fallback.) Inlined: as a call, the stack it needs made every kernel calling it ~2x slower
+// (profiles/r06/ncl_lane/ncl_lane10), although the count <= 14 line kernel runs 3-5 us faster without it (ABL 12).
 __device__ void nc_serial(const DevTable& T, const Target& t, uint32_t count, uint32_t* row, uint8_t* cp) {
     const uint32_t N = T.n;
     const uint32_t lb = N ? node_lower_bound(T, t) : 0;
@@ -5248,8 +5249,9 @@ __device__ __forceinline__ void store_rows_keys16(uint32_t* __restrict__ out_idx
 
 // ABL 1 (timing ablation only, KAD_NC_KERNEL=lane_abl1; results wrong): the lines and the answer, no wave path. ABL 9
 // (lane_abl9): the wave path's loads without its answers; ABL 11 (lane_abl11): the same and a whole row of plain stores
-// per missed query. ABL 5 (lane_stats): out_cnt = the step that answered (1: the line, 2: the wave path, 3: the wave
-// path's serial fallback).
+// per missed query; ABL 12 (lane_abl12): the wave path without its serial fallback (rows of walks past 32 steps a side
+// missing). ABL 5 (lane_stats): out_cnt = the step that answered (1: the line, 2: the wave path, 3: the wave path's
+// serial fallback).
 // WPE: the waves per SIMD the register allocation aims at (5: 85 VGPRs, no spill; 6 and 8 spill: A/B only). NT: threads
 // per workgroup (64: a wave that runs the wave path for a missed query holds only its own slot, not its block's).
 template <int ABL, bool DUAL, int WPE, int NT>
@@ -5282,12 +5284,13 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
             ok = ncl2_lane_answer(d, thi, count, rows + tid * NCL2_RS, m);
         }
     }
-    if (act && ok && out_cnt) out_cnt[i] = (uint8_t)m;
+    if (act && ok && out_cnt) out_cnt[i] = (uint8_t)(ABL == 5 ? 1u : m);
     meta[tid] = m | (ok ? 256u : 0u) | hv;
     if (NT > 64) __syncthreads(); else wave_sync();
     // the lanes the line could not answer (0.11 % of the queries at k = 14): one query at a time by the whole wave,
     // its target read again (wave-uniform) and its slot range from the line header when there is one. The first
     // one's target and window loads go out before the row store, each next one's before the current one's answer.
+    // (Run before the row store instead, the wave path measured the same: profiles/r06/ncl_lane/ncl_lane11.)
     uint64_t pend = ABL == 1 ? 0ull : __ballot(act && !ok);
     const uint64_t fm = DUAL ? __ballot(fam) : 0ull;
     Target u{};
@@ -5326,10 +5329,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
             if (lane < count) out_idx[(size_t)qc * count + lane] = (uint32_t)(wc.k0 ^ wc.k1 ^ uc.hi) + a0 + a1 + c6;
             continue;
         }
-        const bool wok = nc_answer(c6 ? T6 : T4, uc, a0, a1, wc, lane, qc, count, out_idx, out_cnt);
+        const bool wok = nc_answer(c6 ? T6 : T4, uc, a0, a1, wc, lane, qc, count, out_idx, out_cnt, ABL != 12);
         if (ABL == 5 && lane == 0 && out_cnt) out_cnt[qc] = wok ? 2 : 3;
     }
-    if (ABL == 5 && act && ok && out_cnt) out_cnt[i] = 1;
 }
 
 // NodeCache counts 17..64 for two families (af per query): nc_two_pass_kernel with the table chosen per
@@ -9772,6 +9774,9 @@ int kad_nc_closest_batch(const kad_table* t, const uint8_t* targets, uint32_t q,
                            t->d, t->d, nullptr, targets, q, count, out_idx, out_cnt);
     else if ((t->d.flags & TF_NCL) && ev && std::strcmp(ev, "lane_abl11") == 0 && count >= 1 && count <= NCL2_COUNT_MAX)
         hipLaunchKernelGGL((ncl2_lane_kernel<11, false, 5, 64>), dim3(grid64(q)), dim3(64), 0, (hipStream_t)stream,
+                           t->d, t->d, nullptr, targets, q, count, out_idx, out_cnt);
+    else if ((t->d.flags & TF_NCL) && ev && std::strcmp(ev, "lane_abl12") == 0 && count >= 1 && count <= NCL2_COUNT_MAX)
+        hipLaunchKernelGGL((ncl2_lane_kernel<12, false, 5, 64>), dim3(grid64(q)), dim3(64), 0, (hipStream_t)stream,
                            t->d, t->d, nullptr, targets, q, count, out_idx, out_cnt);
     else if ((t->d.flags & TF_NCL) && ev && std::strcmp(ev, "lane_stats") == 0 && count >= 1 && count <= NCL2_COUNT_MAX)
         hipLaunchKernelGGL((ncl2_lane_kernel<5, false, 5, 64>), dim3(grid64(q)), dim3(64), 0, (hipStream_t)stream,

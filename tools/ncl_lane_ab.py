@@ -58,7 +58,8 @@ def checksum(k):
 forms = [("wave1", {"KAD_NCL2_WPE": "5"}), ("wpe6", {"KAD_NCL2_WPE": "6"}), ("block4", {"KAD_NCL2_WPE": "256"})]
 if ABL:
     forms += [("lane_abl1", {"KAD_NC_KERNEL": "lane_abl1"}), ("lane_abl9", {"KAD_NC_KERNEL": "lane_abl9"}),
-              ("lane_abl11", {"KAD_NC_KERNEL": "lane_abl11"}), ("lines_wave", {"KAD_NC_KERNEL": "lines_wave"})]
+              ("lane_abl11", {"KAD_NC_KERNEL": "lane_abl11"}),
+              ("lane_abl12", {"KAD_NC_KERNEL": "lane_abl12"}), ("lines_wave", {"KAD_NC_KERNEL": "lines_wave"})]
 for k in (14, 8, 1):
     for name, env in forms:
         for v in ("KAD_NCL2_WPE", "KAD_NC_KERNEL"):
@@ -66,7 +67,7 @@ for k in (14, 8, 1):
         os.environ.update(env)
         T.nc_closest(tgs[0], k)
         res[f"nc_k{k}_{name}_us"] = timed(k)
-        if not name.startswith("lane_abl"):
+        if not name.startswith("lane_abl") or name == "lane_abl12":
             res[f"nc_k{k}_{name}_sum"] = checksum(k)
     if ABL:
         os.environ.pop("KAD_NCL2_WPE", None)
