@@ -7,7 +7,8 @@ rocprofv3 --pmc pass stays short:
            split-policy table of 4M nodes: rt_sl_kernel (k=8), rt_sl16_kernel (k=14), rt_gl32q_kernel (k=32)
   shard    the north-star step at N = 8 on rank 0's shard of the 100M-node table: rt_shard_kernel over the replicated
            1M batch into 8 home blocks (k = 8 and 32), gather_scatter_link_kernel + gather_merge_kernel over 8 blocks
-  swarm    config 5 at 2M peers: search_init / search_query / search_merge over 256k lookups to convergence
+  swarm    config 5 at 2M peers, 10 % offline: search_init / search_query / search_merge over 256k lookups to convergence
+  swarm0   the same with every peer online (the 16-register merge)
   refresh  the live refresh: rf_nodes_kernel over 300 refreshes of the bench shard at a moving `now`
   route    the owner-routed serving form: route_pack_kernel (N = 8), route_unpack_kernel (k = 8), the owner's query with
            packed rows (rt_ws_packed_kernel) over 8 received blocks, route_unpack_packed4_kernel
@@ -132,6 +133,28 @@ def mode_swarm():
     W.close()
 
 
+def mode_swarm0():
+    """config 5 at 2M peers with every peer online (the 16-register merge), 256k lookups to convergence"""
+    from opendht_amd.swarm import Swarm
+
+    peers, lookups = 2_000_000, 1 << 18
+    ids, _ = S.sort_ids(S.random_ids(peers, 0x0D470500))
+    W = Swarm(ids, device=0)
+    rng = np.random.default_rng(9)
+    src = torch.from_numpy(rng.integers(0, peers, lookups).astype(np.int32)).to(dev)
+    tg = torch.from_numpy(S.random_targets(lookups, seed=0x0D470501)).to(dev)
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    X = W.search(src, tg, 0)
+    hops = X.run()
+    b.record()
+    torch.cuda.synchronize()
+    res["swarm0_2M_256k_ms"] = round(a.elapsed_time(b), 3)
+    res["swarm0_hops"] = int(hops)
+    X.close()
+    W.close()
+
+
 def mode_refresh():
     import bench
 
@@ -198,6 +221,6 @@ def mode_route():
 
 
 if __name__ == "__main__":
-    {"lines": mode_lines, "shard": mode_shard, "swarm": mode_swarm, "refresh": mode_refresh,
+    {"lines": mode_lines, "shard": mode_shard, "swarm": mode_swarm, "swarm0": mode_swarm0, "refresh": mode_refresh,
      "route": mode_route}[sys.argv[1] if len(sys.argv) > 1 else "lines"]()
     print(json.dumps(res), flush=True)
