@@ -2,7 +2,7 @@
 --stats for per-kernel times): rank 0's shard of the 100M-node table (global buckets [0, B/8), no halo), the shard
 kernel over a replicated 1M batch into 8 home blocks, and the finish (kad_rt_home_finish_reset: gather_scatter_link +
 gather_merge) over 8 blocks addressed to home 0, as bench.py's n8_step_model builds them. One JSON line of event
-times.
+times and row checksums.
 
     python tools/ns_finish_probe.py [reps]
 """
@@ -54,6 +54,7 @@ def main():
         b.record(stream)
         torch.cuda.synchronize()
         res[f"finish_k{k}_us"] = a.elapsed_time(b) / reps * 1e3
+        res[f"finish_k{k}_rows_sum"] = int(oi.to(torch.int64).sum().item()) * 31 + int(oc.to(torch.int64).sum().item())
         res[f"parts_received_k{k}"] = ex.parts_received()
         ctr = ex.send.view(8, ex.block)[:, ex.ctr_off:ex.ctr_off + 10 * 32]
         a.record(stream)
