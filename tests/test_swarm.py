@@ -351,3 +351,50 @@ def test_swarm_gpu_10m_peers(gpu):
         assert bad.any()
         X.close()
     M.close()
+
+
+@pytest.mark.gpu
+def test_swarm_gpu_search_state_pool(gpu):
+    """kad_search_destroy hands a search's device state to its swarm and the next kad_search_create of at most as
+    many lookups reuses it: searches of shrinking, equal and growing sizes, two alive at once, with and without
+    offline peers, each run to the end and equal to the oracle's search (stale state from the previous user of the
+    buffers would show in the lists, flags, counts or hop counters)."""
+    from opendht_amd.swarm import Swarm
+    n = 30_000
+    ids = _swarm_ids(n, 0x5A9)
+    M = O.SwarmModel(ids)
+    rng = np.random.default_rng(11)
+
+    def run(W, src, tg, off):
+        X = W.search(torch.from_numpy(src.view(np.int32)).to(gpu), torch.from_numpy(tg).to(gpu), off)
+        X.run()
+        got = X.get(full=True)
+        return X, got
+
+    with Swarm(ids, device=gpu.index or 0) as W:
+        plan = [(3000, 0), (1000, 1500), (1000, 0), (3000, 4000), (5000, 0)]
+        for j, (size, off) in enumerate(plan):
+            src = rng.integers(0, n, size).astype(np.uint32)
+            src = src[~_offline(src, off)]
+            tg = S.random_targets(src.shape[0], seed=40 + j)
+            X, got = run(W, src, tg, off)
+            want = M.search_ex(src, tg, off)
+            for a, b, name in zip(got[:6], want, ("list", "queried", "bad", "n", "hops", "done")):
+                np.testing.assert_array_equal(a, b, err_msg=f"search {j} ({size}, {off}): {name}")
+            X.close()
+        # two searches alive at once: the first takes the pooled state, the second its own
+        src_a = rng.integers(0, n, 2000).astype(np.uint32)
+        src_b = rng.integers(0, n, 2500).astype(np.uint32)
+        tg_a, tg_b = S.random_targets(2000, seed=50), S.random_targets(2500, seed=51)
+        Xa = W.search(torch.from_numpy(src_a.view(np.int32)).to(gpu), torch.from_numpy(tg_a).to(gpu))
+        Xb = W.search(torch.from_numpy(src_b.view(np.int32)).to(gpu), torch.from_numpy(tg_b).to(gpu))
+        Xa.run()
+        Xb.run()
+        for X, src, tg in ((Xa, src_a, tg_a), (Xb, src_b, tg_b)):
+            got = X.get(full=True)
+            want = M.search_ex(src, tg, 0)
+            for a, b, name in zip(got[:6], want, ("list", "queried", "bad", "n", "hops", "done")):
+                np.testing.assert_array_equal(a, b, err_msg=f"concurrent: {name}")
+        Xa.close()
+        Xb.close()
+    M.close()
