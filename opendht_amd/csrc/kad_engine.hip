@@ -4185,7 +4185,7 @@ __global__ __launch_bounds__(BLOCK) void find_bucket_kernel(DevTable T, const ui
 // lower_bound(t): p = lb-1 (or lb at begin), n = lb; take the closer (xorCmp(p, n) < 0 -> p);
 // taking begin() exhausts p; emit non-expired nodes, stop at count. (Serial form: counts > 16 and
 // the group kernel's rare fallback.) Inlined: as a call, the stack it needs made every kernel calling it ~2x slower
-// (profiles/r06/ncl_lane/ncl_lane10), although the count <= 14 line kernel runs 3-5 us faster without it (ABL 12).
+// (profiles/r06/ncl_lane/ncl_lane10).
 __device__ void nc_serial(const DevTable& T, const Target& t, uint32_t count, uint32_t* row, uint8_t* cp) {
     const uint32_t N = T.n;
     const uint32_t lb = N ? node_lower_bound(T, t) : 0;
@@ -5314,6 +5314,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
     };
     if (pend) fetch((uint32_t)__builtin_ctzll(pend));
     store_rows_keys16<NT>(out_idx, q, count, rows, meta, base);
+    uint64_t failed = 0;  // lanes whose query the wave path could not settle
     while (pend) {
         pend &= pend - 1;
         const Target uc = u;
@@ -5329,8 +5330,19 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
             if (lane < count) out_idx[(size_t)qc * count + lane] = (uint32_t)(wc.k0 ^ wc.k1 ^ uc.hi) + a0 + a1 + c6;
             continue;
         }
-        const bool wok = nc_answer(c6 ? T6 : T4, uc, a0, a1, wc, lane, qc, count, out_idx, out_cnt, ABL != 12);
+        const bool wok = nc_answer(c6 ? T6 : T4, uc, a0, a1, wc, lane, qc, count, out_idx, out_cnt, false);
         if (ABL == 5 && lane == 0 && out_cnt) out_cnt[qc] = wok ? 2 : 3;
+        if (!wok) failed |= 1ull << (qc - (i - lane));  // (wave-uniform)
+    }
+    // the walks the wave path could not settle (longer than 32 steps a side, or 64-bit ties it cannot order: never on
+    // the bench shard): lane 0's serial walk, after the loop (its code costs ~1 us per 1M at k = 14 although it never
+    // runs, inside the loop or here: ABL 12, profiles/r06/ncl_lane/ncl_lane13)
+    while (ABL != 12 && failed) {
+        const uint32_t l = (uint32_t)__builtin_ctzll(failed);
+        failed &= failed - 1;
+        const uint32_t qf = i - lane + l;
+        const DevTable& T = (DUAL && ((fm >> l) & 1ull)) ? T6 : T4;
+        if (lane == 0) nc_serial(T, load_target(targets, qf), count, out_idx + (size_t)qf * count, out_cnt ? out_cnt + qf : nullptr);
     }
 }
 

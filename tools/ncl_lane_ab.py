@@ -60,8 +60,11 @@ if ABL:
     forms += [("lane_abl1", {"KAD_NC_KERNEL": "lane_abl1"}), ("lane_abl9", {"KAD_NC_KERNEL": "lane_abl9"}),
               ("lane_abl11", {"KAD_NC_KERNEL": "lane_abl11"}),
               ("lane_abl12", {"KAD_NC_KERNEL": "lane_abl12"}), ("lines_wave", {"KAD_NC_KERNEL": "lines_wave"})]
+ROUNDS = int(os.environ.get("NCL_ROUNDS", "1"))  # >1: every form again in a second pass (order effects), _r<i>
 for k in (14, 8, 1):
-    for name, env in forms:
+    for rnd, (name, env) in [(r, f) for r in range(ROUNDS) for f in forms]:
+        if rnd:
+            name = f"{name}_r{rnd + 1}"
         for v in ("KAD_NCL2_WPE", "KAD_NC_KERNEL"):
             os.environ.pop(v, None)
         os.environ.update(env)
