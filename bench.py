@@ -57,7 +57,7 @@ def parse_args(argv=None):
                     help="headline only: no cold-cache pass, refresh, allgather variant (profiling runs)")
     ap.add_argument("--no-allgather", action="store_true")
     ap.add_argument("--no-graph", action="store_true", help="issue the K steps one by one instead of one HIP graph")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r05.json"))
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r06.json"))
     ap.add_argument("--gather-json", default=os.path.join(ROOT, "profiles", "r03_mb_gather_nt.json"))
     ap.add_argument("--plumbing", action="store_true",
                     help="launcher/rendezvous check without a GPU: gloo ranks, barrier, max-over-ranks, one line")
