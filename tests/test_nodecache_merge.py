@@ -34,3 +34,87 @@ def test_greedy_merge_prefix_max_lemma():
         order, places = _by_prefix_max(vals[:k], vals[k:])
         assert order == _greedy(vals[:k], vals[k:])
         assert places == list(range(len(vals)))
+
+
+def _walk_window(keys, exp, p, t, count):
+    """NodeCache::getCachedNodes' two-pointer walk (node_cache.cpp:36-66) over a window of sorted keys with lb = p,
+    stopped at the window's ends: the non-expired positions it emits, and whether it ran off an end of the window."""
+    out, l, r = [], p - 1, p
+    while len(out) < count and (l >= 0 or r < len(keys)):
+        if l < 0:
+            e, r = r, r + 1
+        elif r >= len(keys):
+            e, l = l, l - 1
+        elif (keys[l] ^ t) < (keys[r] ^ t):
+            e, l = l, l - 1
+        else:
+            e, r = r, r + 1
+        if not exp[e]:
+            out.append(e)
+    return out
+
+
+def _lane_answer(keys, exp, p, t, count, trunc_left, trunc_right):
+    """ncl2_lane_answer's algorithm (kad_engine.hip) on one line, in integers: keys as (run max << 8 | side << 7 |
+    tie-break << 1 | expired) with the tie-break 63 - e on the left and e on the right, the 37 keys followed by NONE
+    as a bitonic sequence of 64 (no shift by p), one half-cleaner at h = 32 and five levels of 16 compare-exchanges,
+    then the first `count` non-expired keys up to the smaller end key of a truncated side. Returns the positions it
+    emits, or None where the kernel sends the query to the wave path."""
+    NONE, S = 0xFFFFFFFF, len(keys)
+    d = [((k ^ t) << 8) | e for k, e in zip(keys, exp)]
+    k = list(d)
+    run = 0
+    for e in range(p - 1, -1, -1):
+        run = max(run, d[e] & ~255)
+        k[e] = run | ((63 - e) << 1) | (d[e] & 1)
+    run = 0
+    for e in range(p, S):
+        run = max(run, d[e] & ~255)
+        k[e] = run | 128 | (e << 1) | (d[e] & 1)
+    lim = min(k[0] | 1 if trunc_left else NONE, k[S - 1] | 1 if trunc_right else NONE)
+    seq = k + [NONE] * (64 - S)
+    # the sequence is bitonic: descending over the left run, ascending over the right run, then NONE
+    w = [min(seq[r], seq[r + 32]) for r in range(32)]
+    h = 16
+    while h:
+        for r in range(32):
+            if r & h == 0 and w[r] > w[r + h]:
+                w[r], w[r + h] = w[r + h], w[r]
+        h //= 2
+    assert w == sorted(k)[:32]
+    keep = [x for x in w if x <= lim and not x & 1]
+    if len(keep) < count and (lim != NONE or w[31] != NONE):
+        return None
+    return [(x >> 1) & 63 if x & 128 else 63 - ((x >> 1) & 63) for x in keep[:count]]
+
+
+def test_lane_answer_is_the_walk():
+    """The count <= 14 NodeCache lane kernel's walk (bitonic merge of the two runs by run maximum, no window shift)
+    equals the reference's two-pointer walk wherever it answers, and sends a query to the wave path only when the
+    walk may leave the line."""
+    rnd = random.Random(11)
+    answered = 0
+    for _ in range(4000):
+        S = 37
+        keys = sorted(rnd.sample(range(1 << 24), S))
+        exp = [rnd.random() < 0.12 for _ in range(S)]
+        p = rnd.randint(11, 26)
+        t = rnd.randint(keys[p - 1] + 1, keys[p]) if keys[p] > keys[p - 1] + 1 else keys[p]
+        count = rnd.randint(1, 14)
+        tl, tr = rnd.random() < 0.8, rnd.random() < 0.8
+        got = _lane_answer(keys, exp, p, t, count, tl, tr)
+        walk = _walk_window(keys, exp, p, t, count)
+        if got is None:
+            continue
+        answered += 1
+        assert got == walk
+        # an answer the kernel trusts never depends on nodes beyond a truncated end of the line: the same walk over
+        # the line with up to 16 more sorted nodes past each truncated end (any keys, any expired flags)
+        nl = rnd.randint(1, 16) if tl else 0
+        nr = rnd.randint(1, 16) if tr else 0
+        left = sorted(rnd.sample(range(keys[0]), min(nl, keys[0]))) if nl else []
+        right = sorted(rnd.sample(range(keys[-1] + 1, 1 << 25), nr)) if nr else []
+        wide = _walk_window(left + keys + right, [rnd.random() < 0.5 for _ in left] + exp +
+                            [rnd.random() < 0.5 for _ in right], p + len(left), t, count)
+        assert [e - len(left) for e in wide] == got
+    assert answered > 3000
