@@ -5145,6 +5145,11 @@ __global__ __launch_bounds__(BLOCK) void nc_line_kernel(DevTable T4, DevTable T6
 // from the key; the lane writes raw keys into its LDS row and the block's store decodes them.
 // ---------------------------------------------------------------------------------------
 constexpr uint32_t NCL2_RS = 17;  // LDS row stride in words (16 keys + 1: the lanes' rows fall into different banks)
+#ifndef KAD_NCL2_STEPS
+#define KAD_NCL2_STEPS 24u
+#endif
+constexpr uint32_t NCL2_STEPS = KAD_NCL2_STEPS;  // walk steps the lane kernel sorts (24, or 32: the whole lower half)
+static_assert(NCL2_STEPS == 24 || NCL2_STEPS == 32, "lane kernel steps");
 
 __device__ __forceinline__ uint32_t ncl2_key24x(const uint32_t (&d)[32], int e) {
     // key24 of line position e (bytes 16 + 3e .. 18 + 3e) as key24 << 8, low byte zero: one byte permute
@@ -5195,20 +5200,40 @@ __device__ __forceinline__ bool ncl2_lane_answer(const uint32_t (&d)[32], uint64
     // the 32 smallest of the bitonic 64 (k, then NONE), sorted
 #pragma unroll
     for (int r = 0; r + 32 < S; r++) k[r] = min(k[r], k[r + 32]);
+    // the first NCL2_STEPS of those sorted: the 16 smallest (a half-cleaner at 16, then four levels), and the 8 next
+    // (the upper 16 are bitonic: the smaller half of one more half-cleaner, then three levels). 24 walk steps hold
+    // count <= 14 non-expired nodes unless more than 10 of them are expired (the wave path then answers)
+    if (NCL2_STEPS == 32) {
 #pragma unroll
-    for (int h = 16; h >= 1; h >>= 1)
+        for (int h = 16; h >= 1; h >>= 1)
 #pragma unroll
-        for (int r = 0; r < 32; r++)
-            if ((r & h) == 0) cx(k[r], k[r + h]);
+            for (int r = 0; r < 32; r++)
+                if ((r & h) == 0) cx(k[r], k[r + h]);
+    } else {
+#pragma unroll
+        for (int r = 0; r < 16; r++) cx(k[r], k[r + 16]);
+#pragma unroll
+        for (int h = 8; h >= 1; h >>= 1)
+#pragma unroll
+            for (int r = 0; r < 16; r++)
+                if ((r & h) == 0) cx(k[r], k[r + h]);
+#pragma unroll
+        for (int r = 16; r < 24; r++) k[r] = min(k[r], k[r + 8]);
+#pragma unroll
+        for (int h = 4; h >= 1; h >>= 1)
+#pragma unroll
+            for (int r = 16; r < 24; r++)
+                if ((r & h) == 0) cx(k[r], k[r + h]);
+    }
     uint32_t have = 0;
 #pragma unroll
-    for (int r = 0; r < 32; r++) {
+    for (int r = 0; r < (int)NCL2_STEPS; r++) {
         const bool keep = k[r] <= lim && !(k[r] & 1u);
         if (keep && have < count) lrow[have] = k[r];
         have += keep ? 1u : 0u;
     }
     m = min(count, have);
-    ex |= have < count && (lim != NONE || k[31] != NONE);  // the walk goes on past the line / step 32
+    ex |= have < count && (lim != NONE || k[NCL2_STEPS - 1] != NONE);  // the walk goes on past the line / the steps
     return !ex;
 }
 

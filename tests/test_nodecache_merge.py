@@ -54,11 +54,12 @@ def _walk_window(keys, exp, p, t, count):
     return out
 
 
-def _lane_answer(keys, exp, p, t, count, trunc_left, trunc_right):
+def _lane_answer(keys, exp, p, t, count, trunc_left, trunc_right, steps=24):
     """ncl2_lane_answer's algorithm (kad_engine.hip) on one line, in integers: keys as (run max << 8 | side << 7 |
     tie-break << 1 | expired) with the tie-break 63 - e on the left and e on the right, the 37 keys followed by NONE
-    as a bitonic sequence of 64 (no shift by p), one half-cleaner at h = 32 and five levels of 16 compare-exchanges,
-    then the first `count` non-expired keys up to the smaller end key of a truncated side. Returns the positions it
+    as a bitonic sequence of 64 (no shift by p), one half-cleaner at h = 32, then the first `steps` sorted (24: the
+    kernel's KAD_NCL2_STEPS; 32: five levels of 16 compare-exchanges), then the first `count` non-expired keys up to
+    the smaller end key of a truncated side. Returns the positions it
     emits, or None where the kernel sends the query to the wave path."""
     NONE, S = 0xFFFFFFFF, len(keys)
     d = [((k ^ t) << 8) | e for k, e in zip(keys, exp)]
@@ -75,15 +76,28 @@ def _lane_answer(keys, exp, p, t, count, trunc_left, trunc_right):
     seq = k + [NONE] * (64 - S)
     # the sequence is bitonic: descending over the left run, ascending over the right run, then NONE
     w = [min(seq[r], seq[r + 32]) for r in range(32)]
-    h = 16
-    while h:
-        for r in range(32):
-            if r & h == 0 and w[r] > w[r + h]:
-                w[r], w[r + h] = w[r + h], w[r]
-        h //= 2
-    assert w == sorted(k)[:32]
+
+    def clean(lo, n, h):  # half-cleaners h, h/2, .., 1 over w[lo:lo+n]
+        while h:
+            for r in range(lo, lo + n):
+                if (r - lo) & h == 0 and w[r] > w[r + h]:
+                    w[r], w[r + h] = w[r + h], w[r]
+            h //= 2
+
+    if steps == 32:
+        clean(0, 32, 16)
+    else:  # KAD_NCL2_STEPS = 24: the 16 smallest sorted, then the smaller half of the upper 16 sorted
+        for r in range(16):
+            if w[r] > w[r + 16]:
+                w[r], w[r + 16] = w[r + 16], w[r]
+        clean(0, 16, 8)
+        for r in range(16, 24):
+            w[r] = min(w[r], w[r + 8])
+        clean(16, 8, 4)
+        w = w[:24]
+    assert w == sorted(k)[:steps]
     keep = [x for x in w if x <= lim and not x & 1]
-    if len(keep) < count and (lim != NONE or w[31] != NONE):
+    if len(keep) < count and (lim != NONE or w[steps - 1] != NONE):
         return None
     return [(x >> 1) & 63 if x & 128 else 63 - ((x >> 1) & 63) for x in keep[:count]]
 
@@ -102,7 +116,7 @@ def test_lane_answer_is_the_walk():
         t = rnd.randint(keys[p - 1] + 1, keys[p]) if keys[p] > keys[p - 1] + 1 else keys[p]
         count = rnd.randint(1, 14)
         tl, tr = rnd.random() < 0.8, rnd.random() < 0.8
-        got = _lane_answer(keys, exp, p, t, count, tl, tr)
+        got = _lane_answer(keys, exp, p, t, count, tl, tr, steps=rnd.choice((24, 32)))
         walk = _walk_window(keys, exp, p, t, count)
         if got is None:
             continue
