@@ -688,13 +688,158 @@ __device__ __forceinline__ bool merge_lookup(const SwarmDev& W, const SearchDev&
     }
 }
 
+// (key, id) compare-exchange: the smaller key first (equal keys stay: the caller sends ties to the sequential form)
+__device__ __forceinline__ void cx_kid(uint64_t& ka, uint32_t& ia, uint64_t& kb, uint32_t& ib) {
+    const bool sw = kb < ka;
+    const uint64_t k0 = sw ? kb : ka, k1 = sw ? ka : kb;
+    const uint32_t i0 = sw ? ib : ia, i1 = sw ? ia : ib;
+    ka = k0; kb = k1; ia = i0; ib = i1;
+}
+
+// The all-online hop's merge as a sorting network (runs where every peer answers). With no bad node and no silent
+// peer, Search::insertNode's sequential inserts (dht.cpp:961-1047) keep exactly the SEARCH_NODES closest of the list
+// and the answers (an insert beyond a full list is refused, a full list drops its farthest after an insert, a node
+// already in the list is skipped): the result does not depend on the order of the inserts. So each queried node's
+// block of <= 8 answers (sorted, from findClosestNodes) loses our own ID and the nodes already in the list (index
+// compares), is re-sorted (19 compare-exchanges), and merges with the 16-slot list as one bitonic half-cleaner (the
+// list ascending, the block descending) and four levels: ~560 VALU operations a block where the sequential inserts
+// took ~250 each answer. Equal 64-bit distances of different nodes (their order needs the 160-bit tails) are adjacent
+// after each merge; a lookup that has one is left untouched with done = 4 and the sequential form merges it next.
+// Queried flags travel in bit 31 of the node index.
+__device__ __forceinline__ bool merge_lookup_net(const SwarmDev& W, const SearchDev& X, uint32_t s) {
+    constexpr uint32_t QB = 0x80000000u, IM = 0x7FFFFFFFu;
+    const uint64_t MAXK = ~0ull;
+    const Tgt t = load_tgt(X.targets, s);
+    const uint32_t n0 = X.ln[s];
+    uint32_t li[16];
+    uint64_t lk[16];
+    {
+        const uint4* pi = reinterpret_cast<const uint4*>(X.li + (size_t)s * LST);
+        const uint4* pk = reinterpret_cast<const uint4*>(X.lk + (size_t)s * LST);
+#pragma unroll
+        for (uint32_t x = 0; x < 4; x++) {
+            const uint4 u = 4 * x < n0 ? pi[x] : make_uint4(NONE, NONE, NONE, NONE);
+            li[4 * x] = u.x; li[4 * x + 1] = u.y; li[4 * x + 2] = u.z; li[4 * x + 3] = u.w;
+        }
+#pragma unroll
+        for (uint32_t x = 0; x < 8; x++) {
+            const uint4 u = 2 * x < n0 ? pk[x] : make_uint4(~0u, ~0u, ~0u, ~0u);
+            lk[2 * x] = 2 * x < n0 ? (((uint64_t)u.y << 32) | u.x) ^ t.hi : MAXK;
+            lk[2 * x + 1] = 2 * x + 1 < n0 ? (((uint64_t)u.w << 32) | u.z) ^ t.hi : MAXK;
+        }
+    }
+    const uint32_t qm0 = load_flags(X.lq, s, n0);
+#pragma unroll
+    for (uint32_t k = 0; k < 16; k++)
+        if (k < n0 && ((qm0 >> k) & 1u)) li[k] |= QB;
+    const uint32_t rn4 = *reinterpret_cast<const uint32_t*>(X.rn + (size_t)s * ALPHA);  // (ALPHA = 4)
+    const uint32_t src = X.src[s];
+    bool tie = false;
+#pragma unroll
+    for (uint32_t k = 0; k + 1 < 16; k++) tie |= li[k + 1] != NONE && lk[k] == lk[k + 1];
+    Answers A;
+#pragma unroll 1
+    for (uint32_t a = 0; a < ALPHA; a++) {  // (not unrolled: one block's answers in registers at a time)
+        const uint32_t rn = (rn4 >> (8 * a)) & 255u;
+        load_answers(X, s * ALPHA + a, rn, A);
+        uint64_t bk[BK];
+        uint32_t bi[BK];
+#pragma unroll
+        for (uint32_t j = 0; j < BK; j++) {
+            const uint32_t r = A.r[j];
+            bool drop = j >= rn || r == src;  // deserializeNodes drops our own ID (network_engine.cpp:798-799)
+#pragma unroll
+            for (uint32_t k = 0; k < 16; k++) drop |= (li[k] & IM) == r;  // already in the list (empty slots: IM)
+            bk[j] = drop ? MAXK : A.k[j] ^ t.hi;
+            bi[j] = drop ? NONE : r;
+        }
+        // Batcher's odd-even merge sort of 8 (the block was sorted; the dropped entries leave MAX holes)
+        cx_kid(bk[0], bi[0], bk[1], bi[1]); cx_kid(bk[2], bi[2], bk[3], bi[3]);
+        cx_kid(bk[4], bi[4], bk[5], bi[5]); cx_kid(bk[6], bi[6], bk[7], bi[7]);
+        cx_kid(bk[0], bi[0], bk[2], bi[2]); cx_kid(bk[1], bi[1], bk[3], bi[3]);
+        cx_kid(bk[4], bi[4], bk[6], bi[6]); cx_kid(bk[5], bi[5], bk[7], bi[7]);
+        cx_kid(bk[1], bi[1], bk[2], bi[2]); cx_kid(bk[5], bi[5], bk[6], bi[6]);
+        cx_kid(bk[0], bi[0], bk[4], bi[4]); cx_kid(bk[1], bi[1], bk[5], bi[5]);
+        cx_kid(bk[2], bi[2], bk[6], bi[6]); cx_kid(bk[3], bi[3], bk[7], bi[7]);
+        cx_kid(bk[2], bi[2], bk[4], bi[4]); cx_kid(bk[3], bi[3], bk[5], bi[5]);
+        cx_kid(bk[1], bi[1], bk[2], bi[2]); cx_kid(bk[3], bi[3], bk[4], bi[4]); cx_kid(bk[5], bi[5], bk[6], bi[6]);
+        // the 16 smallest of (list ascending, block descending): one half-cleaner, then four levels
+#pragma unroll
+        for (uint32_t i = 8; i < 16; i++) {
+            const bool sw = bk[15 - i] < lk[i];
+            lk[i] = sw ? bk[15 - i] : lk[i];
+            li[i] = sw ? bi[15 - i] : li[i];
+        }
+#pragma unroll
+        for (uint32_t h = 8; h >= 1; h >>= 1)
+#pragma unroll
+            for (uint32_t r = 0; r < 16; r++)
+                if ((r & h) == 0) cx_kid(lk[r], li[r], lk[r + h], li[r + h]);
+#pragma unroll
+        for (uint32_t k = 0; k + 1 < 16; k++) tie |= li[k + 1] != NONE && lk[k] == lk[k + 1];
+    }
+    if (tie) {  // the sequential form (search_merge_kernel<false, 16, true>) merges this lookup
+        X.done[s] = 4;
+        return false;
+    }
+    uint32_t n = 0, qm = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < SN; k++) {
+        n += li[k] != NONE ? 1u : 0u;
+        qm |= (li[k] != NONE && (li[k] & QB)) ? 1u << k : 0u;
+        li[k] = li[k] != NONE ? li[k] & IM : NONE;
+    }
+    X.hops[s] += 1;
+    // Search::isSynced: the first TARGET_NODES nodes answered (no bad node here)
+    const uint32_t nm = lo_mask(n);
+    uint32_t first8 = nm;
+    {
+        uint32_t rest = nm;
+#pragma unroll
+        for (uint32_t k = 0; k < BK; k++) rest &= rest - 1u;
+        first8 &= ~rest;
+    }
+    const bool synced = (first8 & ~qm) == 0;
+    if (synced && first8) X.done[s] = 1;
+    else select_next(X, s, n, qm, 0u, li);
+    X.ln[s] = (uint8_t)n;
+    const uint32_t wn = max(n, n0);  // pieces above it hold the padding already
+    {
+        uint4* pi = reinterpret_cast<uint4*>(X.li + (size_t)s * LST);
+        uint4* pk = reinterpret_cast<uint4*>(X.lk + (size_t)s * LST);
+#pragma unroll
+        for (uint32_t x = 0; x < 4; x++)
+            if (4 * x < wn)
+                pi[x] = make_uint4(4 * x < n ? li[4 * x] : NONE, 4 * x + 1 < n ? li[4 * x + 1] : NONE,
+                                   4 * x + 2 < n ? li[4 * x + 2] : NONE, 4 * x + 3 < n ? li[4 * x + 3] : NONE);
+#pragma unroll
+        for (uint32_t x = 0; x < 8; x++) {
+            if (2 * x >= wn) continue;
+            const uint64_t k0 = 2 * x < n ? lk[2 * x] ^ t.hi : ~0ull, k1 = 2 * x + 1 < n ? lk[2 * x + 1] ^ t.hi : ~0ull;
+            pk[x] = make_uint4((uint32_t)k0, (uint32_t)(k0 >> 32), (uint32_t)k1, (uint32_t)(k1 >> 32));
+        }
+    }
+    store_flags(X.lq, s, qm, n, wn);
+    store_flags(X.lb, s, 0u, n, wn);
+    return !X.done[s];
+}
+
+__global__ __launch_bounds__(BLOCK) void search_merge_net_kernel(SwarmDev W, SearchDev X) {
+    const uint32_t s = blockIdx.x * BLOCK + threadIdx.x;
+    const bool running = s < X.S && !X.done[s] && merge_lookup_net(W, X, s);
+    const uint64_t m = __ballot(running);
+    if ((threadIdx.x & 63u) == 0 && m) atomicAdd(X.active, (uint32_t)__builtin_popcountll(m));
+}
+
 // N = 16 (the narrow form): for runs where every peer answers (swarm_offline never true), so that no list holds a bad
 // node and no lookup meets a silent peer: a list keeps at most SEARCH_NODES + 1 entries through a hop, in 16
 // registers instead of LST (and the kernel in a quarter of the VGPRs). N = LST: any run.
-template <bool FUSED, uint32_t N>
+// RETRY: only the lookups search_merge_net_kernel left with done = 4 (a 64-bit distance tie), this hop.
+template <bool FUSED, uint32_t N, bool RETRY = false>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(N == 16 ? SW_NARROW_WPE : 1, 8))) void search_merge_kernel(SwarmDev W, SearchDev X) {
     const uint32_t s = blockIdx.x * BLOCK + threadIdx.x;
-    const bool live = s < X.S && !X.done[s];
+    const bool live = s < X.S && X.done[s] == (RETRY ? 4u : 0u);
+    if (RETRY && live) X.done[s] = 0;
     bool running = false;
     if (live) {
         const uint32_t n0 = X.ln[s];
@@ -937,6 +1082,12 @@ static bool narrow_off() {
     return off;
 }
 
+// KAD_SWARM_SEQ=1 (A/B): the sequential 16-entry merge where every peer answers, not the sorting network.
+static bool net_off() {
+    static const bool off = std::getenv("KAD_SWARM_SEQ") != nullptr;
+    return off;
+}
+
 int kad_search_hop(kad_search* x, uint32_t* n_active) {
     if (!x) return err(KAD_ERR_INVALID, "NULL search");
     Guard g(x->device);
@@ -950,7 +1101,11 @@ int kad_search_hop(kad_search* x, uint32_t* n_active) {
         if (split) {
             hipLaunchKernelGGL(search_query_kernel, dim3(grid_for((uint64_t)X.S * ALPHA)), dim3(BLOCK), 0, x->stream,
                                x->sw->W, X);
-            if (X.offline == 0 && !narrow_off())
+            if (X.offline == 0 && !narrow_off() && !net_off()) {
+                hipLaunchKernelGGL(search_merge_net_kernel, dim3(grid_for(X.S)), dim3(BLOCK), 0, x->stream, x->sw->W, X);
+                hipLaunchKernelGGL((search_merge_kernel<false, 16, true>), dim3(grid_for(X.S)), dim3(BLOCK), 0,
+                                   x->stream, x->sw->W, X);
+            } else if (X.offline == 0 && !narrow_off())
                 hipLaunchKernelGGL((search_merge_kernel<false, 16>), dim3(grid_for(X.S)), dim3(BLOCK), 0, x->stream,
                                    x->sw->W, X);
             else

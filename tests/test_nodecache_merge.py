@@ -132,3 +132,30 @@ def test_lane_answer_is_the_walk():
                             [rnd.random() < 0.5 for _ in right], p + len(left), t, count)
         assert [e - len(left) for e in wide] == got
     assert answered > 3000
+
+
+def test_search_insert_without_bad_nodes_is_order_free():
+    """The premise of the swarm's all-online merge network (kad_swarm.hip, merge_lookup_net): without bad nodes,
+    Search::insertNode (dht.cpp:961-1047: a node already in the list is skipped, an insert beyond a full list of
+    SEARCH_NODES is refused, a list over SEARCH_NODES drops its farthest) keeps exactly the SEARCH_NODES closest of
+    the list and everything inserted, whatever the order of the inserts, each node with the flags it had."""
+    SN = 14
+    rnd = random.Random(17)
+    for _ in range(3000):
+        pool = rnd.sample(range(10 ** 6), 60)
+        start = sorted(rnd.sample(pool, rnd.randint(0, SN)))
+        flags = {x: rnd.random() < 0.5 for x in start}
+        answers = [rnd.choice(pool) for _ in range(rnd.randint(0, 32))]
+        lst = list(start)
+        for a in answers:  # sequential inserts (distance = the value itself)
+            if a in lst:
+                continue
+            pos = sum(x < a for x in lst)
+            if len(lst) >= SN and pos >= len(lst):
+                continue
+            lst.insert(pos, a)
+            if len(lst) > SN:
+                lst.pop()
+        want = sorted(set(start) | set(answers))[:SN]
+        assert lst == want
+        assert [flags.get(x, False) for x in lst] == [flags.get(x, False) for x in want]
