@@ -398,3 +398,42 @@ def test_swarm_gpu_search_state_pool(gpu):
         Xa.close()
         Xb.close()
     M.close()
+
+
+@pytest.mark.gpu
+def test_swarm_gpu_top64_ties_hop_by_hop(gpu):
+    """Pairs of peers that share their top 64 ID bits (their order needs the 160-bit tails): the all-online merge
+    network leaves a lookup whose list or answers hold such a pair to the sequential merge (done = 4 for one launch);
+    every hop equal to the oracle, and ties do occur in the lists."""
+    from opendht_amd.swarm import Swarm
+    n = 20_000
+    ids = _swarm_ids(n, 0x5AB).copy()
+    ids[1::2, :8] = ids[0::2, :8]  # peer 2i+1 takes peer 2i's top 64 bits (its tail differs)
+    ids, _ = S.sort_ids(ids)
+    M = O.SwarmModel(ids)
+    rng = np.random.default_rng(19)
+    Sn = 3000
+    src = rng.integers(0, n, Sn).astype(np.uint32)
+    tg = S.random_targets(Sn, seed=21)
+    tg[:300, :8] = ids[rng.integers(0, n, 300), :8]  # targets right at a tied pair
+    key = _key(ids)
+    with Swarm(ids, device=gpu.index or 0) as W:
+        X = W.search(torch.from_numpy(src.view(np.int32)).to(gpu), torch.from_numpy(tg).to(gpu))
+        ties = 0
+        for h in range(1, 40):
+            active = X.hop()
+            got = X.get()
+            want = M.search(src, tg, max_hops=h)
+            for a, b, name in zip(got, want, ("list", "queried", "n", "hops", "done")):
+                np.testing.assert_array_equal(a, b, err_msg=f"hop {h}: {name}")
+            lst, nn = got[0], got[2]
+            for i in range(0, Sn, 7):
+                li = lst[i, :nn[i]].astype(np.int64)
+                k = key[li]
+                ties += int((k[1:] == k[:-1]).sum())
+            if active == 0:
+                break
+        assert active == 0
+        assert ties > 0
+        X.close()
+    M.close()
