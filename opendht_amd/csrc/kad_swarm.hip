@@ -201,9 +201,36 @@ __device__ __forceinline__ bool tail_less(const SwarmDev& W, const Tgt& t, uint3
     return a4 < b4;
 }
 
+// (key, id) compare-exchange: the smaller key first (equal keys stay: the caller sends ties to the sequential form)
+__device__ __forceinline__ void cx_kid(uint64_t& ka, uint32_t& ia, uint64_t& kb, uint32_t& ib) {
+    const bool sw = kb < ka;
+    const uint64_t k0 = sw ? kb : ka, k1 = sw ? ka : kb;
+    const uint32_t i0 = sw ? ib : ia, i1 = sw ? ia : ib;
+    ka = k0; kb = k1; ia = i0; ib = i1;
+}
+
+// Batcher's odd-even merge sort of 8 (key, id) pairs, 19 compare-exchanges
+__device__ __forceinline__ void sort8_kid(uint64_t (&bk)[BK], uint32_t (&bi)[BK]) {
+    cx_kid(bk[0], bi[0], bk[1], bi[1]); cx_kid(bk[2], bi[2], bk[3], bi[3]);
+    cx_kid(bk[4], bi[4], bk[5], bi[5]); cx_kid(bk[6], bi[6], bk[7], bi[7]);
+    cx_kid(bk[0], bi[0], bk[2], bi[2]); cx_kid(bk[1], bi[1], bk[3], bi[3]);
+    cx_kid(bk[4], bi[4], bk[6], bi[6]); cx_kid(bk[5], bi[5], bk[7], bi[7]);
+    cx_kid(bk[1], bi[1], bk[2], bi[2]); cx_kid(bk[5], bi[5], bk[6], bi[6]);
+    cx_kid(bk[0], bi[0], bk[4], bi[4]); cx_kid(bk[1], bi[1], bk[5], bi[5]);
+    cx_kid(bk[2], bi[2], bk[6], bi[6]); cx_kid(bk[3], bi[3], bk[7], bi[7]);
+    cx_kid(bk[2], bi[2], bk[4], bi[4]); cx_kid(bk[3], bi[3], bk[5], bi[5]);
+    cx_kid(bk[1], bi[1], bk[2], bi[2]); cx_kid(bk[3], bi[3], bk[4], bi[4]); cx_kid(bk[5], bi[5], bk[6], bi[6]);
+}
+
 // RoutingTable::findClosestNodes(t, count) on peer p's table, count <= K. Writes the result's peer
 // indices and keys (sorted by XOR distance) and returns their number.
-template <uint32_t K>
+// NET (K = 8): the window's nodes ranked by a sorting network instead of one insert each: each bucket's 8 slots are
+// sorted (19 compare-exchanges) and merged with the running top 8 (a bitonic half-cleaner and three levels), ~250 VALU
+// operations a bucket where the inserts took ~100 a node. The network orders by the top 64 bits of the distance only,
+// so a result whose order or cut needs the 160-bit tails (two of its distances equal, or its last equal to the
+// nearest node left out) returns TIE and the caller ranks it again with inserts (NET = false).
+constexpr uint32_t TIE = 0xFFFFFFFFu;
+template <uint32_t K, bool NET = false>
 __device__ uint32_t peer_closest(const SwarmDev& W, uint32_t p, const Tgt& t, uint32_t count, uint32_t* oi, uint64_t* ok) {
     const uint32_t* hp = W.hdr + (size_t)p * HDR_WORDS;
     const uint4 h0 = *reinterpret_cast<const uint4*>(hp);  // key, depth (the counts: the same line, cached)
@@ -239,6 +266,9 @@ __device__ uint32_t peer_closest(const SwarmDev& W, uint32_t p, const Tgt& t, ui
 #pragma unroll
     for (uint32_t s = 0; s < K; s++) { L0[s] = ~0ull; LI[s] = NONE; }
     uint32_t nl = 0;
+    uint64_t nin = ~0ull;  // (NET) the nearest node left out
+    bool tie = false;
+    static_assert(!NET || K == BK, "the network ranks 8");
     static_assert(BK == 8, "a level's slots are two 16-byte index loads and four 16-byte key loads");
     // a level's 8 slots in one round of 16-byte loads (the slots from its count on are padding, skipped); the next
     // window bucket's slots are loaded before the current one's are ranked, so the window costs one round trip, not
@@ -272,6 +302,30 @@ __device__ uint32_t peer_closest(const SwarmDev& W, uint32_t p, const Tgt& t, ui
         const uint32_t nb = cur.nb;
         const uint32_t* ei = cur.i;
         const uint64_t* ek = cur.k;
+        if constexpr (NET) {  // (in place in cur's registers; the first bucket merges with an empty top as well)
+#pragma unroll
+            for (uint32_t j = 0; j < BK; j++) {
+                cur.k[j] = j < nb ? cur.k[j] ^ t.hi : ~0ull;
+                cur.i[j] = j < nb ? cur.i[j] : NONE;
+                tie |= j < nb && cur.k[j] == ~0ull;  // (a node as far as the padding)
+            }
+            sort8_kid(cur.k, cur.i);
+#pragma unroll
+            for (uint32_t s = 0; s < K; s++) {  // the 8 smallest of (top ascending, bucket descending)
+                const bool sw = cur.k[K - 1 - s] < L0[s];
+                nin = min(nin, sw ? L0[s] : cur.k[K - 1 - s]);
+                L0[s] = sw ? cur.k[K - 1 - s] : L0[s];
+                LI[s] = sw ? cur.i[K - 1 - s] : LI[s];
+            }
+#pragma unroll
+            for (uint32_t h = K / 2; h >= 1; h >>= 1)
+#pragma unroll
+                for (uint32_t r = 0; r < K; r++)
+                    if ((r & h) == 0) cx_kid(L0[r], LI[r], L0[r + h], LI[r + h]);
+            nl = min(nl + nb, K);
+            if (P < hi) cur = nxt;
+            continue;
+        }
 #pragma unroll 1
         for (uint32_t j = 0; j < nb; j++) {
             uint64_t cd = ek[0];
@@ -296,6 +350,12 @@ __device__ uint32_t peer_closest(const SwarmDev& W, uint32_t p, const Tgt& t, ui
             nl = min(nl + 1, K);
         }
         if (P < hi) cur = nxt;
+    }
+    if constexpr (NET) {
+#pragma unroll
+        for (uint32_t s = 0; s + 1 < K; s++) tie |= L0[s] != ~0ull && L0[s] == L0[s + 1];
+        tie |= nin != ~0ull && L0[K - 1] == nin;
+        if (tie) return TIE;
     }
     const uint32_t m = min(nl, count);
 #pragma unroll
@@ -438,6 +498,11 @@ __global__ __launch_bounds__(BLOCK) void search_init_kernel(SwarmDev W, SearchDe
 }
 
 // one lane per (search, queried node): its findClosestNodes(t, 8), or nothing if it is offline
+// NET: findClosestNodes by the sorting network (peer_closest<BK, true>), by inserts where it returns TIE (a 64-bit tie
+// in the answer). ~1-2 % a hop over inserts alone (profiles/r06/swarm_qnet/: the kernel waits on its level loads, not
+// on VALU); deferring the ties to a second kernel, so that this one does not carry the insert code's registers (134
+// against 138 VGPRs), or aiming it at four waves a SIMD (5 VGPRs spilled) was no faster.
+template <bool NET>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(SW_QUERY_WPE, 8))) void search_query_kernel(SwarmDev W, SearchDev X) {
     const uint32_t g = blockIdx.x * BLOCK + threadIdx.x;
     if (g >= X.S * ALPHA) return;
@@ -446,7 +511,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(SW_QUERY_
     uint32_t oi[BK];
     uint64_t ok[BK];
     const bool up = v < W.n && !swarm_offline(v, X.offline);
-    const uint32_t m = up ? peer_closest<BK>(W, v, load_tgt(X.targets, s), BK, oi, ok) : 0u;
+    const Tgt t = load_tgt(X.targets, s);
+    uint32_t m = up ? (NET ? peer_closest<BK, true>(W, v, t, BK, oi, ok) : TIE) : 0u;
+    if (m == TIE) m = peer_closest<BK>(W, v, t, BK, oi, ok);
     // the answers as whole 16-byte pieces (entries from m on are never read: the merge reads rn of them)
     if (m) {
         uint4* pi = reinterpret_cast<uint4*>(X.ri + (size_t)g * BK);
@@ -688,14 +755,6 @@ __device__ __forceinline__ bool merge_lookup(const SwarmDev& W, const SearchDev&
     }
 }
 
-// (key, id) compare-exchange: the smaller key first (equal keys stay: the caller sends ties to the sequential form)
-__device__ __forceinline__ void cx_kid(uint64_t& ka, uint32_t& ia, uint64_t& kb, uint32_t& ib) {
-    const bool sw = kb < ka;
-    const uint64_t k0 = sw ? kb : ka, k1 = sw ? ka : kb;
-    const uint32_t i0 = sw ? ib : ia, i1 = sw ? ia : ib;
-    ka = k0; kb = k1; ia = i0; ib = i1;
-}
-
 // The all-online hop's merge as a sorting network (runs where every peer answers). With no bad node and no silent
 // peer, Search::insertNode's sequential inserts (dht.cpp:961-1047) keep exactly the SEARCH_NODES closest of the list
 // and the answers (an insert beyond a full list is refused, a full list drops its farthest after an insert, a node
@@ -753,16 +812,7 @@ __device__ __forceinline__ bool merge_lookup_net(const SwarmDev& W, const Search
             bk[j] = drop ? MAXK : A.k[j] ^ t.hi;
             bi[j] = drop ? NONE : r;
         }
-        // Batcher's odd-even merge sort of 8 (the block was sorted; the dropped entries leave MAX holes)
-        cx_kid(bk[0], bi[0], bk[1], bi[1]); cx_kid(bk[2], bi[2], bk[3], bi[3]);
-        cx_kid(bk[4], bi[4], bk[5], bi[5]); cx_kid(bk[6], bi[6], bk[7], bi[7]);
-        cx_kid(bk[0], bi[0], bk[2], bi[2]); cx_kid(bk[1], bi[1], bk[3], bi[3]);
-        cx_kid(bk[4], bi[4], bk[6], bi[6]); cx_kid(bk[5], bi[5], bk[7], bi[7]);
-        cx_kid(bk[1], bi[1], bk[2], bi[2]); cx_kid(bk[5], bi[5], bk[6], bi[6]);
-        cx_kid(bk[0], bi[0], bk[4], bi[4]); cx_kid(bk[1], bi[1], bk[5], bi[5]);
-        cx_kid(bk[2], bi[2], bk[6], bi[6]); cx_kid(bk[3], bi[3], bk[7], bi[7]);
-        cx_kid(bk[2], bi[2], bk[4], bi[4]); cx_kid(bk[3], bi[3], bk[5], bi[5]);
-        cx_kid(bk[1], bi[1], bk[2], bi[2]); cx_kid(bk[3], bi[3], bk[4], bi[4]); cx_kid(bk[5], bi[5], bk[6], bi[6]);
+        sort8_kid(bk, bi);  // (the block was sorted; the dropped entries leave MAX holes)
         // the 16 smallest of (list ascending, block descending): one half-cleaner, then four levels
 #pragma unroll
         for (uint32_t i = 8; i < 16; i++) {
@@ -1088,6 +1138,15 @@ static bool net_off() {
     return off;
 }
 
+// KAD_SWARM_QUERY=ins (A/B): the query kernel's findClosestNodes by inserts, not the sorting network.
+static bool qnet_off() {
+    static const bool off = [] {
+        const char* e = std::getenv("KAD_SWARM_QUERY");
+        return e && !std::strcmp(e, "ins");
+    }();
+    return off;
+}
+
 int kad_search_hop(kad_search* x, uint32_t* n_active) {
     if (!x) return err(KAD_ERR_INVALID, "NULL search");
     Guard g(x->device);
@@ -1099,8 +1158,11 @@ int kad_search_hop(kad_search* x, uint32_t* n_active) {
         // walks run on a quarter of the lanes, behind the merge's registers, with their round trips no longer hidden
         static const bool split = std::getenv("KAD_SWARM_FUSED") == nullptr;
         if (split) {
-            hipLaunchKernelGGL(search_query_kernel, dim3(grid_for((uint64_t)X.S * ALPHA)), dim3(BLOCK), 0, x->stream,
-                               x->sw->W, X);
+            const dim3 qg(grid_for((uint64_t)X.S * ALPHA));
+            if (qnet_off())
+                hipLaunchKernelGGL(search_query_kernel<false>, qg, dim3(BLOCK), 0, x->stream, x->sw->W, X);
+            else
+                hipLaunchKernelGGL(search_query_kernel<true>, qg, dim3(BLOCK), 0, x->stream, x->sw->W, X);
             if (X.offline == 0 && !narrow_off() && !net_off()) {
                 hipLaunchKernelGGL(search_merge_net_kernel, dim3(grid_for(X.S)), dim3(BLOCK), 0, x->stream, x->sw->W, X);
                 hipLaunchKernelGGL((search_merge_kernel<false, 16, true>), dim3(grid_for(X.S)), dim3(BLOCK), 0,

@@ -159,3 +159,72 @@ def test_search_insert_without_bad_nodes_is_order_free():
         want = sorted(set(start) | set(answers))[:SN]
         assert lst == want
         assert [flags.get(x, False) for x in lst] == [flags.get(x, False) for x in want]
+
+
+def _cx(k, i, a, b):
+    if k[b] < k[a]:
+        k[a], k[b] = k[b], k[a]
+        i[a], i[b] = i[b], i[a]
+
+
+_SORT8 = [(0, 1), (2, 3), (4, 5), (6, 7), (0, 2), (1, 3), (4, 6), (5, 7), (1, 2), (5, 6), (0, 4), (1, 5), (2, 6),
+          (3, 7), (2, 4), (3, 5), (1, 2), (3, 4), (5, 6)]
+
+
+def _closest_net(levels, K=8):
+    """kad_swarm.hip peer_closest<8, true> restated: each bucket's slots (64-bit distance, node) sorted by the 19
+    compare-exchanges, merged into the running top 8 by a half-cleaner against the bucket reversed and three levels;
+    None (TIE) where the top 8 holds two equal distances or its last equals the nearest node left out."""
+    MAX = (1 << 64) - 1
+    L0, LI, nin, nl = None, None, MAX, 0
+    for lv in levels:
+        bk = [d for d, _ in lv] + [MAX] * (K - len(lv))
+        bi = [n for _, n in lv] + [None] * (K - len(lv))
+        if any(d == MAX for d, _ in lv):
+            return None
+        for a, b in _SORT8:
+            _cx(bk, bi, a, b)
+        if L0 is None:
+            L0, LI = bk, bi
+        else:
+            for s in range(K):
+                sw = bk[K - 1 - s] < L0[s]
+                nin = min(nin, L0[s] if sw else bk[K - 1 - s])
+                if sw:
+                    L0[s], LI[s] = bk[K - 1 - s], bi[K - 1 - s]
+            h = K // 2
+            while h >= 1:
+                for r in range(K):
+                    if r & h == 0:
+                        _cx(L0, LI, r, r + h)
+                h //= 2
+        nl = min(nl + len(lv), K)
+    if any(L0[s] != MAX and L0[s] == L0[s + 1] for s in range(K - 1)) or (nin != MAX and L0[K - 1] == nin):
+        return None
+    return LI[:nl]
+
+
+def test_query_network_is_the_inserts():
+    """The swarm query kernel's sorting-network findClosestNodes (kad_swarm.hip peer_closest<8, true>) returns the
+    routing_table.cpp:79-110 result (the window's nodes ranked by the full XOR distance: here the 64-bit top, then
+    the tail) wherever it does not return TIE, and returns TIE only where 64-bit distances are equal; distances are
+    drawn from a small range so that ties are common."""
+    rnd = random.Random(23)
+    seen_tie = seen_ok = 0
+    for _ in range(4000):
+        span = rnd.choice([40, 1000, 1 << 64])
+        nodes = iter(range(10 ** 6))
+        levels = [[(rnd.randrange(span), next(nodes)) for _ in range(rnd.randint(1 if j == 0 else 0, 8))]
+                  for j in range(rnd.randint(1, 4))]
+        tail = {n: rnd.random() for lv in levels for _, n in lv}
+        allnodes = [x for lv in levels for x in lv]
+        want = [n for _, n in sorted(allnodes, key=lambda x: (x[0], tail[x[1]]))[:8]]
+        got = _closest_net([list(lv) for lv in levels])
+        if got is None:
+            seen_tie += 1
+            d = sorted(x[0] for x in allnodes)
+            assert len(set(d)) < len(d)
+        else:
+            seen_ok += 1
+            assert got == want
+    assert seen_tie > 100 and seen_ok > 1000
