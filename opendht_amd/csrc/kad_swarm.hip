@@ -233,10 +233,20 @@ constexpr uint32_t TIE = 0xFFFFFFFFu;
 template <uint32_t K, bool NET = false>
 __device__ uint32_t peer_closest(const SwarmDev& W, uint32_t p, const Tgt& t, uint32_t count, uint32_t* oi, uint64_t* ok) {
     const uint32_t* hp = W.hdr + (size_t)p * HDR_WORDS;
-    const uint4 h0 = *reinterpret_cast<const uint4*>(hp);  // key, depth (the counts: the same line, cached)
+    // key, depth and the level counts: the header line's first 48 bytes in one round of 16-byte loads, so the window
+    // rounds below read counts from registers, not one dependent cache round trip each
+    const uint4 h0 = reinterpret_cast<const uint4*>(hp)[0], h1 = reinterpret_cast<const uint4*>(hp)[1],
+                h2 = reinterpret_cast<const uint4*>(hp)[2];
     const uint64_t k = ((uint64_t)h0.y << 32) | h0.x;
     const uint32_t D = h0.z;
-    const uint8_t* cp = reinterpret_cast<const uint8_t*>(hp + 4);
+    static_assert(L <= 32, "the counts are header bytes 16..47");
+    const uint32_t cw[8] = {h1.x, h1.y, h1.z, h1.w, h2.x, h2.y, h2.z, h2.w};
+    auto cnt = [&](uint32_t d) -> uint32_t {  // (a select chain: the words stay in registers)
+        uint32_t w = cw[0];
+#pragma unroll
+        for (uint32_t y = 1; y < (L + 3) / 4; y++) w = (d >> 2) == y ? cw[y] : w;
+        return (w >> (8 * (d & 3u))) & 255u;
+    };
     const uint32_t lv = (uint32_t)(__builtin_bitreverse64(k) & ((1ull << D) - 1));  // bit d = bit d of k from the top
     const uint32_t m1 = lv, m0 = ~lv & (uint32_t)((1ull << D) - 1);
     const uint32_t M = (uint32_t)__builtin_popcount(m1), B = D + 1;
@@ -255,10 +265,10 @@ __device__ uint32_t peer_closest(const SwarmDev& W, uint32_t p, const Tgt& t, ui
         return nth_bit(m0, n0 - 1 - (P - M - 1));
     };
     // window rounds (routing_table.cpp:89-104)
-    uint32_t lo = b > 0 ? b - 1 : 0, hi = b, good = cp[level(b)] + (b > 0 ? cp[level(b - 1)] : 0u);
+    uint32_t lo = b > 0 ? b - 1 : 0, hi = b, good = cnt(level(b)) + (b > 0 ? cnt(level(b - 1)) : 0u);
     while (good < count && !(lo == 0 && hi == B - 1)) {
-        if (hi < B - 1) { hi++; good += cp[level(hi)]; }
-        if (lo > 0) { lo--; good += cp[level(lo)]; }
+        if (hi < B - 1) { hi++; good += cnt(level(hi)); }
+        if (lo > 0) { lo--; good += cnt(level(lo)); }
     }
     // top-count of the window's nodes by (XOR distance, insertion order)
     uint64_t L0[K];
@@ -280,7 +290,7 @@ __device__ uint32_t peer_closest(const SwarmDev& W, uint32_t p, const Tgt& t, ui
     };
     auto load_level = [&](uint32_t P, Slots& S) {
         const uint32_t d = level(P);
-        S.nb = cp[d];
+        S.nb = cnt(d);
         const uint4* ep4 = reinterpret_cast<const uint4*>(W.lvl + ((size_t)p * L + d) * LVL_WORDS);
         const uint4* kp4 = ep4 + BK / 4;
 #pragma unroll
