@@ -79,15 +79,30 @@ int err(int code, const char* fmt, ...) {
 inline uint32_t grid_for(uint64_t n) { return (uint32_t)((n + BLOCK - 1) / BLOCK); }
 
 // A peer's table as one 64-byte header line (HDR_WORDS: its key, depth and the L level counts) and one 128-byte line
-// per level (LVL_WORDS: the 8 entries' peer indices, then their keys): a findClosestNodes on a peer's table reads
-// the header and one line per window bucket, 3 random lines for the usual 2-bucket window, where separate key,
-// depth, count, index and key arrays took 7 (the query kernel is bound by its random line requests).
+// per level (LVL_WORDS: the 8 entries' keys, then the rule giving their peer indices — a bucket's entries are a run of
+// the sorted peers or an even sample of one: first index a, run length m, sample offset, and the index skipped in my
+// own bucket (mine) — then the indices themselves for the host): a findClosestNodes on a peer's table reads the
+// header and the first 80 bytes of one line per window bucket, 3 random lines for the usual 2-bucket window, where
+// separate key, depth, count, index and key arrays took 7 (the query kernel is bound by its random line requests).
 constexpr uint32_t HDR_WORDS = 16, LVL_WORDS = 32;  // header: dw0-1 key, byte 8 depth, bytes 16.. counts
+constexpr uint32_t LVL_RULE = 16, LVL_IDX = 20;      // level line: dw 0-15 keys, 16-19 index rule, 20-27 indices
+
+// Entry j's peer index from a level line's rule (a, m, off, skip) — the build's choice (swarm_build_kernel): a run of
+// m <= 8 sorted peers from a, or my own bucket's run from a without me (skip), or 8 evenly spaced of m > 8 from an
+// offset: a + (off + j m / 8) mod m, where off < m and j m / 8 < m make the mod one subtraction.
+__device__ __forceinline__ uint32_t lvl_index(const uint4& r, uint32_t j) {
+    if (r.y <= 8u || r.w != 0xFFFFFFFFu) {
+        const uint32_t x = r.x + j;
+        return x + (x >= r.w ? 1u : 0u);
+    }
+    const uint32_t o = r.z + (uint32_t)(((uint64_t)j * r.y) >> 3);
+    return r.x + (o >= r.y ? o - r.y : o);
+}
 struct SwarmDev {
     const uint64_t* key;
     const uint32_t* tail;
     uint32_t* hdr;  // [n][HDR_WORDS]
-    uint32_t* lvl;  // [n][L][LVL_WORDS]: dw 0-7 indices, dw 8-23 keys (lo, hi), dw 24-31 zero
+    uint32_t* lvl;  // [n][L][LVL_WORDS]: dw 0-15 keys (lo, hi), dw 16-19 the index rule, dw 20-27 indices, 28-31 zero
     uint32_t n;
 };
 
@@ -142,19 +157,23 @@ __global__ void swarm_build_kernel(SwarmDev W) {
     uint32_t* hp = W.hdr + (size_t)p * HDR_WORDS;
     uint8_t cp[L];
     for (uint32_t d = 0; d < L; d++) cp[d] = 0;
-    // a level line: 8 indices, 8 keys, padding
-    auto put = [&](uint32_t d, const uint32_t (&ei)[BK]) {
+    // a level line: 8 keys, the index rule (lvl_index), 8 indices, padding
+    auto put = [&](uint32_t d, const uint32_t (&ei)[BK], uint32_t a, uint32_t m, uint32_t off, uint32_t skip) {
         uint32_t* lp = W.lvl + ((size_t)p * L + d) * LVL_WORDS;
         for (uint32_t j = 0; j < BK; j++) {
             const uint64_t kk = ei[j] != NONE ? W.key[ei[j]] : ~0ull;
-            lp[j] = ei[j];
-            lp[BK + 2 * j] = (uint32_t)kk;
-            lp[BK + 2 * j + 1] = (uint32_t)(kk >> 32);
+            lp[2 * j] = (uint32_t)kk;
+            lp[2 * j + 1] = (uint32_t)(kk >> 32);
+            lp[LVL_IDX + j] = ei[j];
         }
-        for (uint32_t j = 3 * BK; j < LVL_WORDS; j++) lp[j] = 0;
+        lp[LVL_RULE] = a;
+        lp[LVL_RULE + 1] = m;
+        lp[LVL_RULE + 2] = off;
+        lp[LVL_RULE + 3] = skip;
+        for (uint32_t j = LVL_IDX + BK; j < LVL_WORDS; j++) lp[j] = 0;
     };
     for (uint32_t d = 0; d < L; d++) {
-        uint32_t ei[BK];
+        uint32_t ei[BK], ra = 0, rm = 0, roff = 0, rskip = NONE;
         for (uint32_t j = 0; j < BK; j++) ei[j] = NONE;
         if (d < D) {
             uint32_t a, e;
@@ -163,13 +182,19 @@ __global__ void swarm_build_kernel(SwarmDev W) {
             const uint64_t off = m > BK ? mix(k ^ ((uint64_t)(d + 1) * 0x9E3779B97F4A7C15ull)) % m : 0ull;
             for (uint32_t j = 0; j < c; j++) ei[j] = m > BK ? a + (uint32_t)((off + (uint64_t)j * m / BK) % m) : a + j;
             cp[d] = (uint8_t)c;
+            ra = a;
+            rm = m;
+            roff = (uint32_t)off;
         } else if (d == D) {
             uint32_t c = 0;
             for (uint32_t x = lo; x < hi && c < BK; x++)
                 if (x != p) ei[c++] = x;
             cp[D] = (uint8_t)c;
+            ra = lo;
+            rm = hi - lo;
+            rskip = p;
         }
-        put(d, ei);  // (levels past my bucket: empty lines)
+        put(d, ei, ra, rm, roff, rskip);  // (levels past my bucket: empty lines)
     }
     hp[0] = (uint32_t)k;
     hp[1] = (uint32_t)(k >> 32);
@@ -279,25 +304,20 @@ __device__ uint32_t peer_closest(const SwarmDev& W, uint32_t p, const Tgt& t, ui
     uint64_t nin = ~0ull;  // (NET) the nearest node left out
     bool tie = false;
     static_assert(!NET || K == BK, "the network ranks 8");
-    static_assert(BK == 8, "a level's slots are two 16-byte index loads and four 16-byte key loads");
+    static_assert(BK == 8, "a level's slots are four 16-byte key loads and one 16-byte index rule");
     // a level's 8 slots in one round of 16-byte loads (the slots from its count on are padding, skipped); the next
     // window bucket's slots are loaded before the current one's are ranked, so the window costs one round trip, not
     // one per bucket
     struct Slots {
-        uint32_t i[BK];
         uint64_t k[BK];
+        uint4 rule;
         uint32_t nb;
     };
     auto load_level = [&](uint32_t P, Slots& S) {
         const uint32_t d = level(P);
         S.nb = cnt(d);
-        const uint4* ep4 = reinterpret_cast<const uint4*>(W.lvl + ((size_t)p * L + d) * LVL_WORDS);
-        const uint4* kp4 = ep4 + BK / 4;
-#pragma unroll
-        for (int x = 0; x < 2; x++) {
-            const uint4 u = ep4[x];
-            S.i[4 * x] = u.x; S.i[4 * x + 1] = u.y; S.i[4 * x + 2] = u.z; S.i[4 * x + 3] = u.w;
-        }
+        const uint4* kp4 = reinterpret_cast<const uint4*>(W.lvl + ((size_t)p * L + d) * LVL_WORDS);
+        S.rule = kp4[LVL_RULE / 4];
 #pragma unroll
         for (int x = 0; x < 4; x++) {
             const uint4 u = kp4[x];
@@ -310,22 +330,22 @@ __device__ uint32_t peer_closest(const SwarmDev& W, uint32_t p, const Tgt& t, ui
     for (uint32_t P = lo; P <= hi; P++) {
         if (P < hi) load_level(P + 1, nxt);
         const uint32_t nb = cur.nb;
-        const uint32_t* ei = cur.i;
         const uint64_t* ek = cur.k;
         if constexpr (NET) {  // (in place in cur's registers; the first bucket merges with an empty top as well)
+            uint32_t ej[BK];  // the slots travel through the network, their peer indices are derived after it
 #pragma unroll
             for (uint32_t j = 0; j < BK; j++) {
                 cur.k[j] = j < nb ? cur.k[j] ^ t.hi : ~0ull;
-                cur.i[j] = j < nb ? cur.i[j] : NONE;
+                ej[j] = j;
                 tie |= j < nb && cur.k[j] == ~0ull;  // (a node as far as the padding)
             }
-            sort8_kid(cur.k, cur.i);
+            sort8_kid(cur.k, ej);
 #pragma unroll
             for (uint32_t s = 0; s < K; s++) {  // the 8 smallest of (top ascending, bucket descending)
                 const bool sw = cur.k[K - 1 - s] < L0[s];
                 nin = min(nin, sw ? L0[s] : cur.k[K - 1 - s]);
                 L0[s] = sw ? cur.k[K - 1 - s] : L0[s];
-                LI[s] = sw ? cur.i[K - 1 - s] : LI[s];
+                LI[s] = sw ? (cur.k[K - 1 - s] != ~0ull ? lvl_index(cur.rule, ej[K - 1 - s]) : NONE) : LI[s];
             }
 #pragma unroll
             for (uint32_t h = K / 2; h >= 1; h >>= 1)
@@ -336,6 +356,9 @@ __device__ uint32_t peer_closest(const SwarmDev& W, uint32_t p, const Tgt& t, ui
             if (P < hi) cur = nxt;
             continue;
         }
+        uint32_t ei[BK];
+#pragma unroll
+        for (uint32_t j = 0; j < BK; j++) ei[j] = lvl_index(cur.rule, j);
 #pragma unroll 1
         for (uint32_t j = 0; j < nb; j++) {
             uint64_t cd = ek[0];
@@ -1050,7 +1073,7 @@ int kad_swarm_get_table(const kad_swarm* s, uint32_t peer, uint32_t* depth, uint
     *depth = h[2];
     for (uint32_t d = 0; d < L; d++) {
         counts[d] = (uint8_t)(h[4 + d / 4] >> (8 * (d % 4)));
-        for (uint32_t j = 0; j < BK; j++) entries[d * BK + j] = lv[(size_t)d * LVL_WORDS + j];
+        for (uint32_t j = 0; j < BK; j++) entries[d * BK + j] = lv[(size_t)d * LVL_WORDS + LVL_IDX + j];
     }
     return KAD_OK;
 }
