@@ -798,6 +798,8 @@ __device__ __forceinline__ bool merge_lookup(const SwarmDev& W, const SearchDev&
 // took ~250 each answer. Equal 64-bit distances of different nodes (their order needs the 160-bit tails) are adjacent
 // after each merge; a lookup that has one is left untouched with done = 4 and the sequential form merges it next.
 // Queried flags travel in bit 31 of the node index.
+// PF: the next queried node's answers loaded before the current block is merged (a second Answers in registers).
+template <bool PF>
 __device__ __forceinline__ bool merge_lookup_net(const SwarmDev& W, const SearchDev& X, uint32_t s) {
     constexpr uint32_t QB = 0x80000000u, IM = 0x7FFFFFFFu;
     const uint64_t MAXK = ~0ull;
@@ -829,11 +831,13 @@ __device__ __forceinline__ bool merge_lookup_net(const SwarmDev& W, const Search
     bool tie = false;
 #pragma unroll
     for (uint32_t k = 0; k + 1 < 16; k++) tie |= li[k + 1] != NONE && lk[k] == lk[k + 1];
-    Answers A;
+    Answers A, An;
+    if (PF) load_answers(X, s * ALPHA, rn4 & 255u, A);
 #pragma unroll 1
-    for (uint32_t a = 0; a < ALPHA; a++) {  // (not unrolled: one block's answers in registers at a time)
+    for (uint32_t a = 0; a < ALPHA; a++) {  // (not unrolled: one or two blocks' answers in registers at a time)
         const uint32_t rn = (rn4 >> (8 * a)) & 255u;
-        load_answers(X, s * ALPHA + a, rn, A);
+        if (!PF) load_answers(X, s * ALPHA + a, rn, A);
+        else if (a + 1 < ALPHA) load_answers(X, s * ALPHA + a + 1, (rn4 >> (8 * (a + 1))) & 255u, An);
         uint64_t bk[BK];
         uint32_t bi[BK];
 #pragma unroll
@@ -860,6 +864,7 @@ __device__ __forceinline__ bool merge_lookup_net(const SwarmDev& W, const Search
                 if ((r & h) == 0) cx_kid(lk[r], li[r], lk[r + h], li[r + h]);
 #pragma unroll
         for (uint32_t k = 0; k + 1 < 16; k++) tie |= li[k + 1] != NONE && lk[k] == lk[k + 1];
+        if (PF) A = An;
     }
     if (tie) {  // the sequential form (search_merge_kernel<false, 16, true>) merges this lookup
         X.done[s] = 4;
@@ -907,9 +912,10 @@ __device__ __forceinline__ bool merge_lookup_net(const SwarmDev& W, const Search
     return !X.done[s];
 }
 
+template <bool PF>
 __global__ __launch_bounds__(BLOCK) void search_merge_net_kernel(SwarmDev W, SearchDev X) {
     const uint32_t s = blockIdx.x * BLOCK + threadIdx.x;
-    const bool running = s < X.S && !X.done[s] && merge_lookup_net(W, X, s);
+    const bool running = s < X.S && !X.done[s] && merge_lookup_net<PF>(W, X, s);
     const uint64_t m = __ballot(running);
     if ((threadIdx.x & 63u) == 0 && m) atomicAdd(X.active, (uint32_t)__builtin_popcountll(m));
 }
@@ -1171,6 +1177,15 @@ static bool net_off() {
     return off;
 }
 
+// KAD_SWARM_NETPF=0 (A/B): the merge network without the next block's answers loaded ahead.
+static bool net_pf_off() {
+    static const bool off = [] {
+        const char* e = std::getenv("KAD_SWARM_NETPF");
+        return e && !std::strcmp(e, "0");
+    }();
+    return off;
+}
+
 // KAD_SWARM_QUERY=ins (A/B): the query kernel's findClosestNodes by inserts, not the sorting network.
 static bool qnet_off() {
     static const bool off = [] {
@@ -1197,7 +1212,12 @@ int kad_search_hop(kad_search* x, uint32_t* n_active) {
             else
                 hipLaunchKernelGGL(search_query_kernel<true>, qg, dim3(BLOCK), 0, x->stream, x->sw->W, X);
             if (X.offline == 0 && !narrow_off() && !net_off()) {
-                hipLaunchKernelGGL(search_merge_net_kernel, dim3(grid_for(X.S)), dim3(BLOCK), 0, x->stream, x->sw->W, X);
+                if (net_pf_off())
+                    hipLaunchKernelGGL(search_merge_net_kernel<false>, dim3(grid_for(X.S)), dim3(BLOCK), 0, x->stream,
+                                       x->sw->W, X);
+                else
+                    hipLaunchKernelGGL(search_merge_net_kernel<true>, dim3(grid_for(X.S)), dim3(BLOCK), 0, x->stream,
+                                       x->sw->W, X);
                 hipLaunchKernelGGL((search_merge_kernel<false, 16, true>), dim3(grid_for(X.S)), dim3(BLOCK), 0,
                                    x->stream, x->sw->W, X);
             } else if (X.offline == 0 && !narrow_off())
