@@ -228,3 +228,52 @@ def test_query_network_is_the_inserts():
             seen_ok += 1
             assert got == want
     assert seen_tie > 100 and seen_ok > 1000
+
+
+def _insert_node(lst, x, xbad, SN=14):
+    """Search::insertNode (dht.cpp:961-1047, search not expired) on a list of (distance, bad) sorted by distance."""
+    if any(d == x for d, _ in lst):
+        return
+    n = sum(1 for d, _ in lst if d < x)
+    bad = sum(b for _, b in lst)
+    full = len(lst) - bad >= SN
+    t = len(lst)
+    while t - bad > SN:
+        t -= 1
+        if lst[t][1]:
+            bad -= 1
+    if full:
+        del lst[t:]
+        if n >= t:
+            return
+    lst.insert(n, (x, xbad))
+    bad += xbad
+    while len(lst) - bad > SN:
+        bad -= lst[-1][1]
+        lst.pop()
+
+
+def test_search_insert_with_bad_nodes_depends_on_order():
+    """Why the swarm's merge with offline peers stays sequential: with bad nodes in play,
+    Search::insertNode's list depends on the order of the inserts for some answer sets, so no order-free network can
+    stand in for it; without bad nodes it never does (the premise of merge_lookup_net)."""
+    rnd = random.Random(5)
+    dep = {0.0: 0, 0.2: 0}
+    for share in dep:
+        for _ in range(3000):
+            pool = rnd.sample(range(1000), 60)
+            isbad = {x: int(rnd.random() < share) for x in pool}
+            base = []
+            for x in sorted(rnd.sample(pool, rnd.randint(0, 18))):
+                _insert_node(base, x, isbad[x])
+            ans = [rnd.choice(pool) for _ in range(rnd.randint(0, 32))]
+            res = set()
+            for _ in range(6):
+                a = list(ans)
+                rnd.shuffle(a)
+                lst = list(base)
+                for x in a:
+                    _insert_node(lst, x, isbad[x])
+                res.add(tuple(lst))
+            dep[share] += len(res) > 1
+    assert dep[0.0] == 0 and dep[0.2] > 20
