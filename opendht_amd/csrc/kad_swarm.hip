@@ -540,11 +540,14 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(SW_QUERY_
     const uint32_t g = blockIdx.x * BLOCK + threadIdx.x;
     if (g >= X.S * ALPHA) return;
     const uint32_t s = g / ALPHA;
-    const uint32_t v = X.done[s] ? NONE : X.sel[g];
+    // (the selection, the state and the target loaded together: the selection read whatever the state, so that the
+    // peer's header load waits on one round trip, not two)
+    const uint32_t sv = X.sel[g];
+    const Tgt t = load_tgt(X.targets, s);
+    const uint32_t v = X.done[s] ? NONE : sv;
     uint32_t oi[BK];
     uint64_t ok[BK];
     const bool up = v < W.n && !swarm_offline(v, X.offline);
-    const Tgt t = load_tgt(X.targets, s);
     uint32_t m = up ? (NET ? peer_closest<BK, true>(W, v, t, BK, oi, ok) : TIE) : 0u;
     if (m == TIE) m = peer_closest<BK>(W, v, t, BK, oi, ok);
     // the answers as whole 16-byte pieces (entries from m on are never read: the merge reads rn of them)
