@@ -54,6 +54,13 @@ __global__ __launch_bounds__(BLOCK) void route_pack_kernel(const uint8_t* __rest
             for (int x = 0; x < (KEYS ? 2 : 5); x++) w[r][x] = __builtin_nontemporal_load(p + x);
         }
     }
+    // places in the workgroup's count of each owner, the wave's lanes of one owner at consecutive places (their
+    // records then leave as contiguous runs): each lane's mask of the lanes sharing its owner from one ballot per
+    // owner bit (at most 4 for world <= 16), then one LDS atomic instruction per round for all the wave's owners
+    // (the lowest lane of each owner adds its lane count) and one bpermute of the bases — instead of a ballot, an
+    // atomic and a read-back per owner, `world` dependent LDS round trips per round
+    const uint32_t nbits = world > 1u ? 32u - (uint32_t)__builtin_clz(world - 1u) : 0u;  // (wave-uniform)
+    uint32_t lead[QPT], rank[QPT], bse[QPT];
 #pragma unroll
     for (uint32_t r = 0; r < QPT; r++) {
         const uint64_t i = base + r * BLOCK + tid;
@@ -62,20 +69,19 @@ __global__ __launch_bounds__(BLOCK) void route_pack_kernel(const uint8_t* __rest
             const uint32_t b0 = w[r][0] & 0xFFu;  // InfoHash byte 0: the most significant
             dst[r] = shard_bits ? (b0 >> (8 - shard_bits)) % world : 0u;
         }
-        // places in the workgroup's count of each owner: one LDS atomic per (wave, owner), the wave's lanes of
-        // one owner at consecutive places (their records then leave as contiguous runs)
-        const uint32_t lane = tid & 63u;
-        for (uint32_t d = 0; d < world; d++) {  // (wave-uniform)
-            const uint64_t m = __ballot(dst[r] == d);
-            if (!m) continue;
-            const uint32_t leader = (uint32_t)__builtin_ctzll(m);
-            uint32_t b = 0;
-            if (lane == leader) b = atomicAdd(&hcnt[d], (uint32_t)__builtin_popcountll(m));
-            b = __shfl(b, (int)leader, 64);
-            if (dst[r] == d)
-                pos[r] = b + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        uint64_t m = __ballot(dst[r] != NONE);
+        for (uint32_t bit = 0; bit < nbits; bit++) {
+            const bool set = (dst[r] >> bit) & 1u;
+            const uint64_t bb = __ballot(set);
+            m &= set ? bb : ~bb;
         }
+        rank[r] = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        lead[r] = m ? (uint32_t)__builtin_ctzll(m) : 0u;
+        bse[r] = 0;
+        if (dst[r] != NONE && rank[r] == 0u) bse[r] = atomicAdd(&hcnt[dst[r]], (uint32_t)__builtin_popcountll(m));
     }
+#pragma unroll
+    for (uint32_t r = 0; r < QPT; r++) pos[r] = __shfl(bse[r], (int)lead[r], 64) + rank[r];
     __syncthreads();
     // the workgroup's sub-block of each block: KAD_ROUTE_SUBS counters per block instead of one for every workgroup
     const uint32_t sub = cap / KAD_ROUTE_SUBS, rg = blockIdx.x % KAD_ROUTE_SUBS;
