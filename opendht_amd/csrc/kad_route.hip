@@ -44,15 +44,15 @@ __global__ __launch_bounds__(BLOCK) void route_pack_kernel(const uint8_t* __rest
     const uint64_t base = (uint64_t)blockIdx.x * BLOCK * QPT;
     // every target's loads first (QPT x 5 in flight per lane): the LDS atomics below would otherwise order each
     // round's loads after the previous round's placement, QPT dependent memory round trips per workgroup
-    // (only the words the record carries: the top 8 bytes for a key)
+    // (only the words the record carries: the top 8 bytes for a key). The loads are unconditional — lanes past q
+    // re-read record q - 1 (the kernel runs only for q > 0) and are dropped below — so that no use of a record is
+    // sunk into a per-round branch with its own wait (the key form then waited for each round's load in turn)
 #pragma unroll
     for (uint32_t r = 0; r < QPT; r++) {
-        const uint64_t i = base + r * BLOCK + tid;  // consecutive lanes, consecutive 20-byte records
-        if (i < q) {
-            const uint32_t* p = reinterpret_cast<const uint32_t*>(targets + 20 * i);
+        const uint64_t i = min(base + r * BLOCK + tid, (uint64_t)q - 1u);  // consecutive lanes, consecutive records
+        const uint32_t* p = reinterpret_cast<const uint32_t*>(targets + 20 * i);
 #pragma unroll
-            for (int x = 0; x < (KEYS ? 2 : 5); x++) w[r][x] = __builtin_nontemporal_load(p + x);
-        }
+        for (int x = 0; x < (KEYS ? 2 : 5); x++) w[r][x] = __builtin_nontemporal_load(p + x);
     }
     // places in the workgroup's count of each owner, the wave's lanes of one owner at consecutive places (their
     // records then leave as contiguous runs): each lane's mask of the lanes sharing its owner from one ballot per
