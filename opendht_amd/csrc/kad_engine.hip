@@ -3613,11 +3613,16 @@ __global__ __launch_bounds__(WG) void rt_shard_kernel(DevTable T, ShardCtx S, co
                     if (x < n4) d4[x] = s4[x];
                 }
             } else {
+                // every piece's load issued before the first LDS write: unconditional loads (a lane past the block's
+                // pieces re-reads its last one, n4 >= 1), guarded writes — with the guard around each load the
+                // compiler waited for each round's load before issuing the next
+                constexpr uint32_t K = 5 * QB / (4 * WG);
+                u32x4_t v[K];
 #pragma unroll
-                for (uint32_t k = 0; k < 5 * QB / (4 * WG); k++) {
-                    const uint32_t x = tid + k * WG;
-                    if (x < n4) d4[x] = __builtin_nontemporal_load(s4 + x);
-                }
+                for (uint32_t k = 0; k < K; k++) v[k] = __builtin_nontemporal_load(s4 + min(tid + k * WG, n4 - 1u));
+#pragma unroll
+                for (uint32_t k = 0; k < K; k++)
+                    if (tid + k * WG < n4) d4[tid + k * WG] = v[k];
             }
             o = 4 * n4;
         }
